@@ -1,0 +1,132 @@
+/*
+ * rmbx.h — C ABI of the MI355X-native batched policy-rollout engine.
+ *
+ * Every entry point is extern "C", takes plain pointers (device memory unless stated) and sizes,
+ * returns an int status (RMBX_OK = 0, negative on error; the message is available from
+ * rmbx_last_error(), thread-local) and enqueues its work on the caller's HIP stream
+ * (`stream` is a hipStream_t passed as void*, NULL = the legacy default stream).
+ * No call allocates, frees or synchronises on the hot path, so every hot-path call can be
+ * captured in a hipGraph.  Ownership: the engine owns model constants and per-env state; all
+ * I/O buffers are caller-owned device memory.  Threading: one host thread per engine; calls on
+ * one engine handle are not re-entrant.
+ *
+ * Each function cites the reference (yusuke1127/RoboManipBaselines @2.0.0) interface it replaces
+ * for a batch of environments; paths are relative to the reference package root
+ * robo_manip_baselines/.
+ */
+#ifndef RMBX_H_
+#define RMBX_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define RMBX_OK 0
+#define RMBX_ERR_ARG -1   /* bad argument (maps to Python ValueError) */
+#define RMBX_ERR_HIP -2   /* HIP runtime failure (maps to Python RuntimeError) */
+#define RMBX_ERR_STATE -3 /* engine used in a wrong state */
+
+#define RMBX_ABI_VERSION 1
+
+/* ---------------------------------------------------------------------------------------------
+ * Library
+ * ------------------------------------------------------------------------------------------- */
+int rmbx_abi_version(void);
+const char* rmbx_last_error(void);
+/* Number of visible HIP devices (0 when none). Does not create a context. */
+int rmbx_device_count(int* count);
+
+/* ---------------------------------------------------------------------------------------------
+ * ACT temporal ensembling + action denormalisation, batched over envs.
+ * Replaces policy/act/RolloutAct.py:68-101 (infer_policy: history append/pop at
+ * chunk_size, exponential weights k = 0.01, newest-first accumulation, and the
+ * --no_temp_ensem pop(0) path) followed by common/utils/DataUtils.py:26-40 (denormalize_data).
+ *
+ * hist        f32 [n_env][chunk][chunk][adim]  per-env ring of past chunks (engine-owned layout)
+ * hist_len    i32 [n_env]  number of valid chunks in the ring (TE) / rows left (no TE)
+ * hist_head   i32 [n_env]  ring slot of the oldest chunk (TE) / next row to pop (no TE)
+ * new_chunk   f32 [n_env][chunk][adim]  policy output of this call (read where push != 0)
+ * push        u8  [n_env]  1 = append new_chunk (TE) / reload the buffer (no TE); NULL = all 1
+ * active      u8  [n_env]  0 = env untouched this call; NULL = all active
+ * w_table     f64 [chunk][chunk]  w_table[n-1][i] = exp(-k i) / sum_j exp(-k j), i < n,
+ *             built on the host with numpy exactly as RolloutAct.py:90-92 (bit-exact weights)
+ * dn_scale, dn_sub, dn_add  f64 [adim]: out = dn_scale * (a - dn_sub) + dn_add
+ *             (gaussian: std, 0, mean; limits: range/(out_max-out_min), out_min, min)
+ * out         f64 [n_env][adim]  denormalised action (RolloutAct.py:98 self.policy_action)
+ * Arithmetic: f64, no contraction, reference order (bit-exact vs the reference on golden data).
+ * ------------------------------------------------------------------------------------------- */
+int rmbx_act_ensemble(const float* new_chunk, const uint8_t* push, const uint8_t* active,
+                      float* hist, int32_t* hist_len, int32_t* hist_head,
+                      const double* w_table, const double* dn_scale, const double* dn_sub,
+                      const double* dn_add, double* out, int n_env, int chunk, int adim,
+                      int temporal_ensemble, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Cable-threading success predicate, batched.
+ * Replaces envs/mujoco/ur5e/MujocoUR5eCableEnv.py:48-105 (_get_reward).
+ * cable_xpos f64 [n_env][n_cable][3] (cable_B0..B{n_cable-1} in body-id order),
+ * end_xpos / pole1_xpos / pole2_xpos f64 [n_env][3]; reward f64 [n_env] in {0, 1}.
+ * Bit-exact flags: same f64 comparisons, no contraction, NaN behaviour of numpy max.
+ * ------------------------------------------------------------------------------------------- */
+int rmbx_cable_reward(const double* cable_xpos, const double* end_xpos,
+                      const double* pole1_xpos, const double* pole2_xpos, double* reward,
+                      int n_env, int n_cable, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * UR5e observation mapping, batched.
+ * Replaces envs/mujoco/ur5e/MujocoUR5eEnvBase.py:78-119 (_get_obs):
+ * joint_pos = [6 arm qpos, rad2deg(mean(4 gripper qpos)) / 45 * 255], joint_vel = [6 arm qvel, 0],
+ * wrench = [force(3), torque(3)].
+ * arm_qpos, arm_qvel f64 [n][6]; grip_qpos f64 [n][4] (right_driver, right_spring_link,
+ * left_driver, left_spring_link); force, torque f64 [n][3].
+ * ------------------------------------------------------------------------------------------- */
+int rmbx_ur5e_obs(const double* arm_qpos, const double* arm_qvel, const double* grip_qpos,
+                  const double* force, const double* torque, double* joint_pos,
+                  double* joint_vel, double* wrench, int n_env, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * OpenGL depth-buffer linearisation, batched (f32, numpy NEP-50 semantics).
+ * Replaces envs/mujoco/MujocoEnvBase.py:122-125: depth = near / (1 - z * (1 - near / far)),
+ * near = znear * extent, far = zfar * extent.
+ * ------------------------------------------------------------------------------------------- */
+int rmbx_depth_linearize(const float* zbuf, float* depth, size_t n_pix, double near_,
+                         double far_, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Rollout phase schedule, batched state machine.
+ * Replaces the per-step check_transition/post_update of common/base/RolloutBase.py:28-132
+ * (InitialRolloutPhase, RolloutPhase with --auto_exit, EndRolloutPhase) and the timed
+ * pre-motion phases of common/base/PhaseBase.py:41-106 under
+ * common/manager/PhaseManager.py:20-37, driven by the env clock (MujocoEnvBase.py:201-203).
+ * Called once per env-step AFTER the physics step with that step's sim time and reward.
+ *
+ * pre_durations f64 [n_pre]: durations of the phases before RolloutPhase (Initial first);
+ * phase index n_pre = RolloutPhase, n_pre + 1 = EndRolloutPhase.
+ * ------------------------------------------------------------------------------------------- */
+typedef struct rmbx_sched_t {
+  int32_t phase;            /* current phase index */
+  int32_t rollout_time_idx; /* RolloutBase.py:47,70 */
+  uint8_t done;             /* EndRolloutPhase reached and episode finished */
+  uint8_t success;          /* result["success"] */
+  uint8_t has_success_time; /* success_time is not None */
+  uint8_t pad_[5];
+  double phase_start;   /* PhaseBase.start_time */
+  double success_time;  /* RolloutPhase.success_time (valid if has_success_time) */
+  double result_reward; /* result["reward"] */
+  double duration;      /* result["duration"] */
+} rmbx_sched_t;
+
+int rmbx_sched_reset(rmbx_sched_t* sched, const double* time, const uint8_t* mask, int n_env,
+                     void* stream);
+int rmbx_sched_update(rmbx_sched_t* sched, const double* time, const double* reward,
+                      const double* pre_durations, int n_pre, double max_duration,
+                      double post_success_duration, int n_env, void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* RMBX_H_ */

@@ -1,0 +1,107 @@
+"""ctypes binding of the C ABI declared in include/rmbx.h (librmbx.so, built in-tree for gfx950).
+
+This is the only route from Python to the HIP kernels.  It fails loudly: if the library is
+missing or a symbol is absent, importing a function raises; there is no CPU fallback on the
+product path.
+"""
+
+import ctypes
+import os
+
+import numpy as np
+
+_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "librmbx.so")
+
+_c_int = ctypes.c_int
+_c_p = ctypes.c_void_p
+_c_sz = ctypes.c_size_t
+_c_d = ctypes.c_double
+
+# name -> (restype, argtypes).  Must list every function declared in include/rmbx.h.
+SIGNATURES = {
+    "rmbx_abi_version": (_c_int, []),
+    "rmbx_last_error": (ctypes.c_char_p, []),
+    "rmbx_device_count": (_c_int, [_c_p]),
+    "rmbx_act_ensemble": (
+        _c_int,
+        [_c_p] * 11 + [_c_int, _c_int, _c_int, _c_int, _c_p],
+    ),
+    "rmbx_cable_reward": (_c_int, [_c_p] * 5 + [_c_int, _c_int, _c_p]),
+    "rmbx_ur5e_obs": (_c_int, [_c_p] * 8 + [_c_int, _c_p]),
+    "rmbx_depth_linearize": (_c_int, [_c_p, _c_p, _c_sz, _c_d, _c_d, _c_p]),
+    "rmbx_sched_reset": (_c_int, [_c_p, _c_p, _c_p, _c_int, _c_p]),
+    "rmbx_sched_update": (_c_int, [_c_p, _c_p, _c_p, _c_p, _c_int, _c_d, _c_d, _c_int, _c_p]),
+}
+
+# numpy mirror of rmbx_sched_t (include/rmbx.h)
+SCHED_DTYPE = np.dtype(
+    [
+        ("phase", np.int32),
+        ("rollout_time_idx", np.int32),
+        ("done", np.uint8),
+        ("success", np.uint8),
+        ("has_success_time", np.uint8),
+        ("pad_", np.uint8, 5),
+        ("phase_start", np.float64),
+        ("success_time", np.float64),
+        ("result_reward", np.float64),
+        ("duration", np.float64),
+    ]
+)
+assert SCHED_DTYPE.itemsize == 48
+
+_lib = None
+
+
+class RmbxError(RuntimeError):
+    pass
+
+
+def lib_path():
+    return _LIB_PATH
+
+
+def load():
+    """Load librmbx.so (raises if it has not been built)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(_LIB_PATH):
+        raise RmbxError(
+            f"{_LIB_PATH} not found: build it with `python -c 'import __graft_entry__ as g; g.build()'`"
+        )
+    lib = ctypes.CDLL(_LIB_PATH)
+    for name, (res, args) in SIGNATURES.items():
+        fn = getattr(lib, name)  # AttributeError if the symbol is missing: fail loudly
+        fn.restype = res
+        fn.argtypes = args
+    _lib = lib
+    return lib
+
+
+def check(status):
+    if status != 0:
+        msg = load().rmbx_last_error().decode(errors="replace")
+        if status == -1:
+            raise ValueError(msg)
+        raise RmbxError(f"rmbx error {status}: {msg}")
+
+
+def call(name, *args):
+    check(getattr(load(), name)(*args))
+
+
+def ptr(t):
+    """Device (or host) pointer of a torch tensor / numpy array, or None."""
+    if t is None:
+        return None
+    if hasattr(t, "data_ptr"):
+        return t.data_ptr()
+    return t.ctypes.data
+
+
+def stream_ptr(stream=None):
+    import torch
+
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream

@@ -1,0 +1,201 @@
+"""Torch-facing wrappers of the rmbx C ABI glue kernels (shape/dtype checks + launch).
+
+All tensors must be CUDA (HIP) tensors, contiguous, with the dtypes named below; work is
+enqueued on the current torch stream.  Shape errors raise ValueError, as the reference's
+MotionManager/DataKey do for bad keys (common/manager/MotionManager.py:36-39).
+"""
+
+import numpy as np
+import torch
+
+from . import _native as N
+
+
+def _chk(t, dtype, shape=None, name="tensor"):
+    if not isinstance(t, torch.Tensor):
+        raise ValueError(f"{name} must be a torch.Tensor")
+    if not t.is_cuda:
+        raise ValueError(f"{name} must be a device tensor (got {t.device})")
+    if t.dtype != dtype:
+        raise ValueError(f"{name} must be {dtype} (got {t.dtype})")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if shape is not None and tuple(t.shape) != tuple(shape):
+        raise ValueError(f"{name} must have shape {tuple(shape)} (got {tuple(t.shape)})")
+    return t
+
+
+# ------------------------------------------------------------------------------------------
+# ACT temporal ensemble
+# ------------------------------------------------------------------------------------------
+def ensemble_weight_table(chunk, k=0.01):
+    """w[n-1, i] for n = 1..chunk: the weights of RolloutAct.py:90-92, computed with numpy
+    exactly as the reference does (np.exp then division by the pairwise np.sum)."""
+    w = np.zeros((chunk, chunk), dtype=np.float64)
+    for n in range(1, chunk + 1):
+        e = np.exp(-k * np.arange(n))
+        w[n - 1, :n] = e / e.sum()
+    return w
+
+
+def denorm_coeffs(stats):
+    """(scale, sub, add) such that denormalize_data(a) == scale * (a - sub) + add bit-exactly
+    (common/utils/DataUtils.py:26-40)."""
+    norm_type = stats["norm_config"]["type"] if "norm_config" in stats else "gaussian"
+    if norm_type == "gaussian":
+        std = np.asarray(stats["std"], dtype=np.float64)
+        return std, np.zeros_like(std), np.asarray(stats["mean"], dtype=np.float64)
+    if norm_type == "limits":
+        cfg = stats["norm_config"]
+        rng = np.asarray(stats["range"], dtype=np.float64)
+        scale = rng / (cfg["out_max"] - cfg["out_min"])
+        return scale, np.full_like(rng, cfg["out_min"]), np.asarray(stats["min"], dtype=np.float64)
+    raise ValueError(f"[denormalize_data] Invalid normalization type: {norm_type}")
+
+
+def norm_coeffs(stats):
+    """(scale, sub, add) with normalize_data(x) == (x - sub) * or / ... see DataUtils.py:9-24.
+    Returned as the pair used by the device path: gaussian -> ((x - mean) / std),
+    limits -> scale * (x - min) + out_min."""
+    norm_type = stats["norm_config"]["type"] if "norm_config" in stats else "gaussian"
+    if norm_type == "gaussian":
+        return "gaussian", np.asarray(stats["mean"], np.float64), np.asarray(stats["std"], np.float64)
+    if norm_type == "limits":
+        cfg = stats["norm_config"]
+        scale = (cfg["out_max"] - cfg["out_min"]) / np.asarray(stats["range"], np.float64)
+        return "limits", np.asarray(stats["min"], np.float64), (scale, cfg["out_min"])
+    raise ValueError(f"[normalize_data] Invalid normalization type: {norm_type}")
+
+
+class ActEnsembleState:
+    """Per-env chunk history ring for the batched RolloutAct.infer_policy."""
+
+    def __init__(self, n_env, chunk, adim, stats, device, temporal_ensemble=True, k=0.01):
+        self.n_env, self.chunk, self.adim = n_env, chunk, adim
+        self.te = bool(temporal_ensemble)
+        self.hist = torch.zeros((n_env, chunk if self.te else 1, chunk, adim), dtype=torch.float32, device=device)
+        self.len = torch.zeros(n_env, dtype=torch.int32, device=device)
+        self.head = torch.zeros(n_env, dtype=torch.int32, device=device)
+        self.w = torch.tensor(ensemble_weight_table(chunk, k), device=device)
+        sc, sb, ad = denorm_coeffs(stats)
+        self.dn = [torch.tensor(x, dtype=torch.float64, device=device).contiguous() for x in (sc, sb, ad)]
+        self.out = torch.zeros((n_env, adim), dtype=torch.float64, device=device)
+
+    def reset(self, mask=None):
+        if mask is None:
+            self.len.zero_()
+            self.head.zero_()
+        else:
+            m = mask.bool()
+            self.len[m] = 0
+            self.head[m] = 0
+
+    def __call__(self, new_chunk, push=None, active=None):
+        act_ensemble(
+            new_chunk, push, active, self.hist, self.len, self.head, self.w, *self.dn, self.out,
+            temporal_ensemble=self.te,
+        )
+        return self.out
+
+
+def act_ensemble(new_chunk, push, active, hist, hist_len, hist_head, w_table, dn_scale, dn_sub,
+                 dn_add, out, temporal_ensemble=True):
+    n_env, adim = out.shape
+    chunk = w_table.shape[0]
+    _chk(out, torch.float64, name="out")
+    if temporal_ensemble:
+        _chk(hist, torch.float32, (n_env, chunk, chunk, adim), "hist")
+    else:
+        _chk(hist, torch.float32, (n_env, 1, chunk, adim), "hist")
+    _chk(hist_len, torch.int32, (n_env,), "hist_len")
+    _chk(hist_head, torch.int32, (n_env,), "hist_head")
+    _chk(w_table, torch.float64, (chunk, chunk), "w_table")
+    for t, nm in ((dn_scale, "dn_scale"), (dn_sub, "dn_sub"), (dn_add, "dn_add")):
+        _chk(t, torch.float64, (adim,), nm)
+    if new_chunk is not None:
+        _chk(new_chunk, torch.float32, (n_env, chunk, adim), "new_chunk")
+    if push is not None:
+        _chk(push, torch.uint8, (n_env,), "push")
+    if active is not None:
+        _chk(active, torch.uint8, (n_env,), "active")
+    if new_chunk is None and (push is None or bool(push.any())):
+        raise ValueError("new_chunk is required when pushing")
+    N.call(
+        "rmbx_act_ensemble", N.ptr(new_chunk), N.ptr(push), N.ptr(active), N.ptr(hist),
+        N.ptr(hist_len), N.ptr(hist_head), N.ptr(w_table), N.ptr(dn_scale), N.ptr(dn_sub),
+        N.ptr(dn_add), N.ptr(out), n_env, chunk, adim, int(temporal_ensemble), N.stream_ptr(),
+    )
+    return out
+
+
+# ------------------------------------------------------------------------------------------
+# Cable success predicate, UR5e observation, depth linearisation
+# ------------------------------------------------------------------------------------------
+def cable_reward(cable_xpos, end_xpos, pole1, pole2, out=None):
+    n, nc, _ = cable_xpos.shape
+    _chk(cable_xpos, torch.float64, (n, nc, 3), "cable_xpos")
+    for t, nm in ((end_xpos, "end_xpos"), (pole1, "pole1"), (pole2, "pole2")):
+        _chk(t, torch.float64, (n, 3), nm)
+    if out is None:
+        out = torch.empty(n, dtype=torch.float64, device=cable_xpos.device)
+    _chk(out, torch.float64, (n,), "reward")
+    N.call("rmbx_cable_reward", N.ptr(cable_xpos), N.ptr(end_xpos), N.ptr(pole1), N.ptr(pole2),
+           N.ptr(out), n, nc, N.stream_ptr())
+    return out
+
+
+def ur5e_obs(arm_qpos, arm_qvel, grip_qpos, force, torque):
+    n = arm_qpos.shape[0]
+    _chk(arm_qpos, torch.float64, (n, 6), "arm_qpos")
+    _chk(arm_qvel, torch.float64, (n, 6), "arm_qvel")
+    _chk(grip_qpos, torch.float64, (n, 4), "grip_qpos")
+    _chk(force, torch.float64, (n, 3), "force")
+    _chk(torque, torch.float64, (n, 3), "torque")
+    dev = arm_qpos.device
+    jp = torch.empty((n, 7), dtype=torch.float64, device=dev)
+    jv = torch.empty((n, 7), dtype=torch.float64, device=dev)
+    wr = torch.empty((n, 6), dtype=torch.float64, device=dev)
+    N.call("rmbx_ur5e_obs", N.ptr(arm_qpos), N.ptr(arm_qvel), N.ptr(grip_qpos), N.ptr(force),
+           N.ptr(torque), N.ptr(jp), N.ptr(jv), N.ptr(wr), n, N.stream_ptr())
+    return jp, jv, wr
+
+
+def depth_linearize(zbuf, near, far, out=None):
+    _chk(zbuf, torch.float32, None, "zbuf")
+    if out is None:
+        out = torch.empty_like(zbuf)
+    _chk(out, torch.float32, tuple(zbuf.shape), "depth")
+    N.call("rmbx_depth_linearize", N.ptr(zbuf), N.ptr(out), zbuf.numel(), float(near), float(far),
+           N.stream_ptr())
+    return out
+
+
+# ------------------------------------------------------------------------------------------
+# Phase schedule
+# ------------------------------------------------------------------------------------------
+def sched_alloc(n_env, device):
+    return torch.zeros((n_env, N.SCHED_DTYPE.itemsize), dtype=torch.uint8, device=device)
+
+
+def sched_view(sched_u8):
+    """Host numpy structured view of a sched buffer (copies to host)."""
+    return sched_u8.cpu().numpy().view(N.SCHED_DTYPE).reshape(-1)
+
+
+def sched_reset(sched, time, mask=None):
+    n = sched.shape[0]
+    _chk(sched, torch.uint8, (n, N.SCHED_DTYPE.itemsize), "sched")
+    _chk(time, torch.float64, (n,), "time")
+    if mask is not None:
+        _chk(mask, torch.uint8, (n,), "mask")
+    N.call("rmbx_sched_reset", N.ptr(sched), N.ptr(time), N.ptr(mask), n, N.stream_ptr())
+
+
+def sched_update(sched, time, reward, pre_durations, max_duration, post_success=1.0):
+    n = sched.shape[0]
+    _chk(sched, torch.uint8, (n, N.SCHED_DTYPE.itemsize), "sched")
+    _chk(time, torch.float64, (n,), "time")
+    _chk(reward, torch.float64, (n,), "reward")
+    _chk(pre_durations, torch.float64, None, "pre_durations")
+    N.call("rmbx_sched_update", N.ptr(sched), N.ptr(time), N.ptr(reward), N.ptr(pre_durations),
+           pre_durations.numel(), float(max_duration), float(post_success), n, N.stream_ptr())

@@ -1,0 +1,566 @@
+"""Mint golden fixtures from the reference's OWN hot-path Python (run in the build container only).
+
+This script is test infrastructure. It imports selected modules of the reference checkout at
+/root/reference (read-only) with stub modules standing in for absent, uncalled dependencies
+(cv2, gymnasium, mujoco name lookup, pinocchio SE3 container, torchvision transforms, the ACT
+submodule), drives the reference functions on seeded synthetic inputs, and writes the inputs
+and the reference's outputs as small .npz files under tests/golden/.  Only the .npz data ships;
+no reference source or bytecode is copied (sys.dont_write_bytecode is set).
+
+Functions exercised (reference file:line):
+  * RolloutAct.infer_policy temporal ensemble      policy/act/RolloutAct.py:68-101
+  * normalize_data / denormalize_data              common/utils/DataUtils.py:9-40
+  * MujocoUR5eCableEnv._get_reward                 envs/mujoco/ur5e/MujocoUR5eCableEnv.py:48-105
+  * MujocoUR5eEnvBase._get_obs gripper mapping     envs/mujoco/ur5e/MujocoUR5eEnvBase.py:78-119
+  * MujocoEnvBase._get_info depth linearisation    envs/mujoco/MujocoEnvBase.py:103-126
+  * convert_depth_image_to_pointcloud              common/utils/VisionUtils.py:55-87
+  * crop_pointcloud_bb                             common/utils/Vision3dUtils.py:6-14
+  * Phase schedule (Initial/Reach1/Reach2/Grasp/Rollout/End under PhaseManager)
+                                                   common/base/RolloutBase.py:28-132, 387-415,
+                                                   common/base/PhaseBase.py:9-106,
+                                                   envs/operation/OperationMujocoUR5eCable.py:8-47
+
+Usage:  python tools/gen_golden.py  (writes tests/golden/*.npz)
+"""
+
+import os
+import sys
+import types
+
+import numpy as np
+
+sys.dont_write_bytecode = True
+
+REF = "/root/reference"
+OUT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "..", "tests", "golden")
+
+
+# --------------------------------------------------------------------------------------------
+# Stub modules for dependencies that are absent here and not called on the exercised paths
+# --------------------------------------------------------------------------------------------
+def _mod(name, **attrs):
+    m = types.ModuleType(name)
+    for k, v in attrs.items():
+        setattr(m, k, v)
+    sys.modules[name] = m
+    return m
+
+
+def install_stubs():
+    _mod("cv2", waitKey=lambda *_: -1, imshow=lambda *a: None)
+
+    class _SE3:
+        def __init__(self, rot, pos):
+            self.rotation = np.array(rot, dtype=np.float64)
+            self.translation = np.array(pos, dtype=np.float64)
+
+    _mod("pinocchio", SE3=_SE3)
+
+    class _ObjEnum:
+        mjOBJ_BODY = 1
+        mjOBJ_GEOM = 5
+        mjOBJ_CAMERA = 7
+        mjOBJ_SENSOR = 8
+
+    class _SensEnum:
+        mjSENS_PLUGIN = 99
+
+    _mod(
+        "mujoco",
+        mjtObj=_ObjEnum,
+        mjtSensor=_SensEnum,
+        mj_id2name=lambda model, obj, i: model._id2name(obj, i),
+        mj_name2id=lambda model, obj, name: model._name2id(obj, name),
+    )
+    gym = _mod("gymnasium", make=lambda *a, **k: None)
+    gym.__path__ = []
+    spaces = _mod("gymnasium.spaces", Box=lambda *a, **k: None, Dict=lambda *a, **k: None)
+    gym.spaces = spaces
+    envs = _mod("gymnasium.envs")
+    envs.__path__ = []
+    class _MujocoEnv:
+        pass
+
+    mj = _mod("gymnasium.envs.mujoco", MujocoEnv=_MujocoEnv)
+    mj.__path__ = []
+    _mod("gymnasium.envs.mujoco.mujoco_rendering", OffScreenViewer=object)
+    _mod("gymnasium.envs.registration", register=lambda **k: None)
+
+    tv = _mod("torchvision")
+    tv.__path__ = []
+    tr = _mod("torchvision.transforms")
+    tr.__path__ = []
+    _mod("torchvision.transforms.v2", ToDtype=lambda *a, **k: (lambda x: x))
+
+    detr = _mod("detr")
+    detr.__path__ = []
+    dm = _mod("detr.models")
+    dm.__path__ = []
+    _mod("detr.models.detr_vae", DETRVAE=object)
+    _mod("policy", ACTPolicy=object)
+    _mod("pytorch3d")
+    _mod("pytorch3d.ops")
+
+    # The reference package as a bare namespace (its __init__ imports training/teleop deps).
+    rmb = _mod("robo_manip_baselines", __version__="2.0.0")
+    rmb.__path__ = [os.path.join(REF, "robo_manip_baselines")]
+    common = _mod("robo_manip_baselines.common")
+    common.__path__ = [os.path.join(REF, "robo_manip_baselines", "common")]
+    teleop = _mod(
+        "robo_manip_baselines.teleop",
+        GelloInputDevice=object,
+        KeyboardInputDevice=object,
+        SpacemouseInputDevice=object,
+    )
+    teleop.__path__ = []
+    envs_pkg = _mod("robo_manip_baselines.envs")
+    envs_pkg.__path__ = [os.path.join(REF, "robo_manip_baselines", "envs")]
+    envs_mj = _mod("robo_manip_baselines.envs.mujoco")
+    envs_mj.__path__ = [os.path.join(REF, "robo_manip_baselines", "envs", "mujoco")]
+    envs_op = _mod("robo_manip_baselines.envs.operation")
+    envs_op.__path__ = [os.path.join(REF, "robo_manip_baselines", "envs", "operation")]
+    pol = _mod("robo_manip_baselines.policy")
+    pol.__path__ = [os.path.join(REF, "robo_manip_baselines", "policy")]
+    act = _mod("robo_manip_baselines.policy.act")
+    act.__path__ = [os.path.join(REF, "robo_manip_baselines", "policy", "act")]
+    ur5e = _mod("robo_manip_baselines.envs.mujoco.ur5e")
+    ur5e.__path__ = [os.path.join(REF, "robo_manip_baselines", "envs", "mujoco", "ur5e")]
+
+    import importlib
+
+    DataKey = importlib.import_module("robo_manip_baselines.common.data.DataKey").DataKey
+    EnvDataMixin = importlib.import_module(
+        "robo_manip_baselines.common.data.EnvDataMixin"
+    ).EnvDataMixin
+    du = importlib.import_module("robo_manip_baselines.common.utils.DataUtils")
+    common.DataKey = DataKey
+    common.EnvDataMixin = EnvDataMixin
+    common.normalize_data = du.normalize_data
+    common.denormalize_data = du.denormalize_data
+
+    # ArmManager imports pinocchio-backed MathUtils helpers at module level only.
+    arm = importlib.import_module("robo_manip_baselines.common.body.ArmManager")
+    common.ArmConfig = arm.ArmConfig
+    common.ArmManager = arm.ArmManager
+    pb = importlib.import_module("robo_manip_baselines.common.base.PhaseBase")
+    common.PhaseBase = pb.PhaseBase
+    common.ReachPhaseBase = pb.ReachPhaseBase
+    common.GraspPhaseBase = pb.GraspPhaseBase
+    pm = importlib.import_module("robo_manip_baselines.common.manager.PhaseManager")
+    common.PhaseManager = pm.PhaseManager
+    rb = importlib.import_module("robo_manip_baselines.common.base.RolloutBase")
+    common.RolloutBase = rb.RolloutBase
+    vu = importlib.import_module("robo_manip_baselines.common.utils.VisionUtils")
+    common.convert_depth_image_to_pointcloud = vu.convert_depth_image_to_pointcloud
+    return importlib
+
+
+# --------------------------------------------------------------------------------------------
+# Fixture builders
+# --------------------------------------------------------------------------------------------
+def gen_ensemble(importlib):
+    """RolloutAct.infer_policy (policy/act/RolloutAct.py:68-101) on synthetic chunks."""
+    RolloutAct = importlib.import_module("robo_manip_baselines.policy.act.RolloutAct").RolloutAct
+
+    rng = np.random.default_rng(1234)
+    out = {}
+    cases = [
+        ("gauss_te", False, "gaussian", 130, 100),
+        ("gauss_te_chunk20", False, "gaussian", 45, 20),
+        ("limits_te", False, "limits", 110, 100),
+        ("gauss_no_te", True, "gaussian", 30, 100),
+    ]
+    for name, no_te, norm, n_calls, chunk in cases:
+        A = 7
+        chunks = rng.standard_normal((n_calls, chunk, A)).astype(np.float32)
+        mean = rng.standard_normal(A)
+        std = np.abs(rng.standard_normal(A)) + 0.1
+        if norm == "gaussian":
+            stats = {"norm_config": {"type": "gaussian"}, "mean": mean, "std": std}
+        else:
+            mn = rng.standard_normal(A)
+            rg = np.abs(rng.standard_normal(A)) + 0.2
+            stats = {
+                "norm_config": {"type": "limits", "out_min": -1.0, "out_max": 1.0},
+                "min": mn,
+                "range": rg,
+            }
+            mean, std = mn, rg  # stored for the oracle: min / range
+        op = object.__new__(RolloutAct)
+        op.args = types.SimpleNamespace(no_temp_ensem=no_te)
+        op.model_meta_info = {"data": {"chunk_size": chunk}, "action": stats}
+        op.action_dim = A
+        op.policy_action_list = np.empty((0, A))
+        op.policy_action_buf = []
+        op.policy_action_buf_history = []
+        call = {"i": 0}
+
+        class _T:
+            def __init__(self, a):
+                self.a = a
+
+            def cpu(self):
+                return self
+
+            def detach(self):
+                return self
+
+            def numpy(self):
+                return self.a
+
+        def _policy(state, images, _c=call, _chunks=chunks):
+            a = _chunks[_c["i"]]
+            _c["i"] += 1
+            return [_T(a)]
+
+        op.get_state = lambda: None
+        op.get_images = lambda: None
+        op.policy = _policy
+        actions = []
+        for i in range(n_calls):
+            op.infer_policy()
+            actions.append(op.policy_action.copy())
+        out[name] = dict(
+            chunks=chunks,
+            mean=mean,
+            std=std,
+            norm_limits=np.int32(norm == "limits"),
+            no_temp_ensem=np.int32(no_te),
+            chunk_size=np.int32(chunk),
+            actions=np.array(actions),
+        )
+    for name, d in out.items():
+        np.savez(os.path.join(OUT, f"ensemble_{name}.npz"), **d)
+    print("ensemble:", list(out))
+
+
+class _FakeModel:
+    def __init__(self, body_names, geom_names):
+        self.body_names = body_names
+        self.geom_names = geom_names
+        self.nbody = len(body_names)
+
+    def _id2name(self, obj, i):
+        return self.body_names[i]
+
+    def _name2id(self, obj, name):
+        return self.body_names.index(name)
+
+
+def gen_reward(importlib):
+    """MujocoUR5eCableEnv._get_reward (MujocoUR5eCableEnv.py:48-105) on synthetic cables."""
+    Env = importlib.import_module(
+        "robo_manip_baselines.envs.mujoco.ur5e.MujocoUR5eCableEnv"
+    ).MujocoUR5eCableEnv
+    # body-id order: world, some robot bodies, cable_B0..B24, cable_end, poles
+    body_names = ["world", "ur5e_root_frame", "base"] + [f"cable_B{i}" for i in range(25)]
+    body_names += ["cable_end", "poles"]
+    rng = np.random.default_rng(777)
+    N = 2048
+    cable = np.zeros((N, 25, 3))
+    cable_end = np.zeros((N, 3))
+    pole1 = np.zeros((N, 3))
+    pole2 = np.zeros((N, 3))
+    rewards = np.zeros(N)
+    for n in range(N):
+        p1 = np.array([-0.1, 0.1, 0.845]) + rng.uniform(-0.05, 0.15, 3) * [1, 1, 0.1]
+        p2 = p1 + np.array([0.05, 0.0, 0.0])
+        kind = n % 8
+        # Random polyline with one segment k forced to cross the pole1-pole2 segment.
+        k = int(rng.integers(0, 24))
+        mid = p1[:2] + rng.uniform(0.05, 0.95) * (p2[:2] - p1[:2])
+        sgn = 1.0 if rng.random() < 0.7 else -1.0
+        d = np.array([rng.normal(0, 0.006), sgn * rng.uniform(0.01, 0.02)])
+        pts = np.zeros((25, 3))
+        pts[k, :2] = mid - d * rng.uniform(0.2, 0.8)
+        pts[k + 1, :2] = pts[k, :2] + d
+        for i in range(k - 1, -1, -1):
+            step = rng.normal(0, 1, 2)
+            step = 0.02 * step / np.linalg.norm(step)
+            pts[i, :2] = pts[i + 1, :2] - np.abs(step) * [0.3, 1.0] * sgn * [1, 1]
+        for i in range(k + 2, 25):
+            step = rng.normal(0, 1, 2)
+            step = 0.02 * step / np.linalg.norm(step)
+            pts[i, :2] = pts[i - 1, :2] + step
+        pts[:, 2] = p1[2] - 0.02 + rng.normal(0, 0.003, 25)
+        if kind == 1:
+            pts[rng.integers(25), 2] = p1[2] + 0.05  # too high
+        if kind == 2:
+            pts = pts[::-1].copy()  # reversed traversal flips the crossing sign
+        if kind == 6:
+            pts[10] = pts[11]  # degenerate zero-length segment
+        end = np.array(
+            [p2[0] + rng.uniform(-0.02, 0.1), p1[1] - 0.05 + rng.uniform(-0.1, 0.03), p1[2]]
+        )
+        if kind == 5:
+            # exactly-on-threshold values exercise the strict/non-strict comparisons
+            end[0] = p2[0]
+            end[1] = p1[1] - 0.05
+            pts[3, 2] = p1[2] + 0.01
+        if kind == 7:
+            end[0] = p2[0] - 1e-12
+        cable[n], cable_end[n], pole1[n], pole2[n] = pts, end, p1, p2
+        env = object.__new__(Env)
+        env.model = _FakeModel(body_names, ["pole1", "pole2"])
+        xpos = np.zeros((len(body_names), 3))
+        xpos[3:28] = pts
+        xpos[28] = end
+        geoms = {"pole1": p1, "pole2": p2}
+        env.data = types.SimpleNamespace(
+            xpos=xpos, geom=lambda nm, _g=geoms: types.SimpleNamespace(xpos=_g[nm])
+        )
+        env.cable_body_ids = None
+        rewards[n] = env._get_reward()
+    np.savez(
+        os.path.join(OUT, "reward_cable.npz"),
+        cable=cable,
+        cable_end=cable_end,
+        pole1=pole1,
+        pole2=pole2,
+        reward=rewards,
+    )
+    print("reward: positives", int(rewards.sum()), "of", N)
+
+
+def gen_obs(importlib):
+    """MujocoUR5eEnvBase._get_obs (MujocoUR5eEnvBase.py:78-119)."""
+    Base = importlib.import_module(
+        "robo_manip_baselines.envs.mujoco.ur5e.MujocoUR5eEnvBase"
+    ).MujocoUR5eEnvBase
+    # concrete subclass: modify_world is abstract and not on the exercised path
+    Base = type("ObsOnly", (Base,), {"modify_world": lambda self, *a, **k: None})
+    names = [
+        "shoulder_pan_joint",
+        "shoulder_lift_joint",
+        "elbow_joint",
+        "wrist_1_joint",
+        "wrist_2_joint",
+        "wrist_3_joint",
+        "right_driver_joint",
+        "right_spring_link_joint",
+        "left_driver_joint",
+        "left_spring_link_joint",
+    ]
+    rng = np.random.default_rng(99)
+    N = 512
+    qpos = rng.uniform(-3.5, 3.5, (N, 10))
+    qvel = rng.normal(0, 2, (N, 10))
+    force = rng.normal(0, 5, (N, 3))
+    torque = rng.normal(0, 1, (N, 3))
+    jp, jv, wr = [], [], []
+    for n in range(N):
+        env = object.__new__(Base)
+        qp = dict(zip(names, qpos[n]))
+        qv = dict(zip(names, qvel[n]))
+        sens = {"force_sensor": force[n], "torque_sensor": torque[n]}
+        env.data = types.SimpleNamespace(
+            joint=lambda nm, _p=qp, _v=qv: types.SimpleNamespace(
+                qpos=np.array([_p[nm]]), qvel=np.array([_v[nm]])
+            ),
+            sensor=lambda nm, _s=sens: types.SimpleNamespace(data=np.array(_s[nm])),
+        )
+        o = env._get_obs()
+        jp.append(o["joint_pos"])
+        jv.append(o["joint_vel"])
+        wr.append(o["wrench"])
+    np.savez(
+        os.path.join(OUT, "obs_ur5e.npz"),
+        qpos=qpos,
+        qvel=qvel,
+        force=force,
+        torque=torque,
+        joint_pos=np.array(jp),
+        joint_vel=np.array(jv),
+        wrench=np.array(wr),
+    )
+    print("obs: ok")
+
+
+def gen_depth_and_pointcloud(importlib):
+    """_get_info depth linearisation (MujocoEnvBase.py:103-126) + depth->pointcloud + crop."""
+    Base = importlib.import_module("robo_manip_baselines.envs.mujoco.MujocoEnvBase").MujocoEnvBase
+    vu = importlib.import_module("robo_manip_baselines.common.utils.VisionUtils")
+    v3 = importlib.import_module("robo_manip_baselines.common.utils.Vision3dUtils")
+    Base = type(
+        "InfoOnly",
+        (Base,),
+        {k: (lambda self, *a, **kw: None) for k in ("_get_obs", "modify_world", "setup_robot")},
+    )
+    rng = np.random.default_rng(5)
+    H, W = 48, 64
+    zbuf = rng.uniform(0.0, 1.0, (H, W)).astype(np.float32)
+    zbuf[0, :5] = 1.0  # far plane
+    zbuf[1, :5] = 0.0  # near plane
+    rgb = rng.integers(0, 256, (H, W, 3), dtype=np.uint8)
+    env = object.__new__(Base)
+    env.cameras = {
+        "front": {
+            "id": 0,
+            "viewer": types.SimpleNamespace(
+                make_context_current=lambda: None,
+                render=lambda render_mode, camera_id: rgb if render_mode == "rgb_array" else zbuf,
+            ),
+        }
+    }
+    env.model = types.SimpleNamespace(
+        stat=types.SimpleNamespace(extent=2.0),
+        vis=types.SimpleNamespace(map=types.SimpleNamespace(znear=0.01, zfar=50.0)),
+    )
+    env.intensity_tactile_names = []
+    info = env._get_info()
+    depth = info["depth_images"]["front"]
+    fovy = 45.0
+    xyz, col = vu.convert_depth_image_to_pointcloud(
+        depth.astype(np.float32), fovy, rgb_image=rgb, near_clip=0.05, far_clip=2.0
+    )
+    pc = np.concatenate([xyz, col], axis=1)
+    lo, hi = np.array([-0.4, -0.4, -0.4]), np.array([1.0, 1.0, 1.0])
+    cropped = v3.crop_pointcloud_bb(pc, lo, hi)
+    np.savez(
+        os.path.join(OUT, "depth_pointcloud.npz"),
+        zbuf=zbuf,
+        rgb=rgb,
+        extent=2.0,
+        znear=0.01,
+        zfar=50.0,
+        depth=depth,
+        fovy=fovy,
+        near_clip=0.05,
+        far_clip=2.0,
+        pointcloud=pc,
+        bb_min=lo,
+        bb_max=hi,
+        cropped=cropped,
+    )
+    print("depth/pointcloud:", depth.dtype, pc.shape, cropped.shape)
+
+
+def gen_phase_schedule(importlib):
+    """Reference phases under PhaseManager with a fake env clock advancing 8 x 0.004 per step."""
+    rb = importlib.import_module("robo_manip_baselines.common.base.RolloutBase")
+    pm = importlib.import_module("robo_manip_baselines.common.manager.PhaseManager")
+    opm = importlib.import_module("robo_manip_baselines.envs.operation.OperationMujocoUR5eCable")
+
+    class FakeEnvUnwrapped:
+        def __init__(self):
+            self.time = 0.0
+            self.body_config_list = []
+
+        def get_time(self):
+            return self.time
+
+        def get_body_pose(self, name):
+            return np.array([-0.175, -0.28, 0.8325, 1.0, 0.0, 0.0, 0.0])
+
+    class FakeOp:
+        pass
+
+    cases = []
+    schedules = [
+        ("never", []),
+        ("success_at_400", [(400, 10**9)]),
+        ("success_then_drop", [(300, 305)]),
+        ("success_at_first_rollout_step", [(79, 10**9)]),
+        ("late_success", [(1000, 10**9)]),
+        ("flicker", [(200, 201), (500, 10**9)]),
+    ]
+    for name, ones in schedules:
+        for max_duration, skip in [(30.0, 3), (10.0, 1), (5.0, 4)]:
+            op = FakeOp()
+            env_u = FakeEnvUnwrapped()
+            op.env = types.SimpleNamespace(
+                unwrapped=env_u,
+                action_space=types.SimpleNamespace(
+                    high=np.array([6.28] * 6 + [255.0]), low=np.array([-6.28] * 6 + [0.0])
+                ),
+            )
+            op.args = types.SimpleNamespace(
+                wait_before_start=False,
+                skip=skip,
+                skip_draw=skip,
+                no_plot=True,
+                auto_exit=True,
+                max_duration=max_duration,
+                save_last_image=False,
+                world_idx_list=[0],
+            )
+            op.key = -1
+            op.require_task_desc = False
+            op.world_idx = 0
+            op.result = {"success": [], "reward": [], "duration": []}
+            op.episode_idx = 0
+            op.quit_flag = False
+            op.reset_flag = False
+            op.inference_duration_list = []
+            infer_steps = []
+            step_box = {"t": 0}
+            op.infer_policy = lambda _b=step_box, _l=infer_steps: _l.append(_b["t"])
+            op.set_command_data = lambda: None
+            op.motion_manager = types.SimpleNamespace(
+                set_command_data=lambda *a, **k: None, body_manager_list=[]
+            )
+            phases = [
+                rb.InitialRolloutPhase(op),
+                opm.ReachPhase1(op),
+                opm.ReachPhase2(op),
+                opm.GraspPhase(op),
+                rb.RolloutPhase(op),
+                rb.EndRolloutPhase(op),
+            ]
+            import contextlib
+            import io
+
+            mgr = pm.PhaseManager(phases)
+            with contextlib.redirect_stdout(io.StringIO()):
+                mgr.reset()
+                phase_seq = []
+                reward_seq = []
+                t = 0
+                while True:
+                    step_box["t"] = t
+                    mgr.pre_update()
+                    for _ in range(8):
+                        env_u.time += 0.004
+                    op.reward = 1.0 if any(a <= t < b for a, b in ones) else 0.0
+                    mgr.post_update()
+                    mgr.check_transition()
+                    phase_seq.append(mgr.phase_idx)
+                    reward_seq.append(op.reward)
+                    t += 1
+                    if op.quit_flag or t > 5000:
+                        break
+            cases.append(
+                dict(
+                    name=f"{name}_md{max_duration}_skip{skip}",
+                    reward=np.array(reward_seq),
+                    phase=np.array(phase_seq, dtype=np.int32),
+                    infer_steps=np.array(infer_steps, dtype=np.int32),
+                    success=np.array(op.result["success"]),
+                    result_reward=np.array(op.result["reward"]),
+                    duration=np.array(op.result["duration"]),
+                    max_duration=max_duration,
+                    skip=skip,
+                    n_steps=t,
+                )
+            )
+    d = {}
+    for i, c in enumerate(cases):
+        for k, v in c.items():
+            d[f"c{i}_{k}"] = np.asarray(v)
+    d["n_cases"] = np.int32(len(cases))
+    np.savez(os.path.join(OUT, "phase_schedule.npz"), **d)
+    print("phase cases:", [(c["name"], int(c["n_steps"]), float(c["duration"][0])) for c in cases][:4])
+
+
+def main():
+    os.makedirs(OUT, exist_ok=True)
+    importlib = install_stubs()
+    gen_ensemble(importlib)
+    gen_reward(importlib)
+    gen_obs(importlib)
+    gen_depth_and_pointcloud(importlib)
+    gen_phase_schedule(importlib)
+
+
+if __name__ == "__main__":
+    main()
