@@ -125,6 +125,49 @@ int rmbx_sched_update(rmbx_sched_t* sched, const double* time, const double* rew
                       const double* pre_durations, int n_pre, double max_duration,
                       double post_success_duration, int n_env, void* stream);
 
+
+/* ---------------------------------------------------------------------------------------------
+ * Batched MuJoCo-subset physics engine (the env.step hot path).
+ * Replaces, for n_env environments in lockstep, the per-env
+ *   envs/mujoco/MujocoEnvBase.py:82-97 step() -> gymnasium do_simulation -> mujoco.mj_step x
+ *   frame_skip (MujocoEnvBase.py:12-13: dt 0.004, frame_skip 8) + mj_rnePostConstraint,
+ * and MujocoEnvBase.py:163-165 reset_model (state set by the caller).
+ * One wavefront per environment; nsub substeps fused in one launch.  The model comes from
+ * include/rmbx_model.h (host pointers, copied to the device at create).
+ * ------------------------------------------------------------------------------------------- */
+typedef struct rmbx_engine rmbx_engine;
+struct rmbx_model;
+
+/* Caller-owned device buffers, all [n_env][...] row-major f64 unless noted. */
+typedef struct rmbx_env_buffers {
+  double* time;       /* [n]            simulation time (MujocoEnvBase.get_time) */
+  double* qpos;       /* [n][nq] */
+  double* qvel;       /* [n][nv] */
+  double* qacc_ws;    /* [n][nv]        warm start (MuJoCo qacc_warmstart) */
+  double* ctrl;       /* [n][nu] */
+  double* body_pos;   /* [n][nbody][3]  per-env body offsets (modify_world pole pose) */
+  double* xpos;       /* [n][nbody][3]  out: body positions of the last forward pass */
+  double* xquat;      /* [n][nbody][4]  out */
+  double* gxpos;      /* [n][ngeom][3]  out: geom frames (collision and render geoms) */
+  double* gxmat;      /* [n][ngeom][9]  out */
+  double* sensordata; /* [n][6]         out: force(3) torque(3) site sensors */
+  int32_t* stats;     /* [n][4]         out: ncon, nefc, solver iterations, bad-state flag */
+  void* workspace;    /* engine scratch, rmbx_engine_workspace_bytes() bytes */
+} rmbx_env_buffers;
+
+int rmbx_engine_create(const struct rmbx_model* model, int n_env, rmbx_engine** out);
+int rmbx_engine_destroy(rmbx_engine* eng);
+int rmbx_engine_workspace_bytes(const rmbx_engine* eng, size_t* bytes);
+/* offset (in doubles, within one env's workspace slice) and element count of a named
+ * workspace array (e.g. "M", "qfrc_bias", "qacc", "J"); per-env stride via "stride". */
+int rmbx_engine_ws_offset(const rmbx_engine* eng, const char* name, size_t* offset,
+                          size_t* count);
+int rmbx_engine_bind(rmbx_engine* eng, const rmbx_env_buffers* bufs);
+/* nsub x mj_step on every env with active[e] != 0 (NULL = all). */
+int rmbx_engine_step(rmbx_engine* eng, int nsub, const uint8_t* active, void* stream);
+/* mj_forward only (no integration): fills the outputs and workspace for inspection. */
+int rmbx_engine_forward(rmbx_engine* eng, const uint8_t* active, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -31,7 +31,21 @@ SIGNATURES = {
     "rmbx_depth_linearize": (_c_int, [_c_p, _c_p, _c_sz, _c_d, _c_d, _c_p]),
     "rmbx_sched_reset": (_c_int, [_c_p, _c_p, _c_p, _c_int, _c_p]),
     "rmbx_sched_update": (_c_int, [_c_p, _c_p, _c_p, _c_p, _c_int, _c_d, _c_d, _c_int, _c_p]),
+    "rmbx_engine_create": (_c_int, [_c_p, _c_int, _c_p]),
+    "rmbx_engine_destroy": (_c_int, [_c_p]),
+    "rmbx_engine_workspace_bytes": (_c_int, [_c_p, _c_p]),
+    "rmbx_engine_ws_offset": (_c_int, [_c_p, ctypes.c_char_p, _c_p, _c_p]),
+    "rmbx_engine_bind": (_c_int, [_c_p, _c_p]),
+    "rmbx_engine_step": (_c_int, [_c_p, _c_int, _c_p, _c_p]),
+    "rmbx_engine_forward": (_c_int, [_c_p, _c_p, _c_p]),
 }
+
+
+class EnvBuffers(ctypes.Structure):
+    """ctypes mirror of rmbx_env_buffers (include/rmbx.h)."""
+
+    _fields_ = [(n, _c_p) for n in ("time", "qpos", "qvel", "qacc_ws", "ctrl", "body_pos", "xpos", "xquat",
+                                    "gxpos", "gxmat", "sensordata", "stats", "workspace")]
 
 # numpy mirror of rmbx_sched_t (include/rmbx.h)
 SCHED_DTYPE = np.dtype(

@@ -1,0 +1,1803 @@
+// Batched MuJoCo-subset physics for the rollout hot path (gfx950).
+//
+// Replaces the reference's per-env env.step -> gymnasium do_simulation -> mujoco.mj_step x 8
+// (envs/mujoco/MujocoEnvBase.py:82-97, :12-13) for thousands of envs in lockstep.
+//
+// Execution model: ONE WAVEFRONT (64 lanes) PER ENVIRONMENT, all `nsub` substeps fused in one
+// launch.  Lanes split the data-parallel stages (geoms, pairs, contacts, constraint rows, dofs,
+// matrix rows/columns); tree recursions (kinematics, composite inertia, RNE) run on lane 0.  The
+// dense nv x nv matrix being factorised (M, the Newton Hessian, the implicitfast matrix) lives
+// in LDS (37 KB at nv = 68); per-env vectors and the constraint Jacobian live in a per-env
+// workspace slice in HBM (L2/MALL-resident at these sizes).  Algorithm, stage for stage, is the
+// one restated serially in oracle/dyn_oracle.c (see that header for the MuJoCo mapping).
+
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "rmbx_common.h"
+#include "rmbx_math.h"
+#include "rmbx_model.h"
+
+namespace rmbx {
+
+#define MAXCON_PAIR 8
+
+// ------------------------------------------------------------------------------------------
+// workspace layout (offsets in doubles within one env slice; ints stored in a trailing region)
+// ------------------------------------------------------------------------------------------
+struct Layout {
+  size_t stride;  // doubles per env
+  size_t xmat, xipos, xanchor, xaxis, sxpos, sxmat, cdof, cdofdot, cinert, crb, cvel, cacc, cfrc;
+  size_t M;
+  size_t qfrc_bias, qfrc_passive, qfrc_actuator, qfrc_smooth, qacc_smooth, qfrc_constraint, qacc,
+      res, Mres, grad, search, Ms, tmp;
+  size_t ten_len, ten_vel;
+  size_t con_pos, con_frame, con_dist, con_mu;
+  size_t J, efc_pos, efc_aref, efc_D, efc_R, efc_force, efc_jar, efc_Js, efc_vel, efc_tmp;
+  size_t ints;  // start of the int32 region (in doubles)
+  // int32 offsets relative to the int region
+  size_t con_b1, con_b2, con_condim, con_pair, con_efcadr, efc_type, scal;
+  size_t istride;  // int32 count
+  int nefc_max;
+};
+
+struct rmbx_engine_impl;
+
+}  // namespace rmbx
+
+struct rmbx_engine {
+  rmbx_model host;       // copy of scalars (pointers unused)
+  rmbx_model dev;        // device pointers
+  std::vector<void*> allocations;
+  rmbx::Layout L;
+  int n_env;
+  rmbx_env_buffers bufs;
+  bool bound;
+};
+
+namespace rmbx {
+
+struct Env {
+  const rmbx_model* m;
+  double* ws;
+  int32_t* iw;
+  const Layout* L;
+  double* qpos;
+  double* qvel;
+  double* qacc_ws;
+  double* ctrl;
+  double* body_pos;
+  double* xpos;
+  double* xquat;
+  double* gxpos;
+  double* gxmat;
+  double* sensordata;
+  double* time;
+  int32_t* stats;
+  double* lds;  // nv*nv matrix
+};
+
+#define W(name) (e.ws + e.L->name)
+#define WI(name) (e.iw + e.L->name)
+
+__device__ __forceinline__ void sync() { __syncthreads(); }
+
+// ------------------------------------------------------------------------------------------
+// kinematics (mj_kinematics): lane 0 walks the tree; lanes split geoms / sites
+// ------------------------------------------------------------------------------------------
+__device__ void kinematics(Env& e, int lane) {
+  const rmbx_model& m = *e.m;
+  double* xmat = W(xmat);
+  double* xipos = W(xipos);
+  double* xanchor = W(xanchor);
+  double* xaxis = W(xaxis);
+  if (lane == 0) {
+    e.xpos[0] = e.xpos[1] = e.xpos[2] = 0;
+    e.xquat[0] = 1;
+    e.xquat[1] = e.xquat[2] = e.xquat[3] = 0;
+    quat2mat(e.xquat, xmat);
+    for (int b = 1; b < m.nbody; b++) {
+      const int p = m.body_parent[b];
+      const int ja = m.body_jntadr[b], jn = m.body_jntnum[b];
+      double* xp = e.xpos + 3 * b;
+      double xq[4];
+      if (jn > 0 && m.jnt_type[ja] == RMBX_JNT_FREE) {
+        const int a = m.jnt_qposadr[ja];
+        xp[0] = e.qpos[a];
+        xp[1] = e.qpos[a + 1];
+        xp[2] = e.qpos[a + 2];
+        xq[0] = e.qpos[a + 3];
+        xq[1] = e.qpos[a + 4];
+        xq[2] = e.qpos[a + 5];
+        xq[3] = e.qpos[a + 6];
+        quatnorm(xq);
+        xanchor[3 * ja] = xp[0];
+        xanchor[3 * ja + 1] = xp[1];
+        xanchor[3 * ja + 2] = xp[2];
+        xaxis[3 * ja] = 0;
+        xaxis[3 * ja + 1] = 0;
+        xaxis[3 * ja + 2] = 1;
+      } else {
+        double t[3];
+        matvec3(xmat + 9 * p, e.body_pos + 3 * b, t);
+        for (int i = 0; i < 3; i++) xp[i] = e.xpos[3 * p + i] + t[i];
+        quatmul(e.xquat + 4 * p, m.body_quat + 4 * b, xq);
+        for (int j = ja; j < ja + jn; j++) {
+          double R[9], anc[3], ax[3];
+          quat2mat(xq, R);
+          matvec3(R, m.jnt_pos + 3 * j, t);
+          for (int i = 0; i < 3; i++) anc[i] = xp[i] + t[i];
+          matvec3(R, m.jnt_axis + 3 * j, ax);
+          for (int i = 0; i < 3; i++) {
+            xanchor[3 * j + i] = anc[i];
+            xaxis[3 * j + i] = ax[i];
+          }
+          const int qa = m.jnt_qposadr[j];
+          const double qd = e.qpos[qa] - m.qpos0[qa];
+          if (m.jnt_type[j] == RMBX_JNT_HINGE) {
+            double qr[4];
+            axisangle_quat(m.jnt_axis + 3 * j, qd, qr);
+            quatmul(xq, qr, xq);
+            quatnorm(xq);
+            quat2mat(xq, R);
+            matvec3(R, m.jnt_pos + 3 * j, t);
+            for (int i = 0; i < 3; i++) xp[i] = anc[i] - t[i];
+          } else if (m.jnt_type[j] == RMBX_JNT_SLIDE) {
+            for (int i = 0; i < 3; i++) xp[i] += ax[i] * qd;
+          }
+        }
+      }
+      for (int i = 0; i < 4; i++) e.xquat[4 * b + i] = xq[i];
+      quat2mat(xq, xmat + 9 * b);
+      double t[3];
+      matvec3(xmat + 9 * b, m.body_ipos + 3 * b, t);
+      for (int i = 0; i < 3; i++) xipos[3 * b + i] = xp[i] + t[i];
+    }
+  }
+  sync();
+  for (int g = lane; g < m.ngeom; g += 64) {
+    const int b = m.geom_body[g];
+    const bool col = m.geom_ctype[g] >= 0;
+    const double* gp = col ? m.geom_cpos + 3 * g : m.geom_pos + 3 * g;
+    const double* gq = col ? m.geom_cquat + 4 * g : m.geom_quat + 4 * g;
+    double t[3], R[9];
+    matvec3(xmat + 9 * b, gp, t);
+    for (int i = 0; i < 3; i++) e.gxpos[3 * g + i] = e.xpos[3 * b + i] + t[i];
+    quat2mat(gq, R);
+    matmul3(xmat + 9 * b, R, e.gxmat + 9 * g);
+  }
+  for (int s = lane; s < m.nsite; s += 64) {
+    const int b = m.site_body[s];
+    double t[3], R[9];
+    matvec3(xmat + 9 * b, m.site_pos + 3 * s, t);
+    for (int i = 0; i < 3; i++) W(sxpos)[3 * s + i] = e.xpos[3 * b + i] + t[i];
+    quat2mat(m.site_quat + 4 * s, R);
+    matmul3(xmat + 9 * b, R, W(sxmat) + 9 * s);
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// mj_comPos + mj_crb
+// ------------------------------------------------------------------------------------------
+__device__ void com_pos_crb(Env& e, int lane) {
+  const rmbx_model& m = *e.m;
+  const int nv = m.nv;
+  double* cinert = W(cinert);
+  double* cdof = W(cdof);
+  double* crb = W(crb);
+  for (int b = lane; b < m.nbody; b += 64) {
+    double* I = cinert + 10 * b;
+    if (b == 0) {
+      for (int k = 0; k < 10; k++) I[k] = 0;
+      continue;
+    }
+    const double mass = m.body_mass[b];
+    const double* c = W(xipos) + 3 * b;
+    const double* R = W(xmat) + 9 * b;
+    const double* Ib = m.body_inertia + 9 * b;
+    double T[9], Iw[9], Rt[9];
+    for (int i = 0; i < 3; i++)
+      for (int j = 0; j < 3; j++) Rt[3 * i + j] = R[3 * j + i];
+    matmul3(R, Ib, T);
+    matmul3(T, Rt, Iw);
+    const double cc = dot3(c, c);
+    I[0] = mass;
+    I[1] = mass * c[0];
+    I[2] = mass * c[1];
+    I[3] = mass * c[2];
+    I[4] = Iw[0] + mass * (cc - c[0] * c[0]);
+    I[5] = Iw[4] + mass * (cc - c[1] * c[1]);
+    I[6] = Iw[8] + mass * (cc - c[2] * c[2]);
+    I[7] = Iw[1] - mass * c[0] * c[1];
+    I[8] = Iw[2] - mass * c[0] * c[2];
+    I[9] = Iw[5] - mass * c[1] * c[2];
+  }
+  for (int j = lane; j < m.njnt; j += 64) {
+    const int b = m.jnt_body[j], da = m.jnt_dofadr[j];
+    const double* ax = W(xaxis) + 3 * j;
+    const double* anc = W(xanchor) + 3 * j;
+    double* S = cdof + 6 * da;
+    const int t = m.jnt_type[j];
+    if (t == RMBX_JNT_HINGE) {
+      S[0] = ax[0];
+      S[1] = ax[1];
+      S[2] = ax[2];
+      cross3(anc, ax, S + 3);
+    } else if (t == RMBX_JNT_SLIDE) {
+      S[0] = S[1] = S[2] = 0;
+      S[3] = ax[0];
+      S[4] = ax[1];
+      S[5] = ax[2];
+    } else if (t == RMBX_JNT_FREE) {
+      for (int k = 0; k < 36; k++) S[k] = 0;
+      S[3] = 1;
+      S[10] = 1;
+      S[17] = 1;
+      const double* R = W(xmat) + 9 * b;
+      const double* x = e.xpos + 3 * b;
+      for (int k = 0; k < 3; k++) {
+        double* Sk = S + 6 * (3 + k);
+        const double a[3] = {R[k], R[3 + k], R[6 + k]};
+        Sk[0] = a[0];
+        Sk[1] = a[1];
+        Sk[2] = a[2];
+        cross3(x, a, Sk + 3);
+      }
+    }
+  }
+  sync();
+  // composite rigid-body inertia: children have larger ids (DFS order)
+  for (int k = lane; k < 10 * m.nbody; k += 64) crb[k] = cinert[k];
+  sync();
+  if (lane < 10) {
+    for (int b = m.nbody - 1; b > 0; b--) {
+      const int p = m.body_parent[b];
+      if (p > 0) crb[10 * p + lane] += crb[10 * b + lane];
+    }
+  }
+  sync();
+  double* M = W(M);
+  for (int k = lane; k < nv * nv; k += 64) M[k] = 0;
+  sync();
+  for (int i = lane; i < nv; i += 64) {
+    double F[6];
+    inert_mul(crb + 10 * m.dof_body[i], cdof + 6 * i, F);
+    for (int j = i; j >= 0; j = m.dof_parent[j]) {
+      const double v = dot6(cdof + 6 * j, F);
+      M[i * nv + j] = v;
+      M[j * nv + i] = v;
+    }
+  }
+  sync();
+  for (int i = lane; i < nv; i += 64) M[i * nv + i] += m.dof_armature[i];
+  sync();
+}
+
+// ------------------------------------------------------------------------------------------
+// mj_comVel + mj_rne (bias) ; passive ; tendons ; actuation (lane 0 for tree passes)
+// ------------------------------------------------------------------------------------------
+__device__ void rne_forward(Env& e, const double* qacc) {
+  const rmbx_model& m = *e.m;
+  double* ca = W(cacc);
+  double* cfrc = W(cfrc);
+  const double* cdof = W(cdof);
+  const double* cdofdot = W(cdofdot);
+  ca[0] = ca[1] = ca[2] = 0;
+  ca[3] = -m.gravity[0];
+  ca[4] = -m.gravity[1];
+  ca[5] = -m.gravity[2];
+  for (int b = 1; b < m.nbody; b++) {
+    double a[6];
+    for (int i = 0; i < 6; i++) a[i] = ca[6 * m.body_parent[b] + i];
+    const int da = m.body_dofadr[b], dn = m.body_dofnum[b];
+    for (int k = da; k < da + dn; k++) {
+      for (int i = 0; i < 6; i++) a[i] += cdofdot[6 * k + i] * e.qvel[k];
+      if (qacc)
+        for (int i = 0; i < 6; i++) a[i] += cdof[6 * k + i] * qacc[k];
+    }
+    for (int i = 0; i < 6; i++) ca[6 * b + i] = a[i];
+    double Ia[6], Iv[6], vxIv[6];
+    const double* I = W(cinert) + 10 * b;
+    const double* v = W(cvel) + 6 * b;
+    inert_mul(I, a, Ia);
+    inert_mul(I, v, Iv);
+    cross_force(v, Iv, vxIv);
+    for (int i = 0; i < 6; i++) cfrc[6 * b + i] = Ia[i] + vxIv[i];
+  }
+}
+
+__device__ void rne_backward(Env& e, int lane) {
+  const rmbx_model& m = *e.m;
+  double* cfrc = W(cfrc);
+  if (lane < 6) {
+    for (int b = m.nbody - 1; b > 0; b--) {
+      const int p = m.body_parent[b];
+      if (p > 0) cfrc[6 * p + lane] += cfrc[6 * b + lane];
+    }
+  }
+}
+
+__device__ void velocity_stage(Env& e, int lane) {
+  const rmbx_model& m = *e.m;
+  const int nv = m.nv;
+  double* cvel = W(cvel);
+  double* cdofdot = W(cdofdot);
+  const double* cdof = W(cdof);
+  if (lane == 0) {
+    for (int i = 0; i < 6; i++) cvel[i] = 0;
+    for (int b = 1; b < m.nbody; b++) {
+      double cv[6];
+      for (int i = 0; i < 6; i++) cv[i] = cvel[6 * m.body_parent[b] + i];
+      for (int j = m.body_jntadr[b]; j < m.body_jntadr[b] + m.body_jntnum[b]; j++) {
+        const int da = m.jnt_dofadr[j];
+        if (m.jnt_type[j] == RMBX_JNT_FREE) {
+          for (int k = 0; k < 3; k++)
+            for (int i = 0; i < 6; i++) cdofdot[6 * (da + k) + i] = 0;
+          for (int k = 0; k < 3; k++)
+            for (int i = 0; i < 6; i++) cv[i] += cdof[6 * (da + k) + i] * e.qvel[da + k];
+          for (int k = 3; k < 6; k++) cross_motion(cv, cdof + 6 * (da + k), cdofdot + 6 * (da + k));
+          for (int k = 3; k < 6; k++)
+            for (int i = 0; i < 6; i++) cv[i] += cdof[6 * (da + k) + i] * e.qvel[da + k];
+        } else {
+          cross_motion(cv, cdof + 6 * da, cdofdot + 6 * da);
+          for (int i = 0; i < 6; i++) cv[i] += cdof[6 * da + i] * e.qvel[da];
+        }
+      }
+      for (int i = 0; i < 6; i++) cvel[6 * b + i] = cv[i];
+    }
+    rne_forward(e, nullptr);
+  }
+  sync();
+  rne_backward(e, lane);
+  sync();
+  double* bias = W(qfrc_bias);
+  double* passive = W(qfrc_passive);
+  for (int k = lane; k < nv; k += 64) {
+    bias[k] = dot6(cdof + 6 * k, W(cfrc) + 6 * m.dof_body[k]);
+    passive[k] = -m.dof_damping[k] * e.qvel[k];
+  }
+  sync();
+  for (int j = lane; j < m.njnt; j += 64) {
+    if (m.jnt_stiffness[j] != 0 &&
+        (m.jnt_type[j] == RMBX_JNT_HINGE || m.jnt_type[j] == RMBX_JNT_SLIDE)) {
+      passive[m.jnt_dofadr[j]] -= m.jnt_stiffness[j] * (e.qpos[m.jnt_qposadr[j]] - m.jnt_springref[j]);
+    }
+  }
+  double* act = W(qfrc_actuator);
+  for (int k = lane; k < nv; k += 64) act[k] = 0;
+  sync();
+  if (lane == 0) {
+    double* tl = W(ten_len);
+    double* tv = W(ten_vel);
+    for (int t = 0; t < m.ntendon; t++) {
+      double L = 0, V = 0;
+      for (int w = m.ten_adr[t]; w < m.ten_adr[t] + m.ten_num[t]; w++) {
+        const int j = m.wrap_jnt[w];
+        L += m.wrap_coef[w] * e.qpos[m.jnt_qposadr[j]];
+        V += m.wrap_coef[w] * e.qvel[m.jnt_dofadr[j]];
+      }
+      tl[t] = L;
+      tv[t] = V;
+    }
+    for (int u = 0; u < m.nu; u++) {
+      double c = e.ctrl[u];
+      if (m.act_ctrllimited[u]) {
+        c = c < m.act_ctrlrange[2 * u] ? m.act_ctrlrange[2 * u] : c;
+        c = c > m.act_ctrlrange[2 * u + 1] ? m.act_ctrlrange[2 * u + 1] : c;
+      }
+      const int id = m.act_trnid[u];
+      double len, vel;
+      if (m.act_trntype[u] == RMBX_TRN_JOINT) {
+        len = e.qpos[m.jnt_qposadr[id]];
+        vel = e.qvel[m.jnt_dofadr[id]];
+      } else {
+        len = tl[id];
+        vel = tv[id];
+      }
+      const double* bp = m.act_bias + 3 * u;
+      double f = m.act_gain[u] * c + bp[0] + bp[1] * len + bp[2] * vel;
+      if (m.act_forcelimited[u]) {
+        f = f < m.act_forcerange[2 * u] ? m.act_forcerange[2 * u] : f;
+        f = f > m.act_forcerange[2 * u + 1] ? m.act_forcerange[2 * u + 1] : f;
+      }
+      if (m.act_trntype[u] == RMBX_TRN_JOINT) {
+        act[m.jnt_dofadr[id]] += f;
+      } else {
+        for (int w = m.ten_adr[id]; w < m.ten_adr[id] + m.ten_num[id]; w++)
+          act[m.jnt_dofadr[m.wrap_jnt[w]]] += m.wrap_coef[w] * f;
+      }
+    }
+  }
+  sync();
+  double* sm = W(qfrc_smooth);
+  for (int k = lane; k < nv; k += 64) sm[k] = passive[k] + act[k] - bias[k];
+  sync();
+}
+
+// ------------------------------------------------------------------------------------------
+// collision: lanes over candidate pairs, deterministic wave-scan compaction (pair order)
+// ------------------------------------------------------------------------------------------
+struct Contact {
+  double pos[3], n[3], dist;
+};
+
+__device__ void closest_seg_seg(const double* p1, const double* q1, const double* p2,
+                                const double* q2, double* c1, double* c2) {
+  double d1[3], d2[3], r[3];
+  for (int i = 0; i < 3; i++) {
+    d1[i] = q1[i] - p1[i];
+    d2[i] = q2[i] - p2[i];
+    r[i] = p1[i] - p2[i];
+  }
+  const double a = dot3(d1, d1), ee = dot3(d2, d2), f = dot3(d2, r);
+  double s, t;
+  if (a <= RMBX_MINVAL && ee <= RMBX_MINVAL) {
+    s = t = 0;
+  } else if (a <= RMBX_MINVAL) {
+    s = 0;
+    t = fmin(fmax(f / ee, 0.0), 1.0);
+  } else {
+    const double c = dot3(d1, r);
+    if (ee <= RMBX_MINVAL) {
+      t = 0;
+      s = fmin(fmax(-c / a, 0.0), 1.0);
+    } else {
+      const double b = dot3(d1, d2);
+      const double den = a * ee - b * b;
+      s = den > RMBX_MINVAL ? fmin(fmax((b * f - c * ee) / den, 0.0), 1.0) : 0.0;
+      t = (b * s + f) / ee;
+      if (t < 0) {
+        t = 0;
+        s = fmin(fmax(-c / a, 0.0), 1.0);
+      } else if (t > 1) {
+        t = 1;
+        s = fmin(fmax((b - c) / a, 0.0), 1.0);
+      }
+    }
+  }
+  for (int i = 0; i < 3; i++) {
+    c1[i] = p1[i] + d1[i] * s;
+    c2[i] = p2[i] + d2[i] * t;
+  }
+}
+
+__device__ int col_sphere_sphere(const double* ca, double ra, const double* cb, double rb,
+                                 double margin, Contact* out) {
+  const double v[3] = {cb[0] - ca[0], cb[1] - ca[1], cb[2] - ca[2]};
+  const double l = norm3(v);
+  const double dist = l - ra - rb;
+  if (dist >= margin) return 0;
+  double n[3];
+  if (l < RMBX_MINVAL) {
+    n[0] = 1;
+    n[1] = 0;
+    n[2] = 0;
+  } else {
+    n[0] = v[0] / l;
+    n[1] = v[1] / l;
+    n[2] = v[2] / l;
+  }
+  for (int i = 0; i < 3; i++) {
+    out->n[i] = n[i];
+    out->pos[i] = ca[i] + n[i] * (ra + 0.5 * dist);
+  }
+  out->dist = dist;
+  return 1;
+}
+
+__device__ __forceinline__ void capsule_ends(const double* c, const double* R, double h, double* p,
+                                             double* q) {
+  for (int i = 0; i < 3; i++) {
+    p[i] = c[i] - R[3 * i + 2] * h;
+    q[i] = c[i] + R[3 * i + 2] * h;
+  }
+}
+
+__device__ double point_box(const double* p, const double* cb, const double* Rb, const double* hb,
+                            double* n, double* surf) {
+  const double dlt[3] = {p[0] - cb[0], p[1] - cb[1], p[2] - cb[2]};
+  double l[3], q[3];
+  mattvec3(Rb, dlt, l);
+  bool inside = true;
+  for (int i = 0; i < 3; i++) {
+    q[i] = l[i] < -hb[i] ? -hb[i] : (l[i] > hb[i] ? hb[i] : l[i]);
+    if (q[i] != l[i]) inside = false;
+  }
+  double nl[3], dist;
+  if (!inside) {
+    const double v[3] = {l[0] - q[0], l[1] - q[1], l[2] - q[2]};
+    dist = norm3(v);
+    nl[0] = v[0] / dist;
+    nl[1] = v[1] / dist;
+    nl[2] = v[2] / dist;
+  } else {
+    int k = 0;
+    double best = hb[0] - fabs(l[0]);
+    for (int i = 1; i < 3; i++) {
+      const double pen = hb[i] - fabs(l[i]);
+      if (pen < best) {
+        best = pen;
+        k = i;
+      }
+    }
+    nl[0] = nl[1] = nl[2] = 0;
+    nl[k] = l[k] >= 0 ? 1 : -1;
+    q[k] = nl[k] * hb[k];
+    dist = -best;
+  }
+  matvec3(Rb, nl, n);
+  double qw[3];
+  matvec3(Rb, q, qw);
+  for (int i = 0; i < 3; i++) surf[i] = cb[i] + qw[i];
+  return dist;
+}
+
+__device__ int col_sphere_box(const double* cs, double r, const double* cb, const double* Rb,
+                              const double* hb, double margin, Contact* out) {
+  double n[3], surf[3];
+  const double dist = point_box(cs, cb, Rb, hb, n, surf) - r;
+  if (dist >= margin) return 0;
+  for (int i = 0; i < 3; i++) {
+    out->n[i] = -n[i];
+    out->pos[i] = surf[i] + n[i] * (0.5 * dist);
+  }
+  out->dist = dist;
+  return 1;
+}
+
+__device__ int col_capsule_box(const double* ca, const double* Ra, const double* sa,
+                               const double* cb, const double* Rb, const double* hb, double margin,
+                               Contact* out) {
+  double p[3], q[3];
+  capsule_ends(ca, Ra, sa[1], p, q);
+  Contact c0, c1, cm;
+  const int h0 = col_sphere_box(p, sa[0], cb, Rb, hb, margin, &c0);
+  const int h1 = col_sphere_box(q, sa[0], cb, Rb, hb, margin, &c1);
+  double lo = 0, hi = 1;
+  for (int it = 0; it < 40; it++) {
+    const double t1 = lo + (hi - lo) / 3, t2 = hi - (hi - lo) / 3;
+    double x1[3], x2[3], nn[3], ss[3];
+    for (int i = 0; i < 3; i++) {
+      x1[i] = p[i] + (q[i] - p[i]) * t1;
+      x2[i] = p[i] + (q[i] - p[i]) * t2;
+    }
+    const double f1 = point_box(x1, cb, Rb, hb, nn, ss), f2 = point_box(x2, cb, Rb, hb, nn, ss);
+    if (f1 < f2)
+      hi = t2;
+    else
+      lo = t1;
+  }
+  const double tm = 0.5 * (lo + hi);
+  double xm[3];
+  for (int i = 0; i < 3; i++) xm[i] = p[i] + (q[i] - p[i]) * tm;
+  const int hm = col_sphere_box(xm, sa[0], cb, Rb, hb, margin, &cm);
+  if (h0 && h1) {
+    out[0] = c0;
+    out[1] = c1;
+    return 2;
+  }
+  int n = 0;
+  Contact best;
+  if (h0) {
+    best = c0;
+    n = 1;
+  }
+  if (h1 && (!n || c1.dist < best.dist)) {
+    best = c1;
+    n = 1;
+  }
+  if (hm && (!n || cm.dist < best.dist)) {
+    best = cm;
+    n = 1;
+  }
+  if (n) out[0] = best;
+  return n;
+}
+
+__device__ int col_box_box(const double* ca, const double* Ra, const double* ha, const double* cb,
+                           const double* Rb, const double* hb, double margin, Contact* out) {
+  double axes[15][3];
+  for (int k = 0; k < 3; k++) {
+    axes[k][0] = Ra[k];
+    axes[k][1] = Ra[3 + k];
+    axes[k][2] = Ra[6 + k];
+    axes[3 + k][0] = Rb[k];
+    axes[3 + k][1] = Rb[3 + k];
+    axes[3 + k][2] = Rb[6 + k];
+  }
+  int na = 6;
+  for (int i = 0; i < 3; i++)
+    for (int j = 0; j < 3; j++) {
+      double c[3];
+      cross3(axes[i], axes[3 + j], c);
+      const double l = norm3(c);
+      if (l < 1e-6) {
+        axes[na][0] = axes[na][1] = axes[na][2] = 0;
+      } else {
+        axes[na][0] = c[0] / l;
+        axes[na][1] = c[1] / l;
+        axes[na][2] = c[2] / l;
+      }
+      na++;
+    }
+  const double dc[3] = {cb[0] - ca[0], cb[1] - ca[1], cb[2] - ca[2]};
+  double best = -1e300;
+  int bk = -1;
+  for (int k = 0; k < 15; k++) {
+    const double* a = axes[k];
+    if (a[0] == 0 && a[1] == 0 && a[2] == 0) continue;
+    double ra = 0, rb = 0;
+    for (int i = 0; i < 3; i++) {
+      const double ua[3] = {Ra[i], Ra[3 + i], Ra[6 + i]}, ub[3] = {Rb[i], Rb[3 + i], Rb[6 + i]};
+      ra += ha[i] * fabs(dot3(a, ua));
+      rb += hb[i] * fabs(dot3(a, ub));
+    }
+    const double sep = fabs(dot3(dc, a)) - ra - rb;
+    if (sep >= margin) return 0;
+    const double score = k < 6 ? sep : sep - 1e-6;
+    if (score > best) {
+      best = score;
+      bk = k;
+    }
+  }
+  double n[3] = {axes[bk][0], axes[bk][1], axes[bk][2]};
+  if (dot3(n, dc) < 0) {
+    n[0] = -n[0];
+    n[1] = -n[1];
+    n[2] = -n[2];
+  }
+  Contact cand[16];
+  int nc = 0;
+  for (int side = 0; side < 2; side++) {
+    const double* c = side == 0 ? cb : ca;
+    const double* R = side == 0 ? Rb : Ra;
+    const double* h = side == 0 ? hb : ha;
+    const double* co = side == 0 ? ca : cb;
+    const double* Ro = side == 0 ? Ra : Rb;
+    const double* ho = side == 0 ? ha : hb;
+    for (int v = 0; v < 8; v++) {
+      const double l[3] = {(v & 1) ? h[0] : -h[0], (v & 2) ? h[1] : -h[1], (v & 4) ? h[2] : -h[2]};
+      double w[3];
+      matvec3(R, l, w);
+      const double x[3] = {c[0] + w[0], c[1] + w[1], c[2] + w[2]};
+      const double dl[3] = {x[0] - co[0], x[1] - co[1], x[2] - co[2]};
+      double lo[3];
+      mattvec3(Ro, dl, lo);
+      if (fabs(lo[0]) > ho[0] + margin || fabs(lo[1]) > ho[1] + margin ||
+          fabs(lo[2]) > ho[2] + margin)
+        continue;
+      double sup = 0;
+      for (int i = 0; i < 3; i++) {
+        const double u[3] = {Ro[i], Ro[3 + i], Ro[6 + i]};
+        sup += ho[i] * fabs(dot3(n, u));
+      }
+      const double sgn = side == 0 ? 1.0 : -1.0;
+      const double dist = side == 0 ? (dot3(dl, n) - sup) : (-dot3(dl, n) - sup);
+      if (dist >= margin) continue;
+      if (nc < 16) {
+        Contact* k = cand + nc++;
+        k->dist = dist;
+        for (int i = 0; i < 3; i++) {
+          k->n[i] = n[i];
+          k->pos[i] = x[i] - sgn * n[i] * (0.5 * dist);
+        }
+      }
+    }
+  }
+  if (nc == 0) {
+    double pa[3], pb[3];
+    const double neg[3] = {-n[0], -n[1], -n[2]};
+    for (int i = 0; i < 3; i++) {
+      pa[i] = ca[i];
+      pb[i] = cb[i];
+    }
+    for (int k = 0; k < 3; k++) {
+      const double ua[3] = {Ra[k], Ra[3 + k], Ra[6 + k]}, ub[3] = {Rb[k], Rb[3 + k], Rb[6 + k]};
+      const double sa2 = dot3(ua, n) >= 0 ? ha[k] : -ha[k];
+      const double sb2 = dot3(ub, neg) >= 0 ? hb[k] : -hb[k];
+      for (int i = 0; i < 3; i++) {
+        pa[i] += ua[i] * sa2;
+        pb[i] += ub[i] * sb2;
+      }
+    }
+    const double dist = dot3(n, pb) - dot3(n, pa);
+    if (dist >= margin) return 0;
+    for (int i = 0; i < 3; i++) {
+      out[0].n[i] = n[i];
+      out[0].pos[i] = 0.5 * (pa[i] + pb[i]);
+    }
+    out[0].dist = dist;
+    return 1;
+  }
+  for (int i = 0; i < nc; i++)
+    for (int j = i + 1; j < nc; j++)
+      if (cand[j].dist < cand[i].dist) {
+        const Contact t = cand[i];
+        cand[i] = cand[j];
+        cand[j] = t;
+      }
+  const int k = nc < 4 ? nc : 4;
+  for (int i = 0; i < k; i++) out[i] = cand[i];
+  return k;
+}
+
+__device__ int col_plane(const double* cp, const double* Rp, int tb, const double* cb,
+                         const double* Rb, const double* sb, double margin, Contact* out) {
+  const double n[3] = {Rp[2], Rp[5], Rp[8]};
+  double pts[8][3];
+  double rad = 0;
+  int np = 0;
+  if (tb == RMBX_GEOM_SPHERE) {
+    pts[0][0] = cb[0];
+    pts[0][1] = cb[1];
+    pts[0][2] = cb[2];
+    np = 1;
+    rad = sb[0];
+  } else if (tb == RMBX_GEOM_CAPSULE) {
+    capsule_ends(cb, Rb, sb[1], pts[0], pts[1]);
+    np = 2;
+    rad = sb[0];
+  } else if (tb == RMBX_GEOM_BOX) {
+    for (int v = 0; v < 8; v++) {
+      const double l[3] = {(v & 1) ? sb[0] : -sb[0], (v & 2) ? sb[1] : -sb[1],
+                           (v & 4) ? sb[2] : -sb[2]};
+      double w[3];
+      matvec3(Rb, l, w);
+      for (int i = 0; i < 3; i++) pts[v][i] = cb[i] + w[i];
+    }
+    np = 8;
+  }
+  Contact cand[8];
+  int nc = 0;
+  for (int k = 0; k < np; k++) {
+    const double v[3] = {pts[k][0] - cp[0], pts[k][1] - cp[1], pts[k][2] - cp[2]};
+    const double dist = dot3(v, n) - rad;
+    if (dist >= margin) continue;
+    Contact* c = cand + nc++;
+    c->dist = dist;
+    for (int i = 0; i < 3; i++) {
+      c->n[i] = n[i];
+      c->pos[i] = pts[k][i] - n[i] * (rad + 0.5 * dist);
+    }
+  }
+  for (int i = 0; i < nc; i++)
+    for (int j = i + 1; j < nc; j++)
+      if (cand[j].dist < cand[i].dist) {
+        const Contact t = cand[i];
+        cand[i] = cand[j];
+        cand[j] = t;
+      }
+  const int k = nc < 4 ? nc : 4;
+  for (int i = 0; i < k; i++) out[i] = cand[i];
+  return k;
+}
+
+__device__ void geom_aabb(const Env& e, int g, double* lo, double* hi) {
+  const rmbx_model& m = *e.m;
+  const double* c = e.gxpos + 3 * g;
+  const double* R = e.gxmat + 9 * g;
+  const double* s = m.geom_csize + 3 * g;
+  const int t = m.geom_ctype[g];
+  for (int i = 0; i < 3; i++) {
+    double ex;
+    if (t == RMBX_GEOM_SPHERE)
+      ex = s[0];
+    else if (t == RMBX_GEOM_CAPSULE)
+      ex = fabs(R[3 * i + 2]) * s[1] + s[0];
+    else
+      ex = fabs(R[3 * i]) * s[0] + fabs(R[3 * i + 1]) * s[1] + fabs(R[3 * i + 2]) * s[2];
+    lo[i] = c[i] - ex;
+    hi[i] = c[i] + ex;
+  }
+}
+
+__device__ int pair_collide(const Env& e, int p, Contact* out) {
+  const rmbx_model& m = *e.m;
+  int g1 = m.pair_geom1[p], g2 = m.pair_geom2[p];
+  const double margin = m.pair_margin[p];
+  int t1 = m.geom_ctype[g1], t2 = m.geom_ctype[g2];
+  // broadphase
+  if (t1 == RMBX_GEOM_PLANE || t2 == RMBX_GEOM_PLANE) {
+    const int gp = t1 == RMBX_GEOM_PLANE ? g1 : g2, go = gp == g1 ? g2 : g1;
+    const double* R = e.gxmat + 9 * gp;
+    const double n[3] = {R[2], R[5], R[8]};
+    const double v[3] = {e.gxpos[3 * go] - e.gxpos[3 * gp], e.gxpos[3 * go + 1] - e.gxpos[3 * gp + 1],
+                         e.gxpos[3 * go + 2] - e.gxpos[3 * gp + 2]};
+    if (dot3(v, n) - m.geom_rbound[go] > margin) return 0;
+  } else {
+    double lo1[3], hi1[3], lo2[3], hi2[3];
+    geom_aabb(e, g1, lo1, hi1);
+    geom_aabb(e, g2, lo2, hi2);
+    for (int i = 0; i < 3; i++)
+      if (lo1[i] > hi2[i] + margin || lo2[i] > hi1[i] + margin) return 0;
+  }
+  bool flip = false;
+  if (t1 > t2) {
+    int t = t1;
+    t1 = t2;
+    t2 = t;
+    t = g1;
+    g1 = g2;
+    g2 = t;
+    flip = true;
+  }
+  const double *c1 = e.gxpos + 3 * g1, *R1 = e.gxmat + 9 * g1, *s1 = m.geom_csize + 3 * g1;
+  const double *c2 = e.gxpos + 3 * g2, *R2 = e.gxmat + 9 * g2, *s2 = m.geom_csize + 3 * g2;
+  int n = 0;
+  if (t1 == RMBX_GEOM_PLANE) {
+    n = col_plane(c1, R1, t2, c2, R2, s2, margin, out);
+  } else if (t1 == RMBX_GEOM_SPHERE && t2 == RMBX_GEOM_SPHERE) {
+    n = col_sphere_sphere(c1, s1[0], c2, s2[0], margin, out);
+  } else if (t1 == RMBX_GEOM_SPHERE && t2 == RMBX_GEOM_CAPSULE) {
+    double pp[3], qq[3], c[3], cc[3];
+    capsule_ends(c2, R2, s2[1], pp, qq);
+    closest_seg_seg(c1, c1, pp, qq, cc, c);
+    n = col_sphere_sphere(c1, s1[0], c, s2[0], margin, out);
+  } else if (t1 == RMBX_GEOM_SPHERE && t2 == RMBX_GEOM_BOX) {
+    n = col_sphere_box(c1, s1[0], c2, R2, s2, margin, out);
+  } else if (t1 == RMBX_GEOM_CAPSULE && t2 == RMBX_GEOM_CAPSULE) {
+    double p1[3], q1[3], p2[3], q2[3], cc1[3], cc2[3];
+    capsule_ends(c1, R1, s1[1], p1, q1);
+    capsule_ends(c2, R2, s2[1], p2, q2);
+    closest_seg_seg(p1, q1, p2, q2, cc1, cc2);
+    n = col_sphere_sphere(cc1, s1[0], cc2, s2[0], margin, out);
+  } else if (t1 == RMBX_GEOM_CAPSULE && t2 == RMBX_GEOM_BOX) {
+    n = col_capsule_box(c1, R1, s1, c2, R2, s2, margin, out);
+  } else if (t1 == RMBX_GEOM_BOX && t2 == RMBX_GEOM_BOX) {
+    n = col_box_box(c1, R1, s1, c2, R2, s2, margin, out);
+  }
+  if (flip)
+    for (int i = 0; i < n; i++)
+      for (int k = 0; k < 3; k++) out[i].n[k] = -out[i].n[k];
+  return n;
+}
+
+__device__ void make_frame(const double* n, double* F) {
+  F[0] = n[0];
+  F[1] = n[1];
+  F[2] = n[2];
+  double a[3] = {0, 0, 0};
+  if (fabs(n[0]) < 0.5)
+    a[0] = 1;
+  else
+    a[1] = 1;
+  const double t = dot3(a, n);
+  double t1[3] = {a[0] - t * n[0], a[1] - t * n[1], a[2] - t * n[2]};
+  const double l = norm3(t1);
+  t1[0] /= l;
+  t1[1] /= l;
+  t1[2] /= l;
+  double t2[3];
+  cross3(n, t1, t2);
+  F[3] = t1[0];
+  F[4] = t1[1];
+  F[5] = t1[2];
+  F[6] = t2[0];
+  F[7] = t2[1];
+  F[8] = t2[2];
+}
+
+__device__ int collision(Env& e, int lane) {
+  const rmbx_model& m = *e.m;
+  int ncon = 0;
+  for (int base = 0; base < m.npair; base += 64) {
+    const int p = base + lane;
+    Contact c[4];
+    int n = 0;
+    if (p < m.npair) n = pair_collide(e, p, c);
+    int total;
+    const int off = wave_excl_scan(n, lane, &total);
+    for (int i = 0; i < n; i++) {
+      const int k = ncon + off + i;
+      if (k >= m.max_contacts) break;
+      for (int j = 0; j < 3; j++) W(con_pos)[3 * k + j] = c[i].pos[j];
+      make_frame(c[i].n, W(con_frame) + 9 * k);
+      W(con_dist)[k] = c[i].dist;
+      W(con_mu)[k] = m.pair_friction[3 * p];
+      WI(con_b1)[k] = m.geom_body[m.pair_geom1[p]];
+      WI(con_b2)[k] = m.geom_body[m.pair_geom2[p]];
+      WI(con_condim)[k] = m.pair_condim[p];
+      WI(con_pair)[k] = p;
+    }
+    ncon += total;
+  }
+  return ncon < m.max_contacts ? ncon : m.max_contacts;
+}
+
+// ------------------------------------------------------------------------------------------
+// constraint rows
+// ------------------------------------------------------------------------------------------
+__device__ __forceinline__ int last_dof(const rmbx_model& m, int b) {
+  const int w = m.body_weldid[b];
+  if (w == 0) return -1;
+  return m.body_dofadr[w] + m.body_dofnum[w] - 1;
+}
+
+__device__ void jac_point_dir(const Env& e, int b, const double* p, const double* dir, double sgn,
+                              double* row) {
+  const rmbx_model& m = *e.m;
+  const double* cdof = e.ws + e.L->cdof;
+  for (int k = last_dof(m, b); k >= 0; k = m.dof_parent[k]) {
+    const double* S = cdof + 6 * k;
+    double wxp[3];
+    cross3(S, p, wxp);
+    const double v[3] = {S[3] + wxp[0], S[4] + wxp[1], S[5] + wxp[2]};
+    row[k] += sgn * dot3(v, dir);
+  }
+}
+
+__device__ double impedance(const double* solimp, double x) {
+  double dmin = fmin(fmax(solimp[0], 0.0001), 0.9999);
+  double dmax = fmin(fmax(solimp[1], 0.0001), 0.9999);
+  const double width = solimp[2], mid = solimp[3], power = solimp[4];
+  x = fabs(x);
+  if (width <= RMBX_MINVAL || x >= width) return dmax;
+  x = x / width;
+  double y;
+  if (power == 1)
+    y = x;
+  else if (x <= mid)
+    y = pow(x, power) / pow(mid, power - 1);
+  else
+    y = 1 - pow(1 - x, power) / pow(1 - mid, power - 1);
+  return dmin + y * (dmax - dmin);
+}
+
+// stores b in efc_tmp, k*imp*pos in efc_D, R in efc_R (finalised after J is complete)
+__device__ void set_row(Env& e, int r, int type, double pos, double diag, const double* solref,
+                        const double* solimp, double impx) {
+  const double dmax = fmin(fmax(solimp[1], 0.0001), 0.9999);
+  double tc = solref[0];
+  const double dr = solref[1];
+  const double h2 = 2 * e.m->timestep;
+  if (tc < h2) tc = h2;
+  const double k = 1 / (dmax * dmax * tc * tc * dr * dr);
+  const double b = 2 / (dmax * tc);
+  const double imp = impedance(solimp, impx);
+  WI(efc_type)[r] = type;
+  W(efc_pos)[r] = pos;
+  W(efc_tmp)[r] = b;
+  W(efc_D)[r] = k * imp * pos;
+  double R = (1 - imp) / imp * diag;
+  W(efc_R)[r] = R < RMBX_MINVAL ? RMBX_MINVAL : R;
+}
+
+// returns nefc; equality rows first (count in *ne)
+__device__ int make_constraints(Env& e, int lane, int ncon, int* ne_out) {
+  const rmbx_model& m = *e.m;
+  const int nv = m.nv;
+  const int nefc_max = e.L->nefc_max;
+  double* J = W(J);
+  // count rows: equality
+  int ne = 0;
+  for (int q = 0; q < m.neq; q++) ne += m.eq_type[q] == RMBX_EQ_CONNECT ? 3 : (m.eq_type[q] == RMBX_EQ_WELD ? 6 : 1);
+  // limits: ballot compaction in joint order
+  int nlim = 0;
+  for (int base = 0; base < m.njnt; base += 64) {
+    const int j = base + lane;
+    int cnt = 0;
+    double d0 = 0, d1 = 0;
+    if (j < m.njnt && m.jnt_limited[j]) {
+      const double q = e.qpos[m.jnt_qposadr[j]];
+      d0 = q - m.jnt_range[2 * j];
+      d1 = m.jnt_range[2 * j + 1] - q;
+      cnt = (d0 < 0) + (d1 < 0);
+    }
+    int total;
+    const int off = wave_excl_scan(cnt, lane, &total);
+    (void)off;
+    nlim += total;
+  }
+  // contacts rows
+  int nconrow = 0;
+  for (int c = 0; c < ncon; c++) nconrow += WI(con_condim)[c] == 1 ? 1 : 4;
+  int nefc = ne + nlim + nconrow;
+  if (nefc > nefc_max) nefc = nefc_max;
+  // zero the Jacobian rows in use
+  for (size_t k = lane; k < (size_t)nefc * nv; k += 64) J[k] = 0;
+  sync();
+  // equality rows (lane 0)
+  if (lane == 0) {
+    int r = 0;
+    for (int q = 0; q < m.neq; q++) {
+      const double* data = m.eq_data + RMBX_EQ_DATA * q;
+      const double* sr = m.eq_solref + 2 * q;
+      const double* si = m.eq_solimp + 5 * q;
+      const int o1 = m.eq_obj1[q], o2 = m.eq_obj2[q];
+      const int type = m.eq_type[q];
+      if (type == RMBX_EQ_CONNECT || type == RMBX_EQ_WELD) {
+        double p1[3], p2[3], t[3], err[6];
+        const int nr = type == RMBX_EQ_CONNECT ? 3 : 6;
+        const double* xm = W(xmat);
+        if (type == RMBX_EQ_CONNECT) {
+          matvec3(xm + 9 * o1, data, t);
+          for (int i = 0; i < 3; i++) p1[i] = e.xpos[3 * o1 + i] + t[i];
+          matvec3(xm + 9 * o2, data + 3, t);
+          for (int i = 0; i < 3; i++) p2[i] = e.xpos[3 * o2 + i] + t[i];
+        } else {
+          double Rr[9], ra[3], u[3];
+          quat2mat(data + 6, Rr);
+          matvec3(Rr, data, ra);
+          for (int i = 0; i < 3; i++) u[i] = data[3 + i] + ra[i];
+          matvec3(xm + 9 * o1, u, t);
+          for (int i = 0; i < 3; i++) p1[i] = e.xpos[3 * o1 + i] + t[i];
+          matvec3(xm + 9 * o2, data, t);
+          for (int i = 0; i < 3; i++) p2[i] = e.xpos[3 * o2 + i] + t[i];
+        }
+        for (int i = 0; i < 3; i++) err[i] = p1[i] - p2[i];
+        double q1r[4], qe[4], cq1[4];
+        if (nr == 6) {
+          quatmul(e.xquat + 4 * o1, data + 6, q1r);
+          cq1[0] = q1r[0];
+          cq1[1] = -q1r[1];
+          cq1[2] = -q1r[2];
+          cq1[3] = -q1r[3];
+          quatmul(cq1, e.xquat + 4 * o2, qe);
+          for (int i = 0; i < 3; i++) err[3 + i] = qe[1 + i] * data[10];
+        }
+        double nrm = 0;
+        for (int i = 0; i < nr; i++) nrm += err[i] * err[i];
+        nrm = sqrt(nrm);
+        const double diag_t = m.body_invweight0[2 * o1] + m.body_invweight0[2 * o2];
+        for (int i = 0; i < 3; i++) {
+          double dir[3] = {0, 0, 0};
+          dir[i] = 1;
+          set_row(e, r, 0, err[i], diag_t, sr, si, nrm);
+          jac_point_dir(e, o1, p1, dir, 1.0, J + (size_t)r * nv);
+          jac_point_dir(e, o2, p2, dir, -1.0, J + (size_t)r * nv);
+          r++;
+        }
+        if (nr == 6) {
+          const double diag_r = m.body_invweight0[2 * o1 + 1] + m.body_invweight0[2 * o2 + 1];
+          for (int i = 0; i < 3; i++) set_row(e, r + i, 0, err[3 + i], diag_r, sr, si, nrm);
+          // rotational columns: chains of o2 (+) and o1 (-); dofs shared cancel
+          const double* cdof = W(cdof);
+          for (int pass = 0; pass < 2; pass++) {
+            const int b = pass == 0 ? o2 : o1;
+            const double sg = pass == 0 ? 1.0 : -1.0;
+            for (int k = last_dof(m, b); k >= 0; k = m.dof_parent[k]) {
+              const double wq[4] = {0, sg * cdof[6 * k], sg * cdof[6 * k + 1], sg * cdof[6 * k + 2]};
+              double t1[4], t2[4];
+              quatmul(cq1, wq, t1);
+              quatmul(t1, e.xquat + 4 * o2, t2);
+              for (int i = 0; i < 3; i++) J[(size_t)(r + i) * nv + k] += 0.5 * t2[1 + i] * data[10];
+            }
+          }
+          r += 3;
+        }
+      } else {
+        const int j1 = o1, j2 = o2;
+        const double q1 = e.qpos[m.jnt_qposadr[j1]] - m.qpos0[m.jnt_qposadr[j1]];
+        const double q2 = e.qpos[m.jnt_qposadr[j2]] - m.qpos0[m.jnt_qposadr[j2]];
+        const double* c = data;
+        const double poly = c[0] + q2 * (c[1] + q2 * (c[2] + q2 * (c[3] + q2 * c[4])));
+        const double dpoly = c[1] + q2 * (2 * c[2] + q2 * (3 * c[3] + q2 * 4 * c[4]));
+        const double err = q1 - poly;
+        const int d1 = m.jnt_dofadr[j1], d2 = m.jnt_dofadr[j2];
+        set_row(e, r, 0, err, m.dof_invweight0[d1] + m.dof_invweight0[d2], sr, si, err);
+        J[(size_t)r * nv + d1] += 1;
+        J[(size_t)r * nv + d2] -= dpoly;
+        r++;
+      }
+    }
+  }
+  // limit rows
+  int rbase = ne;
+  for (int base = 0; base < m.njnt; base += 64) {
+    const int j = base + lane;
+    int cnt = 0;
+    double d0 = 0, d1 = 0;
+    if (j < m.njnt && m.jnt_limited[j]) {
+      const double q = e.qpos[m.jnt_qposadr[j]];
+      d0 = q - m.jnt_range[2 * j];
+      d1 = m.jnt_range[2 * j + 1] - q;
+      cnt = (d0 < 0) + (d1 < 0);
+    }
+    int total;
+    const int off = wave_excl_scan(cnt, lane, &total);
+    int r = rbase + off;
+    if (cnt) {
+      const int da = m.jnt_dofadr[j];
+      if (d0 < 0 && r < nefc) {
+        set_row(e, r, 1, d0, m.dof_invweight0[da], m.jnt_solref + 2 * j, m.jnt_solimp + 5 * j, d0);
+        J[(size_t)r * nv + da] = 1.0;
+        r++;
+      }
+      if (d1 < 0 && r < nefc) {
+        set_row(e, r, 1, d1, m.dof_invweight0[da], m.jnt_solref + 2 * j, m.jnt_solimp + 5 * j, d1);
+        J[(size_t)r * nv + da] = -1.0;
+      }
+    }
+    rbase += total;
+  }
+  // contact rows: row address = rbase + 4*c (condim 3) / running offset with condim 1
+  for (int base = 0; base < ncon; base += 64) {
+    const int c = base + lane;
+    const int cnt = c < ncon ? (WI(con_condim)[c] == 1 ? 1 : 4) : 0;
+    int total;
+    const int off = wave_excl_scan(cnt, lane, &total);
+    if (c < ncon) {
+      const int r0 = rbase + off;
+      WI(con_efcadr)[c] = r0;
+      const int p = WI(con_pair)[c];
+      const int b1 = WI(con_b1)[c], b2 = WI(con_b2)[c];
+      const double* F = W(con_frame) + 9 * c;
+      const double* pos = W(con_pos) + 3 * c;
+      const double tran = m.body_invweight0[2 * b1] + m.body_invweight0[2 * b2];
+      const double dist = W(con_dist)[c] - m.pair_margin[p];
+      const double* sr = m.pair_solref + 2 * p;
+      const double* si = m.pair_solimp + 5 * p;
+      if (cnt == 1) {
+        if (r0 < nefc) {
+          set_row(e, r0, 1, dist, tran, sr, si, dist);
+          jac_point_dir(e, b2, pos, F, 1.0, J + (size_t)r0 * nv);
+          jac_point_dir(e, b1, pos, F, -1.0, J + (size_t)r0 * nv);
+        }
+      } else {
+        const double mu = W(con_mu)[c];
+        int r = r0;
+        for (int t = 0; t < 2; t++)
+          for (int sg = 0; sg < 2; sg++) {
+            if (r < nefc) {
+              double dir[3];
+              const double s = sg == 0 ? mu : -mu;
+              for (int i = 0; i < 3; i++) dir[i] = F[i] + s * F[3 * (1 + t) + i];
+              set_row(e, r, 1, dist, tran * (1 + mu * mu), sr, si, dist);
+              jac_point_dir(e, b2, pos, dir, 1.0, J + (size_t)r * nv);
+              jac_point_dir(e, b1, pos, dir, -1.0, J + (size_t)r * nv);
+            }
+            r++;
+          }
+      }
+    }
+    rbase += total;
+  }
+  sync();
+  // aref = -b (J qvel) - k imp pos ; D = 1/R
+  for (int r = lane; r < nefc; r += 64) {
+    const double* Jr = J + (size_t)r * nv;
+    double v = 0;
+    for (int k = 0; k < nv; k++) v += Jr[k] * e.qvel[k];
+    W(efc_vel)[r] = v;
+    W(efc_aref)[r] = -W(efc_tmp)[r] * v - W(efc_D)[r];
+    W(efc_D)[r] = 1.0 / W(efc_R)[r];
+  }
+  sync();
+  *ne_out = ne;
+  return nefc;
+}
+
+// ------------------------------------------------------------------------------------------
+// dense linear algebra on the LDS matrix (one wave)
+// ------------------------------------------------------------------------------------------
+__device__ void lds_cholesky(double* A, int n, int lane) {
+  for (int j = 0; j < n; j++) {
+    // A[j][j] already holds the updated pivot (right-looking)
+    const double s = A[j * n + j];
+    const double d = sqrt(s > RMBX_MINVAL ? s : RMBX_MINVAL);
+    const double inv = 1.0 / d;
+    sync();
+    for (int i = j + 1 + lane; i < n; i += 64) A[i * n + j] *= inv;
+    if (lane == 0) A[j * n + j] = d;
+    sync();
+    for (int i = j + 1 + lane; i < n; i += 64) {
+      const double lij = A[i * n + j];
+      for (int k = j + 1; k <= i; k++) A[i * n + k] -= lij * A[k * n + j];
+    }
+    sync();
+  }
+}
+
+// x = A^-1 b with A = L L^T in LDS; x and b may alias; x in global/LDS visible to the wave
+__device__ void lds_chol_solve(const double* A, int n, const double* b, double* x, int lane) {
+  for (int i = lane; i < n; i += 64) x[i] = b[i];
+  sync();
+  for (int i = 0; i < n; i++) {
+    const double xi = x[i] / A[i * n + i];
+    sync();
+    if (lane == 0) x[i] = xi;
+    for (int k = i + 1 + lane; k < n; k += 64) x[k] -= A[k * n + i] * xi;
+    sync();
+  }
+  for (int i = n - 1; i >= 0; i--) {
+    const double xi = x[i] / A[i * n + i];
+    sync();
+    if (lane == 0) x[i] = xi;
+    for (int k = lane; k < i; k += 64) x[k] -= A[i * n + k] * xi;
+    sync();
+  }
+}
+
+__device__ void matvec_rows(const double* M, const double* x, double* y, int n, int lane) {
+  for (int i = lane; i < n; i += 64) {
+    const double* Mi = M + (size_t)i * n;
+    double s = 0;
+    for (int k = 0; k < n; k++) s += Mi[k] * x[k];
+    y[i] = s;
+  }
+  sync();
+}
+
+// ------------------------------------------------------------------------------------------
+// Newton solver (mj_solNewton), exact line search
+// ------------------------------------------------------------------------------------------
+__device__ double eval_cost(Env& e, const double* a, int nefc, int lane) {
+  const rmbx_model& m = *e.m;
+  const int nv = m.nv;
+  double* res = W(res);
+  double* Mres = W(Mres);
+  for (int k = lane; k < nv; k += 64) res[k] = a[k] - W(qacc_smooth)[k];
+  sync();
+  matvec_rows(W(M), res, Mres, nv, lane);
+  double part = 0;
+  for (int k = lane; k < nv; k += 64) part += res[k] * Mres[k];
+  double cost = 0.5 * wave_sum(part);
+  const double* J = W(J);
+  double cpart = 0;
+  for (int r = lane; r < nefc; r += 64) {
+    const double* Jr = J + (size_t)r * nv;
+    double s = 0;
+    for (int k = 0; k < nv; k++) s += Jr[k] * a[k];
+    const double jar = s - W(efc_aref)[r];
+    W(efc_jar)[r] = jar;
+    if (WI(efc_type)[r] == 0 || jar < 0) cpart += 0.5 * W(efc_D)[r] * jar * jar;
+  }
+  cost += wave_sum(cpart);
+  sync();
+  return cost;
+}
+
+__device__ int solve(Env& e, int nefc, int ne, int lane) {
+  const rmbx_model& m = *e.m;
+  const int nv = m.nv;
+  double* A = e.lds;
+  double* a = W(qacc);
+  const double* M = W(M);
+  const double* J = W(J);
+  // qacc_smooth = M^-1 qfrc_smooth
+  for (int k = lane; k < nv * nv; k += 64) A[k] = M[k];
+  sync();
+  lds_cholesky(A, nv, lane);
+  lds_chol_solve(A, nv, W(qfrc_smooth), W(qacc_smooth), lane);
+  const double c_ws = eval_cost(e, e.qacc_ws, nefc, lane);
+  const double c_sm = eval_cost(e, W(qacc_smooth), nefc, lane);
+  const double* start = c_ws < c_sm ? e.qacc_ws : W(qacc_smooth);
+  for (int k = lane; k < nv; k += 64) a[k] = start[k];
+  sync();
+  double cost = eval_cost(e, a, nefc, lane);
+  const double scale = 1.0 / (m.meaninertia * (nv > 1 ? nv : 1));
+  int it;
+  double* grad = W(grad);
+  double* search = W(search);
+  double* Ms = W(Ms);
+  for (it = 0; it < m.solver_iterations; it++) {
+    // gradient (lanes over columns, rows in order)
+    double gpart = 0;
+    for (int k = lane; k < nv; k += 64) {
+      double g = W(Mres)[k];
+      for (int r = 0; r < nefc; r++) {
+        const double jar = W(efc_jar)[r];
+        if (WI(efc_type)[r] == 0 || jar < 0) g += J[(size_t)r * nv + k] * (W(efc_D)[r] * jar);
+      }
+      grad[k] = g;
+      gpart += g * g;
+    }
+    const double gn = wave_sum(gpart);
+    sync();
+    if (scale * sqrt(gn) < m.solver_tolerance) break;
+    // Hessian rows (lane i owns row i): H[i][k] = M[i][k] + sum_r D_r J_ri J_rk, k <= i
+    for (int i = lane; i < nv; i += 64) {
+      for (int k = 0; k <= i; k++) A[i * nv + k] = M[i * nv + k];
+      for (int r = 0; r < nefc; r++) {
+        const double jar = W(efc_jar)[r];
+        if (!(WI(efc_type)[r] == 0 || jar < 0)) continue;
+        const double* Jr = J + (size_t)r * nv;
+        const double ji = Jr[i];
+        if (ji == 0) continue;
+        const double t = W(efc_D)[r] * ji;
+        for (int k = 0; k <= i; k++) A[i * nv + k] += t * Jr[k];
+      }
+    }
+    sync();
+    lds_cholesky(A, nv, lane);
+    lds_chol_solve(A, nv, grad, search, lane);
+    for (int k = lane; k < nv; k += 64) search[k] = -search[k];
+    sync();
+    matvec_rows(M, search, Ms, nv, lane);
+    double qp = 0, lp = 0;
+    for (int k = lane; k < nv; k += 64) {
+      qp += search[k] * Ms[k];
+      lp += W(res)[k] * Ms[k];
+    }
+    const double qg = wave_sum(qp), lg = wave_sum(lp);
+    for (int r = lane; r < nefc; r += 64) {
+      const double* Jr = J + (size_t)r * nv;
+      double s = 0;
+      for (int k = 0; k < nv; k++) s += Jr[k] * search[k];
+      W(efc_Js)[r] = s;
+    }
+    sync();
+    double alpha = 0, lo = 0, hi = 1e300;
+    for (int ls = 0; ls < m.ls_iterations; ls++) {
+      double p1 = 0, p2 = 0;
+      for (int r = lane; r < nefc; r += 64) {
+        const double js = W(efc_Js)[r];
+        const double x = W(efc_jar)[r] + alpha * js;
+        if (WI(efc_type)[r] == 0 || x < 0) {
+          p1 += W(efc_D)[r] * x * js;
+          p2 += W(efc_D)[r] * js * js;
+        }
+      }
+      const double d1 = alpha * qg + lg + wave_sum(p1);
+      const double d2 = qg + wave_sum(p2);
+      if (d1 == 0) break;
+      if (d1 < 0)
+        lo = alpha;
+      else
+        hi = alpha;
+      double an = alpha - d1 / d2;
+      if (!(an > lo && an < hi)) an = hi < 1e300 ? 0.5 * (lo + hi) : (an > lo ? an : lo);
+      int changed = 0;
+      for (int r = ne + lane; r < nefc; r += 64) {
+        const double js = W(efc_Js)[r];
+        const double x0 = W(efc_jar)[r] + alpha * js, x1 = W(efc_jar)[r] + an * js;
+        changed |= ((x0 < 0) != (x1 < 0));
+      }
+      alpha = an;
+      if (wave_sum_i(changed) == 0) break;
+    }
+    for (int k = lane; k < nv; k += 64) a[k] += alpha * search[k];
+    sync();
+    const double newcost = eval_cost(e, a, nefc, lane);
+    const double improvement = scale * (cost - newcost);
+    cost = newcost;
+    if (improvement < m.solver_tolerance) {
+      it++;
+      break;
+    }
+  }
+  // constraint forces and qfrc_constraint (lanes over columns)
+  for (int r = lane; r < nefc; r += 64) {
+    const double jar = W(efc_jar)[r];
+    W(efc_force)[r] = (WI(efc_type)[r] == 0 || jar < 0) ? -W(efc_D)[r] * jar : 0.0;
+  }
+  sync();
+  for (int k = lane; k < nv; k += 64) {
+    double s = 0;
+    for (int r = 0; r < nefc; r++) s += J[(size_t)r * nv + k] * W(efc_force)[r];
+    W(qfrc_constraint)[k] = s;
+  }
+  sync();
+  return it;
+}
+
+// ------------------------------------------------------------------------------------------
+// sensors (mj_rnePostConstraint -> force/torque at sites)
+// ------------------------------------------------------------------------------------------
+__device__ void sensors(Env& e, int ncon, int lane) {
+  const rmbx_model& m = *e.m;
+  if (m.nsensor == 0) return;
+  if (lane == 0) {
+    rne_forward(e, W(qacc));
+    double* cfrc = W(cfrc);
+    for (int c = 0; c < ncon; c++) {
+      const int r0 = WI(con_efcadr)[c];
+      if (r0 + (WI(con_condim)[c] == 1 ? 1 : 4) > e.L->nefc_max) continue;
+      const double* F = W(con_frame) + 9 * c;
+      double fn, f1 = 0, f2 = 0;
+      const double* f = W(efc_force) + r0;
+      if (WI(con_condim)[c] == 1) {
+        fn = f[0];
+      } else {
+        const double mu = W(con_mu)[c];
+        fn = f[0] + f[1] + f[2] + f[3];
+        f1 = mu * (f[0] - f[1]);
+        f2 = mu * (f[2] - f[3]);
+      }
+      double Fw[3], pxF[3];
+      for (int i = 0; i < 3; i++) Fw[i] = fn * F[i] + f1 * F[3 + i] + f2 * F[6 + i];
+      cross3(W(con_pos) + 3 * c, Fw, pxF);
+      const int b2 = WI(con_b2)[c], b1 = WI(con_b1)[c];
+      for (int i = 0; i < 3; i++) {
+        cfrc[6 * b2 + i] -= pxF[i];
+        cfrc[6 * b2 + 3 + i] -= Fw[i];
+        cfrc[6 * b1 + i] += pxF[i];
+        cfrc[6 * b1 + 3 + i] += Fw[i];
+      }
+    }
+  }
+  sync();
+  rne_backward(e, lane);
+  sync();
+  if (lane < m.nsensor && lane < 2) {
+    const int s = lane;
+    const int site = m.sensor_site[s];
+    const int b = m.site_body[site];
+    const double* f = W(cfrc) + 6 * b;
+    const double* p = W(sxpos) + 3 * site;
+    const double* R = W(sxmat) + 9 * site;
+    double out[3];
+    if (m.sensor_type[s] == RMBX_SENS_FORCE) {
+      mattvec3(R, f + 3, out);
+    } else {
+      double pxf[3], n[3];
+      cross3(p, f + 3, pxf);
+      for (int i = 0; i < 3; i++) n[i] = f[i] - pxf[i];
+      mattvec3(R, n, out);
+    }
+    for (int i = 0; i < 3; i++) e.sensordata[3 * s + i] = out[i];
+  }
+  sync();
+}
+
+// ------------------------------------------------------------------------------------------
+// implicitfast integration
+// ------------------------------------------------------------------------------------------
+__device__ void integrate(Env& e, int lane) {
+  const rmbx_model& m = *e.m;
+  const int nv = m.nv;
+  const double h = m.timestep;
+  double* A = e.lds;
+  const double* M = W(M);
+  for (int k = lane; k < nv * nv; k += 64) A[k] = M[k];
+  sync();
+  for (int k = lane; k < nv; k += 64) A[k * nv + k] += h * m.dof_damping[k];
+  sync();
+  if (lane == 0) {
+    for (int u = 0; u < m.nu; u++) {
+      const double kv = -m.act_bias[3 * u + 2];
+      if (kv == 0) continue;
+      const int id = m.act_trnid[u];
+      if (m.act_trntype[u] == RMBX_TRN_JOINT) {
+        const int k = m.jnt_dofadr[id];
+        A[k * nv + k] += h * kv;
+      } else {
+        for (int w1 = m.ten_adr[id]; w1 < m.ten_adr[id] + m.ten_num[id]; w1++)
+          for (int w2 = m.ten_adr[id]; w2 < m.ten_adr[id] + m.ten_num[id]; w2++) {
+            const int k1 = m.jnt_dofadr[m.wrap_jnt[w1]], k2 = m.jnt_dofadr[m.wrap_jnt[w2]];
+            A[k1 * nv + k2] += h * kv * m.wrap_coef[w1] * m.wrap_coef[w2];
+          }
+      }
+    }
+  }
+  sync();
+  lds_cholesky(A, nv, lane);
+  double* f = W(tmp);
+  for (int k = lane; k < nv; k += 64) f[k] = W(qfrc_smooth)[k] + W(qfrc_constraint)[k];
+  sync();
+  double* qacc = W(qacc);
+  lds_chol_solve(A, nv, f, qacc, lane);
+  bool bad = false;
+  for (int k = lane; k < nv; k += 64) {
+    const double a = qacc[k];
+    if (!isfinite(a) || fabs(a) > 1e10) bad = true;
+    e.qvel[k] += h * a;
+    e.qacc_ws[k] = a;
+  }
+  sync();
+  for (int j = lane; j < m.njnt; j += 64) {
+    const int qa = m.jnt_qposadr[j], da = m.jnt_dofadr[j];
+    if (m.jnt_type[j] == RMBX_JNT_FREE) {
+      for (int i = 0; i < 3; i++) e.qpos[qa + i] += h * e.qvel[da + i];
+      const double* w = e.qvel + da + 3;
+      const double nw = norm3(w);
+      double* q = e.qpos + qa + 3;
+      if (nw > RMBX_MINVAL) {
+        const double ax[3] = {w[0] / nw, w[1] / nw, w[2] / nw};
+        double qr[4];
+        axisangle_quat(ax, nw * h, qr);
+        quatmul(q, qr, q);
+      }
+      quatnorm(q);
+    } else {
+      e.qpos[qa] += h * e.qvel[da];
+    }
+  }
+  if (__any(bad) && lane == 0) e.stats[3] = 1;
+  if (lane == 0) e.time[0] += h;
+  sync();
+}
+
+// ------------------------------------------------------------------------------------------
+// the fused kernel
+// ------------------------------------------------------------------------------------------
+struct KArgs {
+  rmbx_model m;
+  Layout L;
+  rmbx_env_buffers b;
+  const uint8_t* active;
+  int n_env;
+  int nsub;
+  int integrate_flag;
+};
+
+__global__ void __launch_bounds__(64) physics_kernel(KArgs args) {
+  extern __shared__ __attribute__((aligned(16))) double smem[];
+  const int env = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (env >= args.n_env) return;
+  if (args.active && !args.active[env]) return;
+  const rmbx_model& m = args.m;
+  Env e;
+  e.m = &args.m;
+  e.L = &args.L;
+  e.ws = reinterpret_cast<double*>(args.b.workspace) + (size_t)env * args.L.stride;
+  e.iw = reinterpret_cast<int32_t*>(e.ws + args.L.ints);
+  e.qpos = args.b.qpos + (size_t)env * m.nq;
+  e.qvel = args.b.qvel + (size_t)env * m.nv;
+  e.qacc_ws = args.b.qacc_ws + (size_t)env * m.nv;
+  e.ctrl = args.b.ctrl + (size_t)env * m.nu;
+  e.body_pos = args.b.body_pos + (size_t)env * m.nbody * 3;
+  e.xpos = args.b.xpos + (size_t)env * m.nbody * 3;
+  e.xquat = args.b.xquat + (size_t)env * m.nbody * 4;
+  e.gxpos = args.b.gxpos + (size_t)env * m.ngeom * 3;
+  e.gxmat = args.b.gxmat + (size_t)env * m.ngeom * 9;
+  e.sensordata = args.b.sensordata + (size_t)env * 6;
+  e.time = args.b.time + env;
+  e.stats = args.b.stats + (size_t)env * 4;
+  e.lds = smem;
+  const int nsub = args.integrate_flag ? args.nsub : 1;
+  for (int s = 0; s < nsub; s++) {
+    kinematics(e, lane);
+    sync();
+    com_pos_crb(e, lane);
+    velocity_stage(e, lane);
+    const int ncon = collision(e, lane);
+    sync();
+    int ne = 0;
+    const int nefc = make_constraints(e, lane, ncon, &ne);
+    const int iters = solve(e, nefc, ne, lane);
+    sensors(e, ncon, lane);
+    if (lane == 0) {
+      e.stats[0] = ncon;
+      e.stats[1] = nefc;
+      e.stats[2] = iters;
+    }
+    if (args.integrate_flag) integrate(e, lane);
+  }
+}
+
+static Layout make_layout(const rmbx_model& m) {
+  Layout L{};
+  size_t o = 0;
+  auto take = [&](size_t n) {
+    const size_t r = o;
+    o += (n + 1) & ~size_t(1);  // keep 16-byte alignment
+    return r;
+  };
+  const int nv = m.nv, nb = m.nbody, nj = m.njnt, mc = m.max_contacts;
+  L.nefc_max = 4 * mc + 6 * m.neq + 2 * nj + 8;
+  L.xmat = take(9 * nb);
+  L.xipos = take(3 * nb);
+  L.xanchor = take(3 * nj);
+  L.xaxis = take(3 * nj);
+  L.sxpos = take(3 * m.nsite);
+  L.sxmat = take(9 * m.nsite);
+  L.cdof = take(6 * nv);
+  L.cdofdot = take(6 * nv);
+  L.cinert = take(10 * nb);
+  L.crb = take(10 * nb);
+  L.cvel = take(6 * nb);
+  L.cacc = take(6 * nb);
+  L.cfrc = take(6 * nb);
+  L.M = take((size_t)nv * nv);
+  L.qfrc_bias = take(nv);
+  L.qfrc_passive = take(nv);
+  L.qfrc_actuator = take(nv);
+  L.qfrc_smooth = take(nv);
+  L.qacc_smooth = take(nv);
+  L.qfrc_constraint = take(nv);
+  L.qacc = take(nv);
+  L.res = take(nv);
+  L.Mres = take(nv);
+  L.grad = take(nv);
+  L.search = take(nv);
+  L.Ms = take(nv);
+  L.tmp = take(nv);
+  L.ten_len = take(m.ntendon);
+  L.ten_vel = take(m.ntendon);
+  L.con_pos = take(3 * mc);
+  L.con_frame = take(9 * mc);
+  L.con_dist = take(mc);
+  L.con_mu = take(mc);
+  const int ne = L.nefc_max;
+  L.J = take((size_t)ne * nv);
+  L.efc_pos = take(ne);
+  L.efc_aref = take(ne);
+  L.efc_D = take(ne);
+  L.efc_R = take(ne);
+  L.efc_force = take(ne);
+  L.efc_jar = take(ne);
+  L.efc_Js = take(ne);
+  L.efc_vel = take(ne);
+  L.efc_tmp = take(ne);
+  L.ints = o;
+  size_t io = 0;
+  auto itake = [&](size_t n) {
+    const size_t r = io;
+    io += (n + 3) & ~size_t(3);
+    return r;
+  };
+  L.con_b1 = itake(mc);
+  L.con_b2 = itake(mc);
+  L.con_condim = itake(mc);
+  L.con_pair = itake(mc);
+  L.con_efcadr = itake(mc);
+  L.efc_type = itake(ne);
+  L.scal = itake(8);
+  L.istride = io;
+  L.stride = o + (io + 1) / 2;
+  L.stride = (L.stride + 31) & ~size_t(31);  // 256-byte aligned env slices
+  return L;
+}
+
+}  // namespace rmbx
+
+using namespace rmbx;
+
+// ------------------------------------------------------------------------------------------
+// C ABI
+// ------------------------------------------------------------------------------------------
+template <typename T>
+static int upload(rmbx_engine* eng, const T* src, size_t n, const T** dst) {
+  if (n == 0 || src == nullptr) {
+    *dst = nullptr;
+    return RMBX_OK;
+  }
+  void* p = nullptr;
+  RMBX_CHECK_HIP(hipMalloc(&p, n * sizeof(T)));
+  eng->allocations.push_back(p);
+  RMBX_CHECK_HIP(hipMemcpy(p, src, n * sizeof(T), hipMemcpyHostToDevice));
+  *dst = reinterpret_cast<const T*>(p);
+  return RMBX_OK;
+}
+
+extern "C" {
+
+int rmbx_engine_create(const struct rmbx_model* model, int n_env, rmbx_engine** out) {
+  RMBX_CHECK_ARG(model && out && n_env > 0, "bad arguments to rmbx_engine_create");
+  const rmbx_model& h = *model;
+  RMBX_CHECK_ARG(h.nv > 0 && h.nv <= 96, "nv=%d outside the supported range [1, 96]", h.nv);
+  RMBX_CHECK_ARG(h.max_contacts > 0 && h.max_contacts <= 1024, "bad max_contacts=%d",
+                 h.max_contacts);
+  rmbx_engine* eng = new rmbx_engine();
+  eng->host = h;
+  eng->dev = h;
+  eng->n_env = n_env;
+  eng->bound = false;
+  rmbx_model& d = eng->dev;
+  int st = RMBX_OK;
+#define UP(field, count)                                  \
+  if (st == RMBX_OK) st = upload(eng, h.field, (size_t)(count), &d.field);
+  UP(body_parent, h.nbody) UP(body_jntadr, h.nbody) UP(body_jntnum, h.nbody)
+  UP(body_dofadr, h.nbody) UP(body_dofnum, h.nbody) UP(body_weldid, h.nbody)
+  UP(body_rootid, h.nbody) UP(body_pos, 3 * h.nbody) UP(body_quat, 4 * h.nbody)
+  UP(body_mass, h.nbody) UP(body_ipos, 3 * h.nbody) UP(body_inertia, 9 * h.nbody)
+  UP(body_invweight0, 2 * h.nbody)
+  UP(jnt_type, h.njnt) UP(jnt_body, h.njnt) UP(jnt_qposadr, h.njnt) UP(jnt_dofadr, h.njnt)
+  UP(jnt_limited, h.njnt) UP(jnt_pos, 3 * h.njnt) UP(jnt_axis, 3 * h.njnt)
+  UP(jnt_range, 2 * h.njnt) UP(jnt_stiffness, h.njnt) UP(jnt_springref, h.njnt)
+  UP(jnt_solref, 2 * h.njnt) UP(jnt_solimp, 5 * h.njnt)
+  UP(dof_body, h.nv) UP(dof_jnt, h.nv) UP(dof_parent, h.nv) UP(dof_armature, h.nv)
+  UP(dof_damping, h.nv) UP(dof_invweight0, h.nv) UP(qpos0, h.nq)
+  UP(geom_type, h.ngeom) UP(geom_body, h.ngeom) UP(geom_ctype, h.ngeom)
+  UP(geom_size, 3 * h.ngeom) UP(geom_pos, 3 * h.ngeom) UP(geom_quat, 4 * h.ngeom)
+  UP(geom_rgba, 4 * h.ngeom) UP(geom_csize, 3 * h.ngeom) UP(geom_cpos, 3 * h.ngeom)
+  UP(geom_cquat, 4 * h.ngeom) UP(geom_rbound, h.ngeom)
+  UP(pair_geom1, h.npair) UP(pair_geom2, h.npair) UP(pair_condim, h.npair)
+  UP(pair_friction, 3 * h.npair) UP(pair_solref, 2 * h.npair) UP(pair_solimp, 5 * h.npair)
+  UP(pair_margin, h.npair)
+  UP(site_body, h.nsite) UP(site_pos, 3 * h.nsite) UP(site_quat, 4 * h.nsite)
+  UP(act_trntype, h.nu) UP(act_trnid, h.nu) UP(act_ctrllimited, h.nu) UP(act_forcelimited, h.nu)
+  UP(act_gain, h.nu) UP(act_bias, 3 * h.nu) UP(act_ctrlrange, 2 * h.nu)
+  UP(act_forcerange, 2 * h.nu)
+  UP(ten_adr, h.ntendon) UP(ten_num, h.ntendon) UP(wrap_jnt, h.nwrap) UP(wrap_coef, h.nwrap)
+  UP(eq_type, h.neq) UP(eq_obj1, h.neq) UP(eq_obj2, h.neq) UP(eq_data, RMBX_EQ_DATA * h.neq)
+  UP(eq_solref, 2 * h.neq) UP(eq_solimp, 5 * h.neq)
+  UP(sensor_type, h.nsensor) UP(sensor_site, h.nsensor)
+  UP(cam_body, h.ncam) UP(cam_pos, 3 * h.ncam) UP(cam_quat, 4 * h.ncam) UP(cam_fovy, h.ncam)
+#undef UP
+  if (st != RMBX_OK) {
+    rmbx_engine_destroy(eng);
+    return st;
+  }
+  eng->L = make_layout(h);
+  *out = eng;
+  return RMBX_OK;
+}
+
+int rmbx_engine_destroy(rmbx_engine* eng) {
+  if (!eng) return RMBX_OK;
+  for (void* p : eng->allocations) (void)hipFree(p);
+  delete eng;
+  return RMBX_OK;
+}
+
+int rmbx_engine_workspace_bytes(const rmbx_engine* eng, size_t* bytes) {
+  RMBX_CHECK_ARG(eng && bytes, "NULL argument");
+  *bytes = eng->L.stride * sizeof(double) * (size_t)eng->n_env;
+  return RMBX_OK;
+}
+
+int rmbx_engine_ws_offset(const rmbx_engine* eng, const char* name, size_t* offset,
+                          size_t* count) {
+  RMBX_CHECK_ARG(eng && name && offset && count, "NULL argument");
+  const Layout& L = eng->L;
+  const rmbx_model& m = eng->host;
+  const size_t nv = m.nv;
+  struct Item {
+    const char* n;
+    size_t off, cnt;
+  } items[] = {
+      {"stride", L.stride, L.stride},
+      {"M", L.M, nv * nv},
+      {"qfrc_bias", L.qfrc_bias, nv},
+      {"qfrc_passive", L.qfrc_passive, nv},
+      {"qfrc_actuator", L.qfrc_actuator, nv},
+      {"qfrc_smooth", L.qfrc_smooth, nv},
+      {"qacc_smooth", L.qacc_smooth, nv},
+      {"qfrc_constraint", L.qfrc_constraint, nv},
+      {"qacc", L.qacc, nv},
+      {"cdof", L.cdof, 6 * nv},
+      {"xmat", L.xmat, 9 * (size_t)m.nbody},
+      {"con_pos", L.con_pos, 3 * (size_t)m.max_contacts},
+      {"con_dist", L.con_dist, (size_t)m.max_contacts},
+      {"efc_force", L.efc_force, (size_t)L.nefc_max},
+      {"J", L.J, (size_t)L.nefc_max * nv},
+  };
+  for (const Item& it : items) {
+    if (strcmp(it.n, name) == 0) {
+      *offset = it.off;
+      *count = it.cnt;
+      return RMBX_OK;
+    }
+  }
+  rmbx::set_error("unknown workspace array '%s'", name);
+  return RMBX_ERR_ARG;
+}
+
+int rmbx_engine_bind(rmbx_engine* eng, const rmbx_env_buffers* bufs) {
+  RMBX_CHECK_ARG(eng && bufs, "NULL argument");
+  const rmbx_env_buffers& b = *bufs;
+  RMBX_CHECK_ARG(b.time && b.qpos && b.qvel && b.qacc_ws && b.ctrl && b.body_pos && b.xpos &&
+                     b.xquat && b.gxpos && b.gxmat && b.sensordata && b.stats && b.workspace,
+                 "every buffer of rmbx_env_buffers must be set");
+  RMBX_CHECK_ARG((reinterpret_cast<uintptr_t>(b.workspace) & 255) == 0,
+                 "workspace must be 256-byte aligned");
+  eng->bufs = b;
+  eng->bound = true;
+  return RMBX_OK;
+}
+
+static int launch(rmbx_engine* eng, int nsub, int integ, const uint8_t* active, void* stream) {
+  if (!eng->bound) {
+    rmbx::set_error("engine buffers are not bound (rmbx_engine_bind)");
+    return RMBX_ERR_STATE;
+  }
+  KArgs a;
+  a.m = eng->dev;
+  a.L = eng->L;
+  a.b = eng->bufs;
+  a.active = active;
+  a.n_env = eng->n_env;
+  a.nsub = nsub;
+  a.integrate_flag = integ;
+  const size_t lds = (size_t)eng->host.nv * eng->host.nv * sizeof(double);
+  hipLaunchKernelGGL(physics_kernel, dim3(eng->n_env), dim3(64), lds,
+                     reinterpret_cast<hipStream_t>(stream), a);
+  RMBX_CHECK_LAUNCH();
+  return RMBX_OK;
+}
+
+int rmbx_engine_step(rmbx_engine* eng, int nsub, const uint8_t* active, void* stream) {
+  RMBX_CHECK_ARG(eng && nsub >= 1, "bad arguments");
+  return launch(eng, nsub, 1, active, stream);
+}
+
+int rmbx_engine_forward(rmbx_engine* eng, const uint8_t* active, void* stream) {
+  RMBX_CHECK_ARG(eng, "NULL engine");
+  return launch(eng, 1, 0, active, stream);
+}
+
+}  // extern "C"

@@ -1,0 +1,80 @@
+"""Host-side handle of the batched physics engine (C ABI rmbx_engine_*, include/rmbx.h).
+
+Owns the torch device buffers bound to the engine (state, outputs, workspace) and exposes them
+as zero-copy tensors.  All work is enqueued on the current torch stream.
+"""
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _native as N
+from . import model as MD
+
+
+class PhysicsEngine:
+    def __init__(self, arrays, n_env, device="cuda:0"):
+        self.arrays = arrays
+        self.info = MD.ModelInfo(arrays)
+        self.n_env = int(n_env)
+        self.device = torch.device(device)
+        a = arrays
+        self.nq, self.nv, self.nu = int(a["_nq"]), int(a["_nv"]), int(a["_nu"])
+        self.nbody, self.ngeom = int(a["_nbody"]), int(a["_ngeom"])
+        self.timestep = float(a["_timestep"])
+        self._cmodel = MD.as_ctypes(arrays)
+        h = ctypes.c_void_p()
+        N.call("rmbx_engine_create", ctypes.byref(self._cmodel), self.n_env, ctypes.byref(h))
+        self._h = h
+        nbytes = ctypes.c_size_t()
+        N.call("rmbx_engine_workspace_bytes", self._h, ctypes.byref(nbytes))
+        n, dev, f64 = self.n_env, self.device, torch.float64
+        self.time = torch.zeros(n, dtype=f64, device=dev)
+        self.qpos = torch.tensor(np.tile(a["qpos0"], (n, 1)), dtype=f64, device=dev)
+        self.qvel = torch.zeros((n, self.nv), dtype=f64, device=dev)
+        self.qacc_ws = torch.zeros((n, self.nv), dtype=f64, device=dev)
+        self.ctrl = torch.zeros((n, self.nu), dtype=f64, device=dev)
+        self.body_pos = torch.tensor(np.tile(a["body_pos"].reshape(1, -1), (n, 1)), dtype=f64, device=dev).view(n, self.nbody, 3).contiguous()
+        self.xpos = torch.zeros((n, self.nbody, 3), dtype=f64, device=dev)
+        self.xquat = torch.zeros((n, self.nbody, 4), dtype=f64, device=dev)
+        self.gxpos = torch.zeros((n, self.ngeom, 3), dtype=f64, device=dev)
+        self.gxmat = torch.zeros((n, self.ngeom, 9), dtype=f64, device=dev)
+        self.sensordata = torch.zeros((n, 6), dtype=f64, device=dev)
+        self.stats = torch.zeros((n, 4), dtype=torch.int32, device=dev)
+        self.workspace = torch.zeros(nbytes.value, dtype=torch.uint8, device=dev)
+        assert self.workspace.data_ptr() % 256 == 0
+        b = N.EnvBuffers()
+        for name in ("time", "qpos", "qvel", "qacc_ws", "ctrl", "body_pos", "xpos", "xquat", "gxpos", "gxmat",
+                     "sensordata", "stats", "workspace"):
+            setattr(b, name, getattr(self, name).data_ptr())
+        self._bufs = b
+        N.call("rmbx_engine_bind", self._h, ctypes.byref(b))
+
+    def __del__(self):
+        h = getattr(self, "_h", None)
+        if h is not None and h.value:
+            try:
+                N.load().rmbx_engine_destroy(h)
+            except Exception:
+                pass
+            self._h = None
+
+    def step(self, nsub=8, active=None):
+        if active is not None and (active.dtype != torch.uint8 or active.numel() != self.n_env):
+            raise ValueError("active must be a uint8 tensor of n_env elements")
+        N.call("rmbx_engine_step", self._h, int(nsub), N.ptr(active), N.stream_ptr())
+
+    def forward(self, active=None):
+        N.call("rmbx_engine_forward", self._h, N.ptr(active), N.stream_ptr())
+
+    def _off(self, name):
+        off, cnt = ctypes.c_size_t(), ctypes.c_size_t()
+        N.call("rmbx_engine_ws_offset", self._h, name.encode(), ctypes.byref(off), ctypes.byref(cnt))
+        return off.value, cnt.value
+
+    def ws(self, name):
+        """Zero-copy [n_env, count] f64 view of a named workspace array (after step/forward)."""
+        stride, _ = self._off("stride")
+        off, cnt = self._off(name)
+        return self.workspace.view(torch.float64).view(self.n_env, stride)[:, off : off + cnt]
