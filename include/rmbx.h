@@ -168,6 +168,47 @@ int rmbx_engine_step(rmbx_engine* eng, int nsub, const uint8_t* active, void* st
 /* mj_forward only (no integration): fills the outputs and workspace for inspection. */
 int rmbx_engine_forward(rmbx_engine* eng, const uint8_t* active, void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Arm command: batched FK and damped-least-squares IK steps (reach phases).
+ * Replaces common/body/ArmManager.py:213-218 (forward_kinematics) and :220-243
+ * (inverse_kinematics, one iteration per call in the reference; n_iter here) with the Pinocchio
+ * URDF chain of envs/assets/common/robots/ur5e/ur5e.urdf (root pose folded into placement 0).
+ * placement f64 [6][12] (R row-major, p); q_cmd f64 [n][6] updated in place; target_R f64 [n][9];
+ * target_p f64 [n][3]; mask u8 [n] (NULL = all).
+ * ------------------------------------------------------------------------------------------- */
+int rmbx_arm_ik(const double* placement, double* q_cmd, const double* target_R,
+                const double* target_p, const uint8_t* mask, int n_env, int n_iter,
+                void* stream);
+int rmbx_arm_fk(const double* placement, const double* q, double* R_out, double* p_out,
+                int n_env, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Batched camera rendering (ray casting of the scene primitives).
+ * Replaces the per-camera OffScreenViewer rgb/depth renders of envs/mujoco/MujocoEnvBase.py:
+ * 112-126 for one camera over n_env envs.  Primitive table (device): prim_i32 [nprim][4]
+ * = (geom id, type, -, -), prim_f32 [nprim][8] = (size3, rgb3, -, -).  Geom frames come from the
+ * engine outputs gxpos/gxmat; the camera frame from body xpos/xquat + camera offset.
+ * Outputs (each optional): rgb u8 [n][H][W][3]; depth f32 [n][H][W] (linear camera-z distance,
+ * the quantity MujocoEnvBase.py:122-125 recovers); policy tensor [n][3][H][W] in bf16 (dtype 1)
+ * or f32 (dtype 0) = ((u8 / 255) - mean[c]) / std[c] (RolloutBase.py:479-490 + ImageNet
+ * normalisation of the ACT/MLP backbones).
+ * ------------------------------------------------------------------------------------------- */
+typedef struct rmbx_camera {
+  int32_t body;        /* body the camera is attached to (0 = world) */
+  int32_t width, height;
+  float fovy_deg;
+  double pos[3];       /* camera position in the body frame */
+  double quat[4];      /* camera orientation in the body frame (MuJoCo: looks along -z) */
+  float znear, zfar;   /* clip distances for depth (metres) */
+  float mean[3], std[3];
+} rmbx_camera;
+
+int rmbx_render(const rmbx_camera* cam, const int32_t* prim_i32, const float* prim_f32,
+                int nprim, const double* gxpos, const double* gxmat, const double* xpos,
+                const double* xquat, int ngeom, int nbody, uint8_t* rgb, float* depth,
+                void* policy_img, int policy_dtype, const uint8_t* active, int n_env,
+                void* stream);
+
 #ifdef __cplusplus
 }
 #endif

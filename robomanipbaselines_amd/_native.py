@@ -38,7 +38,20 @@ SIGNATURES = {
     "rmbx_engine_bind": (_c_int, [_c_p, _c_p]),
     "rmbx_engine_step": (_c_int, [_c_p, _c_int, _c_p, _c_p]),
     "rmbx_engine_forward": (_c_int, [_c_p, _c_p, _c_p]),
+    "rmbx_arm_ik": (_c_int, [_c_p] * 5 + [_c_int, _c_int, _c_p]),
+    "rmbx_arm_fk": (_c_int, [_c_p] * 4 + [_c_int, _c_p]),
+    "rmbx_render": (_c_int, [_c_p, _c_p, _c_p, _c_int, _c_p, _c_p, _c_p, _c_p, _c_int, _c_int, _c_p, _c_p, _c_p,
+                             _c_int, _c_p, _c_int, _c_p]),
 }
+
+
+class Camera(ctypes.Structure):
+    """ctypes mirror of rmbx_camera (include/rmbx.h)."""
+
+    _fields_ = [("body", ctypes.c_int32), ("width", ctypes.c_int32), ("height", ctypes.c_int32),
+                ("fovy_deg", ctypes.c_float), ("pos", ctypes.c_double * 3), ("quat", ctypes.c_double * 4),
+                ("znear", ctypes.c_float), ("zfar", ctypes.c_float), ("mean", ctypes.c_float * 3),
+                ("std", ctypes.c_float * 3)]
 
 
 class EnvBuffers(ctypes.Structure):

@@ -186,6 +186,9 @@ def pack(M, max_contacts=128, solver_iterations=100, ls_iterations=30, solver_to
     out["names_site"] = np.array([s["name"] for s in M.sites])
     out["names_cam"] = np.array([c["name"] for c in M.cams])
     out["names_act"] = np.array([x["name"] for x in acts])
+    # render-only attributes (not part of rmbx_model)
+    out["geom_group"] = np.array([x["group"] for x in g], dtype=np.int32)
+    out["cam_fovy_deg"] = np.array([c["fovy"] for c in M.cams], dtype=np.float64)
     return out
 
 

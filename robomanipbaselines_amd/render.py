@@ -1,0 +1,92 @@
+"""Batched camera rendering front end (C ABI rmbx_render).
+
+Builds the primitive table of a compiled scene and renders one camera for all envs of a
+PhysicsEngine.  Visual meshes are drawn through their body's collision primitives (capsules,
+mesh bounding boxes) in the mesh's material colour; primitive visual geoms are drawn as they
+are; textures are not sampled (documented substitution: images are not pixel-identical to
+MuJoCo's OpenGL renderer).
+"""
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _native as N
+from .mjcf import compiler as C
+
+IMAGENET_MEAN = (0.485, 0.456, 0.406)
+IMAGENET_STD = (0.229, 0.224, 0.225)
+
+
+def build_prims(arrays):
+    gt, gb, gg = arrays["geom_type"], arrays["geom_body"], arrays["geom_group"]
+    ct, cs, size, rgba = arrays["geom_ctype"], arrays["geom_csize"], arrays["geom_size"], arrays["geom_rgba"]
+    mesh_color = {}
+    for g in range(len(gt)):
+        if gt[g] == C.GEOM_MESH and gg[g] <= 2 and gb[g] not in mesh_color:
+            mesh_color[int(gb[g])] = rgba[g][:3]
+    pi, pf = [], []
+    for g in range(len(gt)):
+        t = int(gt[g])
+        if t != C.GEOM_MESH and gg[g] <= 2 and t in (C.GEOM_PLANE, C.GEOM_SPHERE, C.GEOM_CAPSULE, C.GEOM_CYLINDER, C.GEOM_BOX):
+            pi.append([g, t, 0, 0])
+            pf.append(list(size[g][:3]) + list(rgba[g][:3]) + [0, 0])
+        elif ct[g] >= 0 and gg[g] >= 3 and int(gb[g]) in mesh_color:
+            typ = int(ct[g])
+            pi.append([g, typ, 0, 0])
+            pf.append(list(cs[g][:3]) + list(mesh_color[int(gb[g])]) + [0, 0])
+    return np.array(pi, np.int32), np.array(pf, np.float32)
+
+
+class Renderer:
+    def __init__(self, arrays, device, width=640, height=480):
+        self.arrays = arrays
+        pi, pf = build_prims(arrays)
+        self.nprim = len(pi)
+        self.prim_i32 = torch.tensor(pi, device=device)
+        self.prim_f32 = torch.tensor(pf, device=device)
+        self.width, self.height = width, height
+        self.cam_names = [str(x) for x in arrays["names_cam"]]
+        self.znear = float(arrays["_znear"]) * float(arrays["_extent"])
+        self.zfar = float(arrays["_zfar"]) * float(arrays["_extent"])
+
+    def camera(self, name):
+        a = self.arrays
+        i = self.cam_names.index(name)
+        c = N.Camera()
+        c.body = int(a["cam_body"][i])
+        c.width, c.height = self.width, self.height
+        c.fovy_deg = float(a["cam_fovy"][i])
+        for k in range(3):
+            c.pos[k] = float(a["cam_pos"][i][k])
+        for k in range(4):
+            c.quat[k] = float(a["cam_quat"][i][k])
+        c.znear, c.zfar = self.znear, self.zfar
+        for k in range(3):
+            c.mean[k] = IMAGENET_MEAN[k]
+            c.std[k] = IMAGENET_STD[k]
+        return c
+
+    def render(self, engine, camera_name, rgb=None, depth=None, policy=None, active=None, mean=None, std=None):
+        """Render `camera_name` for every env of `engine` into the given (optional) tensors:
+        rgb u8 [n,H,W,3], depth f32 [n,H,W], policy bf16/f32 [n,3,H,W]."""
+        cam = self.camera(camera_name)
+        if mean is not None:
+            for k in range(3):
+                cam.mean[k] = float(mean[k])
+                cam.std[k] = float(std[k])
+        n, H, W = engine.n_env, self.height, self.width
+        if rgb is not None:
+            assert rgb.dtype == torch.uint8 and tuple(rgb.shape) == (n, H, W, 3) and rgb.is_contiguous()
+        if depth is not None:
+            assert depth.dtype == torch.float32 and tuple(depth.shape) == (n, H, W) and depth.is_contiguous()
+        pdt = 0
+        if policy is not None:
+            assert tuple(policy.shape) == (n, 3, H, W) and policy.is_contiguous()
+            assert policy.dtype in (torch.float32, torch.bfloat16)
+            pdt = 1 if policy.dtype == torch.bfloat16 else 0
+        N.call("rmbx_render", ctypes.byref(cam), N.ptr(self.prim_i32), N.ptr(self.prim_f32), self.nprim,
+               N.ptr(engine.gxpos), N.ptr(engine.gxmat), N.ptr(engine.xpos), N.ptr(engine.xquat),
+               engine.ngeom, engine.nbody, N.ptr(rgb), N.ptr(depth), N.ptr(policy), pdt, N.ptr(active), n,
+               N.stream_ptr())

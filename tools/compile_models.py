@@ -9,12 +9,31 @@ from robomanipbaselines_amd.mjcf import compiler as C  # noqa: E402
 
 REF_ENVS = "/root/reference/robo_manip_baselines/envs/assets/mujoco/envs"
 SCENES = {"ur5e_cable": os.path.join(REF_ENVS, "ur5e", "env_ur5e_cable.xml")}
+UR5E_URDF = "/root/reference/robo_manip_baselines/envs/assets/common/robots/ur5e/ur5e.urdf"
+
+
+def add_arm_ik(M, arrays, root_body="ur5e_root_frame"):
+    """Pinocchio-equivalent joint placements of the UR5e URDF chain with the arm root pose read
+    from the compiled MJCF at qpos0 (MujocoUR5eEnvBase.py:40-45, ArmManager.py:48-71)."""
+    import numpy as np
+    from robomanipbaselines_amd.mjcf import urdf
+
+    xpos, xmat, _, _ = C.kinematics(M, M.qpos0)
+    b = M.body_name.index(root_body)
+    root = np.eye(4)
+    root[:3, :3] = xmat[b]
+    root[:3, 3] = xpos[b]
+    P, axes, names = urdf.arm_chain(UR5E_URDF, 6, root)
+    arrays["arm_placement"] = np.ascontiguousarray(np.concatenate([P[:, :3, :3].reshape(6, 9), P[:, :3, 3]], 1))
+    arrays["arm_axis"] = np.ascontiguousarray(axes)
+    arrays["arm_joint_names"] = np.array(names)
 
 if __name__ == "__main__":
     os.makedirs(MD.ASSET_DIR, exist_ok=True)
     for name, path in SCENES.items():
         M = C.compile_mjcf(path)
         arrays = MD.pack(M)
+        add_arm_ik(M, arrays)
         out = os.path.join(MD.ASSET_DIR, name + ".npz")
         MD.save(arrays, out)
         print(name, "nq", M.nq, "nv", M.nv, "pairs", len(M.pairs), "->", out, os.path.getsize(out), "bytes")
