@@ -167,6 +167,10 @@ int rmbx_engine_bind(rmbx_engine* eng, const rmbx_env_buffers* bufs);
 int rmbx_engine_step(rmbx_engine* eng, int nsub, const uint8_t* active, void* stream);
 /* mj_forward only (no integration): fills the outputs and workspace for inspection. */
 int rmbx_engine_forward(rmbx_engine* eng, const uint8_t* active, void* stream);
+/* Diagnostic: step all envs and accumulate per-stage shader cycles into stage_cycles
+ * [n_env][16] (u64, device): kinematics, com/crb, velocity+rne+actuation, collision,
+ * constraints, solver, sensors, integration. */
+int rmbx_engine_step_profiled(rmbx_engine* eng, int nsub, uint64_t* stage_cycles, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Arm command: batched FK and damped-least-squares IK steps (reach phases).

@@ -38,6 +38,7 @@ SIGNATURES = {
     "rmbx_engine_bind": (_c_int, [_c_p, _c_p]),
     "rmbx_engine_step": (_c_int, [_c_p, _c_int, _c_p, _c_p]),
     "rmbx_engine_forward": (_c_int, [_c_p, _c_p, _c_p]),
+    "rmbx_engine_step_profiled": (_c_int, [_c_p, _c_int, _c_p, _c_p]),
     "rmbx_arm_ik": (_c_int, [_c_p] * 5 + [_c_int, _c_int, _c_p]),
     "rmbx_arm_fk": (_c_int, [_c_p] * 4 + [_c_int, _c_p]),
     "rmbx_render": (_c_int, [_c_p, _c_p, _c_p, _c_int, _c_p, _c_p, _c_p, _c_p, _c_int, _c_int, _c_p, _c_p, _c_p,

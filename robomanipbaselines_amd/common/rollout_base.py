@@ -1,0 +1,287 @@
+"""Batched rollout plugin base: n_env environments step in lockstep on one GPU.
+
+Mirrors common/base/RolloutBase.py of the reference (hook names, argparse flags, phase
+semantics, results schema) for a batch of envs:
+
+* phases: InitialRolloutPhase (1.0 s), the Operation's pre-motion phases (timed reach/grasp),
+  RolloutPhase (policy every `skip` steps, success latch, +1.0 s after success or max_duration,
+  --auto_exit), EndRolloutPhase — RolloutBase.py:28-132, PhaseBase.py:41-106.  All phase
+  transitions are driven by the simulation clock, so the pre-rollout schedule is identical for
+  every env and is tracked on the host; per-env termination/results live in the device
+  schedule (rmbx_sched_update).
+* the step loop (RolloutBase.py:387-426): pre_update -> env action -> env.step ->
+  post_update -> check_transition, with cv2.waitKey / plotting removed (headless).
+* results: {"success": [...], "reward": [...], "duration": [...]} per env in env order, the
+  `Rollout result: success|failure` stdout contract (RolloutBase.py:96-107) and the optional
+  YAML file (RolloutBase.py:417-422); inference-duration statistics (RolloutBase.py:528-539).
+"""
+
+import argparse
+import sys
+import time
+
+import numpy as np
+import torch
+import yaml
+
+from .. import kernels as K
+from ..common.data_key import DataKey
+from ..common.data_utils import make_meta_info
+
+
+class PhaseSpec:
+    """Timed phase of the pre-rollout motion (PhaseBase.ReachPhaseBase / GraspPhaseBase)."""
+
+    def __init__(self, name, duration, kind, pos_z=None):
+        self.name, self.duration, self.kind, self.pos_z = name, duration, kind, pos_z
+
+
+class BatchedRolloutBase:
+    require_task_desc = False
+    policy_name = "Policy"
+
+    def __init__(self, argv=None, **overrides):
+        self.setup_args(argv=argv)
+        for k, v in overrides.items():
+            setattr(self.args, k, v)
+        torch.manual_seed(self.args.seed)
+        np.random.seed(self.args.seed)
+        self.device = torch.device(self.args.device)
+        self.setup_env()
+        self.setup_model_meta_info()
+        self.setup_policy()
+        self.n = self.env.num_envs
+        self.pre_phases = self.get_pre_motion_phases()
+        self.pre_durations = [1.0] + [p.duration for p in self.pre_phases]  # Initial phase: 1.0 s
+        self.result = {key: [] for key in ("success", "reward", "duration")}
+        self.inference_duration_list = []
+
+    # -- arguments (RolloutBase.setup_args :165-284 + batching flags) --------------------------
+    def setup_args(self, parser=None, argv=None):
+        if parser is None:
+            parser = argparse.ArgumentParser(formatter_class=argparse.ArgumentDefaultsHelpFormatter)
+        parser.add_argument("--checkpoint", type=str, default=None, help="checkpoint file (random init if omitted)")
+        parser.add_argument("--world_idx", type=int, default=0)
+        parser.add_argument("--world_idx_list", type=int, nargs="*", default=None)
+        parser.add_argument("--world_random_scale", nargs="+", type=float, default=None)
+        parser.add_argument("--skip", type=int, default=None)
+        parser.add_argument("--skip_draw", type=int, default=None)
+        parser.add_argument("--seed", type=int, default=0)
+        parser.add_argument("--no_render", action="store_true")
+        parser.add_argument("--no_plot", action="store_true")
+        parser.add_argument("--win_xy_plot", type=int, nargs=2)
+        parser.add_argument("--wait_before_start", action="store_true")
+        parser.add_argument("--auto_exit", action="store_true")
+        parser.add_argument("--max_duration", type=float, default=30.0)
+        parser.add_argument("--result_filename", type=str, default=None)
+        parser.add_argument("--save_last_image", action="store_true")
+        parser.add_argument("--output_image_dir", type=str, default=".")
+        # batching (this engine)
+        parser.add_argument("--num_envs", type=int, default=1, help="environments stepped in lockstep")
+        parser.add_argument("--device", type=str, default="cuda:0")
+        parser.add_argument("--precision", choices=["fp32", "bf16"], default="bf16",
+                            help="policy arithmetic: fp32 (parity mode) or bf16 (throughput mode)")
+        parser.add_argument("--max_steps", type=int, default=None, help="hard cap on env-steps")
+        if self.require_task_desc:
+            parser.add_argument("--task_desc", type=str, required=True)
+        self.set_additional_args(parser)
+        if argv is None:
+            argv = sys.argv[1:]
+        self.args = parser.parse_args(argv)
+        if self.args.world_idx_list is None:
+            self.args.world_idx_list = [self.args.world_idx]
+        if self.args.world_random_scale is not None:
+            self.args.world_random_scale = np.array(self.args.world_random_scale)
+        self.args.auto_exit = True  # headless batched evaluation always auto-exits
+
+    def set_additional_args(self, parser):
+        pass
+
+    def setup_model_meta_info(self):
+        self.model_meta_info = make_meta_info(self)
+        self.state_keys = self.model_meta_info["state"]["keys"]
+        self.action_keys = self.model_meta_info["action"]["keys"]
+        self.camera_names = self.model_meta_info["image"]["camera_names"]
+        self.state_dim = len(self.model_meta_info["state"]["example"])
+        self.action_dim = len(self.model_meta_info["action"]["example"])
+        if self.args.skip is None:
+            self.args.skip = self.model_meta_info["data"]["skip"]
+        if self.args.skip_draw is None:
+            self.args.skip_draw = self.args.skip
+
+    def setup_env(self):
+        raise NotImplementedError("defined by the Operation mixin")
+
+    def setup_policy(self):
+        raise NotImplementedError
+
+    def get_pre_motion_phases(self):
+        return []
+
+    def reset_variables(self):
+        pass
+
+    def infer_policy(self):
+        raise NotImplementedError
+
+    def draw_plot(self):
+        pass
+
+    # -- state / images (RolloutBase.get_state :463-477, get_images :479-490) -----------------
+    def get_state(self):
+        jp = self.obs["joint_pos"]
+        st = self.model_meta_info["state"]
+        if st.get("norm_config", {}).get("type", "gaussian") == "gaussian":
+            return ((jp - self._st_mean) / self._st_std).to(torch.float32)
+        scale = (st["norm_config"]["out_max"] - st["norm_config"]["out_min"]) / self._st_range
+        return (scale * (jp - self._st_min) + st["norm_config"]["out_min"]).to(torch.float32)
+
+    def get_images(self, dtype):
+        """Render every policy camera straight into the normalised policy tensor [n,ncam,3,H,W]."""
+        H, W = self.env.renderer.height, self.env.renderer.width
+        if getattr(self, "_img", None) is None or self._img.dtype != dtype:
+            self._img = torch.empty((self.n, len(self.camera_names), 3, H, W), dtype=dtype, device=self.device)
+            self._img_cam = [torch.empty((self.n, 3, H, W), dtype=dtype, device=self.device) for _ in self.camera_names]
+        if len(self.camera_names) == 1:
+            self.env.render_images(self.camera_names[0], policy=self._img.view(self.n, 3, H, W))
+            return self._img
+        for i, cam in enumerate(self.camera_names):
+            self.env.render_images(cam, policy=self._img_cam[i])
+            self._img[:, i].copy_(self._img_cam[i])
+        return self._img
+
+    # -- command routing (MotionManager / ArmManager) ------------------------------------------
+    def _reset_motion(self):
+        env = self.env
+        self.q_cmd = torch.tensor(np.tile(env.init_qpos[:6], (self.n, 1)), dtype=torch.float64, device=self.device)
+        self.grip_cmd = torch.zeros((self.n, 1), dtype=torch.float64, device=self.device)
+        self._placement = torch.tensor(env.arrays["arm_placement"], dtype=torch.float64, device=self.device)
+        self._glo, self._ghi = float(env.action_low[6]), float(env.action_high[6])
+
+    def set_command_data(self):
+        """ArmManager.set_command_joint_pos (:125-129) + gripper clip (:141-146)."""
+        a = self.policy_action
+        self.q_cmd.copy_(a[:, :6])
+        self.grip_cmd.copy_(a[:, 6:7].clamp(self._glo, self._ghi))
+
+    def env_action(self):
+        return torch.cat([self.q_cmd, self.grip_cmd], dim=1)
+
+    def _set_reach_target(self, pos_z):
+        """OperationMujocoUR5eCable.get_target_se3 (:8-11): cable_end xy, fixed z, R=diag(-1,1,-1)."""
+        end = self.env.get_body_pose("cable_end")[:, :3].clone()
+        end[:, 2] = pos_z
+        self._tgt_p = end.contiguous()
+        R = torch.tensor([-1.0, 0, 0, 0, 1.0, 0, 0, 0, -1.0], dtype=torch.float64, device=self.device)
+        self._tgt_R = R.expand(self.n, 9).contiguous()
+
+    def _ik_step(self):
+        from .. import _native as N
+
+        N.call("rmbx_arm_ik", N.ptr(self._placement), N.ptr(self.q_cmd), N.ptr(self._tgt_R), N.ptr(self._tgt_p),
+               None, self.n, 1, N.stream_ptr())
+
+    # -- episode --------------------------------------------------------------------------------
+    def reset(self):
+        self._reset_motion()
+        world = np.array([self.args.world_idx_list[e % len(self.args.world_idx_list)] for e in range(self.n)])
+        self.env.world_random_scale = self.args.world_random_scale
+        self.world_idx = self.env.modify_world(world_idx=world)
+        self.obs, self.info = self.env.reset(seed=self.args.seed)
+        st = self.model_meta_info["state"]
+        dev = self.device
+        if "mean" in st:
+            self._st_mean = torch.tensor(st["mean"], dtype=torch.float64, device=dev)
+            self._st_std = torch.tensor(st["std"], dtype=torch.float64, device=dev)
+        if "min" in st:
+            self._st_min = torch.tensor(st["min"], dtype=torch.float64, device=dev)
+            self._st_range = torch.tensor(st["range"], dtype=torch.float64, device=dev)
+        self.sched = K.sched_alloc(self.n, dev)
+        K.sched_reset(self.sched, self.env.get_time())
+        self._pre = torch.tensor(self.pre_durations, dtype=torch.float64, device=dev)
+        # host mirror of the (env-independent) pre-rollout clock
+        self.phase_idx = 0
+        self.host_time = 0.0
+        self.phase_start = 0.0
+        self.rollout_time_idx = 0
+        self.policy_action = torch.zeros((self.n, self.action_dim), dtype=torch.float64, device=dev)
+        self.reset_variables()
+
+    def _pre_update(self):
+        n_pre = len(self.pre_durations)
+        if self.phase_idx == 0:
+            return
+        if self.phase_idx < n_pre:
+            ph = self.pre_phases[self.phase_idx - 1]
+            if ph.kind == "reach":
+                self._ik_step()
+            elif ph.kind == "grasp":
+                self.grip_cmd.fill_(self._ghi)  # GraspPhaseBase.set_target_close (:78-104)
+        elif self.phase_idx == n_pre:
+            if self.rollout_time_idx % self.args.skip == 0:
+                t0 = time.time()
+                self.infer_policy()
+                self.inference_duration_list.append(time.time() - t0)
+            self.set_command_data()
+
+    def _host_transition(self):
+        """Host mirror of the pre-rollout phase clock (PhaseBase.get_elapsed_duration)."""
+        n_pre = len(self.pre_durations)
+        if self.phase_idx < n_pre:
+            if self.host_time - self.phase_start > self.pre_durations[self.phase_idx]:
+                self.phase_idx += 1
+                self.phase_start = self.host_time
+                if self.phase_idx < n_pre:
+                    ph = self.pre_phases[self.phase_idx - 1]
+                    if ph.kind == "reach":
+                        self._set_reach_target(ph.pos_z)
+                else:
+                    self.rollout_time_idx = 0
+        elif self.phase_idx == n_pre:
+            self.rollout_time_idx += 1
+
+    def step_once(self):
+        self._pre_update()
+        self.obs, self.reward, _, _, _ = self.env.step(self.env_action(), active=self._active)
+        for _ in range(self.env.frame_skip):
+            self.host_time += self.env.sim_timestep
+        K.sched_update(self.sched, self.env.get_time(), self.reward, self._pre, self.args.max_duration)
+        self._host_transition()
+
+    def run(self, max_steps=None):
+        self.reset()
+        self._active = None
+        max_steps = max_steps or self.args.max_steps or 10**9
+        steps = 0
+        while steps < max_steps:
+            self.step_once()
+            steps += 1
+            if self.phase_idx >= len(self.pre_durations) and steps % 16 == 0:
+                v = K.sched_view(self.sched)
+                if v["done"].all():
+                    break
+                self._active = torch.tensor(1 - v["done"], dtype=torch.uint8, device=self.device)
+        self.finish()
+        return steps
+
+    def finish(self):
+        v = K.sched_view(self.sched)
+        for e in range(self.n):
+            succ = bool(v["success"][e])
+            print(f"Rollout result: {'success' if succ else 'failure'}", flush=True)
+            self.result["success"].append(succ)
+            self.result["reward"].append(float(v["result_reward"][e]))
+            self.result["duration"].append(float(v["duration"][e]))
+        if self.args.result_filename is not None:
+            with open(self.args.result_filename, "w") as f:
+                yaml.dump(self.result, f)
+        self.print_statistics()
+
+    def print_statistics(self):
+        print(f"[{self.__class__.__name__}] Statistics on policy inference")
+        if self.inference_duration_list:
+            a = np.array(self.inference_duration_list)
+            print(f"  - Inference duration [s] | mean: {a.mean():.2e}, std: {a.std():.2e} min: {a.min():.2e}, max: {a.max():.2e}")
+            print(f"  - Inference duration per env [us] | mean: {1e6 * a.mean() / self.n:.2f}")
+        if torch.cuda.is_available():
+            print(f"  - GPU memory usage [GB] | {torch.cuda.max_memory_reserved() / 1024**3:.3f}")

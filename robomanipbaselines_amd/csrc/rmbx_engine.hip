@@ -1510,7 +1510,12 @@ struct KArgs {
   int n_env;
   int nsub;
   int integrate_flag;
+  unsigned long long* prof;  // optional [n_env][16] per-stage cycle sums (diagnostic)
 };
+
+__device__ __forceinline__ unsigned long long stamp() {
+  return __builtin_readcyclecounter();
+}
 
 __global__ void __launch_bounds__(64) physics_kernel(KArgs args) {
   extern __shared__ __attribute__((aligned(16))) double smem[];
@@ -1538,24 +1543,43 @@ __global__ void __launch_bounds__(64) physics_kernel(KArgs args) {
   e.stats = args.b.stats + (size_t)env * 4;
   e.lds = smem;
   const int nsub = args.integrate_flag ? args.nsub : 1;
+  unsigned long long* prof = args.prof ? args.prof + (size_t)env * 16 : nullptr;
+  unsigned long long t0 = 0, t1 = 0;
+#define PROF(k)                                   \
+  if (prof) {                                     \
+    sync();                                       \
+    t1 = stamp();                                 \
+    if (lane == 0) prof[k] += t1 - t0;            \
+    t0 = t1;                                      \
+  }
+  if (prof) t0 = stamp();
   for (int s = 0; s < nsub; s++) {
     kinematics(e, lane);
     sync();
+    PROF(0)
     com_pos_crb(e, lane);
+    PROF(1)
     velocity_stage(e, lane);
+    PROF(2)
     const int ncon = collision(e, lane);
     sync();
+    PROF(3)
     int ne = 0;
     const int nefc = make_constraints(e, lane, ncon, &ne);
+    PROF(4)
     const int iters = solve(e, nefc, ne, lane);
+    PROF(5)
     sensors(e, ncon, lane);
+    PROF(6)
     if (lane == 0) {
       e.stats[0] = ncon;
       e.stats[1] = nefc;
       e.stats[2] = iters;
     }
     if (args.integrate_flag) integrate(e, lane);
+    PROF(7)
   }
+#undef PROF
 }
 
 static Layout make_layout(const rmbx_model& m) {
@@ -1770,7 +1794,8 @@ int rmbx_engine_bind(rmbx_engine* eng, const rmbx_env_buffers* bufs) {
   return RMBX_OK;
 }
 
-static int launch(rmbx_engine* eng, int nsub, int integ, const uint8_t* active, void* stream) {
+static int launch(rmbx_engine* eng, int nsub, int integ, const uint8_t* active, void* stream,
+                  unsigned long long* prof = nullptr) {
   if (!eng->bound) {
     rmbx::set_error("engine buffers are not bound (rmbx_engine_bind)");
     return RMBX_ERR_STATE;
@@ -1783,6 +1808,7 @@ static int launch(rmbx_engine* eng, int nsub, int integ, const uint8_t* active, 
   a.n_env = eng->n_env;
   a.nsub = nsub;
   a.integrate_flag = integ;
+  a.prof = prof;
   const size_t lds = (size_t)eng->host.nv * eng->host.nv * sizeof(double);
   hipLaunchKernelGGL(physics_kernel, dim3(eng->n_env), dim3(64), lds,
                      reinterpret_cast<hipStream_t>(stream), a);
@@ -1798,6 +1824,11 @@ int rmbx_engine_step(rmbx_engine* eng, int nsub, const uint8_t* active, void* st
 int rmbx_engine_forward(rmbx_engine* eng, const uint8_t* active, void* stream) {
   RMBX_CHECK_ARG(eng, "NULL engine");
   return launch(eng, 1, 0, active, stream);
+}
+
+int rmbx_engine_step_profiled(rmbx_engine* eng, int nsub, uint64_t* stage_cycles, void* stream) {
+  RMBX_CHECK_ARG(eng && nsub >= 1 && stage_cycles, "bad arguments");
+  return launch(eng, nsub, 1, nullptr, stream, reinterpret_cast<unsigned long long*>(stage_cycles));
 }
 
 }  // extern "C"

@@ -52,6 +52,7 @@ __device__ __forceinline__ void to_local(const PrimCam& P, const float* d, float
 __device__ bool hit_sphere(const float* o, const float* d, float r, float* t, float* n) {
   const float b = dot3f(o, d);
   const float c = dot3f(o, o) - r * r;
+  if (c < 0) return false;  // camera inside: not rendered (OpenGL back-face culling)
   const float a = dot3f(d, d);
   const float disc = b * b - a * c;
   if (disc < 0) return false;
@@ -69,6 +70,7 @@ __device__ bool hit_cylinder(const float* o, const float* d, float r, float h, b
                              float* t, float* n) {
   float best = 1e30f;
   bool hit = false;
+  if (o[0] * o[0] + o[1] * o[1] < r * r && fabsf(o[2]) < h + (caps ? 0.f : r)) return false;  // inside
   const float a = d[0] * d[0] + d[1] * d[1];
   if (a > 1e-12f) {
     const float b = o[0] * d[0] + o[1] * d[1];

@@ -65,6 +65,16 @@ class PhysicsEngine:
             raise ValueError("active must be a uint8 tensor of n_env elements")
         N.call("rmbx_engine_step", self._h, int(nsub), N.ptr(active), N.stream_ptr())
 
+    STAGES = ("kinematics", "com_crb", "velocity_rne_act", "collision", "constraints", "solver",
+              "sensors", "integrate")
+
+    def step_profiled(self, nsub=8):
+        """Diagnostic step: returns mean shader cycles per stage (summed over substeps)."""
+        prof = torch.zeros((self.n_env, 16), dtype=torch.int64, device=self.device)
+        N.call("rmbx_engine_step_profiled", self._h, int(nsub), N.ptr(prof), N.stream_ptr())
+        p = prof.double().mean(0).cpu().numpy()
+        return dict(zip(self.STAGES, p[: len(self.STAGES)]))
+
     def forward(self, active=None):
         N.call("rmbx_engine_forward", self._h, N.ptr(active), N.stream_ptr())
 

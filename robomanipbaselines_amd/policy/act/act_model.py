@@ -1,0 +1,180 @@
+"""ACT (Action Chunking with Transformers) inference network, batched over environments.
+
+Restates the inference path of ACT's DETRVAE + ACTPolicy (third_party/act, a git submodule that
+is absent from the reference checkout; public upstream: tonyzhaozh/act detr/models/detr_vae.py,
+transformer.py, backbone.py, position_encoding.py) with the hyper-parameters the reference
+trains it with (policy/act/TrainAct.py:46-58): hidden 512, feed-forward 3200, 8 heads,
+4 encoder / 7 decoder layers (post-norm), 100 queries, ResNet-18 backbone, latent 32.
+At inference the latent is zero (no VAE encoder), the image is ImageNet-normalised inside
+ACTPolicy.__call__, and the DETRVAE output uses the FIRST decoder layer's normed output
+(`self.transformer(...)[0]`).  Every decoder layer is still computed here (as the reference
+does); `prune_dead_decoder=True` is an opt-in that skips layers 1..6, which cannot change the
+output.  Parity of this restatement with the upstream code is UNPINNED (submodule absent).
+"""
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+from ..backbone import FusedResNet18Trunk, ResNet18Trunk
+
+IMAGENET_MEAN = (0.485, 0.456, 0.406)
+IMAGENET_STD = (0.229, 0.224, 0.225)
+
+
+def sine_pos_embed(h, w, num_pos_feats=256, temperature=10000, device=None, dtype=torch.float32):
+    """PositionEmbeddingSine(normalize=True, scale=2*pi) of ACT: [1, 2*num_pos_feats, h, w]."""
+    scale = 2 * math.pi
+    eps = 1e-6
+    ones = torch.ones(1, h, w, device=device, dtype=torch.float32)
+    y_embed = ones.cumsum(1)
+    x_embed = ones.cumsum(2)
+    y_embed = y_embed / (y_embed[:, -1:, :] + eps) * scale
+    x_embed = x_embed / (x_embed[:, :, -1:] + eps) * scale
+    dim_t = torch.arange(num_pos_feats, dtype=torch.float32, device=device)
+    dim_t = temperature ** (2 * (dim_t // 2) / num_pos_feats)
+    pos_x = x_embed[:, :, :, None] / dim_t
+    pos_y = y_embed[:, :, :, None] / dim_t
+    pos_x = torch.stack((pos_x[:, :, :, 0::2].sin(), pos_x[:, :, :, 1::2].cos()), dim=4).flatten(3)
+    pos_y = torch.stack((pos_y[:, :, :, 0::2].sin(), pos_y[:, :, :, 1::2].cos()), dim=4).flatten(3)
+    return torch.cat((pos_y, pos_x), dim=3).permute(0, 3, 1, 2).to(dtype)
+
+
+class MHA(nn.Module):
+    """nn.MultiheadAttention-compatible parameters (in_proj_weight/bias, out_proj), batch-first
+    compute through scaled_dot_product_attention."""
+
+    def __init__(self, d, heads):
+        super().__init__()
+        self.d, self.h = d, heads
+        self.in_proj_weight = nn.Parameter(torch.empty(3 * d, d))
+        self.in_proj_bias = nn.Parameter(torch.zeros(3 * d))
+        self.out_proj = nn.Linear(d, d)
+        nn.init.xavier_uniform_(self.in_proj_weight)
+        nn.init.zeros_(self.out_proj.bias)
+
+    def forward(self, q, k, v):
+        B, Lq, D = q.shape
+        Lk = k.shape[1]
+        w, b = self.in_proj_weight, self.in_proj_bias
+        if q is k and k is v:
+            qkv = F.linear(q, w, b)
+            qq, kk, vv = qkv.split(D, dim=-1)
+        elif q is k:
+            qk = F.linear(q, w[: 2 * D], b[: 2 * D])
+            qq, kk = qk.split(D, dim=-1)
+            vv = F.linear(v, w[2 * D :], b[2 * D :])
+        else:
+            qq = F.linear(q, w[:D], b[:D])
+            kk = F.linear(k, w[D : 2 * D], b[D : 2 * D])
+            vv = F.linear(v, w[2 * D :], b[2 * D :])
+        hd = D // self.h
+        qq = qq.view(B, Lq, self.h, hd).transpose(1, 2)
+        kk = kk.view(B, Lk, self.h, hd).transpose(1, 2)
+        vv = vv.view(B, Lk, self.h, hd).transpose(1, 2)
+        o = F.scaled_dot_product_attention(qq, kk, vv)
+        return self.out_proj(o.transpose(1, 2).reshape(B, Lq, D))
+
+
+class EncoderLayer(nn.Module):
+    def __init__(self, d, heads, ff):
+        super().__init__()
+        self.self_attn = MHA(d, heads)
+        self.linear1, self.linear2 = nn.Linear(d, ff), nn.Linear(ff, d)
+        self.norm1, self.norm2 = nn.LayerNorm(d), nn.LayerNorm(d)
+
+    def forward(self, src, pos):
+        q = src + pos
+        src = self.norm1(src + self.self_attn(q, q, src))
+        return self.norm2(src + self.linear2(F.relu(self.linear1(src))))
+
+
+class DecoderLayer(nn.Module):
+    def __init__(self, d, heads, ff):
+        super().__init__()
+        self.self_attn = MHA(d, heads)
+        self.multihead_attn = MHA(d, heads)
+        self.linear1, self.linear2 = nn.Linear(d, ff), nn.Linear(ff, d)
+        self.norm1, self.norm2, self.norm3 = nn.LayerNorm(d), nn.LayerNorm(d), nn.LayerNorm(d)
+
+    def forward(self, tgt, memory, pos, query_pos, mem_pos=None):
+        q = tgt + query_pos
+        tgt = self.norm1(tgt + self.self_attn(q, q, tgt))
+        mk = memory + pos if mem_pos is None else mem_pos
+        tgt = self.norm2(tgt + self.multihead_attn(tgt + query_pos, mk, memory))
+        return self.norm3(tgt + self.linear2(F.relu(self.linear1(tgt))))
+
+
+class ActModel(nn.Module):
+    """DETRVAE inference path. forward(qpos [B,S], image [B,ncam,3,H,W] normalised) -> [B,Q,A]."""
+
+    def __init__(self, state_dim=7, action_dim=7, num_queries=100, hidden_dim=512, dim_feedforward=3200,
+                 nheads=8, enc_layers=4, dec_layers=7, num_cams=1, latent_dim=32):
+        super().__init__()
+        d = hidden_dim
+        self.num_queries, self.num_cams, self.latent_dim = num_queries, num_cams, latent_dim
+        self.backbone = ResNet18Trunk()
+        self.input_proj = nn.Conv2d(512, d, kernel_size=1)
+        self.input_proj_robot_state = nn.Linear(state_dim, d)
+        self.latent_out_proj = nn.Linear(latent_dim, d)
+        self.query_embed = nn.Embedding(num_queries, d)
+        self.additional_pos_embed = nn.Embedding(2, d)
+        self.encoder_layers = nn.ModuleList([EncoderLayer(d, nheads, dim_feedforward) for _ in range(enc_layers)])
+        self.decoder_layers = nn.ModuleList([DecoderLayer(d, nheads, dim_feedforward) for _ in range(dec_layers)])
+        self.decoder_norm = nn.LayerNorm(d)
+        self.action_head = nn.Linear(d, action_dim)
+        self.is_pad_head = nn.Linear(d, 1)
+        self.prune_dead_decoder = False
+        self._fused = None
+        self._pos_cache = {}
+
+    def fuse_backbone(self):
+        self._fused = FusedResNet18Trunk(self.backbone)
+        return self
+
+    def _pos(self, h, w, device, dtype):
+        key = (h, w, str(device), dtype)
+        if key not in self._pos_cache:
+            self._pos_cache[key] = sine_pos_embed(h, w, self.input_proj.out_channels // 2, device=device, dtype=dtype)
+        return self._pos_cache[key]
+
+    def forward(self, qpos, image):
+        B = qpos.shape[0]
+        trunk = self._fused if self._fused is not None else self.backbone
+        feats, poss = [], []
+        for c in range(image.shape[1]):
+            x = image[:, c]
+            if self._fused is not None:
+                x = x.contiguous(memory_format=torch.channels_last)
+            f = self.input_proj(trunk(x))  # [B, d, h, w]
+            feats.append(f)
+            poss.append(self._pos(f.shape[2], f.shape[3], f.device, f.dtype))
+        src = torch.cat(feats, dim=3).flatten(2).transpose(1, 2)  # [B, hw, d]
+        pos = torch.cat(poss, dim=3).flatten(2).transpose(1, 2)  # [1, hw, d]
+        latent = self.latent_out_proj(torch.zeros(B, self.latent_dim, device=qpos.device, dtype=src.dtype))
+        proprio = self.input_proj_robot_state(qpos.to(src.dtype))
+        src = torch.cat([latent[:, None], proprio[:, None], src], dim=1)
+        pos = torch.cat([self.additional_pos_embed.weight[None].to(src.dtype), pos], dim=1)
+        mem = src
+        for layer in self.encoder_layers:
+            mem = layer(mem, pos)
+        qe = self.query_embed.weight[None].to(src.dtype)
+        tgt = torch.zeros(B, self.num_queries, mem.shape[2], device=mem.device, dtype=mem.dtype)
+        mem_pos = mem + pos
+        first = None
+        for i, layer in enumerate(self.decoder_layers):
+            tgt = layer(tgt, mem, pos, qe, mem_pos)
+            if i == 0:
+                first = self.decoder_norm(tgt)  # intermediate[0] = norm(output of layer 0)
+                if self.prune_dead_decoder:
+                    break
+        return self.action_head(first)
+
+
+def normalize_images(image):
+    """transforms.Normalize(ImageNet) of ACTPolicy.__call__ on [B, ncam, 3, H, W] in [0, 1]."""
+    m = torch.tensor(IMAGENET_MEAN, device=image.device, dtype=image.dtype).reshape(1, 1, 3, 1, 1)
+    s = torch.tensor(IMAGENET_STD, device=image.device, dtype=image.dtype).reshape(1, 1, 3, 1, 1)
+    return (image - m) / s

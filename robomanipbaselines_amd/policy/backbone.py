@@ -1,0 +1,111 @@
+"""ResNet-18 trunk with frozen batch norm (torchvision.models.resnet18 + FrozenBatchNorm2d, the
+backbone of ACT's DETR (third_party/act, absent from the reference checkout) and of MlpPolicy
+(policy/mlp/MlpPolicy.py:34-39)).  torchvision is not installed here, so the network is
+restated; parameter names follow torchvision's (conv1, bn1, layer1.0.conv1, ...) so a reference
+state_dict maps onto it.  `fuse()` folds each frozen BN into its conv for the MIOpen/MFMA
+inference path (channels_last, bf16); the unfused module is the fp32 reference."""
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class FrozenBatchNorm2d(nn.Module):
+    """torchvision.ops.misc.FrozenBatchNorm2d: y = (x - rm) / sqrt(rv + eps) * w + b."""
+
+    def __init__(self, n, eps=1e-5):
+        super().__init__()
+        self.eps = eps
+        self.register_buffer("weight", torch.ones(n))
+        self.register_buffer("bias", torch.zeros(n))
+        self.register_buffer("running_mean", torch.zeros(n))
+        self.register_buffer("running_var", torch.ones(n))
+
+    def scale_shift(self):
+        scale = self.weight * (self.running_var + self.eps).rsqrt()
+        return scale, self.bias - self.running_mean * scale
+
+    def forward(self, x):
+        s, b = self.scale_shift()
+        return x * s.reshape(1, -1, 1, 1) + b.reshape(1, -1, 1, 1)
+
+
+class BasicBlock(nn.Module):
+    def __init__(self, cin, cout, stride):
+        super().__init__()
+        self.conv1 = nn.Conv2d(cin, cout, 3, stride, 1, bias=False)
+        self.bn1 = FrozenBatchNorm2d(cout)
+        self.conv2 = nn.Conv2d(cout, cout, 3, 1, 1, bias=False)
+        self.bn2 = FrozenBatchNorm2d(cout)
+        self.downsample = None
+        if stride != 1 or cin != cout:
+            self.downsample = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False), FrozenBatchNorm2d(cout))
+
+    def forward(self, x):
+        idt = x if self.downsample is None else self.downsample(x)
+        y = F.relu(self.bn1(self.conv1(x)))
+        y = self.bn2(self.conv2(y))
+        return F.relu(y + idt)
+
+
+class ResNet18Trunk(nn.Module):
+    """conv1..layer4 (no avgpool/fc): [B,3,H,W] -> [B,512,H/32,W/32]."""
+
+    def __init__(self):
+        super().__init__()
+        self.conv1 = nn.Conv2d(3, 64, 7, 2, 3, bias=False)
+        self.bn1 = FrozenBatchNorm2d(64)
+        self.layer1 = nn.Sequential(BasicBlock(64, 64, 1), BasicBlock(64, 64, 1))
+        self.layer2 = nn.Sequential(BasicBlock(64, 128, 2), BasicBlock(128, 128, 1))
+        self.layer3 = nn.Sequential(BasicBlock(128, 256, 2), BasicBlock(256, 256, 1))
+        self.layer4 = nn.Sequential(BasicBlock(256, 512, 2), BasicBlock(512, 512, 1))
+        for m in self.modules():
+            if isinstance(m, nn.Conv2d):
+                nn.init.kaiming_normal_(m.weight, mode="fan_out", nonlinearity="relu")
+
+    def forward(self, x):
+        x = F.relu(self.bn1(self.conv1(x)))
+        x = F.max_pool2d(x, 3, 2, 1)
+        return self.layer4(self.layer3(self.layer2(self.layer1(x))))
+
+
+class _FusedConv(nn.Module):
+    def __init__(self, conv, bn, relu):
+        super().__init__()
+        s, b = bn.scale_shift()
+        w = conv.weight.detach() * s.reshape(-1, 1, 1, 1)
+        self.conv = nn.Conv2d(conv.in_channels, conv.out_channels, conv.kernel_size, conv.stride, conv.padding, bias=True)
+        self.conv.weight.data.copy_(w)
+        self.conv.bias.data.copy_(b.detach())
+        self.relu = relu
+
+    def forward(self, x):
+        y = self.conv(x)
+        return F.relu(y) if self.relu else y
+
+
+class _FusedBlock(nn.Module):
+    def __init__(self, blk):
+        super().__init__()
+        self.c1 = _FusedConv(blk.conv1, blk.bn1, True)
+        self.c2 = _FusedConv(blk.conv2, blk.bn2, False)
+        self.down = None if blk.downsample is None else _FusedConv(blk.downsample[0], blk.downsample[1], False)
+
+    def forward(self, x):
+        idt = x if self.down is None else self.down(x)
+        return F.relu(self.c2(self.c1(x)) + idt)
+
+
+class FusedResNet18Trunk(nn.Module):
+    """Inference form: BN folded into conv weights/bias (identical function, one less pass)."""
+
+    def __init__(self, trunk):
+        super().__init__()
+        self.stem = _FusedConv(trunk.conv1, trunk.bn1, True)
+        blocks = []
+        for layer in (trunk.layer1, trunk.layer2, trunk.layer3, trunk.layer4):
+            blocks += [_FusedBlock(b) for b in layer]
+        self.blocks = nn.Sequential(*blocks)
+
+    def forward(self, x):
+        return self.blocks(F.max_pool2d(self.stem(x), 3, 2, 1))
