@@ -37,9 +37,9 @@ class RolloutAct(BatchedRolloutBase):
             self.policy.load_state_dict(sd, strict=False)
         self.policy.prune_dead_decoder = bool(self.args.act_prune_dead_decoder)
         self.policy_dtype = torch.bfloat16 if self.args.precision == "bf16" else torch.float32
-        self.policy = self.policy.to(self.device).eval().requires_grad_(False)
+        self.policy = self.policy.eval().requires_grad_(False)
         self.policy.fuse_backbone()
-        self.policy = self.policy.to(self.policy_dtype)
+        self.policy = self.policy.to(device=self.device, dtype=self.policy_dtype).requires_grad_(False)
         self.policy._fused = self.policy._fused.to(memory_format=torch.channels_last)
 
     def reset_variables(self):
