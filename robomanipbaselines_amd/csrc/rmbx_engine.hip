@@ -75,7 +75,7 @@ struct Env {
   double* sensordata;
   double* time;
   int32_t* stats;
-  double* lds;  // nv*nv matrix
+  double* sh;  // front-kernel LDS: xpos, xquat, xmat, cvel, cacc, cfrc, cdofdot
 };
 
 #define W(name) (e.ws + e.L->name)
@@ -88,19 +88,22 @@ __device__ __forceinline__ void sync() { __syncthreads(); }
 // ------------------------------------------------------------------------------------------
 __device__ void kinematics(Env& e, int lane) {
   const rmbx_model& m = *e.m;
-  double* xmat = W(xmat);
+  const int nb = m.nbody;
+  double* sx = e.sh;            // xpos  [3 nb]
+  double* sq = sx + 3 * nb;     // xquat [4 nb]
+  double* sm = sq + 4 * nb;     // xmat  [9 nb]
   double* xipos = W(xipos);
   double* xanchor = W(xanchor);
   double* xaxis = W(xaxis);
   if (lane == 0) {
-    e.xpos[0] = e.xpos[1] = e.xpos[2] = 0;
-    e.xquat[0] = 1;
-    e.xquat[1] = e.xquat[2] = e.xquat[3] = 0;
-    quat2mat(e.xquat, xmat);
-    for (int b = 1; b < m.nbody; b++) {
+    sx[0] = sx[1] = sx[2] = 0;
+    sq[0] = 1;
+    sq[1] = sq[2] = sq[3] = 0;
+    quat2mat(sq, sm);
+    for (int b = 1; b < nb; b++) {
       const int p = m.body_parent[b];
       const int ja = m.body_jntadr[b], jn = m.body_jntnum[b];
-      double* xp = e.xpos + 3 * b;
+      double* xp = sx + 3 * b;
       double xq[4];
       if (jn > 0 && m.jnt_type[ja] == RMBX_JNT_FREE) {
         const int a = m.jnt_qposadr[ja];
@@ -120,9 +123,9 @@ __device__ void kinematics(Env& e, int lane) {
         xaxis[3 * ja + 2] = 1;
       } else {
         double t[3];
-        matvec3(xmat + 9 * p, e.body_pos + 3 * b, t);
-        for (int i = 0; i < 3; i++) xp[i] = e.xpos[3 * p + i] + t[i];
-        quatmul(e.xquat + 4 * p, m.body_quat + 4 * b, xq);
+        matvec3(sm + 9 * p, e.body_pos + 3 * b, t);
+        for (int i = 0; i < 3; i++) xp[i] = sx[3 * p + i] + t[i];
+        quatmul(sq + 4 * p, m.body_quat + 4 * b, xq);
         for (int j = ja; j < ja + jn; j++) {
           double R[9], anc[3], ax[3];
           quat2mat(xq, R);
@@ -148,13 +151,18 @@ __device__ void kinematics(Env& e, int lane) {
           }
         }
       }
-      for (int i = 0; i < 4; i++) e.xquat[4 * b + i] = xq[i];
-      quat2mat(xq, xmat + 9 * b);
+      for (int i = 0; i < 4; i++) sq[4 * b + i] = xq[i];
+      quat2mat(xq, sm + 9 * b);
       double t[3];
-      matvec3(xmat + 9 * b, m.body_ipos + 3 * b, t);
+      matvec3(sm + 9 * b, m.body_ipos + 3 * b, t);
       for (int i = 0; i < 3; i++) xipos[3 * b + i] = xp[i] + t[i];
     }
   }
+  sync();
+  for (int k = lane; k < 3 * nb; k += 64) e.xpos[k] = sx[k];
+  for (int k = lane; k < 4 * nb; k += 64) e.xquat[k] = sq[k];
+  for (int k = lane; k < 9 * nb; k += 64) W(xmat)[k] = sm[k];
+  const double* xmat = sm;
   sync();
   for (int g = lane; g < m.ngeom; g += 64) {
     const int b = m.geom_body[g];
@@ -163,7 +171,7 @@ __device__ void kinematics(Env& e, int lane) {
     const double* gq = col ? m.geom_cquat + 4 * g : m.geom_quat + 4 * g;
     double t[3], R[9];
     matvec3(xmat + 9 * b, gp, t);
-    for (int i = 0; i < 3; i++) e.gxpos[3 * g + i] = e.xpos[3 * b + i] + t[i];
+    for (int i = 0; i < 3; i++) e.gxpos[3 * g + i] = sx[3 * b + i] + t[i];
     quat2mat(gq, R);
     matmul3(xmat + 9 * b, R, e.gxmat + 9 * g);
   }
@@ -171,7 +179,7 @@ __device__ void kinematics(Env& e, int lane) {
     const int b = m.site_body[s];
     double t[3], R[9];
     matvec3(xmat + 9 * b, m.site_pos + 3 * s, t);
-    for (int i = 0; i < 3; i++) W(sxpos)[3 * s + i] = e.xpos[3 * b + i] + t[i];
+    for (int i = 0; i < 3; i++) W(sxpos)[3 * s + i] = sx[3 * b + i] + t[i];
     quat2mat(m.site_quat + 4 * s, R);
     matmul3(xmat + 9 * b, R, W(sxmat) + 9 * s);
   }
@@ -277,12 +285,11 @@ __device__ void com_pos_crb(Env& e, int lane) {
 // ------------------------------------------------------------------------------------------
 // mj_comVel + mj_rne (bias) ; passive ; tendons ; actuation (lane 0 for tree passes)
 // ------------------------------------------------------------------------------------------
-__device__ void rne_forward(Env& e, const double* qacc) {
+// RNE forward pass (lane-serial): cacc, cfrc (body arrays, usually LDS) from cvel/cdofdot
+__device__ void rne_forward(Env& e, const double* qacc, double* ca, double* cfrc,
+                            const double* cvel, const double* cdofdot) {
   const rmbx_model& m = *e.m;
-  double* ca = W(cacc);
-  double* cfrc = W(cfrc);
   const double* cdof = W(cdof);
-  const double* cdofdot = W(cdofdot);
   ca[0] = ca[1] = ca[2] = 0;
   ca[3] = -m.gravity[0];
   ca[4] = -m.gravity[1];
@@ -299,7 +306,7 @@ __device__ void rne_forward(Env& e, const double* qacc) {
     for (int i = 0; i < 6; i++) ca[6 * b + i] = a[i];
     double Ia[6], Iv[6], vxIv[6];
     const double* I = W(cinert) + 10 * b;
-    const double* v = W(cvel) + 6 * b;
+    const double* v = cvel + 6 * b;
     inert_mul(I, a, Ia);
     inert_mul(I, v, Iv);
     cross_force(v, Iv, vxIv);
@@ -307,9 +314,7 @@ __device__ void rne_forward(Env& e, const double* qacc) {
   }
 }
 
-__device__ void rne_backward(Env& e, int lane) {
-  const rmbx_model& m = *e.m;
-  double* cfrc = W(cfrc);
+__device__ void rne_backward(const rmbx_model& m, double* cfrc, int lane) {
   if (lane < 6) {
     for (int b = m.nbody - 1; b > 0; b--) {
       const int p = m.body_parent[b];
@@ -320,13 +325,15 @@ __device__ void rne_backward(Env& e, int lane) {
 
 __device__ void velocity_stage(Env& e, int lane) {
   const rmbx_model& m = *e.m;
-  const int nv = m.nv;
-  double* cvel = W(cvel);
-  double* cdofdot = W(cdofdot);
+  const int nv = m.nv, nb = m.nbody;
+  double* cvel = e.sh + 16 * nb;   // LDS
+  double* scacc = cvel + 6 * nb;   // LDS
+  double* scfrc = scacc + 6 * nb;  // LDS
+  double* cdofdot = scfrc + 6 * nb;  // LDS [6 nv]
   const double* cdof = W(cdof);
   if (lane == 0) {
     for (int i = 0; i < 6; i++) cvel[i] = 0;
-    for (int b = 1; b < m.nbody; b++) {
+    for (int b = 1; b < nb; b++) {
       double cv[6];
       for (int i = 0; i < 6; i++) cv[i] = cvel[6 * m.body_parent[b] + i];
       for (int j = m.body_jntadr[b]; j < m.body_jntadr[b] + m.body_jntnum[b]; j++) {
@@ -346,15 +353,17 @@ __device__ void velocity_stage(Env& e, int lane) {
       }
       for (int i = 0; i < 6; i++) cvel[6 * b + i] = cv[i];
     }
-    rne_forward(e, nullptr);
+    rne_forward(e, nullptr, scacc, scfrc, cvel, cdofdot);
   }
   sync();
-  rne_backward(e, lane);
+  rne_backward(m, scfrc, lane);
   sync();
+  for (int k = lane; k < 6 * nb; k += 64) W(cvel)[k] = cvel[k];
+  for (int k = lane; k < 6 * nv; k += 64) W(cdofdot)[k] = cdofdot[k];
   double* bias = W(qfrc_bias);
   double* passive = W(qfrc_passive);
   for (int k = lane; k < nv; k += 64) {
-    bias[k] = dot6(cdof + 6 * k, W(cfrc) + 6 * m.dof_body[k]);
+    bias[k] = dot6(cdof + 6 * k, scfrc + 6 * m.dof_body[k]);
     passive[k] = -m.dof_damping[k] * e.qvel[k];
   }
   sync();
@@ -997,10 +1006,12 @@ __device__ int make_constraints(Env& e, int lane, int ncon, int* ne_out) {
   // zero the Jacobian rows in use
   for (size_t k = lane; k < (size_t)nefc * nv; k += 64) J[k] = 0;
   sync();
-  // equality rows (lane 0)
-  if (lane == 0) {
+  // equality rows: one lane per equality constraint (rows in constraint order)
+  for (int q = lane; q < m.neq; q += 64) {
     int r = 0;
-    for (int q = 0; q < m.neq; q++) {
+    for (int qq = 0; qq < q; qq++)
+      r += m.eq_type[qq] == RMBX_EQ_CONNECT ? 3 : (m.eq_type[qq] == RMBX_EQ_WELD ? 6 : 1);
+    {
       const double* data = m.eq_data + RMBX_EQ_DATA * q;
       const double* sr = m.eq_solref + 2 * q;
       const double* si = m.eq_solimp + 5 * q;
@@ -1128,27 +1139,35 @@ __device__ int make_constraints(Env& e, int lane, int ncon, int* ne_out) {
       const double dist = W(con_dist)[c] - m.pair_margin[p];
       const double* sr = m.pair_solref + 2 * p;
       const double* si = m.pair_solimp + 5 * p;
+      double dirs[4][3];
       if (cnt == 1) {
-        if (r0 < nefc) {
-          set_row(e, r0, 1, dist, tran, sr, si, dist);
-          jac_point_dir(e, b2, pos, F, 1.0, J + (size_t)r0 * nv);
-          jac_point_dir(e, b1, pos, F, -1.0, J + (size_t)r0 * nv);
-        }
+        for (int i = 0; i < 3; i++) dirs[0][i] = F[i];
+        if (r0 < nefc) set_row(e, r0, 1, dist, tran, sr, si, dist);
       } else {
         const double mu = W(con_mu)[c];
-        int r = r0;
+        int t4 = 0;
         for (int t = 0; t < 2; t++)
           for (int sg = 0; sg < 2; sg++) {
-            if (r < nefc) {
-              double dir[3];
-              const double s = sg == 0 ? mu : -mu;
-              for (int i = 0; i < 3; i++) dir[i] = F[i] + s * F[3 * (1 + t) + i];
-              set_row(e, r, 1, dist, tran * (1 + mu * mu), sr, si, dist);
-              jac_point_dir(e, b2, pos, dir, 1.0, J + (size_t)r * nv);
-              jac_point_dir(e, b1, pos, dir, -1.0, J + (size_t)r * nv);
-            }
-            r++;
+            const double s = sg == 0 ? mu : -mu;
+            for (int i = 0; i < 3; i++) dirs[t4][i] = F[i] + s * F[3 * (1 + t) + i];
+            if (r0 + t4 < nefc) set_row(e, r0 + t4, 1, dist, tran * (1 + mu * mu), sr, si, dist);
+            t4++;
           }
+      }
+      const int nrow = min(cnt, nefc - r0);
+      const double* cdof = W(cdof);
+      for (int pass = 0; pass < 2 && nrow > 0; pass++) {
+        const int b = pass == 0 ? b2 : b1;
+        const double sgn = pass == 0 ? 1.0 : -1.0;
+        for (int k = last_dof(m, b); k >= 0; k = m.dof_parent[k]) {
+          const double* Sk = cdof + 6 * k;
+          double wxp[3];
+          cross3(Sk, pos, wxp);
+          const double v[3] = {Sk[3] + wxp[0], Sk[4] + wxp[1], Sk[5] + wxp[2]};
+#pragma unroll
+          for (int t = 0; t < 4; t++)
+            if (t < nrow) J[(size_t)(r0 + t) * nv + k] += sgn * dot3(v, dirs[t]);
+        }
       }
     }
     rbase += total;
@@ -1169,218 +1188,13 @@ __device__ int make_constraints(Env& e, int lane, int ncon, int* ne_out) {
 }
 
 // ------------------------------------------------------------------------------------------
-// dense linear algebra on the LDS matrix (one wave)
-// ------------------------------------------------------------------------------------------
-__device__ void lds_cholesky(double* A, int n, int lane) {
-  for (int j = 0; j < n; j++) {
-    // A[j][j] already holds the updated pivot (right-looking)
-    const double s = A[j * n + j];
-    const double d = sqrt(s > RMBX_MINVAL ? s : RMBX_MINVAL);
-    const double inv = 1.0 / d;
-    sync();
-    for (int i = j + 1 + lane; i < n; i += 64) A[i * n + j] *= inv;
-    if (lane == 0) A[j * n + j] = d;
-    sync();
-    for (int i = j + 1 + lane; i < n; i += 64) {
-      const double lij = A[i * n + j];
-      for (int k = j + 1; k <= i; k++) A[i * n + k] -= lij * A[k * n + j];
-    }
-    sync();
-  }
-}
-
-// x = A^-1 b with A = L L^T in LDS; x and b may alias; x in global/LDS visible to the wave
-__device__ void lds_chol_solve(const double* A, int n, const double* b, double* x, int lane) {
-  for (int i = lane; i < n; i += 64) x[i] = b[i];
-  sync();
-  for (int i = 0; i < n; i++) {
-    const double xi = x[i] / A[i * n + i];
-    sync();
-    if (lane == 0) x[i] = xi;
-    for (int k = i + 1 + lane; k < n; k += 64) x[k] -= A[k * n + i] * xi;
-    sync();
-  }
-  for (int i = n - 1; i >= 0; i--) {
-    const double xi = x[i] / A[i * n + i];
-    sync();
-    if (lane == 0) x[i] = xi;
-    for (int k = lane; k < i; k += 64) x[k] -= A[i * n + k] * xi;
-    sync();
-  }
-}
-
-__device__ void matvec_rows(const double* M, const double* x, double* y, int n, int lane) {
-  for (int i = lane; i < n; i += 64) {
-    const double* Mi = M + (size_t)i * n;
-    double s = 0;
-    for (int k = 0; k < n; k++) s += Mi[k] * x[k];
-    y[i] = s;
-  }
-  sync();
-}
-
-// ------------------------------------------------------------------------------------------
-// Newton solver (mj_solNewton), exact line search
-// ------------------------------------------------------------------------------------------
-__device__ double eval_cost(Env& e, const double* a, int nefc, int lane) {
-  const rmbx_model& m = *e.m;
-  const int nv = m.nv;
-  double* res = W(res);
-  double* Mres = W(Mres);
-  for (int k = lane; k < nv; k += 64) res[k] = a[k] - W(qacc_smooth)[k];
-  sync();
-  matvec_rows(W(M), res, Mres, nv, lane);
-  double part = 0;
-  for (int k = lane; k < nv; k += 64) part += res[k] * Mres[k];
-  double cost = 0.5 * wave_sum(part);
-  const double* J = W(J);
-  double cpart = 0;
-  for (int r = lane; r < nefc; r += 64) {
-    const double* Jr = J + (size_t)r * nv;
-    double s = 0;
-    for (int k = 0; k < nv; k++) s += Jr[k] * a[k];
-    const double jar = s - W(efc_aref)[r];
-    W(efc_jar)[r] = jar;
-    if (WI(efc_type)[r] == 0 || jar < 0) cpart += 0.5 * W(efc_D)[r] * jar * jar;
-  }
-  cost += wave_sum(cpart);
-  sync();
-  return cost;
-}
-
-__device__ int solve(Env& e, int nefc, int ne, int lane) {
-  const rmbx_model& m = *e.m;
-  const int nv = m.nv;
-  double* A = e.lds;
-  double* a = W(qacc);
-  const double* M = W(M);
-  const double* J = W(J);
-  // qacc_smooth = M^-1 qfrc_smooth
-  for (int k = lane; k < nv * nv; k += 64) A[k] = M[k];
-  sync();
-  lds_cholesky(A, nv, lane);
-  lds_chol_solve(A, nv, W(qfrc_smooth), W(qacc_smooth), lane);
-  const double c_ws = eval_cost(e, e.qacc_ws, nefc, lane);
-  const double c_sm = eval_cost(e, W(qacc_smooth), nefc, lane);
-  const double* start = c_ws < c_sm ? e.qacc_ws : W(qacc_smooth);
-  for (int k = lane; k < nv; k += 64) a[k] = start[k];
-  sync();
-  double cost = eval_cost(e, a, nefc, lane);
-  const double scale = 1.0 / (m.meaninertia * (nv > 1 ? nv : 1));
-  int it;
-  double* grad = W(grad);
-  double* search = W(search);
-  double* Ms = W(Ms);
-  for (it = 0; it < m.solver_iterations; it++) {
-    // gradient (lanes over columns, rows in order)
-    double gpart = 0;
-    for (int k = lane; k < nv; k += 64) {
-      double g = W(Mres)[k];
-      for (int r = 0; r < nefc; r++) {
-        const double jar = W(efc_jar)[r];
-        if (WI(efc_type)[r] == 0 || jar < 0) g += J[(size_t)r * nv + k] * (W(efc_D)[r] * jar);
-      }
-      grad[k] = g;
-      gpart += g * g;
-    }
-    const double gn = wave_sum(gpart);
-    sync();
-    if (scale * sqrt(gn) < m.solver_tolerance) break;
-    // Hessian rows (lane i owns row i): H[i][k] = M[i][k] + sum_r D_r J_ri J_rk, k <= i
-    for (int i = lane; i < nv; i += 64) {
-      for (int k = 0; k <= i; k++) A[i * nv + k] = M[i * nv + k];
-      for (int r = 0; r < nefc; r++) {
-        const double jar = W(efc_jar)[r];
-        if (!(WI(efc_type)[r] == 0 || jar < 0)) continue;
-        const double* Jr = J + (size_t)r * nv;
-        const double ji = Jr[i];
-        if (ji == 0) continue;
-        const double t = W(efc_D)[r] * ji;
-        for (int k = 0; k <= i; k++) A[i * nv + k] += t * Jr[k];
-      }
-    }
-    sync();
-    lds_cholesky(A, nv, lane);
-    lds_chol_solve(A, nv, grad, search, lane);
-    for (int k = lane; k < nv; k += 64) search[k] = -search[k];
-    sync();
-    matvec_rows(M, search, Ms, nv, lane);
-    double qp = 0, lp = 0;
-    for (int k = lane; k < nv; k += 64) {
-      qp += search[k] * Ms[k];
-      lp += W(res)[k] * Ms[k];
-    }
-    const double qg = wave_sum(qp), lg = wave_sum(lp);
-    for (int r = lane; r < nefc; r += 64) {
-      const double* Jr = J + (size_t)r * nv;
-      double s = 0;
-      for (int k = 0; k < nv; k++) s += Jr[k] * search[k];
-      W(efc_Js)[r] = s;
-    }
-    sync();
-    double alpha = 0, lo = 0, hi = 1e300;
-    for (int ls = 0; ls < m.ls_iterations; ls++) {
-      double p1 = 0, p2 = 0;
-      for (int r = lane; r < nefc; r += 64) {
-        const double js = W(efc_Js)[r];
-        const double x = W(efc_jar)[r] + alpha * js;
-        if (WI(efc_type)[r] == 0 || x < 0) {
-          p1 += W(efc_D)[r] * x * js;
-          p2 += W(efc_D)[r] * js * js;
-        }
-      }
-      const double d1 = alpha * qg + lg + wave_sum(p1);
-      const double d2 = qg + wave_sum(p2);
-      if (d1 == 0) break;
-      if (d1 < 0)
-        lo = alpha;
-      else
-        hi = alpha;
-      double an = alpha - d1 / d2;
-      if (!(an > lo && an < hi)) an = hi < 1e300 ? 0.5 * (lo + hi) : (an > lo ? an : lo);
-      int changed = 0;
-      for (int r = ne + lane; r < nefc; r += 64) {
-        const double js = W(efc_Js)[r];
-        const double x0 = W(efc_jar)[r] + alpha * js, x1 = W(efc_jar)[r] + an * js;
-        changed |= ((x0 < 0) != (x1 < 0));
-      }
-      alpha = an;
-      if (wave_sum_i(changed) == 0) break;
-    }
-    for (int k = lane; k < nv; k += 64) a[k] += alpha * search[k];
-    sync();
-    const double newcost = eval_cost(e, a, nefc, lane);
-    const double improvement = scale * (cost - newcost);
-    cost = newcost;
-    if (improvement < m.solver_tolerance) {
-      it++;
-      break;
-    }
-  }
-  // constraint forces and qfrc_constraint (lanes over columns)
-  for (int r = lane; r < nefc; r += 64) {
-    const double jar = W(efc_jar)[r];
-    W(efc_force)[r] = (WI(efc_type)[r] == 0 || jar < 0) ? -W(efc_D)[r] * jar : 0.0;
-  }
-  sync();
-  for (int k = lane; k < nv; k += 64) {
-    double s = 0;
-    for (int r = 0; r < nefc; r++) s += J[(size_t)r * nv + k] * W(efc_force)[r];
-    W(qfrc_constraint)[k] = s;
-  }
-  sync();
-  return it;
-}
-
-// ------------------------------------------------------------------------------------------
 // sensors (mj_rnePostConstraint -> force/torque at sites)
 // ------------------------------------------------------------------------------------------
-__device__ void sensors(Env& e, int ncon, int lane) {
+__device__ void sensors(Env& e, int ncon, int lane, double* cacc, double* cfrc) {
   const rmbx_model& m = *e.m;
   if (m.nsensor == 0) return;
   if (lane == 0) {
-    rne_forward(e, W(qacc));
-    double* cfrc = W(cfrc);
+    rne_forward(e, W(qacc), cacc, cfrc, W(cvel), W(cdofdot));
     for (int c = 0; c < ncon; c++) {
       const int r0 = WI(con_efcadr)[c];
       if (r0 + (WI(con_condim)[c] == 1 ? 1 : 4) > e.L->nefc_max) continue;
@@ -1408,13 +1222,13 @@ __device__ void sensors(Env& e, int ncon, int lane) {
     }
   }
   sync();
-  rne_backward(e, lane);
+  rne_backward(m, cfrc, lane);
   sync();
   if (lane < m.nsensor && lane < 2) {
     const int s = lane;
     const int site = m.sensor_site[s];
     const int b = m.site_body[site];
-    const double* f = W(cfrc) + 6 * b;
+    const double* f = cfrc + 6 * b;
     const double* p = W(sxpos) + 3 * site;
     const double* R = W(sxmat) + 9 * site;
     double out[3];
@@ -1432,51 +1246,459 @@ __device__ void sensors(Env& e, int ncon, int lane) {
 }
 
 // ------------------------------------------------------------------------------------------
-// implicitfast integration
+// Solver kernel (256 threads per env): Newton solve of the constraint problem, constraint
+// forces, site sensors and implicitfast integration.  Dense nv x nv matrices are held as 4x4
+// f64 blocks in the registers of the threads that own the lower-triangle blocks (one block per
+// thread, 153 threads at nv = 68); Cholesky, triangular solves and the Hessian J^T D J
+// accumulation run on those register blocks with only one block column / vector staged in LDS.
+// The constraint Jacobian streams from the workspace (HBM/L2) through a 16-row LDS chunk.
 // ------------------------------------------------------------------------------------------
-__device__ void integrate(Env& e, int lane) {
-  const rmbx_model& m = *e.m;
-  const int nv = m.nv;
-  const double h = m.timestep;
-  double* A = e.lds;
-  const double* M = W(M);
-  for (int k = lane; k < nv * nv; k += 64) A[k] = M[k];
-  sync();
-  for (int k = lane; k < nv; k += 64) A[k * nv + k] += h * m.dof_damping[k];
-  sync();
-  if (lane == 0) {
-    for (int u = 0; u < m.nu; u++) {
-      const double kv = -m.act_bias[3 * u + 2];
-      if (kv == 0) continue;
-      const int id = m.act_trnid[u];
-      if (m.act_trntype[u] == RMBX_TRN_JOINT) {
-        const int k = m.jnt_dofadr[id];
-        A[k * nv + k] += h * kv;
-      } else {
-        for (int w1 = m.ten_adr[id]; w1 < m.ten_adr[id] + m.ten_num[id]; w1++)
-          for (int w2 = m.ten_adr[id]; w2 < m.ten_adr[id] + m.ten_num[id]; w2++) {
-            const int k1 = m.jnt_dofadr[m.wrap_jnt[w1]], k2 = m.jnt_dofadr[m.wrap_jnt[w2]];
-            A[k1 * nv + k2] += h * kv * m.wrap_coef[w1] * m.wrap_coef[w2];
-          }
-      }
+#define SOLVER_THREADS 256
+#define MAX_NB 22  // nv <= 88
+#define MAX_NVP (4 * MAX_NB)
+#define RCHUNK 16
+#define MAX_BODY 64
+
+struct SolverShared {
+  double Lcol[MAX_NB][16];
+  double a0[MAX_NVP];    // qacc_smooth
+  double a[MAX_NVP];     // current qacc
+  double res[MAX_NVP];   // a - a0
+  double Mres[MAX_NVP];  // M res
+  double grad[MAX_NVP];
+  double srch[MAX_NVP];
+  double Ms[MAX_NVP];
+  double acc[MAX_NVP];
+  double tmp[MAX_NVP];
+  double jc[RCHUNK][MAX_NVP];  // scaled Jacobian chunk
+  double jw[RCHUNK];           // chunk row weights sqrt(D) (active rows)
+  double jw2[RCHUNK];          // sqrt(D) * jar (gradient)
+  double bacc[6 * MAX_BODY];  // sensors: body accelerations
+  double bfrc[6 * MAX_BODY];  // sensors: body forces
+  double red[8];
+  int ired[8];
+};
+
+__device__ __forceinline__ void blk_coords(int t, int* bi, int* bj) {
+  int i = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+  while ((i + 1) * (i + 2) / 2 <= t) i++;
+  while (i * (i + 1) / 2 > t) i--;
+  *bi = i;
+  *bj = t - i * (i + 1) / 2;
+}
+
+__device__ __forceinline__ double block_sum(double v, SolverShared& S, int tid) {
+  v = wave_sum(v);
+  __syncthreads();
+  if ((tid & 63) == 0) S.red[tid >> 6] = v;
+  __syncthreads();
+  return S.red[0] + S.red[1] + S.red[2] + S.red[3];
+}
+__device__ __forceinline__ int block_sum_i(int v, SolverShared& S, int tid) {
+  v = wave_sum_i(v);
+  __syncthreads();
+  if ((tid & 63) == 0) S.ired[tid >> 6] = v;
+  __syncthreads();
+  return S.ired[0] + S.ired[1] + S.ired[2] + S.ired[3];
+}
+
+// 4x4 in-place lower Cholesky (row-major)
+__device__ __forceinline__ void potrf4(double* a) {
+#pragma unroll
+  for (int j = 0; j < 4; j++) {
+    double s = a[4 * j + j];
+#pragma unroll
+    for (int k = 0; k < j; k++) s -= a[4 * j + k] * a[4 * j + k];
+    const double d = sqrt(s > RMBX_MINVAL ? s : RMBX_MINVAL);
+    a[4 * j + j] = d;
+    const double inv = 1.0 / d;
+#pragma unroll
+    for (int i = j + 1; i < 4; i++) {
+      double t = a[4 * i + j];
+#pragma unroll
+      for (int k = 0; k < j; k++) t -= a[4 * i + k] * a[4 * j + k];
+      a[4 * i + j] = t * inv;
+    }
+#pragma unroll
+    for (int k = j + 1; k < 4; k++) a[4 * j + k] = 0;
+  }
+}
+// a := a * L^-T  (L lower 4x4)
+__device__ __forceinline__ void trsm4(double* a, const double* L) {
+#pragma unroll
+  for (int r = 0; r < 4; r++) {
+#pragma unroll
+    for (int c = 0; c < 4; c++) {
+      double t = a[4 * r + c];
+#pragma unroll
+      for (int k = 0; k < c; k++) t -= a[4 * r + k] * L[4 * c + k];
+      a[4 * r + c] = t / L[4 * c + c];
     }
   }
-  sync();
-  lds_cholesky(A, nv, lane);
-  double* f = W(tmp);
-  for (int k = lane; k < nv; k += 64) f[k] = W(qfrc_smooth)[k] + W(qfrc_constraint)[k];
-  sync();
-  double* qacc = W(qacc);
-  lds_chol_solve(A, nv, f, qacc, lane);
-  bool bad = false;
-  for (int k = lane; k < nv; k += 64) {
-    const double a = qacc[k];
-    if (!isfinite(a) || fabs(a) > 1e10) bad = true;
-    e.qvel[k] += h * a;
-    e.qacc_ws[k] = a;
+}
+
+// Distributed block Cholesky: thread t < nblk owns block (bi, bj) in a[16].
+__device__ void blk_cholesky(double* a, int bi, int bj, bool own, int NB, SolverShared& S) {
+  for (int k = 0; k < NB; k++) {
+    if (own && bi == k && bj == k) {
+      potrf4(a);
+#pragma unroll
+      for (int q = 0; q < 16; q++) S.Lcol[k][q] = a[q];
+    }
+    __syncthreads();
+    if (own && bj == k && bi > k) {
+      trsm4(a, S.Lcol[k]);
+#pragma unroll
+      for (int q = 0; q < 16; q++) S.Lcol[bi][q] = a[q];
+    }
+    __syncthreads();
+    if (own && bj > k) {
+      const double* Li = S.Lcol[bi];
+      const double* Lj = S.Lcol[bj];
+#pragma unroll
+      for (int p = 0; p < 4; p++)
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          double t = a[4 * p + q];
+#pragma unroll
+          for (int r = 0; r < 4; r++) t -= Li[4 * p + r] * Lj[4 * q + r];
+          a[4 * p + q] = t;
+        }
+    }
+    __syncthreads();
   }
-  sync();
-  for (int j = lane; j < m.njnt; j += 64) {
+}
+
+// x = (L L^T)^-1 b ; b, x in LDS (length NVP, may alias); uses S.acc
+__device__ void blk_solve(const double* a, int bi, int bj, bool own, int NB, const double* b,
+                          double* x, SolverShared& S, int tid) {
+  const int NVP = 4 * NB;
+  for (int r = tid; r < NVP; r += SOLVER_THREADS) S.acc[r] = b[r];
+  __syncthreads();
+  // forward: y_j = L_jj^-1 (acc_j); acc_i -= L_ij y_j
+  for (int j = 0; j < NB; j++) {
+    if (own && bi == j && bj == j) {
+      double y[4];
+#pragma unroll
+      for (int p = 0; p < 4; p++) {
+        double t = S.acc[4 * j + p];
+#pragma unroll
+        for (int k = 0; k < p; k++) t -= a[4 * p + k] * y[k];
+        y[p] = t / a[4 * p + p];
+      }
+#pragma unroll
+      for (int p = 0; p < 4; p++) S.acc[4 * j + p] = y[p];
+    }
+    __syncthreads();
+    if (own && bj == j && bi > j) {
+      const double* y = S.acc + 4 * j;
+#pragma unroll
+      for (int p = 0; p < 4; p++)
+        S.acc[4 * bi + p] -= a[4 * p] * y[0] + a[4 * p + 1] * y[1] + a[4 * p + 2] * y[2] + a[4 * p + 3] * y[3];
+    }
+    __syncthreads();
+  }
+  // backward: x_i = L_ii^-T acc_i ; acc_j -= L_ij^T x_i
+  for (int i = NB - 1; i >= 0; i--) {
+    if (own && bi == i && bj == i) {
+      double xx[4];
+#pragma unroll
+      for (int p = 3; p >= 0; p--) {
+        double t = S.acc[4 * i + p];
+#pragma unroll
+        for (int k = p + 1; k < 4; k++) t -= a[4 * k + p] * xx[k];
+        xx[p] = t / a[4 * p + p];
+      }
+#pragma unroll
+      for (int p = 0; p < 4; p++) S.acc[4 * i + p] = xx[p];
+    }
+    __syncthreads();
+    if (own && bi == i && bj < i) {
+      const double* xi = S.acc + 4 * i;
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+        S.acc[4 * bj + q] -= a[q] * xi[0] + a[4 + q] * xi[1] + a[8 + q] * xi[2] + a[12 + q] * xi[3];
+    }
+    __syncthreads();
+  }
+  for (int r = tid; r < NVP; r += SOLVER_THREADS) x[r] = S.acc[r];
+  __syncthreads();
+}
+
+// load block (bi, bj) of the dense nv x nv matrix (zero/identity padding beyond nv)
+__device__ __forceinline__ void load_block(const double* M, int nv, int bi, int bj, double* a) {
+#pragma unroll
+  for (int p = 0; p < 4; p++)
+#pragma unroll
+    for (int q = 0; q < 4; q++) {
+      const int r = 4 * bi + p, c = 4 * bj + q;
+      a[4 * p + q] = (r < nv && c < nv) ? M[(size_t)r * nv + c] : (r == c ? 1.0 : 0.0);
+    }
+}
+
+// y = M x, thread per row (M dense in global), vectors in LDS
+__device__ void mat_vec(const double* M, int nv, const double* x, double* y, int tid) {
+  for (int i = tid; i < nv; i += SOLVER_THREADS) {
+    const double* Mi = M + (size_t)i * nv;
+    double s = 0;
+    for (int k = 0; k < nv; k++) s += Mi[k] * x[k];
+    y[i] = s;
+  }
+  __syncthreads();
+}
+
+// out[r] = J_r . x for r < nefc (thread per row)
+__device__ void jac_vec(const double* J, int nefc, int nv, const double* x, double* out, int tid) {
+  for (int r = tid; r < nefc; r += SOLVER_THREADS) {
+    const double* Jr = J + (size_t)r * nv;
+    double s = 0;
+    for (int k = 0; k < nv; k++) s += Jr[k] * x[k];
+    out[r] = s;
+  }
+  __syncthreads();
+}
+
+struct SolverCtx {
+  const double* J;
+  const double* aref;
+  const double* D;
+  const int32_t* type;
+  double* jar;
+  double* Js;
+  double* force;
+  int nefc, ne, nv, NB, tid;
+};
+
+// cost at S.a (or at x): sets jar, res, Mres; returns cost
+__device__ double solver_cost(const SolverCtx& c, const double* M, const double* x, SolverShared& S) {
+  const int tid = c.tid;
+  for (int k = tid; k < 4 * c.NB; k += SOLVER_THREADS) S.res[k] = k < c.nv ? x[k] - S.a0[k] : 0.0;
+  __syncthreads();
+  mat_vec(M, c.nv, S.res, S.Mres, tid);
+  double part = 0;
+  for (int k = tid; k < c.nv; k += SOLVER_THREADS) part += S.res[k] * S.Mres[k];
+  double cpart = 0;
+  for (int r = tid; r < c.nefc; r += SOLVER_THREADS) {
+    const double* Jr = c.J + (size_t)r * c.nv;
+    double s = 0;
+    for (int k = 0; k < c.nv; k++) s += Jr[k] * x[k];
+    const double jar = s - c.aref[r];
+    c.jar[r] = jar;
+    if (c.type[r] == 0 || jar < 0) cpart += 0.5 * c.D[r] * jar * jar;
+  }
+  return 0.5 * block_sum(part, S, tid) + block_sum(cpart, S, tid);
+}
+
+// Hessian blocks a = M + J^T D_act J and gradient S.grad = Mres + J^T (D_act jar); returns |g|^2
+__device__ double solver_hessian_grad(const SolverCtx& c, const double* M, double* a, int bi,
+                                      int bj, bool own, SolverShared& S) {
+  const int tid = c.tid, nv = c.nv, NVP = 4 * c.NB;
+  if (own) load_block(M, nv, bi, bj, a);
+  // gradient accumulators: thread t < NVP owns column t
+  double g = 0;
+  for (int r0 = 0; r0 < c.nefc; r0 += RCHUNK) {
+    const int nr = min(RCHUNK, c.nefc - r0);
+    __syncthreads();
+    if (tid < RCHUNK) {
+      double w = 0, w2 = 0;
+      if (tid < nr) {
+        const int r = r0 + tid;
+        const double jar = c.jar[r];
+        const bool act = c.type[r] == 0 || jar < 0;
+        w = act ? sqrt(c.D[r]) : 0.0;
+        w2 = w * jar;
+      }
+      S.jw[tid] = w;
+      S.jw2[tid] = w2;
+    }
+    __syncthreads();
+    const double* src = c.J + (size_t)r0 * nv;
+    for (int e = tid; e < RCHUNK * NVP; e += SOLVER_THREADS) {
+      const int rr = e / NVP, k = e - rr * NVP;
+      S.jc[rr][k] = (rr < nr && k < nv) ? src[(size_t)rr * nv + k] * S.jw[rr] : 0.0;
+    }
+    __syncthreads();
+    if (own) {
+      for (int rr = 0; rr < nr; rr++) {
+        const double* ji = S.jc[rr] + 4 * bi;
+        const double* jj = S.jc[rr] + 4 * bj;
+        const double i0 = ji[0], i1 = ji[1], i2 = ji[2], i3 = ji[3];
+        const double j0 = jj[0], j1 = jj[1], j2 = jj[2], j3 = jj[3];
+        a[0] += i0 * j0; a[1] += i0 * j1; a[2] += i0 * j2; a[3] += i0 * j3;
+        a[4] += i1 * j0; a[5] += i1 * j1; a[6] += i1 * j2; a[7] += i1 * j3;
+        a[8] += i2 * j0; a[9] += i2 * j1; a[10] += i2 * j2; a[11] += i2 * j3;
+        a[12] += i3 * j0; a[13] += i3 * j1; a[14] += i3 * j2; a[15] += i3 * j3;
+      }
+    }
+    if (tid < nv) {
+      for (int rr = 0; rr < nr; rr++) g += S.jc[rr][tid] * S.jw2[rr];
+    }
+  }
+  double gn = 0;
+  if (tid < nv) {
+    g += S.Mres[tid];
+    S.grad[tid] = g;
+    gn = g * g;
+  } else if (tid < NVP) {
+    S.grad[tid] = 0;
+  }
+  return block_sum(gn, S, tid);
+}
+
+__device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj, bool own,
+                             int nefc, int ne, int tid) {
+  const rmbx_model& m = *e.m;
+  const int nv = m.nv, NB = (nv + 3) / 4, NVP = 4 * NB;
+  const double* M = W(M);
+  SolverCtx c;
+  c.J = W(J);
+  c.aref = W(efc_aref);
+  c.D = W(efc_D);
+  c.type = WI(efc_type);
+  c.jar = W(efc_jar);
+  c.Js = W(efc_Js);
+  c.force = W(efc_force);
+  c.nefc = nefc;
+  c.ne = ne;
+  c.nv = nv;
+  c.NB = NB;
+  c.tid = tid;
+  // qacc_smooth = M^-1 qfrc_smooth
+  if (own) load_block(M, nv, bi, bj, a);
+  for (int k = tid; k < NVP; k += SOLVER_THREADS) S.tmp[k] = k < nv ? W(qfrc_smooth)[k] : 0.0;
+  __syncthreads();
+  blk_cholesky(a, bi, bj, own, NB, S);
+  blk_solve(a, bi, bj, own, NB, S.tmp, S.a0, S, tid);
+  for (int k = tid; k < NVP; k += SOLVER_THREADS) S.tmp[k] = k < nv ? e.qacc_ws[k] : 0.0;
+  __syncthreads();
+  const double c_ws = solver_cost(c, M, S.tmp, S);
+  const double c_sm = solver_cost(c, M, S.a0, S);
+  const bool use_ws = c_ws < c_sm;
+  for (int k = tid; k < NVP; k += SOLVER_THREADS) S.a[k] = use_ws ? S.tmp[k] : S.a0[k];
+  __syncthreads();
+  double cost = solver_cost(c, M, S.a, S);
+  const double scale = 1.0 / (m.meaninertia * (nv > 1 ? nv : 1));
+  int it;
+  for (it = 0; it < m.solver_iterations; it++) {
+    const double gn = solver_hessian_grad(c, M, a, bi, bj, own, S);
+    if (scale * sqrt(gn) < m.solver_tolerance) break;
+    blk_cholesky(a, bi, bj, own, NB, S);
+    blk_solve(a, bi, bj, own, NB, S.grad, S.srch, S, tid);
+    for (int k = tid; k < NVP; k += SOLVER_THREADS) S.srch[k] = -S.srch[k];
+    __syncthreads();
+    mat_vec(M, nv, S.srch, S.Ms, tid);
+    double qp = 0, lp = 0;
+    for (int k = tid; k < nv; k += SOLVER_THREADS) {
+      qp += S.srch[k] * S.Ms[k];
+      lp += S.res[k] * S.Ms[k];
+    }
+    const double qg = block_sum(qp, S, tid);
+    const double lg = block_sum(lp, S, tid);
+    jac_vec(c.J, nefc, nv, S.srch, c.Js, tid);
+    double alpha = 0, lo = 0, hi = 1e300;
+    for (int ls = 0; ls < m.ls_iterations; ls++) {
+      double p1 = 0, p2 = 0;
+      for (int r = tid; r < nefc; r += SOLVER_THREADS) {
+        const double js = c.Js[r];
+        const double x = c.jar[r] + alpha * js;
+        if (c.type[r] == 0 || x < 0) {
+          p1 += c.D[r] * x * js;
+          p2 += c.D[r] * js * js;
+        }
+      }
+      const double d1 = alpha * qg + lg + block_sum(p1, S, tid);
+      const double d2 = qg + block_sum(p2, S, tid);
+      if (d1 == 0) break;
+      if (d1 < 0)
+        lo = alpha;
+      else
+        hi = alpha;
+      double an = alpha - d1 / d2;
+      if (!(an > lo && an < hi)) an = hi < 1e300 ? 0.5 * (lo + hi) : (an > lo ? an : lo);
+      int changed = 0;
+      for (int r = ne + tid; r < nefc; r += SOLVER_THREADS) {
+        const double js = c.Js[r];
+        const double x0 = c.jar[r] + alpha * js, x1 = c.jar[r] + an * js;
+        changed |= ((x0 < 0) != (x1 < 0));
+      }
+      alpha = an;
+      if (block_sum_i(changed, S, tid) == 0) break;
+    }
+    for (int k = tid; k < NVP; k += SOLVER_THREADS) S.a[k] += alpha * S.srch[k];
+    __syncthreads();
+    const double newcost = solver_cost(c, M, S.a, S);
+    const double improvement = scale * (cost - newcost);
+    cost = newcost;
+    if (improvement < m.solver_tolerance) {
+      it++;
+      break;
+    }
+  }
+  // forces and qfrc_constraint = J^T f
+  for (int r = tid; r < nefc; r += SOLVER_THREADS) {
+    const double jar = c.jar[r];
+    c.force[r] = (c.type[r] == 0 || jar < 0) ? -c.D[r] * jar : 0.0;
+  }
+  __syncthreads();
+  for (int k = tid; k < nv; k += SOLVER_THREADS) {
+    double s = 0;
+    for (int r = 0; r < nefc; r++) s += c.J[(size_t)r * nv + k] * c.force[r];
+    W(qfrc_constraint)[k] = s;
+    W(qacc)[k] = S.a[k];
+  }
+  __syncthreads();
+  return it;
+}
+
+__device__ void solver_integrate(Env& e, SolverShared& S, double* a, int bi, int bj, bool own,
+                                 int tid) {
+  const rmbx_model& m = *e.m;
+  const int nv = m.nv, NB = (nv + 3) / 4, NVP = 4 * NB;
+  const double h = m.timestep;
+  if (own) {
+    load_block(W(M), nv, bi, bj, a);
+    // + h * (damping + actuator velocity gains), tendon terms are rank-1 blocks
+#pragma unroll
+    for (int p = 0; p < 4; p++)
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int r = 4 * bi + p, cc = 4 * bj + q;
+        if (r >= nv || cc >= nv) continue;
+        double add = 0;
+        if (r == cc) add += m.dof_damping[r];
+        for (int u = 0; u < m.nu; u++) {
+          const double kv = -m.act_bias[3 * u + 2];
+          if (kv == 0) continue;
+          const int id = m.act_trnid[u];
+          if (m.act_trntype[u] == RMBX_TRN_JOINT) {
+            if (r == cc && m.jnt_dofadr[id] == r) add += kv;
+          } else {
+            double cr = 0, cq = 0;
+            for (int w = m.ten_adr[id]; w < m.ten_adr[id] + m.ten_num[id]; w++) {
+              const int d = m.jnt_dofadr[m.wrap_jnt[w]];
+              if (d == r) cr += m.wrap_coef[w];
+              if (d == cc) cq += m.wrap_coef[w];
+            }
+            add += kv * cr * cq;
+          }
+        }
+        a[4 * p + q] += h * add;
+      }
+  }
+  for (int k = tid; k < NVP; k += SOLVER_THREADS)
+    S.tmp[k] = k < nv ? W(qfrc_smooth)[k] + W(qfrc_constraint)[k] : 0.0;
+  __syncthreads();
+  blk_cholesky(a, bi, bj, own, NB, S);
+  blk_solve(a, bi, bj, own, NB, S.tmp, S.a, S, tid);
+  bool bad = false;
+  for (int k = tid; k < nv; k += SOLVER_THREADS) {
+    const double acc = S.a[k];
+    if (!isfinite(acc) || fabs(acc) > 1e10) bad = true;
+    e.qvel[k] += h * acc;
+    e.qacc_ws[k] = acc;
+  }
+  __syncthreads();
+  for (int j = tid; j < m.njnt; j += SOLVER_THREADS) {
     const int qa = m.jnt_qposadr[j], da = m.jnt_dofadr[j];
     if (m.jnt_type[j] == RMBX_JNT_FREE) {
       for (int i = 0; i < 3; i++) e.qpos[qa + i] += h * e.qvel[da + i];
@@ -1494,14 +1716,11 @@ __device__ void integrate(Env& e, int lane) {
       e.qpos[qa] += h * e.qvel[da];
     }
   }
-  if (__any(bad) && lane == 0) e.stats[3] = 1;
-  if (lane == 0) e.time[0] += h;
-  sync();
+  if (block_sum_i(bad ? 1 : 0, S, tid) && tid == 0) e.stats[3] = 1;
+  if (tid == 0) e.time[0] += h;
+  __syncthreads();
 }
 
-// ------------------------------------------------------------------------------------------
-// the fused kernel
-// ------------------------------------------------------------------------------------------
 struct KArgs {
   rmbx_model m;
   Layout L;
@@ -1513,18 +1732,10 @@ struct KArgs {
   unsigned long long* prof;  // optional [n_env][16] per-stage cycle sums (diagnostic)
 };
 
-__device__ __forceinline__ unsigned long long stamp() {
-  return __builtin_readcyclecounter();
-}
+__device__ __forceinline__ unsigned long long stamp() { return __builtin_readcyclecounter(); }
 
-__global__ void __launch_bounds__(64) physics_kernel(KArgs args) {
-  extern __shared__ __attribute__((aligned(16))) double smem[];
-  const int env = blockIdx.x;
-  const int lane = threadIdx.x;
-  if (env >= args.n_env) return;
-  if (args.active && !args.active[env]) return;
+__device__ __forceinline__ void make_env(const KArgs& args, int env, Env& e) {
   const rmbx_model& m = args.m;
-  Env e;
   e.m = &args.m;
   e.L = &args.L;
   e.ws = reinterpret_cast<double*>(args.b.workspace) + (size_t)env * args.L.stride;
@@ -1541,45 +1752,77 @@ __global__ void __launch_bounds__(64) physics_kernel(KArgs args) {
   e.sensordata = args.b.sensordata + (size_t)env * 6;
   e.time = args.b.time + env;
   e.stats = args.b.stats + (size_t)env * 4;
-  e.lds = smem;
-  const int nsub = args.integrate_flag ? args.nsub : 1;
-  unsigned long long* prof = args.prof ? args.prof + (size_t)env * 16 : nullptr;
-  unsigned long long t0 = 0, t1 = 0;
+  e.sh = nullptr;
+}
+
+#define PROF_BEGIN()                                        \
+  unsigned long long* prof = args.prof ? args.prof + (size_t)env * 16 : nullptr; \
+  unsigned long long t0 = 0, t1 = 0;                        \
+  if (prof) t0 = stamp();
 #define PROF(k)                                   \
   if (prof) {                                     \
-    sync();                                       \
+    __syncthreads();                              \
     t1 = stamp();                                 \
-    if (lane == 0) prof[k] += t1 - t0;            \
+    if (threadIdx.x == 0) prof[k] += t1 - t0;     \
     t0 = t1;                                      \
   }
-  if (prof) t0 = stamp();
-  for (int s = 0; s < nsub; s++) {
-    kinematics(e, lane);
-    sync();
-    PROF(0)
-    com_pos_crb(e, lane);
-    PROF(1)
-    velocity_stage(e, lane);
-    PROF(2)
-    const int ncon = collision(e, lane);
-    sync();
-    PROF(3)
-    int ne = 0;
-    const int nefc = make_constraints(e, lane, ncon, &ne);
-    PROF(4)
-    const int iters = solve(e, nefc, ne, lane);
-    PROF(5)
-    sensors(e, ncon, lane);
-    PROF(6)
-    if (lane == 0) {
-      e.stats[0] = ncon;
-      e.stats[1] = nefc;
-      e.stats[2] = iters;
-    }
-    if (args.integrate_flag) integrate(e, lane);
-    PROF(7)
+
+// front half of mj_step: kinematics -> constraint rows (one wavefront per env)
+__global__ void __launch_bounds__(64) front_kernel(KArgs args) {
+  extern __shared__ __attribute__((aligned(16))) double front_smem[];
+  const int env = blockIdx.x;
+  const int lane = threadIdx.x;
+  if (env >= args.n_env) return;
+  if (args.active && !args.active[env]) return;
+  Env e;
+  make_env(args, env, e);
+  e.sh = front_smem;
+  PROF_BEGIN()
+  kinematics(e, lane);
+  sync();
+  PROF(0)
+  com_pos_crb(e, lane);
+  PROF(1)
+  velocity_stage(e, lane);
+  PROF(2)
+  const int ncon = collision(e, lane);
+  sync();
+  PROF(3)
+  int ne = 0;
+  const int nefc = make_constraints(e, lane, ncon, &ne);
+  PROF(4)
+  if (lane == 0) {
+    WI(scal)[0] = ncon;
+    WI(scal)[1] = nefc;
+    WI(scal)[2] = ne;
+    e.stats[0] = ncon;
+    e.stats[1] = nefc;
   }
-#undef PROF
+}
+
+// back half: Newton solve, constraint forces, sensors, implicitfast integration (4 waves/env)
+__global__ void __launch_bounds__(SOLVER_THREADS) solver_kernel(KArgs args) {
+  __shared__ SolverShared S;
+  const int env = blockIdx.x;
+  const int tid = threadIdx.x;
+  if (env >= args.n_env) return;
+  if (args.active && !args.active[env]) return;
+  Env e;
+  make_env(args, env, e);
+  const int NB = (args.m.nv + 3) / 4;
+  int bi = 0, bj = 0;
+  const bool own = tid < NB * (NB + 1) / 2;
+  if (own) blk_coords(tid, &bi, &bj);
+  double a[16];
+  PROF_BEGIN()
+  const int ncon = WI(scal)[0], nefc = WI(scal)[1], ne = WI(scal)[2];
+  const int iters = solver_newton(e, S, a, bi, bj, own, nefc, ne, tid);
+  PROF(5)
+  sensors(e, ncon, tid, S.bacc, S.bfrc);
+  PROF(6)
+  if (tid == 0) e.stats[2] = iters;
+  if (args.integrate_flag) solver_integrate(e, S, a, bi, bj, own, tid);
+  PROF(7)
 }
 
 static Layout make_layout(const rmbx_model& m) {
@@ -1682,7 +1925,8 @@ extern "C" {
 int rmbx_engine_create(const struct rmbx_model* model, int n_env, rmbx_engine** out) {
   RMBX_CHECK_ARG(model && out && n_env > 0, "bad arguments to rmbx_engine_create");
   const rmbx_model& h = *model;
-  RMBX_CHECK_ARG(h.nv > 0 && h.nv <= 96, "nv=%d outside the supported range [1, 96]", h.nv);
+  RMBX_CHECK_ARG(h.nv > 0 && h.nv <= MAX_NVP, "nv=%d outside the supported range [1, %d]", h.nv, MAX_NVP);
+  RMBX_CHECK_ARG(h.nbody > 0 && h.nbody <= MAX_BODY, "nbody=%d outside [1, %d]", h.nbody, MAX_BODY);
   RMBX_CHECK_ARG(h.max_contacts > 0 && h.max_contacts <= 1024, "bad max_contacts=%d",
                  h.max_contacts);
   rmbx_engine* eng = new rmbx_engine();
@@ -1809,10 +2053,15 @@ static int launch(rmbx_engine* eng, int nsub, int integ, const uint8_t* active, 
   a.nsub = nsub;
   a.integrate_flag = integ;
   a.prof = prof;
-  const size_t lds = (size_t)eng->host.nv * eng->host.nv * sizeof(double);
-  hipLaunchKernelGGL(physics_kernel, dim3(eng->n_env), dim3(64), lds,
-                     reinterpret_cast<hipStream_t>(stream), a);
-  RMBX_CHECK_LAUNCH();
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  const int reps = integ ? nsub : 1;
+  for (int s = 0; s < reps; s++) {
+    const size_t front_lds = (34 * (size_t)eng->host.nbody + 6 * (size_t)eng->host.nv) * sizeof(double);
+    hipLaunchKernelGGL(front_kernel, dim3(eng->n_env), dim3(64), front_lds, st, a);
+    RMBX_CHECK_LAUNCH();
+    hipLaunchKernelGGL(solver_kernel, dim3(eng->n_env), dim3(SOLVER_THREADS), 0, st, a);
+    RMBX_CHECK_LAUNCH();
+  }
   return RMBX_OK;
 }
 
