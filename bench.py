@@ -114,9 +114,12 @@ def main():
             "--world_random_scale", "0.01", "0.01", "0.0", "--seed", str(rank), "--precision", args.precision]
     if args.act_prune_dead_decoder:
         argv.append("--act_prune_dead_decoder")
+    from robomanipbaselines_amd.distributed import gather_results, pack_results, shard_range
+
     ro = Rollout(argv=argv)
     # per-env world index from the GLOBAL env index so results do not depend on the GPU count
-    ro.args.world_idx_list = [(rank * n + e) % 6 for e in range(n)]
+    g0, g1 = shard_range(rank, world, n * world)
+    ro.args.world_idx_list = [g % 6 for g in range(g0, g1)]
     ro.reset()
     ro._active = None
     n_pre = len(ro.pre_durations)
@@ -141,7 +144,18 @@ def main():
         phys_ms.append((e0, e1))
 
     eng.step = timed_step
-    infer0 = len(ro.inference_duration_list)
+    infer_ev = []
+    orig_infer = ro.infer_policy
+
+    def timed_infer():
+        e0 = torch.cuda.Event(enable_timing=True)
+        e1 = torch.cuda.Event(enable_timing=True)
+        e0.record()
+        orig_infer()
+        e1.record()
+        infer_ev.append((e0, e1))
+
+    ro.infer_policy = timed_infer
     if dist:
         tdist.barrier()
     torch.cuda.synchronize()
@@ -153,18 +167,17 @@ def main():
         tdist.barrier()
     elapsed = time.time() - t0
     eng.step = orig_step
+    ro.infer_policy = orig_infer
     phys = np.array([a.elapsed_time(b) for a, b in phys_ms])
-    infer = np.array(ro.inference_duration_list[infer0:])
+    infer = np.array([a.elapsed_time(b) for a, b in infer_ev]) / 1e3  # seconds (GPU time)
     if dist:
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         elapsed = float(t.item())
-        # RCCL all-gather of per-env episode state (success u8, reward f32, duration f32, steps i32)
+        # RCCL all-gather of per-env episode records (success, reward, duration, steps)
         v = K.sched_view(ro.sched)
-        rec = torch.tensor(np.stack([v["success"], v["result_reward"], v["duration"], v["rollout_time_idx"]], 1),
-                           dtype=torch.float32, device=dev)
-        out = [torch.empty_like(rec) for _ in range(world)]
-        tdist.all_gather(out, rec)
+        gathered = gather_results(pack_results(v["success"], v["result_reward"], v["duration"], v["rollout_time_idx"]), dev)
+        assert gathered.shape[0] == n * world
     total_envs = n * world
     value = total_envs * args.steps / elapsed
     st = eng.stats.cpu().numpy()
