@@ -6,9 +6,11 @@
  * rmbx_last_error(), thread-local) and enqueues its work on the caller's HIP stream
  * (`stream` is a hipStream_t passed as void*, NULL = the legacy default stream).
  * No call allocates, frees or synchronises on the hot path, so every hot-path call can be
- * captured in a hipGraph.  Ownership: the engine owns model constants and per-env state; all
- * I/O buffers are caller-owned device memory.  Threading: one host thread per engine; calls on
- * one engine handle are not re-entrant.
+ * captured in a hipGraph.  Ownership: the engine owns the device copy of the model constants;
+ * per-env state (qpos, qvel, warm start, ctrl, ...) and the solver workspace are caller-owned
+ * device buffers attached with rmbx_engine_bind, so the caller (torch) keeps them resident and
+ * can read them zero-copy.  Threading: one host thread per engine; calls on one engine handle
+ * are not re-entrant.
  *
  * Each function cites the reference (yusuke1127/RoboManipBaselines @2.0.0) interface it replaces
  * for a batch of environments; paths are relative to the reference package root
