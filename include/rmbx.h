@@ -215,6 +215,23 @@ int rmbx_render(const rmbx_camera* cam, const int32_t* prim_i32, const float* pr
                 void* policy_img, int policy_dtype, const uint8_t* active, int n_env,
                 void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Policy vision-trunk epilogues (ResNet-18 with frozen BN folded into the convs), NHWC.
+ * Replace the per-element tail of torchvision's BasicBlock / stem as used by ACT's DETR backbone
+ * (third_party/act, absent submodule) and policy/mlp/MlpPolicy.py:34-39:
+ *   conv -> BN -> ReLU [-> maxpool 3x3/2 pad 1]   and   conv -> BN -> (+ identity/downsample) -> ReLU.
+ * x, res, out: [n_pix][C] activations in the storage dtype (dtype 1 = bf16, 0 = f32), 16-byte
+ * aligned, C a multiple of 8 (bf16) / 4 (f32); bias, res_bias: f32 [C] (values representable in
+ * the storage dtype).  out = relu?(rnd(rnd(x + bias) + rnd(res + res_bias))), res / res_bias
+ * optional (NULL), every intermediate rounded to the storage dtype as the unfused path does.
+ * out may alias x.
+ * ------------------------------------------------------------------------------------------- */
+int rmbx_nhwc_bias_act(const void* x, const float* bias, const void* res, const float* res_bias,
+                       void* out, size_t n_pix, int C, int relu, int dtype, void* stream);
+/* out [N][Ho][Wo][C] = maxpool3x3s2p1(relu(rnd(x + bias))), Ho = (H-1)/2+1, Wo = (W-1)/2+1. */
+int rmbx_nhwc_bias_relu_maxpool(const void* x, const float* bias, void* out, int N, int H, int W,
+                                int C, int dtype, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -43,6 +43,8 @@ SIGNATURES = {
     "rmbx_arm_fk": (_c_int, [_c_p] * 4 + [_c_int, _c_p]),
     "rmbx_render": (_c_int, [_c_p, _c_p, _c_p, _c_int, _c_p, _c_p, _c_p, _c_p, _c_int, _c_int, _c_p, _c_p, _c_p,
                              _c_int, _c_p, _c_int, _c_p]),
+    "rmbx_nhwc_bias_act": (_c_int, [_c_p] * 5 + [_c_sz, _c_int, _c_int, _c_int, _c_p]),
+    "rmbx_nhwc_bias_relu_maxpool": (_c_int, [_c_p] * 3 + [_c_int] * 5 + [_c_p]),
 }
 
 

@@ -199,3 +199,54 @@ def sched_update(sched, time, reward, pre_durations, max_duration, post_success=
     _chk(pre_durations, torch.float64, None, "pre_durations")
     N.call("rmbx_sched_update", N.ptr(sched), N.ptr(time), N.ptr(reward), N.ptr(pre_durations),
            pre_durations.numel(), float(max_duration), float(post_success), n, N.stream_ptr())
+
+
+# ------------------------------------------------------------------------------------------
+# Vision-trunk epilogues (NHWC = torch channels_last)
+# ------------------------------------------------------------------------------------------
+_NN_DTYPES = {torch.bfloat16: 1, torch.float32: 0}
+
+
+def _chk_nhwc(t, name):
+    if not isinstance(t, torch.Tensor) or not t.is_cuda:
+        raise ValueError(f"{name} must be a device tensor")
+    if t.dtype not in _NN_DTYPES:
+        raise ValueError(f"{name} must be bf16 or f32 (got {t.dtype})")
+    if t.dim() != 4 or not t.is_contiguous(memory_format=torch.channels_last):
+        raise ValueError(f"{name} must be a 4-D channels_last tensor")
+    return t
+
+
+def nhwc_bias_act(x, bias, res=None, res_bias=None, relu=True, out=None):
+    """out = relu?(rnd(rnd(x + bias) + rnd(res + res_bias))) on channels_last [N, C, H, W]
+    activations (rmbx_nhwc_bias_act); `bias`/`res_bias` f32 [C]. In place when out is x."""
+    _chk_nhwc(x, "x")
+    C = x.shape[1]
+    _chk(bias, torch.float32, (C,), "bias")
+    if res is not None:
+        _chk_nhwc(res, "res")
+        if res.shape != x.shape or res.dtype != x.dtype:
+            raise ValueError("res must match x in shape and dtype")
+    if res_bias is not None:
+        if res is None:
+            raise ValueError("res_bias needs res")
+        _chk(res_bias, torch.float32, (C,), "res_bias")
+    if out is None:
+        out = torch.empty_like(x, memory_format=torch.channels_last)
+    _chk_nhwc(out, "out")
+    n_pix = x.numel() // C
+    N.call("rmbx_nhwc_bias_act", N.ptr(x), N.ptr(bias), N.ptr(res), N.ptr(res_bias), N.ptr(out), n_pix, C,
+           int(bool(relu)), _NN_DTYPES[x.dtype], N.stream_ptr())
+    return out
+
+
+def nhwc_bias_relu_maxpool(x, bias):
+    """maxpool3x3/2/pad1(relu(rnd(x + bias))) of a channels_last [N, C, H, W] tensor."""
+    _chk_nhwc(x, "x")
+    n, C, H, W = x.shape
+    _chk(bias, torch.float32, (C,), "bias")
+    Ho, Wo = (H - 1) // 2 + 1, (W - 1) // 2 + 1
+    out = torch.empty((n, C, Ho, Wo), dtype=x.dtype, device=x.device, memory_format=torch.channels_last)
+    N.call("rmbx_nhwc_bias_relu_maxpool", N.ptr(x), N.ptr(bias), N.ptr(out), n, H, W, C, _NN_DTYPES[x.dtype],
+           N.stream_ptr())
+    return out

@@ -9,6 +9,8 @@ import torch
 import torch.nn as nn
 import torch.nn.functional as F
 
+from .. import kernels as K
+
 
 class FrozenBatchNorm2d(nn.Module):
     """torchvision.ops.misc.FrozenBatchNorm2d: y = (x - rm) / sqrt(rv + eps) * w + b."""
@@ -70,6 +72,9 @@ class ResNet18Trunk(nn.Module):
 
 
 class _FusedConv(nn.Module):
+    """conv + folded frozen BN.  The conv runs without bias (MIOpen, MFMA); bias, residual and
+    ReLU are applied by the rmbx HIP epilogue in one pass over the output."""
+
     def __init__(self, conv, bn, relu):
         super().__init__()
         s, b = bn.scale_shift()
@@ -78,10 +83,25 @@ class _FusedConv(nn.Module):
         self.conv.weight.data.copy_(w)
         self.conv.bias.data.copy_(b.detach())
         self.relu = relu
+        self._bias_key = None
+        self._bias_f32 = None
+
+    def conv_nobias(self, x):
+        c = self.conv
+        return F.conv2d(x, c.weight, None, c.stride, c.padding)
+
+    def bias_f32(self):
+        """The bias in the storage dtype, widened to f32 for the epilogue (cached)."""
+        b = self.conv.bias
+        key = (b.data_ptr(), b.dtype, b.device)
+        if key != self._bias_key:
+            self._bias_f32 = b.detach().float().contiguous()
+            self._bias_key = key
+        return self._bias_f32
 
     def forward(self, x):
-        y = self.conv(x)
-        return F.relu(y) if self.relu else y
+        y = self.conv_nobias(x)
+        return K.nhwc_bias_act(y, self.bias_f32(), relu=self.relu, out=y)
 
 
 class _FusedBlock(nn.Module):
@@ -92,12 +112,19 @@ class _FusedBlock(nn.Module):
         self.down = None if blk.downsample is None else _FusedConv(blk.downsample[0], blk.downsample[1], False)
 
     def forward(self, x):
-        idt = x if self.down is None else self.down(x)
-        return F.relu(self.c2(self.c1(x)) + idt)
+        y = self.c1(x)
+        z = self.c2.conv_nobias(y)
+        if self.down is None:
+            return K.nhwc_bias_act(z, self.c2.bias_f32(), res=x, relu=True, out=z)
+        d = self.down.conv_nobias(x)
+        return K.nhwc_bias_act(z, self.c2.bias_f32(), res=d, res_bias=self.down.bias_f32(), relu=True, out=z)
 
 
 class FusedResNet18Trunk(nn.Module):
-    """Inference form: BN folded into conv weights/bias (identical function, one less pass)."""
+    """Inference form on the device: BN folded into conv weights/bias, channels_last
+    activations, conv (MIOpen) + one rmbx HIP epilogue per conv (bias / residual / ReLU, and the
+    stem's max-pool).  Same function as ResNet18Trunk; bit-identical to the unfused storage-dtype
+    sequence on the same conv outputs (tests/test_nn_gpu.py)."""
 
     def __init__(self, trunk):
         super().__init__()
@@ -108,4 +135,5 @@ class FusedResNet18Trunk(nn.Module):
         self.blocks = nn.Sequential(*blocks)
 
     def forward(self, x):
-        return self.blocks(F.max_pool2d(self.stem(x), 3, 2, 1))
+        s = self.stem.conv_nobias(x)
+        return self.blocks(K.nhwc_bias_relu_maxpool(s, self.stem.bias_f32()))

@@ -1,0 +1,135 @@
+"""Vision-trunk epilogue kernels (rmbx_nhwc_bias_act / rmbx_nhwc_bias_relu_maxpool) vs the
+unfused PyTorch sequence they replace (bias add -> [residual add] -> ReLU [-> max-pool]), and the
+fused ResNet-18 trunk vs the fp32 FrozenBN reference module."""
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+def _cl(t):
+    return t.contiguous(memory_format=torch.channels_last)
+
+
+def _torch_epilogue(x, b, res=None, rb=None, relu=True):
+    y = x + b.to(x.dtype).reshape(1, -1, 1, 1)
+    if res is not None:
+        r = res if rb is None else res + rb.to(x.dtype).reshape(1, -1, 1, 1)
+        y = y + r
+    return F.relu(y) if relu else y
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("mode", ["bias", "bias_relu", "res_relu", "res_bias_relu", "res_bias"])
+def test_bias_act_bit_exact(dtype, mode):
+    from robomanipbaselines_amd import kernels as K
+
+    g = torch.Generator(device=DEV).manual_seed(1)
+    x = _cl(torch.randn(3, 64, 9, 13, device=DEV, generator=g).to(dtype))
+    b = torch.randn(64, device=DEV, generator=g).to(dtype).float()
+    res = _cl(torch.randn(3, 64, 9, 13, device=DEV, generator=g).to(dtype)) if "res" in mode else None
+    rb = torch.randn(64, device=DEV, generator=g).to(dtype).float() if "res_bias" in mode else None
+    relu = "relu" in mode
+    ref = _torch_epilogue(x, b, res, rb, relu)
+    got = K.nhwc_bias_act(x, b, res, rb, relu=relu)
+    assert torch.equal(got, ref)
+    # in place
+    x2 = x.clone(memory_format=torch.channels_last)
+    K.nhwc_bias_act(x2, b, res, rb, relu=relu, out=x2)
+    assert torch.equal(x2, ref)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("hw", [(17, 23), (16, 16), (240, 320), (1, 1)])
+def test_bias_relu_maxpool_bit_exact(dtype, hw):
+    from robomanipbaselines_amd import kernels as K
+
+    g = torch.Generator(device=DEV).manual_seed(2)
+    H, W = hw
+    x = _cl(torch.randn(2, 64, H, W, device=DEV, generator=g).to(dtype))
+    b = torch.randn(64, device=DEV, generator=g).to(dtype).float()
+    ref = F.max_pool2d(_torch_epilogue(x, b), 3, 2, 1)
+    got = K.nhwc_bias_relu_maxpool(x, b)
+    assert got.shape == ref.shape
+    assert torch.equal(got, ref)
+
+
+def test_epilogue_rejects_bad_layout():
+    from robomanipbaselines_amd import kernels as K
+
+    x = torch.randn(2, 64, 5, 5, device=DEV)  # NCHW-contiguous, not channels_last
+    with pytest.raises(ValueError):
+        K.nhwc_bias_act(x, torch.zeros(64, device=DEV))
+    y = _cl(torch.randn(2, 12, 5, 5, device=DEV, dtype=torch.bfloat16))  # C not a multiple of 8
+    with pytest.raises(ValueError):
+        K.nhwc_bias_act(y, torch.zeros(12, device=DEV))
+
+
+def _trunk_pair(seed=0):
+    from robomanipbaselines_amd.policy.backbone import FusedResNet18Trunk, ResNet18Trunk
+
+    torch.manual_seed(seed)
+    ref = ResNet18Trunk().eval().requires_grad_(False)
+    for m in ref.modules():  # non-trivial frozen BN statistics
+        if hasattr(m, "running_var"):
+            m.weight.uniform_(0.5, 1.5)
+            m.bias.uniform_(-0.2, 0.2)
+            m.running_mean.uniform_(-0.2, 0.2)
+            m.running_var.uniform_(0.5, 2.0)
+    fused = FusedResNet18Trunk(ref)
+    return ref, fused
+
+
+@torch.no_grad()
+def test_fused_trunk_fp32_matches_reference():
+    ref, fused = _trunk_pair()
+    x = torch.rand(2, 3, 96, 128)
+    want = ref(x)
+    fused = fused.to(DEV).to(memory_format=torch.channels_last)
+    got = fused(_cl(x.to(DEV))).cpu()
+    assert got.shape == want.shape == (2, 512, 3, 4)
+    err = (got - want).abs().max().item()
+    assert err <= 1e-3 * max(1.0, want.abs().max().item()), err
+
+
+@torch.no_grad()
+def test_fused_trunk_bf16_epilogues_equal_unfused_sequence():
+    """Walk the trunk with each conv evaluated ONCE; the HIP epilogues and the torch ops applied
+    to the same conv outputs must agree bit for bit at every block (real trunk shapes)."""
+    ref, fused = _trunk_pair(1)
+    fused = fused.to(DEV, torch.bfloat16).to(memory_format=torch.channels_last)
+    from robomanipbaselines_amd import kernels as K
+
+    x = _cl(torch.rand(2, 3, 96, 128, device=DEV).to(torch.bfloat16))
+    s = fused.stem.conv_nobias(x)
+    h = K.nhwc_bias_relu_maxpool(s, fused.stem.bias_f32())
+    assert torch.equal(h, F.max_pool2d(_torch_epilogue(s, fused.stem.bias_f32()), 3, 2, 1))
+    for blk in fused.blocks:
+        c1 = blk.c1.conv_nobias(h)
+        y = K.nhwc_bias_act(c1, blk.c1.bias_f32(), relu=True)
+        assert torch.equal(y, _torch_epilogue(c1, blk.c1.bias_f32()))
+        z = blk.c2.conv_nobias(y)
+        if blk.down is None:
+            out = K.nhwc_bias_act(z, blk.c2.bias_f32(), res=h, relu=True)
+            want = _torch_epilogue(z, blk.c2.bias_f32(), h)
+        else:
+            d = blk.down.conv_nobias(h)
+            out = K.nhwc_bias_act(z, blk.c2.bias_f32(), res=d, res_bias=blk.down.bias_f32(), relu=True)
+            want = _torch_epilogue(z, blk.c2.bias_f32(), d, blk.down.bias_f32())
+        assert torch.equal(out, want)
+        h = out
+
+
+@torch.no_grad()
+def test_fused_trunk_bf16_close_to_fp32_reference():
+    ref, fused = _trunk_pair(2)
+    x = torch.rand(2, 3, 96, 128)
+    want = ref(x)
+    fused = fused.to(DEV, torch.bfloat16).to(memory_format=torch.channels_last)
+    got = fused(_cl(x.to(DEV).to(torch.bfloat16))).float().cpu()
+    rel = (got - want).norm() / want.norm()
+    assert rel < 3e-2, rel.item()
