@@ -136,17 +136,23 @@ class BatchedRolloutBase:
         scale = (st["norm_config"]["out_max"] - st["norm_config"]["out_min"]) / self._st_range
         return (scale * (jp - self._st_min) + st["norm_config"]["out_min"]).to(torch.float32)
 
+    # per-channel (mean, std) the renderer applies to [0, 1] pixels for the policy tensor:
+    # identity = RolloutBase.image_transforms (v2.ToDtype(float32, scale=True), :353); the ACT
+    # policy overrides it with its ImageNet normalisation
+    image_norm = ((0.0, 0.0, 0.0), (1.0, 1.0, 1.0))
+
     def get_images(self, dtype):
         """Render every policy camera straight into the normalised policy tensor [n,ncam,3,H,W]."""
         H, W = self.env.renderer.height, self.env.renderer.width
+        mean, std = self.image_norm
         if getattr(self, "_img", None) is None or self._img.dtype != dtype:
             self._img = torch.empty((self.n, len(self.camera_names), 3, H, W), dtype=dtype, device=self.device)
             self._img_cam = [torch.empty((self.n, 3, H, W), dtype=dtype, device=self.device) for _ in self.camera_names]
         if len(self.camera_names) == 1:
-            self.env.render_images(self.camera_names[0], policy=self._img.view(self.n, 3, H, W))
+            self.env.render_images(self.camera_names[0], policy=self._img.view(self.n, 3, H, W), mean=mean, std=std)
             return self._img
         for i, cam in enumerate(self.camera_names):
-            self.env.render_images(cam, policy=self._img_cam[i])
+            self.env.render_images(cam, policy=self._img_cam[i], mean=mean, std=std)
             self._img[:, i].copy_(self._img_cam[i])
         return self._img
 

@@ -147,7 +147,9 @@ class BatchedMujocoUR5eCableEnv:
         p2 = e.gxpos[:, self._pole_geoms[1]].contiguous()
         return K.cable_reward(cable, end, p1, p2, out=self.reward if self.reward.is_contiguous() else None)
 
-    def render_images(self, camera_name="front", rgb=None, depth=None, policy=None, active=None):
-        """MujocoEnvBase._get_info (:103-126) for one camera, all envs."""
-        self.renderer.render(self.engine, camera_name, rgb=rgb, depth=depth, policy=policy, active=active)
+    def render_images(self, camera_name="front", rgb=None, depth=None, policy=None, active=None, mean=None, std=None):
+        """MujocoEnvBase._get_info (:103-126) for one camera, all envs; `policy` receives
+        ((rgb / 255) - mean) / std as [n, 3, H, W]."""
+        self.renderer.render(self.engine, camera_name, rgb=rgb, depth=depth, policy=policy, active=active,
+                             mean=mean, std=std)
         return rgb, depth, policy

@@ -9,11 +9,13 @@ import torch
 
 from ... import kernels as K
 from ...common.rollout_base import BatchedRolloutBase
-from .act_model import ActModel
+from .act_model import IMAGENET_MEAN, IMAGENET_STD, ActModel
 
 
 class RolloutAct(BatchedRolloutBase):
     policy_name = "Act"
+    # ACTPolicy.__call__ normalises with ImageNet statistics before the backbone
+    image_norm = (IMAGENET_MEAN, IMAGENET_STD)
 
     def set_additional_args(self, parser):
         parser.add_argument("--no_temp_ensem", action="store_true",

@@ -1,0 +1,118 @@
+"""End-to-end batched rollouts on the device (Operation + Rollout<Policy> composition, as
+bin/Rollout.py:83-86 builds it): the scripted pre-motion phases, policy calls every `skip`
+steps, the action buffer / ensemble and the result contract.  The policy output that reaches
+the env is checked against a host f64 recomputation of the reference arithmetic from the
+recorded network outputs (RolloutMlp.py:107-124, RolloutAct.py:68-101, DataUtils.py:26-40), and
+the fused device networks against their unfused fp32 reference modules."""
+
+import numpy as np
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _compose(policy):
+    from robomanipbaselines_amd.envs.operation.OperationMujocoUR5eCable import OperationMujocoUR5eCable
+
+    if policy == "Mlp":
+        from robomanipbaselines_amd.policy.mlp.rollout_mlp import RolloutMlp as P
+    else:
+        from robomanipbaselines_amd.policy.act.rollout_act import RolloutAct as P
+
+    class Rollout(OperationMujocoUR5eCable, P):
+        pass
+
+    return Rollout
+
+
+def _record(ro):
+    rec = []
+    fwd = ro.policy.forward
+
+    def spy(state, images):
+        out = fwd(state, images)
+        rec.append(out.float().cpu().numpy().astype(np.float64))
+        return out
+
+    ro.policy.forward = spy
+    return rec
+
+
+@pytest.mark.parametrize("n_action", [1, 3])
+def test_rollout_mlp_actions_follow_reference_arithmetic(n_action):
+    R = _compose("Mlp")
+    ro = R(argv=["--num_envs", "6", "--device", DEV, "--world_idx_list", "0", "1", "2", "3", "4", "5",
+                 "--precision", "fp32"])
+    ro.model_meta_info["data"]["n_action_steps"] = n_action
+    ro.setup_policy()
+    rec = _record(ro)
+    ro.reset()
+    ro._active = None
+    n_pre = len(ro.pre_durations)
+    while ro.phase_idx < n_pre:
+        ro.step_once()
+    st = ro.model_meta_info["action"]
+    actions = []
+    for _ in range(3 * 4 * n_action):
+        if ro.rollout_time_idx % ro.args.skip == 0:
+            ro.step_once()
+            actions.append(ro.policy_action.cpu().numpy().copy())
+        else:
+            ro.step_once()
+    # network ran once per n_action policy calls
+    assert len(rec) == (len(actions) + n_action - 1) // n_action
+    for i, a in enumerate(actions):
+        out = rec[i // n_action]  # [n, n_action, 7]
+        want = st["std"] * out[:, i % n_action] + st["mean"]
+        assert np.array_equal(a, want), i
+    assert np.isfinite(ro.env.engine.qpos.cpu().numpy()).all()
+
+
+def test_rollout_act_temporal_ensemble_follows_reference_arithmetic():
+    R = _compose("Act")
+    ro = R(argv=["--num_envs", "4", "--device", DEV, "--precision", "fp32"])
+    rec = _record(ro)
+    ro.reset()
+    ro._active = None
+    while ro.phase_idx < len(ro.pre_durations):
+        ro.step_once()
+    st = ro.model_meta_info["action"]
+    w_all = []
+    for _ in range(3 * 5):
+        call = ro.rollout_time_idx % ro.args.skip == 0
+        ro.step_once()
+        if call:
+            got = ro.policy_action.cpu().numpy()
+            hist = rec[-100:]
+            n = len(hist)
+            w = np.exp(-0.01 * np.arange(n))
+            w = w / w.sum()
+            acc = np.zeros((got.shape[0], got.shape[1]))
+            for j in range(n):  # newest first, as RolloutAct.py:93-97
+                k = n - 1 - j
+                acc = acc + w[k] * hist[k][:, j]
+            want = st["std"] * acc + st["mean"]
+            assert np.array_equal(got, want)
+            w_all.append(n)
+    assert w_all == list(range(1, len(w_all) + 1))
+
+
+def test_mlp_fused_fp32_matches_reference_module():
+    from robomanipbaselines_amd.policy.mlp.mlp_model import MlpModel
+
+    torch.manual_seed(0)
+    ref = MlpModel(7, 7, 1, n_obs_steps=2, n_action_steps=3).eval().requires_grad_(False)
+    dev = MlpModel(7, 7, 1, n_obs_steps=2, n_action_steps=3).eval().requires_grad_(False)
+    dev.load_state_dict(ref.state_dict())
+    dev.fuse_backbone()
+    dev = dev.to(DEV)
+    dev._fused = dev._fused.to(memory_format=torch.channels_last)
+    s = torch.randn(3, 2, 7)
+    im = torch.rand(3, 1, 2, 3, 96, 128)
+    with torch.no_grad():
+        want = ref(s, im)
+        got = dev(s.to(DEV), im.to(DEV)).cpu()
+    assert got.shape == (3, 3, 7)
+    assert (got - want).abs().max().item() <= 1e-3 * max(1.0, want.abs().max().item())
