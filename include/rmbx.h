@@ -232,6 +232,43 @@ int rmbx_nhwc_bias_act(const void* x, const float* bias, const void* res, const 
 int rmbx_nhwc_bias_relu_maxpool(const void* x, const float* bias, void* out, int N, int H, int W,
                                 int C, int dtype, void* stream);
 
+/* ---------------------------------------------------------------------------------------------
+ * Diffusion-policy sampler steps, batched over envs (all tensors f32 device, n elements).
+ * Replace one `noise_scheduler.step(model_output, t, sample).prev_sample` of the reference's
+ * conditional_sample loop (diffusion_policy / 3D-Diffusion-Policy submodules, absent; schedulers
+ * from diffusers==0.11.1, pyproject.toml:69), called from
+ * policy/diffusion_policy/RolloutDiffusionPolicy.py:66-87 (DDPMScheduler,
+ * TrainDiffusionPolicy.py:130-138) and policy/diffusion_policy_3d/RolloutDiffusionPolicy3d.py:83-101
+ * (DDIMScheduler, TrainDiffusionPolicy3d.py:203-211).  `coeffs` is a HOST array of per-timestep
+ * f32 scalars computed as the scheduler computes them (robomanipbaselines_amd/policy/diffusion/
+ * schedulers.py); element arithmetic is f32 in the scheduler's order, no contraction.
+ *
+ * DDPM (epsilon, clip_sample, fixed_small): coeffs = {sqrt(1-acp_t), 1/sqrt(acp_t), x0 coeff,
+ *   x_t coeff, sigma_t, t > 0}; noise [n] is read only when t > 0.
+ * DDIM (eta 0, prediction "sample", clip_sample): coeffs = {sqrt(acp_prev),
+ *   sqrt(1-acp_prev), sqrt(acp_t), 1/sqrt(1-acp_t)}; eps_mode 0 = diffusers 0.11.1 direction
+ *   term (the model output), 1 = epsilon re-derived from the unclipped x0 (later releases).
+ * ------------------------------------------------------------------------------------------- */
+int rmbx_ddpm_step(const float* model_output, const float* sample, const float* noise,
+                   float* prev_sample, size_t n, const float* coeffs, void* stream);
+int rmbx_ddim_step(const float* model_output, const float* sample, float* prev_sample, size_t n,
+                   const float* coeffs, int eps_mode, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * Policy-input image preprocessing, batched over envs.
+ * rmbx_resize_crop_u8: src u8 [n][H][W][C] (renderer frames) -> dst [n][C][ch][cw] (f32 dtype 0 /
+ * bf16 dtype 1) = (v * (1/255)) * a + b, v = cv2.resize(src, (rw, rh), INTER_LINEAR)[y0+y, x0+x].
+ * Replaces RolloutDiffusionPolicy.get_images (policy/diffusion_policy/RolloutDiffusionPolicy.py:
+ * 107-138: resize, ToDtype(scale), * 2 - 1) plus the obs encoder's eval centre crop.
+ * rmbx_resize_f32: cv2.resize of f32 [n][H][W] depth to [n][rh][rw]
+ * (RolloutDiffusionPolicy3d.py:138-145).
+ * ------------------------------------------------------------------------------------------- */
+int rmbx_resize_crop_u8(const uint8_t* src, int n_env, int H, int W, int C, int rh, int rw, int y0,
+                        int x0, int ch, int cw, float a, float b, void* dst, int dst_dtype,
+                        void* stream);
+int rmbx_resize_f32(const float* src, float* dst, int n_env, int H, int W, int rh, int rw,
+                    void* stream);
+
 #ifdef __cplusplus
 }
 #endif

@@ -11,7 +11,7 @@ import sys
 
 import yaml
 
-POLICIES = ["Mlp", "Act"]
+POLICIES = ["Mlp", "Act", "DiffusionPolicy"]
 ENVS = ["MujocoUR5eCable"]
 
 

@@ -250,3 +250,37 @@ def nhwc_bias_relu_maxpool(x, bias):
     N.call("rmbx_nhwc_bias_relu_maxpool", N.ptr(x), N.ptr(bias), N.ptr(out), n, H, W, C, _NN_DTYPES[x.dtype],
            N.stream_ptr())
     return out
+
+
+# ------------------------------------------------------------------------------------------
+# Policy-input image preprocessing
+# ------------------------------------------------------------------------------------------
+def resize_crop_u8(src, size, crop=None, a=1.0, b=0.0, dtype=torch.float32, out=None):
+    """src u8 [n, H, W, C] -> [n, C, ch, cw] = cv2.resize(src, size=(rw, rh)) cropped at
+    crop = (y0, x0, ch, cw) (None = full), scaled v / 255 * a + b (rmbx_resize_crop_u8)."""
+    _chk(src, torch.uint8, name="src")
+    if src.dim() != 4:
+        raise ValueError("src must be [n, H, W, C]")
+    n, H, W, C = src.shape
+    rw, rh = int(size[0]), int(size[1])
+    y0, x0, ch, cw = crop if crop is not None else (0, 0, rh, rw)
+    if dtype not in _NN_DTYPES:
+        raise ValueError("dtype must be f32 or bf16")
+    if out is None:
+        out = torch.empty((n, C, ch, cw), dtype=dtype, device=src.device)
+    _chk(out, dtype, (n, C, ch, cw), "out")
+    N.call("rmbx_resize_crop_u8", N.ptr(src), n, H, W, C, rh, rw, y0, x0, ch, cw, float(a), float(b), N.ptr(out),
+           _NN_DTYPES[dtype], N.stream_ptr())
+    return out
+
+
+def resize_f32(src, size, out=None):
+    """cv2.resize of f32 [n, H, W] images to size = (rw, rh) (rmbx_resize_f32)."""
+    _chk(src, torch.float32, name="src")
+    n, H, W = src.shape
+    rw, rh = int(size[0]), int(size[1])
+    if out is None:
+        out = torch.empty((n, rh, rw), dtype=torch.float32, device=src.device)
+    _chk(out, torch.float32, (n, rh, rw), "out")
+    N.call("rmbx_resize_f32", N.ptr(src), N.ptr(out), n, H, W, rh, rw, N.stream_ptr())
+    return out

@@ -1,0 +1,138 @@
+"""ConditionalUnet1D — the denoising network of DiffusionPolicy and 3D-DiffusionPolicy.
+
+Restates the public diffusion_policy model (diffusion_policy/model/diffusion/conditional_unet1d.py;
+the reference's third_party/diffusion_policy and third_party/3D-Diffusion-Policy submodules are
+absent) as the reference configures it: down_dims [512, 1024, 2048], kernel 5, 8 groups,
+diffusion_step_embed_dim 128, global conditioning, FiLM (`cond_predict_scale`)
+(TrainDiffusionPolicy.py:114-129, TrainDiffusionPolicy3d.py:189-200).  Module names follow the
+upstream ones so its state_dict loads.  Parity vs the upstream code is unpinned (absent).
+
+Batched over environments; under rollout the 100 (DP) / 10 (DP3) evaluations per inference are
+captured with the scheduler-step kernels in one HIP graph (see dp_model.DiffusionSampler).
+"""
+
+import math
+
+import torch
+import torch.nn as nn
+import torch.nn.functional as F
+
+
+class SinusoidalPosEmb(nn.Module):
+    def __init__(self, dim):
+        super().__init__()
+        self.dim = dim
+
+    def forward(self, x):
+        half = self.dim // 2
+        emb = math.log(10000) / (half - 1)
+        emb = torch.exp(torch.arange(half, device=x.device) * -emb)
+        emb = x[:, None] * emb[None, :]
+        return torch.cat((emb.sin(), emb.cos()), dim=-1)
+
+
+class Conv1dBlock(nn.Module):
+    """Conv1d -> GroupNorm -> Mish."""
+
+    def __init__(self, inp, out, kernel_size, n_groups=8):
+        super().__init__()
+        self.block = nn.Sequential(nn.Conv1d(inp, out, kernel_size, padding=kernel_size // 2),
+                                   nn.GroupNorm(n_groups, out), nn.Mish())
+
+    def forward(self, x):
+        return self.block(x)
+
+
+class ConditionalResidualBlock1D(nn.Module):
+    def __init__(self, in_channels, out_channels, cond_dim, kernel_size=3, n_groups=8, cond_predict_scale=False):
+        super().__init__()
+        self.blocks = nn.ModuleList([Conv1dBlock(in_channels, out_channels, kernel_size, n_groups),
+                                     Conv1dBlock(out_channels, out_channels, kernel_size, n_groups)])
+        cond_channels = out_channels * 2 if cond_predict_scale else out_channels
+        self.cond_predict_scale = cond_predict_scale
+        self.out_channels = out_channels
+        self.cond_encoder = nn.Sequential(nn.Mish(), nn.Linear(cond_dim, cond_channels))
+        self.residual_conv = nn.Conv1d(in_channels, out_channels, 1) if in_channels != out_channels else nn.Identity()
+
+    def forward(self, x, cond):
+        out = self.blocks[0](x)
+        embed = self.cond_encoder(cond).unsqueeze(-1)
+        if self.cond_predict_scale:
+            embed = embed.reshape(embed.shape[0], 2, self.out_channels, 1)
+            out = embed[:, 0] * out + embed[:, 1]
+        else:
+            out = out + embed
+        out = self.blocks[1](out)
+        return out + self.residual_conv(x)
+
+
+class Downsample1d(nn.Module):
+    def __init__(self, dim):
+        super().__init__()
+        self.conv = nn.Conv1d(dim, dim, 3, 2, 1)
+
+    def forward(self, x):
+        return self.conv(x)
+
+
+class Upsample1d(nn.Module):
+    def __init__(self, dim):
+        super().__init__()
+        self.conv = nn.ConvTranspose1d(dim, dim, 4, 2, 1)
+
+    def forward(self, x):
+        return self.conv(x)
+
+
+class ConditionalUnet1D(nn.Module):
+    def __init__(self, input_dim, global_cond_dim=None, diffusion_step_embed_dim=256, down_dims=(256, 512, 1024),
+                 kernel_size=3, n_groups=8, cond_predict_scale=False):
+        super().__init__()
+        all_dims = [input_dim] + list(down_dims)
+        start_dim = down_dims[0]
+        dsed = diffusion_step_embed_dim
+        self.diffusion_step_encoder = nn.Sequential(SinusoidalPosEmb(dsed), nn.Linear(dsed, dsed * 4), nn.Mish(),
+                                                    nn.Linear(dsed * 4, dsed))
+        cond_dim = dsed + (global_cond_dim or 0)
+        in_out = list(zip(all_dims[:-1], all_dims[1:]))
+        mid_dim = all_dims[-1]
+        kw = dict(cond_dim=cond_dim, kernel_size=kernel_size, n_groups=n_groups, cond_predict_scale=cond_predict_scale)
+        self.mid_modules = nn.ModuleList([ConditionalResidualBlock1D(mid_dim, mid_dim, **kw),
+                                          ConditionalResidualBlock1D(mid_dim, mid_dim, **kw)])
+        self.down_modules = nn.ModuleList()
+        for ind, (dim_in, dim_out) in enumerate(in_out):
+            is_last = ind >= len(in_out) - 1
+            self.down_modules.append(nn.ModuleList([
+                ConditionalResidualBlock1D(dim_in, dim_out, **kw), ConditionalResidualBlock1D(dim_out, dim_out, **kw),
+                Downsample1d(dim_out) if not is_last else nn.Identity()]))
+        self.up_modules = nn.ModuleList()
+        for ind, (dim_in, dim_out) in enumerate(reversed(in_out[1:])):
+            is_last = ind >= len(in_out) - 1
+            self.up_modules.append(nn.ModuleList([
+                ConditionalResidualBlock1D(dim_out * 2, dim_in, **kw), ConditionalResidualBlock1D(dim_in, dim_in, **kw),
+                Upsample1d(dim_in) if not is_last else nn.Identity()]))
+        self.final_conv = nn.Sequential(Conv1dBlock(start_dim, start_dim, kernel_size=kernel_size),
+                                        nn.Conv1d(start_dim, input_dim, 1))
+
+    def forward(self, sample, timestep, global_cond=None):
+        """sample [B, T, input_dim], timestep [B] (or scalar) -> [B, T, input_dim]."""
+        x = sample.transpose(1, 2)
+        if not torch.is_tensor(timestep):
+            timestep = torch.tensor([timestep], dtype=torch.long, device=sample.device)
+        elif timestep.dim() == 0:
+            timestep = timestep[None].to(sample.device)
+        timestep = timestep.expand(sample.shape[0])
+        g = self.diffusion_step_encoder(timestep).to(sample.dtype)
+        if global_cond is not None:
+            g = torch.cat([g, global_cond], dim=-1)
+        h = []
+        for resnet, resnet2, down in self.down_modules:
+            x = resnet2(resnet(x, g), g)
+            h.append(x)
+            x = down(x)
+        for mid in self.mid_modules:
+            x = mid(x, g)
+        for resnet, resnet2, up in self.up_modules:
+            x = torch.cat((x, h.pop()), dim=1)
+            x = up(resnet2(resnet(x, g), g))
+        return self.final_conv(x).transpose(1, 2)
