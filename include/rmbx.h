@@ -257,7 +257,8 @@ int rmbx_ddim_step(const float* model_output, const float* sample, float* prev_s
 /* ---------------------------------------------------------------------------------------------
  * Policy-input image preprocessing, batched over envs.
  * rmbx_resize_crop_u8: src u8 [n][H][W][C] (renderer frames) -> dst [n][C][ch][cw] (f32 dtype 0 /
- * bf16 dtype 1) = (v * (1/255)) * a + b, v = cv2.resize(src, (rw, rh), INTER_LINEAR)[y0+y, x0+x].
+ * bf16 dtype 1) = (v * (1/255)) * a + b, v = cv2.resize(src, (rw, rh), INTER_LINEAR)[y0+y, x0+x];
+ * dst_dtype 2 writes v itself as u8 [n][ch][cw][C] (the resized frame).
  * Replaces RolloutDiffusionPolicy.get_images (policy/diffusion_policy/RolloutDiffusionPolicy.py:
  * 107-138: resize, ToDtype(scale), * 2 - 1) plus the obs encoder's eval centre crop.
  * rmbx_resize_f32: cv2.resize of f32 [n][H][W] depth to [n][rh][rw]
@@ -268,6 +269,24 @@ int rmbx_resize_crop_u8(const uint8_t* src, int n_env, int H, int W, int C, int 
                         void* stream);
 int rmbx_resize_f32(const float* src, float* dst, int n_env, int H, int W, int rh, int rw,
                     void* stream);
+
+/* ---------------------------------------------------------------------------------------------
+ * 3D-diffusion-policy point-cloud observation, batched (one workgroup per env).
+ * Replaces RolloutDiffusionPolicy3d.get_pointcloud (policy/diffusion_policy_3d/
+ * RolloutDiffusionPolicy3d.py:132-160) after the image resize: convert_depth_image_to_pointcloud
+ * (common/utils/VisionUtils.py:55-87), crop_pointcloud_bb (common/utils/Vision3dUtils.py:6-14),
+ * downsample_pointcloud_fps (Vision3dUtils.py:17-25, pytorch3d FPS from index 0) and
+ * normalize_data (common/utils/DataUtils.py:9-24).
+ * depth f32 [n][H][W], rgb u8 [n][H][W][3] (H*W <= 8192); focal_scaling = (1 / tan(fovy/2)) * H / 2;
+ * min_bound / max_bound f64[3] host (NULL = no bound); norm_type 0 gaussian ((x - a) / b) or
+ * 1 limits (b * (x - a) + c), a/b/c f64[6] host; out f32 [n][K][6] normalised (x, y, z, r, g, b),
+ * raw f64 [n][K][6] optional (before normalisation), count i32 [n] = points after the crop.
+ * ------------------------------------------------------------------------------------------- */
+int rmbx_pointcloud_fps(const float* depth, const uint8_t* rgb, int n_env, int H, int W,
+                        double focal_scaling, const double* min_bound, const double* max_bound,
+                        int K, int norm_type, const double* norm_a, const double* norm_b,
+                        const double* norm_c, float* out, double* raw, int32_t* count,
+                        void* stream);
 
 #ifdef __cplusplus
 }

@@ -49,6 +49,8 @@ SIGNATURES = {
     "rmbx_ddim_step": (_c_int, [_c_p] * 3 + [_c_sz, _c_p, _c_int, _c_p]),
     "rmbx_resize_crop_u8": (_c_int, [_c_p] + [_c_int] * 10 + [ctypes.c_float, ctypes.c_float, _c_p, _c_int, _c_p]),
     "rmbx_resize_f32": (_c_int, [_c_p, _c_p] + [_c_int] * 5 + [_c_p]),
+    "rmbx_pointcloud_fps": (_c_int, [_c_p, _c_p, _c_int, _c_int, _c_int, _c_d, _c_p, _c_p, _c_int, _c_int,
+                                     _c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_p]),
 }
 
 

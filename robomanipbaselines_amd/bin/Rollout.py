@@ -11,7 +11,7 @@ import sys
 
 import yaml
 
-POLICIES = ["Mlp", "Act", "DiffusionPolicy"]
+POLICIES = ["Mlp", "Act", "DiffusionPolicy", "DiffusionPolicy3d"]
 ENVS = ["MujocoUR5eCable"]
 
 

@@ -59,8 +59,8 @@ struct ImgArgs {
   int rh, rw;          // resized size
   int y0, x0, ch, cw;  // crop window in resized coordinates
   float a, b;          // out = (v * (1/255)) * a + b
-  void* dst;           // [n][C][ch][cw]
-  int dst_dtype;       // 0 f32, 1 bf16
+  void* dst;           // [n][C][ch][cw] (f32 / bf16) or [n][ch][cw][C] (u8)
+  int dst_dtype;       // 0 f32, 1 bf16, 2 u8 (resized pixels, HWC, no scaling)
   int n_env;
 };
 
@@ -89,6 +89,10 @@ __global__ void __launch_bounds__(256) resize_crop_u8_kernel(ImgArgs g) {
         const int h1 = r1[cx.s0 * g.C + c] * cx.c0 + r1[cx.s1 * g.C + c] * cx.c1;
         v = (h0 * cy.c0 + h1 * cy.c1 + (1 << 21)) >> 22;
         v = v < 0 ? 0 : (v > 255 ? 255 : v);
+      }
+      if (g.dst_dtype == 2) {
+        reinterpret_cast<uint8_t*>(g.dst)[(((size_t)e * g.ch + (y - g.y0)) * g.cw + (x - g.x0)) * g.C + c] = (uint8_t)v;
+        continue;
       }
       const float f = ((float)v * inv255) * g.a + g.b;
       const size_t o = (((size_t)e * g.C + c) * g.ch + (y - g.y0)) * g.cw + (x - g.x0);
@@ -143,7 +147,7 @@ extern "C" int rmbx_resize_crop_u8(const uint8_t* src, int n_env, int H, int W, 
   RMBX_CHECK_ARG(H > 0 && W > 0 && C > 0 && C <= 4 && rh > 0 && rw > 0, "rmbx_resize_crop_u8: bad sizes");
   RMBX_CHECK_ARG(y0 >= 0 && x0 >= 0 && ch > 0 && cw > 0 && y0 + ch <= rh && x0 + cw <= rw,
                  "rmbx_resize_crop_u8: crop (%d,%d,%d,%d) outside %dx%d", y0, x0, ch, cw, rh, rw);
-  RMBX_CHECK_ARG(dst_dtype == 0 || dst_dtype == 1, "rmbx_resize_crop_u8: dst_dtype must be 0 or 1");
+  RMBX_CHECK_ARG(dst_dtype >= 0 && dst_dtype <= 2, "rmbx_resize_crop_u8: dst_dtype must be 0, 1 or 2");
   if (n_env == 0) return RMBX_OK;
   rmbx::ImgArgs g{src, H, W, C, rh, rw, y0, x0, ch, cw, a, b, dst, dst_dtype, n_env};
   hipLaunchKernelGGL(rmbx::resize_crop_u8_kernel, dim3(rmbx::grid_for((size_t)n_env * ch * cw)), dim3(256), 0,

@@ -264,13 +264,17 @@ def resize_crop_u8(src, size, crop=None, a=1.0, b=0.0, dtype=torch.float32, out=
     n, H, W, C = src.shape
     rw, rh = int(size[0]), int(size[1])
     y0, x0, ch, cw = crop if crop is not None else (0, 0, rh, rw)
-    if dtype not in _NN_DTYPES:
-        raise ValueError("dtype must be f32 or bf16")
+    if dtype == torch.uint8:  # the resized frame itself, [n, ch, cw, C]
+        shape, code = (n, ch, cw, C), 2
+    elif dtype in _NN_DTYPES:
+        shape, code = (n, C, ch, cw), _NN_DTYPES[dtype]
+    else:
+        raise ValueError("dtype must be f32, bf16 or u8")
     if out is None:
-        out = torch.empty((n, C, ch, cw), dtype=dtype, device=src.device)
-    _chk(out, dtype, (n, C, ch, cw), "out")
+        out = torch.empty(shape, dtype=dtype, device=src.device)
+    _chk(out, dtype, shape, "out")
     N.call("rmbx_resize_crop_u8", N.ptr(src), n, H, W, C, rh, rw, y0, x0, ch, cw, float(a), float(b), N.ptr(out),
-           _NN_DTYPES[dtype], N.stream_ptr())
+           code, N.stream_ptr())
     return out
 
 
@@ -284,3 +288,42 @@ def resize_f32(src, size, out=None):
     _chk(out, torch.float32, (n, rh, rw), "out")
     N.call("rmbx_resize_f32", N.ptr(src), N.ptr(out), n, H, W, rh, rw, N.stream_ptr())
     return out
+
+
+# ------------------------------------------------------------------------------------------
+# Point-cloud observation (3D diffusion policy)
+# ------------------------------------------------------------------------------------------
+def focal_scaling(fovy_deg, height):
+    """convert_depth_image_to_pointcloud's focal scaling (VisionUtils.py:59), NumPy f64."""
+    return float((1.0 / np.tan(np.deg2rad(fovy_deg) / 2.0)) * height / 2.0)
+
+
+def pointcloud_norm_coeffs(stats):
+    """(norm_type, a, b, c) of normalize_data (DataUtils.py:9-24) for the 6-channel cloud."""
+    t = stats["norm_config"]["type"] if "norm_config" in stats else "gaussian"
+    if t == "gaussian":
+        return 0, np.asarray(stats["mean"], np.float64), np.asarray(stats["std"], np.float64), None
+    cfg = stats["norm_config"]
+    scale = (cfg["out_max"] - cfg["out_min"]) / np.asarray(stats["range"], np.float64)
+    return 1, np.asarray(stats["min"], np.float64), scale, np.full(6, float(cfg["out_min"]))
+
+
+def pointcloud_fps(depth, rgb, fovy_deg, num_points, stats, min_bound=None, max_bound=None, raw=False):
+    """depth f32 [n, H, W] + rgb u8 [n, H, W, 3] -> (normalised f32 [n, K, 6], count i32 [n],
+    raw f64 [n, K, 6] or None) via rmbx_pointcloud_fps."""
+    _chk(depth, torch.float32, name="depth")
+    n, H, W = depth.shape
+    _chk(rgb, torch.uint8, (n, H, W, 3), "rgb")
+    nt, a, b, c = pointcloud_norm_coeffs(stats)
+    a = np.ascontiguousarray(a, np.float64)
+    b = np.ascontiguousarray(b, np.float64)
+    c = None if c is None else np.ascontiguousarray(c, np.float64)
+    lo = None if min_bound is None else np.ascontiguousarray(min_bound, np.float64)
+    hi = None if max_bound is None else np.ascontiguousarray(max_bound, np.float64)
+    out = torch.empty((n, num_points, 6), dtype=torch.float32, device=depth.device)
+    r = torch.empty((n, num_points, 6), dtype=torch.float64, device=depth.device) if raw else None
+    cnt = torch.empty(n, dtype=torch.int32, device=depth.device)
+    N.call("rmbx_pointcloud_fps", N.ptr(depth), N.ptr(rgb), n, H, W, focal_scaling(fovy_deg, H), N.ptr(lo),
+           N.ptr(hi), int(num_points), nt, N.ptr(a), N.ptr(b), N.ptr(c), N.ptr(out), N.ptr(r), N.ptr(cnt),
+           N.stream_ptr())
+    return out, cnt, r

@@ -37,3 +37,13 @@ def test_resize_f32(size):
     got = K.resize_f32(torch.from_numpy(src).to(DEV), size).cpu().numpy()
     want = np.stack([OI.resize_f32(s, size) for s in src])
     assert np.array_equal(got, want)
+
+
+def test_resize_u8_frame():
+    from robomanipbaselines_amd import kernels as K
+
+    rng = np.random.default_rng(2)
+    src = rng.integers(0, 256, (2, 480, 640, 3), dtype=np.uint8)
+    got = K.resize_crop_u8(torch.from_numpy(src).to(DEV), (84, 84), dtype=torch.uint8).cpu().numpy()
+    want = np.stack([OI.resize_u8(s, (84, 84)) for s in src])
+    assert np.array_equal(got, want)
