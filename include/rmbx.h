@@ -228,6 +228,11 @@ int rmbx_render(const rmbx_camera* cam, const int32_t* prim_i32, const float* pr
  * ------------------------------------------------------------------------------------------- */
 int rmbx_nhwc_bias_act(const void* x, const float* bias, const void* res, const float* res_bias,
                        void* out, size_t n_pix, int C, int relu, int dtype, void* stream);
+/* Residual add + LayerNorm over the last dim of [rows][D] rows (D <= 2048, multiple of 8 bf16 / 4
+ * f32): out = LayerNorm(rnd(x + r)) * weight + bias (f32 weight/bias), r optional (NULL); replaces
+ * the add + nn.LayerNorm pair of the ACT transformer's post-norm layers (third_party/act). */
+int rmbx_add_layernorm(const void* x, const void* r, const float* weight, const float* bias, void* out,
+                       int rows, int D, float eps, int dtype, void* stream);
 /* out [N][Ho][Wo][C] = maxpool3x3s2p1(relu(rnd(x + bias))), Ho = (H-1)/2+1, Wo = (W-1)/2+1. */
 int rmbx_nhwc_bias_relu_maxpool(const void* x, const float* bias, void* out, int N, int H, int W,
                                 int C, int dtype, void* stream);

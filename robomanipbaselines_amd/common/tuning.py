@@ -1,0 +1,33 @@
+"""GEMM solution selection for the policy networks on gfx950.
+
+PyTorch TunableOp benchmarks the hipBLASLt/rocBLAS solutions of every GEMM shape it meets and
+keeps the fastest; the table measured on MI355X for the rollout shapes is committed
+(robomanipbaselines_amd/tuning/tunableop_gfx950.csv) and loaded here, so the benchmark runs the
+measured solutions with no tuning cost.  Shapes missing from the table are tuned on first use
+(during warm-up) unless RMBX_GEMM_TUNING=0; results are written to RMBX_TUNABLEOP_OUT (default:
+the table itself) at exit.
+"""
+
+import os
+
+_TABLE = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tuning", "tunableop_gfx950.csv")
+_done = False
+
+
+def enable_gemm_tuning():
+    global _done
+    if _done:
+        return
+    import torch
+
+    if not torch.cuda.is_available():
+        return
+    import torch.cuda.tunable as tun
+
+    tun.enable(True)
+    if os.path.exists(_TABLE):
+        tun.read_file(_TABLE)
+    tun.set_filename(os.environ.get("RMBX_TUNABLEOP_OUT", _TABLE))
+    tun.tuning_enable(os.environ.get("RMBX_GEMM_TUNING", "1") == "1")
+    tun.set_max_tuning_duration(30)
+    _done = True

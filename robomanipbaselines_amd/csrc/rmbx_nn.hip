@@ -214,3 +214,124 @@ extern "C" int rmbx_nhwc_bias_relu_maxpool(const void* x, const float* bias, voi
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
 }
+
+// ---------------------------------------------------------------------------------------------
+// Residual add + LayerNorm of the ACT transformer (post-norm layers: norm(x + sublayer(x))),
+// one wavefront per token row, the row held in registers (D <= 1024): s = rnd(x + r) in the
+// storage dtype (the unfused add), mean and variance in f32 over s (two passes over registers),
+// y = rnd((s - mean) * rstd * w + b).  Replaces the add + nn.LayerNorm pair of
+// EncoderLayer/DecoderLayer (ACT transformer.py, third_party/act [absent]).
+// ---------------------------------------------------------------------------------------------
+namespace rmbx {
+namespace {
+
+template <class T, int PER>
+__global__ void __launch_bounds__(256) add_layernorm_kernel(const typename T::vec_t* __restrict__ x,
+                                                            const typename T::vec_t* __restrict__ r,
+                                                            const float* __restrict__ w, const float* __restrict__ b,
+                                                            typename T::vec_t* __restrict__ out, int rows, int D,
+                                                            float eps) {
+  constexpr int V = T::VEC;
+  const int lane = threadIdx.x & 63;
+  const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (row >= rows) return;
+  const int nvec = D / V;
+  const size_t base = (size_t)row * nvec;
+  float s[PER][V];
+  float sum = 0.f;
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int v = lane + q * 64;
+    if (v < nvec) {
+      float a[V], c[V];
+      T::unpack(x[base + v], a);
+      if (r) {
+        T::unpack(r[base + v], c);
+#pragma unroll
+        for (int k = 0; k < V; ++k) a[k] = T::round(a[k] + c[k]);
+      }
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        s[q][k] = a[k];
+        sum += a[k];
+      }
+    } else {
+#pragma unroll
+      for (int k = 0; k < V; ++k) s[q][k] = 0.f;
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) sum += __shfl_xor(sum, off);
+  const float mean = sum / (float)D;
+  float var = 0.f;
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int v = lane + q * 64;
+    if (v < nvec) {
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        const float d = s[q][k] - mean;
+        var += d * d;
+      }
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) var += __shfl_xor(var, off);
+  const float rstd = rsqrtf(var / (float)D + eps);
+#pragma unroll
+  for (int q = 0; q < PER; ++q) {
+    const int v = lane + q * 64;
+    if (v < nvec) {
+      float y[V];
+#pragma unroll
+      for (int k = 0; k < V; ++k) {
+        const int c = v * V + k;
+        y[k] = (s[q][k] - mean) * rstd * w[c] + b[c];
+      }
+      out[base + v] = T::pack(y);
+    }
+  }
+}
+
+}  // namespace
+}  // namespace rmbx
+
+extern "C" int rmbx_add_layernorm(const void* x, const void* r, const float* weight, const float* bias, void* out,
+                                  int rows, int D, float eps, int dtype, void* stream) {
+  RMBX_CHECK_ARG(x && weight && bias && out, "rmbx_add_layernorm: null pointer");
+  RMBX_CHECK_ARG(dtype == 0 || dtype == 1, "rmbx_add_layernorm: dtype must be 0 (f32) or 1 (bf16)");
+  const int vec = dtype == 1 ? 8 : 4;
+  RMBX_CHECK_ARG(D > 0 && D % vec == 0 && D <= 2048, "rmbx_add_layernorm: D=%d must be a multiple of %d, <= 2048",
+                 D, vec);
+  RMBX_CHECK_ARG(((uintptr_t)x | (uintptr_t)r | (uintptr_t)out) % 16 == 0, "rmbx_add_layernorm: unaligned");
+  if (rows <= 0) return RMBX_OK;
+  hipStream_t s = (hipStream_t)stream;
+  const int grid = (rows + 3) / 4;
+  const int nvec = D / vec;
+  if (dtype == 1) {
+    if (nvec <= 64)
+      hipLaunchKernelGGL((rmbx::add_layernorm_kernel<rmbx::BF16, 1>), dim3(grid), dim3(256), 0, s, (const uint4*)x,
+                         (const uint4*)r, weight, bias, (uint4*)out, rows, D, eps);
+    else if (nvec <= 128)
+      hipLaunchKernelGGL((rmbx::add_layernorm_kernel<rmbx::BF16, 2>), dim3(grid), dim3(256), 0, s, (const uint4*)x,
+                         (const uint4*)r, weight, bias, (uint4*)out, rows, D, eps);
+    else
+      hipLaunchKernelGGL((rmbx::add_layernorm_kernel<rmbx::BF16, 4>), dim3(grid), dim3(256), 0, s, (const uint4*)x,
+                         (const uint4*)r, weight, bias, (uint4*)out, rows, D, eps);
+  } else {
+    if (nvec <= 64)
+      hipLaunchKernelGGL((rmbx::add_layernorm_kernel<rmbx::F32, 1>), dim3(grid), dim3(256), 0, s, (const float4*)x,
+                         (const float4*)r, weight, bias, (float4*)out, rows, D, eps);
+    else if (nvec <= 128)
+      hipLaunchKernelGGL((rmbx::add_layernorm_kernel<rmbx::F32, 2>), dim3(grid), dim3(256), 0, s, (const float4*)x,
+                         (const float4*)r, weight, bias, (float4*)out, rows, D, eps);
+    else if (nvec <= 256)
+      hipLaunchKernelGGL((rmbx::add_layernorm_kernel<rmbx::F32, 4>), dim3(grid), dim3(256), 0, s, (const float4*)x,
+                         (const float4*)r, weight, bias, (float4*)out, rows, D, eps);
+    else
+      hipLaunchKernelGGL((rmbx::add_layernorm_kernel<rmbx::F32, 8>), dim3(grid), dim3(256), 0, s, (const float4*)x,
+                         (const float4*)r, weight, bias, (float4*)out, rows, D, eps);
+  }
+  RMBX_CHECK_LAUNCH();
+  return RMBX_OK;
+}

@@ -327,3 +327,20 @@ def pointcloud_fps(depth, rgb, fovy_deg, num_points, stats, min_bound=None, max_
            N.ptr(hi), int(num_points), nt, N.ptr(a), N.ptr(b), N.ptr(c), N.ptr(out), N.ptr(r), N.ptr(cnt),
            N.stream_ptr())
     return out, cnt, r
+
+
+def add_layernorm(x, r, weight, bias, eps=1e-5, out=None):
+    """LayerNorm(rnd(x + r)) over the last dim (rmbx_add_layernorm); x, r [..., D] contiguous
+    bf16/f32 device tensors (r may be None), weight/bias f32 [D]."""
+    if x.dtype not in _NN_DTYPES or not x.is_cuda or not x.is_contiguous():
+        raise ValueError("x must be a contiguous bf16/f32 device tensor")
+    D = x.shape[-1]
+    if r is not None and (r.shape != x.shape or r.dtype != x.dtype or not r.is_contiguous()):
+        raise ValueError("r must match x")
+    _chk(weight, torch.float32, (D,), "weight")
+    _chk(bias, torch.float32, (D,), "bias")
+    if out is None:
+        out = torch.empty_like(x)
+    N.call("rmbx_add_layernorm", N.ptr(x), N.ptr(r), N.ptr(weight), N.ptr(bias), N.ptr(out), x.numel() // D, D,
+           float(eps), _NN_DTYPES[x.dtype], N.stream_ptr())
+    return out

@@ -78,7 +78,34 @@ class MHA(nn.Module):
         return self.out_proj(o.transpose(1, 2).reshape(B, Lq, D))
 
 
-class EncoderLayer(nn.Module):
+class _LayerOps(nn.Module):
+    """Feed-forward and residual+LayerNorm of a post-norm layer.  With `fused` (device inference)
+    the FFN's first Linear carries its ReLU in the GEMM epilogue (hipBLASLt bias+ReLU) and each
+    residual add + LayerNorm is one rmbx_add_layernorm pass; otherwise the plain module ops."""
+
+    fused = False
+
+    def ffn(self, x):
+        if self.fused:
+            shp = x.shape
+            h = torch._addmm_activation(self.linear1.bias, x.reshape(-1, shp[-1]), self.linear1.weight.t())
+            return self.linear2(h).view(*shp[:-1], -1)
+        return self.linear2(F.relu(self.linear1(x)))
+
+    def addnorm(self, norm, x, r):
+        if self.fused:
+            from ... import kernels as K
+
+            key = (norm.weight.data_ptr(), norm.weight.dtype)
+            cache = norm.__dict__.get("_f32")
+            if cache is None or cache[0] != key:
+                cache = (key, norm.weight.detach().float().contiguous(), norm.bias.detach().float().contiguous())
+                norm.__dict__["_f32"] = cache
+            return K.add_layernorm(x.contiguous(), r.contiguous(), cache[1], cache[2], norm.eps)
+        return norm(x + r)
+
+
+class EncoderLayer(_LayerOps):
     def __init__(self, d, heads, ff):
         super().__init__()
         self.self_attn = MHA(d, heads)
@@ -87,11 +114,11 @@ class EncoderLayer(nn.Module):
 
     def forward(self, src, pos):
         q = src + pos
-        src = self.norm1(src + self.self_attn(q, q, src))
-        return self.norm2(src + self.linear2(F.relu(self.linear1(src))))
+        src = self.addnorm(self.norm1, src, self.self_attn(q, q, src))
+        return self.addnorm(self.norm2, src, self.ffn(src))
 
 
-class DecoderLayer(nn.Module):
+class DecoderLayer(_LayerOps):
     def __init__(self, d, heads, ff):
         super().__init__()
         self.self_attn = MHA(d, heads)
@@ -101,10 +128,10 @@ class DecoderLayer(nn.Module):
 
     def forward(self, tgt, memory, pos, query_pos, mem_pos=None):
         q = tgt + query_pos
-        tgt = self.norm1(tgt + self.self_attn(q, q, tgt))
+        tgt = self.addnorm(self.norm1, tgt, self.self_attn(q, q, tgt))
         mk = memory + pos if mem_pos is None else mem_pos
-        tgt = self.norm2(tgt + self.multihead_attn(tgt + query_pos, mk, memory))
-        return self.norm3(tgt + self.linear2(F.relu(self.linear1(tgt))))
+        tgt = self.addnorm(self.norm2, tgt, self.multihead_attn(tgt + query_pos, mk, memory))
+        return self.addnorm(self.norm3, tgt, self.ffn(tgt))
 
 
 class ActModel(nn.Module):
@@ -132,6 +159,12 @@ class ActModel(nn.Module):
 
     def fuse_backbone(self):
         self._fused = FusedResNet18Trunk(self.backbone)
+        return self
+
+    def fuse_transformer(self, on=True):
+        """Device inference form of the transformer layers (see _LayerOps)."""
+        for layer in list(self.encoder_layers) + list(self.decoder_layers):
+            layer.fused = on
         return self
 
     def _pos(self, h, w, device, dtype):

@@ -46,6 +46,11 @@ class RolloutAct(BatchedRolloutBase):
         self.policy.fuse_backbone()
         self.policy = self.policy.to(device=self.device, dtype=self.policy_dtype).requires_grad_(False)
         self.policy._fused = self.policy._fused.to(memory_format=torch.channels_last)
+        if self.device.type == "cuda":
+            from ...common.tuning import enable_gemm_tuning
+
+            self.policy.fuse_transformer()
+            enable_gemm_tuning()
 
     def reset_variables(self):
         self.ens = K.ActEnsembleState(self.n, self.chunk_size, self.action_dim, self.model_meta_info["action"],

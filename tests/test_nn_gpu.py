@@ -133,3 +133,39 @@ def test_fused_trunk_bf16_close_to_fp32_reference():
     got = fused(_cl(x.to(DEV).to(torch.bfloat16))).float().cpu()
     rel = (got - want).norm() / want.norm()
     assert rel < 3e-2, rel.item()
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_add_layernorm(dtype):
+    from robomanipbaselines_amd import kernels as K
+
+    g = torch.Generator(device=DEV).manual_seed(4)
+    x = (torch.randn(301, 512, device=DEV, generator=g) * 3).to(dtype)
+    r = torch.randn(301, 512, device=DEV, generator=g).to(dtype)
+    w = torch.randn(512, device=DEV, generator=g).to(dtype)
+    b = torch.randn(512, device=DEV, generator=g).to(dtype)
+    s = (x + r).float()  # the rounded sum, as the unfused add produces it
+    want = F.layer_norm(s, (512,), w.float(), b.float(), 1e-5)
+    got = K.add_layernorm(x, r, w.float(), b.float(), 1e-5).float()
+    tol = 1e-5 if dtype == torch.float32 else 2 ** -7  # one bf16 ulp of the output
+    assert ((got - want).abs() <= tol * (1 + want.abs())).all()
+
+
+@torch.no_grad()
+def test_act_device_inference_form_matches_fp32_reference():
+    from robomanipbaselines_amd.policy.act.act_model import ActModel
+
+    torch.manual_seed(0)
+    ref = ActModel(enc_layers=2, dec_layers=2).eval().requires_grad_(False)
+    dev = ActModel(enc_layers=2, dec_layers=2).eval().requires_grad_(False)
+    dev.load_state_dict(ref.state_dict())
+    dev.fuse_backbone()
+    dev = dev.to(DEV)
+    dev._fused = dev._fused.to(memory_format=torch.channels_last)
+    dev.fuse_transformer()
+    q = torch.randn(2, 7)
+    img = torch.rand(2, 1, 3, 96, 128)
+    want = ref(q, img)
+    got = dev(q.to(DEV), img.to(DEV)).cpu()
+    assert got.shape == (2, 100, 7)
+    assert (got - want).abs().max().item() <= 2e-3 * max(1.0, want.abs().max().item())
