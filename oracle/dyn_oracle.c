@@ -782,6 +782,12 @@ static int col_capsule_box(const double* ca, const double* Ra, const double* sa,
 }
 
 /* box (A) vs box (B): SAT axis of least penetration + vertex-in-box manifold (<= 4) */
+/* candidate order of the multi-point contact routines: depth quantised to 1 nm (ties keep
+ * generation order, so face-face configurations do not flip under last-bit geometry changes) */
+static int contact_deeper(const Contact* a, const Contact* b) {
+  return floor(a->dist * 1e9) < floor(b->dist * 1e9);
+}
+
 static int col_box_box(const double* ca, const double* Ra, const double* ha, const double* cb,
                        const double* Rb, const double* hb, double margin, Contact* out) {
   double axes[15][3];
@@ -911,7 +917,7 @@ static int col_box_box(const double* ca, const double* Ra, const double* ha, con
   /* keep the 4 deepest */
   for (int i = 0; i < nc; i++)
     for (int j = i + 1; j < nc; j++)
-      if (cand[j].dist < cand[i].dist) {
+      if (contact_deeper(&cand[j], &cand[i])) {
         Contact t = cand[i];
         cand[i] = cand[j];
         cand[j] = t;
@@ -958,7 +964,7 @@ static int col_plane(const double* cp, const double* Rp, int tb, const double* c
   }
   for (int i = 0; i < nc; i++)
     for (int j = i + 1; j < nc; j++)
-      if (cand[j].dist < cand[i].dist) {
+      if (contact_deeper(&cand[j], &cand[i])) {
         Contact t = cand[i];
         cand[i] = cand[j];
         cand[j] = t;

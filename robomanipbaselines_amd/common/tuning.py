@@ -4,8 +4,8 @@ PyTorch TunableOp benchmarks the hipBLASLt/rocBLAS solutions of every GEMM shape
 keeps the fastest; the table measured on MI355X for the rollout shapes is committed
 (robomanipbaselines_amd/tuning/tunableop_gfx950.csv) and loaded here, so the benchmark runs the
 measured solutions with no tuning cost.  Shapes missing from the table are tuned on first use
-(during warm-up) unless RMBX_GEMM_TUNING=0; results are written to RMBX_TUNABLEOP_OUT (default:
-the table itself) at exit.
+(during warm-up) unless RMBX_GEMM_TUNING=0; newly tuned entries are written to RMBX_TUNABLEOP_OUT (default:
+a file in the temp dir) at exit, to be merged into the table.
 """
 
 import os
@@ -27,7 +27,9 @@ def enable_gemm_tuning():
     tun.enable(True)
     if os.path.exists(_TABLE):
         tun.read_file(_TABLE)
-    tun.set_filename(os.environ.get("RMBX_TUNABLEOP_OUT", _TABLE))
+    import tempfile
+
+    tun.set_filename(os.environ.get("RMBX_TUNABLEOP_OUT", os.path.join(tempfile.gettempdir(), "rmbx_tunableop_new.csv")))
     tun.tuning_enable(os.environ.get("RMBX_GEMM_TUNING", "1") == "1")
     tun.set_max_tuning_duration(30)
     _done = True

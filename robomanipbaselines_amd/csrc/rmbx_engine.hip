@@ -49,6 +49,7 @@ struct rmbx_engine_impl;
 struct rmbx_engine {
   rmbx_model host;       // copy of scalars (pointers unused)
   rmbx_model dev;        // device pointers
+  const int32_t* subtree_end;  // device [nbody]: DFS subtree ranges for the tree passes
   std::vector<void*> allocations;
   rmbx::Layout L;
   int n_env;
@@ -84,9 +85,74 @@ struct Env {
 __device__ __forceinline__ void sync() { __syncthreads(); }
 
 // ------------------------------------------------------------------------------------------
-// kinematics (mj_kinematics): lane 0 walks the tree; lanes split geoms / sites
+// Tree passes, lane = body (nbody <= 64).  Bodies are in DFS preorder, so a subtree is the id
+// range [b, subtree_end[b]).  Root-to-leaf accumulations (frames, velocities, accelerations) are
+// parallel prefix passes by pointer jumping (log2(depth) rounds instead of a depth-long serial
+// chain); leaf-to-root accumulations are per-lane sums over the subtree range.  Every thread of
+// the block calls these (barriers are block-wide); lanes >= nbody idle.
 // ------------------------------------------------------------------------------------------
-__device__ void kinematics(Env& e, int lane) {
+__device__ __forceinline__ void anc_init(const rmbx_model& m, int* s_anc, int lane) {
+  if (lane < m.nbody) s_anc[lane] = lane == 0 ? -1 : m.body_parent[lane];
+  sync();
+}
+
+// X[6b..] <- sum of the increments X over the path world .. b (6-vectors in LDS)
+__device__ void tree_prefix6(const rmbx_model& m, double* X, int* s_anc, int lane) {
+  anc_init(m, s_anc, lane);
+  const int b = lane;
+  while (true) {
+    const int a = b < m.nbody ? s_anc[b] : -1;
+    const bool act = a >= 0;
+    if (!__syncthreads_or(act)) break;
+    double v[6];
+    int an = -1;
+    if (act) {
+      for (int i = 0; i < 6; i++) v[i] = X[6 * a + i] + X[6 * b + i];
+      an = s_anc[a];
+    }
+    sync();
+    if (act) {
+      for (int i = 0; i < 6; i++) X[6 * b + i] = v[i];
+      s_anc[b] = an;
+    }
+    sync();
+  }
+}
+
+// frames (P, Q) relative to the ancestor in s_anc -> world frames: T_b <- T_a o T_b
+__device__ void tree_compose(const rmbx_model& m, double* P, double* Q, int* s_anc, int lane) {
+  anc_init(m, s_anc, lane);
+  const int b = lane;
+  while (true) {
+    const int a = b < m.nbody ? s_anc[b] : -1;
+    const bool act = a >= 0;
+    if (!__syncthreads_or(act)) break;
+    double q[4], p[3];
+    int an = -1;
+    if (act) {
+      double R[9], t[3];
+      quatmul(Q + 4 * a, Q + 4 * b, q);
+      quat2mat(Q + 4 * a, R);
+      matvec3(R, P + 3 * b, t);
+      for (int i = 0; i < 3; i++) p[i] = P[3 * a + i] + t[i];
+      an = s_anc[a];
+    }
+    sync();
+    if (act) {
+      for (int i = 0; i < 4; i++) Q[4 * b + i] = q[i];
+      for (int i = 0; i < 3; i++) P[3 * b + i] = p[i];
+      s_anc[b] = an;
+    }
+    sync();
+  }
+}
+
+// ------------------------------------------------------------------------------------------
+// kinematics (mj_kinematics): each lane builds its body's frame in the parent frame (body offset
+// and its joints, the hinge sin/cos included), one prefix pass composes the world frames, then
+// joint anchors/axes, inertial frames, geoms and sites in parallel
+// ------------------------------------------------------------------------------------------
+__device__ void kinematics(Env& e, int lane, int* s_anc) {
   const rmbx_model& m = *e.m;
   const int nb = m.nbody;
   double* sx = e.sh;            // xpos  [3 nb]
@@ -95,44 +161,32 @@ __device__ void kinematics(Env& e, int lane) {
   double* xipos = W(xipos);
   double* xanchor = W(xanchor);
   double* xaxis = W(xaxis);
-  if (lane == 0) {
-    sx[0] = sx[1] = sx[2] = 0;
-    sq[0] = 1;
-    sq[1] = sq[2] = sq[3] = 0;
-    quat2mat(sq, sm);
-    for (int b = 1; b < nb; b++) {
-      const int p = m.body_parent[b];
+  const int b = lane;
+  bool free_body = false;
+  if (b < nb) {
+    double P[3] = {0, 0, 0}, Q[4] = {1, 0, 0, 0};
+    if (b > 0) {
       const int ja = m.body_jntadr[b], jn = m.body_jntnum[b];
-      double* xp = sx + 3 * b;
-      double xq[4];
       if (jn > 0 && m.jnt_type[ja] == RMBX_JNT_FREE) {
+        free_body = true;  // child of the world: local frame = world frame
         const int a = m.jnt_qposadr[ja];
-        xp[0] = e.qpos[a];
-        xp[1] = e.qpos[a + 1];
-        xp[2] = e.qpos[a + 2];
-        xq[0] = e.qpos[a + 3];
-        xq[1] = e.qpos[a + 4];
-        xq[2] = e.qpos[a + 5];
-        xq[3] = e.qpos[a + 6];
-        quatnorm(xq);
-        xanchor[3 * ja] = xp[0];
-        xanchor[3 * ja + 1] = xp[1];
-        xanchor[3 * ja + 2] = xp[2];
+        for (int i = 0; i < 3; i++) P[i] = e.qpos[a + i];
+        for (int i = 0; i < 4; i++) Q[i] = e.qpos[a + 3 + i];
+        quatnorm(Q);
+        for (int i = 0; i < 3; i++) xanchor[3 * ja + i] = P[i];
         xaxis[3 * ja] = 0;
         xaxis[3 * ja + 1] = 0;
         xaxis[3 * ja + 2] = 1;
       } else {
-        double t[3];
-        matvec3(sm + 9 * p, e.body_pos + 3 * b, t);
-        for (int i = 0; i < 3; i++) xp[i] = sx[3 * p + i] + t[i];
-        quatmul(sq + 4 * p, m.body_quat + 4 * b, xq);
+        for (int i = 0; i < 3; i++) P[i] = e.body_pos[3 * b + i];
+        for (int i = 0; i < 4; i++) Q[i] = m.body_quat[4 * b + i];
         for (int j = ja; j < ja + jn; j++) {
-          double R[9], anc[3], ax[3];
-          quat2mat(xq, R);
+          double R[9], t[3], anc[3], ax[3];
+          quat2mat(Q, R);
           matvec3(R, m.jnt_pos + 3 * j, t);
-          for (int i = 0; i < 3; i++) anc[i] = xp[i] + t[i];
+          for (int i = 0; i < 3; i++) anc[i] = P[i] + t[i];
           matvec3(R, m.jnt_axis + 3 * j, ax);
-          for (int i = 0; i < 3; i++) {
+          for (int i = 0; i < 3; i++) {  // parent-frame anchor/axis; made world below
             xanchor[3 * j + i] = anc[i];
             xaxis[3 * j + i] = ax[i];
           }
@@ -141,22 +195,40 @@ __device__ void kinematics(Env& e, int lane) {
           if (m.jnt_type[j] == RMBX_JNT_HINGE) {
             double qr[4];
             axisangle_quat(m.jnt_axis + 3 * j, qd, qr);
-            quatmul(xq, qr, xq);
-            quatnorm(xq);
-            quat2mat(xq, R);
+            quatmul(Q, qr, Q);
+            quatnorm(Q);
+            quat2mat(Q, R);
             matvec3(R, m.jnt_pos + 3 * j, t);
-            for (int i = 0; i < 3; i++) xp[i] = anc[i] - t[i];
+            for (int i = 0; i < 3; i++) P[i] = anc[i] - t[i];
           } else if (m.jnt_type[j] == RMBX_JNT_SLIDE) {
-            for (int i = 0; i < 3; i++) xp[i] += ax[i] * qd;
+            for (int i = 0; i < 3; i++) P[i] += ax[i] * qd;
           }
         }
       }
-      for (int i = 0; i < 4; i++) sq[4 * b + i] = xq[i];
-      quat2mat(xq, sm + 9 * b);
-      double t[3];
-      matvec3(sm + 9 * b, m.body_ipos + 3 * b, t);
-      for (int i = 0; i < 3; i++) xipos[3 * b + i] = xp[i] + t[i];
     }
+    for (int i = 0; i < 3; i++) sx[3 * b + i] = P[i];
+    for (int i = 0; i < 4; i++) sq[4 * b + i] = Q[i];
+  }
+  sync();
+  tree_compose(m, sx, sq, s_anc, lane);
+  if (b < nb) quat2mat(sq + 4 * b, sm + 9 * b);
+  sync();
+  if (b > 0 && b < nb) {
+    const int p = m.body_parent[b];
+    if (!free_body) {
+      for (int j = m.body_jntadr[b]; j < m.body_jntadr[b] + m.body_jntnum[b]; j++) {
+        double t[3], ax[3];
+        matvec3(sm + 9 * p, xanchor + 3 * j, t);
+        matvec3(sm + 9 * p, xaxis + 3 * j, ax);
+        for (int i = 0; i < 3; i++) {
+          xanchor[3 * j + i] = sx[3 * p + i] + t[i];
+          xaxis[3 * j + i] = ax[i];
+        }
+      }
+    }
+    double t[3];
+    matvec3(sm + 9 * b, m.body_ipos + 3 * b, t);
+    for (int i = 0; i < 3; i++) xipos[3 * b + i] = sx[3 * b + i] + t[i];
   }
   sync();
   for (int k = lane; k < 3 * nb; k += 64) e.xpos[k] = sx[k];
@@ -188,13 +260,20 @@ __device__ void kinematics(Env& e, int lane) {
 // ------------------------------------------------------------------------------------------
 // mj_comPos + mj_crb
 // ------------------------------------------------------------------------------------------
-__device__ void com_pos_crb(Env& e, int lane) {
+// front-kernel LDS map (doubles): xpos 3nb | xquat 4nb | xmat 9nb | cvel 6nb | cacc 6nb |
+// cfrc 6nb | cdofdot 6nv | cinert 10nb | cdof 6nv | crb 10nb
+__host__ __device__ __forceinline__ size_t front_lds_doubles(int nb, int nv) { return 54 * (size_t)nb + 12 * (size_t)nv; }
+#define LDS_CINERT(e) ((e).sh + 34 * (e).m->nbody + 6 * (e).m->nv)
+#define LDS_CDOF(e) (LDS_CINERT(e) + 10 * (e).m->nbody)
+#define LDS_CRB(e) (LDS_CDOF(e) + 6 * (e).m->nv)
+
+__device__ void com_pos_crb(Env& e, int lane, const int32_t* subtree_end) {
   const rmbx_model& m = *e.m;
-  const int nv = m.nv;
-  double* cinert = W(cinert);
-  double* cdof = W(cdof);
-  double* crb = W(crb);
-  for (int b = lane; b < m.nbody; b += 64) {
+  const int nv = m.nv, nb = m.nbody;
+  double* cinert = LDS_CINERT(e);
+  double* cdof = LDS_CDOF(e);
+  double* crb = LDS_CRB(e);
+  for (int b = lane; b < nb; b += 64) {
     double* I = cinert + 10 * b;
     if (b == 0) {
       for (int k = 0; k < 10; k++) I[k] = 0;
@@ -202,7 +281,7 @@ __device__ void com_pos_crb(Env& e, int lane) {
     }
     const double mass = m.body_mass[b];
     const double* c = W(xipos) + 3 * b;
-    const double* R = W(xmat) + 9 * b;
+    const double* R = e.sh + 7 * nb + 9 * b;  // xmat (LDS)
     const double* Ib = m.body_inertia + 9 * b;
     double T[9], Iw[9], Rt[9];
     for (int i = 0; i < 3; i++)
@@ -242,8 +321,8 @@ __device__ void com_pos_crb(Env& e, int lane) {
       S[3] = 1;
       S[10] = 1;
       S[17] = 1;
-      const double* R = W(xmat) + 9 * b;
-      const double* x = e.xpos + 3 * b;
+      const double* R = e.sh + 7 * nb + 9 * b;
+      const double* x = e.sh + 3 * b;
       for (int k = 0; k < 3; k++) {
         double* Sk = S + 6 * (3 + k);
         const double a[3] = {R[k], R[3 + k], R[6 + k]};
@@ -255,48 +334,53 @@ __device__ void com_pos_crb(Env& e, int lane) {
     }
   }
   sync();
-  // composite rigid-body inertia: children have larger ids (DFS order)
-  for (int k = lane; k < 10 * m.nbody; k += 64) crb[k] = cinert[k];
-  sync();
-  if (lane < 10) {
-    for (int b = m.nbody - 1; b > 0; b--) {
-      const int p = m.body_parent[b];
-      if (p > 0) crb[10 * p + lane] += crb[10 * b + lane];
-    }
+  // composite rigid-body inertia = subtree sums (DFS ranges), copies for the solver kernel
+  for (int b = lane; b < nb; b += 64) {
+    double acc[10];
+    for (int k = 0; k < 10; k++) acc[k] = cinert[10 * b + k];
+    if (b > 0)
+      for (int d = b + 1; d < subtree_end[b]; d++)
+        for (int k = 0; k < 10; k++) acc[k] += cinert[10 * d + k];
+    for (int k = 0; k < 10; k++) crb[10 * b + k] = acc[k];
   }
+  for (int k = lane; k < 10 * nb; k += 64) W(cinert)[k] = cinert[k];
+  for (int k = lane; k < 6 * nv; k += 64) W(cdof)[k] = cdof[k];
   sync();
   double* M = W(M);
-  for (int k = lane; k < nv * nv; k += 64) M[k] = 0;
-  sync();
   for (int i = lane; i < nv; i += 64) {
     double F[6];
     inert_mul(crb + 10 * m.dof_body[i], cdof + 6 * i, F);
-    for (int j = i; j >= 0; j = m.dof_parent[j]) {
-      const double v = dot6(cdof + 6 * j, F);
-      M[i * nv + j] = v;
-      M[j * nv + i] = v;
-    }
+    for (int j = 0; j < nv; j++) M[i * nv + j] = 0;
+    for (int j = i; j >= 0; j = m.dof_parent[j]) M[i * nv + j] = dot6(cdof + 6 * j, F);
   }
   sync();
+  // symmetrise (lower triangle computed along each dof's ancestor chain) + armature
+  for (int k = lane; k < nv * nv; k += 64) {
+    const int i = k / nv, j = k % nv;
+    if (j > i) M[k] = M[j * nv + i];
+  }
   for (int i = lane; i < nv; i += 64) M[i * nv + i] += m.dof_armature[i];
   sync();
 }
 
 // ------------------------------------------------------------------------------------------
-// mj_comVel + mj_rne (bias) ; passive ; tendons ; actuation (lane 0 for tree passes)
+// mj_comVel + mj_rne (bias) ; passive ; tendons ; actuation
 // ------------------------------------------------------------------------------------------
-// RNE forward pass (lane-serial): cacc, cfrc (body arrays, usually LDS) from cvel/cdofdot
-__device__ void rne_forward(Env& e, const double* qacc, double* ca, double* cfrc,
-                            const double* cvel, const double* cdofdot) {
+// RNE forward pass, lane = body: cacc = prefix over the tree of the per-body increments
+// (world: -gravity), cfrc = I cacc + cvel x* (I cvel).  cdof/cinert/cvel/cdofdot/qacc may be
+// LDS or global; ca and cfrc are LDS [6 nb].
+__device__ void rne_forward(const Env& e, const double* qacc, double* ca, double* cfrc, const double* cvel,
+                            const double* cdofdot, const double* cdof, const double* cinert, int* s_anc,
+                            int lane) {
   const rmbx_model& m = *e.m;
-  const double* cdof = W(cdof);
-  ca[0] = ca[1] = ca[2] = 0;
-  ca[3] = -m.gravity[0];
-  ca[4] = -m.gravity[1];
-  ca[5] = -m.gravity[2];
-  for (int b = 1; b < m.nbody; b++) {
-    double a[6];
-    for (int i = 0; i < 6; i++) a[i] = ca[6 * m.body_parent[b] + i];
+  const int b = lane;
+  if (b == 0) {
+    ca[0] = ca[1] = ca[2] = 0;
+    ca[3] = -m.gravity[0];
+    ca[4] = -m.gravity[1];
+    ca[5] = -m.gravity[2];
+  } else if (b < m.nbody) {
+    double a[6] = {0, 0, 0, 0, 0, 0};
     const int da = m.body_dofadr[b], dn = m.body_dofnum[b];
     for (int k = da; k < da + dn; k++) {
       for (int i = 0; i < 6; i++) a[i] += cdofdot[6 * k + i] * e.qvel[k];
@@ -304,60 +388,79 @@ __device__ void rne_forward(Env& e, const double* qacc, double* ca, double* cfrc
         for (int i = 0; i < 6; i++) a[i] += cdof[6 * k + i] * qacc[k];
     }
     for (int i = 0; i < 6; i++) ca[6 * b + i] = a[i];
+  }
+  sync();
+  tree_prefix6(m, ca, s_anc, lane);
+  if (b > 0 && b < m.nbody) {
     double Ia[6], Iv[6], vxIv[6];
-    const double* I = W(cinert) + 10 * b;
+    const double* I = cinert + 10 * b;
     const double* v = cvel + 6 * b;
-    inert_mul(I, a, Ia);
+    inert_mul(I, ca + 6 * b, Ia);
     inert_mul(I, v, Iv);
     cross_force(v, Iv, vxIv);
     for (int i = 0; i < 6; i++) cfrc[6 * b + i] = Ia[i] + vxIv[i];
   }
+  sync();
 }
 
-__device__ void rne_backward(const rmbx_model& m, double* cfrc, int lane) {
-  if (lane < 6) {
-    for (int b = m.nbody - 1; b > 0; b--) {
-      const int p = m.body_parent[b];
-      if (p > 0) cfrc[6 * p + lane] += cfrc[6 * b + lane];
-    }
+// RNE backward pass: cfrc[b] <- sum over the subtree of b (b > 0), lane = body
+__device__ void rne_backward(const rmbx_model& m, double* cfrc, const int32_t* subtree_end, int lane) {
+  const int b = lane;
+  double acc[6];
+  const bool act = b > 0 && b < m.nbody;
+  if (act) {
+    for (int i = 0; i < 6; i++) acc[i] = cfrc[6 * b + i];
+    for (int d = b + 1; d < subtree_end[b]; d++)
+      for (int i = 0; i < 6; i++) acc[i] += cfrc[6 * d + i];
   }
+  sync();
+  if (act)
+    for (int i = 0; i < 6; i++) cfrc[6 * b + i] = acc[i];
+  sync();
 }
 
-__device__ void velocity_stage(Env& e, int lane) {
+__device__ void velocity_stage(Env& e, int lane, int* s_anc, const int32_t* subtree_end) {
   const rmbx_model& m = *e.m;
   const int nv = m.nv, nb = m.nbody;
   double* cvel = e.sh + 16 * nb;   // LDS
   double* scacc = cvel + 6 * nb;   // LDS
   double* scfrc = scacc + 6 * nb;  // LDS
   double* cdofdot = scfrc + 6 * nb;  // LDS [6 nv]
-  const double* cdof = W(cdof);
-  if (lane == 0) {
-    for (int i = 0; i < 6; i++) cvel[i] = 0;
-    for (int b = 1; b < nb; b++) {
-      double cv[6];
-      for (int i = 0; i < 6; i++) cv[i] = cvel[6 * m.body_parent[b] + i];
-      for (int j = m.body_jntadr[b]; j < m.body_jntadr[b] + m.body_jntnum[b]; j++) {
-        const int da = m.jnt_dofadr[j];
-        if (m.jnt_type[j] == RMBX_JNT_FREE) {
-          for (int k = 0; k < 3; k++)
-            for (int i = 0; i < 6; i++) cdofdot[6 * (da + k) + i] = 0;
-          for (int k = 0; k < 3; k++)
-            for (int i = 0; i < 6; i++) cv[i] += cdof[6 * (da + k) + i] * e.qvel[da + k];
-          for (int k = 3; k < 6; k++) cross_motion(cv, cdof + 6 * (da + k), cdofdot + 6 * (da + k));
-          for (int k = 3; k < 6; k++)
-            for (int i = 0; i < 6; i++) cv[i] += cdof[6 * (da + k) + i] * e.qvel[da + k];
-        } else {
-          cross_motion(cv, cdof + 6 * da, cdofdot + 6 * da);
-          for (int i = 0; i < 6; i++) cv[i] += cdof[6 * da + i] * e.qvel[da];
-        }
-      }
-      for (int i = 0; i < 6; i++) cvel[6 * b + i] = cv[i];
-    }
-    rne_forward(e, nullptr, scacc, scfrc, cvel, cdofdot);
+  const double* cdof = LDS_CDOF(e);
+  const int b = lane;
+  // body velocity increments, then the prefix over the tree
+  if (b < nb) {
+    double v[6] = {0, 0, 0, 0, 0, 0};
+    if (b > 0)
+      for (int k = m.body_dofadr[b]; k < m.body_dofadr[b] + m.body_dofnum[b]; k++)
+        for (int i = 0; i < 6; i++) v[i] += cdof[6 * k + i] * e.qvel[k];
+    for (int i = 0; i < 6; i++) cvel[6 * b + i] = v[i];
   }
   sync();
-  rne_backward(m, scfrc, lane);
+  tree_prefix6(m, cvel, s_anc, lane);
+  // cdof_dot = (velocity before the dof) x cdof, per body in joint order
+  if (b > 0 && b < nb) {
+    double cv[6];
+    for (int i = 0; i < 6; i++) cv[i] = cvel[6 * m.body_parent[b] + i];
+    for (int j = m.body_jntadr[b]; j < m.body_jntadr[b] + m.body_jntnum[b]; j++) {
+      const int da = m.jnt_dofadr[j];
+      if (m.jnt_type[j] == RMBX_JNT_FREE) {
+        for (int k = 0; k < 3; k++)
+          for (int i = 0; i < 6; i++) cdofdot[6 * (da + k) + i] = 0;
+        for (int k = 0; k < 3; k++)
+          for (int i = 0; i < 6; i++) cv[i] += cdof[6 * (da + k) + i] * e.qvel[da + k];
+        for (int k = 3; k < 6; k++) cross_motion(cv, cdof + 6 * (da + k), cdofdot + 6 * (da + k));
+        for (int k = 3; k < 6; k++)
+          for (int i = 0; i < 6; i++) cv[i] += cdof[6 * (da + k) + i] * e.qvel[da + k];
+      } else {
+        cross_motion(cv, cdof + 6 * da, cdofdot + 6 * da);
+        for (int i = 0; i < 6; i++) cv[i] += cdof[6 * da + i] * e.qvel[da];
+      }
+    }
+  }
   sync();
+  rne_forward(e, nullptr, scacc, scfrc, cvel, cdofdot, cdof, LDS_CINERT(e), s_anc, lane);
+  rne_backward(m, scfrc, subtree_end, lane);
   for (int k = lane; k < 6 * nb; k += 64) W(cvel)[k] = cvel[k];
   for (int k = lane; k < 6 * nv; k += 64) W(cdofdot)[k] = cdofdot[k];
   double* bias = W(qfrc_bias);
@@ -604,6 +707,13 @@ __device__ int col_capsule_box(const double* ca, const double* Ra, const double*
   return n;
 }
 
+// Candidate order for the multi-point contact routines: depth quantised to 1 nm, so candidates of
+// a face-face configuration (equal depth up to rounding) keep their generation order and the
+// selected points do not jump under last-bit changes of the geometry.
+__device__ __forceinline__ bool contact_deeper(const Contact* a, const Contact* b) {
+  return floor(a->dist * 1e9) < floor(b->dist * 1e9);
+}
+
 __device__ int col_box_box(const double* ca, const double* Ra, const double* ha, const double* cb,
                            const double* Rb, const double* hb, double margin, Contact* out) {
   double axes[15][3];
@@ -721,7 +831,7 @@ __device__ int col_box_box(const double* ca, const double* Ra, const double* ha,
   }
   for (int i = 0; i < nc; i++)
     for (int j = i + 1; j < nc; j++)
-      if (cand[j].dist < cand[i].dist) {
+      if (contact_deeper(&cand[j], &cand[i])) {
         const Contact t = cand[i];
         cand[i] = cand[j];
         cand[j] = t;
@@ -772,7 +882,7 @@ __device__ int col_plane(const double* cp, const double* Rp, int tb, const doubl
   }
   for (int i = 0; i < nc; i++)
     for (int j = i + 1; j < nc; j++)
-      if (cand[j].dist < cand[i].dist) {
+      if (contact_deeper(&cand[j], &cand[i])) {
         const Contact t = cand[i];
         cand[i] = cand[j];
         cand[j] = t;
@@ -926,7 +1036,7 @@ __device__ __forceinline__ int last_dof(const rmbx_model& m, int b) {
 __device__ void jac_point_dir(const Env& e, int b, const double* p, const double* dir, double sgn,
                               double* row) {
   const rmbx_model& m = *e.m;
-  const double* cdof = e.ws + e.L->cdof;
+  const double* cdof = LDS_CDOF(e);
   for (int k = last_dof(m, b); k >= 0; k = m.dof_parent[k]) {
     const double* S = cdof + 6 * k;
     double wxp[3];
@@ -1063,7 +1173,7 @@ __device__ int make_constraints(Env& e, int lane, int ncon, int* ne_out) {
           const double diag_r = m.body_invweight0[2 * o1 + 1] + m.body_invweight0[2 * o2 + 1];
           for (int i = 0; i < 3; i++) set_row(e, r + i, 0, err[3 + i], diag_r, sr, si, nrm);
           // rotational columns: chains of o2 (+) and o1 (-); dofs shared cancel
-          const double* cdof = W(cdof);
+          const double* cdof = LDS_CDOF(e);
           for (int pass = 0; pass < 2; pass++) {
             const int b = pass == 0 ? o2 : o1;
             const double sg = pass == 0 ? 1.0 : -1.0;
@@ -1155,7 +1265,7 @@ __device__ int make_constraints(Env& e, int lane, int ncon, int* ne_out) {
           }
       }
       const int nrow = min(cnt, nefc - r0);
-      const double* cdof = W(cdof);
+      const double* cdof = LDS_CDOF(e);
       for (int pass = 0; pass < 2 && nrow > 0; pass++) {
         const int b = pass == 0 ? b2 : b1;
         const double sgn = pass == 0 ? 1.0 : -1.0;
@@ -1190,45 +1300,58 @@ __device__ int make_constraints(Env& e, int lane, int ncon, int* ne_out) {
 // ------------------------------------------------------------------------------------------
 // sensors (mj_rnePostConstraint -> force/torque at sites)
 // ------------------------------------------------------------------------------------------
-__device__ void sensors(Env& e, int ncon, int lane, double* cacc, double* cfrc) {
+__device__ void sensors(Env& e, int ncon, int tid, double* cacc, double* cfrc, double* cw, int* s_anc,
+                        const int32_t* subtree_end) {
   const rmbx_model& m = *e.m;
   if (m.nsensor == 0) return;
-  if (lane == 0) {
-    rne_forward(e, W(qacc), cacc, cfrc, W(cvel), W(cdofdot));
-    for (int c = 0; c < ncon; c++) {
-      const int r0 = WI(con_efcadr)[c];
-      if (r0 + (WI(con_condim)[c] == 1 ? 1 : 4) > e.L->nefc_max) continue;
-      const double* F = W(con_frame) + 9 * c;
-      double fn, f1 = 0, f2 = 0;
-      const double* f = W(efc_force) + r0;
-      if (WI(con_condim)[c] == 1) {
-        fn = f[0];
-      } else {
-        const double mu = W(con_mu)[c];
-        fn = f[0] + f[1] + f[2] + f[3];
-        f1 = mu * (f[0] - f[1]);
-        f2 = mu * (f[2] - f[3]);
-      }
-      double Fw[3], pxF[3];
-      for (int i = 0; i < 3; i++) Fw[i] = fn * F[i] + f1 * F[3 + i] + f2 * F[6 + i];
-      cross3(W(con_pos) + 3 * c, Fw, pxF);
-      const int b2 = WI(con_b2)[c], b1 = WI(con_b1)[c];
-      for (int i = 0; i < 3; i++) {
-        cfrc[6 * b2 + i] -= pxF[i];
-        cfrc[6 * b2 + 3 + i] -= Fw[i];
-        cfrc[6 * b1 + i] += pxF[i];
-        cfrc[6 * b1 + 3 + i] += Fw[i];
-      }
+  const int nb = m.nbody;
+  rne_forward(e, W(qacc), cacc, cfrc, W(cvel), W(cdofdot), W(cdof), W(cinert), s_anc, tid);
+  // contact wrenches about the origin, lanes over contacts: cw[c] = (p x F, F)
+  for (int c = tid; c < ncon; c += blockDim.x) {
+    double* o = cw + 6 * c;
+    const int r0 = WI(con_efcadr)[c];
+    if (r0 + (WI(con_condim)[c] == 1 ? 1 : 4) > e.L->nefc_max) {
+      for (int i = 0; i < 6; i++) o[i] = 0;
+      continue;
     }
+    const double* F = W(con_frame) + 9 * c;
+    double fn, f1 = 0, f2 = 0;
+    const double* f = W(efc_force) + r0;
+    if (WI(con_condim)[c] == 1) {
+      fn = f[0];
+    } else {
+      const double mu = W(con_mu)[c];
+      fn = f[0] + f[1] + f[2] + f[3];
+      f1 = mu * (f[0] - f[1]);
+      f2 = mu * (f[2] - f[3]);
+    }
+    double Fw[3];
+    for (int i = 0; i < 3; i++) Fw[i] = fn * F[i] + f1 * F[3 + i] + f2 * F[6 + i];
+    cross3(W(con_pos) + 3 * c, Fw, o);
+    for (int i = 0; i < 3; i++) o[3 + i] = Fw[i];
   }
   sync();
-  rne_backward(m, cfrc, lane);
+  // per body, in contact order (body 2 receives -w, body 1 +w)
+  if (tid > 0 && tid < nb) {
+    double acc[6];
+    for (int i = 0; i < 6; i++) acc[i] = cfrc[6 * tid + i];
+    for (int c = 0; c < ncon; c++) {
+      if (WI(con_b2)[c] == tid)
+        for (int i = 0; i < 6; i++) acc[i] -= cw[6 * c + i];
+      if (WI(con_b1)[c] == tid)
+        for (int i = 0; i < 6; i++) acc[i] += cw[6 * c + i];
+    }
+    for (int i = 0; i < 6; i++) cfrc[6 * tid + i] = acc[i];
+  }
   sync();
-  if (lane < m.nsensor && lane < 2) {
-    const int s = lane;
+  if (tid < m.nsensor && tid < 2) {
+    const int s = tid;
     const int site = m.sensor_site[s];
     const int b = m.site_body[site];
-    const double* f = cfrc + 6 * b;
+    double f[6];
+    for (int i = 0; i < 6; i++) f[i] = cfrc[6 * b + i];
+    for (int d = b + 1; d < subtree_end[b]; d++)  // interaction force = subtree sum
+      for (int i = 0; i < 6; i++) f[i] += cfrc[6 * d + i];
     const double* p = W(sxpos) + 3 * site;
     const double* R = W(sxmat) + 9 * site;
     double out[3];
@@ -1277,6 +1400,7 @@ struct SolverShared {
   double bfrc[6 * MAX_BODY];  // sensors: body forces
   double red[8];
   int ired[8];
+  int anc[MAX_BODY];          // tree-pass ancestor pointers
 };
 
 __device__ __forceinline__ void blk_coords(int t, int* bi, int* bj) {
@@ -1730,6 +1854,7 @@ struct KArgs {
   int nsub;
   int integrate_flag;
   unsigned long long* prof;  // optional [n_env][16] per-stage cycle sums (diagnostic)
+  const int32_t* subtree_end;  // [nbody] end of each body's DFS subtree id range
 };
 
 __device__ __forceinline__ unsigned long long stamp() { return __builtin_readcyclecounter(); }
@@ -1777,13 +1902,14 @@ __global__ void __launch_bounds__(64) front_kernel(KArgs args) {
   Env e;
   make_env(args, env, e);
   e.sh = front_smem;
+  __shared__ int s_anc[MAX_BODY];
   PROF_BEGIN()
-  kinematics(e, lane);
+  kinematics(e, lane, s_anc);
   sync();
   PROF(0)
-  com_pos_crb(e, lane);
+  com_pos_crb(e, lane, args.subtree_end);
   PROF(1)
-  velocity_stage(e, lane);
+  velocity_stage(e, lane, s_anc, args.subtree_end);
   PROF(2)
   const int ncon = collision(e, lane);
   sync();
@@ -1818,7 +1944,7 @@ __global__ void __launch_bounds__(SOLVER_THREADS) solver_kernel(KArgs args) {
   const int ncon = WI(scal)[0], nefc = WI(scal)[1], ne = WI(scal)[2];
   const int iters = solver_newton(e, S, a, bi, bj, own, nefc, ne, tid);
   PROF(5)
-  sensors(e, ncon, tid, S.bacc, S.bfrc);
+  sensors(e, ncon, tid, S.bacc, S.bfrc, &S.jc[0][0], S.anc, args.subtree_end);
   PROF(6)
   if (tid == 0) e.stats[2] = iters;
   if (args.integrate_flag) solver_integrate(e, S, a, bi, bj, own, tid);
@@ -1927,8 +2053,20 @@ int rmbx_engine_create(const struct rmbx_model* model, int n_env, rmbx_engine** 
   const rmbx_model& h = *model;
   RMBX_CHECK_ARG(h.nv > 0 && h.nv <= MAX_NVP, "nv=%d outside the supported range [1, %d]", h.nv, MAX_NVP);
   RMBX_CHECK_ARG(h.nbody > 0 && h.nbody <= MAX_BODY, "nbody=%d outside [1, %d]", h.nbody, MAX_BODY);
-  RMBX_CHECK_ARG(h.max_contacts > 0 && h.max_contacts <= 1024, "bad max_contacts=%d",
+  RMBX_CHECK_ARG(h.max_contacts > 0 && h.max_contacts <= RCHUNK * MAX_NVP / 6, "bad max_contacts=%d",
                  h.max_contacts);
+  // tree passes need DFS preorder bodies (every subtree a contiguous id range); MJCF order is
+  std::vector<int32_t> subtree_end(h.nbody);
+  for (int b = h.nbody - 1; b >= 0; b--) {
+    subtree_end[b] = b + 1;
+    for (int c = b + 1; c < h.nbody; c++)
+      if (h.body_parent[c] == b) subtree_end[b] = subtree_end[b] > subtree_end[c] ? subtree_end[b] : subtree_end[c];
+  }
+  for (int b = 1; b < h.nbody; b++) {
+    RMBX_CHECK_ARG(h.body_parent[b] >= 0 && h.body_parent[b] < b, "body %d: parent must precede it", b);
+    const int p = h.body_parent[b];
+    RMBX_CHECK_ARG(b < subtree_end[p], "bodies are not in DFS preorder (body %d outside its parent's range)", b);
+  }
   rmbx_engine* eng = new rmbx_engine();
   eng->host = h;
   eng->dev = h;
@@ -1966,6 +2104,11 @@ int rmbx_engine_create(const struct rmbx_model* model, int n_env, rmbx_engine** 
   UP(sensor_type, h.nsensor) UP(sensor_site, h.nsensor)
   UP(cam_body, h.ncam) UP(cam_pos, 3 * h.ncam) UP(cam_quat, 4 * h.ncam) UP(cam_fovy, h.ncam)
 #undef UP
+  if (st != RMBX_OK) {
+    rmbx_engine_destroy(eng);
+    return st;
+  }
+  if (st == RMBX_OK) st = upload(eng, subtree_end.data(), (size_t)h.nbody, &eng->subtree_end);
   if (st != RMBX_OK) {
     rmbx_engine_destroy(eng);
     return st;
@@ -2053,10 +2196,11 @@ static int launch(rmbx_engine* eng, int nsub, int integ, const uint8_t* active, 
   a.nsub = nsub;
   a.integrate_flag = integ;
   a.prof = prof;
+  a.subtree_end = eng->subtree_end;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int reps = integ ? nsub : 1;
   for (int s = 0; s < reps; s++) {
-    const size_t front_lds = (34 * (size_t)eng->host.nbody + 6 * (size_t)eng->host.nv) * sizeof(double);
+    const size_t front_lds = front_lds_doubles(eng->host.nbody, eng->host.nv) * sizeof(double);
     hipLaunchKernelGGL(front_kernel, dim3(eng->n_env), dim3(64), front_lds, st, a);
     RMBX_CHECK_LAUNCH();
     hipLaunchKernelGGL(solver_kernel, dim3(eng->n_env), dim3(SOLVER_THREADS), 0, st, a);
