@@ -45,7 +45,7 @@ typedef struct {
   double *cdof, *cinert, *crb, *cvel, *cdofdot, *cacc, *cfrc;
   double *M, *L, *H, *A;
   double *qfrc_bias, *qfrc_passive, *qfrc_actuator, *qfrc_smooth, *qacc_smooth,
-      *qfrc_constraint, *qacc, *tmpv, *tmpv2, *grad, *search, *Ms, *res;
+      *qfrc_constraint, *qacc, *tmpv, *tmpv2, *tmpv3, *grad, *search, *Ms, *res;
   double *ten_len, *ten_vel, *act_force;
   /* contacts */
   int ncon;
@@ -53,7 +53,7 @@ typedef struct {
   int *con_b1, *con_b2, *con_condim, *con_pair, *con_efcadr;
   /* constraints */
   int nefc, ne; /* ne: equality rows come first */
-  double *J, *efc_pos, *efc_aref, *efc_D, *efc_R, *efc_force, *efc_jar, *efc_Js, *efc_vel;
+  double *J, *efc_pos, *efc_aref, *efc_D, *efc_R, *efc_force, *efc_jar, *efc_Js, *efc_vel, *efc_tmp;
   int* efc_type; /* 0 equality, 1 inequality */
   double sensordata[6];
   int solver_iter;
@@ -252,7 +252,7 @@ void* orc_create(const rmbx_model* m) {
   d->A = dalloc((size_t)nv * nv);
   double** vs[] = {&d->qfrc_bias, &d->qfrc_passive, &d->qfrc_actuator, &d->qfrc_smooth,
                    &d->qacc_smooth, &d->qfrc_constraint, &d->qacc, &d->tmpv, &d->tmpv2,
-                   &d->grad, &d->search, &d->Ms, &d->res};
+                   &d->tmpv3, &d->grad, &d->search, &d->Ms, &d->res};
   for (unsigned i = 0; i < sizeof(vs) / sizeof(vs[0]); i++) *vs[i] = dalloc(nv);
   d->ten_len = dalloc(m->ntendon);
   d->ten_vel = dalloc(m->ntendon);
@@ -276,6 +276,7 @@ void* orc_create(const rmbx_model* m) {
   d->efc_jar = dalloc(ne);
   d->efc_Js = dalloc(ne);
   d->efc_vel = dalloc(ne);
+  d->efc_tmp = dalloc(ne);
   d->efc_type = ialloc(ne);
   return d;
 }
@@ -288,11 +289,11 @@ void orc_destroy(void* p) {
                   d->xipos, d->xanchor, d->xaxis, d->gxpos, d->gxmat, d->sxpos, d->sxmat, d->cdof,
                   d->cdofdot, d->cinert, d->crb, d->cvel, d->cacc, d->cfrc, d->M, d->L, d->H, d->A,
                   d->qfrc_bias, d->qfrc_passive, d->qfrc_actuator, d->qfrc_smooth, d->qacc_smooth,
-                  d->qfrc_constraint, d->qacc, d->tmpv, d->tmpv2, d->grad, d->search, d->Ms, d->res,
+                  d->qfrc_constraint, d->qacc, d->tmpv, d->tmpv2, d->tmpv3, d->grad, d->search, d->Ms, d->res,
                   d->ten_len, d->ten_vel, d->act_force, d->con_pos, d->con_frame, d->con_dist,
                   d->con_mu, d->con_b1, d->con_b2, d->con_condim, d->con_pair, d->con_efcadr, d->J,
                   d->efc_pos, d->efc_aref, d->efc_D, d->efc_R, d->efc_force, d->efc_jar, d->efc_Js,
-                  d->efc_vel, d->efc_type};
+                  d->efc_vel, d->efc_tmp, d->efc_type};
   for (unsigned i = 0; i < sizeof(ptrs) / sizeof(ptrs[0]); i++) free(ptrs[i]);
   free(d);
 }
@@ -1342,14 +1343,31 @@ static void solve(Data* d) {
   memcpy(d->L, d->M, sizeof(double) * nv * nv);
   cholesky(d->L, nv);
   chol_solve(d->L, nv, d->qfrc_smooth, d->qacc_smooth);
-  /* warmstart: pick the lower-cost start */
+  /* warmstart: pick the lower-cost start (cost of qacc_smooth: res = 0, only the rows) */
   double c_ws = eval_cost(d, d->qacc_ws);
-  double c_sm = eval_cost(d, d->qacc_smooth);
-  if (c_ws < c_sm)
+  memcpy(d->tmpv3, d->tmpv2, sizeof(double) * nv); /* M res of the warm start */
+  memcpy(d->efc_tmp, d->efc_jar, sizeof(double) * nefc);
+  double c_sm = 0;
+  for (int r = 0; r < nefc; r++) {
+    const double* Jr = d->J + (size_t)r * nv;
+    double s = 0;
+    for (int k = 0; k < nv; k++) s += Jr[k] * d->qacc_smooth[k];
+    double jar = s - d->efc_aref[r];
+    d->efc_jar[r] = jar;
+    if (d->efc_type[r] == 0 || jar < 0) c_sm += 0.5 * d->efc_D[r] * jar * jar;
+  }
+  double cost;
+  if (c_ws < c_sm) {
     memcpy(a, d->qacc_ws, sizeof(double) * nv);
-  else
+    for (int k = 0; k < nv; k++) d->res[k] = a[k] - d->qacc_smooth[k];
+    memcpy(d->tmpv2, d->tmpv3, sizeof(double) * nv);
+    memcpy(d->efc_jar, d->efc_tmp, sizeof(double) * nefc);
+    cost = c_ws;
+  } else {
     memcpy(a, d->qacc_smooth, sizeof(double) * nv);
-  double cost = eval_cost(d, a);
+    for (int k = 0; k < nv; k++) d->res[k] = d->tmpv2[k] = 0;
+    cost = c_sm;
+  }
   double scale = 1.0 / (m->meaninertia * (nv > 1 ? nv : 1));
   int it;
   for (it = 0; it < m->solver_iterations; it++) {
@@ -1426,8 +1444,21 @@ static void solve(Data* d) {
       alpha = an;
       if (same) break;
     }
-    for (int k = 0; k < nv; k++) a[k] += alpha * d->search[k];
-    double newcost = eval_cost(d, a);
+    /* move along the search direction; res, M res and jar are updated incrementally
+       (mj_solNewton's qacc / Ma / efc_Jaref updates) */
+    for (int k = 0; k < nv; k++) {
+      a[k] += alpha * d->search[k];
+      d->res[k] += alpha * d->search[k];
+      d->tmpv2[k] += alpha * d->Ms[k];
+    }
+    double newcost = 0;
+    for (int k = 0; k < nv; k++) newcost += d->res[k] * d->tmpv2[k];
+    newcost *= 0.5;
+    for (int r = 0; r < nefc; r++) {
+      double jar = d->efc_jar[r] + alpha * d->efc_Js[r];
+      d->efc_jar[r] = jar;
+      if (d->efc_type[r] == 0 || jar < 0) newcost += 0.5 * d->efc_D[r] * jar * jar;
+    }
     double improvement = scale * (cost - newcost);
     cost = newcost;
     if (improvement < m->solver_tolerance) {

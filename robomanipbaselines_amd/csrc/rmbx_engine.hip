@@ -37,7 +37,7 @@ struct Layout {
   size_t J, efc_pos, efc_aref, efc_D, efc_R, efc_force, efc_jar, efc_Js, efc_vel, efc_tmp;
   size_t ints;  // start of the int32 region (in doubles)
   // int32 offsets relative to the int region
-  size_t con_b1, con_b2, con_condim, con_pair, con_efcadr, efc_type, scal;
+  size_t con_b1, con_b2, con_condim, con_pair, con_efcadr, efc_type, efc_act, scal;
   size_t istride;  // int32 count
   int nefc_max;
 };
@@ -83,6 +83,7 @@ struct Env {
 #define WI(name) (e.iw + e.L->name)
 
 __device__ __forceinline__ void sync() { __syncthreads(); }
+__device__ __forceinline__ unsigned long long stamp() { return __builtin_readcyclecounter(); }
 
 // ------------------------------------------------------------------------------------------
 // Tree passes, lane = body (nbody <= 64).  Bodies are in DFS preorder, so a subtree is the id
@@ -1392,6 +1393,7 @@ struct SolverShared {
   double srch[MAX_NVP];
   double Ms[MAX_NVP];
   double acc[MAX_NVP];
+  double acc2[SOLVER_THREADS];  // column-reduction partials
   double tmp[MAX_NVP];
   double jc[RCHUNK][MAX_NVP];  // scaled Jacobian chunk
   double jw[RCHUNK];           // chunk row weights sqrt(D) (active rows)
@@ -1561,25 +1563,56 @@ __device__ __forceinline__ void load_block(const double* M, int nv, int bi, int 
 }
 
 // y = M x, thread per row (M dense in global), vectors in LDS
-__device__ void mat_vec(const double* M, int nv, const double* x, double* y, int tid) {
-  for (int i = tid; i < nv; i += SOLVER_THREADS) {
-    const double* Mi = M + (size_t)i * nv;
-    double s = 0;
-    for (int k = 0; k < nv; k++) s += Mi[k] * x[k];
-    y[i] = s;
+// y = M x (row dots, thread per row; four independent accumulators keep several global loads
+// in flight per thread)
+__device__ __forceinline__ double dot_row(const double* __restrict__ a, const double* x, int n) {
+  double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+  int k = 0;
+  for (; k + 3 < n; k += 4) {
+    s0 += a[k] * x[k];
+    s1 += a[k + 1] * x[k + 1];
+    s2 += a[k + 2] * x[k + 2];
+    s3 += a[k + 3] * x[k + 3];
   }
+  for (; k < n; k++) s0 += a[k] * x[k];
+  return (s0 + s1) + (s2 + s3);
+}
+
+__device__ void mat_vec(const double* M, int nv, const double* x, double* y, int tid) {
+  for (int i = tid; i < nv; i += SOLVER_THREADS) y[i] = dot_row(M + (size_t)i * nv, x, nv);
   __syncthreads();
 }
 
 // out[r] = J_r . x for r < nefc (thread per row)
 __device__ void jac_vec(const double* J, int nefc, int nv, const double* x, double* out, int tid) {
-  for (int r = tid; r < nefc; r += SOLVER_THREADS) {
-    const double* Jr = J + (size_t)r * nv;
-    double s = 0;
-    for (int k = 0; k < nv; k++) s += Jr[k] * x[k];
-    out[r] = s;
+  for (int r = tid; r < nefc; r += SOLVER_THREADS) out[r] = dot_row(J + (size_t)r * nv, x, nv);
+  __syncthreads();
+}
+
+// out[k] = sum_r J[r][k] w[r] (w in LDS): the block splits the rows into G = SOLVER_THREADS / nv
+// interleaved groups (coalesced row reads, 4 rows in flight per thread), partial column sums
+// meet in LDS (part: G * nv doubles).  Returns the column sum for threads tid < nv.
+__device__ double col_reduce(const double* J, int nefc, int nv, const double* w, double* part, int tid) {
+  const int G = SOLVER_THREADS / nv;
+  const int g = tid / nv, k = tid - g * nv;
+  if (g < G) {
+    double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+    int r = g;
+    for (; r + 3 * G < nefc; r += 4 * G) {
+      s0 += J[(size_t)r * nv + k] * w[r];
+      s1 += J[(size_t)(r + G) * nv + k] * w[r + G];
+      s2 += J[(size_t)(r + 2 * G) * nv + k] * w[r + 2 * G];
+      s3 += J[(size_t)(r + 3 * G) * nv + k] * w[r + 3 * G];
+    }
+    for (; r < nefc; r += G) s0 += J[(size_t)r * nv + k] * w[r];
+    part[g * nv + k] = (s0 + s1) + (s2 + s3);
   }
   __syncthreads();
+  double out = 0;
+  if (tid < nv)
+    for (int q = 0; q < G; q++) out += part[q * nv + tid];
+  __syncthreads();
+  return out;
 }
 
 struct SolverCtx {
@@ -1603,38 +1636,61 @@ __device__ double solver_cost(const SolverCtx& c, const double* M, const double*
   for (int k = tid; k < c.nv; k += SOLVER_THREADS) part += S.res[k] * S.Mres[k];
   double cpart = 0;
   for (int r = tid; r < c.nefc; r += SOLVER_THREADS) {
-    const double* Jr = c.J + (size_t)r * c.nv;
-    double s = 0;
-    for (int k = 0; k < c.nv; k++) s += Jr[k] * x[k];
-    const double jar = s - c.aref[r];
+    const double jar = dot_row(c.J + (size_t)r * c.nv, x, c.nv) - c.aref[r];
     c.jar[r] = jar;
     if (c.type[r] == 0 || jar < 0) cpart += 0.5 * c.D[r] * jar * jar;
   }
   return 0.5 * block_sum(part, S, tid) + block_sum(cpart, S, tid);
 }
 
-// Hessian blocks a = M + J^T D_act J and gradient S.grad = Mres + J^T (D_act jar); returns |g|^2
-__device__ double solver_hessian_grad(const SolverCtx& c, const double* M, double* a, int bi,
-                                      int bj, bool own, SolverShared& S) {
+// constraint part of the cost at x: jar = J x - aref (c.jar), sum of 0.5 D jar^2 over active rows
+__device__ double rows_cost(const SolverCtx& c, const double* x, SolverShared& S) {
+  double cpart = 0;
+  for (int r = c.tid; r < c.nefc; r += SOLVER_THREADS) {
+    const double jar = dot_row(c.J + (size_t)r * c.nv, x, c.nv) - c.aref[r];
+    c.jar[r] = jar;
+    if (c.type[r] == 0 || jar < 0) cpart += 0.5 * c.D[r] * jar * jar;
+  }
+  return block_sum(cpart, S, c.tid);
+}
+
+// Gradient S.grad = M res + J^T (D_act jar) (thread per column, coalesced row reads) and the
+// row activity flags; *changed = the active set differs from the one last factorised.
+// Returns |g|^2.
+__device__ double solver_grad(const SolverCtx& c, int32_t* act_flags, SolverShared& S, bool* changed) {
+  const int tid = c.tid, nv = c.nv, NVP = 4 * c.NB;
+  double* w2 = &S.jc[0][0];  // D_act jar per row (nefc <= RCHUNK * MAX_NVP)
+  int diff = 0;
+  for (int r = tid; r < c.nefc; r += SOLVER_THREADS) {
+    const double jar = c.jar[r];
+    const int act = (c.type[r] == 0 || jar < 0) ? 1 : 0;
+    w2[r] = act ? c.D[r] * jar : 0.0;
+    diff |= act != act_flags[r];
+    act_flags[r] = act;
+  }
+  *changed = block_sum_i(diff, S, tid) != 0;  // (barrier inside)
+  const double jtw = col_reduce(c.J, c.nefc, nv, w2, S.acc2, tid);
+  double gn = 0;
+  if (tid < nv) {
+    const double g = S.Mres[tid] + jtw;
+    S.grad[tid] = g;
+    gn = g * g;
+  } else if (tid < NVP) {
+    S.grad[tid] = 0;
+  }
+  return block_sum(gn, S, tid);
+}
+
+// Hessian blocks a = M + J^T D_act J (active rows only; J streamed through LDS in RCHUNK-row
+// chunks scaled by sqrt(D))
+__device__ void solver_hessian(const SolverCtx& c, const double* M, const int32_t* act_flags, double* a, int bi,
+                               int bj, bool own, SolverShared& S) {
   const int tid = c.tid, nv = c.nv, NVP = 4 * c.NB;
   if (own) load_block(M, nv, bi, bj, a);
-  // gradient accumulators: thread t < NVP owns column t
-  double g = 0;
   for (int r0 = 0; r0 < c.nefc; r0 += RCHUNK) {
     const int nr = min(RCHUNK, c.nefc - r0);
     __syncthreads();
-    if (tid < RCHUNK) {
-      double w = 0, w2 = 0;
-      if (tid < nr) {
-        const int r = r0 + tid;
-        const double jar = c.jar[r];
-        const bool act = c.type[r] == 0 || jar < 0;
-        w = act ? sqrt(c.D[r]) : 0.0;
-        w2 = w * jar;
-      }
-      S.jw[tid] = w;
-      S.jw2[tid] = w2;
-    }
+    if (tid < RCHUNK) S.jw[tid] = (tid < nr && act_flags[r0 + tid]) ? sqrt(c.D[r0 + tid]) : 0.0;
     __syncthreads();
     const double* src = c.J + (size_t)r0 * nv;
     for (int e = tid; e < RCHUNK * NVP; e += SOLVER_THREADS) {
@@ -1644,6 +1700,7 @@ __device__ double solver_hessian_grad(const SolverCtx& c, const double* M, doubl
     __syncthreads();
     if (own) {
       for (int rr = 0; rr < nr; rr++) {
+        if (S.jw[rr] == 0.0) continue;
         const double* ji = S.jc[rr] + 4 * bi;
         const double* jj = S.jc[rr] + 4 * bj;
         const double i0 = ji[0], i1 = ji[1], i2 = ji[2], i3 = ji[3];
@@ -1654,24 +1711,22 @@ __device__ double solver_hessian_grad(const SolverCtx& c, const double* M, doubl
         a[12] += i3 * j0; a[13] += i3 * j1; a[14] += i3 * j2; a[15] += i3 * j3;
       }
     }
-    if (tid < nv) {
-      for (int rr = 0; rr < nr; rr++) g += S.jc[rr][tid] * S.jw2[rr];
-    }
   }
-  double gn = 0;
-  if (tid < nv) {
-    g += S.Mres[tid];
-    S.grad[tid] = g;
-    gn = g * g;
-  } else if (tid < NVP) {
-    S.grad[tid] = 0;
-  }
-  return block_sum(gn, S, tid);
+  __syncthreads();
 }
 
+#define SPROF(k)                                  \
+  if (prof) {                                     \
+    __syncthreads();                              \
+    const unsigned long long t_ = stamp();        \
+    if (tid == 0) prof[k] += t_ - tp;             \
+    tp = t_;                                      \
+  }
+
 __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj, bool own,
-                             int nefc, int ne, int tid) {
+                             int nefc, int ne, int tid, unsigned long long* prof) {
   const rmbx_model& m = *e.m;
+  unsigned long long tp = prof ? stamp() : 0;
   const int nv = m.nv, NB = (nv + 3) / 4, NVP = 4 * NB;
   const double* M = W(M);
   SolverCtx c;
@@ -1693,21 +1748,46 @@ __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj,
   __syncthreads();
   blk_cholesky(a, bi, bj, own, NB, S);
   blk_solve(a, bi, bj, own, NB, S.tmp, S.a0, S, tid);
+  SPROF(8)
   for (int k = tid; k < NVP; k += SOLVER_THREADS) S.tmp[k] = k < nv ? e.qacc_ws[k] : 0.0;
   __syncthreads();
+  // warm start vs smooth start (the smooth start has res = 0: only its rows cost anything)
   const double c_ws = solver_cost(c, M, S.tmp, S);
-  const double c_sm = solver_cost(c, M, S.a0, S);
-  const bool use_ws = c_ws < c_sm;
-  for (int k = tid; k < NVP; k += SOLVER_THREADS) S.a[k] = use_ws ? S.tmp[k] : S.a0[k];
+  double* jar_ws = W(efc_tmp);
+  for (int r = tid; r < nefc; r += SOLVER_THREADS) jar_ws[r] = c.jar[r];
+  for (int k = tid; k < NVP; k += SOLVER_THREADS) S.Ms[k] = S.Mres[k];
   __syncthreads();
-  double cost = solver_cost(c, M, S.a, S);
+  const double c_sm = rows_cost(c, S.a0, S);
+  const bool use_ws = c_ws < c_sm;
+  for (int k = tid; k < NVP; k += SOLVER_THREADS) {
+    S.a[k] = use_ws ? S.tmp[k] : S.a0[k];
+    S.res[k] = use_ws ? S.res[k] : 0.0;
+    S.Mres[k] = use_ws ? S.Ms[k] : 0.0;
+  }
+  if (use_ws)
+    for (int r = tid; r < nefc; r += SOLVER_THREADS) c.jar[r] = jar_ws[r];
+  __syncthreads();
+  double cost = use_ws ? c_ws : c_sm;
+  SPROF(9)
   const double scale = 1.0 / (m.meaninertia * (nv > 1 ? nv : 1));
   int it;
+  // The Hessian depends only on the active row set: it is rebuilt and refactorised only when
+  // that set changed since the last factorisation (identical matrix otherwise).
+  int32_t* act_flags = WI(efc_act);
+  bool have_factor = false;
   for (it = 0; it < m.solver_iterations; it++) {
-    const double gn = solver_hessian_grad(c, M, a, bi, bj, own, S);
+    bool changed;
+    const double gn = solver_grad(c, act_flags, S, &changed);
+    SPROF(10)
     if (scale * sqrt(gn) < m.solver_tolerance) break;
-    blk_cholesky(a, bi, bj, own, NB, S);
+    if (changed || !have_factor) {
+      solver_hessian(c, M, act_flags, a, bi, bj, own, S);
+      SPROF(10)
+      blk_cholesky(a, bi, bj, own, NB, S);
+      have_factor = true;
+    }
     blk_solve(a, bi, bj, own, NB, S.grad, S.srch, S, tid);
+    SPROF(11)
     for (int k = tid; k < NVP; k += SOLVER_THREADS) S.srch[k] = -S.srch[k];
     __syncthreads();
     mat_vec(M, nv, S.srch, S.Ms, tid);
@@ -1748,9 +1828,23 @@ __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj,
       alpha = an;
       if (block_sum_i(changed, S, tid) == 0) break;
     }
-    for (int k = tid; k < NVP; k += SOLVER_THREADS) S.a[k] += alpha * S.srch[k];
-    __syncthreads();
-    const double newcost = solver_cost(c, M, S.a, S);
+    SPROF(12)
+    // move along the search direction; res, M res and jar updated incrementally (as
+    // mj_solNewton updates qacc, Ma and efc_Jaref)
+    double part = 0, cpart = 0;
+    for (int k = tid; k < NVP; k += SOLVER_THREADS) {
+      S.a[k] += alpha * S.srch[k];
+      S.res[k] += alpha * S.srch[k];
+      S.Mres[k] += alpha * S.Ms[k];
+      if (k < nv) part += S.res[k] * S.Mres[k];
+    }
+    for (int r = tid; r < nefc; r += SOLVER_THREADS) {
+      const double jar = c.jar[r] + alpha * c.Js[r];
+      c.jar[r] = jar;
+      if (c.type[r] == 0 || jar < 0) cpart += 0.5 * c.D[r] * jar * jar;
+    }
+    const double newcost = 0.5 * block_sum(part, S, tid) + block_sum(cpart, S, tid);
+    SPROF(13)
     const double improvement = scale * (cost - newcost);
     cost = newcost;
     if (improvement < m.solver_tolerance) {
@@ -1759,18 +1853,21 @@ __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj,
     }
   }
   // forces and qfrc_constraint = J^T f
+  double* fl = &S.jc[0][0];  // forces staged in LDS for the column reduction
   for (int r = tid; r < nefc; r += SOLVER_THREADS) {
     const double jar = c.jar[r];
-    c.force[r] = (c.type[r] == 0 || jar < 0) ? -c.D[r] * jar : 0.0;
+    const double f = (c.type[r] == 0 || jar < 0) ? -c.D[r] * jar : 0.0;
+    c.force[r] = f;
+    fl[r] = f;
   }
   __syncthreads();
-  for (int k = tid; k < nv; k += SOLVER_THREADS) {
-    double s = 0;
-    for (int r = 0; r < nefc; r++) s += c.J[(size_t)r * nv + k] * c.force[r];
-    W(qfrc_constraint)[k] = s;
-    W(qacc)[k] = S.a[k];
+  const double qc = col_reduce(c.J, nefc, nv, fl, S.acc2, tid);
+  if (tid < nv) {
+    W(qfrc_constraint)[tid] = qc;
+    W(qacc)[tid] = S.a[tid];
   }
   __syncthreads();
+  SPROF(14)
   return it;
 }
 
@@ -1857,7 +1954,6 @@ struct KArgs {
   const int32_t* subtree_end;  // [nbody] end of each body's DFS subtree id range
 };
 
-__device__ __forceinline__ unsigned long long stamp() { return __builtin_readcyclecounter(); }
 
 __device__ __forceinline__ void make_env(const KArgs& args, int env, Env& e) {
   const rmbx_model& m = args.m;
@@ -1927,7 +2023,7 @@ __global__ void __launch_bounds__(64) front_kernel(KArgs args) {
 }
 
 // back half: Newton solve, constraint forces, sensors, implicitfast integration (4 waves/env)
-__global__ void __launch_bounds__(SOLVER_THREADS) solver_kernel(KArgs args) {
+__global__ void __launch_bounds__(SOLVER_THREADS, 4) solver_kernel(KArgs args) {
   __shared__ SolverShared S;
   const int env = blockIdx.x;
   const int tid = threadIdx.x;
@@ -1942,7 +2038,7 @@ __global__ void __launch_bounds__(SOLVER_THREADS) solver_kernel(KArgs args) {
   double a[16];
   PROF_BEGIN()
   const int ncon = WI(scal)[0], nefc = WI(scal)[1], ne = WI(scal)[2];
-  const int iters = solver_newton(e, S, a, bi, bj, own, nefc, ne, tid);
+  const int iters = solver_newton(e, S, a, bi, bj, own, nefc, ne, tid, prof);
   PROF(5)
   sensors(e, ncon, tid, S.bacc, S.bfrc, &S.jc[0][0], S.anc, args.subtree_end);
   PROF(6)
@@ -2018,6 +2114,7 @@ static Layout make_layout(const rmbx_model& m) {
   L.con_pair = itake(mc);
   L.con_efcadr = itake(mc);
   L.efc_type = itake(ne);
+  L.efc_act = itake(ne);
   L.scal = itake(8);
   L.istride = io;
   L.stride = o + (io + 1) / 2;
@@ -2114,6 +2211,11 @@ int rmbx_engine_create(const struct rmbx_model* model, int n_env, rmbx_engine** 
     return st;
   }
   eng->L = make_layout(h);
+  if (eng->L.nefc_max > RCHUNK * MAX_NVP) {
+    rmbx_engine_destroy(eng);
+    rmbx::set_error("model needs %d constraint rows, more than the solver's %d", eng->L.nefc_max, RCHUNK * MAX_NVP);
+    return RMBX_ERR_ARG;
+  }
   *out = eng;
   return RMBX_OK;
 }

@@ -67,13 +67,18 @@ class PhysicsEngine:
 
     STAGES = ("kinematics", "com_crb", "velocity_rne_act", "collision", "constraints", "solver",
               "sensors", "integrate")
+    # sub-stages of "solver" (slots 8..14)
+    SOLVER_STAGES = ("smooth_factor_solve", "initial_costs", "hessian_grad", "newton_factor_solve",
+                     "line_search", "step_cost", "forces")
 
     def step_profiled(self, nsub=8):
         """Diagnostic step: returns mean shader cycles per stage (summed over substeps)."""
         prof = torch.zeros((self.n_env, 16), dtype=torch.int64, device=self.device)
         N.call("rmbx_engine_step_profiled", self._h, int(nsub), N.ptr(prof), N.stream_ptr())
         p = prof.double().mean(0).cpu().numpy()
-        return dict(zip(self.STAGES, p[: len(self.STAGES)]))
+        out = dict(zip(self.STAGES, p[: len(self.STAGES)]))
+        out.update({"solver." + k: v for k, v in zip(self.SOLVER_STAGES, p[8: 8 + len(self.SOLVER_STAGES)])})
+        return out
 
     def forward(self, active=None):
         N.call("rmbx_engine_forward", self._h, N.ptr(active), N.stream_ptr())

@@ -26,6 +26,6 @@ print(f"n_env {n}: {dt*1e3:.2f} ms per env-step -> {n/dt:.0f} env-steps/s")
 st = env.engine.stats.cpu().numpy()
 print("ncon mean", st[:, 0].mean(), "nefc mean", st[:, 1].mean(), "iters mean", st[:, 2].mean(), "bad", st[:, 3].sum())
 p = env.engine.step_profiled(8)
-tot = sum(p.values())
+tot = sum(v for k, v in p.items() if "." not in k)
 for k, v in p.items():
     print(f"  {k:18s} {v/1e6:8.3f} Mcycles  {100*v/tot:5.1f}%")
