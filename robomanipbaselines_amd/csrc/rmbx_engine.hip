@@ -77,6 +77,7 @@ struct Env {
   double* time;
   int32_t* stats;
   double* sh;  // front-kernel LDS: xpos, xquat, xmat, cvel, cacc, cfrc, cdofdot
+  const int32_t* subtree_end;  // DFS subtree ranges (tree passes, chain membership)
 };
 
 #define W(name) (e.ws + e.L->name)
@@ -1034,6 +1035,27 @@ __device__ __forceinline__ int last_dof(const rmbx_model& m, int b) {
   return m.body_dofadr[w] + m.body_dofnum[w] - 1;
 }
 
+// dot product of a (global) row with x; four independent accumulators keep several loads in
+// flight per thread
+__device__ __forceinline__ double dot_row(const double* __restrict__ a, const double* x, int n) {
+  double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
+  int k = 0;
+  for (; k + 3 < n; k += 4) {
+    s0 += a[k] * x[k];
+    s1 += a[k + 1] * x[k + 1];
+    s2 += a[k + 2] * x[k + 2];
+    s3 += a[k + 3] * x[k + 3];
+  }
+  for (; k < n; k++) s0 += a[k] * x[k];
+  return (s0 + s1) + (s2 + s3);
+}
+
+// dof k moves body b (its body is b or an ancestor of b: DFS subtree range test)
+__device__ __forceinline__ bool dof_on_chain(const Env& e, int k, int b) {
+  const int a = e.m->dof_body[k];
+  return a <= b && b < e.subtree_end[a];
+}
+
 __device__ void jac_point_dir(const Env& e, int b, const double* p, const double* dir, double sgn,
                               double* row) {
   const rmbx_model& m = *e.m;
@@ -1109,86 +1131,103 @@ __device__ int make_constraints(Env& e, int lane, int ncon, int* ne_out) {
     (void)off;
     nlim += total;
   }
-  // contacts rows
+  // contacts rows (wave-parallel count)
   int nconrow = 0;
-  for (int c = 0; c < ncon; c++) nconrow += WI(con_condim)[c] == 1 ? 1 : 4;
+  for (int base = 0; base < ncon; base += 64) {
+    const int c = base + lane;
+    nconrow += wave_sum_i(c < ncon ? (WI(con_condim)[c] == 1 ? 1 : 4) : 0);
+  }
   int nefc = ne + nlim + nconrow;
   if (nefc > nefc_max) nefc = nefc_max;
   // zero the Jacobian rows in use
   for (size_t k = lane; k < (size_t)nefc * nv; k += 64) J[k] = 0;
   sync();
-  // equality rows: one lane per equality constraint (rows in constraint order)
-  for (int q = lane; q < m.neq; q += 64) {
-    int r = 0;
-    for (int qq = 0; qq < q; qq++)
-      r += m.eq_type[qq] == RMBX_EQ_CONNECT ? 3 : (m.eq_type[qq] == RMBX_EQ_WELD ? 6 : 1);
-    {
-      const double* data = m.eq_data + RMBX_EQ_DATA * q;
-      const double* sr = m.eq_solref + 2 * q;
-      const double* si = m.eq_solimp + 5 * q;
-      const int o1 = m.eq_obj1[q], o2 = m.eq_obj2[q];
-      const int type = m.eq_type[q];
-      if (type == RMBX_EQ_CONNECT || type == RMBX_EQ_WELD) {
-        double p1[3], p2[3], t[3], err[6];
-        const int nr = type == RMBX_EQ_CONNECT ? 3 : 6;
-        const double* xm = W(xmat);
-        if (type == RMBX_EQ_CONNECT) {
-          matvec3(xm + 9 * o1, data, t);
-          for (int i = 0; i < 3; i++) p1[i] = e.xpos[3 * o1 + i] + t[i];
-          matvec3(xm + 9 * o2, data + 3, t);
-          for (int i = 0; i < 3; i++) p2[i] = e.xpos[3 * o2 + i] + t[i];
-        } else {
-          double Rr[9], ra[3], u[3];
-          quat2mat(data + 6, Rr);
-          matvec3(Rr, data, ra);
-          for (int i = 0; i < 3; i++) u[i] = data[3 + i] + ra[i];
-          matvec3(xm + 9 * o1, u, t);
-          for (int i = 0; i < 3; i++) p1[i] = e.xpos[3 * o1 + i] + t[i];
-          matvec3(xm + 9 * o2, data, t);
-          for (int i = 0; i < 3; i++) p2[i] = e.xpos[3 * o2 + i] + t[i];
-        }
-        for (int i = 0; i < 3; i++) err[i] = p1[i] - p2[i];
-        double q1r[4], qe[4], cq1[4];
-        if (nr == 6) {
-          quatmul(e.xquat + 4 * o1, data + 6, q1r);
-          cq1[0] = q1r[0];
-          cq1[1] = -q1r[1];
-          cq1[2] = -q1r[2];
-          cq1[3] = -q1r[3];
-          quatmul(cq1, e.xquat + 4 * o2, qe);
-          for (int i = 0; i < 3; i++) err[3 + i] = qe[1 + i] * data[10];
-        }
-        double nrm = 0;
-        for (int i = 0; i < nr; i++) nrm += err[i] * err[i];
-        nrm = sqrt(nrm);
+  // equality rows: every lane evaluates the constraint's anchors/errors (cheap, no broadcast),
+  // lanes < nrows set the row parameters, then the Jacobian is filled lane-per-dof with the
+  // same per-entry accumulation order as the serial chain walks (0 + body-1 term + body-2 term)
+  const double* cdof = LDS_CDOF(e);
+  int r = 0;
+  for (int q = 0; q < m.neq; q++) {
+    const double* data = m.eq_data + RMBX_EQ_DATA * q;
+    const double* sr = m.eq_solref + 2 * q;
+    const double* si = m.eq_solimp + 5 * q;
+    const int o1 = m.eq_obj1[q], o2 = m.eq_obj2[q];
+    const int type = m.eq_type[q];
+    if (type == RMBX_EQ_CONNECT || type == RMBX_EQ_WELD) {
+      double p1[3], p2[3], t[3], err[6];
+      const int nr = type == RMBX_EQ_CONNECT ? 3 : 6;
+      const double* xm = e.sh + 7 * m.nbody;  // xmat (LDS)
+      if (type == RMBX_EQ_CONNECT) {
+        matvec3(xm + 9 * o1, data, t);
+        for (int i = 0; i < 3; i++) p1[i] = e.sh[3 * o1 + i] + t[i];
+        matvec3(xm + 9 * o2, data + 3, t);
+        for (int i = 0; i < 3; i++) p2[i] = e.sh[3 * o2 + i] + t[i];
+      } else {
+        double Rr[9], ra[3], u[3];
+        quat2mat(data + 6, Rr);
+        matvec3(Rr, data, ra);
+        for (int i = 0; i < 3; i++) u[i] = data[3 + i] + ra[i];
+        matvec3(xm + 9 * o1, u, t);
+        for (int i = 0; i < 3; i++) p1[i] = e.sh[3 * o1 + i] + t[i];
+        matvec3(xm + 9 * o2, data, t);
+        for (int i = 0; i < 3; i++) p2[i] = e.sh[3 * o2 + i] + t[i];
+      }
+      for (int i = 0; i < 3; i++) err[i] = p1[i] - p2[i];
+      double q1r[4], qe[4], cq1[4];
+      const double* xq1 = e.sh + 3 * m.nbody + 4 * o1;
+      const double* xq2 = e.sh + 3 * m.nbody + 4 * o2;
+      if (nr == 6) {
+        quatmul(xq1, data + 6, q1r);
+        cq1[0] = q1r[0];
+        cq1[1] = -q1r[1];
+        cq1[2] = -q1r[2];
+        cq1[3] = -q1r[3];
+        quatmul(cq1, xq2, qe);
+        for (int i = 0; i < 3; i++) err[3 + i] = qe[1 + i] * data[10];
+      }
+      double nrm = 0;
+      for (int i = 0; i < nr; i++) nrm += err[i] * err[i];
+      nrm = sqrt(nrm);
+      if (lane < 3) {
         const double diag_t = m.body_invweight0[2 * o1] + m.body_invweight0[2 * o2];
+        set_row(e, r + lane, 0, err[lane], diag_t, sr, si, nrm);
+      } else if (nr == 6 && lane < 6) {
+        const double diag_r = m.body_invweight0[2 * o1 + 1] + m.body_invweight0[2 * o2 + 1];
+        set_row(e, r + lane, 0, err[lane], diag_r, sr, si, nrm);
+      }
+      for (int k = lane; k < nv; k += 64) {
+        const bool c1 = dof_on_chain(e, k, o1), c2 = dof_on_chain(e, k, o2);
+        if (!c1 && !c2) continue;
+        const double* S = cdof + 6 * k;
+        double v1[3], v2[3], w[3];
+        cross3(S, p1, w);
+        for (int i = 0; i < 3; i++) v1[i] = S[3 + i] + w[i];
+        cross3(S, p2, w);
+        for (int i = 0; i < 3; i++) v2[i] = S[3 + i] + w[i];
         for (int i = 0; i < 3; i++) {
           double dir[3] = {0, 0, 0};
           dir[i] = 1;
-          set_row(e, r, 0, err[i], diag_t, sr, si, nrm);
-          jac_point_dir(e, o1, p1, dir, 1.0, J + (size_t)r * nv);
-          jac_point_dir(e, o2, p2, dir, -1.0, J + (size_t)r * nv);
-          r++;
+          double val = 0;
+          if (c1) val += 1.0 * dot3(v1, dir);
+          if (c2) val += -1.0 * dot3(v2, dir);
+          J[(size_t)(r + i) * nv + k] = val;
         }
         if (nr == 6) {
-          const double diag_r = m.body_invweight0[2 * o1 + 1] + m.body_invweight0[2 * o2 + 1];
-          for (int i = 0; i < 3; i++) set_row(e, r + i, 0, err[3 + i], diag_r, sr, si, nrm);
-          // rotational columns: chains of o2 (+) and o1 (-); dofs shared cancel
-          const double* cdof = LDS_CDOF(e);
+          // rotational rows: body-2 chain (+) then body-1 chain (-); shared dofs cancel exactly
           for (int pass = 0; pass < 2; pass++) {
-            const int b = pass == 0 ? o2 : o1;
+            if (!(pass == 0 ? c2 : c1)) continue;
             const double sg = pass == 0 ? 1.0 : -1.0;
-            for (int k = last_dof(m, b); k >= 0; k = m.dof_parent[k]) {
-              const double wq[4] = {0, sg * cdof[6 * k], sg * cdof[6 * k + 1], sg * cdof[6 * k + 2]};
-              double t1[4], t2[4];
-              quatmul(cq1, wq, t1);
-              quatmul(t1, e.xquat + 4 * o2, t2);
-              for (int i = 0; i < 3; i++) J[(size_t)(r + i) * nv + k] += 0.5 * t2[1 + i] * data[10];
-            }
+            const double wq[4] = {0, sg * S[0], sg * S[1], sg * S[2]};
+            double t1[4], t2[4];
+            quatmul(cq1, wq, t1);
+            quatmul(t1, xq2, t2);
+            for (int i = 0; i < 3; i++) J[(size_t)(r + 3 + i) * nv + k] += 0.5 * t2[1 + i] * data[10];
           }
-          r += 3;
         }
-      } else {
+      }
+      r += nr;
+    } else {
+      if (lane == 0) {
         const int j1 = o1, j2 = o2;
         const double q1 = e.qpos[m.jnt_qposadr[j1]] - m.qpos0[m.jnt_qposadr[j1]];
         const double q2 = e.qpos[m.jnt_qposadr[j2]] - m.qpos0[m.jnt_qposadr[j2]];
@@ -1200,8 +1239,8 @@ __device__ int make_constraints(Env& e, int lane, int ncon, int* ne_out) {
         set_row(e, r, 0, err, m.dof_invweight0[d1] + m.dof_invweight0[d2], sr, si, err);
         J[(size_t)r * nv + d1] += 1;
         J[(size_t)r * nv + d2] -= dpoly;
-        r++;
       }
+      r++;
     }
   }
   // limit rows
@@ -1266,18 +1305,21 @@ __device__ int make_constraints(Env& e, int lane, int ncon, int* ne_out) {
           }
       }
       const int nrow = min(cnt, nefc - r0);
-      const double* cdof = LDS_CDOF(e);
+      // both chains are evaluated at the same point with the same directions, so dofs shared
+      // by the two bodies cancel exactly (x - x = +0, the zeroed entry): each chain is walked
+      // only up to the common ancestor and its entries stored (0 + x, as the accumulation gives)
       for (int pass = 0; pass < 2 && nrow > 0; pass++) {
-        const int b = pass == 0 ? b2 : b1;
+        const int b = pass == 0 ? b2 : b1, other = pass == 0 ? b1 : b2;
         const double sgn = pass == 0 ? 1.0 : -1.0;
         for (int k = last_dof(m, b); k >= 0; k = m.dof_parent[k]) {
+          if (dof_on_chain(e, k, other)) break;
           const double* Sk = cdof + 6 * k;
           double wxp[3];
           cross3(Sk, pos, wxp);
           const double v[3] = {Sk[3] + wxp[0], Sk[4] + wxp[1], Sk[5] + wxp[2]};
 #pragma unroll
           for (int t = 0; t < 4; t++)
-            if (t < nrow) J[(size_t)(r0 + t) * nv + k] += sgn * dot3(v, dirs[t]);
+            if (t < nrow) J[(size_t)(r0 + t) * nv + k] = 0.0 + sgn * dot3(v, dirs[t]);
         }
       }
     }
@@ -1286,9 +1328,7 @@ __device__ int make_constraints(Env& e, int lane, int ncon, int* ne_out) {
   sync();
   // aref = -b (J qvel) - k imp pos ; D = 1/R
   for (int r = lane; r < nefc; r += 64) {
-    const double* Jr = J + (size_t)r * nv;
-    double v = 0;
-    for (int k = 0; k < nv; k++) v += Jr[k] * e.qvel[k];
+    const double v = dot_row(J + (size_t)r * nv, e.qvel, nv);
     W(efc_vel)[r] = v;
     W(efc_aref)[r] = -W(efc_tmp)[r] * v - W(efc_D)[r];
     W(efc_D)[r] = 1.0 / W(efc_R)[r];
@@ -1563,21 +1603,7 @@ __device__ __forceinline__ void load_block(const double* M, int nv, int bi, int 
 }
 
 // y = M x, thread per row (M dense in global), vectors in LDS
-// y = M x (row dots, thread per row; four independent accumulators keep several global loads
-// in flight per thread)
-__device__ __forceinline__ double dot_row(const double* __restrict__ a, const double* x, int n) {
-  double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-  int k = 0;
-  for (; k + 3 < n; k += 4) {
-    s0 += a[k] * x[k];
-    s1 += a[k + 1] * x[k + 1];
-    s2 += a[k + 2] * x[k + 2];
-    s3 += a[k + 3] * x[k + 3];
-  }
-  for (; k < n; k++) s0 += a[k] * x[k];
-  return (s0 + s1) + (s2 + s3);
-}
-
+// y = M x (thread per row)
 __device__ void mat_vec(const double* M, int nv, const double* x, double* y, int tid) {
   for (int i = tid; i < nv; i += SOLVER_THREADS) y[i] = dot_row(M + (size_t)i * nv, x, nv);
   __syncthreads();
@@ -1782,7 +1808,7 @@ __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj,
     if (scale * sqrt(gn) < m.solver_tolerance) break;
     if (changed || !have_factor) {
       solver_hessian(c, M, act_flags, a, bi, bj, own, S);
-      SPROF(10)
+      SPROF(15)
       blk_cholesky(a, bi, bj, own, NB, S);
       have_factor = true;
     }
@@ -1998,6 +2024,7 @@ __global__ void __launch_bounds__(64) front_kernel(KArgs args) {
   Env e;
   make_env(args, env, e);
   e.sh = front_smem;
+  e.subtree_end = args.subtree_end;
   __shared__ int s_anc[MAX_BODY];
   PROF_BEGIN()
   kinematics(e, lane, s_anc);

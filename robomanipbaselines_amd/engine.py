@@ -68,8 +68,8 @@ class PhysicsEngine:
     STAGES = ("kinematics", "com_crb", "velocity_rne_act", "collision", "constraints", "solver",
               "sensors", "integrate")
     # sub-stages of "solver" (slots 8..14)
-    SOLVER_STAGES = ("smooth_factor_solve", "initial_costs", "hessian_grad", "newton_factor_solve",
-                     "line_search", "step_cost", "forces")
+    SOLVER_STAGES = ("smooth_factor_solve", "initial_costs", "gradient", "newton_factor_solve",
+                     "line_search", "step_cost", "forces", "hessian")
 
     def step_profiled(self, nsub=8):
         """Diagnostic step: returns mean shader cycles per stage (summed over substeps)."""
