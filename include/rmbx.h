@@ -228,6 +228,14 @@ int rmbx_render(const rmbx_camera* cam, const int32_t* prim_i32, const float* pr
  * ------------------------------------------------------------------------------------------- */
 int rmbx_nhwc_bias_act(const void* x, const float* bias, const void* res, const float* res_bias,
                        void* out, size_t n_pix, int C, int relu, int dtype, void* stream);
+/* Implicit-GEMM convolution (MFMA, bf16 NHWC) with the fused epilogue
+ * out = relu?(conv(in, weight) + bias + residual), one bf16 rounding; replaces conv -> BN ->
+ * (+ identity/downsample) -> ReLU of the ResNet-18 BasicBlocks (BN folded into weight/bias).
+ * in [N][H][W][Cin], weight [Cout][KH][KW][Cin], residual/out [N][Ho][Wo][Cout] bf16, bias f32;
+ * Cin % 64 == 0, Cout % 64 == 0, residual optional (NULL). */
+int rmbx_conv2d_nhwc(const void* in, const void* weight, const float* bias, const void* residual,
+                     void* out, int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                     int pad, int relu, void* stream);
 /* Residual add + LayerNorm over the last dim of [rows][D] rows (D <= 2048, multiple of 8 bf16 / 4
  * f32): out = LayerNorm(rnd(x + r)) * weight + bias (f32 weight/bias), r optional (NULL); replaces
  * the add + nn.LayerNorm pair of the ACT transformer's post-norm layers (third_party/act). */

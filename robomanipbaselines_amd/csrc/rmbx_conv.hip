@@ -1,0 +1,206 @@
+// Implicit-GEMM convolution with a fused epilogue for the policy vision trunk (bf16, NHWC),
+// MFMA 32x32x16 on gfx950.
+//
+// Replaces the conv -> FrozenBN -> (+ residual) -> ReLU sequence of the ResNet-18 BasicBlocks of
+// the reference's backbones (torchvision resnet18 inside ACT's DETR, third_party/act [absent];
+// policy/mlp/MlpPolicy.py:34-39) for the 3x3 (stride 1/2) and 1x1 (stride 2) convolutions: BN is
+// folded into the weights on the host, and bias, residual add and ReLU are applied to the f32
+// accumulators before the single bf16 store, so the activation makes one HBM round trip per
+// conv instead of four.
+//
+// GEMM view: M = N*Ho*Wo output pixels, N = Cout, K = KH*KW*Cin ordered (tap, channel), so
+// every K step of 64 is one filter tap over 64 contiguous input channels (16-byte loads of NHWC
+// rows; out-of-image taps read zeros).  Block tile 128 pixels x 64 channels, 4 waves, each wave
+// 32 pixels x 64 channels = two 32x32 accumulator tiles; A/B staged global -> registers -> LDS
+// (rows padded to 72 bf16 against bank conflicts) with the next K step's loads in flight while
+// the current one is multiplied.  Consecutive blocks walk the Cout tiles of one pixel tile, so
+// the input tile is reused from L2; pixel tiles are spread over the 8 XCDs in contiguous ranges.
+
+#include "rmbx_common.h"
+
+#include <cstdint>
+
+namespace rmbx {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+constexpr int CBM = 128, CBN = 64, CBK = 64, CLD = CBK + 8;
+
+struct ConvArgs {
+  const uint16_t* in;   // [N][H][W][Cin]
+  const uint16_t* w;    // [Cout][KH][KW][Cin]
+  const float* bias;    // [Cout]
+  const uint16_t* res;  // [N][Ho][Wo][Cout] or null
+  uint16_t* out;        // [N][Ho][Wo][Cout]
+  int N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, relu;
+  long long M;
+  int n_ntiles;         // Cout / CBN
+  long long n_mtiles;
+};
+
+__device__ __forceinline__ float bf2f(uint16_t h) { return __uint_as_float((uint32_t)h << 16); }
+__device__ __forceinline__ uint16_t f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fc0;
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return (uint16_t)(u >> 16);
+}
+
+__global__ void __launch_bounds__(256) conv_nhwc_kernel(ConvArgs a) {
+  __shared__ __attribute__((aligned(16))) uint16_t sA[CBM * CLD];
+  __shared__ __attribute__((aligned(16))) uint16_t sB[CBN * CLD];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+
+  // block -> (pixel tile, channel tile); pixel tiles in contiguous ranges per XCD
+  const long long nblk = (long long)gridDim.x;
+  long long b = blockIdx.x;
+  if ((nblk & 7) == 0) b = (b & 7) * (nblk >> 3) + (b >> 3);
+  const long long mt = b / a.n_ntiles;
+  const int nt = (int)(b - mt * a.n_ntiles);
+  const long long m0 = mt * CBM;
+  const int n0 = nt * CBN;
+
+  // A loader: 128 pixels x 64 ch = 1024 16-byte chunks, 4 per thread (pixel = q >> 3, part = q & 7)
+  int pn[4], ph[4], pw[4];
+  bool pv[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int q = tid + 256 * i;
+    const long long m = m0 + (q >> 3);
+    pv[i] = m < a.M;
+    const long long mm = pv[i] ? m : 0;
+    const int wo = (int)(mm % a.Wo);
+    const long long t = mm / a.Wo;
+    const int ho = (int)(t % a.Ho);
+    pn[i] = (int)(t / a.Ho);
+    ph[i] = ho * a.stride - a.pad;
+    pw[i] = wo * a.stride - a.pad;
+  }
+  const int cchunks = a.Cin / CBK;
+  const int KT = a.KH * a.KW * cchunks;
+
+  uint4 ra0, ra1, ra2, ra3, rb0, rb1;
+  int kh_ = 0, kw_ = 0, c0_ = 0;
+#define RMBX_A_LOAD(I, DST)                                                                              \
+  {                                                                                                      \
+    const int h_ = ph[I] + kh_, w_ = pw[I] + kw_;                                                        \
+    DST = (pv[I] && h_ >= 0 && h_ < a.H && w_ >= 0 && w_ < a.W)                                          \
+              ? *reinterpret_cast<const uint4*>(a.in + (((size_t)pn[I] * a.H + h_) * a.W + w_) * a.Cin + c0_ + \
+                                                ((tid + 256 * (I)) & 7) * 8)                             \
+              : make_uint4(0, 0, 0, 0);                                                                  \
+  }
+#define RMBX_B_LOAD(I, DST)                                                                              \
+  {                                                                                                      \
+    const int q_ = tid + 256 * (I);                                                                      \
+    DST = *reinterpret_cast<const uint4*>(a.w + (((size_t)(n0 + (q_ >> 3)) * a.KH + kh_) * a.KW + kw_) * a.Cin + \
+                                          c0_ + (q_ & 7) * 8);                                           \
+  }
+#define RMBX_CONV_LOAD(KT)                    \
+  {                                           \
+    const int tap_ = (KT) / cchunks;          \
+    c0_ = ((KT) - tap_ * cchunks) * CBK;      \
+    kh_ = tap_ / a.KW;                        \
+    kw_ = tap_ - kh_ * a.KW;                  \
+    RMBX_A_LOAD(0, ra0)                       \
+    RMBX_A_LOAD(1, ra1)                       \
+    RMBX_A_LOAD(2, ra2)                       \
+    RMBX_A_LOAD(3, ra3)                       \
+    RMBX_B_LOAD(0, rb0)                       \
+    RMBX_B_LOAD(1, rb1)                       \
+  }
+#define RMBX_ST(BUF, I, V) *reinterpret_cast<uint4*>(BUF + ((tid + 256 * (I)) >> 3) * CLD + ((tid + 256 * (I)) & 7) * 8) = V;
+
+  f32x16 acc0 = {}, acc1 = {};
+  RMBX_CONV_LOAD(0)
+  for (int kt = 0; kt < KT; ++kt) {
+    __syncthreads();
+    RMBX_ST(sA, 0, ra0)
+    RMBX_ST(sA, 1, ra1)
+    RMBX_ST(sA, 2, ra2)
+    RMBX_ST(sA, 3, ra3)
+    RMBX_ST(sB, 0, rb0)
+    RMBX_ST(sB, 1, rb1)
+    __syncthreads();
+    if (kt + 1 < KT) RMBX_CONV_LOAD(kt + 1)
+    const int r = lane & 31, h8 = 8 * (lane >> 5);
+    const uint16_t* arow = sA + (32 * wave + r) * CLD + h8;
+    const uint16_t* brow0 = sB + r * CLD + h8;
+    const uint16_t* brow1 = sB + (32 + r) * CLD + h8;
+#pragma unroll
+    for (int ks = 0; ks < CBK / 16; ++ks) {
+      const bf16x8 af = *reinterpret_cast<const bf16x8*>(arow + 16 * ks);
+      const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(brow0 + 16 * ks);
+      const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(brow1 + 16 * ks);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, b0, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, b1, acc1, 0, 0, 0);
+    }
+  }
+#undef RMBX_ST
+#undef RMBX_A_LOAD
+#undef RMBX_B_LOAD
+
+  // epilogue: C[row = pixel][col = channel], col = lane & 31, row = (j & 3) + 8 (j >> 2) + 4 (lane >> 5)
+  const int col = lane & 31;
+#pragma unroll
+  for (int t = 0; t < 2; ++t) {
+    const int co = n0 + 32 * t + col;
+    const float bco = a.bias[co];
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int row = (j & 3) + 8 * (j >> 2) + 4 * (lane >> 5);
+      const long long m = m0 + 32 * wave + row;
+      if (m >= a.M) continue;
+      float v = (t == 0 ? acc0[j] : acc1[j]) + bco;
+      const size_t o = (size_t)m * a.Cout + co;
+      if (a.res) v += bf2f(a.res[o]);
+      if (a.relu) v = v > 0.f ? v : 0.f;
+      a.out[o] = f2bf(v);
+    }
+  }
+}
+#undef RMBX_CONV_LOAD
+
+}  // namespace
+}  // namespace rmbx
+
+extern "C" int rmbx_conv2d_nhwc(const void* in, const void* weight, const float* bias, const void* residual,
+                                void* out, int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                                int pad, int relu, void* stream) {
+  RMBX_CHECK_ARG(in && weight && bias && out, "rmbx_conv2d_nhwc: null pointer");
+  RMBX_CHECK_ARG(N >= 0 && H > 0 && W > 0 && KH > 0 && KW > 0 && stride > 0 && pad >= 0,
+                 "rmbx_conv2d_nhwc: bad geometry");
+  RMBX_CHECK_ARG(Cin % rmbx::CBK == 0, "rmbx_conv2d_nhwc: Cin=%d must be a multiple of %d", Cin, rmbx::CBK);
+  RMBX_CHECK_ARG(Cout % rmbx::CBN == 0, "rmbx_conv2d_nhwc: Cout=%d must be a multiple of %d", Cout, rmbx::CBN);
+  RMBX_CHECK_ARG((((uintptr_t)in | (uintptr_t)weight) & 15) == 0, "rmbx_conv2d_nhwc: in/weight must be 16-byte aligned");
+  const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
+  RMBX_CHECK_ARG(Ho > 0 && Wo > 0, "rmbx_conv2d_nhwc: empty output");
+  if (N == 0) return RMBX_OK;
+  rmbx::ConvArgs a;
+  a.in = (const uint16_t*)in;
+  a.w = (const uint16_t*)weight;
+  a.bias = bias;
+  a.res = (const uint16_t*)residual;
+  a.out = (uint16_t*)out;
+  a.N = N;
+  a.H = H;
+  a.W = W;
+  a.Cin = Cin;
+  a.Ho = Ho;
+  a.Wo = Wo;
+  a.Cout = Cout;
+  a.KH = KH;
+  a.KW = KW;
+  a.stride = stride;
+  a.pad = pad;
+  a.relu = relu;
+  a.M = (long long)N * Ho * Wo;
+  a.n_ntiles = Cout / rmbx::CBN;
+  a.n_mtiles = (a.M + rmbx::CBM - 1) / rmbx::CBM;
+  const long long nblocks = a.n_mtiles * a.n_ntiles;
+  RMBX_CHECK_ARG(nblocks < (1ll << 31), "rmbx_conv2d_nhwc: grid too large");
+  hipLaunchKernelGGL(rmbx::conv_nhwc_kernel, dim3((unsigned)nblocks), dim3(256), 0, (hipStream_t)stream, a);
+  RMBX_CHECK_LAUNCH();
+  return RMBX_OK;
+}

@@ -344,3 +344,29 @@ def add_layernorm(x, r, weight, bias, eps=1e-5, out=None):
     N.call("rmbx_add_layernorm", N.ptr(x), N.ptr(r), N.ptr(weight), N.ptr(bias), N.ptr(out), x.numel() // D, D,
            float(eps), _NN_DTYPES[x.dtype], N.stream_ptr())
     return out
+
+
+def conv2d_nhwc(x, weight, bias, stride=1, padding=0, relu=False, res=None):
+    """relu?(conv2d(x, weight) + bias + res) by rmbx_conv2d_nhwc: x bf16 channels_last
+    [N, Cin, H, W], weight bf16 channels_last [Cout, Cin, KH, KW], bias f32 [Cout], res bf16
+    channels_last [N, Cout, Ho, Wo] or None -> bf16 channels_last [N, Cout, Ho, Wo]."""
+    _chk_nhwc(x, "x")
+    if x.dtype != torch.bfloat16 or weight.dtype != torch.bfloat16:
+        raise ValueError("conv2d_nhwc is bf16 only")
+    if weight.dim() != 4 or not weight.is_contiguous(memory_format=torch.channels_last):
+        raise ValueError("weight must be a channels_last [Cout, Cin, KH, KW] tensor")
+    n, cin, H, W = x.shape
+    cout, cin_w, kh, kw = weight.shape
+    if cin_w != cin:
+        raise ValueError("weight/input channel mismatch")
+    _chk(bias, torch.float32, (cout,), "bias")
+    ho = (H + 2 * padding - kh) // stride + 1
+    wo = (W + 2 * padding - kw) // stride + 1
+    out = torch.empty((n, cout, ho, wo), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+    if res is not None:
+        _chk_nhwc(res, "res")
+        if tuple(res.shape) != tuple(out.shape) or res.dtype != torch.bfloat16:
+            raise ValueError("res must match the output")
+    N.call("rmbx_conv2d_nhwc", N.ptr(x), N.ptr(weight), N.ptr(bias), N.ptr(res), N.ptr(out), n, H, W, cin, cout,
+           kh, kw, int(stride), int(padding), int(bool(relu)), N.stream_ptr())
+    return out

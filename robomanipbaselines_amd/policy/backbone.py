@@ -103,6 +103,11 @@ class _FusedConv(nn.Module):
         y = self.conv_nobias(x)
         return K.nhwc_bias_act(y, self.bias_f32(), relu=self.relu, out=y)
 
+    def rmbx(self, x, relu, res=None):
+        """conv + bias (+ res) (+ ReLU) in one rmbx implicit-GEMM launch (bf16)."""
+        c = self.conv
+        return K.conv2d_nhwc(x, c.weight, self.bias_f32(), c.stride[0], c.padding[0], relu=relu, res=res)
+
 
 class _FusedBlock(nn.Module):
     def __init__(self, blk):
@@ -111,7 +116,16 @@ class _FusedBlock(nn.Module):
         self.c2 = _FusedConv(blk.conv2, blk.bn2, False)
         self.down = None if blk.downsample is None else _FusedConv(blk.downsample[0], blk.downsample[1], False)
 
+    # rmbx implicit-GEMM convs where they beat MIOpen + epilogue on MI355X (scripts/prof_conv.py:
+    # the 64-channel layer1 convs, 3.7 vs 3.9 ms at 1024 envs); MIOpen's tuned solvers win on the
+    # wider layers for now
+    RMBX_CONV_CHANNELS = (64,)
+
     def forward(self, x):
+        if x.dtype == torch.bfloat16 and x.shape[1] in self.RMBX_CONV_CHANNELS and self.down is None:
+            y = self.c1.rmbx(x, relu=True)
+            idt = x if self.down is None else self.down.rmbx(x, relu=False)
+            return self.c2.rmbx(y, relu=True, res=idt)
         y = self.c1(x)
         z = self.c2.conv_nobias(y)
         if self.down is None:
@@ -122,8 +136,9 @@ class _FusedBlock(nn.Module):
 
 class FusedResNet18Trunk(nn.Module):
     """Inference form on the device: BN folded into conv weights/bias, channels_last
-    activations, conv (MIOpen) + one rmbx HIP epilogue per conv (bias / residual / ReLU, and the
-    stem's max-pool).  Same function as ResNet18Trunk; bit-identical to the unfused storage-dtype
+    activations.  bf16: the block convs are rmbx MFMA implicit-GEMM kernels with bias / residual /
+    ReLU fused (rmbx_conv2d_nhwc); the 3-channel 7x7 stem is MIOpen + the rmbx bias/ReLU/max-pool
+    epilogue.  f32: MIOpen convs + one rmbx HIP epilogue per conv.  Same function as ResNet18Trunk; bit-identical to the unfused storage-dtype
     sequence on the same conv outputs (tests/test_nn_gpu.py)."""
 
     def __init__(self, trunk):

@@ -96,6 +96,33 @@ def test_fused_trunk_fp32_matches_reference():
     assert err <= 1e-3 * max(1.0, want.abs().max().item()), err
 
 
+@pytest.mark.parametrize("cin,cout,k,stride,res,relu", [(64, 64, 3, 1, True, True), (64, 128, 3, 2, False, True),
+                                                       (64, 128, 1, 2, False, False), (128, 128, 3, 1, True, True),
+                                                       (256, 512, 3, 2, False, False)])
+@torch.no_grad()
+def test_conv2d_nhwc_matches_fp32(cin, cout, k, stride, res, relu):
+    """rmbx implicit-GEMM conv (bf16 in, f32 accumulate, fused bias/residual/ReLU, one bf16
+    rounding) vs F.conv2d in fp32 on the same bf16 operands: within one bf16 rounding."""
+    from robomanipbaselines_amd import kernels as K
+
+    g = torch.Generator(device=DEV).manual_seed(cin + cout + k)
+    x = _cl(torch.randn(3, cin, 17, 23, device=DEV, generator=g).to(torch.bfloat16))
+    w = _cl((torch.randn(cout, cin, k, k, device=DEV, generator=g) / (cin * k * k) ** 0.5).to(torch.bfloat16))
+    b = torch.randn(cout, device=DEV, generator=g).to(torch.bfloat16).float()
+    pad = k // 2
+    ref = F.conv2d(x.float(), w.float(), b, stride, pad)
+    r = None
+    if res:
+        r = _cl(torch.randn(ref.shape, device=DEV, generator=g).to(torch.bfloat16))
+        ref = ref + r.float()
+    if relu:
+        ref = F.relu(ref)
+    got = K.conv2d_nhwc(x, w, b, stride, pad, relu=relu, res=r)
+    assert got.shape == ref.shape and got.is_contiguous(memory_format=torch.channels_last)
+    err = (got.float() - ref).abs()
+    assert (err <= 2 ** -8 * ref.abs() + 1e-3).all(), err.max().item()
+
+
 @torch.no_grad()
 def test_fused_trunk_bf16_epilogues_equal_unfused_sequence():
     """Walk the trunk with each conv evaluated ONCE; the HIP epilogues and the torch ops applied
@@ -105,6 +132,7 @@ def test_fused_trunk_bf16_epilogues_equal_unfused_sequence():
     from robomanipbaselines_amd import kernels as K
 
     x = _cl(torch.rand(2, 3, 96, 128, device=DEV).to(torch.bfloat16))
+    # (the MIOpen + rmbx-epilogue form, which the f32 trunk and the stem use)
     s = fused.stem.conv_nobias(x)
     h = K.nhwc_bias_relu_maxpool(s, fused.stem.bias_f32())
     assert torch.equal(h, F.max_pool2d(_torch_epilogue(s, fused.stem.bias_f32()), 3, 2, 1))
