@@ -197,7 +197,9 @@ int rmbx_arm_fk(const double* placement, const double* q, double* R_out, double*
  * Outputs (each optional): rgb u8 [n][H][W][3]; depth f32 [n][H][W] (linear camera-z distance,
  * the quantity MujocoEnvBase.py:122-125 recovers); policy tensor [n][3][H][W] in bf16 (dtype 1)
  * or f32 (dtype 0) = ((u8 / 255) - mean[c]) / std[c] (RolloutBase.py:479-490 + ImageNet
- * normalisation of the ACT/MLP backbones).
+ * normalisation of the ACT/MLP backbones), or (dtype 2) the same values in bf16 as a 2x2
+ * space-to-depth image [n][H/2][W/2][16] (channel (dy*2+dx)*3+c, 12..15 zero) for
+ * rmbx_stem_s2d_conv (H, W even).
  * ------------------------------------------------------------------------------------------- */
 typedef struct rmbx_camera {
   int32_t body;        /* body the camera is attached to (0 = world) */
@@ -236,6 +238,12 @@ int rmbx_nhwc_bias_act(const void* x, const float* bias, const void* res, const 
 int rmbx_conv2d_nhwc(const void* in, const void* weight, const float* bias, const void* residual,
                      void* out, int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
                      int pad, int relu, void* stream);
+/* ResNet stem on a 2x2 space-to-depth image: in [N][Hs][Ws][16] bf16 (channel (dy*2+dx)*3+c,
+ * 12..15 zero; rmbx_render policy_dtype 2 writes this layout), weight packed [Cout][4][4][16] bf16
+ * (the 7x7 / stride-2 / pad-3 conv1 re-indexed), out [N][Hs][Ws][Cout] bf16 = relu?(conv + bias).
+ * Replaces conv1 -> BN -> ReLU of the backbone's stem (max-pool: rmbx_nhwc_bias_relu_maxpool). */
+int rmbx_stem_s2d_conv(const void* in, const void* weight, const float* bias, void* out, int N, int Hs,
+                       int Ws, int Cout, int relu, void* stream);
 /* Residual add + LayerNorm over the last dim of [rows][D] rows (D <= 2048, multiple of 8 bf16 / 4
  * f32): out = LayerNorm(rnd(x + r)) * weight + bias (f32 weight/bias), r optional (NULL); replaces
  * the add + nn.LayerNorm pair of the ACT transformer's post-norm layers (third_party/act). */

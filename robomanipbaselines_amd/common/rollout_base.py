@@ -142,14 +142,18 @@ class BatchedRolloutBase:
     image_norm = ((0.0, 0.0, 0.0), (1.0, 1.0, 1.0))
 
     def get_images(self, dtype):
-        """Render every policy camera straight into the normalised policy tensor [n,ncam,3,H,W]."""
+        """Render every policy camera straight into the normalised policy tensor [n,ncam,3,H,W]
+        (or, for a bf16 device policy that accepts it, the space-to-depth form
+        [n,ncam,H/2,W/2,16] its stem kernel reads)."""
         H, W = self.env.renderer.height, self.env.renderer.width
         mean, std = self.image_norm
-        if getattr(self, "_img", None) is None or self._img.dtype != dtype:
-            self._img = torch.empty((self.n, len(self.camera_names), 3, H, W), dtype=dtype, device=self.device)
-            self._img_cam = [torch.empty((self.n, 3, H, W), dtype=dtype, device=self.device) for _ in self.camera_names]
+        s2d = dtype == torch.bfloat16 and getattr(self.policy, "accepts_s2d", False) and H % 2 == 0 and W % 2 == 0
+        shape = (H // 2, W // 2, 16) if s2d else (3, H, W)
+        if getattr(self, "_img", None) is None or self._img.dtype != dtype or tuple(self._img.shape[2:]) != shape:
+            self._img = torch.empty((self.n, len(self.camera_names)) + shape, dtype=dtype, device=self.device)
+            self._img_cam = [torch.empty((self.n,) + shape, dtype=dtype, device=self.device) for _ in self.camera_names]
         if len(self.camera_names) == 1:
-            self.env.render_images(self.camera_names[0], policy=self._img.view(self.n, 3, H, W), mean=mean, std=std)
+            self.env.render_images(self.camera_names[0], policy=self._img.view((self.n,) + shape), mean=mean, std=std)
             return self._img
         for i, cam in enumerate(self.camera_names):
             self.env.render_images(cam, policy=self._img_cam[i], mean=mean, std=std)

@@ -48,6 +48,13 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   return (uint16_t)(u >> 16);
 }
 
+// MODE 0: KH x KW conv over [N][H][W][Cin], K step = one tap x 64 channels.
+// MODE 1: the ResNet stem (7x7 / stride 2 / pad 3 over 3 channels) on a 2x2 space-to-depth
+//   image [N][H/2][W/2][16] (channel (dy*2+dx)*3+c, 12..15 zero): a 4x4 / stride 1 conv with
+//   pad 2 (before) whose K step is one filter row ky = 4 taps x 16 channels, i.e. the 64
+//   contiguous values of s2d pixels X = ox-2 .. ox+1 of row Y = oy+ky-2; weights packed
+//   [Cout][ky][kx][16] on the host.
+template <int MODE>
 __global__ void __launch_bounds__(256) conv_nhwc_kernel(ConvArgs a) {
   __shared__ __attribute__((aligned(16))) uint16_t sA[CBM * CLD];
   __shared__ __attribute__((aligned(16))) uint16_t sB[CBN * CLD];
@@ -84,11 +91,18 @@ __global__ void __launch_bounds__(256) conv_nhwc_kernel(ConvArgs a) {
   uint4 ra0, ra1, ra2, ra3, rb0, rb1;
   int kh_ = 0, kw_ = 0, c0_ = 0;
 #define RMBX_A_LOAD(I, DST)                                                                              \
-  {                                                                                                      \
+  if (MODE == 0) {                                                                                       \
     const int h_ = ph[I] + kh_, w_ = pw[I] + kw_;                                                        \
     DST = (pv[I] && h_ >= 0 && h_ < a.H && w_ >= 0 && w_ < a.W)                                          \
               ? *reinterpret_cast<const uint4*>(a.in + (((size_t)pn[I] * a.H + h_) * a.W + w_) * a.Cin + c0_ + \
                                                 ((tid + 256 * (I)) & 7) * 8)                             \
+              : make_uint4(0, 0, 0, 0);                                                                  \
+  } else {                                                                                               \
+    const int part_ = (tid + 256 * (I)) & 7;                                                             \
+    const int h_ = ph[I] + kh_, w_ = pw[I] + (part_ >> 1);                                               \
+    DST = (pv[I] && h_ >= 0 && h_ < a.H && w_ >= 0 && w_ < a.W)                                          \
+              ? *reinterpret_cast<const uint4*>(a.in + (((size_t)pn[I] * a.H + h_) * a.W + w_) * 16 +    \
+                                                (part_ & 1) * 8)                                         \
               : make_uint4(0, 0, 0, 0);                                                                  \
   }
 #define RMBX_B_LOAD(I, DST)                                                                              \
@@ -200,7 +214,42 @@ extern "C" int rmbx_conv2d_nhwc(const void* in, const void* weight, const float*
   a.n_mtiles = (a.M + rmbx::CBM - 1) / rmbx::CBM;
   const long long nblocks = a.n_mtiles * a.n_ntiles;
   RMBX_CHECK_ARG(nblocks < (1ll << 31), "rmbx_conv2d_nhwc: grid too large");
-  hipLaunchKernelGGL(rmbx::conv_nhwc_kernel, dim3((unsigned)nblocks), dim3(256), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(rmbx::conv_nhwc_kernel<0>, dim3((unsigned)nblocks), dim3(256), 0, (hipStream_t)stream, a);
+  RMBX_CHECK_LAUNCH();
+  return RMBX_OK;
+}
+
+extern "C" int rmbx_stem_s2d_conv(const void* in, const void* weight, const float* bias, void* out, int N, int Hs,
+                                  int Ws, int Cout, int relu, void* stream) {
+  RMBX_CHECK_ARG(in && weight && bias && out, "rmbx_stem_s2d_conv: null pointer");
+  RMBX_CHECK_ARG(N >= 0 && Hs > 0 && Ws > 0, "rmbx_stem_s2d_conv: bad geometry");
+  RMBX_CHECK_ARG(Cout % rmbx::CBN == 0, "rmbx_stem_s2d_conv: Cout=%d must be a multiple of %d", Cout, rmbx::CBN);
+  RMBX_CHECK_ARG((((uintptr_t)in | (uintptr_t)weight) & 15) == 0, "rmbx_stem_s2d_conv: unaligned");
+  if (N == 0) return RMBX_OK;
+  rmbx::ConvArgs a;
+  a.in = (const uint16_t*)in;
+  a.w = (const uint16_t*)weight;
+  a.bias = bias;
+  a.res = nullptr;
+  a.out = (uint16_t*)out;
+  a.N = N;
+  a.H = Hs;
+  a.W = Ws;
+  a.Cin = 64;  // K step = one filter row: 4 taps x 16 channels
+  a.Ho = Hs;
+  a.Wo = Ws;
+  a.Cout = Cout;
+  a.KH = 4;
+  a.KW = 1;
+  a.stride = 1;
+  a.pad = 2;
+  a.relu = relu;
+  a.M = (long long)N * Hs * Ws;
+  a.n_ntiles = Cout / rmbx::CBN;
+  a.n_mtiles = (a.M + rmbx::CBM - 1) / rmbx::CBM;
+  const long long nblocks = a.n_mtiles * a.n_ntiles;
+  RMBX_CHECK_ARG(nblocks < (1ll << 31), "rmbx_stem_s2d_conv: grid too large");
+  hipLaunchKernelGGL(rmbx::conv_nhwc_kernel<1>, dim3((unsigned)nblocks), dim3(256), 0, (hipStream_t)stream, a);
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
 }

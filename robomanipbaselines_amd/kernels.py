@@ -370,3 +370,46 @@ def conv2d_nhwc(x, weight, bias, stride=1, padding=0, relu=False, res=None):
     N.call("rmbx_conv2d_nhwc", N.ptr(x), N.ptr(weight), N.ptr(bias), N.ptr(res), N.ptr(out), n, H, W, cin, cout,
            kh, kw, int(stride), int(padding), int(bool(relu)), N.stream_ptr())
     return out
+
+
+def pack_stem_s2d(weight):
+    """conv1 weight [Cout, 3, 7, 7] -> [Cout, 4, 4, 16] for rmbx_stem_s2d_conv:
+    W'[co][ky][kx][(dy*2+dx)*3+c] = W[co][c][2ky+dy-1][2kx+dx-1] (0 outside the 7x7 window)."""
+    cout = weight.shape[0]
+    w = torch.zeros((cout, 4, 4, 16), dtype=weight.dtype, device=weight.device)
+    for ky in range(4):
+        for dy in range(2):
+            kh = 2 * ky + dy - 1
+            if not 0 <= kh < 7:
+                continue
+            for kx in range(4):
+                for dx in range(2):
+                    kw = 2 * kx + dx - 1
+                    if not 0 <= kw < 7:
+                        continue
+                    ch = (dy * 2 + dx) * 3
+                    w[:, ky, kx, ch:ch + 3] = weight[:, :, kh, kw]
+    return w.contiguous()
+
+
+def image_to_s2d(img):
+    """[n, 3, H, W] -> [n, H/2, W/2, 16] space-to-depth layout of rmbx_render policy_dtype 2."""
+    n, c, H, W = img.shape
+    x = img.reshape(n, c, H // 2, 2, W // 2, 2).permute(0, 2, 4, 3, 5, 1).reshape(n, H // 2, W // 2, 12)
+    return torch.cat([x, x.new_zeros(n, H // 2, W // 2, 4)], dim=-1).contiguous()
+
+
+def stem_s2d_conv(x_s2d, w_packed, bias, relu=True):
+    """relu?(conv1(x) + bias) for the space-to-depth image: [n, Hs, Ws, 16] bf16 ->
+    channels_last [n, Cout, Hs, Ws] bf16 (rmbx_stem_s2d_conv)."""
+    _chk(x_s2d, torch.bfloat16, name="x_s2d")
+    n, Hs, Ws, c16 = x_s2d.shape
+    if c16 != 16:
+        raise ValueError("x_s2d must be [n, Hs, Ws, 16]")
+    cout = w_packed.shape[0]
+    _chk(w_packed, torch.bfloat16, (cout, 4, 4, 16), "w_packed")
+    _chk(bias, torch.float32, (cout,), "bias")
+    out = torch.empty((n, cout, Hs, Ws), dtype=torch.bfloat16, device=x_s2d.device, memory_format=torch.channels_last)
+    N.call("rmbx_stem_s2d_conv", N.ptr(x_s2d), N.ptr(w_packed), N.ptr(bias), N.ptr(out), n, Hs, Ws, cout,
+           int(bool(relu)), N.stream_ptr())
+    return out

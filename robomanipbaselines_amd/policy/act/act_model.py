@@ -135,7 +135,8 @@ class DecoderLayer(_LayerOps):
 
 
 class ActModel(nn.Module):
-    """DETRVAE inference path. forward(qpos [B,S], image [B,ncam,3,H,W] normalised) -> [B,Q,A]."""
+    """DETRVAE inference path. forward(qpos [B,S], image [B,ncam,3,H,W] normalised, or the
+    space-to-depth form [B,ncam,H/2,W/2,16] on the device) -> [B,Q,A]."""
 
     def __init__(self, state_dim=7, action_dim=7, num_queries=100, hidden_dim=512, dim_feedforward=3200,
                  nheads=8, enc_layers=4, dec_layers=7, num_cams=1, latent_dim=32):
@@ -173,15 +174,25 @@ class ActModel(nn.Module):
             self._pos_cache[key] = sine_pos_embed(h, w, self.input_proj.out_channels // 2, device=device, dtype=dtype)
         return self._pos_cache[key]
 
+    @property
+    def accepts_s2d(self):
+        """The device inference form also takes the renderer's space-to-depth images
+        [B, ncam, H/2, W/2, 16] (bf16) and runs the stem as an rmbx MFMA kernel."""
+        return self._fused is not None
+
     def forward(self, qpos, image):
         B = qpos.shape[0]
         trunk = self._fused if self._fused is not None else self.backbone
+        s2d = image.dim() == 5 and image.shape[-1] == 16
         feats, poss = [], []
         for c in range(image.shape[1]):
             x = image[:, c]
-            if self._fused is not None:
-                x = x.contiguous(memory_format=torch.channels_last)
-            f = self.input_proj(trunk(x))  # [B, d, h, w]
+            if s2d:
+                f = self.input_proj(trunk.forward_s2d(x.contiguous()))
+            else:
+                if self._fused is not None:
+                    x = x.contiguous(memory_format=torch.channels_last)
+                f = self.input_proj(trunk(x))  # [B, d, h, w]
             feats.append(f)
             poss.append(self._pos(f.shape[2], f.shape[3], f.device, f.dtype))
         src = torch.cat(feats, dim=3).flatten(2).transpose(1, 2)  # [B, hw, d]

@@ -152,3 +152,16 @@ class FusedResNet18Trunk(nn.Module):
     def forward(self, x):
         s = self.stem.conv_nobias(x)
         return self.blocks(K.nhwc_bias_relu_maxpool(s, self.stem.bias_f32()))
+
+    def forward_s2d(self, x_s2d):
+        """Same function on the renderer's 2x2 space-to-depth image [B, H/2, W/2, 16] (bf16):
+        the stem runs as an rmbx MFMA implicit GEMM (rmbx_stem_s2d_conv, bias + ReLU fused),
+        then the max-pool."""
+        w = self.stem.conv.weight
+        key = (w.data_ptr(), w.dtype)
+        if getattr(self, "_s2d_key", None) != key:
+            self._s2d_w = K.pack_stem_s2d(w.detach())
+            self._s2d_zero = torch.zeros(w.shape[0], dtype=torch.float32, device=w.device)
+            self._s2d_key = key
+        s = K.stem_s2d_conv(x_s2d, self._s2d_w, self.stem.bias_f32(), relu=True)
+        return self.blocks(K.nhwc_bias_relu_maxpool(s, self._s2d_zero))

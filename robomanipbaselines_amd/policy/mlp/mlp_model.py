@@ -61,10 +61,17 @@ class MlpModel(nn.Module):
             self._fused._apply(fn, *args, **kwargs)
         return self
 
+    @property
+    def accepts_s2d(self):
+        return self._fused is not None
+
     def image_features(self, x):
-        """[B, 3, H, W] in [0, 1] -> [B, 512]."""
+        """[B, 3, H, W] in [0, 1] (or the space-to-depth form [B, H/2, W/2, 16]) -> [B, 512]."""
         if self._fused is not None:
-            f = self._fused(x.contiguous(memory_format=torch.channels_last))
+            if x.shape[-1] == 16 and x.dim() == 4:
+                f = self._fused.forward_s2d(x.contiguous())
+            else:
+                f = self._fused(x.contiguous(memory_format=torch.channels_last))
             return f.float().mean(dim=(2, 3)).to(f.dtype)
         return self.image_feature_extractor(x).flatten(1)
 

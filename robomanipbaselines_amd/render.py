@@ -83,9 +83,13 @@ class Renderer:
             assert depth.dtype == torch.float32 and tuple(depth.shape) == (n, H, W) and depth.is_contiguous()
         pdt = 0
         if policy is not None:
-            assert tuple(policy.shape) == (n, 3, H, W) and policy.is_contiguous()
-            assert policy.dtype in (torch.float32, torch.bfloat16)
-            pdt = 1 if policy.dtype == torch.bfloat16 else 0
+            assert policy.is_contiguous() and policy.dtype in (torch.float32, torch.bfloat16)
+            if tuple(policy.shape) == (n, H // 2, W // 2, 16):  # space-to-depth stem input
+                assert policy.dtype == torch.bfloat16
+                pdt = 2
+            else:
+                assert tuple(policy.shape) == (n, 3, H, W)
+                pdt = 1 if policy.dtype == torch.bfloat16 else 0
         N.call("rmbx_render", ctypes.byref(cam), N.ptr(self.prim_i32), N.ptr(self.prim_f32), self.nprim,
                N.ptr(engine.gxpos), N.ptr(engine.gxmat), N.ptr(engine.xpos), N.ptr(engine.xquat),
                engine.ngeom, engine.nbody, N.ptr(rgb), N.ptr(depth), N.ptr(policy), pdt, N.ptr(active), n,

@@ -197,3 +197,44 @@ def test_act_device_inference_form_matches_fp32_reference():
     got = dev(q.to(DEV), img.to(DEV)).cpu()
     assert got.shape == (2, 100, 7)
     assert (got - want).abs().max().item() <= 2e-3 * max(1.0, want.abs().max().item())
+
+
+@torch.no_grad()
+def test_stem_s2d_conv_matches_fp32():
+    from robomanipbaselines_amd import kernels as K
+
+    g = torch.Generator(device=DEV).manual_seed(7)
+    x = torch.randn(2, 3, 48, 64, device=DEV, generator=g).to(torch.bfloat16)
+    w = (torch.randn(64, 3, 7, 7, device=DEV, generator=g) * 0.1).to(torch.bfloat16)
+    b = torch.randn(64, device=DEV, generator=g)
+    ref = F.relu(F.conv2d(x.float(), w.float(), b, 2, 3))
+    got = K.stem_s2d_conv(K.image_to_s2d(x), K.pack_stem_s2d(w), b)
+    assert got.shape == ref.shape == (2, 64, 24, 32)
+    err = (got.float() - ref).abs()
+    assert (err <= 2 ** -8 * ref.abs() + 1e-3).all(), err.max().item()
+
+
+@torch.no_grad()
+def test_trunk_s2d_matches_standard_layout():
+    ref, fused = _trunk_pair(3)
+    fused = fused.to(DEV, torch.bfloat16).to(memory_format=torch.channels_last)
+    from robomanipbaselines_amd import kernels as K
+
+    x = torch.rand(2, 3, 96, 128, device=DEV).to(torch.bfloat16)
+    a = fused(_cl(x)).float()
+    b = fused.forward_s2d(K.image_to_s2d(x)).float()
+    assert (a - b).norm() / a.norm() < 2e-2
+
+
+def test_render_s2d_layout_equals_standard():
+    from robomanipbaselines_amd import kernels as K
+    from robomanipbaselines_amd.envs.ur5e_cable import BatchedMujocoUR5eCableEnv
+
+    env = BatchedMujocoUR5eCableEnv(3, DEV)
+    env.reset()
+    H, W = env.renderer.height, env.renderer.width
+    std = torch.empty((3, 3, H, W), dtype=torch.bfloat16, device=DEV)
+    s2d = torch.empty((3, H // 2, W // 2, 16), dtype=torch.bfloat16, device=DEV)
+    env.render_images("front", policy=std)
+    env.render_images("front", policy=s2d)
+    assert torch.equal(K.image_to_s2d(std), s2d)
