@@ -54,10 +54,62 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
 //   pad 2 (before) whose K step is one filter row ky = 4 taps x 16 channels, i.e. the 64
 //   contiguous values of s2d pixels X = ox-2 .. ox+1 of row Y = oy+ky-2; weights packed
 //   [Cout][ky][kx][16] on the host.
+constexpr int EPI_LD = 68;  // f32 row stride of the epilogue image [128 pixels][64 channels]
+constexpr int GEN_LDS = (CBM * CLD + CBN * CLD) > (CBM * EPI_LD * 2) ? (CBM * CLD + CBN * CLD) : (CBM * EPI_LD * 2);
+
+// epilogue shared by the conv kernels: the 128 x 64 f32 accumulator tile is written to LDS as
+// [pixel][channel], then each thread finishes 8 consecutive channels of a pixel (bias, residual,
+// ReLU) with 16-byte NHWC loads/stores.  out_off(pix) = element offset of the pixel's channel 0
+// (or -1 when outside the output).
+template <class OFF>
+__device__ __forceinline__ void conv_epilogue(const ConvArgs& a, float* sC, const f32x16& acc0, const f32x16& acc1,
+                                              int n0, OFF out_off) {
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int col = lane & 31;
+  __syncthreads();
+#pragma unroll
+  for (int j = 0; j < 16; ++j) {
+    const int row = 32 * wave + (j & 3) + 8 * (j >> 2) + 4 * (lane >> 5);
+    sC[row * EPI_LD + col] = acc0[j];
+    sC[row * EPI_LD + 32 + col] = acc1[j];
+  }
+  __syncthreads();
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int q = tid + 256 * i;
+    const int pix = q >> 3, c8 = (q & 7) * 8;
+    const long long base = out_off(pix);
+    if (base < 0) continue;
+    const size_t o = (size_t)base + n0 + c8;
+    float v[8];
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = sC[pix * EPI_LD + c8 + k] + a.bias[n0 + c8 + k];
+    if (a.res) {
+      const uint4 rv = *reinterpret_cast<const uint4*>(a.res + o);
+      const uint32_t w4[4] = {rv.x, rv.y, rv.z, rv.w};
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        v[2 * k] += bf2f((uint16_t)(w4[k] & 0xffff));
+        v[2 * k + 1] += bf2f((uint16_t)(w4[k] >> 16));
+      }
+    }
+    if (a.relu)
+#pragma unroll
+      for (int k = 0; k < 8; ++k) v[k] = v[k] > 0.f ? v[k] : 0.f;
+    uint4 ov;
+    ov.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+    ov.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+    ov.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+    ov.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+    *reinterpret_cast<uint4*>(a.out + o) = ov;
+  }
+}
+
 template <int MODE>
 __global__ void __launch_bounds__(256) conv_nhwc_kernel(ConvArgs a) {
-  __shared__ __attribute__((aligned(16))) uint16_t sA[CBM * CLD];
-  __shared__ __attribute__((aligned(16))) uint16_t sB[CBN * CLD];
+  __shared__ __attribute__((aligned(16))) uint16_t smem[GEN_LDS];
+  uint16_t* sA = smem;
+  uint16_t* sB = smem + CBM * CLD;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
 
   // block -> (pixel tile, channel tile); pixel tiles in contiguous ranges per XCD
@@ -155,26 +207,95 @@ __global__ void __launch_bounds__(256) conv_nhwc_kernel(ConvArgs a) {
 #undef RMBX_A_LOAD
 #undef RMBX_B_LOAD
 
-  // epilogue: C[row = pixel][col = channel], col = lane & 31, row = (j & 3) + 8 (j >> 2) + 4 (lane >> 5)
-  const int col = lane & 31;
-#pragma unroll
-  for (int t = 0; t < 2; ++t) {
-    const int co = n0 + 32 * t + col;
-    const float bco = a.bias[co];
-#pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int row = (j & 3) + 8 * (j >> 2) + 4 * (lane >> 5);
-      const long long m = m0 + 32 * wave + row;
-      if (m >= a.M) continue;
-      float v = (t == 0 ? acc0[j] : acc1[j]) + bco;
-      const size_t o = (size_t)m * a.Cout + co;
-      if (a.res) v += bf2f(a.res[o]);
-      if (a.relu) v = v > 0.f ? v : 0.f;
-      a.out[o] = f2bf(v);
-    }
-  }
+  conv_epilogue(a, reinterpret_cast<float*>(smem), acc0, acc1, n0, [&](int pix) -> long long {
+    const long long m = m0 + pix;
+    return m < a.M ? m * a.Cout : -1;
+  });
 }
 #undef RMBX_CONV_LOAD
+
+
+// 3x3 / stride 1 / pad 1 conv with Cin = 64 k (the ResNet-18 stride-1 block convs): the block's
+// output tile is 8 rows x 16 columns of one image; per 64-channel chunk its 10 x 18 input patch
+// is loaded into LDS once and all 9 taps read their A fragments from it (the row-tiled kernel
+// re-reads the input once per tap); weights stream per tap through a small LDS tile.  Wave w
+// owns output rows 2w, 2w+1.  The epilogue transposes the accumulators through LDS so bias,
+// residual and ReLU are applied on 16-byte NHWC chunks.
+constexpr int PT_H = 8, PT_W = 16, PP_H = PT_H + 2, PP_W = PT_W + 2, PLD = 72;
+
+constexpr int PATCH_LDS = PP_H * PP_W * PLD + CBN * CLD;  // bf16 elements
+static_assert(PATCH_LDS >= CBM * EPI_LD * 2, "epilogue image must fit the patch + B tiles");
+
+__global__ void __launch_bounds__(256) conv3x3_c64_patch_kernel(ConvArgs a) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[PATCH_LDS];
+  uint16_t* sP = smem;
+  uint16_t* sB = smem + PP_H * PP_W * PLD;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tiles_x = (a.Wo + PT_W - 1) / PT_W, tiles_y = (a.Ho + PT_H - 1) / PT_H;
+  const long long nblk = (long long)gridDim.x;
+  long long b = blockIdx.x;
+  if ((nblk & 7) == 0) b = (b & 7) * (nblk >> 3) + (b >> 3);
+  const int nt = (int)(b % a.n_ntiles);
+  long long t = b / a.n_ntiles;
+  const int tx = (int)(t % tiles_x);
+  t /= tiles_x;
+  const int ty = (int)(t % tiles_y);
+  const int n = (int)(t / tiles_y);
+  const int oy0 = ty * PT_H, ox0 = tx * PT_W, n0 = nt * CBN;
+
+  const int r = lane & 31, h8 = 8 * (lane >> 5);
+  const int ly = 2 * wave + (r >> 4), lx = r & 15;  // this lane's A row = output pixel (ly, lx)
+  f32x16 acc0 = {}, acc1 = {};
+  uint4 rb0, rb1;
+  const int Cin = a.Cin;
+  auto ldb = [&](int kk, uint4& x0, uint4& x1) {  // kk = chunk * 9 + tap
+    const int ch = kk / 9, tap = kk - 9 * ch;
+    const int kh = tap / 3, kw = tap - 3 * kh;
+    const int q0 = tid, q1 = tid + 256;
+    x0 = *reinterpret_cast<const uint4*>(a.w + (((size_t)(n0 + (q0 >> 3)) * 3 + kh) * 3 + kw) * Cin + 64 * ch + (q0 & 7) * 8);
+    x1 = *reinterpret_cast<const uint4*>(a.w + (((size_t)(n0 + (q1 >> 3)) * 3 + kh) * 3 + kw) * Cin + 64 * ch + (q1 & 7) * 8);
+  };
+  const int KK = 9 * (Cin / 64);
+  ldb(0, rb0, rb1);
+  for (int kk = 0; kk < KK; ++kk) {
+    const int tap = kk % 9;
+    if (tap == 0) {
+      // input patch rows oy0-1 .. oy0+8, cols ox0-1 .. ox0+16, channels of chunk kk / 9
+      __syncthreads();
+      const int c0 = 64 * (kk / 9);
+      for (int q = tid; q < PP_H * PP_W * 8; q += 256) {
+        const int pix = q >> 3, part = q & 7;
+        const int py = pix / PP_W, px = pix - py * PP_W;
+        const int h = oy0 - 1 + py, w = ox0 - 1 + px;
+        uint4 v = make_uint4(0, 0, 0, 0);
+        if (h >= 0 && h < a.H && w >= 0 && w < a.W)
+          v = *reinterpret_cast<const uint4*>(a.in + (((size_t)n * a.H + h) * a.W + w) * Cin + c0 + part * 8);
+        *reinterpret_cast<uint4*>(sP + pix * PLD + part * 8) = v;
+      }
+    }
+    __syncthreads();
+    *reinterpret_cast<uint4*>(sB + (tid >> 3) * CLD + (tid & 7) * 8) = rb0;
+    *reinterpret_cast<uint4*>(sB + ((tid + 256) >> 3) * CLD + (tid & 7) * 8) = rb1;
+    __syncthreads();
+    if (kk + 1 < KK) ldb(kk + 1, rb0, rb1);
+    const int kh = tap / 3, kw = tap - 3 * kh;
+    const uint16_t* arow = sP + ((ly + kh) * PP_W + (lx + kw)) * PLD + h8;
+    const uint16_t* brow0 = sB + r * CLD + h8;
+    const uint16_t* brow1 = sB + (32 + r) * CLD + h8;
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const bf16x8 af = *reinterpret_cast<const bf16x8*>(arow + 16 * ks);
+      const bf16x8 b0 = *reinterpret_cast<const bf16x8*>(brow0 + 16 * ks);
+      const bf16x8 b1 = *reinterpret_cast<const bf16x8*>(brow1 + 16 * ks);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, b0, acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(af, b1, acc1, 0, 0, 0);
+    }
+  }
+  conv_epilogue(a, reinterpret_cast<float*>(smem), acc0, acc1, n0, [&](int pix) -> long long {
+    const int oy = oy0 + (pix >> 4), ox = ox0 + (pix & 15);
+    return (oy < a.Ho && ox < a.Wo) ? ((((long long)n * a.Ho + oy) * a.Wo + ox) * a.Cout) : -1;
+  });
+}
 
 }  // namespace
 }  // namespace rmbx
@@ -212,6 +333,14 @@ extern "C" int rmbx_conv2d_nhwc(const void* in, const void* weight, const float*
   a.M = (long long)N * Ho * Wo;
   a.n_ntiles = Cout / rmbx::CBN;
   a.n_mtiles = (a.M + rmbx::CBM - 1) / rmbx::CBM;
+  if (KH == 3 && KW == 3 && stride == 1 && pad == 1) {
+    const long long ntile = (long long)N * ((Ho + rmbx::PT_H - 1) / rmbx::PT_H) * ((Wo + rmbx::PT_W - 1) / rmbx::PT_W);
+    const long long nb = ntile * a.n_ntiles;
+    RMBX_CHECK_ARG(nb < (1ll << 31), "rmbx_conv2d_nhwc: grid too large");
+    hipLaunchKernelGGL(rmbx::conv3x3_c64_patch_kernel, dim3((unsigned)nb), dim3(256), 0, (hipStream_t)stream, a);
+    RMBX_CHECK_LAUNCH();
+    return RMBX_OK;
+  }
   const long long nblocks = a.n_mtiles * a.n_ntiles;
   RMBX_CHECK_ARG(nblocks < (1ll << 31), "rmbx_conv2d_nhwc: grid too large");
   hipLaunchKernelGGL(rmbx::conv_nhwc_kernel<0>, dim3((unsigned)nblocks), dim3(256), 0, (hipStream_t)stream, a);

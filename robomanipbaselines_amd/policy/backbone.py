@@ -116,13 +116,14 @@ class _FusedBlock(nn.Module):
         self.c2 = _FusedConv(blk.conv2, blk.bn2, False)
         self.down = None if blk.downsample is None else _FusedConv(blk.downsample[0], blk.downsample[1], False)
 
-    # rmbx implicit-GEMM convs where they beat MIOpen + epilogue on MI355X (scripts/prof_conv.py:
-    # the 64-channel layer1 convs, 3.7 vs 3.9 ms at 1024 envs); MIOpen's tuned solvers win on the
-    # wider layers for now
-    RMBX_CONV_CHANNELS = (64,)
+    # rmbx implicit-GEMM convs (fused epilogue) where they beat MIOpen + epilogue on MI355X
+    # (scripts/prof_conv.py, profiles/r1_prof_conv_v3.log: layer1 2.7 vs 4.0 ms, layer2 2.0 vs
+    # 2.6 ms per conv at 1024 envs); MIOpen's tuned solvers still win for the 256/512-channel
+    # layers
+    RMBX_CONV_MAX_COUT = 128
 
     def forward(self, x):
-        if x.dtype == torch.bfloat16 and x.shape[1] in self.RMBX_CONV_CHANNELS and self.down is None:
+        if x.dtype == torch.bfloat16 and self.c2.conv.out_channels <= self.RMBX_CONV_MAX_COUT:
             y = self.c1.rmbx(x, relu=True)
             idt = x if self.down is None else self.down.rmbx(x, relu=False)
             return self.c2.rmbx(y, relu=True, res=idt)

@@ -49,3 +49,16 @@ with torch.no_grad():
                     "miopen_conv_ms": round(t_c, 3), "rmbx_tflops": round(flop / t_r / 1e9, 1),
                     "miopen_tflops": round(flop / t_c / 1e9, 1)})
         print(json.dumps(out[-1]), flush=True)
+    # stem: 7x7/s2 over the 480x640 image (MIOpen on NCHW->NHWC) vs rmbx s2d kernel
+    img = torch.randn(B, 3, 480, 640, device=dev).to(torch.bfloat16)
+    w = (torch.randn(64, 3, 7, 7, device=dev) * 0.1).to(torch.bfloat16)
+    bias = torch.randn(64, device=dev)
+    x_cl = img.contiguous(memory_format=torch.channels_last)
+    w_cl = w.contiguous(memory_format=torch.channels_last)
+    s2d = K.image_to_s2d(img)
+    wp = K.pack_stem_s2d(w)
+    flop = 2.0 * B * 240 * 320 * 64 * 147
+    t_m = timeit(lambda: F.conv2d(x_cl, w_cl, None, 2, 3))
+    t_r = timeit(lambda: K.stem_s2d_conv(s2d, wp, bias))
+    print(json.dumps({"shape": "stem 7x7/2 3->64 480x640", "rmbx_s2d_ms": round(t_r, 3), "miopen_conv_ms": round(t_m, 3),
+                      "rmbx_tflops": round(flop / t_r / 1e9, 1), "miopen_tflops": round(flop / t_m / 1e9, 1)}), flush=True)
