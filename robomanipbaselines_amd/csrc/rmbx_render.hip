@@ -27,7 +27,8 @@ struct PrimCam {
   float s[3];    // size
   float rgb[3];
   int type;
-  float rad;  // bounding radius (0 = unbounded)
+  float rad;   // bounding radius (0 = unbounded)
+  float zmin;  // nearest possible hit depth (camera z) of the bounding sphere; -inf if unbounded
 };
 
 __device__ __forceinline__ float dot3f(const float* a, const float* b) {
@@ -198,16 +199,18 @@ struct RenderArgs {
   const uint8_t* active;
   int n_env;
   int tiles_x, tiles_y;
+  int groups;  // blocks per env (each renders a contiguous range of tiles)
 };
 
 __global__ void __launch_bounds__(256) render_kernel(RenderArgs a) {
   __shared__ PrimCam prims[MAX_PRIM];
   __shared__ int tile_list[MAX_PRIM];
+  __shared__ int tile_sorted[MAX_PRIM];
   __shared__ int tile_count;
   __shared__ CamFrame cf;
   const int ntiles = a.tiles_x * a.tiles_y;
-  const int env = blockIdx.x / ntiles;
-  const int tile = blockIdx.x % ntiles;
+  const int env = blockIdx.x / a.groups;
+  const int grp = blockIdx.x % a.groups;
   if (env >= a.n_env) return;
   if (a.active && !a.active[env]) return;
   const int tid = threadIdx.x;
@@ -225,16 +228,12 @@ __global__ void __launch_bounds__(256) render_kernel(RenderArgs a) {
     matvec3(Rb, a.cam.pos, t);
     for (int i = 0; i < 9; i++) cf.R[i] = (float)R[i];
     for (int i = 0; i < 3; i++) cf.p[i] = (float)(bp[i] + t[i]);
-    tile_count = 0;
   }
   __syncthreads();
-  const int tx0 = (tile % a.tiles_x) * RENDER_TILE, ty0 = (tile / a.tiles_x) * RENDER_TILE;
-  // tile frustum in normalised image coords
-  const float x_lo = (2.0f * tx0 / W - 1.0f) * tanh_ * aspect;
-  const float x_hi = (2.0f * (tx0 + RENDER_TILE) / W - 1.0f) * tanh_ * aspect;
-  const float y_hi = (1.0f - 2.0f * ty0 / H) * tanh_;
-  const float y_lo = (1.0f - 2.0f * (ty0 + RENDER_TILE) / H) * tanh_;
-  for (int p = tid; p < a.nprim && p < MAX_PRIM; p += blockDim.x) {
+  // the env's primitives in the camera frame, once per block (the block then renders a range
+  // of tiles of this env)
+  const int np = a.nprim < MAX_PRIM ? a.nprim : MAX_PRIM;
+  for (int p = tid; p < np; p += blockDim.x) {
     const int g = a.prim_i32[4 * p];
     const int type = a.prim_i32[4 * p + 1];
     const float* f = a.prim_f32 + 8 * p;
@@ -266,7 +265,24 @@ __global__ void __launch_bounds__(256) render_kernel(RenderArgs a) {
     else if (type == RMBX_GEOM_BOX)
       rad = sqrtf(f[0] * f[0] + f[1] * f[1] + f[2] * f[2]);
     P.rad = rad;
+    P.zmin = (type == RMBX_GEOM_PLANE || rad <= 0) ? -1e30f : (-P.c[2] - rad);
     prims[p] = P;
+  }
+  const int t_begin = (int)((long long)ntiles * grp / a.groups);
+  const int t_end = (int)((long long)ntiles * (grp + 1) / a.groups);
+  for (int tile = t_begin; tile < t_end; ++tile) {
+  if (tid == 0) tile_count = 0;
+  __syncthreads();
+  const int tx0 = (tile % a.tiles_x) * RENDER_TILE, ty0 = (tile / a.tiles_x) * RENDER_TILE;
+  // tile frustum in normalised image coords
+  const float x_lo = (2.0f * tx0 / W - 1.0f) * tanh_ * aspect;
+  const float x_hi = (2.0f * (tx0 + RENDER_TILE) / W - 1.0f) * tanh_ * aspect;
+  const float y_hi = (1.0f - 2.0f * ty0 / H) * tanh_;
+  const float y_lo = (1.0f - 2.0f * (ty0 + RENDER_TILE) / H) * tanh_;
+  for (int p = tid; p < np; p += blockDim.x) {
+    const PrimCam& P = prims[p];
+    const int type = P.type;
+    const float rad = P.rad;
     // conservative tile test: sphere vs the 4 tile planes (camera looks along -z)
     bool keep = true;
     if (type != RMBX_GEOM_PLANE && rad > 0) {
@@ -288,17 +304,34 @@ __global__ void __launch_bounds__(256) render_kernel(RenderArgs a) {
     }
   }
   __syncthreads();
-  // deterministic order (ties resolved by prim index)
+  // order the tile's primitives front to back by the depth bound (ties by prim index): a ray can
+  // stop at the first primitive whose bound lies behind its nearest hit so far
+  {
+    const int cnt = tile_count;
+    if (tid < cnt) {
+      const int p = tile_list[tid];
+      const float z = prims[p].zmin;
+      int rank = 0;
+      for (int j = 0; j < cnt; j++) {
+        const int q = tile_list[j];
+        const float zq = prims[q].zmin;
+        rank += (zq < z) || (zq == z && q < p);
+      }
+      tile_sorted[rank] = p;
+    }
+  }
+  __syncthreads();
   const int px = tx0 + (tid % RENDER_TILE), py = ty0 + (tid / RENDER_TILE);
-  if (px >= W || py >= H) return;
+  if (px < W && py < H) {
   const float d[3] = {((2.0f * (px + 0.5f) / W) - 1.0f) * tanh_ * aspect,
                       (1.0f - 2.0f * (py + 0.5f) / H) * tanh_, -1.0f};
   float best = 1e30f, bn[3] = {0, 0, 1};
   int bp = -1;
   const int cnt = tile_count;
   for (int k = 0; k < cnt; k++) {
-    const int p = tile_list[k];
+    const int p = tile_sorted[k];
     const PrimCam& P = prims[p];
+    if (P.zmin > best + 1e-4f) break;  // every later primitive lies behind the current hit
     float o_l[3], d_l[3], t, nl[3];
     to_local(P, d, o_l, d_l);
     bool h = false;
@@ -374,6 +407,9 @@ __global__ void __launch_bounds__(256) render_kernel(RenderArgs a) {
       }
     }
   }
+  }  // pixel
+  __syncthreads();
+  }  // tiles
 }
 
 }  // namespace rmbx
@@ -411,7 +447,8 @@ extern "C" int rmbx_render(const rmbx_camera* cam, const int32_t* prim_i32, cons
   a.n_env = n_env;
   a.tiles_x = (cam->width + RENDER_TILE - 1) / RENDER_TILE;
   a.tiles_y = (cam->height + RENDER_TILE - 1) / RENDER_TILE;
-  const size_t nblocks = (size_t)n_env * a.tiles_x * a.tiles_y;
+  a.groups = 16;
+  const size_t nblocks = (size_t)n_env * a.groups;
   RMBX_CHECK_ARG(nblocks < (1ull << 31), "grid too large");
   hipLaunchKernelGGL(rmbx::render_kernel, dim3((unsigned)nblocks), dim3(256), 0,
                      reinterpret_cast<hipStream_t>(stream), a);
