@@ -29,6 +29,37 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
+FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (spec)
+BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 MFMA dense (spec)
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+
+
+def physics_flops_per_substep(ncon, nefc, iters):
+    """Algorithmic FP64 FLOPs of one substep at the measured constraint regime, from the op-count
+    fixture (tools/count_flops.py over oracle/flopcount.cpp): fitted c0 + c1 ncon + c2 nefc +
+    c3 iters + c4 iters*nefc."""
+    with open(os.path.join(GOLDEN, "oracle_flops.json")) as f:
+        c = json.load(f)["fit"]["coef"]
+    return c[0] + c[1] * ncon + c[2] * nefc + c[3] * iters + c[4] * iters * nefc
+
+
+def pmc_traffic_per_env_step():
+    """Calibrated HBM-side bytes per env per env-step of the physics kernels from the latest committed
+    counter profile (tools/pmc_traffic.py over two rocprofv3 --pmc passes); (bytes, file) or (None, None)."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "*_pmc_physics_traffic_v*.json")),
+                   key=lambda f: (os.path.basename(f).split("_")[0], int(f.rsplit("_v", 1)[1].split(".")[0])))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        return json.load(f)["bytes_per_env_step_per_env"], os.path.relpath(files[-1], ROOT)
+
+
+def policy_flops_per_inference():
+    """FLOPs of one ACT inference per env (tools/count_policy_flops.py, FlopCounterMode)."""
+    with open(os.path.join(GOLDEN, "policy_flops.json")) as f:
+        return json.load(f)["act_480x640"]["flops_per_inference"]
 
 
 def parse():
@@ -185,6 +216,10 @@ def main():
     bytes_env_step = algorithmic_bytes_per_env_step(nq, nv, nu, 8)
     kern_s = float(phys.mean()) / 1e3
     achieved = n * bytes_env_step / kern_s / 1e9
+    ncon, nefc, iters = float(st[:, 0].mean()), float(st[:, 1].mean()), float(st[:, 2].mean())
+    fl_sub = physics_flops_per_substep(ncon, nefc, iters)
+    fp64_tf = n * 8 * fl_sub / kern_s / 1e12
+    traffic_env, traffic_src = pmc_traffic_per_env_step()
     result = {
         "metric": "env-steps/s (whole node) + policy-inference us/step, MujocoUR5eCable x N ACT",
         "value": round(value, 1),
@@ -205,12 +240,26 @@ def main():
         "policy_inference_us_per_env_step": round(1e6 * float(infer.mean()) / (n * ro.args.skip), 3) if len(infer) else None,
         "physics_kernel_ms": round(float(phys.mean()), 3),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 4), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": achieved / HBM_PEAK_GBS, "traffic": None,
-                     "kernel": "rmbx::physics_kernel (8 fused substeps)",
+                     "frac": achieved / HBM_PEAK_GBS,
+                     "traffic": round(traffic_env * n) if traffic_env else None,
+                     "traffic_unit": "bytes per launch sequence (one env-step of all envs)",
+                     "traffic_source": traffic_src,
+                     "kernel": "physics env-step: 8 x (rmbx::front_kernel + rmbx::solver_kernel), one block per env",
                      "algorithmic_bytes_per_env_step": bytes_env_step},
-        "contacts_mean": float(st[:, 0].mean()), "constraint_rows_mean": float(st[:, 1].mean()),
-        "newton_iters_mean": float(st[:, 2].mean()),
+        # the dynamics is not HBM-bound, so also its FP64 fraction on algorithmic FLOPs
+        "roofline_fp64": {"bound": "fp64-valu", "achieved": round(fp64_tf, 4), "peak": FP64_PEAK_TFLOPS,
+                          "unit": "TFLOP/s", "frac": fp64_tf / FP64_PEAK_TFLOPS,
+                          "kernel": "physics env-step: 8 x (rmbx::front_kernel + rmbx::solver_kernel)",
+                          "algorithmic_flops_per_substep": round(fl_sub)},
+        "contacts_mean": ncon, "constraint_rows_mean": nefc, "newton_iters_mean": iters,
     }
+    if len(infer):
+        pol_tf = n * policy_flops_per_inference() / float(infer.mean()) / 1e12
+        # whole batched infer_policy call (render + preprocessing + ACT), all kernels on the stream
+        result["roofline_policy"] = {"bound": "mfma", "achieved": round(pol_tf, 2), "peak": BF16_PEAK_TFLOPS,
+                                     "unit": "TFLOP/s", "frac": pol_tf / BF16_PEAK_TFLOPS,
+                                     "algorithmic_flops_per_inference": policy_flops_per_inference(),
+                                     "scope": "one batched infer_policy call over all envs"}
     if rank == 0 and not args.no_cpu_baseline:
         try:
             result["cpu_baseline"] = cpu_baseline(args.cpu_sample_steps)

@@ -9,15 +9,17 @@ import numpy as np
 
 _DIR = os.path.dirname(os.path.abspath(__file__))
 _LIB = os.path.join(_DIR, "_build", "librmbx_oracle.so")
-_lib = None
+# the same restatement with an op-counting double (oracle/flopcount.cpp)
+_LIB_FLOPS = os.path.join(_DIR, "_build", "librmbx_oracle_flops.so")
+_libs = {}
 
 
-def _load():
-    global _lib
-    if _lib is None:
-        if not os.path.exists(_LIB):
+def _load(flops=False):
+    path = _LIB_FLOPS if flops else _LIB
+    if path not in _libs:
+        if not os.path.exists(path):
             subprocess.run(["make", "-C", _DIR], check=True, capture_output=True)
-        lib = ctypes.CDLL(_LIB)
+        lib = ctypes.CDLL(path)
         vp, ip, dp = ctypes.c_void_p, ctypes.c_int, ctypes.c_double
         lib.orc_create.restype = vp
         lib.orc_create.argtypes = [vp]
@@ -37,8 +39,12 @@ def _load():
             getattr(lib, n).restype = ip
             getattr(lib, n).argtypes = [vp]
         lib.orc_get_contacts.argtypes = [vp, vp, vp, vp, vp]
-        _lib = lib
-    return _lib
+        if flops:
+            lib.orc_flops.restype = ctypes.c_ulonglong
+            lib.orc_special_ops.restype = ctypes.c_ulonglong
+            lib.orc_flops.argtypes = lib.orc_special_ops.argtypes = lib.orc_flops_reset.argtypes = []
+        _libs[path] = lib
+    return _libs[path]
 
 
 def _p(a):
@@ -48,12 +54,12 @@ def _p(a):
 class OracleEnv:
     """One environment of the CPU oracle."""
 
-    def __init__(self, arrays):
+    def __init__(self, arrays, flops=False):
         from robomanipbaselines_amd import model as MD
 
         self.arrays = arrays
         self.cmodel = MD.as_ctypes(arrays)
-        self.lib = _load()
+        self.lib = _load(flops)
         self.h = self.lib.orc_create(ctypes.byref(self.cmodel))
         self.nq, self.nv, self.nu = int(arrays["_nq"]), int(arrays["_nv"]), int(arrays["_nu"])
         self.nbody = int(arrays["_nbody"])

@@ -1,5 +1,5 @@
 import sys, os, time
-sys.path.insert(0, os.getcwd())
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np, torch
 from robomanipbaselines_amd.envs.ur5e_cable import BatchedMujocoUR5eCableEnv
 env = BatchedMujocoUR5eCableEnv(4, "cuda:0", world_random_scale=[0.01, 0.01, 0.0])

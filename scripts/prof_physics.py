@@ -3,13 +3,28 @@ import os
 import sys
 import time
 
-sys.path.insert(0, os.getcwd())
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from robomanipbaselines_amd.envs.ur5e_cable import BatchedMujocoUR5eCableEnv  # noqa: E402
 
-n = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
+_pos = [x for x in sys.argv[1:] if not x.startswith("--")]
+n = int(_pos[0]) if _pos else 1024
+if "--calib" in sys.argv:
+    # known-byte-count copies for calibrating FETCH_SIZE / WRITE_SIZE (scripts/pmc_calib.hip):
+    # 512 MiB read + 512 MiB written per launch, past the 256 MiB Infinity Cache
+    import ctypes
+
+    cal = ctypes.CDLL(os.path.join(os.path.dirname(os.path.abspath(__file__)), "_build", "libpmc_calib.so"))
+    cal.pmc_calib.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int, ctypes.c_void_p]
+    nb = 512 << 20
+    x = torch.zeros(nb // 8, dtype=torch.float64, device="cuda")
+    y = torch.empty_like(x)
+    for wide in (0, 1, 0, 1):
+        assert cal.pmc_calib(x.data_ptr(), y.data_ptr(), nb, wide, None) == 0
+    torch.cuda.synchronize()
+    del x, y
 env = BatchedMujocoUR5eCableEnv(n, "cuda:0")
 env.reset()
 a = env.engine.ctrl.clone()
