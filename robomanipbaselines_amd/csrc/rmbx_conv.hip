@@ -19,6 +19,7 @@
 #include "rmbx_common.h"
 
 #include <cstdint>
+#include <cstdlib>
 
 namespace rmbx {
 namespace {
@@ -37,6 +38,7 @@ struct ConvArgs {
   int N, H, W, Cin, Ho, Wo, Cout, KH, KW, stride, pad, relu;
   long long M;
   int n_ntiles;         // Cout / CBN
+  int dbg;              // diagnostic phase skips (RMBX_CONV_DBG; 0 in production)
   long long n_mtiles;
 };
 
@@ -46,6 +48,30 @@ __device__ __forceinline__ uint16_t f2bf(float f) {
   if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fc0;
   u += 0x7fffu + ((u >> 16) & 1u);
   return (uint16_t)(u >> 16);
+}
+
+// bias (+ residual) (+ ReLU) on 8 consecutive channels of one pixel, rounded once to bf16
+__device__ __forceinline__ uint4 epi_finish8(const float* c, const float* bv, uint4 rv, bool res, bool relu) {
+  float v[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) v[k] = c[k] + bv[k];
+  if (res) {
+    const uint32_t w4[4] = {rv.x, rv.y, rv.z, rv.w};
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      v[2 * k] += bf2f((uint16_t)(w4[k] & 0xffff));
+      v[2 * k + 1] += bf2f((uint16_t)(w4[k] >> 16));
+    }
+  }
+  if (relu)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) v[k] = v[k] > 0.f ? v[k] : 0.f;
+  uint4 ov;
+  ov.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
+  ov.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
+  ov.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
+  ov.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
+  return ov;
 }
 
 // MODE 0: KH x KW conv over [N][H][W][Cin], K step = one tap x 64 channels.
@@ -74,34 +100,26 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, float* sC, cons
     sC[row * EPI_LD + 32 + col] = acc1[j];
   }
   __syncthreads();
+  // this thread's 8 channels are the same in every pass (256 is a multiple of 8): bias once, and
+  // all residual loads in flight before the first store
+  const int c8 = (tid & 7) * 8;
+  float bv[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) bv[k] = a.bias[n0 + c8 + k];
+  long long base[4];
+  uint4 rv[4];
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const int q = tid + 256 * i;
-    const int pix = q >> 3, c8 = (q & 7) * 8;
-    const long long base = out_off(pix);
-    if (base < 0) continue;
-    const size_t o = (size_t)base + n0 + c8;
-    float v[8];
+    base[i] = out_off((tid + 256 * i) >> 3);
+    rv[i] = (a.res && base[i] >= 0) ? *reinterpret_cast<const uint4*>(a.res + (size_t)base[i] + n0 + c8)
+                                    : make_uint4(0, 0, 0, 0);
+  }
 #pragma unroll
-    for (int k = 0; k < 8; ++k) v[k] = sC[pix * EPI_LD + c8 + k] + a.bias[n0 + c8 + k];
-    if (a.res) {
-      const uint4 rv = *reinterpret_cast<const uint4*>(a.res + o);
-      const uint32_t w4[4] = {rv.x, rv.y, rv.z, rv.w};
-#pragma unroll
-      for (int k = 0; k < 4; ++k) {
-        v[2 * k] += bf2f((uint16_t)(w4[k] & 0xffff));
-        v[2 * k + 1] += bf2f((uint16_t)(w4[k] >> 16));
-      }
-    }
-    if (a.relu)
-#pragma unroll
-      for (int k = 0; k < 8; ++k) v[k] = v[k] > 0.f ? v[k] : 0.f;
-    uint4 ov;
-    ov.x = (uint32_t)f2bf(v[0]) | ((uint32_t)f2bf(v[1]) << 16);
-    ov.y = (uint32_t)f2bf(v[2]) | ((uint32_t)f2bf(v[3]) << 16);
-    ov.z = (uint32_t)f2bf(v[4]) | ((uint32_t)f2bf(v[5]) << 16);
-    ov.w = (uint32_t)f2bf(v[6]) | ((uint32_t)f2bf(v[7]) << 16);
-    *reinterpret_cast<uint4*>(a.out + o) = ov;
+  for (int i = 0; i < 4; ++i) {
+    if (base[i] < 0) continue;
+    const int pix = (tid + 256 * i) >> 3;
+    *reinterpret_cast<uint4*>(a.out + (size_t)base[i] + n0 + c8) =
+        epi_finish8(sC + pix * EPI_LD + c8, bv, rv[i], a.res != nullptr, a.relu != 0);
   }
 }
 
@@ -244,7 +262,9 @@ __global__ void __launch_bounds__(256) conv3x3_c64_patch_kernel(ConvArgs a) {
   const int oy0 = ty * PT_H, ox0 = tx * PT_W, n0 = nt * CBN;
 
   const int r = lane & 31, h8 = 8 * (lane >> 5);
-  const int ly = 2 * wave + (r >> 4), lx = r & 15;  // this lane's A row = output pixel (ly, lx)
+  // this lane's A row = output pixel (ly, lx); row 1 rotated by 2 columns (bank-conflict-free
+  // ds_read_b128 groups with the 18-pixel patch pitch, see conv3x3_c64_resident_kernel)
+  const int ly = 2 * wave + (r >> 4), lx = r < 16 ? r : ((r - 2) & 15);
   f32x16 acc0 = {}, acc1 = {};
   uint4 rb0, rb1;
   const int Cin = a.Cin;
@@ -292,9 +312,191 @@ __global__ void __launch_bounds__(256) conv3x3_c64_patch_kernel(ConvArgs a) {
     }
   }
   conv_epilogue(a, reinterpret_cast<float*>(smem), acc0, acc1, n0, [&](int pix) -> long long {
-    const int oy = oy0 + (pix >> 4), ox = ox0 + (pix & 15);
+    const int m = pix & 31;  // epilogue row 32 * wave + m = A row m of wave pix >> 5
+    const int oy = oy0 + 2 * (pix >> 5) + (m >> 4), ox = ox0 + (m < 16 ? m : ((m - 2) & 15));
     return (oy < a.Ho && ox < a.Wo) ? ((((long long)n * a.Ho + oy) * a.Wo + ox) * a.Cout) : -1;
   });
+}
+
+// 3x3 / stride 1 / pad 1 conv with Cin = Cout = 64 (ResNet-18 layer1, the trunk's widest
+// activations): the whole filter bank (9 taps x 64 x 64 bf16 = 72 KiB) stays resident in LDS for
+// the life of a persistent block (one per CU) that walks a contiguous range of 8 x 32 output
+// tiles.  Per tile only the 10 x 34 x 64 input patch moves (prefetched into registers while the
+// previous tile is multiplied), so the L2 -> CU traffic per MFMA drops ~5x against the per-block
+// weight streaming of conv3x3_c64_patch_kernel.  8 waves (2 per SIMD); wave w owns output row w
+// of the tile (32 pixels x 64 channels = two 32x32 accumulators) and reads its A fragments for all
+// 9 taps from the patch (8 x 32 tiles divide the 120 x 160 layer-1 map exactly).  The f32 epilogue image aliases the patch.
+constexpr int RTH = 8, RTW = 32, RPH = RTH + 2, RPW = RTW + 2, RTHREADS = 512;
+constexpr int RW_LDS = 9 * 64 * CLD;  // bf16 elements, [tap][cout][CLD]
+constexpr int EPI_LDR = 72;  // f32 epilogue row stride: the two half-waves' ds_write_b32 hit disjoint banks
+constexpr int RU_LDS = (RTH * RTW * EPI_LDR * 2 > RPH * RPW * PLD) ? RTH * RTW * EPI_LDR * 2 : RPH * RPW * PLD;
+constexpr int RPATCH_CHUNKS = RPH * RPW * 8;
+constexpr int RPATCH_PER_THREAD = (RPATCH_CHUNKS + RTHREADS - 1) / RTHREADS;
+static_assert((RW_LDS + RU_LDS) * 2 <= 160 * 1024, "resident conv must fit the 160 KiB LDS");
+
+__global__ void __launch_bounds__(RTHREADS) conv3x3_c64_resident_kernel(ConvArgs a, int tiles_x, int tiles_y,
+                                                                         long long ntiles) {
+  __shared__ __attribute__((aligned(16))) uint16_t smem[RW_LDS + RU_LDS];
+  uint16_t* sW = smem;
+  uint16_t* sP = smem + RW_LDS;
+  float* sC = reinterpret_cast<float*>(sP);
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // filter bank [cout][kh][kw][c] -> sW[tap][cout][c]
+  for (int q = tid; q < 9 * 64 * 8; q += RTHREADS) {
+    const int part = q & 7, rest = q >> 3;  // rest = cout * 9 + tap
+    const int co = rest / 9, tap = rest - 9 * co;
+    *reinterpret_cast<uint4*>(sW + (tap * 64 + co) * CLD + part * 8) =
+        *reinterpret_cast<const uint4*>(a.w + (size_t)rest * 64 + part * 8);
+  }
+  const long long t_begin = ntiles * blockIdx.x / gridDim.x;
+  const long long t_end = ntiles * (blockIdx.x + 1) / gridDim.x;
+  const int c8 = (tid & 7) * 8;  // this thread's epilogue channels (fixed: 512 % 8 == 0)
+  float bv[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) bv[k] = a.bias[c8 + k];
+  const int r = lane & 31, h8 = 8 * (lane >> 5);
+  // A row r -> output pixel (wave, r): 32 consecutive patch pixels at a 144-byte pitch, so every
+  // 16-lane ds_read_b128 group touches 16 distinct 4-bank quads
+  const int ly = wave, lx = r;
+  uint4 pr[RPATCH_PER_THREAD];
+  constexpr int EPASS = RTH * RTW * 8 / RTHREADS;  // epilogue 16-byte chunks per thread per tile
+  uint4 rres[EPASS];                               // residual chunks of the current tile
+#pragma unroll
+  for (int i = 0; i < EPASS; ++i) rres[i] = make_uint4(0, 0, 0, 0);
+
+#define RMBX_RES_TILE(T, N_, OY0, OX0)                     \
+  {                                                        \
+    long long t_ = (T);                                    \
+    const int tx_ = (int)(t_ % tiles_x);                   \
+    t_ /= tiles_x;                                         \
+    OY0 = (int)(t_ % tiles_y) * RTH;                       \
+    N_ = (int)(t_ / tiles_y);                              \
+    OX0 = tx_ * RTW;                                       \
+  }
+#define RMBX_RES_LOAD(T)                                                                               \
+  {                                                                                                    \
+    int n_, oy0_, ox0_;                                                                                \
+    RMBX_RES_TILE(T, n_, oy0_, ox0_)                                                                   \
+    _Pragma("unroll") for (int i = 0; i < RPATCH_PER_THREAD; ++i) {                                    \
+      const int q = tid + RTHREADS * i;                                                                \
+      const int pix = q >> 3, part = q & 7;                                                            \
+      const int py = pix / RPW, px = pix - py * RPW;                                                   \
+      const int h = oy0_ - 1 + py, w = ox0_ - 1 + px;                                                  \
+      pr[i] = (q < RPATCH_CHUNKS && h >= 0 && h < a.H && w >= 0 && w < a.W)                            \
+                  ? *reinterpret_cast<const uint4*>(a.in + (((size_t)n_ * a.H + h) * a.W + w) * 64 + part * 8) \
+                  : make_uint4(0, 0, 0, 0);                                                            \
+    }                                                                                                  \
+  }
+
+  const int dbg = a.dbg;
+#define RMBX_RESID_LOAD(T)                                                                             \
+  if (a.res) {                                                                                         \
+    int n_, oy0_, ox0_;                                                                                \
+    RMBX_RES_TILE(T, n_, oy0_, ox0_)                                                                   \
+    _Pragma("unroll") for (int i = 0; i < EPASS; ++i) {                                                \
+      const int pix = (tid + RTHREADS * i) >> 3;                                                       \
+      const int oy = oy0_ + (pix >> 5), ox = ox0_ + (pix & 31);                                        \
+      if (oy < a.Ho && ox < a.Wo)                                                                      \
+        rres[i] = *reinterpret_cast<const uint4*>(a.res + (((size_t)n_ * a.Ho + oy) * a.Wo + ox) * 64 + c8); \
+    }                                                                                                  \
+  }
+  if (t_begin < t_end && !(dbg & 4)) {
+    RMBX_RES_LOAD(t_begin)
+    RMBX_RESID_LOAD(t_begin)
+  }
+  // finished bf16 chunks of the previous tile: stored only after the next patch is in LDS, so
+  // the vmcnt wait in front of a patch store never waits on the output stores just issued
+  uint4 ov[EPASS];
+  int pn = -1, poy0 = 0, pox0 = 0;  // tile whose chunks are pending in ov (pn < 0: none)
+#define RMBX_RES_STORE()                                                                               \
+  if (pn >= 0) {                                                                                       \
+    _Pragma("unroll") for (int i = 0; i < EPASS; ++i) {                                                \
+      const int pix = (tid + RTHREADS * i) >> 3;                                                       \
+      const int oy = poy0 + (pix >> 5), ox = pox0 + (pix & 31);                                        \
+      if (oy < a.Ho && ox < a.Wo)                                                                      \
+        *reinterpret_cast<uint4*>(a.out + (((size_t)pn * a.Ho + oy) * a.Wo + ox) * 64 + c8) = ov[i];   \
+    }                                                                                                  \
+  }
+  for (long long t = t_begin; t < t_end; ++t) {
+    int n, oy0, ox0;
+    RMBX_RES_TILE(t, n, oy0, ox0)
+    __syncthreads();  // previous epilogue done with the aliased region (and sW written)
+#pragma unroll
+    for (int i = 0; i < RPATCH_PER_THREAD; ++i) {
+      const int q = tid + RTHREADS * i;
+      if (q < RPATCH_CHUNKS) *reinterpret_cast<uint4*>(sP + (q >> 3) * PLD + (q & 7) * 8) = pr[i];
+    }
+    __syncthreads();
+    RMBX_RES_STORE()
+    if (t + 1 < t_end && !(dbg & 4)) RMBX_RES_LOAD(t + 1)
+    f32x16 acc0 = {}, acc1 = {};
+    if (!(dbg & 1)) {
+    // A/B fragments double-buffered in registers by half-tap groups (2 k-steps: 6 LDS reads,
+    // 4 MFMAs): group g + 1's reads are in flight while group g multiplies
+    bf16x8 fa[2][2], fb0[2][2], fb1[2][2];
+#define RMBX_RES_FRAGS(BUF, G)                                                                     \
+  {                                                                                                \
+    const int tap_ = (G) >> 1, k0_ = 32 * ((G) & 1);                                               \
+    const int kh_ = tap_ / 3, kw_ = tap_ - 3 * kh_;                                                \
+    const uint16_t* arow_ = sP + ((ly + kh_) * RPW + (lx + kw_)) * PLD + h8 + k0_;                 \
+    const uint16_t* brow_ = sW + (tap_ * 64 + r) * CLD + h8 + k0_;                                 \
+    _Pragma("unroll") for (int ks = 0; ks < 2; ++ks) {                                             \
+      fa[BUF][ks] = *reinterpret_cast<const bf16x8*>(arow_ + 16 * ks);                             \
+      fb0[BUF][ks] = *reinterpret_cast<const bf16x8*>(brow_ + 16 * ks);                            \
+      fb1[BUF][ks] = *reinterpret_cast<const bf16x8*>(brow_ + 32 * CLD + 16 * ks);                 \
+    }                                                                                              \
+  }
+    RMBX_RES_FRAGS(0, 0)
+#pragma unroll
+    for (int g = 0; g < 18; ++g) {
+      const int cur = g & 1;
+      if (g < 17) RMBX_RES_FRAGS(cur ^ 1, g + 1)
+      __builtin_amdgcn_sched_barrier(0);  // keep the prefetch above this group's MFMAs
+#pragma unroll
+      for (int ks = 0; ks < 2; ++ks) {
+        acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[cur][ks], fb0[cur][ks], acc0, 0, 0, 0);
+        acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fa[cur][ks], fb1[cur][ks], acc1, 0, 0, 0);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    }
+#undef RMBX_RES_FRAGS
+    // the next patch has landed in registers by now: consume the wait here so that the vmcnt
+    // wait before the next patch store does not also wait for this tile's output stores
+#pragma unroll
+    for (int i = 0; i < RPATCH_PER_THREAD; ++i) asm volatile("" ::"v"(pr[i].x), "v"(pr[i].y), "v"(pr[i].z), "v"(pr[i].w));
+    __syncthreads();  // every wave is done reading the patch
+    if (dbg & 2) continue;
+    const int col = lane & 31;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int row = 32 * wave + (j & 3) + 8 * (j >> 2) + 4 * (lane >> 5);  // = tile pixel
+      sC[row * EPI_LDR + col] = acc0[j];
+      sC[row * EPI_LDR + 32 + col] = acc1[j];
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < EPASS; ++i) {
+      const int pix = (tid + RTHREADS * i) >> 3;
+      ov[i] = epi_finish8(sC + pix * EPI_LDR + c8, bv, rres[i], a.res != nullptr, a.relu != 0);
+    }
+    pn = n;
+    poy0 = oy0;
+    pox0 = ox0;
+    if (t + 1 < t_end && !(dbg & 4)) RMBX_RESID_LOAD(t + 1)
+  }
+  RMBX_RES_STORE()
+#undef RMBX_RES_STORE
+#undef RMBX_RESID_LOAD
+#undef RMBX_RES_LOAD
+#undef RMBX_RES_TILE
+}
+
+int device_cus() {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 256;
+  return cus > 0 ? cus : 256;
 }
 
 }  // namespace
@@ -333,6 +535,18 @@ extern "C" int rmbx_conv2d_nhwc(const void* in, const void* weight, const float*
   a.M = (long long)N * Ho * Wo;
   a.n_ntiles = Cout / rmbx::CBN;
   a.n_mtiles = (a.M + rmbx::CBM - 1) / rmbx::CBM;
+  const char* dbg_env = std::getenv("RMBX_CONV_DBG");
+  a.dbg = dbg_env ? std::atoi(dbg_env) : 0;
+  if (KH == 3 && KW == 3 && stride == 1 && pad == 1 && Cin == 64 && Cout == 64 &&
+      std::getenv("RMBX_CONV_NO_RESIDENT") == nullptr) {
+    const int tiles_x = (Wo + rmbx::RTW - 1) / rmbx::RTW, tiles_y = (Ho + rmbx::RTH - 1) / rmbx::RTH;
+    const long long ntiles = (long long)N * tiles_x * tiles_y;
+    const int grid = (int)(ntiles < rmbx::device_cus() ? ntiles : rmbx::device_cus());
+    hipLaunchKernelGGL(rmbx::conv3x3_c64_resident_kernel, dim3(grid), dim3(rmbx::RTHREADS), 0,
+                       (hipStream_t)stream, a, tiles_x, tiles_y, ntiles);
+    RMBX_CHECK_LAUNCH();
+    return RMBX_OK;
+  }
   if (KH == 3 && KW == 3 && stride == 1 && pad == 1) {
     const long long ntile = (long long)N * ((Ho + rmbx::PT_H - 1) / rmbx::PT_H) * ((Wo + rmbx::PT_W - 1) / rmbx::PT_W);
     const long long nb = ntile * a.n_ntiles;
@@ -356,6 +570,7 @@ extern "C" int rmbx_stem_s2d_conv(const void* in, const void* weight, const floa
   RMBX_CHECK_ARG((((uintptr_t)in | (uintptr_t)weight) & 15) == 0, "rmbx_stem_s2d_conv: unaligned");
   if (N == 0) return RMBX_OK;
   rmbx::ConvArgs a;
+  a.dbg = 0;
   a.in = (const uint16_t*)in;
   a.w = (const uint16_t*)weight;
   a.bias = bias;

@@ -124,6 +124,27 @@ def test_conv2d_nhwc_matches_fp32(cin, cout, k, stride, res, relu):
 
 
 @torch.no_grad()
+def test_conv3x3_c64_resident_equals_streaming_kernel(monkeypatch):
+    """The persistent resident-filter kernel (Cin = Cout = 64) walks several 16x16 tiles per block
+    (768 tiles > CU count, ragged edges) and must equal the per-tile streaming kernel bit for bit
+    (same MFMA order), and the fp32 reference within one bf16 rounding."""
+    from robomanipbaselines_amd import kernels as K
+
+    g = torch.Generator(device=DEV).manual_seed(7)
+    x = _cl(torch.randn(64, 64, 40, 57, device=DEV, generator=g).to(torch.bfloat16))
+    w = _cl((torch.randn(64, 64, 3, 3, device=DEV, generator=g) / 24).to(torch.bfloat16))
+    b = torch.randn(64, device=DEV, generator=g)
+    r = _cl(torch.randn(64, 64, 40, 57, device=DEV, generator=g).to(torch.bfloat16))
+    got = K.conv2d_nhwc(x, w, b, 1, 1, relu=True, res=r)
+    monkeypatch.setenv("RMBX_CONV_NO_RESIDENT", "1")
+    alt = K.conv2d_nhwc(x, w, b, 1, 1, relu=True, res=r)
+    assert torch.equal(got, alt)
+    ref = F.relu(F.conv2d(x.float(), w.float(), b, 1, 1) + r.float())
+    err = (got.float() - ref).abs()
+    assert (err <= 2 ** -8 * ref.abs() + 1e-3).all(), err.max().item()
+
+
+@torch.no_grad()
 def test_fused_trunk_bf16_epilogues_equal_unfused_sequence():
     """Walk the trunk with each conv evaluated ONCE; the HIP epilogues and the torch ops applied
     to the same conv outputs must agree bit for bit at every block (real trunk shapes)."""
