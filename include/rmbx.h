@@ -244,6 +244,14 @@ int rmbx_conv2d_nhwc(const void* in, const void* weight, const float* bias, cons
  * Replaces conv1 -> BN -> ReLU of the backbone's stem (max-pool: rmbx_nhwc_bias_relu_maxpool). */
 int rmbx_stem_s2d_conv(const void* in, const void* weight, const float* bias, void* out, int N, int Hs,
                        int Ws, int Cout, int relu, void* stream);
+/* The whole stem in one pass: out [N][Hp][Wp][64] bf16 = maxpool3x3s2p1(relu(conv + bias)) with
+ * Hp = (Hs-1)/2+1, Wp = (Ws-1)/2+1, Cout = 64, Ws <= 320; same in/weight/bias as
+ * rmbx_stem_s2d_conv and bit-identical to rmbx_stem_s2d_conv followed by
+ * rmbx_nhwc_bias_relu_maxpool (zero bias), without the full-resolution stem map in HBM.
+ * band_rows: pool rows per block (<= 0: chosen from N).  Replaces conv1 -> bn1 -> relu -> maxpool
+ * of the backbones' resnet18 (third_party/act [absent]; policy/mlp/MlpPolicy.py:34-39). */
+int rmbx_stem_s2d_conv_maxpool(const void* in, const void* weight, const float* bias, void* out, int N,
+                               int Hs, int Ws, int band_rows, void* stream);
 /* Residual add + LayerNorm over the last dim of [rows][D] rows (D <= 2048, multiple of 8 bf16 / 4
  * f32): out = LayerNorm(rnd(x + r)) * weight + bias (f32 weight/bias), r optional (NULL); replaces
  * the add + nn.LayerNorm pair of the ACT transformer's post-norm layers (third_party/act). */

@@ -1,0 +1,298 @@
+// ResNet-18 stem fused end to end: conv1 (7x7 / stride 2 / pad 3, BN folded) + bias + ReLU +
+// max-pool 3x3 / stride 2 / pad 1, from the renderer's 2x2 space-to-depth image straight to the
+// pooled [N][Hp][Wp][64] bf16 activation that layer1 reads (MFMA 32x32x16 bf16, gfx950).
+//
+// Replaces the stem of the backbones' torchvision resnet18 (ACT's DETR backbone, third_party/act
+// [absent]; policy/mlp/MlpPolicy.py:34-39): conv1 -> bn1 -> relu -> maxpool.  The unfused form
+// (rmbx_stem_s2d_conv + rmbx_nhwc_bias_relu_maxpool) writes the 64-channel stem map at full
+// resolution (240 x 320 x 64 bf16 = 9.8 MB per 480 x 640 image) and reads it back for the pool;
+// here that map never leaves the CU: HBM sees the s2d image once (2.5 MB) and the pooled output
+// once (2.5 MB).
+//
+// Mapping.  One block per (image, band of pool rows); wave w owns stem columns 32w .. 32w+31 for
+// the whole band.  Per pool row py the block computes stem rows 2py and 2py+1 as a transposed
+// implicit GEMM C^T[cout][pixel] = W[cout][k] * X[k][pixel] with k = (ky, kx, 16 s2d channels)
+// in the order of rmbx_stem_s2d_conv (so the f32 accumulation chains, and therefore the bf16
+// stem values, are identical to the unfused kernel's).  The A operand rows are the output
+// channels permuted so that accumulator register j of lane-half h holds channel 16h + j of
+// the 32-channel tile: after bias + ReLU + rounding each lane owns 16 consecutive channels of ONE
+// stem pixel, so
+//   * the vertical pool is a running max in registers (row 2py-1 carried from the previous row
+//     pair; packed bf16 max as u16 is exact because every value is >= 0 after the ReLU),
+//   * the horizontal pool is two lane shuffles (left/right neighbour pixel) plus one LDS edge
+//     value from the wave on the left,
+//   * the pooled pixel's 32 channels leave as two 16-byte stores.
+// The filter bank (16 taps x 64 x 16 bf16 = 32 KiB) stays in LDS for the block's life; the input
+// rows live in a 5-row LDS ring (rows 2py-2 .. 2py+2), the next two rows prefetched into
+// registers while the current pair is multiplied.
+
+#include "rmbx_common.h"
+
+#include <cstdint>
+
+namespace rmbx {
+namespace {
+
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x2 __attribute__((ext_vector_type(2)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+constexpr int SP_MAX_WAVES = 10;               // stem columns <= 320
+constexpr int SP_THREADS = 64 * SP_MAX_WAVES;  // launch bound
+constexpr int SP_RING = 5;                     // s2d rows 2py-2 .. 2py+2
+constexpr int SP_RC_MAX = 32 * SP_MAX_WAVES + 4;
+constexpr int SP_LDS_U16 = 16 * 2 * 64 * 8 + SP_RING * 2 * SP_RC_MAX * 8 + 2 * 64 + SP_MAX_WAVES * 2 * 16 * 2;
+static_assert(SP_LDS_U16 * 2 <= 160 * 1024, "stem+pool LDS must fit the 160 KiB of a CU");
+
+__device__ __forceinline__ uint32_t sp_f2bf(float f) {
+  uint32_t u = __float_as_uint(f);
+  if ((u & 0x7fffffffu) > 0x7f800000u) return 0x7fc0;
+  u += 0x7fffu + ((u >> 16) & 1u);
+  return u >> 16;
+}
+
+typedef short i16x2 __attribute__((ext_vector_type(2)));
+// per-half max of two packed bf16 pairs as signed 16-bit integers (v_pk_max_i16): for bf16 values
+// >= +0 the integer order is the value order, and every negative value (sign bit set, -0 included)
+// is below +0, so pk_max(x, 0) is the ReLU of a packed pair
+__device__ __forceinline__ uint32_t pk_max(uint32_t a, uint32_t b) {
+  return __builtin_bit_cast(uint32_t, __builtin_elementwise_max(__builtin_bit_cast(i16x2, a), __builtin_bit_cast(i16x2, b)));
+}
+
+struct StemPoolArgs {
+  const uint16_t* in;   // [N][Hs][Ws][16]
+  const uint16_t* w;    // [64][16 taps][16]
+  const float* bias;    // [64]
+  uint16_t* out;        // [N][Hp][Wp][64]
+  int N, Hs, Ws, Hp, Wp;
+  int nct;              // column tiles (= waves per block)
+  int rc;               // ring columns = 32 * nct + 4 (s2d cols -2 .. 32 * nct + 1)
+  int bands, band_rows; // pool-row bands per image
+};
+
+__global__ void __launch_bounds__(SP_THREADS) stem_pool_kernel(StemPoolArgs a) {
+  __shared__ __attribute__((aligned(16))) uint16_t sp_smem[SP_LDS_U16];
+  uint16_t* sW = sp_smem;                          // [16 taps][2 halves][64 cout][8]
+  uint16_t* sR = sW + 16 * 2 * 64 * 8;             // [5 slots][2 halves][rc][8]
+  float* sBias = reinterpret_cast<float*>(sR + SP_RING * 2 * a.rc * 8);  // [64]
+  uint32_t* sEdge = reinterpret_cast<uint32_t*>(sBias + 64);              // [nct][2][16]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nthreads = blockDim.x;
+  const int img = blockIdx.x / a.bands, band = blockIdx.x - img * a.bands;
+  const int py0 = band * a.band_rows;
+  const int py1 = min(a.Hp, py0 + a.band_rows);
+  if (py0 >= py1) return;
+  const int pys = py0 > 0 ? py0 - 1 : 0;  // a compute-only row pair supplies the carried row
+  const size_t row_elems = (size_t)a.Ws * 16;
+  const uint16_t* in_img = a.in + (size_t)img * a.Hs * row_elems;
+
+  // filter bank: global [cout][tap][16] -> sW[tap][half][cout][8]
+  for (int q = tid; q < 64 * 16 * 2; q += nthreads) {
+    const int half = q & 1, rest = q >> 1;  // rest = cout * 16 + tap
+    const int co = rest >> 4, tap = rest & 15;
+    *reinterpret_cast<uint4*>(sW + ((tap * 2 + half) * 64 + co) * 8) =
+        *reinterpret_cast<const uint4*>(a.w + (size_t)rest * 16 + half * 8);
+  }
+  if (tid < 64) sBias[tid] = a.bias[tid];
+
+  // 16-byte chunk q of s2d row y -> (half, ring col); zero outside the image
+  const int row_chunks = 2 * a.rc;
+  auto load_chunk = [&](int y, int q) -> uint4 {
+    const int half = q / a.rc, c = q - half * a.rc;
+    const int x = c - 2;
+    if (y < 0 || y >= a.Hs || x < 0 || x >= a.Ws) return make_uint4(0, 0, 0, 0);
+    return *reinterpret_cast<const uint4*>(in_img + (size_t)y * row_elems + (size_t)x * 16 + half * 8);
+  };
+  auto slot_of = [](int y) { return (y + 2 * SP_RING) % SP_RING; };
+  // initial ring: rows 2pys-2 .. 2pys+2
+  for (int q = tid; q < SP_RING * row_chunks; q += nthreads) {
+    const int r = q / row_chunks, qq = q - r * row_chunks;
+    const int y = 2 * pys - 2 + r;
+    *reinterpret_cast<uint4*>(sR + ((size_t)slot_of(y) * row_chunks + qq) * 8) = load_chunk(y, qq);
+  }
+
+  const int n = lane & 31, h = lane >> 5;  // B: pixel column in the tile / k half; C: channel half
+  const int X = 32 * wave + n;             // this lane's stem column
+  const int m = lane & 31;                 // A row -> output channel sigma(m) of the tile
+  const int sig = 16 * ((m >> 2) & 1) + (m & 3) + 4 * (m >> 3);
+  const bool col_ok = X < a.Ws;
+
+  // register prefetch of the next pair's two new rows (2 * row_chunks chunks over the block):
+  // branch-free (clamped address, zero applied when the chunk is written to the ring)
+  constexpr int PF_MAX = 3;  // (2 rows * 2 halves * 324 cols) / 640 threads, rounded up
+  uint4 pf[PF_MAX];
+  uint32_t pf_ok = 0;
+  const int pf_chunks = 2 * row_chunks;
+  int pf_r[PF_MAX], pf_q[PF_MAX];
+#pragma unroll
+  for (int i = 0; i < PF_MAX; ++i) {
+    const int q = min(tid + nthreads * i, pf_chunks - 1);
+    pf_r[i] = q / row_chunks;
+    pf_q[i] = q - pf_r[i] * row_chunks;
+  }
+
+  uint32_t carry[2][8];  // stem row 2py-1 (bf16 pairs): [cout tile][channel pair]
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int k = 0; k < 8; ++k) carry[t][k] = 0;
+
+  __syncthreads();
+  for (int py = pys; py < py1; ++py) {
+    const int Y0 = 2 * py;
+    const bool more = py + 1 < py1;
+    if (more) {
+      pf_ok = 0;
+#pragma unroll
+      for (int i = 0; i < PF_MAX; ++i) {
+        const int y = Y0 + 3 + pf_r[i];
+        const int half = pf_q[i] / a.rc, x = pf_q[i] - half * a.rc - 2;
+        const bool ok = tid + nthreads * i < pf_chunks && y < a.Hs && x >= 0 && x < a.Ws;
+        const size_t off = ok ? (size_t)y * row_elems + (size_t)x * 16 + half * 8 : 0;
+        pf[i] = *reinterpret_cast<const uint4*>(in_img + off);
+        pf_ok |= (uint32_t)ok << i;
+      }
+    }
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) acc[r][t] = f32x16{};
+    int slot[5];
+#pragma unroll
+    for (int d = 0; d < 5; ++d) slot[d] = slot_of(Y0 - 2 + d);
+#pragma unroll
+    for (int tap = 0; tap < 16; ++tap) {
+      const int ky = tap >> 2, kx = tap & 3;
+      bf16x8 bx[2], aw[2];
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+        bx[r] = *reinterpret_cast<const bf16x8*>(sR + (((size_t)slot[r + ky] * 2 + h) * a.rc + X + kx) * 8);
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+        aw[t] = *reinterpret_cast<const bf16x8*>(sW + ((tap * 2 + h) * 64 + 32 * t + sig) * 8);
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+#pragma unroll
+        for (int t = 0; t < 2; ++t) acc[r][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aw[t], bx[r], acc[r][t], 0, 0, 0);
+    }
+
+    // bias + bf16 (round-to-nearest-even, v_cvt_pk_bf16_f32) + ReLU on the packed pair,
+    // vertical max with the carried row, packed channel pairs
+    const bool row1_ok = Y0 + 1 < a.Hs;
+    uint32_t vm[2][8];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+      const float4* bp = reinterpret_cast<const float4*>(sBias + 32 * t + 16 * h);
+      float bv[16];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const float4 b4 = bp[k];
+        bv[4 * k] = b4.x;
+        bv[4 * k + 1] = b4.y;
+        bv[4 * k + 2] = b4.z;
+        bv[4 * k + 3] = b4.w;
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        f32x2 v0, v1;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          v0[e] = acc[0][t][2 * k + e] + bv[2 * k + e];
+          v1[e] = acc[1][t][2 * k + e] + bv[2 * k + e];
+        }
+        // ReLU after rounding == rounding after ReLU (RNE keeps the sign; -0 and negatives -> +0)
+        const uint32_t p0 = __builtin_bit_cast(uint32_t, __builtin_convertvector(v0, bf16x2));
+        const uint32_t p1 = row1_ok ? pk_max(__builtin_bit_cast(uint32_t, __builtin_convertvector(v1, bf16x2)), 0u) : 0u;
+        vm[t][k] = col_ok ? pk_max(pk_max(carry[t][k], p0), p1) : 0u;  // >= 0 through p1
+        carry[t][k] = p1;
+      }
+    }
+    // the tile's last column feeds the right neighbour wave's first pool window
+    if (n == 31) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) sEdge[(wave * 2 + h) * 16 + 8 * t + k] = vm[t][k];
+    }
+    __syncthreads();  // edges visible; every wave is done with ring rows 2py-2, 2py-1
+
+    // refill the ring first (the prefetch has landed long ago), so the wait for it never waits
+    // on this row's output stores
+    if (more) {
+#pragma unroll
+      for (int i = 0; i < PF_MAX; ++i) {
+        if (tid + nthreads * i < pf_chunks) {
+          const uint4 v = ((pf_ok >> i) & 1u) ? pf[i] : make_uint4(0, 0, 0, 0);
+          const int dst_slot = pf_r[i] ? slot[1] : slot[0];  // row Y0+3+r replaces row Y0-2+r
+          *reinterpret_cast<uint4*>(sR + ((size_t)dst_slot * row_chunks + pf_q[i]) * 8) = v;
+        }
+      }
+    }
+    if (py >= py0) {
+      uint32_t o[2][8];
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int k = 0; k < 8; ++k) {
+          uint32_t left = (uint32_t)__shfl_up((int)vm[t][k], 1);
+          const uint32_t right = (uint32_t)__shfl_down((int)vm[t][k], 1);
+          if (n == 0) left = wave > 0 ? sEdge[((wave - 1) * 2 + h) * 16 + 8 * t + k] : 0u;
+          o[t][k] = pk_max(pk_max(left, vm[t][k]), right);
+        }
+      const int px = 16 * wave + (n >> 1);
+      if ((n & 1) == 0 && px < a.Wp) {
+        uint16_t* dst = a.out + (((size_t)img * a.Hp + py) * a.Wp + px) * 64 + 16 * h;
+#pragma unroll
+        for (int t = 0; t < 2; ++t) {
+          *reinterpret_cast<uint4*>(dst + 32 * t) = make_uint4(o[t][0], o[t][1], o[t][2], o[t][3]);
+          *reinterpret_cast<uint4*>(dst + 32 * t + 8) = make_uint4(o[t][4], o[t][5], o[t][6], o[t][7]);
+        }
+      }
+    }
+    __syncthreads();  // ring refilled; edge reads done before the next pair overwrites them
+  }
+}
+
+}  // namespace
+}  // namespace rmbx
+
+extern "C" int rmbx_stem_s2d_conv_maxpool(const void* in, const void* weight, const float* bias, void* out, int N,
+                                          int Hs, int Ws, int band_rows, void* stream) {
+  RMBX_CHECK_ARG(in && weight && bias && out, "rmbx_stem_s2d_conv_maxpool: null pointer");
+  RMBX_CHECK_ARG(N >= 0 && Hs > 0 && Ws > 0, "rmbx_stem_s2d_conv_maxpool: bad geometry");
+  RMBX_CHECK_ARG(Ws <= 32 * rmbx::SP_MAX_WAVES, "rmbx_stem_s2d_conv_maxpool: Ws=%d exceeds %d", Ws,
+                 32 * rmbx::SP_MAX_WAVES);
+  RMBX_CHECK_ARG((((uintptr_t)in | (uintptr_t)weight | (uintptr_t)out) & 15) == 0,
+                 "rmbx_stem_s2d_conv_maxpool: in/weight/out must be 16-byte aligned");
+  if (N == 0) return RMBX_OK;
+  rmbx::StemPoolArgs a;
+  a.in = (const uint16_t*)in;
+  a.w = (const uint16_t*)weight;
+  a.bias = bias;
+  a.out = (uint16_t*)out;
+  a.N = N;
+  a.Hs = Hs;
+  a.Ws = Ws;
+  a.Hp = (Hs - 1) / 2 + 1;
+  a.Wp = (Ws - 1) / 2 + 1;
+  a.nct = (Ws + 31) / 32;
+  a.rc = 32 * a.nct + 4;
+  RMBX_CHECK_ARG(2 * 2 * a.rc <= 3 * 64 * a.nct, "rmbx_stem_s2d_conv_maxpool: prefetch does not fit");
+  // bands: the whole image per block once there are enough images to fill the chip
+  if (band_rows <= 0) {
+    const int want_blocks = 512;
+    int bands = (want_blocks + N - 1) / N;
+    if (bands > a.Hp) bands = a.Hp;
+    band_rows = (a.Hp + bands - 1) / bands;
+  }
+  a.band_rows = band_rows;
+  a.bands = (a.Hp + band_rows - 1) / band_rows;
+  const long long nblocks = (long long)N * a.bands;
+  RMBX_CHECK_ARG(nblocks < (1ll << 31), "rmbx_stem_s2d_conv_maxpool: grid too large");
+  hipLaunchKernelGGL(rmbx::stem_pool_kernel, dim3((unsigned)nblocks), dim3(64 * a.nct), 0, (hipStream_t)stream, a);
+  RMBX_CHECK_LAUNCH();
+  return RMBX_OK;
+}

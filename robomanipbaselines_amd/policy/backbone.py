@@ -164,5 +164,8 @@ class FusedResNet18Trunk(nn.Module):
             self._s2d_w = K.pack_stem_s2d(w.detach())
             self._s2d_zero = torch.zeros(w.shape[0], dtype=torch.float32, device=w.device)
             self._s2d_key = key
+        if w.shape[0] == 64 and x_s2d.shape[2] <= K.STEM_POOL_MAX_WS:
+            # conv + bias + ReLU + max-pool in one kernel: the full-resolution stem map stays on chip
+            return self.blocks(K.stem_s2d_conv_maxpool(x_s2d, self._s2d_w, self.stem.bias_f32()))
         s = K.stem_s2d_conv(x_s2d, self._s2d_w, self.stem.bias_f32(), relu=True)
         return self.blocks(K.nhwc_bias_relu_maxpool(s, self._s2d_zero))

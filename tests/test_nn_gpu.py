@@ -236,6 +236,36 @@ def test_stem_s2d_conv_matches_fp32():
 
 
 @torch.no_grad()
+@pytest.mark.parametrize("n,H,W,band_rows", [(2, 48, 64, 0), (3, 480, 640, 0), (2, 480, 640, 7),
+                                             (2, 46, 630, 5), (1, 34, 90, 1), (5, 20, 40, 0)])
+def test_stem_conv_maxpool_fused_equals_unfused(n, H, W, band_rows):
+    """rmbx_stem_s2d_conv_maxpool == rmbx_stem_s2d_conv + rmbx_nhwc_bias_relu_maxpool bit for bit
+    (full 480x640 frames, pool-row bands that split images, widths not a multiple of 32, odd
+    stem-map sizes)."""
+    from robomanipbaselines_amd import kernels as K
+
+    g = torch.Generator(device=DEV).manual_seed(11)
+    x = (torch.rand(n, 3, H, W, device=DEV, generator=g) * 4 - 2).to(torch.bfloat16)
+    w = (torch.randn(64, 3, 7, 7, device=DEV, generator=g) * 0.1).to(torch.bfloat16)
+    b = torch.randn(64, device=DEV, generator=g) * 0.5
+    xs, wp = K.image_to_s2d(x), K.pack_stem_s2d(w)
+    want = K.nhwc_bias_relu_maxpool(K.stem_s2d_conv(xs, wp, b), torch.zeros(64, device=DEV))
+    got = K.stem_s2d_conv_maxpool(xs, wp, b, band_rows=band_rows)
+    torch.cuda.synchronize()
+    assert got.shape == want.shape
+    assert torch.equal(got, want), (got.float() - want.float()).abs().max().item()
+
+
+def test_stem_conv_maxpool_rejects_wide_images():
+    from robomanipbaselines_amd import kernels as K
+
+    x = torch.zeros(1, 8, 322, 16, dtype=torch.bfloat16, device=DEV)
+    with pytest.raises(ValueError):
+        K.stem_s2d_conv_maxpool(x, torch.zeros(64, 4, 4, 16, dtype=torch.bfloat16, device=DEV),
+                                torch.zeros(64, device=DEV))
+
+
+@torch.no_grad()
 def test_trunk_s2d_matches_standard_layout():
     ref, fused = _trunk_pair(3)
     fused = fused.to(DEV, torch.bfloat16).to(memory_format=torch.channels_last)
