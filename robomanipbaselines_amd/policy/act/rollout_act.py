@@ -10,6 +10,7 @@ import torch
 from ... import kernels as K
 from ...common.rollout_base import BatchedRolloutBase
 from .act_model import IMAGENET_MEAN, IMAGENET_STD, ActModel
+from .checkpoint import load_act_checkpoint
 
 
 class RolloutAct(BatchedRolloutBase):
@@ -35,8 +36,8 @@ class RolloutAct(BatchedRolloutBase):
             num_cams=len(meta["image"]["camera_names"]),
         )
         if self.args.checkpoint:
-            sd = torch.load(self.args.checkpoint, map_location="cpu", weights_only=True)
-            self.policy.load_state_dict(sd, strict=False)
+            # the reference's ACTPolicy checkpoint (or ActModel's own), strictly (RolloutBase.py:376-385)
+            load_act_checkpoint(self.policy, self.args.checkpoint)
         self.policy.prune_dead_decoder = bool(self.args.act_prune_dead_decoder)
         self.policy_dtype = torch.bfloat16 if self.args.precision == "bf16" else torch.float32
         # MIOpen Find (measured solver choice per conv shape; once per shape, during warm-up):

@@ -1,0 +1,82 @@
+"""Trained-checkpoint loading: a reference ACTPolicy state_dict (keys of the
+upstream DETRVAE under `model.`, CVAE training-only modules included) loads strictly into
+ActModel; unknown or missing keys fail loudly.  CPU only."""
+
+import os
+import re
+
+import pytest
+import torch
+
+from robomanipbaselines_amd.policy.act.act_model import ActModel
+from robomanipbaselines_amd.policy.act.checkpoint import act_state_dict_from_reference, load_act_checkpoint
+
+
+def _small_act(seed):
+    torch.manual_seed(seed)
+    return ActModel(hidden_dim=64, dim_feedforward=96, nheads=4, enc_layers=2, dec_layers=3, num_queries=10)
+
+
+def _to_reference_names(sd):
+    """ActModel names -> ACTPolicy.state_dict() names (inverse of the loader's mapping), plus the
+    CVAE-encoder entries a trained ACTPolicy also carries."""
+    out = {}
+    for k, v in sd.items():
+        r = k
+        r = re.sub(r"^backbone\.", "backbones.0.0.body.", r)
+        r = re.sub(r"^encoder_layers\.(\d+)\.", r"transformer.encoder.layers.\1.", r)
+        r = re.sub(r"^decoder_layers\.(\d+)\.", r"transformer.decoder.layers.\1.", r)
+        r = re.sub(r"^decoder_norm\.", "transformer.decoder.norm.", r)
+        out["model." + r] = v.clone()
+    d = 64
+    out["model.cls_embed.weight"] = torch.randn(1, d)
+    out["model.encoder_action_proj.weight"] = torch.randn(d, 7)
+    out["model.encoder_action_proj.bias"] = torch.randn(d)
+    out["model.encoder_joint_proj.weight"] = torch.randn(d, 7)
+    out["model.encoder_joint_proj.bias"] = torch.randn(d)
+    out["model.latent_proj.weight"] = torch.randn(64, d)
+    out["model.latent_proj.bias"] = torch.randn(64)
+    out["model.pos_table"] = torch.randn(1, 12, d)
+    out["model.encoder.layers.0.self_attn.in_proj_weight"] = torch.randn(3 * d, d)
+    out["model.encoder.layers.0.linear1.weight"] = torch.randn(96, d)
+    return out
+
+
+def test_reference_checkpoint_roundtrip(tmp_path):
+    src = _small_act(1)
+    ref_sd = _to_reference_names(src.state_dict())
+    assert any(k.startswith("model.backbones.0.0.body.layer1.0.conv1") for k in ref_sd)
+    path = os.path.join(tmp_path, "policy_last.ckpt")
+    torch.save(ref_sd, path)
+    dst = _small_act(2)
+    load_act_checkpoint(dst, path)
+    for k, v in src.state_dict().items():
+        assert torch.equal(dst.state_dict()[k], v), k
+    x = torch.randn(2, 7)
+    img = torch.rand(2, 1, 3, 64, 96)
+    with torch.no_grad():
+        assert torch.equal(src.eval()(x, img), dst.eval()(x, img))
+
+
+def test_own_checkpoint_loads():
+    src, dst = _small_act(3), _small_act(4)
+    load_act_checkpoint(dst, src.state_dict())
+    assert all(torch.equal(dst.state_dict()[k], v) for k, v in src.state_dict().items())
+
+
+def test_mapping_drops_only_training_modules():
+    sd = act_state_dict_from_reference(_to_reference_names(_small_act(5).state_dict()))
+    assert set(sd) == set(_small_act(6).state_dict())
+
+
+@pytest.mark.parametrize("mutate", ["missing", "unexpected", "shape"])
+def test_mismatched_checkpoint_fails_loudly(mutate):
+    ref_sd = _to_reference_names(_small_act(7).state_dict())
+    if mutate == "missing":
+        del ref_sd["model.action_head.weight"]
+    elif mutate == "unexpected":
+        ref_sd["model.transformer.decoder.layers.9.linear1.weight"] = torch.zeros(96, 64)
+    else:
+        ref_sd["model.query_embed.weight"] = torch.zeros(11, 64)
+    with pytest.raises(ValueError):
+        load_act_checkpoint(_small_act(8), ref_sd)
