@@ -126,6 +126,11 @@ int rmbx_sched_reset(rmbx_sched_t* sched, const double* time, const uint8_t* mas
 int rmbx_sched_update(rmbx_sched_t* sched, const double* time, const double* reward,
                       const double* pre_durations, int n_pre, double max_duration,
                       double post_success_duration, int n_env, void* stream);
+/* active[e] = 1 while env e has not reached EndRolloutPhase (phase <= n_pre and not done), else
+ * 0: the step mask that freezes each env at its RolloutPhase -> EndRolloutPhase transition, so
+ * its final state (and a --save_last_image frame, RolloutBase.py:109-110, 541-561) is the
+ * transition step's, as the reference's saved image is. */
+int rmbx_sched_active(const rmbx_sched_t* sched, int n_pre, uint8_t* active, int n_env, void* stream);
 
 
 /* ---------------------------------------------------------------------------------------------

@@ -30,6 +30,7 @@ SIGNATURES = {
     "rmbx_ur5e_obs": (_c_int, [_c_p] * 8 + [_c_int, _c_p]),
     "rmbx_depth_linearize": (_c_int, [_c_p, _c_p, _c_sz, _c_d, _c_d, _c_p]),
     "rmbx_sched_reset": (_c_int, [_c_p, _c_p, _c_p, _c_int, _c_p]),
+    "rmbx_sched_active": (_c_int, [_c_p, _c_int, _c_p, _c_int, _c_p]),
     "rmbx_sched_update": (_c_int, [_c_p, _c_p, _c_p, _c_p, _c_int, _c_d, _c_d, _c_int, _c_p]),
     "rmbx_engine_create": (_c_int, [_c_p, _c_int, _c_p]),
     "rmbx_engine_destroy": (_c_int, [_c_p]),

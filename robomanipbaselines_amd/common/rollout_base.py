@@ -17,6 +17,8 @@ semantics, results schema) for a batch of envs:
 """
 
 import argparse
+import datetime
+import os
 import sys
 import time
 
@@ -55,6 +57,8 @@ class BatchedRolloutBase:
         self.pre_durations = [1.0] + [p.duration for p in self.pre_phases]  # Initial phase: 1.0 s
         self.result = {key: [] for key in ("success", "reward", "duration")}
         self.inference_duration_list = []
+        self.datetime_now = datetime.datetime.now()
+        self._active = None  # optional caller override of the per-env step mask
 
     # -- arguments (RolloutBase.setup_args :165-284 + batching flags) --------------------------
     def setup_args(self, parser=None, argv=None):
@@ -77,7 +81,9 @@ class BatchedRolloutBase:
         parser.add_argument("--save_last_image", action="store_true")
         parser.add_argument("--output_image_dir", type=str, default=".")
         # batching (this engine)
-        parser.add_argument("--num_envs", type=int, default=1, help="environments stepped in lockstep")
+        parser.add_argument("--num_envs", type=int, default=None,
+                            help="environments stepped in lockstep (default: one per --world_idx_list entry, "
+                                 "the episodes the reference runs one after another)")
         parser.add_argument("--device", type=str, default="cuda:0")
         parser.add_argument("--precision", choices=["fp32", "bf16"], default="bf16",
                             help="policy arithmetic: fp32 (parity mode) or bf16 (throughput mode)")
@@ -90,6 +96,8 @@ class BatchedRolloutBase:
         self.args = parser.parse_args(argv)
         if self.args.world_idx_list is None:
             self.args.world_idx_list = [self.args.world_idx]
+        if self.args.num_envs is None:
+            self.args.num_envs = len(self.args.world_idx_list)
         if self.args.world_random_scale is not None:
             self.args.world_random_scale = np.array(self.args.world_random_scale)
         self.args.auto_exit = True  # headless batched evaluation always auto-exits
@@ -208,6 +216,9 @@ class BatchedRolloutBase:
             self._st_range = torch.tensor(st["range"], dtype=torch.float64, device=dev)
         self.sched = K.sched_alloc(self.n, dev)
         K.sched_reset(self.sched, self.env.get_time())
+        # device-side step mask: an env stops stepping at its RolloutPhase -> EndRolloutPhase
+        # transition (rmbx_sched_active), freezing the state its results were recorded from
+        self._step_mask = torch.ones(self.n, dtype=torch.uint8, device=dev)
         self._pre = torch.tensor(self.pre_durations, dtype=torch.float64, device=dev)
         # host mirror of the (env-independent) pre-rollout clock
         self.phase_idx = 0
@@ -252,25 +263,25 @@ class BatchedRolloutBase:
 
     def step_once(self):
         self._pre_update()
-        self.obs, self.reward, _, _, _ = self.env.step(self.env_action(), active=self._active)
+        active = self._active if self._active is not None else self._step_mask
+        self.obs, self.reward, _, _, _ = self.env.step(self.env_action(), active=active)
         for _ in range(self.env.frame_skip):
             self.host_time += self.env.sim_timestep
         K.sched_update(self.sched, self.env.get_time(), self.reward, self._pre, self.args.max_duration)
+        K.sched_active(self.sched, len(self.pre_durations), out=self._step_mask)
         self._host_transition()
 
     def run(self, max_steps=None):
         self.reset()
-        self._active = None
         max_steps = max_steps or self.args.max_steps or 10**9
         steps = 0
         while steps < max_steps:
             self.step_once()
             steps += 1
+            # finished envs are frozen on the device (step mask); the host only polls for the end
             if self.phase_idx >= len(self.pre_durations) and steps % 16 == 0:
-                v = K.sched_view(self.sched)
-                if v["done"].all():
+                if K.sched_view(self.sched)["done"].all():
                     break
-                self._active = torch.tensor(1 - v["done"], dtype=torch.uint8, device=self.device)
         self.finish()
         return steps
 
@@ -282,10 +293,40 @@ class BatchedRolloutBase:
             self.result["success"].append(succ)
             self.result["reward"].append(float(v["result_reward"][e]))
             self.result["duration"].append(float(v["duration"][e]))
+        if self.args.save_last_image:
+            self.save_rgb_images(v)
         if self.args.result_filename is not None:
+            print(f"[{self.__class__.__name__}] Save the rollout results: {self.args.result_filename}")
             with open(self.args.result_filename, "w") as f:
                 yaml.dump(self.result, f)
         self.print_statistics()
+
+    def save_rgb_images(self, v=None):
+        """RolloutBase.save_rgb_image (:541-561) for every env: the last frame of all cameras side
+        by side (cv2.hconcat of info["rgb_images"]), named
+        Rollout<Policy>_<Env>_world<idx>_<success|failure>_<datetime>.png in --output_image_dir.
+        Each env is frozen at its episode's end, so its frame is the transition step's."""
+        from .image_io import write_png
+
+        if v is None:
+            v = K.sched_view(self.sched)
+        H, W = self.env.renderer.height, self.env.renderer.width
+        frames = []
+        for cam in self.env.camera_names:
+            rgb = torch.empty((self.n, H, W, 3), dtype=torch.uint8, device=self.device)
+            self.env.render_images(cam, rgb=rgb)
+            frames.append(rgb)
+        image = torch.cat(frames, dim=2).cpu().numpy()
+        demo_name = self.env.demo_name
+        os.makedirs(self.args.output_image_dir, exist_ok=True)
+        for e in range(self.n):
+            success_str = "success" if v["success"][e] else "failure"
+            path = os.path.abspath(os.path.join(
+                self.args.output_image_dir,
+                f"Rollout{self.policy_name}_{demo_name}_world{int(self.world_idx[e]):0>1}_{success_str}_"
+                f"{self.datetime_now:%Y%m%d_%H%M%S}_env{e}.png"))
+            print(f"[{self.__class__.__name__}] Save the observation image of the last frame: {path}")
+            write_png(path, image[e])
 
     def print_statistics(self):
         print(f"[{self.__class__.__name__}] Statistics on policy inference")

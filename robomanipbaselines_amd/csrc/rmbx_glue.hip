@@ -280,6 +280,13 @@ __global__ void sched_update_kernel(rmbx_sched_t* __restrict__ s, const double* 
   s[e] = v;
 }
 
+__global__ void sched_active_kernel(const rmbx_sched_t* __restrict__ s, int n_pre, uint8_t* __restrict__ active,
+                                    int n_env) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n_env) return;
+  active[e] = (!s[e].done && s[e].phase <= n_pre) ? 1 : 0;
+}
+
 }  // namespace rmbx
 
 // =========================================================================================
@@ -378,6 +385,15 @@ int rmbx_sched_update(rmbx_sched_t* sched, const double* time, const double* rew
   hipLaunchKernelGGL(sched_update_kernel, dim3((n_env + 255) / 256), dim3(256), 0,
                      as_stream(stream), sched, time, reward, pre_durations, n_pre, max_duration,
                      post_success_duration, n_env);
+  RMBX_CHECK_LAUNCH();
+  return RMBX_OK;
+}
+
+int rmbx_sched_active(const rmbx_sched_t* sched, int n_pre, uint8_t* active, int n_env, void* stream) {
+  RMBX_CHECK_ARG(sched && active && n_env >= 0 && n_pre >= 0, "rmbx_sched_active: bad arguments");
+  if (n_env == 0) return RMBX_OK;
+  hipLaunchKernelGGL(sched_active_kernel, dim3((n_env + 255) / 256), dim3(256), 0, as_stream(stream), sched, n_pre,
+                     active, n_env);
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
 }

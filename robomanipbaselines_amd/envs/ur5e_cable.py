@@ -31,6 +31,7 @@ class BatchedMujocoUR5eCableEnv:
     sim_timestep = 0.004  # MujocoEnvBase.py:12
     frame_skip = 8  # MujocoEnvBase.py:13
     command_keys_for_step = ["command_joint_pos"]  # EnvDataMixin.py:5-7
+    demo_name = "MujocoUR5eCable"  # remove_suffix(env.spec.name, "Env") (RolloutBase.py:545)
 
     def __init__(self, num_envs, device="cuda:0", world_random_scale=None, seed=0, image_size=(480, 640),
                  model_name="ur5e_cable"):

@@ -201,6 +201,17 @@ def sched_update(sched, time, reward, pre_durations, max_duration, post_success=
            pre_durations.numel(), float(max_duration), float(post_success), n, N.stream_ptr())
 
 
+def sched_active(sched, n_pre, out=None):
+    """uint8 [n] step mask: 1 until the env reaches EndRolloutPhase (rmbx_sched_active)."""
+    n = sched.shape[0]
+    _chk(sched, torch.uint8, (n, N.SCHED_DTYPE.itemsize), "sched")
+    if out is None:
+        out = torch.empty(n, dtype=torch.uint8, device=sched.device)
+    _chk(out, torch.uint8, (n,), "out")
+    N.call("rmbx_sched_active", N.ptr(sched), int(n_pre), N.ptr(out), n, N.stream_ptr())
+    return out
+
+
 # ------------------------------------------------------------------------------------------
 # Vision-trunk epilogues (NHWC = torch channels_last)
 # ------------------------------------------------------------------------------------------

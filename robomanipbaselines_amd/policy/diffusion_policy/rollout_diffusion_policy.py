@@ -52,7 +52,9 @@ class RolloutDiffusionPolicy(BatchedRolloutBase):
             sd = torch.load(self.args.checkpoint, map_location="cpu", weights_only=True)
             self.policy.load_state_dict(sd, strict=False)
         self.policy_dtype = torch.bfloat16 if self.args.precision == "bf16" else torch.float32
-        torch.backends.cudnn.benchmark = True
+        # heuristic (not benchmarked) MIOpen solver choice: with cudnn.benchmark the selected
+        # solvers, and so the bits of the UNet's outputs, can differ from call to call
+        torch.backends.cudnn.benchmark = False
         # deterministic MIOpen solvers: without them the UNet's conv1d results vary run to run
         # (atomic split-K), so the same seed would not reproduce the same episodes
         torch.backends.cudnn.deterministic = True

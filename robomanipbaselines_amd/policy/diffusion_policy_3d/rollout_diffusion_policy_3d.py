@@ -50,7 +50,9 @@ class RolloutDiffusionPolicy3d(RolloutDiffusionPolicy):
             sd = torch.load(self.args.checkpoint, map_location="cpu", weights_only=True)
             self.policy.load_state_dict(sd, strict=False)
         self.policy_dtype = torch.bfloat16 if self.args.precision == "bf16" else torch.float32
-        torch.backends.cudnn.benchmark = True
+        # heuristic (not benchmarked) MIOpen solver choice: with cudnn.benchmark the selected
+        # solvers, and so the bits of the UNet's outputs, can differ from call to call
+        torch.backends.cudnn.benchmark = False
         torch.backends.cudnn.deterministic = True
         self.policy = self.policy.eval().requires_grad_(False).to(device=self.device, dtype=self.policy_dtype)
 

@@ -20,7 +20,8 @@ def _small_model(**kw):
 
 @torch.no_grad()
 def test_graph_replay_equals_eager():
-    torch.backends.cudnn.deterministic = True  # as RolloutDiffusionPolicy sets it
+    torch.backends.cudnn.deterministic = True  # as RolloutDiffusionPolicy sets them
+    torch.backends.cudnn.benchmark = False
     m = _small_model(num_inference_steps=100).to(DEV)
     B = 5
     g = torch.Generator(device=DEV).manual_seed(3)
