@@ -77,6 +77,15 @@ int rmbx_cable_reward(const double* cable_xpos, const double* end_xpos,
                       const double* pole1_xpos, const double* pole2_xpos, double* reward,
                       int n_env, int n_cable, void* stream);
 
+/* Peg-in-hole success predicate, batched.
+ * Replaces envs/mujoco/ur5e/MujocoUR5eInsertEnv.py:43-63 (_get_reward): 1 iff
+ * max|peg.xy - hole.xy| < xy_thre (0.012), peg.z < hole.z + z_offset (0.05) and
+ * dot(peg z axis, (0, 0, -1)) > cos_tilt (np.cos(np.deg2rad(10)), passed in from the host).
+ * peg_xpos / hole_xpos f64 [n_env][3], peg_xquat f64 [n_env][4] (z axis = column 2 of
+ * mju_quat2Mat); reward f64 [n_env].  Bit-exact: numpy's operation order, NaN -> 0. */
+int rmbx_insert_reward(const double* peg_xpos, const double* hole_xpos, const double* peg_xquat, double* reward,
+                       int n_env, double xy_thre, double z_offset, double cos_tilt, void* stream);
+
 /* ---------------------------------------------------------------------------------------------
  * UR5e observation mapping, batched.
  * Replaces envs/mujoco/ur5e/MujocoUR5eEnvBase.py:78-119 (_get_obs):

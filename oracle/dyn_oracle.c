@@ -789,6 +789,8 @@ static int contact_deeper(const Contact* a, const Contact* b) {
   return floor(a->dist * 1e9) < floor(b->dist * 1e9);
 }
 
+#define BOX_INSIDE_TOL 1e-9 /* m */
+
 static int col_box_box(const double* ca, const double* Ra, const double* ha, const double* cb,
                        const double* Rb, const double* hb, double margin, Contact* out) {
   double axes[15][3];
@@ -860,10 +862,13 @@ static int col_box_box(const double* ca, const double* Ra, const double* ha, con
       double l[3] = {(v & 1) ? h[0] : -h[0], (v & 2) ? h[1] : -h[1], (v & 4) ? h[2] : -h[2]}, w[3];
       matvec3(R, l, w);
       double x[3] = {c[0] + w[0], c[1] + w[1], c[2] + w[2]};
-      /* inside the other box (with margin)? */
+      /* inside the other box (with margin)?  A vertex within BOX_INSIDE_TOL of a face plane
+       * counts as inside, so aligned equal faces (the gripper pads closing on each other) give
+       * the same manifold however the last bits of the poses fall */
       double dl[3] = {x[0] - co[0], x[1] - co[1], x[2] - co[2]}, lo[3];
       mattvec3(Ro, dl, lo);
-      if (fabs(lo[0]) > ho[0] + margin || fabs(lo[1]) > ho[1] + margin || fabs(lo[2]) > ho[2] + margin)
+      const double tol = margin + BOX_INSIDE_TOL;
+      if (fabs(lo[0]) > ho[0] + tol || fabs(lo[1]) > ho[1] + tol || fabs(lo[2]) > ho[2] + tol)
         continue;
       /* penetration along n relative to the other box's support plane */
       double sup = 0;

@@ -95,6 +95,33 @@ def cable_reward(cable, end, p1, p2):
 # ------------------------------------------------------------------------------------------
 # envs/mujoco/ur5e/MujocoUR5eEnvBase.py:78-119
 # ------------------------------------------------------------------------------------------
+def quat2mat(q):
+    """mju_quat2Mat (mujoco==3.1.6 engine_util_spatial.c, external): row-major 3x3."""
+    q = np.asarray(q, dtype=np.float64)
+    if q[0] == 1 and q[1] == 0 and q[2] == 0 and q[3] == 0:
+        return np.eye(3)
+    q00, q01, q02, q03 = q[0] * q[0], q[0] * q[1], q[0] * q[2], q[0] * q[3]
+    q11, q12, q13 = q[1] * q[1], q[1] * q[2], q[1] * q[3]
+    q22, q23, q33 = q[2] * q[2], q[2] * q[3], q[3] * q[3]
+    return np.array([[q00 + q11 - q22 - q33, 2 * (q12 - q03), 2 * (q13 + q02)],
+                     [2 * (q12 + q03), q00 - q11 + q22 - q33, 2 * (q23 - q01)],
+                     [2 * (q13 - q02), 2 * (q23 + q01), q00 - q11 - q22 + q33]])
+
+
+def insert_reward(peg_pos, hole_pos, peg_quat):
+    """envs/mujoco/ur5e/MujocoUR5eInsertEnv.py:43-63 (_get_reward), with the peg's xmat from its
+    xquat (the engine keeps body orientations as quaternions)."""
+    peg_z_axis = quat2mat(peg_quat)[:, 2]
+    world_z_axis = np.array([0.0, 0.0, -1.0])
+    xy_thre = 0.012
+    z_thre = hole_pos[2] + 0.05
+    tilt_thre = 10
+    if (np.max(np.abs(peg_pos[:2] - hole_pos[:2])) < xy_thre) and (peg_pos[2] < z_thre) and (
+            np.dot(peg_z_axis, world_z_axis) > np.cos(np.deg2rad(tilt_thre))):
+        return 1.0
+    return 0.0
+
+
 def ur5e_obs(arm_qpos, arm_qvel, grip_qpos, force, torque):
     g = np.rad2deg(np.asarray(grip_qpos, np.float64).mean(keepdims=True)) / 45.0 * 255.0
     return (

@@ -34,8 +34,9 @@ from ..common.data_utils import make_meta_info
 class PhaseSpec:
     """Timed phase of the pre-rollout motion (PhaseBase.ReachPhaseBase / GraspPhaseBase)."""
 
-    def __init__(self, name, duration, kind, pos_z=None):
-        self.name, self.duration, self.kind, self.pos_z = name, duration, kind, pos_z
+    def __init__(self, name, duration, kind, pos_z=None, grip=None):
+        # grip: gripper command of a grasp phase (None = action_space.high, set_target_close)
+        self.name, self.duration, self.kind, self.pos_z, self.grip = name, duration, kind, pos_z, grip
 
 
 class BatchedRolloutBase:
@@ -237,7 +238,8 @@ class BatchedRolloutBase:
             if ph.kind == "reach":
                 self._ik_step()
             elif ph.kind == "grasp":
-                self.grip_cmd.fill_(self._ghi)  # GraspPhaseBase.set_target_close (:78-104)
+                # GraspPhaseBase.pre_update (:66-69): set_target_close (:78-104) or a fixed value
+                self.grip_cmd.fill_(self._ghi if ph.grip is None else float(ph.grip))
         elif self.phase_idx == n_pre:
             if self.rollout_time_idx % self.args.skip == 0:
                 t0 = time.time()

@@ -716,6 +716,8 @@ __device__ __forceinline__ bool contact_deeper(const Contact* a, const Contact* 
   return floor(a->dist * 1e9) < floor(b->dist * 1e9);
 }
 
+constexpr double BOX_INSIDE_TOL = 1e-9;  // m
+
 __device__ int col_box_box(const double* ca, const double* Ra, const double* ha, const double* cb,
                            const double* Rb, const double* hb, double margin, Contact* out) {
   double axes[15][3];
@@ -785,8 +787,10 @@ __device__ int col_box_box(const double* ca, const double* Ra, const double* ha,
       const double dl[3] = {x[0] - co[0], x[1] - co[1], x[2] - co[2]};
       double lo[3];
       mattvec3(Ro, dl, lo);
-      if (fabs(lo[0]) > ho[0] + margin || fabs(lo[1]) > ho[1] + margin ||
-          fabs(lo[2]) > ho[2] + margin)
+      // a vertex within BOX_INSIDE_TOL of a face plane counts as inside (aligned equal faces, e.g.
+      // the gripper pads closing on each other, keep one manifold whatever their last bits)
+      const double tol = margin + BOX_INSIDE_TOL;
+      if (fabs(lo[0]) > ho[0] + tol || fabs(lo[1]) > ho[1] + tol || fabs(lo[2]) > ho[2] + tol)
         continue;
       double sup = 0;
       for (int i = 0; i < 3; i++) {

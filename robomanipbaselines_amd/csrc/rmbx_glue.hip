@@ -172,6 +172,40 @@ __global__ void cable_reward_kernel(const double* __restrict__ cable_xpos,
 }
 
 // -----------------------------------------------------------------------------------------
+// Peg-in-hole success predicate (envs/mujoco/ur5e/MujocoUR5eInsertEnv.py:43-63)
+// -----------------------------------------------------------------------------------------
+__device__ double insert_reward_one(const double* __restrict__ peg, const double* __restrict__ hole,
+                                    const double* __restrict__ q, double xy_thre, double z_off, double cos_tilt) {
+  // np.max(np.abs(peg_pos[:2] - hole_pos[:2])) < xy_thre, NaN-propagating like numpy's max
+  const double dx = fabs(peg[0] - hole[0]), dy = fabs(peg[1] - hole[1]);
+  if (isnan(dx) || isnan(dy)) return 0.0;
+  const double m = dy > dx ? dy : dx;
+  if (!(m < xy_thre)) return 0.0;
+  const double z_thre = hole[2] + z_off;
+  if (!(peg[2] < z_thre)) return 0.0;
+  // peg z axis = xmat[:, 2] (mju_quat2Mat of xquat); np.dot with (0, 0, -1) in numpy's order
+  const double q00 = q[0] * q[0], q01 = q[0] * q[1], q02 = q[0] * q[2];
+  const double q11 = q[1] * q[1], q13 = q[1] * q[3], q22 = q[2] * q[2], q23 = q[2] * q[3], q33 = q[3] * q[3];
+  const bool ident = q[0] == 1.0 && q[1] == 0.0 && q[2] == 0.0 && q[3] == 0.0;
+  const double zx = ident ? 0.0 : 2.0 * (q13 + q02);
+  const double zy = ident ? 0.0 : 2.0 * (q23 - q01);
+  const double zz = ident ? 1.0 : ((q00 - q11) - q22) + q33;
+  double dot = zx * 0.0;
+  dot = dot + zy * 0.0;
+  dot = dot + zz * -1.0;
+  return dot > cos_tilt ? 1.0 : 0.0;
+}
+
+__global__ void insert_reward_kernel(const double* __restrict__ peg_xpos, const double* __restrict__ hole_xpos,
+                                     const double* __restrict__ peg_xquat, double* __restrict__ reward, int n_env,
+                                     double xy_thre, double z_off, double cos_tilt) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n_env) return;
+  reward[e] = insert_reward_one(peg_xpos + 3 * (size_t)e, hole_xpos + 3 * (size_t)e, peg_xquat + 4 * (size_t)e,
+                                xy_thre, z_off, cos_tilt);
+}
+
+// -----------------------------------------------------------------------------------------
 // UR5e observation mapping (envs/mujoco/ur5e/MujocoUR5eEnvBase.py:78-119)
 // -----------------------------------------------------------------------------------------
 __device__ __forceinline__ double gripper_joint_pos(const double* g) {
@@ -335,6 +369,17 @@ int rmbx_cable_reward(const double* cable_xpos, const double* end_xpos, const do
   hipLaunchKernelGGL(cable_reward_kernel, dim3((n_env + 255) / 256), dim3(256), 0,
                      as_stream(stream), cable_xpos, end_xpos, pole1_xpos, pole2_xpos, reward,
                      n_env, n_cable);
+  RMBX_CHECK_LAUNCH();
+  return RMBX_OK;
+}
+
+int rmbx_insert_reward(const double* peg_xpos, const double* hole_xpos, const double* peg_xquat, double* reward,
+                       int n_env, double xy_thre, double z_offset, double cos_tilt, void* stream) {
+  RMBX_CHECK_ARG(n_env >= 0, "bad n_env=%d", n_env);
+  RMBX_CHECK_ARG(peg_xpos && hole_xpos && peg_xquat && reward, "NULL buffer");
+  if (n_env == 0) return RMBX_OK;
+  hipLaunchKernelGGL(insert_reward_kernel, dim3((n_env + 255) / 256), dim3(256), 0, as_stream(stream), peg_xpos,
+                     hole_xpos, peg_xquat, reward, n_env, xy_thre, z_offset, cos_tilt);
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
 }

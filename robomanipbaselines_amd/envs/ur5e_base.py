@@ -1,0 +1,155 @@
+"""Batched UR5e MuJoCo environment base (n_env instances in lockstep on one GPU).
+
+Counterpart of envs/mujoco/ur5e/MujocoUR5eEnvBase.py + envs/mujoco/MujocoEnvBase.py of the
+reference, with the gymnasium-style API and the Isaac-style vector attributes (num_envs,
+rep_env_idx; envs/isaac/IsaacUR5eEnvBase.py:104-106, 379-431) the reference's only vectorised env
+exposes.  Every per-step computation runs in HIP kernels behind the C ABI: physics
+(rmbx_engine_step), observation mapping (rmbx_ur5e_obs), the task's success predicate and camera
+rendering (rmbx_render).  Tensors stay resident on the device.  Task subclasses
+(ur5e_cable.py, ur5e_insert.py) name the compiled scene, the initial arm/gripper pose, the body
+that modify_world moves per world index, and the reward kernel.
+"""
+
+import numpy as np
+import torch
+
+from .. import _native as N  # noqa: F401  (fails loudly if librmbx.so is missing)
+from .. import kernels as K
+from .. import model as MD
+from ..engine import PhysicsEngine
+from ..render import Renderer
+
+ARM_JOINTS = ["shoulder_pan_joint", "shoulder_lift_joint", "elbow_joint", "wrist_1_joint", "wrist_2_joint", "wrist_3_joint"]
+GRIPPER_JOINTS = ["right_driver_joint", "right_spring_link_joint", "left_driver_joint", "left_spring_link_joint"]
+
+
+class BatchedMujocoUR5eEnvBase:
+    sim_timestep = 0.004  # MujocoEnvBase.py:12
+    frame_skip = 8  # MujocoEnvBase.py:13
+    command_keys_for_step = ["command_joint_pos"]  # EnvDataMixin.py:5-7
+    # task definition (subclasses)
+    model_name = None
+    demo_name = None  # remove_suffix(env.spec.name, "Env") (RolloutBase.py:545)
+    init_qpos_head = None  # the env's init_qpos[:14] (6 arm joints + 8 gripper joints)
+    world_body = None  # body moved by modify_world
+    world_offsets = None  # [n_world, 3] offsets of world_body per world index
+
+    def __init__(self, num_envs, device="cuda:0", world_random_scale=None, seed=0, image_size=(480, 640),
+                 model_name=None):
+        model_name = model_name or self.model_name
+        self.num_envs = int(num_envs)
+        self.device = torch.device(device)
+        self.arrays = MD.load(model_name)
+        self.info = MD.ModelInfo(self.arrays)
+        self.engine = PhysicsEngine(self.arrays, self.num_envs, device)
+        self.renderer = Renderer(self.arrays, device, width=image_size[1], height=image_size[0])
+        self.world_random_scale = world_random_scale
+        self.seed = int(seed)
+        self.rep_env_idx = 0
+        inf = self.info
+        self._arm_qadr = torch.tensor([inf.qposadr(j) for j in ARM_JOINTS], device=self.device)
+        self._arm_dadr = torch.tensor([inf.dofadr(j) for j in ARM_JOINTS], device=self.device)
+        self._grip_qadr = torch.tensor([inf.qposadr(j) for j in GRIPPER_JOINTS], device=self.device)
+        names = [str(x) for x in self.arrays["names_body"]]
+        self._names_body = names
+        self._world_body = names.index(self.world_body)
+        self.original_world_pos = self.arrays["body_pos"][self._world_body].copy()
+        self.init_qpos = self.arrays["qpos0"].copy()
+        self.init_qpos[: len(self.init_qpos_head)] = self.init_qpos_head
+        self._setup_task()
+        ctrl = self.arrays["act_ctrlrange"]
+        self.action_low, self.action_high = ctrl[:, 0].copy(), ctrl[:, 1].copy()
+        self.camera_names = [str(x) for x in self.arrays["names_cam"]]
+        self.reward = torch.zeros(self.num_envs, dtype=torch.float64, device=self.device)
+        self.world_idx = np.zeros(self.num_envs, dtype=np.int64)
+
+    # -- reference API ----------------------------------------------------------------------
+    def _setup_task(self):
+        pass
+
+    def modify_world(self, world_idx=None, cumulative_idx=None):
+        """<Task>Env.modify_world for every env (MujocoUR5eCableEnv.py:107-118,
+        MujocoUR5eInsertEnv.py:65-76): the task body's offset per world index plus U(-s, s)^3
+        noise from a per-env Philox stream (seed, env index)."""
+        n = self.num_envs
+        offsets = np.asarray(self.world_offsets, dtype=np.float64)
+        if world_idx is None:
+            world_idx = np.asarray(cumulative_idx) % len(offsets)
+        world_idx = np.broadcast_to(np.asarray(world_idx, dtype=np.int64), (n,)).copy()
+        pos = self.original_world_pos[None] + offsets[world_idx]
+        if self.world_random_scale is not None:
+            s = np.asarray(self.world_random_scale, dtype=np.float64)
+            for e in range(n):
+                rng = np.random.Generator(np.random.Philox(key=self.seed, counter=[e, 0, 0, 0]))
+                pos[e] += rng.uniform(low=-1.0 * s, high=s, size=3)
+        bp = self.engine.body_pos
+        bp[:, self._world_body, :] = torch.tensor(pos, dtype=torch.float64, device=self.device)
+        self.world_idx = world_idx
+        return world_idx
+
+    def reset(self, seed=None, mask=None):
+        """MujocoEnvBase.reset_model (:163-165): qpos = init_qpos, qvel = 0, time = 0, then
+        mj_forward; returns (obs, info)."""
+        e = self.engine
+        q0 = torch.tensor(self.init_qpos, dtype=torch.float64, device=self.device)
+        ctrl0 = torch.tensor(np.concatenate([self.init_qpos[:6], [0.0]]), dtype=torch.float64, device=self.device)
+        if mask is None:
+            e.qpos.copy_(q0.expand_as(e.qpos))
+            e.qvel.zero_()
+            e.qacc_ws.zero_()
+            e.time.zero_()
+            e.ctrl.copy_(ctrl0.expand_as(e.ctrl))
+            e.stats.zero_()
+        else:
+            m = mask.bool()
+            e.qpos[m] = q0
+            e.qvel[m] = 0
+            e.qacc_ws[m] = 0
+            e.time[m] = 0
+            e.ctrl[m] = ctrl0
+            e.stats[m] = 0
+        e.forward()
+        self.reward = self._get_reward()
+        return self._get_obs(), {}
+
+    def step(self, action, active=None):
+        """MujocoEnvBase.step (:82-97): ctrl = action; frame_skip x mj_step; obs; reward.
+        action: f64 [n, nu] device tensor.  Images are rendered on demand (render_images)."""
+        e = self.engine
+        if action is not None:
+            e.ctrl.copy_(action)
+        e.step(self.frame_skip, active=active)
+        obs = self._get_obs()
+        self.reward = self._get_reward()
+        return obs, self.reward, False, False, {}
+
+    def get_time(self):
+        return self.engine.time
+
+    def get_camera_fovy(self, camera_name):
+        return float(self.arrays["cam_fovy"][self.camera_names.index(camera_name)])
+
+    def get_body_pose(self, body_name):
+        b = self.info.body[body_name]
+        return torch.cat([self.engine.xpos[:, b], self.engine.xquat[:, b]], dim=1)
+
+    # -- internals ----------------------------------------------------------------------------
+    def _get_obs(self):
+        e = self.engine
+        arm_q = e.qpos.index_select(1, self._arm_qadr).contiguous()
+        arm_v = e.qvel.index_select(1, self._arm_dadr).contiguous()
+        grip = e.qpos.index_select(1, self._grip_qadr).contiguous()
+        force = e.sensordata[:, 0:3].contiguous()
+        torque = e.sensordata[:, 3:6].contiguous()
+        jp, jv, wr = K.ur5e_obs(arm_q, arm_v, grip, force, torque)
+        return {"joint_pos": jp, "joint_vel": jv, "wrench": wr}
+
+    def _get_reward(self):
+        raise NotImplementedError
+
+    def render_images(self, camera_name="front", rgb=None, depth=None, policy=None, active=None, mean=None, std=None):
+        """MujocoEnvBase._get_info (:103-126) for one camera, all envs; `policy` receives
+        ((rgb / 255) - mean) / std as [n, 3, H, W]."""
+        self.renderer.render(self.engine, camera_name, rgb=rgb, depth=depth, policy=policy, active=active,
+                             mean=mean, std=std)
+        return rgb, depth, policy

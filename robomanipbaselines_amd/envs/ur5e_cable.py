@@ -1,21 +1,10 @@
-"""Batched MujocoUR5eCable environment (n_env instances in lockstep on one GPU).
-
-Counterpart of envs/mujoco/ur5e/MujocoUR5eCableEnv.py + MujocoUR5eEnvBase.py + MujocoEnvBase.py
-of the reference, with the gymnasium-style API and the Isaac-style vector attributes
-(num_envs, rep_env_idx; envs/isaac/IsaacUR5eEnvBase.py:104-106, 379-431) the reference's only
-vectorised env exposes.  Every per-step computation runs in HIP kernels behind the C ABI:
-physics (rmbx_engine_step), observation mapping (rmbx_ur5e_obs), success predicate
-(rmbx_cable_reward) and camera rendering (rmbx_render).  Tensors stay resident on the device.
-"""
+"""Batched MujocoUR5eCable environment: envs/mujoco/ur5e/MujocoUR5eCableEnv.py of the reference
+on the batched UR5e base (ur5e_base.py); success predicate = rmbx_cable_reward."""
 
 import numpy as np
-import torch
 
-from .. import _native as N  # noqa: F401  (fails loudly if librmbx.so is missing)
 from .. import kernels as K
-from .. import model as MD
-from ..engine import PhysicsEngine
-from ..render import Renderer
+from .ur5e_base import ARM_JOINTS, GRIPPER_JOINTS, BatchedMujocoUR5eEnvBase  # noqa: F401
 
 # MujocoUR5eCableEnv.py:20-30 (init_qpos[:14])
 CABLE_INIT_QPOS = np.array([np.pi, -np.pi / 2, -0.75 * np.pi, -0.25 * np.pi, np.pi / 2, np.pi / 2, *np.zeros(8)])
@@ -23,123 +12,25 @@ CABLE_INIT_QPOS = np.array([np.pi, -np.pi / 2, -0.75 * np.pi, -0.25 * np.pi, np.
 POLE_POS_OFFSETS = np.array(
     [[-0.03, 0.0, 0.0], [0.0, 0.0, 0.0], [0.03, 0.0, 0.0], [0.06, 0.0, 0.0], [0.09, 0.0, 0.0], [0.12, 0.0, 0.0]]
 )
-ARM_JOINTS = ["shoulder_pan_joint", "shoulder_lift_joint", "elbow_joint", "wrist_1_joint", "wrist_2_joint", "wrist_3_joint"]
-GRIPPER_JOINTS = ["right_driver_joint", "right_spring_link_joint", "left_driver_joint", "left_spring_link_joint"]
 
 
-class BatchedMujocoUR5eCableEnv:
-    sim_timestep = 0.004  # MujocoEnvBase.py:12
-    frame_skip = 8  # MujocoEnvBase.py:13
-    command_keys_for_step = ["command_joint_pos"]  # EnvDataMixin.py:5-7
-    demo_name = "MujocoUR5eCable"  # remove_suffix(env.spec.name, "Env") (RolloutBase.py:545)
+class BatchedMujocoUR5eCableEnv(BatchedMujocoUR5eEnvBase):
+    model_name = "ur5e_cable"
+    demo_name = "MujocoUR5eCable"
+    init_qpos_head = CABLE_INIT_QPOS
+    world_body = "poles"
+    world_offsets = POLE_POS_OFFSETS
 
-    def __init__(self, num_envs, device="cuda:0", world_random_scale=None, seed=0, image_size=(480, 640),
-                 model_name="ur5e_cable"):
-        self.num_envs = int(num_envs)
-        self.device = torch.device(device)
-        self.arrays = MD.load(model_name)
-        self.info = MD.ModelInfo(self.arrays)
-        self.engine = PhysicsEngine(self.arrays, self.num_envs, device)
-        self.renderer = Renderer(self.arrays, device, width=image_size[1], height=image_size[0])
-        self.world_random_scale = world_random_scale
-        self.seed = int(seed)
-        self.rep_env_idx = 0
-        inf = self.info
-        self._arm_qadr = torch.tensor([inf.qposadr(j) for j in ARM_JOINTS], device=self.device)
-        self._arm_dadr = torch.tensor([inf.dofadr(j) for j in ARM_JOINTS], device=self.device)
-        self._grip_qadr = torch.tensor([inf.qposadr(j) for j in GRIPPER_JOINTS], device=self.device)
-        names = [str(x) for x in self.arrays["names_body"]]
+    def _setup_task(self):
+        names, inf = self._names_body, self.info
         self._cable_bodies = [i for i, n in enumerate(names) if n.startswith("cable_B")]
         assert self._cable_bodies == list(range(self._cable_bodies[0], self._cable_bodies[0] + len(self._cable_bodies)))
         self._cable_end = names.index("cable_end")
-        self._poles_body = names.index("poles")
         self._pole_geoms = [inf.geom["pole1"], inf.geom["pole2"]]
-        self.original_pole_pos = self.arrays["body_pos"][self._poles_body].copy()
-        self.init_qpos = self.arrays["qpos0"].copy()
-        self.init_qpos[: len(CABLE_INIT_QPOS)] = CABLE_INIT_QPOS
-        ctrl = self.arrays["act_ctrlrange"]
-        self.action_low, self.action_high = ctrl[:, 0].copy(), ctrl[:, 1].copy()
-        self.camera_names = [str(x) for x in self.arrays["names_cam"]]
-        self.reward = torch.zeros(self.num_envs, dtype=torch.float64, device=self.device)
-        self.world_idx = np.zeros(self.num_envs, dtype=np.int64)
-
-    # -- reference API ----------------------------------------------------------------------
-    def modify_world(self, world_idx=None, cumulative_idx=None):
-        """MujocoUR5eCableEnv.modify_world (:107-118) for every env: pole offset per world index
-        plus U(-s, s)^3 noise from a per-env Philox stream (seed, env index)."""
-        n = self.num_envs
-        if world_idx is None:
-            world_idx = np.asarray(cumulative_idx) % len(POLE_POS_OFFSETS)
-        world_idx = np.broadcast_to(np.asarray(world_idx, dtype=np.int64), (n,)).copy()
-        pos = self.original_pole_pos[None] + POLE_POS_OFFSETS[world_idx]
-        if self.world_random_scale is not None:
-            s = np.asarray(self.world_random_scale, dtype=np.float64)
-            for e in range(n):
-                rng = np.random.Generator(np.random.Philox(key=self.seed, counter=[e, 0, 0, 0]))
-                pos[e] += rng.uniform(low=-1.0 * s, high=s, size=3)
-        bp = self.engine.body_pos
-        bp[:, self._poles_body, :] = torch.tensor(pos, dtype=torch.float64, device=self.device)
-        self.world_idx = world_idx
-        return world_idx
-
-    def reset(self, seed=None, mask=None):
-        """MujocoEnvBase.reset_model (:163-165): qpos = init_qpos, qvel = 0, time = 0, then
-        mj_forward; returns (obs, info)."""
-        e = self.engine
-        q0 = torch.tensor(self.init_qpos, dtype=torch.float64, device=self.device)
-        ctrl0 = torch.tensor(np.concatenate([self.init_qpos[:6], [0.0]]), dtype=torch.float64, device=self.device)
-        if mask is None:
-            e.qpos.copy_(q0.expand_as(e.qpos))
-            e.qvel.zero_()
-            e.qacc_ws.zero_()
-            e.time.zero_()
-            e.ctrl.copy_(ctrl0.expand_as(e.ctrl))
-            e.stats.zero_()
-        else:
-            m = mask.bool()
-            e.qpos[m] = q0
-            e.qvel[m] = 0
-            e.qacc_ws[m] = 0
-            e.time[m] = 0
-            e.ctrl[m] = ctrl0
-            e.stats[m] = 0
-        e.forward()
-        self.reward = self._get_reward()
-        return self._get_obs(), {}
-
-    def step(self, action, active=None):
-        """MujocoEnvBase.step (:82-97): ctrl = action; frame_skip x mj_step; obs; reward.
-        action: f64 [n, nu] device tensor.  Images are rendered on demand (render_images)."""
-        e = self.engine
-        if action is not None:
-            e.ctrl.copy_(action)
-        e.step(self.frame_skip, active=active)
-        obs = self._get_obs()
-        self.reward = self._get_reward()
-        return obs, self.reward, False, False, {}
-
-    def get_time(self):
-        return self.engine.time
-
-    def get_camera_fovy(self, camera_name):
-        return float(self.arrays["cam_fovy"][self.camera_names.index(camera_name)])
-
-    def get_body_pose(self, body_name):
-        b = self.info.body[body_name]
-        return torch.cat([self.engine.xpos[:, b], self.engine.xquat[:, b]], dim=1)
-
-    # -- internals ----------------------------------------------------------------------------
-    def _get_obs(self):
-        e = self.engine
-        arm_q = e.qpos.index_select(1, self._arm_qadr).contiguous()
-        arm_v = e.qvel.index_select(1, self._arm_dadr).contiguous()
-        grip = e.qpos.index_select(1, self._grip_qadr).contiguous()
-        force = e.sensordata[:, 0:3].contiguous()
-        torque = e.sensordata[:, 3:6].contiguous()
-        jp, jv, wr = K.ur5e_obs(arm_q, arm_v, grip, force, torque)
-        return {"joint_pos": jp, "joint_vel": jv, "wrench": wr}
+        self.original_pole_pos = self.original_world_pos
 
     def _get_reward(self):
+        """MujocoUR5eCableEnv._get_reward (:48-105)."""
         e = self.engine
         c0, c1 = self._cable_bodies[0], self._cable_bodies[-1] + 1
         cable = e.xpos[:, c0:c1].contiguous()
@@ -147,10 +38,3 @@ class BatchedMujocoUR5eCableEnv:
         p1 = e.gxpos[:, self._pole_geoms[0]].contiguous()
         p2 = e.gxpos[:, self._pole_geoms[1]].contiguous()
         return K.cable_reward(cable, end, p1, p2, out=self.reward if self.reward.is_contiguous() else None)
-
-    def render_images(self, camera_name="front", rgb=None, depth=None, policy=None, active=None, mean=None, std=None):
-        """MujocoEnvBase._get_info (:103-126) for one camera, all envs; `policy` receives
-        ((rgb / 255) - mean) / std as [n, 3, H, W]."""
-        self.renderer.render(self.engine, camera_name, rgb=rgb, depth=depth, policy=policy, active=active,
-                             mean=mean, std=std)
-        return rgb, depth, policy

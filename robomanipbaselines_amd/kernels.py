@@ -144,6 +144,20 @@ def cable_reward(cable_xpos, end_xpos, pole1, pole2, out=None):
     return out
 
 
+def insert_reward(peg_xpos, hole_xpos, peg_xquat, xy_thre, z_offset, cos_tilt, out=None):
+    """MujocoUR5eInsertEnv._get_reward for n envs (rmbx_insert_reward)."""
+    n = peg_xpos.shape[0]
+    _chk(peg_xpos, torch.float64, (n, 3), "peg_xpos")
+    _chk(hole_xpos, torch.float64, (n, 3), "hole_xpos")
+    _chk(peg_xquat, torch.float64, (n, 4), "peg_xquat")
+    if out is None:
+        out = torch.empty(n, dtype=torch.float64, device=peg_xpos.device)
+    _chk(out, torch.float64, (n,), "reward")
+    N.call("rmbx_insert_reward", N.ptr(peg_xpos), N.ptr(hole_xpos), N.ptr(peg_xquat), N.ptr(out), n,
+           float(xy_thre), float(z_offset), float(cos_tilt), N.stream_ptr())
+    return out
+
+
 def ur5e_obs(arm_qpos, arm_qvel, grip_qpos, force, torque):
     n = arm_qpos.shape[0]
     _chk(arm_qpos, torch.float64, (n, 6), "arm_qpos")

@@ -76,6 +76,15 @@ def test_cable_reward_bitexact():
     np.testing.assert_array_equal(r.cpu().numpy(), d["reward"])
 
 
+def test_insert_reward_bitexact():
+    """rmbx_insert_reward vs the reference's MujocoUR5eInsertEnv._get_reward (golden)."""
+    from robomanipbaselines_amd.envs.ur5e_insert import INSERT_COS_TILT, INSERT_XY_THRE, INSERT_Z_OFFSET
+
+    d = _load("reward_insert.npz")
+    r = K.insert_reward(_t(d["peg"]), _t(d["hole"]), _t(d["quat"]), INSERT_XY_THRE, INSERT_Z_OFFSET, INSERT_COS_TILT)
+    np.testing.assert_array_equal(r.cpu().numpy(), d["reward"])
+
+
 def test_cable_reward_nan_and_edges():
     d = _load("reward_cable.npz")
     cab = d["cable"][:64].copy()

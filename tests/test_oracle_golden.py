@@ -43,6 +43,15 @@ def test_reward_oracle_bitexact():
     assert 0 < d["reward"].sum() < len(d["reward"])  # both outcomes are covered
 
 
+def test_insert_reward_oracle_bitexact():
+    """oracle/glue.insert_reward vs MujocoUR5eInsertEnv._get_reward (MujocoUR5eInsertEnv.py:43-63)."""
+    d = _load("reward_insert.npz")
+    got = np.array([glue.insert_reward(p, h, q) for p, h, q in zip(d["peg"], d["hole"], d["quat"])])
+    np.testing.assert_array_equal(got, d["reward"])
+    assert 0 < d["reward"].sum() < len(d["reward"])
+    assert float(d["cos_tilt"]) == float(np.cos(np.deg2rad(10)))
+
+
 def test_obs_oracle_bitexact():
     d = _load("obs_ur5e.npz")
     for n in range(len(d["qpos"])):

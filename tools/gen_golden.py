@@ -11,6 +11,7 @@ Functions exercised (reference file:line):
   * RolloutAct.infer_policy temporal ensemble      policy/act/RolloutAct.py:68-101
   * normalize_data / denormalize_data              common/utils/DataUtils.py:9-40
   * MujocoUR5eCableEnv._get_reward                 envs/mujoco/ur5e/MujocoUR5eCableEnv.py:48-105
+  * MujocoUR5eInsertEnv._get_reward                envs/mujoco/ur5e/MujocoUR5eInsertEnv.py:43-63
   * MujocoUR5eEnvBase._get_obs gripper mapping     envs/mujoco/ur5e/MujocoUR5eEnvBase.py:78-119
   * MujocoEnvBase._get_info depth linearisation    envs/mujoco/MujocoEnvBase.py:103-126
   * convert_depth_image_to_pointcloud              common/utils/VisionUtils.py:55-87
@@ -322,6 +323,68 @@ def gen_reward(importlib):
     print("reward: positives", int(rewards.sum()), "of", N)
 
 
+def _quat2mat(q):
+    """mju_quat2Mat (the same restatement as oracle/glue.quat2mat; MuJoCo is absent here)."""
+    if q[0] == 1 and q[1] == 0 and q[2] == 0 and q[3] == 0:
+        return np.eye(3)
+    q00, q01, q02, q03 = q[0] * q[0], q[0] * q[1], q[0] * q[2], q[0] * q[3]
+    q11, q12, q13 = q[1] * q[1], q[1] * q[2], q[1] * q[3]
+    q22, q23, q33 = q[2] * q[2], q[2] * q[3], q[3] * q[3]
+    return np.array([[q00 + q11 - q22 - q33, 2 * (q12 - q03), 2 * (q13 + q02)],
+                     [2 * (q12 + q03), q00 - q11 + q22 - q33, 2 * (q23 - q01)],
+                     [2 * (q13 - q02), 2 * (q23 + q01), q00 - q11 - q22 + q33]])
+
+
+def gen_reward_insert(importlib):
+    """MujocoUR5eInsertEnv._get_reward (MujocoUR5eInsertEnv.py:43-63) on synthetic peg/hole poses
+    around every threshold (xy box, height, 10 deg tilt), exact-threshold and NaN cases."""
+    Env = importlib.import_module("robo_manip_baselines.envs.mujoco.ur5e.MujocoUR5eInsertEnv").MujocoUR5eInsertEnv
+    rng = np.random.default_rng(4242)
+    N = 2048
+    peg = np.zeros((N, 3))
+    hole = np.zeros((N, 3))
+    quat = np.zeros((N, 4))
+    rewards = np.zeros(N)
+    cos10 = np.cos(np.deg2rad(10))
+    for n in range(N):
+        h = np.array([-0.08, -0.08, 0.815]) + rng.uniform(-0.01, 0.01, 3) * [1, 8, 0.1]
+        kind = n % 8
+        p = h + np.array([rng.normal(0, 0.01), rng.normal(0, 0.01), rng.uniform(0.0, 0.08)])
+        # peg pointing down (its z axis along world -z) tilted about a random horizontal axis
+        tilt = np.deg2rad(rng.uniform(0, 20))
+        ax = rng.normal(0, 1, 3) * [1, 1, 0]
+        ax /= np.linalg.norm(ax)
+        qt = np.array([np.cos(tilt / 2), *(np.sin(tilt / 2) * ax)])
+        qdown = np.array([0.0, 1.0, 0.0, 0.0])  # 180 deg about x: z -> -z
+        w1, v1, w2, v2 = qt[0], qt[1:], qdown[0], qdown[1:]
+        q = np.array([w1 * w2 - v1 @ v2, *(w1 * v2 + w2 * v1 + np.cross(v1, v2))])
+        if kind == 1:
+            q = np.array([1.0, 0.0, 0.0, 0.0])  # identity: z axis up, never a success
+        if kind == 2:
+            p[0] = h[0] + 0.012  # exactly on the xy threshold (strict <)
+        if kind == 3:
+            p[2] = h[2] + 0.05  # exactly on the height threshold (strict <)
+        if kind == 4:
+            tilt = np.deg2rad(10)  # at the tilt threshold
+            qt = np.array([np.cos(tilt / 2), np.sin(tilt / 2), 0.0, 0.0])
+            w1, v1 = qt[0], qt[1:]
+            q = np.array([w1 * w2 - v1 @ v2, *(w1 * v2 + w2 * v1 + np.cross(v1, v2))])
+        if kind == 5:
+            p[1] = np.nan
+        if kind == 6:
+            p[:2] = h[:2] + rng.uniform(-0.004, 0.004, 2)
+            p[2] = h[2] + 0.02
+        peg[n], hole[n], quat[n] = p, h, q
+        env = object.__new__(Env)
+        bodies = {"peg": types.SimpleNamespace(xpos=p.copy(), xmat=_quat2mat(q).reshape(9)),
+                  "hole": types.SimpleNamespace(xpos=h.copy(), xmat=np.eye(3).reshape(9))}
+        env.data = types.SimpleNamespace(body=lambda nm, _b=bodies: _b[nm])
+        rewards[n] = env._get_reward()
+    np.savez(os.path.join(OUT, "reward_insert.npz"), peg=peg, hole=hole, quat=quat, reward=rewards,
+             cos_tilt=np.float64(cos10))
+    print("insert reward: positives", int(rewards.sum()), "of", N)
+
+
 def gen_obs(importlib):
     """MujocoUR5eEnvBase._get_obs (MujocoUR5eEnvBase.py:78-119)."""
     Base = importlib.import_module(
@@ -557,6 +620,7 @@ def main():
     importlib = install_stubs()
     gen_ensemble(importlib)
     gen_reward(importlib)
+    gen_reward_insert(importlib)
     gen_obs(importlib)
     gen_depth_and_pointcloud(importlib)
     gen_phase_schedule(importlib)
