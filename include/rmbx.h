@@ -266,11 +266,25 @@ int rmbx_stem_s2d_conv(const void* in, const void* weight, const float* bias, vo
  * of the backbones' resnet18 (third_party/act [absent]; policy/mlp/MlpPolicy.py:34-39). */
 int rmbx_stem_s2d_conv_maxpool(const void* in, const void* weight, const float* bias, void* out, int N,
                                int Hs, int Ws, int band_rows, void* stream);
+/* Multi-head attention forward, bf16: out[b][i][h*64 + d] = sum_j softmax_j(scale * q_i . k_j) v_j[d]
+ * over the heads of q/k/v rows [b][row][h*64 .. h*64+63] (row/batch strides in elements, last dim
+ * contiguous), f32 softmax and accumulation, head dim 64, Lk <= 320, no mask; out contiguous
+ * [B][Lq][heads*64].  Replaces scaled_dot_product_attention inside nn.MultiheadAttention of ACT's
+ * transformer (third_party/act transformer.py [absent]; d 512, 8 heads, policy/act/TrainAct.py:46-58). */
+int rmbx_attention_bf16(const void* q, const void* k, const void* v, void* out, int B, int heads, int Lq, int Lk,
+                        long long q_bstride, int q_rstride, long long k_bstride, int k_rstride, long long v_bstride,
+                        int v_rstride, float scale, void* stream);
 /* Residual add + LayerNorm over the last dim of [rows][D] rows (D <= 2048, multiple of 8 bf16 / 4
  * f32): out = LayerNorm(rnd(x + r)) * weight + bias (f32 weight/bias), r optional (NULL); replaces
  * the add + nn.LayerNorm pair of the ACT transformer's post-norm layers (third_party/act). */
 int rmbx_add_layernorm(const void* x, const void* r, const float* weight, const float* bias, void* out,
                        int rows, int D, float eps, int dtype, void* stream);
+/* rmbx_add_layernorm that also writes out_pos = rnd(out + pos[row % pos_rows]) (pos [pos_rows][D] in
+ * the storage dtype): the `src + pos` / `tgt + query_pos` query input of the next attention block
+ * of ACT's post-norm transformer layers, fused into the LayerNorm pass (out_pos NULL: plain). */
+int rmbx_add_layernorm_pos(const void* x, const void* r, const float* weight, const float* bias, void* out,
+                           const void* pos, int pos_rows, void* out_pos, int rows, int D, float eps, int dtype,
+                           void* stream);
 /* out [N][Ho][Wo][C] = maxpool3x3s2p1(relu(rnd(x + bias))), Ho = (H-1)/2+1, Wo = (W-1)/2+1. */
 int rmbx_nhwc_bias_relu_maxpool(const void* x, const float* bias, void* out, int N, int H, int W,
                                 int C, int dtype, void* stream);

@@ -230,7 +230,8 @@ __global__ void __launch_bounds__(256) add_layernorm_kernel(const typename T::ve
                                                             const typename T::vec_t* __restrict__ r,
                                                             const float* __restrict__ w, const float* __restrict__ b,
                                                             typename T::vec_t* __restrict__ out, int rows, int D,
-                                                            float eps) {
+                                                            float eps, const typename T::vec_t* __restrict__ pos,
+                                                            int pos_rows, typename T::vec_t* __restrict__ out_pos) {
   constexpr int V = T::VEC;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
@@ -288,7 +289,18 @@ __global__ void __launch_bounds__(256) add_layernorm_kernel(const typename T::ve
         const int c = v * V + k;
         y[k] = (s[q][k] - mean) * rstd * w[c] + b[c];
       }
-      out[base + v] = T::pack(y);
+      const typename T::vec_t yv = T::pack(y);
+      out[base + v] = yv;
+      if (out_pos) {
+        // the next attention's query input: rnd(y + pos[row % pos_rows]) on the rounded y, as the
+        // separate `x + pos` of the unfused module computes it
+        float yr[V], pv[V];
+        T::unpack(yv, yr);
+        T::unpack(pos[(size_t)(row % pos_rows) * nvec + v], pv);
+#pragma unroll
+        for (int k = 0; k < V; ++k) yr[k] = yr[k] + pv[k];
+        out_pos[base + v] = T::pack(yr);
+      }
     }
   }
 }
@@ -296,8 +308,20 @@ __global__ void __launch_bounds__(256) add_layernorm_kernel(const typename T::ve
 }  // namespace
 }  // namespace rmbx
 
+extern "C" int rmbx_add_layernorm_pos(const void* x, const void* r, const float* weight, const float* bias, void* out,
+                                      const void* pos, int pos_rows, void* out_pos, int rows, int D, float eps,
+                                      int dtype, void* stream);
+
 extern "C" int rmbx_add_layernorm(const void* x, const void* r, const float* weight, const float* bias, void* out,
                                   int rows, int D, float eps, int dtype, void* stream) {
+  return rmbx_add_layernorm_pos(x, r, weight, bias, out, nullptr, 0, nullptr, rows, D, eps, dtype, stream);
+}
+
+extern "C" int rmbx_add_layernorm_pos(const void* x, const void* r, const float* weight, const float* bias, void* out,
+                                      const void* pos, int pos_rows, void* out_pos, int rows, int D, float eps,
+                                      int dtype, void* stream) {
+  RMBX_CHECK_ARG(!out_pos || (pos && pos_rows > 0), "rmbx_add_layernorm_pos: out_pos needs pos and pos_rows > 0");
+  RMBX_CHECK_ARG(((uintptr_t)pos | (uintptr_t)out_pos) % 16 == 0, "rmbx_add_layernorm_pos: unaligned");
   RMBX_CHECK_ARG(x && weight && bias && out, "rmbx_add_layernorm: null pointer");
   RMBX_CHECK_ARG(dtype == 0 || dtype == 1, "rmbx_add_layernorm: dtype must be 0 (f32) or 1 (bf16)");
   const int vec = dtype == 1 ? 8 : 4;
@@ -311,26 +335,33 @@ extern "C" int rmbx_add_layernorm(const void* x, const void* r, const float* wei
   if (dtype == 1) {
     if (nvec <= 64)
       hipLaunchKernelGGL((rmbx::add_layernorm_kernel<rmbx::BF16, 1>), dim3(grid), dim3(256), 0, s, (const uint4*)x,
-                         (const uint4*)r, weight, bias, (uint4*)out, rows, D, eps);
+                         (const uint4*)r, weight, bias, (uint4*)out, rows, D, eps, (const uint4*)pos, pos_rows,
+                         (uint4*)out_pos);
     else if (nvec <= 128)
       hipLaunchKernelGGL((rmbx::add_layernorm_kernel<rmbx::BF16, 2>), dim3(grid), dim3(256), 0, s, (const uint4*)x,
-                         (const uint4*)r, weight, bias, (uint4*)out, rows, D, eps);
+                         (const uint4*)r, weight, bias, (uint4*)out, rows, D, eps, (const uint4*)pos, pos_rows,
+                         (uint4*)out_pos);
     else
       hipLaunchKernelGGL((rmbx::add_layernorm_kernel<rmbx::BF16, 4>), dim3(grid), dim3(256), 0, s, (const uint4*)x,
-                         (const uint4*)r, weight, bias, (uint4*)out, rows, D, eps);
+                         (const uint4*)r, weight, bias, (uint4*)out, rows, D, eps, (const uint4*)pos, pos_rows,
+                         (uint4*)out_pos);
   } else {
     if (nvec <= 64)
       hipLaunchKernelGGL((rmbx::add_layernorm_kernel<rmbx::F32, 1>), dim3(grid), dim3(256), 0, s, (const float4*)x,
-                         (const float4*)r, weight, bias, (float4*)out, rows, D, eps);
+                         (const float4*)r, weight, bias, (float4*)out, rows, D, eps, (const float4*)pos, pos_rows,
+                         (float4*)out_pos);
     else if (nvec <= 128)
       hipLaunchKernelGGL((rmbx::add_layernorm_kernel<rmbx::F32, 2>), dim3(grid), dim3(256), 0, s, (const float4*)x,
-                         (const float4*)r, weight, bias, (float4*)out, rows, D, eps);
+                         (const float4*)r, weight, bias, (float4*)out, rows, D, eps, (const float4*)pos, pos_rows,
+                         (float4*)out_pos);
     else if (nvec <= 256)
       hipLaunchKernelGGL((rmbx::add_layernorm_kernel<rmbx::F32, 4>), dim3(grid), dim3(256), 0, s, (const float4*)x,
-                         (const float4*)r, weight, bias, (float4*)out, rows, D, eps);
+                         (const float4*)r, weight, bias, (float4*)out, rows, D, eps, (const float4*)pos, pos_rows,
+                         (float4*)out_pos);
     else
       hipLaunchKernelGGL((rmbx::add_layernorm_kernel<rmbx::F32, 8>), dim3(grid), dim3(256), 0, s, (const float4*)x,
-                         (const float4*)r, weight, bias, (float4*)out, rows, D, eps);
+                         (const float4*)r, weight, bias, (float4*)out, rows, D, eps, (const float4*)pos, pos_rows,
+                         (float4*)out_pos);
   }
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;

@@ -371,6 +371,28 @@ def add_layernorm(x, r, weight, bias, eps=1e-5, out=None):
     return out
 
 
+def add_layernorm_pos(x, r, weight, bias, pos, eps=1e-5):
+    """(y, y + pos) with y = LayerNorm(rnd(x + r)) in one pass (rmbx_add_layernorm_pos); pos
+    [P, D] (or [1, P, D]) in x's dtype, broadcast over the leading dims row-wise (row % P)."""
+    if x.dtype not in _NN_DTYPES or not x.is_cuda or not x.is_contiguous():
+        raise ValueError("x must be a contiguous bf16/f32 device tensor")
+    D = x.shape[-1]
+    if r is not None and (r.shape != x.shape or r.dtype != x.dtype or not r.is_contiguous()):
+        raise ValueError("r must match x")
+    _chk(weight, torch.float32, (D,), "weight")
+    _chk(bias, torch.float32, (D,), "bias")
+    pos2 = pos.reshape(-1, D)
+    if pos2.dtype != x.dtype or not pos2.is_contiguous() or not pos2.is_cuda:
+        raise ValueError("pos must be a contiguous device tensor of x's dtype")
+    if x.dim() < 2 or x.shape[-2] % pos2.shape[0] != 0:
+        raise ValueError("pos rows must divide the sequence length")
+    out = torch.empty_like(x)
+    out_pos = torch.empty_like(x)
+    N.call("rmbx_add_layernorm_pos", N.ptr(x), N.ptr(r), N.ptr(weight), N.ptr(bias), N.ptr(out), N.ptr(pos2),
+           pos2.shape[0], N.ptr(out_pos), x.numel() // D, D, float(eps), _NN_DTYPES[x.dtype], N.stream_ptr())
+    return out, out_pos
+
+
 def conv2d_nhwc(x, weight, bias, stride=1, padding=0, relu=False, res=None):
     """relu?(conv2d(x, weight) + bias + res) by rmbx_conv2d_nhwc: x bf16 channels_last
     [N, Cin, H, W], weight bf16 channels_last [Cout, Cin, KH, KW], bias f32 [Cout], res bf16
@@ -459,4 +481,32 @@ def stem_s2d_conv_maxpool(x_s2d, w_packed, bias, band_rows=0):
     out = torch.empty((n, 64, Hp, Wp), dtype=torch.bfloat16, device=x_s2d.device, memory_format=torch.channels_last)
     N.call("rmbx_stem_s2d_conv_maxpool", N.ptr(x_s2d), N.ptr(w_packed), N.ptr(bias), N.ptr(out), n, Hs, Ws,
            int(band_rows), N.stream_ptr())
+    return out
+
+
+# ------------------------------------------------------------------------------------------
+# Transformer attention
+# ------------------------------------------------------------------------------------------
+ATTN_MAX_LK = 320
+
+
+def attention_bf16(q, k, v, heads, scale=None):
+    """softmax(scale * q k^T) v per head for bf16 [B, L, heads * 64] views (last dim contiguous,
+    any row/batch strides, e.g. slices of a fused QKV projection) -> contiguous [B, Lq, heads * 64]
+    (rmbx_attention_bf16; f32 softmax)."""
+    for t, nm in ((q, "q"), (k, "k"), (v, "v")):
+        if not isinstance(t, torch.Tensor) or not t.is_cuda or t.dtype != torch.bfloat16 or t.dim() != 3:
+            raise ValueError(f"{nm} must be a bf16 [B, L, D] device tensor")
+        if t.stride(2) != 1 or t.shape[2] != heads * 64:
+            raise ValueError(f"{nm} must have a contiguous last dim of heads * 64")
+    B, Lq, D = q.shape
+    Lk = k.shape[1]
+    if k.shape != v.shape or k.shape[0] != B:
+        raise ValueError("k and v must be [B, Lk, D] like q")
+    if Lk > ATTN_MAX_LK:
+        raise ValueError(f"attention_bf16: Lk={Lk} exceeds {ATTN_MAX_LK}")
+    scale = 1.0 / 8.0 if scale is None else float(scale)
+    out = torch.empty((B, Lq, D), dtype=torch.bfloat16, device=q.device)
+    N.call("rmbx_attention_bf16", N.ptr(q), N.ptr(k), N.ptr(v), N.ptr(out), B, heads, Lq, Lk,
+           q.stride(0), q.stride(1), k.stride(0), k.stride(1), v.stride(0), v.stride(1), scale, N.stream_ptr())
     return out

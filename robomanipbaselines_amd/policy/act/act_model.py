@@ -46,6 +46,8 @@ class MHA(nn.Module):
     """nn.MultiheadAttention-compatible parameters (in_proj_weight/bias, out_proj), batch-first
     compute through scaled_dot_product_attention."""
 
+    fused_attention = False  # device inference form: rmbx_attention_bf16 instead of SDPA
+
     def __init__(self, d, heads):
         super().__init__()
         self.d, self.h = d, heads
@@ -71,6 +73,12 @@ class MHA(nn.Module):
             kk = F.linear(k, w[D : 2 * D], b[D : 2 * D])
             vv = F.linear(v, w[2 * D :], b[2 * D :])
         hd = D // self.h
+        if self.fused_attention and qq.dtype == torch.bfloat16 and hd == 64 and Lk <= 320 and qq.is_cuda:
+            from ... import kernels as K
+
+            # rmbx_attention_bf16 reads the head slices of the projections in place and writes the
+            # [B, Lq, D] layout out_proj consumes
+            return self.out_proj(K.attention_bf16(qq, kk, vv, self.h))
         qq = qq.view(B, Lq, self.h, hd).transpose(1, 2)
         kk = kk.view(B, Lk, self.h, hd).transpose(1, 2)
         vv = vv.view(B, Lk, self.h, hd).transpose(1, 2)
@@ -92,17 +100,34 @@ class _LayerOps(nn.Module):
             return self.linear2(h).view(*shp[:-1], -1)
         return self.linear2(F.relu(self.linear1(x)))
 
+    @staticmethod
+    def _norm_f32(norm):
+        """The LayerNorm's weight/bias widened to f32 for the rmbx kernel (cached per storage)."""
+        key = (norm.weight.data_ptr(), norm.weight.dtype)
+        cache = norm.__dict__.get("_f32")
+        if cache is None or cache[0] != key:
+            cache = (key, norm.weight.detach().float().contiguous(), norm.bias.detach().float().contiguous())
+            norm.__dict__["_f32"] = cache
+        return cache[1], cache[2]
+
     def addnorm(self, norm, x, r):
         if self.fused:
             from ... import kernels as K
 
-            key = (norm.weight.data_ptr(), norm.weight.dtype)
-            cache = norm.__dict__.get("_f32")
-            if cache is None or cache[0] != key:
-                cache = (key, norm.weight.detach().float().contiguous(), norm.bias.detach().float().contiguous())
-                norm.__dict__["_f32"] = cache
-            return K.add_layernorm(x.contiguous(), r.contiguous(), cache[1], cache[2], norm.eps)
+            w, b = self._norm_f32(norm)
+            return K.add_layernorm(x.contiguous(), r.contiguous(), w, b, norm.eps)
         return norm(x + r)
+
+    def addnorm_pos(self, norm, x, r, pos):
+        """(y, y + pos) with y = addnorm(norm, x, r): the layer output and the next attention's
+        query input, one rmbx_add_layernorm_pos pass when fused."""
+        if self.fused:
+            from ... import kernels as K
+
+            w, b = self._norm_f32(norm)
+            return K.add_layernorm_pos(x.contiguous(), r.contiguous(), w, b, pos.contiguous(), norm.eps)
+        y = norm(x + r)
+        return y, y + pos
 
 
 class EncoderLayer(_LayerOps):
@@ -116,6 +141,13 @@ class EncoderLayer(_LayerOps):
         q = src + pos
         src = self.addnorm(self.norm1, src, self.self_attn(q, q, src))
         return self.addnorm(self.norm2, src, self.ffn(src))
+
+    def forward_q(self, src, q, pos, want_next_q):
+        """forward() with the query input q = src + pos given, returning (out, out + pos or None)."""
+        src = self.addnorm(self.norm1, src, self.self_attn(q, q, src))
+        if want_next_q:
+            return self.addnorm_pos(self.norm2, src, self.ffn(src), pos)
+        return self.addnorm(self.norm2, src, self.ffn(src)), None
 
 
 class DecoderLayer(_LayerOps):
@@ -132,6 +164,15 @@ class DecoderLayer(_LayerOps):
         mk = memory + pos if mem_pos is None else mem_pos
         tgt = self.addnorm(self.norm2, tgt, self.multihead_attn(tgt + query_pos, mk, memory))
         return self.addnorm(self.norm3, tgt, self.ffn(tgt))
+
+    def forward_q(self, tgt, q, memory, query_pos, mem_pos, want_next_q):
+        """forward() with q = tgt + query_pos given; both later `+ query_pos` adds are fused into
+        the LayerNorm passes that produce their operands.  Returns (out, out + query_pos or None)."""
+        tgt, q2 = self.addnorm_pos(self.norm1, tgt, self.self_attn(q, q, tgt), query_pos)
+        tgt = self.addnorm(self.norm2, tgt, self.multihead_attn(q2, mem_pos, memory))
+        if want_next_q:
+            return self.addnorm_pos(self.norm3, tgt, self.ffn(tgt), query_pos)
+        return self.addnorm(self.norm3, tgt, self.ffn(tgt)), None
 
 
 class ActModel(nn.Module):
@@ -166,6 +207,9 @@ class ActModel(nn.Module):
         """Device inference form of the transformer layers (see _LayerOps)."""
         for layer in list(self.encoder_layers) + list(self.decoder_layers):
             layer.fused = on
+            for m in layer.modules():
+                if isinstance(m, MHA):
+                    m.fused_attention = on
         return self
 
     def _pos(self, h, w, device, dtype):
@@ -202,18 +246,22 @@ class ActModel(nn.Module):
         src = torch.cat([latent[:, None], proprio[:, None], src], dim=1)
         pos = torch.cat([self.additional_pos_embed.weight[None].to(src.dtype), pos], dim=1)
         mem = src
-        for layer in self.encoder_layers:
-            mem = layer(mem, pos)
+        # each layer's query input (x + pos) comes out of the previous LayerNorm pass (same values
+        # as the separate add: the sum of the rounded layer output and pos, rounded once)
+        q = src + pos
+        n_enc = len(self.encoder_layers)
+        for i, layer in enumerate(self.encoder_layers):
+            mem, q = layer.forward_q(mem, q, pos, want_next_q=i + 1 < n_enc)
         qe = self.query_embed.weight[None].to(src.dtype)
         tgt = torch.zeros(B, self.num_queries, mem.shape[2], device=mem.device, dtype=mem.dtype)
         mem_pos = mem + pos
+        q = tgt + qe
         first = None
-        for i, layer in enumerate(self.decoder_layers):
-            tgt = layer(tgt, mem, pos, qe, mem_pos)
+        n_dec = 1 if self.prune_dead_decoder else len(self.decoder_layers)
+        for i in range(n_dec):
+            tgt, q = self.decoder_layers[i].forward_q(tgt, q, mem, qe, mem_pos, want_next_q=i + 1 < n_dec)
             if i == 0:
                 first = self.decoder_norm(tgt)  # intermediate[0] = norm(output of layer 0)
-                if self.prune_dead_decoder:
-                    break
         return self.action_head(first)
 
 

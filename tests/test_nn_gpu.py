@@ -200,6 +200,23 @@ def test_add_layernorm(dtype):
     assert ((got - want).abs() <= tol * (1 + want.abs())).all()
 
 
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+def test_add_layernorm_pos_equals_separate_add(dtype):
+    """rmbx_add_layernorm_pos: out is rmbx_add_layernorm's, out_pos == (out + pos) as torch adds
+    them in the storage dtype, bit for bit (pos broadcast per sequence position)."""
+    from robomanipbaselines_amd import kernels as K
+
+    g = torch.Generator(device=DEV).manual_seed(5)
+    x = (torch.randn(3, 302, 512, device=DEV, generator=g) * 3).to(dtype)
+    r = torch.randn(3, 302, 512, device=DEV, generator=g).to(dtype)
+    w = torch.randn(512, device=DEV, generator=g)
+    b = torch.randn(512, device=DEV, generator=g)
+    pos = torch.randn(1, 302, 512, device=DEV, generator=g).to(dtype)
+    y, yp = K.add_layernorm_pos(x, r, w, b, pos, 1e-5)
+    assert torch.equal(y, K.add_layernorm(x, r, w, b, 1e-5))
+    assert torch.equal(yp, y + pos)
+
+
 @torch.no_grad()
 def test_act_device_inference_form_matches_fp32_reference():
     from robomanipbaselines_amd.policy.act.act_model import ActModel
