@@ -13,6 +13,8 @@
 #include <hip/hip_bf16.h>
 
 #include "rmbx_common.h"
+
+#include <cstdlib>
 #include "rmbx_math.h"
 #include "rmbx_model.h"
 
@@ -200,6 +202,7 @@ struct RenderArgs {
   int n_env;
   int tiles_x, tiles_y;
   int groups;  // blocks per env (each renders a contiguous range of tiles)
+  int dbg;     // diagnostic (RMBX_RENDER_DBG; 0 in production): 1 no ray loop, 2 no stores, 4 test counts, 8 sphere bounds only
 };
 
 __global__ void __launch_bounds__(256) render_kernel(RenderArgs a) {
@@ -217,6 +220,8 @@ __global__ void __launch_bounds__(256) render_kernel(RenderArgs a) {
   const int W = a.cam.width, H = a.cam.height;
   const float tanh_ = tanf(0.5f * a.cam.fovy_deg * 3.14159265358979f / 180.0f);
   const float aspect = (float)W / (float)H;
+  // cosine of the widest ray (image corner) against the view axis
+  const float cos_max = rsqrtf(1.0f + tanh_ * tanh_ * (1.0f + aspect * aspect));
   if (tid == 0) {
     // camera pose in world
     double Rb[9], Rc[9], R[9], t[3];
@@ -266,6 +271,32 @@ __global__ void __launch_bounds__(256) render_kernel(RenderArgs a) {
       rad = sqrtf(f[0] * f[0] + f[1] * f[1] + f[2] * f[2]);
     P.rad = rad;
     P.zmin = (type == RMBX_GEOM_PLANE || rad <= 0) ? -1e30f : (-P.c[2] - rad);
+    if (!(a.dbg & 8) && type != RMBX_GEOM_PLANE) {
+      // tighter bound for large primitives (the 10 m walls, the table): every hit point lies at
+      // least the camera-to-primitive distance r away, so its camera depth is >= r * cos_max
+      // (cos_max: the widest ray angle of the image).  The walls then sort behind the table and
+      // floor and the rays stop before testing them.
+      float ol[3];
+      for (int i = 0; i < 3; i++) ol[i] = -(P.R[i] * P.c[0] + P.R[3 + i] * P.c[1] + P.R[6 + i] * P.c[2]);
+      float r = -1.f;
+      if (type == RMBX_GEOM_BOX) {
+        float d2 = 0.f;
+        for (int i = 0; i < 3; i++) {
+          const float e = fabsf(ol[i]) - P.s[i];
+          if (e > 0.f) d2 += e * e;
+        }
+        r = sqrtf(d2);
+      } else if (type == RMBX_GEOM_SPHERE) {
+        r = sqrtf(ol[0] * ol[0] + ol[1] * ol[1] + ol[2] * ol[2]) - P.s[0];
+      } else if (type == RMBX_GEOM_CAPSULE || type == RMBX_GEOM_CYLINDER) {
+        const float h = P.s[1];
+        const float z = fminf(fmaxf(ol[2], -h), h);
+        const float dz = ol[2] - z;
+        const float rad_c = type == RMBX_GEOM_CYLINDER ? sqrtf(P.s[0] * P.s[0]) : P.s[0];
+        r = sqrtf(ol[0] * ol[0] + ol[1] * ol[1] + dz * dz) - rad_c;
+      }
+      if (r > 0.f) P.zmin = fmaxf(P.zmin, r * cos_max * (1.0f - 1e-5f) - 1e-5f);
+    }
     prims[p] = P;
   }
   const int t_begin = (int)((long long)ntiles * grp / a.groups);
@@ -328,10 +359,12 @@ __global__ void __launch_bounds__(256) render_kernel(RenderArgs a) {
   float best = 1e30f, bn[3] = {0, 0, 1};
   int bp = -1;
   const int cnt = tile_count;
-  for (int k = 0; k < cnt; k++) {
+  int ntest = 0;
+  for (int k = 0; k < ((a.dbg & 1) ? 0 : cnt); k++) {
     const int p = tile_sorted[k];
     const PrimCam& P = prims[p];
     if (P.zmin > best + 1e-4f) break;  // every later primitive lies behind the current hit
+    ++ntest;
     float o_l[3], d_l[3], t, nl[3];
     to_local(P, d, o_l, d_l);
     bool h = false;
@@ -377,16 +410,17 @@ __global__ void __launch_bounds__(256) render_kernel(RenderArgs a) {
   }
   const size_t pix = (size_t)py * W + px;
   const size_t hw = (size_t)H * W;
+  const bool do_store = !(a.dbg & 2) || col[0] == 12345.f;  // (diagnostic: keep the shading live)
   uint8_t u[3];
   for (int i = 0; i < 3; i++) u[i] = (uint8_t)(col[i] * 255.0f + 0.5f);
-  if (a.rgb) {
+  if (a.rgb && do_store) {
     uint8_t* o = a.rgb + ((size_t)env * hw + pix) * 3;
     o[0] = u[0];
     o[1] = u[1];
     o[2] = u[2];
   }
-  if (a.depth) a.depth[(size_t)env * hw + pix] = depth;
-  if (a.policy) {
+  if (a.depth && do_store) a.depth[(size_t)env * hw + pix] = (a.dbg & 4) ? (float)(ntest + 1000 * cnt) : depth;
+  if (a.policy && do_store) {
     if (a.policy_dtype == 2) {
       // 2x2 space-to-depth [n][H/2][W/2][16]: channel (dy*2+dx)*3+c, 12..15 zero
       const int Hs = H >> 1, Ws = W >> 1;
@@ -448,6 +482,8 @@ extern "C" int rmbx_render(const rmbx_camera* cam, const int32_t* prim_i32, cons
   a.tiles_x = (cam->width + RENDER_TILE - 1) / RENDER_TILE;
   a.tiles_y = (cam->height + RENDER_TILE - 1) / RENDER_TILE;
   a.groups = 16;
+  const char* dbg_env = std::getenv("RMBX_RENDER_DBG");
+  a.dbg = dbg_env ? std::atoi(dbg_env) : 0;
   const size_t nblocks = (size_t)n_env * a.groups;
   RMBX_CHECK_ARG(nblocks < (1ull << 31), "grid too large");
   hipLaunchKernelGGL(rmbx::render_kernel, dim3((unsigned)nblocks), dim3(256), 0,

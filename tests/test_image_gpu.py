@@ -47,3 +47,28 @@ def test_resize_u8_frame():
     got = K.resize_crop_u8(torch.from_numpy(src).to(DEV), (84, 84), dtype=torch.uint8).cpu().numpy()
     want = np.stack([OI.resize_u8(s, (84, 84)) for s in src])
     assert np.array_equal(got, want)
+
+
+def test_render_depth_bounds_do_not_change_pixels(monkeypatch):
+    """The per-primitive depth bound that lets rays stop before the far walls is exact: every
+    camera renders the same rgb / depth bits with it (default) as with bounding spheres only
+    (RMBX_RENDER_DBG=8)."""
+    import numpy as np
+    import torch
+
+    from robomanipbaselines_amd.envs.ur5e_cable import BatchedMujocoUR5eCableEnv
+
+    env = BatchedMujocoUR5eCableEnv(4, "cuda:0", world_random_scale=[0.01, 0.01, 0.0])
+    env.modify_world(world_idx=np.arange(4))
+    env.reset()
+    H, W = env.renderer.height, env.renderer.width
+    for cam in env.camera_names:
+        out = {}
+        for dbg in ("0", "8"):
+            monkeypatch.setenv("RMBX_RENDER_DBG", dbg)
+            rgb = torch.empty((4, H, W, 3), dtype=torch.uint8, device="cuda:0")
+            depth = torch.empty((4, H, W), dtype=torch.float32, device="cuda:0")
+            env.render_images(cam, rgb=rgb, depth=depth)
+            out[dbg] = (rgb, depth)
+        assert torch.equal(out["0"][0], out["8"][0]), cam
+        assert torch.equal(out["0"][1], out["8"][1]), cam
