@@ -30,7 +30,8 @@ struct PrimCam {
   float rgb[3];
   int type;
   float rad;   // bounding radius (0 = unbounded)
-  float zmin;  // nearest possible hit depth (camera z) of the bounding sphere; -inf if unbounded
+  float zmin;  // lower bound of any hit's depth (camera z) in the image; -1e30 if unbounded
+  float ol[3];  // the camera (ray origin) in the primitive's local frame: R^T (0 - c)
 };
 
 __device__ __forceinline__ float dot3f(const float* a, const float* b) {
@@ -45,9 +46,9 @@ struct CamFrame {
 
 // ray (origin 0, direction d) intersections in the primitive's local frame ------------------
 __device__ __forceinline__ void to_local(const PrimCam& P, const float* d, float* o_l, float* d_l) {
-  // local = R^T (x - c); origin is the camera (0)
+  // local = R^T (x - c); the origin (the camera) is transformed once per primitive (P.ol)
   for (int i = 0; i < 3; i++) {
-    o_l[i] = -(P.R[i] * P.c[0] + P.R[3 + i] * P.c[1] + P.R[6 + i] * P.c[2]);
+    o_l[i] = P.ol[i];
     d_l[i] = P.R[i] * d[0] + P.R[3 + i] * d[1] + P.R[6 + i] * d[2];
   }
 }
@@ -271,13 +272,13 @@ __global__ void __launch_bounds__(256) render_kernel(RenderArgs a) {
       rad = sqrtf(f[0] * f[0] + f[1] * f[1] + f[2] * f[2]);
     P.rad = rad;
     P.zmin = (type == RMBX_GEOM_PLANE || rad <= 0) ? -1e30f : (-P.c[2] - rad);
+    for (int i = 0; i < 3; i++) P.ol[i] = -(P.R[i] * P.c[0] + P.R[3 + i] * P.c[1] + P.R[6 + i] * P.c[2]);
     if (!(a.dbg & 8) && type != RMBX_GEOM_PLANE) {
       // tighter bound for large primitives (the 10 m walls, the table): every hit point lies at
       // least the camera-to-primitive distance r away, so its camera depth is >= r * cos_max
       // (cos_max: the widest ray angle of the image).  The walls then sort behind the table and
       // floor and the rays stop before testing them.
-      float ol[3];
-      for (int i = 0; i < 3; i++) ol[i] = -(P.R[i] * P.c[0] + P.R[3 + i] * P.c[1] + P.R[6 + i] * P.c[2]);
+      const float* ol = P.ol;
       float r = -1.f;
       if (type == RMBX_GEOM_BOX) {
         float d2 = 0.f;
