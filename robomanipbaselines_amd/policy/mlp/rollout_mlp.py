@@ -11,6 +11,8 @@
   refills on the same call for every env.
 """
 
+import os
+
 import torch
 
 from ... import kernels as K
@@ -38,6 +40,9 @@ class RolloutMlp(BatchedRolloutBase):
         self.policy = self.policy.eval().requires_grad_(False)
         self.policy.fuse_backbone()
         torch.backends.cudnn.benchmark = True
+        # ... without timing MIOpen's naive reference solver, which takes seconds per shape at
+        # rollout batch sizes and is never the one selected
+        os.environ.setdefault("MIOPEN_DEBUG_CONV_DIRECT_NAIVE_CONV_FWD", "0")
         self.policy = self.policy.to(device=self.device, dtype=self.policy_dtype)
         self.policy._fused = self.policy._fused.to(memory_format=torch.channels_last)
 
