@@ -70,7 +70,8 @@ def parse():
     p.add_argument("--num_envs", type=int, default=1024, help="environments per GPU")
     p.add_argument("--precision", choices=["bf16", "fp32"], default="bf16")
     p.add_argument("--no_cpu_baseline", action="store_true")
-    p.add_argument("--cpu_sample_steps", type=int, default=6)
+    p.add_argument("--cpu_sample_steps", type=int, default=240,
+                   help="timed env-steps of the CPU baseline sample (about 10 s of host work)")
     p.add_argument("--act_prune_dead_decoder", action="store_true")
     return p.parse_args()
 
@@ -105,8 +106,11 @@ def cpu_baseline(sample_steps, skip=3):
     stats = {"norm_config": {"type": "gaussian"}, "mean": ctrl.copy(), "std": np.full(7, 0.1)}
     ens = glue.ActEnsembleOracle(100, stats)
     img = torch.rand(1, 1, 3, 480, 640)
+    warm = 3  # untimed: first-call allocations of PyTorch-CPU
     t0 = time.time()
-    for s in range(sample_steps):
+    for s in range(-warm, sample_steps):
+        if s == 0:
+            t0 = time.time()
         if s % skip == 0:
             state = torch.tensor(((qpos[:7] - ctrl) / 0.1)[None], dtype=torch.float32)
             with torch.no_grad():
@@ -116,8 +120,9 @@ def cpu_baseline(sample_steps, skip=3):
         env.step(8)
     dt = time.time() - t0
     return {"value": sample_steps / dt, "unit": "env-steps/s", "cores": int(threads), "kind": "port",
-            "sample": f"{sample_steps} env-steps of 1 env: C oracle physics (1 thread) + ACT fp32 PyTorch-CPU "
-                      f"batch 1 every {skip} steps ({threads} threads) + numpy ensemble; rendering excluded"}
+            "sample": f"{sample_steps} env-steps of 1 env (after {warm} untimed): C oracle physics (1 thread) + ACT "
+                      f"fp32 PyTorch-CPU batch 1 every {skip} steps ({threads} threads) + numpy ensemble; "
+                      f"rendering excluded", "seconds": round(dt, 2)}
 
 
 def main():

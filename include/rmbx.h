@@ -86,6 +86,16 @@ int rmbx_cable_reward(const double* cable_xpos, const double* end_xpos,
 int rmbx_insert_reward(const double* peg_xpos, const double* hole_xpos, const double* peg_xquat, double* reward,
                        int n_env, double xy_thre, double z_offset, double cos_tilt, void* stream);
 
+/* Door-opening reward, batched.
+ * Replaces envs/mujoco/ur5e/MujocoUR5eDoorEnv.py:52-67 (_get_reward): 0.5 * (reaching + opening)
+ * with reaching = exp(-10 max(|pinch - handle| - margin, 0)) (1 once the door is open),
+ * opening = clip(door_angle / target_angle, 0, 1); margin 0.08, target np.deg2rad(-45) from the
+ * host.  pinch_xpos (site "pinch"), handle_xpos (geom "door_handle") f64 [n_env][3], door_angle
+ * f64 [n_env].  The success flag (reward >= 1.0 <=> opening >= 1) is bit-exact; the reward value
+ * follows numpy's operation order, exp from the device libm (within 1 ulp of numpy's). */
+int rmbx_door_reward(const double* pinch_xpos, const double* handle_xpos, const double* door_angle, double* reward,
+                     int n_env, double margin, double target_angle, void* stream);
+
 /* ---------------------------------------------------------------------------------------------
  * UR5e observation mapping, batched.
  * Replaces envs/mujoco/ur5e/MujocoUR5eEnvBase.py:78-119 (_get_obs):

@@ -122,6 +122,18 @@ def insert_reward(peg_pos, hole_pos, peg_quat):
     return 0.0
 
 
+def door_reward(gripper_pos, handle_pos, door_angle):
+    """envs/mujoco/ur5e/MujocoUR5eDoorEnv.py:52-67 (_get_reward)."""
+    gripper_handle_dist = np.linalg.norm(gripper_pos - handle_pos)
+    gripper_handle_dist_margin = 0.08
+    reaching_reward = np.exp(-10.0 * np.max([gripper_handle_dist - gripper_handle_dist_margin, 0.0]))
+    door_angle_target = np.deg2rad(-45.0)
+    opening_reward = np.clip(door_angle / door_angle_target, 0.0, 1.0)
+    if opening_reward >= 1.0:
+        reaching_reward = 1.0
+    return 0.5 * (reaching_reward + opening_reward)
+
+
 def ur5e_obs(arm_qpos, arm_qvel, grip_qpos, force, torque):
     g = np.rad2deg(np.asarray(grip_qpos, np.float64).mean(keepdims=True)) / 45.0 * 255.0
     return (

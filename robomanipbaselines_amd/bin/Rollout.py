@@ -12,7 +12,7 @@ import sys
 import yaml
 
 POLICIES = ["Mlp", "Act", "DiffusionPolicy", "DiffusionPolicy3d"]
-ENVS = ["MujocoUR5eCable", "MujocoUR5eInsert"]
+ENVS = ["MujocoUR5eCable", "MujocoUR5eInsert", "MujocoUR5eDoor"]
 
 
 def camel_to_snake(name):

@@ -35,7 +35,8 @@ class PhaseSpec:
     """Timed phase of the pre-rollout motion (PhaseBase.ReachPhaseBase / GraspPhaseBase)."""
 
     def __init__(self, name, duration, kind, pos_z=None, grip=None):
-        # grip: gripper command of a grasp phase (None = action_space.high, set_target_close)
+        # grip: gripper command of a grasp phase (None = action_space.high, set_target_close;
+        # "low" = action_space.low, set_target_open; or a value)
         self.name, self.duration, self.kind, self.pos_z, self.grip = name, duration, kind, pos_z, grip
 
 
@@ -238,8 +239,10 @@ class BatchedRolloutBase:
             if ph.kind == "reach":
                 self._ik_step()
             elif ph.kind == "grasp":
-                # GraspPhaseBase.pre_update (:66-69): set_target_close (:78-104) or a fixed value
-                self.grip_cmd.fill_(self._ghi if ph.grip is None else float(ph.grip))
+                # GraspPhaseBase.pre_update (:66-69): set_target_close / set_target_open
+                # (action_space high / low, :78-104) or a fixed value
+                g = self._ghi if ph.grip is None else (self._glo if ph.grip == "low" else float(ph.grip))
+                self.grip_cmd.fill_(g)
         elif self.phase_idx == n_pre:
             if self.rollout_time_idx % self.args.skip == 0:
                 t0 = time.time()

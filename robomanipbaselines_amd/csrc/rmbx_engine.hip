@@ -2285,6 +2285,7 @@ int rmbx_engine_ws_offset(const rmbx_engine* eng, const char* name, size_t* offs
       {"qacc", L.qacc, nv},
       {"cdof", L.cdof, 6 * nv},
       {"xmat", L.xmat, 9 * (size_t)m.nbody},
+      {"sxpos", L.sxpos, 3 * (size_t)m.nsite},
       {"con_pos", L.con_pos, 3 * (size_t)m.max_contacts},
       {"con_dist", L.con_dist, (size_t)m.max_contacts},
       {"efc_force", L.efc_force, (size_t)L.nefc_max},

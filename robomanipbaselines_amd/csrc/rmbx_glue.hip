@@ -196,6 +196,36 @@ __device__ double insert_reward_one(const double* __restrict__ peg, const double
   return dot > cos_tilt ? 1.0 : 0.0;
 }
 
+// -----------------------------------------------------------------------------------------
+// Door-opening reward (envs/mujoco/ur5e/MujocoUR5eDoorEnv.py:52-67): continuous, success iff 1.0
+// -----------------------------------------------------------------------------------------
+__device__ double door_reward_one(const double* __restrict__ pinch, const double* __restrict__ handle, double angle,
+                                  double margin, double target) {
+  // np.linalg.norm(gripper_pos - handle_pos) = sqrt(x . x)
+  const double d0 = pinch[0] - handle[0], d1 = pinch[1] - handle[1], d2 = pinch[2] - handle[2];
+  double ss = d0 * d0;
+  ss = ss + d1 * d1;
+  ss = ss + d2 * d2;
+  const double dist = sqrt(ss);
+  // np.exp(-10.0 * np.max([dist - margin, 0.0])) (numpy max propagates NaN)
+  const double ex = dist - margin;
+  const double mx = isnan(ex) ? ex : (ex > 0.0 ? ex : 0.0);
+  double reaching = exp(-10.0 * mx);
+  // np.clip(door_angle / target, 0.0, 1.0)
+  double opening = angle / target;
+  opening = opening < 0.0 ? 0.0 : (opening > 1.0 ? 1.0 : opening);
+  if (opening >= 1.0) reaching = 1.0;
+  return 0.5 * (reaching + opening);
+}
+
+__global__ void door_reward_kernel(const double* __restrict__ pinch, const double* __restrict__ handle,
+                                   const double* __restrict__ angle, double* __restrict__ reward, int n_env,
+                                   double margin, double target) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n_env) return;
+  reward[e] = door_reward_one(pinch + 3 * (size_t)e, handle + 3 * (size_t)e, angle[e], margin, target);
+}
+
 __global__ void insert_reward_kernel(const double* __restrict__ peg_xpos, const double* __restrict__ hole_xpos,
                                      const double* __restrict__ peg_xquat, double* __restrict__ reward, int n_env,
                                      double xy_thre, double z_off, double cos_tilt) {
@@ -369,6 +399,17 @@ int rmbx_cable_reward(const double* cable_xpos, const double* end_xpos, const do
   hipLaunchKernelGGL(cable_reward_kernel, dim3((n_env + 255) / 256), dim3(256), 0,
                      as_stream(stream), cable_xpos, end_xpos, pole1_xpos, pole2_xpos, reward,
                      n_env, n_cable);
+  RMBX_CHECK_LAUNCH();
+  return RMBX_OK;
+}
+
+int rmbx_door_reward(const double* pinch_xpos, const double* handle_xpos, const double* door_angle, double* reward,
+                     int n_env, double margin, double target_angle, void* stream) {
+  RMBX_CHECK_ARG(n_env >= 0, "bad n_env=%d", n_env);
+  RMBX_CHECK_ARG(pinch_xpos && handle_xpos && door_angle && reward, "NULL buffer");
+  if (n_env == 0) return RMBX_OK;
+  hipLaunchKernelGGL(door_reward_kernel, dim3((n_env + 255) / 256), dim3(256), 0, as_stream(stream), pinch_xpos,
+                     handle_xpos, door_angle, reward, n_env, margin, target_angle);
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
 }

@@ -144,6 +144,20 @@ def cable_reward(cable_xpos, end_xpos, pole1, pole2, out=None):
     return out
 
 
+def door_reward(pinch_xpos, handle_xpos, door_angle, margin, target_angle, out=None):
+    """MujocoUR5eDoorEnv._get_reward for n envs (rmbx_door_reward)."""
+    n = pinch_xpos.shape[0]
+    _chk(pinch_xpos, torch.float64, (n, 3), "pinch_xpos")
+    _chk(handle_xpos, torch.float64, (n, 3), "handle_xpos")
+    _chk(door_angle, torch.float64, (n,), "door_angle")
+    if out is None:
+        out = torch.empty(n, dtype=torch.float64, device=pinch_xpos.device)
+    _chk(out, torch.float64, (n,), "reward")
+    N.call("rmbx_door_reward", N.ptr(pinch_xpos), N.ptr(handle_xpos), N.ptr(door_angle), N.ptr(out), n,
+           float(margin), float(target_angle), N.stream_ptr())
+    return out
+
+
 def insert_reward(peg_xpos, hole_xpos, peg_xquat, xy_thre, z_offset, cos_tilt, out=None):
     """MujocoUR5eInsertEnv._get_reward for n envs (rmbx_insert_reward)."""
     n = peg_xpos.shape[0]

@@ -85,6 +85,22 @@ def test_insert_reward_bitexact():
     np.testing.assert_array_equal(r.cpu().numpy(), d["reward"])
 
 
+def test_door_reward_matches_golden():
+    """rmbx_door_reward vs the reference's MujocoUR5eDoorEnv._get_reward (golden): success flags
+    (reward >= 1) and NaNs bit-exact, values within a few ulp (device exp vs numpy libm exp)."""
+    from robomanipbaselines_amd.envs.ur5e_door import DOOR_HANDLE_MARGIN, DOOR_TARGET_ANGLE
+
+    d = _load("reward_door.npz")
+    assert DOOR_TARGET_ANGLE == float(d["target"])
+    r = K.door_reward(_t(d["pinch"]), _t(d["handle"]), _t(d["angle"]), DOOR_HANDLE_MARGIN, DOOR_TARGET_ANGLE)
+    r = r.cpu().numpy()
+    want = d["reward"]
+    np.testing.assert_array_equal(np.isnan(r), np.isnan(want))
+    ok = ~np.isnan(want)
+    np.testing.assert_array_equal(r[ok] >= 1.0, want[ok] >= 1.0)
+    np.testing.assert_allclose(r[ok], want[ok], rtol=1e-15, atol=2.5e-16)
+
+
 def test_cable_reward_nan_and_edges():
     d = _load("reward_cable.npz")
     cab = d["cable"][:64].copy()

@@ -52,6 +52,14 @@ def test_insert_reward_oracle_bitexact():
     assert float(d["cos_tilt"]) == float(np.cos(np.deg2rad(10)))
 
 
+def test_door_reward_oracle_bitexact():
+    """oracle/glue.door_reward vs MujocoUR5eDoorEnv._get_reward (MujocoUR5eDoorEnv.py:52-67)."""
+    d = _load("reward_door.npz")
+    got = np.array([glue.door_reward(p, h, a) for p, h, a in zip(d["pinch"], d["handle"], d["angle"])])
+    np.testing.assert_array_equal(got, d["reward"])  # NaN where the reference gives NaN
+    assert 0 < (d["reward"] >= 1.0).sum() < len(d["reward"])
+
+
 def test_obs_oracle_bitexact():
     d = _load("obs_ur5e.npz")
     for n in range(len(d["qpos"])):

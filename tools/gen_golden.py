@@ -12,6 +12,7 @@ Functions exercised (reference file:line):
   * normalize_data / denormalize_data              common/utils/DataUtils.py:9-40
   * MujocoUR5eCableEnv._get_reward                 envs/mujoco/ur5e/MujocoUR5eCableEnv.py:48-105
   * MujocoUR5eInsertEnv._get_reward                envs/mujoco/ur5e/MujocoUR5eInsertEnv.py:43-63
+  * MujocoUR5eDoorEnv._get_reward                  envs/mujoco/ur5e/MujocoUR5eDoorEnv.py:52-67
   * MujocoUR5eEnvBase._get_obs gripper mapping     envs/mujoco/ur5e/MujocoUR5eEnvBase.py:78-119
   * MujocoEnvBase._get_info depth linearisation    envs/mujoco/MujocoEnvBase.py:103-126
   * convert_depth_image_to_pointcloud              common/utils/VisionUtils.py:55-87
@@ -385,6 +386,47 @@ def gen_reward_insert(importlib):
     print("insert reward: positives", int(rewards.sum()), "of", N)
 
 
+def gen_reward_door(importlib):
+    """MujocoUR5eDoorEnv._get_reward (MujocoUR5eDoorEnv.py:52-67) on synthetic gripper / handle
+    positions and door angles around the 0.08 m margin and the -45 deg target (exact values, NaN)."""
+    Env = importlib.import_module("robo_manip_baselines.envs.mujoco.ur5e.MujocoUR5eDoorEnv").MujocoUR5eDoorEnv
+    rng = np.random.default_rng(5150)
+    N = 2048
+    pinch = np.zeros((N, 3))
+    handle = np.zeros((N, 3))
+    angle = np.zeros(N)
+    rewards = np.zeros(N)
+    target = np.deg2rad(-45.0)
+    for n in range(N):
+        h = np.array([0.115, -0.125, 0.965]) + rng.normal(0, 0.02, 3)
+        kind = n % 8
+        direction = rng.normal(0, 1, 3)
+        direction /= np.linalg.norm(direction)
+        dist = rng.uniform(0.0, 0.3)
+        if kind == 1:
+            dist = 0.08  # on the margin
+        p = h + dist * direction
+        a = rng.uniform(-1.2, 0.1)
+        if kind == 2:
+            a = target  # exactly at the target angle
+        if kind == 3:
+            a = target * (1 + 1e-15)
+        if kind == 4:
+            a = 0.0
+        if kind == 5:
+            p[2] = np.nan
+        pinch[n], handle[n], angle[n] = p, h, a
+        env = object.__new__(Env)
+        env.data = types.SimpleNamespace(
+            site=lambda nm, _p=p.copy(): types.SimpleNamespace(xpos=_p),
+            geom=lambda nm, _h=h.copy(): types.SimpleNamespace(xpos=_h),
+            joint=lambda nm, _a=a: types.SimpleNamespace(qpos=np.array([_a])))
+        rewards[n] = env._get_reward()
+    np.savez(os.path.join(OUT, "reward_door.npz"), pinch=pinch, handle=handle, angle=angle, reward=rewards,
+             target=np.float64(target))
+    print("door reward: successes", int((rewards >= 1.0).sum()), "of", N)
+
+
 def gen_obs(importlib):
     """MujocoUR5eEnvBase._get_obs (MujocoUR5eEnvBase.py:78-119)."""
     Base = importlib.import_module(
@@ -621,6 +663,7 @@ def main():
     gen_ensemble(importlib)
     gen_reward(importlib)
     gen_reward_insert(importlib)
+    gen_reward_door(importlib)
     gen_obs(importlib)
     gen_depth_and_pointcloud(importlib)
     gen_phase_schedule(importlib)
