@@ -236,11 +236,14 @@ __global__ void __launch_bounds__(256) conv_nhwc_kernel(ConvArgs a) {
 // 3x3 / stride 1 / pad 1 conv with Cin = 64 k (the ResNet-18 stride-1 block convs): the block's
 // output tile is 8 rows x 16 columns of one image; per 64-channel chunk its 10 x 18 input patch
 // is loaded into LDS once and all 9 taps read their A fragments from it (the row-tiled kernel
-// re-reads the input once per tap); weights stream per tap through a small LDS tile.  Wave w
-// owns output rows 2w, 2w+1.  The epilogue transposes the accumulators through LDS so bias,
-// residual and ReLU are applied on 16-byte NHWC chunks.
+// re-reads the input once per tap); weights stream per tap through a small LDS tile (keeping the
+// block at 35 KiB of LDS, 4 blocks per CU).  The next chunk's patch is loaded into registers with
+// all of its loads in flight together while the current chunk is multiplied.  Wave w owns output
+// rows 2w, 2w+1.  The epilogue transposes the accumulators through LDS so bias, residual and ReLU
+// are applied on 16-byte NHWC chunks.
 constexpr int PT_H = 8, PT_W = 16, PP_H = PT_H + 2, PP_W = PT_W + 2, PLD = 72;
-
+constexpr int P_CHUNKS = PP_H * PP_W * 8;                 // 16-byte chunks of one patch
+constexpr int P_PER_THREAD = (P_CHUNKS + 255) / 256;      // 6
 constexpr int PATCH_LDS = PP_H * PP_W * PLD + CBN * CLD;  // bf16 elements
 static_assert(PATCH_LDS >= CBM * EPI_LD * 2, "epilogue image must fit the patch + B tiles");
 
@@ -275,25 +278,34 @@ __global__ void __launch_bounds__(256) conv3x3_c64_patch_kernel(ConvArgs a) {
     x0 = *reinterpret_cast<const uint4*>(a.w + (((size_t)(n0 + (q0 >> 3)) * 3 + kh) * 3 + kw) * Cin + 64 * ch + (q0 & 7) * 8);
     x1 = *reinterpret_cast<const uint4*>(a.w + (((size_t)(n0 + (q1 >> 3)) * 3 + kh) * 3 + kw) * Cin + 64 * ch + (q1 & 7) * 8);
   };
+  // input patch rows oy0-1 .. oy0+8, cols ox0-1 .. ox0+16 of chunk ch (zero outside the image)
+  uint4 pr[P_PER_THREAD];
+  auto ldp = [&](int ch) {
+#pragma unroll
+    for (int i = 0; i < P_PER_THREAD; ++i) {
+      const int q = tid + 256 * i;
+      const int pix = q >> 3, part = q & 7;
+      const int py = pix / PP_W, px = pix - py * PP_W;
+      const int h = oy0 - 1 + py, w = ox0 - 1 + px;
+      const bool ok = q < P_CHUNKS && h >= 0 && h < a.H && w >= 0 && w < a.W;
+      pr[i] = *reinterpret_cast<const uint4*>(a.in + (ok ? (((size_t)n * a.H + h) * a.W + w) * Cin + 64 * ch + part * 8 : 0));
+      if (!ok) pr[i] = make_uint4(0, 0, 0, 0);
+    }
+  };
   const int KK = 9 * (Cin / 64);
+  ldp(0);
   ldb(0, rb0, rb1);
   for (int kk = 0; kk < KK; ++kk) {
     const int tap = kk % 9;
-    if (tap == 0) {
-      // input patch rows oy0-1 .. oy0+8, cols ox0-1 .. ox0+16, channels of chunk kk / 9
-      __syncthreads();
-      const int c0 = 64 * (kk / 9);
-      for (int q = tid; q < PP_H * PP_W * 8; q += 256) {
-        const int pix = q >> 3, part = q & 7;
-        const int py = pix / PP_W, px = pix - py * PP_W;
-        const int h = oy0 - 1 + py, w = ox0 - 1 + px;
-        uint4 v = make_uint4(0, 0, 0, 0);
-        if (h >= 0 && h < a.H && w >= 0 && w < a.W)
-          v = *reinterpret_cast<const uint4*>(a.in + (((size_t)n * a.H + h) * a.W + w) * Cin + c0 + part * 8);
-        *reinterpret_cast<uint4*>(sP + pix * PLD + part * 8) = v;
-      }
-    }
     __syncthreads();
+    if (tap == 0) {
+#pragma unroll
+      for (int i = 0; i < P_PER_THREAD; ++i) {
+        const int q = tid + 256 * i;
+        if (q < P_CHUNKS) *reinterpret_cast<uint4*>(sP + (q >> 3) * PLD + (q & 7) * 8) = pr[i];
+      }
+      if (kk + 9 < KK) ldp(kk / 9 + 1);
+    }
     *reinterpret_cast<uint4*>(sB + (tid >> 3) * CLD + (tid & 7) * 8) = rb0;
     *reinterpret_cast<uint4*>(sB + ((tid + 256) >> 3) * CLD + (tid & 7) * 8) = rb1;
     __syncthreads();
