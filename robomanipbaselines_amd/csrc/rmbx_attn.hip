@@ -17,6 +17,7 @@
 #include "rmbx_common.h"
 
 #include <cstdint>
+#include <cstdlib>
 
 namespace rmbx {
 namespace {
@@ -40,6 +41,7 @@ struct AttnArgs {
   int o_rstride;                              // = heads * 64
   int heads, Lq, Lk;
   float scale_log2;                           // softmax scale * log2(e)
+  int dbg;                                    // diagnostic (RMBX_ATTN_DBG; 0 in production): 1 staging only
 };
 
 __device__ __forceinline__ int at_sigma(int i) { return 16 * ((i >> 2) & 1) + (i & 3) + 4 * (i >> 3); }
@@ -101,6 +103,10 @@ __global__ void __launch_bounds__(64 * AT_MAX_WAVES) attn_fwd_kernel(AttnArgs a)
   const float c = a.scale_log2;
   const bool ragged = (Lk & 31) != 0;
   __syncthreads();
+  if (a.dbg & 1) {
+    if (tid == 0 && sK[0] == 0x7fff && sVt[1] == 0x7fff) a.o[0] = 0;  // keep the staging live
+    return;
+  }
 
   // wave w takes the 32-query groups w, w + nwaves, ... (K/V staged once for all of them)
   const int ngroups = (a.Lq + 31) >> 5, nwaves = blockDim.x >> 6;
@@ -121,16 +127,25 @@ __global__ void __launch_bounds__(64 * AT_MAX_WAVES) attn_fwd_kernel(AttnArgs a)
     f32x16 acc0 = {}, acc1 = {};  // O^T: dims sigma(i) (+32), query r32
     float m_run = -INFINITY;      // running max of the raw scores (scale > 0 commutes with max)
     float l_run = 0.f;            // this lane's partial softmax denominator
-    for (int t = 0; t < nkt; ++t) {
-      // S^T tile: rows = keys 32 t + (lane-row layout), cols = this wave's 32 queries
-      f32x16 s = {};
+    // S^T tile t: rows = keys 32 t + (lane-row layout), cols = this wave's 32 queries
+    auto score_tile = [&](int t) {
+      f32x16 st = {};
 #pragma unroll
       for (int ks = 0; ks < 4; ++ks) {
         const int key = 32 * t + r32;
         const int cc = 2 * ks + kh;
         const bf16x8 fk = *reinterpret_cast<const bf16x8*>(sK + key * 64 + ((cc ^ ((key >> 1) & 7)) * 8));
-        s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fk, fq[ks], s, 0, 0, 0);
+        st = __builtin_amdgcn_mfma_f32_32x32x16_bf16(fk, fq[ks], st, 0, 0, 0);
       }
+      return st;
+    };
+    // software pipeline: tile t + 1's score MFMAs are issued before tile t's softmax, so the
+    // matrix core works while the wave's VALU does the exponentials
+    f32x16 s_next = score_tile(0);
+    for (int t = 0; t < nkt; ++t) {
+      f32x16 s = s_next;
+      if (t + 1 < nkt) s_next = score_tile(t + 1);
+      __builtin_amdgcn_sched_barrier(0);
       // this lane's 16 keys: 32 t + 4 kh + (j & 3) + 8 (j >> 2); padding keys only in the last tile
       if (ragged && t == nkt - 1) {
 #pragma unroll
@@ -230,6 +245,8 @@ extern "C" int rmbx_attention_bf16(const void* q, const void* k, const void* v, 
   a.Lq = Lq;
   a.Lk = Lk;
   a.scale_log2 = scale * 1.4426950408889634f;
+  const char* dbg_env = std::getenv("RMBX_ATTN_DBG");
+  a.dbg = dbg_env ? std::atoi(dbg_env) : 0;
   RMBX_CHECK_ARG(scale > 0.f, "rmbx_attention_bf16: scale must be positive");
   const long long nblocks = (long long)B * heads;
   RMBX_CHECK_ARG(nblocks < (1ll << 31), "rmbx_attention_bf16: grid too large");

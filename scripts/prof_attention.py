@@ -38,11 +38,15 @@ with torch.no_grad():
             return F.scaled_dot_product_attention(qh, kh, vh).transpose(1, 2).reshape(B, Lq, 512)
 
         t_r = timed(lambda: K.attention_bf16(q, k, v, 8))
+        os.environ["RMBX_ATTN_DBG"] = "1"
+        t_stage = timed(lambda: K.attention_bf16(q, k, v, 8))
+        os.environ["RMBX_ATTN_DBG"] = "0"
         t_t = timed(sdpa)
         err = (K.attention_bf16(q, k, v, 8).float() - sdpa().float()).abs().max().item()
         flops = 4.0 * B * 8 * Lq * Lk * 64
         io = B * (2 * Lq + 2 * Lk) * 512 * 2
-        print(json.dumps({"shape": name, "rmbx_ms": round(t_r, 3), "sdpa_ms": round(t_t, 3),
+        print(json.dumps({"shape": name, "rmbx_ms": round(t_r, 3), "rmbx_staging_only_ms": round(t_stage, 3),
+                          "sdpa_ms": round(t_t, 3),
                           "rmbx_tflops": round(flops / t_r / 1e9, 1), "rmbx_gbs": round(io / t_r / 1e6, 1),
                           "max_abs_diff_vs_sdpa": err}), flush=True)
         del q, kv
