@@ -194,8 +194,9 @@ int rmbx_engine_step(rmbx_engine* eng, int nsub, const uint8_t* active, void* st
 /* mj_forward only (no integration): fills the outputs and workspace for inspection. */
 int rmbx_engine_forward(rmbx_engine* eng, const uint8_t* active, void* stream);
 /* Diagnostic: step all envs and accumulate per-stage shader cycles into stage_cycles
- * [n_env][16] (u64, device): kinematics, com/crb, velocity+rne+actuation, collision,
- * constraints, solver, sensors, integration. */
+ * [n_env][24] (u64, device): kinematics, com/crb, velocity+rne+actuation, collision,
+ * constraints, solver, sensors, integration; 8-15 solver sub-stages, 16-18 collision
+ * sub-stages, 20-23 constraint sub-stages. */
 int rmbx_engine_step_profiled(rmbx_engine* eng, int nsub, uint64_t* stage_cycles, void* stream);
 
 /* ---------------------------------------------------------------------------------------------

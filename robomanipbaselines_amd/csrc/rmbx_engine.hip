@@ -34,6 +34,7 @@ struct Layout {
       res, Mres, grad, search, Ms, tmp;
   size_t ten_len, ten_vel;
   size_t con_pos, con_frame, con_dist, con_mu;
+  size_t con_tmp;  // collision stage: 4 candidate contacts (pos, normal, dist) per survivor
   size_t J, efc_pos, efc_aref, efc_D, efc_R, efc_force, efc_jar, efc_Js, efc_vel, efc_tmp;
   size_t ints;  // start of the int32 region (in doubles)
   // int32 offsets relative to the int region
@@ -85,6 +86,15 @@ struct Env {
 
 __device__ __forceinline__ void sync() { __syncthreads(); }
 __device__ __forceinline__ unsigned long long stamp() { return __builtin_readcyclecounter(); }
+// diagnostic cycle slots per env: 0-7 stages, 8-15 solver, 16-19 collision, 20-23 constraints
+#define RMBX_PROF_SLOTS 24
+#define SUBPROF(k)                                \
+  if (prof) {                                     \
+    __syncthreads();                              \
+    const unsigned long long t_ = stamp();        \
+    if (threadIdx.x == 0) prof[k] += t_ - tp;     \
+    tp = t_;                                      \
+  }
 
 // ------------------------------------------------------------------------------------------
 // Tree passes, lane = body (nbody <= 64).  Bodies are in DFS preorder, so a subtree is the id
@@ -898,79 +908,117 @@ __device__ int col_plane(const double* cp, const double* Rp, int tb, const doubl
   return k;
 }
 
-__device__ void geom_aabb(const Env& e, int g, double* lo, double* hi) {
+// Narrow-phase classes.  The collision stage first classifies every pair (broadphase + type
+// combination), then runs one collider at a time over the compacted survivors of its class, so a
+// wave never executes the union of the colliders its 64 pairs happen to need.
+enum { CLS_PLANE = 0, CLS_SPH_SPH, CLS_SPH_CAP, CLS_SPH_BOX, CLS_CAP_CAP, CLS_CAP_BOX, CLS_BOX_BOX, NCLS };
+
+// Broadphase record of one geom in LDS (8 doubles): centre, AABB half-extent (a plane: its
+// normal), bounding radius, type.
+__device__ void geom_record(const Env& e, int g, double* r) {
   const rmbx_model& m = *e.m;
   const double* c = e.gxpos + 3 * g;
   const double* R = e.gxmat + 9 * g;
   const double* s = m.geom_csize + 3 * g;
   const int t = m.geom_ctype[g];
+  double x[8];
   for (int i = 0; i < 3; i++) {
-    double ex;
-    if (t == RMBX_GEOM_SPHERE)
-      ex = s[0];
+    x[i] = c[i];
+    if (t == RMBX_GEOM_PLANE)
+      x[3 + i] = R[3 * i + 2];
+    else if (t == RMBX_GEOM_SPHERE)
+      x[3 + i] = s[0];
     else if (t == RMBX_GEOM_CAPSULE)
-      ex = fabs(R[3 * i + 2]) * s[1] + s[0];
+      x[3 + i] = fabs(R[3 * i + 2]) * s[1] + s[0];
     else
-      ex = fabs(R[3 * i]) * s[0] + fabs(R[3 * i + 1]) * s[1] + fabs(R[3 * i + 2]) * s[2];
-    lo[i] = c[i] - ex;
-    hi[i] = c[i] + ex;
+      x[3 + i] = fabs(R[3 * i]) * s[0] + fabs(R[3 * i + 1]) * s[1] + fabs(R[3 * i + 2]) * s[2];
   }
+  x[6] = m.geom_rbound[g];
+  x[7] = (double)t;
+  for (int i = 0; i < 8; i++) r[i] = x[i];
 }
 
-__device__ int pair_collide(const Env& e, int p, Contact* out) {
+// broadphase of pair p (geoms g1, g2, records in LDS); returns its narrow-phase class, or -1
+// when it cannot touch (or the type combination has no collider: no contacts)
+__device__ int pair_class(const double* grec, int g1, int g2, double margin) {
+  double r1[8], r2[8];
+  for (int i = 0; i < 8; i++) {
+    r1[i] = grec[8 * g1 + i];
+    r2[i] = grec[8 * g2 + i];
+  }
+  const int t1 = (int)r1[7], t2 = (int)r2[7];
+  if (t1 == RMBX_GEOM_PLANE || t2 == RMBX_GEOM_PLANE) {
+    const double* rp = t1 == RMBX_GEOM_PLANE ? r1 : r2;
+    const double* ro = t1 == RMBX_GEOM_PLANE ? r2 : r1;
+    const double v[3] = {ro[0] - rp[0], ro[1] - rp[1], ro[2] - rp[2]};
+    if (dot3(v, rp + 3) - ro[6] > margin) return -1;
+    return CLS_PLANE;
+  }
+  for (int i = 0; i < 3; i++) {
+    const double lo1 = r1[i] - r1[3 + i], hi1 = r1[i] + r1[3 + i];
+    const double lo2 = r2[i] - r2[3 + i], hi2 = r2[i] + r2[3 + i];
+    if (lo1 > hi2 + margin || lo2 > hi1 + margin) return -1;
+  }
+  const int a = t1 < t2 ? t1 : t2, b = t1 < t2 ? t2 : t1;
+  if (a == RMBX_GEOM_SPHERE) {
+    if (b == RMBX_GEOM_SPHERE) return CLS_SPH_SPH;
+    if (b == RMBX_GEOM_CAPSULE) return CLS_SPH_CAP;
+    if (b == RMBX_GEOM_BOX) return CLS_SPH_BOX;
+  } else if (a == RMBX_GEOM_CAPSULE) {
+    if (b == RMBX_GEOM_CAPSULE) return CLS_CAP_CAP;
+    if (b == RMBX_GEOM_BOX) return CLS_CAP_BOX;
+  } else if (a == RMBX_GEOM_BOX && b == RMBX_GEOM_BOX) {
+    return CLS_BOX_BOX;
+  }
+  return -1;
+}
+
+// narrow phase of a pair that passed pair_class (cls uniform across the wave)
+__device__ int pair_narrow(const Env& e, int p, int cls, Contact* out) {
   const rmbx_model& m = *e.m;
   int g1 = m.pair_geom1[p], g2 = m.pair_geom2[p];
   const double margin = m.pair_margin[p];
-  int t1 = m.geom_ctype[g1], t2 = m.geom_ctype[g2];
-  // broadphase
-  if (t1 == RMBX_GEOM_PLANE || t2 == RMBX_GEOM_PLANE) {
-    const int gp = t1 == RMBX_GEOM_PLANE ? g1 : g2, go = gp == g1 ? g2 : g1;
-    const double* R = e.gxmat + 9 * gp;
-    const double n[3] = {R[2], R[5], R[8]};
-    const double v[3] = {e.gxpos[3 * go] - e.gxpos[3 * gp], e.gxpos[3 * go + 1] - e.gxpos[3 * gp + 1],
-                         e.gxpos[3 * go + 2] - e.gxpos[3 * gp + 2]};
-    if (dot3(v, n) - m.geom_rbound[go] > margin) return 0;
-  } else {
-    double lo1[3], hi1[3], lo2[3], hi2[3];
-    geom_aabb(e, g1, lo1, hi1);
-    geom_aabb(e, g2, lo2, hi2);
-    for (int i = 0; i < 3; i++)
-      if (lo1[i] > hi2[i] + margin || lo2[i] > hi1[i] + margin) return 0;
-  }
-  bool flip = false;
-  if (t1 > t2) {
-    int t = t1;
-    t1 = t2;
-    t2 = t;
-    t = g1;
+  const int t1 = m.geom_ctype[g1], t2 = m.geom_ctype[g2];
+  const bool flip = t1 > t2;
+  if (flip) {
+    const int t = g1;
     g1 = g2;
     g2 = t;
-    flip = true;
   }
   const double *c1 = e.gxpos + 3 * g1, *R1 = e.gxmat + 9 * g1, *s1 = m.geom_csize + 3 * g1;
   const double *c2 = e.gxpos + 3 * g2, *R2 = e.gxmat + 9 * g2, *s2 = m.geom_csize + 3 * g2;
   int n = 0;
-  if (t1 == RMBX_GEOM_PLANE) {
-    n = col_plane(c1, R1, t2, c2, R2, s2, margin, out);
-  } else if (t1 == RMBX_GEOM_SPHERE && t2 == RMBX_GEOM_SPHERE) {
-    n = col_sphere_sphere(c1, s1[0], c2, s2[0], margin, out);
-  } else if (t1 == RMBX_GEOM_SPHERE && t2 == RMBX_GEOM_CAPSULE) {
-    double pp[3], qq[3], c[3], cc[3];
-    capsule_ends(c2, R2, s2[1], pp, qq);
-    closest_seg_seg(c1, c1, pp, qq, cc, c);
-    n = col_sphere_sphere(c1, s1[0], c, s2[0], margin, out);
-  } else if (t1 == RMBX_GEOM_SPHERE && t2 == RMBX_GEOM_BOX) {
-    n = col_sphere_box(c1, s1[0], c2, R2, s2, margin, out);
-  } else if (t1 == RMBX_GEOM_CAPSULE && t2 == RMBX_GEOM_CAPSULE) {
-    double p1[3], q1[3], p2[3], q2[3], cc1[3], cc2[3];
-    capsule_ends(c1, R1, s1[1], p1, q1);
-    capsule_ends(c2, R2, s2[1], p2, q2);
-    closest_seg_seg(p1, q1, p2, q2, cc1, cc2);
-    n = col_sphere_sphere(cc1, s1[0], cc2, s2[0], margin, out);
-  } else if (t1 == RMBX_GEOM_CAPSULE && t2 == RMBX_GEOM_BOX) {
-    n = col_capsule_box(c1, R1, s1, c2, R2, s2, margin, out);
-  } else if (t1 == RMBX_GEOM_BOX && t2 == RMBX_GEOM_BOX) {
-    n = col_box_box(c1, R1, s1, c2, R2, s2, margin, out);
+  switch (cls) {
+    case CLS_PLANE:
+      n = col_plane(c1, R1, flip ? t1 : t2, c2, R2, s2, margin, out);
+      break;
+    case CLS_SPH_SPH:
+      n = col_sphere_sphere(c1, s1[0], c2, s2[0], margin, out);
+      break;
+    case CLS_SPH_CAP: {
+      double pp[3], qq[3], c[3], cc[3];
+      capsule_ends(c2, R2, s2[1], pp, qq);
+      closest_seg_seg(c1, c1, pp, qq, cc, c);
+      n = col_sphere_sphere(c1, s1[0], c, s2[0], margin, out);
+      break;
+    }
+    case CLS_SPH_BOX:
+      n = col_sphere_box(c1, s1[0], c2, R2, s2, margin, out);
+      break;
+    case CLS_CAP_CAP: {
+      double p1[3], q1[3], p2[3], q2[3], cc1[3], cc2[3];
+      capsule_ends(c1, R1, s1[1], p1, q1);
+      capsule_ends(c2, R2, s2[1], p2, q2);
+      closest_seg_seg(p1, q1, p2, q2, cc1, cc2);
+      n = col_sphere_sphere(cc1, s1[0], cc2, s2[0], margin, out);
+      break;
+    }
+    case CLS_CAP_BOX:
+      n = col_capsule_box(c1, R1, s1, c2, R2, s2, margin, out);
+      break;
+    default:
+      n = col_box_box(c1, R1, s1, c2, R2, s2, margin, out);
+      break;
   }
   if (flip)
     for (int i = 0; i < n; i++)
@@ -1003,22 +1051,141 @@ __device__ void make_frame(const double* n, double* F) {
   F[8] = t2[2];
 }
 
-__device__ int collision(Env& e, int lane) {
+// LDS scratch of the collision stage.  It lives in the front kernel's velocity/RNE arrays, dead
+// once velocity_stage has copied them out (extra dynamic LDS only for models where that region
+// is too small): geom broadphase records; per pair its class (pass 1) then its survivor index
+// (pass 2, -1 = rejected); the class-major survivor list; the contact count of each survivor.
+struct CollisionLds {
+  double* geom;
+  int16_t* slot;
+  int16_t* list;
+  uint8_t* count;
+};
+__host__ __device__ __forceinline__ size_t collision_lds_doubles(int ngeom, int npair) {
+  return 8 * (size_t)ngeom + ((((size_t)5 * npair + 7) / 8 + 1) & ~size_t(1));
+}
+__host__ __device__ __forceinline__ size_t collision_lds_free_doubles(int nb, int nv) {
+  return 28 * (size_t)nb + 6 * (size_t)nv;  // cvel, cacc, cfrc, cdofdot, cinert
+}
+// (cdof, still live, follows the free region: a model that does not fit takes its own space)
+static inline size_t front_kernel_lds_bytes(const rmbx_model& h) {
+  const size_t need = collision_lds_doubles(h.ngeom, h.npair);
+  const size_t extra = need <= collision_lds_free_doubles(h.nbody, h.nv) ? 0 : need;
+  return (front_lds_doubles(h.nbody, h.nv) + extra) * sizeof(double);
+}
+__device__ __forceinline__ CollisionLds collision_lds(const Env& e) {
   const rmbx_model& m = *e.m;
-  int ncon = 0;
-  for (int base = 0; base < m.npair; base += 64) {
+  CollisionLds cl;
+  const bool fits = collision_lds_doubles(m.ngeom, m.npair) <= collision_lds_free_doubles(m.nbody, m.nv);
+  cl.geom = fits ? e.sh + 16 * m.nbody : e.sh + front_lds_doubles(m.nbody, m.nv);
+  cl.slot = reinterpret_cast<int16_t*>(cl.geom + 8 * m.ngeom);
+  cl.list = cl.slot + m.npair;
+  cl.count = reinterpret_cast<uint8_t*>(cl.list + m.npair);
+  return cl;
+}
+
+// Contacts in pair order, at most max_contacts (the serial per-pair loop's result, bit for bit):
+// 1. broadphase + class of every pair (geom records staged in LDS), class counts by ballot
+// 2. survivors compacted class-major (pair order inside a class)
+// 3. one collider at a time over its class's survivors, contacts into con_tmp[survivor]
+// 4. pair-order scan of the counts, contacts copied to their final slots
+__device__ int collision(Env& e, int lane, const CollisionLds& cl, unsigned long long* prof) {
+  const rmbx_model& m = *e.m;
+  unsigned long long tp = prof ? stamp() : 0;
+  const int np = m.npair;
+  const unsigned long long below = (1ull << lane) - 1;
+  for (int g = lane; g < m.ngeom; g += 64) geom_record(e, g, cl.geom + 8 * g);
+  sync();
+  SUBPROF(16)
+  int cnt[NCLS];
+#pragma unroll
+  for (int k = 0; k < NCLS; k++) cnt[k] = 0;
+  // pair indices and margins of the next chunk are loaded before this chunk's tests
+  int g1n = 0, g2n = 0;
+  double mn = 0;
+  if (lane < np) {
+    g1n = m.pair_geom1[lane];
+    g2n = m.pair_geom2[lane];
+    mn = m.pair_margin[lane];
+  }
+  for (int base = 0; base < np; base += 64) {
     const int p = base + lane;
-    Contact c[4];
-    int n = 0;
-    if (p < m.npair) n = pair_collide(e, p, c);
+    const int g1 = g1n, g2 = g2n;
+    const double mg = mn;
+    if (p + 64 < np) {
+      g1n = m.pair_geom1[p + 64];
+      g2n = m.pair_geom2[p + 64];
+      mn = m.pair_margin[p + 64];
+    }
+    const int c = p < np ? pair_class(cl.geom, g1, g2, mg) : -1;
+    if (p < np) cl.slot[p] = (int16_t)c;
+#pragma unroll
+    for (int k = 0; k < NCLS; k++) cnt[k] += __popcll(__ballot(c == k));
+  }
+  int off[NCLS], run[NCLS];
+  int nsurv = 0;
+#pragma unroll
+  for (int k = 0; k < NCLS; k++) {
+    off[k] = run[k] = nsurv;
+    nsurv += cnt[k];
+  }
+  if (nsurv == 0) return 0;
+  sync();
+  for (int base = 0; base < np; base += 64) {
+    const int p = base + lane;
+    const int c = p < np ? cl.slot[p] : -1;
+#pragma unroll
+    for (int k = 0; k < NCLS; k++) {
+      const unsigned long long mk = __ballot(c == k);
+      if (c == k) {
+        const int idx = run[k] + __popcll(mk & below);
+        cl.list[idx] = (int16_t)p;
+        cl.slot[p] = (int16_t)idx;
+      }
+      run[k] += __popcll(mk);
+    }
+  }
+  sync();
+  SUBPROF(17)
+  double* tmp = W(con_tmp);
+#pragma unroll 1
+  for (int k = 0; k < NCLS; k++) {
+    const int end = off[k] + cnt[k];
+    for (int i0 = off[k]; i0 < end; i0 += 64) {
+      const int i = i0 + lane;
+      if (i < end) {
+        Contact c[4];
+        const int n = pair_narrow(e, cl.list[i], k, c);
+        cl.count[i] = (uint8_t)n;
+        double* t = tmp + 28 * (size_t)i;
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+          if (j < n) {
+            for (int d = 0; d < 3; d++) {
+              t[7 * j + d] = c[j].pos[d];
+              t[7 * j + 3 + d] = c[j].n[d];
+            }
+            t[7 * j + 6] = c[j].dist;
+          }
+      }
+    }
+  }
+  sync();
+  SUBPROF(18)
+  int ncon = 0;
+  for (int base = 0; base < np && ncon < m.max_contacts; base += 64) {
+    const int p = base + lane;
+    const int idx = p < np ? cl.slot[p] : -1;
+    const int n = idx >= 0 ? cl.count[idx] : 0;
     int total;
-    const int off = wave_excl_scan(n, lane, &total);
+    const int o = wave_excl_scan(n, lane, &total);
+    const double* t = tmp + 28 * (size_t)(idx >= 0 ? idx : 0);
     for (int i = 0; i < n; i++) {
-      const int k = ncon + off + i;
+      const int k = ncon + o + i;
       if (k >= m.max_contacts) break;
-      for (int j = 0; j < 3; j++) W(con_pos)[3 * k + j] = c[i].pos[j];
-      make_frame(c[i].n, W(con_frame) + 9 * k);
-      W(con_dist)[k] = c[i].dist;
+      for (int j = 0; j < 3; j++) W(con_pos)[3 * k + j] = t[7 * i + j];
+      make_frame(t + 7 * i + 3, W(con_frame) + 9 * k);
+      W(con_dist)[k] = t[7 * i + 6];
       W(con_mu)[k] = m.pair_friction[3 * p];
       WI(con_b1)[k] = m.geom_body[m.pair_geom1[p]];
       WI(con_b2)[k] = m.geom_body[m.pair_geom2[p]];
@@ -1110,8 +1277,9 @@ __device__ void set_row(Env& e, int r, int type, double pos, double diag, const 
 }
 
 // returns nefc; equality rows first (count in *ne)
-__device__ int make_constraints(Env& e, int lane, int ncon, int* ne_out) {
+__device__ int make_constraints(Env& e, int lane, int ncon, int* ne_out, unsigned long long* prof) {
   const rmbx_model& m = *e.m;
+  unsigned long long tp = prof ? stamp() : 0;
   const int nv = m.nv;
   const int nefc_max = e.L->nefc_max;
   double* J = W(J);
@@ -1146,6 +1314,7 @@ __device__ int make_constraints(Env& e, int lane, int ncon, int* ne_out) {
   // zero the Jacobian rows in use
   for (size_t k = lane; k < (size_t)nefc * nv; k += 64) J[k] = 0;
   sync();
+  SUBPROF(20)
   // equality rows: every lane evaluates the constraint's anchors/errors (cheap, no broadcast),
   // lanes < nrows set the row parameters, then the Jacobian is filled lane-per-dof with the
   // same per-entry accumulation order as the serial chain walks (0 + body-1 term + body-2 term)
@@ -1247,6 +1416,7 @@ __device__ int make_constraints(Env& e, int lane, int ncon, int* ne_out) {
       r++;
     }
   }
+  SUBPROF(21)
   // limit rows
   int rbase = ne;
   for (int base = 0; base < m.njnt; base += 64) {
@@ -1330,6 +1500,7 @@ __device__ int make_constraints(Env& e, int lane, int ncon, int* ne_out) {
     rbase += total;
   }
   sync();
+  SUBPROF(22)
   // aref = -b (J qvel) - k imp pos ; D = 1/R
   for (int r = lane; r < nefc; r += 64) {
     const double v = dot_row(J + (size_t)r * nv, e.qvel, nv);
@@ -1338,6 +1509,7 @@ __device__ int make_constraints(Env& e, int lane, int ncon, int* ne_out) {
     W(efc_D)[r] = 1.0 / W(efc_R)[r];
   }
   sync();
+  SUBPROF(23)
   *ne_out = ne;
   return nefc;
 }
@@ -2007,7 +2179,7 @@ __device__ __forceinline__ void make_env(const KArgs& args, int env, Env& e) {
 }
 
 #define PROF_BEGIN()                                        \
-  unsigned long long* prof = args.prof ? args.prof + (size_t)env * 16 : nullptr; \
+  unsigned long long* prof = args.prof ? args.prof + (size_t)env * RMBX_PROF_SLOTS : nullptr; \
   unsigned long long t0 = 0, t1 = 0;                        \
   if (prof) t0 = stamp();
 #define PROF(k)                                   \
@@ -2038,11 +2210,11 @@ __global__ void __launch_bounds__(64) front_kernel(KArgs args) {
   PROF(1)
   velocity_stage(e, lane, s_anc, args.subtree_end);
   PROF(2)
-  const int ncon = collision(e, lane);
+  const int ncon = collision(e, lane, collision_lds(e), prof);
   sync();
   PROF(3)
   int ne = 0;
-  const int nefc = make_constraints(e, lane, ncon, &ne);
+  const int nefc = make_constraints(e, lane, ncon, &ne, prof);
   PROF(4)
   if (lane == 0) {
     WI(scal)[0] = ncon;
@@ -2132,6 +2304,10 @@ static Layout make_layout(const rmbx_model& m) {
   L.efc_Js = take(ne);
   L.efc_vel = take(ne);
   L.efc_tmp = take(ne);
+  // the candidate contacts are dead before make_constraints zeroes and fills J: share its rows
+  // when they are large enough
+  const size_t ntmp = 28 * (size_t)m.npair;
+  L.con_tmp = (size_t)ne * nv >= ntmp ? L.J : take(ntmp);
   L.ints = o;
   size_t io = 0;
   auto itake = [&](size_t n) {
@@ -2183,6 +2359,10 @@ int rmbx_engine_create(const struct rmbx_model* model, int n_env, rmbx_engine** 
   RMBX_CHECK_ARG(h.nbody > 0 && h.nbody <= MAX_BODY, "nbody=%d outside [1, %d]", h.nbody, MAX_BODY);
   RMBX_CHECK_ARG(h.max_contacts > 0 && h.max_contacts <= RCHUNK * MAX_NVP / 6, "bad max_contacts=%d",
                  h.max_contacts);
+  RMBX_CHECK_ARG(h.npair >= 0 && h.npair < 32768, "npair=%d outside [0, 32767]", h.npair);
+  RMBX_CHECK_ARG(front_kernel_lds_bytes(h) <= 65536,
+                 "model too large for the front kernel's LDS (nbody=%d nv=%d ngeom=%d npair=%d)", h.nbody,
+                 h.nv, h.ngeom, h.npair);
   // tree passes need DFS preorder bodies (every subtree a contiguous id range); MJCF order is
   std::vector<int32_t> subtree_end(h.nbody);
   for (int b = h.nbody - 1; b >= 0; b--) {
@@ -2334,7 +2514,7 @@ static int launch(rmbx_engine* eng, int nsub, int integ, const uint8_t* active, 
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int reps = integ ? nsub : 1;
   for (int s = 0; s < reps; s++) {
-    const size_t front_lds = front_lds_doubles(eng->host.nbody, eng->host.nv) * sizeof(double);
+    const size_t front_lds = front_kernel_lds_bytes(eng->host);
     hipLaunchKernelGGL(front_kernel, dim3(eng->n_env), dim3(64), front_lds, st, a);
     RMBX_CHECK_LAUNCH();
     hipLaunchKernelGGL(solver_kernel, dim3(eng->n_env), dim3(SOLVER_THREADS), 0, st, a);

@@ -70,14 +70,19 @@ class PhysicsEngine:
     # sub-stages of "solver" (slots 8..14)
     SOLVER_STAGES = ("smooth_factor_solve", "initial_costs", "gradient", "newton_factor_solve",
                      "line_search", "step_cost", "forces", "hessian")
+    # sub-stages of "collision" (slots 16..18) and "constraints" (slots 20..23)
+    COLLISION_STAGES = ("geom_records", "classify_compact", "narrow")
+    CONSTRAINT_STAGES = ("count_zero", "equality", "limit_contact_rows", "aref")
 
     def step_profiled(self, nsub=8):
         """Diagnostic step: returns mean shader cycles per stage (summed over substeps)."""
-        prof = torch.zeros((self.n_env, 16), dtype=torch.int64, device=self.device)
+        prof = torch.zeros((self.n_env, 24), dtype=torch.int64, device=self.device)
         N.call("rmbx_engine_step_profiled", self._h, int(nsub), N.ptr(prof), N.stream_ptr())
         p = prof.double().mean(0).cpu().numpy()
         out = dict(zip(self.STAGES, p[: len(self.STAGES)]))
         out.update({"solver." + k: v for k, v in zip(self.SOLVER_STAGES, p[8: 8 + len(self.SOLVER_STAGES)])})
+        out.update({"collision." + k: v for k, v in zip(self.COLLISION_STAGES, p[16:19])})
+        out.update({"constraints." + k: v for k, v in zip(self.CONSTRAINT_STAGES, p[20:24])})
         return out
 
     def forward(self, active=None):

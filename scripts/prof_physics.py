@@ -43,4 +43,4 @@ print("ncon mean", st[:, 0].mean(), "nefc mean", st[:, 1].mean(), "iters mean", 
 p = env.engine.step_profiled(8)
 tot = sum(v for k, v in p.items() if "." not in k)
 for k, v in p.items():
-    print(f"  {k:18s} {v/1e6:8.3f} Mcycles  {100*v/tot:5.1f}%")
+    print(f"  {k:34s} {v/1e6:8.3f} Mcycles  {100*v/tot:5.1f}%")
