@@ -23,7 +23,11 @@ import sys
 import time
 
 import numpy as np
-import torch
+
+# MIOpen Find at 1024-env batch sizes: skip timing the naive reference solver (seconds per conv
+# shape, never the one selected); must be set before MIOpen's first use in this process
+os.environ.setdefault("MIOPEN_DEBUG_CONV_DIRECT_NAIVE_CONV_FWD", "0")
+import torch  # noqa: E402
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)

@@ -86,6 +86,15 @@ int rmbx_cable_reward(const double* cable_xpos, const double* end_xpos,
 int rmbx_insert_reward(const double* peg_xpos, const double* hole_xpos, const double* peg_xquat, double* reward,
                        int n_env, double xy_thre, double z_offset, double cos_tilt, void* stream);
 
+/* Cabinet reward, batched.
+ * Replaces envs/mujoco/ur5e/MujocoUR5eCabinetEnv.py:57-73 (_get_reward): 1.0 when the "hinge"
+ * joint exceeds hinge_thre (np.deg2rad(120)) and/or the "slide" joint exceeds slide_thre
+ * (0.12 m), per target_task (0 = None: either, 1 = "hinge", 2 = "slide"; anything else is the
+ * reference's ValueError -> -1).  qpos f64 [n_env][qpos_stride]; hinge_adr / slide_adr are the
+ * joints' qpos addresses.  Bit-exact (comparisons only). */
+int rmbx_cabinet_reward(const double* qpos, int qpos_stride, int hinge_adr, int slide_adr, double hinge_thre,
+                        double slide_thre, int target_task, double* reward, int n_env, void* stream);
+
 /* Door-opening reward, batched.
  * Replaces envs/mujoco/ur5e/MujocoUR5eDoorEnv.py:52-67 (_get_reward): 0.5 * (reaching + opening)
  * with reaching = exp(-10 max(|pinch - handle| - margin, 0)) (1 once the door is open),

@@ -231,3 +231,16 @@ def phase_schedule(reward_fn, pre_durations=CABLE_PRE_DURATIONS, skip=3, max_dur
         if done:
             break
     return dict(phase=np.array(phases), infer_steps=np.array(infer), result=result, n_steps=step)
+
+
+def cabinet_reward(hinge_qpos, slide_qpos, target_task=None):
+    """envs/mujoco/ur5e/MujocoUR5eCabinetEnv.py:57-73 (_get_reward)."""
+    hinge_success = hinge_qpos > np.deg2rad(120.0)
+    slide_success = slide_qpos > 0.12
+    if target_task is None:
+        return 1.0 if hinge_success or slide_success else 0.0
+    if target_task == "hinge":
+        return 1.0 if hinge_success else 0.0
+    if target_task == "slide":
+        return 1.0 if slide_success else 0.0
+    raise ValueError(f"Invalid target task: {target_task}")

@@ -6,13 +6,14 @@ order matters, :82-86); remaining arguments go to the inner parser.
 """
 
 import argparse
+import os
 import importlib
 import sys
 
 import yaml
 
 POLICIES = ["Mlp", "Act", "DiffusionPolicy", "DiffusionPolicy3d"]
-ENVS = ["MujocoUR5eCable", "MujocoUR5eInsert", "MujocoUR5eDoor"]
+ENVS = ["MujocoUR5eCable", "MujocoUR5eInsert", "MujocoUR5eDoor", "MujocoUR5eCabinet"]
 
 
 def camel_to_snake(name):
@@ -49,6 +50,15 @@ def main(argv=None):
     if args.config is not None:
         with open(args.config) as f:
             config = yaml.safe_load(f) or {}
+    pre = argparse.ArgumentParser(add_help=False)
+    pre.add_argument("--num_envs", type=int, default=None)
+    pre.add_argument("--world_idx_list", type=int, nargs="*", default=None)
+    ns, _ = pre.parse_known_args(remaining)
+    n_envs = ns.num_envs or len(ns.world_idx_list or [0])
+    if n_envs >= 256 and args.policy in ("Act", "Mlp"):
+        # large conv batches: keep MIOpen Find from timing its naive reference solver (seconds per
+        # shape, never selected); process-wide, read by MIOpen on first use
+        os.environ.setdefault("MIOPEN_DEBUG_CONV_DIRECT_NAIVE_CONV_FWD", "0")
     rollout = Rollout(argv=remaining + (["--help"] if args.help else []), **config)
     rollout.run()
     return rollout

@@ -768,7 +768,9 @@ __device__ int col_box_box(const double* ca, const double* Ra, const double* ha,
     }
     const double sep = fabs(dot3(dc, a)) - ra - rb;
     if (sep >= margin) return 0;
-    const double score = k < 6 ? sep : sep - 1e-6;
+    // B's face axes yield to A's within 1e-12 m (parallel faces tie up to rounding), edge axes
+    // to faces within 1 um
+    const double score = k < 3 ? sep : (k < 6 ? sep - 1e-12 : sep - 1e-6);
     if (score > best) {
       best = score;
       bk = k;

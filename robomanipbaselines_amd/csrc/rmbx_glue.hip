@@ -226,6 +226,23 @@ __global__ void door_reward_kernel(const double* __restrict__ pinch, const doubl
   reward[e] = door_reward_one(pinch + 3 * (size_t)e, handle + 3 * (size_t)e, angle[e], margin, target);
 }
 
+// -----------------------------------------------------------------------------------------
+// Cabinet reward (envs/mujoco/ur5e/MujocoUR5eCabinetEnv.py:57-73): hinge opened past the angle
+// threshold and/or drawer slid past the distance threshold, per target task (0 any, 1 hinge,
+// 2 slide); NaN joint values compare false, as numpy's
+// -----------------------------------------------------------------------------------------
+__global__ void cabinet_reward_kernel(const double* __restrict__ qpos, int qpos_stride, int hinge_adr, int slide_adr,
+                                      double hinge_thre, double slide_thre, int target_task,
+                                      double* __restrict__ reward, int n_env) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n_env) return;
+  const double* q = qpos + (size_t)e * qpos_stride;
+  const bool hinge = q[hinge_adr] > hinge_thre;
+  const bool slide = q[slide_adr] > slide_thre;
+  const bool ok = target_task == 1 ? hinge : (target_task == 2 ? slide : (hinge || slide));
+  reward[e] = ok ? 1.0 : 0.0;
+}
+
 __global__ void insert_reward_kernel(const double* __restrict__ peg_xpos, const double* __restrict__ hole_xpos,
                                      const double* __restrict__ peg_xquat, double* __restrict__ reward, int n_env,
                                      double xy_thre, double z_off, double cos_tilt) {
@@ -399,6 +416,20 @@ int rmbx_cable_reward(const double* cable_xpos, const double* end_xpos, const do
   hipLaunchKernelGGL(cable_reward_kernel, dim3((n_env + 255) / 256), dim3(256), 0,
                      as_stream(stream), cable_xpos, end_xpos, pole1_xpos, pole2_xpos, reward,
                      n_env, n_cable);
+  RMBX_CHECK_LAUNCH();
+  return RMBX_OK;
+}
+
+int rmbx_cabinet_reward(const double* qpos, int qpos_stride, int hinge_adr, int slide_adr, double hinge_thre,
+                        double slide_thre, int target_task, double* reward, int n_env, void* stream) {
+  RMBX_CHECK_ARG(n_env >= 0, "bad n_env=%d", n_env);
+  RMBX_CHECK_ARG(qpos && reward, "NULL buffer");
+  RMBX_CHECK_ARG(hinge_adr >= 0 && hinge_adr < qpos_stride && slide_adr >= 0 && slide_adr < qpos_stride,
+                 "joint addresses (%d, %d) outside qpos rows of %d", hinge_adr, slide_adr, qpos_stride);
+  RMBX_CHECK_ARG(target_task >= 0 && target_task <= 2, "Invalid target task: %d", target_task);
+  if (n_env == 0) return RMBX_OK;
+  hipLaunchKernelGGL(cabinet_reward_kernel, dim3((n_env + 255) / 256), dim3(256), 0, as_stream(stream), qpos,
+                     qpos_stride, hinge_adr, slide_adr, hinge_thre, slide_thre, target_task, reward, n_env);
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
 }

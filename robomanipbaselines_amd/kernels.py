@@ -144,6 +144,23 @@ def cable_reward(cable_xpos, end_xpos, pole1, pole2, out=None):
     return out
 
 
+CABINET_TASKS = {None: 0, "hinge": 1, "slide": 2}
+
+
+def cabinet_reward(qpos, hinge_adr, slide_adr, hinge_thre, slide_thre, target_task=None, out=None):
+    """MujocoUR5eCabinetEnv._get_reward for n envs (rmbx_cabinet_reward); qpos [n, nq] f64."""
+    if target_task not in CABINET_TASKS:
+        raise ValueError(f"[MujocoUR5eCabinetEnv] Invalid target task: {target_task}")
+    n, nq = qpos.shape
+    _chk(qpos, torch.float64, (n, nq), "qpos")
+    if out is None:
+        out = torch.empty(n, dtype=torch.float64, device=qpos.device)
+    _chk(out, torch.float64, (n,), "reward")
+    N.call("rmbx_cabinet_reward", N.ptr(qpos), nq, int(hinge_adr), int(slide_adr), float(hinge_thre),
+           float(slide_thre), CABINET_TASKS[target_task], N.ptr(out), n, N.stream_ptr())
+    return out
+
+
 def door_reward(pinch_xpos, handle_xpos, door_angle, margin, target_angle, out=None):
     """MujocoUR5eDoorEnv._get_reward for n envs (rmbx_door_reward)."""
     n = pinch_xpos.shape[0]

@@ -5,7 +5,6 @@ chunk history + temporal ensembling + denormalisation in one HIP kernel (rmbx_ac
 bit-exact with the reference's f64 numpy arithmetic.
 """
 
-import os
 
 import torch
 
@@ -45,9 +44,10 @@ class RolloutAct(BatchedRolloutBase):
         # MIOpen Find (measured solver choice per conv shape; once per shape, during warm-up):
         # 66 -> 53 ms for the 1024-env trunk on MI355X (scripts/prof_act.py)
         torch.backends.cudnn.benchmark = True
-        # ... without timing MIOpen's naive reference solver, which takes seconds per shape at
-        # rollout batch sizes and is never the one selected
-        os.environ.setdefault("MIOPEN_DEBUG_CONV_DIRECT_NAIVE_CONV_FWD", "0")
+        # (MIOpen's naive reference solver, which Find times for seconds per shape at 1024-env batch
+        # sizes and never selects, is excluded by bench.py / bin/Rollout.py for large batches via
+        # MIOPEN_DEBUG_CONV_DIRECT_NAIVE_CONV_FWD=0: process-wide, so not set here, where a
+        # diffusion policy's small convs may need it)
         self.policy = self.policy.eval().requires_grad_(False)
         self.policy.fuse_backbone()
         self.policy = self.policy.to(device=self.device, dtype=self.policy_dtype).requires_grad_(False)

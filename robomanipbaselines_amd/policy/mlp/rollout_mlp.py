@@ -11,7 +11,6 @@
   refills on the same call for every env.
 """
 
-import os
 
 import torch
 
@@ -40,9 +39,10 @@ class RolloutMlp(BatchedRolloutBase):
         self.policy = self.policy.eval().requires_grad_(False)
         self.policy.fuse_backbone()
         torch.backends.cudnn.benchmark = True
-        # ... without timing MIOpen's naive reference solver, which takes seconds per shape at
-        # rollout batch sizes and is never the one selected
-        os.environ.setdefault("MIOPEN_DEBUG_CONV_DIRECT_NAIVE_CONV_FWD", "0")
+        # (MIOpen's naive reference solver, which Find times for seconds per shape at 1024-env batch
+        # sizes and never selects, is excluded by bench.py / bin/Rollout.py for large batches via
+        # MIOPEN_DEBUG_CONV_DIRECT_NAIVE_CONV_FWD=0: process-wide, so not set here, where a
+        # diffusion policy's small convs may need it)
         self.policy = self.policy.to(device=self.device, dtype=self.policy_dtype)
         self.policy._fused = self.policy._fused.to(memory_format=torch.channels_last)
 

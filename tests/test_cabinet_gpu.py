@@ -1,0 +1,107 @@
+"""MujocoUR5eCabinet on the batched kernels: the compiled cabinet scene (hinged
+lid + sliding drawer) steps on the GPU engine in agreement with the C oracle, the env's reward is
+rmbx_cabinet_reward bit-exact against the reference's _get_reward golden vectors, and the AutoEval
+command line runs the task."""
+
+import os
+
+import numpy as np
+import pytest
+import torch
+import yaml
+
+from conftest import GOLDEN
+from oracle.dyn import OracleEnv
+from robomanipbaselines_amd import kernels as K
+from robomanipbaselines_amd import model as MD
+from robomanipbaselines_amd.engine import PhysicsEngine
+from robomanipbaselines_amd.envs.ur5e_cabinet import (CABINET_HINGE_THRE, CABINET_INIT_QPOS,
+                                                      CABINET_SLIDE_THRE)
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def test_cabinet_engine_matches_oracle():
+    arrays = MD.load("ur5e_cabinet")
+    info = MD.ModelInfo(arrays)
+    hq, sq = info.qposadr("hinge"), info.qposadr("slide")
+    rng = np.random.default_rng(4)
+    states = []
+    for i in range(4):
+        e = OracleEnv(arrays)
+        qpos = arrays["qpos0"].copy()
+        qpos[:14] = CABINET_INIT_QPOS
+        qpos[hq] = 0.4 * i  # lid partly open
+        qpos[sq] = 0.03 * i  # drawer partly out
+        ctrl = np.concatenate([CABINET_INIT_QPOS[:6] + rng.normal(0, 0.05, 6), [rng.uniform(0, 255)]])
+        e.set_state(0.0, qpos, np.zeros(e.nv), np.zeros(e.nv), ctrl)
+        for _ in range((0, 5, 20, 40)[i]):
+            e.step(8)
+        states.append((*e.state(), ctrl))
+    eng = PhysicsEngine(arrays, 4, DEV)
+    eng.time.copy_(torch.tensor([s[0] for s in states], dtype=torch.float64))
+    for k, name in ((1, "qpos"), (2, "qvel"), (3, "qacc_ws"), (4, "ctrl")):
+        getattr(eng, name).copy_(torch.tensor(np.array([s[k] for s in states])))
+    eng.step(8)
+    torch.cuda.synchronize()
+    qp1 = eng.qpos.cpu().numpy()
+    for _ in range(24):
+        eng.step(8)
+    qp25 = eng.qpos.cpu().numpy()
+    for i, (t, qp, qv, qa, c) in enumerate(states):
+        o = OracleEnv(arrays)
+        o.set_state(t, qp, qv, qa, c)
+        o.step(8)
+        np.testing.assert_allclose(qp1[i], o.state()[1], rtol=0, atol=1e-8)
+        for _ in range(24):
+            o.step(8)
+        np.testing.assert_allclose(qp25[i], o.state()[1], rtol=0, atol=1e-4)
+
+
+def test_cabinet_reward_matches_golden():
+    d = np.load(os.path.join(GOLDEN, "reward_cabinet.npz"))
+    n = len(d["reward"])
+    qpos = torch.zeros((n, 16), dtype=torch.float64)
+    qpos[:, 15] = torch.from_numpy(d["hinge"])
+    qpos[:, 14] = torch.from_numpy(d["slide"])
+    qpos = qpos.to(DEV)
+    got = np.zeros(n)
+    tasks = [None, "hinge", "slide"]
+    for t in range(3):
+        r = K.cabinet_reward(qpos, 15, 14, CABINET_HINGE_THRE, CABINET_SLIDE_THRE, tasks[t]).cpu().numpy()
+        sel = d["task"] == t
+        got[sel] = r[sel]
+    np.testing.assert_array_equal(got, d["reward"])
+    with pytest.raises(ValueError):
+        K.cabinet_reward(qpos, 15, 14, CABINET_HINGE_THRE, CABINET_SLIDE_THRE, "lid")
+
+
+def test_cabinet_env_reward_on_engine_state():
+    from robomanipbaselines_amd.envs.ur5e_cabinet import BatchedMujocoUR5eCabinetEnv
+
+    env = BatchedMujocoUR5eCabinetEnv(6, DEV)
+    env.modify_world(world_idx=np.arange(6))
+    env.reset()
+    env.engine.qpos[:, env._hinge_qadr] = torch.tensor([0.0, 2.0, 2.2, 0.5, 0.0, 2.5], dtype=torch.float64)
+    env.engine.qpos[:, env._slide_qadr] = torch.tensor([0.0, 0.0, 0.0, 0.13, 0.125, 0.14], dtype=torch.float64)
+    r = env._get_reward().cpu().numpy()
+    np.testing.assert_array_equal(r, [0, 0, 1, 1, 1, 1])
+    env.target_task = "hinge"
+    np.testing.assert_array_equal(env._get_reward().cpu().numpy(), [0, 0, 1, 0, 0, 1])
+    env.target_task = "slide"
+    np.testing.assert_array_equal(env._get_reward().cpu().numpy(), [0, 0, 0, 1, 1, 1])
+
+
+def test_cabinet_autoeval_command_line(tmp_path):
+    from robomanipbaselines_amd.bin.Rollout import main
+
+    res = os.path.join(tmp_path, "result.yaml")
+    ro = main(["Mlp", "MujocoUR5eCabinet", "--auto_exit", "--no_plot", "--no_render", "--world_idx_list", "0", "5",
+               "--result_filename", res, "--max_duration", "1.0"])
+    with open(res) as f:
+        data = yaml.safe_load(f)
+    assert len(data["success"]) == 2
+    for d in data["duration"]:
+        assert 1.0 < d <= 1.0 + 0.032 + 1e-9
+    assert np.isfinite(ro.env.engine.qpos.cpu().numpy()).all()

@@ -60,6 +60,18 @@ def test_door_reward_oracle_bitexact():
     assert 0 < (d["reward"] >= 1.0).sum() < len(d["reward"])
 
 
+def test_cabinet_reward_oracle_bitexact():
+    """oracle/glue.cabinet_reward vs MujocoUR5eCabinetEnv._get_reward (MujocoUR5eCabinetEnv.py:57-73),
+    every target task, thresholds hit exactly and by one ulp, NaN joints."""
+    d = _load("reward_cabinet.npz")
+    tasks = [None, "hinge", "slide"]
+    got = np.array([glue.cabinet_reward(h, s, tasks[t]) for h, s, t in zip(d["hinge"], d["slide"], d["task"])])
+    np.testing.assert_array_equal(got, d["reward"])
+    assert 0 < d["reward"].sum() < len(d["reward"])
+    with pytest.raises(ValueError):
+        glue.cabinet_reward(0.0, 0.0, "lid")
+
+
 def test_obs_oracle_bitexact():
     d = _load("obs_ur5e.npz")
     for n in range(len(d["qpos"])):

@@ -10,7 +10,8 @@ from robomanipbaselines_amd.mjcf import compiler as C  # noqa: E402
 REF_ENVS = "/root/reference/robo_manip_baselines/envs/assets/mujoco/envs"
 SCENES = {"ur5e_cable": os.path.join(REF_ENVS, "ur5e", "env_ur5e_cable.xml"),
           "ur5e_insert": os.path.join(REF_ENVS, "ur5e", "env_ur5e_insert.xml"),
-          "ur5e_door": os.path.join(REF_ENVS, "ur5e", "env_ur5e_door.xml")}
+          "ur5e_door": os.path.join(REF_ENVS, "ur5e", "env_ur5e_door.xml"),
+          "ur5e_cabinet": os.path.join(REF_ENVS, "ur5e", "env_ur5e_cabinet.xml")}
 UR5E_URDF = "/root/reference/robo_manip_baselines/envs/assets/common/robots/ur5e/ur5e.urdf"
 
 

@@ -427,6 +427,42 @@ def gen_reward_door(importlib):
     print("door reward: successes", int((rewards >= 1.0).sum()), "of", N)
 
 
+def gen_reward_cabinet(importlib):
+    """MujocoUR5eCabinetEnv._get_reward (MujocoUR5eCabinetEnv.py:57-73) on synthetic hinge / slide
+    joint values around the 120 deg and 0.12 m thresholds (exact values, NaN) for every target task."""
+    Env = importlib.import_module("robo_manip_baselines.envs.mujoco.ur5e.MujocoUR5eCabinetEnv").MujocoUR5eCabinetEnv
+    rng = np.random.default_rng(6061)
+    N = 1536
+    tasks = [None, "hinge", "slide"]
+    hinge = rng.uniform(0.0, 3.1415, N)
+    slide = rng.uniform(0.0, 0.15, N)
+    hthre = np.deg2rad(120.0)
+    for n in range(N):
+        kind = n % 12
+        if kind == 1:
+            hinge[n] = hthre
+        if kind == 2:
+            hinge[n] = np.nextafter(hthre, 4.0)
+        if kind == 3:
+            slide[n] = 0.12
+        if kind == 4:
+            slide[n] = np.nextafter(0.12, 1.0)
+        if kind == 5:
+            hinge[n] = np.nan
+        if kind == 6:
+            slide[n] = np.nan
+    task = np.array([n % 3 for n in range(N)], dtype=np.int32)
+    rewards = np.zeros(N)
+    for n in range(N):
+        env = object.__new__(Env)
+        joints = {"hinge": hinge[n], "slide": slide[n]}
+        env.data = types.SimpleNamespace(joint=lambda nm, _j=joints: types.SimpleNamespace(qpos=np.array([_j[nm]])))
+        env.target_task = tasks[task[n]]
+        rewards[n] = env._get_reward()
+    np.savez(os.path.join(OUT, "reward_cabinet.npz"), hinge=hinge, slide=slide, task=task, reward=rewards)
+    print("cabinet reward: successes", int(rewards.sum()), "of", N)
+
+
 def gen_obs(importlib):
     """MujocoUR5eEnvBase._get_obs (MujocoUR5eEnvBase.py:78-119)."""
     Base = importlib.import_module(
@@ -664,6 +700,7 @@ def main():
     gen_reward(importlib)
     gen_reward_insert(importlib)
     gen_reward_door(importlib)
+    gen_reward_cabinet(importlib)
     gen_obs(importlib)
     gen_depth_and_pointcloud(importlib)
     gen_phase_schedule(importlib)
