@@ -95,6 +95,14 @@ int rmbx_insert_reward(const double* peg_xpos, const double* hole_xpos, const do
 int rmbx_cabinet_reward(const double* qpos, int qpos_stride, int hinge_adr, int slide_adr, double hinge_thre,
                         double slide_thre, int target_task, double* reward, int n_env, void* stream);
 
+/* Toolbox placement reward, batched.
+ * Replaces envs/mujoco/ur5e/MujocoUR5eToolboxEnv.py:46-57 (_get_reward): 1.0 iff
+ * max(|toolbox - mat|_xy) < xy_thre (0.03 m; NaN fails, as numpy's max propagates it) and
+ * toolbox_z < mat_z + z_offset (0.005 m).  toolbox_xpos, mat_xpos: body xpos f64 [n_env][3].
+ * Bit-exact (comparisons only). */
+int rmbx_toolbox_reward(const double* toolbox_xpos, const double* mat_xpos, double* reward, int n_env,
+                        double xy_thre, double z_offset, void* stream);
+
 /* Door-opening reward, batched.
  * Replaces envs/mujoco/ur5e/MujocoUR5eDoorEnv.py:52-67 (_get_reward): 0.5 * (reaching + opening)
  * with reaching = exp(-10 max(|pinch - handle| - margin, 0)) (1 once the door is open),

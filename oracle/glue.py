@@ -244,3 +244,12 @@ def cabinet_reward(hinge_qpos, slide_qpos, target_task=None):
     if target_task == "slide":
         return 1.0 if slide_success else 0.0
     raise ValueError(f"Invalid target task: {target_task}")
+
+
+def toolbox_reward(toolbox_pos, mat_pos):
+    """envs/mujoco/ur5e/MujocoUR5eToolboxEnv.py:46-57 (_get_reward)."""
+    xy_thre = 0.03
+    z_thre = mat_pos[2] + 0.005
+    if (np.max(np.abs(toolbox_pos[:2] - mat_pos[:2])) < xy_thre) and (toolbox_pos[2] < z_thre):
+        return 1.0
+    return 0.0

@@ -13,7 +13,7 @@ import sys
 import yaml
 
 POLICIES = ["Mlp", "Act", "DiffusionPolicy", "DiffusionPolicy3d"]
-ENVS = ["MujocoUR5eCable", "MujocoUR5eInsert", "MujocoUR5eDoor", "MujocoUR5eCabinet"]
+ENVS = ["MujocoUR5eCable", "MujocoUR5eInsert", "MujocoUR5eDoor", "MujocoUR5eCabinet", "MujocoUR5eToolbox"]
 
 
 def camel_to_snake(name):

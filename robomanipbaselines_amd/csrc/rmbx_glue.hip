@@ -197,6 +197,26 @@ __device__ double insert_reward_one(const double* __restrict__ peg, const double
 }
 
 // -----------------------------------------------------------------------------------------
+// Toolbox placement reward (envs/mujoco/ur5e/MujocoUR5eToolboxEnv.py:46-57): toolbox within
+// xy_thre of the mat in x and y (numpy max, NaN -> fail) and below the mat height + z_off
+// -----------------------------------------------------------------------------------------
+__global__ void toolbox_reward_kernel(const double* __restrict__ box, const double* __restrict__ mat,
+                                      double* __restrict__ reward, int n_env, double xy_thre, double z_off) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n_env) return;
+  const double* b = box + 3 * (size_t)e;
+  const double* t = mat + 3 * (size_t)e;
+  const double dx = fabs(b[0] - t[0]), dy = fabs(b[1] - t[1]);
+  double r = 0.0;
+  if (!isnan(dx) && !isnan(dy)) {
+    const double m = dy > dx ? dy : dx;
+    const double z_thre = t[2] + z_off;
+    if (m < xy_thre && b[2] < z_thre) r = 1.0;
+  }
+  reward[e] = r;
+}
+
+// -----------------------------------------------------------------------------------------
 // Door-opening reward (envs/mujoco/ur5e/MujocoUR5eDoorEnv.py:52-67): continuous, success iff 1.0
 // -----------------------------------------------------------------------------------------
 __device__ double door_reward_one(const double* __restrict__ pinch, const double* __restrict__ handle, double angle,
@@ -430,6 +450,17 @@ int rmbx_cabinet_reward(const double* qpos, int qpos_stride, int hinge_adr, int 
   if (n_env == 0) return RMBX_OK;
   hipLaunchKernelGGL(cabinet_reward_kernel, dim3((n_env + 255) / 256), dim3(256), 0, as_stream(stream), qpos,
                      qpos_stride, hinge_adr, slide_adr, hinge_thre, slide_thre, target_task, reward, n_env);
+  RMBX_CHECK_LAUNCH();
+  return RMBX_OK;
+}
+
+int rmbx_toolbox_reward(const double* toolbox_xpos, const double* mat_xpos, double* reward, int n_env,
+                        double xy_thre, double z_offset, void* stream) {
+  RMBX_CHECK_ARG(n_env >= 0, "bad n_env=%d", n_env);
+  RMBX_CHECK_ARG(toolbox_xpos && mat_xpos && reward, "NULL buffer");
+  if (n_env == 0) return RMBX_OK;
+  hipLaunchKernelGGL(toolbox_reward_kernel, dim3((n_env + 255) / 256), dim3(256), 0, as_stream(stream),
+                     toolbox_xpos, mat_xpos, reward, n_env, xy_thre, z_offset);
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
 }

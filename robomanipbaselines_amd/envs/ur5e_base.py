@@ -6,7 +6,8 @@ rep_env_idx; envs/isaac/IsaacUR5eEnvBase.py:104-106, 379-431) the reference's on
 exposes.  Every per-step computation runs in HIP kernels behind the C ABI: physics
 (rmbx_engine_step), observation mapping (rmbx_ur5e_obs), the task's success predicate and camera
 rendering (rmbx_render).  Tensors stay resident on the device.  Task subclasses
-(ur5e_cable.py, ur5e_insert.py) name the compiled scene, the initial arm/gripper pose, the body
+(ur5e_cable.py, ur5e_insert.py, ur5e_door.py, ur5e_cabinet.py, ur5e_toolbox.py) name the
+compiled scene, the initial arm/gripper pose, the body
 that modify_world moves per world index, and the reward kernel.
 """
 
@@ -56,6 +57,7 @@ class BatchedMujocoUR5eEnvBase:
         self.original_world_pos = self.arrays["body_pos"][self._world_body].copy()
         self.init_qpos = self.arrays["qpos0"].copy()
         self.init_qpos[: len(self.init_qpos_head)] = self.init_qpos_head
+        self.init_qpos_env = None  # [n, nq] when the task's modify_world writes init qpos per env
         self._setup_task()
         ctrl = self.arrays["act_ctrlrange"]
         self.action_low, self.action_high = ctrl[:, 0].copy(), ctrl[:, 1].copy()
@@ -71,6 +73,15 @@ class BatchedMujocoUR5eEnvBase:
         """<Task>Env.modify_world for every env (MujocoUR5eCableEnv.py:107-118,
         MujocoUR5eInsertEnv.py:65-76): the task body's offset per world index plus U(-s, s)^3
         noise from a per-env Philox stream (seed, env index)."""
+        world_idx, pos = self._world_positions(world_idx, cumulative_idx)
+        bp = self.engine.body_pos
+        bp[:, self._world_body, :] = torch.tensor(pos, dtype=torch.float64, device=self.device)
+        self.world_idx = world_idx
+        return world_idx
+
+    def _world_positions(self, world_idx, cumulative_idx):
+        """Per-env world index and task-body position: offset per world index plus U(-s, s)^3
+        noise from a per-env Philox stream (seed, env index)."""
         n = self.num_envs
         offsets = np.asarray(self.world_offsets, dtype=np.float64)
         if world_idx is None:
@@ -82,16 +93,15 @@ class BatchedMujocoUR5eEnvBase:
             for e in range(n):
                 rng = np.random.Generator(np.random.Philox(key=self.seed, counter=[e, 0, 0, 0]))
                 pos[e] += rng.uniform(low=-1.0 * s, high=s, size=3)
-        bp = self.engine.body_pos
-        bp[:, self._world_body, :] = torch.tensor(pos, dtype=torch.float64, device=self.device)
-        self.world_idx = world_idx
-        return world_idx
+        return world_idx, pos
 
     def reset(self, seed=None, mask=None):
         """MujocoEnvBase.reset_model (:163-165): qpos = init_qpos, qvel = 0, time = 0, then
         mj_forward; returns (obs, info)."""
         e = self.engine
-        q0 = torch.tensor(self.init_qpos, dtype=torch.float64, device=self.device)
+        # per-env initial qpos when modify_world placed a free body (init_qpos_env), else shared
+        init = self.init_qpos if self.init_qpos_env is None else self.init_qpos_env
+        q0 = torch.tensor(init, dtype=torch.float64, device=self.device)
         ctrl0 = torch.tensor(np.concatenate([self.init_qpos[:6], [0.0]]), dtype=torch.float64, device=self.device)
         if mask is None:
             e.qpos.copy_(q0.expand_as(e.qpos))
@@ -102,7 +112,7 @@ class BatchedMujocoUR5eEnvBase:
             e.stats.zero_()
         else:
             m = mask.bool()
-            e.qpos[m] = q0
+            e.qpos[m] = q0 if q0.dim() == 1 else q0[m]
             e.qvel[m] = 0
             e.qacc_ws[m] = 0
             e.time[m] = 0

@@ -144,6 +144,19 @@ def cable_reward(cable_xpos, end_xpos, pole1, pole2, out=None):
     return out
 
 
+def toolbox_reward(toolbox_xpos, mat_xpos, xy_thre, z_offset, out=None):
+    """MujocoUR5eToolboxEnv._get_reward for n envs (rmbx_toolbox_reward)."""
+    n = toolbox_xpos.shape[0]
+    _chk(toolbox_xpos, torch.float64, (n, 3), "toolbox_xpos")
+    _chk(mat_xpos, torch.float64, (n, 3), "mat_xpos")
+    if out is None:
+        out = torch.empty(n, dtype=torch.float64, device=toolbox_xpos.device)
+    _chk(out, torch.float64, (n,), "reward")
+    N.call("rmbx_toolbox_reward", N.ptr(toolbox_xpos), N.ptr(mat_xpos), N.ptr(out), n, float(xy_thre),
+           float(z_offset), N.stream_ptr())
+    return out
+
+
 CABINET_TASKS = {None: 0, "hinge": 1, "slide": 2}
 
 

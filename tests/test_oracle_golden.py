@@ -72,6 +72,14 @@ def test_cabinet_reward_oracle_bitexact():
         glue.cabinet_reward(0.0, 0.0, "lid")
 
 
+def test_toolbox_reward_oracle_bitexact():
+    """oracle/glue.toolbox_reward vs MujocoUR5eToolboxEnv._get_reward (MujocoUR5eToolboxEnv.py:46-57)."""
+    d = _load("reward_toolbox.npz")
+    got = np.array([glue.toolbox_reward(b, t) for b, t in zip(d["toolbox"], d["mat"])])
+    np.testing.assert_array_equal(got, d["reward"])
+    assert 0 < d["reward"].sum() < len(d["reward"])
+
+
 def test_obs_oracle_bitexact():
     d = _load("obs_ur5e.npz")
     for n in range(len(d["qpos"])):

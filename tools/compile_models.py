@@ -11,7 +11,8 @@ REF_ENVS = "/root/reference/robo_manip_baselines/envs/assets/mujoco/envs"
 SCENES = {"ur5e_cable": os.path.join(REF_ENVS, "ur5e", "env_ur5e_cable.xml"),
           "ur5e_insert": os.path.join(REF_ENVS, "ur5e", "env_ur5e_insert.xml"),
           "ur5e_door": os.path.join(REF_ENVS, "ur5e", "env_ur5e_door.xml"),
-          "ur5e_cabinet": os.path.join(REF_ENVS, "ur5e", "env_ur5e_cabinet.xml")}
+          "ur5e_cabinet": os.path.join(REF_ENVS, "ur5e", "env_ur5e_cabinet.xml"),
+          "ur5e_toolbox": os.path.join(REF_ENVS, "ur5e", "env_ur5e_toolbox.xml")}
 UR5E_URDF = "/root/reference/robo_manip_baselines/envs/assets/common/robots/ur5e/ur5e.urdf"
 
 

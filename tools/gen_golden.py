@@ -463,6 +463,39 @@ def gen_reward_cabinet(importlib):
     print("cabinet reward: successes", int(rewards.sum()), "of", N)
 
 
+def gen_reward_toolbox(importlib):
+    """MujocoUR5eToolboxEnv._get_reward (MujocoUR5eToolboxEnv.py:46-57) on synthetic toolbox / mat
+    positions around the 3 cm x/y window and the mat height + 5 mm (exact values, NaN)."""
+    Env = importlib.import_module("robo_manip_baselines.envs.mujoco.ur5e.MujocoUR5eToolboxEnv").MujocoUR5eToolboxEnv
+    rng = np.random.default_rng(7071)
+    N = 2048
+    box = np.zeros((N, 3))
+    mat = np.zeros((N, 3))
+    rewards = np.zeros(N)
+    for n in range(N):
+        t = np.array([0.0, 0.2, 0.815]) + rng.normal(0, 0.01, 3)
+        b = t + np.array([*rng.uniform(-0.05, 0.05, 2), rng.uniform(-0.01, 0.02)])
+        kind = n % 8
+        if kind == 1:
+            b[0] = t[0] + 0.03  # on the x/y window edge
+        if kind == 2:
+            b[2] = t[2] + 0.005  # on the height threshold
+        if kind == 3:
+            b[:2] = t[:2] + rng.uniform(-0.02, 0.02, 2)
+            b[2] = t[2] + rng.uniform(-0.002, 0.004)
+        if kind == 4:
+            b[1] = np.nan
+        if kind == 5:
+            t[2] = np.nan
+        box[n], mat[n] = b, t
+        env = object.__new__(Env)
+        bodies = {"toolbox": types.SimpleNamespace(xpos=b.copy()), "mat": types.SimpleNamespace(xpos=t.copy())}
+        env.data = types.SimpleNamespace(body=lambda nm, _b=bodies: _b[nm])
+        rewards[n] = env._get_reward()
+    np.savez(os.path.join(OUT, "reward_toolbox.npz"), toolbox=box, mat=mat, reward=rewards)
+    print("toolbox reward: successes", int(rewards.sum()), "of", N)
+
+
 def gen_obs(importlib):
     """MujocoUR5eEnvBase._get_obs (MujocoUR5eEnvBase.py:78-119)."""
     Base = importlib.import_module(
@@ -701,6 +734,7 @@ def main():
     gen_reward_insert(importlib)
     gen_reward_door(importlib)
     gen_reward_cabinet(importlib)
+    gen_reward_toolbox(importlib)
     gen_obs(importlib)
     gen_depth_and_pointcloud(importlib)
     gen_phase_schedule(importlib)
