@@ -1602,7 +1602,8 @@ __device__ void sensors(Env& e, int ncon, int tid, double* cacc, double* cfrc, d
 #define MAX_BODY 64
 
 struct SolverShared {
-  double Lcol[MAX_NB][16];
+  double Lcol[MAX_NB][16];  // Cholesky: current block column, by block row
+  double Ldiag[16];         // Cholesky: factor of the current diagonal block
   double a0[MAX_NVP];    // qacc_smooth
   double a[MAX_NVP];     // current qacc
   double res[MAX_NVP];   // a - a0
@@ -1667,8 +1668,12 @@ __device__ __forceinline__ void potrf4(double* a) {
     for (int k = j + 1; k < 4; k++) a[4 * j + k] = 0;
   }
 }
-// a := a * L^-T  (L lower 4x4)
+// a := a * L^-T  (L lower 4x4); the four independent reciprocals of the diagonal replace the
+// sixteen dependent divisions on the step's critical path
 __device__ __forceinline__ void trsm4(double* a, const double* L) {
+  double inv[4];
+#pragma unroll
+  for (int c = 0; c < 4; c++) inv[c] = 1.0 / L[4 * c + c];
 #pragma unroll
   for (int r = 0; r < 4; r++) {
 #pragma unroll
@@ -1676,22 +1681,24 @@ __device__ __forceinline__ void trsm4(double* a, const double* L) {
       double t = a[4 * r + c];
 #pragma unroll
       for (int k = 0; k < c; k++) t -= a[4 * r + k] * L[4 * c + k];
-      a[4 * r + c] = t / L[4 * c + c];
+      a[4 * r + c] = t * inv[c];
     }
   }
 }
 
-// Distributed block Cholesky: thread t < nblk owns block (bi, bj) in a[16].
+// Distributed block Cholesky: thread t < nblk owns block (bi, bj) in a[16].  Lookahead: the
+// owner of diagonal block k+1 factors it right after its own step-k update (every update of
+// that block is its own), so a step costs two barriers and the potrf overlaps the other updates.
 __device__ void blk_cholesky(double* a, int bi, int bj, bool own, int NB, SolverShared& S) {
-  for (int k = 0; k < NB; k++) {
-    if (own && bi == k && bj == k) {
-      potrf4(a);
+  if (own && bi == 0 && bj == 0) {
+    potrf4(a);
 #pragma unroll
-      for (int q = 0; q < 16; q++) S.Lcol[k][q] = a[q];
-    }
+    for (int q = 0; q < 16; q++) S.Ldiag[q] = a[q];
+  }
+  for (int k = 0; k < NB; k++) {
     __syncthreads();
     if (own && bj == k && bi > k) {
-      trsm4(a, S.Lcol[k]);
+      trsm4(a, S.Ldiag);
 #pragma unroll
       for (int q = 0; q < 16; q++) S.Lcol[bi][q] = a[q];
     }
@@ -1708,9 +1715,14 @@ __device__ void blk_cholesky(double* a, int bi, int bj, bool own, int NB, Solver
           for (int r = 0; r < 4; r++) t -= Li[4 * p + r] * Lj[4 * q + r];
           a[4 * p + q] = t;
         }
+      if (bi == k + 1 && bj == k + 1) {
+        potrf4(a);
+#pragma unroll
+        for (int q = 0; q < 16; q++) S.Ldiag[q] = a[q];  // read after the next barrier
+      }
     }
-    __syncthreads();
   }
+  __syncthreads();
 }
 
 // x = (L L^T)^-1 b ; b, x in LDS (length NVP, may alias); uses S.acc
@@ -1722,13 +1734,15 @@ __device__ void blk_solve(const double* a, int bi, int bj, bool own, int NB, con
   // forward: y_j = L_jj^-1 (acc_j); acc_i -= L_ij y_j
   for (int j = 0; j < NB; j++) {
     if (own && bi == j && bj == j) {
-      double y[4];
+      double y[4], inv[4];
+#pragma unroll
+      for (int p = 0; p < 4; p++) inv[p] = 1.0 / a[4 * p + p];
 #pragma unroll
       for (int p = 0; p < 4; p++) {
         double t = S.acc[4 * j + p];
 #pragma unroll
         for (int k = 0; k < p; k++) t -= a[4 * p + k] * y[k];
-        y[p] = t / a[4 * p + p];
+        y[p] = t * inv[p];
       }
 #pragma unroll
       for (int p = 0; p < 4; p++) S.acc[4 * j + p] = y[p];
@@ -1745,13 +1759,15 @@ __device__ void blk_solve(const double* a, int bi, int bj, bool own, int NB, con
   // backward: x_i = L_ii^-T acc_i ; acc_j -= L_ij^T x_i
   for (int i = NB - 1; i >= 0; i--) {
     if (own && bi == i && bj == i) {
-      double xx[4];
+      double xx[4], inv[4];
+#pragma unroll
+      for (int p = 0; p < 4; p++) inv[p] = 1.0 / a[4 * p + p];
 #pragma unroll
       for (int p = 3; p >= 0; p--) {
         double t = S.acc[4 * i + p];
 #pragma unroll
         for (int k = p + 1; k < 4; k++) t -= a[4 * k + p] * xx[k];
-        xx[p] = t / a[4 * p + p];
+        xx[p] = t * inv[p];
       }
 #pragma unroll
       for (int p = 0; p < 4; p++) S.acc[4 * i + p] = xx[p];
