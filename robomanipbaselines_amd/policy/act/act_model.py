@@ -58,8 +58,7 @@ class MHA(nn.Module):
         nn.init.zeros_(self.out_proj.bias)
 
     def forward(self, q, k, v):
-        B, Lq, D = q.shape
-        Lk = k.shape[1]
+        D = q.shape[2]
         w, b = self.in_proj_weight, self.in_proj_bias
         if q is k and k is v:
             qkv = F.linear(q, w, b)
@@ -72,6 +71,17 @@ class MHA(nn.Module):
             qq = F.linear(q, w[:D], b[:D])
             kk = F.linear(k, w[D : 2 * D], b[D : 2 * D])
             vv = F.linear(v, w[2 * D :], b[2 * D :])
+        return self._attend(qq, kk, vv)
+
+    def attend_kv(self, q, kk, vv):
+        """forward(q, k, v) with the key / value projections kk, vv already computed (e.g. column
+        slices of one GEMM shared by several layers)."""
+        D = q.shape[2]
+        return self._attend(F.linear(q, self.in_proj_weight[:D], self.in_proj_bias[:D]), kk, vv)
+
+    def _attend(self, qq, kk, vv):
+        B, Lq, D = qq.shape
+        Lk = kk.shape[1]
         hd = D // self.h
         if self.fused_attention and qq.dtype == torch.bfloat16 and hd == 64 and Lk <= 320 and qq.is_cuda:
             from ... import kernels as K
@@ -165,11 +175,17 @@ class DecoderLayer(_LayerOps):
         tgt = self.addnorm(self.norm2, tgt, self.multihead_attn(tgt + query_pos, mk, memory))
         return self.addnorm(self.norm3, tgt, self.ffn(tgt))
 
-    def forward_q(self, tgt, q, memory, query_pos, mem_pos, want_next_q):
+    def forward_q(self, tgt, q, memory, query_pos, mem_pos, want_next_q, cross_kv=None):
         """forward() with q = tgt + query_pos given; both later `+ query_pos` adds are fused into
-        the LayerNorm passes that produce their operands.  Returns (out, out + query_pos or None)."""
+        the LayerNorm passes that produce their operands.  cross_kv: this layer's cross-attention
+        key / value projections of the memory, when computed for all layers at once.  Returns
+        (out, out + query_pos or None)."""
         tgt, q2 = self.addnorm_pos(self.norm1, tgt, self.self_attn(q, q, tgt), query_pos)
-        tgt = self.addnorm(self.norm2, tgt, self.multihead_attn(q2, mem_pos, memory))
+        if cross_kv is not None:
+            ca = self.multihead_attn.attend_kv(q2, *cross_kv)
+        else:
+            ca = self.multihead_attn(q2, mem_pos, memory)
+        tgt = self.addnorm(self.norm2, tgt, ca)
         if want_next_q:
             return self.addnorm_pos(self.norm3, tgt, self.ffn(tgt), query_pos)
         return self.addnorm(self.norm3, tgt, self.ffn(tgt)), None
@@ -211,6 +227,32 @@ class ActModel(nn.Module):
                 if isinstance(m, MHA):
                     m.fused_attention = on
         return self
+
+    batch_cross_kv = True
+
+    def _cross_kv(self, mem_pos, mem, n_dec):
+        """Device inference: the memory's cross-attention keys (from mem + pos) and values (from
+        mem) of all n_dec decoder layers as two GEMMs with N = n_dec * d instead of 2 * n_dec GEMMs
+        with N = d (the memory is the same for every layer); per layer, column slices of them."""
+        layers = self.decoder_layers[:n_dec]
+        if not self.batch_cross_kv or n_dec < 2 or not all(getattr(l, "fused", False) for l in layers):
+            return None
+        D = mem.shape[2]
+        ws = [l.multihead_attn.in_proj_weight for l in layers]
+        bs = [l.multihead_attn.in_proj_bias for l in layers]
+        key = tuple((w.data_ptr(), w.dtype) for w in ws)
+        cache = self.__dict__.get("_cross_w")
+        if cache is None or cache[0] != key:
+            wk = torch.cat([w[D: 2 * D] for w in ws]).contiguous()
+            bk = torch.cat([b[D: 2 * D] for b in bs]).contiguous()
+            wv = torch.cat([w[2 * D:] for w in ws]).contiguous()
+            bv = torch.cat([b[2 * D:] for b in bs]).contiguous()
+            cache = (key, wk, bk, wv, bv)
+            self.__dict__["_cross_w"] = cache
+        _, wk, bk, wv, bv = cache
+        k_all = F.linear(mem_pos, wk, bk)
+        v_all = F.linear(mem, wv, bv)
+        return [(k_all[..., i * D: (i + 1) * D], v_all[..., i * D: (i + 1) * D]) for i in range(n_dec)]
 
     def _pos(self, h, w, device, dtype):
         key = (h, w, str(device), dtype)
@@ -258,8 +300,10 @@ class ActModel(nn.Module):
         q = tgt + qe
         first = None
         n_dec = 1 if self.prune_dead_decoder else len(self.decoder_layers)
+        cross = self._cross_kv(mem_pos, mem, n_dec)
         for i in range(n_dec):
-            tgt, q = self.decoder_layers[i].forward_q(tgt, q, mem, qe, mem_pos, want_next_q=i + 1 < n_dec)
+            tgt, q = self.decoder_layers[i].forward_q(tgt, q, mem, qe, mem_pos, want_next_q=i + 1 < n_dec,
+                                                      cross_kv=cross[i] if cross else None)
             if i == 0:
                 first = self.decoder_norm(tgt)  # intermediate[0] = norm(output of layer 0)
         return self.action_head(first)
