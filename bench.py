@@ -74,7 +74,7 @@ def parse():
     p.add_argument("--num_envs", type=int, default=1024, help="environments per GPU")
     p.add_argument("--precision", choices=["bf16", "fp32"], default="bf16")
     p.add_argument("--no_cpu_baseline", action="store_true")
-    p.add_argument("--cpu_sample_steps", type=int, default=240,
+    p.add_argument("--cpu_sample_steps", type=int, default=600,
                    help="timed env-steps of the CPU baseline sample (about 10 s of host work)")
     p.add_argument("--act_prune_dead_decoder", action="store_true")
     return p.parse_args()
