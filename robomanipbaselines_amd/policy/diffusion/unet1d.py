@@ -31,6 +31,49 @@ class SinusoidalPosEmb(nn.Module):
         return torch.cat((emb.sin(), emb.cos()), dim=-1)
 
 
+def conv1d_gemm(x, conv):
+    """Conv1d as one GEMM: the k-tap windows of x [B, C, T] (padding, stride) unfolded to
+    [B*To, C*k] rows times the weight viewed [Cout, C*k] (hipBLASLt), -> [B, Cout, To].  At
+    rollout batch sizes the trajectories are short (T = horizon, 16) and wide (C up to 2048), a
+    shape the library GEMM runs far better than the convolution solvers."""
+    k, p, st = conv.kernel_size[0], conv.padding[0], conv.stride[0]
+    B, C, T = x.shape
+    cols = (F.pad(x, (p, p)) if p else x).unfold(2, k, st)
+    To = cols.shape[2]
+    cols = cols.permute(0, 2, 1, 3).reshape(B * To, C * k)
+    y = F.linear(cols, conv.weight.reshape(conv.out_channels, C * k), conv.bias)
+    return y.view(B, To, -1).transpose(1, 2).contiguous()
+
+
+def conv_transpose1d_gemm(x, conv):
+    """ConvTranspose1d(k=4, stride=2, padding=1) as one GEMM: P_k = W_kᵀ x_i for the four taps,
+    then y[2m] = P_1[m] + P_3[m-1], y[2m+1] = P_2[m] + P_0[m+1] (+ bias)."""
+    B, C, T = x.shape
+    Co = conv.weight.shape[1]
+    wk = conv.weight.permute(2, 1, 0).reshape(4 * Co, C)
+    P = F.linear(x.transpose(1, 2).reshape(B * T, C), wk).view(B, T, 4, Co)
+    even = P[:, :, 1] + F.pad(P[:, :-1, 3], (0, 0, 1, 0))
+    odd = P[:, :, 2] + F.pad(P[:, 1:, 0], (0, 0, 0, 1))
+    y = torch.stack([even, odd], dim=2).view(B, 2 * T, Co)
+    if conv.bias is not None:
+        y = y + conv.bias
+    return y.transpose(1, 2).contiguous()
+
+
+def _device_form(x):
+    return x.is_cuda and x.dtype in (torch.bfloat16, torch.float16)
+
+
+def run_conv(conv, x):
+    """conv(x), through the GEMM forms above in the device inference form (bf16)."""
+    if isinstance(conv, nn.Identity) or not _device_form(x):
+        return conv(x)
+    if isinstance(conv, nn.ConvTranspose1d):
+        assert conv.kernel_size[0] == 4 and conv.stride[0] == 2 and conv.padding[0] == 1
+        return conv_transpose1d_gemm(x, conv)
+    return conv1d_gemm(x, conv)
+
+
 class Conv1dBlock(nn.Module):
     """Conv1d -> GroupNorm -> Mish."""
 
@@ -40,7 +83,8 @@ class Conv1dBlock(nn.Module):
                                    nn.GroupNorm(n_groups, out), nn.Mish())
 
     def forward(self, x):
-        return self.block(x)
+        conv, norm, act = self.block
+        return act(norm(run_conv(conv, x)))
 
 
 class ConditionalResidualBlock1D(nn.Module):
@@ -63,7 +107,7 @@ class ConditionalResidualBlock1D(nn.Module):
         else:
             out = out + embed
         out = self.blocks[1](out)
-        return out + self.residual_conv(x)
+        return out + run_conv(self.residual_conv, x)
 
 
 class Downsample1d(nn.Module):
@@ -72,7 +116,7 @@ class Downsample1d(nn.Module):
         self.conv = nn.Conv1d(dim, dim, 3, 2, 1)
 
     def forward(self, x):
-        return self.conv(x)
+        return run_conv(self.conv, x)
 
 
 class Upsample1d(nn.Module):
@@ -81,7 +125,7 @@ class Upsample1d(nn.Module):
         self.conv = nn.ConvTranspose1d(dim, dim, 4, 2, 1)
 
     def forward(self, x):
-        return self.conv(x)
+        return run_conv(self.conv, x)
 
 
 class ConditionalUnet1D(nn.Module):
@@ -122,7 +166,12 @@ class ConditionalUnet1D(nn.Module):
         elif timestep.dim() == 0:
             timestep = timestep[None].to(sample.device)
         timestep = timestep.expand(sample.shape[0])
-        g = self.diffusion_step_encoder(timestep).to(sample.dtype)
+        # the sinusoidal embedding is computed in f32 and fed to the MLP in the weights' dtype
+        enc = self.diffusion_step_encoder
+        g = enc[0](timestep).to(enc[1].weight.dtype)
+        for m in list(enc)[1:]:
+            g = m(g)
+        g = g.to(sample.dtype)
         if global_cond is not None:
             g = torch.cat([g, global_cond], dim=-1)
         h = []
@@ -135,4 +184,4 @@ class ConditionalUnet1D(nn.Module):
         for resnet, resnet2, up in self.up_modules:
             x = torch.cat((x, h.pop()), dim=1)
             x = up(resnet2(resnet(x, g), g))
-        return self.final_conv(x).transpose(1, 2)
+        return run_conv(self.final_conv[1], self.final_conv[0](x)).transpose(1, 2)

@@ -146,6 +146,11 @@ class DiffusionPolicyModel(nn.Module):
                 traj = s.step(i, out, traj)
         return traj
 
+    # Capturing the loop at 256 and 1024 envs crashed the process inside the capture on MI355X (ROCm 7.0
+    # PyTorch, 64 envs capture fine); above this batch the loop runs eagerly, where kernel time
+    # dominates the launch overhead the graph removes.
+    graph_max_batch = 64
+
     def conditional_sample(self, global_cond, use_graph=True, x0=None, noise=None):
         """Sample [B, horizon, A].  x0 (initial trajectory) and noise ([n_noise, B, horizon, A])
         default to fresh torch.randn draws (the reference draws them with torch.randn too)."""
@@ -159,7 +164,7 @@ class DiffusionPolicyModel(nn.Module):
             x0 = torch.randn(shape, device=dev)
         if noise is None:
             noise = torch.randn((nn_,) + shape, device=dev) if nn_ else None
-        if not use_graph or dev.type != "cuda":
+        if not use_graph or dev.type != "cuda" or B > self.graph_max_batch:
             return self._sample_loop(global_cond, x0.contiguous(), noise)
         key = (B, self.dtype)
         if key not in self._graphs:

@@ -6,6 +6,7 @@ batched rollout's env actions follow the reference's pop + limits-denormalisatio
 import numpy as np
 import pytest
 import torch
+import torch.nn.functional as F
 
 pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
@@ -136,3 +137,57 @@ def test_rollout_dp3_pointcloud_and_actions():
                                          ro.model_meta_info["pointcloud"])
         assert c_ref > 0
         assert np.array_equal(pc_last[e], n_ref)
+
+
+@pytest.mark.parametrize("B,C,Co,T,k", [(4, 64, 128, 16, 5), (3, 256, 256, 8, 5), (2, 32, 64, 4, 3)])
+def test_conv1d_gemm_matches_conv1d(B, C, Co, T, k):
+    """The bf16 device form of the UNet's stride-1 Conv1d (unfold + one hipBLASLt GEMM) agrees with
+    F.conv1d in f32 on the same bf16 operands to bf16 output rounding."""
+    import torch.nn as nn
+
+    from robomanipbaselines_amd.policy.diffusion.unet1d import conv1d_gemm
+
+    g = torch.Generator(device=DEV).manual_seed(11)
+    conv = nn.Conv1d(C, Co, k, padding=k // 2).to(DEV)
+    x = torch.randn(B, C, T, device=DEV, generator=g).to(torch.bfloat16)
+    convb = conv.to(torch.bfloat16)
+    got = conv1d_gemm(x, convb).float()
+    want = F.conv1d(x.float(), convb.weight.float(), convb.bias.float(), padding=k // 2)
+    assert got.shape == want.shape == (B, Co, T)
+    assert (got - want).abs().max().item() <= 2 ** -7 * want.abs().max().item() + 1e-3
+
+
+def test_conv_transpose1d_gemm_matches():
+    import torch.nn as nn
+
+    from robomanipbaselines_amd.policy.diffusion.unet1d import conv_transpose1d_gemm
+
+    g = torch.Generator(device=DEV).manual_seed(12)
+    ct = nn.ConvTranspose1d(128, 64, 4, 2, 1).to(DEV).to(torch.bfloat16)
+    x = torch.randn(5, 128, 8, device=DEV, generator=g).to(torch.bfloat16)
+    got = conv_transpose1d_gemm(x, ct).float()
+    want = F.conv_transpose1d(x.float(), ct.weight.float(), ct.bias.float(), 2, 1)
+    assert got.shape == want.shape == (5, 64, 16)
+    assert (got - want).abs().max().item() <= 2 ** -6 * want.abs().max().item() + 1e-3
+
+
+@torch.no_grad()
+def test_unet1d_device_form_matches_fp32():
+    """The whole ConditionalUnet1D in its bf16 device form (every conv as a GEMM) against the f32
+    module on the CPU."""
+    from robomanipbaselines_amd.policy.diffusion.unet1d import ConditionalUnet1D
+
+    torch.manual_seed(0)
+    ref = ConditionalUnet1D(7, global_cond_dim=64, down_dims=(64, 128, 256), kernel_size=5,
+                            cond_predict_scale=True).eval()
+    dev = ConditionalUnet1D(7, global_cond_dim=64, down_dims=(64, 128, 256), kernel_size=5,
+                            cond_predict_scale=True).eval()
+    dev.load_state_dict(ref.state_dict())
+    dev = dev.to(DEV, torch.bfloat16)
+    x = torch.randn(6, 16, 7)
+    gc = torch.randn(6, 64)
+    t = torch.tensor(37)
+    want = ref(x, t, gc)
+    got = dev(x.to(DEV, torch.bfloat16), t.to(DEV), gc.to(DEV, torch.bfloat16)).float().cpu()
+    assert got.shape == want.shape
+    assert (got - want).abs().max().item() <= 5e-2 * max(1.0, want.abs().max().item())
