@@ -35,10 +35,11 @@ struct Layout {
   size_t ten_len, ten_vel;
   size_t con_pos, con_frame, con_dist, con_mu;
   size_t con_tmp;  // collision stage: 4 candidate contacts (pos, normal, dist) per survivor
+  size_t hsave;    // solver: Hessian blocks of the last build (incremental updates)
   size_t J, efc_pos, efc_aref, efc_D, efc_R, efc_force, efc_jar, efc_Js, efc_vel, efc_tmp;
   size_t ints;  // start of the int32 region (in doubles)
   // int32 offsets relative to the int region
-  size_t con_b1, con_b2, con_condim, con_pair, con_efcadr, efc_type, efc_act, scal;
+  size_t con_b1, con_b2, con_condim, con_pair, con_efcadr, efc_type, efc_act, efc_hact, scal;
   size_t istride;  // int32 count
   int nefc_max;
 };
@@ -1616,6 +1617,7 @@ struct SolverShared {
   double tmp[MAX_NVP];
   double jc[RCHUNK][MAX_NVP];  // scaled Jacobian chunk
   double jw[RCHUNK];           // chunk row weights sqrt(D) (active rows)
+  double jsg[RCHUNK];          // chunk row signs (incremental Hessian: +1 added, -1 removed)
   double jw2[RCHUNK];          // sqrt(D) * jar (gradient)
   double bacc[6 * MAX_BODY];  // sensors: body accelerations
   double bfrc[6 * MAX_BODY];  // sensors: body forces
@@ -1903,15 +1905,49 @@ __device__ double solver_grad(const SolverCtx& c, int32_t* act_flags, SolverShar
 
 // Hessian blocks a = M + J^T D_act J (active rows only; J streamed through LDS in RCHUNK-row
 // chunks scaled by sqrt(D))
-__device__ void solver_hessian(const SolverCtx& c, const double* M, const int32_t* act_flags, double* a, int bi,
-                               int bj, bool own, SolverShared& S) {
+// Hessian blocks a = M + J^T D_act J (active rows only; J streamed through LDS in RCHUNK-row
+// chunks scaled by sqrt(D)).  The first build of a substep starts from M; later ones start from
+// the previous H (saved in the workspace) and only add / subtract the rows whose active flag
+// changed since (hess_flags), skipping chunks without such rows — MuJoCo's Newton solver updates
+// its Hessian incrementally in the same way.
+__device__ void solver_hessian(const SolverCtx& c, const double* M, const int32_t* act_flags, int32_t* hess_flags,
+                               double* hsave, bool incremental, double* a, int bi, int bj, bool own,
+                               SolverShared& S) {
   const int tid = c.tid, nv = c.nv, NVP = 4 * c.NB;
-  if (own) load_block(M, nv, bi, bj, a);
+  if (own) {
+    if (incremental) {
+#pragma unroll
+      for (int q = 0; q < 16; q++) a[q] = hsave[16 * tid + q];
+    } else {
+      load_block(M, nv, bi, bj, a);
+    }
+  }
   for (int r0 = 0; r0 < c.nefc; r0 += RCHUNK) {
     const int nr = min(RCHUNK, c.nefc - r0);
     __syncthreads();
-    if (tid < RCHUNK) S.jw[tid] = (tid < nr && act_flags[r0 + tid]) ? sqrt(c.D[r0 + tid]) : 0.0;
+    if (tid < RCHUNK) {
+      double w = 0.0, sg = 1.0;
+      if (tid < nr) {
+        const int r = r0 + tid;
+        const int act = act_flags[r];
+        if (incremental) {
+          if (act != hess_flags[r]) {
+            w = sqrt(c.D[r]);
+            sg = act ? 1.0 : -1.0;
+          }
+        } else if (act) {
+          w = sqrt(c.D[r]);
+        }
+        hess_flags[r] = act;
+      }
+      S.jw[tid] = w;
+      S.jsg[tid] = sg;
+    }
     __syncthreads();
+    bool any = false;
+#pragma unroll
+    for (int k = 0; k < RCHUNK; k++) any |= S.jw[k] != 0.0;
+    if (!any) continue;  // uniform: every thread read the same flags
     const double* src = c.J + (size_t)r0 * nv;
     for (int e = tid; e < RCHUNK * NVP; e += SOLVER_THREADS) {
       const int rr = e / NVP, k = e - rr * NVP;
@@ -1921,9 +1957,10 @@ __device__ void solver_hessian(const SolverCtx& c, const double* M, const int32_
     if (own) {
       for (int rr = 0; rr < nr; rr++) {
         if (S.jw[rr] == 0.0) continue;
+        const double sg = S.jsg[rr];  // -1: a row that left the active set is taken back out
         const double* ji = S.jc[rr] + 4 * bi;
         const double* jj = S.jc[rr] + 4 * bj;
-        const double i0 = ji[0], i1 = ji[1], i2 = ji[2], i3 = ji[3];
+        const double i0 = sg * ji[0], i1 = sg * ji[1], i2 = sg * ji[2], i3 = sg * ji[3];
         const double j0 = jj[0], j1 = jj[1], j2 = jj[2], j3 = jj[3];
         a[0] += i0 * j0; a[1] += i0 * j1; a[2] += i0 * j2; a[3] += i0 * j3;
         a[4] += i1 * j0; a[5] += i1 * j1; a[6] += i1 * j2; a[7] += i1 * j3;
@@ -1931,6 +1968,10 @@ __device__ void solver_hessian(const SolverCtx& c, const double* M, const int32_
         a[12] += i3 * j0; a[13] += i3 * j1; a[14] += i3 * j2; a[15] += i3 * j3;
       }
     }
+  }
+  if (own) {
+#pragma unroll
+    for (int q = 0; q < 16; q++) hsave[16 * tid + q] = a[q];
   }
   __syncthreads();
 }
@@ -2001,7 +2042,7 @@ __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj,
     SPROF(10)
     if (scale * sqrt(gn) < m.solver_tolerance) break;
     if (changed || !have_factor) {
-      solver_hessian(c, M, act_flags, a, bi, bj, own, S);
+      solver_hessian(c, M, act_flags, WI(efc_hact), W(hsave), have_factor, a, bi, bj, own, S);
       SPROF(15)
       blk_cholesky(a, bi, bj, own, NB, S);
       have_factor = true;
@@ -2312,6 +2353,8 @@ static Layout make_layout(const rmbx_model& m) {
   L.con_dist = take(mc);
   L.con_mu = take(mc);
   const int ne = L.nefc_max;
+  const int nb4 = (nv + 3) / 4;
+  L.hsave = take(16 * (size_t)(nb4 * (nb4 + 1) / 2));
   L.J = take((size_t)ne * nv);
   L.efc_pos = take(ne);
   L.efc_aref = take(ne);
@@ -2340,6 +2383,7 @@ static Layout make_layout(const rmbx_model& m) {
   L.con_efcadr = itake(mc);
   L.efc_type = itake(ne);
   L.efc_act = itake(ne);
+  L.efc_hact = itake(ne);
   L.scal = itake(8);
   L.istride = io;
   L.stride = o + (io + 1) / 2;
