@@ -146,9 +146,10 @@ class DiffusionPolicyModel(nn.Module):
                 traj = s.step(i, out, traj)
         return traj
 
-    # Capturing the loop at 256 and 1024 envs crashed the process inside the capture on MI355X (ROCm 7.0
-    # PyTorch, 64 envs capture fine); above this batch the loop runs eagerly, where kernel time
-    # dominates the launch overhead the graph removes.
+    # Graph replay removes launch overhead, which matters at small batches only: at 1024 envs the
+    # DP3 loop takes 75.0 ms eager vs 75.4 ms replayed (scripts/diag_dp3.py).  With MIOpen's
+    # conv1d (the f32 form) capturing at 256+ envs crashed the process, so larger batches run
+    # eagerly.
     graph_max_batch = 64
 
     def conditional_sample(self, global_cond, use_graph=True, x0=None, noise=None):

@@ -47,5 +47,15 @@ log("state")
 pcb = pc[:, None].repeat(1, ro.n_obs_steps, 1, 1)
 out = ro.policy.predict_action(state, pcb, use_graph=False)
 log(f"predict eager {tuple(out.shape)}")
+ro.policy.graph_max_batch = 1 << 20  # capture at this batch too
 out = ro.policy.predict_action(state, pcb, use_graph=True)
 log(f"predict graph {tuple(out.shape)}")
+for mode in (False, True):
+    torch.cuda.synchronize()
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(5):
+        ro.policy.predict_action(state, pcb, use_graph=mode)
+    e1.record()
+    torch.cuda.synchronize()
+    log(f"predict use_graph={mode}: {e0.elapsed_time(e1) / 5:.2f} ms")
