@@ -1605,6 +1605,7 @@ __device__ void sensors(Env& e, int ncon, int tid, double* cacc, double* cfrc, d
 struct SolverShared {
   double Lcol[MAX_NB][16];  // Cholesky: current block column, by block row
   double Ldiag[16];         // Cholesky: factor of the current diagonal block
+  double Ldinv[4];          // Cholesky: reciprocals of its diagonal
   double a0[MAX_NVP];    // qacc_smooth
   double a[MAX_NVP];     // current qacc
   double res[MAX_NVP];   // a - a0
@@ -1650,32 +1651,35 @@ __device__ __forceinline__ int block_sum_i(int v, SolverShared& S, int tid) {
 }
 
 // 4x4 in-place lower Cholesky (row-major)
-__device__ __forceinline__ void potrf4(double* a) {
+// 4x4 Cholesky in place (lower); inv[j] = 1 / L_jj.  1/sqrt comes from v_rsq_f64 refined by
+// two Newton steps (a shorter dependent chain than sqrt followed by a division, on the
+// factorisation's critical path)
+__device__ __forceinline__ void potrf4(double* a, double* inv) {
 #pragma unroll
   for (int j = 0; j < 4; j++) {
     double s = a[4 * j + j];
 #pragma unroll
     for (int k = 0; k < j; k++) s -= a[4 * j + k] * a[4 * j + k];
-    const double d = sqrt(s > RMBX_MINVAL ? s : RMBX_MINVAL);
-    a[4 * j + j] = d;
-    const double inv = 1.0 / d;
+    const double sc = s > RMBX_MINVAL ? s : RMBX_MINVAL;
+    double y = __builtin_amdgcn_rsq(sc);
+    const double hs = 0.5 * sc;
+    y = y * fma(-hs * y, y, 1.5);
+    y = y * fma(-hs * y, y, 1.5);
+    a[4 * j + j] = sc * y;
+    inv[j] = y;
 #pragma unroll
     for (int i = j + 1; i < 4; i++) {
       double t = a[4 * i + j];
 #pragma unroll
       for (int k = 0; k < j; k++) t -= a[4 * i + k] * a[4 * j + k];
-      a[4 * i + j] = t * inv;
+      a[4 * i + j] = t * y;
     }
 #pragma unroll
     for (int k = j + 1; k < 4; k++) a[4 * j + k] = 0;
   }
 }
-// a := a * L^-T  (L lower 4x4); the four independent reciprocals of the diagonal replace the
-// sixteen dependent divisions on the step's critical path
-__device__ __forceinline__ void trsm4(double* a, const double* L) {
-  double inv[4];
-#pragma unroll
-  for (int c = 0; c < 4; c++) inv[c] = 1.0 / L[4 * c + c];
+// a := a * L^-T  (L lower 4x4, inv = 1 / diag(L) from potrf4)
+__device__ __forceinline__ void trsm4(double* a, const double* L, const double* inv) {
 #pragma unroll
   for (int r = 0; r < 4; r++) {
 #pragma unroll
@@ -1693,14 +1697,17 @@ __device__ __forceinline__ void trsm4(double* a, const double* L) {
 // that block is its own), so a step costs two barriers and the potrf overlaps the other updates.
 __device__ void blk_cholesky(double* a, int bi, int bj, bool own, int NB, SolverShared& S) {
   if (own && bi == 0 && bj == 0) {
-    potrf4(a);
+    double inv[4];
+    potrf4(a, inv);
 #pragma unroll
     for (int q = 0; q < 16; q++) S.Ldiag[q] = a[q];
+#pragma unroll
+    for (int q = 0; q < 4; q++) S.Ldinv[q] = inv[q];
   }
   for (int k = 0; k < NB; k++) {
     __syncthreads();
     if (own && bj == k && bi > k) {
-      trsm4(a, S.Ldiag);
+      trsm4(a, S.Ldiag, S.Ldinv);
 #pragma unroll
       for (int q = 0; q < 16; q++) S.Lcol[bi][q] = a[q];
     }
@@ -1718,9 +1725,12 @@ __device__ void blk_cholesky(double* a, int bi, int bj, bool own, int NB, Solver
           a[4 * p + q] = t;
         }
       if (bi == k + 1 && bj == k + 1) {
-        potrf4(a);
+        double inv[4];
+        potrf4(a, inv);
 #pragma unroll
         for (int q = 0; q < 16; q++) S.Ldiag[q] = a[q];  // read after the next barrier
+#pragma unroll
+        for (int q = 0; q < 4; q++) S.Ldinv[q] = inv[q];
       }
     }
   }
