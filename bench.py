@@ -1,24 +1,35 @@
 """Headline benchmark: env-steps/s of the batched MujocoUR5eCable + ACT rollout hot path.
 
-`python bench.py --gpus N --steps K --warmup W` (N > 1 under torch.distributed.run, one rank
-per GPU, envs sharded per rank, results all-gathered over RCCL at the end).
+`python bench.py --gpus N --steps K --warmup W`.  Under torch.distributed.run (WORLD_SIZE set)
+each process is one rank on one GPU; with --gpus N > 1 and no WORLD_SIZE, bench.py spawns the N
+ranks itself (before any GPU call).  Envs are sharded per rank by global env index; results are
+all-gathered over RCCL at the end.
 
-Workload (BASELINE.json configs[1] at N = 1): 1024 MujocoUR5eCable envs per GPU, ACT policy
-(ResNet-18 + 4/7-layer transformer, random init, bf16), synthetic episodes (world_idx = env % 6,
+Workload (BASELINE.json configs[1] at N = 1): 1024 MujocoUR5eCable envs per GPU (weak scaling;
+--total_envs T fixes the whole-job count instead, e.g. configs[2]: --total_envs 4096 on 8 GPUs),
+ACT policy (ResNet-18 + 4/7-layer transformer, random init) in **fp32, the reference's
+precision** (the credited `value`), synthetic episodes (world_idx = global env % 6,
 world_random_scale [0.01, 0.01, 0], seed 0).  Every env is first driven through the scripted
-pre-rollout phases (Initial 1.0 s, Reach 0.7 + 0.3 s, Grasp 0.5 s; untimed), then W warm-up
-and K timed env-steps of the RolloutPhase hot loop: render + ACT every `skip` = 3 steps,
-temporal ensemble, command routing, 8 physics substeps, observation, success predicate and
-phase bookkeeping, all on the device.  One `step` = one env-step of every env.
+pre-rollout phases (Initial 1.0 s, Reach 0.7 + 0.3 s, Grasp 0.5 s; untimed), then W warm-up and
+K timed env-steps of the RolloutPhase hot loop: render + ACT every `skip` = 3 steps, temporal
+ensemble, command routing, 8 physics substeps, observation, success predicate and phase
+bookkeeping, all on the device.  One `step` = one env-step of every env.  The ACT decoder runs
+layer 0 only: the DETRVAE output reads that layer's normed intermediate, layers 1..6 are dead
+(exact; tests/test_act_full_gpu.py; --act_full_decoder runs all seven).
 
-Prints ONE JSON line (rank 0) with the roofline of the dominant kernel (the fused physics
-kernel: algorithmic bytes per env-step / measured kernel time) and the CPU baseline (oracle
-physics + ACT in PyTorch-CPU on a bounded sample).
+The same workload with the policy in bf16 (throughput mode) is reported as `secondary_bf16`
+with its measured action error against fp32 on the same inputs; it is never `value`.
+
+Prints ONE JSON line (rank 0) with the roofline of the physics kernels (algorithmic bytes per
+env-step / HIP-event kernel time), FP64 and policy-MFMA fractions, and the CPU
+baseline (the oracle's C physics + ACT in PyTorch-CPU: a throughput leg of single-threaded
+1-env processes, a 1-env latency leg and the C1 MLP leg, on bounded samples).
 """
 
 import argparse
 import json
 import os
+import subprocess
 import sys
 import time
 
@@ -34,8 +45,9 @@ sys.path.insert(0, ROOT)
 
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (spec)
-BF16_PEAK_TFLOPS = 2500.0  # MI355X_MICROARCH.md: BF16 MFMA dense (spec)
+MFMA_PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2500.0}  # MI355X_MICROARCH.md: F32 / BF16 MFMA dense
 GOLDEN = os.path.join(ROOT, "tests", "golden")
+CPU_WORKERS_MAX = 16  # the GPU box's CPU share per GPU
 
 
 def physics_flops_per_substep(ncon, nefc, iters):
@@ -60,24 +72,31 @@ def pmc_traffic_per_env_step():
         return json.load(f)["bytes_per_env_step_per_env"], os.path.relpath(files[-1], ROOT)
 
 
-def policy_flops_per_inference():
+def policy_flops_per_inference(full_decoder):
     """FLOPs of one ACT inference per env (tools/count_policy_flops.py, FlopCounterMode)."""
     with open(os.path.join(GOLDEN, "policy_flops.json")) as f:
-        return json.load(f)["act_480x640"]["flops_per_inference"]
+        return json.load(f)["act_480x640" if full_decoder else "act_480x640_dec0"]["flops_per_inference"]
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=30)
     p.add_argument("--warmup", type=int, default=6)
-    p.add_argument("--num_envs", type=int, default=1024, help="environments per GPU")
-    p.add_argument("--precision", choices=["bf16", "fp32"], default="bf16")
+    p.add_argument("--num_envs", type=int, default=1024, help="environments per GPU (weak scaling)")
+    p.add_argument("--total_envs", type=int, default=None,
+                   help="whole-job environment count, sharded over the GPUs (strong scaling)")
+    p.add_argument("--precision", choices=["fp32", "bf16"], default="fp32", help="policy precision of `value`")
+    p.add_argument("--no_bf16_secondary", action="store_true")
     p.add_argument("--no_cpu_baseline", action="store_true")
-    p.add_argument("--cpu_sample_steps", type=int, default=600,
-                   help="timed env-steps of the CPU baseline sample (about 10 s of host work)")
-    p.add_argument("--act_prune_dead_decoder", action="store_true")
-    return p.parse_args()
+    p.add_argument("--act_full_decoder", action="store_true", help="also run the dead decoder layers 1..6")
+    p.add_argument("--cpu_steps", type=int, default=60, help="timed env-steps per CPU throughput worker")
+    p.add_argument("--cpu_latency_steps", type=int, default=150, help="timed env-steps of the 1-env latency leg")
+    p.add_argument("--cpu_mlp_steps", type=int, default=150, help="timed env-steps of the C1 MLP leg")
+    p.add_argument("--_cpu_worker", choices=["act", "mlp"], default=None, help=argparse.SUPPRESS)
+    p.add_argument("--_threads", type=int, default=1, help=argparse.SUPPRESS)
+    p.add_argument("--_sync", action="store_true", help=argparse.SUPPRESS)
+    return p.parse_args(argv)
 
 
 def algorithmic_bytes_per_env_step(nq, nv, nu, nsub):
@@ -87,16 +106,29 @@ def algorithmic_bytes_per_env_step(nq, nv, nu, nsub):
     return (nq + 2 * nv + nu + 1) * 8 + (nq + 2 * nv + 1) * 8 + 160 + 5
 
 
-def cpu_baseline(sample_steps, skip=3):
-    """Reference-path CPU baseline: the oracle's serial C physics (1 thread) + ACT in
-    PyTorch-CPU (batch 1, all host threads) + numpy temporal ensemble, on `sample_steps`
-    env-steps of one env (an inference every `skip` steps).  Rendering is not included (no
-    CPU OpenGL renderer in this image)."""
-    from oracle.dyn import OracleEnv
+# --------------------------------------------------------------------------------------------
+# CPU baseline (the reference's CPU path, restated: oracle C physics + PyTorch-CPU policy)
+# --------------------------------------------------------------------------------------------
+def cpu_model_name():
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+def _cpu_worker(kind, steps, threads, sync, skip=3, warm=3):
+    """One env of the reference loop on the CPU: C oracle physics (8 substeps per env-step),
+    policy in PyTorch-CPU fp32 batch 1 every `skip` steps (ACT + numpy temporal ensemble, or the
+    C1 MLP), `threads` intra-op threads.  Prints one JSON line {steps, seconds}."""
+    torch.set_num_threads(threads)
     from oracle import glue
+    from oracle.dyn import OracleEnv
     from robomanipbaselines_amd import model as MD
     from robomanipbaselines_amd.envs.ur5e_cable import CABLE_INIT_QPOS
-    from robomanipbaselines_amd.policy.act.act_model import ActModel
 
     arrays = MD.load("ur5e_cable")
     env = OracleEnv(arrays)
@@ -105,32 +137,189 @@ def cpu_baseline(sample_steps, skip=3):
     ctrl = np.concatenate([CABLE_INIT_QPOS[:6], [0.0]])
     env.set_state(0.0, qpos, np.zeros(env.nv), np.zeros(env.nv), ctrl)
     torch.manual_seed(0)
-    threads = torch.get_num_threads()
-    pol = ActModel().eval().requires_grad_(False)
     stats = {"norm_config": {"type": "gaussian"}, "mean": ctrl.copy(), "std": np.full(7, 0.1)}
-    ens = glue.ActEnsembleOracle(100, stats)
     img = torch.rand(1, 1, 3, 480, 640)
-    warm = 3  # untimed: first-call allocations of PyTorch-CPU
+    if kind == "act":
+        from robomanipbaselines_amd.policy.act.act_model import ActModel
+
+        pol = ActModel().eval().requires_grad_(False)
+        ens = glue.ActEnsembleOracle(100, stats)
+
+        def act(state):
+            chunk = pol(state, img)[0].numpy()
+            return ens.step(lambda: chunk)
+    else:
+        from robomanipbaselines_amd.policy.mlp.mlp_model import MlpModel
+
+        pol = MlpModel(7, 7, 1).eval().requires_grad_(False)
+
+        def act(state):
+            return glue.denormalize(pol(state[:, None], img[:, :, None])[0, 0].numpy().astype(np.float64), stats)
+
     t0 = time.time()
-    for s in range(-warm, sample_steps):
+    for s in range(-warm, steps):
         if s == 0:
+            if sync:  # start together with the other workers
+                print("ready", flush=True)
+                sys.stdin.readline()
             t0 = time.time()
         if s % skip == 0:
-            state = torch.tensor(((qpos[:7] - ctrl) / 0.1)[None], dtype=torch.float32)
+            _, qp, _, _ = env.state()
+            state = torch.tensor(((qp[:7] - ctrl) / 0.1)[None], dtype=torch.float32)
             with torch.no_grad():
-                chunk = pol(state, img)[0].numpy()
-            act = ens.step(lambda: chunk)
-            env.set_ctrl(np.clip(act, -6.28, 255))
+                a = act(state)
+            env.set_ctrl(np.clip(a, -6.28, 255))
         env.step(8)
-    dt = time.time() - t0
-    return {"value": sample_steps / dt, "unit": "env-steps/s", "cores": int(threads), "kind": "port",
-            "sample": f"{sample_steps} env-steps of 1 env (after {warm} untimed): C oracle physics (1 thread) + ACT "
-                      f"fp32 PyTorch-CPU batch 1 every {skip} steps ({threads} threads) + numpy ensemble; "
-                      f"rendering excluded", "seconds": round(dt, 2)}
+    print(json.dumps({"steps": steps, "seconds": time.time() - t0}), flush=True)
 
 
-def main():
-    args = parse()
+def _spawn_workers(kind, count, steps, threads):
+    env = dict(os.environ, OMP_NUM_THREADS=str(threads), HIP_VISIBLE_DEVICES="", CUDA_VISIBLE_DEVICES="")
+    cmd = [sys.executable, os.path.abspath(__file__), "--_cpu_worker", kind, "--cpu_steps", str(steps),
+           "--_threads", str(threads)] + (["--_sync"] if count > 1 else [])
+    procs = [subprocess.Popen(cmd, stdin=subprocess.PIPE, stdout=subprocess.PIPE, text=True, env=env)
+             for _ in range(count)]
+    if count > 1:
+        for p in procs:
+            assert p.stdout.readline().strip() == "ready"
+        for p in procs:
+            p.stdin.write("go\n")
+            p.stdin.flush()
+    outs = []
+    for p in procs:
+        out, _ = p.communicate(timeout=600)
+        if p.returncode != 0:
+            raise RuntimeError(f"cpu worker exited with {p.returncode}")
+        outs.append(json.loads(out.strip().splitlines()[-1]))
+    return outs
+
+
+def cpu_baseline(args, skip=3):
+    """SURVEY §8(d) CPU baseline on the box's host cores (bounded samples, about 30 s in all):
+    throughput = P single-threaded processes with 1 env each started together (P = the CPU share,
+    at most 16), latency = 1 env with P threads, C1 = 1 env with the MLP policy and P threads.
+    Rendering is excluded (the reference renders 3 cameras with MuJoCo's OpenGL renderer; there
+    is no CPU renderer in this image)."""
+    cores = len(os.sched_getaffinity(0))
+    P = max(1, min(cores, CPU_WORKERS_MAX))
+    t0 = time.time()
+    thr = _spawn_workers("act", P, args.cpu_steps, 1)
+    thr_value = P * args.cpu_steps / max(o["seconds"] for o in thr)
+    lat = _spawn_workers("act", 1, args.cpu_latency_steps, P)[0]
+    mlp = _spawn_workers("mlp", 1, args.cpu_mlp_steps, P)[0]
+    return {"value": thr_value, "unit": "env-steps/s", "cores": P, "kind": "port",
+            "cpu_model": cpu_model_name(), "host_cpus_visible": cores,
+            "sample": f"throughput leg: {P} single-threaded processes x 1 env x {args.cpu_steps} env-steps (after 3 "
+                      f"untimed, started together): C oracle physics (8 substeps) + ACT fp32 PyTorch-CPU batch 1 "
+                      f"every {skip} steps + numpy temporal ensemble; rendering excluded",
+            "latency_leg": {"value": lat["steps"] / lat["seconds"], "unit": "env-steps/s", "threads": P,
+                            "sample": f"1 env x {lat['steps']} env-steps, ACT with {P} intra-op threads"},
+            "c1_mlp_leg": {"value": mlp["steps"] / mlp["seconds"], "unit": "env-steps/s", "threads": P,
+                           "sample": f"config C1: 1 env x {mlp['steps']} env-steps, MLP policy (ResNet-18 + "
+                                     f"[512, 512]) fp32 every {skip} steps, {P} threads"},
+            "seconds": round(time.time() - t0, 1)}
+
+
+# --------------------------------------------------------------------------------------------
+# GPU rollout
+# --------------------------------------------------------------------------------------------
+def make_rollout(args, dev, precision, n_local, g0):
+    from robomanipbaselines_amd.envs.operation.OperationMujocoUR5eCable import OperationMujocoUR5eCable
+    from robomanipbaselines_amd.policy.act.rollout_act import RolloutAct
+
+    class Rollout(OperationMujocoUR5eCable, RolloutAct):
+        pass
+
+    argv = ["--num_envs", str(n_local), "--device", dev, "--world_idx_list", *[str(i) for i in range(6)],
+            "--world_random_scale", "0.01", "0.01", "0.0", "--seed", "0", "--env_offset", str(g0),
+            "--precision", precision]
+    if not args.act_full_decoder:
+        argv.append("--act_prune_dead_decoder")
+    ro = Rollout(argv=argv)
+    ro.reset()
+    ro._active = None
+    while ro.phase_idx < len(ro.pre_durations):  # scripted pre-rollout phases (untimed)
+        ro.step_once()
+    return ro
+
+
+def timed_run(ro, args, dist):
+    """W warm-up + K timed env-steps; HIP events around every physics launch sequence and every
+    infer_policy call (same stream)."""
+    for _ in range(args.warmup):  # also MIOpen / hipBLASLt algorithm selection
+        ro.step_once()
+    phys_ev, infer_ev = [], []
+    eng = ro.env.engine
+    orig_step, orig_infer = eng.step, ro.infer_policy
+
+    def timed_step(nsub=8, active=None):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        orig_step(nsub, active)
+        e1.record()
+        phys_ev.append((e0, e1))
+
+    def timed_infer():
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        orig_infer()
+        e1.record()
+        infer_ev.append((e0, e1))
+
+    eng.step, ro.infer_policy = timed_step, timed_infer
+    if dist:
+        import torch.distributed as tdist
+
+        tdist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.time()
+    for _ in range(args.steps):
+        ro.step_once()
+    torch.cuda.synchronize()
+    if dist:
+        tdist.barrier()
+    elapsed = time.time() - t0
+    eng.step, ro.infer_policy = orig_step, orig_infer
+    phys = np.array([a.elapsed_time(b) for a, b in phys_ev])
+    infer = np.array([a.elapsed_time(b) for a, b in infer_ev]) / 1e3
+    if dist:
+        import torch.distributed as tdist
+
+        t = torch.tensor([elapsed], dtype=torch.float64, device=ro.device)
+        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
+        elapsed = float(t.item())
+    return elapsed, phys, infer
+
+
+@torch.no_grad()
+def bf16_action_error(ro32, ro16, n=16):
+    """Max |action| difference of the bf16 policy against the fp32 policy (same weights, same
+    rendered frame and state of the first n envs), on the denormalised scale: std_a x |d chunk|,
+    which bounds the ensembled action difference (the ensemble weights sum to 1)."""
+    from robomanipbaselines_amd import kernels as K
+
+    n = min(n, ro32.n)
+    state = ro32.get_state()[:n]
+    img32 = ro32.get_images(torch.float32)[:n]
+    c32 = ro32.policy(state, img32).float()
+    s2d = K.image_to_s2d(img32[:, 0].to(torch.bfloat16))[:, None]
+    c16 = ro16.policy(state.to(torch.bfloat16), s2d).float()
+    std = torch.tensor(ro32.model_meta_info["action"]["std"], dtype=torch.float32, device=c32.device)
+    return float(((c16 - c32).abs() * std).max().item()), float(((c16 - c32).norm() / c32.norm()).item())
+
+
+def job_shard(args, rank, world):
+    """(strong scaling?, whole-job env count, global index of this rank's first env, its env count):
+    weak scaling keeps --num_envs per GPU, --total_envs shards a fixed job over the ranks."""
+    from robomanipbaselines_amd.distributed import shard_range
+
+    strong = args.total_envs is not None
+    total = args.total_envs if strong else args.num_envs * world
+    g0, g1 = shard_range(rank, world, total)
+    return strong, total, g0, g1 - g0
+
+
+def rank_main(args):
     rank = int(os.environ.get("RANK", 0))
     world = int(os.environ.get("WORLD_SIZE", 1))
     local_rank = int(os.environ.get("LOCAL_RANK", 0))
@@ -141,94 +330,29 @@ def main():
         torch.cuda.set_device(local_rank)
         tdist.init_process_group("nccl", device_id=torch.device(f"cuda:{local_rank}"))
     dev = f"cuda:{local_rank}"
-    from robomanipbaselines_amd.bin.Rollout import main as rollout_main  # noqa: F401
-    from robomanipbaselines_amd.envs.operation.OperationMujocoUR5eCable import OperationMujocoUR5eCable
-    from robomanipbaselines_amd.policy.act.rollout_act import RolloutAct
     from robomanipbaselines_amd import kernels as K
+    from robomanipbaselines_amd.distributed import gather_results, pack_results
 
-    class Rollout(OperationMujocoUR5eCable, RolloutAct):
-        pass
+    strong, total, g0, n = job_shard(args, rank, world)
 
-    n = args.num_envs
-    argv = ["--num_envs", str(n), "--device", dev, "--world_idx_list", *[str(i) for i in range(6)],
-            "--world_random_scale", "0.01", "0.01", "0.0", "--seed", str(rank), "--precision", args.precision]
-    if args.act_prune_dead_decoder:
-        argv.append("--act_prune_dead_decoder")
-    from robomanipbaselines_amd.distributed import gather_results, pack_results, shard_range
-
-    ro = Rollout(argv=argv)
-    # per-env world index from the GLOBAL env index so results do not depend on the GPU count
-    g0, g1 = shard_range(rank, world, n * world)
-    ro.args.world_idx_list = [g % 6 for g in range(g0, g1)]
-    ro.reset()
-    ro._active = None
-    n_pre = len(ro.pre_durations)
-    # scripted pre-rollout phases (untimed)
-    while ro.phase_idx < n_pre:
-        ro.step_once()
-    # warm-up (also MIOpen/hipBLASLt algorithm selection)
-    for _ in range(args.warmup):
-        ro.step_once()
-
-    # kernel timing: HIP events around every physics launch (same stream)
-    phys_ms = []
-    eng = ro.env.engine
-    orig_step = eng.step
-
-    def timed_step(nsub=8, active=None):
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record()
-        orig_step(nsub, active)
-        e1.record()
-        phys_ms.append((e0, e1))
-
-    eng.step = timed_step
-    infer_ev = []
-    orig_infer = ro.infer_policy
-
-    def timed_infer():
-        e0 = torch.cuda.Event(enable_timing=True)
-        e1 = torch.cuda.Event(enable_timing=True)
-        e0.record()
-        orig_infer()
-        e1.record()
-        infer_ev.append((e0, e1))
-
-    ro.infer_policy = timed_infer
+    ro = make_rollout(args, dev, args.precision, n, g0)
+    elapsed, phys, infer = timed_run(ro, args, dist)
+    value = total * args.steps / elapsed
     if dist:
-        tdist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.time()
-    for _ in range(args.steps):
-        ro.step_once()
-    torch.cuda.synchronize()
-    if dist:
-        tdist.barrier()
-    elapsed = time.time() - t0
-    eng.step = orig_step
-    ro.infer_policy = orig_infer
-    phys = np.array([a.elapsed_time(b) for a, b in phys_ms])
-    infer = np.array([a.elapsed_time(b) for a, b in infer_ev]) / 1e3  # seconds (GPU time)
-    if dist:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
-        elapsed = float(t.item())
         # RCCL all-gather of per-env episode records (success, reward, duration, steps)
         v = K.sched_view(ro.sched)
         gathered = gather_results(pack_results(v["success"], v["result_reward"], v["duration"], v["rollout_time_idx"]), dev)
-        assert gathered.shape[0] == n * world
-    total_envs = n * world
-    value = total_envs * args.steps / elapsed
+        assert gathered.shape[0] == total
+    eng = ro.env.engine
     st = eng.stats.cpu().numpy()
-    nq, nv, nu = eng.nq, eng.nv, eng.nu
-    bytes_env_step = algorithmic_bytes_per_env_step(nq, nv, nu, 8)
+    bytes_env_step = algorithmic_bytes_per_env_step(eng.nq, eng.nv, eng.nu, 8)
     kern_s = float(phys.mean()) / 1e3
     achieved = n * bytes_env_step / kern_s / 1e9
     ncon, nefc, iters = float(st[:, 0].mean()), float(st[:, 1].mean()), float(st[:, 2].mean())
     fl_sub = physics_flops_per_substep(ncon, nefc, iters)
     fp64_tf = n * 8 * fl_sub / kern_s / 1e12
     traffic_env, traffic_src = pmc_traffic_per_env_step()
+    pol_flops = policy_flops_per_inference(args.act_full_decoder)
     result = {
         "metric": "env-steps/s (whole node) + policy-inference us/step, MujocoUR5eCable x N ACT",
         "value": round(value, 1),
@@ -238,13 +362,15 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(1e3 * elapsed / args.steps, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": f"f64 physics + {args.precision} policy",
         "data": "synthetic (random-init ACT weights, seeded worlds)",
-        "config": {"workload": f"MujocoUR5eCable x{n} per GPU, ACT (ResNet-18 + transformer, chunk 100, skip 3, "
-                               f"temporal ensembling), RolloutPhase hot loop", "num_envs_per_gpu": n,
-                   "total_envs": total_envs, "parallelism": f"env-sharded x{world}, RCCL all-gather of results"},
+        "config": {"workload": f"MujocoUR5eCable x{total} ({n} per GPU), ACT (ResNet-18 + transformer 4/7 layers, "
+                               f"chunk 100, skip 3, temporal ensembling), {args.precision} policy, RolloutPhase hot loop",
+                   "num_envs_per_gpu": n, "total_envs": total,
+                   "parallelism": f"env-sharded x{world}, RCCL all-gather of results",
+                   "act_decoder_layers_run": 7 if args.act_full_decoder else 1},
         "policy_inference_us_per_call": round(1e6 * float(infer.mean()), 1) if len(infer) else None,
         "policy_inference_us_per_env_step": round(1e6 * float(infer.mean()) / (n * ro.args.skip), 3) if len(infer) else None,
         "physics_kernel_ms": round(float(phys.mean()), 3),
@@ -263,21 +389,67 @@ def main():
         "contacts_mean": ncon, "constraint_rows_mean": nefc, "newton_iters_mean": iters,
     }
     if len(infer):
-        pol_tf = n * policy_flops_per_inference() / float(infer.mean()) / 1e12
+        pol_tf = n * pol_flops / float(infer.mean()) / 1e12
+        peak = MFMA_PEAK_TFLOPS[args.precision]
         # whole batched infer_policy call (render + preprocessing + ACT), all kernels on the stream
-        result["roofline_policy"] = {"bound": "mfma", "achieved": round(pol_tf, 2), "peak": BF16_PEAK_TFLOPS,
-                                     "unit": "TFLOP/s", "frac": pol_tf / BF16_PEAK_TFLOPS,
-                                     "algorithmic_flops_per_inference": policy_flops_per_inference(),
+        result["roofline_policy"] = {"bound": "mfma", "achieved": round(pol_tf, 2), "peak": peak,
+                                     "unit": "TFLOP/s", "frac": pol_tf / peak, "dtype": args.precision,
+                                     "algorithmic_flops_per_inference": pol_flops,
                                      "scope": "one batched infer_policy call over all envs"}
-    if rank == 0 and not args.no_cpu_baseline:
+    if args.precision == "fp32" and not args.no_bf16_secondary:
+        ro16 = make_rollout(args, dev, "bf16", n, g0)
+        el16, _, inf16 = timed_run(ro16, args, dist)
+        err_abs, err_rel = bf16_action_error(ro, ro16)
+        result["secondary_bf16"] = {
+            "value": round(total * args.steps / el16, 1), "unit": "env-steps/s",
+            "ms_per_step": round(1e3 * el16 / args.steps, 3), "dtype": "f64 physics + bf16 policy",
+            "policy_inference_us_per_call": round(1e6 * float(inf16.mean()), 1) if len(inf16) else None,
+            "max_abs_action_err_vs_fp32": err_abs, "chunk_rel_l2_err_vs_fp32": err_rel,
+            "note": "throughput mode, NOT reference precision: same workload with the ACT policy in bf16; "
+                    "action error measured on the first 16 envs' frame (same weights, same inputs)"}
+        if len(inf16):
+            tf16 = n * pol_flops / float(inf16.mean()) / 1e12
+            result["secondary_bf16"]["roofline_policy"] = {"bound": "mfma", "achieved": round(tf16, 2),
+                                                           "peak": MFMA_PEAK_TFLOPS["bf16"], "unit": "TFLOP/s",
+                                                           "frac": tf16 / MFMA_PEAK_TFLOPS["bf16"]}
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
         try:
-            result["cpu_baseline"] = cpu_baseline(args.cpu_sample_steps)
+            result["cpu_baseline"] = cpu_baseline(args)
         except Exception as exc:  # keep the GPU line even if the oracle is unavailable
             result["cpu_baseline"] = {"error": repr(exc)}
     if rank == 0:
         print(json.dumps(result), flush=True)
     if dist:
+        import torch.distributed as tdist
+
         tdist.destroy_process_group()
+
+
+def _spawned_rank(local_rank, world, port, argv):
+    os.environ.update(RANK=str(local_rank), LOCAL_RANK=str(local_rank), WORLD_SIZE=str(world),
+                      MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    rank_main(parse(argv))
+
+
+def main(argv=None):
+    args = parse(argv)
+    if args._cpu_worker:
+        _cpu_worker(args._cpu_worker, args.cpu_steps, args._threads, args._sync)
+        return
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # launch the N ranks here (nothing has touched the GPU yet in this process)
+        import socket
+
+        import torch.multiprocessing as mp
+
+        s = socket.socket()
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+        s.close()
+        mp.spawn(_spawned_rank, args=(args.gpus, port, sys.argv[1:] if argv is None else argv), nprocs=args.gpus,
+                 join=True)
+        return
+    rank_main(args)
 
 
 if __name__ == "__main__":

@@ -29,19 +29,35 @@ def fk(placement, q):
     return frames
 
 
+TAYLOR3 = np.finfo(np.float64).eps ** 0.25  # Pinocchio's TaylorSeriesExpansion precision<3>()
+
+
 def log3(R):
-    tr = np.clip((np.trace(R) - 1) / 2, -1.0, 1.0)
-    t = np.arccos(tr)
-    if t < 1e-8:
-        return 0.5 * np.array([R[2, 1] - R[1, 2], R[0, 2] - R[2, 0], R[1, 0] - R[0, 1]]), t
-    w = t / (2 * np.sin(t)) * np.array([R[2, 1] - R[1, 2], R[0, 2] - R[2, 0], R[1, 0] - R[0, 1]])
-    return w, t
+    """pin.log3 (spatial/log.hxx [ext]): within 1e-2 of pi the axis comes from the diagonal
+    (the antisymmetric part has lost its digits there), signs from R - R^T; below eps^(1/4) the
+    factor theta / sin(theta) is 1."""
+    tr = np.trace(R)
+    if tr >= 3.0:
+        t = 0.0
+    elif tr <= -1.0:
+        t = np.pi
+    else:
+        t = np.arccos((tr - 1.0) / 2.0)
+    if t >= np.pi - 1e-2:
+        cphi = np.cos(t - np.pi)
+        beta = t * t / (1.0 + cphi)
+        tmp = (np.diag(R) + cphi) * beta
+        sgn = np.array([1.0 if R[2, 1] > R[1, 2] else -1.0, 1.0 if R[0, 2] > R[2, 0] else -1.0,
+                        1.0 if R[1, 0] > R[0, 1] else -1.0])
+        return sgn * np.where(tmp > 0, np.sqrt(np.maximum(tmp, 0.0)), 0.0), t
+    f = (t / np.sin(t) if t > TAYLOR3 else 1.0) / 2.0
+    return f * np.array([R[2, 1] - R[1, 2], R[0, 2] - R[2, 0], R[1, 0] - R[0, 1]]), t
 
 
 def log6(R, p):
     w, t = log3(R)
-    if t < 1e-8:
-        alpha, beta = 1 - t * t / 12, 1.0 / 12
+    if t < TAYLOR3:
+        alpha, beta = 1 - t * t / 12 - t ** 4 / 720, 1.0 / 12 + t * t / 720
     else:
         st, ct = np.sin(t), np.cos(t)
         alpha = t * st / (2 * (1 - ct))
@@ -51,7 +67,7 @@ def log6(R, p):
 
 
 def jlog3(t, w):
-    if t < 1e-8:
+    if t < TAYLOR3:
         return np.eye(3) + 0.5 * skew(w)
     st, ct = np.sin(t), np.cos(t)
     st1mct = st / (1 - ct)
@@ -61,7 +77,7 @@ def jlog3(t, w):
 def jlog6(R, p):
     w, t = log3(R)
     A = jlog3(t, w)
-    if t < 1e-8:
+    if t < TAYLOR3:
         beta, bdot = 1.0 / 12 + t * t / 720, 1.0 / 360
     else:
         st, ct = np.sin(t), np.cos(t)

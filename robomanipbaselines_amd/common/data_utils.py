@@ -2,7 +2,7 @@
 
 The reference reads `model_meta_info.pkl` next to the checkpoint (RolloutBase.py:289-309) whose
 schema TrainBase writes (common/base/TrainBase.py:190-217, 325-344).  For synthetic benchmarks
-(no trained checkpoint exists offline) `make_meta_info` builds the same schema with gaussian
+(no trained checkpoint exists offline, --checkpoint omitted) `make_meta_info` builds the same schema with gaussian
 statistics mean = initial joint position, std = 0.1.  A meta file next to a
 given checkpoint is read with a restricted unpickler that only reconstructs numpy arrays and
 plain containers (nothing else in the file executes).
@@ -38,9 +38,12 @@ def load_meta_info(path):
 def make_meta_info(op):
     ck = getattr(op.args, "checkpoint", None)
     if ck:
+        # RolloutBase.setup_model_meta_info (:289-293) opens the file unconditionally: a trained
+        # policy without its normalisation statistics / skip / chunk size must not run
         p = os.path.join(os.path.dirname(ck), "model_meta_info.pkl")
-        if os.path.exists(p):
-            return load_meta_info(p)
+        if not os.path.exists(p):
+            raise FileNotFoundError(f"model meta info not found next to the checkpoint: {p}")
+        return load_meta_info(p)
     init = np.concatenate([op.env.init_qpos[:6], [0.0]])
     stats = {"norm_config": {"type": "gaussian"}, "mean": init.copy(), "std": np.full(7, 0.1),
              "min": init - 1.0, "max": init + 1.0, "range": np.full(7, 2.0), "example": init.copy()}

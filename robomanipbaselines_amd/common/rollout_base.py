@@ -59,6 +59,7 @@ class BatchedRolloutBase:
         self.pre_durations = [1.0] + [p.duration for p in self.pre_phases]  # Initial phase: 1.0 s
         self.result = {key: [] for key in ("success", "reward", "duration")}
         self.inference_duration_list = []
+        self._infer_events = []
         self.datetime_now = datetime.datetime.now()
         self._active = None  # optional caller override of the per-env step mask
 
@@ -90,6 +91,12 @@ class BatchedRolloutBase:
         parser.add_argument("--precision", choices=["fp32", "bf16"], default="bf16",
                             help="policy arithmetic: fp32 (parity mode) or bf16 (throughput mode)")
         parser.add_argument("--max_steps", type=int, default=None, help="hard cap on env-steps")
+        parser.add_argument("--num_gpus", type=int, default=1,
+                            help="shard the envs over this many GPUs of the node (bin/Rollout.py launches one "
+                                 "process per GPU; results all-gathered over RCCL)")
+        parser.add_argument("--env_offset", type=int, default=0,
+                            help="global index of local env 0 (this rank's shard start under --num_gpus): world "
+                                 "indices and noise streams follow the global env index")
         if self.require_task_desc:
             parser.add_argument("--task_desc", type=str, required=True)
         self.set_additional_args(parser)
@@ -138,7 +145,19 @@ class BatchedRolloutBase:
         pass
 
     # -- state / images (RolloutBase.get_state :463-477, get_images :479-490) -----------------
+    def _bind_state_stats(self):
+        """The state normalisation statistics as f64 device tensors (read once per episode)."""
+        st, dev = self.model_meta_info["state"], self.device
+        if "mean" in st:
+            self._st_mean = torch.tensor(st["mean"], dtype=torch.float64, device=dev)
+            self._st_std = torch.tensor(st["std"], dtype=torch.float64, device=dev)
+        if "min" in st:
+            self._st_min = torch.tensor(st["min"], dtype=torch.float64, device=dev)
+            self._st_range = torch.tensor(st["range"], dtype=torch.float64, device=dev)
+
     def get_state(self):
+        """normalize_data (DataUtils.py:9-24) of the measured joint positions in f64 (same
+        operations and order as numpy), then the f32 cast of RolloutBase.get_state (:475)."""
         jp = self.obs["joint_pos"]
         st = self.model_meta_info["state"]
         if st.get("norm_config", {}).get("type", "gaussian") == "gaussian":
@@ -204,18 +223,13 @@ class BatchedRolloutBase:
     # -- episode --------------------------------------------------------------------------------
     def reset(self):
         self._reset_motion()
-        world = np.array([self.args.world_idx_list[e % len(self.args.world_idx_list)] for e in range(self.n)])
+        g0, wl = self.args.env_offset, self.args.world_idx_list
+        world = np.array([wl[(g0 + e) % len(wl)] for e in range(self.n)])
         self.env.world_random_scale = self.args.world_random_scale
         self.world_idx = self.env.modify_world(world_idx=world)
         self.obs, self.info = self.env.reset(seed=self.args.seed)
-        st = self.model_meta_info["state"]
+        self._bind_state_stats()
         dev = self.device
-        if "mean" in st:
-            self._st_mean = torch.tensor(st["mean"], dtype=torch.float64, device=dev)
-            self._st_std = torch.tensor(st["std"], dtype=torch.float64, device=dev)
-        if "min" in st:
-            self._st_min = torch.tensor(st["min"], dtype=torch.float64, device=dev)
-            self._st_range = torch.tensor(st["range"], dtype=torch.float64, device=dev)
         self.sched = K.sched_alloc(self.n, dev)
         K.sched_reset(self.sched, self.env.get_time())
         # device-side step mask: an env stops stepping at its RolloutPhase -> EndRolloutPhase
@@ -245,10 +259,29 @@ class BatchedRolloutBase:
                 self.grip_cmd.fill_(g)
         elif self.phase_idx == n_pre:
             if self.rollout_time_idx % self.args.skip == 0:
-                t0 = time.time()
-                self.infer_policy()
-                self.inference_duration_list.append(time.time() - t0)
+                self._timed_infer()
             self.set_command_data()
+
+    def _timed_infer(self):
+        """infer_policy timed like the reference's figure (RolloutAct.py:74-76 includes the .cpu()
+        sync): device events around the call on the current stream, read in finish() so the
+        loop never waits on the device; wall clock on a CPU device."""
+        if self.device.type == "cuda":
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            self.infer_policy()
+            e1.record()
+            self._infer_events.append((e0, e1))
+        else:
+            t0 = time.time()
+            self.infer_policy()
+            self.inference_duration_list.append(time.time() - t0)
+
+    def _collect_inference_durations(self):
+        if self._infer_events:
+            self._infer_events[-1][1].synchronize()
+            self.inference_duration_list.extend(a.elapsed_time(b) / 1e3 for a, b in self._infer_events)
+            self._infer_events = []
 
     def _host_transition(self):
         """Host mirror of the pre-rollout phase clock (PhaseBase.get_elapsed_duration)."""
@@ -290,21 +323,44 @@ class BatchedRolloutBase:
         self.finish()
         return steps
 
+    def _dist_world(self):
+        """(rank, world) of the torch.distributed group this rollout is a shard of (bin/Rollout.py
+        --num_gpus), else (0, 1)."""
+        import torch.distributed as dist
+
+        if dist.is_available() and dist.is_initialized():
+            return dist.get_rank(), dist.get_world_size()
+        return 0, 1
+
     def finish(self):
+        """RolloutPhase / EndRolloutPhase result bookkeeping (RolloutBase.py:96-110, 417-422) for
+        every env.  Under --num_gpus the per-env records of all shards are all-gathered (one RCCL
+        all_gather, distributed.py) and rank 0 prints and writes them in global env order."""
         v = K.sched_view(self.sched)
-        for e in range(self.n):
-            succ = bool(v["success"][e])
-            print(f"Rollout result: {'success' if succ else 'failure'}", flush=True)
-            self.result["success"].append(succ)
-            self.result["reward"].append(float(v["result_reward"][e]))
-            self.result["duration"].append(float(v["duration"][e]))
+        succ, rew, dur = v["success"].astype(bool), v["result_reward"].astype(np.float64), v["duration"]
+        rank, world = self._dist_world()
+        if world > 1:
+            import torch.distributed as dist
+
+            from ..distributed import gather_results, pack_results
+
+            dev = self.device if dist.get_backend() == "nccl" else "cpu"
+            g = gather_results(pack_results(succ, rew, dur, v["rollout_time_idx"]), dev)
+            succ, rew, dur = g[:, 0] != 0, g[:, 1], g[:, 2]
+        if rank == 0:
+            for e in range(len(succ)):
+                print(f"Rollout result: {'success' if succ[e] else 'failure'}", flush=True)
+                self.result["success"].append(bool(succ[e]))
+                self.result["reward"].append(float(rew[e]))
+                self.result["duration"].append(float(dur[e]))
         if self.args.save_last_image:
             self.save_rgb_images(v)
-        if self.args.result_filename is not None:
+        if rank == 0 and self.args.result_filename is not None:
             print(f"[{self.__class__.__name__}] Save the rollout results: {self.args.result_filename}")
             with open(self.args.result_filename, "w") as f:
                 yaml.dump(self.result, f)
-        self.print_statistics()
+        if rank == 0:
+            self.print_statistics()
 
     def save_rgb_images(self, v=None):
         """RolloutBase.save_rgb_image (:541-561) for every env: the last frame of all cameras side
@@ -329,11 +385,12 @@ class BatchedRolloutBase:
             path = os.path.abspath(os.path.join(
                 self.args.output_image_dir,
                 f"Rollout{self.policy_name}_{demo_name}_world{int(self.world_idx[e]):0>1}_{success_str}_"
-                f"{self.datetime_now:%Y%m%d_%H%M%S}_env{e}.png"))
+                f"{self.datetime_now:%Y%m%d_%H%M%S}_env{self.args.env_offset + e}.png"))
             print(f"[{self.__class__.__name__}] Save the observation image of the last frame: {path}")
             write_png(path, image[e])
 
     def print_statistics(self):
+        self._collect_inference_durations()
         print(f"[{self.__class__.__name__}] Statistics on policy inference")
         if self.inference_duration_list:
             a = np.array(self.inference_duration_list)

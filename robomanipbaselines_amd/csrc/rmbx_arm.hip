@@ -48,20 +48,42 @@ __device__ void skew3(const double* v, double* S) {
   S[8] = 0;
 }
 
+// Pinocchio's log3 (spatial/log.hxx [ext], restated): theta from the clamped trace; within 1e-2
+// of pi the axis comes from the diagonal (sqrt((R_ii + cos(theta - pi)) * theta^2 / (1 +
+// cos(theta - pi))), sign from the antisymmetric part), where theta / (2 sin theta) * (R - R^T)
+// loses its digits; below the Taylor threshold eps^(1/4) the factor is 1/2.
+constexpr double kPi = 3.14159265358979323846;
+constexpr double kTaylor3 = 1.2207031250000000e-04;  // DBL_EPSILON^(1/4) = 2^-13
+
 __device__ double log3(const double* R, double* w) {
-  double tr = (R[0] + R[4] + R[8] - 1) * 0.5;
-  tr = tr > 1 ? 1 : (tr < -1 ? -1 : tr);
-  const double t = acos(tr);
-  const double v[3] = {R[7] - R[5], R[2] - R[6], R[3] - R[1]};
-  const double f = t < 1e-8 ? 0.5 : t / (2 * sin(t));
-  for (int i = 0; i < 3; i++) w[i] = f * v[i];
+  const double tr = R[0] + R[4] + R[8];
+  double t;
+  if (tr >= 3.0)
+    t = 0.0;
+  else if (tr <= -1.0)
+    t = kPi;
+  else
+    t = acos((tr - 1.0) * 0.5);
+  if (t >= kPi - 1e-2) {
+    const double cphi = cos(t - kPi);
+    const double beta = t * t / (1.0 + cphi);
+    const double tmp0 = (R[0] + cphi) * beta, tmp1 = (R[4] + cphi) * beta, tmp2 = (R[8] + cphi) * beta;
+    w[0] = (R[7] > R[5] ? 1.0 : -1.0) * (tmp0 > 0 ? sqrt(tmp0) : 0.0);
+    w[1] = (R[2] > R[6] ? 1.0 : -1.0) * (tmp1 > 0 ? sqrt(tmp1) : 0.0);
+    w[2] = (R[3] > R[1] ? 1.0 : -1.0) * (tmp2 > 0 ? sqrt(tmp2) : 0.0);
+    return t;
+  }
+  const double f = (t > kTaylor3 ? t / sin(t) : 1.0) * 0.5;
+  w[0] = f * (R[7] - R[5]);
+  w[1] = f * (R[2] - R[6]);
+  w[2] = f * (R[3] - R[1]);
   return t;
 }
 
 __device__ void jlog3(double t, const double* w, double* A) {
   double S[9];
   skew3(w, S);
-  if (t < 1e-8) {
+  if (t < kTaylor3) {
     for (int i = 0; i < 9; i++) A[i] = 0.5 * S[i];
     A[0] += 1;
     A[4] += 1;
@@ -82,7 +104,7 @@ __device__ void jlog6(const double* R, const double* p, double* J) {
   const double t = log3(R, w);
   jlog3(t, w, A);
   double beta, bdot;
-  if (t < 1e-8) {
+  if (t < kTaylor3) {
     beta = 1.0 / 12 + t * t / 720;
     bdot = 1.0 / 360;
   } else {
@@ -114,9 +136,9 @@ __device__ void log6(const double* R, const double* p, double* e) {
   double w[3];
   const double t = log3(R, w);
   double alpha, beta;
-  if (t < 1e-8) {
-    alpha = 1 - t * t / 12;
-    beta = 1.0 / 12;
+  if (t < kTaylor3) {
+    alpha = 1 - t * t / 12 - t * t * t * t / 720;
+    beta = 1.0 / 12 + t * t / 720;
   } else {
     const double st = sin(t), ct = cos(t);
     alpha = t * st / (2 * (1 - ct));

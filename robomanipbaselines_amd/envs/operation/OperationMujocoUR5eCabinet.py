@@ -9,7 +9,8 @@ from ..ur5e_cabinet import BatchedMujocoUR5eCabinetEnv
 class OperationMujocoUR5eCabinet:
     def setup_env(self, render_mode=None):
         self.env = BatchedMujocoUR5eCabinetEnv(
-            self.args.num_envs, self.args.device, world_random_scale=self.args.world_random_scale, seed=self.args.seed
+            self.args.num_envs, self.args.device, world_random_scale=self.args.world_random_scale, seed=self.args.seed,
+            env_offset=self.args.env_offset,
         )
 
     def get_pre_motion_phases(self):

@@ -36,7 +36,7 @@ class BatchedMujocoUR5eEnvBase:
     world_offsets = None  # [n_world, 3] offsets of world_body per world index
 
     def __init__(self, num_envs, device="cuda:0", world_random_scale=None, seed=0, image_size=(480, 640),
-                 model_name=None):
+                 model_name=None, env_offset=0):
         model_name = model_name or self.model_name
         self.num_envs = int(num_envs)
         self.device = torch.device(device)
@@ -46,6 +46,9 @@ class BatchedMujocoUR5eEnvBase:
         self.renderer = Renderer(self.arrays, device, width=image_size[1], height=image_size[0])
         self.world_random_scale = world_random_scale
         self.seed = int(seed)
+        # global index of local env 0 (the rank's shard start): noise streams are keyed by the
+        # GLOBAL env index so placements do not depend on the GPU count (distributed.py)
+        self.env_offset = int(env_offset)
         self.rep_env_idx = 0
         inf = self.info
         self._arm_qadr = torch.tensor([inf.qposadr(j) for j in ARM_JOINTS], device=self.device)
@@ -72,7 +75,7 @@ class BatchedMujocoUR5eEnvBase:
     def modify_world(self, world_idx=None, cumulative_idx=None):
         """<Task>Env.modify_world for every env (MujocoUR5eCableEnv.py:107-118,
         MujocoUR5eInsertEnv.py:65-76): the task body's offset per world index plus U(-s, s)^3
-        noise from a per-env Philox stream (seed, env index)."""
+        noise from a per-env Philox stream (seed, global env index)."""
         world_idx, pos = self._world_positions(world_idx, cumulative_idx)
         bp = self.engine.body_pos
         bp[:, self._world_body, :] = torch.tensor(pos, dtype=torch.float64, device=self.device)
@@ -81,7 +84,7 @@ class BatchedMujocoUR5eEnvBase:
 
     def _world_positions(self, world_idx, cumulative_idx):
         """Per-env world index and task-body position: offset per world index plus U(-s, s)^3
-        noise from a per-env Philox stream (seed, env index)."""
+        noise from a per-env Philox stream (seed, global env index = env_offset + local index)."""
         n = self.num_envs
         offsets = np.asarray(self.world_offsets, dtype=np.float64)
         if world_idx is None:
@@ -91,7 +94,7 @@ class BatchedMujocoUR5eEnvBase:
         if self.world_random_scale is not None:
             s = np.asarray(self.world_random_scale, dtype=np.float64)
             for e in range(n):
-                rng = np.random.Generator(np.random.Philox(key=self.seed, counter=[e, 0, 0, 0]))
+                rng = np.random.Generator(np.random.Philox(key=self.seed, counter=[self.env_offset + e, 0, 0, 0]))
                 pos[e] += rng.uniform(low=-1.0 * s, high=s, size=3)
         return world_idx, pos
 

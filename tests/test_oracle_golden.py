@@ -122,3 +122,13 @@ def test_phase_schedule_oracle_bitexact(case):
     assert succ == bool(case["success"][0])
     assert rew == float(case["result_reward"][0])
     assert dur == float(case["duration"][0])  # bit-exact fp64 time accumulation
+
+
+@pytest.mark.parametrize("case", ["gauss", "gauss_noconfig", "limits", "limits01"])
+def test_normalize_oracle_bitexact(case):
+    from test_product_schedule import NORM_CASES
+
+    d = _load("normalize.npz")
+    st = NORM_CASES[case](d)
+    np.testing.assert_array_equal(glue.normalize(d["data"], st), d[f"{case}_norm"])
+    np.testing.assert_array_equal(glue.denormalize(d["data"], st), d[f"{case}_denorm"])

@@ -40,6 +40,14 @@ def main():
         per_op["attention (analytic)"] = attn
         out["act_480x640"] = {"flops_per_inference": total + attn, "per_op": per_op,
                               "config": "ACT (ResNet-18 to layer4, enc 4 / dec 7, d 512, ff 3200, chunk 100), 1 cam 480x640"}
+        # the computation the output depends on: the DETRVAE reads decoder layer 0's normed
+        # intermediate only, so layers 1..6 are dead (prune_dead_decoder; exact, tests/test_act_full_gpu.py)
+        act.prune_dead_decoder = True
+        total, per_op = count(lambda: act(state, img))
+        attn = 4 * (len(act.encoder_layers) * S * S + (Q * Q + Q * S)) * d
+        per_op["attention (analytic)"] = attn
+        out["act_480x640_dec0"] = {"flops_per_inference": total + attn, "per_op": per_op,
+                                   "config": "as act_480x640 with decoder layers 1..6 skipped (outputs unused)"}
     path = os.path.join(ROOT, "tests", "golden", "policy_flops.json")
     with open(path, "w") as f:
         json.dump(out, f, indent=1)
