@@ -48,6 +48,12 @@ FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (spec)
 MFMA_PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2500.0}  # MI355X_MICROARCH.md: F32 / BF16 MFMA dense
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 CPU_WORKERS_MAX = 16  # the GPU box's CPU share per GPU
+_T0 = time.time()
+
+
+def progress(msg):
+    """Progress on stderr (stdout carries only the JSON line)."""
+    print(f"[bench {time.time() - _T0:7.1f}s] {msg}", file=sys.stderr, flush=True)
 
 
 def physics_flops_per_substep(ncon, nefc, iters):
@@ -203,6 +209,7 @@ def cpu_baseline(args, skip=3):
     cores = len(os.sched_getaffinity(0))
     P = max(1, min(cores, CPU_WORKERS_MAX))
     t0 = time.time()
+    progress(f"CPU baseline: {P} workers")
     thr = _spawn_workers("act", P, args.cpu_steps, 1)
     thr_value = P * args.cpu_steps / max(o["seconds"] for o in thr)
     lat = _spawn_workers("act", 1, args.cpu_latency_steps, P)[0]
@@ -238,6 +245,7 @@ def make_rollout(args, dev, precision, n_local, g0):
     ro = Rollout(argv=argv)
     ro.reset()
     ro._active = None
+    progress(f"{precision} rollout of {n_local} envs built; scripted pre-rollout phases")
     while ro.phase_idx < len(ro.pre_durations):  # scripted pre-rollout phases (untimed)
         ro.step_once()
     return ro
@@ -246,8 +254,10 @@ def make_rollout(args, dev, precision, n_local, g0):
 def timed_run(ro, args, dist):
     """W warm-up + K timed env-steps; HIP events around every physics launch sequence and every
     infer_policy call (same stream)."""
-    for _ in range(args.warmup):  # also MIOpen / hipBLASLt algorithm selection
+    for i in range(args.warmup):  # also MIOpen / hipBLASLt algorithm selection
         ro.step_once()
+        torch.cuda.synchronize()
+        progress(f"warm-up step {i + 1}/{args.warmup}")
     phys_ev, infer_ev = [], []
     eng = ro.env.engine
     orig_step, orig_infer = eng.step, ro.infer_policy
@@ -279,6 +289,7 @@ def timed_run(ro, args, dist):
     if dist:
         tdist.barrier()
     elapsed = time.time() - t0
+    progress(f"timed {args.steps} steps: {elapsed:.3f} s")
     eng.step, ro.infer_policy = orig_step, orig_infer
     phys = np.array([a.elapsed_time(b) for a, b in phys_ev])
     infer = np.array([a.elapsed_time(b) for a, b in infer_ev]) / 1e3
@@ -300,10 +311,11 @@ def bf16_action_error(ro32, ro16, n=16):
 
     n = min(n, ro32.n)
     state = ro32.get_state()[:n]
-    img32 = ro32.get_images(torch.float32)[:n]
+    img32 = ro32.get_images(torch.float32)[:n]  # the renderer's f32 space-to-depth frame
     c32 = ro32.policy(state, img32).float()
-    s2d = K.image_to_s2d(img32[:, 0].to(torch.bfloat16))[:, None]
-    c16 = ro16.policy(state.to(torch.bfloat16), s2d).float()
+    if img32.shape[-1] != 16:
+        img32 = K.image_to_s2d(img32[:, 0])[:, None]
+    c16 = ro16.policy(state.to(torch.bfloat16), img32.to(torch.bfloat16)).float()
     std = torch.tensor(ro32.model_meta_info["action"]["std"], dtype=torch.float32, device=c32.device)
     return float(((c16 - c32).abs() * std).max().item()), float(((c16 - c32).norm() / c32.norm()).item())
 
@@ -431,11 +443,25 @@ def _spawned_rank(local_rank, world, port, argv):
     rank_main(parse(argv))
 
 
+def _heartbeat(period=60.0):
+    """A line on stderr every `period` s, so one long first call (MIOpen Find, kernel
+    compilation) is not mistaken for a hang."""
+    import threading
+
+    def beat():
+        while True:
+            time.sleep(period)
+            progress("alive")
+
+    threading.Thread(target=beat, daemon=True).start()
+
+
 def main(argv=None):
     args = parse(argv)
     if args._cpu_worker:
         _cpu_worker(args._cpu_worker, args.cpu_steps, args._threads, args._sync)
         return
+    _heartbeat()
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         # launch the N ranks here (nothing has touched the GPU yet in this process)
         import socket

@@ -241,7 +241,8 @@ int rmbx_arm_fk(const double* placement, const double* q, double* R_out, double*
  * or f32 (dtype 0) = ((u8 / 255) - mean[c]) / std[c] (RolloutBase.py:479-490 + ImageNet
  * normalisation of the ACT/MLP backbones), or (dtype 2) the same values in bf16 as a 2x2
  * space-to-depth image [n][H/2][W/2][16] (channel (dy*2+dx)*3+c, 12..15 zero) for
- * rmbx_stem_s2d_conv (H, W even).
+ * rmbx_stem_s2d_conv (H, W even), or (dtype 3) that space-to-depth image in f32 for
+ * rmbx_stem_s2d_conv_maxpool_f32.
  * ------------------------------------------------------------------------------------------- */
 typedef struct rmbx_camera {
   int32_t body;        /* body the camera is attached to (0 = world) */
@@ -294,6 +295,12 @@ int rmbx_stem_s2d_conv(const void* in, const void* weight, const float* bias, vo
  * of the backbones' resnet18 (third_party/act [absent]; policy/mlp/MlpPolicy.py:34-39). */
 int rmbx_stem_s2d_conv_maxpool(const void* in, const void* weight, const float* bias, void* out, int N,
                                int Hs, int Ws, int band_rows, void* stream);
+/* The same fused stem in f32 (the reference's precision): in [N][Hs][Ws][16] f32 (rmbx_render
+ * policy_dtype 3; channels 12..15 ignored), weight packed [64][4][4][16] f32, bias f32 [64],
+ * out [N][Hp][Wp][64] f32 = maxpool3x3s2p1(relu(conv + bias)); exact f32 products with f32
+ * accumulation (v_mfma_f32_32x32x2_f32).  Replaces the same reference ops as above. */
+int rmbx_stem_s2d_conv_maxpool_f32(const float* in, const float* weight, const float* bias, float* out,
+                                   int N, int Hs, int Ws, int band_rows, void* stream);
 /* Multi-head attention forward, bf16: out[b][i][h*64 + d] = sum_j softmax_j(scale * q_i . k_j) v_j[d]
  * over the heads of q/k/v rows [b][row][h*64 .. h*64+63] (row/batch strides in elements, last dim
  * contiguous), f32 softmax and accumulation, head dim 64, Lk <= 320, no mask; out contiguous

@@ -172,11 +172,12 @@ class BatchedRolloutBase:
 
     def get_images(self, dtype):
         """Render every policy camera straight into the normalised policy tensor [n,ncam,3,H,W]
-        (or, for a bf16 device policy that accepts it, the space-to-depth form
-        [n,ncam,H/2,W/2,16] its stem kernel reads)."""
+        (or, for a device policy that accepts it, the bf16 / f32 space-to-depth form
+        [n,ncam,H/2,W/2,16] its fused stem kernel reads)."""
         H, W = self.env.renderer.height, self.env.renderer.width
         mean, std = self.image_norm
-        s2d = dtype == torch.bfloat16 and getattr(self.policy, "accepts_s2d", False) and H % 2 == 0 and W % 2 == 0
+        s2d = (dtype in (torch.bfloat16, torch.float32) and self.device.type == "cuda"
+               and getattr(self.policy, "accepts_s2d", False) and H % 2 == 0 and W % 2 == 0)
         shape = (H // 2, W // 2, 16) if s2d else (3, H, W)
         if getattr(self, "_img", None) is None or self._img.dtype != dtype or tuple(self._img.shape[2:]) != shape:
             self._img = torch.empty((self.n, len(self.camera_names)) + shape, dtype=dtype, device=self.device)

@@ -256,6 +256,194 @@ __global__ void __launch_bounds__(SP_THREADS) stem_pool_kernel(StemPoolArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// f32 form (the reference's precision): the same fused stem on the renderer's f32 space-to-depth
+// image [N][Hs][Ws][16] (12 channels used) with v_mfma_f32_32x32x2_f32 (exact f32 products,
+// f32 accumulation), output [N][Hp][Wp][64] f32 (channels_last) for the layer-1 convs.
+// K per tap = 12 s2d channels = 6 MFMA k-pairs; the 4 zero pad channels are skipped.
+// LDS: filter bank sW[tap][kpair][h][64 cout] (48 KiB), input ring sR[slot][kpair][rc][2]
+// (5 x 6 x 324 x 8 B = 76 KiB), edges.  One block per (image, band) as in the bf16 kernel.
+// ---------------------------------------------------------------------------------------------
+constexpr int SF_LDS_F32 = 16 * 6 * 2 * 64 + SP_RING * 6 * SP_RC_MAX * 2 + 64 + SP_MAX_WAVES * 2 * 32;
+static_assert(SF_LDS_F32 * 4 <= 160 * 1024, "f32 stem+pool LDS must fit the 160 KiB of a CU");
+
+struct StemPoolF32Args {
+  const float* in;   // [N][Hs][Ws][16]
+  const float* w;    // [64][16 taps][16]
+  const float* bias; // [64]
+  float* out;        // [N][Hp][Wp][64]
+  int N, Hs, Ws, Hp, Wp;
+  int nct, rc, bands, band_rows;
+};
+
+__global__ void __launch_bounds__(SP_THREADS) stem_pool_f32_kernel(StemPoolF32Args a) {
+  __shared__ __attribute__((aligned(16))) float sf_smem[SF_LDS_F32];
+  float* sW = sf_smem;                            // [16 taps][6 kpairs][2 h][64 cout]
+  float* sR = sW + 16 * 6 * 2 * 64;               // [5 slots][6 kpairs][rc][2]
+  float* sBias = sR + SP_RING * 6 * a.rc * 2;     // [64]
+  float* sEdge = sBias + 64;                      // [nct][2 h][32]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nthreads = blockDim.x;
+  const int img = blockIdx.x / a.bands, band = blockIdx.x - img * a.bands;
+  const int py0 = band * a.band_rows;
+  const int py1 = min(a.Hp, py0 + a.band_rows);
+  if (py0 >= py1) return;
+  const int pys = py0 > 0 ? py0 - 1 : 0;
+  const size_t row_elems = (size_t)a.Ws * 16;
+  const float* in_img = a.in + (size_t)img * a.Hs * row_elems;
+
+  // filter bank: global [cout][tap][16] -> sW[tap][kp][h][cout] (channels 0..11)
+  for (int q = tid; q < 64 * 16 * 12; q += nthreads) {
+    const int c = q % 12, rest = q / 12;  // rest = cout * 16 + tap
+    const int co = rest >> 4, tap = rest & 15;
+    sW[((tap * 6 + (c >> 1)) * 2 + (c & 1)) * 64 + co] = a.w[(size_t)rest * 16 + c];
+  }
+  if (tid < 64) sBias[tid] = a.bias[tid];
+
+  // 16-byte chunk q (pixel column c = q / 3 of the ring, channel quad j = q % 3) of s2d row y
+  const int row_chunks = 3 * a.rc;
+  auto load_chunk = [&](int y, int q) -> float4 {
+    const int c = q / 3, j = q - 3 * c;
+    const int x = c - 2;
+    if (y < 0 || y >= a.Hs || x < 0 || x >= a.Ws) return make_float4(0.f, 0.f, 0.f, 0.f);
+    return *reinterpret_cast<const float4*>(in_img + (size_t)y * row_elems + (size_t)x * 16 + 4 * j);
+  };
+  auto store_chunk = [&](int slot, int q, float4 v) {
+    const int c = q / 3, j = q - 3 * c;  // channels 4j..4j+3 = kpairs 2j, 2j+1
+    float* base = sR + (size_t)slot * 6 * a.rc * 2;
+    *reinterpret_cast<float2*>(base + ((size_t)(2 * j) * a.rc + c) * 2) = make_float2(v.x, v.y);
+    *reinterpret_cast<float2*>(base + ((size_t)(2 * j + 1) * a.rc + c) * 2) = make_float2(v.z, v.w);
+  };
+  auto slot_of = [](int y) { return (y + 2 * SP_RING) % SP_RING; };
+  for (int q = tid; q < SP_RING * row_chunks; q += nthreads) {
+    const int r = q / row_chunks, qq = q - r * row_chunks;
+    const int y = 2 * pys - 2 + r;
+    store_chunk(slot_of(y), qq, load_chunk(y, qq));
+  }
+
+  const int n = lane & 31, h = lane >> 5;
+  const int X = 32 * wave + n;
+  const int m = lane & 31;
+  const int sig = 16 * ((m >> 2) & 1) + (m & 3) + 4 * (m >> 3);
+  const bool col_ok = X < a.Ws;
+
+  constexpr int PF_MAX = 4;  // (2 rows * 3 quads * 324 cols) / 640 threads, rounded up
+  float4 pf[PF_MAX];
+  uint32_t pf_ok = 0;
+  const int pf_chunks = 2 * row_chunks;
+  int pf_r[PF_MAX], pf_q[PF_MAX];
+#pragma unroll
+  for (int i = 0; i < PF_MAX; ++i) {
+    const int q = min(tid + nthreads * i, pf_chunks - 1);
+    pf_r[i] = q / row_chunks;
+    pf_q[i] = q - pf_r[i] * row_chunks;
+  }
+
+  float carry[2][16];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) carry[t][k] = 0.f;
+
+  __syncthreads();
+  for (int py = pys; py < py1; ++py) {
+    const int Y0 = 2 * py;
+    const bool more = py + 1 < py1;
+    if (more) {
+      pf_ok = 0;
+#pragma unroll
+      for (int i = 0; i < PF_MAX; ++i) {
+        const int y = Y0 + 3 + pf_r[i];
+        const int c = pf_q[i] / 3, j = pf_q[i] - 3 * c, x = c - 2;
+        const bool ok = tid + nthreads * i < pf_chunks && y < a.Hs && x >= 0 && x < a.Ws;
+        const size_t off = ok ? (size_t)y * row_elems + (size_t)x * 16 + 4 * j : 0;
+        pf[i] = *reinterpret_cast<const float4*>(in_img + off);
+        pf_ok |= (uint32_t)ok << i;
+      }
+    }
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) acc[r][t] = f32x16{};
+    int slot[5];
+#pragma unroll
+    for (int d = 0; d < 5; ++d) slot[d] = slot_of(Y0 - 2 + d);
+#pragma unroll 2
+    for (int tap = 0; tap < 16; ++tap) {
+      const int ky = tap >> 2, kx = tap & 3;
+#pragma unroll
+      for (int kp = 0; kp < 6; ++kp) {
+        float bx[2], aw[2];
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+          bx[r] = sR[(((size_t)slot[r + ky] * 6 + kp) * a.rc + X + kx) * 2 + h];
+#pragma unroll
+        for (int t = 0; t < 2; ++t) aw[t] = sW[((tap * 6 + kp) * 2 + h) * 64 + 32 * t + sig];
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+            acc[r][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(aw[t], bx[r], acc[r][t], 0, 0, 0);
+      }
+    }
+
+    // bias + ReLU, vertical max with the carried row (all values >= 0, so 0 is the pool padding);
+    // the window max overwrites acc[0] in place (register pressure)
+    const bool row1_ok = Y0 + 1 < a.Hs;
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const float b = sBias[32 * t + 16 * h + k];
+        const float p0 = fmaxf(acc[0][t][k] + b, 0.f);
+        const float p1 = row1_ok ? fmaxf(acc[1][t][k] + b, 0.f) : 0.f;
+        acc[0][t][k] = col_ok ? fmaxf(fmaxf(carry[t][k], p0), p1) : 0.f;
+        carry[t][k] = p1;
+      }
+    }
+    if (n == 31) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) sEdge[(wave * 2 + h) * 32 + 16 * t + k] = acc[0][t][k];
+    }
+    __syncthreads();
+
+    if (more) {
+#pragma unroll
+      for (int i = 0; i < PF_MAX; ++i) {
+        if (tid + nthreads * i < pf_chunks) {
+          const float4 v = ((pf_ok >> i) & 1u) ? pf[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+          store_chunk(pf_r[i] ? slot[1] : slot[0], pf_q[i], v);
+        }
+      }
+    }
+    if (py >= py0) {
+      const int px = 16 * wave + (n >> 1);
+      const bool store = (n & 1) == 0 && px < a.Wp;
+      float* dst = a.out + (((size_t)img * a.Hp + py) * a.Wp + px) * 64 + 16 * h;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int k4 = 0; k4 < 4; ++k4) {
+          float o[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int k = 4 * k4 + e;
+            float left = __shfl_up(acc[0][t][k], 1);
+            const float right = __shfl_down(acc[0][t][k], 1);
+            if (n == 0) left = wave > 0 ? sEdge[((wave - 1) * 2 + h) * 32 + 16 * t + k] : 0.f;
+            o[e] = fmaxf(fmaxf(left, acc[0][t][k]), right);
+          }
+          if (store) *reinterpret_cast<float4*>(dst + 32 * t + 4 * k4) = make_float4(o[0], o[1], o[2], o[3]);
+        }
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace
 }  // namespace rmbx
 
@@ -293,6 +481,43 @@ extern "C" int rmbx_stem_s2d_conv_maxpool(const void* in, const void* weight, co
   const long long nblocks = (long long)N * a.bands;
   RMBX_CHECK_ARG(nblocks < (1ll << 31), "rmbx_stem_s2d_conv_maxpool: grid too large");
   hipLaunchKernelGGL(rmbx::stem_pool_kernel, dim3((unsigned)nblocks), dim3(64 * a.nct), 0, (hipStream_t)stream, a);
+  RMBX_CHECK_LAUNCH();
+  return RMBX_OK;
+}
+
+extern "C" int rmbx_stem_s2d_conv_maxpool_f32(const float* in, const float* weight, const float* bias, float* out,
+                                              int N, int Hs, int Ws, int band_rows, void* stream) {
+  RMBX_CHECK_ARG(in && weight && bias && out, "rmbx_stem_s2d_conv_maxpool_f32: null pointer");
+  RMBX_CHECK_ARG(N >= 0 && Hs > 0 && Ws > 0, "rmbx_stem_s2d_conv_maxpool_f32: bad geometry");
+  RMBX_CHECK_ARG(Ws <= 32 * rmbx::SP_MAX_WAVES, "rmbx_stem_s2d_conv_maxpool_f32: Ws=%d exceeds %d", Ws,
+                 32 * rmbx::SP_MAX_WAVES);
+  RMBX_CHECK_ARG((((uintptr_t)in | (uintptr_t)out) & 15) == 0,
+                 "rmbx_stem_s2d_conv_maxpool_f32: in/out must be 16-byte aligned");
+  if (N == 0) return RMBX_OK;
+  rmbx::StemPoolF32Args a;
+  a.in = in;
+  a.w = weight;
+  a.bias = bias;
+  a.out = out;
+  a.N = N;
+  a.Hs = Hs;
+  a.Ws = Ws;
+  a.Hp = (Hs - 1) / 2 + 1;
+  a.Wp = (Ws - 1) / 2 + 1;
+  a.nct = (Ws + 31) / 32;
+  a.rc = 32 * a.nct + 4;
+  RMBX_CHECK_ARG(2 * 3 * a.rc <= 4 * 64 * a.nct, "rmbx_stem_s2d_conv_maxpool_f32: prefetch does not fit");
+  if (band_rows <= 0) {
+    const int want_blocks = 512;
+    int bands = (want_blocks + N - 1) / N;
+    if (bands > a.Hp) bands = a.Hp;
+    band_rows = (a.Hp + bands - 1) / bands;
+  }
+  a.band_rows = band_rows;
+  a.bands = (a.Hp + band_rows - 1) / band_rows;
+  const long long nblocks = (long long)N * a.bands;
+  RMBX_CHECK_ARG(nblocks < (1ll << 31), "rmbx_stem_s2d_conv_maxpool_f32: grid too large");
+  hipLaunchKernelGGL(rmbx::stem_pool_f32_kernel, dim3((unsigned)nblocks), dim3(64 * a.nct), 0, (hipStream_t)stream, a);
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
 }

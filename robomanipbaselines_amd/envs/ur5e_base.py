@@ -67,6 +67,9 @@ class BatchedMujocoUR5eEnvBase:
         self.camera_names = [str(x) for x in self.arrays["names_cam"]]
         self.reward = torch.zeros(self.num_envs, dtype=torch.float64, device=self.device)
         self.world_idx = np.zeros(self.num_envs, dtype=np.int64)
+        # MuJoCo's bad-state reset (mj_checkAcc -> mj_resetData): the model's qpos0, per env count
+        self._qpos0 = torch.tensor(self.arrays["qpos0"], dtype=torch.float64, device=self.device)
+        self.bad_resets = torch.zeros(self.num_envs, dtype=torch.int32, device=self.device)
 
     # -- reference API ----------------------------------------------------------------------
     def _setup_task(self):
@@ -113,6 +116,7 @@ class BatchedMujocoUR5eEnvBase:
             e.time.zero_()
             e.ctrl.copy_(ctrl0.expand_as(e.ctrl))
             e.stats.zero_()
+            self.bad_resets.zero_()
         else:
             m = mask.bool()
             e.qpos[m] = q0 if q0.dim() == 1 else q0[m]
@@ -121,6 +125,7 @@ class BatchedMujocoUR5eEnvBase:
             e.time[m] = 0
             e.ctrl[m] = ctrl0
             e.stats[m] = 0
+            self.bad_resets[m] = 0
         e.forward()
         self.reward = self._get_reward()
         return self._get_obs(), {}
@@ -132,9 +137,30 @@ class BatchedMujocoUR5eEnvBase:
         if action is not None:
             e.ctrl.copy_(action)
         e.step(self.frame_skip, active=active)
+        self._reset_bad_states()
         obs = self._get_obs()
         self.reward = self._get_reward()
         return obs, self.reward, False, False, {}
+
+    def _reset_bad_states(self):
+        """MuJoCo's divergence guard (mj_step -> mj_checkAcc, [ext] mujoco 3.1.6): an env whose
+        qacc went non-finite or above 1e10 during the env-step (the physics kernel flags it in
+        stats[:, 3]) is reset as mj_resetData does -- qpos = the model's qpos0, qvel = qacc_warmstart
+        = ctrl = 0, time = 0 -- and forwarded again; bad_resets counts these per env (MuJoCo's
+        mjWARN_BADQACC counter).  Device-side masked updates, no host sync.  Granularity: MuJoCo
+        resets inside the offending substep and integrates the reset state for the remaining
+        substeps; here the reset lands at the end of the env-step."""
+        e = self.engine
+        bad = e.stats[:, 3] != 0
+        col = bad[:, None]
+        torch.where(col, self._qpos0, e.qpos, out=e.qpos)
+        e.qvel.masked_fill_(col, 0.0)
+        e.qacc_ws.masked_fill_(col, 0.0)
+        e.ctrl.masked_fill_(col, 0.0)
+        e.time.masked_fill_(bad, 0.0)
+        self.bad_resets += bad.to(torch.int32)
+        e.stats[:, 3] = 0
+        e.forward(active=bad.to(torch.uint8))
 
     def get_time(self):
         return self.engine.time

@@ -512,7 +512,10 @@ STEM_POOL_MAX_WS = 320
 def stem_s2d_conv_maxpool(x_s2d, w_packed, bias, band_rows=0):
     """maxpool3x3/2/pad1(relu(conv1(x) + bias)) for the space-to-depth image in one kernel:
     [n, Hs, Ws, 16] bf16 -> channels_last [n, 64, (Hs-1)//2+1, (Ws-1)//2+1] bf16
-    (rmbx_stem_s2d_conv_maxpool; bit-identical to stem_s2d_conv + nhwc_bias_relu_maxpool)."""
+    (rmbx_stem_s2d_conv_maxpool; bit-identical to stem_s2d_conv + nhwc_bias_relu_maxpool);
+    f32 in -> f32 out through rmbx_stem_s2d_conv_maxpool_f32."""
+    if x_s2d.dtype == torch.float32:
+        return _stem_s2d_conv_maxpool_f32(x_s2d, w_packed, bias, band_rows)
     _chk(x_s2d, torch.bfloat16, name="x_s2d")
     n, Hs, Ws, c16 = x_s2d.shape
     if c16 != 16:
@@ -524,6 +527,22 @@ def stem_s2d_conv_maxpool(x_s2d, w_packed, bias, band_rows=0):
     Hp, Wp = (Hs - 1) // 2 + 1, (Ws - 1) // 2 + 1
     out = torch.empty((n, 64, Hp, Wp), dtype=torch.bfloat16, device=x_s2d.device, memory_format=torch.channels_last)
     N.call("rmbx_stem_s2d_conv_maxpool", N.ptr(x_s2d), N.ptr(w_packed), N.ptr(bias), N.ptr(out), n, Hs, Ws,
+           int(band_rows), N.stream_ptr())
+    return out
+
+
+def _stem_s2d_conv_maxpool_f32(x_s2d, w_packed, bias, band_rows=0):
+    _chk(x_s2d, torch.float32, name="x_s2d")
+    n, Hs, Ws, c16 = x_s2d.shape
+    if c16 != 16:
+        raise ValueError("x_s2d must be [n, Hs, Ws, 16]")
+    if Ws > STEM_POOL_MAX_WS:
+        raise ValueError(f"stem_s2d_conv_maxpool: Ws={Ws} exceeds {STEM_POOL_MAX_WS}")
+    _chk(w_packed, torch.float32, (64, 4, 4, 16), "w_packed")
+    _chk(bias, torch.float32, (64,), "bias")
+    Hp, Wp = (Hs - 1) // 2 + 1, (Ws - 1) // 2 + 1
+    out = torch.empty((n, 64, Hp, Wp), dtype=torch.float32, device=x_s2d.device, memory_format=torch.channels_last)
+    N.call("rmbx_stem_s2d_conv_maxpool_f32", N.ptr(x_s2d), N.ptr(w_packed), N.ptr(bias), N.ptr(out), n, Hs, Ws,
            int(band_rows), N.stream_ptr())
     return out
 

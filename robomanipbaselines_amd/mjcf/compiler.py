@@ -635,6 +635,11 @@ def compile_mjcf(path, missing_mesh_box=(0.045, 0.0125, 0.0125)):
             bias = (_floats(a.get("biasprm", "0 0 0")) + [0, 0, 0])[:3]
             if a.get("biastype", "none") == "none":
                 bias = [0.0, 0.0, 0.0]
+            if g.tag == "position":  # MuJoCo shortcut: gain kp, affine bias (0, -kp, -kv)
+                kp, kv = float(a.get("kp", 1)), float(a.get("kv", 0))
+                gain, bias = [kp, 0.0, 0.0], [0.0, -kp, -kv]
+            elif g.tag == "motor":  # gain 1 (gear 1), no bias
+                gain, bias = [1.0, 0.0, 0.0], [0.0, 0.0, 0.0]
             cr = _floats(a["ctrlrange"]) if "ctrlrange" in a else [0, 0]
             fr = _floats(a["forcerange"]) if "forcerange" in a else [0, 0]
             acts.append(dict(name=a.get("name", ""), trn=trn, trnid=tid, gain=gain[0], bias=bias,

@@ -155,9 +155,9 @@ class FusedResNet18Trunk(nn.Module):
         return self.blocks(K.nhwc_bias_relu_maxpool(s, self.stem.bias_f32()))
 
     def forward_s2d(self, x_s2d):
-        """Same function on the renderer's 2x2 space-to-depth image [B, H/2, W/2, 16] (bf16):
-        the stem runs as an rmbx MFMA implicit GEMM (rmbx_stem_s2d_conv, bias + ReLU fused),
-        then the max-pool."""
+        """Same function on the renderer's 2x2 space-to-depth image [B, H/2, W/2, 16] (bf16 or
+        f32): conv + bias + ReLU + max-pool in one rmbx MFMA kernel (rmbx_stem_s2d_conv_maxpool
+        / _f32); wider bf16 images: rmbx_stem_s2d_conv then the max-pool."""
         w = self.stem.conv.weight
         key = (w.data_ptr(), w.dtype)
         if getattr(self, "_s2d_key", None) != key:
@@ -167,5 +167,7 @@ class FusedResNet18Trunk(nn.Module):
         if w.shape[0] == 64 and x_s2d.shape[2] <= K.STEM_POOL_MAX_WS:
             # conv + bias + ReLU + max-pool in one kernel: the full-resolution stem map stays on chip
             return self.blocks(K.stem_s2d_conv_maxpool(x_s2d, self._s2d_w, self.stem.bias_f32()))
+        if x_s2d.dtype != torch.bfloat16:
+            raise ValueError(f"forward_s2d: f32 images wider than {2 * K.STEM_POOL_MAX_WS} pixels are not supported")
         s = K.stem_s2d_conv(x_s2d, self._s2d_w, self.stem.bias_f32(), relu=True)
         return self.blocks(K.nhwc_bias_relu_maxpool(s, self._s2d_zero))

@@ -17,6 +17,7 @@ import torch
 
 from ... import kernels as K
 from ...common.rollout_base import BatchedRolloutBase
+from ..diffusion.checkpoint import load_dp_checkpoint
 from .dp_model import DiffusionPolicyModel
 
 
@@ -49,8 +50,8 @@ class RolloutDiffusionPolicy(BatchedRolloutBase):
             horizon=int(d["horizon"]), n_obs_steps=self.n_obs_steps, n_action_steps=self.n_action_steps,
             crop_hw=(self.crop_size[1], self.crop_size[0]), num_inference_steps=100)
         if self.args.checkpoint:
-            sd = torch.load(self.args.checkpoint, map_location="cpu", weights_only=True)
-            self.policy.load_state_dict(sd, strict=False)
+            # the reference's DiffusionUnetHybridImagePolicy checkpoint, strictly (RolloutBase.py:376-385)
+            load_dp_checkpoint(self.policy, self.args.checkpoint, self.camera_names)
         self.policy_dtype = torch.bfloat16 if self.args.precision == "bf16" else torch.float32
         # heuristic (not benchmarked) MIOpen solver choice: with cudnn.benchmark the selected
         # solvers, and so the bits of the UNet's outputs, can differ from call to call

@@ -17,6 +17,7 @@ import torch
 
 from ... import kernels as K
 from ..diffusion_policy.rollout_diffusion_policy import RolloutDiffusionPolicy, _limits_meta
+from ..diffusion.checkpoint import load_dp3_checkpoint
 from .dp3_model import DP3Model
 
 
@@ -47,8 +48,8 @@ class RolloutDiffusionPolicy3d(RolloutDiffusionPolicy):
                                n_obs_steps=self.n_obs_steps, n_action_steps=self.n_action_steps,
                                use_pc_color=bool(d["use_pc_color"]))
         if self.args.checkpoint:
-            sd = torch.load(self.args.checkpoint, map_location="cpu", weights_only=True)
-            self.policy.load_state_dict(sd, strict=False)
+            # the reference's DP3 checkpoint, strictly (RolloutBase.py:376-385)
+            load_dp3_checkpoint(self.policy, self.args.checkpoint)
         self.policy_dtype = torch.bfloat16 if self.args.precision == "bf16" else torch.float32
         # heuristic (not benchmarked) MIOpen solver choice: with cudnn.benchmark the selected
         # solvers, and so the bits of the UNet's outputs, can differ from call to call

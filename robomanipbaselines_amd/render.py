@@ -85,8 +85,7 @@ class Renderer:
         if policy is not None:
             assert policy.is_contiguous() and policy.dtype in (torch.float32, torch.bfloat16)
             if tuple(policy.shape) == (n, H // 2, W // 2, 16):  # space-to-depth stem input
-                assert policy.dtype == torch.bfloat16
-                pdt = 2
+                pdt = 2 if policy.dtype == torch.bfloat16 else 3
             else:
                 assert tuple(policy.shape) == (n, 3, H, W)
                 pdt = 1 if policy.dtype == torch.bfloat16 else 0

@@ -89,7 +89,10 @@ def test_act_production_config_fp32_within_1e4_and_bf16_error():
     want = np.array(want)
 
     dev32 = _device_form(ref, torch.float32)
-    got_chunks = [dev32(s.to(DEV), im.to(DEV)) for s, im in inputs]
+    # the bench path: the renderer's f32 space-to-depth image into the fused f32 stem
+    got_chunks = [dev32(s.to(DEV), K.image_to_s2d(im[:, 0].to(DEV))[:, None]) for s, im in inputs]
+    std_form = dev32(inputs[0][0].to(DEV), inputs[0][1].to(DEV))  # CHW image: MIOpen stem
+    assert (std_form.cpu() - want_chunks[0]).abs().max().item() <= 1e-4
     got = np.array(_ensemble_actions(got_chunks))
     chunk_err = max((g.cpu() - w).abs().max().item() for g, w in zip(got_chunks, want_chunks))
     err32 = np.abs(got - want).max()

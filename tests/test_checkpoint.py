@@ -80,3 +80,84 @@ def test_mismatched_checkpoint_fails_loudly(mutate):
         ref_sd["model.query_embed.weight"] = torch.zeros(11, 64)
     with pytest.raises(ValueError):
         load_act_checkpoint(_small_act(8), ref_sd)
+
+
+def _upstream_dp_sd(model, cam="front"):
+    """A DiffusionUnetHybridImagePolicy-layout state_dict of `model`'s weights: robomimic VisualCore
+    names with their `nets.*` aliases, identity LinearNormalizer entries."""
+    sd = {}
+    for k, v in model.state_dict().items():
+        if k.startswith("obs_nets.0."):
+            rest = k[len("obs_nets.0."):]
+            base = f"obs_encoder.obs_nets.{cam}_rgb_image."
+            sd[base + rest] = v.clone()
+            alias = {"backbone.": "nets.0.", "pool.": "nets.1.", "linear.": "nets.3."}
+            for a, b in alias.items():
+                if rest.startswith(a):
+                    sd[base + b + rest[len(a):]] = v.clone()
+        else:
+            sd[k] = v.clone()
+    sd["normalizer.params_dict.action.scale"] = torch.ones(7)
+    sd["normalizer.params_dict.action.offset"] = torch.zeros(7)
+    sd["normalizer.params_dict.action.input_stats.max"] = torch.ones(7)
+    return sd
+
+
+def _small_dp(seed):
+    from robomanipbaselines_amd.policy.diffusion_policy.dp_model import DiffusionPolicyModel
+
+    torch.manual_seed(seed)
+    return DiffusionPolicyModel(7, 7, 1, crop_hw=(32, 48), down_dims=(32, 64, 128))
+
+
+def test_dp_reference_checkpoint_loads_strictly(tmp_path):
+    from robomanipbaselines_amd.policy.diffusion.checkpoint import load_dp_checkpoint
+
+    src, dst = _small_dp(0), _small_dp(1)
+    path = tmp_path / "policy_last.ckpt"
+    torch.save(_upstream_dp_sd(src), path)
+    load_dp_checkpoint(dst, str(path), ["front"])
+    for k, v in src.state_dict().items():
+        assert torch.equal(dst.state_dict()[k], v), k
+
+
+def test_dp_checkpoint_rejects_bad_dicts():
+    from robomanipbaselines_amd.policy.diffusion.checkpoint import load_dp_checkpoint
+
+    src = _small_dp(0)
+    sd = _upstream_dp_sd(src)
+    bad = dict(sd, **{"obs_encoder.obs_nets.front_rgb_image.extra.weight": torch.zeros(1)})
+    with pytest.raises(ValueError):
+        load_dp_checkpoint(_small_dp(1), bad, ["front"])
+    missing = {k: v for k, v in sd.items() if not k.startswith("model.final_conv")}
+    with pytest.raises(RuntimeError):  # strict load_state_dict: missing keys
+        load_dp_checkpoint(_small_dp(1), missing, ["front"])
+    alias = dict(sd)
+    k = "obs_encoder.obs_nets.front_rgb_image.nets.0.nets.0.weight"
+    alias[k] = alias[k] + 1
+    with pytest.raises(ValueError):
+        load_dp_checkpoint(_small_dp(1), alias, ["front"])
+    norm = dict(sd, **{"normalizer.params_dict.action.scale": torch.full((7,), 2.0)})
+    with pytest.raises(ValueError):
+        load_dp_checkpoint(_small_dp(1), norm, ["front"])
+    with pytest.raises(ValueError):  # a camera the rollout does not have
+        load_dp_checkpoint(_small_dp(1), sd, ["hand"])
+
+
+def test_dp3_reference_checkpoint_loads_strictly():
+    from robomanipbaselines_amd.policy.diffusion.checkpoint import load_dp3_checkpoint
+    from robomanipbaselines_amd.policy.diffusion_policy_3d.dp3_model import DP3Model
+
+    torch.manual_seed(0)
+    src = DP3Model(7, 7, down_dims=(32, 64, 128))
+    torch.manual_seed(1)
+    dst = DP3Model(7, 7, down_dims=(32, 64, 128))
+    sd = dict(src.state_dict())
+    sd["normalizer.params_dict.point_cloud.offset"] = torch.zeros(3)
+    load_dp3_checkpoint(dst, sd)
+    for k, v in src.state_dict().items():
+        assert torch.equal(dst.state_dict()[k], v), k
+    with pytest.raises(ValueError):
+        load_dp3_checkpoint(dst, dict(sd, **{"ema.decay": torch.zeros(1)}))
+    with pytest.raises(RuntimeError):
+        load_dp3_checkpoint(dst, {k: v for k, v in sd.items() if "state_mlp" not in k})

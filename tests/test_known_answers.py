@@ -1,0 +1,224 @@
+"""Analytic known-answer tests of the dynamics: the pipeline both the C oracle and the
+HIP engine restate (MuJoCo 3.1.6's mj_step with the implicitfast integrator, [ext]) is checked
+against closed-form mechanics on small models (tests/kat/*.xml, compiled by the build's MJCF
+compiler), independently of either implementation:
+
+* pendulum period: small amplitude vs 2 pi sqrt(I / m g L), large amplitude vs the elliptic
+  integral 4 sqrt(I / m g L) K(sin^2(theta0 / 2));
+* energy: conserved without damping (semi-implicit Euler is symplectic: bounded error), strictly
+  dissipated with joint damping;
+* free fall: the discrete closed form of semi-implicit Euler z_n = z0 - g dt^2 n (n + 1) / 2, and
+  torque-free spin about a principal axis (constant angular velocity, quaternion = q0 exp(w t));
+* static servo equilibrium: position servos holding a 2-link arm against gravity settle where
+  kp (ctrl - q) = gravity torque (solved independently with scipy);
+* contact: a ball settles on the floor at its radius (soft-contact penetration below 2 mm) with
+  the normal force carrying its weight.
+
+CPU tests run the oracle; -m gpu tests run the engine on a batch and also require it to match
+the oracle (1e-10 per the engine's parity bar)."""
+
+import os
+
+import numpy as np
+import pytest
+
+KAT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "kat")
+G = 9.81
+
+
+def _arrays(name):
+    from robomanipbaselines_amd import model as MD
+    from robomanipbaselines_amd.mjcf import compiler as C
+
+    return MD.pack(C.compile_mjcf(os.path.join(KAT, name + ".xml")))
+
+
+class _OracleRun:
+    """Run one model in the C oracle, recording qpos/qvel after every substep."""
+
+    def __init__(self, arrays, qpos, qvel=None, ctrl=None):
+        from oracle.dyn import OracleEnv
+
+        self.env = OracleEnv(arrays)
+        nv, nu = self.env.nv, self.env.nu
+        self.env.set_state(0.0, qpos, np.zeros(nv) if qvel is None else qvel, np.zeros(nv),
+                           np.zeros(max(nu, 1)) if ctrl is None else ctrl)
+
+    def run(self, nsteps):
+        qs, vs = [], []
+        for _ in range(nsteps):
+            self.env.step(1)
+            _, q, v, _ = self.env.state()
+            qs.append(q)
+            vs.append(v)
+        return np.array(qs), np.array(vs)
+
+
+class _EngineRun:
+    """The same on the HIP engine, n identical envs; every `chunk` substeps per launch."""
+
+    def __init__(self, arrays, qpos, qvel=None, ctrl=None, n=3):
+        import torch
+
+        from robomanipbaselines_amd.engine import PhysicsEngine
+
+        self.e = PhysicsEngine(arrays, n, "cuda:0")
+        self.e.qpos.copy_(torch.tensor(np.tile(qpos, (n, 1))))
+        if qvel is not None:
+            self.e.qvel.copy_(torch.tensor(np.tile(qvel, (n, 1))))
+        if ctrl is not None:
+            self.e.ctrl.copy_(torch.tensor(np.tile(ctrl, (n, 1))))
+
+    def run(self, nsteps):
+        qs, vs = [], []
+        for _ in range(nsteps):
+            self.e.step(1)
+            qs.append(self.e.qpos.cpu().numpy().copy())
+            vs.append(self.e.qvel.cpu().numpy().copy())
+        q, v = np.array(qs), np.array(vs)
+        assert np.array_equal(q[:, 0], q[:, -1])  # identical envs stay identical
+        return q[:, 0], v[:, 0]
+
+
+def _runner(kind):
+    return _OracleRun if kind == "oracle" else _EngineRun
+
+
+KINDS = ["oracle", pytest.param("engine", marks=pytest.mark.gpu)]
+
+# pendulum constants (tests/kat/pendulum.xml): bob mass 1 at L = 0.5, sphere r = 0.05
+M_BOB, L_BOB, R_BOB = 1.0, 0.5, 0.05
+I_PIVOT = M_BOB * L_BOB ** 2 + 0.4 * M_BOB * R_BOB ** 2
+
+
+def _period(theta, dt):
+    """Mean period from the downward zero crossings (linear interpolation)."""
+    s = np.sign(theta)
+    idx = np.where((s[:-1] > 0) & (s[1:] <= 0))[0]
+    t = (idx + theta[idx] / (theta[idx] - theta[idx + 1])) * dt
+    return np.diff(t).mean()
+
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("theta0", [0.01, 1.0])
+def test_pendulum_period(kind, theta0):
+    from scipy.special import ellipk
+
+    a = _arrays("pendulum")
+    dt = float(a["_timestep"])
+    q, _ = _runner(kind)(a, np.array([theta0])).run(6000)
+    w0 = np.sqrt(M_BOB * G * L_BOB / I_PIVOT)
+    T = 4.0 / w0 * ellipk(np.sin(theta0 / 2) ** 2)
+    assert abs(_period(q[:, 0], dt) / T - 1) < 2e-4, (_period(q[:, 0], dt), T)
+
+
+def _energy(theta, omega):
+    return 0.5 * I_PIVOT * omega ** 2 - M_BOB * G * L_BOB * np.cos(theta)
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_pendulum_energy_conserved_without_damping(kind):
+    a = _arrays("pendulum")
+    q, v = _runner(kind)(a, np.array([1.0])).run(10000)
+    E = _energy(q[:, 0], v[:, 0])
+    E0 = _energy(1.0, 0.0)
+    # symplectic Euler: O(dt) bounded oscillation, no secular drift
+    assert np.abs(E - E0).max() < 5e-3 * abs(E0)
+    assert abs(E[-1000:].mean() - E[:1000].mean()) < 5e-4 * abs(E0)
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_pendulum_energy_dissipated_with_damping(kind):
+    a = _arrays("pendulum_damped")
+    q, v = _runner(kind)(a, np.array([1.0])).run(4000)
+    E = _energy(q[:, 0], v[:, 0])
+    # d/dt E = -b w^2 <= 0 (up to the integrator's O(dt) exchange), so a coarse envelope must fall
+    env = E.reshape(40, 100).max(1)
+    assert np.all(np.diff(env) < 0)
+    assert E[-1] < E[0] - 0.05
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_free_fall_discrete_closed_form(kind):
+    a = _arrays("free_body")
+    dt = float(a["_timestep"])
+    q0 = np.array([0.0, 0.0, 10.0, 1.0, 0.0, 0.0, 0.0])
+    q, v = _runner(kind)(a, q0).run(500)
+    n = np.arange(1, 501)
+    np.testing.assert_allclose(q[:, 2], 10.0 - G * dt * dt * n * (n + 1) / 2, rtol=0, atol=1e-12)
+    np.testing.assert_allclose(v[:, 2], -G * dt * n, rtol=0, atol=1e-12)
+    assert np.all(q[:, :2] == 0) and np.all(q[:, 3:] == q0[3:])
+
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("axis", [0, 1, 2])
+def test_torque_free_spin_about_principal_axis(kind, axis):
+    a = _arrays("free_body")
+    dt = float(a["_timestep"])
+    q0 = np.array([0.0, 0.0, 10.0, 1.0, 0.0, 0.0, 0.0])
+    w = 3.0
+    v0 = np.zeros(6)
+    v0[3 + axis] = w
+    q, v = _runner(kind)(a, q0, v0).run(400)
+    np.testing.assert_allclose(v[:, 3:], np.tile(v0[3:], (400, 1)), rtol=0, atol=1e-10)
+    t = dt * np.arange(1, 401)
+    quat = np.zeros((400, 4))
+    quat[:, 0] = np.cos(w * t / 2)
+    quat[:, 1 + axis] = np.sin(w * t / 2)
+    np.testing.assert_allclose(q[:, 3:], quat, rtol=0, atol=1e-9)
+
+
+def _servo_equilibrium(ctrl):
+    """kp_i (ctrl_i - q_i) = gravity torque_i of the 2-link arm (joints about +y, links along +x
+    at q = 0; a rotation q about +y takes +x towards -z)."""
+    from scipy.optimize import fsolve
+
+    m1, l1c, m2, l1, l2c = 1.5, 0.4, 0.8, 0.4, 0.3
+    kp = np.array([200.0, 120.0])
+
+    def res(q):
+        q1, q12 = q[0], q[0] + q[1]
+        # torque about +y of gravity (0, 0, -m g) at r = (x, 0, z): tau_y = z F_x - x F_z = m g x
+        x1, x2 = l1c * np.cos(q1), l1 * np.cos(q1) + l2c * np.cos(q12)
+        tau1 = m1 * G * x1 + m2 * G * x2
+        tau2 = m2 * G * l2c * np.cos(q12)
+        return kp * (ctrl - q) + np.array([tau1, tau2])
+
+    return fsolve(res, ctrl, xtol=1e-14)
+
+
+@pytest.mark.parametrize("kind", KINDS)
+@pytest.mark.parametrize("ctrl", [(0.0, 0.0), (0.6, -0.9), (-0.4, 1.2)])
+def test_servo_static_equilibrium(kind, ctrl):
+    a = _arrays("servo_arm")
+    ctrl = np.array(ctrl)
+    q, v = _runner(kind)(a, ctrl.copy(), ctrl=ctrl).run(4000)
+    np.testing.assert_allclose(q[-1], _servo_equilibrium(ctrl), rtol=0, atol=1e-7)
+    assert np.abs(v[-1]).max() < 1e-7
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_ball_settles_on_floor(kind):
+    a = _arrays("sphere_plane")
+    q0 = np.array([0.0, 0.0, 0.3, 1.0, 0.0, 0.0, 0.0])
+    q, v = _runner(kind)(a, q0).run(2000)
+    z = q[-1, 2]
+    assert 0.05 - 2e-3 < z <= 0.05, z
+    assert np.abs(v[-1]).max() < 1e-4
+    assert np.abs(q[-1, :2]).max() < 1e-9  # a vertical drop stays vertical
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name,q0,v0,ctrl,steps", [
+    ("pendulum", [1.0], None, None, 2000),
+    ("servo_arm", [0.6, -0.9], None, [0.6, -0.9], 500),
+    ("sphere_plane", [0.0, 0.0, 0.3, 1.0, 0.0, 0.0, 0.0], None, None, 400),
+    ("free_body", [0.0, 0.0, 10.0, 1.0, 0.0, 0.0, 0.0], [0.1, 0.2, 0.3, 1.0, 2.0, 3.0], None, 300),
+])
+def test_engine_matches_oracle_on_known_answer_models(name, q0, v0, ctrl, steps):
+    a = _arrays(name)
+    args = (np.array(q0), None if v0 is None else np.array(v0), None if ctrl is None else np.array(ctrl))
+    qo, vo = _OracleRun(a, *args).run(steps)
+    qe, ve = _EngineRun(a, *args).run(steps)
+    np.testing.assert_allclose(qe, qo, rtol=0, atol=1e-10)
+    np.testing.assert_allclose(ve, vo, rtol=0, atol=1e-9)

@@ -306,3 +306,38 @@ def test_render_s2d_layout_equals_standard():
     env.render_images("front", policy=std)
     env.render_images("front", policy=s2d)
     assert torch.equal(K.image_to_s2d(std), s2d)
+
+
+@torch.no_grad()
+@pytest.mark.parametrize("n,H,W,band_rows", [(2, 48, 64, 0), (3, 480, 640, 0), (2, 480, 640, 7), (2, 46, 630, 5),
+                                             (1, 34, 90, 1)])
+def test_stem_conv_maxpool_f32_matches_fp32_reference(n, H, W, band_rows):
+    """rmbx_stem_s2d_conv_maxpool_f32 (f32 MFMA) vs F.conv2d + bias + ReLU + max_pool2d in fp32 on
+    the same image: within f32 accumulation-order rounding."""
+    from robomanipbaselines_amd import kernels as K
+
+    g = torch.Generator(device=DEV).manual_seed(13)
+    x = torch.rand(n, 3, H, W, device=DEV, generator=g) * 4 - 2
+    w = torch.randn(64, 3, 7, 7, device=DEV, generator=g) * 0.1
+    b = torch.randn(64, device=DEV, generator=g) * 0.5
+    want = F.max_pool2d(F.relu(F.conv2d(x, w, b, 2, 3)), 3, 2, 1)
+    got = K.stem_s2d_conv_maxpool(K.image_to_s2d(x), K.pack_stem_s2d(w), b, band_rows=band_rows)
+    torch.cuda.synchronize()
+    assert got.shape == want.shape and got.dtype == torch.float32
+    assert got.is_contiguous(memory_format=torch.channels_last)
+    err = (got - want).abs().max().item()
+    assert err <= 2e-5 * max(1.0, want.abs().max().item()), err
+
+
+def test_render_s2d_f32_layout_equals_standard():
+    from robomanipbaselines_amd import kernels as K
+    from robomanipbaselines_amd.envs.ur5e_cable import BatchedMujocoUR5eCableEnv
+
+    env = BatchedMujocoUR5eCableEnv(2, DEV)
+    env.reset()
+    H, W = env.renderer.height, env.renderer.width
+    std = torch.empty((2, 3, H, W), dtype=torch.float32, device=DEV)
+    s2d = torch.empty((2, H // 2, W // 2, 16), dtype=torch.float32, device=DEV)
+    env.render_images("front", policy=std, mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225))
+    env.render_images("front", policy=s2d, mean=(0.485, 0.456, 0.406), std=(0.229, 0.224, 0.225))
+    assert torch.equal(K.image_to_s2d(std), s2d)
