@@ -53,17 +53,10 @@ class RolloutDiffusionPolicy(BatchedRolloutBase):
             # the reference's DiffusionUnetHybridImagePolicy checkpoint, strictly (RolloutBase.py:376-385)
             load_dp_checkpoint(self.policy, self.args.checkpoint, self.camera_names)
         self.policy_dtype = torch.bfloat16 if self.args.precision == "bf16" else torch.float32
-        # heuristic (not benchmarked) MIOpen solver choice: with cudnn.benchmark the selected
-        # solvers, and so the bits of the UNet's outputs, can differ from call to call
-        # deterministic MIOpen solvers: without them the UNet's conv1d results vary run to run
-        # (atomic split-K), so the same seed would not reproduce the same episodes.
-        # bf16 device form: the UNet's convs are GEMMs (deterministic), only the image encoder's
-        # 2-D convs go to MIOpen; at rollout batch sizes their only deterministic solver is the
-        # naive reference one (tens of seconds per inference at 2048 envs), so Find picks them
-        # among all solvers, once per shape
-        bf16 = self.policy_dtype == torch.bfloat16
-        torch.backends.cudnn.benchmark = bf16
-        torch.backends.cudnn.deterministic = not bf16
+        # (the UNet's convs are GEMMs in both precisions, so MIOpen serves the image encoder only:
+        # Find picks its solvers once per shape, outside the captured denoising loop)
+        torch.backends.cudnn.benchmark = True
+        torch.backends.cudnn.deterministic = False
         self.policy = self.policy.eval().requires_grad_(False).to(device=self.device, dtype=self.policy_dtype)
         self.policy.obs_nets = self.policy.obs_nets.to(memory_format=torch.channels_last)
 

@@ -51,8 +51,8 @@ class RolloutDiffusionPolicy3d(RolloutDiffusionPolicy):
             # the reference's DP3 checkpoint, strictly (RolloutBase.py:376-385)
             load_dp3_checkpoint(self.policy, self.args.checkpoint)
         self.policy_dtype = torch.bfloat16 if self.args.precision == "bf16" else torch.float32
-        # heuristic (not benchmarked) MIOpen solver choice: with cudnn.benchmark the selected
-        # solvers, and so the bits of the UNet's outputs, can differ from call to call
+        # the DP3 encoder is PointNet Linears and the UNet's convs are GEMMs (deterministic
+        # hipBLASLt) in both precisions: no MIOpen call in the captured denoising loop
         torch.backends.cudnn.benchmark = False
         torch.backends.cudnn.deterministic = True
         self.policy = self.policy.eval().requires_grad_(False).to(device=self.device, dtype=self.policy_dtype)

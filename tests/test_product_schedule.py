@@ -123,3 +123,51 @@ def test_product_loop_schedule_matches_reference(md, skip):
         assert v["duration"][i] == float(c["duration"][0]), name
     # an env frozen at its end keeps its clock: its time is the golden duration's clock
     assert np.isfinite(ro.env.get_time().cpu().numpy()).all()
+
+
+@pytest.mark.gpu
+def test_reach_phases_follow_reference_ik():
+    """Pre-motion reach phases (OperationMujocoUR5eCable.py:8-30, PhaseBase.py:41-56,
+    ArmManager.py:148-153, 220-243) through the product loop: each reach phase's target is
+    (diag(-1, 1, -1), cable_end xy of the env at the phase start, fixed z), and every env-step's
+    command update is one DLS IK iteration from the previous command (oracle/arm_ik.py)."""
+    from oracle import arm_ik
+    from robomanipbaselines_amd.envs.operation.OperationMujocoUR5eCable import OperationMujocoUR5eCable
+    from robomanipbaselines_amd.policy.mlp.rollout_mlp import RolloutMlp
+
+    class Rollout(OperationMujocoUR5eCable, RolloutMlp):
+        pass
+
+    n = 5
+    ro = Rollout(argv=["--num_envs", str(n), "--device", "cuda:0", "--world_idx_list", "0", "1", "2", "3", "4",
+                       "--world_random_scale", "0.01", "0.01", "0.0"])
+    recs, targets = [], []
+    ik, settgt = ro._ik_step, ro._set_reach_target
+
+    def rec_ik():
+        before = ro.q_cmd.cpu().numpy().copy()
+        ik()
+        recs.append((before, ro._tgt_R.cpu().numpy().copy(), ro._tgt_p.cpu().numpy().copy(),
+                     ro.q_cmd.cpu().numpy().copy()))
+
+    def rec_target(pos_z):
+        end = ro.env.get_body_pose("cable_end")[:, :3].cpu().numpy().copy()
+        settgt(pos_z)
+        targets.append((pos_z, end, ro._tgt_R.cpu().numpy().copy(), ro._tgt_p.cpu().numpy().copy()))
+
+    ro._ik_step, ro._set_reach_target = rec_ik, rec_target
+    ro.reset()
+    while ro.phase_idx < len(ro.pre_durations):
+        ro.step_once()
+    # Reach1 0.7 s and Reach2 0.3 s at 32 ms per env-step (transitions on the strict > of the clock)
+    assert [t[0] for t in targets] == [1.02, 0.995]
+    assert len(recs) == 22 + 10
+    for pos_z, end, R, p in targets:
+        np.testing.assert_array_equal(R.reshape(n, 3, 3), np.tile(np.diag([-1.0, 1.0, -1.0]), (n, 1, 1)))
+        np.testing.assert_array_equal(p[:, :2], end[:, :2])
+        assert np.all(p[:, 2] == pos_z)
+    P = np.ascontiguousarray(ro.env.arrays["arm_placement"], dtype=np.float64)
+    for before, R, p, after in recs:
+        for e in range(n):
+            want = arm_ik.ik_step(P, before[e], R[e].reshape(3, 3), p[e])
+            np.testing.assert_allclose(after[e], want, rtol=0, atol=1e-8 * max(1.0, np.abs(want - before[e]).max()))
