@@ -202,7 +202,8 @@ int rmbx_engine_create(const struct rmbx_model* model, int n_env, rmbx_engine** 
 int rmbx_engine_destroy(rmbx_engine* eng);
 int rmbx_engine_workspace_bytes(const rmbx_engine* eng, size_t* bytes);
 /* offset (in doubles, within one env's workspace slice) and element count of a named
- * workspace array (e.g. "M", "qfrc_bias", "qacc", "J"); per-env stride via "stride". */
+ * workspace array (e.g. "M", "qfrc_bias", "qacc", "J", "con_pos"); per-env stride via "stride".
+ * The int32 arrays "con_b1" / "con_b2" (contact bodies) report offsets in int32 units. */
 int rmbx_engine_ws_offset(const rmbx_engine* eng, const char* name, size_t* offset,
                           size_t* count);
 int rmbx_engine_bind(rmbx_engine* eng, const rmbx_env_buffers* bufs);

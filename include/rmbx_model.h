@@ -35,6 +35,7 @@ typedef struct rmbx_model {
   int32_t solver_iterations; /* Newton iterations (MuJoCo default 100) */
   int32_t ls_iterations;     /* exact line-search iterations cap */
   int32_t max_contacts;      /* contact capacity per env */
+  int32_t nhullvert;         /* convex-hull vertices of all mesh collision geoms */
   double timestep;
   double gravity[3];
   double meaninertia; /* mean diag(M) at qpos0 (mj_setConst) */
@@ -79,6 +80,11 @@ typedef struct rmbx_model {
   /* cameras [ncam] */
   const int32_t* cam_body;
   const double *cam_pos /*3*/, *cam_quat /*4*/, *cam_fovy;
+  /* convex hulls of mesh collision geoms (ctype RMBX_GEOM_MESH): geom g's vertices are
+     hull_vert[geom_hulladr[g] .. + geom_hullnum[g]] (3 each) in the geom's collision frame
+     (geom_cpos / geom_cquat); geom_hulladr -1 for other geoms */
+  const int32_t *geom_hulladr, *geom_hullnum;
+  const double* hull_vert; /* [nhullvert][3] */
 } rmbx_model;
 
 #ifdef __cplusplus

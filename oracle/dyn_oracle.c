@@ -57,7 +57,8 @@ typedef struct {
   int* efc_type; /* 0 equality, 1 inequality */
   double sensordata[6];
   int solver_iter;
-  int bad;
+  int bad;     /* substep of the last divergence reset (orc_step) */
+  int substep; /* 1-based substep being integrated */
 } Data;
 
 /* ------------------------------------------------------------------------------------------
@@ -844,6 +845,7 @@ static int col_box_box(const double* ca, const double* Ra, const double* ha, con
       bk = k;
     }
   }
+  if (bk < 0) return 0; /* non-finite geometry (a diverged env): no axis scored */
   double n[3] = {axes[bk][0], axes[bk][1], axes[bk][2]};
   if (dot3(n, dc) < 0) {
     n[0] = -n[0];
@@ -982,6 +984,441 @@ static int col_plane(const double* cp, const double* Rp, int tb, const double* c
   return k;
 }
 
+/* ------------------------------------------------------------------------------------------
+ * Convex narrow phase (meshes through their convex hulls, exact cylinders): MPR, restating
+ * libccd's ccdMPRPenetration (mpr.c) as MuJoCo 3.1.6's mjc_Convex calls it [ext]: support points
+ * of the Minkowski difference from the geoms' support functions (mjccd_support: sphere,
+ * capsule, cylinder, box, mesh hull; inflated by margin / 2), tolerance 1e-6 (mjOption
+ * mpr_tolerance), at most 50 refinement iterations (mpr_iterations); one contact per pair with
+ * dist = margin - depth, normal = the penetration direction (from geom 1 to geom 2) and
+ * position = the midpoint of the two witness points.
+ * ---------------------------------------------------------------------------------------- */
+#define CCD_EPS 2.2204460492503131e-16 /* DBL_EPSILON (libccd CCD_DOUBLE) */
+#define MPR_TOLERANCE 1e-6
+#define MPR_ITERATIONS 50
+
+typedef struct {
+  const double *c, *R, *s, *hv;
+  int type, nhv;
+  double margin;
+} ConvexObj;
+
+typedef struct {
+  double v[3], v1[3], v2[3];
+} SupportPt;
+
+static int ccd_is_zero(double x) { return fabs(x) < CCD_EPS; }
+static int ccd_eq(double a, double b) {
+  double ab = fabs(a - b);
+  if (ab < CCD_EPS) return 1;
+  double fa = fabs(a), fb = fabs(b);
+  return fb > fa ? ab < CCD_EPS * fb : ab < CCD_EPS * fa;
+}
+static int vec_eq(const double* a, const double* b) {
+  return ccd_eq(a[0], b[0]) && ccd_eq(a[1], b[1]) && ccd_eq(a[2], b[2]);
+}
+static void vec_normalize(double* v) {
+  double k = 1.0 / sqrt(dot3(v, v));
+  v[0] *= k;
+  v[1] *= k;
+  v[2] *= k;
+}
+static double sgn0(double x) { return x < 0 ? -1.0 : (x > 0 ? 1.0 : 0.0); }
+
+/* mjccd_support: farthest point of the object along the world direction dir */
+static void convex_support(const ConvexObj* o, const double* dir, double* out) {
+  double ld[3], res[3] = {0, 0, 0};
+  mattvec3(o->R, dir, ld);
+  const double* s = o->s;
+  if (o->type == RMBX_GEOM_SPHERE || o->type == RMBX_GEOM_CAPSULE) {
+    double n = norm3(ld);
+    if (n > MINVAL)
+      for (int i = 0; i < 3; i++) res[i] = ld[i] * (s[0] / n);
+    if (o->type == RMBX_GEOM_CAPSULE) res[2] += sgn0(ld[2]) * s[1];
+  } else if (o->type == RMBX_GEOM_CYLINDER) {
+    double n = sqrt(ld[0] * ld[0] + ld[1] * ld[1]);
+    if (n > MINVAL) {
+      res[0] = ld[0] * (s[0] / n);
+      res[1] = ld[1] * (s[0] / n);
+    }
+    res[2] = sgn0(ld[2]) * s[1];
+  } else if (o->type == RMBX_GEOM_BOX) {
+    for (int i = 0; i < 3; i++) res[i] = sgn0(ld[i]) * s[i];
+  } else { /* mesh: hull vertex of largest projection (first on ties) */
+    int best = 0;
+    double bd = -1e300;
+    for (int k = 0; k < o->nhv; k++) {
+      double dd = dot3(o->hv + 3 * k, ld);
+      if (dd > bd) {
+        bd = dd;
+        best = k;
+      }
+    }
+    for (int i = 0; i < 3; i++) res[i] = o->hv[3 * best + i];
+  }
+  if (o->margin > 0) {
+    double n = norm3(ld);
+    if (n > MINVAL)
+      for (int i = 0; i < 3; i++) res[i] += ld[i] * (0.5 * o->margin / n);
+  }
+  double w[3];
+  matvec3(o->R, res, w);
+  for (int i = 0; i < 3; i++) out[i] = o->c[i] + w[i];
+}
+
+static void mpr_support(const ConvexObj* a, const ConvexObj* b, const double* dir, SupportPt* p) {
+  double nd[3] = {-dir[0], -dir[1], -dir[2]};
+  convex_support(a, dir, p->v1);
+  convex_support(b, nd, p->v2);
+  for (int i = 0; i < 3; i++) p->v[i] = p->v1[i] - p->v2[i];
+}
+
+static double point_segment_dist2(const double* P, const double* x0, const double* b, double* witness) {
+  double d[3] = {b[0] - x0[0], b[1] - x0[1], b[2] - x0[2]}, a[3] = {x0[0] - P[0], x0[1] - P[1], x0[2] - P[2]};
+  double t = -1.0 * dot3(a, d);
+  t /= dot3(d, d);
+  double dist;
+  if (t < 0 || ccd_is_zero(t)) {
+    memcpy(witness, x0, sizeof(double) * 3);
+  } else if (t > 1 || ccd_eq(t, 1.0)) {
+    memcpy(witness, b, sizeof(double) * 3);
+  } else {
+    for (int i = 0; i < 3; i++) witness[i] = d[i] * t + x0[i];
+  }
+  double w[3] = {witness[0] - P[0], witness[1] - P[1], witness[2] - P[2]};
+  dist = dot3(w, w);
+  return dist;
+}
+
+/* ccdVec3PointTriDist2 with a witness point (here P is the origin) */
+static double point_tri_dist2(const double* P, const double* x0, const double* B, const double* C, double* witness) {
+  double d1[3], d2[3], a[3];
+  for (int i = 0; i < 3; i++) {
+    d1[i] = B[i] - x0[i];
+    d2[i] = C[i] - x0[i];
+    a[i] = x0[i] - P[i];
+  }
+  double v = dot3(d1, d1), w = dot3(d2, d2), p = dot3(a, d1), q = dot3(a, d2), r = dot3(d1, d2);
+  double dd = w * v - r * r, s, t;
+  if (ccd_is_zero(dd)) {
+    s = t = -1.0;
+  } else {
+    s = (q * r - w * p) / dd;
+    t = (-s * r - q) / w;
+  }
+  if ((ccd_is_zero(s) || s > 0) && (ccd_eq(s, 1.0) || s < 1) && (ccd_is_zero(t) || t > 0) &&
+      (ccd_eq(t, 1.0) || t < 1) && (ccd_eq(t + s, 1.0) || t + s < 1)) {
+    for (int i = 0; i < 3; i++) witness[i] = x0[i] + d1[i] * s + d2[i] * t;
+    double e[3] = {witness[0] - P[0], witness[1] - P[1], witness[2] - P[2]};
+    return dot3(e, e);
+  }
+  double w2[3];
+  double dist = point_segment_dist2(P, x0, B, witness);
+  double dist2 = point_segment_dist2(P, x0, C, w2);
+  if (dist2 < dist) {
+    dist = dist2;
+    memcpy(witness, w2, sizeof(w2));
+  }
+  dist2 = point_segment_dist2(P, B, C, w2);
+  if (dist2 < dist) {
+    dist = dist2;
+    memcpy(witness, w2, sizeof(w2));
+  }
+  return dist;
+}
+
+static void portal_dir(const SupportPt* pt, double* dir) {
+  double v2v1[3], v3v1[3];
+  for (int i = 0; i < 3; i++) {
+    v2v1[i] = pt[2].v[i] - pt[1].v[i];
+    v3v1[i] = pt[3].v[i] - pt[1].v[i];
+  }
+  cross3(v2v1, v3v1, dir);
+  vec_normalize(dir);
+}
+
+static int portal_reach_tolerance(const SupportPt* pt, const SupportPt* v4, const double* dir) {
+  double dv1 = dot3(pt[1].v, dir), dv2 = dot3(pt[2].v, dir), dv3 = dot3(pt[3].v, dir), dv4 = dot3(v4->v, dir);
+  double d1 = dv4 - dv1, d2 = dv4 - dv2, d3 = dv4 - dv3;
+  d1 = d1 < d2 ? d1 : d2;
+  d1 = d1 < d3 ? d1 : d3;
+  return ccd_eq(d1, MPR_TOLERANCE) || d1 < MPR_TOLERANCE;
+}
+
+static void expand_portal(SupportPt* pt, const SupportPt* v4) {
+  double v4v0[3];
+  cross3(v4->v, pt[0].v, v4v0);
+  double dot = dot3(pt[1].v, v4v0);
+  if (dot > 0) {
+    dot = dot3(pt[2].v, v4v0);
+    if (dot > 0)
+      pt[1] = *v4;
+    else
+      pt[3] = *v4;
+  } else {
+    dot = dot3(pt[3].v, v4v0);
+    if (dot > 0)
+      pt[2] = *v4;
+    else
+      pt[1] = *v4;
+  }
+}
+
+/* 0 portal found, 1 origin on v1 (touch), 2 origin on segment v0-v1, -1 no intersection */
+static int discover_portal(const ConvexObj* a, const ConvexObj* b, SupportPt* pt) {
+  double dir[3], va[3], vb[3];
+  memcpy(pt[0].v1, a->c, sizeof(double) * 3);
+  memcpy(pt[0].v2, b->c, sizeof(double) * 3);
+  for (int i = 0; i < 3; i++) pt[0].v[i] = pt[0].v1[i] - pt[0].v2[i];
+  const double zero[3] = {0, 0, 0};
+  if (vec_eq(pt[0].v, zero)) pt[0].v[0] += CCD_EPS * 10.0;
+  for (int i = 0; i < 3; i++) dir[i] = -pt[0].v[i];
+  vec_normalize(dir);
+  mpr_support(a, b, dir, &pt[1]);
+  double dot = dot3(pt[1].v, dir);
+  if (ccd_is_zero(dot) || dot < 0) return -1;
+  cross3(pt[0].v, pt[1].v, dir);
+  if (ccd_is_zero(dot3(dir, dir))) return vec_eq(pt[1].v, zero) ? 1 : 2;
+  vec_normalize(dir);
+  mpr_support(a, b, dir, &pt[2]);
+  dot = dot3(pt[2].v, dir);
+  if (ccd_is_zero(dot) || dot < 0) return -1;
+  for (int i = 0; i < 3; i++) {
+    va[i] = pt[1].v[i] - pt[0].v[i];
+    vb[i] = pt[2].v[i] - pt[0].v[i];
+  }
+  cross3(va, vb, dir);
+  vec_normalize(dir);
+  if (dot3(dir, pt[0].v) > 0) {
+    SupportPt t = pt[1];
+    pt[1] = pt[2];
+    pt[2] = t;
+    for (int i = 0; i < 3; i++) dir[i] = -dir[i];
+  }
+  for (int guard = 0; guard < 1000; guard++) {
+    mpr_support(a, b, dir, &pt[3]);
+    dot = dot3(pt[3].v, dir);
+    if (ccd_is_zero(dot) || dot < 0) return -1;
+    int cont = 0;
+    cross3(pt[1].v, pt[3].v, va);
+    dot = dot3(va, pt[0].v);
+    if (dot < 0 && !ccd_is_zero(dot)) {
+      pt[2] = pt[3];
+      cont = 1;
+    }
+    if (!cont) {
+      cross3(pt[3].v, pt[2].v, va);
+      dot = dot3(va, pt[0].v);
+      if (dot < 0 && !ccd_is_zero(dot)) {
+        pt[1] = pt[3];
+        cont = 1;
+      }
+    }
+    if (!cont) return 0;
+    for (int i = 0; i < 3; i++) {
+      va[i] = pt[1].v[i] - pt[0].v[i];
+      vb[i] = pt[2].v[i] - pt[0].v[i];
+    }
+    cross3(va, vb, dir);
+    vec_normalize(dir);
+  }
+  return -1;
+}
+
+static int refine_portal(const ConvexObj* a, const ConvexObj* b, SupportPt* pt) {
+  double dir[3];
+  SupportPt v4;
+  for (int guard = 0; guard < 1000; guard++) {
+    portal_dir(pt, dir);
+    double dot = dot3(pt[1].v, dir);
+    if (ccd_is_zero(dot) || dot > 0) return 0; /* portal encapsulates the origin */
+    mpr_support(a, b, dir, &v4);
+    dot = dot3(v4.v, dir);
+    if (!(ccd_is_zero(dot) || dot > 0) || portal_reach_tolerance(pt, &v4, dir)) return -1;
+    expand_portal(pt, &v4);
+  }
+  return -1;
+}
+
+static void find_pos(const SupportPt* pt, double* pos) {
+  double dir[3], vec[3], bc[4];
+  portal_dir(pt, dir);
+  cross3(pt[1].v, pt[2].v, vec);
+  bc[0] = dot3(vec, pt[3].v);
+  cross3(pt[3].v, pt[2].v, vec);
+  bc[1] = dot3(vec, pt[0].v);
+  cross3(pt[0].v, pt[1].v, vec);
+  bc[2] = dot3(vec, pt[3].v);
+  cross3(pt[2].v, pt[1].v, vec);
+  bc[3] = dot3(vec, pt[0].v);
+  double sum = bc[0] + bc[1] + bc[2] + bc[3];
+  if (ccd_is_zero(sum) || sum < 0) {
+    bc[0] = 0;
+    cross3(pt[2].v, pt[3].v, vec);
+    bc[1] = dot3(vec, dir);
+    cross3(pt[3].v, pt[1].v, vec);
+    bc[2] = dot3(vec, dir);
+    cross3(pt[1].v, pt[2].v, vec);
+    bc[3] = dot3(vec, dir);
+    sum = bc[1] + bc[2] + bc[3];
+  }
+  double inv = 1.0 / sum, p1[3] = {0, 0, 0}, p2[3] = {0, 0, 0};
+  for (int k = 0; k < 4; k++)
+    for (int i = 0; i < 3; i++) {
+      p1[i] += pt[k].v1[i] * bc[k];
+      p2[i] += pt[k].v2[i] * bc[k];
+    }
+  for (int i = 0; i < 3; i++) pos[i] = (p1[i] * inv + p2[i] * inv) * 0.5;
+}
+
+/* 1 with (depth, dir, pos) when the objects intersect, else 0 */
+static int mpr_penetration(const ConvexObj* a, const ConvexObj* b, double* depth, double* dir, double* pos) {
+  SupportPt pt[4];
+  int res = discover_portal(a, b, pt);
+  if (res < 0) return 0;
+  if (res == 1) { /* touching contact: no normal */
+    *depth = 0;
+    dir[0] = dir[1] = dir[2] = 0;
+    for (int i = 0; i < 3; i++) pos[i] = (pt[1].v1[i] + pt[1].v2[i]) * 0.5;
+    return 1;
+  }
+  if (res == 2) { /* origin on the segment v0-v1 */
+    for (int i = 0; i < 3; i++) {
+      pos[i] = (pt[1].v1[i] + pt[1].v2[i]) * 0.5;
+      dir[i] = pt[1].v[i];
+    }
+    *depth = sqrt(dot3(dir, dir));
+    vec_normalize(dir);
+    return 1;
+  }
+  if (refine_portal(a, b, pt) < 0) return 0;
+  SupportPt v4;
+  for (int it = 0;; it++) {
+    double pd[3];
+    portal_dir(pt, pd);
+    mpr_support(a, b, pd, &v4);
+    if (portal_reach_tolerance(pt, &v4, pd) || it > MPR_ITERATIONS) {
+      const double zero[3] = {0, 0, 0};
+      *depth = sqrt(point_tri_dist2(zero, pt[1].v, pt[2].v, pt[3].v, dir));
+      if (ccd_is_zero(*depth))
+        dir[0] = dir[1] = dir[2] = 0;
+      else
+        vec_normalize(dir);
+      find_pos(pt, pos);
+      return 1;
+    }
+    expand_portal(pt, &v4);
+  }
+}
+
+static void convex_obj(const Data* d, int g, double margin, ConvexObj* o) {
+  const rmbx_model* m = d->m;
+  o->c = d->gxpos + 3 * g;
+  o->R = d->gxmat + 9 * g;
+  o->s = m->geom_csize + 3 * g;
+  o->type = m->geom_ctype[g];
+  o->hv = o->type == RMBX_GEOM_MESH ? m->hull_vert + 3 * m->geom_hulladr[g] : NULL;
+  o->nhv = o->type == RMBX_GEOM_MESH ? m->geom_hullnum[g] : 0;
+  o->margin = margin;
+}
+
+/* mjc_Convex: one contact from MPR (normal from A to B) */
+static int col_convex(const Data* d, int ga, int gb, double margin, Contact* out) {
+  ConvexObj a, b;
+  convex_obj(d, ga, margin, &a);
+  convex_obj(d, gb, margin, &b);
+  double depth, dir[3], pos[3];
+  if (!mpr_penetration(&a, &b, &depth, dir, pos)) return 0;
+  if (dir[0] == 0 && dir[1] == 0 && dir[2] == 0) return 0; /* touching: normal undefined */
+  double dist = margin - depth;
+  if (dist >= margin) return 0;
+  memcpy(out->n, dir, sizeof(dir));
+  memcpy(out->pos, pos, sizeof(pos));
+  out->dist = dist;
+  return 1;
+}
+
+/* stable top-4 of a candidate stream by contact_deeper (earlier candidates win ties) */
+static void top4_insert(Contact* best, int* nb, const Contact* c) {
+  int k = *nb < 4 ? *nb : 4;
+  int at = k;
+  while (at > 0 && contact_deeper(c, &best[at - 1])) at--;
+  if (at >= 4) return;
+  for (int i = (k < 4 ? k : 3); i > at; i--) best[i] = best[i - 1];
+  best[at] = *c;
+  if (*nb < 4) (*nb)++;
+}
+
+/* plane (A, normal = local z) vs a convex hull (B): every hull vertex below the margin is a
+ * candidate, the 4 deepest are kept (mjc_PlaneConvex's vertex contacts) */
+static int col_plane_mesh(const double* cp, const double* Rp, const double* cb, const double* Rb,
+                          const double* hv, int nhv, double margin, Contact* out) {
+  double n[3] = {Rp[2], Rp[5], Rp[8]};
+  int nb = 0;
+  for (int k = 0; k < nhv; k++) {
+    double w[3], x[3];
+    matvec3(Rb, hv + 3 * k, w);
+    for (int i = 0; i < 3; i++) x[i] = cb[i] + w[i];
+    double v[3] = {x[0] - cp[0], x[1] - cp[1], x[2] - cp[2]};
+    Contact c;
+    c.dist = dot3(v, n);
+    if (c.dist >= margin) continue;
+    for (int i = 0; i < 3; i++) {
+      c.n[i] = n[i];
+      c.pos[i] = x[i] - n[i] * (0.5 * c.dist);
+    }
+    top4_insert(out, &nb, &c);
+  }
+  return nb;
+}
+
+/* plane (A) vs cylinder (B), after mjc_PlaneCylinder: the deepest rim point of each disk and
+ * two more rim points of the deeper disk forming an equilateral triangle with its deepest */
+static int col_plane_cylinder(const double* cp, const double* Rp, const double* cb, const double* Rb,
+                              const double* sb, double margin, Contact* out) {
+  double n[3] = {Rp[2], Rp[5], Rp[8]}, ax[3] = {Rb[2], Rb[5], Rb[8]};
+  double r = sb[0], h = sb[1];
+  double prj = dot3(n, ax);
+  double u[3] = {-(n[0] - prj * ax[0]), -(n[1] - prj * ax[1]), -(n[2] - prj * ax[2])};
+  double lu = norm3(u), v[3];
+  if (lu < 1e-12) { /* axis along the normal: the disk's own x / y axes */
+    u[0] = Rb[0];
+    u[1] = Rb[3];
+    u[2] = Rb[6];
+  } else {
+    for (int i = 0; i < 3; i++) u[i] /= lu;
+  }
+  cross3(ax, u, v);
+  /* the deeper disk is the one whose centre lies further along -n */
+  double sgn = prj > 0 ? -1.0 : 1.0; /* cap at c + sgn h ax is the deeper one */
+  double cd[3], cs[3];
+  for (int i = 0; i < 3; i++) {
+    cd[i] = cb[i] + sgn * h * ax[i];
+    cs[i] = cb[i] - sgn * h * ax[i];
+  }
+  double pts[4][3];
+  const double s3 = 0.86602540378443864676;
+  for (int i = 0; i < 3; i++) {
+    pts[0][i] = cd[i] + r * u[i];
+    pts[1][i] = cs[i] + r * u[i];
+    pts[2][i] = cd[i] - 0.5 * r * u[i] + s3 * r * v[i];
+    pts[3][i] = cd[i] - 0.5 * r * u[i] - s3 * r * v[i];
+  }
+  int nb = 0;
+  for (int k = 0; k < 4; k++) {
+    double w[3] = {pts[k][0] - cp[0], pts[k][1] - cp[1], pts[k][2] - cp[2]};
+    Contact c;
+    c.dist = dot3(w, n);
+    if (c.dist >= margin) continue;
+    for (int i = 0; i < 3; i++) {
+      c.n[i] = n[i];
+      c.pos[i] = pts[k][i] - n[i] * (0.5 * c.dist);
+    }
+    top4_insert(out, &nb, &c);
+  }
+  return nb;
+}
+
 static int narrowphase(Data* d, int g1, int g2, double margin, Contact* out) {
   const rmbx_model* m = d->m;
   int t1 = m->geom_ctype[g1], t2 = m->geom_ctype[g2];
@@ -998,8 +1435,14 @@ static int narrowphase(Data* d, int g1, int g2, double margin, Contact* out) {
   const double *c1 = d->gxpos + 3 * g1, *R1 = d->gxmat + 9 * g1, *s1 = m->geom_csize + 3 * g1;
   const double *c2 = d->gxpos + 3 * g2, *R2 = d->gxmat + 9 * g2, *s2 = m->geom_csize + 3 * g2;
   int n = 0;
-  if (t1 == RMBX_GEOM_PLANE) {
+  if (t1 == RMBX_GEOM_PLANE && t2 == RMBX_GEOM_MESH) {
+    n = col_plane_mesh(c1, R1, c2, R2, m->hull_vert + 3 * m->geom_hulladr[g2], m->geom_hullnum[g2], margin, out);
+  } else if (t1 == RMBX_GEOM_PLANE && t2 == RMBX_GEOM_CYLINDER) {
+    n = col_plane_cylinder(c1, R1, c2, R2, s2, margin, out);
+  } else if (t1 == RMBX_GEOM_PLANE) {
     n = col_plane(c1, R1, t2, c2, R2, s2, margin, out);
+  } else if (t2 == RMBX_GEOM_MESH || t2 == RMBX_GEOM_CYLINDER) {
+    n = col_convex(d, g1, g2, margin, out);
   } else if (t1 == RMBX_GEOM_SPHERE && t2 == RMBX_GEOM_SPHERE) {
     n = col_sphere_sphere(c1, s1[0], c2, s2[0], margin, out);
   } else if (t1 == RMBX_GEOM_SPHERE && t2 == RMBX_GEOM_CAPSULE) {
@@ -1030,7 +1473,7 @@ static void geom_aabb(const Data* d, int g, double* lo, double* hi) {
     double e;
     if (t == RMBX_GEOM_SPHERE)
       e = s[0];
-    else if (t == RMBX_GEOM_CAPSULE)
+    else if (t == RMBX_GEOM_CAPSULE || t == RMBX_GEOM_CYLINDER)
       e = fabs(R[3 * i + 2]) * s[1] + s[0];
     else
       e = fabs(R[3 * i]) * s[0] + fabs(R[3 * i + 1]) * s[1] + fabs(R[3 * i + 2]) * s[2];
@@ -1060,9 +1503,14 @@ static void make_frame(const double* n, double* F) {
   memcpy(F + 6, t2, sizeof(t2));
 }
 
+/* broadphase survivors taken into the narrow phase: at most this many, in pair order (the
+ * engine's LDS survivor list has the same cap) */
+#define MAX_CANDIDATES 2048
+
 static void collision(Data* d) {
   const rmbx_model* m = d->m;
   d->ncon = 0;
+  int cap = m->npair < MAX_CANDIDATES ? m->npair : MAX_CANDIDATES, nsurv = 0;
   for (int p = 0; p < m->npair; p++) {
     int g1 = m->pair_geom1[p], g2 = m->pair_geom2[p];
     double margin = m->pair_margin[p];
@@ -1083,6 +1531,8 @@ static void collision(Data* d) {
         if (lo1[i] > hi2[i] + margin || lo2[i] > hi1[i] + margin) sep = 1;
       if (sep) continue;
     }
+    if (nsurv >= cap) break;
+    nsurv++;
     Contact c[MAXCON_PAIR];
     int n = narrowphase(d, g1, g2, margin, c);
     for (int i = 0; i < n && d->ncon < m->max_contacts; i++) {
@@ -1565,6 +2015,17 @@ static void integrate(Data* d) {
   cholesky(d->A, nv);
   for (int k = 0; k < nv; k++) d->tmpv[k] = d->qfrc_smooth[k] + d->qfrc_constraint[k];
   chol_solve(d->A, nv, d->tmpv, d->qacc);
+  for (int k = 0; k < nv; k++)
+    if (!isfinite(d->qacc[k]) || fabs(d->qacc[k]) > 1e10) {
+      /* MuJoCo's mj_checkAcc -> mj_resetData: qpos0, zero velocity / warm start / ctrl, time 0 */
+      memcpy(d->qpos, m->qpos0, sizeof(double) * m->nq);
+      memset(d->qvel, 0, sizeof(double) * nv);
+      memset(d->qacc_ws, 0, sizeof(double) * nv);
+      memset(d->ctrl, 0, sizeof(double) * m->nu);
+      d->time = 0;
+      d->bad = d->substep;
+      return;
+    }
   for (int k = 0; k < nv; k++) d->qvel[k] += h * d->qacc[k];
   memcpy(d->qacc_ws, d->qacc, sizeof(double) * nv);
   for (int j = 0; j < m->njnt; j++) {
@@ -1586,12 +2047,6 @@ static void integrate(Data* d) {
   d->time += h;
 }
 
-static int finite_state(const Data* d) {
-  for (int k = 0; k < d->m->nv; k++)
-    if (!isfinite(d->qacc[k]) || fabs(d->qacc[k]) > 1e10) return 0;
-  return 1;
-}
-
 void orc_forward(void* p) {
   Data* d = (Data*)p;
   kinematics(d);
@@ -1609,12 +2064,15 @@ void orc_forward(void* p) {
   sensors(d);
 }
 
+/* returns the 1-based substep of the last divergence reset in this call (0: none), the
+ * engine's stats[3] */
 int orc_step(void* p, int nsub) {
   Data* d = (Data*)p;
+  d->bad = 0;
   for (int s = 0; s < nsub; s++) {
+    d->substep = s + 1;
     orc_forward(d);
     integrate(d);
-    if (!finite_state(d)) d->bad = 1;
   }
   return d->bad;
 }

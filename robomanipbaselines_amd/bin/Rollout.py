@@ -19,7 +19,7 @@ import sys
 import yaml
 
 POLICIES = ["Mlp", "Act", "DiffusionPolicy", "DiffusionPolicy3d"]
-ENVS = ["MujocoUR5eCable", "MujocoUR5eInsert", "MujocoUR5eDoor", "MujocoUR5eCabinet", "MujocoUR5eToolbox"]
+ENVS = ["MujocoUR5eCable", "MujocoUR5eInsert", "MujocoUR5eDoor", "MujocoUR5eCabinet", "MujocoUR5eToolbox", "MujocoUR5ePick"]
 
 
 def camel_to_snake(name):

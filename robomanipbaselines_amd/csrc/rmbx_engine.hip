@@ -777,6 +777,7 @@ __device__ int col_box_box(const double* ca, const double* Ra, const double* ha,
       bk = k;
     }
   }
+  if (bk < 0) return 0; /* non-finite geometry (a diverged env): no axis scored */
   double n[3] = {axes[bk][0], axes[bk][1], axes[bk][2]};
   if (dot3(n, dc) < 0) {
     n[0] = -n[0];
@@ -911,10 +912,438 @@ __device__ int col_plane(const double* cp, const double* Rp, int tb, const doubl
   return k;
 }
 
+// Convex narrow phase: MPR (libccd's ccdMPRPenetration as MuJoCo 3.1.6's mjc_Convex calls it,
+// [ext]) for pairs with a convex-hull mesh or a cylinder; the same algorithm and operation
+// order as oracle/dyn_oracle.c (tolerance 1e-6, at most 50 refinement iterations, supports
+// inflated by margin / 2, one contact: dist = margin - depth, normal from geom 1 to geom 2,
+// position = the witness points' midpoint).  One lane per pair; the hull support is a serial
+// scan of the hull's vertices (<= 64 for the scanned objects).
+#define CCD_EPS 2.2204460492503131e-16
+#define MPR_TOLERANCE 1e-6
+#define MPR_ITERATIONS 50
+
+struct ConvexObj {
+  const double *c, *R, *s, *hv;
+  int type, nhv;
+  double margin;
+};
+struct SupportPt {
+  double v[3], v1[3], v2[3];
+};
+
+__device__ __forceinline__ bool ccd_is_zero(double x) { return fabs(x) < CCD_EPS; }
+__device__ __forceinline__ bool ccd_eq(double a, double b) {
+  const double ab = fabs(a - b);
+  if (ab < CCD_EPS) return true;
+  const double fa = fabs(a), fb = fabs(b);
+  return fb > fa ? ab < CCD_EPS * fb : ab < CCD_EPS * fa;
+}
+__device__ __forceinline__ bool vec_eq0(const double* a) {
+  return ccd_eq(a[0], 0.0) && ccd_eq(a[1], 0.0) && ccd_eq(a[2], 0.0);
+}
+__device__ __forceinline__ void vec_normalize(double* v) {
+  const double k = 1.0 / sqrt(dot3(v, v));
+  v[0] *= k;
+  v[1] *= k;
+  v[2] *= k;
+}
+__device__ __forceinline__ double sgn0(double x) { return x < 0 ? -1.0 : (x > 0 ? 1.0 : 0.0); }
+
+__device__ void convex_support(const ConvexObj& o, const double* dir, double* out) {
+  double ld[3], res[3] = {0, 0, 0};
+  mattvec3(o.R, dir, ld);
+  const double* s = o.s;
+  if (o.type == RMBX_GEOM_SPHERE || o.type == RMBX_GEOM_CAPSULE) {
+    const double n = norm3(ld);
+    if (n > RMBX_MINVAL)
+      for (int i = 0; i < 3; i++) res[i] = ld[i] * (s[0] / n);
+    if (o.type == RMBX_GEOM_CAPSULE) res[2] += sgn0(ld[2]) * s[1];
+  } else if (o.type == RMBX_GEOM_CYLINDER) {
+    const double n = sqrt(ld[0] * ld[0] + ld[1] * ld[1]);
+    if (n > RMBX_MINVAL) {
+      res[0] = ld[0] * (s[0] / n);
+      res[1] = ld[1] * (s[0] / n);
+    }
+    res[2] = sgn0(ld[2]) * s[1];
+  } else if (o.type == RMBX_GEOM_BOX) {
+    for (int i = 0; i < 3; i++) res[i] = sgn0(ld[i]) * s[i];
+  } else {
+    int best = 0;
+    double bd = -1e300;
+    for (int k = 0; k < o.nhv; k++) {
+      const double dd = dot3(o.hv + 3 * k, ld);
+      if (dd > bd) {
+        bd = dd;
+        best = k;
+      }
+    }
+    for (int i = 0; i < 3; i++) res[i] = o.hv[3 * best + i];
+  }
+  if (o.margin > 0) {
+    const double n = norm3(ld);
+    if (n > RMBX_MINVAL)
+      for (int i = 0; i < 3; i++) res[i] += ld[i] * (0.5 * o.margin / n);
+  }
+  double w[3];
+  matvec3(o.R, res, w);
+  for (int i = 0; i < 3; i++) out[i] = o.c[i] + w[i];
+}
+
+__device__ void mpr_support(const ConvexObj& a, const ConvexObj& b, const double* dir, SupportPt& p) {
+  const double nd[3] = {-dir[0], -dir[1], -dir[2]};
+  convex_support(a, dir, p.v1);
+  convex_support(b, nd, p.v2);
+  for (int i = 0; i < 3; i++) p.v[i] = p.v1[i] - p.v2[i];
+}
+
+__device__ double point_segment_dist2(const double* P, const double* x0, const double* b, double* witness) {
+  const double d[3] = {b[0] - x0[0], b[1] - x0[1], b[2] - x0[2]};
+  const double a[3] = {x0[0] - P[0], x0[1] - P[1], x0[2] - P[2]};
+  double t = -1.0 * dot3(a, d);
+  t /= dot3(d, d);
+  if (t < 0 || ccd_is_zero(t)) {
+    for (int i = 0; i < 3; i++) witness[i] = x0[i];
+  } else if (t > 1 || ccd_eq(t, 1.0)) {
+    for (int i = 0; i < 3; i++) witness[i] = b[i];
+  } else {
+    for (int i = 0; i < 3; i++) witness[i] = d[i] * t + x0[i];
+  }
+  const double w[3] = {witness[0] - P[0], witness[1] - P[1], witness[2] - P[2]};
+  return dot3(w, w);
+}
+
+__device__ double point_tri_dist2(const double* P, const double* x0, const double* B, const double* C,
+                                  double* witness) {
+  double d1[3], d2[3], a[3];
+  for (int i = 0; i < 3; i++) {
+    d1[i] = B[i] - x0[i];
+    d2[i] = C[i] - x0[i];
+    a[i] = x0[i] - P[i];
+  }
+  const double v = dot3(d1, d1), w = dot3(d2, d2), p = dot3(a, d1), q = dot3(a, d2), r = dot3(d1, d2);
+  const double dd = w * v - r * r;
+  double s, t;
+  if (ccd_is_zero(dd)) {
+    s = t = -1.0;
+  } else {
+    s = (q * r - w * p) / dd;
+    t = (-s * r - q) / w;
+  }
+  if ((ccd_is_zero(s) || s > 0) && (ccd_eq(s, 1.0) || s < 1) && (ccd_is_zero(t) || t > 0) &&
+      (ccd_eq(t, 1.0) || t < 1) && (ccd_eq(t + s, 1.0) || t + s < 1)) {
+    for (int i = 0; i < 3; i++) witness[i] = x0[i] + d1[i] * s + d2[i] * t;
+    const double e3[3] = {witness[0] - P[0], witness[1] - P[1], witness[2] - P[2]};
+    return dot3(e3, e3);
+  }
+  double w2[3];
+  double dist = point_segment_dist2(P, x0, B, witness);
+  double dist2 = point_segment_dist2(P, x0, C, w2);
+  if (dist2 < dist) {
+    dist = dist2;
+    for (int i = 0; i < 3; i++) witness[i] = w2[i];
+  }
+  dist2 = point_segment_dist2(P, B, C, w2);
+  if (dist2 < dist) {
+    dist = dist2;
+    for (int i = 0; i < 3; i++) witness[i] = w2[i];
+  }
+  return dist;
+}
+
+__device__ void portal_dir(const SupportPt* pt, double* dir) {
+  double v2v1[3], v3v1[3];
+  for (int i = 0; i < 3; i++) {
+    v2v1[i] = pt[2].v[i] - pt[1].v[i];
+    v3v1[i] = pt[3].v[i] - pt[1].v[i];
+  }
+  cross3(v2v1, v3v1, dir);
+  vec_normalize(dir);
+}
+
+__device__ bool portal_reach_tolerance(const SupportPt* pt, const SupportPt& v4, const double* dir) {
+  const double dv1 = dot3(pt[1].v, dir), dv2 = dot3(pt[2].v, dir), dv3 = dot3(pt[3].v, dir), dv4 = dot3(v4.v, dir);
+  double d1 = dv4 - dv1;
+  const double d2 = dv4 - dv2, d3 = dv4 - dv3;
+  d1 = d1 < d2 ? d1 : d2;
+  d1 = d1 < d3 ? d1 : d3;
+  return ccd_eq(d1, MPR_TOLERANCE) || d1 < MPR_TOLERANCE;
+}
+
+__device__ void expand_portal(SupportPt* pt, const SupportPt& v4) {
+  double v4v0[3];
+  cross3(v4.v, pt[0].v, v4v0);
+  double dot = dot3(pt[1].v, v4v0);
+  if (dot > 0) {
+    dot = dot3(pt[2].v, v4v0);
+    if (dot > 0)
+      pt[1] = v4;
+    else
+      pt[3] = v4;
+  } else {
+    dot = dot3(pt[3].v, v4v0);
+    if (dot > 0)
+      pt[2] = v4;
+    else
+      pt[1] = v4;
+  }
+}
+
+__device__ int discover_portal(const ConvexObj& a, const ConvexObj& b, SupportPt* pt) {
+  double dir[3], va[3], vb[3];
+  for (int i = 0; i < 3; i++) {
+    pt[0].v1[i] = a.c[i];
+    pt[0].v2[i] = b.c[i];
+    pt[0].v[i] = pt[0].v1[i] - pt[0].v2[i];
+  }
+  if (vec_eq0(pt[0].v)) pt[0].v[0] += CCD_EPS * 10.0;
+  for (int i = 0; i < 3; i++) dir[i] = -pt[0].v[i];
+  vec_normalize(dir);
+  mpr_support(a, b, dir, pt[1]);
+  double dot = dot3(pt[1].v, dir);
+  if (ccd_is_zero(dot) || dot < 0) return -1;
+  cross3(pt[0].v, pt[1].v, dir);
+  if (ccd_is_zero(dot3(dir, dir))) return vec_eq0(pt[1].v) ? 1 : 2;
+  vec_normalize(dir);
+  mpr_support(a, b, dir, pt[2]);
+  dot = dot3(pt[2].v, dir);
+  if (ccd_is_zero(dot) || dot < 0) return -1;
+  for (int i = 0; i < 3; i++) {
+    va[i] = pt[1].v[i] - pt[0].v[i];
+    vb[i] = pt[2].v[i] - pt[0].v[i];
+  }
+  cross3(va, vb, dir);
+  vec_normalize(dir);
+  if (dot3(dir, pt[0].v) > 0) {
+    const SupportPt t = pt[1];
+    pt[1] = pt[2];
+    pt[2] = t;
+    for (int i = 0; i < 3; i++) dir[i] = -dir[i];
+  }
+  for (int guard = 0; guard < 1000; guard++) {
+    mpr_support(a, b, dir, pt[3]);
+    dot = dot3(pt[3].v, dir);
+    if (ccd_is_zero(dot) || dot < 0) return -1;
+    bool cont = false;
+    cross3(pt[1].v, pt[3].v, va);
+    dot = dot3(va, pt[0].v);
+    if (dot < 0 && !ccd_is_zero(dot)) {
+      pt[2] = pt[3];
+      cont = true;
+    }
+    if (!cont) {
+      cross3(pt[3].v, pt[2].v, va);
+      dot = dot3(va, pt[0].v);
+      if (dot < 0 && !ccd_is_zero(dot)) {
+        pt[1] = pt[3];
+        cont = true;
+      }
+    }
+    if (!cont) return 0;
+    for (int i = 0; i < 3; i++) {
+      va[i] = pt[1].v[i] - pt[0].v[i];
+      vb[i] = pt[2].v[i] - pt[0].v[i];
+    }
+    cross3(va, vb, dir);
+    vec_normalize(dir);
+  }
+  return -1;
+}
+
+__device__ int refine_portal(const ConvexObj& a, const ConvexObj& b, SupportPt* pt) {
+  double dir[3];
+  SupportPt v4;
+  for (int guard = 0; guard < 1000; guard++) {
+    portal_dir(pt, dir);
+    double dot = dot3(pt[1].v, dir);
+    if (ccd_is_zero(dot) || dot > 0) return 0;
+    mpr_support(a, b, dir, v4);
+    dot = dot3(v4.v, dir);
+    if (!(ccd_is_zero(dot) || dot > 0) || portal_reach_tolerance(pt, v4, dir)) return -1;
+    expand_portal(pt, v4);
+  }
+  return -1;
+}
+
+__device__ void find_pos(const SupportPt* pt, double* pos) {
+  double dir[3], vec[3], bc[4];
+  portal_dir(pt, dir);
+  cross3(pt[1].v, pt[2].v, vec);
+  bc[0] = dot3(vec, pt[3].v);
+  cross3(pt[3].v, pt[2].v, vec);
+  bc[1] = dot3(vec, pt[0].v);
+  cross3(pt[0].v, pt[1].v, vec);
+  bc[2] = dot3(vec, pt[3].v);
+  cross3(pt[2].v, pt[1].v, vec);
+  bc[3] = dot3(vec, pt[0].v);
+  double sum = bc[0] + bc[1] + bc[2] + bc[3];
+  if (ccd_is_zero(sum) || sum < 0) {
+    bc[0] = 0;
+    cross3(pt[2].v, pt[3].v, vec);
+    bc[1] = dot3(vec, dir);
+    cross3(pt[3].v, pt[1].v, vec);
+    bc[2] = dot3(vec, dir);
+    cross3(pt[1].v, pt[2].v, vec);
+    bc[3] = dot3(vec, dir);
+    sum = bc[1] + bc[2] + bc[3];
+  }
+  const double inv = 1.0 / sum;
+  double p1[3] = {0, 0, 0}, p2[3] = {0, 0, 0};
+  for (int k = 0; k < 4; k++)
+    for (int i = 0; i < 3; i++) {
+      p1[i] += pt[k].v1[i] * bc[k];
+      p2[i] += pt[k].v2[i] * bc[k];
+    }
+  for (int i = 0; i < 3; i++) pos[i] = (p1[i] * inv + p2[i] * inv) * 0.5;
+}
+
+__device__ bool mpr_penetration(const ConvexObj& a, const ConvexObj& b, double* depth, double* dir, double* pos) {
+  SupportPt pt[4];
+  const int res = discover_portal(a, b, pt);
+  if (res < 0) return false;
+  if (res == 1) {
+    *depth = 0;
+    dir[0] = dir[1] = dir[2] = 0;
+    for (int i = 0; i < 3; i++) pos[i] = (pt[1].v1[i] + pt[1].v2[i]) * 0.5;
+    return true;
+  }
+  if (res == 2) {
+    for (int i = 0; i < 3; i++) {
+      pos[i] = (pt[1].v1[i] + pt[1].v2[i]) * 0.5;
+      dir[i] = pt[1].v[i];
+    }
+    *depth = sqrt(dot3(dir, dir));
+    vec_normalize(dir);
+    return true;
+  }
+  if (refine_portal(a, b, pt) < 0) return false;
+  SupportPt v4;
+  for (int it = 0;; it++) {
+    double pd[3];
+    portal_dir(pt, pd);
+    mpr_support(a, b, pd, v4);
+    if (portal_reach_tolerance(pt, v4, pd) || it > MPR_ITERATIONS) {
+      const double zero[3] = {0, 0, 0};
+      *depth = sqrt(point_tri_dist2(zero, pt[1].v, pt[2].v, pt[3].v, dir));
+      if (ccd_is_zero(*depth))
+        dir[0] = dir[1] = dir[2] = 0;
+      else
+        vec_normalize(dir);
+      find_pos(pt, pos);
+      return true;
+    }
+    expand_portal(pt, v4);
+  }
+}
+
+__device__ void convex_obj(const Env& e, int g, double margin, ConvexObj& o) {
+  const rmbx_model& m = *e.m;
+  o.c = e.gxpos + 3 * g;
+  o.R = e.gxmat + 9 * g;
+  o.s = m.geom_csize + 3 * g;
+  o.type = m.geom_ctype[g];
+  o.hv = o.type == RMBX_GEOM_MESH ? m.hull_vert + 3 * m.geom_hulladr[g] : nullptr;
+  o.nhv = o.type == RMBX_GEOM_MESH ? m.geom_hullnum[g] : 0;
+  o.margin = margin;
+}
+
+__device__ int col_convex(const Env& e, int ga, int gb, double margin, Contact* out) {
+  ConvexObj a, b;
+  convex_obj(e, ga, margin, a);
+  convex_obj(e, gb, margin, b);
+  double depth, dir[3], pos[3];
+  if (!mpr_penetration(a, b, &depth, dir, pos)) return 0;
+  if (dir[0] == 0 && dir[1] == 0 && dir[2] == 0) return 0;
+  const double dist = margin - depth;
+  if (dist >= margin) return 0;
+  for (int i = 0; i < 3; i++) {
+    out->n[i] = dir[i];
+    out->pos[i] = pos[i];
+  }
+  out->dist = dist;
+  return 1;
+}
+
+// stable top-4 of a candidate stream by contact_deeper (earlier candidates win ties)
+__device__ void top4_insert(Contact* best, int* nb, const Contact& c) {
+  const int k = *nb < 4 ? *nb : 4;
+  int at = k;
+  while (at > 0 && contact_deeper(&c, &best[at - 1])) at--;
+  if (at >= 4) return;
+  for (int i = (k < 4 ? k : 3); i > at; i--) best[i] = best[i - 1];
+  best[at] = c;
+  if (*nb < 4) (*nb)++;
+}
+
+__device__ int col_plane_mesh(const double* cp, const double* Rp, const double* cb, const double* Rb,
+                              const double* hv, int nhv, double margin, Contact* out) {
+  const double n[3] = {Rp[2], Rp[5], Rp[8]};
+  int nb = 0;
+  for (int k = 0; k < nhv; k++) {
+    double w[3], x[3];
+    matvec3(Rb, hv + 3 * k, w);
+    for (int i = 0; i < 3; i++) x[i] = cb[i] + w[i];
+    const double v[3] = {x[0] - cp[0], x[1] - cp[1], x[2] - cp[2]};
+    Contact c;
+    c.dist = dot3(v, n);
+    if (c.dist >= margin) continue;
+    for (int i = 0; i < 3; i++) {
+      c.n[i] = n[i];
+      c.pos[i] = x[i] - n[i] * (0.5 * c.dist);
+    }
+    top4_insert(out, &nb, c);
+  }
+  return nb;
+}
+
+__device__ int col_plane_cylinder(const double* cp, const double* Rp, const double* cb, const double* Rb,
+                                  const double* sb, double margin, Contact* out) {
+  const double n[3] = {Rp[2], Rp[5], Rp[8]}, ax[3] = {Rb[2], Rb[5], Rb[8]};
+  const double r = sb[0], h = sb[1];
+  const double prj = dot3(n, ax);
+  double u[3] = {-(n[0] - prj * ax[0]), -(n[1] - prj * ax[1]), -(n[2] - prj * ax[2])};
+  const double lu = norm3(u);
+  double v[3];
+  if (lu < 1e-12) {
+    u[0] = Rb[0];
+    u[1] = Rb[3];
+    u[2] = Rb[6];
+  } else {
+    for (int i = 0; i < 3; i++) u[i] /= lu;
+  }
+  cross3(ax, u, v);
+  const double sgn = prj > 0 ? -1.0 : 1.0;
+  double cd[3], cs[3];
+  for (int i = 0; i < 3; i++) {
+    cd[i] = cb[i] + sgn * h * ax[i];
+    cs[i] = cb[i] - sgn * h * ax[i];
+  }
+  double pts[4][3];
+  const double s3 = 0.86602540378443864676;
+  for (int i = 0; i < 3; i++) {
+    pts[0][i] = cd[i] + r * u[i];
+    pts[1][i] = cs[i] + r * u[i];
+    pts[2][i] = cd[i] - 0.5 * r * u[i] + s3 * r * v[i];
+    pts[3][i] = cd[i] - 0.5 * r * u[i] - s3 * r * v[i];
+  }
+  int nb = 0;
+  for (int k = 0; k < 4; k++) {
+    const double w[3] = {pts[k][0] - cp[0], pts[k][1] - cp[1], pts[k][2] - cp[2]};
+    Contact c;
+    c.dist = dot3(w, n);
+    if (c.dist >= margin) continue;
+    for (int i = 0; i < 3; i++) {
+      c.n[i] = n[i];
+      c.pos[i] = pts[k][i] - n[i] * (0.5 * c.dist);
+    }
+    top4_insert(out, &nb, c);
+  }
+  return nb;
+}
+
 // Narrow-phase classes.  The collision stage first classifies every pair (broadphase + type
 // combination), then runs one collider at a time over the compacted survivors of its class, so a
 // wave never executes the union of the colliders its 64 pairs happen to need.
-enum { CLS_PLANE = 0, CLS_SPH_SPH, CLS_SPH_CAP, CLS_SPH_BOX, CLS_CAP_CAP, CLS_CAP_BOX, CLS_BOX_BOX, NCLS };
+enum { CLS_PLANE = 0, CLS_SPH_SPH, CLS_SPH_CAP, CLS_SPH_BOX, CLS_CAP_CAP, CLS_CAP_BOX, CLS_BOX_BOX, CLS_CONVEX, NCLS };
 
 // Broadphase record of one geom in LDS (8 doubles): centre, AABB half-extent (a plane: its
 // normal), bounding radius, type.
@@ -931,7 +1360,7 @@ __device__ void geom_record(const Env& e, int g, double* r) {
       x[3 + i] = R[3 * i + 2];
     else if (t == RMBX_GEOM_SPHERE)
       x[3 + i] = s[0];
-    else if (t == RMBX_GEOM_CAPSULE)
+    else if (t == RMBX_GEOM_CAPSULE || t == RMBX_GEOM_CYLINDER)
       x[3 + i] = fabs(R[3 * i + 2]) * s[1] + s[0];
     else
       x[3 + i] = fabs(R[3 * i]) * s[0] + fabs(R[3 * i + 1]) * s[1] + fabs(R[3 * i + 2]) * s[2];
@@ -963,6 +1392,7 @@ __device__ int pair_class(const double* grec, int g1, int g2, double margin) {
     if (lo1 > hi2 + margin || lo2 > hi1 + margin) return -1;
   }
   const int a = t1 < t2 ? t1 : t2, b = t1 < t2 ? t2 : t1;
+  if (b == RMBX_GEOM_MESH || b == RMBX_GEOM_CYLINDER) return CLS_CONVEX;
   if (a == RMBX_GEOM_SPHERE) {
     if (b == RMBX_GEOM_SPHERE) return CLS_SPH_SPH;
     if (b == RMBX_GEOM_CAPSULE) return CLS_SPH_CAP;
@@ -992,8 +1422,18 @@ __device__ int pair_narrow(const Env& e, int p, int cls, Contact* out) {
   const double *c2 = e.gxpos + 3 * g2, *R2 = e.gxmat + 9 * g2, *s2 = m.geom_csize + 3 * g2;
   int n = 0;
   switch (cls) {
-    case CLS_PLANE:
-      n = col_plane(c1, R1, flip ? t1 : t2, c2, R2, s2, margin, out);
+    case CLS_PLANE: {
+      const int to = flip ? t1 : t2;
+      if (to == RMBX_GEOM_MESH)
+        n = col_plane_mesh(c1, R1, c2, R2, m.hull_vert + 3 * m.geom_hulladr[g2], m.geom_hullnum[g2], margin, out);
+      else if (to == RMBX_GEOM_CYLINDER)
+        n = col_plane_cylinder(c1, R1, c2, R2, s2, margin, out);
+      else
+        n = col_plane(c1, R1, to, c2, R2, s2, margin, out);
+      break;
+    }
+    case CLS_CONVEX:
+      n = col_convex(e, g1, g2, margin, out);
       break;
     case CLS_SPH_SPH:
       n = col_sphere_sphere(c1, s1[0], c2, s2[0], margin, out);
@@ -1056,16 +1496,22 @@ __device__ void make_frame(const double* n, double* F) {
 
 // LDS scratch of the collision stage.  It lives in the front kernel's velocity/RNE arrays, dead
 // once velocity_stage has copied them out (extra dynamic LDS only for models where that region
-// is too small): geom broadphase records; per pair its class (pass 1) then its survivor index
-// (pass 2, -1 = rejected); the class-major survivor list; the contact count of each survivor.
+// is too small): geom broadphase records; the survivors of the broadphase in pair order (pair
+// index, narrow-phase class, contact count; at most collision_cap(npair), the same cap as the
+// oracle's) and the class-major list of survivor indices.
+#define RMBX_MAX_CANDIDATES 2048
 struct CollisionLds {
   double* geom;
-  int16_t* slot;
+  int32_t* spair;
   int16_t* list;
   uint8_t* count;
+  uint8_t* scls;
 };
+__host__ __device__ __forceinline__ int collision_cap(int npair) {
+  return npair < RMBX_MAX_CANDIDATES ? npair : RMBX_MAX_CANDIDATES;
+}
 __host__ __device__ __forceinline__ size_t collision_lds_doubles(int ngeom, int npair) {
-  return 8 * (size_t)ngeom + ((((size_t)5 * npair + 7) / 8 + 1) & ~size_t(1));
+  return 8 * (size_t)ngeom + (size_t)collision_cap(npair) + 2;  // 8 bytes per survivor
 }
 __host__ __device__ __forceinline__ size_t collision_lds_free_doubles(int nb, int nv) {
   return 28 * (size_t)nb + 6 * (size_t)nv;  // cvel, cacc, cfrc, cdofdot, cinert
@@ -1080,29 +1526,30 @@ __device__ __forceinline__ CollisionLds collision_lds(const Env& e) {
   const rmbx_model& m = *e.m;
   CollisionLds cl;
   const bool fits = collision_lds_doubles(m.ngeom, m.npair) <= collision_lds_free_doubles(m.nbody, m.nv);
+  const int cap = collision_cap(m.npair);
   cl.geom = fits ? e.sh + 16 * m.nbody : e.sh + front_lds_doubles(m.nbody, m.nv);
-  cl.slot = reinterpret_cast<int16_t*>(cl.geom + 8 * m.ngeom);
-  cl.list = cl.slot + m.npair;
-  cl.count = reinterpret_cast<uint8_t*>(cl.list + m.npair);
+  cl.spair = reinterpret_cast<int32_t*>(cl.geom + 8 * m.ngeom);
+  cl.list = reinterpret_cast<int16_t*>(cl.spair + cap);
+  cl.count = reinterpret_cast<uint8_t*>(cl.list + cap);
+  cl.scls = cl.count + cap;
   return cl;
 }
 
 // Contacts in pair order, at most max_contacts (the serial per-pair loop's result, bit for bit):
-// 1. broadphase + class of every pair (geom records staged in LDS), class counts by ballot
-// 2. survivors compacted class-major (pair order inside a class)
+// 1. broadphase + class of every pair (geom records staged in LDS); survivors appended in pair
+//    order (at most collision_cap(npair): the scan stops there, as the oracle's loop does)
+// 2. survivors listed class-major
 // 3. one collider at a time over its class's survivors, contacts into con_tmp[survivor]
-// 4. pair-order scan of the counts, contacts copied to their final slots
+// 4. pair-order scan of the survivors' counts, contacts copied to their final slots
 __device__ int collision(Env& e, int lane, const CollisionLds& cl, unsigned long long* prof) {
   const rmbx_model& m = *e.m;
   unsigned long long tp = prof ? stamp() : 0;
   const int np = m.npair;
+  const int cap = collision_cap(np);
   const unsigned long long below = (1ull << lane) - 1;
   for (int g = lane; g < m.ngeom; g += 64) geom_record(e, g, cl.geom + 8 * g);
   sync();
   SUBPROF(16)
-  int cnt[NCLS];
-#pragma unroll
-  for (int k = 0; k < NCLS; k++) cnt[k] = 0;
   // pair indices and margins of the next chunk are loaded before this chunk's tests
   int g1n = 0, g2n = 0;
   double mn = 0;
@@ -1111,7 +1558,8 @@ __device__ int collision(Env& e, int lane, const CollisionLds& cl, unsigned long
     g2n = m.pair_geom2[lane];
     mn = m.pair_margin[lane];
   }
-  for (int base = 0; base < np; base += 64) {
+  int nsurv = 0;
+  for (int base = 0; base < np && nsurv < cap; base += 64) {
     const int p = base + lane;
     const int g1 = g1n, g2 = g2n;
     const double mg = mn;
@@ -1121,30 +1569,39 @@ __device__ int collision(Env& e, int lane, const CollisionLds& cl, unsigned long
       mn = m.pair_margin[p + 64];
     }
     const int c = p < np ? pair_class(cl.geom, g1, g2, mg) : -1;
-    if (p < np) cl.slot[p] = (int16_t)c;
+    const unsigned long long mk = __ballot(c >= 0);
+    const int idx = nsurv + __popcll(mk & below);
+    if (c >= 0 && idx < cap) {
+      cl.spair[idx] = p;
+      cl.scls[idx] = (uint8_t)c;
+    }
+    nsurv += __popcll(mk);
+  }
+  nsurv = nsurv < cap ? nsurv : cap;
+  if (nsurv == 0) return 0;
+  sync();
+  int cnt[NCLS], off[NCLS], run[NCLS];
+#pragma unroll
+  for (int k = 0; k < NCLS; k++) cnt[k] = 0;
+  for (int base = 0; base < nsurv; base += 64) {
+    const int i = base + lane;
+    const int c = i < nsurv ? cl.scls[i] : -1;
 #pragma unroll
     for (int k = 0; k < NCLS; k++) cnt[k] += __popcll(__ballot(c == k));
   }
-  int off[NCLS], run[NCLS];
-  int nsurv = 0;
+  int acc = 0;
 #pragma unroll
   for (int k = 0; k < NCLS; k++) {
-    off[k] = run[k] = nsurv;
-    nsurv += cnt[k];
+    off[k] = run[k] = acc;
+    acc += cnt[k];
   }
-  if (nsurv == 0) return 0;
-  sync();
-  for (int base = 0; base < np; base += 64) {
-    const int p = base + lane;
-    const int c = p < np ? cl.slot[p] : -1;
+  for (int base = 0; base < nsurv; base += 64) {
+    const int i = base + lane;
+    const int c = i < nsurv ? cl.scls[i] : -1;
 #pragma unroll
     for (int k = 0; k < NCLS; k++) {
       const unsigned long long mk = __ballot(c == k);
-      if (c == k) {
-        const int idx = run[k] + __popcll(mk & below);
-        cl.list[idx] = (int16_t)p;
-        cl.slot[p] = (int16_t)idx;
-      }
+      if (c == k) cl.list[run[k] + __popcll(mk & below)] = (int16_t)i;
       run[k] += __popcll(mk);
     }
   }
@@ -1157,10 +1614,11 @@ __device__ int collision(Env& e, int lane, const CollisionLds& cl, unsigned long
     for (int i0 = off[k]; i0 < end; i0 += 64) {
       const int i = i0 + lane;
       if (i < end) {
+        const int sv = cl.list[i];
         Contact c[4];
-        const int n = pair_narrow(e, cl.list[i], k, c);
-        cl.count[i] = (uint8_t)n;
-        double* t = tmp + 28 * (size_t)i;
+        const int n = pair_narrow(e, cl.spair[sv], k, c);
+        cl.count[sv] = (uint8_t)n;
+        double* t = tmp + 28 * (size_t)sv;
 #pragma unroll
         for (int j = 0; j < 4; j++)
           if (j < n) {
@@ -1176,13 +1634,13 @@ __device__ int collision(Env& e, int lane, const CollisionLds& cl, unsigned long
   sync();
   SUBPROF(18)
   int ncon = 0;
-  for (int base = 0; base < np && ncon < m.max_contacts; base += 64) {
-    const int p = base + lane;
-    const int idx = p < np ? cl.slot[p] : -1;
-    const int n = idx >= 0 ? cl.count[idx] : 0;
+  for (int base = 0; base < nsurv && ncon < m.max_contacts; base += 64) {
+    const int sv = base + lane;
+    const int n = sv < nsurv ? cl.count[sv] : 0;
+    const int p = sv < nsurv ? cl.spair[sv] : 0;
     int total;
     const int o = wave_excl_scan(n, lane, &total);
-    const double* t = tmp + 28 * (size_t)(idx >= 0 ? idx : 0);
+    const double* t = tmp + 28 * (size_t)(sv < nsurv ? sv : 0);
     for (int i = 0; i < n; i++) {
       const int k = ncon + o + i;
       if (k >= m.max_contacts) break;
@@ -1199,6 +1657,7 @@ __device__ int collision(Env& e, int lane, const CollisionLds& cl, unsigned long
   }
   return ncon < m.max_contacts ? ncon : m.max_contacts;
 }
+
 
 // ------------------------------------------------------------------------------------------
 // constraint rows
@@ -2143,7 +2602,7 @@ __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj,
 }
 
 __device__ void solver_integrate(Env& e, SolverShared& S, double* a, int bi, int bj, bool own,
-                                 int tid) {
+                                 int tid, int sub) {
   const rmbx_model& m = *e.m;
   const int nv = m.nv, NB = (nv + 3) / 4, NVP = 4 * NB;
   const double h = m.timestep;
@@ -2186,6 +2645,26 @@ __device__ void solver_integrate(Env& e, SolverShared& S, double* a, int bi, int
   for (int k = tid; k < nv; k += SOLVER_THREADS) {
     const double acc = S.a[k];
     if (!isfinite(acc) || fabs(acc) > 1e10) bad = true;
+  }
+  if (block_sum_i(bad ? 1 : 0, S, tid)) {
+    // MuJoCo's divergence guard (mj_checkAcc -> mj_resetData): the model's qpos0, zero velocity,
+    // warm start and ctrl, time 0, in this substep (the remaining substeps of the env-step run
+    // from it, with ctrl 0 as in MuJoCo); stats[3] = the 1-based substep of the reset
+    for (int k = tid; k < m.nq; k += SOLVER_THREADS) e.qpos[k] = m.qpos0[k];
+    for (int k = tid; k < nv; k += SOLVER_THREADS) {
+      e.qvel[k] = 0.0;
+      e.qacc_ws[k] = 0.0;
+    }
+    for (int k = tid; k < m.nu; k += SOLVER_THREADS) e.ctrl[k] = 0.0;
+    if (tid == 0) {
+      e.time[0] = 0.0;
+      e.stats[3] = sub;
+    }
+    __syncthreads();
+    return;
+  }
+  for (int k = tid; k < nv; k += SOLVER_THREADS) {
+    const double acc = S.a[k];
     e.qvel[k] += h * acc;
     e.qacc_ws[k] = acc;
   }
@@ -2208,7 +2687,6 @@ __device__ void solver_integrate(Env& e, SolverShared& S, double* a, int bi, int
       e.qpos[qa] += h * e.qvel[da];
     }
   }
-  if (block_sum_i(bad ? 1 : 0, S, tid) && tid == 0) e.stats[3] = 1;
   if (tid == 0) e.time[0] += h;
   __syncthreads();
 }
@@ -2220,6 +2698,7 @@ struct KArgs {
   const uint8_t* active;
   int n_env;
   int nsub;
+  int sub;  // 1-based substep index of this launch
   int integrate_flag;
   unsigned long long* prof;  // optional [n_env][16] per-stage cycle sums (diagnostic)
   const int32_t* subtree_end;  // [nbody] end of each body's DFS subtree id range
@@ -2315,7 +2794,7 @@ __global__ void __launch_bounds__(SOLVER_THREADS, 4) solver_kernel(KArgs args) {
   sensors(e, ncon, tid, S.bacc, S.bfrc, &S.jc[0][0], S.anc, args.subtree_end);
   PROF(6)
   if (tid == 0) e.stats[2] = iters;
-  if (args.integrate_flag) solver_integrate(e, S, a, bi, bj, own, tid);
+  if (args.integrate_flag) solver_integrate(e, S, a, bi, bj, own, tid, args.sub);
   PROF(7)
 }
 
@@ -2377,7 +2856,7 @@ static Layout make_layout(const rmbx_model& m) {
   L.efc_tmp = take(ne);
   // the candidate contacts are dead before make_constraints zeroes and fills J: share its rows
   // when they are large enough
-  const size_t ntmp = 28 * (size_t)m.npair;
+  const size_t ntmp = 28 * (size_t)collision_cap(m.npair);
   L.con_tmp = (size_t)ne * nv >= ntmp ? L.J : take(ntmp);
   L.ints = o;
   size_t io = 0;
@@ -2431,7 +2910,7 @@ int rmbx_engine_create(const struct rmbx_model* model, int n_env, rmbx_engine** 
   RMBX_CHECK_ARG(h.nbody > 0 && h.nbody <= MAX_BODY, "nbody=%d outside [1, %d]", h.nbody, MAX_BODY);
   RMBX_CHECK_ARG(h.max_contacts > 0 && h.max_contacts <= RCHUNK * MAX_NVP / 6, "bad max_contacts=%d",
                  h.max_contacts);
-  RMBX_CHECK_ARG(h.npair >= 0 && h.npair < 32768, "npair=%d outside [0, 32767]", h.npair);
+  RMBX_CHECK_ARG(h.npair >= 0 && h.npair < (1 << 24), "npair=%d outside [0, 2^24)", h.npair);
   RMBX_CHECK_ARG(front_kernel_lds_bytes(h) <= 65536,
                  "model too large for the front kernel's LDS (nbody=%d nv=%d ngeom=%d npair=%d)", h.nbody,
                  h.nv, h.ngeom, h.npair);
@@ -2483,6 +2962,7 @@ int rmbx_engine_create(const struct rmbx_model* model, int n_env, rmbx_engine** 
   UP(eq_solref, 2 * h.neq) UP(eq_solimp, 5 * h.neq)
   UP(sensor_type, h.nsensor) UP(sensor_site, h.nsensor)
   UP(cam_body, h.ncam) UP(cam_pos, 3 * h.ncam) UP(cam_quat, 4 * h.ncam) UP(cam_fovy, h.ncam)
+  UP(geom_hulladr, h.ngeom) UP(geom_hullnum, h.ngeom) UP(hull_vert, 3 * h.nhullvert)
 #undef UP
   if (st != RMBX_OK) {
     rmbx_engine_destroy(eng);
@@ -2542,6 +3022,9 @@ int rmbx_engine_ws_offset(const rmbx_engine* eng, const char* name, size_t* offs
       {"con_dist", L.con_dist, (size_t)m.max_contacts},
       {"efc_force", L.efc_force, (size_t)L.nefc_max},
       {"J", L.J, (size_t)L.nefc_max * nv},
+      // int32 arrays: offsets in int32 units from the workspace start (2 per double)
+      {"con_b1", 2 * L.ints + L.con_b1, (size_t)m.max_contacts},
+      {"con_b2", 2 * L.ints + L.con_b2, (size_t)m.max_contacts},
   };
   for (const Item& it : items) {
     if (strcmp(it.n, name) == 0) {
@@ -2586,6 +3069,7 @@ static int launch(rmbx_engine* eng, int nsub, int integ, const uint8_t* active, 
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int reps = integ ? nsub : 1;
   for (int s = 0; s < reps; s++) {
+    a.sub = s + 1;
     const size_t front_lds = front_kernel_lds_bytes(eng->host);
     hipLaunchKernelGGL(front_kernel, dim3(eng->n_env), dim3(64), front_lds, st, a);
     RMBX_CHECK_LAUNCH();

@@ -98,3 +98,9 @@ class PhysicsEngine:
         stride, _ = self._off("stride")
         off, cnt = self._off(name)
         return self.workspace.view(torch.float64).view(self.n_env, stride)[:, off : off + cnt]
+
+    def wsi(self, name):
+        """Zero-copy [n_env, count] int32 view of a named integer workspace array (con_b1, con_b2)."""
+        stride, _ = self._off("stride")
+        off, cnt = self._off(name)
+        return self.workspace.view(torch.int32).view(self.n_env, 2 * stride)[:, off : off + cnt]

@@ -67,8 +67,7 @@ class BatchedMujocoUR5eEnvBase:
         self.camera_names = [str(x) for x in self.arrays["names_cam"]]
         self.reward = torch.zeros(self.num_envs, dtype=torch.float64, device=self.device)
         self.world_idx = np.zeros(self.num_envs, dtype=np.int64)
-        # MuJoCo's bad-state reset (mj_checkAcc -> mj_resetData): the model's qpos0, per env count
-        self._qpos0 = torch.tensor(self.arrays["qpos0"], dtype=torch.float64, device=self.device)
+        # MuJoCo's bad-state resets (mj_checkAcc -> mj_resetData) per env
         self.bad_resets = torch.zeros(self.num_envs, dtype=torch.int32, device=self.device)
 
     # -- reference API ----------------------------------------------------------------------
@@ -143,24 +142,19 @@ class BatchedMujocoUR5eEnvBase:
         return obs, self.reward, False, False, {}
 
     def _reset_bad_states(self):
-        """MuJoCo's divergence guard (mj_step -> mj_checkAcc, [ext] mujoco 3.1.6): an env whose
-        qacc went non-finite or above 1e10 during the env-step (the physics kernel flags it in
-        stats[:, 3]) is reset as mj_resetData does -- qpos = the model's qpos0, qvel = qacc_warmstart
-        = ctrl = 0, time = 0 -- and forwarded again; bad_resets counts these per env (MuJoCo's
-        mjWARN_BADQACC counter).  Device-side masked updates, no host sync.  Granularity: MuJoCo
-        resets inside the offending substep and integrates the reset state for the remaining
-        substeps; here the reset lands at the end of the env-step."""
+        """MuJoCo's divergence guard (mj_step -> mj_checkAcc -> mj_resetData, [ext] mujoco 3.1.6):
+        the physics kernel resets an env whose qacc went non-finite or above 1e10 inside the
+        substep where it happened (the model's qpos0, zero velocity / warm start / ctrl, time 0;
+        the remaining substeps run from there) and reports that substep in stats[:, 3].  Here the
+        resets are counted per env (MuJoCo's mjWARN_BADQACC counter) and an env reset in the
+        last substep is forwarded again, so its frames describe the reset state as after MuJoCo's
+        post-reset mj_forward.  Device-side masked updates, no host sync."""
         e = self.engine
-        bad = e.stats[:, 3] != 0
-        col = bad[:, None]
-        torch.where(col, self._qpos0, e.qpos, out=e.qpos)
-        e.qvel.masked_fill_(col, 0.0)
-        e.qacc_ws.masked_fill_(col, 0.0)
-        e.ctrl.masked_fill_(col, 0.0)
-        e.time.masked_fill_(bad, 0.0)
-        self.bad_resets += bad.to(torch.int32)
+        sub = e.stats[:, 3]
+        self.bad_resets += (sub != 0).to(torch.int32)
+        last = (sub == self.frame_skip).to(torch.uint8)
         e.stats[:, 3] = 0
-        e.forward(active=bad.to(torch.uint8))
+        e.forward(active=last)
 
     def get_time(self):
         return self.engine.time

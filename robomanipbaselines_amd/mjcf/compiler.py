@@ -19,10 +19,12 @@ reference, pyproject.toml:34) that the reference's MujocoUR5eCable scene uses
     anchors in body2 frames.
 
 Substitutions (MuJoCo parity is unpinned: no MuJoCo in this image):
-  * collision meshes are replaced by their oriented bounding box in the geom frame (box-box
-    narrowphase); a mesh that is missing from the checkout (the reference's
-    .MISSING_LARGE_BLOBS) falls back to a box of the D435i housing size 90x25x25 mm;
-  * cylinders collide as capsules of the same radius and half-length.
+  * by default collision meshes are replaced by their oriented bounding box in the geom frame
+    (box-box narrowphase) and cylinders collide as capsules of the same radius and half-length;
+    with convex_meshes=True mesh geoms collide through their convex hull and cylinders exactly
+    (MPR narrow phase, as MuJoCo 3.1.6's mjc_Convex does through libccd);
+  * a mesh that is missing from the checkout (the reference's .MISSING_LARGE_BLOBS) falls back
+    to a box of the D435i housing size 90x25x25 mm.
 """
 
 import math
@@ -250,32 +252,69 @@ class Model:
     """Plain container of compiled arrays (see compile_mjcf)."""
 
 
-def _expand_includes(node, main_dir):
+_ASSET_FILE_TAGS = ("mesh", "texture", "hfield", "skin")
+
+
+def _expand_includes(node, main_dir, missing):
     out = []
     for child in list(node):
         if child.tag == "include":
             path = os.path.join(main_dir, child.attrib["file"])
+            if not os.path.exists(path) and missing is not None:
+                missing.append(child.attrib["file"])  # absent from the checkout (e.g. YCB_sim)
+                continue
             root = ET.parse(path).getroot()
-            _expand_includes_inplace(root, main_dir)
+            _expand_includes_inplace(root, main_dir, missing)
+            # asset files of an included file that sit next to it (MuJoCo resolves them from the
+            # including file's directory, e.g. mujoco_scanned_objects/<obj>/model.obj)
+            inc_dir = os.path.dirname(path)
+            for el in root.iter():
+                f = el.attrib.get("file")
+                if el.tag in _ASSET_FILE_TAGS and f and not os.path.isabs(f) and os.path.exists(os.path.join(inc_dir, f)):
+                    el.attrib["file"] = os.path.abspath(os.path.join(inc_dir, f))
             out.extend(list(root))
         else:
-            _expand_includes_inplace(child, main_dir)
+            _expand_includes_inplace(child, main_dir, missing)
             out.append(child)
     return out
 
 
-def _expand_includes_inplace(node, main_dir):
-    new = _expand_includes(node, main_dir)
+def _expand_includes_inplace(node, main_dir, missing=None):
+    new = _expand_includes(node, main_dir, missing)
     for c in list(node):
         node.remove(c)
     for c in new:
         node.append(c)
 
 
-def compile_mjcf(path, missing_mesh_box=(0.045, 0.0125, 0.0125)):
+def _drop_empty_free_bodies(node):
+    """Remove bodies left with a free joint and nothing else (their geoms came from an include
+    that is absent from the checkout): MuJoCo rejects massless moving bodies."""
+    dropped = []
+    for child in list(node):
+        if child.tag == "body":
+            _drop_empty_free_bodies(child)
+            kinds = {c.tag for c in child}
+            if kinds and kinds <= {"freejoint", "joint"} and any(
+                    c.tag == "freejoint" or c.attrib.get("type") == "free" for c in child):
+                node.remove(child)
+                dropped.append(child.attrib.get("name", child.attrib.get("pos", "")))
+        else:
+            dropped += _drop_empty_free_bodies(child)
+    return dropped
+
+
+def compile_mjcf(path, missing_mesh_box=(0.045, 0.0125, 0.0125), convex_meshes=False, skip_missing_includes=False):
+    """Compile the MJCF at `path`.  convex_meshes: mesh geoms collide through the convex hull of
+    their vertices (MuJoCo's own mesh collision model) and cylinders as true cylinders, both
+    through the MPR narrow phase, instead of the mesh-OBB / capsule substitutes.
+    skip_missing_includes: includes absent from the checkout are dropped together with the free
+    bodies they would have filled (the Pick scene minus its YCB_sim objects)."""
     main_dir = os.path.dirname(os.path.abspath(path))
     root = ET.parse(path).getroot()
-    _expand_includes_inplace(root, main_dir)
+    missing = [] if skip_missing_includes else None
+    _expand_includes_inplace(root, main_dir, missing)
+    dropped_bodies = _drop_empty_free_bodies(root) if skip_missing_includes else []
 
     # ---- compiler / option / statistic / visual
     meshdir = main_dir
@@ -443,6 +482,7 @@ def compile_mjcf(path, missing_mesh_box=(0.045, 0.0125, 0.0125)):
 
     # ---- geom post-processing: mesh OBBs (collision) and missing meshes
     for g in geoms:
+        g["exact_cylinder"] = convex_meshes
         if g["type"] == GEOM_MESH or (g["mesh_name"] is not None and g["type"] in (GEOM_CAPSULE, GEOM_BOX)):
             if g["mesh"] is None:
                 # missing blob: box of the D435i housing (documented substitution)
@@ -457,6 +497,11 @@ def compile_mjcf(path, missing_mesh_box=(0.045, 0.0125, 0.0125)):
                 g["obb_rot"] = np.eye(3)
                 g["obb_half"] = (hi - lo) / 2
                 g["mesh_missing"] = False
+            if (convex_meshes and g["type"] == GEOM_MESH and not g["mesh_missing"]
+                    and (g["contype"] or g["conaffinity"])):
+                hull = _convex_hull(g["mesh"])
+                if hull is not None:
+                    g["hull"], g["hull_com"] = hull
             if g["type"] == GEOM_CAPSULE:
                 # capsule fitted to the mesh AABB along its longest axis (MuJoCo fitaabb-like)
                 h = g["obb_half"]
@@ -571,6 +616,8 @@ def compile_mjcf(path, missing_mesh_box=(0.045, 0.0125, 0.0125)):
             qpos0[a] = jt["ref"]
 
     M = Model()
+    M.missing_includes = missing or []
+    M.dropped_bodies = dropped_bodies
     M.name = root.attrib.get("model", "")
     M.timestep = timestep
     M.gravity = gravity
@@ -689,12 +736,29 @@ def compile_mjcf(path, missing_mesh_box=(0.045, 0.0125, 0.0125)):
 # ------------------------------------------------------------------------------------------
 # static contact-pair filtering + parameter mixing (mj_collision filters, mj_contactParam)
 # ------------------------------------------------------------------------------------------
+def _convex_hull(mesh):
+    """(hull vertices relative to the mesh's centre of mass, that centre) -- MuJoCo collides mesh
+    geoms through the convex hull of their vertices (qhull; scipy wraps the same library), in
+    the mesh frame it recentres at the mesh's centre of mass."""
+    from scipy.spatial import ConvexHull
+
+    verts, faces = mesh
+    try:
+        idx = np.sort(ConvexHull(verts).vertices)
+    except Exception:  # degenerate (flat) mesh: keep the OBB substitute
+        return None
+    _, com, _ = mesh_mass_props(verts, faces)
+    if not np.all(np.isfinite(com)):
+        com = verts[idx].mean(0)
+    return verts[idx] - com, com
+
+
 def _collision_type(g):
     t = g["type"]
     if t == GEOM_MESH:
-        return GEOM_BOX
+        return GEOM_MESH if "hull" in g else GEOM_BOX
     if t == GEOM_CYLINDER:
-        return GEOM_CAPSULE
+        return GEOM_CYLINDER if g.get("exact_cylinder") else GEOM_CAPSULE
     return t
 
 

@@ -19,7 +19,7 @@ I32 = np.int32
 F64 = np.float64
 
 _INT_FIELDS = ["nq", "nv", "nbody", "njnt", "ngeom", "nsite", "nu", "neq", "ntendon", "nwrap",
-               "npair", "nsensor", "ncam", "solver_iterations", "ls_iterations", "max_contacts"]
+               "npair", "nsensor", "ncam", "solver_iterations", "ls_iterations", "max_contacts", "nhullvert"]
 _DBL_FIELDS = ["timestep", ("gravity", 3), "meaninertia", "solver_tolerance", "extent", "znear", "zfar"]
 # (name, dtype) in struct order
 _PTR_FIELDS = [
@@ -46,6 +46,7 @@ _PTR_FIELDS = [
     ("eq_solimp", F64),
     ("sensor_type", I32), ("sensor_site", I32),
     ("cam_body", I32), ("cam_pos", F64), ("cam_quat", F64), ("cam_fovy", F64),
+    ("geom_hulladr", I32), ("geom_hullnum", I32), ("hull_vert", F64),
 ]
 
 
@@ -82,13 +83,21 @@ def pack(M, max_contacts=128, solver_iterations=100, ls_iterations=30, solver_to
     for x in g:
         if not (x["contype"] or x["conaffinity"]):
             ct.append(-1)
-            cs.append(x["size"])
-            cp.append(x["pos"])
+            if x["type"] == C.GEOM_MESH and "obb_half" in x:  # visual mesh: its box (renderer)
+                cs.append(np.asarray(x["obb_half"]))
+                cp.append(x["pos"] + C.quat2mat(x["quat"]) @ x["obb_center"])
+            else:
+                cs.append(x["size"])
+                cp.append(x["pos"])
             cq.append(x["quat"])
             rb.append(0.0)
             continue
         t = C._collision_type(x)
-        if x["type"] == C.GEOM_MESH:
+        if t == C.GEOM_MESH:  # convex hull, in its frame at the mesh's centre of mass
+            size = np.abs(x["hull"]).max(0)
+            pos = x["pos"] + C.quat2mat(x["quat"]) @ x["hull_com"]
+            quat = x["quat"]
+        elif x["type"] == C.GEOM_MESH:
             size = np.asarray(x["obb_half"])
             pos = x["pos"] + C.quat2mat(x["quat"]) @ x["obb_center"]
             quat = x["quat"]
@@ -104,9 +113,24 @@ def pack(M, max_contacts=128, solver_iterations=100, ls_iterations=30, solver_to
             rb.append(size[0] + size[1])
         elif t == C.GEOM_BOX:
             rb.append(float(np.linalg.norm(size)))
+        elif t == C.GEOM_CYLINDER:
+            rb.append(float(np.hypot(size[0], size[1])))
+        elif t == C.GEOM_MESH:
+            rb.append(float(np.linalg.norm(x["hull"], axis=1).max()))
         else:
             rb.append(0.0)  # plane: unbounded
     a["geom_ctype"], a["geom_csize"], a["geom_cpos"], a["geom_cquat"], a["geom_rbound"] = ct, cs, cp, cq, rb
+    hadr, hnum, hv = [], [], []
+    for x, t in zip(g, ct):
+        if t == C.GEOM_MESH:
+            hadr.append(len(hv))
+            hnum.append(len(x["hull"]))
+            hv.extend(x["hull"])
+        else:
+            hadr.append(-1)
+            hnum.append(0)
+    a["geom_hulladr"], a["geom_hullnum"] = hadr, hnum
+    a["hull_vert"] = np.asarray(hv, F64).reshape(-1, 3)
     p1, p2, cd, fr, sr, si, mg = [], [], [], [], [], [], []
     for i, j in M.pairs:
         condim, f, r, s, margin, gap = C.mix_contact_params(g[i], g[j])
@@ -167,11 +191,14 @@ def pack(M, max_contacts=128, solver_iterations=100, ls_iterations=30, solver_to
     out = {}
     for name, dt in _PTR_FIELDS:
         arr = np.asarray(a[name], dtype=dt)
+        if arr.size == 0:
+            out[name] = np.ascontiguousarray(arr.reshape(0) if arr.ndim <= 1 else arr.reshape(0, int(np.prod(arr.shape[1:]))))
+            continue
         out[name] = np.ascontiguousarray(arr.reshape(-1) if arr.ndim <= 1 else arr.reshape(arr.shape[0], -1))
     sizes = dict(nq=M.nq, nv=M.nv, nbody=M.nbody, njnt=M.njnt, ngeom=len(g), nsite=len(M.sites), nu=M.nu,
                  neq=len(M.equalities), ntendon=len(M.tendons), nwrap=len(a["wrap_jnt"]), npair=len(M.pairs),
                  nsensor=len(M.sensors), ncam=len(M.cams), solver_iterations=solver_iterations,
-                 ls_iterations=ls_iterations, max_contacts=max_contacts)
+                 ls_iterations=ls_iterations, max_contacts=max_contacts, nhullvert=len(a["hull_vert"]))
     for k, v in sizes.items():
         out["_" + k] = np.int32(v)
     out["_timestep"] = np.float64(M.timestep)
@@ -199,11 +226,23 @@ def save(arrays, path):
 def load(name_or_path):
     path = name_or_path if os.path.exists(name_or_path) else os.path.join(ASSET_DIR, name_or_path + ".npz")
     with np.load(path, allow_pickle=False) as f:
-        return {k: f[k] for k in f.files}
+        return _with_defaults({k: f[k] for k in f.files})
+
+
+def _with_defaults(arrays):
+    """Assets packed before the convex-hull fields existed: no hulls."""
+    if "geom_hulladr" not in arrays:
+        ng = int(arrays["_ngeom"])
+        arrays["geom_hulladr"] = np.full(ng, -1, I32)
+        arrays["geom_hullnum"] = np.zeros(ng, I32)
+        arrays["hull_vert"] = np.zeros((0, 3), F64)
+        arrays["_nhullvert"] = np.int32(0)
+    return arrays
 
 
 def as_ctypes(arrays):
     """rmbx_model struct referencing the arrays (keep `arrays` alive while it is used)."""
+    arrays = _with_defaults(arrays)
     m = RmbxModel()
     for n in _INT_FIELDS:
         setattr(m, n, int(arrays["_" + n]))

@@ -27,12 +27,20 @@ def build_prims(arrays):
         if gt[g] == C.GEOM_MESH and gg[g] <= 2 and gb[g] not in mesh_color:
             mesh_color[int(gb[g])] = rgba[g][:3]
     pi, pf = [], []
+    # visual meshes that carry their own bounding box (scenes packed with it) are drawn as that
+    # box; the other mesh bodies through their collision primitives (boxes / capsules)
+    boxed = {int(gb[g]) for g in range(len(gt))
+             if gt[g] == C.GEOM_MESH and gg[g] <= 2 and ct[g] < 0 and np.any(cs[g][:3] > 0)}
     for g in range(len(gt)):
         t = int(gt[g])
         if t != C.GEOM_MESH and gg[g] <= 2 and t in (C.GEOM_PLANE, C.GEOM_SPHERE, C.GEOM_CAPSULE, C.GEOM_CYLINDER, C.GEOM_BOX):
             pi.append([g, t, 0, 0])
             pf.append(list(size[g][:3]) + list(rgba[g][:3]) + [0, 0])
-        elif ct[g] >= 0 and gg[g] >= 3 and int(gb[g]) in mesh_color:
+        elif t == C.GEOM_MESH and gg[g] <= 2 and int(gb[g]) in boxed and ct[g] < 0:
+            pi.append([g, C.GEOM_BOX, 0, 0])
+            pf.append(list(cs[g][:3]) + list(rgba[g][:3]) + [0, 0])
+        elif (ct[g] >= 0 and gg[g] >= 3 and int(gb[g]) in mesh_color and int(gb[g]) not in boxed
+              and int(ct[g]) in (C.GEOM_SPHERE, C.GEOM_CAPSULE, C.GEOM_CYLINDER, C.GEOM_BOX)):
             typ = int(ct[g])
             pi.append([g, typ, 0, 0])
             pf.append(list(cs[g][:3]) + list(mesh_color[int(gb[g])]) + [0, 0])

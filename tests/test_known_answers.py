@@ -26,11 +26,11 @@ KAT = os.path.join(os.path.dirname(os.path.abspath(__file__)), "kat")
 G = 9.81
 
 
-def _arrays(name):
+def _arrays(name, convex=False):
     from robomanipbaselines_amd import model as MD
     from robomanipbaselines_amd.mjcf import compiler as C
 
-    return MD.pack(C.compile_mjcf(os.path.join(KAT, name + ".xml")))
+    return MD.pack(C.compile_mjcf(os.path.join(KAT, name + ".xml"), convex_meshes=convex))
 
 
 class _OracleRun:
@@ -208,16 +208,33 @@ def test_ball_settles_on_floor(kind):
     assert np.abs(q[-1, :2]).max() < 1e-9  # a vertical drop stays vertical
 
 
+@pytest.mark.parametrize("kind", KINDS)
+def test_convex_hull_and_cylinders_rest_on_the_floor(kind):
+    """The MPR / hull-vertex / cylinder colliders (convex_meshes): a cube mesh rests on the floor
+    at its half height, an upright cylinder at its half length, a lying one at its radius (soft
+    contact penetration below 1 mm), and the stacked cube and the ball stay on top."""
+    a = _arrays("hull_stack", convex=True)
+    assert list(a["geom_ctype"]) == [0, 7, 7, 2, 5, 5]
+    q, v = _runner(kind)(a, a["qpos0"].copy()).run(500)
+    z = q[-1, [2, 9, 16, 23, 30]]
+    assert abs(z[0] - 0.05) < 1e-3 and abs(z[3] - 0.05) < 1e-3 and abs(z[4] - 0.03) < 1e-3, z
+    assert 0.13 < z[1] < 0.151 and 0.19 < z[2] < 0.22, z  # on top of the first cube / the second
+    # (the stacked cube rocks on its single MPR contact, as in MuJoCo without multiccd)
+    assert np.abs(v[-1, :6]).max() < 0.5 and np.abs(v[-1, 18:]).max() < 1e-3
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("name,q0,v0,ctrl,steps", [
     ("pendulum", [1.0], None, None, 2000),
     ("servo_arm", [0.6, -0.9], None, [0.6, -0.9], 500),
     ("sphere_plane", [0.0, 0.0, 0.3, 1.0, 0.0, 0.0, 0.0], None, None, 400),
     ("free_body", [0.0, 0.0, 10.0, 1.0, 0.0, 0.0, 0.0], [0.1, 0.2, 0.3, 1.0, 2.0, 3.0], None, 300),
+    ("hull_stack", None, None, None, 150),
 ])
 def test_engine_matches_oracle_on_known_answer_models(name, q0, v0, ctrl, steps):
-    a = _arrays(name)
-    args = (np.array(q0), None if v0 is None else np.array(v0), None if ctrl is None else np.array(ctrl))
+    a = _arrays(name, convex=name.startswith("hull"))
+    args = (a["qpos0"].copy() if q0 is None else np.array(q0), None if v0 is None else np.array(v0),
+            None if ctrl is None else np.array(ctrl))
     qo, vo = _OracleRun(a, *args).run(steps)
     qe, ve = _EngineRun(a, *args).run(steps)
     np.testing.assert_allclose(qe, qo, rtol=0, atol=1e-10)

@@ -12,7 +12,12 @@ SCENES = {"ur5e_cable": os.path.join(REF_ENVS, "ur5e", "env_ur5e_cable.xml"),
           "ur5e_insert": os.path.join(REF_ENVS, "ur5e", "env_ur5e_insert.xml"),
           "ur5e_door": os.path.join(REF_ENVS, "ur5e", "env_ur5e_door.xml"),
           "ur5e_cabinet": os.path.join(REF_ENVS, "ur5e", "env_ur5e_cabinet.xml"),
-          "ur5e_toolbox": os.path.join(REF_ENVS, "ur5e", "env_ur5e_toolbox.xml")}
+          "ur5e_toolbox": os.path.join(REF_ENVS, "ur5e", "env_ur5e_toolbox.xml"),
+          "ur5e_pick": os.path.join(REF_ENVS, "ur5e", "env_ur5e_pick.xml")}
+# per-scene compile options: the Pick scene (BASELINE configs 4/5) collides its scanned objects
+# through their convex hulls (MPR) and drops the YCB_sim objects, absent from the checkout
+OPTIONS = {"ur5e_pick": dict(convex_meshes=True, skip_missing_includes=True)}
+PACK_OPTIONS = {"ur5e_pick": dict(max_contacts=200)}
 UR5E_URDF = "/root/reference/robo_manip_baselines/envs/assets/common/robots/ur5e/ur5e.urdf"
 
 
@@ -34,9 +39,12 @@ def add_arm_ik(M, arrays, root_body="ur5e_root_frame"):
 
 if __name__ == "__main__":
     os.makedirs(MD.ASSET_DIR, exist_ok=True)
+    only = sys.argv[1:]
     for name, path in SCENES.items():
-        M = C.compile_mjcf(path)
-        arrays = MD.pack(M)
+        if only and name not in only:
+            continue
+        M = C.compile_mjcf(path, **OPTIONS.get(name, {}))
+        arrays = MD.pack(M, **PACK_OPTIONS.get(name, {}))
         add_arm_ik(M, arrays)
         out = os.path.join(MD.ASSET_DIR, name + ".npz")
         MD.save(arrays, out)
