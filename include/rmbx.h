@@ -103,6 +103,16 @@ int rmbx_cabinet_reward(const double* qpos, int qpos_stride, int hinge_adr, int 
 int rmbx_toolbox_reward(const double* toolbox_xpos, const double* mat_xpos, double* reward, int n_env,
                         double xy_thre, double z_offset, void* stream);
 
+/* Ring-on-pole reward, batched.
+ * Replaces envs/mujoco/ur5e/MujocoUR5eRingEnv.py:46-75 (_get_reward): 0 if the highest ring
+ * body is above pole_z + 0.08 (numpy max: NaN never compares above); else 1 iff
+ * matplotlib.path.Path(ring xy + ring[0] xy).contains_point(pole xy) -- crossing-number test,
+ * non-finite vertices dropped with the next finite one opening a new subpath, exactly as
+ * matplotlib's point_in_path / PathNanRemover.  ring_xpos f64 [n_env][n_ring][3] (ring_B*
+ * bodies in body order), pole_xpos f64 [n_env][3].  Bit-exact (no contraction). */
+int rmbx_ring_reward(const double* ring_xpos, const double* pole_xpos, double* reward, int n_env, int n_ring,
+                     void* stream);
+
 /* Door-opening reward, batched.
  * Replaces envs/mujoco/ur5e/MujocoUR5eDoorEnv.py:52-67 (_get_reward): 0.5 * (reaching + opening)
  * with reaching = exp(-10 max(|pinch - handle| - margin, 0)) (1 once the door is open),

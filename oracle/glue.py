@@ -253,3 +253,91 @@ def toolbox_reward(toolbox_pos, mat_pos):
     if (np.max(np.abs(toolbox_pos[:2] - mat_pos[:2])) < xy_thre) and (toolbox_pos[2] < z_thre):
         return 1.0
     return 0.0
+
+
+def _finite(v):
+    return np.isfinite(v)
+
+
+def point_in_polygon_mpl(xy, tx, ty):
+    """matplotlib Path(xy).contains_point((tx, ty)) for a code-less path, radius 0, identity
+    transform ([ext] matplotlib 3.x src/_path.h point_in_path_impl, src/path_converters.h
+    PathNanRemover fast path, agg conv_transform): the identity affine maps a vertex to
+    (x*1 + y*0 + 0, x*0 + y*1 + 0), so a non-finite coordinate poisons both; non-finite
+    vertices are dropped and the next finite one opens a new subpath (MOVETO); each subpath is
+    tested with the crossing-number rule and closed back to its start only when the path ends
+    (a subpath cut by a MOVETO is left open); the point is inside if any subpath says so."""
+    if not (_finite(tx) and _finite(ty)):
+        return False
+    verts = []
+    for x, y in xy:
+        x, y = float(x), float(y)
+        X = x * 1.0 + y * 0.0 + 0.0
+        Y = x * 0.0 + y * 1.0 + 0.0
+        verts.append((X, Y))
+    # vertex stream after the NaN remover: (code, x, y); code 1 MOVETO, 2 LINETO, 0 STOP
+    stream = []
+    first = True
+    pending_move = False
+    for X, Y in verts:
+        if not (_finite(X) and _finite(Y)):
+            pending_move = True
+            continue
+        stream.append((1 if (first or pending_move) else 2, X, Y))
+        first = False
+        pending_move = False
+    stream.append((0, 0.0, 0.0))
+    pos = 0
+
+    def nxt():
+        nonlocal pos
+        c = stream[pos]
+        pos += 1
+        return c
+
+    inside = False
+    code = -1
+    x = y = 0.0
+    while True:
+        if code != 1:
+            code, x, y = nxt()
+            if code == 0:
+                break
+        sx = vtx0 = vtx1 = x
+        sy = vty0 = vty1 = y
+        yflag0 = vty0 >= ty
+        flag = False
+        while True:
+            code, x, y = nxt()
+            if code == 0:
+                x, y = sx, sy
+            elif code == 1:
+                break
+            yflag1 = vty1 >= ty
+            if yflag0 != yflag1:
+                if ((vty1 - ty) * (vtx0 - vtx1) >= (vtx1 - tx) * (vty0 - vty1)) == yflag1:
+                    flag = not flag
+            yflag0 = yflag1
+            vtx0, vty0 = vtx1, vty1
+            vtx1, vty1 = x, y
+            if code == 0:
+                break
+        yflag1 = vty1 >= ty
+        if yflag0 != yflag1:
+            if ((vty1 - ty) * (vtx0 - vtx1) >= (vtx1 - tx) * (vty0 - vty1)) == yflag1:
+                flag = not flag
+        inside = inside or flag
+        if inside or code == 0:
+            break
+    return inside
+
+
+def ring_reward(ring_pos, pole_pos):
+    """envs/mujoco/ur5e/MujocoUR5eRingEnv.py:46-75 (_get_reward): 0 if the highest ring body
+    is above pole z + 0.08 (numpy max: NaN never compares above), else 1 iff the pole's xy lies
+    in the polygon of the ring bodies' xy closed by repeating the first (matplotlib Path)."""
+    z_thre = pole_pos[2] + 0.08
+    if np.max(ring_pos[:, 2]) > z_thre:
+        return 0.0
+    xy = np.vstack([ring_pos[:, :2], ring_pos[:1, :2]])
+    return 1.0 if point_in_polygon_mpl(xy, pole_pos[0], pole_pos[1]) else 0.0

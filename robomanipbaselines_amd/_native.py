@@ -29,6 +29,7 @@ SIGNATURES = {
     "rmbx_cable_reward": (_c_int, [_c_p] * 5 + [_c_int, _c_int, _c_p]),
     "rmbx_door_reward": (_c_int, [_c_p, _c_p, _c_p, _c_p, _c_int, _c_d, _c_d, _c_p]),
     "rmbx_toolbox_reward": (_c_int, [_c_p, _c_p, _c_p, _c_int, _c_d, _c_d, _c_p]),
+    "rmbx_ring_reward": (_c_int, [_c_p, _c_p, _c_p, _c_int, _c_int, _c_p]),
     "rmbx_cabinet_reward": (_c_int, [_c_p, _c_int, _c_int, _c_int, _c_d, _c_d, _c_int, _c_p, _c_int, _c_p]),
     "rmbx_insert_reward": (_c_int, [_c_p, _c_p, _c_p, _c_p, _c_int, _c_d, _c_d, _c_d, _c_p]),
     "rmbx_ur5e_obs": (_c_int, [_c_p] * 8 + [_c_int, _c_p]),

@@ -19,7 +19,8 @@ import sys
 import yaml
 
 POLICIES = ["Mlp", "Act", "DiffusionPolicy", "DiffusionPolicy3d"]
-ENVS = ["MujocoUR5eCable", "MujocoUR5eInsert", "MujocoUR5eDoor", "MujocoUR5eCabinet", "MujocoUR5eToolbox", "MujocoUR5ePick"]
+ENVS = ["MujocoUR5eCable", "MujocoUR5eInsert", "MujocoUR5eDoor", "MujocoUR5eCabinet", "MujocoUR5eToolbox", "MujocoUR5ePick",
+        "MujocoUR5eRing"]
 
 
 def camel_to_snake(name):

@@ -34,10 +34,13 @@ from ..common.data_utils import make_meta_info
 class PhaseSpec:
     """Timed phase of the pre-rollout motion (PhaseBase.ReachPhaseBase / GraspPhaseBase)."""
 
-    def __init__(self, name, duration, kind, pos_z=None, grip=None):
+    def __init__(self, name, duration, kind, pos_z=None, grip=None, target=None):
         # grip: gripper command of a grasp phase (None = action_space.high, set_target_close;
         # "low" = action_space.low, set_target_open; or a value)
+        # target: reach phases of tasks other than the cable: callable(rollout) -> (R [n, 9],
+        # p [n, 3]) f64 device tensors, the phase's set_target (evaluated when the phase starts)
         self.name, self.duration, self.kind, self.pos_z, self.grip = name, duration, kind, pos_z, grip
+        self.target = target
 
 
 class BatchedRolloutBase:
@@ -94,6 +97,8 @@ class BatchedRolloutBase:
         parser.add_argument("--num_gpus", type=int, default=1,
                             help="shard the envs over this many GPUs of the node (bin/Rollout.py launches one "
                                  "process per GPU; results all-gathered over RCCL)")
+        parser.add_argument("--tactile", action="store_true",
+                            help="scenes with tactile pads: info['intensity_tactile'] every env-step")
         parser.add_argument("--env_offset", type=int, default=0,
                             help="global index of local env 0 (this rank's shard start under --num_gpus): world "
                                  "indices and noise streams follow the global env index")
@@ -294,7 +299,11 @@ class BatchedRolloutBase:
                 if self.phase_idx < n_pre:
                     ph = self.pre_phases[self.phase_idx - 1]
                     if ph.kind == "reach":
-                        self._set_reach_target(ph.pos_z)
+                        if ph.target is not None:
+                            R, p = ph.target(self)
+                            self._tgt_R, self._tgt_p = R.contiguous(), p.contiguous()
+                        else:
+                            self._set_reach_target(ph.pos_z)
                 else:
                     self.rollout_time_idx = 0
         elif self.phase_idx == n_pre:
@@ -303,7 +312,7 @@ class BatchedRolloutBase:
     def step_once(self):
         self._pre_update()
         active = self._active if self._active is not None else self._step_mask
-        self.obs, self.reward, _, _, _ = self.env.step(self.env_action(), active=active)
+        self.obs, self.reward, _, _, self.info = self.env.step(self.env_action(), active=active)
         for _ in range(self.env.frame_skip):
             self.host_time += self.env.sim_timestep
         K.sched_update(self.sched, self.env.get_time(), self.reward, self._pre, self.args.max_duration)

@@ -217,6 +217,104 @@ __global__ void toolbox_reward_kernel(const double* __restrict__ box, const doub
 }
 
 // -----------------------------------------------------------------------------------------
+// Ring-on-pole reward (envs/mujoco/ur5e/MujocoUR5eRingEnv.py:46-75): z gate, then matplotlib's
+// Path(ring xy + first).contains_point(pole xy) -- code-less path, radius 0, identity transform
+// ([ext] matplotlib src/_path.h point_in_path_impl, path_converters.h PathNanRemover): the
+// identity affine poisons both coordinates of a vertex with a non-finite one, non-finite
+// vertices are dropped and the next finite vertex opens a new subpath, a subpath is closed to
+// its start only at the end of the path, crossing-number test per subpath, OR over subpaths.
+// -----------------------------------------------------------------------------------------
+struct MplVertexStream {
+  const double* ring;
+  int n;    // ring bodies; the path has n + 1 vertices (the first repeated)
+  int pos;  // next path vertex
+  bool first;
+  // returns 1 MOVETO, 2 LINETO, 0 STOP
+  __device__ int next(double* x, double* y) {
+    bool gap = false;
+    while (pos <= n) {
+      const double* v = ring + 3 * (pos < n ? pos : 0);
+      pos++;
+      const double X = (v[0] * 1.0 + v[1] * 0.0) + 0.0;
+      const double Y = (v[0] * 0.0 + v[1] * 1.0) + 0.0;
+      if (!(isfinite(X) && isfinite(Y))) {
+        gap = true;
+        continue;
+      }
+      *x = X;
+      *y = Y;
+      const int code = (first || gap) ? 1 : 2;
+      first = false;
+      return code;
+    }
+    return 0;
+  }
+};
+
+__device__ __forceinline__ bool mpl_cross(double vtx0, double vty0, double vtx1, double vty1, double tx, double ty,
+                                          bool yflag1) {
+  return (((vty1 - ty) * (vtx0 - vtx1)) >= ((vtx1 - tx) * (vty0 - vty1))) == yflag1;
+}
+
+__device__ double ring_reward_one(const double* __restrict__ ring, const double* __restrict__ pole, int n) {
+  const double z_thre = pole[2] + 0.08;
+  double zmax = ring[2];
+  bool nan = isnan(zmax);
+  for (int i = 1; i < n; ++i) {
+    const double z = ring[3 * i + 2];
+    nan |= isnan(z);
+    zmax = z > zmax ? z : zmax;
+  }
+  if (!nan && zmax > z_thre) return 0.0;
+  const double tx = pole[0], ty = pole[1];
+  if (!(isfinite(tx) && isfinite(ty))) return 0.0;
+  MplVertexStream st{ring, n, 0, true};
+  bool inside = false;
+  int code = -1;
+  double x = 0.0, y = 0.0;
+  while (true) {
+    if (code != 1) {
+      code = st.next(&x, &y);
+      if (code == 0) break;
+    }
+    const double sx = x, sy = y;
+    double vtx0 = x, vty0 = y, vtx1 = x, vty1 = y;
+    bool yflag0 = vty0 >= ty;
+    bool flag = false;
+    while (true) {
+      code = st.next(&x, &y);
+      if (code == 0) {
+        x = sx;
+        y = sy;
+      } else if (code == 1) {
+        break;
+      }
+      const bool yflag1 = vty1 >= ty;
+      if (yflag0 != yflag1 && mpl_cross(vtx0, vty0, vtx1, vty1, tx, ty, yflag1)) flag = !flag;
+      yflag0 = yflag1;
+      vtx0 = vtx1;
+      vty0 = vty1;
+      vtx1 = x;
+      vty1 = y;
+      if (code == 0) break;
+    }
+    const bool yflag1 = vty1 >= ty;
+    if (yflag0 != yflag1 && mpl_cross(vtx0, vty0, vtx1, vty1, tx, ty, yflag1)) flag = !flag;
+    inside = inside || flag;
+    if (inside || code == 0) break;
+  }
+  return inside ? 1.0 : 0.0;
+}
+
+__global__ void ring_reward_kernel(const double* __restrict__ ring_xpos, const double* __restrict__ pole_xpos,
+                                   double* __restrict__ reward, int n_env, int n_ring) {
+  const int e = blockIdx.x * blockDim.x + threadIdx.x;
+  if (e >= n_env) return;
+  reward[e] = ring_reward_one(ring_xpos + (size_t)e * n_ring * 3, pole_xpos + 3 * (size_t)e, n_ring);
+}
+
+
+// -----------------------------------------------------------------------------------------
 // Door-opening reward (envs/mujoco/ur5e/MujocoUR5eDoorEnv.py:52-67): continuous, success iff 1.0
 // -----------------------------------------------------------------------------------------
 __device__ double door_reward_one(const double* __restrict__ pinch, const double* __restrict__ handle, double angle,
@@ -461,6 +559,17 @@ int rmbx_toolbox_reward(const double* toolbox_xpos, const double* mat_xpos, doub
   if (n_env == 0) return RMBX_OK;
   hipLaunchKernelGGL(toolbox_reward_kernel, dim3((n_env + 255) / 256), dim3(256), 0, as_stream(stream),
                      toolbox_xpos, mat_xpos, reward, n_env, xy_thre, z_offset);
+  RMBX_CHECK_LAUNCH();
+  return RMBX_OK;
+}
+
+int rmbx_ring_reward(const double* ring_xpos, const double* pole_xpos, double* reward, int n_env, int n_ring,
+                     void* stream) {
+  RMBX_CHECK_ARG(n_env >= 0 && n_ring >= 1, "bad sizes n_env=%d n_ring=%d", n_env, n_ring);
+  RMBX_CHECK_ARG(ring_xpos && pole_xpos && reward, "NULL buffer");
+  if (n_env == 0) return RMBX_OK;
+  hipLaunchKernelGGL(ring_reward_kernel, dim3((n_env + 255) / 256), dim3(256), 0, as_stream(stream), ring_xpos,
+                     pole_xpos, reward, n_env, n_ring);
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
 }

@@ -34,7 +34,9 @@ class PhysicsEngine:
         self.qpos = torch.tensor(np.tile(a["qpos0"], (n, 1)), dtype=f64, device=dev)
         self.qvel = torch.zeros((n, self.nv), dtype=f64, device=dev)
         self.qacc_ws = torch.zeros((n, self.nv), dtype=f64, device=dev)
-        self.ctrl = torch.zeros((n, self.nu), dtype=f64, device=dev)
+        # (a model without actuators still binds a non-NULL ctrl: a 1-column store viewed as 0)
+        self._ctrl_store = torch.zeros((n, max(self.nu, 1)), dtype=f64, device=dev)
+        self.ctrl = self._ctrl_store[:, : self.nu]
         self.body_pos = torch.tensor(np.tile(a["body_pos"].reshape(1, -1), (n, 1)), dtype=f64, device=dev).view(n, self.nbody, 3).contiguous()
         self.xpos = torch.zeros((n, self.nbody, 3), dtype=f64, device=dev)
         self.xquat = torch.zeros((n, self.nbody, 4), dtype=f64, device=dev)
@@ -47,7 +49,7 @@ class PhysicsEngine:
         b = N.EnvBuffers()
         for name in ("time", "qpos", "qvel", "qacc_ws", "ctrl", "body_pos", "xpos", "xquat", "gxpos", "gxmat",
                      "sensordata", "stats", "workspace"):
-            setattr(b, name, getattr(self, name).data_ptr())
+            setattr(b, name, (self._ctrl_store if name == "ctrl" else getattr(self, name)).data_ptr())
         self._bufs = b
         N.call("rmbx_engine_bind", self._h, ctypes.byref(b))
 

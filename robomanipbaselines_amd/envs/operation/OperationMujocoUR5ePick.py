@@ -10,7 +10,7 @@ class OperationMujocoUR5ePick:
     def setup_env(self, render_mode=None):
         self.env = BatchedMujocoUR5ePickEnv(
             self.args.num_envs, self.args.device, world_random_scale=self.args.world_random_scale, seed=self.args.seed,
-            env_offset=self.args.env_offset,
+            env_offset=self.args.env_offset, tactile=getattr(self.args, "tactile", False),
         )
 
     def get_pre_motion_phases(self):

@@ -166,6 +166,14 @@ class BatchedMujocoUR5eEnvBase:
         b = self.info.body[body_name]
         return torch.cat([self.engine.xpos[:, b], self.engine.xquat[:, b]], dim=1)
 
+    def get_geom_pose(self, geom_name):
+        """MujocoEnvBase.get_geom_pose: [n, 7] = geom xpos + quaternion of geom xmat (mju_mat2Quat:
+        the largest of trace / diagonal branches)."""
+        g = self.info.geom[geom_name]
+        pos = self.engine.gxpos[:, g]
+        R = self.engine.gxmat[:, g].view(-1, 3, 3)
+        return torch.cat([pos, _mat2quat(R)], dim=1)
+
     # -- internals ----------------------------------------------------------------------------
     def _get_obs(self):
         e = self.engine
@@ -186,3 +194,24 @@ class BatchedMujocoUR5eEnvBase:
         self.renderer.render(self.engine, camera_name, rgb=rgb, depth=depth, policy=policy, active=active,
                              mean=mean, std=std)
         return rgb, depth, policy
+
+
+
+def _mat2quat(R):
+    """mju_mat2Quat for a batch of rotation matrices [n, 3, 3] -> [n, 4] (w, x, y, z): the branch
+    of the largest of the trace and the diagonal, then normalised, as MuJoCo."""
+    m = R.reshape(-1, 9)
+    one = 1.0
+    q0 = 0.5 * torch.sqrt((one + m[:, 0] + m[:, 4] + m[:, 8]).clamp(min=0.0))
+    a = torch.stack([q0, 0.25 * (m[:, 7] - m[:, 5]) / q0, 0.25 * (m[:, 2] - m[:, 6]) / q0, 0.25 * (m[:, 3] - m[:, 1]) / q0], 1)
+    q1 = 0.5 * torch.sqrt((one + m[:, 0] - m[:, 4] - m[:, 8]).clamp(min=0.0))
+    b = torch.stack([0.25 * (m[:, 7] - m[:, 5]) / q1, q1, 0.25 * (m[:, 1] + m[:, 3]) / q1, 0.25 * (m[:, 2] + m[:, 6]) / q1], 1)
+    q2 = 0.5 * torch.sqrt((one - m[:, 0] + m[:, 4] - m[:, 8]).clamp(min=0.0))
+    c = torch.stack([0.25 * (m[:, 2] - m[:, 6]) / q2, 0.25 * (m[:, 1] + m[:, 3]) / q2, q2, 0.25 * (m[:, 5] + m[:, 7]) / q2], 1)
+    q3 = 0.5 * torch.sqrt((one - m[:, 0] - m[:, 4] + m[:, 8]).clamp(min=0.0))
+    d = torch.stack([0.25 * (m[:, 3] - m[:, 1]) / q3, 0.25 * (m[:, 2] + m[:, 6]) / q3, 0.25 * (m[:, 5] + m[:, 7]) / q3, q3], 1)
+    tr = (m[:, 0] + m[:, 4] + m[:, 8]) > 0
+    c1 = (m[:, 0] > m[:, 4]) & (m[:, 0] > m[:, 8])
+    c2 = m[:, 4] > m[:, 8]
+    q = torch.where(tr[:, None], a, torch.where(c1[:, None], b, torch.where(c2[:, None], c, d)))
+    return q / q.norm(dim=1, keepdim=True)

@@ -46,6 +46,19 @@ class BatchedMujocoUR5ePickEnv(BatchedMujocoUR5eEnvBase):
     world_offsets = np.zeros((1, 3))
     intensity_tactile_names = TACTILE_SITES
 
+    def __init__(self, *args, tactile=False, **kw):
+        # tactile=True: step() returns info["intensity_tactile"] every env-step, as
+        # MujocoEnvBase._get_info does when the scene declares tactile sensors (:128-153)
+        self.tactile_enabled = bool(tactile)
+        super().__init__(*args, **kw)
+
+    def step(self, action, active=None):
+        obs, reward, term, trunc, info = super().step(action, active=active)
+        if self.tactile_enabled:
+            tac = self.tactile()
+            info = {"intensity_tactile": {name: tac[:, s] for s, name in enumerate(TACTILE_SITES)}}
+        return obs, reward, term, trunc, info
+
     def _setup_task(self):
         a = self.arrays
         sites = [str(x) for x in a["names_site"]]

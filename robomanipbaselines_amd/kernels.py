@@ -144,6 +144,18 @@ def cable_reward(cable_xpos, end_xpos, pole1, pole2, out=None):
     return out
 
 
+def ring_reward(ring_xpos, pole_xpos, out=None):
+    """MujocoUR5eRingEnv._get_reward for n envs (rmbx_ring_reward); ring_xpos [n, 11, 3] f64."""
+    n, nr, _ = ring_xpos.shape
+    _chk(ring_xpos, torch.float64, (n, nr, 3), "ring_xpos")
+    _chk(pole_xpos, torch.float64, (n, 3), "pole_xpos")
+    if out is None:
+        out = torch.empty(n, dtype=torch.float64, device=ring_xpos.device)
+    _chk(out, torch.float64, (n,), "reward")
+    N.call("rmbx_ring_reward", N.ptr(ring_xpos), N.ptr(pole_xpos), N.ptr(out), n, nr, N.stream_ptr())
+    return out
+
+
 def toolbox_reward(toolbox_xpos, mat_xpos, xy_thre, z_offset, out=None):
     """MujocoUR5eToolboxEnv._get_reward for n envs (rmbx_toolbox_reward)."""
     n = toolbox_xpos.shape[0]

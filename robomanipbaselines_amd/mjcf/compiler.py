@@ -17,6 +17,8 @@ reference, pyproject.toml:34) that the reference's MujocoUR5eCable scene uses
   * <fixed> tendons, <equality> weld/connect/joint, force/torque site sensors, cameras
   * mj_setConst-style constants at qpos0: body/dof inverse weights, mean inertia, connect
     anchors in body2 frames.
+  * <composite type="loop"> (env_ur5e_ring.xml): expanded into its body chain before compiling
+    (_expand_composites).
 
 Substitutions (MuJoCo parity is unpinned: no MuJoCo in this image):
   * by default collision meshes are replaced by their oriented bounding box in the geom frame
@@ -304,6 +306,74 @@ def _drop_empty_free_bodies(node):
     return dropped
 
 
+def _expand_composites(node):
+    """Expand <composite type="loop"> (MuJoCo 3.1.6 user_composite: MakeRope + the loop closure;
+    used by env_ur5e_ring.xml) into explicit MJCF before compiling.  The host body must be named
+    `{prefix}B{ox}`; `count` elements of length `spacing` follow it as a chain of child bodies
+    `{prefix}B{i}` (right of ox, then left of it), each with geom `{prefix}G{i}` (the composite's
+    geom, its axis along the chain: quat rotating z to x) and, except the host, two hinge joints
+    `{prefix}J0_{i}` / `{prefix}J1_{i}` (axes y and z, at the element's start vertex, attributes
+    of <joint kind="main">).  A loop is laid out as the regular polygon it closes into (each
+    element turned 2 pi / count about its z axis from the previous one, so every joint vertex
+    and the closure coincide at qpos0) and closed by a connect equality between the first
+    element's start vertex and the last element's end vertex.  The two closing elements are
+    excluded from colliding with each other like the chain's parent/child neighbours (MuJoCo
+    parity unpinned: MuJoCo is absent from the image).  Returns the number expanded."""
+    count_expanded = 0
+    for body in list(node.iter("body")):
+        for comp in [c for c in body if c.tag == "composite"]:
+            a = comp.attrib
+            if a.get("type") != "loop":
+                raise ValueError(f"composite type {a.get('type')!r} is not supported")
+            prefix = a.get("prefix", "")
+            n = int(_floats(a["count"])[0])
+            s = float(a["spacing"])
+            name = body.attrib.get("name", "")
+            if not name.startswith(prefix + "B"):
+                raise ValueError(f"composite host body {name!r} must be named {prefix}B<index>")
+            ox = int(name[len(prefix) + 1:])
+            if not 0 <= ox < n:
+                raise ValueError("composite host body index out of range")
+            geom_a = next((dict(c.attrib) for c in comp if c.tag == "geom"), {})
+            joint_a = next((dict(c.attrib) for c in comp if c.tag == "joint" and c.attrib.get("kind") == "main"), {})
+            joint_a.pop("kind", None)
+            alpha = 2.0 * math.pi / n
+            r2 = math.sqrt(0.5)
+
+            def element(parent, i):
+                g = ET.SubElement(parent, "geom", dict(geom_a))
+                g.set("name", f"{prefix}G{i}")
+                g.set("pos", "0 0 0")
+                g.set("quat", f"{r2!r} 0 {r2!r} 0")
+
+            body.remove(comp)
+            element(body, ox)
+            for direction in (1, -1):
+                parent = body
+                for i in range(ox + direction, n if direction > 0 else -1, direction):
+                    # next element: to the shared vertex, turn by +-alpha about z, half a spacing on
+                    turn = direction * alpha
+                    child = ET.SubElement(parent, "body", {
+                        "name": f"{prefix}B{i}",
+                        "pos": f"{direction * 0.5 * s * (1 + math.cos(alpha))!r} {0.5 * s * math.sin(alpha)!r} 0",
+                        "quat": f"{math.cos(0.5 * turn)!r} 0 0 {math.sin(0.5 * turn)!r}"})
+                    for k, ax in enumerate(("0 1 0", "0 0 1")):
+                        j = ET.SubElement(child, "joint", dict(joint_a))
+                        j.set("name", f"{prefix}J{k}_{i}")
+                        j.set("type", "hinge")
+                        j.set("pos", f"{-direction * 0.5 * s!r} 0 0")
+                        j.set("axis", ax)
+                    element(child, i)
+                    parent = child
+            eq = ET.SubElement(node, "equality")
+            ET.SubElement(eq, "connect", {"body1": f"{prefix}B0", "body2": f"{prefix}B{n - 1}",
+                                          "anchor": f"{-0.5 * s!r} 0 0"})
+            ct = ET.SubElement(node, "contact")
+            ET.SubElement(ct, "exclude", {"body1": f"{prefix}B0", "body2": f"{prefix}B{n - 1}"})
+            count_expanded += 1
+    return count_expanded
+
+
 def compile_mjcf(path, missing_mesh_box=(0.045, 0.0125, 0.0125), convex_meshes=False, skip_missing_includes=False):
     """Compile the MJCF at `path`.  convex_meshes: mesh geoms collide through the convex hull of
     their vertices (MuJoCo's own mesh collision model) and cylinders as true cylinders, both
@@ -315,6 +385,7 @@ def compile_mjcf(path, missing_mesh_box=(0.045, 0.0125, 0.0125), convex_meshes=F
     missing = [] if skip_missing_includes else None
     _expand_includes_inplace(root, main_dir, missing)
     dropped_bodies = _drop_empty_free_bodies(root) if skip_missing_includes else []
+    _expand_composites(root)
 
     # ---- compiler / option / statistic / visual
     meshdir = main_dir

@@ -146,11 +146,15 @@ class DiffusionPolicyModel(nn.Module):
                 traj = s.step(i, out, traj)
         return traj
 
-    # Graph replay removes launch overhead, which matters at small batches only: at 1024 envs the
-    # DP3 loop takes 75.0 ms eager vs 75.4 ms replayed (scripts/diag_dp3.py).  With MIOpen's
-    # conv1d (the f32 form) capturing at 256+ envs crashed the process, so larger batches run
-    # eagerly.
-    graph_max_batch = 64
+    # Graph replay removes launch overhead, which matters at small batches (at 1024 envs the DP3
+    # loop takes 75.0 ms eager vs 75.4 ms replayed, scripts/diag_dp3.py).  Root cause of the
+    # round-1 capture crash: the f32 UNet ran its Conv1d through MIOpen, whose first call at a new
+    # rollout batch searched solvers (85 s at 1024 envs) and then segfaulted inside the capture
+    # (profiles/r2_dp_capture_1024_fp32_100steps_segv.log).  Every UNet conv is now a hipBLASLt
+    # GEMM in both precisions (unet1d._device_form), so the loop holds no MIOpen call and captures
+    # at 1024 / 2048 envs with replay == eager bit for bit (profiles/r2_dp_capture_gemm_*.log,
+    # tests/test_diffusion_policy_gpu.py): no batch cap.
+    graph_max_batch = None
 
     def conditional_sample(self, global_cond, use_graph=True, x0=None, noise=None):
         """Sample [B, horizon, A].  x0 (initial trajectory) and noise ([n_noise, B, horizon, A])
@@ -165,7 +169,7 @@ class DiffusionPolicyModel(nn.Module):
             x0 = torch.randn(shape, device=dev)
         if noise is None:
             noise = torch.randn((nn_,) + shape, device=dev) if nn_ else None
-        if not use_graph or dev.type != "cuda" or B > self.graph_max_batch:
+        if not use_graph or dev.type != "cuda" or (self.graph_max_batch is not None and B > self.graph_max_batch):
             return self._sample_loop(global_cond, x0.contiguous(), noise)
         key = (B, self.dtype)
         if key not in self._graphs:

@@ -20,15 +20,28 @@ def _small_model(**kw):
 
 
 @torch.no_grad()
-def test_graph_replay_equals_eager():
+@pytest.mark.parametrize("widths,B,dtype", [((64, 128, 256), 5, torch.float32),
+                                            ((512, 1024, 2048), 1024, torch.float32),
+                                            ((512, 1024, 2048), 2048, torch.bfloat16)])
+def test_graph_replay_equals_eager(widths, B, dtype):
+    """The captured 100-step DDPM loop replays bit-identically to the eager loop, up to the
+    production widths and batches of BASELINE configs 3 (DP x2048).  (With MIOpen's f32 conv1d in
+    the loop, capture at 1024 envs crashed the process after an 85 s MIOpen Find: profiles/
+    r2_dp_capture_1024_fp32_100steps_segv.log; the GEMM device form has no MIOpen call to capture:
+    profiles/r2_dp_capture_gemm_*.log.)"""
+    from robomanipbaselines_amd.policy.diffusion_policy.dp_model import DiffusionPolicyModel
+
     torch.backends.cudnn.deterministic = True  # as RolloutDiffusionPolicy sets them
     torch.backends.cudnn.benchmark = False
-    m = _small_model(num_inference_steps=100).to(DEV)
-    B = 5
+    torch.manual_seed(0)
+    m = DiffusionPolicyModel(7, 7, 1, crop_hw=(64, 96), down_dims=widths, num_inference_steps=100)
+    m = m.eval().requires_grad_(False).to(DEV, dtype)
+    assert m.graph_max_batch is None or B <= m.graph_max_batch
     g = torch.Generator(device=DEV).manual_seed(3)
     gc = torch.randn(B, m.obs_feature_dim * 2, device=DEV, generator=g)
     x0 = torch.randn(B, 16, 7, device=DEV, generator=g)
     noise = torch.randn(m._n_noise(), B, 16, 7, device=DEV, generator=g)
+    gc = gc.to(dtype)
     eager = m.conditional_sample(gc, use_graph=False, x0=x0, noise=noise).clone()
     eager2 = m.conditional_sample(gc, use_graph=False, x0=x0, noise=noise).clone()
     graph = m.conditional_sample(gc, use_graph=True, x0=x0, noise=noise).clone()
@@ -191,3 +204,34 @@ def test_unet1d_device_form_matches_fp32():
     got = dev(x.to(DEV, torch.bfloat16), t.to(DEV), gc.to(DEV, torch.bfloat16)).float().cpu()
     assert got.shape == want.shape
     assert (got - want).abs().max().item() <= 5e-2 * max(1.0, want.abs().max().item())
+
+
+@torch.no_grad()
+@pytest.mark.parametrize("kind", ["dp", "dp3"])
+def test_unet1d_production_widths_fp32_and_bf16_error(kind):
+    """ConditionalUnet1D at the production widths (512, 1024, 2048) with DP's / DP3's global
+    condition sizes: the f32 device form (every conv as an f32 hipBLASLt GEMM) against the f32
+    module on the CPU within 1e-4 relative; the bf16 device form's error is measured and bounded."""
+    from robomanipbaselines_amd.policy.diffusion.unet1d import ConditionalUnet1D
+
+    cond = 2 * (512 + 7) if kind == "dp" else 2 * (64 + 64)
+    torch.manual_seed(1)
+    ref = ConditionalUnet1D(7, global_cond_dim=cond, down_dims=(512, 1024, 2048), kernel_size=5,
+                            cond_predict_scale=True).eval()
+    x = torch.randn(8, 16, 7)
+    gc = torch.randn(8, cond)
+    t = torch.tensor(61)
+    want = ref(x, t, gc)
+    scale = max(1.0, want.abs().max().item())
+    dev32 = ConditionalUnet1D(7, global_cond_dim=cond, down_dims=(512, 1024, 2048), kernel_size=5,
+                              cond_predict_scale=True).eval()
+    dev32.load_state_dict(ref.state_dict())
+    dev32 = dev32.to(DEV)
+    got32 = dev32(x.to(DEV), t.to(DEV), gc.to(DEV)).cpu()
+    err32 = (got32 - want).abs().max().item()
+    assert err32 <= 1e-4 * scale, err32
+    dev16 = dev32.to(torch.bfloat16)
+    got16 = dev16(x.to(DEV, torch.bfloat16), t.to(DEV), gc.to(DEV, torch.bfloat16)).float().cpu()
+    err16 = (got16 - want).abs().max().item()
+    print(f"{kind}: fp32 max|d| {err32:.3e}, bf16 max|d| {err16:.3e} (scale {scale:.3f})")
+    assert err16 <= 5e-2 * scale, err16

@@ -80,6 +80,16 @@ def test_toolbox_reward_oracle_bitexact():
     assert 0 < d["reward"].sum() < len(d["reward"])
 
 
+def test_ring_reward_oracle_bitexact():
+    """oracle/glue.ring_reward vs MujocoUR5eRingEnv._get_reward (MujocoUR5eRingEnv.py:46-75,
+    matplotlib Path.contains_point): ties on vertices and edges, self-intersecting rings, the z
+    gate at its threshold, NaN / inf vertices (dropped, subpath split) and NaN poles."""
+    d = _load("reward_ring.npz")
+    got = np.array([glue.ring_reward(r, p) for r, p in zip(d["ring"], d["pole"])])
+    np.testing.assert_array_equal(got, d["reward"])
+    assert 0 < d["reward"].sum() < len(d["reward"])
+
+
 def test_obs_oracle_bitexact():
     d = _load("obs_ur5e.npz")
     for n in range(len(d["qpos"])):

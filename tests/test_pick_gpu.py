@@ -1,0 +1,185 @@
+"""The UR5e Pick scene (BASELINE configs 4/5: env_ur5e_pick.xml minus YCB_sim, dt 0.002 x 16,
+convex-hull collisions for the scanned objects, basket, bin and gripper meshes) through the
+engine against the C oracle, and the synthetic tactile channel (envs/ur5e_pick.py) against a
+numpy restatement of its definition on the oracle's own contacts.
+
+Bars as in test_engine_gpu.py: forward (contact set, constraint rows, qacc 1e-6 relative to
+|qacc|+1), one env-step of 16 substeps qpos 1e-8, a bounded horizon 1e-4 on the arm/gripper."""
+
+import numpy as np
+import pytest
+
+from robomanipbaselines_amd import model as MD
+from robomanipbaselines_amd.envs.ur5e_pick import PICK_INIT_QPOS, TACTILE_INTERVAL, TACTILE_SHAPE, TACTILE_SITES
+
+DEV = "cuda:0"
+FRAME_SKIP = 16
+
+
+@pytest.fixture(scope="module")
+def arrays():
+    return MD.load("ur5e_pick")
+
+
+def _quat2mat(q):
+    w, x, y, z = q
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - z * w), 2 * (x * z + y * w)],
+                     [2 * (x * y + z * w), 1 - 2 * (x * x + z * z), 2 * (y * z - x * w)],
+                     [2 * (x * z - y * w), 2 * (y * z + x * w), 1 - 2 * (x * x + y * y)]])
+
+
+def _oracle(arrays, grip, steps):
+    from oracle.dyn import OracleEnv
+
+    o = OracleEnv(arrays)
+    q = arrays["qpos0"].copy()
+    q[:14] = PICK_INIT_QPOS
+    o.set_state(0.0, q, np.zeros(o.nv), np.zeros(o.nv), np.r_[PICK_INIT_QPOS[:6], grip])
+    for _ in range(steps):
+        assert o.step(FRAME_SKIP) == 0
+    return o
+
+
+def _tactile_ref(arrays, o):
+    """The tactile definition of envs/ur5e_pick.py restated in numpy on oracle contacts."""
+    sites = [str(x) for x in arrays["names_site"]]
+    xpos, xquat = o.xpos()
+    c = o.contacts()
+    cb = np.stack([arrays["geom_body"][arrays["pair_geom1"][c["pair"]]],
+                   arrays["geom_body"][arrays["pair_geom2"][c["pair"]]]], 1)
+    rows, cols = TACTILE_SHAPE
+    out = np.zeros((2, rows, cols))
+    for s, name in enumerate(TACTILE_SITES):
+        si = sites.index(name)
+        b = int(arrays["site_body"][si])
+        Rb = _quat2mat(xquat[b])
+        Rs = Rb @ _quat2mat(arrays["site_quat"][si])
+        sp = xpos[b] + Rb @ arrays["site_pos"][si]
+        nrm = Rs[:, 2]
+        for r in range(rows):
+            for k in range(cols):
+                loc = np.array([(k - (cols - 1) / 2) * TACTILE_INTERVAL, (r - (rows - 1) / 2) * TACTILE_INTERVAL, 0.0])
+                tx = sp + Rs @ loc
+                for j in range(len(c["dist"])):
+                    if b not in cb[j]:
+                        continue
+                    d = c["pos"][j] - tx
+                    d = d - (d @ nrm) * nrm
+                    out[s, r, k] += max(-c["dist"][j], 0.0) * 1000.0 * np.exp(-(d @ d) / (2 * TACTILE_INTERVAL ** 2))
+    return out
+
+
+def test_pick_scene_settles_in_the_oracle(arrays):
+    """The scene is well posed: 40 env-steps from the reference's init_qpos keep every state
+    finite with no divergence reset, and the free objects come to rest."""
+    o = _oracle(arrays, 0.0, 40)
+    _, q, v, _ = o.state()
+    assert np.isfinite(q).all() and np.isfinite(v).all()
+    assert np.abs(v[14:]).max() < 0.05  # the scanned objects' dofs
+    assert np.abs(q[:6] - PICK_INIT_QPOS[:6]).max() < 2e-2  # position-servo sag under gravity
+
+
+def test_oracle_tactile_reference_sees_the_closed_pads(arrays):
+    """Closing the gripper on nothing presses the two pads together: both pads feel it; with the
+    gripper open nothing touches them."""
+    t_open = _tactile_ref(arrays, _oracle(arrays, 0.0, 5))
+    t_closed = _tactile_ref(arrays, _oracle(arrays, 255.0, 20))
+    assert np.all(t_open == 0.0)
+    assert t_closed[0].max() > 1e-4 and t_closed[1].max() > 1e-4
+
+
+def _engine_from(arrays, orcs):
+    import torch
+
+    from robomanipbaselines_amd.engine import PhysicsEngine
+
+    eng = PhysicsEngine(arrays, len(orcs), DEV)
+    st = [o.state() for o in orcs]
+    eng.time.copy_(torch.tensor([s[0] for s in st], dtype=torch.float64))
+    eng.qpos.copy_(torch.tensor(np.array([s[1] for s in st])))
+    eng.qvel.copy_(torch.tensor(np.array([s[2] for s in st])))
+    eng.qacc_ws.copy_(torch.tensor(np.array([s[3] for s in st])))
+    eng.ctrl.copy_(torch.tensor(np.array([o.ctrl for o in orcs])))
+    return eng
+
+
+def _orcs(arrays):
+    out = []
+    for grip, steps in ((0.0, 0), (0.0, 10), (255.0, 20), (120.0, 30)):
+        o = _oracle(arrays, grip, steps)
+        o.ctrl = np.r_[PICK_INIT_QPOS[:6], grip]
+        out.append(o)
+    return out
+
+
+@pytest.mark.gpu
+def test_pick_forward_matches_oracle(arrays):
+    import torch
+
+    orcs = _orcs(arrays)
+    eng = _engine_from(arrays, orcs)
+    eng.forward()
+    torch.cuda.synchronize()
+    stats = eng.stats.cpu().numpy()
+    qacc = eng.ws("qacc").cpu().numpy()
+    xpos = eng.xpos.cpu().numpy()
+    for i, o in enumerate(orcs):
+        o.forward()
+        np.testing.assert_allclose(xpos[i], o.xpos()[0], rtol=0, atol=1e-12)
+        assert stats[i, 0] == o.lib.orc_ncon(o.h), "contact count"
+        assert stats[i, 1] == o.nefc(), "constraint rows"
+        v = o.vecs()
+        scale = np.abs(v["qacc"]).max() + 1.0
+        np.testing.assert_allclose(qacc[i], v["qacc"], rtol=0, atol=1e-6 * scale)
+
+
+@pytest.mark.gpu
+def test_pick_env_step_and_horizon_match_oracle(arrays):
+    import torch
+
+    orcs = _orcs(arrays)
+    eng = _engine_from(arrays, orcs)
+    eng.step(FRAME_SKIP)
+    torch.cuda.synchronize()
+    q1 = eng.qpos.cpu().numpy()
+    for i, o in enumerate(orcs):
+        assert o.step(FRAME_SKIP) == 0
+        np.testing.assert_allclose(q1[i], o.state()[1], rtol=0, atol=1e-8)
+    for _ in range(9):
+        eng.step(FRAME_SKIP)
+        for o in orcs:
+            o.step(FRAME_SKIP)
+    torch.cuda.synchronize()
+    q = eng.qpos.cpu().numpy()
+    for i, o in enumerate(orcs):
+        np.testing.assert_allclose(q[i][:14], o.state()[1][:14], rtol=0, atol=1e-4)
+    assert int(eng.stats[:, 3].sum()) == 0
+    np.testing.assert_allclose(eng.time.cpu().numpy(), [o.state()[0] for o in orcs], rtol=0, atol=1e-12)
+
+
+@pytest.mark.gpu
+def test_pick_env_tactile_matches_reference_definition(arrays):
+    """BatchedMujocoUR5ePickEnv.tactile() on engine state equals the numpy restatement on the
+    oracle's contacts for the same state (open and closed gripper)."""
+    import torch
+
+    from robomanipbaselines_amd.envs.ur5e_pick import BatchedMujocoUR5ePickEnv
+
+    orcs = [_oracle(arrays, 0.0, 5), _oracle(arrays, 255.0, 20)]
+    env = BatchedMujocoUR5ePickEnv(2, DEV)
+    env.reset()
+    e = env.engine
+    st = [o.state() for o in orcs]
+    e.time.copy_(torch.tensor([s[0] for s in st], dtype=torch.float64))
+    e.qpos.copy_(torch.tensor(np.array([s[1] for s in st])))
+    e.qvel.copy_(torch.tensor(np.array([s[2] for s in st])))
+    e.qacc_ws.copy_(torch.tensor(np.array([s[3] for s in st])))
+    e.ctrl.copy_(torch.tensor(np.array([np.r_[PICK_INIT_QPOS[:6], g] for g in (0.0, 255.0)])))
+    e.forward()
+    tac = env.tactile().cpu().numpy()
+    assert tac.shape == (2, 2) + TACTILE_SHAPE
+    for i, o in enumerate(orcs):
+        o.forward()
+        want = _tactile_ref(arrays, o)
+        np.testing.assert_allclose(tac[i], want, rtol=1e-6, atol=1e-9)
+    assert np.all(tac[0] == 0.0) and tac[1].max() > 1e-4

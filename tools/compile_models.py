@@ -13,10 +13,11 @@ SCENES = {"ur5e_cable": os.path.join(REF_ENVS, "ur5e", "env_ur5e_cable.xml"),
           "ur5e_door": os.path.join(REF_ENVS, "ur5e", "env_ur5e_door.xml"),
           "ur5e_cabinet": os.path.join(REF_ENVS, "ur5e", "env_ur5e_cabinet.xml"),
           "ur5e_toolbox": os.path.join(REF_ENVS, "ur5e", "env_ur5e_toolbox.xml"),
-          "ur5e_pick": os.path.join(REF_ENVS, "ur5e", "env_ur5e_pick.xml")}
+          "ur5e_pick": os.path.join(REF_ENVS, "ur5e", "env_ur5e_pick.xml"),
+          "ur5e_ring": os.path.join(REF_ENVS, "ur5e", "env_ur5e_ring.xml")}
 # per-scene compile options: the Pick scene (BASELINE configs 4/5) collides its scanned objects
 # through their convex hulls (MPR) and drops the YCB_sim objects, absent from the checkout
-OPTIONS = {"ur5e_pick": dict(convex_meshes=True, skip_missing_includes=True)}
+OPTIONS = {"ur5e_pick": dict(convex_meshes=True, skip_missing_includes=True), "ur5e_ring": dict(convex_meshes=True)}
 PACK_OPTIONS = {"ur5e_pick": dict(max_contacts=200)}
 UR5E_URDF = "/root/reference/robo_manip_baselines/envs/assets/common/robots/ur5e/ur5e.urdf"
 

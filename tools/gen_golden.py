@@ -464,6 +464,68 @@ def gen_reward_cabinet(importlib):
     print("cabinet reward: successes", int(rewards.sum()), "of", N)
 
 
+def gen_reward_ring(importlib):
+    """MujocoUR5eRingEnv._get_reward (MujocoUR5eRingEnv.py:46-75: z gate, then matplotlib's
+    Path.contains_point of the pole xy in the ring-body polygon) on synthetic 11-body rings:
+    regular and jittered polygons, self-intersecting ones, the pole inside / outside / on a
+    vertex / on a horizontal or vertical edge, z exactly at the threshold, and NaN / inf in the
+    ring (matplotlib drops non-finite vertices and opens a new subpath) or in the pole."""
+    Env = importlib.import_module("robo_manip_baselines.envs.mujoco.ur5e.MujocoUR5eRingEnv").MujocoUR5eRingEnv
+    rng = np.random.default_rng(7171)
+    N, K = 2048, 11
+    ring = np.zeros((N, K, 3))
+    pole = np.zeros((N, 3))
+    rewards = np.zeros(N)
+    for n in range(N):
+        kind = n % 16
+        c = np.array([0.0, 0.1, 0.8]) + rng.normal(0, 0.02, 3)
+        r = rng.uniform(0.04, 0.09)
+        th = 2 * np.pi * np.arange(K) / K + rng.uniform(0, 2 * np.pi)
+        if kind in (1, 2):
+            th = th + rng.normal(0, 0.3, K)  # jittered, may self-intersect
+        rr = r * (1 + rng.normal(0, 0.1, K)) if kind != 3 else r * np.ones(K)
+        pts = np.stack([c[0] + rr * np.cos(th), c[1] + rr * np.sin(th), c[2] + rng.uniform(-0.02, 0.02, K)], 1)
+        if kind == 4:
+            pts[:, :2] = np.round(pts[:, :2] * 64) / 64  # exact binary grid: on-edge / vertex ties
+        p = np.array([c[0], c[1], c[2] - rng.uniform(0.0, 0.12)]) + np.r_[rng.normal(0, 0.05, 2), 0.0]
+        if kind == 5:
+            p[:2] = pts[rng.integers(K), :2]  # on a vertex
+        if kind == 6:
+            i = rng.integers(K)
+            j = (i + 1) % K
+            pts[j, 1] = pts[i, 1]  # a horizontal edge, pole on it
+            p[:2] = [0.5 * (pts[i, 0] + pts[j, 0]), pts[i, 1]]
+        if kind == 7:
+            i = rng.integers(K)
+            j = (i + 1) % K
+            pts[j, 0] = pts[i, 0]  # a vertical edge, pole on it
+            p[:2] = [pts[i, 0], 0.5 * (pts[i, 1] + pts[j, 1])]
+        if kind == 8:
+            p[2] = pts[:, 2].max() - 0.08  # z exactly at the threshold (strict >)
+        if kind == 9:
+            p[2] = pts[:, 2].max() - 0.07  # ring above the threshold
+        if kind == 10:
+            pts[rng.integers(K), 2] = np.nan
+        if kind == 11:
+            pts[rng.integers(K), rng.integers(2)] = np.nan  # vertex dropped, subpath split
+        if kind == 12:
+            pts[0, 0] = np.nan  # the first (and closing) vertex dropped
+        if kind == 13:
+            pts[rng.integers(K), 1] = np.inf
+        if kind == 14:
+            p[rng.integers(2)] = np.nan
+        if kind == 15:
+            p[:2] = c[:2] + rng.normal(0, 0.005, 2)  # well inside
+        ring[n], pole[n] = pts, p
+        env = object.__new__(Env)
+        env.ring_body_ids = list(range(K))
+        env.data = types.SimpleNamespace(xpos=pts.copy(),
+                                         body=lambda nm, _p=p.copy(): types.SimpleNamespace(xpos=_p))
+        rewards[n] = env._get_reward()
+    np.savez(os.path.join(OUT, "reward_ring.npz"), ring=ring, pole=pole, reward=rewards)
+    print("ring reward: successes", int(rewards.sum()), "of", N)
+
+
 def gen_reward_toolbox(importlib):
     """MujocoUR5eToolboxEnv._get_reward (MujocoUR5eToolboxEnv.py:46-57) on synthetic toolbox / mat
     positions around the 3 cm x/y window and the mat height + 5 mm (exact values, NaN)."""
@@ -832,6 +894,7 @@ def main():
     gen_reward_door(importlib)
     gen_reward_cabinet(importlib)
     gen_reward_toolbox(importlib)
+    gen_reward_ring(importlib)
     gen_obs(importlib)
     gen_depth_and_pointcloud(importlib)
     gen_phase_schedule(importlib)
