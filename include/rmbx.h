@@ -185,8 +185,13 @@ int rmbx_sched_active(const rmbx_sched_t* sched, int n_pre, uint8_t* active, int
  *   envs/mujoco/MujocoEnvBase.py:82-97 step() -> gymnasium do_simulation -> mujoco.mj_step x
  *   frame_skip (MujocoEnvBase.py:12-13: dt 0.004, frame_skip 8) + mj_rnePostConstraint,
  * and MujocoEnvBase.py:163-165 reset_model (state set by the caller).
- * One wavefront per environment; nsub substeps fused in one launch.  The model comes from
- * include/rmbx_model.h (host pointers, copied to the device at create).
+ * Per substep two launches over all envs: a front kernel (one wavefront per env: kinematics,
+ * composite inertia, RNE, collision, constraint rows) and a solver kernel (256 threads per env:
+ * Newton solve, forces, sensors, implicitfast integration).  The constraint Jacobian is never
+ * stored (rows are described by contact / joint / equality data; J x, J^T w and the Hessian
+ * chunks are computed from the dof axes in LDS) and the mass matrix is kept as packed lower
+ * 4x4 blocks.  The model comes from include/rmbx_model.h (host pointers, copied to the device
+ * at create).
  * ------------------------------------------------------------------------------------------- */
 typedef struct rmbx_engine rmbx_engine;
 struct rmbx_model;
@@ -222,9 +227,9 @@ int rmbx_engine_step(rmbx_engine* eng, int nsub, const uint8_t* active, void* st
 /* mj_forward only (no integration): fills the outputs and workspace for inspection. */
 int rmbx_engine_forward(rmbx_engine* eng, const uint8_t* active, void* stream);
 /* Diagnostic: step all envs and accumulate per-stage shader cycles into stage_cycles
- * [n_env][24] (u64, device): kinematics, com/crb, velocity+rne+actuation, collision,
+ * [n_env][32] (u64, device): kinematics, com/crb, velocity+rne+actuation, collision,
  * constraints, solver, sensors, integration; 8-15 solver sub-stages, 16-18 collision
- * sub-stages, 20-23 constraint sub-stages. */
+ * sub-stages, 20-23 constraint sub-stages, 24-30 J^T w / J x / M x pass internals. */
 int rmbx_engine_step_profiled(rmbx_engine* eng, int nsub, uint64_t* stage_cycles, void* stream);
 
 /* ---------------------------------------------------------------------------------------------

@@ -3,13 +3,14 @@
 // Replaces the reference's per-env env.step -> gymnasium do_simulation -> mujoco.mj_step x 8
 // (envs/mujoco/MujocoEnvBase.py:82-97, :12-13) for thousands of envs in lockstep.
 //
-// Execution model: ONE WAVEFRONT (64 lanes) PER ENVIRONMENT, all `nsub` substeps fused in one
-// launch.  Lanes split the data-parallel stages (geoms, pairs, contacts, constraint rows, dofs,
-// matrix rows/columns); tree recursions (kinematics, composite inertia, RNE) run on lane 0.  The
-// dense nv x nv matrix being factorised (M, the Newton Hessian, the implicitfast matrix) lives
-// in LDS (37 KB at nv = 68); per-env vectors and the constraint Jacobian live in a per-env
-// workspace slice in HBM (L2/MALL-resident at these sizes).  Algorithm, stage for stage, is the
-// one restated serially in oracle/dyn_oracle.c (see that header for the MuJoCo mapping).
+// Execution model, per substep: front_kernel (ONE WAVEFRONT per env; lanes split the
+// data-parallel stages -- bodies for the tree passes (pointer-jumping prefixes, DFS subtree
+// ranges), geoms, pairs, contacts, constraint rows) then solver_kernel (256 threads per env: the
+// nv x nv Newton Hessian / mass-matrix factorisations as 4x4 register blocks, one per thread of
+// the lower triangle).  Between the two, per-env data lives in a workspace slice (mass matrix
+// as packed lower 4x4 blocks, dof axes, contacts, row data); the constraint Jacobian is never
+// materialised (see the ROW_* comment below).  Algorithm, stage for stage, is the one restated
+// serially in oracle/dyn_oracle.c (see that header for the MuJoCo mapping).
 
 #include <cstring>
 #include <string>
@@ -29,20 +30,36 @@ namespace rmbx {
 struct Layout {
   size_t stride;  // doubles per env
   size_t xmat, xipos, xanchor, xaxis, sxpos, sxmat, cdof, cdofdot, cinert, crb, cvel, cacc, cfrc;
-  size_t M;
+  size_t Mblk;  // mass matrix as packed lower-triangle 4x4 blocks (block t = bi(bi+1)/2 + bj)
   size_t qfrc_bias, qfrc_passive, qfrc_actuator, qfrc_smooth, qacc_smooth, qfrc_constraint, qacc,
       res, Mres, grad, search, Ms, tmp;
   size_t ten_len, ten_vel;
   size_t con_pos, con_frame, con_dist, con_mu;
   size_t con_tmp;  // collision stage: 4 candidate contacts (pos, normal, dist) per survivor
   size_t hsave;    // solver: Hessian blocks of the last build (incremental updates)
-  size_t J, efc_pos, efc_aref, efc_D, efc_R, efc_force, efc_jar, efc_Js, efc_vel, efc_tmp;
+  size_t efc_pos, efc_aref, efc_D, efc_sqD, efc_R, efc_force, efc_jar, efc_Js, efc_vel, efc_tmp;
+  size_t efc_rho;  // contact rows: (p x dir, dir), J_r = efc_rho . (V_b2 - V_b1)
+  size_t eqr_rho, eqr_coef;  // equality rows: 2 body-side 6-vectors, 2 dof coefficients
   size_t ints;  // start of the int32 region (in doubles)
   // int32 offsets relative to the int region
-  size_t con_b1, con_b2, con_condim, con_pair, con_efcadr, efc_type, efc_act, efc_hact, scal;
+  size_t con_b1, con_b2, con_condim, con_pair, con_efcadr, efc_type, efc_act, efc_hact, efc_kind,
+      efc_obj, eqr_body, eqr_dof, scal;
   size_t istride;  // int32 count
   int nefc_max;
+  int neqr_max;  // equality rows (6 per weld)
 };
+
+// Constraint rows are never materialised as a dense Jacobian.  Row r is described by
+// (efc_kind[r] = kind | sub << 3, efc_obj[r]):
+//   ROW_CONTACT  obj = contact c, sub = pyramid edge t (0..3) or 4 (frictionless normal):
+//                J_r = dir_t . (v_b2(p) - v_b1(p)), the relative velocity at the contact point,
+//                = efc_rho . (V_b2 - V_b1) with efc_rho = (p x dir_t, dir_t)
+//   ROW_LIMIT    obj = dof, sub = 0 (+1) / 1 (-1)
+//   ROW_EQ       obj = equality-row slot s: J_r = sum over the two sides of
+//                [dof on chain(eqr_body)] cdof . eqr_rho + the dof terms (eqr_dof, eqr_coef)
+// so J x is a tree pass (body velocities of x) plus one 6-dot per row, J^T w a pass of body
+// wrenches summed over subtrees, and a Hessian chunk is computed from cdof in LDS.
+enum { ROW_CONTACT = 0, ROW_LIMIT = 1, ROW_EQ = 2 };
 
 struct rmbx_engine_impl;
 
@@ -52,6 +69,7 @@ struct rmbx_engine {
   rmbx_model host;       // copy of scalars (pointers unused)
   rmbx_model dev;        // device pointers
   const int32_t* subtree_end;  // device [nbody]: DFS subtree ranges for the tree passes
+  int tree_rounds;             // ceil(log2(max body depth + 1)) (solver pointer jumping)
   std::vector<void*> allocations;
   rmbx::Layout L;
   int n_env;
@@ -86,9 +104,15 @@ struct Env {
 #define WI(name) (e.iw + e.L->name)
 
 __device__ __forceinline__ void sync() { __syncthreads(); }
+// Block barrier for LDS traffic only (the CK block_sync_lds idiom): waits for this wave's LDS
+// and scalar-memory operations, then s_barrier.  __syncthreads() is a workgroup fence as well and
+// drains every outstanding global load and store (vmcnt(0)) -- ~1-2k cycles after a global store
+// -- so it stays only where threads hand data to each other through global memory.
+__device__ __forceinline__ void lds_sync() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 __device__ __forceinline__ unsigned long long stamp() { return __builtin_readcyclecounter(); }
-// diagnostic cycle slots per env: 0-7 stages, 8-15 solver, 16-19 collision, 20-23 constraints
-#define RMBX_PROF_SLOTS 24
+// diagnostic cycle slots per env: 0-7 stages, 8-15 solver, 16-19 collision, 20-23 constraints,
+// 24-27 J^T w passes, 28-31 J x / M x passes
+#define RMBX_PROF_SLOTS 32
 #define SUBPROF(k)                                \
   if (prof) {                                     \
     __syncthreads();                              \
@@ -359,20 +383,39 @@ __device__ void com_pos_crb(Env& e, int lane, const int32_t* subtree_end) {
   for (int k = lane; k < 10 * nb; k += 64) W(cinert)[k] = cinert[k];
   for (int k = lane; k < 6 * nv; k += 64) W(cdof)[k] = cdof[k];
   sync();
-  double* M = W(M);
-  for (int i = lane; i < nv; i += 64) {
-    double F[6];
-    inert_mul(crb + 10 * m.dof_body[i], cdof + 6 * i, F);
-    for (int j = 0; j < nv; j++) M[i * nv + j] = 0;
-    for (int j = i; j >= 0; j = m.dof_parent[j]) M[i * nv + j] = dot6(cdof + 6 * j, F);
+  // lower triangle, lane = row i: M_ij = cdof_j . (crb_body(i) cdof_i) for dofs j on i's chain,
+  // written straight into the packed 4x4 blocks the solver loads (zeros off the chain; the
+  // upper half of a diagonal block is never read; padding rows get the identity)
+  double* Mb = W(Mblk);
+  const int NVP = 4 * ((nv + 3) / 4);
+  for (int i = lane; i < NVP; i += 64) {
+    double F[6] = {0, 0, 0, 0, 0, 0};
+    int bi_ = 0;
+    if (i < nv) {
+      bi_ = m.dof_body[i];
+      inert_mul(crb + 10 * bi_, cdof + 6 * i, F);
+    }
+    const int bi = i >> 2, p = i & 3;
+    for (int bj = 0; bj <= bi; bj++) {
+      double* blk = Mb + 16 * (bi * (bi + 1) / 2 + bj) + 4 * p;
+#pragma unroll
+      for (int q = 0; q < 4; q++) {
+        const int c = 4 * bj + q;
+        double v;
+        if (i >= nv || c >= nv) {
+          v = i == c ? 1.0 : 0.0;
+        } else if (c > i) {
+          v = 0.0;
+        } else {
+          const int bc = m.dof_body[c];
+          const bool anc = bc == bi_ || (bc < bi_ && bi_ < subtree_end[bc]);
+          v = anc ? dot6(cdof + 6 * c, F) : 0.0;
+          if (c == i) v += m.dof_armature[i];
+        }
+        blk[q] = v;
+      }
+    }
   }
-  sync();
-  // symmetrise (lower triangle computed along each dof's ancestor chain) + armature
-  for (int k = lane; k < nv * nv; k += 64) {
-    const int i = k / nv, j = k % nv;
-    if (j > i) M[k] = M[j * nv + i];
-  }
-  for (int i = lane; i < nv; i += 64) M[i * nv + i] += m.dof_armature[i];
   sync();
 }
 
@@ -1668,38 +1711,10 @@ __device__ __forceinline__ int last_dof(const rmbx_model& m, int b) {
   return m.body_dofadr[w] + m.body_dofnum[w] - 1;
 }
 
-// dot product of a (global) row with x; four independent accumulators keep several loads in
-// flight per thread
-__device__ __forceinline__ double dot_row(const double* __restrict__ a, const double* x, int n) {
-  double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-  int k = 0;
-  for (; k + 3 < n; k += 4) {
-    s0 += a[k] * x[k];
-    s1 += a[k + 1] * x[k + 1];
-    s2 += a[k + 2] * x[k + 2];
-    s3 += a[k + 3] * x[k + 3];
-  }
-  for (; k < n; k++) s0 += a[k] * x[k];
-  return (s0 + s1) + (s2 + s3);
-}
-
 // dof k moves body b (its body is b or an ancestor of b: DFS subtree range test)
 __device__ __forceinline__ bool dof_on_chain(const Env& e, int k, int b) {
   const int a = e.m->dof_body[k];
   return a <= b && b < e.subtree_end[a];
-}
-
-__device__ void jac_point_dir(const Env& e, int b, const double* p, const double* dir, double sgn,
-                              double* row) {
-  const rmbx_model& m = *e.m;
-  const double* cdof = LDS_CDOF(e);
-  for (int k = last_dof(m, b); k >= 0; k = m.dof_parent[k]) {
-    const double* S = cdof + 6 * k;
-    double wxp[3];
-    cross3(S, p, wxp);
-    const double v[3] = {S[3] + wxp[0], S[4] + wxp[1], S[5] + wxp[2]};
-    row[k] += sgn * dot3(v, dir);
-  }
 }
 
 __device__ double impedance(const double* solimp, double x) {
@@ -1738,13 +1753,53 @@ __device__ void set_row(Env& e, int r, int type, double pos, double diag, const 
   W(efc_R)[r] = R < RMBX_MINVAL ? RMBX_MINVAL : R;
 }
 
-// returns nefc; equality rows first (count in *ne)
-__device__ int make_constraints(Env& e, int lane, int ncon, int* ne_out, unsigned long long* prof) {
+// pyramid edge t of a contact (t = 4: the normal of a frictionless contact), the row directions
+// of mj_instantiateContact: normal +- mu * tangent_(t/2)
+__device__ __forceinline__ void contact_dir(const double* F, double mu, int t, double* dir) {
+  if (t == 4) {
+    dir[0] = F[0];
+    dir[1] = F[1];
+    dir[2] = F[2];
+    return;
+  }
+  const double s = (t & 1) ? -mu : mu;
+  const double* T = F + 3 * (1 + (t >> 1));
+#pragma unroll
+  for (int i = 0; i < 3; i++) dir[i] = F[i] + s * T[i];
+}
+
+// 6-dot with a depth-3 dependency tree (three products, two pair sums, one final sum) instead
+// of the 6-long FMA chain of dot6: each dependent f64 op costs ~32 cycles on a wave
+__device__ __forceinline__ double dot6t(const double* a, const double* b) {
+  const double p0 = fma(a[0], b[0], a[1] * b[1]);
+  const double p1 = fma(a[2], b[2], a[3] * b[3]);
+  const double p2 = fma(a[4], b[4], a[5] * b[5]);
+  return (p0 + p1) + p2;
+}
+
+// velocity of point p on body b2 relative to body b1, from per-body spatial velocities V
+// (6 per body: angular, linear at the world origin; V of the world body is zero)
+__device__ __forceinline__ void rel_point_vel(const double* V, int b1, int b2, const double* p, double* u) {
+  double d[6];
+#pragma unroll
+  for (int i = 0; i < 6; i++) d[i] = V[6 * b2 + i] - V[6 * b1 + i];
+  double wxp[3];
+  cross3(d, p, wxp);
+#pragma unroll
+  for (int i = 0; i < 3; i++) u[i] = d[3 + i] + wxp[i];
+}
+
+// returns nefc; equality rows first (count in *ne).  Rows are described, not materialised (see
+// the ROW_* comment at the top): each row gets its kind/object, the equality rows their two
+// body-side 6-vectors, and efc_vel = J qvel is evaluated from the body velocities cvel.
+__device__ int make_constraints(Env& e, int lane, int ncon, int* ne_out, int* nlim_out, unsigned long long* prof) {
   const rmbx_model& m = *e.m;
   unsigned long long tp = prof ? stamp() : 0;
-  const int nv = m.nv;
   const int nefc_max = e.L->nefc_max;
-  double* J = W(J);
+  const double* cvel = W(cvel);  // (the LDS copy is collision scratch by now)
+  int32_t* kind = WI(efc_kind);
+  int32_t* obj = WI(efc_obj);
+  double* vel = W(efc_vel);
   // count rows: equality
   int ne = 0;
   for (int q = 0; q < m.neq; q++) ne += m.eq_type[q] == RMBX_EQ_CONNECT ? 3 : (m.eq_type[q] == RMBX_EQ_WELD ? 6 : 1);
@@ -1753,17 +1808,11 @@ __device__ int make_constraints(Env& e, int lane, int ncon, int* ne_out, unsigne
   for (int base = 0; base < m.njnt; base += 64) {
     const int j = base + lane;
     int cnt = 0;
-    double d0 = 0, d1 = 0;
     if (j < m.njnt && m.jnt_limited[j]) {
       const double q = e.qpos[m.jnt_qposadr[j]];
-      d0 = q - m.jnt_range[2 * j];
-      d1 = m.jnt_range[2 * j + 1] - q;
-      cnt = (d0 < 0) + (d1 < 0);
+      cnt = (q - m.jnt_range[2 * j] < 0) + (m.jnt_range[2 * j + 1] - q < 0);
     }
-    int total;
-    const int off = wave_excl_scan(cnt, lane, &total);
-    (void)off;
-    nlim += total;
+    nlim += wave_sum_i(cnt);
   }
   // contacts rows (wave-parallel count)
   int nconrow = 0;
@@ -1773,15 +1822,16 @@ __device__ int make_constraints(Env& e, int lane, int ncon, int* ne_out, unsigne
   }
   int nefc = ne + nlim + nconrow;
   if (nefc > nefc_max) nefc = nefc_max;
-  // zero the Jacobian rows in use
-  for (size_t k = lane; k < (size_t)nefc * nv; k += 64) J[k] = 0;
-  sync();
   SUBPROF(20)
   // equality rows: every lane evaluates the constraint's anchors/errors (cheap, no broadcast),
-  // lanes < nrows set the row parameters, then the Jacobian is filled lane-per-dof with the
-  // same per-entry accumulation order as the serial chain walks (0 + body-1 term + body-2 term)
-  const double* cdof = LDS_CDOF(e);
-  int r = 0;
+  // lane i < nrows describes row i: connect/weld translation J = J_p1(o1) e_i - J_p2(o2) e_i,
+  // i.e. body-side vectors (p1 x e_i, e_i) and -(p2 x e_i, e_i); weld rotation
+  // J = 0.5 d10 Im(conj(q1 r) (0, w) q2)_i with w = +cdof_ang on chain(o2), -cdof_ang on chain(o1)
+  int r = 0, s = 0;
+  double* eq_rho = W(eqr_rho);
+  double* eq_coef = W(eqr_coef);
+  int32_t* eq_body = WI(eqr_body);
+  int32_t* eq_dof = WI(eqr_dof);
   for (int q = 0; q < m.neq; q++) {
     const double* data = m.eq_data + RMBX_EQ_DATA * q;
     const double* sr = m.eq_solref + 2 * q;
@@ -1823,44 +1873,49 @@ __device__ int make_constraints(Env& e, int lane, int ncon, int* ne_out, unsigne
       double nrm = 0;
       for (int i = 0; i < nr; i++) nrm += err[i] * err[i];
       nrm = sqrt(nrm);
-      if (lane < 3) {
-        const double diag_t = m.body_invweight0[2 * o1] + m.body_invweight0[2 * o2];
-        set_row(e, r + lane, 0, err[lane], diag_t, sr, si, nrm);
-      } else if (nr == 6 && lane < 6) {
-        const double diag_r = m.body_invweight0[2 * o1 + 1] + m.body_invweight0[2 * o2 + 1];
-        set_row(e, r + lane, 0, err[lane], diag_r, sr, si, nrm);
-      }
-      for (int k = lane; k < nv; k += 64) {
-        const bool c1 = dof_on_chain(e, k, o1), c2 = dof_on_chain(e, k, o2);
-        if (!c1 && !c2) continue;
-        const double* S = cdof + 6 * k;
-        double v1[3], v2[3], w[3];
-        cross3(S, p1, w);
-        for (int i = 0; i < 3; i++) v1[i] = S[3 + i] + w[i];
-        cross3(S, p2, w);
-        for (int i = 0; i < 3; i++) v2[i] = S[3 + i] + w[i];
-        for (int i = 0; i < 3; i++) {
-          double dir[3] = {0, 0, 0};
-          dir[i] = 1;
-          double val = 0;
-          if (c1) val += 1.0 * dot3(v1, dir);
-          if (c2) val += -1.0 * dot3(v2, dir);
-          J[(size_t)(r + i) * nv + k] = val;
-        }
-        if (nr == 6) {
-          // rotational rows: body-2 chain (+) then body-1 chain (-); shared dofs cancel exactly
-          for (int pass = 0; pass < 2; pass++) {
-            if (!(pass == 0 ? c2 : c1)) continue;
-            const double sg = pass == 0 ? 1.0 : -1.0;
-            const double wq[4] = {0, sg * S[0], sg * S[1], sg * S[2]};
-            double t1[4], t2[4];
+      if (lane < nr) {
+        double rho1[6], rho2[6];
+        if (lane < 3) {
+          const double diag_t = m.body_invweight0[2 * o1] + m.body_invweight0[2 * o2];
+          set_row(e, r + lane, 0, err[lane], diag_t, sr, si, nrm);
+          double ei[3] = {0, 0, 0}, c2[3];
+          ei[lane] = 1;
+          cross3(p1, ei, rho1);
+          cross3(p2, ei, c2);
+          for (int i = 0; i < 3; i++) {
+            rho1[3 + i] = ei[i];
+            rho2[i] = -c2[i];
+            rho2[3 + i] = -ei[i];
+          }
+        } else {
+          const double diag_r = m.body_invweight0[2 * o1 + 1] + m.body_invweight0[2 * o2 + 1];
+          set_row(e, r + lane, 0, err[lane], diag_r, sr, si, nrm);
+          const int i = lane - 3;
+          for (int j = 0; j < 3; j++) {
+            double wq[4] = {0, 0, 0, 0}, t1[4], t2[4];
+            wq[1 + j] = 1;
             quatmul(cq1, wq, t1);
             quatmul(t1, xq2, t2);
-            for (int i = 0; i < 3; i++) J[(size_t)(r + 3 + i) * nv + k] += 0.5 * t2[1 + i] * data[10];
+            rho2[j] = 0.5 * t2[1 + i] * data[10];
+            rho1[j] = -rho2[j];
+            rho1[3 + j] = rho2[3 + j] = 0.0;
           }
         }
+        const int sl = s + lane;
+        for (int i = 0; i < 6; i++) {
+          eq_rho[12 * sl + i] = rho1[i];
+          eq_rho[12 * sl + 6 + i] = rho2[i];
+        }
+        eq_body[2 * sl] = o1;
+        eq_body[2 * sl + 1] = o2;
+        eq_dof[2 * sl] = eq_dof[2 * sl + 1] = -1;
+        eq_coef[2 * sl] = eq_coef[2 * sl + 1] = 0.0;
+        kind[r + lane] = ROW_EQ;
+        obj[r + lane] = sl;
+        vel[r + lane] = dot6(rho1, cvel + 6 * o1) + dot6(rho2, cvel + 6 * o2);
       }
       r += nr;
+      s += nr;
     } else {
       if (lane == 0) {
         const int j1 = o1, j2 = o2;
@@ -1872,10 +1927,18 @@ __device__ int make_constraints(Env& e, int lane, int ncon, int* ne_out, unsigne
         const double err = q1 - poly;
         const int d1 = m.jnt_dofadr[j1], d2 = m.jnt_dofadr[j2];
         set_row(e, r, 0, err, m.dof_invweight0[d1] + m.dof_invweight0[d2], sr, si, err);
-        J[(size_t)r * nv + d1] += 1;
-        J[(size_t)r * nv + d2] -= dpoly;
+        for (int i = 0; i < 12; i++) eq_rho[12 * s + i] = 0.0;
+        eq_body[2 * s] = eq_body[2 * s + 1] = 0;
+        eq_dof[2 * s] = d1;
+        eq_dof[2 * s + 1] = d2;
+        eq_coef[2 * s] = 1.0;
+        eq_coef[2 * s + 1] = -dpoly;
+        kind[r] = ROW_EQ;
+        obj[r] = s;
+        vel[r] = e.qvel[d1] - dpoly * e.qvel[d2];
       }
       r++;
+      s++;
     }
   }
   SUBPROF(21)
@@ -1898,12 +1961,16 @@ __device__ int make_constraints(Env& e, int lane, int ncon, int* ne_out, unsigne
       const int da = m.jnt_dofadr[j];
       if (d0 < 0 && r < nefc) {
         set_row(e, r, 1, d0, m.dof_invweight0[da], m.jnt_solref + 2 * j, m.jnt_solimp + 5 * j, d0);
-        J[(size_t)r * nv + da] = 1.0;
+        kind[r] = ROW_LIMIT;
+        obj[r] = da;
+        vel[r] = e.qvel[da];
         r++;
       }
       if (d1 < 0 && r < nefc) {
         set_row(e, r, 1, d1, m.dof_invweight0[da], m.jnt_solref + 2 * j, m.jnt_solimp + 5 * j, d1);
-        J[(size_t)r * nv + da] = -1.0;
+        kind[r] = ROW_LIMIT | (1 << 3);
+        obj[r] = da;
+        vel[r] = -e.qvel[da];
       }
     }
     rbase += total;
@@ -1925,38 +1992,22 @@ __device__ int make_constraints(Env& e, int lane, int ncon, int* ne_out, unsigne
       const double dist = W(con_dist)[c] - m.pair_margin[p];
       const double* sr = m.pair_solref + 2 * p;
       const double* si = m.pair_solimp + 5 * p;
-      double dirs[4][3];
-      if (cnt == 1) {
-        for (int i = 0; i < 3; i++) dirs[0][i] = F[i];
-        if (r0 < nefc) set_row(e, r0, 1, dist, tran, sr, si, dist);
-      } else {
-        const double mu = W(con_mu)[c];
-        int t4 = 0;
-        for (int t = 0; t < 2; t++)
-          for (int sg = 0; sg < 2; sg++) {
-            const double s = sg == 0 ? mu : -mu;
-            for (int i = 0; i < 3; i++) dirs[t4][i] = F[i] + s * F[3 * (1 + t) + i];
-            if (r0 + t4 < nefc) set_row(e, r0 + t4, 1, dist, tran * (1 + mu * mu), sr, si, dist);
-            t4++;
-          }
-      }
-      const int nrow = min(cnt, nefc - r0);
-      // both chains are evaluated at the same point with the same directions, so dofs shared
-      // by the two bodies cancel exactly (x - x = +0, the zeroed entry): each chain is walked
-      // only up to the common ancestor and its entries stored (0 + x, as the accumulation gives)
-      for (int pass = 0; pass < 2 && nrow > 0; pass++) {
-        const int b = pass == 0 ? b2 : b1, other = pass == 0 ? b1 : b2;
-        const double sgn = pass == 0 ? 1.0 : -1.0;
-        for (int k = last_dof(m, b); k >= 0; k = m.dof_parent[k]) {
-          if (dof_on_chain(e, k, other)) break;
-          const double* Sk = cdof + 6 * k;
-          double wxp[3];
-          cross3(Sk, pos, wxp);
-          const double v[3] = {Sk[3] + wxp[0], Sk[4] + wxp[1], Sk[5] + wxp[2]};
-#pragma unroll
-          for (int t = 0; t < 4; t++)
-            if (t < nrow) J[(size_t)(r0 + t) * nv + k] = 0.0 + sgn * dot3(v, dirs[t]);
-        }
+      const double mu = W(con_mu)[c];
+      double dv[6];
+      for (int i = 0; i < 6; i++) dv[i] = cvel[6 * b2 + i] - cvel[6 * b1 + i];
+      for (int t = 0; t < cnt; t++) {
+        const int rr = r0 + t;
+        if (rr >= nefc) break;
+        const int tt = cnt == 1 ? 4 : t;
+        set_row(e, rr, 1, dist, cnt == 1 ? tran : tran * (1 + mu * mu), sr, si, dist);
+        double rho[6];
+        contact_dir(F, mu, tt, rho + 3);
+        cross3(pos, rho + 3, rho);
+        double* dst = W(efc_rho) + 6 * (size_t)rr;
+        for (int i = 0; i < 6; i++) dst[i] = rho[i];
+        kind[rr] = ROW_CONTACT | (tt << 3);
+        obj[rr] = c;
+        vel[rr] = dot6t(rho, dv);
       }
     }
     rbase += total;
@@ -1965,14 +2016,15 @@ __device__ int make_constraints(Env& e, int lane, int ncon, int* ne_out, unsigne
   SUBPROF(22)
   // aref = -b (J qvel) - k imp pos ; D = 1/R
   for (int r = lane; r < nefc; r += 64) {
-    const double v = dot_row(J + (size_t)r * nv, e.qvel, nv);
-    W(efc_vel)[r] = v;
-    W(efc_aref)[r] = -W(efc_tmp)[r] * v - W(efc_D)[r];
-    W(efc_D)[r] = 1.0 / W(efc_R)[r];
+    W(efc_aref)[r] = -W(efc_tmp)[r] * vel[r] - W(efc_D)[r];
+    const double D = 1.0 / W(efc_R)[r];
+    W(efc_D)[r] = D;
+    W(efc_sqD)[r] = sqrt(D);  // the Hessian's row weight
   }
   sync();
   SUBPROF(23)
   *ne_out = ne;
+  *nlim_out = min(nlim, nefc - ne);
   return nefc;
 }
 
@@ -2056,10 +2108,15 @@ __device__ void sensors(Env& e, int ncon, int tid, double* cacc, double* cfrc, d
 // The constraint Jacobian streams from the workspace (HBM/L2) through a 16-row LDS chunk.
 // ------------------------------------------------------------------------------------------
 #define SOLVER_THREADS 256
-#define MAX_NB 22  // nv <= 88
+#define MAX_NB 18  // nv <= 72
 #define MAX_NVP (4 * MAX_NB)
 #define RCHUNK 16
 #define MAX_BODY 64
+#define NEQR 24     // equality rows staged in LDS (6 per weld, 3 per connect, 1 per joint)
+#define MAX_LIM 128 // limit rows staged in LDS (2 per limited joint)
+#define MAX_CON 208  // contacts (J^T w: one wrench per contact in S.cw)
+#define EQ_TAG 1024
+static_assert(NEQR + MAX_LIM <= RCHUNK * 12, "J^T w stages the equality/limit row weights in S.jrho");
 
 struct SolverShared {
   double Lcol[MAX_NB][16];  // Cholesky: current block column, by block row
@@ -2073,18 +2130,60 @@ struct SolverShared {
   double srch[MAX_NVP];
   double Ms[MAX_NVP];
   double acc[MAX_NVP];
-  double acc2[SOLVER_THREADS];  // column-reduction partials
   double tmp[MAX_NVP];
-  double jc[RCHUNK][MAX_NVP];  // scaled Jacobian chunk
+  union {
+    double jc[RCHUNK][MAX_NVP];  // Hessian: scaled Jacobian chunk
+    double cw[6 * MAX_CON];      // J^T w: contact wrenches (sensors: the same)
+  };
+  double jrho[RCHUNK][12];     // chunk rows: the two body-side 6-vectors
+  double jcoef[RCHUNK][2];     // chunk rows: dof-term coefficients
   double jw[RCHUNK];           // chunk row weights sqrt(D) (active rows)
   double jsg[RCHUNK];          // chunk row signs (incremental Hessian: +1 added, -1 removed)
-  double jw2[RCHUNK];          // sqrt(D) * jar (gradient)
-  double bacc[6 * MAX_BODY];  // sensors: body accelerations
-  double bfrc[6 * MAX_BODY];  // sensors: body forces
+  double bv[6 * MAX_BODY];     // body velocities of a dof vector / subtree sums (sensors: cacc)
+  double bf[6 * MAX_BODY];     // body forces (sensors: cfrc)
+  double cdof[6 * MAX_NVP];    // motion axes of the dofs (from the front kernel)
+  double cinert[10 * MAX_BODY];
   double red[8];
   int ired[8];
-  int anc[MAX_BODY];          // tree-pass ancestor pointers
+  int jb[RCHUNK][2];           // chunk rows: the two bodies
+  int jd[RCHUNK][2];           // chunk rows: dof terms (-1: none)
+  double eqrho[NEQR][12];      // equality rows: body-side 6-vectors, dof coefficients,
+  double eqcoef[NEQR][2];      //   bodies, dofs (-1: none) -- staged once per launch
+  int16_t eqb[NEQR][2];
+  int16_t eqd[NEQR][2];
+  int16_t ccb[MAX_CON][2];     // contact bodies (b1, b2)
+  // per-body list of the wrenches J^T w collects, in contact order then equality-row order:
+  // entry 2q (+, body = b2 of contact q), 2q + 1 (-, b1), EQ_TAG + 2s + side (equality row s)
+  int16_t blist[2 * MAX_CON + 2 * NEQR];
+  int16_t boff[MAX_BODY + 1];
+  int16_t lim[MAX_LIM];        // limit rows: 2 * dof + (1 if the row's sign is -1)
+  int anc[MAX_BODY];           // tree-pass ancestor pointers
+  int16_t par[MAX_BODY];       // body parents
+  int16_t send[MAX_BODY];      // end of each body's DFS subtree id range
+  int16_t kb[MAX_NVP];         // dof -> body
 };
+
+// X[6b..] <- sum of the increments X over the path world .. b (solver block; parents from LDS)
+__device__ void tree_prefix6_s(SolverShared& S, int nbody, int rounds, double* X, int b) {
+  if (b < nbody) S.anc[b] = b == 0 ? -1 : S.par[b];
+  lds_sync();
+  for (int round = 0; round < rounds; round++) {  // ceil(log2(tree depth + 1)) pointer jumps
+    const int a = b < nbody ? S.anc[b] : -1;
+    const bool act = a >= 0;
+    double v[6];
+    int an = -1;
+    if (act) {
+      for (int i = 0; i < 6; i++) v[i] = X[6 * a + i] + X[6 * b + i];
+      an = S.anc[a];
+    }
+    lds_sync();
+    if (act) {
+      for (int i = 0; i < 6; i++) X[6 * b + i] = v[i];
+      S.anc[b] = an;
+    }
+    lds_sync();
+  }
+}
 
 __device__ __forceinline__ void blk_coords(int t, int* bi, int* bj) {
   int i = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
@@ -2096,16 +2195,16 @@ __device__ __forceinline__ void blk_coords(int t, int* bi, int* bj) {
 
 __device__ __forceinline__ double block_sum(double v, SolverShared& S, int tid) {
   v = wave_sum(v);
-  __syncthreads();
+  lds_sync();
   if ((tid & 63) == 0) S.red[tid >> 6] = v;
-  __syncthreads();
+  lds_sync();
   return S.red[0] + S.red[1] + S.red[2] + S.red[3];
 }
 __device__ __forceinline__ int block_sum_i(int v, SolverShared& S, int tid) {
   v = wave_sum_i(v);
-  __syncthreads();
+  lds_sync();
   if ((tid & 63) == 0) S.ired[tid >> 6] = v;
-  __syncthreads();
+  lds_sync();
   return S.ired[0] + S.ired[1] + S.ired[2] + S.ired[3];
 }
 
@@ -2164,13 +2263,13 @@ __device__ void blk_cholesky(double* a, int bi, int bj, bool own, int NB, Solver
     for (int q = 0; q < 4; q++) S.Ldinv[q] = inv[q];
   }
   for (int k = 0; k < NB; k++) {
-    __syncthreads();
+    lds_sync();
     if (own && bj == k && bi > k) {
       trsm4(a, S.Ldiag, S.Ldinv);
 #pragma unroll
       for (int q = 0; q < 16; q++) S.Lcol[bi][q] = a[q];
     }
-    __syncthreads();
+    lds_sync();
     if (own && bj > k) {
       const double* Li = S.Lcol[bi];
       const double* Lj = S.Lcol[bj];
@@ -2193,7 +2292,107 @@ __device__ void blk_cholesky(double* a, int bi, int bj, bool own, int NB, Solver
       }
     }
   }
-  __syncthreads();
+  lds_sync();
+}
+
+// y_k = L_kk^-1 S.acc[4k..4k+3] in place (inv = reciprocals of diag(L_kk) from potrf4)
+__device__ __forceinline__ void fwd4(const double* a, const double* inv, double* y) {
+  double v[4];
+#pragma unroll
+  for (int p = 0; p < 4; p++) {
+    double t = y[p];
+#pragma unroll
+    for (int k = 0; k < p; k++) t -= a[4 * p + k] * v[k];
+    v[p] = t * inv[p];
+  }
+#pragma unroll
+  for (int p = 0; p < 4; p++) y[p] = v[p];
+}
+
+// blk_cholesky with the forward substitution of b folded in: on return the blocks hold L and
+// S.acc holds y = L^-1 b (b: LDS, length NVP).  No extra barriers: in each step's trsm phase the
+// owners of column k also eliminate y_k from their rows of the right-hand side, and the owner of
+// the next diagonal block solves its block of y right after factoring it.
+__device__ void blk_cholesky_fwd(double* a, int bi, int bj, bool own, int NB, const double* b, SolverShared& S,
+                                 int tid) {
+  for (int r = tid; r < 4 * NB; r += SOLVER_THREADS) S.acc[r] = b[r];
+  lds_sync();
+  if (own && bi == 0 && bj == 0) {
+    double inv[4];
+    potrf4(a, inv);
+#pragma unroll
+    for (int q = 0; q < 16; q++) S.Ldiag[q] = a[q];
+#pragma unroll
+    for (int q = 0; q < 4; q++) S.Ldinv[q] = inv[q];
+    fwd4(a, inv, S.acc);
+  }
+  for (int k = 0; k < NB; k++) {
+    lds_sync();
+    if (own && bj == k && bi > k) {
+      trsm4(a, S.Ldiag, S.Ldinv);
+#pragma unroll
+      for (int q = 0; q < 16; q++) S.Lcol[bi][q] = a[q];
+      const double* y = S.acc + 4 * k;
+#pragma unroll
+      for (int p = 0; p < 4; p++)
+        S.acc[4 * bi + p] -= a[4 * p] * y[0] + a[4 * p + 1] * y[1] + a[4 * p + 2] * y[2] + a[4 * p + 3] * y[3];
+    }
+    lds_sync();
+    if (own && bj > k) {
+      const double* Li = S.Lcol[bi];
+      const double* Lj = S.Lcol[bj];
+#pragma unroll
+      for (int p = 0; p < 4; p++)
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+          double t = a[4 * p + q];
+#pragma unroll
+          for (int r = 0; r < 4; r++) t -= Li[4 * p + r] * Lj[4 * q + r];
+          a[4 * p + q] = t;
+        }
+      if (bi == k + 1 && bj == k + 1) {
+        double inv[4];
+        potrf4(a, inv);
+#pragma unroll
+        for (int q = 0; q < 16; q++) S.Ldiag[q] = a[q];  // read after the next barrier
+#pragma unroll
+        for (int q = 0; q < 4; q++) S.Ldinv[q] = inv[q];
+        fwd4(a, inv, S.acc + 4 * (k + 1));
+      }
+    }
+  }
+  lds_sync();
+}
+
+// x = L^-T S.acc (the backward half of blk_solve; S.acc = L^-1 b from blk_cholesky_fwd)
+__device__ void blk_solve_back(const double* a, int bi, int bj, bool own, int NB, double* x, SolverShared& S,
+                               int tid) {
+  for (int i = NB - 1; i >= 0; i--) {
+    if (own && bi == i && bj == i) {
+      double xx[4], inv[4];
+#pragma unroll
+      for (int p = 0; p < 4; p++) inv[p] = 1.0 / a[4 * p + p];
+#pragma unroll
+      for (int p = 3; p >= 0; p--) {
+        double t = S.acc[4 * i + p];
+#pragma unroll
+        for (int k = p + 1; k < 4; k++) t -= a[4 * k + p] * xx[k];
+        xx[p] = t * inv[p];
+      }
+#pragma unroll
+      for (int p = 0; p < 4; p++) S.acc[4 * i + p] = xx[p];
+    }
+    lds_sync();
+    if (own && bi == i && bj < i) {
+      const double* xi = S.acc + 4 * i;
+#pragma unroll
+      for (int q = 0; q < 4; q++)
+        S.acc[4 * bj + q] -= a[q] * xi[0] + a[4 + q] * xi[1] + a[8 + q] * xi[2] + a[12 + q] * xi[3];
+    }
+    lds_sync();
+  }
+  for (int r = tid; r < 4 * NB; r += SOLVER_THREADS) x[r] = S.acc[r];
+  lds_sync();
 }
 
 // x = (L L^T)^-1 b ; b, x in LDS (length NVP, may alias); uses S.acc
@@ -2201,7 +2400,7 @@ __device__ void blk_solve(const double* a, int bi, int bj, bool own, int NB, con
                           double* x, SolverShared& S, int tid) {
   const int NVP = 4 * NB;
   for (int r = tid; r < NVP; r += SOLVER_THREADS) S.acc[r] = b[r];
-  __syncthreads();
+  lds_sync();
   // forward: y_j = L_jj^-1 (acc_j); acc_i -= L_ij y_j
   for (int j = 0; j < NB; j++) {
     if (own && bi == j && bj == j) {
@@ -2218,14 +2417,14 @@ __device__ void blk_solve(const double* a, int bi, int bj, bool own, int NB, con
 #pragma unroll
       for (int p = 0; p < 4; p++) S.acc[4 * j + p] = y[p];
     }
-    __syncthreads();
+    lds_sync();
     if (own && bj == j && bi > j) {
       const double* y = S.acc + 4 * j;
 #pragma unroll
       for (int p = 0; p < 4; p++)
         S.acc[4 * bi + p] -= a[4 * p] * y[0] + a[4 * p + 1] * y[1] + a[4 * p + 2] * y[2] + a[4 * p + 3] * y[3];
     }
-    __syncthreads();
+    lds_sync();
   }
   // backward: x_i = L_ii^-T acc_i ; acc_j -= L_ij^T x_i
   for (int i = NB - 1; i >= 0; i--) {
@@ -2243,91 +2442,246 @@ __device__ void blk_solve(const double* a, int bi, int bj, bool own, int NB, con
 #pragma unroll
       for (int p = 0; p < 4; p++) S.acc[4 * i + p] = xx[p];
     }
-    __syncthreads();
+    lds_sync();
     if (own && bi == i && bj < i) {
       const double* xi = S.acc + 4 * i;
 #pragma unroll
       for (int q = 0; q < 4; q++)
         S.acc[4 * bj + q] -= a[q] * xi[0] + a[4 + q] * xi[1] + a[8 + q] * xi[2] + a[12 + q] * xi[3];
     }
-    __syncthreads();
+    lds_sync();
   }
   for (int r = tid; r < NVP; r += SOLVER_THREADS) x[r] = S.acc[r];
-  __syncthreads();
+  lds_sync();
 }
 
-// load block (bi, bj) of the dense nv x nv matrix (zero/identity padding beyond nv)
-__device__ __forceinline__ void load_block(const double* M, int nv, int bi, int bj, double* a) {
+// load this thread's block of the packed mass matrix (16 contiguous doubles)
+__device__ __forceinline__ void load_blockp(const double* Mb, int t, double* a) {
+  const double2* src = reinterpret_cast<const double2*>(Mb + 16 * (size_t)t);
 #pragma unroll
-  for (int p = 0; p < 4; p++)
-#pragma unroll
-    for (int q = 0; q < 4; q++) {
-      const int r = 4 * bi + p, c = 4 * bj + q;
-      a[4 * p + q] = (r < nv && c < nv) ? M[(size_t)r * nv + c] : (r == c ? 1.0 : 0.0);
-    }
-}
-
-// y = M x, thread per row (M dense in global), vectors in LDS
-// y = M x (thread per row)
-__device__ void mat_vec(const double* M, int nv, const double* x, double* y, int tid) {
-  for (int i = tid; i < nv; i += SOLVER_THREADS) y[i] = dot_row(M + (size_t)i * nv, x, nv);
-  __syncthreads();
-}
-
-// out[r] = J_r . x for r < nefc (thread per row)
-__device__ void jac_vec(const double* J, int nefc, int nv, const double* x, double* out, int tid) {
-  for (int r = tid; r < nefc; r += SOLVER_THREADS) out[r] = dot_row(J + (size_t)r * nv, x, nv);
-  __syncthreads();
-}
-
-// out[k] = sum_r J[r][k] w[r] (w in LDS): the block splits the rows into G = SOLVER_THREADS / nv
-// interleaved groups (coalesced row reads, 4 rows in flight per thread), partial column sums
-// meet in LDS (part: G * nv doubles).  Returns the column sum for threads tid < nv.
-__device__ double col_reduce(const double* J, int nefc, int nv, const double* w, double* part, int tid) {
-  const int G = SOLVER_THREADS / nv;
-  const int g = tid / nv, k = tid - g * nv;
-  if (g < G) {
-    double s0 = 0, s1 = 0, s2 = 0, s3 = 0;
-    int r = g;
-    for (; r + 3 * G < nefc; r += 4 * G) {
-      s0 += J[(size_t)r * nv + k] * w[r];
-      s1 += J[(size_t)(r + G) * nv + k] * w[r + G];
-      s2 += J[(size_t)(r + 2 * G) * nv + k] * w[r + 2 * G];
-      s3 += J[(size_t)(r + 3 * G) * nv + k] * w[r + 3 * G];
-    }
-    for (; r < nefc; r += G) s0 += J[(size_t)r * nv + k] * w[r];
-    part[g * nv + k] = (s0 + s1) + (s2 + s3);
+  for (int q = 0; q < 8; q++) {
+    const double2 v = src[q];
+    a[2 * q] = v.x;
+    a[2 * q + 1] = v.y;
   }
-  __syncthreads();
-  double out = 0;
-  if (tid < nv)
-    for (int q = 0; q < G; q++) out += part[q * nv + tid];
-  __syncthreads();
-  return out;
 }
 
 struct SolverCtx {
-  const double* J;
+  const rmbx_model* m;
   const double* aref;
   const double* D;
+  const double* sqD;
+  const double* rho;
   const int32_t* type;
+  const int32_t* kind;
+  const int32_t* obj;
+  const double* cpos;
+  const double* cframe;
+  const double* cmu;
+  const int32_t* cb1;
+  const int32_t* cb2;
+  const int32_t* ccondim;
+  const int32_t* cefcadr;
+  const double* eq_rho;
+  const double* eq_coef;
+  const int32_t* eq_body;
+  const int32_t* eq_dof;
   double* jar;
   double* Js;
   double* force;
-  int nefc, ne, nv, NB, tid;
+  double* wrow;  // per-row weights handed to jac_tmul
+  unsigned long long* prof;  // diagnostic cycle slots (or NULL)
+  int nefc, ne, nlim, ncon, nv, NB, tid, tree_rounds;
 };
+#define CPROF(k)                                  \
+  if (c.prof) {                                   \
+    lds_sync();                                   \
+    const unsigned long long t_ = stamp();        \
+    if (c.tid == 0) c.prof[k] += t_ - tp_;        \
+    tp_ = t_;                                     \
+  }
 
-// cost at S.a (or at x): sets jar, res, Mres; returns cost
-__device__ double solver_cost(const SolverCtx& c, const double* M, const double* x, SolverShared& S) {
+// body velocities of the dof vector x (LDS): S.bv[b] = sum over the dofs on b's chain of
+// cdof_k x_k -- per-body increments, then the pointer-jumping prefix over the tree
+__device__ void body_vel(const SolverCtx& c, const double* x, SolverShared& S) {
+  const rmbx_model& m = *c.m;
+  const int b = c.tid;
+  unsigned long long tp_ = c.prof ? stamp() : 0;
+  if (b < m.nbody) {
+    double v[6] = {0, 0, 0, 0, 0, 0};
+    if (b > 0)
+      for (int k = m.body_dofadr[b]; k < m.body_dofadr[b] + m.body_dofnum[b]; k++) {
+        const double xk = x[k];
+#pragma unroll
+        for (int i = 0; i < 6; i++) v[i] += S.cdof[6 * k + i] * xk;
+      }
+#pragma unroll
+    for (int i = 0; i < 6; i++) S.bv[6 * b + i] = v[i];
+  }
+  lds_sync();
+  CPROF(28)
+  tree_prefix6_s(S, m.nbody, c.tree_rounds, S.bv, b);
+  CPROF(29)
+}
+
+// (J x)_r from the body velocities of x (S.bv) and x itself
+__device__ __forceinline__ double row_dot(const SolverCtx& c, int r, const SolverShared& S, const double* x) {
+  const int kd = c.kind[r], k = kd & 7, sub = kd >> 3, o = c.obj[r];
+  if (k == ROW_CONTACT) {
+    const double* rho = c.rho + 6 * (size_t)r;
+    const double* v2 = S.bv + 6 * S.ccb[o][1];
+    const double* v1 = S.bv + 6 * S.ccb[o][0];
+    double d[6];
+#pragma unroll
+    for (int i = 0; i < 6; i++) d[i] = v2[i] - v1[i];
+    return dot6t(rho, d);
+  }
+  if (k == ROW_LIMIT) return sub ? -x[o] : x[o];
+  const double* rho = S.eqrho[o];
+  double v = dot6t(rho, S.bv + 6 * S.eqb[o][0]) + dot6t(rho + 6, S.bv + 6 * S.eqb[o][1]);
+  const int d1 = S.eqd[o][0], d2 = S.eqd[o][1];
+  if (d1 >= 0) v += S.eqcoef[o][0] * x[d1];
+  if (d2 >= 0) v += S.eqcoef[o][1] * x[d2];
+  return v;
+}
+
+// S.bv[b] <- sum of S.bf over b's subtree (b > 0; the world's entry is left alone).  Bodies are
+// in DFS preorder, so a subtree is the id range [b, send[b]): wave 0 (lane = body) takes an
+// inclusive prefix scan over the ids (6 shuffle rounds) and each subtree sum is the difference
+// of two prefix values -- instead of a loop over up to nbody descendants per lane.
+__device__ __forceinline__ void subtree_sums(const SolverCtx& c, SolverShared& S) {
+  const int b = c.tid;
+  const int nb = c.m->nbody;
+  if (b < 64) {
+    double x[6];
+#pragma unroll
+    for (int i = 0; i < 6; i++) x[i] = (b > 0 && b < nb) ? S.bf[6 * b + i] : 0.0;  // (world: unused)
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+#pragma unroll
+      for (int i = 0; i < 6; i++) {
+        const double y = __shfl_up(x[i], off, 64);
+        if (b >= off) x[i] += y;
+      }
+    }
+    if (b < nb)
+#pragma unroll
+      for (int i = 0; i < 6; i++) S.bf[6 * b + i] = x[i];
+  }
+  lds_sync();
+  if (b > 0 && b < nb) {
+    const double* hi = S.bf + 6 * (S.send[b] - 1);
+    const double* lo = S.bf + 6 * (b - 1);
+#pragma unroll
+    for (int i = 0; i < 6; i++) S.bv[6 * b + i] = hi[i] - lo[i];
+  }
+  lds_sync();
+}
+
+// y = M x without M: body forces cinert_b V_b(x) summed over subtrees, projected on the dofs
+// (plus armature).  Expects S.bv = body_vel(x); S.bv is consumed (holds the subtree sums after).
+__device__ void mass_tail(const SolverCtx& c, const double* x, double* y, SolverShared& S) {
+  const rmbx_model& m = *c.m;
+  const int tid = c.tid;
+  unsigned long long tp_ = c.prof ? stamp() : 0;
+  if (tid > 0 && tid < m.nbody) {
+    double f[6];
+    inert_mul(S.cinert + 10 * tid, S.bv + 6 * tid, f);
+#pragma unroll
+    for (int i = 0; i < 6; i++) S.bf[6 * tid + i] = f[i];
+  }
+  lds_sync();
+  subtree_sums(c, S);
+  for (int k = tid; k < 4 * c.NB; k += SOLVER_THREADS)
+    y[k] = k < c.nv ? dot6(S.cdof + 6 * k, S.bv + 6 * S.kb[k]) + m.dof_armature[k] * x[k] : 0.0;
+  lds_sync();
+  CPROF(30)
+}
+
+// out = J^T w (w: per-row weights in global, out: LDS dof vector).  Contact rows fold into one
+// wrench per contact about the origin ((p x f, f), f = sum of w_r dir_r), bodies collect their
+// contacts' (+ on b2, - on b1) and equality rows' wrenches in a fixed order, subtree sums carry
+// them to the dofs, and the limit / joint-equality dof terms are added per dof.
+__device__ void jac_tmul(const SolverCtx& c, const double* w, double* out, SolverShared& S) {
+  const rmbx_model& m = *c.m;
+  const int tid = c.tid;
+  double* cw = S.cw;
+  double* wst = &S.jrho[0][0];  // w of the equality and limit rows (NEQR + MAX_LIM <= 16 * 12)
+  __syncthreads();  // w was written row-per-thread through global memory: full fence
+  unsigned long long tp_ = c.prof ? stamp() : 0;
+  // contact wrench about the origin = sum over the contact's rows of w_r (p x dir_r, dir_r)
+  for (int q = tid; q < c.ncon; q += SOLVER_THREADS) {
+    const int r0 = c.cefcadr[q];
+    const int cnt = min(c.ccondim[q] == 1 ? 1 : 4, c.nefc - r0);
+    double f[6] = {0, 0, 0, 0, 0, 0};
+    for (int t = 0; t < cnt; t++) {
+      const double wr = w[r0 + t];
+      const double* rho = c.rho + 6 * (size_t)(r0 + t);
+#pragma unroll
+      for (int i = 0; i < 6; i++) f[i] += wr * rho[i];
+    }
+#pragma unroll
+    for (int i = 0; i < 6; i++) cw[6 * q + i] = f[i];
+  }
+  for (int i = tid; i < c.ne + c.nlim; i += SOLVER_THREADS) wst[i] = w[i];
+  lds_sync();
+  CPROF(24)
+  if (tid > 0 && tid < m.nbody) {
+    double acc[6] = {0, 0, 0, 0, 0, 0};
+    for (int l = S.boff[tid]; l < S.boff[tid + 1]; l++) {
+      const int en = S.blist[l];
+      if (en < EQ_TAG) {
+        const double* wq = cw + 6 * (en >> 1);
+        const double sg = (en & 1) ? -1.0 : 1.0;
+#pragma unroll
+        for (int i = 0; i < 6; i++) acc[i] += sg * wq[i];
+      } else {
+        const int s = (en - EQ_TAG) >> 1;
+        const double ws = wst[s];
+        const double* rho = S.eqrho[s] + 6 * (en & 1);
+#pragma unroll
+        for (int i = 0; i < 6; i++) acc[i] += ws * rho[i];
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 6; i++) S.bf[6 * tid + i] = acc[i];
+  }
+  lds_sync();
+  CPROF(25)
+  subtree_sums(c, S);
+  CPROF(26)
+  for (int k = tid; k < 4 * c.NB; k += SOLVER_THREADS) {
+    double v = 0.0;
+    if (k < c.nv) {
+      v = dot6(S.cdof + 6 * k, S.bv + 6 * S.kb[k]);
+      for (int s = 0; s < c.ne; s++) {
+        if (S.eqd[s][0] == k) v += S.eqcoef[s][0] * wst[s];
+        if (S.eqd[s][1] == k) v += S.eqcoef[s][1] * wst[s];
+      }
+      for (int i = 0; i < c.nlim; i++) {
+        const int l = S.lim[i];
+        if ((l >> 1) == k) v += (l & 1) ? -wst[c.ne + i] : wst[c.ne + i];
+      }
+    }
+    out[k] = v;
+  }
+  lds_sync();
+  CPROF(27)
+}
+
+// cost at x: sets jar (J x - aref), S.res, S.Mres; returns cost
+__device__ double solver_cost(const SolverCtx& c, const double* x, SolverShared& S) {
   const int tid = c.tid;
   for (int k = tid; k < 4 * c.NB; k += SOLVER_THREADS) S.res[k] = k < c.nv ? x[k] - S.a0[k] : 0.0;
-  __syncthreads();
-  mat_vec(M, c.nv, S.res, S.Mres, tid);
+  lds_sync();
+  body_vel(c, S.res, S);
+  mass_tail(c, S.res, S.Mres, S);
   double part = 0;
   for (int k = tid; k < c.nv; k += SOLVER_THREADS) part += S.res[k] * S.Mres[k];
+  body_vel(c, x, S);
   double cpart = 0;
   for (int r = tid; r < c.nefc; r += SOLVER_THREADS) {
-    const double jar = dot_row(c.J + (size_t)r * c.nv, x, c.nv) - c.aref[r];
+    const double jar = row_dot(c, r, S, x) - c.aref[r];
     c.jar[r] = jar;
     if (c.type[r] == 0 || jar < 0) cpart += 0.5 * c.D[r] * jar * jar;
   }
@@ -2336,34 +2690,33 @@ __device__ double solver_cost(const SolverCtx& c, const double* M, const double*
 
 // constraint part of the cost at x: jar = J x - aref (c.jar), sum of 0.5 D jar^2 over active rows
 __device__ double rows_cost(const SolverCtx& c, const double* x, SolverShared& S) {
+  body_vel(c, x, S);
   double cpart = 0;
   for (int r = c.tid; r < c.nefc; r += SOLVER_THREADS) {
-    const double jar = dot_row(c.J + (size_t)r * c.nv, x, c.nv) - c.aref[r];
+    const double jar = row_dot(c, r, S, x) - c.aref[r];
     c.jar[r] = jar;
     if (c.type[r] == 0 || jar < 0) cpart += 0.5 * c.D[r] * jar * jar;
   }
   return block_sum(cpart, S, c.tid);
 }
 
-// Gradient S.grad = M res + J^T (D_act jar) (thread per column, coalesced row reads) and the
-// row activity flags; *changed = the active set differs from the one last factorised.
-// Returns |g|^2.
+// Gradient S.grad = M res + J^T (D_act jar) and the row activity flags; *changed = the active
+// set differs from the one last factorised.  Returns |g|^2.
 __device__ double solver_grad(const SolverCtx& c, int32_t* act_flags, SolverShared& S, bool* changed) {
   const int tid = c.tid, nv = c.nv, NVP = 4 * c.NB;
-  double* w2 = &S.jc[0][0];  // D_act jar per row (nefc <= RCHUNK * MAX_NVP)
   int diff = 0;
   for (int r = tid; r < c.nefc; r += SOLVER_THREADS) {
     const double jar = c.jar[r];
     const int act = (c.type[r] == 0 || jar < 0) ? 1 : 0;
-    w2[r] = act ? c.D[r] * jar : 0.0;
+    c.wrow[r] = act ? c.D[r] * jar : 0.0;
     diff |= act != act_flags[r];
     act_flags[r] = act;
   }
   *changed = block_sum_i(diff, S, tid) != 0;  // (barrier inside)
-  const double jtw = col_reduce(c.J, c.nefc, nv, w2, S.acc2, tid);
+  jac_tmul(c, c.wrow, S.acc, S);
   double gn = 0;
   if (tid < nv) {
-    const double g = S.Mres[tid] + jtw;
+    const double g = S.Mres[tid] + S.acc[tid];
     S.grad[tid] = g;
     gn = g * g;
   } else if (tid < NVP) {
@@ -2372,57 +2725,109 @@ __device__ double solver_grad(const SolverCtx& c, int32_t* act_flags, SolverShar
   return block_sum(gn, S, tid);
 }
 
-// Hessian blocks a = M + J^T D_act J (active rows only; J streamed through LDS in RCHUNK-row
-// chunks scaled by sqrt(D))
-// Hessian blocks a = M + J^T D_act J (active rows only; J streamed through LDS in RCHUNK-row
-// chunks scaled by sqrt(D)).  The first build of a substep starts from M; later ones start from
-// the previous H (saved in the workspace) and only add / subtract the rows whose active flag
-// changed since (hess_flags), skipping chunks without such rows — MuJoCo's Newton solver updates
-// its Hessian incrementally in the same way.
-__device__ void solver_hessian(const SolverCtx& c, const double* M, const int32_t* act_flags, int32_t* hess_flags,
+// Hessian blocks a = M + J^T D_act J (active rows only), in RCHUNK-row chunks of J computed in
+// LDS from the row descriptions and cdof (scaled by sqrt(D)).  The first build of a substep
+// starts from M; later ones start from the previous H (saved in the workspace) and only add /
+// subtract the rows whose active flag changed since (hess_flags), skipping chunks without such
+// rows -- MuJoCo's Newton solver updates its Hessian incrementally in the same way.
+__device__ void solver_hessian(const SolverCtx& c, const double* Mb, const int32_t* act_flags, int32_t* hess_flags,
                                double* hsave, bool incremental, double* a, int bi, int bj, bool own,
                                SolverShared& S) {
   const int tid = c.tid, nv = c.nv, NVP = 4 * c.NB;
+  __syncthreads();  // act_flags were written row-per-thread through global memory: full fence
+  unsigned long long tp_ = c.prof ? stamp() : 0;
   if (own) {
     if (incremental) {
 #pragma unroll
       for (int q = 0; q < 16; q++) a[q] = hsave[16 * tid + q];
     } else {
-      load_block(M, nv, bi, bj, a);
+      load_blockp(Mb, tid, a);
     }
   }
   for (int r0 = 0; r0 < c.nefc; r0 += RCHUNK) {
     const int nr = min(RCHUNK, c.nefc - r0);
-    __syncthreads();
+    lds_sync();
     if (tid < RCHUNK) {
       double w = 0.0, sg = 1.0;
       if (tid < nr) {
         const int r = r0 + tid;
         const int act = act_flags[r];
+        const double Dr = c.sqD[r];
+        const int kd = c.kind[r], o = c.obj[r];
         if (incremental) {
           if (act != hess_flags[r]) {
-            w = sqrt(c.D[r]);
+            w = Dr;
             sg = act ? 1.0 : -1.0;
           }
         } else if (act) {
-          w = sqrt(c.D[r]);
+          w = Dr;
         }
         hess_flags[r] = act;
+        if (w != 0.0) {
+          // describe row r: sides (body, 6-vector) and dof terms
+          const int k = kd & 7, sub = kd >> 3;
+          double* rho = S.jrho[tid];
+          int b1 = 0, b2 = 0, d1 = -1, d2 = -1;
+          double c1 = 0, c2 = 0;
+          if (k == ROW_CONTACT) {
+            const double* src = c.rho + 6 * (size_t)r;
+            for (int i = 0; i < 6; i++) {
+              const double v = src[i];
+              rho[6 + i] = v;
+              rho[i] = -v;
+            }
+            b1 = S.ccb[o][0];
+            b2 = S.ccb[o][1];
+          } else if (k == ROW_LIMIT) {
+            for (int i = 0; i < 12; i++) rho[i] = 0.0;
+            d1 = o;
+            c1 = sub ? -1.0 : 1.0;
+          } else {
+            for (int i = 0; i < 12; i++) rho[i] = S.eqrho[o][i];
+            b1 = S.eqb[o][0];
+            b2 = S.eqb[o][1];
+            d1 = S.eqd[o][0];
+            d2 = S.eqd[o][1];
+            c1 = S.eqcoef[o][0];
+            c2 = S.eqcoef[o][1];
+          }
+          S.jb[tid][0] = b1;
+          S.jb[tid][1] = b2;
+          S.jd[tid][0] = d1;
+          S.jd[tid][1] = d2;
+          S.jcoef[tid][0] = c1;
+          S.jcoef[tid][1] = c2;
+        }
       }
       S.jw[tid] = w;
       S.jsg[tid] = sg;
     }
-    __syncthreads();
+    lds_sync();
+    CPROF(19)
     bool any = false;
 #pragma unroll
     for (int k = 0; k < RCHUNK; k++) any |= S.jw[k] != 0.0;
     if (!any) continue;  // uniform: every thread read the same flags
-    const double* src = c.J + (size_t)r0 * nv;
+    // J_rk = [k on chain(b1)] cdof_k . rho1 + [k on chain(b2)] cdof_k . rho2 + dof terms; a
+    // contact's two sides are exact negatives, so dofs on both chains give exactly 0
     for (int e = tid; e < RCHUNK * NVP; e += SOLVER_THREADS) {
       const int rr = e / NVP, k = e - rr * NVP;
-      S.jc[rr][k] = (rr < nr && k < nv) ? src[(size_t)rr * nv + k] * S.jw[rr] : 0.0;
+      double v = 0.0;
+      const double w = S.jw[rr];
+      if (rr < nr && k < nv && w != 0.0) {
+        const int kb = S.kb[k], kend = S.send[kb];
+        const int b1 = S.jb[rr][0], b2 = S.jb[rr][1];
+        const double* Sk = S.cdof + 6 * k;
+        if (kb <= b1 && b1 < kend) v += dot6t(Sk, S.jrho[rr]);
+        if (kb <= b2 && b2 < kend) v += dot6t(Sk, S.jrho[rr] + 6);
+        if (S.jd[rr][0] == k) v += S.jcoef[rr][0];
+        if (S.jd[rr][1] == k) v += S.jcoef[rr][1];
+        v *= w;
+      }
+      S.jc[rr][k] = v;
     }
-    __syncthreads();
+    lds_sync();
+    CPROF(31)
     if (own) {
       for (int rr = 0; rr < nr; rr++) {
         if (S.jw[rr] == 0.0) continue;
@@ -2442,51 +2847,72 @@ __device__ void solver_hessian(const SolverCtx& c, const double* M, const int32_
 #pragma unroll
     for (int q = 0; q < 16; q++) hsave[16 * tid + q] = a[q];
   }
-  __syncthreads();
+  lds_sync();
 }
 
 #define SPROF(k)                                  \
   if (prof) {                                     \
-    __syncthreads();                              \
+    lds_sync();                                   \
     const unsigned long long t_ = stamp();        \
     if (tid == 0) prof[k] += t_ - tp;             \
     tp = t_;                                      \
   }
 
 __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj, bool own,
-                             int nefc, int ne, int tid, unsigned long long* prof) {
+                             int ncon, int nefc, int ne, int nlim, int tree_rounds, int tid,
+                             unsigned long long* prof) {
   const rmbx_model& m = *e.m;
   unsigned long long tp = prof ? stamp() : 0;
   const int nv = m.nv, NB = (nv + 3) / 4, NVP = 4 * NB;
-  const double* M = W(M);
+  const double* Mb = W(Mblk);
   SolverCtx c;
-  c.J = W(J);
+  c.m = e.m;
   c.aref = W(efc_aref);
   c.D = W(efc_D);
+  c.sqD = W(efc_sqD);
+  c.rho = W(efc_rho);
   c.type = WI(efc_type);
+  c.kind = WI(efc_kind);
+  c.obj = WI(efc_obj);
+  c.cpos = W(con_pos);
+  c.cframe = W(con_frame);
+  c.cmu = W(con_mu);
+  c.cb1 = WI(con_b1);
+  c.cb2 = WI(con_b2);
+  c.ccondim = WI(con_condim);
+  c.cefcadr = WI(con_efcadr);
+  c.eq_rho = W(eqr_rho);
+  c.eq_coef = W(eqr_coef);
+  c.eq_body = WI(eqr_body);
+  c.eq_dof = WI(eqr_dof);
   c.jar = W(efc_jar);
   c.Js = W(efc_Js);
   c.force = W(efc_force);
+  c.wrow = W(efc_tmp);
+  c.prof = prof;
+  c.tree_rounds = tree_rounds;
   c.nefc = nefc;
   c.ne = ne;
+  c.nlim = nlim;
+  c.ncon = ncon;
   c.nv = nv;
   c.NB = NB;
   c.tid = tid;
   // qacc_smooth = M^-1 qfrc_smooth
-  if (own) load_block(M, nv, bi, bj, a);
+  if (own) load_blockp(Mb, tid, a);
   for (int k = tid; k < NVP; k += SOLVER_THREADS) S.tmp[k] = k < nv ? W(qfrc_smooth)[k] : 0.0;
-  __syncthreads();
-  blk_cholesky(a, bi, bj, own, NB, S);
-  blk_solve(a, bi, bj, own, NB, S.tmp, S.a0, S, tid);
+  lds_sync();
+  blk_cholesky_fwd(a, bi, bj, own, NB, S.tmp, S, tid);
+  blk_solve_back(a, bi, bj, own, NB, S.a0, S, tid);
   SPROF(8)
   for (int k = tid; k < NVP; k += SOLVER_THREADS) S.tmp[k] = k < nv ? e.qacc_ws[k] : 0.0;
-  __syncthreads();
+  lds_sync();
   // warm start vs smooth start (the smooth start has res = 0: only its rows cost anything)
-  const double c_ws = solver_cost(c, M, S.tmp, S);
-  double* jar_ws = W(efc_tmp);
+  const double c_ws = solver_cost(c, S.tmp, S);
+  double* jar_ws = W(efc_Js);  // (Js is dead until the first line search)
   for (int r = tid; r < nefc; r += SOLVER_THREADS) jar_ws[r] = c.jar[r];
   for (int k = tid; k < NVP; k += SOLVER_THREADS) S.Ms[k] = S.Mres[k];
-  __syncthreads();
+  lds_sync();
   const double c_sm = rows_cost(c, S.a0, S);
   const bool use_ws = c_ws < c_sm;
   for (int k = tid; k < NVP; k += SOLVER_THREADS) {
@@ -2496,7 +2922,7 @@ __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj,
   }
   if (use_ws)
     for (int r = tid; r < nefc; r += SOLVER_THREADS) c.jar[r] = jar_ws[r];
-  __syncthreads();
+  lds_sync();
   double cost = use_ws ? c_ws : c_sm;
   SPROF(9)
   const double scale = 1.0 / (m.meaninertia * (nv > 1 ? nv : 1));
@@ -2511,16 +2937,21 @@ __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj,
     SPROF(10)
     if (scale * sqrt(gn) < m.solver_tolerance) break;
     if (changed || !have_factor) {
-      solver_hessian(c, M, act_flags, WI(efc_hact), W(hsave), have_factor, a, bi, bj, own, S);
+      solver_hessian(c, Mb, act_flags, WI(efc_hact), W(hsave), have_factor, a, bi, bj, own, S);
       SPROF(15)
-      blk_cholesky(a, bi, bj, own, NB, S);
+      blk_cholesky_fwd(a, bi, bj, own, NB, S.grad, S, tid);
+      blk_solve_back(a, bi, bj, own, NB, S.srch, S, tid);
       have_factor = true;
+    } else {
+      blk_solve(a, bi, bj, own, NB, S.grad, S.srch, S, tid);
     }
-    blk_solve(a, bi, bj, own, NB, S.grad, S.srch, S, tid);
     SPROF(11)
     for (int k = tid; k < NVP; k += SOLVER_THREADS) S.srch[k] = -S.srch[k];
-    __syncthreads();
-    mat_vec(M, nv, S.srch, S.Ms, tid);
+    lds_sync();
+    // J search (rows) and M search from one pass of body velocities of the search direction
+    body_vel(c, S.srch, S);
+    for (int r = tid; r < nefc; r += SOLVER_THREADS) c.Js[r] = row_dot(c, r, S, S.srch);
+    mass_tail(c, S.srch, S.Ms, S);
     double qp = 0, lp = 0;
     for (int k = tid; k < nv; k += SOLVER_THREADS) {
       qp += S.srch[k] * S.Ms[k];
@@ -2528,7 +2959,6 @@ __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj,
     }
     const double qg = block_sum(qp, S, tid);
     const double lg = block_sum(lp, S, tid);
-    jac_vec(c.J, nefc, nv, S.srch, c.Js, tid);
     double alpha = 0, lo = 0, hi = 1e300;
     for (int ls = 0; ls < m.ls_iterations; ls++) {
       double p1 = 0, p2 = 0;
@@ -2583,31 +3013,27 @@ __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj,
     }
   }
   // forces and qfrc_constraint = J^T f
-  double* fl = &S.jc[0][0];  // forces staged in LDS for the column reduction
   for (int r = tid; r < nefc; r += SOLVER_THREADS) {
     const double jar = c.jar[r];
-    const double f = (c.type[r] == 0 || jar < 0) ? -c.D[r] * jar : 0.0;
-    c.force[r] = f;
-    fl[r] = f;
+    c.force[r] = (c.type[r] == 0 || jar < 0) ? -c.D[r] * jar : 0.0;
   }
-  __syncthreads();
-  const double qc = col_reduce(c.J, nefc, nv, fl, S.acc2, tid);
+  lds_sync();
+  jac_tmul(c, c.force, S.acc, S);
   if (tid < nv) {
-    W(qfrc_constraint)[tid] = qc;
+    W(qfrc_constraint)[tid] = S.acc[tid];
     W(qacc)[tid] = S.a[tid];
   }
-  __syncthreads();
+  __syncthreads();  // the sensors read qacc body-per-thread: full fence
   SPROF(14)
   return it;
 }
-
 __device__ void solver_integrate(Env& e, SolverShared& S, double* a, int bi, int bj, bool own,
                                  int tid, int sub) {
   const rmbx_model& m = *e.m;
   const int nv = m.nv, NB = (nv + 3) / 4, NVP = 4 * NB;
   const double h = m.timestep;
   if (own) {
-    load_block(W(M), nv, bi, bj, a);
+    load_blockp(W(Mblk), threadIdx.x, a);
     // + h * (damping + actuator velocity gains), tendon terms are rank-1 blocks
 #pragma unroll
     for (int p = 0; p < 4; p++)
@@ -2638,9 +3064,9 @@ __device__ void solver_integrate(Env& e, SolverShared& S, double* a, int bi, int
   }
   for (int k = tid; k < NVP; k += SOLVER_THREADS)
     S.tmp[k] = k < nv ? W(qfrc_smooth)[k] + W(qfrc_constraint)[k] : 0.0;
-  __syncthreads();
-  blk_cholesky(a, bi, bj, own, NB, S);
-  blk_solve(a, bi, bj, own, NB, S.tmp, S.a, S, tid);
+  lds_sync();
+  blk_cholesky_fwd(a, bi, bj, own, NB, S.tmp, S, tid);
+  blk_solve_back(a, bi, bj, own, NB, S.a, S, tid);
   bool bad = false;
   for (int k = tid; k < nv; k += SOLVER_THREADS) {
     const double acc = S.a[k];
@@ -2668,7 +3094,7 @@ __device__ void solver_integrate(Env& e, SolverShared& S, double* a, int bi, int
     e.qvel[k] += h * acc;
     e.qacc_ws[k] = acc;
   }
-  __syncthreads();
+  __syncthreads();  // the joint loop reads qvel joint-per-thread: full fence
   for (int j = tid; j < m.njnt; j += SOLVER_THREADS) {
     const int qa = m.jnt_qposadr[j], da = m.jnt_dofadr[j];
     if (m.jnt_type[j] == RMBX_JNT_FREE) {
@@ -2702,6 +3128,7 @@ struct KArgs {
   int integrate_flag;
   unsigned long long* prof;  // optional [n_env][16] per-stage cycle sums (diagnostic)
   const int32_t* subtree_end;  // [nbody] end of each body's DFS subtree id range
+  int tree_rounds;             // pointer-jumping rounds covering the deepest body chain
 };
 
 
@@ -2761,13 +3188,14 @@ __global__ void __launch_bounds__(64) front_kernel(KArgs args) {
   const int ncon = collision(e, lane, collision_lds(e), prof);
   sync();
   PROF(3)
-  int ne = 0;
-  const int nefc = make_constraints(e, lane, ncon, &ne, prof);
+  int ne = 0, nlim = 0;
+  const int nefc = make_constraints(e, lane, ncon, &ne, &nlim, prof);
   PROF(4)
   if (lane == 0) {
     WI(scal)[0] = ncon;
     WI(scal)[1] = nefc;
     WI(scal)[2] = ne;
+    WI(scal)[3] = nlim;
     e.stats[0] = ncon;
     e.stats[1] = nefc;
   }
@@ -2788,10 +3216,67 @@ __global__ void __launch_bounds__(SOLVER_THREADS, 4) solver_kernel(KArgs args) {
   if (own) blk_coords(tid, &bi, &bj);
   double a[16];
   PROF_BEGIN()
-  const int ncon = WI(scal)[0], nefc = WI(scal)[1], ne = WI(scal)[2];
-  const int iters = solver_newton(e, S, a, bi, bj, own, nefc, ne, tid, prof);
+  const rmbx_model& m = args.m;
+  // stage the dof axes, composite inertias and tree ranges the J-free row passes read
+  for (int k = tid; k < 6 * m.nv; k += SOLVER_THREADS) S.cdof[k] = W(cdof)[k];
+  for (int k = tid; k < 10 * m.nbody; k += SOLVER_THREADS) S.cinert[k] = W(cinert)[k];
+  for (int k = tid; k < m.nbody; k += SOLVER_THREADS) S.send[k] = (int16_t)args.subtree_end[k];
+  for (int k = tid; k < m.nv; k += SOLVER_THREADS) S.kb[k] = (int16_t)m.dof_body[k];
+  for (int k = tid; k < m.nbody; k += SOLVER_THREADS) S.par[k] = (int16_t)m.body_parent[k];
+  if (tid < 6) S.bv[tid] = 0.0;  // the world body's velocity (row passes read it)
+  const int ncon = WI(scal)[0], nefc = WI(scal)[1], ne = WI(scal)[2], nlim = WI(scal)[3];
+  // per-launch row structure: contact bodies, equality rows, limit rows
+  // (a body welded to the world moves with it: no dof sees its wrench and its velocity is
+  // zero, so it is staged as the world body and the row passes skip it)
+  for (int q = tid; q < ncon; q += SOLVER_THREADS) {
+    const int b1 = WI(con_b1)[q], b2 = WI(con_b2)[q];
+    S.ccb[q][0] = (int16_t)(m.body_weldid[b1] == 0 ? 0 : b1);
+    S.ccb[q][1] = (int16_t)(m.body_weldid[b2] == 0 ? 0 : b2);
+  }
+  for (int q = tid; q < ne; q += SOLVER_THREADS) {
+    for (int i = 0; i < 12; i++) S.eqrho[q][i] = W(eqr_rho)[12 * q + i];
+    for (int i = 0; i < 2; i++) {
+      S.eqcoef[q][i] = W(eqr_coef)[2 * q + i];
+      const int eb = WI(eqr_body)[2 * q + i];
+      S.eqb[q][i] = (int16_t)(m.body_weldid[eb] == 0 ? 0 : eb);
+      S.eqd[q][i] = (int16_t)WI(eqr_dof)[2 * q + i];
+    }
+  }
+  for (int i = tid; i < nlim; i += SOLVER_THREADS)
+    S.lim[i] = (int16_t)(2 * WI(efc_obj)[ne + i] + (WI(efc_kind)[ne + i] >> 3));
+  __syncthreads();
+  // per-body wrench lists for J^T w (counted, scanned over bodies in wave 0, then filled)
+  {
+    int cnt = 0;
+    const int b = tid;
+    const bool body = b > 0 && b < m.nbody;
+    if (body) {
+      for (int q = 0; q < ncon; q++) cnt += (S.ccb[q][1] == b) + (S.ccb[q][0] == b);
+      for (int q = 0; q < ne; q++) cnt += (S.eqb[q][0] == b) + (S.eqb[q][1] == b);
+    }
+    if (tid < 64) {
+      int total;
+      const int off = wave_excl_scan(cnt, tid, &total);
+      if (b < m.nbody) S.boff[b] = (int16_t)off;
+      if (tid == 0) S.boff[m.nbody] = (int16_t)total;
+    }
+    __syncthreads();
+    if (body) {
+      int l = S.boff[b];
+      for (int q = 0; q < ncon; q++) {
+        if (S.ccb[q][1] == b) S.blist[l++] = (int16_t)(2 * q);
+        if (S.ccb[q][0] == b) S.blist[l++] = (int16_t)(2 * q + 1);
+      }
+      for (int q = 0; q < ne; q++) {
+        if (S.eqb[q][0] == b) S.blist[l++] = (int16_t)(EQ_TAG + 2 * q);
+        if (S.eqb[q][1] == b) S.blist[l++] = (int16_t)(EQ_TAG + 2 * q + 1);
+      }
+    }
+    __syncthreads();
+  }
+  const int iters = solver_newton(e, S, a, bi, bj, own, ncon, nefc, ne, nlim, args.tree_rounds, tid, prof);
   PROF(5)
-  sensors(e, ncon, tid, S.bacc, S.bfrc, &S.jc[0][0], S.anc, args.subtree_end);
+  sensors(e, ncon, tid, S.bv, S.bf, S.cw, S.anc, args.subtree_end);
   PROF(6)
   if (tid == 0) e.stats[2] = iters;
   if (args.integrate_flag) solver_integrate(e, S, a, bi, bj, own, tid, args.sub);
@@ -2821,7 +3306,8 @@ static Layout make_layout(const rmbx_model& m) {
   L.cvel = take(6 * nb);
   L.cacc = take(6 * nb);
   L.cfrc = take(6 * nb);
-  L.M = take((size_t)nv * nv);
+  const int nb4 = (nv + 3) / 4;
+  L.Mblk = take(16 * (size_t)(nb4 * (nb4 + 1) / 2));
   L.qfrc_bias = take(nv);
   L.qfrc_passive = take(nv);
   L.qfrc_actuator = take(nv);
@@ -2842,22 +3328,22 @@ static Layout make_layout(const rmbx_model& m) {
   L.con_dist = take(mc);
   L.con_mu = take(mc);
   const int ne = L.nefc_max;
-  const int nb4 = (nv + 3) / 4;
+  L.neqr_max = 6 * m.neq > 0 ? 6 * m.neq : 1;
   L.hsave = take(16 * (size_t)(nb4 * (nb4 + 1) / 2));
-  L.J = take((size_t)ne * nv);
   L.efc_pos = take(ne);
   L.efc_aref = take(ne);
   L.efc_D = take(ne);
+  L.efc_sqD = take(ne);
+  L.efc_rho = take(6 * (size_t)ne);
   L.efc_R = take(ne);
   L.efc_force = take(ne);
   L.efc_jar = take(ne);
   L.efc_Js = take(ne);
   L.efc_vel = take(ne);
   L.efc_tmp = take(ne);
-  // the candidate contacts are dead before make_constraints zeroes and fills J: share its rows
-  // when they are large enough
-  const size_t ntmp = 28 * (size_t)collision_cap(m.npair);
-  L.con_tmp = (size_t)ne * nv >= ntmp ? L.J : take(ntmp);
+  L.eqr_rho = take(12 * (size_t)L.neqr_max);
+  L.eqr_coef = take(2 * (size_t)L.neqr_max);
+  L.con_tmp = take(28 * (size_t)collision_cap(m.npair));
   L.ints = o;
   size_t io = 0;
   auto itake = [&](size_t n) {
@@ -2873,6 +3359,10 @@ static Layout make_layout(const rmbx_model& m) {
   L.efc_type = itake(ne);
   L.efc_act = itake(ne);
   L.efc_hact = itake(ne);
+  L.efc_kind = itake(ne);
+  L.efc_obj = itake(ne);
+  L.eqr_body = itake(2 * (size_t)L.neqr_max);
+  L.eqr_dof = itake(2 * (size_t)L.neqr_max);
   L.scal = itake(8);
   L.istride = io;
   L.stride = o + (io + 1) / 2;
@@ -2908,8 +3398,14 @@ int rmbx_engine_create(const struct rmbx_model* model, int n_env, rmbx_engine** 
   const rmbx_model& h = *model;
   RMBX_CHECK_ARG(h.nv > 0 && h.nv <= MAX_NVP, "nv=%d outside the supported range [1, %d]", h.nv, MAX_NVP);
   RMBX_CHECK_ARG(h.nbody > 0 && h.nbody <= MAX_BODY, "nbody=%d outside [1, %d]", h.nbody, MAX_BODY);
-  RMBX_CHECK_ARG(h.max_contacts > 0 && h.max_contacts <= RCHUNK * MAX_NVP / 6, "bad max_contacts=%d",
-                 h.max_contacts);
+  RMBX_CHECK_ARG(h.max_contacts > 0 && h.max_contacts <= MAX_CON, "max_contacts=%d outside [1, %d]",
+                 h.max_contacts, MAX_CON);
+  RMBX_CHECK_ARG(2 * h.njnt <= MAX_LIM, "njnt=%d: more limit rows than the solver stages (%d)", h.njnt, MAX_LIM);
+  {
+    int neqr = 0;
+    for (int q = 0; q < h.neq; q++) neqr += h.eq_type[q] == RMBX_EQ_CONNECT ? 3 : (h.eq_type[q] == RMBX_EQ_WELD ? 6 : 1);
+    RMBX_CHECK_ARG(neqr <= NEQR, "%d equality rows, more than the solver stages (%d)", neqr, NEQR);
+  }
   RMBX_CHECK_ARG(h.npair >= 0 && h.npair < (1 << 24), "npair=%d outside [0, 2^24)", h.npair);
   RMBX_CHECK_ARG(front_kernel_lds_bytes(h) <= 65536,
                  "model too large for the front kernel's LDS (nbody=%d nv=%d ngeom=%d npair=%d)", h.nbody,
@@ -2927,6 +3423,17 @@ int rmbx_engine_create(const struct rmbx_model* model, int n_env, rmbx_engine** 
     RMBX_CHECK_ARG(b < subtree_end[p], "bodies are not in DFS preorder (body %d outside its parent's range)", b);
   }
   rmbx_engine* eng = new rmbx_engine();
+  {
+    int maxd = 0;
+    std::vector<int> depth(h.nbody, 0);
+    for (int b = 1; b < h.nbody; b++) {
+      depth[b] = depth[h.body_parent[b]] + 1;
+      maxd = depth[b] > maxd ? depth[b] : maxd;
+    }
+    int r = 0;
+    while ((1 << r) < maxd + 1) r++;
+    eng->tree_rounds = r;
+  }
   eng->host = h;
   eng->dev = h;
   eng->n_env = n_env;
@@ -2974,11 +3481,6 @@ int rmbx_engine_create(const struct rmbx_model* model, int n_env, rmbx_engine** 
     return st;
   }
   eng->L = make_layout(h);
-  if (eng->L.nefc_max > RCHUNK * MAX_NVP) {
-    rmbx_engine_destroy(eng);
-    rmbx::set_error("model needs %d constraint rows, more than the solver's %d", eng->L.nefc_max, RCHUNK * MAX_NVP);
-    return RMBX_ERR_ARG;
-  }
   *out = eng;
   return RMBX_OK;
 }
@@ -3007,7 +3509,7 @@ int rmbx_engine_ws_offset(const rmbx_engine* eng, const char* name, size_t* offs
     size_t off, cnt;
   } items[] = {
       {"stride", L.stride, L.stride},
-      {"M", L.M, nv * nv},
+      {"Mblk", L.Mblk, 16 * (size_t)(((nv + 3) / 4) * ((nv + 3) / 4 + 1) / 2)},
       {"qfrc_bias", L.qfrc_bias, nv},
       {"qfrc_passive", L.qfrc_passive, nv},
       {"qfrc_actuator", L.qfrc_actuator, nv},
@@ -3021,7 +3523,8 @@ int rmbx_engine_ws_offset(const rmbx_engine* eng, const char* name, size_t* offs
       {"con_pos", L.con_pos, 3 * (size_t)m.max_contacts},
       {"con_dist", L.con_dist, (size_t)m.max_contacts},
       {"efc_force", L.efc_force, (size_t)L.nefc_max},
-      {"J", L.J, (size_t)L.nefc_max * nv},
+      {"efc_D", L.efc_D, (size_t)L.nefc_max},
+      {"efc_aref", L.efc_aref, (size_t)L.nefc_max},
       // int32 arrays: offsets in int32 units from the workspace start (2 per double)
       {"con_b1", 2 * L.ints + L.con_b1, (size_t)m.max_contacts},
       {"con_b2", 2 * L.ints + L.con_b2, (size_t)m.max_contacts},
@@ -3066,6 +3569,7 @@ static int launch(rmbx_engine* eng, int nsub, int integ, const uint8_t* active, 
   a.integrate_flag = integ;
   a.prof = prof;
   a.subtree_end = eng->subtree_end;
+  a.tree_rounds = eng->tree_rounds;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int reps = integ ? nsub : 1;
   for (int s = 0; s < reps; s++) {

@@ -75,16 +75,21 @@ class PhysicsEngine:
     # sub-stages of "collision" (slots 16..18) and "constraints" (slots 20..23)
     COLLISION_STAGES = ("geom_records", "classify_compact", "narrow")
     CONSTRAINT_STAGES = ("count_zero", "equality", "limit_contact_rows", "aref")
+    # J^T w (slots 24..27) and J x / M x (28..30) pass internals
+    ROWPASS_STAGES = ("jtw_contact_wrench", "jtw_body_collect", "jtw_subtree", "jtw_dof",
+                      "bodyvel_local", "bodyvel_prefix", "mass_tail")
 
     def step_profiled(self, nsub=8):
         """Diagnostic step: returns mean shader cycles per stage (summed over substeps)."""
-        prof = torch.zeros((self.n_env, 24), dtype=torch.int64, device=self.device)
+        prof = torch.zeros((self.n_env, 32), dtype=torch.int64, device=self.device)
         N.call("rmbx_engine_step_profiled", self._h, int(nsub), N.ptr(prof), N.stream_ptr())
         p = prof.double().mean(0).cpu().numpy()
         out = dict(zip(self.STAGES, p[: len(self.STAGES)]))
         out.update({"solver." + k: v for k, v in zip(self.SOLVER_STAGES, p[8: 8 + len(self.SOLVER_STAGES)])})
         out.update({"collision." + k: v for k, v in zip(self.COLLISION_STAGES, p[16:19])})
         out.update({"constraints." + k: v for k, v in zip(self.CONSTRAINT_STAGES, p[20:24])})
+        out.update({"rowpass." + k: v for k, v in zip(self.ROWPASS_STAGES, p[24:31])})
+        out.update({"hessian.describe": p[19], "hessian.entries": p[31]})
         return out
 
     def forward(self, active=None):
@@ -95,8 +100,27 @@ class PhysicsEngine:
         N.call("rmbx_engine_ws_offset", self._h, name.encode(), ctypes.byref(off), ctypes.byref(cnt))
         return off.value, cnt.value
 
+    def mass_matrix(self):
+        """Dense [n_env, nv*nv] copy of the mass matrix (the engine keeps only the packed lower
+        4x4 blocks the solver loads: block t = bi(bi+1)/2 + bj, entry 4p+q = M[4bi+p][4bj+q])."""
+        nv = self.nv
+        nb = (nv + 3) // 4
+        blk = self.ws("Mblk").view(self.n_env, -1, 4, 4)
+        full = torch.zeros((self.n_env, 4 * nb, 4 * nb), dtype=torch.float64, device=self.device)
+        t = 0
+        for bi in range(nb):
+            for bj in range(bi + 1):
+                full[:, 4 * bi: 4 * bi + 4, 4 * bj: 4 * bj + 4] = blk[:, t]
+                t += 1
+        low = torch.tril(full)
+        full = low + low.transpose(1, 2) - torch.diag_embed(torch.diagonal(low, dim1=1, dim2=2))
+        return full[:, :nv, :nv].reshape(self.n_env, nv * nv)
+
     def ws(self, name):
-        """Zero-copy [n_env, count] f64 view of a named workspace array (after step/forward)."""
+        """Zero-copy [n_env, count] f64 view of a named workspace array (after step/forward);
+        "M" is the exception: a dense copy unpacked from the solver's blocks."""
+        if name == "M":
+            return self.mass_matrix()
         stride, _ = self._off("stride")
         off, cnt = self._off(name)
         return self.workspace.view(torch.float64).view(self.n_env, stride)[:, off : off + cnt]
