@@ -372,6 +372,7 @@ __device__ void com_pos_crb(Env& e, int lane, const int32_t* subtree_end) {
   }
   sync();
   // composite rigid-body inertia = subtree sums (DFS ranges), copies for the solver kernel
+  // (exact range sums: a prefix-difference scan would cost ~1e-12 relative on the light links)
   for (int b = lane; b < nb; b += 64) {
     double acc[10];
     for (int k = 0; k < 10; k++) acc[k] = cinert[10 * b + k];
@@ -386,18 +387,28 @@ __device__ void com_pos_crb(Env& e, int lane, const int32_t* subtree_end) {
   // lower triangle, lane = row i: M_ij = cdof_j . (crb_body(i) cdof_i) for dofs j on i's chain,
   // written straight into the packed 4x4 blocks the solver loads (zeros off the chain; the
   // upper half of a diagonal block is never read; padding rows get the identity)
+  // (lane per row: F_i = crb_body(i) cdof_i into the velocity stage's not yet used LDS; then
+  // lane per block, so the triangle's 153 blocks spread evenly over the lanes)
   double* Mb = W(Mblk);
-  const int NVP = 4 * ((nv + 3) / 4);
-  for (int i = lane; i < NVP; i += 64) {
-    double F[6] = {0, 0, 0, 0, 0, 0};
-    int bi_ = 0;
-    if (i < nv) {
-      bi_ = m.dof_body[i];
-      inert_mul(crb + 10 * bi_, cdof + 6 * i, F);
+  const int NB = (nv + 3) / 4;
+  double* Fr = e.sh + 16 * nb;  // [6 nv] (cvel/cacc region: free until velocity_stage)
+  for (int i = lane; i < nv; i += 64) inert_mul(crb + 10 * m.dof_body[i], cdof + 6 * i, Fr + 6 * i);
+  sync();
+  for (int t = lane; t < NB * (NB + 1) / 2; t += 64) {
+    int bi, bj;
+    {
+      int r = (int)((sqrt(8.0 * t + 1.0) - 1.0) * 0.5);
+      while ((r + 1) * (r + 2) / 2 <= t) r++;
+      while (r * (r + 1) / 2 > t) r--;
+      bi = r;
+      bj = t - r * (r + 1) / 2;
     }
-    const int bi = i >> 2, p = i & 3;
-    for (int bj = 0; bj <= bi; bj++) {
-      double* blk = Mb + 16 * (bi * (bi + 1) / 2 + bj) + 4 * p;
+    double* dstb = Mb + 16 * (size_t)t;
+#pragma unroll 1
+    for (int p = 0; p < 4; p++) {
+      double row[4];
+      const int i = 4 * bi + p;
+      const int bi_ = i < nv ? m.dof_body[i] : 0;
 #pragma unroll
       for (int q = 0; q < 4; q++) {
         const int c = 4 * bj + q;
@@ -405,15 +416,18 @@ __device__ void com_pos_crb(Env& e, int lane, const int32_t* subtree_end) {
         if (i >= nv || c >= nv) {
           v = i == c ? 1.0 : 0.0;
         } else if (c > i) {
-          v = 0.0;
+          v = 0.0;  // (upper half of a diagonal block: never read)
         } else {
           const int bc = m.dof_body[c];
           const bool anc = bc == bi_ || (bc < bi_ && bi_ < subtree_end[bc]);
-          v = anc ? dot6(cdof + 6 * c, F) : 0.0;
+          v = anc ? dot6(cdof + 6 * c, Fr + 6 * i) : 0.0;
           if (c == i) v += m.dof_armature[i];
         }
-        blk[q] = v;
+        row[q] = v;
       }
+      double2* dst = reinterpret_cast<double2*>(dstb + 4 * p);
+      dst[0] = make_double2(row[0], row[1]);
+      dst[1] = make_double2(row[2], row[3]);
     }
   }
   sync();

@@ -79,10 +79,13 @@ class PhysicsEngine:
     ROWPASS_STAGES = ("jtw_contact_wrench", "jtw_body_collect", "jtw_subtree", "jtw_dof",
                       "bodyvel_local", "bodyvel_prefix", "mass_tail")
 
-    def step_profiled(self, nsub=8):
-        """Diagnostic step: returns mean shader cycles per stage (summed over substeps)."""
+    def step_profiled(self, nsub=8, raw=False):
+        """Diagnostic step: returns mean shader cycles per stage (summed over substeps); with
+        raw=True the [n_env, 32] per-env cycle array instead."""
         prof = torch.zeros((self.n_env, 32), dtype=torch.int64, device=self.device)
         N.call("rmbx_engine_step_profiled", self._h, int(nsub), N.ptr(prof), N.stream_ptr())
+        if raw:
+            return prof.cpu().numpy()
         p = prof.double().mean(0).cpu().numpy()
         out = dict(zip(self.STAGES, p[: len(self.STAGES)]))
         out.update({"solver." + k: v for k, v in zip(self.SOLVER_STAGES, p[8: 8 + len(self.SOLVER_STAGES)])})

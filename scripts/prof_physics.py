@@ -44,3 +44,9 @@ p = env.engine.step_profiled(8)
 tot = sum(v for k, v in p.items() if "." not in k)
 for k, v in p.items():
     print(f"  {k:34s} {v/1e6:8.3f} Mcycles  {100*v/tot:5.1f}%")
+raw = env.engine.step_profiled(8, raw=True).astype(np.float64)
+front, solver = raw[:, 0:5].sum(1), raw[:, 5:8].sum(1)
+for name, v in (("front stages", front), ("solver stages", solver)):
+    print(f"  per-env {name:14s} mean {v.mean()/1e6:6.3f}  p50 {np.median(v)/1e6:6.3f}  p99 {np.percentile(v, 99)/1e6:6.3f}  max {v.max()/1e6:6.3f} Mcycles")
+st = env.engine.stats.cpu().numpy()
+print("  ncon max", st[:, 0].max(), "nefc max", st[:, 1].max(), "iters max", st[:, 2].max())
