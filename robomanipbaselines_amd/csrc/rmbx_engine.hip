@@ -70,6 +70,7 @@ struct rmbx_engine {
   rmbx_model dev;        // device pointers
   const int32_t* subtree_end;  // device [nbody]: DFS subtree ranges for the tree passes
   int tree_rounds;             // ceil(log2(max body depth + 1)) (solver pointer jumping)
+  const double* hBblk;         // device: h * (damping + actuator velocity gains), packed 4x4 blocks
   std::vector<void*> allocations;
   rmbx::Layout L;
   int n_env;
@@ -3042,39 +3043,18 @@ __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj,
   return it;
 }
 __device__ void solver_integrate(Env& e, SolverShared& S, double* a, int bi, int bj, bool own,
-                                 int tid, int sub) {
+                                 int tid, int sub, const double* hB) {
   const rmbx_model& m = *e.m;
   const int nv = m.nv, NB = (nv + 3) / 4, NVP = 4 * NB;
   const double h = m.timestep;
   if (own) {
+    // M + h * (damping + actuator velocity gains): the second term is a model constant built
+    // once at create (rmbx_engine_create) in the same packed block order
     load_blockp(W(Mblk), threadIdx.x, a);
-    // + h * (damping + actuator velocity gains), tendon terms are rank-1 blocks
+    double hb[16];
+    load_blockp(hB, threadIdx.x, hb);
 #pragma unroll
-    for (int p = 0; p < 4; p++)
-#pragma unroll
-      for (int q = 0; q < 4; q++) {
-        const int r = 4 * bi + p, cc = 4 * bj + q;
-        if (r >= nv || cc >= nv) continue;
-        double add = 0;
-        if (r == cc) add += m.dof_damping[r];
-        for (int u = 0; u < m.nu; u++) {
-          const double kv = -m.act_bias[3 * u + 2];
-          if (kv == 0) continue;
-          const int id = m.act_trnid[u];
-          if (m.act_trntype[u] == RMBX_TRN_JOINT) {
-            if (r == cc && m.jnt_dofadr[id] == r) add += kv;
-          } else {
-            double cr = 0, cq = 0;
-            for (int w = m.ten_adr[id]; w < m.ten_adr[id] + m.ten_num[id]; w++) {
-              const int d = m.jnt_dofadr[m.wrap_jnt[w]];
-              if (d == r) cr += m.wrap_coef[w];
-              if (d == cc) cq += m.wrap_coef[w];
-            }
-            add += kv * cr * cq;
-          }
-        }
-        a[4 * p + q] += h * add;
-      }
+    for (int q = 0; q < 16; q++) a[q] += hb[q];
   }
   for (int k = tid; k < NVP; k += SOLVER_THREADS)
     S.tmp[k] = k < nv ? W(qfrc_smooth)[k] + W(qfrc_constraint)[k] : 0.0;
@@ -3142,6 +3122,7 @@ struct KArgs {
   int integrate_flag;
   unsigned long long* prof;  // optional [n_env][16] per-stage cycle sums (diagnostic)
   const int32_t* subtree_end;  // [nbody] end of each body's DFS subtree id range
+  const double* hBblk;         // implicitfast: h * (damping + kv terms), packed like Mblk
   int tree_rounds;             // pointer-jumping rounds covering the deepest body chain
 };
 
@@ -3293,7 +3274,7 @@ __global__ void __launch_bounds__(SOLVER_THREADS, 4) solver_kernel(KArgs args) {
   sensors(e, ncon, tid, S.bv, S.bf, S.cw, S.anc, args.subtree_end);
   PROF(6)
   if (tid == 0) e.stats[2] = iters;
-  if (args.integrate_flag) solver_integrate(e, S, a, bi, bj, own, tid, args.sub);
+  if (args.integrate_flag) solver_integrate(e, S, a, bi, bj, own, tid, args.sub, args.hBblk);
   PROF(7)
 }
 
@@ -3490,6 +3471,39 @@ int rmbx_engine_create(const struct rmbx_model* model, int n_env, rmbx_engine** 
     return st;
   }
   if (st == RMBX_OK) st = upload(eng, subtree_end.data(), (size_t)h.nbody, &eng->subtree_end);
+  {
+    // h * (dof damping + actuator velocity gains -kv: joint actuators on the diagonal, tendon
+    // actuators as kv * coef_r * coef_c), the implicitfast addition to M, in packed 4x4 blocks
+    const int nv = h.nv, NB = (nv + 3) / 4;
+    std::vector<double> hb(16 * (size_t)(NB * (NB + 1) / 2), 0.0);
+    for (int bi = 0, t = 0; bi < NB; bi++)
+      for (int bj = 0; bj <= bi; bj++, t++)
+        for (int p = 0; p < 4; p++)
+          for (int q = 0; q < 4; q++) {
+            const int r = 4 * bi + p, cc = 4 * bj + q;
+            if (r >= nv || cc >= nv) continue;
+            double add = 0;
+            if (r == cc) add += h.dof_damping[r];
+            for (int u = 0; u < h.nu; u++) {
+              const double kv = -h.act_bias[3 * u + 2];
+              if (kv == 0) continue;
+              const int id = h.act_trnid[u];
+              if (h.act_trntype[u] == RMBX_TRN_JOINT) {
+                if (r == cc && h.jnt_dofadr[id] == r) add += kv;
+              } else {
+                double cr = 0, cq = 0;
+                for (int w = h.ten_adr[id]; w < h.ten_adr[id] + h.ten_num[id]; w++) {
+                  const int d = h.jnt_dofadr[h.wrap_jnt[w]];
+                  if (d == r) cr += h.wrap_coef[w];
+                  if (d == cc) cq += h.wrap_coef[w];
+                }
+                add += kv * cr * cq;
+              }
+            }
+            hb[16 * t + 4 * p + q] = h.timestep * add;
+          }
+    if (st == RMBX_OK) st = upload(eng, hb.data(), hb.size(), &eng->hBblk);
+  }
   if (st != RMBX_OK) {
     rmbx_engine_destroy(eng);
     return st;
@@ -3584,6 +3598,7 @@ static int launch(rmbx_engine* eng, int nsub, int integ, const uint8_t* active, 
   a.prof = prof;
   a.subtree_end = eng->subtree_end;
   a.tree_rounds = eng->tree_rounds;
+  a.hBblk = eng->hBblk;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int reps = integ ? nsub : 1;
   for (int s = 0; s < reps; s++) {

@@ -102,6 +102,12 @@ def test_cabinet_autoeval_command_line(tmp_path):
     with open(res) as f:
         data = yaml.safe_load(f)
     assert len(data["success"]) == 2
-    for d in data["duration"]:
-        assert 1.0 < d <= 1.0 + 0.032 + 1e-9
+    for ok, d in zip(data["success"], data["duration"]):
+        if ok:
+            # the random-init policy flails against the lid / drawer, and whether it knocks one
+            # open within the second is chaotic (last-bit changes flip it): after a success the
+            # RolloutPhase runs on for 1 s past the success time (RolloutBase.py:79-86)
+            assert 1.0 < d <= 2.0 + 0.032 + 1e-9
+        else:
+            assert 1.0 < d <= 1.0 + 0.032 + 1e-9  # max_duration, then one more env-step
     assert np.isfinite(ro.env.engine.qpos.cpu().numpy()).all()
