@@ -2215,6 +2215,34 @@ __device__ __forceinline__ double block_sum(double v, SolverShared& S, int tid) 
   lds_sync();
   return S.red[0] + S.red[1] + S.red[2] + S.red[3];
 }
+// two / three sums in one reduction (same summation order as block_sum: bit-identical)
+__device__ __forceinline__ void block_sum2(double& a, double& b, SolverShared& S, int tid) {
+  a = wave_sum(a);
+  b = wave_sum(b);
+  lds_sync();
+  if ((tid & 63) == 0) {
+    S.red[tid >> 6] = a;
+    S.red[4 + (tid >> 6)] = b;
+  }
+  lds_sync();
+  a = S.red[0] + S.red[1] + S.red[2] + S.red[3];
+  b = S.red[4] + S.red[5] + S.red[6] + S.red[7];
+}
+__device__ __forceinline__ void block_sum3(double& a, double& b, int& c, SolverShared& S, int tid) {
+  a = wave_sum(a);
+  b = wave_sum(b);
+  c = wave_sum_i(c);
+  lds_sync();
+  if ((tid & 63) == 0) {
+    S.red[tid >> 6] = a;
+    S.red[4 + (tid >> 6)] = b;
+    S.ired[tid >> 6] = c;
+  }
+  lds_sync();
+  a = S.red[0] + S.red[1] + S.red[2] + S.red[3];
+  b = S.red[4] + S.red[5] + S.red[6] + S.red[7];
+  c = S.ired[0] + S.ired[1] + S.ired[2] + S.ired[3];
+}
 __device__ __forceinline__ int block_sum_i(int v, SolverShared& S, int tid) {
   v = wave_sum_i(v);
   lds_sync();
@@ -2700,7 +2728,8 @@ __device__ double solver_cost(const SolverCtx& c, const double* x, SolverShared&
     c.jar[r] = jar;
     if (c.type[r] == 0 || jar < 0) cpart += 0.5 * c.D[r] * jar * jar;
   }
-  return 0.5 * block_sum(part, S, tid) + block_sum(cpart, S, tid);
+  block_sum2(part, cpart, S, tid);
+  return 0.5 * part + cpart;
 }
 
 // constraint part of the cost at x: jar = J x - aref (c.jar), sum of 0.5 D jar^2 over active rows
@@ -2972,21 +3001,28 @@ __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj,
       qp += S.srch[k] * S.Ms[k];
       lp += S.res[k] * S.Ms[k];
     }
-    const double qg = block_sum(qp, S, tid);
-    const double lg = block_sum(lp, S, tid);
-    double alpha = 0, lo = 0, hi = 1e300;
+    block_sum2(qp, lp, S, tid);
+    const double qg = qp, lg = lp;
+    // exact line search on the piecewise quadratic (Newton steps on the derivative, bracketed);
+    // the test "did any inequality row change side between the last two points" of step ls is
+    // folded into the derivative reduction of step ls + 1 (one block reduction per step)
+    double alpha = 0, prev = 0, lo = 0, hi = 1e300;
     for (int ls = 0; ls < m.ls_iterations; ls++) {
       double p1 = 0, p2 = 0;
+      int changed = 0;
       for (int r = tid; r < nefc; r += SOLVER_THREADS) {
-        const double js = c.Js[r];
-        const double x = c.jar[r] + alpha * js;
+        const double js = c.Js[r], jr = c.jar[r];
+        const double x = jr + alpha * js;
         if (c.type[r] == 0 || x < 0) {
           p1 += c.D[r] * x * js;
           p2 += c.D[r] * js * js;
         }
+        if (r >= ne) changed |= ((jr + prev * js < 0) != (x < 0));
       }
-      const double d1 = alpha * qg + lg + block_sum(p1, S, tid);
-      const double d2 = qg + block_sum(p2, S, tid);
+      block_sum3(p1, p2, changed, S, tid);
+      if (ls > 0 && changed == 0) break;
+      const double d1 = alpha * qg + lg + p1;
+      const double d2 = qg + p2;
       if (d1 == 0) break;
       if (d1 < 0)
         lo = alpha;
@@ -2994,14 +3030,8 @@ __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj,
         hi = alpha;
       double an = alpha - d1 / d2;
       if (!(an > lo && an < hi)) an = hi < 1e300 ? 0.5 * (lo + hi) : (an > lo ? an : lo);
-      int changed = 0;
-      for (int r = ne + tid; r < nefc; r += SOLVER_THREADS) {
-        const double js = c.Js[r];
-        const double x0 = c.jar[r] + alpha * js, x1 = c.jar[r] + an * js;
-        changed |= ((x0 < 0) != (x1 < 0));
-      }
+      prev = alpha;
       alpha = an;
-      if (block_sum_i(changed, S, tid) == 0) break;
     }
     SPROF(12)
     // move along the search direction; res, M res and jar updated incrementally (as
@@ -3018,7 +3048,8 @@ __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj,
       c.jar[r] = jar;
       if (c.type[r] == 0 || jar < 0) cpart += 0.5 * c.D[r] * jar * jar;
     }
-    const double newcost = 0.5 * block_sum(part, S, tid) + block_sum(cpart, S, tid);
+    block_sum2(part, cpart, S, tid);
+    const double newcost = 0.5 * part + cpart;
     SPROF(13)
     const double improvement = scale * (cost - newcost);
     cost = newcost;
@@ -3042,6 +3073,107 @@ __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj,
   SPROF(14)
   return it;
 }
+// Sensors (mj_rnePostConstraint -> force / torque at sites) in the solver block: body
+// accelerations by the LDS tree prefix, contact wrenches (p x F, F) with F the contact's world force
+// collected per body from the J^T w lists (body 2 receives -w, body 1 +w, contact order; equality
+// rows do not enter), then each sensor site body's subtree sum.
+__device__ void solver_sensors(Env& e, SolverShared& S, int ncon, int tree_rounds, int tid) {
+  const rmbx_model& m = *e.m;
+  if (m.nsensor == 0) return;
+  const int nb = m.nbody;
+  double* cacc = S.bv;
+  double* cfrc = S.bf;
+  double* cw = S.cw;
+  const double* cvel = W(cvel);
+  const double* cdofdot = W(cdofdot);
+  if (tid == 0) {
+    cacc[0] = cacc[1] = cacc[2] = 0;
+    cacc[3] = -m.gravity[0];
+    cacc[4] = -m.gravity[1];
+    cacc[5] = -m.gravity[2];
+  } else if (tid < nb) {
+    double a[6] = {0, 0, 0, 0, 0, 0};
+    const int da = m.body_dofadr[tid], dn = m.body_dofnum[tid];
+    for (int k = da; k < da + dn; k++) {
+      for (int i = 0; i < 6; i++) a[i] += cdofdot[6 * k + i] * e.qvel[k];
+      for (int i = 0; i < 6; i++) a[i] += S.cdof[6 * k + i] * S.a[k];
+    }
+    for (int i = 0; i < 6; i++) cacc[6 * tid + i] = a[i];
+  }
+  lds_sync();
+  tree_prefix6_s(S, nb, tree_rounds, cacc, tid);
+  if (tid > 0 && tid < nb) {
+    double Ia[6], Iv[6], vxIv[6];
+    const double* I = S.cinert + 10 * tid;
+    const double* v = cvel + 6 * tid;
+    inert_mul(I, cacc + 6 * tid, Ia);
+    inert_mul(I, v, Iv);
+    cross_force(v, Iv, vxIv);
+    for (int i = 0; i < 6; i++) cfrc[6 * tid + i] = Ia[i] + vxIv[i];
+  }
+  for (int c = tid; c < ncon; c += SOLVER_THREADS) {
+    double* o = cw + 6 * c;
+    const int r0 = WI(con_efcadr)[c];
+    if (r0 + (WI(con_condim)[c] == 1 ? 1 : 4) > e.L->nefc_max) {
+      for (int i = 0; i < 6; i++) o[i] = 0;
+      continue;
+    }
+    const double* F = W(con_frame) + 9 * c;
+    double fn, f1 = 0, f2 = 0;
+    const double* f = W(efc_force) + r0;
+    if (WI(con_condim)[c] == 1) {
+      fn = f[0];
+    } else {
+      const double mu = W(con_mu)[c];
+      fn = f[0] + f[1] + f[2] + f[3];
+      f1 = mu * (f[0] - f[1]);
+      f2 = mu * (f[2] - f[3]);
+    }
+    double Fw[3];
+    for (int i = 0; i < 3; i++) Fw[i] = fn * F[i] + f1 * F[3 + i] + f2 * F[6 + i];
+    cross3(W(con_pos) + 3 * c, Fw, o);
+    for (int i = 0; i < 3; i++) o[3 + i] = Fw[i];
+  }
+  lds_sync();
+  if (tid > 0 && tid < nb) {
+    double acc[6];
+    for (int i = 0; i < 6; i++) acc[i] = cfrc[6 * tid + i];
+    for (int l = S.boff[tid]; l < S.boff[tid + 1]; l++) {
+      const int en = S.blist[l];
+      if (en >= EQ_TAG) continue;
+      const double* wq = cw + 6 * (en >> 1);
+      if (en & 1)
+        for (int i = 0; i < 6; i++) acc[i] += wq[i];
+      else
+        for (int i = 0; i < 6; i++) acc[i] -= wq[i];
+    }
+    for (int i = 0; i < 6; i++) cfrc[6 * tid + i] = acc[i];
+  }
+  lds_sync();
+  if (tid < m.nsensor && tid < 2) {
+    const int s = tid;
+    const int site = m.sensor_site[s];
+    const int b = m.site_body[site];
+    double f[6];
+    for (int i = 0; i < 6; i++) f[i] = cfrc[6 * b + i];
+    for (int d = b + 1; d < S.send[b]; d++)  // interaction force = subtree sum
+      for (int i = 0; i < 6; i++) f[i] += cfrc[6 * d + i];
+    const double* p = W(sxpos) + 3 * site;
+    const double* R = W(sxmat) + 9 * site;
+    double out[3];
+    if (m.sensor_type[s] == RMBX_SENS_FORCE) {
+      mattvec3(R, f + 3, out);
+    } else {
+      double pxf[3], n[3];
+      cross3(p, f + 3, pxf);
+      for (int i = 0; i < 3; i++) n[i] = f[i] - pxf[i];
+      mattvec3(R, n, out);
+    }
+    for (int i = 0; i < 3; i++) e.sensordata[3 * s + i] = out[i];
+  }
+  lds_sync();
+}
+
 __device__ void solver_integrate(Env& e, SolverShared& S, double* a, int bi, int bj, bool own,
                                  int tid, int sub, const double* hB) {
   const rmbx_model& m = *e.m;
@@ -3271,7 +3403,7 @@ __global__ void __launch_bounds__(SOLVER_THREADS, 4) solver_kernel(KArgs args) {
   }
   const int iters = solver_newton(e, S, a, bi, bj, own, ncon, nefc, ne, nlim, args.tree_rounds, tid, prof);
   PROF(5)
-  sensors(e, ncon, tid, S.bv, S.bf, S.cw, S.anc, args.subtree_end);
+  solver_sensors(e, S, ncon, args.tree_rounds, tid);
   PROF(6)
   if (tid == 0) e.stats[2] = iters;
   if (args.integrate_flag) solver_integrate(e, S, a, bi, bj, own, tid, args.sub, args.hBblk);
