@@ -15,9 +15,12 @@ SCENES = {"ur5e_cable": os.path.join(REF_ENVS, "ur5e", "env_ur5e_cable.xml"),
           "ur5e_toolbox": os.path.join(REF_ENVS, "ur5e", "env_ur5e_toolbox.xml"),
           "ur5e_pick": os.path.join(REF_ENVS, "ur5e", "env_ur5e_pick.xml"),
           "ur5e_ring": os.path.join(REF_ENVS, "ur5e", "env_ur5e_ring.xml")}
-# per-scene compile options: the Pick scene (BASELINE configs 4/5) collides its scanned objects
-# through their convex hulls (MPR) and drops the YCB_sim objects, absent from the checkout
-OPTIONS = {"ur5e_pick": dict(convex_meshes=True, skip_missing_includes=True), "ur5e_ring": dict(convex_meshes=True)}
+# per-scene compile options: every scene collides its mesh geoms (the gripper_collision class of
+# ur5e_integrated_shared_config.xml:51-52, the scanned objects) through their convex hulls (MPR)
+# and its cylinders exactly, as MuJoCo does; the Pick scene (BASELINE configs 4/5) drops the
+# YCB_sim objects, absent from the checkout
+OPTIONS = {name: dict(convex_meshes=True) for name in SCENES}
+OPTIONS["ur5e_pick"] = dict(convex_meshes=True, skip_missing_includes=True)
 PACK_OPTIONS = {"ur5e_pick": dict(max_contacts=200)}
 UR5E_URDF = "/root/reference/robo_manip_baselines/envs/assets/common/robots/ur5e/ur5e.urdf"
 
