@@ -93,6 +93,9 @@ def parse(argv=None):
     p.add_argument("--total_envs", type=int, default=None,
                    help="whole-job environment count, sharded over the GPUs (strong scaling)")
     p.add_argument("--precision", choices=["fp32", "bf16"], default="fp32", help="policy precision of `value`")
+    p.add_argument("--groups", type=int, default=1,
+                   help="env groups per GPU, each on its own HIP stream with its policy steps offset by one env-step "
+                        "(measured: no gain at 1024 envs, DESIGN.md section 5)")
     p.add_argument("--no_bf16_secondary", action="store_true")
     p.add_argument("--no_cpu_baseline", action="store_true")
     p.add_argument("--act_full_decoder", action="store_true", help="also run the dead decoder layers 1..6")
@@ -251,32 +254,20 @@ def make_rollout(args, dev, precision, n_local, g0):
     return ro
 
 
-def timed_run(ro, args, dist):
-    """W warm-up + K timed env-steps; HIP events around every physics launch sequence and every
-    infer_policy call (same stream)."""
+def timed_run(groups, args, dist):
+    """W warm-up + K timed env-steps of every group, group g on HIP stream g (its policy steps
+    offset by g env-steps: group g takes g extra warm-up steps), then isolated probes: the physics
+    launch sequence of every group and one infer_policy call of group 0, each bracketed by HIP
+    events with nothing else queued (in-loop events would include the other groups' kernels)."""
+    streams = [torch.cuda.current_stream()] + [torch.cuda.Stream() for _ in groups[1:]]
     for i in range(args.warmup):  # also MIOpen / hipBLASLt algorithm selection
-        ro.step_once()
+        for ro in groups:
+            ro.step_once()
         torch.cuda.synchronize()
         progress(f"warm-up step {i + 1}/{args.warmup}")
-    phys_ev, infer_ev = [], []
-    eng = ro.env.engine
-    orig_step, orig_infer = eng.step, ro.infer_policy
-
-    def timed_step(nsub=8, active=None):
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        orig_step(nsub, active)
-        e1.record()
-        phys_ev.append((e0, e1))
-
-    def timed_infer():
-        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-        e0.record()
-        orig_infer()
-        e1.record()
-        infer_ev.append((e0, e1))
-
-    eng.step, ro.infer_policy = timed_step, timed_infer
+    for g, ro in enumerate(groups):
+        for _ in range(g % max(1, ro.args.skip)):
+            ro.step_once()
     if dist:
         import torch.distributed as tdist
 
@@ -284,22 +275,39 @@ def timed_run(ro, args, dist):
     torch.cuda.synchronize()
     t0 = time.time()
     for _ in range(args.steps):
-        ro.step_once()
+        for ro, st in zip(groups, streams):
+            with torch.cuda.stream(st):
+                ro.step_once()
     torch.cuda.synchronize()
     if dist:
         tdist.barrier()
     elapsed = time.time() - t0
     progress(f"timed {args.steps} steps: {elapsed:.3f} s")
-    eng.step, ro.infer_policy = orig_step, orig_infer
-    phys = np.array([a.elapsed_time(b) for a, b in phys_ev])
-    infer = np.array([a.elapsed_time(b) for a, b in infer_ev]) / 1e3
+    # isolated probes (after the timed region)
+    phys = []
+    for _ in range(3):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for ro in groups:
+            ro.env.engine.step(8, ro._active if ro._active is not None else ro._step_mask)
+        e1.record()
+        torch.cuda.synchronize()
+        phys.append(e0.elapsed_time(e1))
+    infer = []
+    for _ in range(2):
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        groups[0].infer_policy()
+        e1.record()
+        torch.cuda.synchronize()
+        infer.append(e0.elapsed_time(e1) / 1e3)
     if dist:
         import torch.distributed as tdist
 
-        t = torch.tensor([elapsed], dtype=torch.float64, device=ro.device)
+        t = torch.tensor([elapsed], dtype=torch.float64, device=groups[0].device)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         elapsed = float(t.item())
-    return elapsed, phys, infer
+    return elapsed, np.array(phys), np.array(infer)
 
 
 @torch.no_grad()
@@ -346,17 +354,26 @@ def rank_main(args):
     from robomanipbaselines_amd.distributed import gather_results, pack_results
 
     strong, total, g0, n = job_shard(args, rank, world)
+    G = max(1, min(args.groups, n))
+    bounds = [n * g // G for g in range(G + 1)]
 
-    ro = make_rollout(args, dev, args.precision, n, g0)
-    elapsed, phys, infer = timed_run(ro, args, dist)
+    def make_groups(precision):
+        return [make_rollout(args, dev, precision, bounds[g + 1] - bounds[g], g0 + bounds[g]) for g in range(G)]
+
+    groups = make_groups(args.precision)
+    ro = groups[0]
+    elapsed, phys, infer = timed_run(groups, args, dist)
     value = total * args.steps / elapsed
     if dist:
         # RCCL all-gather of per-env episode records (success, reward, duration, steps)
-        v = K.sched_view(ro.sched)
-        gathered = gather_results(pack_results(v["success"], v["result_reward"], v["duration"], v["rollout_time_idx"]), dev)
+        parts = []
+        for r in groups:
+            v = K.sched_view(r.sched)
+            parts.append(pack_results(v["success"], v["result_reward"], v["duration"], v["rollout_time_idx"]))
+        gathered = gather_results(np.concatenate(parts), dev)
         assert gathered.shape[0] == total
     eng = ro.env.engine
-    st = eng.stats.cpu().numpy()
+    st = np.concatenate([r.env.engine.stats.cpu().numpy() for r in groups])
     bytes_env_step = algorithmic_bytes_per_env_step(eng.nq, eng.nv, eng.nu, 8)
     kern_s = float(phys.mean()) / 1e3
     achieved = n * bytes_env_step / kern_s / 1e9
@@ -382,10 +399,13 @@ def rank_main(args):
                                f"chunk 100, skip 3, temporal ensembling), {args.precision} policy, RolloutPhase hot loop",
                    "num_envs_per_gpu": n, "total_envs": total,
                    "parallelism": f"env-sharded x{world}, RCCL all-gather of results",
+                   "env_groups": G,
                    "act_decoder_layers_run": 7 if args.act_full_decoder else 1},
         "policy_inference_us_per_call": round(1e6 * float(infer.mean()), 1) if len(infer) else None,
-        "policy_inference_us_per_env_step": round(1e6 * float(infer.mean()) / (n * ro.args.skip), 3) if len(infer) else None,
+        "policy_inference_batch": groups[0].n,
+        "policy_inference_us_per_env_step": round(1e6 * float(infer.mean()) / (groups[0].n * ro.args.skip), 3) if len(infer) else None,
         "physics_kernel_ms": round(float(phys.mean()), 3),
+        "physics_probe": f"isolated HIP-event time of one env-step of all {n} envs ({G} engine launch sequences back to back)",
         "roofline": {"bound": "hbm", "achieved": round(achieved, 4), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "traffic": round(traffic_env * n) if traffic_env else None,
@@ -401,7 +421,7 @@ def rank_main(args):
         "contacts_mean": ncon, "constraint_rows_mean": nefc, "newton_iters_mean": iters,
     }
     if len(infer):
-        pol_tf = n * pol_flops / float(infer.mean()) / 1e12
+        pol_tf = groups[0].n * pol_flops / float(infer.mean()) / 1e12
         peak = MFMA_PEAK_TFLOPS[args.precision]
         # whole batched infer_policy call (render + preprocessing + ACT), all kernels on the stream
         result["roofline_policy"] = {"bound": "mfma", "achieved": round(pol_tf, 2), "peak": peak,
@@ -409,9 +429,12 @@ def rank_main(args):
                                      "algorithmic_flops_per_inference": pol_flops,
                                      "scope": "one batched infer_policy call over all envs"}
     if args.precision == "fp32" and not args.no_bf16_secondary:
-        ro16 = make_rollout(args, dev, "bf16", n, g0)
-        el16, _, inf16 = timed_run(ro16, args, dist)
-        err_abs, err_rel = bf16_action_error(ro, ro16)
+        del groups, ro, eng
+        torch.cuda.empty_cache()
+        groups16 = make_groups("bf16")
+        el16, _, inf16 = timed_run(groups16, args, dist)
+        ro32 = make_rollout(args, dev, "fp32", 16, g0)  # same weights (seeded), its own 16-env frame
+        err_abs, err_rel = bf16_action_error(ro32, groups16[0])
         result["secondary_bf16"] = {
             "value": round(total * args.steps / el16, 1), "unit": "env-steps/s",
             "ms_per_step": round(1e3 * el16 / args.steps, 3), "dtype": "f64 physics + bf16 policy",
@@ -420,7 +443,7 @@ def rank_main(args):
             "note": "throughput mode, NOT reference precision: same workload with the ACT policy in bf16; "
                     "action error measured on the first 16 envs' frame (same weights, same inputs)"}
         if len(inf16):
-            tf16 = n * pol_flops / float(inf16.mean()) / 1e12
+            tf16 = groups16[0].n * pol_flops / float(inf16.mean()) / 1e12
             result["secondary_bf16"]["roofline_policy"] = {"bound": "mfma", "achieved": round(tf16, 2),
                                                            "peak": MFMA_PEAK_TFLOPS["bf16"], "unit": "TFLOP/s",
                                                            "frac": tf16 / MFMA_PEAK_TFLOPS["bf16"]}
