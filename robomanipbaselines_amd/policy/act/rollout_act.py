@@ -41,6 +41,11 @@ class RolloutAct(BatchedRolloutBase):
             load_act_checkpoint(self.policy, self.args.checkpoint)
         self.policy.prune_dead_decoder = bool(self.args.act_prune_dead_decoder)
         self.policy_dtype = torch.bfloat16 if self.args.precision == "bf16" else torch.float32
+        if self.policy_dtype == torch.float32:
+            # the reference's precision: IEEE fp32 convolutions and GEMMs, never a TF32-style
+            # reduced-mantissa mode (torch enables it for cuDNN/MIOpen convs by default)
+            torch.backends.cudnn.allow_tf32 = False
+            torch.backends.cuda.matmul.allow_tf32 = False
         # MIOpen Find (measured solver choice per conv shape; once per shape, during warm-up):
         # 66 -> 53 ms for the 1024-env trunk on MI355X (scripts/prof_act.py)
         torch.backends.cudnn.benchmark = True
