@@ -2161,6 +2161,8 @@ struct SolverShared {
   double red[8];
   int ired[8];
   int jb[RCHUNK][2];           // chunk rows: the two bodies
+  int jlist[RCHUNK];           // chunk rows with a nonzero weight, in row order
+  int jn;
   int jd[RCHUNK][2];           // chunk rows: dof terms (-1: none)
   double eqrho[NEQR][12];      // equality rows: body-side 6-vectors, dof coefficients,
   double eqcoef[NEQR][2];      //   bodies, dofs (-1: none) -- staged once per launch
@@ -2845,6 +2847,10 @@ __device__ void solver_hessian(const SolverCtx& c, const double* Mb, const int32
       }
       S.jw[tid] = w;
       S.jsg[tid] = sg;
+      // compact the rows that update the Hessian (wave 0, lanes < RCHUNK)
+      const unsigned long long nz = __ballot(w != 0.0) & ((1ull << RCHUNK) - 1);
+      if (w != 0.0) S.jlist[__popcll(nz & ((1ull << tid) - 1))] = tid;
+      if (tid == 0) S.jn = __popcll(nz);
     }
     lds_sync();
     CPROF(19)
@@ -2873,17 +2879,33 @@ __device__ void solver_hessian(const SolverCtx& c, const double* Mb, const int32
     lds_sync();
     CPROF(31)
     if (own) {
-      for (int rr = 0; rr < nr; rr++) {
-        if (S.jw[rr] == 0.0) continue;
-        const double sg = S.jsg[rr];  // -1: a row that left the active set is taken back out
-        const double* ji = S.jc[rr] + 4 * bi;
-        const double* jj = S.jc[rr] + 4 * bj;
-        const double i0 = sg * ji[0], i1 = sg * ji[1], i2 = sg * ji[2], i3 = sg * ji[3];
-        const double j0 = jj[0], j1 = jj[1], j2 = jj[2], j3 = jj[3];
+      // rank-1 updates over the chunk's nonzero rows; the next row's slices are loaded before
+      // this row's 16 FMAs so the LDS latency hides under them
+      const int n = S.jn;
+      int rr = n > 0 ? S.jlist[0] : 0;
+      double2 ia = *reinterpret_cast<const double2*>(S.jc[rr] + 4 * bi);
+      double2 ib = *reinterpret_cast<const double2*>(S.jc[rr] + 4 * bi + 2);
+      double2 ja = *reinterpret_cast<const double2*>(S.jc[rr] + 4 * bj);
+      double2 jb = *reinterpret_cast<const double2*>(S.jc[rr] + 4 * bj + 2);
+      double sg = S.jsg[rr];  // -1: a row that left the active set is taken back out
+      for (int l = 0; l < n; l++) {
+        const int rn = S.jlist[l + 1 < n ? l + 1 : l];
+        const double2 ia2 = *reinterpret_cast<const double2*>(S.jc[rn] + 4 * bi);
+        const double2 ib2 = *reinterpret_cast<const double2*>(S.jc[rn] + 4 * bi + 2);
+        const double2 ja2 = *reinterpret_cast<const double2*>(S.jc[rn] + 4 * bj);
+        const double2 jb2 = *reinterpret_cast<const double2*>(S.jc[rn] + 4 * bj + 2);
+        const double sg2 = S.jsg[rn];
+        const double i0 = sg * ia.x, i1 = sg * ia.y, i2 = sg * ib.x, i3 = sg * ib.y;
+        const double j0 = ja.x, j1 = ja.y, j2 = jb.x, j3 = jb.y;
         a[0] += i0 * j0; a[1] += i0 * j1; a[2] += i0 * j2; a[3] += i0 * j3;
         a[4] += i1 * j0; a[5] += i1 * j1; a[6] += i1 * j2; a[7] += i1 * j3;
         a[8] += i2 * j0; a[9] += i2 * j1; a[10] += i2 * j2; a[11] += i2 * j3;
         a[12] += i3 * j0; a[13] += i3 * j1; a[14] += i3 * j2; a[15] += i3 * j3;
+        ia = ia2;
+        ib = ib2;
+        ja = ja2;
+        jb = jb2;
+        sg = sg2;
       }
     }
   }
