@@ -31,6 +31,7 @@ def _load(flops=False):
         lib.orc_get_state.argtypes = [vp, vp, vp, vp, vp]
         lib.orc_set_body_pos.argtypes = [vp, ip, vp]
         lib.orc_get_xpos.argtypes = [vp, vp, vp]
+        lib.orc_get_efc.argtypes = [vp, vp, vp]
         lib.orc_get_geom.argtypes = [vp, vp, vp]
         lib.orc_get_sensor.argtypes = [vp, vp]
         lib.orc_get_M.argtypes = [vp, vp]
@@ -130,6 +131,14 @@ class OracleEnv:
 
     def nefc(self):
         return self.lib.orc_nefc(self.h)
+
+    def efc(self):
+        """(J [nefc, nv], D [nefc]) of the last forward / step (MuJoCo's dense efc_J, efc_D)."""
+        n = self.nefc()
+        J, D = np.zeros((n, self.nv)), np.zeros(n)
+        if n:
+            self.lib.orc_get_efc(self.h, J.ctypes.data, D.ctypes.data)
+        return J, D
 
     def solver_iter(self):
         return self.lib.orc_solver_iter(self.h)

@@ -2126,6 +2126,12 @@ void orc_get_vecs(void* p, double* bias, double* passive, double* actuator, doub
   if (constraint) memcpy(constraint, d->qfrc_constraint, n);
   if (qacc) memcpy(qacc, d->qacc, n);
 }
+/* constraint Jacobian (dense, nefc x nv) and row weights D of the last forward / step */
+void orc_get_efc(void* p, double* J, double* D) {
+  Data* d = (Data*)p;
+  if (J) memcpy(J, d->J, sizeof(double) * (size_t)d->nefc * d->m->nv);
+  if (D) memcpy(D, d->efc_D, sizeof(double) * (size_t)d->nefc);
+}
 int orc_ncon(void* p) { return ((Data*)p)->ncon; }
 int orc_nefc(void* p) { return ((Data*)p)->nefc; }
 int orc_solver_iter(void* p) { return ((Data*)p)->solver_iter; }

@@ -3706,10 +3706,13 @@ int rmbx_engine_ws_offset(const rmbx_engine* eng, const char* name, size_t* offs
       {"con_dist", L.con_dist, (size_t)m.max_contacts},
       {"efc_force", L.efc_force, (size_t)L.nefc_max},
       {"efc_D", L.efc_D, (size_t)L.nefc_max},
+      {"hsave", L.hsave, 16 * (size_t)(((nv + 3) / 4) * ((nv + 3) / 4 + 1) / 2)},
       {"efc_aref", L.efc_aref, (size_t)L.nefc_max},
       // int32 arrays: offsets in int32 units from the workspace start (2 per double)
       {"con_b1", 2 * L.ints + L.con_b1, (size_t)m.max_contacts},
       {"con_b2", 2 * L.ints + L.con_b2, (size_t)m.max_contacts},
+      {"efc_hact", 2 * L.ints + L.efc_hact, (size_t)L.nefc_max},
+      {"efc_act", 2 * L.ints + L.efc_act, (size_t)L.nefc_max},
   };
   for (const Item& it : items) {
     if (strcmp(it.n, name) == 0) {

@@ -103,12 +103,13 @@ class PhysicsEngine:
         N.call("rmbx_engine_ws_offset", self._h, name.encode(), ctypes.byref(off), ctypes.byref(cnt))
         return off.value, cnt.value
 
-    def mass_matrix(self):
+    def mass_matrix(self, name="Mblk"):
         """Dense [n_env, nv*nv] copy of the mass matrix (the engine keeps only the packed lower
-        4x4 blocks the solver loads: block t = bi(bi+1)/2 + bj, entry 4p+q = M[4bi+p][4bj+q])."""
+        4x4 blocks the solver loads: block t = bi(bi+1)/2 + bj, entry 4p+q = M[4bi+p][4bj+q]);
+        name="hsave": the Newton Hessian of the last build, in the same packing."""
         nv = self.nv
         nb = (nv + 3) // 4
-        blk = self.ws("Mblk").view(self.n_env, -1, 4, 4)
+        blk = self.ws(name).view(self.n_env, -1, 4, 4)
         full = torch.zeros((self.n_env, 4 * nb, 4 * nb), dtype=torch.float64, device=self.device)
         t = 0
         for bi in range(nb):
