@@ -163,3 +163,44 @@ def test_arm_fk_kernel_matches_oracle():
         R6, p6 = arm_ik.fk(P, q[e])[-1]
         np.testing.assert_allclose(R[e].reshape(3, 3), R6, rtol=0, atol=1e-14)
         np.testing.assert_allclose(p[e], p6, rtol=0, atol=1e-14)
+
+
+def test_fk_restatement_agrees_with_the_reference_mjcf():
+    """Known answer from independent reference data: the oracle's Pinocchio FK runs on the URDF
+    chain (envs/assets/common/robots/ur5e/ur5e.urdf, as ArmManager does), MuJoCo on the MJCF
+    (ur5e_integrated_body.xml) -- the same arm described twice.  Up to one constant frame offset
+    (fixed at the init pose), the wrist_3 frame orientations agree to 1e-9 over random joint
+    angles (axes and rotation order pinned); positions agree within 2 mm, the link-offset
+    difference between the two reference assets (1.46 mm max measured)."""
+    from scipy.spatial.transform import Rotation
+
+    from oracle.dyn import OracleEnv
+    from robomanipbaselines_amd import model as MD
+
+    a = MD.load("ur5e_cable")
+    P = _placement()
+    jn = [str(x) for x in a["names_jnt"]]
+    b6 = int(a["jnt_body"][jn.index("wrist_3_joint")])
+    qadr = [int(a["jnt_qposadr"][jn.index(str(n))]) for n in a["arm_joint_names"]]
+    o = OracleEnv(a)
+
+    def mjcf_frame(q):
+        qp = a["qpos0"].copy()
+        qp[qadr] = q
+        o.set_state(0.0, qp, np.zeros(o.nv), np.zeros(o.nv), np.zeros(max(o.nu, 1)))
+        o.forward()
+        xp, xq = o.xpos()
+        return Rotation.from_quat(xq[b6][[1, 2, 3, 0]]).as_matrix(), xp[b6]
+
+    q0 = a["qpos0"][qadr]
+    Ru0, pu0 = arm_ik.fk(P, q0)[-1]
+    Rm0, pm0 = mjcf_frame(q0)
+    TR, Tp = Ru0.T @ Rm0, Ru0.T @ (pm0 - pu0)
+    np.testing.assert_allclose(np.abs(TR).max(0), 1.0, atol=1e-9)  # a signed axis permutation
+    rng = np.random.default_rng(0)
+    for _ in range(20):
+        q = rng.uniform(-np.pi, np.pi, 6)
+        Ru, pu = arm_ik.fk(P, q)[-1]
+        Rm, pm = mjcf_frame(q)
+        np.testing.assert_allclose(Ru @ TR, Rm, rtol=0, atol=1e-9)
+        np.testing.assert_allclose(pu + Ru @ Tp, pm, rtol=0, atol=2e-3)
