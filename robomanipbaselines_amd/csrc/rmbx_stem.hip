@@ -260,12 +260,21 @@ __global__ void __launch_bounds__(SP_THREADS) stem_pool_kernel(StemPoolArgs a) {
 // f32 form (the reference's precision): the same fused stem on the renderer's f32 space-to-depth
 // image [N][Hs][Ws][16] (12 channels used) with v_mfma_f32_32x32x2_f32 (exact f32 products,
 // f32 accumulation), output [N][Hp][Wp][64] f32 (channels_last) for the layer-1 convs.
-// K per tap = 12 s2d channels = 6 MFMA k-pairs; the 4 zero pad channels are skipped.
-// LDS: filter bank sW[tap][kpair][h][64 cout] (48 KiB), input ring sR[slot][kpair][rc][2]
-// (5 x 6 x 324 x 8 B = 76 KiB), edges.  One block per (image, band) as in the bf16 kernel.
+// K per tap = 12 s2d channels = 6 MFMA k-pairs; the 4 zero pad channels are skipped, and so are
+// the k-pairs that are zero in every re-indexed 7x7 filter (pack_stem_s2d: ky = 0 has no dy = 0
+// rows -> k-pairs 0..2; kx = 0 has no dx = 0 columns -> k-pairs 0 and 3): 77 of 96 k-pair steps.
+// f32 MFMA issues at 64 cycles per 32x32x2 on each SIMD, so the kernel is MFMA-bound and the
+// work is split evenly over the 4 SIMDs: 4 waves per block (one per SIMD), wave w owns output
+// channel tile t = w & 1 (32 channels) of column tiles 5 (w >> 1) .. 5 (w >> 1) + 4 (32 stem
+// columns each) for both stem rows of a pool row: 10 independent accumulators per wave.
+// LDS: filter bank sW[tap][kpair][h][64 cout] (48 KiB), input ring sR[slot][kpair][324][2]
+// (76 KiB), edges.  One block per (image, band) as in the bf16 kernel; Ws <= 320.
 // ---------------------------------------------------------------------------------------------
-constexpr int SF_LDS_F32 = 16 * 6 * 2 * 64 + SP_RING * 6 * SP_RC_MAX * 2 + 64 + SP_MAX_WAVES * 2 * 32;
+constexpr int SF_WAVES = 4, SF_TILES = 5, SF_THREADS = 64 * SF_WAVES;
+constexpr int SF_RC = SP_RC_MAX;  // ring columns: s2d cols -2 .. 321 (zeros beyond the image)
+constexpr int SF_LDS_F32 = 16 * 6 * 2 * 64 + SP_RING * 6 * SF_RC * 2 + 64 + SF_WAVES * 2 * 16;
 static_assert(SF_LDS_F32 * 4 <= 160 * 1024, "f32 stem+pool LDS must fit the 160 KiB of a CU");
+static_assert(2 * SF_TILES * 32 == 32 * SP_MAX_WAVES, "the two wave pairs cover the 320 columns");
 
 struct StemPoolF32Args {
   const float* in;   // [N][Hs][Ws][16]
@@ -273,18 +282,43 @@ struct StemPoolF32Args {
   const float* bias; // [64]
   float* out;        // [N][Hp][Wp][64]
   int N, Hs, Ws, Hp, Wp;
-  int nct, rc, bands, band_rows;
+  int bands, band_rows;
 };
 
-__global__ void __launch_bounds__(SP_THREADS) stem_pool_f32_kernel(StemPoolF32Args a) {
+// one filter row ky of the f32 stem: 4 taps x the k-pairs from KP_LO, minus the kx = 0 pairs that
+// hold only dx = 0 channels; straight-line so that the next k-pair's LDS reads are issued under
+// the current k-pair's 10 MFMAs
+template <int KP_LO>
+__device__ __forceinline__ void sf_filter_row(f32x16 (&acc)[SF_TILES][2], const float* row0, const float* row1,
+                                              const float* wrow) {
+#pragma unroll
+  for (int kx = 0; kx < 4; ++kx) {
+#pragma unroll
+    for (int kp = KP_LO; kp < 6; ++kp) {
+      if (kx == 0 && (kp == 0 || kp == 3)) continue;  // dx = 0 column of the 8x8 window
+      const float aw = wrow[(kx * 6 + kp) * 128];
+      float bx[SF_TILES][2];
+#pragma unroll
+      for (int i = 0; i < SF_TILES; ++i) {
+        bx[i][0] = row0[(kp * SF_RC + 32 * i + kx) * 2];
+        bx[i][1] = row1[(kp * SF_RC + 32 * i + kx) * 2];
+      }
+#pragma unroll
+      for (int i = 0; i < SF_TILES; ++i)
+#pragma unroll
+        for (int r = 0; r < 2; ++r) acc[i][r] = __builtin_amdgcn_mfma_f32_32x32x2f32(aw, bx[i][r], acc[i][r], 0, 0, 0);
+    }
+  }
+}
+
+__global__ void __launch_bounds__(SF_THREADS) stem_pool_f32_kernel(StemPoolF32Args a) {
   __shared__ __attribute__((aligned(16))) float sf_smem[SF_LDS_F32];
   float* sW = sf_smem;                            // [16 taps][6 kpairs][2 h][64 cout]
-  float* sR = sW + 16 * 6 * 2 * 64;               // [5 slots][6 kpairs][rc][2]
-  float* sBias = sR + SP_RING * 6 * a.rc * 2;     // [64]
-  float* sEdge = sBias + 64;                      // [nct][2 h][32]
+  float* sR = sW + 16 * 6 * 2 * 64;               // [5 slots][6 kpairs][SF_RC][2]
+  float* sBias = sR + SP_RING * 6 * SF_RC * 2;    // [64]
+  float* sEdge = sBias + 64;                      // [waves][2 h][16]
 
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int nthreads = blockDim.x;
   const int img = blockIdx.x / a.bands, band = blockIdx.x - img * a.bands;
   const int py0 = band * a.band_rows;
   const int py1 = min(a.Hp, py0 + a.band_rows);
@@ -294,15 +328,15 @@ __global__ void __launch_bounds__(SP_THREADS) stem_pool_f32_kernel(StemPoolF32Ar
   const float* in_img = a.in + (size_t)img * a.Hs * row_elems;
 
   // filter bank: global [cout][tap][16] -> sW[tap][kp][h][cout] (channels 0..11)
-  for (int q = tid; q < 64 * 16 * 12; q += nthreads) {
+  for (int q = tid; q < 64 * 16 * 12; q += SF_THREADS) {
     const int c = q % 12, rest = q / 12;  // rest = cout * 16 + tap
     const int co = rest >> 4, tap = rest & 15;
     sW[((tap * 6 + (c >> 1)) * 2 + (c & 1)) * 64 + co] = a.w[(size_t)rest * 16 + c];
   }
   if (tid < 64) sBias[tid] = a.bias[tid];
 
-  // 16-byte chunk q (pixel column c = q / 3 of the ring, channel quad j = q % 3) of s2d row y
-  const int row_chunks = 3 * a.rc;
+  // 16-byte chunk q (ring column c = q / 3, channel quad j = q % 3) of s2d row y
+  constexpr int row_chunks = 3 * SF_RC;
   auto load_chunk = [&](int y, int q) -> float4 {
     const int c = q / 3, j = q - 3 * c;
     const int x = c - 2;
@@ -311,40 +345,33 @@ __global__ void __launch_bounds__(SP_THREADS) stem_pool_f32_kernel(StemPoolF32Ar
   };
   auto store_chunk = [&](int slot, int q, float4 v) {
     const int c = q / 3, j = q - 3 * c;  // channels 4j..4j+3 = kpairs 2j, 2j+1
-    float* base = sR + (size_t)slot * 6 * a.rc * 2;
-    *reinterpret_cast<float2*>(base + ((size_t)(2 * j) * a.rc + c) * 2) = make_float2(v.x, v.y);
-    *reinterpret_cast<float2*>(base + ((size_t)(2 * j + 1) * a.rc + c) * 2) = make_float2(v.z, v.w);
+    float* base = sR + (size_t)slot * 6 * SF_RC * 2;
+    *reinterpret_cast<float2*>(base + ((size_t)(2 * j) * SF_RC + c) * 2) = make_float2(v.x, v.y);
+    *reinterpret_cast<float2*>(base + ((size_t)(2 * j + 1) * SF_RC + c) * 2) = make_float2(v.z, v.w);
   };
   auto slot_of = [](int y) { return (y + 2 * SP_RING) % SP_RING; };
-  for (int q = tid; q < SP_RING * row_chunks; q += nthreads) {
+  for (int q = tid; q < SP_RING * row_chunks; q += SF_THREADS) {
     const int r = q / row_chunks, qq = q - r * row_chunks;
     const int y = 2 * pys - 2 + r;
     store_chunk(slot_of(y), qq, load_chunk(y, qq));
   }
 
   const int n = lane & 31, h = lane >> 5;
-  const int X = 32 * wave + n;
-  const int m = lane & 31;
-  const int sig = 16 * ((m >> 2) & 1) + (m & 3) + 4 * (m >> 3);
-  const bool col_ok = X < a.Ws;
+  const int t = wave & 1;                  // output channel tile
+  const int ct0 = SF_TILES * (wave >> 1);  // first column tile
+  const int sig = 16 * ((n >> 2) & 1) + (n & 3) + 4 * (n >> 3);
+  const float* wcol = sW + h * 64 + 32 * t + sig;  // + (tap * 6 + kp) * 128
+  const int xcol = 32 * ct0 + n;                   // this lane's stem column in tile 0
 
-  constexpr int PF_MAX = 4;  // (2 rows * 3 quads * 324 cols) / 640 threads, rounded up
+  constexpr int PF_MAX = (2 * row_chunks + SF_THREADS - 1) / SF_THREADS;  // next two s2d rows
   float4 pf[PF_MAX];
   uint32_t pf_ok = 0;
-  const int pf_chunks = 2 * row_chunks;
-  int pf_r[PF_MAX], pf_q[PF_MAX];
-#pragma unroll
-  for (int i = 0; i < PF_MAX; ++i) {
-    const int q = min(tid + nthreads * i, pf_chunks - 1);
-    pf_r[i] = q / row_chunks;
-    pf_q[i] = q - pf_r[i] * row_chunks;
-  }
 
-  float carry[2][16];
+  float carry[SF_TILES][16];
 #pragma unroll
-  for (int t = 0; t < 2; ++t)
+  for (int i = 0; i < SF_TILES; ++i)
 #pragma unroll
-    for (int k = 0; k < 16; ++k) carry[t][k] = 0.f;
+    for (int k = 0; k < 16; ++k) carry[i][k] = 0.f;
 
   __syncthreads();
   for (int py = pys; py < py1; ++py) {
@@ -354,91 +381,86 @@ __global__ void __launch_bounds__(SP_THREADS) stem_pool_f32_kernel(StemPoolF32Ar
       pf_ok = 0;
 #pragma unroll
       for (int i = 0; i < PF_MAX; ++i) {
-        const int y = Y0 + 3 + pf_r[i];
-        const int c = pf_q[i] / 3, j = pf_q[i] - 3 * c, x = c - 2;
-        const bool ok = tid + nthreads * i < pf_chunks && y < a.Hs && x >= 0 && x < a.Ws;
+        const int q = tid + SF_THREADS * i;
+        const int r = q / row_chunks, qq = q - r * row_chunks;
+        const int y = Y0 + 3 + r;
+        const int c = qq / 3, j = qq - 3 * c, x = c - 2;
+        const bool ok = q < 2 * row_chunks && y < a.Hs && x >= 0 && x < a.Ws;
         const size_t off = ok ? (size_t)y * row_elems + (size_t)x * 16 + 4 * j : 0;
         pf[i] = *reinterpret_cast<const float4*>(in_img + off);
         pf_ok |= (uint32_t)ok << i;
       }
     }
-    f32x16 acc[2][2];
+    f32x16 acc[SF_TILES][2];
 #pragma unroll
-    for (int r = 0; r < 2; ++r)
+    for (int i = 0; i < SF_TILES; ++i)
 #pragma unroll
-      for (int t = 0; t < 2; ++t) acc[r][t] = f32x16{};
-    int slot[5];
-#pragma unroll
-    for (int d = 0; d < 5; ++d) slot[d] = slot_of(Y0 - 2 + d);
-#pragma unroll 2
-    for (int tap = 0; tap < 16; ++tap) {
-      const int ky = tap >> 2, kx = tap & 3;
-#pragma unroll
-      for (int kp = 0; kp < 6; ++kp) {
-        float bx[2], aw[2];
-#pragma unroll
-        for (int r = 0; r < 2; ++r)
-          bx[r] = sR[(((size_t)slot[r + ky] * 6 + kp) * a.rc + X + kx) * 2 + h];
-#pragma unroll
-        for (int t = 0; t < 2; ++t) aw[t] = sW[((tap * 6 + kp) * 2 + h) * 64 + 32 * t + sig];
-#pragma unroll
-        for (int r = 0; r < 2; ++r)
-#pragma unroll
-          for (int t = 0; t < 2; ++t)
-            acc[r][t] = __builtin_amdgcn_mfma_f32_32x32x2f32(aw[t], bx[r], acc[r][t], 0, 0, 0);
-      }
-    }
+      for (int r = 0; r < 2; ++r) acc[i][r] = f32x16{};
+    // ring rows of stem rows Y0 (r = 0) and Y0 + 1 (r = 1) for filter row ky
+    auto ring_row = [&](int y) { return sR + (size_t)slot_of(y) * 6 * SF_RC * 2 + h + 2 * xcol; };
+    sf_filter_row<3>(acc, ring_row(Y0 - 2), ring_row(Y0 - 1), wcol);  // ky = 0: no dy = 0 rows
+#pragma unroll 1
+    for (int ky = 1; ky < 4; ++ky) sf_filter_row<0>(acc, ring_row(Y0 - 2 + ky), ring_row(Y0 - 1 + ky), wcol + ky * 4 * 6 * 128);
 
     // bias + ReLU, vertical max with the carried row (all values >= 0, so 0 is the pool padding);
-    // the window max overwrites acc[0] in place (register pressure)
+    // the window max overwrites acc[i][0] in place
     const bool row1_ok = Y0 + 1 < a.Hs;
 #pragma unroll
-    for (int t = 0; t < 2; ++t) {
+    for (int i = 0; i < SF_TILES; ++i) {
+      const bool col_ok = xcol + 32 * i < a.Ws;
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
         const float b = sBias[32 * t + 16 * h + k];
-        const float p0 = fmaxf(acc[0][t][k] + b, 0.f);
-        const float p1 = row1_ok ? fmaxf(acc[1][t][k] + b, 0.f) : 0.f;
-        acc[0][t][k] = col_ok ? fmaxf(fmaxf(carry[t][k], p0), p1) : 0.f;
-        carry[t][k] = p1;
+        const float p0 = fmaxf(acc[i][0][k] + b, 0.f);
+        const float p1 = row1_ok ? fmaxf(acc[i][1][k] + b, 0.f) : 0.f;
+        acc[i][0][k] = col_ok ? fmaxf(fmaxf(carry[i][k], p0), p1) : 0.f;
+        carry[i][k] = p1;
       }
     }
     if (n == 31) {
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
-#pragma unroll
-        for (int k = 0; k < 16; ++k) sEdge[(wave * 2 + h) * 32 + 16 * t + k] = acc[0][t][k];
+      for (int k = 0; k < 16; ++k) sEdge[(wave * 2 + h) * 16 + k] = acc[SF_TILES - 1][0][k];
     }
     __syncthreads();
 
     if (more) {
 #pragma unroll
       for (int i = 0; i < PF_MAX; ++i) {
-        if (tid + nthreads * i < pf_chunks) {
+        const int q = tid + SF_THREADS * i;
+        if (q < 2 * row_chunks) {
+          const int r = q / row_chunks, qq = q - r * row_chunks;
           const float4 v = ((pf_ok >> i) & 1u) ? pf[i] : make_float4(0.f, 0.f, 0.f, 0.f);
-          store_chunk(pf_r[i] ? slot[1] : slot[0], pf_q[i], v);
+          store_chunk(slot_of(Y0 + 3 + r), qq, v);
         }
       }
     }
     if (py >= py0) {
-      const int px = 16 * wave + (n >> 1);
-      const bool store = (n & 1) == 0 && px < a.Wp;
-      float* dst = a.out + (((size_t)img * a.Hp + py) * a.Wp + px) * 64 + 16 * h;
+      // horizontal window: stem columns 2px - 1, 2px, 2px + 1 around the even lanes; column
+      // 32 ct - 1 comes from the previous tile's lane 31 (or the left wave pair's edge)
 #pragma unroll
-      for (int t = 0; t < 2; ++t)
+      for (int i = 0; i < SF_TILES; ++i) {
+        const int px = 16 * (ct0 + i) + (n >> 1);
+        const bool store = (n & 1) == 0 && px < a.Wp;
+        float* dst = a.out + (((size_t)img * a.Hp + py) * a.Wp + px) * 64 + 32 * t + 16 * h;
 #pragma unroll
         for (int k4 = 0; k4 < 4; ++k4) {
           float o[4];
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int k = 4 * k4 + e;
-            float left = __shfl_up(acc[0][t][k], 1);
-            const float right = __shfl_down(acc[0][t][k], 1);
-            if (n == 0) left = wave > 0 ? sEdge[((wave - 1) * 2 + h) * 32 + 16 * t + k] : 0.f;
-            o[e] = fmaxf(fmaxf(left, acc[0][t][k]), right);
+            float left = __shfl_up(acc[i][0][k], 1);
+            const float right = __shfl_down(acc[i][0][k], 1);
+            float prev;
+            if (i > 0)
+              prev = __shfl(acc[i - 1][0][k], (lane & 32) | 31);
+            else
+              prev = wave >= 2 ? sEdge[((wave - 2) * 2 + h) * 16 + k] : 0.f;
+            if (n == 0) left = prev;
+            o[e] = fmaxf(fmaxf(left, acc[i][0][k]), right);
           }
-          if (store) *reinterpret_cast<float4*>(dst + 32 * t + 4 * k4) = make_float4(o[0], o[1], o[2], o[3]);
+          if (store) *reinterpret_cast<float4*>(dst + 4 * k4) = make_float4(o[0], o[1], o[2], o[3]);
         }
+      }
     }
     __syncthreads();
   }
@@ -504,9 +526,6 @@ extern "C" int rmbx_stem_s2d_conv_maxpool_f32(const float* in, const float* weig
   a.Ws = Ws;
   a.Hp = (Hs - 1) / 2 + 1;
   a.Wp = (Ws - 1) / 2 + 1;
-  a.nct = (Ws + 31) / 32;
-  a.rc = 32 * a.nct + 4;
-  RMBX_CHECK_ARG(2 * 3 * a.rc <= 4 * 64 * a.nct, "rmbx_stem_s2d_conv_maxpool_f32: prefetch does not fit");
   if (band_rows <= 0) {
     const int want_blocks = 512;
     int bands = (want_blocks + N - 1) / N;
@@ -517,7 +536,7 @@ extern "C" int rmbx_stem_s2d_conv_maxpool_f32(const float* in, const float* weig
   a.bands = (a.Hp + band_rows - 1) / band_rows;
   const long long nblocks = (long long)N * a.bands;
   RMBX_CHECK_ARG(nblocks < (1ll << 31), "rmbx_stem_s2d_conv_maxpool_f32: grid too large");
-  hipLaunchKernelGGL(rmbx::stem_pool_f32_kernel, dim3((unsigned)nblocks), dim3(64 * a.nct), 0, (hipStream_t)stream, a);
+  hipLaunchKernelGGL(rmbx::stem_pool_f32_kernel, dim3((unsigned)nblocks), dim3(rmbx::SF_THREADS), 0, (hipStream_t)stream, a);
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
 }

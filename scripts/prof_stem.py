@@ -1,5 +1,7 @@
 """Diagnostic: the ResNet-18 stem at batch B on 480x640 frames — unfused (rmbx_stem_s2d_conv +
-rmbx_nhwc_bias_relu_maxpool) vs fused (rmbx_stem_s2d_conv_maxpool), timed with HIP events."""
+rmbx_nhwc_bias_relu_maxpool) vs fused (rmbx_stem_s2d_conv_maxpool), bf16, and the fused f32 form
+(rmbx_stem_s2d_conv_maxpool_f32, the fp32 policy's stem) against the f32 MFMA peak, timed with
+HIP events."""
 import json
 import os
 import sys
@@ -40,3 +42,10 @@ with torch.no_grad():
     print(json.dumps({"B": B, "unfused_conv_ms": round(ms_conv, 3), "unfused_pool_ms": round(ms_pool, 3),
                       "fused_ms": round(ms_fused, 3), "fused_tflops_alg": round(flop / ms_fused / 1e9, 1),
                       "fused_io_gbs": round(io / ms_fused / 1e6, 1)}), flush=True)
+    del xs
+    xf = torch.rand(B, 240, 320, 16, device=dev)
+    wf = K.pack_stem_s2d(torch.randn(64, 3, 7, 7, device=dev) * 0.1)
+    ms_f32 = timed(lambda: K.stem_s2d_conv_maxpool(xf, wf, b))
+    print(json.dumps({"B": B, "f32_fused_ms": round(ms_f32, 3), "f32_tflops_alg": round(flop / ms_f32 / 1e9, 1),
+                      "f32_frac_of_157": round(flop / ms_f32 / 1e9 / 157.3, 3)}), flush=True)
+
