@@ -297,6 +297,14 @@ int rmbx_nhwc_bias_act(const void* x, const float* bias, const void* res, const 
 int rmbx_conv2d_nhwc(const void* in, const void* weight, const float* bias, const void* residual,
                      void* out, int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
                      int pad, int relu, void* stream);
+/* The same conv in f32 (the reference's fp32 policy): in/weight/residual/out f32 in the layouts
+ * above, exact f32 products with f32 accumulation (v_mfma_f32_32x32x2_f32), bias + residual +
+ * ReLU applied to the accumulators before the single store.  Implemented for the ResNet-18
+ * layer-1 conv only (KH = KW = 3, stride 1, pad 1, Cin = Cout = 64); other shapes return
+ * RMBX_ERR_ARG. */
+int rmbx_conv2d_nhwc_f32(const float* in, const float* weight, const float* bias, const float* residual,
+                         float* out, int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                         int pad, int relu, void* stream);
 /* ResNet stem on a 2x2 space-to-depth image: in [N][Hs][Ws][16] bf16 (channel (dy*2+dx)*3+c,
  * 12..15 zero; rmbx_render policy_dtype 2 writes this layout), weight packed [Cout][4][4][16] bf16
  * (the 7x7 / stride-2 / pad-3 conv1 re-indexed), out [N][Hs][Ws][Cout] bf16 = relu?(conv + bias).
@@ -314,7 +322,9 @@ int rmbx_stem_s2d_conv_maxpool(const void* in, const void* weight, const float* 
 /* The same fused stem in f32 (the reference's precision): in [N][Hs][Ws][16] f32 (rmbx_render
  * policy_dtype 3; channels 12..15 ignored), weight packed [64][4][4][16] f32, bias f32 [64],
  * out [N][Hp][Wp][64] f32 = maxpool3x3s2p1(relu(conv + bias)); exact f32 products with f32
- * accumulation (v_mfma_f32_32x32x2_f32).  Replaces the same reference ops as above. */
+ * accumulation (v_mfma_f32_32x32x2_f32).  The weight must be a re-indexed 7x7 filter as
+ * pack_stem_s2d writes it: the taps ky = 0 / dy = 0 and kx = 0 / dx = 0 (outside the 7x7 window)
+ * are zero and are not multiplied.  Replaces the same reference ops as above. */
 int rmbx_stem_s2d_conv_maxpool_f32(const float* in, const float* weight, const float* bias, float* out,
                                    int N, int Hs, int Ws, int band_rows, void* stream);
 /* Multi-head attention forward, bf16: out[b][i][h*64 + d] = sum_j softmax_j(scale * q_i . k_j) v_j[d]

@@ -504,6 +504,201 @@ __global__ void __launch_bounds__(RTHREADS) conv3x3_c64_resident_kernel(ConvArgs
 #undef RMBX_RES_TILE
 }
 
+// ---------------------------------------------------------------------------------------------
+// f32 form of the layer-1 conv (3x3 / stride 1 / pad 1, Cin = Cout = 64; the reference's fp32
+// policy) with the same fused epilogue, v_mfma_f32_32x32x2_f32 (exact f32 products, f32
+// accumulation).  f32 MFMA issues at 64 cycles per instruction, so unlike the bf16 kernels this
+// one is MFMA-bound and is laid out to keep the four SIMDs issuing:
+//  * a persistent block per CU (8 waves, two per SIMD, so one wave's LDS reads hide under the
+//    other's MFMAs) keeps the filter taps of its 32 output channels resident in LDS
+//    (9 x 64 x 32 f32 = 72 KiB) and walks a contiguous range of 8 x 32 output tiles (120 x 160
+//    splits exactly); wave w owns output row w of the tile (32 pixels) x the block's 32 channels:
+//    one accumulator, 288 MFMAs per tile;
+//  * the tile's 10 x 34 x 64 f32 input patch (85 KiB) is staged in LDS once for all 9 taps as two
+//    channel halves: the MFMAs run over half 0 (all taps), then half 1, and the next tile's half 0
+//    (prefetched into registers at the top of the tile) is written while half 1 is multiplied --
+//    the patch traffic hides under the MFMAs instead of stalling every wave between tiles;
+//  * the A rows (output channels) are permuted so that each lane finishes 16 consecutive channels
+//    of ONE pixel: bias, residual and ReLU are applied in registers and leave as 16-byte stores
+//    (no LDS transpose), and the barriers order LDS only, so the stores drain under the next
+//    tile's MFMAs;
+//  * the two channel halves of a tile run on blocks b and b + 8 (the same XCD under round-robin
+//    dispatch), so each input patch is fetched from HBM once per XCD.
+// ---------------------------------------------------------------------------------------------
+constexpr int FC_TH = 8, FC_TW = 32, FC_PH = FC_TH + 2, FC_PW = FC_TW + 2, FC_COUT = 32, FC_THREADS = 512;
+constexpr int FC_W_FLOATS = 9 * 32 * FC_COUT * 2;            // sW[tap][kpair][cout][2]
+constexpr int FC_PKP = FC_PH * FC_PW * 2;                    // floats per k-pair plane of the patch
+constexpr int FC_P_FLOATS = 32 * FC_PKP;                     // sP[kpair][py][px][2]
+constexpr int FC_HCHUNKS = FC_PH * FC_PW * 8;                // float4 chunks of one channel half
+constexpr int FC_PPT = (FC_HCHUNKS + FC_THREADS / 2 - 1) / (FC_THREADS / 2);  // per thread
+static_assert((FC_W_FLOATS + FC_P_FLOATS) * 4 <= 160 * 1024, "f32 conv LDS must fit the 160 KiB of a CU");
+static_assert(FC_THREADS % 16 == 0, "a thread's channel quad is the same in every patch chunk");
+static_assert(FC_PPT <= 12, "three filter rows carry a thread's patch stores");
+
+// workgroup barrier that orders LDS only: unlike __syncthreads() it does not wait for the
+// wave's outstanding global stores (the previous tile's outputs drain under the next tile's MFMAs)
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+struct ConvF32Args {
+  const float* in;    // [N][H][W][64]
+  const float* w;     // [64][3][3][64]
+  const float* bias;  // [64]
+  const float* res;   // [N][H][W][64] or null
+  float* out;         // [N][H][W][64]
+  int N, H, W, relu;
+  int tiles_x, tiles_y;
+  long long ntiles;
+  int dbg;  // diagnostic phase skips (RMBX_CONV_DBG: 1 = no MFMAs, 2 = no patch loads, 4 = no patch
+            // stores / residual loads / output stores; 0 in production)
+};
+
+// the 9 taps x 16 k-pairs of one channel half (KP0 = 0 or 16) into acc; hook(kh) runs after
+// each filter row (the patch stores of the next tile are spread over the MFMA stream this way)
+template <int KP0, class Hook>
+__device__ __forceinline__ void fc_half(f32x16& acc, const float* wl, const float* pl, Hook&& hook) {
+#pragma unroll
+  for (int kh = 0; kh < 3; ++kh) {
+#pragma unroll
+    for (int kw = 0; kw < 3; ++kw) {
+      const float* wt = wl + ((kh * 3 + kw) * 32 + KP0) * 64;
+      const float* pt = pl + KP0 * FC_PKP + (kh * FC_PW + kw) * 2;
+#pragma unroll
+      for (int kp = 0; kp < 16; ++kp)
+        acc = __builtin_amdgcn_mfma_f32_32x32x2f32(wt[kp * 64], pt[kp * FC_PKP], acc, 0, 0, 0);
+    }
+    hook(kh);
+  }
+}
+
+__global__ void __launch_bounds__(FC_THREADS) conv3x3_c64_f32_kernel(ConvF32Args a) {
+  __shared__ __attribute__((aligned(16))) float smem[FC_W_FLOATS + FC_P_FLOATS];
+  float* sW = smem;
+  float* sP = smem + FC_W_FLOATS;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int b = blockIdx.x;
+  const int half = (b >> 3) & 1;              // output channels 32 half .. 32 half + 31
+  const int G = gridDim.x >> 1;               // tile groups (gridDim.x % 16 == 0)
+  const int g = (b & 7) + 8 * (b >> 4);
+  const long long t_begin = a.ntiles * g / G, t_end = a.ntiles * (g + 1) / G;
+  if (t_begin >= t_end) return;
+  const int co0 = FC_COUT * half;
+
+  // filter taps of the block's channels: global [cout][tap][cin] -> sW[tap][kp][cout_local][2]
+  for (int q = tid; q < FC_COUT * 9 * 16; q += FC_THREADS) {
+    const int quad = q & 15, rest = q >> 4;  // rest = cout_local * 9 + tap
+    const int cl = rest / 9, tap = rest - 9 * cl;
+    const float4 v = *reinterpret_cast<const float4*>(a.w + ((size_t)(co0 + cl) * 9 + tap) * 64 + 4 * quad);
+    *reinterpret_cast<float2*>(sW + (((size_t)tap * 32 + 2 * quad) * FC_COUT + cl) * 2) = make_float2(v.x, v.y);
+    *reinterpret_cast<float2*>(sW + (((size_t)tap * 32 + 2 * quad + 1) * FC_COUT + cl) * 2) = make_float2(v.z, v.w);
+  }
+
+  const int n = lane & 31, h = lane >> 5;
+  const int sig = 16 * ((n >> 2) & 1) + (n & 3) + 4 * (n >> 3);  // A row n -> channel sig
+  const float* wl = sW + sig * 2 + h;                    // + (tap * 32 + kp) * 64
+  const float* pl = sP + (wave * FC_PW + n) * 2 + h;     // B column n = tile pixel (wave, n)
+  float bv[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) bv[j] = a.bias[co0 + 16 * h + j];
+
+  auto tile_of = [&](long long t, int& img, int& oy0, int& ox0) {
+    const int tx = (int)(t % a.tiles_x);
+    const long long r = t / a.tiles_x;
+    oy0 = (int)(r % a.tiles_y) * FC_TH;
+    img = (int)(r / a.tiles_y);
+    ox0 = tx * FC_TW;
+  };
+  // Waves 0..3 stage channel half 0 of the patches (k-pairs 0..15), waves 4..7 half 1: chunk
+  // c = (tid & 255) + 256 i of a half = pixel c >> 3 x channel quad (c & 7) + 8 hi.  A wave's
+  // next-tile chunks are loaded into registers after it has stored the current ones, and stored
+  // while the OTHER half is multiplied (hi waves during half 0, the others during half 1).
+  const bool hi = wave >= 4;
+  const int ht = tid & (FC_THREADS / 2 - 1);
+  const int quad = (ht & 7) + 8 * hi;
+  // loads are unconditional (clamped to a valid address) and the out-of-image chunks are zeroed
+  // only when stored, so no wait on them is forced before the MFMAs they should hide under
+  float4 pf[FC_PPT];
+  uint32_t pf_ok = 0;
+  auto load_patch = [&](long long t) {
+    int img, oy0, ox0;
+    tile_of(t, img, oy0, ox0);
+    pf_ok = 0;
+#pragma unroll
+    for (int i = 0; i < FC_PPT; ++i) {
+      const int c = ht + (FC_THREADS / 2) * i;
+      const int pp = c >> 3;
+      const int py = pp / FC_PW, px = pp - py * FC_PW;
+      const int y = oy0 - 1 + py, x = ox0 - 1 + px;
+      const bool ok = c < FC_HCHUNKS && y >= 0 && y < a.H && x >= 0 && x < a.W;
+      const size_t off = ok ? (((size_t)img * a.H + y) * a.W + x) * 64 + 4 * quad : 0;
+      pf[i] = *reinterpret_cast<const float4*>(a.in + off);
+      pf_ok |= (uint32_t)ok << i;
+    }
+  };
+  auto store_chunk = [&](int i) {
+    const int c = ht + (FC_THREADS / 2) * i;
+    if (c < FC_HCHUNKS) {
+      const float4 v = ((pf_ok >> i) & 1u) ? pf[i] : make_float4(0.f, 0.f, 0.f, 0.f);
+      float* dst = sP + (size_t)(2 * quad) * FC_PKP + (c >> 3) * 2;
+      *reinterpret_cast<float2*>(dst) = make_float2(v.x, v.y);
+      *reinterpret_cast<float2*>(dst + FC_PKP) = make_float2(v.z, v.w);
+    }
+  };
+  auto store_third = [&](int kh) {  // chunks 4 kh .. 4 kh + 3, after filter row kh
+#pragma unroll
+    for (int i = 4 * kh; i < 4 * kh + 4; ++i)
+      if (i < FC_PPT) store_chunk(i);
+  };
+  load_patch(t_begin);
+#pragma unroll
+  for (int i = 0; i < FC_PPT; ++i) store_chunk(i);
+  lds_barrier();  // sW and the first patch are in LDS
+
+  for (long long t = t_begin; t < t_end; ++t) {
+    int img, oy0, ox0;
+    tile_of(t, img, oy0, ox0);
+    const bool more = t + 1 < t_end;
+    if (!hi && more && !(a.dbg & 2)) load_patch(t + 1);
+    const int oy = oy0 + wave, ox = ox0 + n;
+    const bool pix_ok = oy < a.H && ox < a.W;
+    const size_t pix_off = (((size_t)img * a.H + oy) * a.W + ox) * 64 + co0 + 16 * h;
+    float4 rv[4];
+    if (a.res && !(a.dbg & 4)) {
+      const float* rp = a.res + (pix_ok ? pix_off : 0);
+#pragma unroll
+      for (int k4 = 0; k4 < 4; ++k4) rv[k4] = *reinterpret_cast<const float4*>(rp + 4 * k4);
+    }
+
+    // half 0 (P0 = k-pairs 0..15 of this tile); the hi waves write this tile's half 1 meanwhile
+    const bool st1 = hi && t > t_begin && !(a.dbg & 4);
+    f32x16 acc = {};
+    if (!(a.dbg & 1)) fc_half<0>(acc, wl, pl, [&](int kh) { if (st1) store_third(kh); });
+    lds_barrier();  // every wave is done with half 0 of this tile's patch, and half 1 is visible
+    if (hi && more && !(a.dbg & 2)) load_patch(t + 1);
+    // half 1; the other waves write the next tile's half 0 meanwhile
+    const bool st0 = !hi && more && !(a.dbg & 4);
+    if (!(a.dbg & 1)) fc_half<16>(acc, wl, pl, [&](int kh) { if (st0) store_third(kh); });
+    lds_barrier();  // every wave is done with half 1; the next half 0 is visible
+    if (pix_ok && !(a.dbg & 4)) {
+      float o[16];
+#pragma unroll
+      for (int k4 = 0; k4 < 4; ++k4) {
+        const float r4[4] = {rv[k4].x, rv[k4].y, rv[k4].z, rv[k4].w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int j = 4 * k4 + e;
+          float v = acc[j] + bv[j];
+          if (a.res) v += r4[e];
+          if (a.relu) v = v > 0.f ? v : (v != v ? v : 0.f);
+          o[j] = v;
+        }
+      }
+#pragma unroll
+      for (int k4 = 0; k4 < 4; ++k4)
+        *reinterpret_cast<float4*>(a.out + pix_off + 4 * k4) = make_float4(o[4 * k4], o[4 * k4 + 1], o[4 * k4 + 2], o[4 * k4 + 3]);
+    }
+  }
+}
+
 int device_cus() {
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -606,6 +801,39 @@ extern "C" int rmbx_stem_s2d_conv(const void* in, const void* weight, const floa
   const long long nblocks = a.n_mtiles * a.n_ntiles;
   RMBX_CHECK_ARG(nblocks < (1ll << 31), "rmbx_stem_s2d_conv: grid too large");
   hipLaunchKernelGGL(rmbx::conv_nhwc_kernel<1>, dim3((unsigned)nblocks), dim3(256), 0, (hipStream_t)stream, a);
+  RMBX_CHECK_LAUNCH();
+  return RMBX_OK;
+}
+
+extern "C" int rmbx_conv2d_nhwc_f32(const float* in, const float* weight, const float* bias, const float* residual,
+                                    float* out, int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
+                                    int pad, int relu, void* stream) {
+  RMBX_CHECK_ARG(in && weight && bias && out, "rmbx_conv2d_nhwc_f32: null pointer");
+  RMBX_CHECK_ARG(N >= 0 && H > 0 && W > 0, "rmbx_conv2d_nhwc_f32: bad geometry");
+  RMBX_CHECK_ARG(Cin == 64 && Cout == 64 && KH == 3 && KW == 3 && stride == 1 && pad == 1,
+                 "rmbx_conv2d_nhwc_f32: only the 3x3 / stride 1 / pad 1 conv with Cin = Cout = 64 is implemented");
+  RMBX_CHECK_ARG((((uintptr_t)in | (uintptr_t)weight | (uintptr_t)out | (uintptr_t)residual) & 15) == 0,
+                 "rmbx_conv2d_nhwc_f32: tensors must be 16-byte aligned");
+  if (N == 0) return RMBX_OK;
+  rmbx::ConvF32Args a;
+  a.in = in;
+  a.w = weight;
+  a.bias = bias;
+  a.res = residual;
+  a.out = out;
+  a.N = N;
+  a.H = H;
+  a.W = W;
+  a.relu = relu;
+  a.tiles_x = (W + rmbx::FC_TW - 1) / rmbx::FC_TW;
+  a.tiles_y = (H + rmbx::FC_TH - 1) / rmbx::FC_TH;
+  a.ntiles = (long long)N * a.tiles_x * a.tiles_y;
+  const char* dbg_env = std::getenv("RMBX_CONV_DBG");
+  a.dbg = dbg_env ? std::atoi(dbg_env) : 0;
+  // one persistent block per CU, the two channel halves of a tile group on blocks b, b + 8
+  int grid = rmbx::device_cus();
+  grid = grid < 16 ? 16 : grid - grid % 16;
+  hipLaunchKernelGGL(rmbx::conv3x3_c64_f32_kernel, dim3(grid), dim3(rmbx::FC_THREADS), 0, (hipStream_t)stream, a);
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
 }

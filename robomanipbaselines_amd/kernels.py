@@ -450,12 +450,14 @@ def add_layernorm_pos(x, r, weight, bias, pos, eps=1e-5):
 
 
 def conv2d_nhwc(x, weight, bias, stride=1, padding=0, relu=False, res=None):
-    """relu?(conv2d(x, weight) + bias + res) by rmbx_conv2d_nhwc: x bf16 channels_last
-    [N, Cin, H, W], weight bf16 channels_last [Cout, Cin, KH, KW], bias f32 [Cout], res bf16
-    channels_last [N, Cout, Ho, Wo] or None -> bf16 channels_last [N, Cout, Ho, Wo]."""
+    """relu?(conv2d(x, weight) + bias + res) by rmbx_conv2d_nhwc (bf16) / rmbx_conv2d_nhwc_f32
+    (f32: the 3x3 / stride-1 / pad-1 conv with Cin = Cout = 64 only): x channels_last
+    [N, Cin, H, W], weight channels_last [Cout, Cin, KH, KW] of the same dtype, bias f32 [Cout],
+    res channels_last [N, Cout, Ho, Wo] or None -> channels_last [N, Cout, Ho, Wo]."""
     _chk_nhwc(x, "x")
-    if x.dtype != torch.bfloat16 or weight.dtype != torch.bfloat16:
-        raise ValueError("conv2d_nhwc is bf16 only")
+    dt = x.dtype
+    if dt not in (torch.bfloat16, torch.float32) or weight.dtype != dt:
+        raise ValueError("conv2d_nhwc: x and weight must both be bf16 or both f32")
     if weight.dim() != 4 or not weight.is_contiguous(memory_format=torch.channels_last):
         raise ValueError("weight must be a channels_last [Cout, Cin, KH, KW] tensor")
     n, cin, H, W = x.shape
@@ -465,14 +467,20 @@ def conv2d_nhwc(x, weight, bias, stride=1, padding=0, relu=False, res=None):
     _chk(bias, torch.float32, (cout,), "bias")
     ho = (H + 2 * padding - kh) // stride + 1
     wo = (W + 2 * padding - kw) // stride + 1
-    out = torch.empty((n, cout, ho, wo), dtype=torch.bfloat16, device=x.device, memory_format=torch.channels_last)
+    out = torch.empty((n, cout, ho, wo), dtype=dt, device=x.device, memory_format=torch.channels_last)
     if res is not None:
         _chk_nhwc(res, "res")
-        if tuple(res.shape) != tuple(out.shape) or res.dtype != torch.bfloat16:
+        if tuple(res.shape) != tuple(out.shape) or res.dtype != dt:
             raise ValueError("res must match the output")
-    N.call("rmbx_conv2d_nhwc", N.ptr(x), N.ptr(weight), N.ptr(bias), N.ptr(res), N.ptr(out), n, H, W, cin, cout,
+    fn = "rmbx_conv2d_nhwc" if dt == torch.bfloat16 else "rmbx_conv2d_nhwc_f32"
+    N.call(fn, N.ptr(x), N.ptr(weight), N.ptr(bias), N.ptr(res), N.ptr(out), n, H, W, cin, cout,
            kh, kw, int(stride), int(padding), int(bool(relu)), N.stream_ptr())
     return out
+
+
+def conv2d_nhwc_f32_supported(cin, cout, kernel_size, stride, padding):
+    """Whether rmbx_conv2d_nhwc_f32 implements this conv (ResNet-18 layer 1)."""
+    return (cin, cout, tuple(kernel_size), stride, padding) == (64, 64, (3, 3), 1, 1)
 
 
 def pack_stem_s2d(weight):

@@ -104,9 +104,17 @@ class _FusedConv(nn.Module):
         return K.nhwc_bias_act(y, self.bias_f32(), relu=self.relu, out=y)
 
     def rmbx(self, x, relu, res=None):
-        """conv + bias (+ res) (+ ReLU) in one rmbx implicit-GEMM launch (bf16)."""
+        """conv + bias (+ res) (+ ReLU) in one rmbx implicit-GEMM launch (bf16, or f32 for the
+        layer-1 shape)."""
         c = self.conv
-        return K.conv2d_nhwc(x, c.weight, self.bias_f32(), c.stride[0], c.padding[0], relu=relu, res=res)
+        w = c.weight
+        if not w.is_contiguous(memory_format=torch.channels_last):
+            w = w.contiguous(memory_format=torch.channels_last)
+        return K.conv2d_nhwc(x, w, self.bias_f32(), c.stride[0], c.padding[0], relu=relu, res=res)
+
+    def rmbx_f32_ok(self):
+        c = self.conv
+        return K.conv2d_nhwc_f32_supported(c.in_channels, c.out_channels, c.kernel_size, c.stride[0], c.padding[0])
 
 
 class _FusedBlock(nn.Module):
@@ -127,6 +135,11 @@ class _FusedBlock(nn.Module):
             y = self.c1.rmbx(x, relu=True)
             idt = x if self.down is None else self.down.rmbx(x, relu=False)
             return self.c2.rmbx(y, relu=True, res=idt)
+        if x.dtype == torch.float32 and self.down is None and self.c1.rmbx_f32_ok() and self.c2.rmbx_f32_ok():
+            # f32 layer 1: rmbx f32 MFMA convs with the epilogue fused (the f32 MIOpen solvers
+            # need a separate bias/residual/ReLU pass and a split-K zero fill per conv)
+            y = self.c1.rmbx(x, relu=True)
+            return self.c2.rmbx(y, relu=True, res=x)
         y = self.c1(x)
         z = self.c2.conv_nobias(y)
         if self.down is None:
@@ -139,7 +152,8 @@ class FusedResNet18Trunk(nn.Module):
     """Inference form on the device: BN folded into conv weights/bias, channels_last
     activations.  bf16: the block convs are rmbx MFMA implicit-GEMM kernels with bias / residual /
     ReLU fused (rmbx_conv2d_nhwc); the 3-channel 7x7 stem is MIOpen + the rmbx bias/ReLU/max-pool
-    epilogue.  f32: MIOpen convs + one rmbx HIP epilogue per conv.  Same function as ResNet18Trunk; bit-identical to the unfused storage-dtype
+    epilogue.  f32: layer 1 on rmbx_conv2d_nhwc_f32 (epilogue fused), layers 2-4 MIOpen convs +
+    one rmbx HIP epilogue per conv.  Same function as ResNet18Trunk; bit-identical to the unfused storage-dtype
     sequence on the same conv outputs (tests/test_nn_gpu.py)."""
 
     def __init__(self, trunk):

@@ -124,6 +124,41 @@ def test_conv2d_nhwc_matches_fp32(cin, cout, k, stride, res, relu):
 
 
 @torch.no_grad()
+@pytest.mark.parametrize("n,H,W,res,relu", [(5, 37, 45, True, True), (2, 16, 32, False, True), (3, 9, 17, True, False),
+                                            (1, 120, 160, True, True)])
+def test_conv2d_nhwc_f32_matches_fp32(n, H, W, res, relu):
+    """rmbx_conv2d_nhwc_f32 (layer-1 conv, f32 MFMA, fused bias/residual/ReLU) vs F.conv2d in fp32:
+    within f32 accumulation-order rounding (ragged tiles, several tiles per persistent block)."""
+    from robomanipbaselines_amd import kernels as K
+
+    g = torch.Generator(device=DEV).manual_seed(n * 1000 + H)
+    x = _cl(torch.randn(n, 64, H, W, device=DEV, generator=g))
+    w = _cl(torch.randn(64, 64, 3, 3, device=DEV, generator=g) / 24)
+    b = torch.randn(64, device=DEV, generator=g)
+    ref = F.conv2d(x, w, b, 1, 1)
+    r = None
+    if res:
+        r = _cl(torch.randn(ref.shape, device=DEV, generator=g))
+        ref = ref + r
+    if relu:
+        ref = F.relu(ref)
+    got = K.conv2d_nhwc(x, w, b, 1, 1, relu=relu, res=r)
+    assert got.dtype == torch.float32 and got.shape == ref.shape
+    assert got.is_contiguous(memory_format=torch.channels_last)
+    err = (got - ref).abs().max().item()
+    assert err <= 2e-5 * max(1.0, ref.abs().max().item()), err
+
+
+def test_conv2d_nhwc_f32_rejects_other_shapes():
+    from robomanipbaselines_amd import kernels as K
+
+    x = _cl(torch.randn(1, 128, 8, 8, device=DEV))
+    w = _cl(torch.randn(128, 128, 3, 3, device=DEV))
+    with pytest.raises(ValueError):
+        K.conv2d_nhwc(x, w, torch.zeros(128, device=DEV), 1, 1)
+
+
+@torch.no_grad()
 def test_conv3x3_c64_resident_equals_streaming_kernel(monkeypatch):
     """The persistent resident-filter kernel (Cin = Cout = 64) walks several 16x16 tiles per block
     (768 tiles > CU count, ragged edges) and must equal the per-tile streaming kernel bit for bit
