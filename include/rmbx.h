@@ -335,6 +335,12 @@ int rmbx_stem_s2d_conv_maxpool_f32(const float* in, const float* weight, const f
 int rmbx_attention_bf16(const void* q, const void* k, const void* v, void* out, int B, int heads, int Lq, int Lk,
                         long long q_bstride, int q_rstride, long long k_bstride, int k_rstride, long long v_bstride,
                         int v_rstride, float scale, void* stream);
+/* The same attention in f32 (the reference's fp32 policy): q/k/v/out f32 with the layouts and
+ * strides above (strides multiples of 4 elements, 16-byte aligned), any Lk; exact f32 products
+ * and accumulation (v_mfma_f32_32x32x2_f32), f32 online softmax in the log2 domain. */
+int rmbx_attention_f32(const float* q, const float* k, const float* v, float* out, int B, int heads, int Lq, int Lk,
+                       long long q_bstride, int q_rstride, long long k_bstride, int k_rstride, long long v_bstride,
+                       int v_rstride, float scale, void* stream);
 /* Residual add + LayerNorm over the last dim of [rows][D] rows (D <= 2048, multiple of 8 bf16 / 4
  * f32): out = LayerNorm(rnd(x + r)) * weight + bias (f32 weight/bias), r optional (NULL); replaces
  * the add + nn.LayerNorm pair of the ACT transformer's post-norm layers (third_party/act). */

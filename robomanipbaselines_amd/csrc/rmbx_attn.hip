@@ -214,6 +214,166 @@ __global__ void __launch_bounds__(64 * AT_MAX_WAVES) attn_fwd_kernel(AttnArgs a)
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// f32 form (the reference's fp32 policy): exact f32 products and accumulation on
+// v_mfma_f32_32x32x2_f32, f32 online softmax.  f32 MFMA is 16x slower than bf16, so this kernel is
+// MFMA-bound and is laid out for occupancy rather than for LDS reuse: a block of 4-5 waves takes
+// up to 5 32-query groups of one (batch, head) (302 queries: two blocks), the keys stream through
+// a double-buffered LDS tile of 32 keys (K and V, 17 KiB each buffer, one barrier per tile, the
+// next tile prefetched into registers under the current tile's MFMAs), so 3-4 blocks share a CU.
+// Per wave and key tile: S^T = K Q^T (32 MFMAs, Q held in registers pre-scaled by scale*log2 e,
+// dims 32h + kk on lane half h), the online softmax in-lane plus one exchange with lane ^ 32, and
+// O^T += V^T P^T (2 x 16 MFMAs) with P fed straight from the S accumulator registers (MFMA t
+// consumes key 8(t/4) + 4h + t%4 on half h, the key the S register t of that half holds) and
+// V's dims permuted (at_sigma) so each lane finishes 16 consecutive dims of its query.
+// ---------------------------------------------------------------------------------------------
+constexpr int AF_MAX_WAVES = 5;
+constexpr int AF_KP = 65;  // K tile row pitch (floats): lanes (key i, half h) at i*65 + 32h hit 64 banks
+constexpr int AF_VP = 72;  // V tile row pitch: the halves' keys (4 apart) land 32 banks apart
+constexpr int AF_TILE = 32 * AF_KP + 32 * AF_VP;  // floats of one K + V tile buffer
+
+struct AttnF32Args {
+  const float* q;
+  const float* k;
+  const float* v;
+  float* o;
+  long long q_bstride, k_bstride, v_bstride;
+  int q_rstride, k_rstride, v_rstride;
+  int o_rstride;
+  int heads, Lq, Lk, parts;
+  float scale_log2;
+};
+
+__global__ void __launch_bounds__(64 * AF_MAX_WAVES) __attribute__((amdgpu_waves_per_eu(4))) attn_fwd_f32_kernel(AttnF32Args a) {
+  __shared__ __attribute__((aligned(16))) float sT[2 * AF_TILE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nthreads = blockDim.x, nwaves = nthreads >> 6;
+  const int bh = blockIdx.x / a.parts, part = blockIdx.x - bh * a.parts;
+  const int b = bh / a.heads, head = bh - b * a.heads;
+  const int n = lane & 31, h = lane >> 5;
+  const int qrow = (part * nwaves + wave) * 32 + n;
+  const bool qok = qrow < a.Lq;
+  const float* kbase = a.k + (size_t)b * a.k_bstride + head * 64;
+  const float* vbase = a.v + (size_t)b * a.v_bstride + head * 64;
+
+  // this lane's query dims 32h .. 32h + 31, pre-scaled into the log2 domain
+  float qv[32];
+  {
+    const float* qp = a.q + (size_t)b * a.q_bstride + (size_t)(qok ? qrow : 0) * a.q_rstride + head * 64 + 32 * h;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const float4 x = *reinterpret_cast<const float4*>(qp + 4 * c);
+      qv[4 * c] = x.x * a.scale_log2;
+      qv[4 * c + 1] = x.y * a.scale_log2;
+      qv[4 * c + 2] = x.z * a.scale_log2;
+      qv[4 * c + 3] = x.w * a.scale_log2;
+    }
+  }
+
+  // key tile jt -> registers in two halves (K rows, then V rows: 512 16-byte chunks each, at most
+  // 2 per thread), each loaded one phase ahead of its store so that only 8 staging registers live
+  const int nt = (a.Lk + 31) >> 5;
+  constexpr int PF = 2;
+  float4 pf[PF];
+  auto load_half = [&](int jt, const float* base, int rstride) {
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      const int c = tid + nthreads * i;
+      const int key = 32 * jt + (c >> 4), quad = c & 15;
+      const bool ok = c < 512 && key < a.Lk;
+      pf[i] = ok ? *reinterpret_cast<const float4*>(base + (size_t)key * rstride + 4 * quad) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto store_k = [&](float* buf) {
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      const int c = tid + nthreads * i;
+      if (c >= 512) continue;
+      float* d = buf + (c >> 4) * AF_KP + 4 * (c & 15);  // 4-byte aligned rows
+      d[0] = pf[i].x;
+      d[1] = pf[i].y;
+      d[2] = pf[i].z;
+      d[3] = pf[i].w;
+    }
+  };
+  auto store_v = [&](float* buf) {
+#pragma unroll
+    for (int i = 0; i < PF; ++i) {
+      const int c = tid + nthreads * i;
+      if (c < 512) *reinterpret_cast<float4*>(buf + 32 * AF_KP + (c >> 4) * AF_VP + 4 * (c & 15)) = pf[i];
+    }
+  };
+  load_half(0, kbase, a.k_rstride);
+  store_k(sT);
+  load_half(0, vbase, a.v_rstride);
+  store_v(sT);
+  __syncthreads();
+
+  const int sg = at_sigma(n);
+  f32x16 o0 = {}, o1 = {};
+  float m = -INFINITY, l = 0.f;
+  for (int jt = 0; jt < nt; ++jt) {
+    float* buf = sT + (jt & 1) * AF_TILE;
+    float* nbuf = sT + ((jt + 1) & 1) * AF_TILE;  // read last in tile jt - 1
+    const bool more = jt + 1 < nt;
+    if (more) load_half(jt + 1, kbase, a.k_rstride);
+    // S^T tile: rows = keys, cols = queries
+    f32x16 s = {};
+    const float* kr = buf + n * AF_KP + 32 * h;
+#pragma unroll
+    for (int kk = 0; kk < 32; ++kk) s = __builtin_amdgcn_mfma_f32_32x32x2f32(kr[kk], qv[kk], s, 0, 0, 0);
+    if (more) {
+      store_k(nbuf);
+      load_half(jt + 1, vbase, a.v_rstride);
+    }
+    float mx = -INFINITY;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      const int key = 32 * jt + 8 * (j >> 2) + 4 * h + (j & 3);
+      if (key >= a.Lk) s[j] = -INFINITY;
+      mx = fmaxf(mx, s[j]);
+    }
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const float mn = fmaxf(m, mx);  // finite: every tile holds >= 1 key
+    const float alpha = exp2f(m - mn);
+    float ps = 0.f;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      s[j] = exp2f(s[j] - mn);
+      ps += s[j];
+    }
+    ps += __shfl_xor(ps, 32);
+    l = l * alpha + ps;
+    m = mn;
+#pragma unroll
+    for (int j = 0; j < 16; ++j) {
+      o0[j] *= alpha;
+      o1[j] *= alpha;
+    }
+    // O^T += V^T P^T: MFMA t takes key 8(t/4) + 4h + t%4 of this tile on half h
+    const float* vr = buf + 32 * AF_KP + sg;
+#pragma unroll
+    for (int t = 0; t < 16; ++t) {
+      const float* vk = vr + (8 * (t >> 2) + 4 * h + (t & 3)) * AF_VP;
+      o0 = __builtin_amdgcn_mfma_f32_32x32x2f32(vk[0], s[t], o0, 0, 0, 0);
+      o1 = __builtin_amdgcn_mfma_f32_32x32x2f32(vk[32], s[t], o1, 0, 0, 0);
+    }
+    if (more) store_v(nbuf);
+    __syncthreads();
+  }
+  if (qok) {
+    const float inv = 1.f / l;
+    float* op = a.o + ((size_t)b * a.Lq + qrow) * a.o_rstride + head * 64 + 16 * h;
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      *reinterpret_cast<float4*>(op + 4 * c) =
+          make_float4(o0[4 * c] * inv, o0[4 * c + 1] * inv, o0[4 * c + 2] * inv, o0[4 * c + 3] * inv);
+      *reinterpret_cast<float4*>(op + 32 + 4 * c) =
+          make_float4(o1[4 * c] * inv, o1[4 * c + 1] * inv, o1[4 * c + 2] * inv, o1[4 * c + 3] * inv);
+    }
+  }
+}
+
 }  // namespace
 }  // namespace rmbx
 
@@ -256,6 +416,45 @@ extern "C" int rmbx_attention_bf16(const void* q, const void* k, const void* v, 
   const int passes = (ngroups + rmbx::AT_MAX_WAVES - 1) / rmbx::AT_MAX_WAVES;
   const int waves = (ngroups + passes - 1) / passes;
   hipLaunchKernelGGL(rmbx::attn_fwd_kernel, dim3((unsigned)nblocks), dim3(64 * waves), 0, (hipStream_t)stream, a);
+  RMBX_CHECK_LAUNCH();
+  return RMBX_OK;
+}
+
+extern "C" int rmbx_attention_f32(const float* q, const float* k, const float* v, float* out, int B, int heads, int Lq,
+                                  int Lk, long long q_bstride, int q_rstride, long long k_bstride, int k_rstride,
+                                  long long v_bstride, int v_rstride, float scale, void* stream) {
+  RMBX_CHECK_ARG(q && k && v && out, "rmbx_attention_f32: null pointer");
+  RMBX_CHECK_ARG(B >= 0 && heads > 0 && Lq > 0 && Lk > 0, "rmbx_attention_f32: bad geometry");
+  RMBX_CHECK_ARG(scale > 0.f, "rmbx_attention_f32: scale must be positive");
+  RMBX_CHECK_ARG(q_rstride % 4 == 0 && k_rstride % 4 == 0 && v_rstride % 4 == 0 && q_bstride % 4 == 0 &&
+                     k_bstride % 4 == 0 && v_bstride % 4 == 0,
+                 "rmbx_attention_f32: strides must be multiples of 4 elements");
+  RMBX_CHECK_ARG((((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)out) & 15) == 0,
+                 "rmbx_attention_f32: pointers must be 16-byte aligned");
+  if (B == 0) return RMBX_OK;
+  rmbx::AttnF32Args a;
+  a.q = q;
+  a.k = k;
+  a.v = v;
+  a.o = out;
+  a.q_bstride = q_bstride;
+  a.k_bstride = k_bstride;
+  a.v_bstride = v_bstride;
+  a.q_rstride = q_rstride;
+  a.k_rstride = k_rstride;
+  a.v_rstride = v_rstride;
+  a.o_rstride = heads * 64;
+  a.heads = heads;
+  a.Lq = Lq;
+  a.Lk = Lk;
+  a.scale_log2 = scale * 1.4426950408889634f;
+  // 4 or 5 waves (one 32-query group each; >= 256 threads stage a key tile in 4 chunks each)
+  const int ngroups = (Lq + 31) / 32;
+  const int waves = ngroups >= rmbx::AF_MAX_WAVES ? rmbx::AF_MAX_WAVES : 4;
+  a.parts = (ngroups + waves - 1) / waves;
+  const long long nblocks = (long long)B * heads * a.parts;
+  RMBX_CHECK_ARG(nblocks < (1ll << 31), "rmbx_attention_f32: grid too large");
+  hipLaunchKernelGGL(rmbx::attn_fwd_f32_kernel, dim3((unsigned)nblocks), dim3(64 * waves), 0, (hipStream_t)stream, a);
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
 }

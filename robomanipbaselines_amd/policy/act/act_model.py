@@ -46,7 +46,7 @@ class MHA(nn.Module):
     """nn.MultiheadAttention-compatible parameters (in_proj_weight/bias, out_proj), batch-first
     compute through scaled_dot_product_attention."""
 
-    fused_attention = False  # device inference form: rmbx_attention_bf16 instead of SDPA
+    fused_attention = False  # device inference form: rmbx_attention_bf16 / _f32 instead of SDPA
 
     def __init__(self, d, heads):
         super().__init__()
@@ -89,6 +89,10 @@ class MHA(nn.Module):
             # rmbx_attention_bf16 reads the head slices of the projections in place and writes the
             # [B, Lq, D] layout out_proj consumes
             return self.out_proj(K.attention_bf16(qq, kk, vv, self.h))
+        if self.fused_attention and qq.dtype == torch.float32 and hd == 64 and qq.is_cuda:
+            from ... import kernels as K
+
+            return self.out_proj(K.attention_f32(qq, kk, vv, self.h))
         qq = qq.view(B, Lq, self.h, hd).transpose(1, 2)
         kk = kk.view(B, Lk, self.h, hd).transpose(1, 2)
         vv = vv.view(B, Lk, self.h, hd).transpose(1, 2)

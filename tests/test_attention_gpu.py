@@ -57,3 +57,34 @@ def test_attention_rejects_long_sequences():
     x = torch.zeros(1, 321, 64, device=DEV, dtype=torch.bfloat16)
     with pytest.raises(ValueError):
         K.attention_bf16(x, x, x, 1)
+
+
+@torch.no_grad()
+@pytest.mark.parametrize("B,H,Lq,Lk", [(3, 8, 302, 302), (4, 8, 100, 100), (2, 8, 100, 302), (1, 8, 1, 1),
+                                       (2, 2, 257, 33), (1, 1, 130, 650)])
+def test_attention_f32_matches_fp32(B, H, Lq, Lk):
+    """rmbx_attention_f32 (f32 MFMA, f32 online softmax) vs the fp32 reference: within f32
+    accumulation-order rounding (1e-5 of the output scale), ragged query groups and key tiles."""
+    from robomanipbaselines_amd import kernels as K
+
+    g = torch.Generator(device=DEV).manual_seed(Lq * 37 + Lk)
+    D = H * 64
+    q = torch.randn(B, Lq, D, device=DEV, generator=g) * 2
+    k = torch.randn(B, Lk, D, device=DEV, generator=g) * 2
+    v = torch.randn(B, Lk, D, device=DEV, generator=g).clamp(-4, 4)
+    got = K.attention_f32(q, k, v, H)
+    want = _ref(q, k, v, H)
+    torch.cuda.synchronize()
+    assert (got - want).abs().max().item() <= 1e-5 * 4
+
+
+@torch.no_grad()
+def test_attention_f32_strided_qkv_views():
+    from robomanipbaselines_amd import kernels as K
+
+    g = torch.Generator(device=DEV).manual_seed(11)
+    qkv = torch.randn(2, 150, 3 * 512, device=DEV, generator=g)
+    q, k, v = qkv.split(512, dim=-1)
+    got = K.attention_f32(q, k, v, 8)
+    want = _ref(q, k, v, 8)
+    assert (got - want).abs().max().item() <= 1e-5 * 4
