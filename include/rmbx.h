@@ -305,6 +305,16 @@ int rmbx_conv2d_nhwc(const void* in, const void* weight, const float* bias, cons
 int rmbx_conv2d_nhwc_f32(const float* in, const float* weight, const float* bias, const float* residual,
                          float* out, int N, int H, int W, int Cin, int Cout, int KH, int KW, int stride,
                          int pad, int relu, void* stream);
+/* Winograd F(2x2, 3x3) form of the fp32 stride-1 / pad-1 3x3 conv of the ResNet-18 BasicBlocks
+ * (Cin = Cout = C in {64, 128, 256, 512}; replaces the same conv -> FrozenBN -> (+ residual) ->
+ * ReLU steps as rmbx_conv2d_nhwc_f32, for every stride-1 layer of the fp32 policy trunk):
+ * in / residual / out [N][H][W][C] f32 (out must not alias in or residual), u_packed = the
+ * filter transform G g G^T of the BN-folded weights in the kernel's staging order
+ * [C/64][C/8][16][2][32][8] f32 (robomanipbaselines_amd.kernels.pack_winograd_f32), bias [C] f32.
+ * out = relu?(conv + bias + residual), f32 MFMA products, f32 accumulation. */
+int rmbx_conv3x3_winograd_f32(const float* in, const float* u_packed, const float* bias,
+                              const float* residual, float* out, int N, int H, int W, int C, int relu,
+                              void* stream);
 /* ResNet stem on a 2x2 space-to-depth image: in [N][Hs][Ws][16] bf16 (channel (dy*2+dx)*3+c,
  * 12..15 zero; rmbx_render policy_dtype 2 writes this layout), weight packed [Cout][4][4][16] bf16
  * (the 7x7 / stride-2 / pad-3 conv1 re-indexed), out [N][Hs][Ws][Cout] bf16 = relu?(conv + bias).

@@ -1,0 +1,350 @@
+// f32 3x3 / stride-1 / pad-1 convolution by Winograd F(2x2, 3x3) on f32 MFMA, with the
+// bias / residual / ReLU epilogue fused (NHWC, Cin = Cout = C in {64, 128, 256, 512}).
+//
+// Replaces the stride-1 conv -> FrozenBN -> (+ residual) -> ReLU steps of the ResNet-18
+// BasicBlocks in ACT's backbone (torchvision resnet18 inside third_party/act [absent]; the
+// reference runs the policy in fp32, RolloutAct.py / ACTPolicy) for the fp32 policy path.  gfx950
+// has no TF32, so f32 convs run on v_mfma_f32_32x32x2_f32 at the f32 vector rate (157 TF/s); the
+// direct algorithm needs 9 products per output per input channel, F(2x2, 3x3) needs 16 per 2x2
+// output tile = 4 per output (2.25x fewer MFMAs).  The transforms are additions and halvings
+// (B, A: 0 / +-1; G: 0 / +-1/2), so the result is the same convolution up to f32 rounding of a
+// few extra adds (measured against the direct fp32 conv in tests/test_winograd_gpu.py).
+//
+//   V = B^T d B  (4x4 input window d of a 2x2 output tile, per input channel)
+//   U = G g G^T  (per filter; packed once on the host in f64, rounded to f32)
+//   M[p] = sum_c U[p][co][c] V[p][c][tile]    p = 0..15: sixteen GEMMs with K = Cin
+//   Y = A^T M A  (2x2 outputs per tile)
+//
+// Mapping (MI355X: 256 CUs in 8 XCDs, 160 KiB LDS, 512 registers per lane at one wave per SIMD):
+//  * a block = 4 waves (one per SIMD) owns 64 output channels x 64 tiles; wave (cw, tw) keeps
+//    32 channels x 32 tiles for ALL 16 positions in 16 accumulators (256 registers), so the output
+//    transform runs in registers and each lane finishes 16 consecutive channels of one tile
+//    (A rows permuted in the packed U), leaving as 16-byte stores;
+//  * K runs in chunks of 8 input channels: U (32 KiB, pre-packed in the exact LDS image) and V
+//    (32 KiB, computed from the gathered 4x4 windows) are double-buffered in LDS (128 KiB); the
+//    next chunk's global loads are issued before this chunk's 64 MFMAs per wave and its LDS
+//    stores are spread over the second half of the MFMA stream, one LDS-only barrier per chunk;
+//  * persistent blocks, one per CU; the output-channel block is fixed per XCD (blockIdx % 8) so
+//    each XCD's L2 holds the U slice it streams (2 MiB at C = 512), and the chunk pipeline runs
+//    on across tile blocks (the next tile block's first chunk is staged under the last MFMAs of
+//    the current one).
+#include "rmbx_common.h"
+
+#include <cstdint>
+#include <cstdlib>
+
+namespace rmbx {
+namespace {
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+constexpr int WG_THREADS = 512;
+constexpr int WG_TILES = 64;                   // tiles per block unit
+constexpr int WG_COUT = 64;                    // output channels per block unit
+constexpr int WG_KC = 8;                       // input channels per K chunk
+constexpr int WG_PLANE = 64 * WG_KC;           // floats per position plane: [64 rows][8 channels]
+constexpr int WG_CHUNK = 16 * WG_PLANE;        // floats of one U or V chunk (32 KiB)
+static_assert(4 * WG_CHUNK * 4 <= 160 * 1024, "double-buffered U and V must fit the LDS of a CU");
+
+struct WinoArgs {
+  const float* in;    // [N][H][W][C]
+  const float* u;     // packed [C/64][C/8][16][64][8]
+  const float* bias;  // [C]
+  const float* res;   // [N][H][W][C] or null
+  float* out;         // [N][H][W][C]
+  int N, H, W, C, relu;
+  int tiles_x, tiles_y;
+  int ntiles;         // N * tiles_y * tiles_x (< 2^31, checked on the host)
+  int ntb;            // tile blocks of WG_TILES
+  int ncb, nk, nk_log2;  // C / 64, C / 8, log2(nk)
+  int dbg;            // diagnostic phase skips (RMBX_WINO_DBG: 1 = no MFMAs, 2 = no window loads,
+                      // 4 = no V transform / stores, 8 = no U loads; 0 in production)
+};
+
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+template <int DBG>
+__global__ void __launch_bounds__(WG_THREADS, 1) wino_f32_kernel(WinoArgs a) {
+  __shared__ __attribute__((aligned(16))) float smem[4 * WG_CHUNK];  // sU[2], sV[2]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cq = wave & 3, th = wave >> 2;  // MFMA work: channels 16 cq.. of the unit, tiles 32 th..
+  const int li = lane & 15, lq = lane >> 4;  // 16x16x4 operand lane: row / column li, k group lq
+  const bool loader = wave < 4;              // waves 0-3 gather and transform the windows, 4-7 move U
+
+  // persistent schedule: output-channel block cb fixed per XCD (blockIdx % 8)
+  const int G = gridDim.x;  // multiple of 8 (host)
+  const int xcd = blockIdx.x & 7;
+  const int cb = xcd % a.ncb;
+  const int per_cb = G / a.ncb;
+  const int r = (blockIdx.x >> 3) * (8 / a.ncb) + xcd / a.ncb;
+  if (r >= a.ntb) return;
+  const int nunits = (a.ntb - r + per_cb - 1) / per_cb;
+  const int nsteps = nunits << a.nk_log2;
+
+  // ---- loader state: this thread's 4x4 window of 2 channels (loader waves)
+  const int lt = (tid >> 2) & 63, cp = tid & 3;  // loader tile (0..63) and channel pair
+  float2 xreg[16];
+  uint32_t xok = 0;
+  int ld_unit = -1, ld_o0 = 0;  // loader tile window origin (element offset, may be < 0 at the top-left
+  uint32_t ld_mask = 0;         // halo; masked pixels read element 0) and in-image mask of ld_unit
+  auto tile_pos = [&](int t, int& img, int& ty, int& tx) {
+    const int q = t / a.tiles_x;
+    tx = t - q * a.tiles_x;
+    img = q / a.tiles_y;
+    ty = q - img * a.tiles_y;
+  };
+  // step s: U waves copy the chunk's U image global -> LDS buffer (s & 1) by LDS-DMA (the packed U
+  // is the exact LDS image: 8 KiB per wave as 8 lane-linear 1-KiB pieces); loader threads load
+  // their window into registers
+  auto load_u = [&](int s) {  // U waves
+    const int k = s & (a.nk - 1);
+    const float* ug = a.u + ((size_t)cb * a.nk + k) * WG_CHUNK + (wave - 4) * 2048 + lane * 4;
+    float* ul = smem + (s & 1) * WG_CHUNK + (wave - 4) * 2048;
+    if (!(DBG & 8))
+#pragma unroll
+      for (int j = 0; j < 8; ++j)
+        __builtin_amdgcn_global_load_lds(const_cast<float*>(ug + 256 * j), ul + 256 * j, 16, 0, 0);
+  };
+  auto load_window = [&](int s) {  // loader threads
+    const int unit = s >> a.nk_log2;
+    const int k = s & (a.nk - 1);
+    if (unit != ld_unit) {  // the loader tile's window origin and in-image mask, once per unit
+      ld_unit = unit;
+      const int t = (r + unit * per_cb) * WG_TILES + lt;
+      const bool tok = t < a.ntiles;
+      int img, ty, tx;
+      tile_pos(tok ? t : a.ntiles - 1, img, ty, tx);
+      const int y0 = 2 * ty - 1, x0 = 2 * tx - 1;
+      ld_o0 = ((img * a.H + y0) * a.W + x0) * a.C + 2 * cp;
+      ld_mask = 0;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int y = y0 + (i >> 2), x = x0 + (i & 3);
+        ld_mask |= (uint32_t)(tok && y >= 0 && y < a.H && x >= 0 && x < a.W) << i;
+      }
+    }
+    xok = ld_mask;
+    const int o = ld_o0 + k * WG_KC;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) {
+      const int off = ((ld_mask >> i) & 1u) ? o + ((i >> 2) * a.W + (i & 3)) * a.C : 0;
+      xreg[i] = *reinterpret_cast<const float2*>(a.in + off);
+    }
+  };
+  // ---- V = B^T d B of the loaded window into LDS buffer `buf` (loader threads), in 8 pieces
+  // (hook(q), q = 0..7): piece 0 masks the window and forms tmp = B^T d (all four rows); piece q
+  // writes V[q / 2][2 (q & 1) .. 2 (q & 1) + 1] = tmp row q / 2 times B
+  float2 tmp[4][4];
+  auto store_piece = [&](int buf, int q) {
+    if (q == 0) {
+#pragma unroll
+      for (int x = 0; x < 4; ++x) {
+        float2 d[4];
+#pragma unroll
+        for (int y = 0; y < 4; ++y) d[y] = ((xok >> (y * 4 + x)) & 1u) ? xreg[y * 4 + x] : make_float2(0.f, 0.f);
+        tmp[0][x] = make_float2(d[0].x - d[2].x, d[0].y - d[2].y);
+        tmp[1][x] = make_float2(d[1].x + d[2].x, d[1].y + d[2].y);
+        tmp[2][x] = make_float2(d[2].x - d[1].x, d[2].y - d[1].y);
+        tmp[3][x] = make_float2(d[1].x - d[3].x, d[1].y - d[3].y);
+      }
+    }
+    float* vb = smem + (2 + buf) * WG_CHUNK + lt * WG_KC + 2 * cp;
+    const int xi = q >> 1;
+    const float2* t = tmp[xi];
+    if ((q & 1) == 0) {
+      *reinterpret_cast<float2*>(vb + (xi * 4 + 0) * WG_PLANE) = make_float2(t[0].x - t[2].x, t[0].y - t[2].y);
+      *reinterpret_cast<float2*>(vb + (xi * 4 + 1) * WG_PLANE) = make_float2(t[1].x + t[2].x, t[1].y + t[2].y);
+    } else {
+      *reinterpret_cast<float2*>(vb + (xi * 4 + 2) * WG_PLANE) = make_float2(t[2].x - t[1].x, t[2].y - t[1].y);
+      *reinterpret_cast<float2*>(vb + (xi * 4 + 3) * WG_PLANE) = make_float2(t[1].x - t[3].x, t[1].y - t[3].y);
+    }
+  };
+
+  // accumulators: position p x tile group g (16 tiles) of 16 channels; lane (li, lq) holds
+  // channels 4 lq .. 4 lq + 3 of tile li
+  f32x4 acc[16][2];
+  // one K chunk: per position one A read and two B reads (float2 = the lane's 2 channels of the
+  // chunk: k group lq holds channels 2 lq, 2 lq + 1), 4 MFMAs; operands of position p + 1 are read
+  // while the MFMAs of position p run; loader threads store the next chunk's V over the second half
+  // chunk s: MFMAs on LDS buffer s & 1.  U waves: the LDS-DMA of U(s + 1) into the other buffer is
+  // issued first and retired (vmcnt(0)) before the closing barrier.  Loader waves: V(s + 1) is
+  // transformed from the window registers over the last quarter of the MFMA stream, then the window
+  // of step s + 2 is loaded; those loads stay in flight across the barrier (the loader waves'
+  // barrier waits on LDS only) and have a whole chunk to land.
+  auto chunk = [&](int s) {
+    const int buf = s & 1;
+    const bool more = s + 1 < nsteps;
+    if (!loader && more) load_u(s + 1);
+    const float* Ub = smem + buf * WG_CHUNK + (cq * 16 + li) * WG_KC + 2 * lq;
+    const float* Vb = smem + (2 + buf) * WG_CHUNK + (th * 32 + li) * WG_KC + 2 * lq;
+    float2 av = *reinterpret_cast<const float2*>(Ub);
+    float2 b0 = *reinterpret_cast<const float2*>(Vb);
+    float2 b1 = *reinterpret_cast<const float2*>(Vb + 16 * WG_KC);
+#pragma unroll
+    for (int p = 0; p < 16; ++p) {
+      float2 an = av, n0 = b0, n1 = b1;
+      if (p < 15) {
+        an = *reinterpret_cast<const float2*>(Ub + (p + 1) * WG_PLANE);
+        n0 = *reinterpret_cast<const float2*>(Vb + (p + 1) * WG_PLANE);
+        n1 = *reinterpret_cast<const float2*>(Vb + (p + 1) * WG_PLANE + 16 * WG_KC);
+      }
+      if (!(DBG & 1)) {
+        acc[p][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, b0.x, acc[p][0], 0, 0, 0);
+        acc[p][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.x, b1.x, acc[p][1], 0, 0, 0);
+        acc[p][0] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, b0.y, acc[p][0], 0, 0, 0);
+        acc[p][1] = __builtin_amdgcn_mfma_f32_16x16x4f32(av.y, b1.y, acc[p][1], 0, 0, 0);
+      } else {
+        acc[p][0][0] += av.x * b0.x + av.y * b1.y;
+      }
+      // the window loads were issued at the top of the chunk: their stores wait for the last
+      // quarter of the MFMA stream
+      if (loader && p >= 12 && more && !(DBG & 4)) {
+        store_piece(buf ^ 1, 2 * (p - 12));
+        store_piece(buf ^ 1, 2 * (p - 12) + 1);
+      }
+      av = an;
+      b0 = n0;
+      b1 = n1;
+    }
+    if (loader && s + 2 < nsteps && !(DBG & 2)) load_window(s + 2);
+    // U waves: the LDS-DMA of the next U chunk has landed; all: every wave is done with this buffer
+    if (!loader) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+  };
+
+  if (loader) {
+    load_window(0);
+#pragma unroll
+    for (int q = 0; q < 8; ++q) store_piece(0, q);
+    if (nsteps > 1) load_window(1);
+  } else {
+    load_u(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  lds_barrier();
+
+  int s = 0;
+  for (int unit = 0; unit < nunits; ++unit) {
+#pragma unroll
+    for (int p = 0; p < 16; ++p) acc[p][0] = acc[p][1] = f32x4{};
+    for (int k = 0; k < a.nk; ++k, ++s) chunk(s);
+
+    // Y = A^T M A per channel, + bias (+ residual), ReLU; per tile group: 4 pixels x 4 channels,
+    // one 16-byte store per pixel
+    const int co0 = cb * WG_COUT + cq * 16 + 4 * lq;
+    const float4 b4 = *reinterpret_cast<const float4*>(a.bias + co0);
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      const int t_out = (r + unit * per_cb) * WG_TILES + th * 32 + g * 16 + li;
+      const bool t_ok = t_out < a.ntiles;
+      int oimg, oty, otx;
+      tile_pos(t_ok ? t_out : a.ntiles - 1, oimg, oty, otx);
+      int off[4];
+      bool pok[4];
+      float4 rv[4];
+#pragma unroll
+      for (int px = 0; px < 4; ++px) {
+        const int y = 2 * oty + (px >> 1), x = 2 * otx + (px & 1);
+        pok[px] = t_ok && y < a.H && x < a.W;
+        off[px] = pok[px] ? ((oimg * a.H + y) * a.W + x) * a.C + co0 : 0;
+        if (a.res) rv[px] = *reinterpret_cast<const float4*>(a.res + off[px]);
+      }
+      float o[4][4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float t0[4], t1[4];
+#pragma unroll
+        for (int x = 0; x < 4; ++x) {
+          t0[x] = acc[x][g][e] + acc[4 + x][g][e] + acc[8 + x][g][e];
+          t1[x] = acc[4 + x][g][e] - acc[8 + x][g][e] - acc[12 + x][g][e];
+        }
+        const float bj = e == 0 ? b4.x : e == 1 ? b4.y : e == 2 ? b4.z : b4.w;
+        o[0][e] = t0[0] + t0[1] + t0[2] + bj;
+        o[1][e] = t0[1] - t0[2] - t0[3] + bj;
+        o[2][e] = t1[0] + t1[1] + t1[2] + bj;
+        o[3][e] = t1[1] - t1[2] - t1[3] + bj;
+      }
+#pragma unroll
+      for (int px = 0; px < 4; ++px) {
+        if (a.res) {
+          o[px][0] += rv[px].x;
+          o[px][1] += rv[px].y;
+          o[px][2] += rv[px].z;
+          o[px][3] += rv[px].w;
+        }
+        if (a.relu) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o[px][e] = o[px][e] > 0.f ? o[px][e] : (o[px][e] != o[px][e] ? o[px][e] : 0.f);
+        }
+        if (pok[px]) *reinterpret_cast<float4*>(a.out + off[px]) = make_float4(o[px][0], o[px][1], o[px][2], o[px][3]);
+      }
+    }
+  }
+}
+
+int device_cus() {
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+    return 256;
+  return cus > 0 ? cus : 256;
+}
+
+}  // namespace
+}  // namespace rmbx
+
+extern "C" int rmbx_conv3x3_winograd_f32(const float* in, const float* u_packed, const float* bias,
+                                         const float* residual, float* out, int N, int H, int W, int C,
+                                         int relu, void* stream) {
+  RMBX_CHECK_ARG(in && u_packed && bias && out, "rmbx_conv3x3_winograd_f32: null pointer");
+  RMBX_CHECK_ARG(N >= 0 && H > 0 && W > 0, "rmbx_conv3x3_winograd_f32: bad geometry");
+  RMBX_CHECK_ARG(C == 64 || C == 128 || C == 256 || C == 512,
+                 "rmbx_conv3x3_winograd_f32: C=%d (implemented: 64, 128, 256, 512)", C);
+  RMBX_CHECK_ARG((((uintptr_t)in | (uintptr_t)u_packed | (uintptr_t)out | (uintptr_t)residual) & 15) == 0,
+                 "rmbx_conv3x3_winograd_f32: tensors must be 16-byte aligned");
+  RMBX_CHECK_ARG(in != out && (residual == nullptr || residual != out),
+                 "rmbx_conv3x3_winograd_f32: the output must not alias the input or the residual");
+  if (N == 0) return RMBX_OK;
+  rmbx::WinoArgs a;
+  a.in = in;
+  a.u = u_packed;
+  a.bias = bias;
+  a.res = residual;
+  a.out = out;
+  a.N = N;
+  a.H = H;
+  a.W = W;
+  a.C = C;
+  a.relu = relu;
+  a.tiles_x = (W + 1) / 2;
+  a.tiles_y = (H + 1) / 2;
+  const long long ntiles = (long long)N * a.tiles_x * a.tiles_y;
+  RMBX_CHECK_ARG(ntiles + rmbx::WG_TILES < (1ll << 31) && (long long)N * H * W * C < (1ll << 31),
+                 "rmbx_conv3x3_winograd_f32: tensor too large for 32-bit element offsets");
+  a.ntiles = (int)ntiles;
+  a.ntb = (a.ntiles + rmbx::WG_TILES - 1) / rmbx::WG_TILES;
+  a.ncb = C / rmbx::WG_COUT;
+  a.nk = C / rmbx::WG_KC;
+  const char* dbg_env = std::getenv("RMBX_WINO_DBG");
+  a.dbg = dbg_env ? std::atoi(dbg_env) : 0;
+  a.nk_log2 = 0;
+  while ((1 << a.nk_log2) < a.nk) ++a.nk_log2;
+  // one persistent block per CU (grid a multiple of 8: blockIdx % 8 is the XCD under round-robin
+  // dispatch); blocks beyond the work exit at once
+  int grid = rmbx::device_cus();
+  grid = grid < 8 ? 8 : grid - grid % 8;
+  const dim3 g(grid), blk(rmbx::WG_THREADS);
+  hipStream_t st = (hipStream_t)stream;
+  switch (a.dbg) {
+    case 0: hipLaunchKernelGGL(rmbx::wino_f32_kernel<0>, g, blk, 0, st, a); break;
+    case 1: hipLaunchKernelGGL(rmbx::wino_f32_kernel<1>, g, blk, 0, st, a); break;
+    case 2: hipLaunchKernelGGL(rmbx::wino_f32_kernel<2>, g, blk, 0, st, a); break;
+    case 4: hipLaunchKernelGGL(rmbx::wino_f32_kernel<4>, g, blk, 0, st, a); break;
+    case 6: hipLaunchKernelGGL(rmbx::wino_f32_kernel<6>, g, blk, 0, st, a); break;
+    case 8: hipLaunchKernelGGL(rmbx::wino_f32_kernel<8>, g, blk, 0, st, a); break;
+    case 14: hipLaunchKernelGGL(rmbx::wino_f32_kernel<14>, g, blk, 0, st, a); break;
+    case 15: hipLaunchKernelGGL(rmbx::wino_f32_kernel<15>, g, blk, 0, st, a); break;
+    default: RMBX_CHECK_ARG(false, "rmbx_conv3x3_winograd_f32: RMBX_WINO_DBG=%d not instantiated", a.dbg);
+  }
+  RMBX_CHECK_LAUNCH();
+  return RMBX_OK;
+}

@@ -483,6 +483,43 @@ def conv2d_nhwc_f32_supported(cin, cout, kernel_size, stride, padding):
     return (cin, cout, tuple(kernel_size), stride, padding) == (64, 64, (3, 3), 1, 1)
 
 
+_WINO_G = ((1.0, 0.0, 0.0), (0.5, 0.5, 0.5), (0.5, -0.5, 0.5), (0.0, 0.0, 1.0))
+WINOGRAD_F32_CHANNELS = (64, 128, 256, 512)
+
+
+def pack_winograd_f32(weight):
+    """3x3 conv weight [C, C, 3, 3] -> the Winograd F(2x2, 3x3) filter transform U = G g G^T
+    (computed in f64, rounded once to f32) in the LDS image rmbx_conv3x3_winograd_f32 stages per
+    K chunk: [C/64 channel blocks][C/8 chunks][16 positions][64 output channels][8 input channels]."""
+    C = weight.shape[0]
+    if tuple(weight.shape) != (C, C, 3, 3) or C not in WINOGRAD_F32_CHANNELS:
+        raise ValueError(f"pack_winograd_f32: weight {tuple(weight.shape)} is not [C, C, 3, 3] with C in {WINOGRAD_F32_CHANNELS}")
+    w = weight.detach().to(torch.float64)
+    G = torch.tensor(_WINO_G, dtype=torch.float64, device=w.device)
+    U = torch.einsum("xa,oiab,yb->xyoi", G, w, G).reshape(16, C // 64, 64, C // 8, 8)  # [p][cb][co][k][c]
+    return U.permute(1, 3, 0, 2, 4).contiguous().to(torch.float32)
+
+
+def conv3x3_winograd_f32(x, u_packed, bias, relu=False, res=None):
+    """relu?(conv2d(x, w, stride 1, pad 1) + bias + res) by rmbx_conv3x3_winograd_f32 (Winograd
+    F(2x2, 3x3) on f32 MFMA): x channels_last f32 [N, C, H, W], u_packed = pack_winograd_f32(w),
+    bias f32 [C], res channels_last [N, C, H, W] or None -> channels_last [N, C, H, W]."""
+    _chk_nhwc(x, "x")
+    n, C, H, W = x.shape
+    if x.dtype != torch.float32 or C not in WINOGRAD_F32_CHANNELS:
+        raise ValueError(f"conv3x3_winograd_f32: x must be f32 with C in {WINOGRAD_F32_CHANNELS}")
+    _chk(u_packed, torch.float32, (C // 64, C // 8, 16, 64, 8), "u_packed")
+    _chk(bias, torch.float32, (C,), "bias")
+    if res is not None:
+        _chk_nhwc(res, "res")
+        if tuple(res.shape) != tuple(x.shape) or res.dtype != torch.float32:
+            raise ValueError("res must match the output")
+    out = torch.empty_like(x, memory_format=torch.channels_last)
+    N.call("rmbx_conv3x3_winograd_f32", N.ptr(x), N.ptr(u_packed), N.ptr(bias), N.ptr(res), N.ptr(out),
+           n, H, W, C, int(bool(relu)), N.stream_ptr())
+    return out
+
+
 def pack_stem_s2d(weight):
     """conv1 weight [Cout, 3, 7, 7] -> [Cout, 4, 4, 16] for rmbx_stem_s2d_conv:
     W'[co][ky][kx][(dy*2+dx)*3+c] = W[co][c][2ky+dy-1][2kx+dx-1] (0 outside the 7x7 window)."""

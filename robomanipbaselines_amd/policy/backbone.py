@@ -5,6 +5,8 @@ restated; parameter names follow torchvision's (conv1, bn1, layer1.0.conv1, ...)
 state_dict maps onto it.  `fuse()` folds each frozen BN into its conv for the MIOpen/MFMA
 inference path (channels_last, bf16); the unfused module is the fp32 reference."""
 
+import os
+
 import torch
 import torch.nn as nn
 import torch.nn.functional as F
@@ -116,6 +118,22 @@ class _FusedConv(nn.Module):
         c = self.conv
         return K.conv2d_nhwc_f32_supported(c.in_channels, c.out_channels, c.kernel_size, c.stride[0], c.padding[0])
 
+    def wino_ok(self):
+        c = self.conv
+        return (c.in_channels == c.out_channels and c.in_channels in K.WINOGRAD_F32_CHANNELS
+                and tuple(c.kernel_size) == (3, 3) and c.stride[0] == 1 and c.padding[0] == 1)
+
+    def wino(self, x, relu, res=None, bias=None):
+        """f32 conv + bias (+ res) (+ ReLU) in one rmbx Winograd F(2x2, 3x3) launch; the packed
+        filter transform is cached per weight storage."""
+        w = self.conv.weight
+        key = (w.data_ptr(), w.dtype, w.device)
+        cache = self.__dict__.get("_wino")
+        if cache is None or cache[0] != key:
+            cache = (key, K.pack_winograd_f32(w))
+            self.__dict__["_wino"] = cache
+        return K.conv3x3_winograd_f32(x, cache[1], self.bias_f32() if bias is None else bias, relu=relu, res=res)
+
 
 class _FusedBlock(nn.Module):
     def __init__(self, blk):
@@ -130,7 +148,30 @@ class _FusedBlock(nn.Module):
     # layers
     RMBX_CONV_MAX_COUT = 128
 
+    # fp32 stride-1 3x3 convs: "winograd" (rmbx_conv3x3_winograd_f32, every layer) or "direct"
+    # (layer 1 on rmbx_conv2d_nhwc_f32, layers 2-4 MIOpen + epilogue pass); env RMBX_F32_CONV
+    F32_CONV = os.environ.get("RMBX_F32_CONV", "winograd")
+
+    def _bias_sum(self):
+        """c2's bias + the downsample's (the residual's bias folded into c2's epilogue), cached."""
+        key = (self.c2.bias_f32().data_ptr(), self.down.bias_f32().data_ptr())
+        cache = self.__dict__.get("_bsum")
+        if cache is None or cache[0] != key:
+            cache = (key, (self.c2.bias_f32() + self.down.bias_f32()).contiguous())
+            self.__dict__["_bsum"] = cache
+        return cache[1]
+
     def forward(self, x):
+        if x.dtype == torch.float32 and self.F32_CONV == "winograd" and self.c2.wino_ok():
+            if self.down is None and self.c1.wino_ok():
+                y = self.c1.wino(x, relu=True)
+                return self.c2.wino(y, relu=True, res=x)
+            if self.down is not None:
+                # stride-2 c1 and the 1x1 downsample stay MIOpen convs; c2 (stride 1) adds the
+                # downsample branch and both biases in its epilogue
+                y = self.c1(x)
+                d = self.down.conv_nobias(x)
+                return self.c2.wino(y, relu=True, res=d, bias=self._bias_sum())
         if x.dtype == torch.bfloat16 and self.c2.conv.out_channels <= self.RMBX_CONV_MAX_COUT:
             y = self.c1.rmbx(x, relu=True)
             idt = x if self.down is None else self.down.rmbx(x, relu=False)
