@@ -193,8 +193,9 @@ class FusedResNet18Trunk(nn.Module):
     """Inference form on the device: BN folded into conv weights/bias, channels_last
     activations.  bf16: the block convs are rmbx MFMA implicit-GEMM kernels with bias / residual /
     ReLU fused (rmbx_conv2d_nhwc); the 3-channel 7x7 stem is MIOpen + the rmbx bias/ReLU/max-pool
-    epilogue.  f32: layer 1 on rmbx_conv2d_nhwc_f32 (epilogue fused), layers 2-4 MIOpen convs +
-    one rmbx HIP epilogue per conv.  Same function as ResNet18Trunk; bit-identical to the unfused storage-dtype
+    epilogue.  f32: every stride-1 3x3 conv on rmbx_conv3x3_winograd_f32 (Winograd F(2x2, 3x3), epilogue
+    fused; RMBX_F32_CONV=direct restores layer 1 on rmbx_conv2d_nhwc_f32), the stride-2 and 1x1
+    convs MIOpen + one rmbx HIP epilogue per conv.  Same function as ResNet18Trunk; bit-identical to the unfused storage-dtype
     sequence on the same conv outputs (tests/test_nn_gpu.py)."""
 
     def __init__(self, trunk):

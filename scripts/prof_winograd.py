@@ -34,7 +34,11 @@ with torch.no_grad():
     torch.backends.cudnn.benchmark = True
     torch.backends.cudnn.allow_tf32 = False
     cl = torch.channels_last
-    for C, H, W in ((64, 120, 160), (128, 60, 80), (256, 30, 40), (512, 15, 20)):
+    shapes = ((64, 120, 160), (128, 60, 80), (256, 30, 40), (512, 15, 20))
+    only = os.environ.get("WINO_C")
+    for C, H, W in shapes:
+        if only and str(C) not in only.split(","):
+            continue
         x = torch.randn(B, C, H, W, device=dev).contiguous(memory_format=cl)
         r = torch.randn(B, C, H, W, device=dev).contiguous(memory_format=cl)
         w = (torch.randn(C, C, 3, 3, device=dev) / (9 * C) ** 0.5).contiguous(memory_format=cl)
@@ -56,7 +60,7 @@ with torch.no_grad():
                                      res=r[:8].contiguous(memory_format=cl))
         err = (got - ref).abs().max().item() / max(1.0, ref.abs().max().item())
         dbg = {}
-        for d in ("2", "4", "6", "15"):  # phase skips (RMBX_WINO_DBG bits)
+        for d in os.environ.get("WINO_DBGS", "2,4,6,15").split(","):  # phase skips (RMBX_WINO_DBG bits)
             os.environ["RMBX_WINO_DBG"] = d
             dbg["dbg" + d] = round(timed(lambda: K.conv3x3_winograd_f32(x, u, b, relu=True, res=r)), 3)
         os.environ.pop("RMBX_WINO_DBG")
