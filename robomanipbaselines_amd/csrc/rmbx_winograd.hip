@@ -63,6 +63,20 @@ struct WinoArgs {
 
 __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
+// LDS-DMA of 16 bytes per lane (global_load_lds_dwordx4: the wave's 64 x 16 B land contiguously at
+// the wave-uniform LDS byte address lds_dst).  Issued from inline asm so that hipcc does not insert
+// its conservative vmcnt(0) before the next LDS read -- which would also make the loader waves wait
+// for their in-flight window loads at the top of every chunk; completion is counted by hand
+// (s_waitcnt vmcnt(0) of the U waves) before the barrier that publishes the chunk.
+__device__ __forceinline__ void glds16(const float* gsrc, const float* lds_dst) {
+  const uint32_t dst = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) float*)lds_dst;
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(dst))
+               : "memory");
+}
+
 template <int DBG>
 __global__ void __launch_bounds__(WG_THREADS, 1) wino_f32_kernel(WinoArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[4 * WG_CHUNK];  // sU[2], sV[2]
@@ -103,7 +117,7 @@ __global__ void __launch_bounds__(WG_THREADS, 1) wino_f32_kernel(WinoArgs a) {
     if (!(DBG & 8))
 #pragma unroll
       for (int j = 0; j < 8; ++j)
-        __builtin_amdgcn_global_load_lds(const_cast<float*>(ug + 256 * j), ul + 256 * j, 16, 0, 0);
+        glds16(ug + 256 * j, ul + 256 * j);
   };
   auto load_window = [&](int s) {  // loader threads
     const int unit = s >> a.nk_log2;
