@@ -60,6 +60,11 @@ with torch.no_grad():
                                      res=r[:8].contiguous(memory_format=cl))
         err = (got - ref).abs().max().item() / max(1.0, ref.abs().max().item())
         dbg = {}
+        for stg in os.environ.get("WINO_STAGGERS", "").split(","):
+            if stg:
+                os.environ["RMBX_WINO_STAGGER"] = stg
+                dbg["stagger" + stg] = round(timed(lambda: K.conv3x3_winograd_f32(x, u, b, relu=True, res=r)), 3)
+        os.environ.pop("RMBX_WINO_STAGGER", None)
         for d in os.environ.get("WINO_DBGS", "2,4,6,15").split(","):  # phase skips (RMBX_WINO_DBG bits)
             os.environ["RMBX_WINO_DBG"] = d
             dbg["dbg" + d] = round(timed(lambda: K.conv3x3_winograd_f32(x, u, b, relu=True, res=r)), 3)
