@@ -244,6 +244,7 @@ struct AttnF32Args {
   float scale_log2;
 };
 
+template <int DBG>
 __global__ void __launch_bounds__(64 * AF_MAX_WAVES) __attribute__((amdgpu_waves_per_eu(4))) attn_fwd_f32_kernel(AttnF32Args a) {
   __shared__ __attribute__((aligned(16))) float sT[2 * AF_TILE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -316,23 +317,32 @@ __global__ void __launch_bounds__(64 * AF_MAX_WAVES) __attribute__((amdgpu_waves
     float* buf = sT + (jt & 1) * AF_TILE;
     float* nbuf = sT + ((jt + 1) & 1) * AF_TILE;  // read last in tile jt - 1
     const bool more = jt + 1 < nt;
-    if (more) load_half(jt + 1, kbase, a.k_rstride);
+    if (more && !(DBG & 8)) load_half(jt + 1, kbase, a.k_rstride);
     // S^T tile: rows = keys, cols = queries
     f32x16 s = {};
     const float* kr = buf + n * AF_KP + 32 * h;
+    if (!(DBG & 1)) {
 #pragma unroll
-    for (int kk = 0; kk < 32; ++kk) s = __builtin_amdgcn_mfma_f32_32x32x2f32(kr[kk], qv[kk], s, 0, 0, 0);
-    if (more) {
+      for (int kk = 0; kk < 32; ++kk) s = __builtin_amdgcn_mfma_f32_32x32x2f32(kr[kk], qv[kk], s, 0, 0, 0);
+    } else {
+#pragma unroll
+      for (int j = 0; j < 16; ++j) s[j] = kr[j] * qv[j];
+    }
+    if (more && !(DBG & 8)) {
       store_k(nbuf);
       load_half(jt + 1, vbase, a.v_rstride);
     }
+    if (!(DBG & 2)) {
     float mx = -INFINITY;
+    if (32 * jt + 32 > a.Lk) {  // the ragged last tile only (uniform branch)
 #pragma unroll
-    for (int j = 0; j < 16; ++j) {
-      const int key = 32 * jt + 8 * (j >> 2) + 4 * h + (j & 3);
-      if (key >= a.Lk) s[j] = -INFINITY;
-      mx = fmaxf(mx, s[j]);
+      for (int j = 0; j < 16; ++j) {
+        const int key = 32 * jt + 8 * (j >> 2) + 4 * h + (j & 3);
+        if (key >= a.Lk) s[j] = -INFINITY;
+      }
     }
+#pragma unroll
+    for (int j = 0; j < 16; ++j) mx = fmaxf(mx, s[j]);
     mx = fmaxf(mx, __shfl_xor(mx, 32));
     const float mn = fmaxf(m, mx);  // finite: every tile holds >= 1 key
     const float alpha = exp2f(m - mn);
@@ -350,15 +360,23 @@ __global__ void __launch_bounds__(64 * AF_MAX_WAVES) __attribute__((amdgpu_waves
       o0[j] *= alpha;
       o1[j] *= alpha;
     }
+    } else {
+      l += s[0];
+    }
     // O^T += V^T P^T: MFMA t takes key 8(t/4) + 4h + t%4 of this tile on half h
     const float* vr = buf + 32 * AF_KP + sg;
+    if (!(DBG & 4)) {
 #pragma unroll
-    for (int t = 0; t < 16; ++t) {
-      const float* vk = vr + (8 * (t >> 2) + 4 * h + (t & 3)) * AF_VP;
-      o0 = __builtin_amdgcn_mfma_f32_32x32x2f32(vk[0], s[t], o0, 0, 0, 0);
-      o1 = __builtin_amdgcn_mfma_f32_32x32x2f32(vk[32], s[t], o1, 0, 0, 0);
+      for (int t = 0; t < 16; ++t) {
+        const float* vk = vr + (8 * (t >> 2) + 4 * h + (t & 3)) * AF_VP;
+        o0 = __builtin_amdgcn_mfma_f32_32x32x2f32(vk[0], s[t], o0, 0, 0, 0);
+        o1 = __builtin_amdgcn_mfma_f32_32x32x2f32(vk[32], s[t], o1, 0, 0, 0);
+      }
+    } else {
+#pragma unroll
+      for (int t = 0; t < 16; ++t) o0[t] += vr[t] * s[t];
     }
-    if (more) store_v(nbuf);
+    if (more && !(DBG & 8)) store_v(nbuf);
     __syncthreads();
   }
   if (qok) {
@@ -454,7 +472,19 @@ extern "C" int rmbx_attention_f32(const float* q, const float* k, const float* v
   a.parts = (ngroups + waves - 1) / waves;
   const long long nblocks = (long long)B * heads * a.parts;
   RMBX_CHECK_ARG(nblocks < (1ll << 31), "rmbx_attention_f32: grid too large");
-  hipLaunchKernelGGL(rmbx::attn_fwd_f32_kernel, dim3((unsigned)nblocks), dim3(64 * waves), 0, (hipStream_t)stream, a);
+  const char* dbg_env = std::getenv("RMBX_ATTN_F32_DBG");
+  const int dbg = dbg_env ? std::atoi(dbg_env) : 0;
+  const dim3 g((unsigned)nblocks), blk(64 * waves);
+  switch (dbg) {  // diagnostic phase skips: 1 = no S MFMAs, 2 = no softmax, 4 = no PV MFMAs, 8 = no tile loads
+    case 0: hipLaunchKernelGGL(rmbx::attn_fwd_f32_kernel<0>, g, blk, 0, (hipStream_t)stream, a); break;
+    case 1: hipLaunchKernelGGL(rmbx::attn_fwd_f32_kernel<1>, g, blk, 0, (hipStream_t)stream, a); break;
+    case 2: hipLaunchKernelGGL(rmbx::attn_fwd_f32_kernel<2>, g, blk, 0, (hipStream_t)stream, a); break;
+    case 4: hipLaunchKernelGGL(rmbx::attn_fwd_f32_kernel<4>, g, blk, 0, (hipStream_t)stream, a); break;
+    case 8: hipLaunchKernelGGL(rmbx::attn_fwd_f32_kernel<8>, g, blk, 0, (hipStream_t)stream, a); break;
+    case 5: hipLaunchKernelGGL(rmbx::attn_fwd_f32_kernel<5>, g, blk, 0, (hipStream_t)stream, a); break;
+    case 10: hipLaunchKernelGGL(rmbx::attn_fwd_f32_kernel<10>, g, blk, 0, (hipStream_t)stream, a); break;
+    default: RMBX_CHECK_ARG(false, "rmbx_attention_f32: RMBX_ATTN_F32_DBG=%d not instantiated", dbg);
+  }
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
 }

@@ -43,6 +43,12 @@ with torch.no_grad():
             return F.scaled_dot_product_attention(qh, kh, vh)
 
         ms_t = timed(sdpa)
-        out[name] = {"rmbx_ms": round(ms_r, 3), "rmbx_tflops": round(flop / ms_r / 1e9, 1),
+        dbg = {}
+        for d in os.environ.get("ATTN_DBGS", "").split(","):
+            if d:
+                os.environ["RMBX_ATTN_F32_DBG"] = d
+                dbg["dbg" + d] = round(timed(lambda: K.attention_f32(q, k, v, 8)), 3)
+        os.environ.pop("RMBX_ATTN_F32_DBG", None)
+        out[name] = {"rmbx_ms": round(ms_r, 3), **dbg, "rmbx_tflops": round(flop / ms_r / 1e9, 1),
                      "rmbx_frac_of_157": round(flop / ms_r / 1e9 / 157.3, 3), "sdpa_ms": round(ms_t, 3)}
     print(json.dumps(out), flush=True)
