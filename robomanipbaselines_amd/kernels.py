@@ -485,6 +485,7 @@ def conv2d_nhwc_f32_supported(cin, cout, kernel_size, stride, padding):
 
 _WINO_G = ((1.0, 0.0, 0.0), (0.5, 0.5, 0.5), (0.5, -0.5, 0.5), (0.0, 0.0, 1.0))
 WINOGRAD_F32_CHANNELS = (64, 128, 256, 512)
+WINOGRAD_MAX_ELEMS = (1 << 31) - 1  # per launch (32-bit element offsets in the kernel)
 
 
 def pack_winograd_f32(weight):
@@ -515,8 +516,14 @@ def conv3x3_winograd_f32(x, u_packed, bias, relu=False, res=None):
         if tuple(res.shape) != tuple(x.shape) or res.dtype != torch.float32:
             raise ValueError("res must match the output")
     out = torch.empty_like(x, memory_format=torch.channels_last)
-    N.call("rmbx_conv3x3_winograd_f32", N.ptr(x), N.ptr(u_packed), N.ptr(bias), N.ptr(res), N.ptr(out),
-           n, H, W, C, int(bool(relu)), N.stream_ptr())
+    # the kernel indexes with 32-bit element offsets: larger batches run as slices of whole images
+    per = max(1, WINOGRAD_MAX_ELEMS // (H * W * C))
+    for i0 in range(0, n, per):
+        i1 = min(n, i0 + per)
+        xs, os_ = x[i0:i1], out[i0:i1]
+        rs = None if res is None else res[i0:i1]
+        N.call("rmbx_conv3x3_winograd_f32", N.ptr(xs), N.ptr(u_packed), N.ptr(bias), N.ptr(rs), N.ptr(os_),
+               i1 - i0, H, W, C, int(bool(relu)), N.stream_ptr())
     return out
 
 

@@ -28,8 +28,15 @@ def timeit(fn, iters=5):
     return a.elapsed_time(b) / iters
 
 
+s2d32 = torch.empty((n, H // 2, W // 2, 16), dtype=torch.float32, device="cuda:0")
 res = {"n_env": n, "policy_s2d_ms": timeit(lambda: env.render_images("front", policy=s2d)),
+       "policy_s2d_f32_ms": timeit(lambda: env.render_images("front", policy=s2d32)),
        "rgb_ms": timeit(lambda: env.render_images("front", rgb=rgb))}
+for d in os.environ.get("RENDER_DBGS", "").split(","):  # phase skips (RMBX_RENDER_DBG bits)
+    if d:
+        os.environ["RMBX_RENDER_DBG"] = d
+        res["f32_dbg" + d] = timeit(lambda: env.render_images("front", policy=s2d32))
+os.environ.pop("RMBX_RENDER_DBG", None)
 img = rgb.float().mean().item()
 res["rgb_mean"] = img
 print(json.dumps(res), flush=True)

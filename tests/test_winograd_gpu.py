@@ -78,3 +78,15 @@ def test_winograd_rejects_bad_arguments():
     with pytest.raises(ValueError):  # packed filter of another width
         K.conv3x3_winograd_f32(x, K.pack_winograd_f32(torch.randn(128, 128, 3, 3, device=DEV)),
                                torch.zeros(64, device=DEV))
+
+
+@torch.no_grad()
+def test_winograd_batch_slices_equal_one_launch(monkeypatch):
+    """Batches beyond the kernel's 32-bit offsets run as slices of whole images: same output."""
+    from robomanipbaselines_amd import kernels as K
+
+    x, w, b, r = _case(5, 64, 12, 10, seed=3)
+    whole = _run(x, w, b, r, relu=True)
+    monkeypatch.setattr(K, "WINOGRAD_MAX_ELEMS", 2 * 12 * 10 * 64)  # two images per launch
+    sliced = _run(x, w, b, r, relu=True)
+    assert torch.equal(whole, sliced)
