@@ -208,9 +208,9 @@ struct RenderArgs {
 
 __global__ void __launch_bounds__(256) render_kernel(RenderArgs a) {
   __shared__ PrimCam prims[MAX_PRIM];
-  __shared__ int tile_list[MAX_PRIM];
-  __shared__ int tile_sorted[MAX_PRIM];
-  __shared__ int tile_count;
+  __shared__ int order[MAX_PRIM];        // the block's primitives sorted front to back, once
+  __shared__ int tile_sorted[MAX_PRIM];  // the tile's survivors in that order
+  __shared__ int wcount[4];
   __shared__ CamFrame cf;
   const int ntiles = a.tiles_x * a.tiles_y;
   const int env = blockIdx.x / a.groups;
@@ -300,23 +300,37 @@ __global__ void __launch_bounds__(256) render_kernel(RenderArgs a) {
     }
     prims[p] = P;
   }
+  __syncthreads();
+  // order the primitives front to back by the depth bound (ties by index) once per block: a tile
+  // keeps this order for its survivors, and a ray stops at the first primitive whose bound lies
+  // behind its nearest hit so far
+  for (int p = tid; p < np; p += blockDim.x) {
+    const float z = prims[p].zmin;
+    int rank = 0;
+    for (int j = 0; j < np; j++) {
+      const float zq = prims[j].zmin;
+      rank += (zq < z) || (zq == z && j < p);
+    }
+    order[rank] = p;
+  }
   const int t_begin = (int)((long long)ntiles * grp / a.groups);
   const int t_end = (int)((long long)ntiles * (grp + 1) / a.groups);
   for (int tile = t_begin; tile < t_end; ++tile) {
-  if (tid == 0) tile_count = 0;
-  __syncthreads();
+  __syncthreads();  // the previous tile's rays are done with tile_sorted (and order is complete)
   const int tx0 = (tile % a.tiles_x) * RENDER_TILE, ty0 = (tile / a.tiles_x) * RENDER_TILE;
   // tile frustum in normalised image coords
   const float x_lo = (2.0f * tx0 / W - 1.0f) * tanh_ * aspect;
   const float x_hi = (2.0f * (tx0 + RENDER_TILE) / W - 1.0f) * tanh_ * aspect;
   const float y_hi = (1.0f - 2.0f * ty0 / H) * tanh_;
   const float y_lo = (1.0f - 2.0f * (ty0 + RENDER_TILE) / H) * tanh_;
-  for (int p = tid; p < np; p += blockDim.x) {
-    const PrimCam& P = prims[p];
+  bool keep = false;
+  const int p_cull = tid < np ? order[tid] : 0;  // np <= MAX_PRIM <= blockDim.x: one primitive per thread
+  if (tid < np) {
+    const PrimCam& P = prims[p_cull];
     const int type = P.type;
     const float rad = P.rad;
     // conservative tile test: sphere vs the 4 tile planes (camera looks along -z)
-    bool keep = true;
+    keep = true;
     if (type != RMBX_GEOM_PLANE && rad > 0) {
       const float z = -P.c[2];
       if (z + rad <= 1e-3f) keep = false;  // behind the camera
@@ -330,28 +344,15 @@ __global__ void __launch_bounds__(256) render_kernel(RenderArgs a) {
         if ((y_hi * z - P.c[1]) * ny_hi < -rad) keep = false;
       }
     }
-    if (keep) {
-      const int slot = atomicAdd(&tile_count, 1);
-      tile_list[slot] = p;
-    }
   }
+  // compact the survivors in sorted order: ballot per wave, wave offsets through LDS
+  const unsigned long long kb = __ballot(keep);
+  if ((tid & 63) == 0) wcount[tid >> 6] = __popcll(kb);
   __syncthreads();
-  // order the tile's primitives front to back by the depth bound (ties by prim index): a ray can
-  // stop at the first primitive whose bound lies behind its nearest hit so far
-  {
-    const int cnt = tile_count;
-    if (tid < cnt) {
-      const int p = tile_list[tid];
-      const float z = prims[p].zmin;
-      int rank = 0;
-      for (int j = 0; j < cnt; j++) {
-        const int q = tile_list[j];
-        const float zq = prims[q].zmin;
-        rank += (zq < z) || (zq == z && q < p);
-      }
-      tile_sorted[rank] = p;
-    }
-  }
+  int base = 0;
+  for (int w = 0; w < (tid >> 6); ++w) base += wcount[w];
+  if (keep) tile_sorted[base + __popcll(kb & ((1ull << (tid & 63)) - 1))] = p_cull;
+  const int tile_cnt = wcount[0] + wcount[1] + wcount[2] + wcount[3];
   __syncthreads();
   const int px = tx0 + (tid % RENDER_TILE), py = ty0 + (tid / RENDER_TILE);
   if (px < W && py < H) {
@@ -359,7 +360,7 @@ __global__ void __launch_bounds__(256) render_kernel(RenderArgs a) {
                       (1.0f - 2.0f * (py + 0.5f) / H) * tanh_, -1.0f};
   float best = 1e30f, bn[3] = {0, 0, 1};
   int bp = -1;
-  const int cnt = tile_count;
+  const int cnt = tile_cnt;
   int ntest = 0;
   for (int k = 0; k < ((a.dbg & 1) ? 0 : cnt); k++) {
     const int p = tile_sorted[k];
