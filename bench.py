@@ -15,7 +15,8 @@ K timed env-steps of the RolloutPhase hot loop: render + ACT every `skip` = 3 st
 ensemble, command routing, 8 physics substeps, observation, success predicate and phase
 bookkeeping, all on the device.  One `step` = one env-step of every env.  The ACT decoder runs
 layer 0 only: the DETRVAE output reads that layer's normed intermediate, layers 1..6 are dead
-(exact; tests/test_act_full_gpu.py; --act_full_decoder runs all seven).
+(exact; tests/test_act_full_gpu.py; --act_full_decoder runs all seven); the JSON line also prices
+the step with all seven computed (`all_decoder_layers`, from one isolated 7-layer call).
 
 The same workload with the policy in bf16 (throughput mode) is reported as `secondary_bf16`
 with its measured action error against fp32 on the same inputs; it is never `value`.
@@ -314,13 +315,27 @@ def timed_run(groups, args, dist):
         e1.record()
         torch.cuda.synchronize()
         infer.append(e0.elapsed_time(e1) / 1e3)
+    # the same call with all 7 decoder layers computed (the dead layers 1..6 included), for the
+    # sensitivity line `all_decoder_layers`: the second call is timed
+    infer_full = []
+    pol = getattr(groups[0], "policy", None)
+    if pol is not None and getattr(pol, "prune_dead_decoder", False):
+        pol.prune_dead_decoder = False
+        for _ in range(2):
+            e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            e0.record()
+            groups[0].infer_policy()
+            e1.record()
+            torch.cuda.synchronize()
+            infer_full = [e0.elapsed_time(e1) / 1e3]
+        pol.prune_dead_decoder = True
     if dist:
         import torch.distributed as tdist
 
         t = torch.tensor([elapsed], dtype=torch.float64, device=groups[0].device)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         elapsed = float(t.item())
-    return elapsed, np.array(phys), np.array(infer)
+    return elapsed, np.array(phys), np.array(infer), np.array(infer_full)
 
 
 @torch.no_grad()
@@ -375,7 +390,7 @@ def rank_main(args):
 
     groups = make_groups(args.precision)
     ro = groups[0]
-    elapsed, phys, infer = timed_run(groups, args, dist)
+    elapsed, phys, infer, infer_full = timed_run(groups, args, dist)
     value = total * args.steps / elapsed
     if dist:
         # RCCL all-gather of per-env episode records (success, reward, duration, steps)
@@ -453,11 +468,20 @@ def rank_main(args):
                 "frac_executed": ex_tf / peak,
                 "note": "stride-1 3x3 convs by Winograd F(2x2,3x3) (rmbx_conv3x3_winograd_f32): achieved/frac "
                         "price the direct-algorithm FLOPs, *_executed the FLOPs the kernels run"})
+    if len(infer) and len(infer_full):
+        # exact either way (the DETRVAE output reads decoder layer 0 only); priced here so that the
+        # credited line can be compared with a rollout that also computes the dead layers
+        extra = (float(infer_full.mean()) - float(infer.mean())) / ro.args.skip
+        result["all_decoder_layers"] = {
+            "policy_inference_us_per_call": round(1e6 * float(infer_full.mean()), 1),
+            "value_estimate": round(total / (elapsed / args.steps + extra), 1), "unit": "env-steps/s",
+            "note": "the same step with decoder layers 1..6 computed too (their output is never read): "
+                    "timed value with the per-env-step policy time replaced by the measured 7-layer call"}
     if args.precision == "fp32" and not args.no_bf16_secondary:
         del groups, ro, eng
         torch.cuda.empty_cache()
         groups16 = make_groups("bf16")
-        el16, _, inf16 = timed_run(groups16, args, dist)
+        el16, _, inf16, _ = timed_run(groups16, args, dist)
         ro32 = make_rollout(args, dev, "fp32", 16, g0)  # same weights (seeded), its own 16-env frame
         err_abs, err_rel = bf16_action_error(ro32, groups16[0])
         result["secondary_bf16"] = {
