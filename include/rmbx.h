@@ -247,6 +247,49 @@ int rmbx_arm_fk(const double* placement, const double* q, double* R_out, double*
                 int n_env, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
+ * DataKey routing for the UR5e arm + gripper (one ArmManager, eef_idx 0).
+ * Key codes name common/data/DataKey.py:14-58; RMBX_MAX_DATA_KEYS keys per call.
+ *
+ * rmbx_motion_state replaces RolloutBase.get_state's concatenation (RolloutBase.py:463-473) of
+ * MotionManager.get_data (MotionManager.py:41-130): the raw f64 state [n][state_dim] of the keys
+ * in order, before normalize_data.  measured_* keys read the observation (joint_pos f64 [n][7],
+ * joint_vel f64 [n][7], wrench f64 [n][6]); measured_eef_pose = FK of the measured arm joints as
+ * (t, qw, qx, qy, qz) (ArmManager.py:161-165, MathUtils.py:27-31); command_* keys read the command
+ * state (q_cmd f64 [n][6], grip_cmd f64 [n], IK target target_R f64 [n][9] / target_p f64 [n][3]).
+ * Keys the reference cannot serve as state (the *_rel keys, MotionManager.py:87-90) are
+ * RMBX_ERR_ARG.
+ *
+ * rmbx_motion_command replaces RolloutBase.set_command_data (RolloutBase.py:496-509) ->
+ * MotionManager.set_command_data (:25-39) -> ArmManager.set_command_data (ArmManager.py:88-159):
+ * slices of action f64 [n][action_dim] applied key by key to the command state in place:
+ * command_joint_pos (arm + gripper; IK target := FK), command_joint_pos_rel (added unless
+ * is_skip), command_gripper_joint_pos (clipped to [grip_low, grip_high]), command_eef_pose
+ * (target := SE3(quaternion(w, x, y, z), t), one DLS IK step), command_eef_pose_rel (target :=
+ * target * SE3(rpy, t) on every call, as the reference does not forward is_skip there; one IK
+ * step).  Other keys are RMBX_ERR_ARG (MotionManager.py:36-39).  mask u8 [n] (NULL = all).
+ * ------------------------------------------------------------------------------------------- */
+#define RMBX_MAX_DATA_KEYS 8
+#define RMBX_KEY_MEASURED_JOINT_POS 1
+#define RMBX_KEY_MEASURED_JOINT_VEL 2
+#define RMBX_KEY_MEASURED_GRIPPER_JOINT_POS 3
+#define RMBX_KEY_MEASURED_EEF_POSE 4
+#define RMBX_KEY_MEASURED_EEF_WRENCH 5
+#define RMBX_KEY_COMMAND_JOINT_POS 16
+#define RMBX_KEY_COMMAND_JOINT_POS_REL 17
+#define RMBX_KEY_COMMAND_GRIPPER_JOINT_POS 18
+#define RMBX_KEY_COMMAND_EEF_POSE 19
+#define RMBX_KEY_COMMAND_EEF_POSE_REL 20
+
+int rmbx_motion_state(const double* placement, const double* joint_pos, const double* joint_vel,
+                      const double* wrench, const double* q_cmd, const double* grip_cmd,
+                      const double* target_R, const double* target_p, const int32_t* keys,
+                      int n_keys, double* state_out, int state_dim, int n_env, void* stream);
+int rmbx_motion_command(const double* placement, const double* action, int action_dim,
+                        const int32_t* keys, int n_keys, int is_skip, double grip_low,
+                        double grip_high, double* q_cmd, double* grip_cmd, double* target_R,
+                        double* target_p, const uint8_t* mask, int n_env, void* stream);
+
+/* ---------------------------------------------------------------------------------------------
  * Batched camera rendering (ray casting of the scene primitives).
  * Replaces the per-camera OffScreenViewer rgb/depth renders of envs/mujoco/MujocoEnvBase.py:
  * 112-126 for one camera over n_env envs.  Primitive table (device): prim_i32 [nprim][4]

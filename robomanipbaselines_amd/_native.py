@@ -47,6 +47,9 @@ SIGNATURES = {
     "rmbx_engine_step_profiled": (_c_int, [_c_p, _c_int, _c_p, _c_p]),
     "rmbx_arm_ik": (_c_int, [_c_p] * 5 + [_c_int, _c_int, _c_p]),
     "rmbx_arm_fk": (_c_int, [_c_p] * 4 + [_c_int, _c_p]),
+    "rmbx_motion_state": (_c_int, [_c_p] * 9 + [_c_int, _c_p, _c_int, _c_int, _c_p]),
+    "rmbx_motion_command": (_c_int, [_c_p, _c_p, _c_int, _c_p, _c_int, _c_int, _c_d, _c_d] + [_c_p] * 5
+                            + [_c_int, _c_p]),
     "rmbx_render": (_c_int, [_c_p, _c_p, _c_p, _c_int, _c_p, _c_p, _c_p, _c_p, _c_int, _c_int, _c_p, _c_p, _c_p,
                              _c_int, _c_p, _c_int, _c_p]),
     "rmbx_nhwc_bias_act": (_c_int, [_c_p] * 5 + [_c_sz, _c_int, _c_int, _c_int, _c_p]),

@@ -79,8 +79,8 @@ def main(argv=None):
     ns, _ = pre.parse_known_args(remaining)
     n_envs = ns.num_envs or len(ns.world_idx_list or [ns.world_idx])
     if int(os.environ.get("WORLD_SIZE", 1)) > 1:
-        remaining = remaining + _shard_args(n_envs)
-        n_envs = int(remaining[remaining.index("--num_envs") + 1])
+        shard, n_envs = _shard_args(n_envs)
+        remaining = remaining + shard  # argparse takes the last --num_envs: this rank's shard
     if n_envs >= 256 and args.policy in ("Act", "Mlp"):
         # large conv batches: keep MIOpen Find from timing its naive reference solver (seconds per
         # shape, never selected); process-wide, read by MIOpen on first use
@@ -95,7 +95,8 @@ def main(argv=None):
 
 
 def _shard_args(total):
-    """Join this rank's process group (RCCL) and return the inner-parser overrides of its shard."""
+    """Join this rank's process group (RCCL); return the inner-parser overrides of its shard and
+    the shard's env count."""
     import torch
     import torch.distributed as dist
 
@@ -106,7 +107,7 @@ def _shard_args(total):
     torch.cuda.set_device(local)
     dist.init_process_group("nccl", device_id=torch.device(f"cuda:{local}"))
     g0, g1 = shard_range(rank, world, total)
-    return ["--num_envs", str(g1 - g0), "--env_offset", str(g0), "--device", f"cuda:{local}"]
+    return ["--num_envs", str(g1 - g0), "--env_offset", str(g0), "--device", f"cuda:{local}"], g1 - g0
 
 
 def _rank_entry(local_rank, world, port, argv):

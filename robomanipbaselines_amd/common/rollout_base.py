@@ -27,7 +27,7 @@ import torch
 import yaml
 
 from .. import kernels as K
-from ..common.data_key import DataKey
+from ..common.data_key import DataKey, action_key_codes, state_key_codes
 from ..common.data_utils import make_meta_info
 
 
@@ -99,6 +99,12 @@ class BatchedRolloutBase:
                                  "process per GPU; results all-gathered over RCCL)")
         parser.add_argument("--tactile", action="store_true",
                             help="scenes with tactile pads: info['intensity_tactile'] every env-step")
+        parser.add_argument("--state_keys", type=str, nargs="*", default=None,
+                            help="synthetic runs (no --checkpoint) only: state keys of the synthetic model meta "
+                                 "info (TrainBase --state_keys; default measured_joint_pos)")
+        parser.add_argument("--action_keys", type=str, nargs="+", default=None,
+                            help="synthetic runs (no --checkpoint) only: action keys of the synthetic model meta "
+                                 "info (TrainBase --action_keys; default command_joint_pos)")
         parser.add_argument("--env_offset", type=int, default=0,
                             help="global index of local env 0 (this rank's shard start under --num_gpus): world "
                                  "indices and noise streams follow the global env index")
@@ -126,6 +132,13 @@ class BatchedRolloutBase:
         self.camera_names = self.model_meta_info["image"]["camera_names"]
         self.state_dim = len(self.model_meta_info["state"]["example"])
         self.action_dim = len(self.model_meta_info["action"]["example"])
+        # device routing codes; unsupported keys raise ValueError as MotionManager does
+        self._state_codes = state_key_codes(self.state_keys)
+        self._action_codes = action_key_codes(self.action_keys)
+        for what, keys, dim in (("state", self.state_keys, self.state_dim), ("action", self.action_keys, self.action_dim)):
+            kd = sum(DataKey.get_dim(k, self.env) for k in keys)
+            if kd != dim:
+                raise ValueError(f"{what} keys {keys} have dimension {kd}, the model meta info {dim}")
         if self.args.skip is None:
             self.args.skip = self.model_meta_info["data"]["skip"]
         if self.args.skip_draw is None:
@@ -160,15 +173,28 @@ class BatchedRolloutBase:
             self._st_min = torch.tensor(st["min"], dtype=torch.float64, device=dev)
             self._st_range = torch.tensor(st["range"], dtype=torch.float64, device=dev)
 
+    def get_raw_state(self):
+        """RolloutBase.get_state's key concatenation (:463-473): MotionManager.get_data of every
+        state key in order, f64 [n, state_dim], on the device (rmbx_motion_state)."""
+        if not self.state_keys:
+            return torch.zeros((self.n, 0), dtype=torch.float64, device=self.device)
+        return K.motion_state(self._placement, self.obs, self.q_cmd, self.grip_cmd, self._tgt_R, self._tgt_p,
+                              self._state_codes, self.state_dim)
+
     def get_state(self):
-        """normalize_data (DataUtils.py:9-24) of the measured joint positions in f64 (same
-        operations and order as numpy), then the f32 cast of RolloutBase.get_state (:475)."""
-        jp = self.obs["joint_pos"]
+        """RolloutBase.get_state (:463-477): the routed state, normalised, as f32 [n, state_dim]."""
+        return self.normalize_state(self.get_raw_state())
+
+    def normalize_state(self, x):
+        """normalize_data (DataUtils.py:9-24) in f64 (same operations and order as numpy), then the
+        f32 cast of RolloutBase.get_state (:475)."""
+        if x.shape[-1] == 0:
+            return x.to(torch.float32)
         st = self.model_meta_info["state"]
         if st.get("norm_config", {}).get("type", "gaussian") == "gaussian":
-            return ((jp - self._st_mean) / self._st_std).to(torch.float32)
+            return ((x - self._st_mean) / self._st_std).to(torch.float32)
         scale = (st["norm_config"]["out_max"] - st["norm_config"]["out_min"]) / self._st_range
-        return (scale * (jp - self._st_min) + st["norm_config"]["out_min"]).to(torch.float32)
+        return (scale * (x - self._st_min) + st["norm_config"]["out_min"]).to(torch.float32)
 
     # per-channel (mean, std) the renderer applies to [0, 1] pixels for the policy tensor:
     # identity = RolloutBase.image_transforms (v2.ToDtype(float32, scale=True), :353); the ACT
@@ -181,8 +207,11 @@ class BatchedRolloutBase:
         [n,ncam,H/2,W/2,16] its fused stem kernel reads)."""
         H, W = self.env.renderer.height, self.env.renderer.width
         mean, std = self.image_norm
+        # (the fused f32 stem kernel takes space-to-depth rows of at most STEM_POOL_MAX_WS: wider
+        # f32 images go through the NCHW path)
         s2d = (dtype in (torch.bfloat16, torch.float32) and self.device.type == "cuda"
-               and getattr(self.policy, "accepts_s2d", False) and H % 2 == 0 and W % 2 == 0)
+               and getattr(self.policy, "accepts_s2d", False) and H % 2 == 0 and W % 2 == 0
+               and (dtype == torch.bfloat16 or W // 2 <= K.STEM_POOL_MAX_WS))
         shape = (H // 2, W // 2, 16) if s2d else (3, H, W)
         if getattr(self, "_img", None) is None or self._img.dtype != dtype or tuple(self._img.shape[2:]) != shape:
             self._img = torch.empty((self.n, len(self.camera_names)) + shape, dtype=dtype, device=self.device)
@@ -197,17 +226,26 @@ class BatchedRolloutBase:
 
     # -- command routing (MotionManager / ArmManager) ------------------------------------------
     def _reset_motion(self):
-        env = self.env
-        self.q_cmd = torch.tensor(np.tile(env.init_qpos[:6], (self.n, 1)), dtype=torch.float64, device=self.device)
-        self.grip_cmd = torch.zeros((self.n, 1), dtype=torch.float64, device=self.device)
-        self._placement = torch.tensor(env.arrays["arm_placement"], dtype=torch.float64, device=self.device)
+        """ArmManager.reset (:75-86): arm / gripper command = the initial pose, IK target = its FK."""
+        env, dev = self.env, self.device
+        self.q_cmd = torch.tensor(np.tile(env.init_qpos[:6], (self.n, 1)), dtype=torch.float64, device=dev)
+        self.grip_cmd = torch.zeros((self.n, 1), dtype=torch.float64, device=dev)
+        self._placement = torch.tensor(env.arrays["arm_placement"], dtype=torch.float64, device=dev).contiguous()
         self._glo, self._ghi = float(env.action_low[6]), float(env.action_high[6])
+        self._tgt_R = torch.empty((self.n, 9), dtype=torch.float64, device=dev)
+        self._tgt_p = torch.empty((self.n, 3), dtype=torch.float64, device=dev)
+        from .. import _native as N
+
+        N.call("rmbx_arm_fk", N.ptr(self._placement), N.ptr(self.q_cmd), N.ptr(self._tgt_R), N.ptr(self._tgt_p),
+               self.n, N.stream_ptr())
 
     def set_command_data(self):
-        """ArmManager.set_command_joint_pos (:125-129) + gripper clip (:141-146)."""
-        a = self.policy_action
-        self.q_cmd.copy_(a[:, :6])
-        self.grip_cmd.copy_(a[:, 6:7].clamp(self._glo, self._ghi))
+        """RolloutBase.set_command_data (:496-509): the policy action routed key by key through
+        MotionManager / ArmManager (joint / relative joint / gripper / eef pose / relative eef
+        pose commands, rmbx_motion_command), with is_skip = rollout_time_idx % skip != 0."""
+        is_skip = self.rollout_time_idx % self.args.skip != 0
+        K.motion_command(self._placement, self.policy_action, self._action_codes, is_skip, self._glo, self._ghi,
+                         self.q_cmd, self.grip_cmd, self._tgt_R, self._tgt_p)
 
     def env_action(self):
         return torch.cat([self.q_cmd, self.grip_cmd], dim=1)
@@ -216,9 +254,9 @@ class BatchedRolloutBase:
         """OperationMujocoUR5eCable.get_target_se3 (:8-11): cable_end xy, fixed z, R=diag(-1,1,-1)."""
         end = self.env.get_body_pose("cable_end")[:, :3].clone()
         end[:, 2] = pos_z
-        self._tgt_p = end.contiguous()
+        self._tgt_p.copy_(end)
         R = torch.tensor([-1.0, 0, 0, 0, 1.0, 0, 0, 0, -1.0], dtype=torch.float64, device=self.device)
-        self._tgt_R = R.expand(self.n, 9).contiguous()
+        self._tgt_R.copy_(R.expand(self.n, 9))
 
     def _ik_step(self):
         from .. import _native as N
@@ -301,7 +339,8 @@ class BatchedRolloutBase:
                     if ph.kind == "reach":
                         if ph.target is not None:
                             R, p = ph.target(self)
-                            self._tgt_R, self._tgt_p = R.contiguous(), p.contiguous()
+                            self._tgt_R.copy_(R)
+                            self._tgt_p.copy_(p)
                         else:
                             self._set_reach_target(ph.pos_z)
                 else:

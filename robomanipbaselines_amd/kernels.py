@@ -230,6 +230,55 @@ def ur5e_obs(arm_qpos, arm_qvel, grip_qpos, force, torque):
     return jp, jv, wr
 
 
+# ------------------------------------------------------------------------------------------
+# DataKey routing (MotionManager / ArmManager on the device)
+# ------------------------------------------------------------------------------------------
+def _key_array(codes):
+    return np.ascontiguousarray(np.asarray(codes, dtype=np.int32).reshape(-1))
+
+
+def motion_state(placement, obs, q_cmd, grip_cmd, tgt_R, tgt_p, codes, dim, out=None):
+    """Raw f64 state [n, dim] of the state keys (rmbx_motion_state)."""
+    jp = obs["joint_pos"]
+    n = jp.shape[0]
+    _chk(placement, torch.float64, (6, 12), "placement")
+    _chk(jp, torch.float64, (n, 7), "joint_pos")
+    _chk(obs["joint_vel"], torch.float64, (n, 7), "joint_vel")
+    _chk(obs["wrench"], torch.float64, (n, 6), "wrench")
+    _chk(q_cmd, torch.float64, (n, 6), "q_cmd")
+    _chk(grip_cmd, torch.float64, (n, 1), "grip_cmd")
+    _chk(tgt_R, torch.float64, (n, 9), "target_R")
+    _chk(tgt_p, torch.float64, (n, 3), "target_p")
+    if out is None:
+        out = torch.empty((n, dim), dtype=torch.float64, device=jp.device)
+    _chk(out, torch.float64, (n, dim), "state")
+    keys = _key_array(codes)
+    N.call("rmbx_motion_state", N.ptr(placement), N.ptr(jp), N.ptr(obs["joint_vel"]), N.ptr(obs["wrench"]),
+           N.ptr(q_cmd), N.ptr(grip_cmd), N.ptr(tgt_R), N.ptr(tgt_p), N.ptr(keys), len(keys), N.ptr(out), dim, n,
+           N.stream_ptr())
+    return out
+
+
+def motion_command(placement, action, codes, is_skip, grip_low, grip_high, q_cmd, grip_cmd, tgt_R, tgt_p,
+                   mask=None):
+    """Apply the policy action to the command state in place (rmbx_motion_command)."""
+    n = q_cmd.shape[0]
+    _chk(placement, torch.float64, (6, 12), "placement")
+    _chk(action, torch.float64, None, "action")
+    if action.dim() != 2 or action.shape[0] != n:
+        raise ValueError(f"action must be [{n}, action_dim] (got {tuple(action.shape)})")
+    _chk(q_cmd, torch.float64, (n, 6), "q_cmd")
+    _chk(grip_cmd, torch.float64, (n, 1), "grip_cmd")
+    _chk(tgt_R, torch.float64, (n, 9), "target_R")
+    _chk(tgt_p, torch.float64, (n, 3), "target_p")
+    if mask is not None:
+        _chk(mask, torch.uint8, (n,), "mask")
+    keys = _key_array(codes)
+    N.call("rmbx_motion_command", N.ptr(placement), N.ptr(action), action.shape[1], N.ptr(keys), len(keys),
+           int(bool(is_skip)), float(grip_low), float(grip_high), N.ptr(q_cmd), N.ptr(grip_cmd), N.ptr(tgt_R),
+           N.ptr(tgt_p), N.ptr(mask), n, N.stream_ptr())
+
+
 def depth_linearize(zbuf, near, far, out=None):
     _chk(zbuf, torch.float32, None, "zbuf")
     if out is None:

@@ -33,6 +33,14 @@ def _check_normalizer(key, value):
         raise ValueError(f"non-identity normalizer {key}: the rollout feeds normalised data")
 
 
+def _is_dummy(key, value):
+    """diffusion_policy's ModuleAttrMixin registers `_dummy_variable = nn.Parameter()` (an empty
+    tensor used only to find the module's device/dtype) on the policy and on its
+    LowdimMaskGenerator, so a real state_dict carries `_dummy_variable` and
+    `mask_generator._dummy_variable`.  They hold no weights; drop them (an empty tensor only)."""
+    return (key == "_dummy_variable" or key.endswith("._dummy_variable")) and value.numel() == 0
+
+
 def _put(out, key, value, src):
     if key in out:
         if out[key].shape != value.shape or not torch.equal(out[key], value):
@@ -48,6 +56,8 @@ def dp_state_dict_from_reference(sd, camera_names):
     vis = re.compile(r"^obs_encoder\.obs_nets\.([^.]+)\.(.*)$")
     out, unexpected = {}, []
     for k, v in sd.items():
+        if _is_dummy(k, v):
+            continue
         if k.startswith("model.") or k.startswith("obs_nets."):
             _put(out, k, v, k)
             continue
@@ -76,6 +86,8 @@ def dp3_state_dict_from_reference(sd):
     """Map a DP3 state_dict onto DP3Model's names (identical apart from the normalizer)."""
     out, unexpected = {}, []
     for k, v in sd.items():
+        if _is_dummy(k, v):
+            continue
         if k.startswith("normalizer."):
             _check_normalizer(k, v)
         elif k.startswith("model.") or k.startswith("obs_encoder."):

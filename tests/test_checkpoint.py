@@ -100,6 +100,9 @@ def _upstream_dp_sd(model, cam="front"):
     sd["normalizer.params_dict.action.scale"] = torch.ones(7)
     sd["normalizer.params_dict.action.offset"] = torch.zeros(7)
     sd["normalizer.params_dict.action.input_stats.max"] = torch.ones(7)
+    # ModuleAttrMixin's parameter-free device probes (policy and LowdimMaskGenerator)
+    sd["_dummy_variable"] = torch.empty(0)
+    sd["mask_generator._dummy_variable"] = torch.empty(0)
     return sd
 
 
@@ -154,6 +157,8 @@ def test_dp3_reference_checkpoint_loads_strictly():
     dst = DP3Model(7, 7, down_dims=(32, 64, 128))
     sd = dict(src.state_dict())
     sd["normalizer.params_dict.point_cloud.offset"] = torch.zeros(3)
+    sd["_dummy_variable"] = torch.empty(0)
+    sd["mask_generator._dummy_variable"] = torch.empty(0)
     load_dp3_checkpoint(dst, sd)
     for k, v in src.state_dict().items():
         assert torch.equal(dst.state_dict()[k], v), k
@@ -161,3 +166,5 @@ def test_dp3_reference_checkpoint_loads_strictly():
         load_dp3_checkpoint(dst, dict(sd, **{"ema.decay": torch.zeros(1)}))
     with pytest.raises(RuntimeError):
         load_dp3_checkpoint(dst, {k: v for k, v in sd.items() if "state_mlp" not in k})
+    with pytest.raises(ValueError):  # a non-empty "_dummy_variable" is a real tensor: not dropped
+        load_dp3_checkpoint(dst, dict(sd, _dummy_variable=torch.zeros(1)))

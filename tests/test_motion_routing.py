@@ -1,0 +1,197 @@
+"""DataKey routing: RolloutBase.get_state / set_command_data over MotionManager /
+ArmManager (common/base/RolloutBase.py:463-509, common/manager/MotionManager.py:25-130,
+common/body/ArmManager.py:75-186) for every state / action key TrainBase accepts
+(common/base/TrainBase.py:73-88).
+
+tests/golden/motion.npz was minted by running the reference's own classes (tools/gen_golden.py
+gen_motion) with the pinocchio math supplied by the oracle's restatement (pinocchio is absent:
+that arithmetic is unpinned; the routing -- key order, slices, is_skip, clipping, which command
+state each key reads and writes -- is the reference's).
+
+* CPU: oracle/motion.py against the golden (bit-exact), the key validation against the keys the
+  reference rejects.
+* GPU: rmbx_motion_state / rmbx_motion_command through the C ABI against the golden over the
+  whole 12-step sequences of 6 envs, batched: bit-exact where no pinocchio arithmetic is
+  involved; FK / IK / quaternion paths within 1e-9 (f64 sin/cos and contraction differ in the
+  last bits from numpy); and a product rollout with non-default keys."""
+
+import numpy as np
+import pytest
+
+from oracle import motion
+from robomanipbaselines_amd.common.data_key import action_key_codes, state_key_codes
+
+G = np.load("tests/golden/motion.npz")
+CASES = [str(c) for c in G["cases"]]
+EEF_KEYS = {"measured_eef_pose", "command_eef_pose", "command_eef_pose_rel"}
+
+
+def _stats(name):
+    st = {"norm_config": {"type": str(G[f"{name}_norm"])}}
+    for k in ("mean", "std", "min", "range"):
+        if f"{name}_stat_{k}" in G:
+            st[k] = G[f"{name}_stat_{k}"]
+    if st["norm_config"]["type"] == "limits":
+        st["norm_config"].update(out_min=-1.0, out_max=1.0)
+    return st
+
+
+def _normalize(x, st):
+    if st["norm_config"]["type"] == "gaussian":
+        return (x - st["mean"]) / st["std"]
+    cfg = st["norm_config"]
+    return (cfg["out_max"] - cfg["out_min"]) / st["range"] * (x - st["min"]) + cfg["out_min"]
+
+
+def _uses_eef(name):
+    keys = {str(k) for k in G[f"{name}_skeys"]} | {str(k) for k in G[f"{name}_akeys"]}
+    return bool(keys & EEF_KEYS)
+
+
+@pytest.mark.parametrize("name", CASES)
+def test_oracle_routing_matches_reference_golden(name):
+    skeys = [str(k) for k in G[f"{name}_skeys"]]
+    akeys = [str(k) for k in G[f"{name}_akeys"]]
+    st = _stats(name)
+    P, q0 = G["placement"], G["q0"]
+    E, T, skip = int(G["E"]), int(G["T"]), int(G["skip"])
+    for e in range(E):
+        arm = motion.ArmCommand(P, q0)
+        for t in range(T):
+            raw = motion.get_raw_state(skeys, G[f"{name}_jp"][e, t], G[f"{name}_jv"][e, t], G[f"{name}_wr"][e, t], arm)
+            np.testing.assert_array_equal(_normalize(raw, st).astype(np.float32), G[f"{name}_state"][e, t])
+            env_action = motion.set_command(akeys, G[f"{name}_act"][e, t], t % skip != 0, arm, G["low"][6], G["high"][6])
+            np.testing.assert_array_equal(env_action, G[f"{name}_env_action"][e, t], err_msg=f"{name} env {e} step {t}")
+            np.testing.assert_array_equal(motion.pose_from_se3(arm.R, arm.p), G[f"{name}_target"][e, t])
+
+
+def test_golden_covers_every_trainable_key():
+    keys = set()
+    for name in CASES:
+        keys |= {str(k) for k in G[f"{name}_skeys"]} | {str(k) for k in G[f"{name}_akeys"]}
+    trainable_state = {"measured_joint_pos", "measured_joint_vel", "measured_gripper_joint_pos", "measured_eef_pose",
+                       "measured_eef_wrench"}
+    trainable_action = {"command_joint_pos", "command_joint_pos_rel", "command_gripper_joint_pos", "command_eef_pose",
+                        "command_eef_pose_rel"}
+    assert trainable_state | trainable_action <= keys
+    # NaN gripper commands propagate through np.clip
+    assert np.isnan(G["default_env_action"][1, 4, 6])
+
+
+def test_rejected_keys_raise_like_the_reference():
+    for skey, akey, err in G["rejected"]:
+        assert err == "ValueError"
+        with pytest.raises(ValueError):
+            state_key_codes([str(skey)])
+            action_key_codes([str(akey)])
+    with pytest.raises(ValueError):
+        state_key_codes(["no_such_key"])
+    assert state_key_codes([]) == []
+
+
+def _device_case(name):
+    import torch
+
+    from robomanipbaselines_amd import kernels as K
+    from robomanipbaselines_amd import _native as N
+
+    dev = "cuda:0"
+    skeys = [str(k) for k in G[f"{name}_skeys"]]
+    akeys = [str(k) for k in G[f"{name}_akeys"]]
+    scodes, acodes = state_key_codes(skeys), action_key_codes(akeys)
+    sdim = G[f"{name}_state"].shape[2]
+    st = _stats(name)
+    E, T, skip = int(G["E"]), int(G["T"]), int(G["skip"])
+    P = torch.tensor(G["placement"], device=dev)
+    q = torch.tensor(np.tile(G["q0"], (E, 1)), device=dev)
+    g = torch.zeros((E, 1), dtype=torch.float64, device=dev)
+    R = torch.empty((E, 9), dtype=torch.float64, device=dev)
+    p = torch.empty((E, 3), dtype=torch.float64, device=dev)
+    N.call("rmbx_arm_fk", N.ptr(P), N.ptr(q), N.ptr(R), N.ptr(p), E, N.stream_ptr())
+    states, actions, targets = [], [], []
+    for t in range(T):
+        obs = {"joint_pos": torch.tensor(G[f"{name}_jp"][:, t], device=dev),
+               "joint_vel": torch.tensor(G[f"{name}_jv"][:, t], device=dev),
+               "wrench": torch.tensor(G[f"{name}_wr"][:, t], device=dev)}
+        if skeys:
+            raw = K.motion_state(P, obs, q, g, R, p, scodes, sdim).cpu().numpy()
+            states.append(np.stack([_normalize(raw[e], st) for e in range(E)]).astype(np.float32))
+        a = torch.tensor(np.ascontiguousarray(G[f"{name}_act"][:, t]), device=dev)
+        K.motion_command(P, a, acodes, t % skip != 0, G["low"][6], G["high"][6], q, g, R, p)
+        actions.append(torch.cat([q, g], 1).cpu().numpy())
+        Rn, pn = R.cpu().numpy(), p.cpu().numpy()
+        targets.append(np.stack([motion.pose_from_se3(Rn[e].reshape(3, 3), pn[e]) for e in range(E)]))
+    return states, actions, targets
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("name", CASES)
+def test_device_routing_matches_reference_golden(name):
+    states, actions, targets = _device_case(name)
+    T = int(G["T"])
+    exact = not _uses_eef(name)
+    for t in range(T):
+        want_a, want_t = G[f"{name}_env_action"][:, t], G[f"{name}_target"][:, t]
+        if exact:
+            if states:
+                np.testing.assert_array_equal(states[t], G[f"{name}_state"][:, t], err_msg=f"step {t}")
+            np.testing.assert_array_equal(actions[t], want_a, err_msg=f"step {t}")
+        else:
+            if states:
+                # f32 states: FK differences of ~1e-15 may flip the last f32 bit
+                np.testing.assert_allclose(states[t], G[f"{name}_state"][:, t], rtol=1e-6, atol=1e-6)
+            np.testing.assert_allclose(actions[t], want_a, rtol=0, atol=1e-9, err_msg=f"step {t}")
+        np.testing.assert_allclose(targets[t], want_t, rtol=0, atol=1e-12 if exact else 1e-9, err_msg=f"step {t}")
+
+
+@pytest.mark.gpu
+def test_device_routing_rejects_bad_keys_through_the_abi():
+    import torch
+
+    from robomanipbaselines_amd import kernels as K
+
+    dev = "cuda:0"
+    P = torch.tensor(G["placement"], device=dev)
+    q = torch.zeros((2, 6), dtype=torch.float64, device=dev)
+    g = torch.zeros((2, 1), dtype=torch.float64, device=dev)
+    R = torch.zeros((2, 9), dtype=torch.float64, device=dev)
+    p = torch.zeros((2, 3), dtype=torch.float64, device=dev)
+    with pytest.raises(ValueError):  # measured key as an action (ArmManager.py:120-123)
+        K.motion_command(P, torch.zeros((2, 7), dtype=torch.float64, device=dev), [1], False, 0, 255, q, g, R, p)
+    with pytest.raises(ValueError):  # action width disagrees with the keys
+        K.motion_command(P, torch.zeros((2, 6), dtype=torch.float64, device=dev), [16], False, 0, 255, q, g, R, p)
+    obs = {"joint_pos": torch.zeros((2, 7), dtype=torch.float64, device=dev),
+           "joint_vel": torch.zeros((2, 7), dtype=torch.float64, device=dev),
+           "wrench": torch.zeros((2, 6), dtype=torch.float64, device=dev)}
+    with pytest.raises(ValueError):  # relative key as state (MotionManager.py:87-90)
+        K.motion_state(P, obs, q, g, R, p, [17], 7)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("skeys,akeys", [
+    (["measured_eef_pose", "measured_gripper_joint_pos"], ["command_eef_pose", "command_gripper_joint_pos"]),
+    (["measured_joint_pos", "measured_joint_vel", "measured_eef_wrench"], ["command_joint_pos_rel"]),
+    ([], ["command_eef_pose_rel", "command_gripper_joint_pos"]),
+])
+def test_product_rollout_with_routed_keys(skeys, akeys):
+    """A synthetic MLP rollout on 4 Cable envs with non-default keys: the policy's widths follow
+    the keys, the routed commands reach the physics, and the episodes run to completion."""
+    import torch
+
+    from robomanipbaselines_amd.envs.operation.OperationMujocoUR5eCable import OperationMujocoUR5eCable
+    from robomanipbaselines_amd.policy.mlp.rollout_mlp import RolloutMlp
+
+    class R(OperationMujocoUR5eCable, RolloutMlp):
+        pass
+
+    argv = ["--num_envs", "4", "--precision", "fp32", "--max_steps", "120", "--action_keys", *akeys,
+            "--state_keys", *skeys]
+    ro = R(argv=argv)
+    assert ro.state_dim == sum(motion.DIMS[k] for k in skeys)
+    assert ro.action_dim == sum(motion.DIMS[k] for k in akeys)
+    steps = ro.run()
+    assert steps == 120
+    assert torch.isfinite(ro.env.engine.qpos).all()
+    assert torch.isfinite(ro.q_cmd).all()
+    # the rollout phase moved the arm command away from the last reach-phase IK result
+    assert ro.rollout_time_idx > 0

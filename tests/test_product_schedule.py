@@ -1,7 +1,7 @@
 """Product-path parity of the rollout plugin (BatchedRolloutBase) against fixtures minted from
 the reference's own Python (tools/gen_golden.py):
 
-* state normalisation: BatchedRolloutBase.get_state vs normalize_data (DataUtils.py:9-24) and
+* state normalisation: BatchedRolloutBase.normalize_state vs normalize_data (DataUtils.py:9-24) and
   the f32 cast of RolloutBase.get_state (:463-477), bit-exact;
 * the phase schedule as the product loop runs it: BatchedRolloutBase.step_once drives the real
   batched cable env (physics clock advanced by the engine, 8 x 0.004 s per env-step), with the
@@ -35,8 +35,7 @@ def _get_state(device, case):
     ro.device = torch.device(device)
     ro.model_meta_info = {"state": NORM_CASES[case](d)}
     ro._bind_state_stats()
-    ro.obs = {"joint_pos": torch.tensor(d["data"], dtype=torch.float64, device=device)}
-    got = ro.get_state().cpu().numpy()
+    got = ro.normalize_state(torch.tensor(d["data"], dtype=torch.float64, device=device)).cpu().numpy()
     want = d[f"{case}_norm"].astype(np.float32)  # torch.tensor(state, dtype=float32)
     return got, want
 

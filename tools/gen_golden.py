@@ -881,6 +881,239 @@ def gen_phase_schedule(importlib):
     print("phase cases:", [(c["name"], int(c["n_steps"]), float(c["duration"][0])) for c in cases][:4])
 
 
+def _install_pinocchio_math(placement):
+    """Give the pinocchio stub the functions ArmManager / MathUtils call, backed by the oracle's
+    restatement (oracle/arm_ik.py, oracle/motion.py): the reference's routing code then runs
+    unchanged on top.  The model's joint placements are the compiled scene's `arm_placement`
+    (the arm root pose already folded in; the ArmConfig below passes the identity root pose)."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    from oracle import arm_ik, motion
+
+    pin = sys.modules["pinocchio"]
+
+    class Quaternion:
+        def __init__(self, *a):
+            if len(a) == 1:
+                self.wxyz = motion.quat_from_mat(np.asarray(a[0], dtype=np.float64))
+            else:
+                self.wxyz = np.array(a, dtype=np.float64)
+
+        def coeffs(self):
+            return self.wxyz[[1, 2, 3, 0]].copy()
+
+        def matrix(self):
+            return motion.mat_from_quat(*self.wxyz)
+
+    class SE3:
+        def __init__(self, rot, trans):
+            self.rotation = rot.matrix() if isinstance(rot, Quaternion) else np.array(rot, dtype=np.float64)
+            self.translation = np.array(trans, dtype=np.float64)
+
+        def copy(self):
+            return SE3(self.rotation.copy(), self.translation.copy())
+
+        def __mul__(self, o):
+            return SE3(self.rotation @ o.rotation, self.translation + self.rotation @ o.translation)
+
+        def act(self, o):
+            return self * o
+
+        def actInv(self, o):
+            R = self.rotation
+            return SE3(R.T @ o.rotation, R.T @ (o.translation - self.translation))
+
+        def inverse(self):
+            return SE3(self.rotation.T, -self.rotation.T @ self.translation)
+
+    class Model:
+        nq = 6
+
+        def __init__(self):
+            self.jointPlacements = [SE3(np.eye(3), np.zeros(3))] + [
+                SE3(placement[k, :9].reshape(3, 3), placement[k, 9:12]) for k in range(6)]
+
+        def createData(self):
+            return types.SimpleNamespace(oMi=[SE3(np.eye(3), np.zeros(3)) for _ in range(7)])
+
+        def existJointName(self, name):
+            return False
+
+    def _placements(model):
+        return np.stack([np.concatenate([s.rotation.reshape(9), s.translation]) for s in model.jointPlacements[1:]])
+
+    def forwardKinematics(model, data, q):
+        for k, (R, p) in enumerate(arm_ik.fk(_placements(model), np.asarray(q, dtype=np.float64))):
+            data.oMi[k + 1] = SE3(R, p)
+
+    def computeJointJacobian(model, data, q, jid):
+        assert jid == 6
+        return arm_ik.joint_jacobian_local(arm_ik.fk(_placements(model), np.asarray(q, dtype=np.float64)))
+
+    pin.SE3 = SE3
+    pin.Quaternion = Quaternion
+    pin.buildModelFromUrdf = lambda path: Model()
+    pin.forwardKinematics = forwardKinematics
+    pin.computeJointJacobian = computeJointJacobian
+    pin.log = lambda M: types.SimpleNamespace(vector=arm_ik.log6(M.rotation, M.translation))
+    pin.Jlog6 = lambda M: arm_ik.jlog6(M.rotation, M.translation)
+    pin.integrate = lambda model, q, v: q + v
+    pin.rpy = types.SimpleNamespace(rpyToMatrix=lambda rpy: motion.rpy_to_mat(*rpy))
+    return motion
+
+
+def gen_motion(importlib):
+    """DataKey routing: the reference's RolloutBase.get_state / set_command_data (RolloutBase.py:463-509)
+    over MotionManager (MotionManager.py:25-130) and ArmManager (ArmManager.py:75-186), for state /
+    action key combinations TrainBase accepts (TrainBase.py:73-88), on E envs x T steps of synthetic
+    observations and policy actions (rollout_time_idx = step, skip 3 -> is_skip pattern).  Records
+    the normalised f32 state each step and, after each command, the env action (command_joint_pos,
+    EnvDataMixin.py:5-7) and the IK target pose (get_command_data(command_eef_pose)).  Key sets
+    the reference rejects are recorded with the exception it raised."""
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+    from robomanipbaselines_amd import model as MD
+
+    arrays = MD.load("ur5e_cable")
+    placement = np.ascontiguousarray(arrays["arm_placement"], dtype=np.float64)
+    motion = _install_pinocchio_math(placement)
+    arm_mod = importlib.import_module("robo_manip_baselines.common.body.ArmManager")
+    mm_mod = importlib.import_module("robo_manip_baselines.common.manager.MotionManager")
+    rb = importlib.import_module("robo_manip_baselines.common.base.RolloutBase")
+    DataKey = importlib.import_module("robo_manip_baselines.common.data.DataKey").DataKey
+    Rollout = type("RoutingOnly", (rb.RolloutBase,), {k: (lambda self, *a, **kw: None)
+                                                        for k in ("setup_policy", "infer_policy", "draw_plot")})
+    q0 = np.array([np.pi, -np.pi / 2, -0.75 * np.pi, -0.25 * np.pi, np.pi / 2, np.pi / 2])
+    low = np.array([-2 * np.pi] * 6 + [0.0])
+    high = np.array([2 * np.pi] * 6 + [255.0])
+
+    def make_env():
+        cfg = arm_mod.ArmConfig(arm_urdf_path="ur5e.urdf", arm_root_pose=np.array([0, 0, 0, 1.0, 0, 0, 0]),
+                                ik_eef_joint_id=6, arm_joint_idxes=np.arange(6),
+                                gripper_joint_idxes=np.array([6]),
+                                gripper_joint_idxes_in_gripper_joint_pos=np.array([0]), eef_idx=0,
+                                init_arm_joint_pos=q0.copy(), init_gripper_joint_pos=np.zeros(1))
+        u = types.SimpleNamespace(body_config_list=[cfg], command_keys_for_step=[DataKey.COMMAND_JOINT_POS])
+        u.get_joint_pos_from_obs = lambda obs: obs["joint_pos"]
+        u.get_joint_vel_from_obs = lambda obs: obs["joint_vel"]
+        u.get_eef_wrench_from_obs = lambda obs: obs["wrench"]
+
+        def _grip(obs):
+            g = np.zeros(1)
+            g[cfg.gripper_joint_idxes_in_gripper_joint_pos] = obs["joint_pos"][cfg.gripper_joint_idxes]
+            return g
+
+        u.get_gripper_joint_pos_from_obs = _grip
+        env = types.SimpleNamespace(unwrapped=u, action_space=types.SimpleNamespace(low=low, high=high))
+        return env
+
+    cases = [
+        ("default", ["measured_joint_pos"], ["command_joint_pos"]),
+        ("vel_wrench_rel", ["measured_joint_pos", "measured_joint_vel", "measured_eef_wrench"], ["command_joint_pos_rel"]),
+        ("eef_abs", ["measured_gripper_joint_pos", "measured_eef_pose"], ["command_eef_pose", "command_gripper_joint_pos"]),
+        ("eef_rel", ["measured_eef_pose", "measured_eef_wrench"], ["command_eef_pose_rel", "command_gripper_joint_pos"]),
+        ("joint_and_grip", [], ["command_joint_pos", "command_gripper_joint_pos"]),
+        ("mixed_rel", ["measured_joint_vel", "measured_gripper_joint_pos"], ["command_joint_pos_rel", "command_eef_pose_rel"]),
+        ("command_state", ["command_joint_pos", "command_eef_pose", "command_gripper_joint_pos"], ["command_eef_pose"]),
+        ("limits_norm", ["measured_joint_pos", "measured_eef_pose"], ["command_eef_pose_rel"]),
+    ]
+    rng = np.random.default_rng(9090)
+    E, T, skip = 6, 12, 3
+    d = {"placement": placement, "q0": q0, "low": low, "high": high, "E": np.int32(E), "T": np.int32(T),
+         "skip": np.int32(skip)}
+    Rinit, pinit = motion.arm_ik.fk(placement, q0)[-1]
+    pose0 = motion.pose_from_se3(Rinit, pinit)
+    names = []
+    for name, skeys, akeys in cases:
+        sdim = sum(DataKey.get_dim(k, make_env()) for k in skeys)
+        adim = sum(DataKey.get_dim(k, make_env()) for k in akeys)
+        if name == "limits_norm":
+            mn = rng.normal(0, 1, sdim) - 2.0
+            stats = {"norm_config": {"type": "limits", "out_min": -1.0, "out_max": 1.0}, "min": mn,
+                     "max": mn + 4.0, "range": np.full(sdim, 4.0)}
+        else:
+            stats = {"norm_config": {"type": "gaussian"}, "mean": rng.normal(0, 1, sdim),
+                     "std": np.abs(rng.normal(0, 1, sdim)) + 0.05}
+        jp = np.concatenate([q0, [0.0]])[None, None] + rng.normal(0, 0.2, (E, T, 7))
+        jp[..., 6] = rng.uniform(0, 255, (E, T))
+        jv = rng.normal(0, 1, (E, T, 7))
+        jv[..., 6] = 0.0
+        wr = rng.normal(0, 5, (E, T, 6))
+        act = np.zeros((E, T, adim))
+        off = 0
+        for k in akeys:
+            dk = DataKey.get_dim(k, make_env())
+            if k == "command_joint_pos":
+                a = np.concatenate([q0, [100.0]])[None, None] + rng.normal(0, 0.1, (E, T, 7)) * ([1.0] * 6 + [200.0])
+            elif k == "command_joint_pos_rel":
+                a = rng.normal(0, 0.05, (E, T, 7)) * ([1.0] * 6 + [80.0])
+            elif k == "command_gripper_joint_pos":
+                a = rng.uniform(-60, 320, (E, T, 1))
+            elif k == "command_eef_pose":
+                a = pose0[None, None] + rng.normal(0, 0.03, (E, T, 7))  # quaternion not unit
+            else:  # command_eef_pose_rel
+                a = rng.normal(0, 0.01, (E, T, 6))
+            act[..., off:off + dk] = a
+            off += dk
+        if "command_joint_pos" in akeys:
+            act[1, 4, 6] = np.nan  # np.clip propagates NaN
+        states = np.zeros((E, T, sdim), dtype=np.float32)
+        env_action = np.zeros((E, T, 7))
+        target = np.zeros((E, T, 7))
+        for e in range(E):
+            env = make_env()
+            op = object.__new__(Rollout)
+            op.env = env
+            op.motion_manager = mm_mod.MotionManager(env)
+            op.motion_manager.reset()
+            op.state_keys, op.action_keys = list(skeys), list(akeys)
+            op.model_meta_info = {"state": stats}
+            op.device = "cpu"
+            op.args = types.SimpleNamespace(skip=skip)
+            for t in range(T):
+                op.obs = {"joint_pos": jp[e, t], "joint_vel": jv[e, t], "wrench": wr[e, t]}
+                op.rollout_time_idx = t
+                states[e, t] = op.get_state()[0].numpy()
+                op.policy_action = act[e, t].copy()
+                op.set_command_data()
+                env_action[e, t] = np.concatenate([op.motion_manager.get_command_data(k)
+                                                   for k in env.unwrapped.command_keys_for_step])
+                target[e, t] = op.motion_manager.get_command_data(DataKey.COMMAND_EEF_POSE)
+        names.append(name)
+        d.update({f"{name}_skeys": np.array(skeys, dtype="U32"), f"{name}_akeys": np.array(akeys, dtype="U32"),
+                  f"{name}_norm": np.array(stats["norm_config"]["type"], dtype="U16"),
+                  f"{name}_jp": jp, f"{name}_jv": jv, f"{name}_wr": wr, f"{name}_act": act,
+                  f"{name}_state": states, f"{name}_env_action": env_action, f"{name}_target": target})
+        for k, v in stats.items():
+            if k != "norm_config":
+                d[f"{name}_stat_{k}"] = np.asarray(v)
+    # key sets the reference rejects (ValueError from MotionManager / DataKey)
+    rejected = []
+    for skeys, akeys in ((["measured_joint_pos_rel"], ["command_joint_pos"]),
+                         (["measured_eef_pose_rel"], ["command_joint_pos"]),
+                         (["measured_joint_pos"], ["command_mobile_omni_vel"]),
+                         (["measured_joint_pos"], ["measured_joint_pos"])):
+        env = make_env()
+        op = object.__new__(Rollout)
+        op.env = env
+        op.motion_manager = mm_mod.MotionManager(env)
+        op.motion_manager.reset()
+        op.state_keys, op.action_keys = skeys, akeys
+        op.model_meta_info = {"state": {"norm_config": {"type": "gaussian"}, "mean": np.zeros(7), "std": np.ones(7)}}
+        op.device, op.args, op.rollout_time_idx = "cpu", types.SimpleNamespace(skip=3), 0
+        op.obs = {"joint_pos": np.zeros(7), "joint_vel": np.zeros(7), "wrench": np.zeros(6)}
+        err = ""
+        try:
+            op.get_state()
+            op.policy_action = np.zeros(7)
+            op.set_command_data()
+        except (ValueError, AttributeError) as ex:
+            err = type(ex).__name__
+        rejected.append((skeys[0], akeys[0], err))
+    d["rejected"] = np.array(rejected, dtype="U40")
+    d["cases"] = np.array(names, dtype="U32")
+    np.savez_compressed(os.path.join(OUT, "motion.npz"), **d)
+    print("motion:", names, "rejected:", rejected)
+
+
 def main():
     os.makedirs(OUT, exist_ok=True)
     importlib = install_stubs()
@@ -900,6 +1133,7 @@ def main():
     gen_phase_schedule(importlib)
     gen_normalize(importlib)
     gen_mlp_policy(importlib)
+    gen_motion(importlib)
 
 
 if __name__ == "__main__":
