@@ -358,6 +358,13 @@ int rmbx_conv2d_nhwc_f32(const float* in, const float* weight, const float* bias
 int rmbx_conv3x3_winograd_f32(const float* in, const float* u_packed, const float* bias,
                               const float* residual, float* out, int N, int H, int W, int C, int relu,
                               void* stream);
+/* Winograd F(4x4, 3x3) form of the same conv (2.25 products per output instead of 4): same
+ * operands and result as rmbx_conv3x3_winograd_f32 with u_packed = G g G^T for the 6x3 G of the
+ * points {0, +-1, +-2, inf} in the staging order [C/64][C/4][36][64][4] f32
+ * (robomanipbaselines_amd.kernels.pack_winograd4_f32).  f32 MFMA products, f32 accumulation. */
+int rmbx_conv3x3_winograd4_f32(const float* in, const float* u_packed, const float* bias,
+                               const float* residual, float* out, int N, int H, int W, int C, int relu,
+                               void* stream);
 /* ResNet stem on a 2x2 space-to-depth image: in [N][Hs][Ws][16] bf16 (channel (dy*2+dx)*3+c,
  * 12..15 zero; rmbx_render policy_dtype 2 writes this layout), weight packed [Cout][4][4][16] bf16
  * (the 7x7 / stride-2 / pad-3 conv1 re-indexed), out [N][Hs][Ws][Cout] bf16 = relu?(conv + bias).

@@ -57,6 +57,7 @@ SIGNATURES = {
     "rmbx_conv2d_nhwc": (_c_int, [_c_p] * 5 + [_c_int] * 10 + [_c_p]),
     "rmbx_conv2d_nhwc_f32": (_c_int, [_c_p] * 5 + [_c_int] * 10 + [_c_p]),
     "rmbx_conv3x3_winograd_f32": (_c_int, [_c_p] * 5 + [_c_int] * 5 + [_c_p]),
+    "rmbx_conv3x3_winograd4_f32": (_c_int, [_c_p] * 5 + [_c_int] * 5 + [_c_p]),
     "rmbx_stem_s2d_conv": (_c_int, [_c_p] * 4 + [_c_int] * 5 + [_c_p]),
     "rmbx_stem_s2d_conv_maxpool": (_c_int, [_c_p] * 4 + [_c_int] * 4 + [_c_p]),
     "rmbx_stem_s2d_conv_maxpool_f32": (_c_int, [_c_p] * 4 + [_c_int] * 4 + [_c_p]),

@@ -301,6 +301,243 @@ __global__ void __launch_bounds__(WG_THREADS, 1) wino_f32_kernel(WinoArgs a) {
   }
 }
 
+// =============================================================================================
+// Winograd F(4x4, 3x3): 36 positions per 6x6 input window / 4x4 output tile = 2.25 products per
+// output (F(2x2, 3x3): 4), points {0, +-1, +-2, inf}:
+//   V = B^T d B (input, exact small-integer coefficients), U = G g G^T (packed once on the host in
+//   f64 -> f32; G holds 1/4, 1/6, 1/12, 1/24), M[p] = sum_c U[p][co][c] V[p][c][tile],
+//   Y = A^T M A (coefficients 0, +-1, +-2, 4, +-8).
+// Mapping: a block = 8 waves owns 64 output channels x 32 tiles (512 output pixels); wave (cq, tg)
+// keeps 16 channels x 16 tiles for all 36 positions in 36 accumulators (144 registers), one
+// v_mfma_f32_16x16x4_f32 per position per K chunk of 4 input channels.  U (36 KiB per chunk,
+// pre-packed LDS image) is moved by LDS-DMA from waves 4-7.  The windows (32 tiles x 4 channels
+// per chunk, one whole 6x6 window per thread) are gathered and transformed by two loader groups
+// (waves 0-1 and 2-3) that alternate chunks: group c & 1 issues the window loads of chunk c after
+// its MFMA stream of chunk c - 2 (they stay in flight across the LDS-only barrier) and transforms
+// them into V buffer c & 1 under the second half of the MFMA stream of chunk c - 1: B^T down the
+// six columns in registers, then along the six rows with the LDS stores.  (Measured slower: the
+// column and row passes split over two chunks so both groups transform in every chunk on
+// complementary SIMDs, with the loads issued mid-stream -- 6.42 vs 5.71 ms at 512 channels; four
+// groups including the U waves, 6.90 ms.)
+// LDS: U and V double buffered, 108 KiB.  Persistent blocks and the per-XCD output-channel block
+// as F(2x2).
+// =============================================================================================
+constexpr int W4_TILES = 32;
+constexpr int W4_COUT = 64;
+constexpr int W4_KC = 4;
+constexpr int W4_UCH = 36 * W4_COUT * W4_KC;   // 9216 floats
+constexpr int W4_VCH = 36 * W4_TILES * W4_KC;  // 4608 floats
+static_assert((2 * W4_UCH + 2 * W4_VCH) * 4 <= 160 * 1024, "W4 LDS");
+
+template <int DBG>
+__global__ void __launch_bounds__(WG_THREADS, 1) wino4_f32_kernel(WinoArgs a) {
+  __shared__ __attribute__((aligned(16))) float smem[2 * W4_UCH + 2 * W4_VCH];  // sU[2], sV[2]
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int cq = wave & 3, tg = wave >> 2;
+  const int li = lane & 15, lq = lane >> 4;
+  const bool loader = wave < 4;  // waves 0-3: window loaders, waves 4-7: U LDS-DMA
+  const int lgrp = wave >> 1;    // loader group: chunks c with c & 1 == lgrp
+
+  const int G = gridDim.x;
+  const int xcd = blockIdx.x & 7;
+  const int cb = xcd % a.ncb;
+  const int per_cb = G / a.ncb;
+  const int r = (blockIdx.x >> 3) * (8 / a.ncb) + xcd / a.ncb;
+  if (r >= a.ntb) return;
+  const int nunits = (a.ntb - r + per_cb - 1) / per_cb;
+  const int nsteps = nunits << a.nk_log2;
+
+  // loader thread: window of tile lt (0..31), channel lc (0..3) of the chunk, by buffer loads: the
+  // lane's window origin in the 32-bit voffset, each pixel's (uniform) offset in soffset, so no
+  // per-load address arithmetic; offsets before the buffer or past its end (the top / bottom halo
+  // of the batch) read 0, and the pixels outside their image are zeroed by the in-image mask in
+  // the column pass
+  const int lt = (tid & 127) >> 2, lc = tid & 3;
+  float xr[36];
+  uint32_t ld_mlo = 0, ld_mhi = 0;  // in-image bits of the 36 window pixels
+  int ld_unit = -1, ld_o0 = 0;
+  const __amdgpu_buffer_rsrc_t in_rsrc =
+      __builtin_amdgcn_make_buffer_rsrc((void*)a.in, 0, (int)((uint32_t)a.N * a.H * a.W * a.C * 4u), 0x00020000);
+  auto tile_pos = [&](int t, int& img, int& ty, int& tx) {
+    const int q = t / a.tiles_x;
+    tx = t - q * a.tiles_x;
+    img = q / a.tiles_y;
+    ty = q - img * a.tiles_y;
+  };
+  auto load_u = [&](int s) {  // U waves: 9 KiB each as 9 lane-linear 1-KiB LDS-DMA pieces
+    const int k = s & (a.nk - 1);
+    const float* ug = a.u + ((size_t)cb * a.nk + k) * W4_UCH + (wave - 4) * 2304 + lane * 4;
+    float* ul = smem + (s & 1) * W4_UCH + (wave - 4) * 2304;
+    if (!(DBG & 8))
+#pragma unroll
+      for (int j = 0; j < 9; ++j) glds16(ug + 256 * j, ul + 256 * j);
+  };
+  auto load_window = [&](int s) {
+    if (DBG & 2) return;
+    const int unit = s >> a.nk_log2;
+    const int k = s & (a.nk - 1);
+    if (unit != ld_unit) {
+      ld_unit = unit;
+      const int t = (r + unit * per_cb) * W4_TILES + lt;
+      const bool tok = t < a.ntiles;
+      int img, ty, tx;
+      tile_pos(tok ? t : a.ntiles - 1, img, ty, tx);
+      const int y0 = 4 * ty - 1, x0 = 4 * tx - 1;
+      ld_o0 = ((img * a.H + y0) * a.W + x0) * a.C + lc;
+      ld_mlo = ld_mhi = 0;
+#pragma unroll
+      for (int i = 0; i < 36; ++i) {
+        const int y = y0 + i / 6, x = x0 + i % 6;
+        const uint32_t bit = (uint32_t)(tok && y >= 0 && y < a.H && x >= 0 && x < a.W);
+        if (i < 32)
+          ld_mlo |= bit << i;
+        else
+          ld_mhi |= bit << (i - 32);
+      }
+    }
+    const int voff = (ld_o0 + k * W4_KC) * 4;
+#pragma unroll
+    for (int i = 0; i < 36; ++i)
+      xr[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
+                                            in_rsrc, voff, ((i / 6) * a.W + (i % 6)) * a.C * 4, 0));
+  };
+  auto bt6 = [](float d0, float d1, float d2, float d3, float d4, float d5, float* v) {
+    v[0] = 4.f * d0 - 5.f * d2 + d4;
+    v[1] = (d3 + d4) - 4.f * (d1 + d2);
+    v[2] = (d4 - d3) + 4.f * (d1 - d2);
+    v[3] = (d4 - d2) + 2.f * (d3 - d1);
+    v[4] = (d4 - d2) - 2.f * (d3 - d1);
+    v[5] = 4.f * d1 - 5.f * d3 + d5;
+  };
+  auto col_piece = [&](int x) {  // mask, then B^T down window column x, in place
+    if (DBG & 4) return;
+    float d[6], v[6];
+#pragma unroll
+    for (int y = 0; y < 6; ++y) {
+      const int i = 6 * y + x;
+      const uint32_t bit = i < 32 ? (ld_mlo >> i) & 1u : (ld_mhi >> (i - 32)) & 1u;
+      d[y] = bit ? xr[i] : 0.f;
+    }
+    bt6(d[0], d[1], d[2], d[3], d[4], d[5], v);
+#pragma unroll
+    for (int y = 0; y < 6; ++y) xr[6 * y + x] = v[y];
+  };
+  auto row_piece = [&](int buf, int y) {  // B^T along row y, stored as positions 6 y .. 6 y + 5
+    if (DBG & 4) return;
+    float v[6];
+    bt6(xr[6 * y], xr[6 * y + 1], xr[6 * y + 2], xr[6 * y + 3], xr[6 * y + 4], xr[6 * y + 5], v);
+    float* vb = smem + 2 * W4_UCH + buf * W4_VCH + lt * W4_KC + lc;
+#pragma unroll
+    for (int x = 0; x < 6; ++x) vb[(6 * y + x) * (W4_TILES * W4_KC)] = v[x];
+  };
+
+  f32x4 acc[36];
+  auto chunk = [&](int c) {
+    const int buf = c & 1;
+    const bool more = c + 1 < nsteps;
+    if (!loader && more) load_u(c + 1);
+    const bool tf = loader && lgrp == ((c + 1) & 1) && c + 1 < nsteps;  // V(c + 1) -> other buffer
+    const float* Ub = smem + buf * W4_UCH + cq * 64 + li * 4 + lq;
+    const float* Vb = smem + 2 * W4_UCH + buf * W4_VCH + tg * 64 + li * 4 + lq;
+    float av = Ub[0], bv = Vb[0];
+#pragma unroll
+    for (int p = 0; p < 36; ++p) {
+      float an = av, bn = bv;
+      if (p < 35) {
+        an = Ub[(p + 1) * (W4_COUT * W4_KC)];
+        bn = Vb[(p + 1) * (W4_TILES * W4_KC)];
+      }
+      if (!(DBG & 1))
+        acc[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[p], 0, 0, 0);
+      else
+        acc[p][0] += av * bv;
+      if (tf && p >= 8 && p <= 18 && (p & 1) == 0) col_piece((p - 8) >> 1);
+      if (tf && p >= 20 && (p - 20) % 3 == 0) row_piece(buf ^ 1, (p - 20) / 3);
+      av = an;
+      bv = bn;
+    }
+    if (loader && lgrp == (c & 1) && c + 2 < nsteps) load_window(c + 2);
+    // U waves: the LDS-DMA of U(c + 1) has landed (loader waves keep their window loads in flight
+    // across the LDS-only barrier)
+    if (!loader) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+  };
+
+  // prologue: U(0); V(0) complete (group 0); the window of chunk 1 in flight (group 1)
+  if (!loader) {
+    load_u(0);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  } else if (lgrp < nsteps) {
+    load_window(lgrp);
+    if (lgrp == 0) {
+#pragma unroll
+      for (int x = 0; x < 6; ++x) col_piece(x);
+#pragma unroll
+      for (int y = 0; y < 6; ++y) row_piece(0, y);
+    }
+  }
+  lds_barrier();
+
+  int s = 0;
+  for (int unit = 0; unit < nunits; ++unit) {
+#pragma unroll
+    for (int p = 0; p < 36; ++p) acc[p] = f32x4{};
+    for (int k = 0; k < a.nk; ++k, ++s) chunk(s);
+
+    // Y = A^T M A (+ bias, + residual, ReLU): lane (li, lq) finishes channels 4 lq .. 4 lq + 3 of
+    // tile li of its group, output row by row: 16 pixels, one 16-byte store each
+    const int co0 = cb * W4_COUT + cq * 16 + 4 * lq;
+    const float4 b4 = *reinterpret_cast<const float4*>(a.bias + co0);
+    const int t_out = (r + unit * per_cb) * W4_TILES + tg * 16 + li;
+    const bool t_ok = t_out < a.ntiles;
+    int oimg, oty, otx;
+    tile_pos(t_ok ? t_out : a.ntiles - 1, oimg, oty, otx);
+    // row by row (output row i of the tile): t_i = (A^T M)[i] per channel, then its 4 pixels
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float y[4][4];  // [pixel q][channel e]
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        float t[6];
+#pragma unroll
+        for (int x = 0; x < 6; ++x) {
+          const float m0 = acc[x][e], m1 = acc[6 + x][e], m2 = acc[12 + x][e], m3 = acc[18 + x][e],
+                      m4 = acc[24 + x][e], m5 = acc[30 + x][e];
+          const float s12 = m1 + m2, d12 = m1 - m2, s34 = m3 + m4, d34 = m3 - m4;
+          t[x] = i == 0 ? m0 + s12 + s34 : i == 1 ? d12 + 2.f * d34 : i == 2 ? s12 + 4.f * s34 : d12 + 8.f * d34 + m5;
+        }
+        const float bj = e == 0 ? b4.x : e == 1 ? b4.y : e == 2 ? b4.z : b4.w;
+        const float s12 = t[1] + t[2], d12 = t[1] - t[2], s34 = t[3] + t[4], d34 = t[3] - t[4];
+        y[0][e] = t[0] + s12 + s34 + bj;
+        y[1][e] = d12 + 2.f * d34 + bj;
+        y[2][e] = s12 + 4.f * s34 + bj;
+        y[3][e] = d12 + 8.f * d34 + t[5] + bj;
+      }
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int yy = 4 * oty + i, xx = 4 * otx + q;
+        const bool ok = t_ok && yy < a.H && xx < a.W;
+        const int off = ok ? ((oimg * a.H + yy) * a.W + xx) * a.C + co0 : 0;
+        float o0 = y[q][0], o1 = y[q][1], o2 = y[q][2], o3 = y[q][3];
+        if (a.res) {
+          const float4 rv = *reinterpret_cast<const float4*>(a.res + off);
+          o0 += rv.x;
+          o1 += rv.y;
+          o2 += rv.z;
+          o3 += rv.w;
+        }
+        if (a.relu) {
+          o0 = o0 > 0.f ? o0 : (o0 != o0 ? o0 : 0.f);
+          o1 = o1 > 0.f ? o1 : (o1 != o1 ? o1 : 0.f);
+          o2 = o2 > 0.f ? o2 : (o2 != o2 ? o2 : 0.f);
+          o3 = o3 > 0.f ? o3 : (o3 != o3 ? o3 : 0.f);
+        }
+        if (ok) *reinterpret_cast<float4*>(a.out + off) = make_float4(o0, o1, o2, o3);
+      }
+    }
+  }
+}
+
 int device_cus() {
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -366,6 +603,60 @@ extern "C" int rmbx_conv3x3_winograd_f32(const float* in, const float* u_packed,
     case 14: hipLaunchKernelGGL(rmbx::wino_f32_kernel<14>, g, blk, 0, st, a); break;
     case 15: hipLaunchKernelGGL(rmbx::wino_f32_kernel<15>, g, blk, 0, st, a); break;
     default: RMBX_CHECK_ARG(false, "rmbx_conv3x3_winograd_f32: RMBX_WINO_DBG=%d not instantiated", a.dbg);
+  }
+  RMBX_CHECK_LAUNCH();
+  return RMBX_OK;
+}
+
+extern "C" int rmbx_conv3x3_winograd4_f32(const float* in, const float* u_packed, const float* bias,
+                                          const float* residual, float* out, int N, int H, int W, int C,
+                                          int relu, void* stream) {
+  RMBX_CHECK_ARG(in && u_packed && bias && out, "rmbx_conv3x3_winograd4_f32: null pointer");
+  RMBX_CHECK_ARG(N >= 0 && H > 0 && W > 0, "rmbx_conv3x3_winograd4_f32: bad geometry");
+  RMBX_CHECK_ARG(C == 64 || C == 128 || C == 256 || C == 512,
+                 "rmbx_conv3x3_winograd4_f32: C=%d (implemented: 64, 128, 256, 512)", C);
+  RMBX_CHECK_ARG((((uintptr_t)in | (uintptr_t)u_packed | (uintptr_t)out | (uintptr_t)residual) & 15) == 0,
+                 "rmbx_conv3x3_winograd4_f32: tensors must be 16-byte aligned");
+  RMBX_CHECK_ARG(in != out && (residual == nullptr || residual != out),
+                 "rmbx_conv3x3_winograd4_f32: the output must not alias the input or the residual");
+  if (N == 0) return RMBX_OK;
+  rmbx::WinoArgs a;
+  a.in = in;
+  a.u = u_packed;
+  a.bias = bias;
+  a.res = residual;
+  a.out = out;
+  a.N = N;
+  a.H = H;
+  a.W = W;
+  a.C = C;
+  a.relu = relu;
+  a.tiles_x = (W + 3) / 4;
+  a.tiles_y = (H + 3) / 4;
+  const long long ntiles = (long long)N * a.tiles_x * a.tiles_y;
+  RMBX_CHECK_ARG(ntiles + rmbx::W4_TILES < (1ll << 31) && (long long)N * H * W * C < (1ll << 30),
+                 "rmbx_conv3x3_winograd4_f32: tensor too large for 32-bit byte offsets");
+  a.ntiles = (int)ntiles;
+  a.ntb = (a.ntiles + rmbx::W4_TILES - 1) / rmbx::W4_TILES;
+  a.ncb = C / rmbx::W4_COUT;
+  a.nk = C / rmbx::W4_KC;
+  a.stagger = 0;
+  const char* dbg_env = std::getenv("RMBX_WINO_DBG");
+  a.dbg = dbg_env ? std::atoi(dbg_env) : 0;
+  a.nk_log2 = 0;
+  while ((1 << a.nk_log2) < a.nk) ++a.nk_log2;
+  int grid = rmbx::device_cus();
+  grid = grid < 8 ? 8 : grid - grid % 8;
+  const dim3 g(grid), blk(rmbx::WG_THREADS);
+  hipStream_t st = (hipStream_t)stream;
+  switch (a.dbg) {
+    case 0: hipLaunchKernelGGL(rmbx::wino4_f32_kernel<0>, g, blk, 0, st, a); break;
+    case 1: hipLaunchKernelGGL(rmbx::wino4_f32_kernel<1>, g, blk, 0, st, a); break;
+    case 2: hipLaunchKernelGGL(rmbx::wino4_f32_kernel<2>, g, blk, 0, st, a); break;
+    case 4: hipLaunchKernelGGL(rmbx::wino4_f32_kernel<4>, g, blk, 0, st, a); break;
+    case 8: hipLaunchKernelGGL(rmbx::wino4_f32_kernel<8>, g, blk, 0, st, a); break;
+    case 14: hipLaunchKernelGGL(rmbx::wino4_f32_kernel<14>, g, blk, 0, st, a); break;
+    default: RMBX_CHECK_ARG(false, "rmbx_conv3x3_winograd4_f32: RMBX_WINO_DBG=%d not instantiated", a.dbg);
   }
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;

@@ -535,6 +535,7 @@ def conv2d_nhwc_f32_supported(cin, cout, kernel_size, stride, padding):
 _WINO_G = ((1.0, 0.0, 0.0), (0.5, 0.5, 0.5), (0.5, -0.5, 0.5), (0.0, 0.0, 1.0))
 WINOGRAD_F32_CHANNELS = (64, 128, 256, 512)
 WINOGRAD_MAX_ELEMS = (1 << 31) - 1  # per launch (32-bit element offsets in the kernel)
+WINOGRAD4_MAX_ELEMS = (1 << 30) - 1  # per launch (32-bit byte offsets of the F(4x4) buffer loads)
 
 
 def pack_winograd_f32(weight):
@@ -572,6 +573,48 @@ def conv3x3_winograd_f32(x, u_packed, bias, relu=False, res=None):
         xs, os_ = x[i0:i1], out[i0:i1]
         rs = None if res is None else res[i0:i1]
         N.call("rmbx_conv3x3_winograd_f32", N.ptr(xs), N.ptr(u_packed), N.ptr(bias), N.ptr(rs), N.ptr(os_),
+               i1 - i0, H, W, C, int(bool(relu)), N.stream_ptr())
+    return out
+
+
+_WINO4_G = ((0.25, 0.0, 0.0), (-1 / 6, -1 / 6, -1 / 6), (-1 / 6, 1 / 6, -1 / 6), (1 / 24, 1 / 12, 1 / 6),
+            (1 / 24, -1 / 12, 1 / 6), (0.0, 0.0, 1.0))
+
+
+def pack_winograd4_f32(weight):
+    """3x3 conv weight [C, C, 3, 3] -> the Winograd F(4x4, 3x3) filter transform U = G g G^T
+    (computed in f64, rounded once to f32) in the LDS image rmbx_conv3x3_winograd4_f32 stages per
+    K chunk: [C/64 channel blocks][C/4 chunks][36 positions][64 output channels][4 input channels]."""
+    C = weight.shape[0]
+    if tuple(weight.shape) != (C, C, 3, 3) or C not in WINOGRAD_F32_CHANNELS:
+        raise ValueError(f"pack_winograd4_f32: weight {tuple(weight.shape)} is not [C, C, 3, 3] with C in {WINOGRAD_F32_CHANNELS}")
+    w = weight.detach().to(torch.float64)
+    G = torch.tensor(_WINO4_G, dtype=torch.float64, device=w.device)
+    U = torch.einsum("xa,oiab,yb->xyoi", G, w, G).reshape(36, C // 64, 64, C // 4, 4)  # [p][cb][co][k][c]
+    return U.permute(1, 3, 0, 2, 4).contiguous().to(torch.float32)
+
+
+def conv3x3_winograd4_f32(x, u_packed, bias, relu=False, res=None):
+    """relu?(conv2d(x, w, stride 1, pad 1) + bias + res) by rmbx_conv3x3_winograd4_f32 (Winograd
+    F(4x4, 3x3) on f32 MFMA): as conv3x3_winograd_f32 with u_packed = pack_winograd4_f32(w)."""
+    _chk_nhwc(x, "x")
+    n, C, H, W = x.shape
+    if x.dtype != torch.float32 or C not in WINOGRAD_F32_CHANNELS:
+        raise ValueError(f"conv3x3_winograd4_f32: x must be f32 with C in {WINOGRAD_F32_CHANNELS}")
+    _chk(u_packed, torch.float32, (C // 64, C // 4, 36, 64, 4), "u_packed")
+    _chk(bias, torch.float32, (C,), "bias")
+    if res is not None:
+        _chk_nhwc(res, "res")
+        if tuple(res.shape) != tuple(x.shape) or res.dtype != torch.float32:
+            raise ValueError("res must match the output")
+    out = torch.empty_like(x, memory_format=torch.channels_last)
+    # the kernel addresses the input with 32-bit byte offsets (buffer loads): slices of whole images
+    per = max(1, WINOGRAD4_MAX_ELEMS // (H * W * C))
+    for i0 in range(0, n, per):
+        i1 = min(n, i0 + per)
+        xs, os_ = x[i0:i1], out[i0:i1]
+        rs = None if res is None else res[i0:i1]
+        N.call("rmbx_conv3x3_winograd4_f32", N.ptr(xs), N.ptr(u_packed), N.ptr(bias), N.ptr(rs), N.ptr(os_),
                i1 - i0, H, W, C, int(bool(relu)), N.stream_ptr())
     return out
 

@@ -123,16 +123,23 @@ class _FusedConv(nn.Module):
         return (c.in_channels == c.out_channels and c.in_channels in K.WINOGRAD_F32_CHANNELS
                 and tuple(c.kernel_size) == (3, 3) and c.stride[0] == 1 and c.padding[0] == 1)
 
+    # Winograd tile of the f32 stride-1 convs: "f2" = F(2x2, 3x3) (rmbx_conv3x3_winograd_f32), "f4" =
+    # F(4x4, 3x3) (rmbx_conv3x3_winograd4_f32: 2.25 instead of 4 products per output); env
+    # RMBX_WINO_TILE
+    WINO_TILE = os.environ.get("RMBX_WINO_TILE", "f2")
+
     def wino(self, x, relu, res=None, bias=None):
-        """f32 conv + bias (+ res) (+ ReLU) in one rmbx Winograd F(2x2, 3x3) launch; the packed
-        filter transform is cached per weight storage."""
+        """f32 conv + bias (+ res) (+ ReLU) in one rmbx Winograd launch; the packed filter
+        transform is cached per weight storage."""
         w = self.conv.weight
-        key = (w.data_ptr(), w.dtype, w.device)
+        f4 = self.WINO_TILE == "f4"
+        key = (w.data_ptr(), w.dtype, w.device, f4)
         cache = self.__dict__.get("_wino")
         if cache is None or cache[0] != key:
-            cache = (key, K.pack_winograd_f32(w))
+            cache = (key, K.pack_winograd4_f32(w) if f4 else K.pack_winograd_f32(w))
             self.__dict__["_wino"] = cache
-        return K.conv3x3_winograd_f32(x, cache[1], self.bias_f32() if bias is None else bias, relu=relu, res=res)
+        fn = K.conv3x3_winograd4_f32 if f4 else K.conv3x3_winograd_f32
+        return fn(x, cache[1], self.bias_f32() if bias is None else bias, relu=relu, res=res)
 
 
 class _FusedBlock(nn.Module):
