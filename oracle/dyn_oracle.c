@@ -1990,7 +1990,24 @@ static void sensors(Data* d) {
 /* ------------------------------------------------------------------------------------------
  * implicitfast integration + mj_step
  * ---------------------------------------------------------------------------------------- */
+void orc_forward(void* p);
+
+/* mj_step after mj_forward (MuJoCo 3.1.6 [ext]): mj_checkAcc on the forward (constraint-solver)
+ * qacc -- a non-finite or |qacc| > 1e10 entry resets the data (mj_resetData: qpos0, zero velocity
+ * / warm start / ctrl, time 0) and runs mj_forward on the reset state -- then the implicitfast
+ * integration of this substep, from the reset state when there was one. */
 static void integrate(Data* d) {
+  for (int k = 0; k < d->m->nv; k++)
+    if (!isfinite(d->qacc[k]) || fabs(d->qacc[k]) > 1e10) {
+      memcpy(d->qpos, d->m->qpos0, sizeof(double) * d->m->nq);
+      memset(d->qvel, 0, sizeof(double) * d->m->nv);
+      memset(d->qacc_ws, 0, sizeof(double) * d->m->nv);
+      memset(d->ctrl, 0, sizeof(double) * d->m->nu);
+      d->time = 0;
+      d->bad = d->substep;
+      orc_forward(d);
+      break;
+    }
   const rmbx_model* m = d->m;
   int nv = m->nv;
   double h = m->timestep;
@@ -2015,17 +2032,6 @@ static void integrate(Data* d) {
   cholesky(d->A, nv);
   for (int k = 0; k < nv; k++) d->tmpv[k] = d->qfrc_smooth[k] + d->qfrc_constraint[k];
   chol_solve(d->A, nv, d->tmpv, d->qacc);
-  for (int k = 0; k < nv; k++)
-    if (!isfinite(d->qacc[k]) || fabs(d->qacc[k]) > 1e10) {
-      /* MuJoCo's mj_checkAcc -> mj_resetData: qpos0, zero velocity / warm start / ctrl, time 0 */
-      memcpy(d->qpos, m->qpos0, sizeof(double) * m->nq);
-      memset(d->qvel, 0, sizeof(double) * nv);
-      memset(d->qacc_ws, 0, sizeof(double) * nv);
-      memset(d->ctrl, 0, sizeof(double) * m->nu);
-      d->time = 0;
-      d->bad = d->substep;
-      return;
-    }
   for (int k = 0; k < nv; k++) d->qvel[k] += h * d->qacc[k];
   memcpy(d->qacc_ws, d->qacc, sizeof(double) * nv);
   for (int j = 0; j < m->njnt; j++) {

@@ -3213,17 +3213,21 @@ __device__ void solver_integrate(Env& e, SolverShared& S, double* a, int bi, int
   for (int k = tid; k < NVP; k += SOLVER_THREADS)
     S.tmp[k] = k < nv ? W(qfrc_smooth)[k] + W(qfrc_constraint)[k] : 0.0;
   lds_sync();
-  blk_cholesky_fwd(a, bi, bj, own, NB, S.tmp, S, tid);
-  blk_solve_back(a, bi, bj, own, NB, S.a, S, tid);
+  // MuJoCo's divergence guard (mj_step -> mj_checkAcc) on the forward (constraint-solver) qacc
   bool bad = false;
   for (int k = tid; k < nv; k += SOLVER_THREADS) {
-    const double acc = S.a[k];
+    const double acc = W(qacc)[k];
     if (!isfinite(acc) || fabs(acc) > 1e10) bad = true;
   }
+  blk_cholesky_fwd(a, bi, bj, own, NB, S.tmp, S, tid);
+  blk_solve_back(a, bi, bj, own, NB, S.a, S, tid);
   if (block_sum_i(bad ? 1 : 0, S, tid)) {
-    // MuJoCo's divergence guard (mj_checkAcc -> mj_resetData): the model's qpos0, zero velocity,
-    // warm start and ctrl, time 0, in this substep (the remaining substeps of the env-step run
-    // from it, with ctrl 0 as in MuJoCo); stats[3] = the 1-based substep of the reset
+    // mj_resetData: the model's qpos0, zero velocity, warm start and ctrl, time 0 (ctrl stays 0
+    // for the rest of the env-step, as in MuJoCo); stats[3] = the 1-based substep of the reset.
+    // MuJoCo then runs mj_forward on the reset state and integrates this substep from it: here
+    // the remaining substeps run from the reset state and the engine adds one masked substep
+    // after the env-step (launch(): redo pass) for the envs that reset, so each env ends the
+    // env-step with its full count of integrated substeps and MuJoCo's time.
     for (int k = tid; k < m.nq; k += SOLVER_THREADS) e.qpos[k] = m.qpos0[k];
     for (int k = tid; k < nv; k += SOLVER_THREADS) {
       e.qvel[k] = 0.0;
@@ -3274,6 +3278,7 @@ struct KArgs {
   int nsub;
   int sub;  // 1-based substep index of this launch
   int integrate_flag;
+  int redo;  // the extra substep after an env-step: only envs reset during it (stats[3] != 0) run
   unsigned long long* prof;  // optional [n_env][16] per-stage cycle sums (diagnostic)
   const int32_t* subtree_end;  // [nbody] end of each body's DFS subtree id range
   const double* hBblk;         // implicitfast: h * (damping + kv terms), packed like Mblk
@@ -3323,6 +3328,9 @@ __global__ void __launch_bounds__(64) front_kernel(KArgs args) {
   if (args.active && !args.active[env]) return;
   Env e;
   make_env(args, env, e);
+  if (args.redo && e.stats[3] == 0) return;
+  // a new env-step clears the divergence-reset marker (read by the host between env-steps)
+  if (args.integrate_flag && args.sub == 1 && lane == 0) e.stats[3] = 0;
   e.sh = front_smem;
   e.subtree_end = args.subtree_end;
   __shared__ int s_anc[MAX_BODY];
@@ -3359,6 +3367,7 @@ __global__ void __launch_bounds__(SOLVER_THREADS, 4) solver_kernel(KArgs args) {
   if (args.active && !args.active[env]) return;
   Env e;
   make_env(args, env, e);
+  if (args.redo && e.stats[3] == 0) return;
   const int NB = (args.m.nv + 3) / 4;
   int bi = 0, bj = 0;
   const bool own = tid < NB * (NB + 1) / 2;
@@ -3752,6 +3761,7 @@ static int launch(rmbx_engine* eng, int nsub, int integ, const uint8_t* active, 
   a.n_env = eng->n_env;
   a.nsub = nsub;
   a.integrate_flag = integ;
+  a.redo = 0;
   a.prof = prof;
   a.subtree_end = eng->subtree_end;
   a.tree_rounds = eng->tree_rounds;
@@ -3760,6 +3770,18 @@ static int launch(rmbx_engine* eng, int nsub, int integ, const uint8_t* active, 
   const int reps = integ ? nsub : 1;
   for (int s = 0; s < reps; s++) {
     a.sub = s + 1;
+    const size_t front_lds = front_kernel_lds_bytes(eng->host);
+    hipLaunchKernelGGL(front_kernel, dim3(eng->n_env), dim3(64), front_lds, st, a);
+    RMBX_CHECK_LAUNCH();
+    hipLaunchKernelGGL(solver_kernel, dim3(eng->n_env), dim3(SOLVER_THREADS), 0, st, a);
+    RMBX_CHECK_LAUNCH();
+  }
+  if (integ) {
+    // redo pass: one more substep (forward + integration) for the envs that reset during this
+    // env-step, the substep MuJoCo integrates from the reset state; every other env exits at once
+    a.sub = nsub + 1;
+    a.redo = 1;
+    a.prof = nullptr;
     const size_t front_lds = front_kernel_lds_bytes(eng->host);
     hipLaunchKernelGGL(front_kernel, dim3(eng->n_env), dim3(64), front_lds, st, a);
     RMBX_CHECK_LAUNCH();

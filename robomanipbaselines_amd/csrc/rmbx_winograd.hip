@@ -322,6 +322,7 @@ __global__ void __launch_bounds__(WG_THREADS, 1) wino_f32_kernel(WinoArgs a) {
 // LDS: U and V double buffered, 108 KiB.  Persistent blocks and the per-XCD output-channel block
 // as F(2x2).
 // =============================================================================================
+__device__ float g_wino_zero[4];  // zero-initialised: the pixels outside the image
 constexpr int W4_TILES = 32;
 constexpr int W4_COUT = 64;
 constexpr int W4_KC = 4;
@@ -329,7 +330,7 @@ constexpr int W4_UCH = 36 * W4_COUT * W4_KC;   // 9216 floats
 constexpr int W4_VCH = 36 * W4_TILES * W4_KC;  // 4608 floats
 static_assert((2 * W4_UCH + 2 * W4_VCH) * 4 <= 160 * 1024, "W4 LDS");
 
-template <int DBG>
+template <int DBG, int SPLIT>
 __global__ void __launch_bounds__(WG_THREADS, 1) wino4_f32_kernel(WinoArgs a) {
   __shared__ __attribute__((aligned(16))) float smem[2 * W4_UCH + 2 * W4_VCH];  // sU[2], sV[2]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -347,17 +348,13 @@ __global__ void __launch_bounds__(WG_THREADS, 1) wino4_f32_kernel(WinoArgs a) {
   const int nunits = (a.ntb - r + per_cb - 1) / per_cb;
   const int nsteps = nunits << a.nk_log2;
 
-  // loader thread: window of tile lt (0..31), channel lc (0..3) of the chunk, by buffer loads: the
-  // lane's window origin in the 32-bit voffset, each pixel's (uniform) offset in soffset, so no
-  // per-load address arithmetic; offsets before the buffer or past its end (the top / bottom halo
-  // of the batch) read 0, and the pixels outside their image are zeroed by the in-image mask in
-  // the column pass
+  // loader thread: window of tile lt (0..31), channel lc (0..3) of the chunk; out-of-image pixels
+  // read a device zero, so the transform needs no mask (measured slower: buffer loads with the
+  // in-image mask applied in the column pass, 9.2 vs 8.1 ms at 64 channels)
   const int lt = (tid & 127) >> 2, lc = tid & 3;
   float xr[36];
   uint32_t ld_mlo = 0, ld_mhi = 0;  // in-image bits of the 36 window pixels
   int ld_unit = -1, ld_o0 = 0;
-  const __amdgpu_buffer_rsrc_t in_rsrc =
-      __builtin_amdgcn_make_buffer_rsrc((void*)a.in, 0, (int)((uint32_t)a.N * a.H * a.W * a.C * 4u), 0x00020000);
   auto tile_pos = [&](int t, int& img, int& ty, int& tx) {
     const int q = t / a.tiles_x;
     tx = t - q * a.tiles_x;
@@ -395,11 +392,13 @@ __global__ void __launch_bounds__(WG_THREADS, 1) wino4_f32_kernel(WinoArgs a) {
           ld_mhi |= bit << (i - 32);
       }
     }
-    const int voff = (ld_o0 + k * W4_KC) * 4;
+    const float* base = a.in + ld_o0 + k * W4_KC;
 #pragma unroll
-    for (int i = 0; i < 36; ++i)
-      xr[i] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(
-                                            in_rsrc, voff, ((i / 6) * a.W + (i % 6)) * a.C * 4, 0));
+    for (int i = 0; i < 36; ++i) {
+      const uint32_t bit = i < 32 ? (ld_mlo >> i) & 1u : (ld_mhi >> (i - 32)) & 1u;
+      const float* src = bit ? base + ((i / 6) * a.W + (i % 6)) * a.C : &g_wino_zero[0];
+      xr[i] = *src;
+    }
   };
   auto bt6 = [](float d0, float d1, float d2, float d3, float d4, float d5, float* v) {
     v[0] = 4.f * d0 - 5.f * d2 + d4;
@@ -409,16 +408,10 @@ __global__ void __launch_bounds__(WG_THREADS, 1) wino4_f32_kernel(WinoArgs a) {
     v[4] = (d4 - d2) - 2.f * (d3 - d1);
     v[5] = 4.f * d1 - 5.f * d3 + d5;
   };
-  auto col_piece = [&](int x) {  // mask, then B^T down window column x, in place
+  auto col_piece = [&](int x) {  // B^T down window column x, in place
     if (DBG & 4) return;
-    float d[6], v[6];
-#pragma unroll
-    for (int y = 0; y < 6; ++y) {
-      const int i = 6 * y + x;
-      const uint32_t bit = i < 32 ? (ld_mlo >> i) & 1u : (ld_mhi >> (i - 32)) & 1u;
-      d[y] = bit ? xr[i] : 0.f;
-    }
-    bt6(d[0], d[1], d[2], d[3], d[4], d[5], v);
+    float v[6];
+    bt6(xr[x], xr[6 + x], xr[12 + x], xr[18 + x], xr[24 + x], xr[30 + x], v);
 #pragma unroll
     for (int y = 0; y < 6; ++y) xr[6 * y + x] = v[y];
   };
@@ -437,6 +430,7 @@ __global__ void __launch_bounds__(WG_THREADS, 1) wino4_f32_kernel(WinoArgs a) {
     const bool more = c + 1 < nsteps;
     if (!loader && more) load_u(c + 1);
     const bool tf = loader && lgrp == ((c + 1) & 1) && c + 1 < nsteps;  // V(c + 1) -> other buffer
+    const bool cols2 = SPLIT && loader && lgrp == (c & 1) && c + 2 < nsteps;  // SPLIT: columns of V(c + 2)
     const float* Ub = smem + buf * W4_UCH + cq * 64 + li * 4 + lq;
     const float* Vb = smem + 2 * W4_UCH + buf * W4_VCH + tg * 64 + li * 4 + lq;
     float av = Ub[0], bv = Vb[0];
@@ -451,12 +445,19 @@ __global__ void __launch_bounds__(WG_THREADS, 1) wino4_f32_kernel(WinoArgs a) {
         acc[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[p], 0, 0, 0);
       else
         acc[p][0] += av * bv;
-      if (tf && p >= 8 && p <= 18 && (p & 1) == 0) col_piece((p - 8) >> 1);
-      if (tf && p >= 20 && (p - 20) % 3 == 0) row_piece(buf ^ 1, (p - 20) / 3);
+      if (!SPLIT) {
+        if (tf && p >= 8 && p <= 18 && (p & 1) == 0) col_piece((p - 8) >> 1);
+        if (tf && p >= 20 && (p - 20) % 3 == 0) row_piece(buf ^ 1, (p - 20) / 3);
+      } else {
+        // rows of V(c + 1) over the first half, columns of V(c + 2) over the second
+        if (tf && p >= 2 && p <= 17 && (p - 2) % 3 == 0) row_piece(buf ^ 1, (p - 2) / 3);
+        if (cols2 && p >= 20 && (p - 20) % 3 == 0) col_piece((p - 20) / 3);
+      }
       av = an;
       bv = bn;
     }
-    if (loader && lgrp == (c & 1) && c + 2 < nsteps) load_window(c + 2);
+    if (!SPLIT && loader && lgrp == (c & 1) && c + 2 < nsteps) load_window(c + 2);
+    if (SPLIT && tf && c + 3 < nsteps) load_window(c + 3);  // the group's next window
     // U waves: the LDS-DMA of U(c + 1) has landed (loader waves keep their window loads in flight
     // across the LDS-only barrier)
     if (!loader) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -474,6 +475,10 @@ __global__ void __launch_bounds__(WG_THREADS, 1) wino4_f32_kernel(WinoArgs a) {
       for (int x = 0; x < 6; ++x) col_piece(x);
 #pragma unroll
       for (int y = 0; y < 6; ++y) row_piece(0, y);
+      if (SPLIT && nsteps > 2) load_window(2);
+    } else if (SPLIT) {
+#pragma unroll
+      for (int x = 0; x < 6; ++x) col_piece(x);
     }
   }
   lds_barrier();
@@ -649,15 +654,23 @@ extern "C" int rmbx_conv3x3_winograd4_f32(const float* in, const float* u_packed
   grid = grid < 8 ? 8 : grid - grid % 8;
   const dim3 g(grid), blk(rmbx::WG_THREADS);
   hipStream_t st = (hipStream_t)stream;
+  const char* sp_env = std::getenv("RMBX_WINO4_SPLIT");
+  const int split = sp_env ? std::atoi(sp_env) : 0;
+#define RMBX_W4_LAUNCH(D)                                                  \
+  if (split)                                                               \
+    hipLaunchKernelGGL((rmbx::wino4_f32_kernel<D, 1>), g, blk, 0, st, a);  \
+  else                                                                     \
+    hipLaunchKernelGGL((rmbx::wino4_f32_kernel<D, 0>), g, blk, 0, st, a);
   switch (a.dbg) {
-    case 0: hipLaunchKernelGGL(rmbx::wino4_f32_kernel<0>, g, blk, 0, st, a); break;
-    case 1: hipLaunchKernelGGL(rmbx::wino4_f32_kernel<1>, g, blk, 0, st, a); break;
-    case 2: hipLaunchKernelGGL(rmbx::wino4_f32_kernel<2>, g, blk, 0, st, a); break;
-    case 4: hipLaunchKernelGGL(rmbx::wino4_f32_kernel<4>, g, blk, 0, st, a); break;
-    case 8: hipLaunchKernelGGL(rmbx::wino4_f32_kernel<8>, g, blk, 0, st, a); break;
-    case 14: hipLaunchKernelGGL(rmbx::wino4_f32_kernel<14>, g, blk, 0, st, a); break;
+    case 0: RMBX_W4_LAUNCH(0) break;
+    case 1: RMBX_W4_LAUNCH(1) break;
+    case 2: RMBX_W4_LAUNCH(2) break;
+    case 4: RMBX_W4_LAUNCH(4) break;
+    case 8: RMBX_W4_LAUNCH(8) break;
+    case 14: RMBX_W4_LAUNCH(14) break;
     default: RMBX_CHECK_ARG(false, "rmbx_conv3x3_winograd4_f32: RMBX_WINO_DBG=%d not instantiated", a.dbg);
   }
+#undef RMBX_W4_LAUNCH
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
 }

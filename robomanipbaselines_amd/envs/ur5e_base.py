@@ -143,18 +143,16 @@ class BatchedMujocoUR5eEnvBase:
 
     def _reset_bad_states(self):
         """MuJoCo's divergence guard (mj_step -> mj_checkAcc -> mj_resetData, [ext] mujoco 3.1.6):
-        the physics kernel resets an env whose qacc went non-finite or above 1e10 inside the
-        substep where it happened (the model's qpos0, zero velocity / warm start / ctrl, time 0;
-        the remaining substeps run from there) and reports that substep in stats[:, 3].  Here the
-        resets are counted per env (MuJoCo's mjWARN_BADQACC counter) and an env reset in the
-        last substep is forwarded again, so its frames describe the reset state as after MuJoCo's
-        post-reset mj_forward.  Device-side masked updates, no host sync."""
+        the physics kernel resets an env whose forward qacc went non-finite or above 1e10 inside
+        the substep where it happened (the model's qpos0, zero velocity / warm start / ctrl, time
+        0), the env-step integrates its full count of substeps from the reset state (the engine's
+        redo pass) and the substep of the reset is reported in stats[:, 3].  Here the resets are
+        counted per env (MuJoCo's mjWARN_BADQACC counter) and the marker consumed.  Device-side,
+        no host sync."""
         e = self.engine
         sub = e.stats[:, 3]
         self.bad_resets += (sub != 0).to(torch.int32)
-        last = (sub == self.frame_skip).to(torch.uint8)
         e.stats[:, 3] = 0
-        e.forward(active=last)
 
     def get_time(self):
         return self.engine.time

@@ -41,7 +41,10 @@ for C, H, W in ((64, 120, 160), (128, 60, 80), (256, 30, 40), (512, 15, 20)):
     flops = 2.0 * n * H * W * C * C * 9
     out = {}
     for name, groups, fn in (("F2", None, lambda: K.conv3x3_winograd_f32(x, u2, b, relu=True, res=r)),
-                             ("F4", "4", lambda: K.conv3x3_winograd4_f32(x, u4, b, relu=True, res=r))):
+                             ("F4", "0", lambda: K.conv3x3_winograd4_f32(x, u4, b, relu=True, res=r)),
+                             ("F4split", "1", lambda: K.conv3x3_winograd4_f32(x, u4, b, relu=True, res=r))):
+        if groups:
+            os.environ["RMBX_WINO4_SPLIT"] = groups
         y = fn()
         err = ((y[:2] - ref).abs().max() / ref.abs().max()).item()
         ms = timed(fn)
@@ -58,5 +61,5 @@ for C, H, W in ((64, 120, 160), (128, 60, 80), (256, 30, 40), (512, 15, 20)):
             os.environ["RMBX_WINO_DBG"] = "0"
             line += "  [" + ", ".join(parts) + "]"
         print(line, flush=True)
-    print(f"  speedup F4 vs F2: {out['F2'] / out['F4']:.2f}x", flush=True)
+    print(f"  speedup vs F2: F4 {out['F2'] / out['F4']:.2f}x, F4split {out['F2'] / out['F4split']:.2f}x", flush=True)
     del x, r

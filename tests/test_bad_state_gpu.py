@@ -1,9 +1,10 @@
 """MuJoCo's divergence guard on the batched env (mj_step -> mj_checkAcc -> mj_resetData, [ext]
 mujoco 3.1.6; the reference inherits it through gymnasium do_simulation, MujocoEnvBase.py:82-83):
 an env driven to a non-finite qacc is reset inside that substep to the model's qpos0 with zero
-velocity, warm start, ctrl and time, the remaining substeps of the env-step run from there (ctrl
-0, as MuJoCo's do_simulation leaves it), the reset is counted, and the other envs are untouched
-bit for bit.  The C oracle restates the same guard (CPU test); the engine must match it."""
+velocity, warm start, ctrl and time, forwarded and integrated from there in the same substep (as
+mj_step does after mj_checkAcc; the engine's redo pass), the remaining substeps of the env-step
+run from there (ctrl 0, as MuJoCo's do_simulation leaves it), the reset is counted, and the other
+envs are untouched bit for bit.  The C oracle restates the same guard (CPU test); the engine must match it."""
 
 import numpy as np
 import pytest
@@ -35,7 +36,10 @@ def test_oracle_resets_diverged_state_like_mujoco():
     assert env.step(8) == 1  # reset in the first substep
     t, qpos, qvel, _ = env.state()
     h = float(a["_timestep"])
-    assert t == sum([h] * 7)  # time restarts at 0 and runs the 7 remaining substeps
+    want = 0.0
+    for _ in range(8):  # reset + mj_forward + integration in substep 1, then the 7 remaining
+        want += h
+    assert t == want
     assert np.isfinite(qpos).all() and np.isfinite(qvel).all()
     assert env.step(8) == 0  # ctrl is 0 after the reset: no further divergence
 
