@@ -71,6 +71,13 @@ struct rmbx_engine {
   const int32_t* subtree_end;  // device [nbody]: DFS subtree ranges for the tree passes
   int tree_rounds;             // ceil(log2(max body depth + 1)) (solver pointer jumping)
   const double* hBblk;         // device: h * (damping + actuator velocity gains), packed 4x4 blocks
+  // two-level broadphase (models with long runs of same-body-pair geom pairs, e.g. the Pick
+  // scene's convex-hull meshes): nprun = 0 disables it
+  int nprun;
+  const int32_t* prun_start;   // device [nprun + 1]: pair range of each run
+  const int32_t* prun_body;    // device [nprun][2]: the run's two bodies
+  const double* prun_margin;   // device [nprun]: largest pair margin of the run
+  const int32_t* body_cgeom;   // device [nbody][2]: first collision geom, count
   std::vector<void*> allocations;
   rmbx::Layout L;
   int n_env;
@@ -1558,39 +1565,153 @@ __device__ void make_frame(const double* n, double* F) {
 // index, narrow-phase class, contact count; at most collision_cap(npair), the same cap as the
 // oracle's) and the class-major list of survivor indices.
 #define RMBX_MAX_CANDIDATES 2048
+// Two-level broadphase (models whose candidate pairs come in long runs with the same two bodies,
+// e.g. the Pick scene's 32-hull meshes: 35,591 pairs in 1,301 runs): a run is tested first on its
+// bodies' AABBs (the union of their collision geoms' broadphase boxes, a plane geom making it
+// infinite) grown by the run's largest margin, and only the pairs of the runs that pass are
+// classified.  Every pair pair_class accepts lies in a run that passes (its geoms' boxes lie in
+// their bodies' boxes, its margin is at most the run's, and rounding is monotone), so the
+// survivors -- and with them the contacts and their order -- are exactly the one-level pass's.
+struct PairRuns {
+  int n;                      // runs; 0: one-level broadphase
+  const int32_t* start;       // [n + 1] pair range of each run
+  const int32_t* body;        // [n][2] the run's two bodies
+  const double* margin;       // [n] largest pair margin of the run
+  const int32_t* body_cgeom;  // [nbody][2] first collision geom of the body, count
+};
 struct CollisionLds {
   double* geom;
   int32_t* spair;
   int16_t* list;
   uint8_t* count;
   uint8_t* scls;
+  double* bbox;      // [nbody][6] body AABB (two-level only)
+  int32_t* run_pre;  // [65] flat pair offsets of the kept runs of a 64-run chunk (two-level only)
+  int32_t* run_id;   // [64] kept runs of the chunk, in order (two-level only)
 };
 __host__ __device__ __forceinline__ int collision_cap(int npair) {
   return npair < RMBX_MAX_CANDIDATES ? npair : RMBX_MAX_CANDIDATES;
 }
-__host__ __device__ __forceinline__ size_t collision_lds_doubles(int ngeom, int npair) {
-  return 8 * (size_t)ngeom + (size_t)collision_cap(npair) + 2;  // 8 bytes per survivor
+__host__ __device__ __forceinline__ size_t collision_lds_doubles(int ngeom, int npair, int nbody, int nprun) {
+  // 8 bytes per survivor; two-level: 6 doubles per body + 129 int32 of run-chunk bookkeeping
+  const size_t runs = nprun > 0 ? 6 * (size_t)nbody + 65 : 0;
+  return 8 * (size_t)ngeom + (size_t)collision_cap(npair) + 2 + runs;
 }
 __host__ __device__ __forceinline__ size_t collision_lds_free_doubles(int nb, int nv) {
   return 28 * (size_t)nb + 6 * (size_t)nv;  // cvel, cacc, cfrc, cdofdot, cinert
 }
 // (cdof, still live, follows the free region: a model that does not fit takes its own space)
-static inline size_t front_kernel_lds_bytes(const rmbx_model& h) {
-  const size_t need = collision_lds_doubles(h.ngeom, h.npair);
+static inline size_t front_kernel_lds_bytes(const rmbx_model& h, int nprun) {
+  const size_t need = collision_lds_doubles(h.ngeom, h.npair, h.nbody, nprun);
   const size_t extra = need <= collision_lds_free_doubles(h.nbody, h.nv) ? 0 : need;
   return (front_lds_doubles(h.nbody, h.nv) + extra) * sizeof(double);
 }
-__device__ __forceinline__ CollisionLds collision_lds(const Env& e) {
+__device__ __forceinline__ CollisionLds collision_lds(const Env& e, const PairRuns& pr) {
   const rmbx_model& m = *e.m;
   CollisionLds cl;
-  const bool fits = collision_lds_doubles(m.ngeom, m.npair) <= collision_lds_free_doubles(m.nbody, m.nv);
+  const bool fits = collision_lds_doubles(m.ngeom, m.npair, m.nbody, pr.n) <= collision_lds_free_doubles(m.nbody, m.nv);
   const int cap = collision_cap(m.npair);
   cl.geom = fits ? e.sh + 16 * m.nbody : e.sh + front_lds_doubles(m.nbody, m.nv);
   cl.spair = reinterpret_cast<int32_t*>(cl.geom + 8 * m.ngeom);
   cl.list = reinterpret_cast<int16_t*>(cl.spair + cap);
   cl.count = reinterpret_cast<uint8_t*>(cl.list + cap);
   cl.scls = cl.count + cap;
+  // (cap + 2 doubles hold spair, list, count, scls: 8 bytes per survivor)
+  cl.bbox = cl.geom + 8 * m.ngeom + cap + 2;
+  cl.run_pre = reinterpret_cast<int32_t*>(cl.bbox + 6 * m.nbody);
+  cl.run_id = cl.run_pre + 65;
   return cl;
+}
+
+// the two-level broadphase (PairRuns): survivors in pair order, at most cap (inlined: an
+// out-of-line call made the front kernel save its live registers around it, +1.5 KiB of scratch)
+__device__ __forceinline__ int broadphase_runs(const Env& e, int lane, const CollisionLds& cl,
+                                                         const PairRuns& pr, int cap) {
+  const rmbx_model& m = *e.m;
+  const unsigned long long below = (1ull << lane) - 1;
+  int nsurv = 0;
+  // level 1: body AABBs (lane per body), then the runs on them, kept runs compacted in order
+  // with the flat offsets of their pairs
+  for (int b = lane; b < m.nbody; b += 64) {
+    double lx = 1e300, ly = 1e300, lz = 1e300, hx = -1e300, hy = -1e300, hz = -1e300;
+    bool inf = false;
+    const int g0 = pr.body_cgeom[2 * b], gn = pr.body_cgeom[2 * b + 1];
+    for (int g = g0; g < g0 + gn; g++) {
+      const double* r = cl.geom + 8 * g;
+      if (m.geom_ctype[g] < 0) continue;  // visual only
+      if ((int)r[7] == RMBX_GEOM_PLANE) {
+        inf = true;
+        continue;
+      }
+      lx = fmin(lx, r[0] - r[3]);
+      ly = fmin(ly, r[1] - r[4]);
+      lz = fmin(lz, r[2] - r[5]);
+      hx = fmax(hx, r[0] + r[3]);
+      hy = fmax(hy, r[1] + r[4]);
+      hz = fmax(hz, r[2] + r[5]);
+    }
+    double* bb = cl.bbox + 6 * b;
+    bb[0] = inf ? -1e300 : lx;
+    bb[1] = inf ? -1e300 : ly;
+    bb[2] = inf ? -1e300 : lz;
+    bb[3] = inf ? 1e300 : hx;
+    bb[4] = inf ? 1e300 : hy;
+    bb[5] = inf ? 1e300 : hz;
+  }
+  sync();
+  // runs in chunks of 64: the chunk's kept runs are compacted in order with the flat offsets
+  // of their pairs, then those pairs are classified (level 2), lane i of a pair chunk finding
+  // its run by binary search over the kept runs' offsets -- survivors stay in pair order
+  for (int rbase = 0; rbase < pr.n && nsurv < cap; rbase += 64) {
+    const int r = rbase + lane;
+    bool ok = false;
+    int size = 0;
+    if (r < pr.n) {
+      const double* b1 = cl.bbox + 6 * pr.body[2 * r];
+      const double* b2 = cl.bbox + 6 * pr.body[2 * r + 1];
+      const double mg = pr.margin[r];
+      ok = true;
+      for (int i = 0; i < 3; i++)
+        if (b1[i] > b2[3 + i] + mg || b2[i] > b1[3 + i] + mg) ok = false;
+      size = ok ? pr.start[r + 1] - pr.start[r] : 0;
+    }
+    int total;
+    const int off = wave_excl_scan(size, lane, &total);
+    const unsigned long long rk = __ballot(ok);
+    const int nkeep = __popcll(rk);
+    if (ok) {
+      const int k = __popcll(rk & below);
+      cl.run_id[k] = r;
+      cl.run_pre[k] = off;
+    }
+    if (lane == 0) cl.run_pre[nkeep] = total;
+    sync();
+    for (int base = 0; base < total && nsurv < cap; base += 64) {
+      const int i = base + lane;
+      int c = -1, p = 0;
+      if (i < total) {
+        int lo = 0, hi = nkeep;  // run_pre[lo] <= i < run_pre[hi]
+        while (hi - lo > 1) {
+          const int mid = (lo + hi) >> 1;
+          if (cl.run_pre[mid] <= i)
+            lo = mid;
+          else
+            hi = mid;
+        }
+        p = pr.start[cl.run_id[lo]] + (i - cl.run_pre[lo]);
+        c = pair_class(cl.geom, m.pair_geom1[p], m.pair_geom2[p], m.pair_margin[p]);
+      }
+      const unsigned long long mk = __ballot(c >= 0);
+      const int idx = nsurv + __popcll(mk & below);
+      if (c >= 0 && idx < cap) {
+        cl.spair[idx] = p;
+        cl.scls[idx] = (uint8_t)c;
+      }
+      nsurv += __popcll(mk);
+    }
+    sync();
+  }
+  return nsurv;
 }
 
 // Contacts in pair order, at most max_contacts (the serial per-pair loop's result, bit for bit):
@@ -1599,7 +1720,8 @@ __device__ __forceinline__ CollisionLds collision_lds(const Env& e) {
 // 2. survivors listed class-major
 // 3. one collider at a time over its class's survivors, contacts into con_tmp[survivor]
 // 4. pair-order scan of the survivors' counts, contacts copied to their final slots
-__device__ int collision(Env& e, int lane, const CollisionLds& cl, unsigned long long* prof) {
+template <bool RUNS>
+__device__ int collision(Env& e, int lane, const CollisionLds& cl, const PairRuns& pr, unsigned long long* prof) {
   const rmbx_model& m = *e.m;
   unsigned long long tp = prof ? stamp() : 0;
   const int np = m.npair;
@@ -1608,32 +1730,36 @@ __device__ int collision(Env& e, int lane, const CollisionLds& cl, unsigned long
   for (int g = lane; g < m.ngeom; g += 64) geom_record(e, g, cl.geom + 8 * g);
   sync();
   SUBPROF(16)
-  // pair indices and margins of the next chunk are loaded before this chunk's tests
-  int g1n = 0, g2n = 0;
-  double mn = 0;
-  if (lane < np) {
-    g1n = m.pair_geom1[lane];
-    g2n = m.pair_geom2[lane];
-    mn = m.pair_margin[lane];
-  }
   int nsurv = 0;
-  for (int base = 0; base < np && nsurv < cap; base += 64) {
-    const int p = base + lane;
-    const int g1 = g1n, g2 = g2n;
-    const double mg = mn;
-    if (p + 64 < np) {
-      g1n = m.pair_geom1[p + 64];
-      g2n = m.pair_geom2[p + 64];
-      mn = m.pair_margin[p + 64];
+  if constexpr (RUNS) {
+    nsurv = broadphase_runs(e, lane, cl, pr, cap);
+  } else {
+    // pair indices and margins of the next chunk are loaded before this chunk's tests
+    int g1n = 0, g2n = 0;
+    double mn = 0;
+    if (lane < np) {
+      g1n = m.pair_geom1[lane];
+      g2n = m.pair_geom2[lane];
+      mn = m.pair_margin[lane];
     }
-    const int c = p < np ? pair_class(cl.geom, g1, g2, mg) : -1;
-    const unsigned long long mk = __ballot(c >= 0);
-    const int idx = nsurv + __popcll(mk & below);
-    if (c >= 0 && idx < cap) {
-      cl.spair[idx] = p;
-      cl.scls[idx] = (uint8_t)c;
+    for (int base = 0; base < np && nsurv < cap; base += 64) {
+      const int p = base + lane;
+      const int g1 = g1n, g2 = g2n;
+      const double mg = mn;
+      if (p + 64 < np) {
+        g1n = m.pair_geom1[p + 64];
+        g2n = m.pair_geom2[p + 64];
+        mn = m.pair_margin[p + 64];
+      }
+      const int c = p < np ? pair_class(cl.geom, g1, g2, mg) : -1;
+      const unsigned long long mk = __ballot(c >= 0);
+      const int idx = nsurv + __popcll(mk & below);
+      if (c >= 0 && idx < cap) {
+        cl.spair[idx] = p;
+        cl.scls[idx] = (uint8_t)c;
+      }
+      nsurv += __popcll(mk);
     }
-    nsurv += __popcll(mk);
   }
   nsurv = nsurv < cap ? nsurv : cap;
   if (nsurv == 0) return 0;
@@ -3282,6 +3408,7 @@ struct KArgs {
   unsigned long long* prof;  // optional [n_env][16] per-stage cycle sums (diagnostic)
   const int32_t* subtree_end;  // [nbody] end of each body's DFS subtree id range
   const double* hBblk;         // implicitfast: h * (damping + kv terms), packed like Mblk
+  PairRuns runs;               // two-level broadphase (rmbx_engine::nprun > 0)
   int tree_rounds;             // pointer-jumping rounds covering the deepest body chain
 };
 
@@ -3320,6 +3447,9 @@ __device__ __forceinline__ void make_env(const KArgs& args, int env, Env& e) {
   }
 
 // front half of mj_step: kinematics -> constraint rows (one wavefront per env)
+// RUNS: the two-level broadphase (a separate instantiation, so models without pair runs keep the
+// one-level kernel's register allocation)
+template <bool RUNS>
 __global__ void __launch_bounds__(64) front_kernel(KArgs args) {
   extern __shared__ __attribute__((aligned(16))) double front_smem[];
   const int env = blockIdx.x;
@@ -3342,7 +3472,7 @@ __global__ void __launch_bounds__(64) front_kernel(KArgs args) {
   PROF(1)
   velocity_stage(e, lane, s_anc, args.subtree_end);
   PROF(2)
-  const int ncon = collision(e, lane, collision_lds(e), prof);
+  const int ncon = collision<RUNS>(e, lane, collision_lds(e, args.runs), args.runs, prof);
   sync();
   PROF(3)
   int ne = 0, nlim = 0;
@@ -3565,9 +3695,33 @@ int rmbx_engine_create(const struct rmbx_model* model, int n_env, rmbx_engine** 
     RMBX_CHECK_ARG(neqr <= NEQR, "%d equality rows, more than the solver stages (%d)", neqr, NEQR);
   }
   RMBX_CHECK_ARG(h.npair >= 0 && h.npair < (1 << 24), "npair=%d outside [0, 2^24)", h.npair);
-  RMBX_CHECK_ARG(front_kernel_lds_bytes(h) <= 65536,
+  // runs of consecutive candidate pairs with the same two bodies: the two-level broadphase pays
+  // where runs are long (at least 4 pairs on average) and its LDS fits
+  std::vector<int32_t> prun_start, prun_body;
+  std::vector<double> prun_margin;
+  for (int p = 0; p < h.npair; p++) {
+    const int b1 = h.geom_body[h.pair_geom1[p]], b2 = h.geom_body[h.pair_geom2[p]];
+    if (p == 0 || b1 != prun_body[prun_body.size() - 2] || b2 != prun_body.back()) {
+      prun_start.push_back(p);
+      prun_body.push_back(b1);
+      prun_body.push_back(b2);
+      prun_margin.push_back(h.pair_margin[p]);
+    } else if (h.pair_margin[p] > prun_margin.back()) {
+      prun_margin.back() = h.pair_margin[p];
+    }
+  }
+  int nprun = (int)prun_margin.size();
+  prun_start.push_back(h.npair);
+  if (nprun == 0 || h.npair < 4 * nprun || front_kernel_lds_bytes(h, nprun) > 65536) nprun = 0;
+  RMBX_CHECK_ARG(front_kernel_lds_bytes(h, nprun) <= 65536,
                  "model too large for the front kernel's LDS (nbody=%d nv=%d ngeom=%d npair=%d)", h.nbody,
                  h.nv, h.ngeom, h.npair);
+  std::vector<int32_t> body_cgeom(2 * (size_t)h.nbody, 0);
+  for (int g = h.ngeom - 1; g >= 0; g--) {
+    const int b = h.geom_body[g];
+    body_cgeom[2 * b] = g;  // geoms of a body are consecutive (MJCF order)
+    body_cgeom[2 * b + 1]++;
+  }
   // tree passes need DFS preorder bodies (every subtree a contiguous id range); MJCF order is
   std::vector<int32_t> subtree_end(h.nbody);
   for (int b = h.nbody - 1; b >= 0; b--) {
@@ -3634,6 +3788,15 @@ int rmbx_engine_create(const struct rmbx_model* model, int n_env, rmbx_engine** 
     return st;
   }
   if (st == RMBX_OK) st = upload(eng, subtree_end.data(), (size_t)h.nbody, &eng->subtree_end);
+  eng->nprun = nprun;
+  eng->prun_start = eng->prun_body = eng->body_cgeom = nullptr;
+  eng->prun_margin = nullptr;
+  if (nprun > 0) {
+    if (st == RMBX_OK) st = upload(eng, prun_start.data(), prun_start.size(), &eng->prun_start);
+    if (st == RMBX_OK) st = upload(eng, prun_body.data(), prun_body.size(), &eng->prun_body);
+    if (st == RMBX_OK) st = upload(eng, prun_margin.data(), prun_margin.size(), &eng->prun_margin);
+    if (st == RMBX_OK) st = upload(eng, body_cgeom.data(), body_cgeom.size(), &eng->body_cgeom);
+  }
   {
     // h * (dof damping + actuator velocity gains -kv: joint actuators on the diagonal, tendon
     // actuators as kv * coef_r * coef_c), the implicitfast addition to M, in packed 4x4 blocks
@@ -3766,12 +3929,20 @@ static int launch(rmbx_engine* eng, int nsub, int integ, const uint8_t* active, 
   a.subtree_end = eng->subtree_end;
   a.tree_rounds = eng->tree_rounds;
   a.hBblk = eng->hBblk;
+  a.runs.n = eng->nprun;
+  a.runs.start = eng->prun_start;
+  a.runs.body = eng->prun_body;
+  a.runs.margin = eng->prun_margin;
+  a.runs.body_cgeom = eng->body_cgeom;
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   const int reps = integ ? nsub : 1;
   for (int s = 0; s < reps; s++) {
     a.sub = s + 1;
-    const size_t front_lds = front_kernel_lds_bytes(eng->host);
-    hipLaunchKernelGGL(front_kernel, dim3(eng->n_env), dim3(64), front_lds, st, a);
+    const size_t front_lds = front_kernel_lds_bytes(eng->host, eng->nprun);
+    if (eng->nprun > 0)
+      hipLaunchKernelGGL(front_kernel<true>, dim3(eng->n_env), dim3(64), front_lds, st, a);
+    else
+      hipLaunchKernelGGL(front_kernel<false>, dim3(eng->n_env), dim3(64), front_lds, st, a);
     RMBX_CHECK_LAUNCH();
     hipLaunchKernelGGL(solver_kernel, dim3(eng->n_env), dim3(SOLVER_THREADS), 0, st, a);
     RMBX_CHECK_LAUNCH();
@@ -3782,8 +3953,11 @@ static int launch(rmbx_engine* eng, int nsub, int integ, const uint8_t* active, 
     a.sub = nsub + 1;
     a.redo = 1;
     a.prof = nullptr;
-    const size_t front_lds = front_kernel_lds_bytes(eng->host);
-    hipLaunchKernelGGL(front_kernel, dim3(eng->n_env), dim3(64), front_lds, st, a);
+    const size_t front_lds = front_kernel_lds_bytes(eng->host, eng->nprun);
+    if (eng->nprun > 0)
+      hipLaunchKernelGGL(front_kernel<true>, dim3(eng->n_env), dim3(64), front_lds, st, a);
+    else
+      hipLaunchKernelGGL(front_kernel<false>, dim3(eng->n_env), dim3(64), front_lds, st, a);
     RMBX_CHECK_LAUNCH();
     hipLaunchKernelGGL(solver_kernel, dim3(eng->n_env), dim3(SOLVER_THREADS), 0, st, a);
     RMBX_CHECK_LAUNCH();

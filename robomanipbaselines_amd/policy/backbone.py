@@ -123,10 +123,11 @@ class _FusedConv(nn.Module):
         return (c.in_channels == c.out_channels and c.in_channels in K.WINOGRAD_F32_CHANNELS
                 and tuple(c.kernel_size) == (3, 3) and c.stride[0] == 1 and c.padding[0] == 1)
 
-    # Winograd tile of the f32 stride-1 convs: "f2" = F(2x2, 3x3) (rmbx_conv3x3_winograd_f32), "f4" =
-    # F(4x4, 3x3) (rmbx_conv3x3_winograd4_f32: 2.25 instead of 4 products per output); env
+    # Winograd tile of the f32 stride-1 convs: "f4" = F(4x4, 3x3) (rmbx_conv3x3_winograd4_f32: 2.25
+    # instead of 4 products per output; the default: ACT call 240.5 -> 232.1 ms at 1024 envs,
+    # profiles/r3_bench_f4b.json.log), "f2" = F(2x2, 3x3) (rmbx_conv3x3_winograd_f32); env
     # RMBX_WINO_TILE
-    WINO_TILE = os.environ.get("RMBX_WINO_TILE", "f2")
+    WINO_TILE = os.environ.get("RMBX_WINO_TILE", "f4")
 
     def wino(self, x, relu, res=None, bias=None):
         """f32 conv + bias (+ res) (+ ReLU) in one rmbx Winograd launch; the packed filter
