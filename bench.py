@@ -79,17 +79,93 @@ def pmc_traffic_per_env_step():
         return json.load(f)["bytes_per_env_step_per_env"], os.path.relpath(files[-1], ROOT)
 
 
-def winograd_flops_saved_per_inference(H=480, W=640):
-    """Direct-algorithm MFMA FLOPs minus the FLOPs rmbx_conv3x3_winograd_f32 executes, per image, for
-    the stride-1 3x3 convs of the fp32 ResNet-18 trunk (F(2x2, 3x3): 16 products per 2x2 tile and
-    input channel instead of 36; odd maps pad the last tile row)."""
+def winograd_flops_saved_per_inference(tile="f4", H=480, W=640):
+    """Direct-algorithm MFMA FLOPs minus the FLOPs the Winograd kernels execute, per image, for the
+    stride-1 3x3 convs of the fp32 ResNet-18 trunk: F(4x4, 3x3) (rmbx_conv3x3_winograd4_f32) runs
+    36 products per 4x4 output tile and input channel, F(2x2, 3x3) (rmbx_conv3x3_winograd_f32) 16
+    per 2x2 tile, the direct algorithm 9 per output; maps that are not a multiple of the tile pad
+    the last tile row / column (30x40 -> 32x40, 15x20 -> 16x20 under F(4x4))."""
     saved = 0
     for c, n_conv, s in ((64, 4, 4), (128, 3, 8), (256, 3, 16), (512, 3, 32)):
         h, w = -(-H // s), -(-W // s)
-        direct = 2 * h * w * c * c * 9
-        wino = 2 * 16 * c * c * (-(-h // 2)) * (-(-w // 2))
-        saved += n_conv * (direct - wino)
+        saved += n_conv * (2 * h * w * c * c * 9 - winograd_launch_flops((1, c, h, w), tile))
     return saved
+
+
+def winograd_launch_flops(shape, tile):
+    """MFMA FLOPs one Winograd conv call executes on an NCHW `shape` (all frames, all launches)."""
+    n, c, h, w = shape
+    t = 4 if tile == "f4" else 2
+    return 2 * (t + 2) ** 2 * c * c * (-(-h // t)) * (-(-w // t)) * n
+
+
+def winograd_kernel_launches(shape, tile):
+    """Kernel launches of one call: kernels.py slices the frames at *_MAX_ELEMS elements."""
+    from robomanipbaselines_amd import kernels as K
+
+    n, c, h, w = shape
+    per = max(1, (K.WINOGRAD4_MAX_ELEMS if tile == "f4" else K.WINOGRAD_MAX_ELEMS) // (h * w * c))
+    return -(-n // per)
+
+
+def winograd_pmc_traffic(tile):
+    """HBM counter bytes per conv call at 1024 frames, per layer shape, from the committed PMC
+    passes (scripts/gpurun/wino_pmc.sh + tools/pmc_traffic.py --winograd); ({}, None) if absent."""
+    path = os.path.join(ROOT, "profiles", "r3_pmc_winograd4_traffic.json" if tile == "f4"
+                        else "r2_pmc_winograd_traffic_v1.json")
+    if not os.path.exists(path):
+        return {}, None
+    with open(path) as f:
+        d = json.load(f)
+    layers = d.get("layers", {})
+    return ({int(k[1:].split("_")[0]): v.get("traffic_bytes_per_call", v.get("traffic_bytes_per_launch"))
+             for k, v in layers.items()}, os.path.relpath(path, ROOT))
+
+
+def winograd_probe(ro):
+    """One infer_policy call of `ro` with HIP events around every Winograd conv call (on the stream
+    it is launched on, nothing else queued): the dominant policy kernel's executed MFMA rate."""
+    from robomanipbaselines_amd.policy.backbone import _FusedConv
+
+    _FusedConv.PROBE = probe = []
+    try:
+        ro.infer_policy()
+        torch.cuda.synchronize()
+    finally:
+        _FusedConv.PROBE = None
+    if not probe:
+        return None
+    tile = probe[0][1]
+    ms = flops = launches = 0
+    layers = {}
+    for shape, t, e0, e1 in probe:
+        dt = e0.elapsed_time(e1)
+        fl = winograd_launch_flops(shape, t)
+        ms += dt
+        flops += fl
+        launches += winograd_kernel_launches(shape, t)
+        L = layers.setdefault(shape[1], {"calls": 0, "ms": 0.0, "flops": 0})
+        L["calls"] += 1
+        L["ms"] += dt
+        L["flops"] += fl
+    tf = flops / ms / 1e9
+    traffic, src = winograd_pmc_traffic(tile)
+    frames = probe[0][0][0]
+    tr = None
+    if traffic and all(c in traffic for c in layers):
+        tr = round(sum(traffic[c] * L["calls"] for c, L in layers.items()) * frames / 1024 / len(probe))
+    return {"bound": "mfma", "achieved": round(tf, 2), "peak": MFMA_PEAK_TFLOPS["fp32"], "unit": "TFLOP/s",
+            "frac": tf / MFMA_PEAK_TFLOPS["fp32"], "traffic": tr,
+            "traffic_unit": "HBM bytes per conv call (one layer over all frames), mean over the calls of one inference",
+            "traffic_source": src,
+            "algorithmic_bytes_per_call": round(sum(3 * 4 * s[0] * s[1] * s[2] * s[3] for s, *_ in probe) / len(probe)),
+            "kernel": ("rmbx::wino4_f32_kernel (Winograd F(4x4,3x3) f32 MFMA, bias+res+ReLU fused)" if tile == "f4"
+                       else "rmbx::wino_f32_kernel (Winograd F(2x2,3x3) f32 MFMA)"),
+            "flops": "executed MFMA FLOPs (2*(m+2)^2*C^2 per output tile and frame)",
+            "calls_per_inference": len(probe), "launches_per_inference": launches,
+            "avg_launch_us": round(1e3 * ms / launches, 1), "frames": frames,
+            "per_layer": {f"C{c}": {"calls": L["calls"], "ms_per_call": round(L["ms"] / L["calls"], 3),
+                                    "TFLOPs": round(L["flops"] / L["ms"] / 1e9, 2)} for c, L in sorted(layers.items())}}
 
 
 def policy_flops_per_inference(full_decoder):
@@ -295,6 +371,9 @@ def timed_run(groups, args, dist):
         import torch.distributed as tdist
 
         tdist.barrier()
+    markers = os.environ.get("RMBX_TRACE_MARKERS") == "1"  # scripts/trace_window.py --marker spin_kernel
+    if markers:
+        torch.cuda._sleep(1000)
     torch.cuda.synchronize()
     t0 = time.time()
     for _ in range(args.steps):
@@ -305,6 +384,9 @@ def timed_run(groups, args, dist):
     if dist:
         tdist.barrier()
     elapsed = time.time() - t0
+    if markers:
+        torch.cuda._sleep(1000)
+        torch.cuda.synchronize()
     progress(f"timed {args.steps} steps: {elapsed:.3f} s")
     # isolated probes (after the timed region)
     phys = []
@@ -443,7 +525,7 @@ def rank_main(args):
         "policy_inference_us_per_env_step": round(1e6 * float(infer.mean()) / (groups[0].n * ro.args.skip), 3) if len(infer) else None,
         "physics_kernel_ms": round(float(phys.mean()), 3),
         "physics_probe": f"isolated HIP-event time of one env-step of all {n} envs ({G} engine launch sequences back to back)",
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 4), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+        "roofline_physics": {"bound": "hbm", "achieved": round(achieved, 4), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": achieved / HBM_PEAK_GBS,
                      "traffic": round(traffic_env * n) if traffic_env else None,
                      "traffic_unit": "bytes per launch sequence (one env-step of all envs)",
@@ -465,18 +547,26 @@ def rank_main(args):
                                      "unit": "TFLOP/s", "frac": pol_tf / peak, "dtype": args.precision,
                                      "algorithmic_flops_per_inference": pol_flops,
                                      "scope": "one batched infer_policy call over all envs"}
-        from robomanipbaselines_amd.policy.backbone import _FusedBlock
+        from robomanipbaselines_amd.policy.backbone import _FusedBlock, _FusedConv
 
         if args.precision == "fp32" and _FusedBlock.F32_CONV == "winograd":
-            # the stride-1 convs run as Winograd F(2x2, 3x3): fewer MFMA FLOPs than the direct
-            # algorithm the algorithmic count (FlopCounterMode) prices; report both rates
-            executed = pol_flops - winograd_flops_saved_per_inference()
+            # the stride-1 convs run as Winograd: fewer MFMA FLOPs than the direct algorithm the
+            # algorithmic count (FlopCounterMode) prices.  achieved/frac: the FLOPs the kernels
+            # execute; *_direct: the direct-algorithm count at the same time
+            tile = _FusedConv.WINO_TILE
+            executed = pol_flops - winograd_flops_saved_per_inference(tile)
             ex_tf = groups[0].n * executed / float(infer.mean()) / 1e12
             result["roofline_policy"].update({
-                "executed_flops_per_inference": executed, "achieved_executed": round(ex_tf, 2),
-                "frac_executed": ex_tf / peak,
-                "note": "stride-1 3x3 convs by Winograd F(2x2,3x3) (rmbx_conv3x3_winograd_f32): achieved/frac "
-                        "price the direct-algorithm FLOPs, *_executed the FLOPs the kernels run"})
+                "achieved": round(ex_tf, 2), "frac": ex_tf / peak, "executed_flops_per_inference": executed,
+                "achieved_direct": round(pol_tf, 2), "frac_direct": pol_tf / peak,
+                "note": f"stride-1 3x3 convs by Winograd {'F(4x4,3x3)' if tile == 'f4' else 'F(2x2,3x3)'}: "
+                        "achieved/frac price the FLOPs the kernels execute, *_direct the direct-algorithm FLOPs"})
+            wp = winograd_probe(groups[0])
+            if wp is not None:
+                # the dominant kernel of the step: the physics line stays as roofline_physics
+                result["roofline"] = wp
+    if "roofline" not in result:  # bf16 policy / direct convs: the physics env-step line
+        result["roofline"] = result["roofline_physics"]
     if len(infer) and len(infer_full):
         # exact either way (the DETRVAE output reads decoder layer 0 only); priced here so that the
         # credited line can be compared with a rollout that also computes the dead layers

@@ -328,10 +328,24 @@ constexpr int W4_COUT = 64;
 constexpr int W4_KC = 4;
 constexpr int W4_UCH = 36 * W4_COUT * W4_KC;   // 9216 floats
 constexpr int W4_VCH = 36 * W4_TILES * W4_KC;  // 4608 floats
+constexpr int W4_DEFAULT_VAR = 0;
 static_assert((2 * W4_UCH + 2 * W4_VCH) * 4 <= 160 * 1024, "W4 LDS");
 
-template <int DBG, int SPLIT>
+// VAR bits: 1 = SPLIT schedule (above), 2 = the window loads of chunk c + 2 issued before (not
+// after) the MFMA stream of chunk c, 4 = LDS operands prefetched 4 positions ahead, 16 = window
+// gathers as buffer loads whose out-of-image pixels read 0 through the descriptor's range check
+// (voffset past the end), the window column and the K chunk in the scalar offset: one v_or per
+// pixel instead of a 64-bit address select.  Measured (profiles/r3_winograd4_variants.log): 6
+// best at 64 / 128 channels, 16 at 256 / 512 (6 | 16 spills); position-quad LDS images (one
+// ds_read_b128 per operand feeding 4 MFMAs) no faster than 6, and a one-wave-per-SIMD kernel
+// (4 waves, accumulators in AGPRs) slower at every shape: its U waits also wait for the window
+// gathers issued before them (vmcnt is in order), which the 8-wave split keeps in other waves
+template <int DBG, int VAR>
 __global__ void __launch_bounds__(WG_THREADS, 1) wino4_f32_kernel(WinoArgs a) {
+  constexpr int SPLIT = VAR & 1;
+  constexpr bool EARLY = (VAR & 2) != 0;
+  constexpr bool DEEP = (VAR & 4) != 0;
+  constexpr bool BUF = (VAR & 16) != 0;
   __shared__ __attribute__((aligned(16))) float smem[2 * W4_UCH + 2 * W4_VCH];  // sU[2], sV[2]
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int cq = wave & 3, tg = wave >> 2;
@@ -369,8 +383,50 @@ __global__ void __launch_bounds__(WG_THREADS, 1) wino4_f32_kernel(WinoArgs a) {
 #pragma unroll
       for (int j = 0; j < 9; ++j) glds16(ug + 256 * j, ul + 256 * j);
   };
+  // BUF: descriptor based one pixel before the input, so a window's first column (x0 = -1) has a
+  // non-negative voffset; a pixel outside the image gets a voffset past the end (reads 0)
+  const __amdgpu_buffer_rsrc_t in_rsrc = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(a.in - a.C), 0, (int)(((long long)a.N * a.H * a.W * a.C + a.C) * 4), 0x00020000);
+  constexpr uint32_t W4_PAST_END = 0xfffffff0u;
+  uint32_t ld_base = 0;  // byte offset of pixel (y0, x0) (descriptor based one pixel early)
+  uint32_t ld_ok = 0;    // bits 0-5: window row y in the image, bits 8-13: column x
+  auto load_window_buf = [&](int s) {
+    const int unit = s >> a.nk_log2;
+    const int k = s & (a.nk - 1);
+    if (unit != ld_unit) {
+      ld_unit = unit;
+      const int t = (r + unit * per_cb) * W4_TILES + lt;
+      const bool tok = t < a.ntiles;
+      int img, ty, tx;
+      tile_pos(tok ? t : a.ntiles - 1, img, ty, tx);
+      const int y0 = 4 * ty - 1, x0 = 4 * tx - 1;
+      ld_base = (uint32_t)(((img * a.H + y0) * a.W + x0 + 1) * a.C + lc) * 4u;
+      ld_ok = 0;
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        ld_ok |= (uint32_t)(tok && y0 + j >= 0 && y0 + j < a.H) << j;
+        ld_ok |= (uint32_t)(x0 + j >= 0 && x0 + j < a.W) << (8 + j);
+      }
+    }
+    const int row_bytes = __builtin_amdgcn_readfirstlane(a.W * a.C * 4);
+    uint32_t rv[6];  // row y's voffset, or past the end
+#pragma unroll
+    for (int y = 0; y < 6; ++y) rv[y] = (ld_base + y * row_bytes) | (((ld_ok >> y) & 1u) ? 0u : W4_PAST_END);
+#pragma unroll
+    for (int x = 0; x < 6; ++x) {
+      const int soff = __builtin_amdgcn_readfirstlane((x * a.C + k * W4_KC) * 4);
+      const uint32_t cmask = ((ld_ok >> (8 + x)) & 1u) ? 0u : W4_PAST_END;  // OR-ed in: past the end
+#pragma unroll
+      for (int y = 0; y < 6; ++y)
+        xr[6 * y + x] = __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(in_rsrc, rv[y] | cmask, soff, 0));
+    }
+  };
   auto load_window = [&](int s) {
     if (DBG & 2) return;
+    if (BUF) {
+      load_window_buf(s);
+      return;
+    }
     const int unit = s >> a.nk_log2;
     const int k = s & (a.nk - 1);
     if (unit != ld_unit) {
@@ -433,13 +489,20 @@ __global__ void __launch_bounds__(WG_THREADS, 1) wino4_f32_kernel(WinoArgs a) {
     const bool cols2 = SPLIT && loader && lgrp == (c & 1) && c + 2 < nsteps;  // SPLIT: columns of V(c + 2)
     const float* Ub = smem + buf * W4_UCH + cq * 64 + li * 4 + lq;
     const float* Vb = smem + 2 * W4_UCH + buf * W4_VCH + tg * 64 + li * 4 + lq;
-    float av = Ub[0], bv = Vb[0];
+    if (!SPLIT && EARLY && loader && lgrp == (c & 1) && c + 2 < nsteps) load_window(c + 2);
+    constexpr int PD = DEEP ? 4 : 1;  // operand prefetch distance (positions)
+    float ar[PD], br[PD];
+#pragma unroll
+    for (int j = 0; j < PD; ++j) {
+      ar[j] = Ub[j * (W4_COUT * W4_KC)];
+      br[j] = Vb[j * (W4_TILES * W4_KC)];
+    }
 #pragma unroll
     for (int p = 0; p < 36; ++p) {
-      float an = av, bn = bv;
-      if (p < 35) {
-        an = Ub[(p + 1) * (W4_COUT * W4_KC)];
-        bn = Vb[(p + 1) * (W4_TILES * W4_KC)];
+      const float av = ar[p % PD], bv = br[p % PD];
+      if (p + PD < 36) {
+        ar[p % PD] = Ub[(p + PD) * (W4_COUT * W4_KC)];
+        br[p % PD] = Vb[(p + PD) * (W4_TILES * W4_KC)];
       }
       if (!(DBG & 1))
         acc[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[p], 0, 0, 0);
@@ -453,10 +516,8 @@ __global__ void __launch_bounds__(WG_THREADS, 1) wino4_f32_kernel(WinoArgs a) {
         if (tf && p >= 2 && p <= 17 && (p - 2) % 3 == 0) row_piece(buf ^ 1, (p - 2) / 3);
         if (cols2 && p >= 20 && (p - 20) % 3 == 0) col_piece((p - 20) / 3);
       }
-      av = an;
-      bv = bn;
     }
-    if (!SPLIT && loader && lgrp == (c & 1) && c + 2 < nsteps) load_window(c + 2);
+    if (!SPLIT && !EARLY && loader && lgrp == (c & 1) && c + 2 < nsteps) load_window(c + 2);
     if (SPLIT && tf && c + 3 < nsteps) load_window(c + 3);  // the group's next window
     // U waves: the LDS-DMA of U(c + 1) has landed (loader waves keep their window loads in flight
     // across the LDS-only barrier)
@@ -639,7 +700,9 @@ extern "C" int rmbx_conv3x3_winograd4_f32(const float* in, const float* u_packed
   a.tiles_x = (W + 3) / 4;
   a.tiles_y = (H + 3) / 4;
   const long long ntiles = (long long)N * a.tiles_x * a.tiles_y;
-  RMBX_CHECK_ARG(ntiles + rmbx::W4_TILES < (1ll << 31) && (long long)N * H * W * C < (1ll << 30),
+  // 32-bit byte offsets, and the buffer descriptor's range (one pixel more, below a past-the-end
+  // voffset of 2^32 - 16): at most 2^30 - 1024 elements per launch (kernels.WINOGRAD4_MAX_ELEMS)
+  RMBX_CHECK_ARG(ntiles + rmbx::W4_TILES < (1ll << 31) && (long long)N * H * W * C <= (1ll << 30) - 1024,
                  "rmbx_conv3x3_winograd4_f32: tensor too large for 32-bit byte offsets");
   a.ntiles = (int)ntiles;
   a.ntb = (a.ntiles + rmbx::W4_TILES - 1) / rmbx::W4_TILES;
@@ -654,21 +717,35 @@ extern "C" int rmbx_conv3x3_winograd4_f32(const float* in, const float* u_packed
   grid = grid < 8 ? 8 : grid - grid % 8;
   const dim3 g(grid), blk(rmbx::WG_THREADS);
   hipStream_t st = (hipStream_t)stream;
-  const char* sp_env = std::getenv("RMBX_WINO4_SPLIT");
-  const int split = sp_env ? std::atoi(sp_env) : 0;
-#define RMBX_W4_LAUNCH(D)                                                  \
-  if (split)                                                               \
-    hipLaunchKernelGGL((rmbx::wino4_f32_kernel<D, 1>), g, blk, 0, st, a);  \
-  else                                                                     \
-    hipLaunchKernelGGL((rmbx::wino4_f32_kernel<D, 0>), g, blk, 0, st, a);
-  switch (a.dbg) {
-    case 0: RMBX_W4_LAUNCH(0) break;
-    case 1: RMBX_W4_LAUNCH(1) break;
-    case 2: RMBX_W4_LAUNCH(2) break;
-    case 4: RMBX_W4_LAUNCH(4) break;
-    case 8: RMBX_W4_LAUNCH(8) break;
-    case 14: RMBX_W4_LAUNCH(14) break;
-    default: RMBX_CHECK_ARG(false, "rmbx_conv3x3_winograd4_f32: RMBX_WINO_DBG=%d not instantiated", a.dbg);
+  // schedule variant (RMBX_WINO4_VAR, wino4_f32_kernel's VAR bits); the phase-skip builds
+  // (RMBX_WINO_DBG) exist for the default only
+  // default by channel count (scripts/prof_winograd4.py, profiles/r3_winograd4_variants.log):
+  // early window loads + deep LDS prefetch (6) at 64 / 128 channels, buffer-load window gathers
+  // (16) at 256 / 512
+  const char* var_env = std::getenv("RMBX_WINO4_VAR");
+  const int var = var_env ? std::atoi(var_env) : (C >= 256 ? 16 : 6);
+  RMBX_CHECK_ARG(a.dbg == 0 || var == rmbx::W4_DEFAULT_VAR,
+                 "rmbx_conv3x3_winograd4_f32: RMBX_WINO_DBG needs RMBX_WINO4_VAR=%d", rmbx::W4_DEFAULT_VAR);
+#define RMBX_W4_LAUNCH(D, V) hipLaunchKernelGGL((rmbx::wino4_f32_kernel<D, V>), g, blk, 0, st, a)
+  if (a.dbg == 0) {
+    switch (var) {
+      case 0: RMBX_W4_LAUNCH(0, 0); break;
+      case 1: RMBX_W4_LAUNCH(0, 1); break;
+      case 2: RMBX_W4_LAUNCH(0, 2); break;
+      case 4: RMBX_W4_LAUNCH(0, 4); break;
+      case 6: RMBX_W4_LAUNCH(0, 6); break;
+      case 16: RMBX_W4_LAUNCH(0, 16); break;
+      default: RMBX_CHECK_ARG(false, "rmbx_conv3x3_winograd4_f32: RMBX_WINO4_VAR=%d not instantiated", var);
+    }
+  } else {
+    switch (a.dbg) {
+      case 1: RMBX_W4_LAUNCH(1, rmbx::W4_DEFAULT_VAR); break;
+      case 2: RMBX_W4_LAUNCH(2, rmbx::W4_DEFAULT_VAR); break;
+      case 4: RMBX_W4_LAUNCH(4, rmbx::W4_DEFAULT_VAR); break;
+      case 8: RMBX_W4_LAUNCH(8, rmbx::W4_DEFAULT_VAR); break;
+      case 14: RMBX_W4_LAUNCH(14, rmbx::W4_DEFAULT_VAR); break;
+      default: RMBX_CHECK_ARG(false, "rmbx_conv3x3_winograd4_f32: RMBX_WINO_DBG=%d not instantiated", a.dbg);
+    }
   }
 #undef RMBX_W4_LAUNCH
   RMBX_CHECK_LAUNCH();

@@ -535,7 +535,7 @@ def conv2d_nhwc_f32_supported(cin, cout, kernel_size, stride, padding):
 _WINO_G = ((1.0, 0.0, 0.0), (0.5, 0.5, 0.5), (0.5, -0.5, 0.5), (0.0, 0.0, 1.0))
 WINOGRAD_F32_CHANNELS = (64, 128, 256, 512)
 WINOGRAD_MAX_ELEMS = (1 << 31) - 1  # per launch (32-bit element offsets in the kernel)
-WINOGRAD4_MAX_ELEMS = (1 << 30) - 1  # per launch (32-bit byte offsets of the F(4x4) buffer loads)
+WINOGRAD4_MAX_ELEMS = (1 << 30) - 1024  # per launch (32-bit byte offsets + the buffer range of the F(4x4) loads)
 
 
 def pack_winograd_f32(weight):
@@ -583,15 +583,16 @@ _WINO4_G = ((0.25, 0.0, 0.0), (-1 / 6, -1 / 6, -1 / 6), (-1 / 6, 1 / 6, -1 / 6),
 
 def pack_winograd4_f32(weight):
     """3x3 conv weight [C, C, 3, 3] -> the Winograd F(4x4, 3x3) filter transform U = G g G^T
-    (computed in f64, rounded once to f32) in the LDS image rmbx_conv3x3_winograd4_f32 stages per
-    K chunk: [C/64 channel blocks][C/4 chunks][36 positions][64 output channels][4 input channels]."""
+    (computed in f64 on the host, rounded once to f32) in the LDS image rmbx_conv3x3_winograd4_f32
+    stages per K chunk: [C/64 channel blocks][C/4 chunks][36 positions][64 output channels][4 input
+    channels]."""
     C = weight.shape[0]
     if tuple(weight.shape) != (C, C, 3, 3) or C not in WINOGRAD_F32_CHANNELS:
         raise ValueError(f"pack_winograd4_f32: weight {tuple(weight.shape)} is not [C, C, 3, 3] with C in {WINOGRAD_F32_CHANNELS}")
-    w = weight.detach().to(torch.float64)
-    G = torch.tensor(_WINO4_G, dtype=torch.float64, device=w.device)
-    U = torch.einsum("xa,oiab,yb->xyoi", G, w, G).reshape(36, C // 64, 64, C // 4, 4)  # [p][cb][co][k][c]
-    return U.permute(1, 3, 0, 2, 4).contiguous().to(torch.float32)
+    w = weight.detach().to("cpu", torch.float64)
+    G = torch.tensor(_WINO4_G, dtype=torch.float64)
+    U = torch.einsum("xa,oiab,yb->xyoi", G, w, G).reshape(36, C // 64, 64, C // 4, 4)  # [p][cb][co][kc][k]
+    return U.permute(1, 3, 0, 2, 4).to(torch.float32).to(weight.device).contiguous()
 
 
 def conv3x3_winograd4_f32(x, u_packed, bias, relu=False, res=None):

@@ -140,7 +140,19 @@ class _FusedConv(nn.Module):
             cache = (key, K.pack_winograd4_f32(w) if f4 else K.pack_winograd_f32(w))
             self.__dict__["_wino"] = cache
         fn = K.conv3x3_winograd4_f32 if f4 else K.conv3x3_winograd_f32
-        return fn(x, cache[1], self.bias_f32() if bias is None else bias, relu=relu, res=res)
+        probe = _FusedConv.PROBE
+        if probe is None:
+            return fn(x, cache[1], self.bias_f32() if bias is None else bias, relu=relu, res=res)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        out = fn(x, cache[1], self.bias_f32() if bias is None else bias, relu=relu, res=res)
+        e1.record()
+        probe.append((tuple(x.shape), "f4" if f4 else "f2", e0, e1))
+        return out
+
+    # bench.py's Winograd probe: a list to which wino() appends (shape, tile, HIP events around the
+    # launch) on the current stream; None = no events
+    PROBE = None
 
 
 class _FusedBlock(nn.Module):

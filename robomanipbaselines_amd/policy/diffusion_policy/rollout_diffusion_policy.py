@@ -54,9 +54,11 @@ class RolloutDiffusionPolicy(BatchedRolloutBase):
             load_dp_checkpoint(self.policy, self.args.checkpoint, self.camera_names)
         self.policy_dtype = torch.bfloat16 if self.args.precision == "bf16" else torch.float32
         # (the UNet's convs are GEMMs in both precisions, so MIOpen serves the image encoder only:
-        # Find picks its solvers once per shape, outside the captured denoising loop)
+        # Find picks its solvers once per shape, outside the captured denoising loop).  fp32 is the
+        # parity mode: deterministic MIOpen solvers only (no atomic split-K), so a seed reproduces
+        # its episodes bit for bit, as the reference's TrainDiffusionPolicy/rollout setup intends
         torch.backends.cudnn.benchmark = True
-        torch.backends.cudnn.deterministic = False
+        torch.backends.cudnn.deterministic = self.policy_dtype == torch.float32
         self.policy = self.policy.eval().requires_grad_(False).to(device=self.device, dtype=self.policy_dtype)
         self.policy.obs_nets = self.policy.obs_nets.to(memory_format=torch.channels_last)
 

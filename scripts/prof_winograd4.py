@@ -3,7 +3,11 @@ F(2x2, 3x3) (rmbx_conv3x3_winograd_f32) vs F(4x4, 3x3) (rmbx_conv3x3_winograd4_f
 two frames, and F(4x4) phase skips (RMBX_WINO_DBG: 1 no MFMAs, 2 no window loads, 4 no V
 transform/stores, 8 no U loads, 14 = 2|4|8 the MFMA + LDS-read skeleton).
 
-usage: python scripts/prof_winograd4.py [n_frames] [--dbg]"""
+F(4x4) schedule variants (RMBX_WINO4_VAR bits: 1 split, 2 early window loads, 4 deep LDS prefetch,
+16 buffer-load window gathers)
+are timed side by side with --vars 0,2,4,6.
+
+usage: python scripts/prof_winograd4.py [n_frames] [--dbg] [--vars 0,1]"""
 import os
 import sys
 
@@ -15,6 +19,7 @@ from robomanipbaselines_amd import kernels as K  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 and sys.argv[1].isdigit() else 1024
 dbg = "--dbg" in sys.argv
+VARS = sys.argv[sys.argv.index("--vars") + 1].split(",") if "--vars" in sys.argv else ["0", "1"]
 dev = "cuda:0"
 g = torch.Generator(device=dev).manual_seed(0)
 
@@ -40,11 +45,13 @@ for C, H, W in ((64, 120, 160), (128, 60, 80), (256, 30, 40), (512, 15, 20)):
     ref = F.relu(F.conv2d(x[:2].float(), w, b, 1, 1) + r[:2])
     flops = 2.0 * n * H * W * C * C * 9
     out = {}
-    for name, groups, fn in (("F2", None, lambda: K.conv3x3_winograd_f32(x, u2, b, relu=True, res=r)),
-                             ("F4", "0", lambda: K.conv3x3_winograd4_f32(x, u4, b, relu=True, res=r)),
-                             ("F4split", "1", lambda: K.conv3x3_winograd4_f32(x, u4, b, relu=True, res=r))):
+    def f4(v):  # v: RMBX_WINO4_VAR value
+        return lambda: K.conv3x3_winograd4_f32(x, u4, b, relu=True, res=r)
+
+    for name, groups, fn in [("F2", None, lambda: K.conv3x3_winograd_f32(x, u2, b, relu=True, res=r))] + \
+            [(f"F4v{v}", v, f4(v)) for v in VARS]:
         if groups:
-            os.environ["RMBX_WINO4_SPLIT"] = groups
+            os.environ["RMBX_WINO4_VAR"] = groups
         y = fn()
         err = ((y[:2] - ref).abs().max() / ref.abs().max()).item()
         ms = timed(fn)
@@ -53,7 +60,7 @@ for C, H, W in ((64, 120, 160), (128, 60, 80), (256, 30, 40), (512, 15, 20)):
         out[name] = ms
         line = (f"C={C:3d} {H}x{W} {name}: {ms:7.3f} ms  direct-equiv {flops / ms / 1e9:7.1f} TF/s  "
                 f"executed {ex / ms / 1e9:6.1f} TF/s ({ex / ms / 1e9 / 157.3:.2f} of f32 peak)  rel err {err:.2e}")
-        if dbg and groups:
+        if dbg and groups == "0":
             parts = []
             for d in ("1", "2", "4", "8", "14"):
                 os.environ["RMBX_WINO_DBG"] = d
@@ -61,5 +68,5 @@ for C, H, W in ((64, 120, 160), (128, 60, 80), (256, 30, 40), (512, 15, 20)):
             os.environ["RMBX_WINO_DBG"] = "0"
             line += "  [" + ", ".join(parts) + "]"
         print(line, flush=True)
-    print(f"  speedup vs F2: F4 {out['F2'] / out['F4']:.2f}x, F4split {out['F2'] / out['F4split']:.2f}x", flush=True)
+    print("  speedup vs F2: " + ", ".join(f"{k} {out['F2'] / v:.2f}x" for k, v in out.items() if k != "F2"), flush=True)
     del x, r

@@ -235,3 +235,24 @@ def test_unet1d_production_widths_fp32_and_bf16_error(kind):
     err16 = (got16 - want).abs().max().item()
     print(f"{kind}: fp32 max|d| {err32:.3e}, bf16 max|d| {err16:.3e} (scale {scale:.3f})")
     assert err16 <= 5e-2 * scale, err16
+
+
+@torch.no_grad()
+def test_rollout_dp_fp32_encoder_is_deterministic():
+    """fp32 (the parity mode) restricts MIOpen to deterministic solvers: the image
+    encoder at the production crop gives bit-identical features on repeated calls."""
+    from robomanipbaselines_amd.envs.operation.OperationMujocoUR5eCable import OperationMujocoUR5eCable
+    from robomanipbaselines_amd.policy.diffusion_policy.rollout_diffusion_policy import RolloutDiffusionPolicy
+
+    class Rollout(OperationMujocoUR5eCable, RolloutDiffusionPolicy):
+        pass
+
+    ro = Rollout(argv=["--num_envs", "2", "--device", DEV, "--precision", "fp32"])
+    assert torch.backends.cudnn.deterministic
+    B, ncam = 64, len(ro.camera_names)
+    g = torch.Generator(device=DEV).manual_seed(5)
+    st = torch.randn(B, ro.n_obs_steps, len(ro.model_meta_info["state"]["example"]), device=DEV, generator=g)
+    im = torch.rand(B, ncam, ro.n_obs_steps, 3, ro.crop_size[1], ro.crop_size[0], device=DEV, generator=g) * 2 - 1
+    a = ro.policy.encode_obs(st, im).clone()
+    b = ro.policy.encode_obs(st, im).clone()
+    assert torch.isfinite(a).all() and torch.equal(a, b)

@@ -15,6 +15,7 @@ import collections
 import csv
 import json
 import os
+import re
 import statistics
 
 CAL_BYTES = 512 << 20
@@ -31,14 +32,60 @@ def medians(path):
             {k: statistics.median(v) for k, v in dur.items()})
 
 
+def winograd(a):
+    """--winograd: the Winograd launches of scripts/prof_winograd_pmc.py in dispatch order, 3 per
+    layer shape (shapes and algorithmic bytes parsed from its log), scaled by the 16-B-lane factors
+    (the kernel's global accesses are float4)."""
+    def per_launch(path):
+        rows = sorted((int(r["Dispatch_Id"]), r["Kernel_Name"], float(r["Counter_Value"]) * 1024.0,
+                       (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3) for r in csv.DictReader(open(path)))
+        cal = [v for _, n, v, _ in rows if n.startswith("calib_f32x4")]
+        return [(v, us) for _, n, v, us in rows if "wino" in n], statistics.median(cal)
+    fetch, cf = per_launch(os.path.join(a.dir, "pmc_fetch", "run_counter_collection.csv"))
+    write, cw = per_launch(os.path.join(a.dir, "pmc_write", "run_counter_collection.csv"))
+    rf, wf = CAL_BYTES / cf, CAL_BYTES / cw
+    shapes = re.findall(r"(f\d) C=(\d+) (\d+)x(\d+): algorithmic bytes per launch (\d+)",
+                        open(os.path.join(a.dir, "fetch.log")).read())
+    # a call over more elements than *_MAX_ELEMS runs as several launches (slices of whole frames):
+    # traffic per call = sum over its launches
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    from robomanipbaselines_amd import kernels as K
+    frames = a.frames
+    calls = []
+    for tile, c, h, w, alg in shapes:
+        lim = K.WINOGRAD4_MAX_ELEMS if tile == "f4" else K.WINOGRAD_MAX_ELEMS
+        calls.append(-(-frames // max(1, lim // (int(h) * int(w) * int(c)))))
+    assert len(fetch) == len(write) == 3 * sum(calls), (len(fetch), len(write), calls)
+    out = {"calibration": {"x16_read_factor": rf, "x16_write_factor": wf}, "frames": frames, "layers": {}}
+    i = 0
+    for (tile, c, h, w, alg), L in zip(shapes, calls):
+        rd = statistics.median(sum(v for v, _ in fetch[i + j * L:i + (j + 1) * L]) for j in range(3)) * rf
+        wr = statistics.median(sum(v for v, _ in write[i + j * L:i + (j + 1) * L]) for j in range(3)) * wf
+        us = statistics.median(sum(t for _, t in fetch[i + j * L:i + (j + 1) * L]) for j in range(3))
+        i += 3 * L
+        out["layers"][f"C{c}_{h}x{w}"] = {
+            "tile": tile, "launches_per_call": L, "read_bytes_per_call": rd, "write_bytes_per_call": wr,
+            "traffic_bytes_per_launch": (rd + wr) / L, "traffic_bytes_per_call": rd + wr,
+            "algorithmic_bytes_per_call": int(alg), "traffic_over_algorithmic": (rd + wr) / int(alg),
+            "median_us_per_call_under_pmc": us}
+    with open(a.out, "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps(out, indent=1))
+
+
 def main():
     p = argparse.ArgumentParser()
+    p.add_argument("--winograd", action="store_true", help="reduce scripts/gpurun/wino_pmc.sh output")
+    p.add_argument("--frames", type=int, default=1024, help="--winograd: frames per call")
     p.add_argument("dir")
     p.add_argument("--out", required=True)
     p.add_argument("--kernels", nargs="+", default=["rmbx::front_kernel", "rmbx::solver_kernel"])
     p.add_argument("--launches_per_unit", type=int, default=8, help="launches of each kernel per env-step")
     p.add_argument("--units", type=int, default=1024, help="envs per launch")
     a = p.parse_args()
+    if a.winograd:
+        return winograd(a)
     fetch, nf, dur = medians(os.path.join(a.dir, "pmc_fetch", "run_counter_collection.csv"))
     write, nw, _ = medians(os.path.join(a.dir, "pmc_write", "run_counter_collection.csv"))
     cal = {
