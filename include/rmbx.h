@@ -401,6 +401,18 @@ int rmbx_attention_bf16(const void* q, const void* k, const void* v, void* out, 
 int rmbx_attention_f32(const float* q, const float* k, const float* v, float* out, int B, int heads, int Lq, int Lk,
                        long long q_bstride, int q_rstride, long long k_bstride, int k_rstride, long long v_bstride,
                        int v_rstride, float scale, void* stream);
+/* fp32-accurate linear layer on the bf16 matrix cores (replaces the fp32 nn.Linear /
+ * MultiheadAttention in-projections of ACT's transformer, third_party/act detr/models/transformer.py
+ * [absent submodule], run by policy/act/RolloutAct.py in fp32): c[M][N] = relu?(a[M][K] . W^T + bias)
+ * with a, c f32 (row strides lda, ldc) and W given as its three bf16 pieces W = W0 + W1 + W2
+ * (rmbx_split_bf16x3; plane p, row n at w_planes + p * w_plane_stride + n * ldw elements); a is split
+ * the same way in registers and the six piece products with i + j <= 2 are accumulated in f32 (error
+ * of the f32 GEMM class).  N % 128 == 0, K % 32 == 0, a and w_planes 16-byte aligned, bias [N] or NULL. */
+int rmbx_linear_f32x6(const float* a, long long lda, const void* w_planes, long long ldw, long long w_plane_stride,
+                      const float* bias, float* c, long long ldc, int M, int N, int K, int relu, void* stream);
+/* planes[p * n + i] = bf16 piece p of x[i], x = x0 + x1 + x2 exactly (round-to-nearest-even at each
+ * level): the weight form rmbx_linear_f32x6 reads. */
+int rmbx_split_bf16x3(const float* x, void* planes, long long n, void* stream);
 /* Residual add + LayerNorm over the last dim of [rows][D] rows (D <= 2048, multiple of 8 bf16 / 4
  * f32): out = LayerNorm(rnd(x + r)) * weight + bias (f32 weight/bias), r optional (NULL); replaces
  * the add + nn.LayerNorm pair of the ACT transformer's post-norm layers (third_party/act). */

@@ -1,0 +1,262 @@
+// fp32-accurate GEMM on the bf16 matrix cores: C = relu?(A . W^T + bias), A and C f32.
+//
+// Replaces the fp32 nn.Linear / nn.MultiheadAttention in-projections of ACT's transformer
+// (third_party/act [absent]: detr/models/transformer.py; the reference runs the policy in fp32,
+// policy/act/RolloutAct.py) for the fp32 policy path.  gfx950 runs f32-input MFMA at the f32
+// vector rate (157 TF/s, no TF32) but bf16 MFMA at 2.5 PF/s, 16x more.  Every f32 operand is
+// split exactly into three bf16 pieces, x = x0 + x1 + x2 (round-to-nearest-even at each level,
+// so |x1| <= 2^-8 |x|, |x2| <= 2^-16 |x|; 3 x 8 significant bits hold all 24 of an f32), and the
+// product is the sum of the six piece products with i + j <= 2:
+//
+//   a.b ~ a0 b0 + (a0 b1 + a1 b0) + (a0 b2 + a1 b1 + a2 b0)        (dropped terms <= 2^-24 |ab|)
+//
+// Each piece product is exact in the f32 accumulator (8 x 8 significant bits), so the result
+// differs from an exact dot product by the f32 accumulation rounding plus <= ~2^-23 relative per
+// term: the same error class as an f32 GEMM (measured lower than hipBLASLt's f32 GEMM against an
+// f64 product, tests/test_gemm_gpu.py).  Six bf16 MFMAs per f32 product step = 2.67x the f32
+// MFMA rate at equal efficiency.
+//
+// W is split once per weight on the device (rmbx_split_bf16x3, planes [3][N][K]); A (the
+// activations) is split in registers as the MFMA fragments are read from LDS.
+//
+// Mapping: block = 8 waves (2 per SIMD) owns a 256 x 128 output tile; wave (wm, wn) a 64 x 64
+// sub-tile = 2 x 2 v_mfma_f32_32x32x16_bf16 accumulators.  K runs in steps of 32: the A tile
+// (256 x 32 f32, 32 KiB) and the three W planes (3 x 128 x 32 bf16, 24 KiB) are copied
+// global -> LDS by LDS-DMA (global_load_lds_dwordx4), double-buffered (112 KiB), with XOR-
+// swizzled 16-byte slots (the swizzle is applied on the global source address, the LDS image is
+// lane-linear) so both fragment reads are bank-conflict-free ds_read_b128.  Blocks are mapped
+// XCD-contiguously and in groups of 8 row tiles x all column tiles, so the A rows and W columns
+// an XCD streams stay in its L2.
+#include "rmbx_common.h"
+
+#include <cstdint>
+
+namespace rmbx {
+namespace {
+
+typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef float f32x2v __attribute__((ext_vector_type(2)));
+
+constexpr int GM_BM = 256, GM_BN = 128, GM_BK = 32;
+constexpr int GM_THREADS = 512;
+constexpr int GM_A_BYTES = GM_BM * GM_BK * 4;            // 32 KiB
+constexpr int GM_B_PLANE = GM_BN * GM_BK * 2;            // 8 KiB
+constexpr int GM_STAGE = GM_A_BYTES + 3 * GM_B_PLANE;    // 56 KiB
+constexpr int GM_GROUP = 8;                              // row tiles per block group
+static_assert(2 * GM_STAGE <= 160 * 1024, "two K stages must fit the LDS of a CU");
+
+struct GemmArgs {
+  const float* A;      // [M][lda]
+  const uint16_t* W;   // plane p, row n at W + p * wps + n * ldw (bf16 bits)
+  const float* bias;   // [N] or null
+  float* C;            // [M][ldc]
+  long long lda, ldc, ldw, wps;
+  int M, N, K, relu;
+  int tiles_m, tiles_n;
+};
+
+__device__ __forceinline__ uint32_t pk_bf16(float x, float y) {
+  f32x2v v = {x, y};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2v));  // v_cvt_pk_bf16_f32 (RNE)
+}
+
+// (x, y) -> three packed bf16 pairs with x = x0 + x1 + x2 exactly (each level rounded to nearest even)
+__device__ __forceinline__ void split_pair(float x, float y, uint32_t& p0, uint32_t& p1, uint32_t& p2) {
+  p0 = pk_bf16(x, y);
+  const float rx = x - __uint_as_float(p0 << 16), ry = y - __uint_as_float(p0 & 0xffff0000u);
+  p1 = pk_bf16(rx, ry);
+  const float sx = rx - __uint_as_float(p1 << 16), sy = ry - __uint_as_float(p1 & 0xffff0000u);
+  p2 = pk_bf16(sx, sy);
+}
+
+// LDS-DMA of 16 bytes per lane: the wave's 64 x 16 B land contiguously at the wave-uniform LDS
+// address lds_dst (global_load_lds_dwordx4); completion is waited for by hand (vmcnt(0)) before
+// the barrier that publishes the stage.
+__device__ __forceinline__ void glds16(const void* gsrc, const void* lds_dst) {
+  const uint32_t dst = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)lds_dst;
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(dst))
+               : "memory");
+}
+
+__global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * GM_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 3, wn = wave >> 2;
+  const int lr = lane & 31, lh = lane >> 5;
+
+  // block -> tile: XCD-contiguous ranges (blocks bid, bid + 8, ... run on one XCD), then groups of
+  // GM_GROUP row tiles x all column tiles, row tile fastest
+  const int nblk = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q = nblk >> 3, r = nblk & 7;
+  const int lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int per_group = GM_GROUP * g.tiles_n;
+  const int first_m = (lin / per_group) * GM_GROUP;
+  const int gsize = min(g.tiles_m - first_m, GM_GROUP);
+  const int in_group = lin - (lin / per_group) * per_group;
+  const int tm = first_m + in_group % gsize, tn = in_group / gsize;
+  const int m0 = tm * GM_BM, n0 = tn * GM_BN;
+
+  // LDS-DMA sources.  A: 32 pieces of 8 rows x 128 B, wave w copies pieces 4w..4w+3; lane l of a
+  // piece fills LDS row 8i + l/8, physical slot l%8, which holds logical 16-B slot
+  // (l%8) ^ ((row >> 1) & 7) of that row.  Rows past M re-read row M-1 (their outputs are not
+  // stored).  W: 24 pieces (8 per plane) of 16 rows x 64 B, wave w copies pieces 3w..3w+2;
+  // physical slot l%4 holds logical slot (l%4) ^ ((row >> 2) & 3).
+  const float* asrc[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const int row = (wave * 4 + t) * 8 + (lane >> 3);
+    const int s = (lane & 7) ^ ((row >> 1) & 7);
+    const int grow = min(m0 + row, g.M - 1);
+    asrc[t] = g.A + (long long)grow * g.lda + s * 4;
+  }
+  const uint16_t* bsrc[3];
+#pragma unroll
+  for (int t = 0; t < 3; ++t) {
+    const int i = wave * 3 + t, p = i >> 3;
+    const int row = (i & 7) * 16 + (lane >> 2);
+    const int s = (lane & 3) ^ ((row >> 2) & 3);
+    bsrc[t] = g.W + p * g.wps + (long long)(n0 + row) * g.ldw + s * 8;
+  }
+  auto stage = [&](int kt, int buf) {
+    unsigned char* base = smem + buf * GM_STAGE;
+    const int k0 = kt * GM_BK;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) glds16(asrc[t] + k0, base + (wave * 4 + t) * 1024);
+#pragma unroll
+    for (int t = 0; t < 3; ++t) glds16(bsrc[t] + k0, base + GM_A_BYTES + (wave * 3 + t) * 1024);
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < 2; ++j)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+
+  const int KT = g.K / GM_BK;
+  stage(0, 0);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+
+  for (int kt = 0; kt < KT; ++kt) {
+    const int buf = kt & 1;
+    if (kt + 1 < KT) stage(kt + 1, buf ^ 1);
+    const unsigned char* As = smem + buf * GM_STAGE;
+    const unsigned char* Bs = As + GM_A_BYTES;
+#pragma unroll
+    for (int s = 0; s < 2; ++s) {
+      // A fragments: lane (lr, lh) holds A[row lr][k = 16 s + 8 lh + j], j = 0..7 (two 16-B slots)
+      bf16x8 a[2][3];
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) {
+        const int row = wm * 64 + mi * 32 + lr;
+        const int sw = (row >> 1) & 7;
+        const unsigned char* rp = As + row * 128;
+        const float4 lo = *(const float4*)(rp + (((4 * s + 2 * lh) ^ sw) << 4));
+        const float4 hi = *(const float4*)(rp + (((4 * s + 2 * lh + 1) ^ sw) << 4));
+        uint32_t p0[4], p1[4], p2[4];
+        split_pair(lo.x, lo.y, p0[0], p1[0], p2[0]);
+        split_pair(lo.z, lo.w, p0[1], p1[1], p2[1]);
+        split_pair(hi.x, hi.y, p0[2], p1[2], p2[2]);
+        split_pair(hi.z, hi.w, p0[3], p1[3], p2[3]);
+        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+        a[mi][0] = __builtin_bit_cast(bf16x8, (u32x4){p0[0], p0[1], p0[2], p0[3]});
+        a[mi][1] = __builtin_bit_cast(bf16x8, (u32x4){p1[0], p1[1], p1[2], p1[3]});
+        a[mi][2] = __builtin_bit_cast(bf16x8, (u32x4){p2[0], p2[1], p2[2], p2[3]});
+      }
+      // W fragments: lane holds W_p[n = lr][k = 16 s + 8 lh + j] (one 16-B slot per plane)
+      bf16x8 b[2][3];
+#pragma unroll
+      for (int ni = 0; ni < 2; ++ni) {
+        const int row = wn * 64 + ni * 32 + lr;
+        const int off = row * 64 + (((2 * s + lh) ^ ((row >> 2) & 3)) << 4);
+#pragma unroll
+        for (int p = 0; p < 3; ++p) b[ni][p] = *(const bf16x8*)(Bs + p * GM_B_PLANE + off);
+      }
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 2; ++ni) {
+          f32x16 c = acc[mi][ni];
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi][2], b[ni][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi][1], b[ni][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi][0], b[ni][2], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi][1], b[ni][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi][0], b[ni][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi][0], b[ni][0], c, 0, 0, 0);
+          acc[mi][ni] = c;
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+  }
+
+  // epilogue: accumulator register e of lane (lr, lh) is C[row (e&3) + 8(e>>2) + 4 lh][col lr]
+#pragma unroll
+  for (int ni = 0; ni < 2; ++ni) {
+    const int n = n0 + wn * 64 + ni * 32 + lr;
+    const float bn = g.bias ? g.bias[n] : 0.f;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+      const int mb = m0 + wm * 64 + mi * 32 + 4 * lh;
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int m = mb + (e & 3) + 8 * (e >> 2);
+        float v = acc[mi][ni][e] + bn;
+        if (g.relu) v = fmaxf(v, 0.f);
+        if (m < g.M) g.C[(long long)m * g.ldc + n] = v;
+      }
+    }
+  }
+}
+
+// planes[p * n + i] = piece p of x[i] (x = x0 + x1 + x2, bf16 bits)
+__global__ void split_bf16x3_kernel(const float* __restrict__ x, uint16_t* __restrict__ planes, long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    uint32_t p0, p1, p2;
+    split_pair(x[i], 0.f, p0, p1, p2);
+    planes[i] = (uint16_t)(p0 & 0xffff);
+    planes[n + i] = (uint16_t)(p1 & 0xffff);
+    planes[2 * n + i] = (uint16_t)(p2 & 0xffff);
+  }
+}
+
+}  // namespace
+}  // namespace rmbx
+
+extern "C" int rmbx_split_bf16x3(const float* x, void* planes, long long n, void* stream) {
+  RMBX_CHECK_ARG(x && planes && n >= 0, "rmbx_split_bf16x3: bad arguments");
+  if (n == 0) return RMBX_OK;
+  const long long blocks = (n + 255) / 256;
+  hipLaunchKernelGGL(rmbx::split_bf16x3_kernel, dim3((unsigned)(blocks < 65536 ? blocks : 65536)), dim3(256), 0,
+                     (hipStream_t)stream, x, (uint16_t*)planes, n);
+  RMBX_CHECK_LAUNCH();
+  return RMBX_OK;
+}
+
+extern "C" int rmbx_linear_f32x6(const float* a, long long lda, const void* w_planes, long long ldw,
+                                 long long w_plane_stride, const float* bias, float* c, long long ldc, int M, int N,
+                                 int K, int relu, void* stream) {
+  RMBX_CHECK_ARG(a && w_planes && c, "rmbx_linear_f32x6: null pointer");
+  RMBX_CHECK_ARG(M >= 0 && N > 0 && K > 0, "rmbx_linear_f32x6: bad shape M=%d N=%d K=%d", M, N, K);
+  RMBX_CHECK_ARG(N % rmbx::GM_BN == 0, "rmbx_linear_f32x6: N=%d must be a multiple of %d", N, rmbx::GM_BN);
+  RMBX_CHECK_ARG(K % rmbx::GM_BK == 0, "rmbx_linear_f32x6: K=%d must be a multiple of %d", K, rmbx::GM_BK);
+  RMBX_CHECK_ARG(lda >= K && lda % 4 == 0 && ldc >= N && ldw >= K && ldw % 8 == 0 && w_plane_stride % 8 == 0,
+                 "rmbx_linear_f32x6: bad strides lda=%lld ldc=%lld ldw=%lld wps=%lld", lda, ldc, ldw, w_plane_stride);
+  RMBX_CHECK_ARG(((uintptr_t)a | (uintptr_t)w_planes) % 16 == 0, "rmbx_linear_f32x6: operands must be 16-B aligned");
+  if (M == 0) return RMBX_OK;
+  rmbx::GemmArgs g{a, (const uint16_t*)w_planes, bias, c, lda, ldc, ldw, w_plane_stride, M, N, K, relu ? 1 : 0,
+                   (M + rmbx::GM_BM - 1) / rmbx::GM_BM, N / rmbx::GM_BN};
+  const long long blocks = (long long)g.tiles_m * g.tiles_n;
+  RMBX_CHECK_ARG(blocks < (1ll << 31), "rmbx_linear_f32x6: too many tiles");
+  hipLaunchKernelGGL(rmbx::gemm_f32x6_kernel, dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0, (hipStream_t)stream,
+                     g);
+  RMBX_CHECK_LAUNCH();
+  return RMBX_OK;
+}

@@ -749,3 +749,51 @@ def attention_f32(q, k, v, heads, scale=None):
     N.call("rmbx_attention_f32", N.ptr(q), N.ptr(k), N.ptr(v), N.ptr(out), B, heads, Lq, Lk,
            q.stride(0), q.stride(1), k.stride(0), k.stride(1), v.stride(0), v.stride(1), scale, N.stream_ptr())
     return out
+
+
+# ------------------------------------------------------------------------------------------
+# fp32-accurate linear layers on the bf16 matrix cores (rmbx_linear_f32x6)
+# ------------------------------------------------------------------------------------------
+LINEAR_F32X6_BN, LINEAR_F32X6_BK = 128, 32
+
+
+def split_bf16x3(w):
+    """The three bf16 pieces of an f32 tensor, w = w0 + w1 + w2 exactly: [3, *w.shape] bf16
+    (rmbx_split_bf16x3)."""
+    _chk(w, torch.float32, name="w")
+    planes = torch.empty((3,) + tuple(w.shape), dtype=torch.bfloat16, device=w.device)
+    N.call("rmbx_split_bf16x3", N.ptr(w), N.ptr(planes), w.numel(), N.stream_ptr())
+    return planes
+
+
+def linear_f32x6_supported(x, n_out):
+    """Shapes rmbx_linear_f32x6 takes: f32 device input whose last dim (K) is a multiple of 32,
+    N a multiple of 128."""
+    return (x.is_cuda and x.dtype == torch.float32 and x.shape[-1] % LINEAR_F32X6_BK == 0
+            and n_out % LINEAR_F32X6_BN == 0)
+
+
+def linear_f32x6(x, planes, bias=None, relu=False, out=None):
+    """relu?(x @ W^T + bias) with x f32 [..., K] and W given as split_bf16x3(W) [3, N, K] (or a row
+    slice planes[:, a:b] of one); f32 result [..., N] (rmbx_linear_f32x6).  x's rows may be strided
+    (last dim contiguous, row stride a multiple of 4 elements)."""
+    if planes.dim() != 3 or planes.shape[0] != 3 or planes.dtype != torch.bfloat16 or not planes.is_cuda:
+        raise ValueError("planes must be a [3, N, K] bf16 device tensor from split_bf16x3")
+    Nn, K = planes.shape[1], planes.shape[2]
+    if planes.stride(2) != 1:
+        raise ValueError("planes rows must be contiguous")
+    if x.dtype != torch.float32 or not x.is_cuda or x.shape[-1] != K:
+        raise ValueError(f"x must be an f32 device tensor [..., {K}]")
+    x2 = x.reshape(-1, K)
+    if x2.stride(1) != 1 or x2.stride(0) % 4 != 0 or x2.data_ptr() % 16 != 0:
+        x2 = x2.contiguous()
+    M = x2.shape[0]
+    if bias is not None:
+        _chk(bias, torch.float32, (Nn,), "bias")
+    if out is None:
+        out = torch.empty((M, Nn), dtype=torch.float32, device=x.device)
+    elif out.dtype != torch.float32 or out.stride(-1) != 1 or out.shape != (M, Nn):
+        raise ValueError("out must be an f32 [M, N] tensor with contiguous rows")
+    N.call("rmbx_linear_f32x6", N.ptr(x2), x2.stride(0), N.ptr(planes), planes.stride(1), planes.stride(0),
+           N.ptr(bias), N.ptr(out), out.stride(0), M, Nn, K, 1 if relu else 0, N.stream_ptr())
+    return out.view(*x.shape[:-1], Nn)

@@ -13,6 +13,7 @@ output.  Parity of this restatement with the upstream code is UNPINNED (submodul
 """
 
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -42,6 +43,39 @@ def sine_pos_embed(h, w, num_pos_feats=256, temperature=10000, device=None, dtyp
     return torch.cat((pos_y, pos_x), dim=3).permute(0, 3, 1, 2).to(dtype)
 
 
+# f32 GEMMs of the fused device form: "x6" = rmbx_linear_f32x6 (each f32 operand split into three
+# bf16 pieces, six piece products on the bf16 matrix cores, f32 accumulation: the f32 GEMM error
+# class at 2.67x the f32 MFMA rate, tests/test_gemm_gpu.py), "blas" = hipBLASLt f32; env RMBX_F32_GEMM
+F32_GEMM = os.environ.get("RMBX_F32_GEMM", "x6")
+
+
+def _x6_ok(x, n_out):
+    if F32_GEMM != "x6":
+        return False
+    from ... import kernels as K
+
+    return K.linear_f32x6_supported(x, n_out)
+
+
+def _x6_planes(owner, name, w):
+    """split_bf16x3(w), cached on `owner` per weight storage and version."""
+    from ... import kernels as K
+
+    key = (w.data_ptr(), w._version, tuple(w.shape))
+    cache = owner.__dict__.setdefault("_x6", {})
+    ent = cache.get(name)
+    if ent is None or ent[0] != key:
+        ent = (key, K.split_bf16x3(w.detach().contiguous()))
+        cache[name] = ent
+    return ent[1]
+
+
+def _x6_linear(owner, name, x, w, b, relu=False):
+    from ... import kernels as K
+
+    return K.linear_f32x6(x, _x6_planes(owner, name, w), b, relu=relu)
+
+
 class MHA(nn.Module):
     """nn.MultiheadAttention-compatible parameters (in_proj_weight/bias, out_proj), batch-first
     compute through scaled_dot_product_attention."""
@@ -57,27 +91,40 @@ class MHA(nn.Module):
         nn.init.xavier_uniform_(self.in_proj_weight)
         nn.init.zeros_(self.out_proj.bias)
 
+    def _in_proj(self, x, a, b):
+        """x @ in_proj_weight[a:b]^T + in_proj_bias[a:b]."""
+        w, bb = self.in_proj_weight, self.in_proj_bias
+        if self.fused_attention and _x6_ok(x, b - a):
+            from ... import kernels as K
+
+            return K.linear_f32x6(x, _x6_planes(self, "in_proj", w)[:, a:b], bb[a:b])
+        return F.linear(x, w[a:b], bb[a:b])
+
+    def _out_proj(self, o):
+        if self.fused_attention and _x6_ok(o, self.out_proj.out_features):
+            return _x6_linear(self, "out_proj", o, self.out_proj.weight, self.out_proj.bias)
+        return self.out_proj(o)
+
     def forward(self, q, k, v):
         D = q.shape[2]
-        w, b = self.in_proj_weight, self.in_proj_bias
         if q is k and k is v:
-            qkv = F.linear(q, w, b)
+            qkv = self._in_proj(q, 0, 3 * D)
             qq, kk, vv = qkv.split(D, dim=-1)
         elif q is k:
-            qk = F.linear(q, w[: 2 * D], b[: 2 * D])
+            qk = self._in_proj(q, 0, 2 * D)
             qq, kk = qk.split(D, dim=-1)
-            vv = F.linear(v, w[2 * D :], b[2 * D :])
+            vv = self._in_proj(v, 2 * D, 3 * D)
         else:
-            qq = F.linear(q, w[:D], b[:D])
-            kk = F.linear(k, w[D : 2 * D], b[D : 2 * D])
-            vv = F.linear(v, w[2 * D :], b[2 * D :])
+            qq = self._in_proj(q, 0, D)
+            kk = self._in_proj(k, D, 2 * D)
+            vv = self._in_proj(v, 2 * D, 3 * D)
         return self._attend(qq, kk, vv)
 
     def attend_kv(self, q, kk, vv):
         """forward(q, k, v) with the key / value projections kk, vv already computed (e.g. column
         slices of one GEMM shared by several layers)."""
         D = q.shape[2]
-        return self._attend(F.linear(q, self.in_proj_weight[:D], self.in_proj_bias[:D]), kk, vv)
+        return self._attend(self._in_proj(q, 0, D), kk, vv)
 
     def _attend(self, qq, kk, vv):
         B, Lq, D = qq.shape
@@ -88,11 +135,11 @@ class MHA(nn.Module):
 
             # rmbx_attention_bf16 reads the head slices of the projections in place and writes the
             # [B, Lq, D] layout out_proj consumes
-            return self.out_proj(K.attention_bf16(qq, kk, vv, self.h))
+            return self._out_proj(K.attention_bf16(qq, kk, vv, self.h))
         if self.fused_attention and qq.dtype == torch.float32 and hd == 64 and qq.is_cuda:
             from ... import kernels as K
 
-            return self.out_proj(K.attention_f32(qq, kk, vv, self.h))
+            return self._out_proj(K.attention_f32(qq, kk, vv, self.h))
         qq = qq.view(B, Lq, self.h, hd).transpose(1, 2)
         kk = kk.view(B, Lk, self.h, hd).transpose(1, 2)
         vv = vv.view(B, Lk, self.h, hd).transpose(1, 2)
@@ -108,6 +155,9 @@ class _LayerOps(nn.Module):
     fused = False
 
     def ffn(self, x):
+        if self.fused and _x6_ok(x, self.linear1.out_features) and self.linear2.out_features % 128 == 0:
+            h = _x6_linear(self, "linear1", x, self.linear1.weight, self.linear1.bias, relu=True)
+            return _x6_linear(self, "linear2", h, self.linear2.weight, self.linear2.bias)
         if self.fused:
             shp = x.shape
             h = torch._addmm_activation(self.linear1.bias, x.reshape(-1, shp[-1]), self.linear1.weight.t())
@@ -254,8 +304,12 @@ class ActModel(nn.Module):
             cache = (key, wk, bk, wv, bv)
             self.__dict__["_cross_w"] = cache
         _, wk, bk, wv, bv = cache
-        k_all = F.linear(mem_pos, wk, bk)
-        v_all = F.linear(mem, wv, bv)
+        if _x6_ok(mem, wk.shape[0]):
+            k_all = _x6_linear(self, "cross_k", mem_pos, wk, bk)
+            v_all = _x6_linear(self, "cross_v", mem, wv, bv)
+        else:
+            k_all = F.linear(mem_pos, wk, bk)
+            v_all = F.linear(mem, wv, bv)
         return [(k_all[..., i * D: (i + 1) * D], v_all[..., i * D: (i + 1) * D]) for i in range(n_dec)]
 
     def _pos(self, h, w, device, dtype):
