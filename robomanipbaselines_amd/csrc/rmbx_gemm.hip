@@ -30,20 +30,22 @@
 #include "rmbx_common.h"
 
 #include <cstdint>
+#include <cstdlib>
 
 namespace rmbx {
 namespace {
 
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
-typedef float f32x16 __attribute__((ext_vector_type(16)));
+typedef float f32x4v __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
 typedef float f32x2v __attribute__((ext_vector_type(2)));
 
 constexpr int GM_BM = 256, GM_BN = 128, GM_BK = 32;
 constexpr int GM_THREADS = 512;
-constexpr int GM_A_BYTES = GM_BM * GM_BK * 4;            // 32 KiB
+constexpr int GM_A_PLANE = GM_BM * GM_BK * 2;            // 16 KiB per bf16 piece plane
 constexpr int GM_B_PLANE = GM_BN * GM_BK * 2;            // 8 KiB
-constexpr int GM_STAGE = GM_A_BYTES + 3 * GM_B_PLANE;    // 56 KiB
+constexpr int GM_A_BYTES = 3 * GM_A_PLANE;               // 48 KiB
+constexpr int GM_STAGE = GM_A_BYTES + 3 * GM_B_PLANE;    // 72 KiB
 constexpr int GM_GROUP = 8;                              // row tiles per block group
 static_assert(2 * GM_STAGE <= 160 * 1024, "two K stages must fit the LDS of a CU");
 
@@ -83,6 +85,13 @@ __device__ __forceinline__ void glds16(const void* gsrc, const void* lds_dst) {
                : "memory");
 }
 
+// s_waitcnt vmcnt(n) with n a compile-time count
+template <int N>
+__device__ __forceinline__ void wait_vm() {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+template <int V>
 __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * GM_STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -101,114 +110,146 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
   const int tm = first_m + in_group % gsize, tn = in_group / gsize;
   const int m0 = tm * GM_BM, n0 = tn * GM_BN;
 
-  // LDS-DMA sources.  A: 32 pieces of 8 rows x 128 B, wave w copies pieces 4w..4w+3; lane l of a
-  // piece fills LDS row 8i + l/8, physical slot l%8, which holds logical 16-B slot
-  // (l%8) ^ ((row >> 1) & 7) of that row.  Rows past M re-read row M-1 (their outputs are not
-  // stored).  W: 24 pieces (8 per plane) of 16 rows x 64 B, wave w copies pieces 3w..3w+2;
-  // physical slot l%4 holds logical slot (l%4) ^ ((row >> 2) & 3).
-  const float* asrc[4];
-#pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const int row = (wave * 4 + t) * 8 + (lane >> 3);
-    const int s = (lane & 7) ^ ((row >> 1) & 7);
-    const int grow = min(m0 + row, g.M - 1);
-    asrc[t] = g.A + (long long)grow * g.lda + s * 4;
-  }
+  // LDS images: every plane row is 32 k = four 16-B slots (8 k each), physical slot =
+  // logical ^ ((row >> 2) & 2): conflict-free for the 16x16x32 fragment reads (lane l reads row
+  // l%16, slot l/16), the LDS-DMA pieces and the A stores below.
+  // A staging (registers): thread -> rows tid/4 and tid/4 + 128, k quarter tid%4 (8 f32 = 32 B
+  // each); the three pieces go to the three LDS planes [256 rows][32 k].  Rows past M re-read
+  // row M-1 (their outputs are not stored).
+  const int aq = tid & 3, arow = tid >> 2;
+  const float* ag0 = g.A + (long long)min(m0 + arow, g.M - 1) * g.lda + 8 * aq;
+  const float* ag1 = g.A + (long long)min(m0 + arow + 128, g.M - 1) * g.lda + 8 * aq;
+  const int aoff0 = arow * 64 + ((aq ^ ((arow >> 2) & 2)) << 4);
+  const int aoff1 = (arow + 128) * 64 + ((aq ^ (((arow + 128) >> 2) & 2)) << 4);
+  // W: LDS-DMA of 24 pieces (8 per plane) of 16 rows x 64 B, wave w copies pieces 3w..3w+2
   const uint16_t* bsrc[3];
 #pragma unroll
   for (int t = 0; t < 3; ++t) {
     const int i = wave * 3 + t, p = i >> 3;
     const int row = (i & 7) * 16 + (lane >> 2);
-    const int s = (lane & 3) ^ ((row >> 2) & 3);
-    bsrc[t] = g.W + p * g.wps + (long long)(n0 + row) * g.ldw + s * 8;
+    const int sl = (lane & 3) ^ ((row >> 2) & 2);
+    bsrc[t] = g.W + p * g.wps + (long long)(n0 + row) * g.ldw + sl * 8;
   }
-  auto stage = [&](int kt, int buf) {
+  auto stage_b = [&](int kt, int buf) {
+    unsigned char* base = smem + buf * GM_STAGE + GM_A_BYTES;
+#pragma unroll
+    for (int t = 0; t < 3; ++t) glds16(bsrc[t] + kt * GM_BK, base + (wave * 3 + t) * 1024);
+  };
+  auto load_a = [&](float4 (&R)[4], int kt) {
+    const float4* p0 = (const float4*)(ag0 + kt * GM_BK);
+    const float4* p1 = (const float4*)(ag1 + kt * GM_BK);
+    R[0] = p0[0];
+    R[1] = p0[1];
+    R[2] = p1[0];
+    R[3] = p1[1];
+  };
+  auto store_a = [&](const float4 (&R)[4], int buf) {
+    uint32_t p0[8], p1[8], p2[8];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      split_pair(R[i].x, R[i].y, p0[2 * i], p1[2 * i], p2[2 * i]);
+      split_pair(R[i].z, R[i].w, p0[2 * i + 1], p1[2 * i + 1], p2[2 * i + 1]);
+    }
     unsigned char* base = smem + buf * GM_STAGE;
-    const int k0 = kt * GM_BK;
-#pragma unroll
-    for (int t = 0; t < 4; ++t) glds16(asrc[t] + k0, base + (wave * 4 + t) * 1024);
-#pragma unroll
-    for (int t = 0; t < 3; ++t) glds16(bsrc[t] + k0, base + GM_A_BYTES + (wave * 3 + t) * 1024);
+    *(uint4*)(base + aoff0) = make_uint4(p0[0], p0[1], p0[2], p0[3]);
+    *(uint4*)(base + GM_A_PLANE + aoff0) = make_uint4(p1[0], p1[1], p1[2], p1[3]);
+    *(uint4*)(base + 2 * GM_A_PLANE + aoff0) = make_uint4(p2[0], p2[1], p2[2], p2[3]);
+    *(uint4*)(base + aoff1) = make_uint4(p0[4], p0[5], p0[6], p0[7]);
+    *(uint4*)(base + GM_A_PLANE + aoff1) = make_uint4(p1[4], p1[5], p1[6], p1[7]);
+    *(uint4*)(base + 2 * GM_A_PLANE + aoff1) = make_uint4(p2[4], p2[5], p2[6], p2[7]);
   };
 
-  f32x16 acc[2][2];
+  // wave (wm, wn) owns rows 64 wm.., columns 64 wn..: 4 x 4 accumulators of 16 x 16
+  f32x4v acc[4][4];
 #pragma unroll
-  for (int i = 0; i < 2; ++i)
+  for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 2; ++j)
-#pragma unroll
-      for (int e = 0; e < 16; ++e) acc[i][j][e] = 0.f;
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4v){0.f, 0.f, 0.f, 0.f};
 
-  const int KT = g.K / GM_BK;
-  stage(0, 0);
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-
-  for (int kt = 0; kt < KT; ++kt) {
-    const int buf = kt & 1;
-    if (kt + 1 < KT) stage(kt + 1, buf ^ 1);
+  // 16x16x32 fragments: lane l holds X_p[row l%16][k = 8 (l/16) + j], j = 0..7 (one 16-B slot)
+  const int fr = lane & 15, fs = lane >> 4;
+  auto frag_off = [&](int row) { return row * 64 + ((fs ^ ((row >> 2) & 2)) << 4); };
+  // half h of a K step: m-tiles 2h, 2h+1 against all four n-tiles (48 MFMAs, small terms first)
+  auto half_step = [&](int buf, int h, const bf16x8 (&b)[4][3]) {
     const unsigned char* As = smem + buf * GM_STAGE;
-    const unsigned char* Bs = As + GM_A_BYTES;
+    bf16x8 a[2][3];
 #pragma unroll
-    for (int s = 0; s < 2; ++s) {
-      // A fragments: lane (lr, lh) holds A[row lr][k = 16 s + 8 lh + j], j = 0..7 (two 16-B slots)
-      bf16x8 a[2][3];
+    for (int i = 0; i < 2; ++i) {
+      const int off = frag_off(wm * 64 + (2 * h + i) * 16 + fr);
 #pragma unroll
-      for (int mi = 0; mi < 2; ++mi) {
-        const int row = wm * 64 + mi * 32 + lr;
-        const int sw = (row >> 1) & 7;
-        const unsigned char* rp = As + row * 128;
-        const float4 lo = *(const float4*)(rp + (((4 * s + 2 * lh) ^ sw) << 4));
-        const float4 hi = *(const float4*)(rp + (((4 * s + 2 * lh + 1) ^ sw) << 4));
-        uint32_t p0[4], p1[4], p2[4];
-        split_pair(lo.x, lo.y, p0[0], p1[0], p2[0]);
-        split_pair(lo.z, lo.w, p0[1], p1[1], p2[1]);
-        split_pair(hi.x, hi.y, p0[2], p1[2], p2[2]);
-        split_pair(hi.z, hi.w, p0[3], p1[3], p2[3]);
-        typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
-        a[mi][0] = __builtin_bit_cast(bf16x8, (u32x4){p0[0], p0[1], p0[2], p0[3]});
-        a[mi][1] = __builtin_bit_cast(bf16x8, (u32x4){p1[0], p1[1], p1[2], p1[3]});
-        a[mi][2] = __builtin_bit_cast(bf16x8, (u32x4){p2[0], p2[1], p2[2], p2[3]});
-      }
-      // W fragments: lane holds W_p[n = lr][k = 16 s + 8 lh + j] (one 16-B slot per plane)
-      bf16x8 b[2][3];
-#pragma unroll
-      for (int ni = 0; ni < 2; ++ni) {
-        const int row = wn * 64 + ni * 32 + lr;
-        const int off = row * 64 + (((2 * s + lh) ^ ((row >> 2) & 3)) << 4);
-#pragma unroll
-        for (int p = 0; p < 3; ++p) b[ni][p] = *(const bf16x8*)(Bs + p * GM_B_PLANE + off);
-      }
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < 2; ++ni) {
-          f32x16 c = acc[mi][ni];
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi][2], b[ni][0], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi][1], b[ni][1], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi][0], b[ni][2], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi][1], b[ni][0], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi][0], b[ni][1], c, 0, 0, 0);
-          c = __builtin_amdgcn_mfma_f32_32x32x16_bf16(a[mi][0], b[ni][0], c, 0, 0, 0);
-          acc[mi][ni] = c;
-        }
+      for (int p = 0; p < 3; ++p) a[i][p] = *(const bf16x8*)(As + p * GM_A_PLANE + off);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int nj = 0; nj < 4; ++nj) {
+        f32x4v c = acc[2 * h + i][nj];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][2], b[nj][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[nj][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[nj][2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[nj][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[nj][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[nj][0], c, 0, 0, 0);
+        acc[2 * h + i][nj] = c;
+      }
+  };
+  auto read_b = [&](bf16x8 (&b)[4][3], int buf) {
+    const unsigned char* Bs = smem + buf * GM_STAGE + GM_A_BYTES;
+#pragma unroll
+    for (int nj = 0; nj < 4; ++nj) {
+      const int off = frag_off(wn * 64 + nj * 16 + fr);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) b[nj][p] = *(const bf16x8*)(Bs + p * GM_B_PLANE + off);
+    }
+  };
+
+  // K steps of 32, two LDS stages, one barrier per step.  Step kt computes stage kt while W of
+  // kt + 1 arrives by LDS-DMA, A of kt + 1 (loaded during step kt - 1) is split and stored between
+  // the step's two MFMA halves, and A of kt + 2 is loaded into registers.  Issue order per step:
+  // W DMA, then the A loads, so the counted wait at the end (vmcnt(4): the 4 A loads of kt + 2 may
+  // stay in flight) retires the W DMA; hipcc's own wait before the split (for A of kt + 1) is at
+  // least as strict.
+  const int KT = g.K / GM_BK;
+  float4 Ra[4], Rb[4];
+  load_a(Ra, 0);
+  stage_b(0, 0);
+  load_a(Rb, min(1, KT - 1));
+  store_a(Ra, 0);
+  wait_vm<4>();
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  auto step = [&](int kt, float4 (&Rcur)[4], float4 (&Rnext)[4]) {
+    const int buf = kt & 1;
+    const bool more = kt + 1 < KT;
+    if (more) stage_b(kt + 1, buf ^ 1);
+    load_a(Rnext, min(kt + 2, KT - 1));  // unconditional (a redundant reload at the end) so that
+                                         // hipcc's wait before the split stays counted
+    bf16x8 b[4][3];
+    read_b(b, buf);
+    half_step(buf, 0, b);
+    if (more) store_a(Rcur, buf ^ 1);
+    half_step(buf, 1, b);
+    if (more) {
+      wait_vm<4>();
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+  };
+  for (int kt = 0; kt < KT; kt += 2) {
+    step(kt, Rb, Ra);
+    if (kt + 1 < KT) step(kt + 1, Ra, Rb);
   }
 
-  // epilogue: accumulator register e of lane (lr, lh) is C[row (e&3) + 8(e>>2) + 4 lh][col lr]
+  // epilogue: accumulator register e of lane l is C[row 4 (l/16) + e][col l%16] of its tile
 #pragma unroll
-  for (int ni = 0; ni < 2; ++ni) {
-    const int n = n0 + wn * 64 + ni * 32 + lr;
+  for (int nj = 0; nj < 4; ++nj) {
+    const int n = n0 + wn * 64 + nj * 16 + fr;
     const float bn = g.bias ? g.bias[n] : 0.f;
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi) {
-      const int mb = m0 + wm * 64 + mi * 32 + 4 * lh;
+    for (int mi = 0; mi < 4; ++mi) {
+      const int mb = m0 + wm * 64 + mi * 16 + 4 * fs;
 #pragma unroll
-      for (int e = 0; e < 16; ++e) {
-        const int m = mb + (e & 3) + 8 * (e >> 2);
-        float v = acc[mi][ni][e] + bn;
+      for (int e = 0; e < 4; ++e) {
+        const int m = mb + e;
+        float v = acc[mi][nj][e] + bn;
         if (g.relu) v = fmaxf(v, 0.f);
         if (m < g.M) g.C[(long long)m * g.ldc + n] = v;
       }
@@ -255,8 +296,17 @@ extern "C" int rmbx_linear_f32x6(const float* a, long long lda, const void* w_pl
                    (M + rmbx::GM_BM - 1) / rmbx::GM_BM, N / rmbx::GM_BN};
   const long long blocks = (long long)g.tiles_m * g.tiles_n;
   RMBX_CHECK_ARG(blocks < (1ll << 31), "rmbx_linear_f32x6: too many tiles");
-  hipLaunchKernelGGL(rmbx::gemm_f32x6_kernel, dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0, (hipStream_t)stream,
-                     g);
+  // RMBX_GEMM_VARIANT (profiling): 0 = compiler-scheduled pipeline, 1 = MFMA/VALU interleave (default)
+  static const int variant = [] {
+    const char* e = getenv("RMBX_GEMM_VARIANT");
+    return e ? atoi(e) : 1;
+  }();
+  if (variant == 0)
+    hipLaunchKernelGGL(rmbx::gemm_f32x6_kernel<0>, dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0,
+                       (hipStream_t)stream, g);
+  else
+    hipLaunchKernelGGL(rmbx::gemm_f32x6_kernel<1>, dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0,
+                       (hipStream_t)stream, g);
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
 }
