@@ -410,6 +410,14 @@ int rmbx_attention_f32(const float* q, const float* k, const float* v, float* ou
  * of the f32 GEMM class).  N % 128 == 0, K % 32 == 0, a and w_planes 16-byte aligned, bias [N] or NULL. */
 int rmbx_linear_f32x6(const float* a, long long lda, const void* w_planes, long long ldw, long long w_plane_stride,
                       const float* bias, float* c, long long ldc, int M, int N, int K, int relu, void* stream);
+/* The same fp32-accurate bf16x6 products as an implicit-GEMM convolution (replaces the stride-2
+ * 3x3 convs and 1x1 downsample convs + FrozenBatchNorm of the fp32 ResNet-18 trunk in ACT's backbone,
+ * third_party/act [absent], torchvision resnet18): out[N][Ho][Wo][Cout] = relu?(conv(in) + bias + res)
+ * with in NHWC f32 [N][H][W][C], w_planes = rmbx_split_bf16x3 of the weight laid out [Cout][KH][KW][C],
+ * res NHWC like out or NULL.  C % 32 == 0, Cout % 128 == 0. */
+int rmbx_conv2d_f32x6(const float* in, int N, int H, int W, int C, const void* w_planes, const float* bias,
+                      const float* res, float* out, int Cout, int KH, int KW, int stride, int pad, int relu,
+                      void* stream);
 /* planes[p * n + i] = bf16 piece p of x[i], x = x0 + x1 + x2 exactly (round-to-nearest-even at each
  * level): the weight form rmbx_linear_f32x6 reads. */
 int rmbx_split_bf16x3(const float* x, void* planes, long long n, void* stream);

@@ -17,16 +17,18 @@
 // MFMA rate at equal efficiency.
 //
 // W is split once per weight on the device (rmbx_split_bf16x3, planes [3][N][K]); A (the
-// activations) is split in registers as the MFMA fragments are read from LDS.
+// activations) is split once per block as it is staged into LDS.
 //
 // Mapping: block = 8 waves (2 per SIMD) owns a 256 x 128 output tile; wave (wm, wn) a 64 x 64
-// sub-tile = 2 x 2 v_mfma_f32_32x32x16_bf16 accumulators.  K runs in steps of 32: the A tile
-// (256 x 32 f32, 32 KiB) and the three W planes (3 x 128 x 32 bf16, 24 KiB) are copied
-// global -> LDS by LDS-DMA (global_load_lds_dwordx4), double-buffered (112 KiB), with XOR-
-// swizzled 16-byte slots (the swizzle is applied on the global source address, the LDS image is
-// lane-linear) so both fragment reads are bank-conflict-free ds_read_b128.  Blocks are mapped
-// XCD-contiguously and in groups of 8 row tiles x all column tiles, so the A rows and W columns
-// an XCD streams stay in its L2.
+// sub-tile = 4 x 4 v_mfma_f32_16x16x32_bf16 accumulators (the 16x16x32 form holds a higher clock
+// than 32x32x16 on random data under DVFS, MI355X_MICROARCH.md).  K runs in steps of 32 over two
+// LDS stages of 72 KiB: the three W planes (3 x 128 x 32 bf16) arrive by LDS-DMA
+// (global_load_lds_dwordx4); the A tile (256 x 32 f32) is loaded into registers two steps ahead,
+// split into its three bf16 pieces (VALU) and stored as three planes (3 x 256 x 32 bf16) between
+// the two MFMA halves of the step before it is used.  Every plane row (32 k) is four 16-B slots,
+// XOR-swizzled by (row >> 2) & 2 so the fragment reads, the DMA pieces and the A stores are all
+// LDS-bank-conflict-free.  Blocks are mapped XCD-contiguously and in groups of 8 row tiles x all
+// column tiles, so the A rows and W columns an XCD streams stay in its L2.
 #include "rmbx_common.h"
 
 #include <cstdint>
@@ -57,6 +59,10 @@ struct GemmArgs {
   long long lda, ldc, ldw, wps;
   int M, N, K, relu;
   int tiles_m, tiles_n;
+  const float* res;    // [M][ldc] added before the ReLU, or null
+  // implicit-GEMM convolution (gemm_f32x6_kernel<true>): A = the NHWC input [img][ih][iw][ic], row
+  // m = output pixel (img, oy, ox) of [img][oh][ow], k = (ky * kw + kx) * ic + c
+  int ih, iw, ic, oh, ow, kw, stride, pad;
 };
 
 __device__ __forceinline__ uint32_t pk_bf16(float x, float y) {
@@ -91,7 +97,7 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <int V>
+template <bool CONV>
 __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * GM_STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -135,15 +141,57 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
 #pragma unroll
     for (int t = 0; t < 3; ++t) glds16(bsrc[t] + kt * GM_BK, base + (wave * 3 + t) * 1024);
   };
-  auto load_a = [&](float4 (&R)[4], int kt) {
-    const float4* p0 = (const float4*)(ag0 + kt * GM_BK);
-    const float4* p1 = (const float4*)(ag1 + kt * GM_BK);
-    R[0] = p0[0];
-    R[1] = p0[1];
-    R[2] = p1[0];
-    R[3] = p1[1];
+  // convolution: each staged row's window origin (iy0, ix0) and its element offset in the input;
+  // a K step of 32 lies inside one filter tap (C % 32 == 0), so a row's 8 channels are one
+  // contiguous 32-B load, or zeros where the tap falls in the padding (the load then reads
+  // element 0 and the values are dropped at the split)
+  long long cbase[2] = {0, 0};
+  int cy[2] = {0, 0}, cx[2] = {0, 0};
+  if constexpr (CONV) {
+#pragma unroll
+    for (int r2 = 0; r2 < 2; ++r2) {
+      const int m = min(m0 + arow + 128 * r2, g.M - 1);
+      const int hw = g.oh * g.ow;
+      const int img = m / hw, rem = m - img * hw;
+      const int oy = rem / g.ow, ox = rem - oy * g.ow;
+      cy[r2] = oy * g.stride - g.pad;
+      cx[r2] = ox * g.stride - g.pad;
+      cbase[r2] = ((long long)(img * g.ih + cy[r2]) * g.iw + cx[r2]) * g.ic + 8 * aq;
+    }
+  }
+  // returns the in-image flags of the two rows (bit r)
+  auto load_a = [&](float4 (&R)[4], int kt) -> int {
+    if constexpr (!CONV) {
+      const float4* p0 = (const float4*)(ag0 + kt * GM_BK);
+      const float4* p1 = (const float4*)(ag1 + kt * GM_BK);
+      R[0] = p0[0];
+      R[1] = p0[1];
+      R[2] = p1[0];
+      R[3] = p1[1];
+      return 3;
+    } else {
+      const int k0 = kt * GM_BK;
+      const int tap = k0 / g.ic, c0 = k0 - tap * g.ic;
+      const int ky = tap / g.kw, kx = tap - ky * g.kw;
+      int ok = 0;
+#pragma unroll
+      for (int r2 = 0; r2 < 2; ++r2) {
+        const bool v = (unsigned)(cy[r2] + ky) < (unsigned)g.ih && (unsigned)(cx[r2] + kx) < (unsigned)g.iw;
+        const float4* p = (const float4*)(g.A + (v ? cbase[r2] + (long long)(ky * g.iw + kx) * g.ic + c0 : 0));
+        R[2 * r2] = p[0];
+        R[2 * r2 + 1] = p[1];
+        ok |= (int)v << r2;
+      }
+      return ok;
+    }
   };
-  auto store_a = [&](const float4 (&R)[4], int buf) {
+  auto store_a = [&](const float4 (&Rin)[4], int ok, int buf) {
+    float4 R[4] = {Rin[0], Rin[1], Rin[2], Rin[3]};
+    if constexpr (CONV) {
+      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
+      if (!(ok & 1)) R[0] = R[1] = z;
+      if (!(ok & 2)) R[2] = R[3] = z;
+    }
     uint32_t p0[8], p1[8], p2[8];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -211,22 +259,23 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
   // least as strict.
   const int KT = g.K / GM_BK;
   float4 Ra[4], Rb[4];
-  load_a(Ra, 0);
+  int oka, okb;
+  oka = load_a(Ra, 0);
   stage_b(0, 0);
-  load_a(Rb, min(1, KT - 1));
-  store_a(Ra, 0);
+  okb = load_a(Rb, min(1, KT - 1));
+  store_a(Ra, oka, 0);
   wait_vm<4>();
   asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  auto step = [&](int kt, float4 (&Rcur)[4], float4 (&Rnext)[4]) {
+  auto step = [&](int kt, float4 (&Rcur)[4], int& okcur, float4 (&Rnext)[4], int& oknext) {
     const int buf = kt & 1;
     const bool more = kt + 1 < KT;
     if (more) stage_b(kt + 1, buf ^ 1);
-    load_a(Rnext, min(kt + 2, KT - 1));  // unconditional (a redundant reload at the end) so that
+    oknext = load_a(Rnext, min(kt + 2, KT - 1));  // unconditional (a redundant reload at the end) so that
                                          // hipcc's wait before the split stays counted
     bf16x8 b[4][3];
     read_b(b, buf);
     half_step(buf, 0, b);
-    if (more) store_a(Rcur, buf ^ 1);
+    if (more) store_a(Rcur, okcur, buf ^ 1);
     half_step(buf, 1, b);
     if (more) {
       wait_vm<4>();
@@ -234,8 +283,8 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
     }
   };
   for (int kt = 0; kt < KT; kt += 2) {
-    step(kt, Rb, Ra);
-    if (kt + 1 < KT) step(kt + 1, Ra, Rb);
+    step(kt, Rb, okb, Ra, oka);
+    if (kt + 1 < KT) step(kt + 1, Ra, oka, Rb, okb);
   }
 
   // epilogue: accumulator register e of lane l is C[row 4 (l/16) + e][col l%16] of its tile
@@ -249,9 +298,12 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int m = mb + e;
-        float v = acc[mi][nj][e] + bn;
-        if (g.relu) v = fmaxf(v, 0.f);
-        if (m < g.M) g.C[(long long)m * g.ldc + n] = v;
+        if (m < g.M) {
+          float v = acc[mi][nj][e] + bn;
+          if (g.res) v += g.res[(long long)m * g.ldc + n];
+          if (g.relu) v = fmaxf(v, 0.f);
+          g.C[(long long)m * g.ldc + n] = v;
+        }
       }
     }
   }
@@ -293,20 +345,37 @@ extern "C" int rmbx_linear_f32x6(const float* a, long long lda, const void* w_pl
   RMBX_CHECK_ARG(((uintptr_t)a | (uintptr_t)w_planes) % 16 == 0, "rmbx_linear_f32x6: operands must be 16-B aligned");
   if (M == 0) return RMBX_OK;
   rmbx::GemmArgs g{a, (const uint16_t*)w_planes, bias, c, lda, ldc, ldw, w_plane_stride, M, N, K, relu ? 1 : 0,
-                   (M + rmbx::GM_BM - 1) / rmbx::GM_BM, N / rmbx::GM_BN};
+                   (M + rmbx::GM_BM - 1) / rmbx::GM_BM, N / rmbx::GM_BN, nullptr};
   const long long blocks = (long long)g.tiles_m * g.tiles_n;
   RMBX_CHECK_ARG(blocks < (1ll << 31), "rmbx_linear_f32x6: too many tiles");
-  // RMBX_GEMM_VARIANT (profiling): 0 = compiler-scheduled pipeline, 1 = MFMA/VALU interleave (default)
-  static const int variant = [] {
-    const char* e = getenv("RMBX_GEMM_VARIANT");
-    return e ? atoi(e) : 1;
-  }();
-  if (variant == 0)
-    hipLaunchKernelGGL(rmbx::gemm_f32x6_kernel<0>, dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0,
-                       (hipStream_t)stream, g);
-  else
-    hipLaunchKernelGGL(rmbx::gemm_f32x6_kernel<1>, dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0,
-                       (hipStream_t)stream, g);
+  hipLaunchKernelGGL(rmbx::gemm_f32x6_kernel<false>, dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0,
+                     (hipStream_t)stream, g);
+  RMBX_CHECK_LAUNCH();
+  return RMBX_OK;
+}
+
+extern "C" int rmbx_conv2d_f32x6(const float* in, int N, int H, int W, int C, const void* w_planes, const float* bias,
+                                 const float* res, float* out, int Cout, int KH, int KW, int stride, int pad, int relu,
+                                 void* stream) {
+  RMBX_CHECK_ARG(in && w_planes && out, "rmbx_conv2d_f32x6: null pointer");
+  RMBX_CHECK_ARG(N >= 0 && H > 0 && W > 0 && KH > 0 && KW > 0 && stride > 0 && pad >= 0,
+                 "rmbx_conv2d_f32x6: bad geometry");
+  RMBX_CHECK_ARG(C % rmbx::GM_BK == 0, "rmbx_conv2d_f32x6: C=%d must be a multiple of %d", C, rmbx::GM_BK);
+  RMBX_CHECK_ARG(Cout % rmbx::GM_BN == 0, "rmbx_conv2d_f32x6: Cout=%d must be a multiple of %d", Cout, rmbx::GM_BN);
+  RMBX_CHECK_ARG(((uintptr_t)in | (uintptr_t)w_planes) % 16 == 0, "rmbx_conv2d_f32x6: operands must be 16-B aligned");
+  const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
+  RMBX_CHECK_ARG(Ho > 0 && Wo > 0, "rmbx_conv2d_f32x6: empty output");
+  const long long M = (long long)N * Ho * Wo;
+  RMBX_CHECK_ARG(M < (1ll << 31) && (long long)N * H * W < (1ll << 31), "rmbx_conv2d_f32x6: too many pixels");
+  if (M == 0) return RMBX_OK;
+  const int K = KH * KW * C;
+  rmbx::GemmArgs g{in, (const uint16_t*)w_planes, bias, out, 0, Cout, K, (long long)Cout * K, (int)M, Cout, K,
+                   relu ? 1 : 0, (int)((M + rmbx::GM_BM - 1) / rmbx::GM_BM), Cout / rmbx::GM_BN, res,
+                   H, W, C, Ho, Wo, KW, stride, pad};
+  const long long blocks = (long long)g.tiles_m * g.tiles_n;
+  RMBX_CHECK_ARG(blocks < (1ll << 31), "rmbx_conv2d_f32x6: too many tiles");
+  hipLaunchKernelGGL(rmbx::gemm_f32x6_kernel<true>, dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0,
+                     (hipStream_t)stream, g);
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
 }

@@ -797,3 +797,46 @@ def linear_f32x6(x, planes, bias=None, relu=False, out=None):
     N.call("rmbx_linear_f32x6", N.ptr(x2), x2.stride(0), N.ptr(planes), planes.stride(1), planes.stride(0),
            N.ptr(bias), N.ptr(out), out.stride(0), M, Nn, K, 1 if relu else 0, N.stream_ptr())
     return out.view(*x.shape[:-1], Nn)
+
+
+def pack_conv_f32x6(weight):
+    """split_bf16x3 of a conv weight [Cout, C, KH, KW] laid out [Cout][KH][KW][C] (the k order of
+    rmbx_conv2d_f32x6): [3, Cout, KH*KW*C] bf16."""
+    if weight.dim() != 4:
+        raise ValueError("pack_conv_f32x6: weight must be [Cout, C, KH, KW]")
+    w = weight.detach().float().permute(0, 2, 3, 1).reshape(weight.shape[0], -1).contiguous()
+    return split_bf16x3(w)
+
+
+def conv2d_f32x6_supported(cin, cout):
+    return cin % LINEAR_F32X6_BK == 0 and cout % LINEAR_F32X6_BN == 0
+
+
+def conv2d_f32x6(x, planes, bias, kernel_size, stride=1, padding=0, relu=False, res=None):
+    """relu?(conv2d(x, w, stride, padding) + bias + res) by rmbx_conv2d_f32x6 (fp32-accurate bf16x6
+    implicit GEMM) with planes = pack_conv_f32x6(w); x f32 [N, C, H, W] channels_last; result
+    channels_last [N, Cout, Ho, Wo]."""
+    if x.dtype != torch.float32 or not x.is_cuda or x.dim() != 4:
+        raise ValueError("conv2d_f32x6: x must be an f32 device tensor [N, C, H, W]")
+    if not x.is_contiguous(memory_format=torch.channels_last):
+        raise ValueError("conv2d_f32x6: x must be channels_last")
+    n, c, h, w_ = x.shape
+    kh, kw = (kernel_size, kernel_size) if isinstance(kernel_size, int) else kernel_size
+    if planes.dim() != 3 or planes.shape[0] != 3 or planes.shape[2] != kh * kw * c or planes.dtype != torch.bfloat16:
+        raise ValueError("conv2d_f32x6: planes must be pack_conv_f32x6(weight) for this input")
+    if not planes.is_contiguous():
+        raise ValueError("conv2d_f32x6: planes must be contiguous")
+    cout = planes.shape[1]
+    if not conv2d_f32x6_supported(c, cout):
+        raise ValueError(f"conv2d_f32x6: C={c} must be a multiple of 32 and Cout={cout} of 128")
+    ho = (h + 2 * padding - kh) // stride + 1
+    wo = (w_ + 2 * padding - kw) // stride + 1
+    if bias is not None:
+        _chk(bias, torch.float32, (cout,), "bias")
+    out = torch.empty((n, cout, ho, wo), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
+    if res is not None:
+        if res.shape != out.shape or res.dtype != torch.float32 or not res.is_contiguous(memory_format=torch.channels_last):
+            raise ValueError("conv2d_f32x6: res must be a channels_last f32 tensor shaped like the output")
+    N.call("rmbx_conv2d_f32x6", N.ptr(x), n, h, w_, c, N.ptr(planes), N.ptr(bias), N.ptr(res), N.ptr(out), cout,
+           kh, kw, stride, padding, 1 if relu else 0, N.stream_ptr())
+    return out

@@ -150,6 +150,25 @@ class _FusedConv(nn.Module):
         probe.append((tuple(x.shape), "f4" if f4 else "f2", e0, e1))
         return out
 
+    def x6_ok(self):
+        c = self.conv
+        return (c.stride[0] == c.stride[1] and c.padding[0] == c.padding[1]
+                and K.conv2d_f32x6_supported(c.in_channels, c.out_channels))
+
+    def x6(self, x, relu, res=None, bias=True):
+        """f32 conv (+ bias) (+ res) (+ ReLU) as one rmbx_conv2d_f32x6 launch (fp32-accurate bf16x6
+        implicit GEMM, epilogue fused); bias=False: no bias.  The split weight is cached per
+        weight storage."""
+        c = self.conv
+        w = c.weight
+        key = (w.data_ptr(), w._version, w.device)
+        cache = self.__dict__.get("_x6")
+        if cache is None or cache[0] != key:
+            cache = (key, K.pack_conv_f32x6(w))
+            self.__dict__["_x6"] = cache
+        return K.conv2d_f32x6(x, cache[1], self.bias_f32() if bias else None, c.kernel_size, c.stride[0],
+                              c.padding[0], relu=relu, res=res)
+
     # bench.py's Winograd probe: a list to which wino() appends (shape, tile, HIP events around the
     # launch) on the current stream; None = no events
     PROBE = None
@@ -171,6 +190,7 @@ class _FusedBlock(nn.Module):
     # fp32 stride-1 3x3 convs: "winograd" (rmbx_conv3x3_winograd_f32, every layer) or "direct"
     # (layer 1 on rmbx_conv2d_nhwc_f32, layers 2-4 MIOpen + epilogue pass); env RMBX_F32_CONV
     F32_CONV = os.environ.get("RMBX_F32_CONV", "winograd")
+    F32_CONV_S2 = os.environ.get("RMBX_F32_CONV_S2", "x6")
 
     def _bias_sum(self):
         """c2's bias + the downsample's (the residual's bias folded into c2's epilogue), cached."""
@@ -187,10 +207,15 @@ class _FusedBlock(nn.Module):
                 y = self.c1.wino(x, relu=True)
                 return self.c2.wino(y, relu=True, res=x)
             if self.down is not None:
-                # stride-2 c1 and the 1x1 downsample stay MIOpen convs; c2 (stride 1) adds the
+                # stride-2 c1 and the 1x1 downsample: rmbx_conv2d_f32x6 (RMBX_F32_CONV_S2 = "x6",
+                # the default) or MIOpen + the epilogue pass ("miopen"); c2 (stride 1) adds the
                 # downsample branch and both biases in its epilogue
-                y = self.c1(x)
-                d = self.down.conv_nobias(x)
+                if self.F32_CONV_S2 == "x6" and self.c1.x6_ok() and self.down.x6_ok():
+                    y = self.c1.x6(x, relu=True)
+                    d = self.down.x6(x, relu=False, bias=False)
+                else:
+                    y = self.c1(x)
+                    d = self.down.conv_nobias(x)
                 return self.c2.wino(y, relu=True, res=d, bias=self._bias_sum())
         if x.dtype == torch.bfloat16 and self.c2.conv.out_channels <= self.RMBX_CONV_MAX_COUT:
             y = self.c1.rmbx(x, relu=True)

@@ -1,8 +1,10 @@
 """rmbx_linear_f32x6 (fp32-accurate GEMM on the bf16 matrix cores: both operands split into three
 bf16 pieces, six piece products accumulated in f32) against an f64 product of the same f32
 operands, beside the device's own f32 GEMM (hipBLASLt, the path it replaces in the fp32 ACT
-transformer).  The bar is the f32 GEMM error class: max |err| <= 4e-6 * max |ref| and no worse
-than 2x hipBLASLt's f32 GEMM error on the same inputs (measured ~0.3-0.8e-6 vs 1-2e-6)."""
+transformer).  The bar is the f32 GEMM error class: max |err| <= 4e-6 * max |ref|, and for the
+linear layers no worse than 2x hipBLASLt's f32 GEMM error on the same inputs (measured ~0.3-0.8e-6
+vs 1-2e-6).  rmbx_conv2d_f32x6 (the same kernel as an implicit-GEMM convolution) is held to the
+4e-6 bar against an f64 F.conv2d."""
 
 import pytest
 import torch
@@ -84,3 +86,57 @@ def test_linear_f32x6_rejects_bad_shapes():
         K_.linear_f32x6(x, K_.split_bf16x3(torch.randn(128, 48, device=DEV)))
     with pytest.raises((ValueError, RuntimeError)):
         K_.linear_f32x6(torch.randn(8, 64, device=DEV), K_.split_bf16x3(torch.randn(100, 64, device=DEV)))
+
+
+def _conv_ref(x, w, b, stride, pad, relu, res):
+    ref = F.conv2d(x.double(), w.double(), None if b is None else b.double(), stride, pad)
+    if res is not None:
+        ref = ref + res.double()
+    return ref.clamp_min(0) if relu else ref
+
+
+@torch.no_grad()
+@pytest.mark.parametrize("n,C,H,W,Cout,k,stride,pad,relu,res,bias", [
+    (2, 64, 17, 23, 128, 3, 2, 1, True, False, True),     # layer-2 c1 shape class, odd sizes
+    (3, 128, 15, 20, 256, 1, 2, 0, False, False, False),  # 1x1 downsample
+    (2, 256, 9, 11, 512, 3, 2, 1, True, False, True),
+    (2, 64, 12, 16, 128, 3, 1, 1, True, True, True),      # stride 1 with a residual
+])
+def test_conv2d_f32x6_vs_f64(n, C, H, W, Cout, k, stride, pad, relu, res, bias):
+    from robomanipbaselines_amd import kernels as K_
+
+    g = torch.Generator(device="cpu").manual_seed(n * 1000 + C + k)
+    x = torch.randn(n, C, H, W, generator=g)
+    w = torch.randn(Cout, C, k, k, generator=g) / (C * k * k) ** 0.5
+    b = torch.randn(Cout, generator=g) if bias else None
+    Ho, Wo = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+    r = torch.randn(n, Cout, Ho, Wo, generator=g) if res else None
+    cl = torch.channels_last
+    got = K_.conv2d_f32x6(x.to(DEV).contiguous(memory_format=cl), K_.pack_conv_f32x6(w.to(DEV)),
+                          None if b is None else b.to(DEV), k, stride, pad, relu=relu,
+                          res=None if r is None else r.to(DEV).contiguous(memory_format=cl))
+    assert got.shape == (n, Cout, Ho, Wo) and got.is_contiguous(memory_format=cl)
+    ref = _conv_ref(x, w, b, stride, pad, relu, r)
+    base = F.conv2d(x.to(DEV), w.to(DEV), None if b is None else b.to(DEV), stride, pad).cpu()
+    if r is not None:
+        base = base + r
+    if relu:
+        base = base.clamp_min(0)
+    e, e32 = _err(got.cpu(), ref), _err(base, ref)
+    # the f32-GEMM error class (sequential f32 accumulation over K = KH*KW*C up to 2304; MIOpen's
+    # direct fp32 conv sums in a different order and can land lower, ~2e-7 here)
+    assert e <= 4e-6, (e, e32)
+
+
+@torch.no_grad()
+def test_conv2d_f32x6_trunk_shape_8_frames():
+    """The layer-2 stride-2 conv at the policy's 120x160 feature size (8 frames), f64 reference."""
+    from robomanipbaselines_amd import kernels as K_
+
+    g = torch.Generator(device="cpu").manual_seed(3)
+    x = torch.randn(8, 64, 120, 160, generator=g).clamp_min(0)
+    w = torch.randn(128, 64, 3, 3, generator=g) / (64 * 9) ** 0.5
+    b = torch.randn(128, generator=g)
+    got = K_.conv2d_f32x6(x.to(DEV).contiguous(memory_format=torch.channels_last), K_.pack_conv_f32x6(w.to(DEV)),
+                          b.to(DEV), 3, 2, 1, relu=True)
+    assert _err(got.cpu(), _conv_ref(x, w, b, 2, 1, True, None)) <= 4e-6
