@@ -418,6 +418,18 @@ int rmbx_linear_f32x6(const float* a, long long lda, const void* w_planes, long 
 int rmbx_conv2d_f32x6(const float* in, int N, int H, int W, int C, const void* w_planes, const float* bias,
                       const float* res, float* out, int Cout, int KH, int KW, int stride, int pad, int relu,
                       void* stream);
+/* rmbx_linear_f32x6 over `batch` independent problems: item b reads a + b * a_bs, w_planes + b * w_bs
+ * and writes c + b * c_bs (element strides; the 36 position GEMMs of the explicit Winograd conv). */
+int rmbx_linear_f32x6_batched(const float* a, long long lda, long long a_bs, const void* w_planes, long long ldw,
+                              long long w_plane_stride, long long w_bs, const float* bias, float* c, long long ldc,
+                              long long c_bs, int batch, int M, int N, int K, int relu, void* stream);
+/* Winograd F(4x4, 3x3) transforms of the explicit fp32 Winograd conv (the stride-1 3x3 convs of the
+ * 256/512-channel ResNet-18 layers in ACT's backbone, third_party/act [absent]): V[36][T][C] =
+ * B^T d B of every 6x6 input window (in NHWC [N][H][W][C], T = N * ceil(H/4) * ceil(W/4) tiles), and
+ * out NHWC = relu?(A^T M A + bias + res) from the position GEMM results M[36][T][C]. */
+int rmbx_wino4_input_f32(const float* in, int N, int H, int W, int C, float* V, void* stream);
+int rmbx_wino4_output_f32(const float* M, int N, int H, int W, int C, const float* bias, const float* res, float* out,
+                          int relu, void* stream);
 /* planes[p * n + i] = bf16 piece p of x[i], x = x0 + x1 + x2 exactly (round-to-nearest-even at each
  * level): the weight form rmbx_linear_f32x6 reads. */
 int rmbx_split_bf16x3(const float* x, void* planes, long long n, void* stream);

@@ -63,6 +63,9 @@ struct GemmArgs {
   // implicit-GEMM convolution (gemm_f32x6_kernel<true>): A = the NHWC input [img][ih][iw][ic], row
   // m = output pixel (img, oy, ox) of [img][oh][ow], k = (ky * kw + kx) * ic + c
   int ih, iw, ic, oh, ow, kw, stride, pad;
+  // batched GEMM (rmbx_linear_f32x6_batched): batch item b uses A + b a_bs, W + b w_bs, C + b c_bs
+  int batch;
+  long long a_bs, w_bs, c_bs;
 };
 
 __device__ __forceinline__ uint32_t pk_bf16(float x, float y) {
@@ -108,7 +111,15 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
   // GM_GROUP row tiles x all column tiles, row tile fastest
   const int nblk = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, q = nblk >> 3, r = nblk & 7;
-  const int lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  int lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  if (g.batch > 1) {  // consecutive tiles of an XCD stay inside one batch item
+    const int per_item = g.tiles_m * g.tiles_n;
+    const int item = lin / per_item;
+    lin -= item * per_item;
+    g.A += item * g.a_bs;
+    g.W += item * g.w_bs;
+    g.C += item * g.c_bs;
+  }
   const int per_group = GM_GROUP * g.tiles_n;
   const int first_m = (lin / per_group) * GM_GROUP;
   const int gsize = min(g.tiles_m - first_m, GM_GROUP);
@@ -348,6 +359,33 @@ extern "C" int rmbx_linear_f32x6(const float* a, long long lda, const void* w_pl
                    (M + rmbx::GM_BM - 1) / rmbx::GM_BM, N / rmbx::GM_BN, nullptr};
   const long long blocks = (long long)g.tiles_m * g.tiles_n;
   RMBX_CHECK_ARG(blocks < (1ll << 31), "rmbx_linear_f32x6: too many tiles");
+  hipLaunchKernelGGL(rmbx::gemm_f32x6_kernel<false>, dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0,
+                     (hipStream_t)stream, g);
+  RMBX_CHECK_LAUNCH();
+  return RMBX_OK;
+}
+
+extern "C" int rmbx_linear_f32x6_batched(const float* a, long long lda, long long a_bs, const void* w_planes,
+                                         long long ldw, long long w_plane_stride, long long w_bs, const float* bias,
+                                         float* c, long long ldc, long long c_bs, int batch, int M, int N, int K,
+                                         int relu, void* stream) {
+  RMBX_CHECK_ARG(a && w_planes && c, "rmbx_linear_f32x6_batched: null pointer");
+  RMBX_CHECK_ARG(batch >= 1 && M >= 0 && N > 0 && K > 0, "rmbx_linear_f32x6_batched: bad shape");
+  RMBX_CHECK_ARG(N % rmbx::GM_BN == 0 && K % rmbx::GM_BK == 0, "rmbx_linear_f32x6_batched: N=%d / K=%d not multiples of %d / %d",
+                 N, K, rmbx::GM_BN, rmbx::GM_BK);
+  RMBX_CHECK_ARG(lda >= K && lda % 4 == 0 && a_bs % 4 == 0 && ldc >= N && ldw >= K && ldw % 8 == 0 &&
+                     w_plane_stride % 8 == 0 && w_bs % 8 == 0,
+                 "rmbx_linear_f32x6_batched: bad strides");
+  RMBX_CHECK_ARG(((uintptr_t)a | (uintptr_t)w_planes) % 16 == 0, "rmbx_linear_f32x6_batched: operands must be 16-B aligned");
+  if (M == 0) return RMBX_OK;
+  rmbx::GemmArgs g{a, (const uint16_t*)w_planes, bias, c, lda, ldc, ldw, w_plane_stride, M, N, K, relu ? 1 : 0,
+                   (M + rmbx::GM_BM - 1) / rmbx::GM_BM, N / rmbx::GM_BN, nullptr};
+  g.batch = batch;
+  g.a_bs = a_bs;
+  g.w_bs = w_bs;
+  g.c_bs = c_bs;
+  const long long blocks = (long long)g.tiles_m * g.tiles_n * batch;
+  RMBX_CHECK_ARG(blocks < (1ll << 31), "rmbx_linear_f32x6_batched: too many tiles");
   hipLaunchKernelGGL(rmbx::gemm_f32x6_kernel<false>, dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0,
                      (hipStream_t)stream, g);
   RMBX_CHECK_LAUNCH();

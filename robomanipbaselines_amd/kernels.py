@@ -756,6 +756,20 @@ def attention_f32(q, k, v, heads, scale=None):
 # ------------------------------------------------------------------------------------------
 LINEAR_F32X6_BN, LINEAR_F32X6_BK = 128, 32
 
+# bench.py's GEMM probe: a list to which every rmbx_linear_f32x6(_batched) / rmbx_conv2d_f32x6 launch
+# appends (name, fp32-equivalent FLOPs, HIP events around it on the current stream); None = no events
+GEMM_PROBE = None
+
+
+def _gemm_launch(name, flops, fn, *args):
+    if GEMM_PROBE is None:
+        return N.call(fn, *args)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    N.call(fn, *args)
+    e1.record()
+    GEMM_PROBE.append((name, flops, e0, e1))
+
 
 def split_bf16x3(w):
     """The three bf16 pieces of an f32 tensor, w = w0 + w1 + w2 exactly: [3, *w.shape] bf16
@@ -794,8 +808,9 @@ def linear_f32x6(x, planes, bias=None, relu=False, out=None):
         out = torch.empty((M, Nn), dtype=torch.float32, device=x.device)
     elif out.dtype != torch.float32 or out.stride(-1) != 1 or out.shape != (M, Nn):
         raise ValueError("out must be an f32 [M, N] tensor with contiguous rows")
-    N.call("rmbx_linear_f32x6", N.ptr(x2), x2.stride(0), N.ptr(planes), planes.stride(1), planes.stride(0),
-           N.ptr(bias), N.ptr(out), out.stride(0), M, Nn, K, 1 if relu else 0, N.stream_ptr())
+    _gemm_launch(f"linear M={M} N={Nn} K={K}", 2.0 * M * Nn * K, "rmbx_linear_f32x6", N.ptr(x2), x2.stride(0),
+                 N.ptr(planes), planes.stride(1), planes.stride(0), N.ptr(bias), N.ptr(out), out.stride(0), M, Nn, K,
+                 1 if relu else 0, N.stream_ptr())
     return out.view(*x.shape[:-1], Nn)
 
 
@@ -837,6 +852,56 @@ def conv2d_f32x6(x, planes, bias, kernel_size, stride=1, padding=0, relu=False, 
     if res is not None:
         if res.shape != out.shape or res.dtype != torch.float32 or not res.is_contiguous(memory_format=torch.channels_last):
             raise ValueError("conv2d_f32x6: res must be a channels_last f32 tensor shaped like the output")
-    N.call("rmbx_conv2d_f32x6", N.ptr(x), n, h, w_, c, N.ptr(planes), N.ptr(bias), N.ptr(res), N.ptr(out), cout,
-           kh, kw, stride, padding, 1 if relu else 0, N.stream_ptr())
+    _gemm_launch(f"conv {kh}x{kw}/{stride} {c}->{cout} {h}x{w_}", 2.0 * n * ho * wo * cout * c * kh * kw,
+                 "rmbx_conv2d_f32x6", N.ptr(x), n, h, w_, c, N.ptr(planes), N.ptr(bias), N.ptr(res), N.ptr(out), cout,
+                 kh, kw, stride, padding, 1 if relu else 0, N.stream_ptr())
+    return out
+
+
+WINO_X6_CHANNELS = (256, 512)
+
+
+def pack_wino4_x6(weight):
+    """3x3 conv weight [Cout, C, 3, 3] -> split_bf16x3 of the Winograd F(4x4, 3x3) filter transform
+    U = G g G^T (f64 on the host, rounded once to f32) laid out [36 positions][Cout][C]:
+    [3, 36 * Cout, C] bf16 (the W operand of the 36 position GEMMs)."""
+    if weight.dim() != 4 or tuple(weight.shape[2:]) != (3, 3):
+        raise ValueError("pack_wino4_x6: weight must be [Cout, C, 3, 3]")
+    co, ci = weight.shape[0], weight.shape[1]
+    w = weight.detach().to("cpu", torch.float64)
+    G = torch.tensor(_WINO4_G, dtype=torch.float64)
+    U = torch.einsum("xa,oiab,yb->xyoi", G, w, G).reshape(36 * co, ci)
+    return split_bf16x3(U.to(torch.float32).to(weight.device).contiguous())
+
+
+def conv3x3_wino4_x6(x, planes, bias, relu=False, res=None):
+    """relu?(conv2d(x, w, stride 1, pad 1) + bias + res) as the explicit Winograd F(4x4, 3x3): input
+    transform pass (rmbx_wino4_input_f32), 36 fp32-accurate bf16x6 position GEMMs
+    (rmbx_linear_f32x6_batched, planes = pack_wino4_x6(w)), output transform pass with the epilogue
+    (rmbx_wino4_output_f32).  x f32 channels_last [N, C, H, W]."""
+    _chk_nhwc(x, "x")
+    if x.dtype != torch.float32:
+        raise ValueError("conv3x3_wino4_x6: x must be f32")
+    n, C, H, W = x.shape
+    if planes.dim() != 3 or planes.shape[0] != 3 or planes.shape[2] != C or planes.shape[1] % 36:
+        raise ValueError("conv3x3_wino4_x6: planes must be pack_wino4_x6(weight) for this input")
+    co = planes.shape[1] // 36
+    if not conv2d_f32x6_supported(C, co):
+        raise ValueError(f"conv3x3_wino4_x6: C={C} must be a multiple of 32 and Cout={co} of 128")
+    if bias is not None:
+        _chk(bias, torch.float32, (co,), "bias")
+    out = torch.empty((n, co, H, W), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
+    if res is not None:
+        _chk_nhwc(res, "res")
+        if tuple(res.shape) != tuple(out.shape) or res.dtype != torch.float32:
+            raise ValueError("res must match the output")
+    T = n * ((H + 3) // 4) * ((W + 3) // 4)
+    V = torch.empty((36, T, C), dtype=torch.float32, device=x.device)
+    N.call("rmbx_wino4_input_f32", N.ptr(x), n, H, W, C, N.ptr(V), N.stream_ptr())
+    M = torch.empty((36, T, co), dtype=torch.float32, device=x.device)
+    _gemm_launch(f"winograd x36 M={T} N={co} K={C}", 2.0 * 36 * T * co * C, "rmbx_linear_f32x6_batched", N.ptr(V), C,
+                 T * C, N.ptr(planes), planes.stride(1), planes.stride(0), co * C, None, N.ptr(M), co, T * co, 36, T,
+                 co, C, 0, N.stream_ptr())
+    N.call("rmbx_wino4_output_f32", N.ptr(M), n, H, W, co, N.ptr(bias), N.ptr(res), N.ptr(out), 1 if relu else 0,
+           N.stream_ptr())
     return out

@@ -129,10 +129,22 @@ class _FusedConv(nn.Module):
     # RMBX_WINO_TILE
     WINO_TILE = os.environ.get("RMBX_WINO_TILE", "f4")
 
+    # the 256/512-channel stride-1 convs as the explicit Winograd F(4x4, 3x3) with the 36 position
+    # GEMMs on rmbx_linear_f32x6 (kernels.conv3x3_wino4_x6); env RMBX_WINO_X6=0 keeps them on the
+    # fused f32-MFMA kernel
+    WINO_X6 = os.environ.get("RMBX_WINO_X6", "1") != "0"
+
     def wino(self, x, relu, res=None, bias=None):
-        """f32 conv + bias (+ res) (+ ReLU) in one rmbx Winograd launch; the packed filter
-        transform is cached per weight storage."""
+        """f32 conv + bias (+ res) (+ ReLU) in one rmbx Winograd launch (or the explicit x6 form at
+        256/512 channels); the packed filter transform is cached per weight storage."""
         w = self.conv.weight
+        if self.WINO_X6 and w.shape[0] in K.WINO_X6_CHANNELS:
+            key = (w.data_ptr(), w._version, w.device, "x6")
+            cache = self.__dict__.get("_wino")
+            if cache is None or cache[0] != key:
+                cache = (key, K.pack_wino4_x6(w))
+                self.__dict__["_wino"] = cache
+            return K.conv3x3_wino4_x6(x, cache[1], self.bias_f32() if bias is None else bias, relu=relu, res=res)
         f4 = self.WINO_TILE == "f4"
         key = (w.data_ptr(), w.dtype, w.device, f4)
         cache = self.__dict__.get("_wino")

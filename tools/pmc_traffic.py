@@ -74,9 +74,39 @@ def winograd(a):
     print(json.dumps(out, indent=1))
 
 
+def gemm(a):
+    """--gemm: the gemm_f32x6_kernel launches of the SECOND fp32 ACT inference of
+    scripts/prof_act_gemm_pmc.py (dispatch order), scaled by the 16-B-lane factors (its global loads
+    are dwordx4 and LDS-DMA of 16 B per lane): HBM bytes per launch, mean over the inference."""
+    def per_launch(path):
+        rows = sorted((int(r["Dispatch_Id"]), r["Kernel_Name"], float(r["Counter_Value"]) * 1024.0,
+                       (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3) for r in csv.DictReader(open(path)))
+        cal = [v for _, n, v, _ in rows if n.startswith("calib_f32x4")]
+        g = [(v, us) for _, n, v, us in rows if "gemm_f32x6" in n]
+        assert len(g) % 2 == 0, len(g)
+        return g[len(g) // 2:], statistics.median(cal)
+    fetch, cf = per_launch(os.path.join(a.dir, "pmc_fetch", "run_counter_collection.csv"))
+    write, cw = per_launch(os.path.join(a.dir, "pmc_write", "run_counter_collection.csv"))
+    assert len(fetch) == len(write)
+    rf, wf = CAL_BYTES / cf, CAL_BYTES / cw
+    rd = sum(v for v, _ in fetch) * rf
+    wr = sum(v for v, _ in write) * wf
+    n = len(fetch)
+    out = {"calibration": {"x16_read_factor": rf, "x16_write_factor": wf}, "kernel": "rmbx::gemm_f32x6_kernel",
+           "launches_per_inference": n, "read_bytes_per_inference": rd, "write_bytes_per_inference": wr,
+           "traffic_bytes_per_launch": (rd + wr) / n,
+           "us_per_inference_under_pmc": sum(t for _, t in fetch),
+           "per_launch": [{"read_bytes": f[0] * rf, "write_bytes": w[0] * wf, "us_under_pmc": f[1]}
+                          for f, w in zip(fetch, write)]}
+    with open(a.out, "w") as f:
+        json.dump(out, f, indent=1)
+    print(json.dumps({k: v for k, v in out.items() if k != "per_launch"}, indent=1))
+
+
 def main():
     p = argparse.ArgumentParser()
     p.add_argument("--winograd", action="store_true", help="reduce scripts/gpurun/wino_pmc.sh output")
+    p.add_argument("--gemm", action="store_true", help="reduce scripts/gpurun/gemm_pmc.sh output")
     p.add_argument("--frames", type=int, default=1024, help="--winograd: frames per call")
     p.add_argument("dir")
     p.add_argument("--out", required=True)
@@ -86,6 +116,8 @@ def main():
     a = p.parse_args()
     if a.winograd:
         return winograd(a)
+    if a.gemm:
+        return gemm(a)
     fetch, nf, dur = medians(os.path.join(a.dir, "pmc_fetch", "run_counter_collection.csv"))
     write, nw, _ = medians(os.path.join(a.dir, "pmc_write", "run_counter_collection.csv"))
     cal = {
