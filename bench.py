@@ -194,12 +194,13 @@ def gemm_probe(ro):
         K.GEMM_PROBE = None
     if not probe:
         return None
-    ms = flops = 0.0
+    ms = flops = nbytes = 0.0
     shapes = {}
-    for name, fl, e0, e1 in probe:
+    for name, fl, nb, e0, e1 in probe:
         dt = e0.elapsed_time(e1)
         ms += dt
         flops += fl
+        nbytes += nb
         L = shapes.setdefault(name, {"launches": 0, "ms": 0.0, "flops": 0.0})
         L["launches"] += 1
         L["ms"] += dt
@@ -212,7 +213,7 @@ def gemm_probe(ro):
             "frac": ex / MFMA_PEAK_TFLOPS["bf16"], "traffic": None if traffic is None else round(traffic),
             "traffic_unit": "HBM bytes per launch, mean over the launches of one fp32 ACT inference at 1024 envs",
             "traffic_source": src,
-            "algorithmic_bytes_per_launch": None,
+            "algorithmic_bytes_per_launch": round(nbytes / len(probe)),
             "kernel": "rmbx::gemm_f32x6_kernel (fp32-accurate GEMM / implicit-GEMM conv on v_mfma_f32_16x16x32_bf16: "
                       "each f32 operand split into three bf16 pieces, six piece products, f32 accumulation)",
             "flops": "executed bf16 MFMA FLOPs = 6 x the f32 problem's 2*M*N*K",

@@ -761,14 +761,16 @@ LINEAR_F32X6_BN, LINEAR_F32X6_BK = 128, 32
 GEMM_PROBE = None
 
 
-def _gemm_launch(name, flops, fn, *args):
+def _gemm_launch(name, flops, nbytes, fn, *args):
+    """nbytes: the launch's algorithmic HBM bytes (f32 A in, the three bf16 W planes, f32 C out and
+    the residual if any)."""
     if GEMM_PROBE is None:
         return N.call(fn, *args)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     N.call(fn, *args)
     e1.record()
-    GEMM_PROBE.append((name, flops, e0, e1))
+    GEMM_PROBE.append((name, flops, nbytes, e0, e1))
 
 
 def split_bf16x3(w):
@@ -808,7 +810,7 @@ def linear_f32x6(x, planes, bias=None, relu=False, out=None):
         out = torch.empty((M, Nn), dtype=torch.float32, device=x.device)
     elif out.dtype != torch.float32 or out.stride(-1) != 1 or out.shape != (M, Nn):
         raise ValueError("out must be an f32 [M, N] tensor with contiguous rows")
-    _gemm_launch(f"linear M={M} N={Nn} K={K}", 2.0 * M * Nn * K, "rmbx_linear_f32x6", N.ptr(x2), x2.stride(0),
+    _gemm_launch(f"linear M={M} N={Nn} K={K}", 2.0 * M * Nn * K, 4 * M * K + 6 * Nn * K + 4 * M * Nn, "rmbx_linear_f32x6", N.ptr(x2), x2.stride(0),
                  N.ptr(planes), planes.stride(1), planes.stride(0), N.ptr(bias), N.ptr(out), out.stride(0), M, Nn, K,
                  1 if relu else 0, N.stream_ptr())
     return out.view(*x.shape[:-1], Nn)
@@ -853,6 +855,7 @@ def conv2d_f32x6(x, planes, bias, kernel_size, stride=1, padding=0, relu=False, 
         if res.shape != out.shape or res.dtype != torch.float32 or not res.is_contiguous(memory_format=torch.channels_last):
             raise ValueError("conv2d_f32x6: res must be a channels_last f32 tensor shaped like the output")
     _gemm_launch(f"conv {kh}x{kw}/{stride} {c}->{cout} {h}x{w_}", 2.0 * n * ho * wo * cout * c * kh * kw,
+                 4 * n * h * w_ * c + 6 * cout * c * kh * kw + 4 * n * ho * wo * cout * (1 if res is None else 2),
                  "rmbx_conv2d_f32x6", N.ptr(x), n, h, w_, c, N.ptr(planes), N.ptr(bias), N.ptr(res), N.ptr(out), cout,
                  kh, kw, stride, padding, 1 if relu else 0, N.stream_ptr())
     return out
@@ -899,7 +902,8 @@ def conv3x3_wino4_x6(x, planes, bias, relu=False, res=None):
     V = torch.empty((36, T, C), dtype=torch.float32, device=x.device)
     N.call("rmbx_wino4_input_f32", N.ptr(x), n, H, W, C, N.ptr(V), N.stream_ptr())
     M = torch.empty((36, T, co), dtype=torch.float32, device=x.device)
-    _gemm_launch(f"winograd x36 M={T} N={co} K={C}", 2.0 * 36 * T * co * C, "rmbx_linear_f32x6_batched", N.ptr(V), C,
+    _gemm_launch(f"winograd x36 M={T} N={co} K={C}", 2.0 * 36 * T * co * C, 36 * (4 * T * C + 6 * co * C + 4 * T * co),
+                 "rmbx_linear_f32x6_batched", N.ptr(V), C,
                  T * C, N.ptr(planes), planes.stride(1), planes.stride(0), co * C, None, N.ptr(M), co, T * co, 36, T,
                  co, C, 0, N.stream_ptr())
     N.call("rmbx_wino4_output_f32", N.ptr(M), n, H, W, co, N.ptr(bias), N.ptr(res), N.ptr(out), 1 if relu else 0,

@@ -312,6 +312,16 @@ class ActModel(nn.Module):
             v_all = F.linear(mem, wv, bv)
         return [(k_all[..., i * D: (i + 1) * D], v_all[..., i * D: (i + 1) * D]) for i in range(n_dec)]
 
+    def _input_proj(self, feat):
+        """input_proj (1x1 conv 512 -> d) of the trunk's features; on the device in f32 with
+        channels_last features it is one rmbx_linear_f32x6 over the NHWC pixels (no layout copy)."""
+        c = self.input_proj
+        if (self._fused is not None and feat.is_contiguous(memory_format=torch.channels_last)
+                and _x6_ok(feat.permute(0, 2, 3, 1), c.out_channels)):
+            y = _x6_linear(self, "input_proj", feat.permute(0, 2, 3, 1), c.weight.view(c.out_channels, -1), c.bias)
+            return y.permute(0, 3, 1, 2)
+        return c(feat)
+
     def _pos(self, h, w, device, dtype):
         key = (h, w, str(device), dtype)
         if key not in self._pos_cache:
@@ -332,11 +342,11 @@ class ActModel(nn.Module):
         for c in range(image.shape[1]):
             x = image[:, c]
             if s2d:
-                f = self.input_proj(trunk.forward_s2d(x.contiguous()))
+                f = self._input_proj(trunk.forward_s2d(x.contiguous()))
             else:
                 if self._fused is not None:
                     x = x.contiguous(memory_format=torch.channels_last)
-                f = self.input_proj(trunk(x))  # [B, d, h, w]
+                f = self._input_proj(trunk(x))  # [B, d, h, w]
             feats.append(f)
             poss.append(self._pos(f.shape[2], f.shape[3], f.device, f.dtype))
         src = torch.cat(feats, dim=3).flatten(2).transpose(1, 2)  # [B, hw, d]
