@@ -17,6 +17,8 @@
 #include <vector>
 
 #include "rmbx_common.h"
+
+#include <cstdlib>
 #include "rmbx_math.h"
 #include "rmbx_model.h"
 
@@ -3489,7 +3491,8 @@ __global__ void __launch_bounds__(64) front_kernel(KArgs args) {
 }
 
 // back half: Newton solve, constraint forces, sensors, implicitfast integration (4 waves/env)
-__global__ void __launch_bounds__(SOLVER_THREADS, 4) solver_kernel(KArgs args) {
+template <int MINB>
+__global__ void __launch_bounds__(SOLVER_THREADS, MINB) solver_kernel(KArgs args) {
   __shared__ SolverShared S;
   const int env = blockIdx.x;
   const int tid = threadIdx.x;
@@ -3569,6 +3572,21 @@ __global__ void __launch_bounds__(SOLVER_THREADS, 4) solver_kernel(KArgs args) {
   if (tid == 0) e.stats[2] = iters;
   if (args.integrate_flag) solver_integrate(e, S, a, bi, bj, own, tid, args.sub, args.hBblk);
   PROF(7)
+}
+
+// solver blocks resident per CU (launch bound): 4 (<= 128 VGPRs, spills) by default;
+// RMBX_SOLVER_MINB = 3 / 2 for the register-budget measurement (scripts/prof_physics.py)
+static void launch_solver(int n_env, hipStream_t st, const KArgs& a) {
+  static const int minb = [] {
+    const char* v = getenv("RMBX_SOLVER_MINB");
+    return v ? atoi(v) : 4;
+  }();
+  if (minb == 2)
+    hipLaunchKernelGGL(solver_kernel<2>, dim3(n_env), dim3(SOLVER_THREADS), 0, st, a);
+  else if (minb == 3)
+    hipLaunchKernelGGL(solver_kernel<3>, dim3(n_env), dim3(SOLVER_THREADS), 0, st, a);
+  else
+    hipLaunchKernelGGL(solver_kernel<4>, dim3(n_env), dim3(SOLVER_THREADS), 0, st, a);
 }
 
 static Layout make_layout(const rmbx_model& m) {
@@ -3944,7 +3962,7 @@ static int launch(rmbx_engine* eng, int nsub, int integ, const uint8_t* active, 
     else
       hipLaunchKernelGGL(front_kernel<false>, dim3(eng->n_env), dim3(64), front_lds, st, a);
     RMBX_CHECK_LAUNCH();
-    hipLaunchKernelGGL(solver_kernel, dim3(eng->n_env), dim3(SOLVER_THREADS), 0, st, a);
+    launch_solver(eng->n_env, st, a);
     RMBX_CHECK_LAUNCH();
   }
   if (integ) {
@@ -3959,7 +3977,7 @@ static int launch(rmbx_engine* eng, int nsub, int integ, const uint8_t* active, 
     else
       hipLaunchKernelGGL(front_kernel<false>, dim3(eng->n_env), dim3(64), front_lds, st, a);
     RMBX_CHECK_LAUNCH();
-    hipLaunchKernelGGL(solver_kernel, dim3(eng->n_env), dim3(SOLVER_THREADS), 0, st, a);
+    launch_solver(eng->n_env, st, a);
     RMBX_CHECK_LAUNCH();
   }
   return RMBX_OK;
