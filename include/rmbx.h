@@ -430,6 +430,12 @@ int rmbx_linear_f32x6_batched(const float* a, long long lda, long long a_bs, con
 int rmbx_wino4_input_f32(const float* in, int N, int H, int W, int C, float* V, void* stream);
 int rmbx_wino4_output_f32(const float* M, int N, int H, int W, int C, const float* bias, const float* res, float* out,
                           int relu, void* stream);
+/* Direct f32 convolution for few input channels (the 3-channel 7x7 / stride-2 stem of the diffusion
+ * policy's GroupNorm ResNet-18 encoder, third_party/diffusion_policy [absent]): out NHWC [N][Ho][Wo][Cout]
+ * = conv(in NHWC [N][H][W][C], w [Cout][KH][KW][C]) + bias (NULL: none); fixed f32 summation order
+ * (deterministic).  Cout % 16 == 0, Cout * KH * KW * C <= 12544. */
+int rmbx_conv2d_direct_f32(const float* in, int N, int H, int W, int C, const float* w, const float* bias, float* out,
+                           int Cout, int KH, int KW, int stride, int pad, void* stream);
 /* planes[p * n + i] = bf16 piece p of x[i], x = x0 + x1 + x2 exactly (round-to-nearest-even at each
  * level): the weight form rmbx_linear_f32x6 reads. */
 int rmbx_split_bf16x3(const float* x, void* planes, long long n, void* stream);

@@ -100,8 +100,13 @@ __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
 }
 
-template <bool CONV>
+// VAR (profiling, RMBX_GEMM_VAR): bit 0 = s_setprio(1) around each MFMA half-step, bits 1-2 = row
+// tiles per block group 8 (0), 4 (1), 16 (2), bit 3 = no output stores (phase skip: the epilogue's
+// cost; the result is not written), bit 4 = epilogue through LDS with 16-byte stores (needs
+// ldc % 4 == 0 and 16-B aligned C / res / bias rows)
+template <bool CONV, int VAR = 0>
 __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
+  constexpr int GROUP = ((VAR >> 1) & 3) == 1 ? 4 : ((VAR >> 1) & 3) == 2 ? 16 : GM_GROUP;
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * GM_STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 3, wn = wave >> 2;
@@ -120,9 +125,9 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
     g.W += item * g.w_bs;
     g.C += item * g.c_bs;
   }
-  const int per_group = GM_GROUP * g.tiles_n;
-  const int first_m = (lin / per_group) * GM_GROUP;
-  const int gsize = min(g.tiles_m - first_m, GM_GROUP);
+  const int per_group = GROUP * g.tiles_n;
+  const int first_m = (lin / per_group) * GROUP;
+  const int gsize = min(g.tiles_m - first_m, GROUP);
   const int in_group = lin - (lin / per_group) * per_group;
   const int tm = first_m + in_group % gsize, tn = in_group / gsize;
   const int m0 = tm * GM_BM, n0 = tn * GM_BN;
@@ -285,9 +290,13 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
                                          // hipcc's wait before the split stays counted
     bf16x8 b[4][3];
     read_b(b, buf);
+    if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(1);
     half_step(buf, 0, b);
+    if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(0);
     if (more) store_a(Rcur, okcur, buf ^ 1);
+    if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(1);
     half_step(buf, 1, b);
+    if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(0);
     if (more) {
       wait_vm<4>();
       asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -298,6 +307,44 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
     if (kt + 1 < KT) step(kt + 1, Ra, oka, Rb, okb);
   }
 
+  if constexpr ((VAR & 16) != 0) {
+    // epilogue through LDS: each wave writes its 64 x 64 accumulator tile row-major into its own
+    // 16 KiB of the (now idle) stage buffers (row pitch 68 floats: the 16 lanes of a column group
+    // write 16 consecutive floats, rows 4 apart land on different banks), then reads it back as
+    // float4 rows so every lane stores 16 contiguous bytes (16 stores per lane instead of 64)
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    constexpr int PITCH = 68;
+    float* T = reinterpret_cast<float*>(smem) + wave * (64 * PITCH);
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int nj = 0; nj < 4; ++nj)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) T[(mi * 16 + 4 * fs + e) * PITCH + nj * 16 + fr] = acc[mi][nj][e];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave reads only its own tile
+    const int c4 = (lane & 15) * 4;                      // 4 columns of the 64
+    const int n = n0 + wn * 64 + c4;
+    float4 bn = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (g.bias) bn = *(const float4*)(g.bias + n);
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int r = it * 4 + (lane >> 4);
+      const int m = m0 + wm * 64 + r;
+      if (m < g.M) {
+        float4 v = *(const float4*)(T + r * PITCH + c4);
+        v.x += bn.x; v.y += bn.y; v.z += bn.z; v.w += bn.w;
+        if (g.res) {
+          const float4 rv = *(const float4*)(g.res + (long long)m * g.ldc + n);
+          v.x += rv.x; v.y += rv.y; v.z += rv.z; v.w += rv.w;
+        }
+        if (g.relu) {
+          v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+        }
+        *(float4*)(g.C + (long long)m * g.ldc + n) = v;
+      }
+    }
+    return;
+  }
   // epilogue: accumulator register e of lane l is C[row 4 (l/16) + e][col l%16] of its tile
 #pragma unroll
   for (int nj = 0; nj < 4; ++nj) {
@@ -309,7 +356,7 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
         const int m = mb + e;
-        if (m < g.M) {
+        if (!(VAR & 8) && m < g.M) {
           float v = acc[mi][nj][e] + bn;
           if (g.res) v += g.res[(long long)m * g.ldc + n];
           if (g.relu) v = fmaxf(v, 0.f);
@@ -328,6 +375,30 @@ __global__ void split_bf16x3_kernel(const float* __restrict__ x, uint16_t* __res
     planes[i] = (uint16_t)(p0 & 0xffff);
     planes[n + i] = (uint16_t)(p1 & 0xffff);
     planes[2 * n + i] = (uint16_t)(p2 & 0xffff);
+  }
+}
+
+// default: the LDS-transposed epilogue with 16-byte stores (VAR 16: 1.04-1.08x over 64 scalar
+// stores per lane, profiles/r3_gemm_var_sweep.log) whenever the output / residual / bias rows allow
+// 16-byte accesses; RMBX_GEMM_VAR overrides (profiling)
+template <bool CONV>
+void launch_gemm(long long blocks, const GemmArgs& g, hipStream_t st) {
+  static const int env_var = [] {
+    const char* e = getenv("RMBX_GEMM_VAR");
+    return e ? atoi(e) : -1;
+  }();
+  const bool vec_ok = g.ldc % 4 == 0 && ((uintptr_t)g.C | (uintptr_t)g.res | (uintptr_t)g.bias) % 16 == 0 &&
+                      (g.batch <= 1 || g.c_bs % 4 == 0);
+  int var = env_var >= 0 ? env_var : 16;
+  if (!vec_ok) var &= ~16;
+  switch (var) {
+    case 1: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 1>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
+    case 2: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 2>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
+    case 4: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 4>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
+    case 8: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 8>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
+    case 16: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 16>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
+    case 18: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 18>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
+    default: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 0>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g);
   }
 }
 
@@ -359,8 +430,7 @@ extern "C" int rmbx_linear_f32x6(const float* a, long long lda, const void* w_pl
                    (M + rmbx::GM_BM - 1) / rmbx::GM_BM, N / rmbx::GM_BN, nullptr};
   const long long blocks = (long long)g.tiles_m * g.tiles_n;
   RMBX_CHECK_ARG(blocks < (1ll << 31), "rmbx_linear_f32x6: too many tiles");
-  hipLaunchKernelGGL(rmbx::gemm_f32x6_kernel<false>, dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0,
-                     (hipStream_t)stream, g);
+  rmbx::launch_gemm<false>(blocks, g, (hipStream_t)stream);
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
 }
@@ -386,8 +456,7 @@ extern "C" int rmbx_linear_f32x6_batched(const float* a, long long lda, long lon
   g.c_bs = c_bs;
   const long long blocks = (long long)g.tiles_m * g.tiles_n * batch;
   RMBX_CHECK_ARG(blocks < (1ll << 31), "rmbx_linear_f32x6_batched: too many tiles");
-  hipLaunchKernelGGL(rmbx::gemm_f32x6_kernel<false>, dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0,
-                     (hipStream_t)stream, g);
+  rmbx::launch_gemm<false>(blocks, g, (hipStream_t)stream);
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
 }
@@ -412,8 +481,7 @@ extern "C" int rmbx_conv2d_f32x6(const float* in, int N, int H, int W, int C, co
                    H, W, C, Ho, Wo, KW, stride, pad};
   const long long blocks = (long long)g.tiles_m * g.tiles_n;
   RMBX_CHECK_ARG(blocks < (1ll << 31), "rmbx_conv2d_f32x6: too many tiles");
-  hipLaunchKernelGGL(rmbx::gemm_f32x6_kernel<true>, dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0,
-                     (hipStream_t)stream, g);
+  rmbx::launch_gemm<true>(blocks, g, (hipStream_t)stream);
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
 }

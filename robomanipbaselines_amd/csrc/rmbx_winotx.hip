@@ -153,3 +153,82 @@ extern "C" int rmbx_wino4_output_f32(const float* M, int N, int H, int W, int C,
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
 }
+
+// ---------------------------------------------------------------------------------------------
+// Direct f32 convolution for few input channels (the 3-channel 7x7 / stride-2 stem of the
+// diffusion policy's GroupNorm ResNet-18 image encoder, robomimic ResNet18Conv inside
+// third_party/diffusion_policy [absent], run by policy/diffusion_policy/RolloutDiffusionPolicy.py in
+// fp32): out[n][oy][ox][co] = sum_{ky,kx,c} in[n][iy][ix][c] w[co][ky][kx][c] (+ bias), NHWC.
+// MIOpen's deterministic solver set for this shape is its naive kernel (4.3 s per 4096-image
+// call); this one keeps the fixed f32 summation order (deterministic) at the VALU rate.  Thread =
+// one output pixel x 16 output channels (consecutive threads: consecutive pixels of one channel
+// group); the filter bank [Cout][KH*KW*C] sits in LDS and is read as a broadcast.
+// ---------------------------------------------------------------------------------------------
+namespace rmbx {
+namespace {
+
+constexpr int DC_MAX_W = 64 * 7 * 7 * 4;  // filter floats held in LDS (Cout <= 64, K <= 196)
+
+__global__ void __launch_bounds__(256) conv_direct_f32_kernel(const float* __restrict__ in, const float* __restrict__ w,
+                                                              const float* __restrict__ bias, float* __restrict__ out,
+                                                              int N, int H, int W, int C, int Ho, int Wo, int Cout,
+                                                              int KH, int KW, int stride, int pad) {
+  __shared__ float sw[DC_MAX_W];
+  const int K = KH * KW * C;
+  for (int i = threadIdx.x; i < Cout * K; i += blockDim.x) sw[i] = w[i];
+  __syncthreads();
+  const int groups = Cout / 16;
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long npix = (long long)N * Ho * Wo;
+  if (idx >= npix * groups) return;
+  const int cg = (int)(idx / npix);  // a wave shares its filter group: broadcast weight reads
+  const long long p = idx - cg * npix;
+  const int ox = (int)(p % Wo);
+  const long long q = p / Wo;
+  const int oy = (int)(q % Ho);
+  const long long n = q / Ho;
+  float acc[16];
+#pragma unroll
+  for (int j = 0; j < 16; ++j) acc[j] = bias ? bias[16 * cg + j] : 0.f;
+  const float* wb = sw + (16 * cg) * K;
+  for (int ky = 0; ky < KH; ++ky) {
+    const int iy = oy * stride - pad + ky;
+    if ((unsigned)iy >= (unsigned)H) continue;
+    for (int kx = 0; kx < KW; ++kx) {
+      const int ix = ox * stride - pad + kx;
+      if ((unsigned)ix >= (unsigned)W) continue;
+      const float* src = in + ((n * H + iy) * W + ix) * C;
+      const int k0 = (ky * KW + kx) * C;
+      for (int c = 0; c < C; ++c) {
+        const float v = src[c];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) acc[j] = fmaf(v, wb[j * K + k0 + c], acc[j]);
+      }
+    }
+  }
+  float4* o = (float4*)(out + p * Cout + 16 * cg);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) o[j] = make_float4(acc[4 * j], acc[4 * j + 1], acc[4 * j + 2], acc[4 * j + 3]);
+}
+
+}  // namespace
+}  // namespace rmbx
+
+extern "C" int rmbx_conv2d_direct_f32(const float* in, int N, int H, int W, int C, const float* w, const float* bias,
+                                      float* out, int Cout, int KH, int KW, int stride, int pad, void* stream) {
+  RMBX_CHECK_ARG(in && w && out && N >= 0 && H > 0 && W > 0 && C > 0 && KH > 0 && KW > 0 && stride > 0 && pad >= 0,
+                 "rmbx_conv2d_direct_f32: bad arguments");
+  RMBX_CHECK_ARG(Cout % 16 == 0 && Cout * KH * KW * C <= rmbx::DC_MAX_W,
+                 "rmbx_conv2d_direct_f32: Cout=%d must be a multiple of 16 and the filter bank fit %d floats", Cout,
+                 rmbx::DC_MAX_W);
+  RMBX_CHECK_ARG(((uintptr_t)out) % 16 == 0, "rmbx_conv2d_direct_f32: out must be 16-B aligned");
+  const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
+  RMBX_CHECK_ARG(Ho > 0 && Wo > 0, "rmbx_conv2d_direct_f32: empty output");
+  const long long n = (long long)N * Ho * Wo * (Cout / 16);
+  if (n == 0) return RMBX_OK;
+  RMBX_CHECK_ARG((n + 255) / 256 < (1ll << 31), "rmbx_conv2d_direct_f32: too many pixels");
+  hipLaunchKernelGGL(rmbx::conv_direct_f32_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0,
+                     (hipStream_t)stream, in, w, bias, out, N, H, W, C, Ho, Wo, Cout, KH, KW, stride, pad);
+  RMBX_CHECK_LAUNCH();
+  return RMBX_OK;
+}

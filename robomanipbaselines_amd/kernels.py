@@ -909,3 +909,23 @@ def conv3x3_wino4_x6(x, planes, bias, relu=False, res=None):
     N.call("rmbx_wino4_output_f32", N.ptr(M), n, H, W, co, N.ptr(bias), N.ptr(res), N.ptr(out), 1 if relu else 0,
            N.stream_ptr())
     return out
+
+
+def conv2d_direct_f32(x, weight, bias, stride=1, padding=0):
+    """conv2d(x, weight, bias, stride, padding) for few input channels by rmbx_conv2d_direct_f32
+    (deterministic f32 VALU kernel); x f32 channels_last [N, C, H, W], weight [Cout, C, KH, KW];
+    result channels_last."""
+    if x.dtype != torch.float32 or not x.is_cuda or not x.is_contiguous(memory_format=torch.channels_last):
+        raise ValueError("conv2d_direct_f32: x must be an f32 channels_last device tensor")
+    n, c, h, w_ = x.shape
+    co, ci, kh, kw = weight.shape
+    if ci != c:
+        raise ValueError("conv2d_direct_f32: channel mismatch")
+    wp = weight.detach().float().permute(0, 2, 3, 1).contiguous()
+    if bias is not None:
+        _chk(bias, torch.float32, (co,), "bias")
+    ho, wo = (h + 2 * padding - kh) // stride + 1, (w_ + 2 * padding - kw) // stride + 1
+    out = torch.empty((n, co, ho, wo), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
+    N.call("rmbx_conv2d_direct_f32", N.ptr(x), n, h, w_, c, N.ptr(wp), N.ptr(bias), N.ptr(out), co, kh, kw, stride,
+           padding, N.stream_ptr())
+    return out

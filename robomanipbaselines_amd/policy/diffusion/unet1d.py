@@ -31,6 +31,24 @@ class SinusoidalPosEmb(nn.Module):
         return torch.cat((emb.sin(), emb.cos()), dim=-1)
 
 
+def _gemm(owner, name, x2, w2, bias):
+    """F.linear(x2, w2, bias) with w2 derived from owner.weight; f32 on the device through
+    rmbx_linear_f32x6 (fp32-accurate bf16x6 GEMM) where the shape allows, with w2's bf16 pieces
+    cached on `owner` per version of owner.weight."""
+    from ... import kernels as K
+
+    if x2.is_cuda and x2.dtype == torch.float32 and K.linear_f32x6_supported(x2, w2.shape[0]):
+        src = owner.weight
+        key = (src.data_ptr(), src._version, tuple(w2.shape))
+        cache = owner.__dict__.setdefault("_x6", {})
+        ent = cache.get(name)
+        if ent is None or ent[0] != key:
+            ent = (key, K.split_bf16x3(w2.detach().contiguous()))
+            cache[name] = ent
+        return K.linear_f32x6(x2, ent[1], bias)
+    return F.linear(x2, w2, bias)
+
+
 def conv1d_gemm(x, conv):
     """Conv1d as one GEMM: the k-tap windows of x [B, C, T] (padding, stride) unfolded to
     [B*To, C*k] rows times the weight viewed [Cout, C*k] (hipBLASLt), -> [B, Cout, To].  At
@@ -41,7 +59,7 @@ def conv1d_gemm(x, conv):
     cols = (F.pad(x, (p, p)) if p else x).unfold(2, k, st)
     To = cols.shape[2]
     cols = cols.permute(0, 2, 1, 3).reshape(B * To, C * k)
-    y = F.linear(cols, conv.weight.reshape(conv.out_channels, C * k), conv.bias)
+    y = _gemm(conv, "w", cols, conv.weight.reshape(conv.out_channels, C * k), conv.bias)
     return y.view(B, To, -1).transpose(1, 2).contiguous()
 
 
@@ -51,7 +69,7 @@ def conv_transpose1d_gemm(x, conv):
     B, C, T = x.shape
     Co = conv.weight.shape[1]
     wk = conv.weight.permute(2, 1, 0).reshape(4 * Co, C)
-    P = F.linear(x.transpose(1, 2).reshape(B * T, C), wk).view(B, T, 4, Co)
+    P = _gemm(conv, "wt", x.transpose(1, 2).reshape(B * T, C), wk, None).view(B, T, 4, Co)
     even = P[:, :, 1] + F.pad(P[:, :-1, 3], (0, 0, 1, 0))
     odd = P[:, :, 2] + F.pad(P[:, 1:, 0], (0, 0, 0, 1))
     y = torch.stack([even, odd], dim=2).view(B, 2 * T, Co)
@@ -65,8 +83,9 @@ def _device_form(x):
 
 
 def run_conv(conv, x):
-    """conv(x), through the GEMM forms above on the device (bf16 and f32: hipBLASLt GEMMs are
-    deterministic, so the captured denoising loop holds no MIOpen call)."""
+    """conv(x), through the GEMM forms above on the device (bf16: hipBLASLt; f32: rmbx_linear_f32x6
+    where the shape allows, else hipBLASLt -- all deterministic, so the captured denoising loop
+    holds no MIOpen call)."""
     if isinstance(conv, nn.Identity) or not _device_form(x):
         return conv(x)
     if isinstance(conv, nn.ConvTranspose1d):

@@ -25,6 +25,38 @@ from ..diffusion.schedulers import DDIMSampler, DDPMSampler
 from ..diffusion.unet1d import ConditionalUnet1D
 
 
+def _conv(conv, x):
+    """conv(x) (bias-free); f32 channels_last on the device through the rmbx kernels (deterministic,
+    no MIOpen Find): rmbx_conv2d_f32x6 (fp32-accurate bf16x6 implicit GEMM) where C % 32 == 0 and
+    Cout % 128 == 0, the fused Winograd F(4x4) f32 kernel for the 64-channel stride-1 3x3 convs,
+    rmbx_conv2d_direct_f32 for the 3-channel stem (MIOpen's only deterministic solver for it is its
+    naive kernel: 4.3 s per 4096-image call); MIOpen otherwise."""
+    from ... import kernels as K
+
+    if not (x.is_cuda and x.dtype == torch.float32):
+        return conv(x)
+    # (torch's GroupNorm hands back NCHW-contiguous tensors: re-lay them out, a memory-bound copy)
+    x = x.contiguous(memory_format=torch.channels_last)
+    w = conv.weight
+    key = (w.data_ptr(), w._version)
+    cache = conv.__dict__.get("_rmbx")
+    if K.conv2d_f32x6_supported(conv.in_channels, conv.out_channels) and conv.stride[0] == conv.stride[1]:
+        if cache is None or cache[0] != key:
+            cache = (key, K.pack_conv_f32x6(w))
+            conv.__dict__["_rmbx"] = cache
+        return K.conv2d_f32x6(x, cache[1], None, conv.kernel_size, conv.stride[0], conv.padding[0])
+    if (conv.in_channels == conv.out_channels == 64 and tuple(conv.kernel_size) == (3, 3) and conv.stride[0] == 1
+            and conv.padding[0] == 1):
+        if cache is None or cache[0] != key:
+            cache = (key, (K.pack_winograd4_f32(w), torch.zeros(64, device=w.device)))
+            conv.__dict__["_rmbx"] = cache
+        return K.conv3x3_winograd4_f32(x, cache[1][0], cache[1][1])
+    if conv.in_channels <= 4 and conv.out_channels % 16 == 0 and conv.stride[0] == conv.stride[1] \
+            and conv.padding[0] == conv.padding[1]:
+        return K.conv2d_direct_f32(x, w, conv.bias, conv.stride[0], conv.padding[0])
+    return conv(x)
+
+
 class GNBasicBlock(nn.Module):
     def __init__(self, cin, cout, stride):
         super().__init__()
@@ -37,9 +69,9 @@ class GNBasicBlock(nn.Module):
             self.downsample = nn.Sequential(nn.Conv2d(cin, cout, 1, stride, bias=False), nn.GroupNorm(cout // 16, cout))
 
     def forward(self, x):
-        idt = x if self.downsample is None else self.downsample(x)
-        y = F.relu(self.bn1(self.conv1(x)))
-        return F.relu(self.bn2(self.conv2(y)) + idt)
+        idt = x if self.downsample is None else self.downsample[1](_conv(self.downsample[0], x))
+        y = F.relu(self.bn1(_conv(self.conv1, x)))
+        return F.relu(self.bn2(_conv(self.conv2, y)) + idt)
 
 
 class ResNet18GNConv(nn.Module):
@@ -55,7 +87,11 @@ class ResNet18GNConv(nn.Module):
         self.nets = nn.Sequential(*layers)
 
     def forward(self, x):
-        return self.nets(x)
+        stem = self.nets[0]
+        x = _conv(stem, x)
+        for layer in list(self.nets)[1:]:
+            x = layer(x)
+        return x
 
 
 class SpatialSoftmax(nn.Module):
@@ -70,8 +106,32 @@ class SpatialSoftmax(nn.Module):
         self.register_buffer("pos_x", torch.from_numpy(px.reshape(1, h * w)).float())
         self.register_buffer("pos_y", torch.from_numpy(py.reshape(1, h * w)).float())
 
+    def _keypoint_maps(self, f):
+        """the 1x1 keypoint conv; f32 channels_last on the device: one rmbx_linear_f32x6 over the NHWC
+        pixels with the 32 keypoint rows zero-padded to the kernel's 128-column tile (deterministic)."""
+        from ... import kernels as K
+
+        c = self.nets
+        if not (f.is_cuda and f.dtype == torch.float32 and c.in_channels % 32 == 0):
+            return c(f)
+        f = f.contiguous(memory_format=torch.channels_last)
+        w = c.weight
+        key = (w.data_ptr(), w._version)
+        cache = self.__dict__.get("_x6")
+        if cache is None or cache[0] != key:
+            n_pad = -(-c.out_channels // 128) * 128
+            wp = torch.zeros(n_pad, c.in_channels, dtype=torch.float32, device=w.device)
+            wp[: c.out_channels] = w.detach().reshape(c.out_channels, -1)
+            bp = torch.zeros(n_pad, dtype=torch.float32, device=w.device)
+            bp[: c.out_channels] = c.bias.detach()
+            cache = (key, K.split_bf16x3(wp), bp)
+            self.__dict__["_x6"] = cache
+        B, C, H, W = f.shape
+        y = K.linear_f32x6(f.permute(0, 2, 3, 1), cache[1], cache[2])[..., : c.out_channels]  # [B, H, W, kp]
+        return y.permute(0, 3, 1, 2)
+
     def forward(self, f):
-        f = self.nets(f).reshape(-1, self.h * self.w)
+        f = self._keypoint_maps(f).reshape(-1, self.h * self.w)
         att = F.softmax(f.float(), dim=-1)
         ex = torch.sum(self.pos_x * att, dim=1, keepdim=True)
         ey = torch.sum(self.pos_y * att, dim=1, keepdim=True)

@@ -13,6 +13,8 @@ horizon 16, n_obs_steps 2, n_action_steps 8, image_size 320x240, crop 288x216.
 """
 
 import numpy as np
+import os
+
 import torch
 
 from ... import kernels as K
@@ -58,7 +60,8 @@ class RolloutDiffusionPolicy(BatchedRolloutBase):
         # parity mode: deterministic MIOpen solvers only (no atomic split-K), so a seed reproduces
         # its episodes bit for bit, as the reference's TrainDiffusionPolicy/rollout setup intends
         torch.backends.cudnn.benchmark = True
-        torch.backends.cudnn.deterministic = self.policy_dtype == torch.float32
+        torch.backends.cudnn.deterministic = (self.policy_dtype == torch.float32
+                                              and os.environ.get("RMBX_DP_DETERMINISTIC", "1") != "0")
         self.policy = self.policy.eval().requires_grad_(False).to(device=self.device, dtype=self.policy_dtype)
         self.policy.obs_nets = self.policy.obs_nets.to(memory_format=torch.channels_last)
 

@@ -140,3 +140,25 @@ def test_conv2d_f32x6_trunk_shape_8_frames():
     got = K_.conv2d_f32x6(x.to(DEV).contiguous(memory_format=torch.channels_last), K_.pack_conv_f32x6(w.to(DEV)),
                           b.to(DEV), 3, 2, 1, relu=True)
     assert _err(got.cpu(), _conv_ref(x, w, b, 2, 1, True, None)) <= 4e-6
+
+
+@torch.no_grad()
+@pytest.mark.parametrize("n,C,H,W,Cout,k,stride,pad,bias", [(3, 3, 37, 45, 64, 7, 2, 3, False),
+                                                          (2, 3, 216, 288, 64, 7, 2, 3, True),
+                                                          (2, 4, 9, 11, 32, 3, 1, 1, True)])
+def test_conv2d_direct_f32_vs_f64(n, C, H, W, Cout, k, stride, pad, bias):
+    """rmbx_conv2d_direct_f32 (the diffusion policy's 3-channel stem): f32 FMA in a fixed order,
+    deterministic, vs an f64 F.conv2d (bar 1e-5 relative; K <= 196 terms)."""
+    from robomanipbaselines_amd import kernels as K_
+
+    g = torch.Generator(device="cpu").manual_seed(H * W)
+    x = torch.randn(n, C, H, W, generator=g)
+    w = torch.randn(Cout, C, k, k, generator=g) / (C * k * k) ** 0.5
+    b = torch.randn(Cout, generator=g) if bias else None
+    xd = x.to(DEV).contiguous(memory_format=torch.channels_last)
+    got = K_.conv2d_direct_f32(xd, w.to(DEV), None if b is None else b.to(DEV), stride, pad)
+    again = K_.conv2d_direct_f32(xd, w.to(DEV), None if b is None else b.to(DEV), stride, pad)
+    assert torch.equal(got, again)
+    ref = F.conv2d(x.double(), w.double(), None if b is None else b.double(), stride, pad)
+    assert got.shape == ref.shape and got.is_contiguous(memory_format=torch.channels_last)
+    assert _err(got.cpu(), ref) <= 1e-5
