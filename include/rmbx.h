@@ -439,6 +439,12 @@ int rmbx_conv2d_direct_f32(const float* in, int N, int H, int W, int C, const fl
 /* planes[p * n + i] = bf16 piece p of x[i], x = x0 + x1 + x2 exactly (round-to-nearest-even at each
  * level): the weight form rmbx_linear_f32x6 reads. */
 int rmbx_split_bf16x3(const float* x, void* planes, long long n, void* stream);
+/* rmbx_attention_f32 with fp32-accurate products on the bf16 matrix cores: Q, K, V and the softmax
+ * probabilities split into three bf16 pieces, six piece products per product accumulated in f32 (the
+ * rmbx_linear_f32x6 scheme); same layouts, strides and output as rmbx_attention_f32. */
+int rmbx_attention_f32x6(const float* q, const float* k, const float* v, float* out, int B, int heads, int Lq, int Lk,
+                         long long q_bstride, int q_rstride, long long k_bstride, int k_rstride, long long v_bstride,
+                         int v_rstride, float scale, void* stream);
 /* Residual add + LayerNorm over the last dim of [rows][D] rows (D <= 2048, multiple of 8 bf16 / 4
  * f32): out = LayerNorm(rnd(x + r)) * weight + bias (f32 weight/bias), r optional (NULL); replaces
  * the add + nn.LayerNorm pair of the ACT transformer's post-norm layers (third_party/act). */

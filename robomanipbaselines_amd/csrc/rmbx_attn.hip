@@ -392,6 +392,221 @@ __global__ void __launch_bounds__(64 * AF_MAX_WAVES) __attribute__((amdgpu_waves
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// fp32-accurate form on the bf16 matrix cores (rmbx_attention_f32x6; the reference's fp32 policy):
+// every f32 operand of the two products (Q, K, V and the probabilities P) is split into three bf16
+// pieces x = x0 + x1 + x2 and each product accumulates the six piece products with i + j <= 2 in f32
+// (the rmbx_linear_f32x6 scheme, csrc/rmbx_gemm.hip): the f32 GEMM error class at 2.67x the f32
+// MFMA rate.  Layout of the bf16 kernel above (S^T = K Q^T with each lane owning one query, P fed
+// from the S accumulator registers, V's dims permuted so each lane finishes 16 consecutive dims),
+// keys streamed through double-buffered 32-key LDS tiles as in the f32 kernel: per tile and buffer
+// K [3 pieces][32 keys][64 dims] (16-byte chunk c of key row r at c ^ ((r >> 1) & 7)) and V^T
+// [3 pieces][64 dims][32 positions] (position p holds key at_key_of_pos(p); chunk c of dim row d at
+// c ^ ((d >> 2) & 3)), 24 KiB; the block's threads load the next tile into registers under this
+// tile's MFMAs and split + store it after them; one barrier per tile.
+// ---------------------------------------------------------------------------------------------
+constexpr int AX_MAX_WAVES = 5;
+constexpr int AX_PLANE = 32 * 64;               // bf16 elements of one piece of a K or V^T tile
+constexpr int AX_BUF = 6 * AX_PLANE;            // K pieces then V^T pieces
+constexpr int AX_CH = (1024 + 64 * 4 - 1) / (64 * 4);  // staged 16-byte chunks per thread (>= 256 threads)
+
+__device__ __forceinline__ uint32_t ax_pk(float x, float y) {
+  f32x2 v = {x, y};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, bf16x2));
+}
+// (x, y) -> three packed bf16 pairs, x = x0 + x1 + x2 exactly (round-to-nearest-even at each level)
+__device__ __forceinline__ void ax_split(float x, float y, uint32_t& p0, uint32_t& p1, uint32_t& p2) {
+  p0 = ax_pk(x, y);
+  const float rx = x - __uint_as_float(p0 << 16), ry = y - __uint_as_float(p0 & 0xffff0000u);
+  p1 = ax_pk(rx, ry);
+  const float sx = rx - __uint_as_float(p1 << 16), sy = ry - __uint_as_float(p1 & 0xffff0000u);
+  p2 = ax_pk(sx, sy);
+}
+// position of tile key k (0..31) in the V^T image (inverse of at_key_of_pos)
+__device__ __forceinline__ int ax_pos_of_key(int k) {
+  const int r = k & 15;
+  return 16 * (k >> 4) + 8 * ((r >> 2) & 1) + (r & 3) + 4 * (r >> 3);
+}
+
+__global__ void __launch_bounds__(64 * AX_MAX_WAVES) attn_fwd_f32x6_kernel(AttnF32Args a) {
+  __shared__ __attribute__((aligned(16))) uint16_t sA[2 * AX_BUF];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nthreads = blockDim.x;
+  const int bh = blockIdx.x / a.parts, part = blockIdx.x - bh * a.parts;
+  const int b = bh / a.heads, hd = bh - b * a.heads;
+  const int r32 = lane & 31, kh = lane >> 5;
+  const int qi = (part * (nthreads >> 6) + wave) * 32 + r32;
+  const bool q_ok = qi < a.Lq;
+  const float* kbase = a.k + (size_t)b * a.k_bstride + hd * 64;
+  const float* vbase = a.v + (size_t)b * a.v_bstride + hd * 64;
+  const int nt = (a.Lk + 31) >> 5;
+
+  // Q^T pieces (B operand of S^T = K Q^T): dims 16 s + 8 kh .. +7 of query qi
+  bf16x8 fq[4][3];
+  {
+    const float* qp = a.q + (size_t)b * a.q_bstride + (size_t)(q_ok ? qi : 0) * a.q_rstride + hd * 64 + 8 * kh;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const float4 x0 = *reinterpret_cast<const float4*>(qp + 16 * s);
+      const float4 x1 = *reinterpret_cast<const float4*>(qp + 16 * s + 4);
+      uint32_t p0[4], p1[4], p2[4];
+      ax_split(x0.x, x0.y, p0[0], p1[0], p2[0]);
+      ax_split(x0.z, x0.w, p0[1], p1[1], p2[1]);
+      ax_split(x1.x, x1.y, p0[2], p1[2], p2[2]);
+      ax_split(x1.z, x1.w, p0[3], p1[3], p2[3]);
+      fq[s][0] = __builtin_bit_cast(bf16x8, make_uint4(p0[0], p0[1], p0[2], p0[3]));
+      fq[s][1] = __builtin_bit_cast(bf16x8, make_uint4(p1[0], p1[1], p1[2], p1[3]));
+      fq[s][2] = __builtin_bit_cast(bf16x8, make_uint4(p2[0], p2[1], p2[2], p2[3]));
+    }
+  }
+
+  // staging: chunk q < 512 = K[key q/16][4 (q%16) ..], q >= 512 = V[key (q-512)/16][...]
+  float4 st[AX_CH];
+  auto load_tile = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < AX_CH; ++i) {
+      const int q = tid + nthreads * i;
+      const int qq = q & 511, key = 32 * t + (qq >> 4), quad = qq & 15;
+      const bool ok = q < 1024 && key < a.Lk;
+      const float* src = q < 512 ? kbase + (size_t)key * a.k_rstride : vbase + (size_t)key * a.v_rstride;
+      st[i] = ok ? *reinterpret_cast<const float4*>(src + 4 * quad) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto store_tile = [&](uint16_t* buf) {
+#pragma unroll
+    for (int i = 0; i < AX_CH; ++i) {
+      const int q = tid + nthreads * i;
+      if (q >= 1024) continue;
+      const int qq = q & 511, key = qq >> 4, quad = qq & 15;
+      uint32_t p0[2], p1[2], p2[2];
+      ax_split(st[i].x, st[i].y, p0[0], p1[0], p2[0]);
+      ax_split(st[i].z, st[i].w, p0[1], p1[1], p2[1]);
+      if (q < 512) {  // K: 4 dims = half a 16-byte chunk of the key row
+        const int off = key * 64 + (((quad >> 1) ^ ((key >> 1) & 7)) << 3) + 4 * (quad & 1);
+        *reinterpret_cast<uint2*>(buf + off) = make_uint2(p0[0], p0[1]);
+        *reinterpret_cast<uint2*>(buf + AX_PLANE + off) = make_uint2(p1[0], p1[1]);
+        *reinterpret_cast<uint2*>(buf + 2 * AX_PLANE + off) = make_uint2(p2[0], p2[1]);
+      } else {  // V^T: 4 dims of one key = one element in each of 4 rows
+        const int pos = ax_pos_of_key(key);
+        const uint32_t pk[3][2] = {{p0[0], p0[1]}, {p1[0], p1[1]}, {p2[0], p2[1]}};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int d = 4 * quad + e;
+          const int off = 3 * AX_PLANE + d * 32 + ((((pos >> 3) ^ ((d >> 2) & 3))) << 3) + (pos & 7);
+#pragma unroll
+          for (int pc = 0; pc < 3; ++pc)
+            buf[off + pc * AX_PLANE] = (uint16_t)((pk[pc][e >> 1] >> (16 * (e & 1))) & 0xffff);
+        }
+      }
+    }
+  };
+  load_tile(0);
+  store_tile(sA);
+  __syncthreads();
+
+  const float c = a.scale_log2;
+  const bool ragged = (a.Lk & 31) != 0;
+  const int d0 = at_sigma(r32), d1 = d0 + 32;
+  f32x16 acc0 = {}, acc1 = {};
+  float m_run = -INFINITY, l_run = 0.f;
+  for (int t = 0; t < nt; ++t) {
+    const uint16_t* buf = sA + (t & 1) * AX_BUF;
+    const bool more = t + 1 < nt;
+    if (more) load_tile(t + 1);
+    // S^T tile: six piece products per 16-dim step
+    f32x16 s = {};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int off = r32 * 64 + (((2 * ks + kh) ^ ((r32 >> 1) & 7)) << 3);
+      const bf16x8 k0 = *reinterpret_cast<const bf16x8*>(buf + off);
+      const bf16x8 k1 = *reinterpret_cast<const bf16x8*>(buf + AX_PLANE + off);
+      const bf16x8 k2 = *reinterpret_cast<const bf16x8*>(buf + 2 * AX_PLANE + off);
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k2, fq[ks][0], s, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, fq[ks][1], s, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, fq[ks][2], s, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k1, fq[ks][0], s, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, fq[ks][1], s, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_32x32x16_bf16(k0, fq[ks][0], s, 0, 0, 0);
+    }
+    // this lane's 16 keys: 32 t + 4 kh + (j & 3) + 8 (j >> 2); padding keys only in the last tile
+    if (ragged && t == nt - 1) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (32 * t + 4 * kh + (j & 3) + 8 * (j >> 2) >= a.Lk) s[j] = -INFINITY;
+    }
+    float mx = s[0];
+#pragma unroll
+    for (int j = 1; j < 16; ++j) mx = fmaxf(mx, s[j]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const float m_new = fmaxf(m_run, mx);
+    if (__any(m_new != m_run)) {
+      const float alpha = exp2f((m_run - m_new) * c);  // first tile: exp2(-inf) = 0
+      l_run *= alpha;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        acc0[j] *= alpha;
+        acc1[j] *= alpha;
+      }
+      m_run = m_new;
+    }
+    const float mc = m_run * c;
+    // P pieces: the B operand of O^T += V^T P^T, k-step u from registers 8 u .. 8 u + 7
+    bf16x8 fp[2][3];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      uint32_t p0[4], p1[4], p2[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float pa = exp2f(fmaf(s[8 * u + 2 * e], c, -mc));
+        const float pb = exp2f(fmaf(s[8 * u + 2 * e + 1], c, -mc));
+        l_run += pa + pb;
+        ax_split(pa, pb, p0[e], p1[e], p2[e]);
+      }
+      fp[u][0] = __builtin_bit_cast(bf16x8, make_uint4(p0[0], p0[1], p0[2], p0[3]));
+      fp[u][1] = __builtin_bit_cast(bf16x8, make_uint4(p1[0], p1[1], p1[2], p1[3]));
+      fp[u][2] = __builtin_bit_cast(bf16x8, make_uint4(p2[0], p2[1], p2[2], p2[3]));
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int cc = 2 * u + kh;
+      const int o0 = 3 * AX_PLANE + d0 * 32 + ((cc ^ ((d0 >> 2) & 3)) << 3);
+      const int o1 = 3 * AX_PLANE + d1 * 32 + ((cc ^ ((d1 >> 2) & 3)) << 3);
+      bf16x8 v0[3], v1[3];
+#pragma unroll
+      for (int pc = 0; pc < 3; ++pc) {
+        v0[pc] = *reinterpret_cast<const bf16x8*>(buf + o0 + pc * AX_PLANE);
+        v1[pc] = *reinterpret_cast<const bf16x8*>(buf + o1 + pc * AX_PLANE);
+      }
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v0[2], fp[u][0], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v1[2], fp[u][0], acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v0[1], fp[u][1], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v1[1], fp[u][1], acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v0[0], fp[u][2], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v1[0], fp[u][2], acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v0[1], fp[u][0], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v1[1], fp[u][0], acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v0[0], fp[u][1], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v1[0], fp[u][1], acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v0[0], fp[u][0], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_bf16(v1[0], fp[u][0], acc1, 0, 0, 0);
+    }
+    if (more) store_tile(sA + ((t + 1) & 1) * AX_BUF);
+    __syncthreads();
+  }
+  const float l_tot = l_run + __shfl_xor(l_run, 32);
+  if (!q_ok) return;
+  const float inv = 1.f / l_tot;
+  // acc0 register e = dim 16 kh + e, acc1 = dim 32 + 16 kh + e
+  float* op = a.o + ((size_t)b * a.Lq + qi) * a.o_rstride + hd * 64 + 16 * kh;
+#pragma unroll
+  for (int q4 = 0; q4 < 4; ++q4) {
+    *reinterpret_cast<float4*>(op + 4 * q4) =
+        make_float4(acc0[4 * q4] * inv, acc0[4 * q4 + 1] * inv, acc0[4 * q4 + 2] * inv, acc0[4 * q4 + 3] * inv);
+    *reinterpret_cast<float4*>(op + 32 + 4 * q4) =
+        make_float4(acc1[4 * q4] * inv, acc1[4 * q4 + 1] * inv, acc1[4 * q4 + 2] * inv, acc1[4 * q4 + 3] * inv);
+  }
+}
+
 }  // namespace
 }  // namespace rmbx
 
@@ -485,6 +700,44 @@ extern "C" int rmbx_attention_f32(const float* q, const float* k, const float* v
     case 10: hipLaunchKernelGGL(rmbx::attn_fwd_f32_kernel<10>, g, blk, 0, (hipStream_t)stream, a); break;
     default: RMBX_CHECK_ARG(false, "rmbx_attention_f32: RMBX_ATTN_F32_DBG=%d not instantiated", dbg);
   }
+  RMBX_CHECK_LAUNCH();
+  return RMBX_OK;
+}
+
+extern "C" int rmbx_attention_f32x6(const float* q, const float* k, const float* v, float* out, int B, int heads,
+                                    int Lq, int Lk, long long q_bstride, int q_rstride, long long k_bstride,
+                                    int k_rstride, long long v_bstride, int v_rstride, float scale, void* stream) {
+  RMBX_CHECK_ARG(q && k && v && out, "rmbx_attention_f32x6: null pointer");
+  RMBX_CHECK_ARG(B >= 0 && heads > 0 && Lq > 0 && Lk > 0, "rmbx_attention_f32x6: bad geometry");
+  RMBX_CHECK_ARG(scale > 0.f, "rmbx_attention_f32x6: scale must be positive");
+  RMBX_CHECK_ARG(q_rstride % 4 == 0 && k_rstride % 4 == 0 && v_rstride % 4 == 0 && q_bstride % 4 == 0 &&
+                     k_bstride % 4 == 0 && v_bstride % 4 == 0,
+                 "rmbx_attention_f32x6: strides must be multiples of 4 elements");
+  RMBX_CHECK_ARG((((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)out) & 15) == 0,
+                 "rmbx_attention_f32x6: pointers must be 16-byte aligned");
+  if (B == 0) return RMBX_OK;
+  rmbx::AttnF32Args a;
+  a.q = q;
+  a.k = k;
+  a.v = v;
+  a.o = out;
+  a.q_bstride = q_bstride;
+  a.k_bstride = k_bstride;
+  a.v_bstride = v_bstride;
+  a.q_rstride = q_rstride;
+  a.k_rstride = k_rstride;
+  a.v_rstride = v_rstride;
+  a.o_rstride = heads * 64;
+  a.heads = heads;
+  a.Lq = Lq;
+  a.Lk = Lk;
+  a.scale_log2 = scale * 1.4426950408889634f;
+  const int ngroups = (Lq + 31) / 32;
+  const int waves = ngroups >= rmbx::AX_MAX_WAVES ? rmbx::AX_MAX_WAVES : 4;
+  a.parts = (ngroups + waves - 1) / waves;
+  const long long nblocks = (long long)B * heads * a.parts;
+  RMBX_CHECK_ARG(nblocks < (1ll << 31), "rmbx_attention_f32x6: grid too large");
+  hipLaunchKernelGGL(rmbx::attn_fwd_f32x6_kernel, dim3((unsigned)nblocks), dim3(64 * waves), 0, (hipStream_t)stream, a);
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
 }

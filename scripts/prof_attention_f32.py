@@ -35,6 +35,7 @@ with torch.no_grad():
         k, v = kv.split(512, dim=-1)
         flop = 4.0 * B * 8 * Lq * Lk * 64
         ms_r = timed(lambda: K.attention_f32(q, k, v, 8))
+        ms_6 = timed(lambda: K.attention_f32(q, k, v, 8, x6=True))
 
         def sdpa():
             qh = q.view(B, Lq, 8, 64).transpose(1, 2)
@@ -49,6 +50,7 @@ with torch.no_grad():
                 os.environ["RMBX_ATTN_F32_DBG"] = d
                 dbg["dbg" + d] = round(timed(lambda: K.attention_f32(q, k, v, 8)), 3)
         os.environ.pop("RMBX_ATTN_F32_DBG", None)
-        out[name] = {"rmbx_ms": round(ms_r, 3), **dbg, "rmbx_tflops": round(flop / ms_r / 1e9, 1),
+        out[name] = {"rmbx_ms": round(ms_r, 3), "rmbx_x6_ms": round(ms_6, 3),
+                     "rmbx_x6_bf16_mfma_frac": round(6 * flop / ms_6 / 1e9 / 2500, 3), **dbg, "rmbx_tflops": round(flop / ms_r / 1e9, 1),
                      "rmbx_frac_of_157": round(flop / ms_r / 1e9 / 157.3, 3), "sdpa_ms": round(ms_t, 3)}
     print(json.dumps(out), flush=True)

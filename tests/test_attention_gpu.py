@@ -88,3 +88,45 @@ def test_attention_f32_strided_qkv_views():
     got = K.attention_f32(q, k, v, 8)
     want = _ref(q, k, v, 8)
     assert (got - want).abs().max().item() <= 1e-5 * 4
+
+
+def _ref64(q, k, v, heads):
+    B, Lq, D = q.shape
+    Lk = k.shape[1]
+    qh = q.double().reshape(B, Lq, heads, 64).transpose(1, 2)
+    kh = k.double().reshape(B, Lk, heads, 64).transpose(1, 2)
+    vh = v.double().reshape(B, Lk, heads, 64).transpose(1, 2)
+    p = torch.softmax(qh @ kh.transpose(-1, -2) / 8.0, dim=-1)
+    return (p @ vh).transpose(1, 2).reshape(B, Lq, D)
+
+
+@torch.no_grad()
+@pytest.mark.parametrize("B,H,Lq,Lk", [(3, 8, 302, 302), (4, 8, 100, 100), (2, 8, 100, 302), (1, 8, 1, 1),
+                                       (2, 2, 257, 33), (1, 1, 130, 650)])
+def test_attention_f32x6_matches_f64(B, H, Lq, Lk):
+    """rmbx_attention_f32x6 (Q, K, V, P split into three bf16 pieces, six piece products per
+    product on the bf16 matrix cores, f32 accumulation and softmax) vs an f64 reference, beside the
+    f32-MFMA kernel it replaces: both within 1e-5 of the output scale (|v| <= 4)."""
+    from robomanipbaselines_amd import kernels as K
+
+    g = torch.Generator(device=DEV).manual_seed(Lq * 41 + Lk)
+    D = H * 64
+    q = torch.randn(B, Lq, D, device=DEV, generator=g) * 2
+    k = torch.randn(B, Lk, D, device=DEV, generator=g) * 2
+    v = torch.randn(B, Lk, D, device=DEV, generator=g).clamp(-4, 4)
+    want = _ref64(q, k, v, H)
+    e6 = (K.attention_f32(q, k, v, H, x6=True).double() - want).abs().max().item()
+    e32 = (K.attention_f32(q, k, v, H).double() - want).abs().max().item()
+    print(f"\nB={B} H={H} Lq={Lq} Lk={Lk}: x6 {e6:.2e}  f32 {e32:.2e}")
+    assert e6 <= 1e-5 * 4, (e6, e32)
+
+
+@torch.no_grad()
+def test_attention_f32x6_strided_qkv_views():
+    from robomanipbaselines_amd import kernels as K
+
+    g = torch.Generator(device=DEV).manual_seed(13)
+    qkv = torch.randn(2, 150, 3 * 512, device=DEV, generator=g)
+    q, k, v = qkv.split(512, dim=-1)
+    got = K.attention_f32(q, k, v, 8, x6=True)
+    assert (got.double() - _ref64(q, k, v, 8)).abs().max().item() <= 1e-5 * 4
