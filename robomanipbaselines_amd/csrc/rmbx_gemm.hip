@@ -103,7 +103,8 @@ __device__ __forceinline__ void wait_vm() {
 // VAR (profiling, RMBX_GEMM_VAR): bit 0 = s_setprio(1) around each MFMA half-step, bits 1-2 = row
 // tiles per block group 8 (0), 4 (1), 16 (2), bit 3 = no output stores (phase skip: the epilogue's
 // cost; the result is not written), bit 4 = epilogue through LDS with 16-byte stores (needs
-// ldc % 4 == 0 and 16-B aligned C / res / bias rows)
+// ldc % 4 == 0 and 16-B aligned C / res / bias rows), bit 5 = no A split (phase skip: the split's
+// VALU cost; truncated pieces, wrong values)
 template <bool CONV, int VAR = 0>
 __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
   constexpr int GROUP = ((VAR >> 1) & 3) == 1 ? 4 : ((VAR >> 1) & 3) == 2 ? 16 : GM_GROUP;
@@ -211,8 +212,17 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
     uint32_t p0[8], p1[8], p2[8];
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      split_pair(R[i].x, R[i].y, p0[2 * i], p1[2 * i], p2[2 * i]);
-      split_pair(R[i].z, R[i].w, p0[2 * i + 1], p1[2 * i + 1], p2[2 * i + 1]);
+      if constexpr ((VAR & 32) != 0) {  // phase skip: truncated bf16 pieces (realistic values, no split VALU)
+        p0[2 * i] = __builtin_amdgcn_perm(__float_as_uint(R[i].y), __float_as_uint(R[i].x), 0x07060302u);
+        p0[2 * i + 1] = __builtin_amdgcn_perm(__float_as_uint(R[i].w), __float_as_uint(R[i].z), 0x07060302u);
+        p1[2 * i] = p0[2 * i + 1];
+        p1[2 * i + 1] = p0[2 * i];
+        p2[2 * i] = p0[2 * i];
+        p2[2 * i + 1] = p0[2 * i + 1];
+      } else {
+        split_pair(R[i].x, R[i].y, p0[2 * i], p1[2 * i], p2[2 * i]);
+        split_pair(R[i].z, R[i].w, p0[2 * i + 1], p1[2 * i + 1], p2[2 * i + 1]);
+      }
     }
     unsigned char* base = smem + buf * GM_STAGE;
     *(uint4*)(base + aoff0) = make_uint4(p0[0], p0[1], p0[2], p0[3]);
@@ -398,6 +408,7 @@ void launch_gemm(long long blocks, const GemmArgs& g, hipStream_t st) {
     case 8: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 8>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
     case 16: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 16>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
     case 18: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 18>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
+    case 48: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 48>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
     default: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 0>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g);
   }
 }
