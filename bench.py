@@ -496,7 +496,10 @@ def bf16_action_error(ro32, ro16, n=16):
     state = ro32.get_state()[:n]
     img32 = ro32.get_images(torch.float32)[:n]  # the renderer's f32 space-to-depth frame
     c32 = ro32.policy(state, img32).float()
-    if img32.shape[-1] != 16:
+    if img32.dtype == torch.uint8:  # the 8-bit frame of the f32 stem: the bf16 policy takes it normalised
+        mean, std = ro32.image_norm
+        img32 = K.s2d_u8_normalize(img32, mean, std)
+    elif img32.shape[-1] != 16:
         img32 = K.image_to_s2d(img32[:, 0])[:, None]
     c16 = ro16.policy(state.to(torch.bfloat16), img32.to(torch.bfloat16)).float()
     std = torch.tensor(ro32.model_meta_info["action"]["std"], dtype=torch.float32, device=c32.device)

@@ -301,7 +301,8 @@ int rmbx_motion_command(const double* placement, const double* action, int actio
  * normalisation of the ACT/MLP backbones), or (dtype 2) the same values in bf16 as a 2x2
  * space-to-depth image [n][H/2][W/2][16] (channel (dy*2+dx)*3+c, 12..15 zero) for
  * rmbx_stem_s2d_conv (H, W even), or (dtype 3) that space-to-depth image in f32 for
- * rmbx_stem_s2d_conv_maxpool_f32.
+ * rmbx_stem_s2d_conv_maxpool_f32, or (dtype 4) the space-to-depth image of the 8-bit values u
+ * themselves (u8, mean/std not applied) for rmbx_stem_s2d_conv_maxpool_u8.
  * ------------------------------------------------------------------------------------------- */
 typedef struct rmbx_camera {
   int32_t body;        /* body the camera is attached to (0 = world) */
@@ -387,6 +388,19 @@ int rmbx_stem_s2d_conv_maxpool(const void* in, const void* weight, const float* 
  * are zero and are not multiplied.  Replaces the same reference ops as above. */
 int rmbx_stem_s2d_conv_maxpool_f32(const float* in, const float* weight, const float* bias, float* out,
                                    int N, int Hs, int Ws, int band_rows, void* stream);
+/* The f32 stem on the quantised image (the reference's precision, fewer MFMA cycles): in
+ * [N][Hs][Ws][16] u8 (rmbx_render policy_dtype 4: the 8-bit pixel values u, channel
+ * (dy*2+dx)*3+c, 12..15 zero); w_planes bf16 [3][64][16 taps][16] = the three exact bf16 pieces
+ * (RNE at each level) of W'[co][tap][ch] = W[co][tap][ch] / (255 std[ch % 3]) for the packed
+ * filter W of pack_stem_s2d; bias f32 [64] = conv bias - sum over all taps of W mean/std; edge f32
+ * [16][16][64] = the mean/std term of the out-of-image taps, indexed by the row mask of ky and the
+ * column mask of kx that fall outside the image.  out [N][Hp][Wp][64] f32 =
+ * maxpool3x3s2p1(relu(conv(x) + bias)) for x = (u / 255 - mean) / std, the renderer's policy
+ * pixels: the piece products are exact and accumulate in f32 (v_mfma_f32_32x32x16_bf16).
+ * Replaces the same reference ops as rmbx_stem_s2d_conv_maxpool_f32 plus the image
+ * normalisation (RolloutBase.py:479-490, the ACT backbone's ImageNet Normalize). */
+int rmbx_stem_s2d_conv_maxpool_u8(const uint8_t* in, const void* w_planes, const float* bias, const float* edge,
+                                  float* out, int N, int Hs, int Ws, int band_rows, void* stream);
 /* Multi-head attention forward, bf16: out[b][i][h*64 + d] = sum_j softmax_j(scale * q_i . k_j) v_j[d]
  * over the heads of q/k/v rows [b][row][h*64 .. h*64+63] (row/batch strides in elements, last dim
  * contiguous), f32 softmax and accumulation, head dim 64, Lk <= 320, no mask; out contiguous

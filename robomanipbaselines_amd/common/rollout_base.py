@@ -213,6 +213,9 @@ class BatchedRolloutBase:
                and getattr(self.policy, "accepts_s2d", False) and H % 2 == 0 and W % 2 == 0
                and (dtype == torch.bfloat16 or W // 2 <= K.STEM_POOL_MAX_WS))
         shape = (H // 2, W // 2, 16) if s2d else (3, H, W)
+        if s2d and dtype == torch.float32 and getattr(self.policy, "accepts_u8_s2d", False):
+            # the f32 policy folds mean / std into its stem: the renderer hands over the 8-bit values
+            dtype = torch.uint8
         if getattr(self, "_img", None) is None or self._img.dtype != dtype or tuple(self._img.shape[2:]) != shape:
             self._img = torch.empty((self.n, len(self.camera_names)) + shape, dtype=dtype, device=self.device)
             self._img_cam = [torch.empty((self.n,) + shape, dtype=dtype, device=self.device) for _ in self.camera_names]

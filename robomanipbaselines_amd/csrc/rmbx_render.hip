@@ -440,6 +440,15 @@ __global__ void __launch_bounds__(256) render_kernel(RenderArgs a) {
       for (int c = 0; c < 3; c++) o[q + c] = ((float)u[c] / 255.0f - a.cam.mean[c]) / a.cam.std[c];
       if ((py & 1) && (px & 1))
         for (int c = 12; c < 16; c++) o[c] = 0.0f;
+    } else if (a.policy_dtype == 4) {
+      // the same space-to-depth layout holding the 8-bit pixel values themselves (the f32 stem on
+      // the quantised image, rmbx_stem_s2d_conv_maxpool_u8, applies mean / std exactly)
+      const int Hs = H >> 1, Ws = W >> 1;
+      uint8_t* o = reinterpret_cast<uint8_t*>(a.policy) + (((size_t)env * Hs + (py >> 1)) * Ws + (px >> 1)) * 16;
+      const int q = ((py & 1) * 2 + (px & 1)) * 3;
+      for (int c = 0; c < 3; c++) o[q + c] = u[c];
+      if ((py & 1) && (px & 1))
+        for (int c = 12; c < 16; c++) o[c] = 0;
     } else {
       for (int c = 0; c < 3; c++) {
         const float v = ((float)u[c] / 255.0f - a.cam.mean[c]) / a.cam.std[c];
@@ -468,8 +477,8 @@ extern "C" int rmbx_render(const rmbx_camera* cam, const int32_t* prim_i32, cons
   RMBX_CHECK_ARG(cam->width > 0 && cam->height > 0 && cam->width <= 8192 && cam->height <= 8192,
                  "bad image size %dx%d", cam->width, cam->height);
   RMBX_CHECK_ARG(cam->body >= 0 && cam->body < nbody, "bad camera body %d", cam->body);
-  RMBX_CHECK_ARG(policy_dtype >= 0 && policy_dtype <= 3,
-                 "policy_dtype must be 0 (f32), 1 (bf16), 2 (bf16 s2d) or 3 (f32 s2d)");
+  RMBX_CHECK_ARG(policy_dtype >= 0 && policy_dtype <= 4,
+                 "policy_dtype must be 0 (f32), 1 (bf16), 2 (bf16 s2d), 3 (f32 s2d) or 4 (u8 s2d)");
   RMBX_CHECK_ARG(policy_dtype < 2 || (cam->width % 2 == 0 && cam->height % 2 == 0),
                  "space-to-depth policy output needs an even image size");
   if (n_env == 0) return RMBX_OK;

@@ -29,6 +29,7 @@
 #include "rmbx_common.h"
 
 #include <cstdint>
+#include <cstdlib>
 
 namespace rmbx {
 namespace {
@@ -466,6 +467,418 @@ __global__ void __launch_bounds__(SF_THREADS) stem_pool_f32_kernel(StemPoolF32Ar
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// f32-accurate form on the quantised image (rmbx_render policy_dtype 4): the pixels the policy
+// sees are x = (u / 255 - mean[c]) / std[c] with u an 8-bit integer (RolloutBase.py:479-490 +
+// the backbone's ImageNet normalisation), so
+//   conv(x)[co] = sum_in W'[co][tap][ch] u[tap][ch]  +  bias  -  sum_in W[co][tap][ch] mean/std
+// with W' = W / (255 std) and "in" = the taps inside the image.  u is exact in bf16 (<= 8
+// significant bits), W' is split exactly into three bf16 pieces (RNE at each level, as
+// rmbx_linear_f32x6), so the three piece products W'_p u are exact in the f32 accumulator:
+// v_mfma_f32_32x32x16_bf16, 3 MFMAs of 32 cycles per 16-channel tap against 8 of 64 cycles for
+// the f32 kernel's 32x32x2_f32 (per k: 6 cycles vs 32).  The mean term is constant except where
+// taps fall outside the image: bias_eff = bias - (the term of all 16 taps) and edge[rm][cm][co]
+// adds back the term of the out-of-range taps (row mask rm of ky, column mask cm of kx).
+// Mapping as the bf16 kernel: wave w = stem column tile w (32 columns), two stem rows x two
+// 32-channel tiles = 4 accumulators; the three weight planes stay in LDS (96 KiB), the input
+// rows in a 5-row LDS ring of bf16 integers converted from the u8 image (16 B per s2d pixel).
+// ---------------------------------------------------------------------------------------------
+constexpr int SQ_LDS_BYTES = 16 * 3 * 2 * 64 * 16 + SP_RING * 2 * SP_RC_MAX * 16 + 64 * 4 + SP_MAX_WAVES * 2 * 32 * 4;
+static_assert(SQ_LDS_BYTES <= 160 * 1024, "u8 stem+pool LDS must fit the 160 KiB of a CU");
+
+struct StemPoolU8Args {
+  const uint8_t* in;    // [N][Hs][Ws][16] u8
+  const uint16_t* w;    // [3 pieces][64][16 taps][16] bf16 bits
+  const float* bias;    // [64] bias_eff
+  const float* edge;    // [16 rm][16 cm][64]
+  float* out;           // [N][Hp][Wp][64]
+  int N, Hs, Ws, Hp, Wp;
+  int nct, rc;
+  int bands, band_rows;
+};
+
+// 16 u8 pixels channels -> two 16-B halves of bf16 integers (exact: <= 8 significant bits)
+__device__ __forceinline__ void u8x16_to_bf16(uint4 v, uint4& lo, uint4& hi) {
+  uint32_t o[8];
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const uint32_t b0 = __float_as_uint((float)(w[i] & 0xffu)), b1 = __float_as_uint((float)((w[i] >> 8) & 0xffu));
+    const uint32_t b2 = __float_as_uint((float)((w[i] >> 16) & 0xffu)), b3 = __float_as_uint((float)(w[i] >> 24));
+    o[2 * i] = (b0 >> 16) | (b1 & 0xffff0000u);
+    o[2 * i + 1] = (b2 >> 16) | (b3 & 0xffff0000u);
+  }
+  lo = make_uint4(o[0], o[1], o[2], o[3]);
+  hi = make_uint4(o[4], o[5], o[6], o[7]);
+}
+
+__global__ void __launch_bounds__(SP_THREADS) stem_pool_u8_kernel(StemPoolU8Args a) {
+  __shared__ __attribute__((aligned(16))) unsigned char sq_smem[SQ_LDS_BYTES];
+  uint16_t* sW = reinterpret_cast<uint16_t*>(sq_smem);       // [16 taps][3 pieces][2 halves][64 cout][8]
+  uint16_t* sR = sW + 16 * 3 * 2 * 64 * 8;                   // [5 slots][2 halves][rc][8]
+  float* sBias = reinterpret_cast<float*>(sR + SP_RING * 2 * a.rc * 8);  // [64]
+  float* sEdge = sBias + 64;                                             // [nct][2 h][2 t][16]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nthreads = blockDim.x;
+  const int img = blockIdx.x / a.bands, band = blockIdx.x - img * a.bands;
+  const int py0 = band * a.band_rows;
+  const int py1 = min(a.Hp, py0 + a.band_rows);
+  if (py0 >= py1) return;
+  const int pys = py0 > 0 ? py0 - 1 : 0;
+  const size_t row_px = (size_t)a.Ws;
+  const uint8_t* in_img = a.in + (size_t)img * a.Hs * row_px * 16;
+
+  // weight planes: global [p][cout][tap][16] -> sW[tap][p][half][cout][8]
+  for (int q = tid; q < 3 * 64 * 16 * 2; q += nthreads) {
+    const int half = q & 1, rest = q >> 1;  // rest = (p * 64 + cout) * 16 + tap
+    const int tap = rest & 15, pc = rest >> 4;
+    const int co = pc & 63, p = pc >> 6;
+    *reinterpret_cast<uint4*>(sW + (((tap * 3 + p) * 2 + half) * 64 + co) * 8) =
+        *reinterpret_cast<const uint4*>(a.w + (size_t)rest * 16 + half * 8);
+  }
+  if (tid < 64) sBias[tid] = a.bias[tid];
+
+  // s2d pixel (ring col c) of row y -> both halves; zero outside the image
+  auto load_px = [&](int y, int c) -> uint4 {
+    const int x = c - 2;
+    if (y < 0 || y >= a.Hs || x < 0 || x >= a.Ws) return make_uint4(0, 0, 0, 0);
+    return *reinterpret_cast<const uint4*>(in_img + ((size_t)y * row_px + x) * 16);
+  };
+  auto store_px = [&](int slot, int c, uint4 v) {
+    uint4 lo, hi;
+    u8x16_to_bf16(v, lo, hi);
+    *reinterpret_cast<uint4*>(sR + ((size_t)(slot * 2) * a.rc + c) * 8) = lo;
+    *reinterpret_cast<uint4*>(sR + ((size_t)(slot * 2 + 1) * a.rc + c) * 8) = hi;
+  };
+  auto slot_of = [](int y) { return (y + 2 * SP_RING) % SP_RING; };
+  for (int q = tid; q < SP_RING * a.rc; q += nthreads) {
+    const int r = q / a.rc, c = q - r * a.rc;
+    const int y = 2 * pys - 2 + r;
+    store_px(slot_of(y), c, load_px(y, c));
+  }
+
+  const int n = lane & 31, h = lane >> 5;
+  const int X = 32 * wave + n;
+  const int m = lane & 31;
+  const int sig = 16 * ((m >> 2) & 1) + (m & 3) + 4 * (m >> 3);
+  const bool col_ok = X < a.Ws;
+  // out-of-image kx taps of this lane's stem column (the mean term added back by the edge table)
+  int cm = 0;
+#pragma unroll
+  for (int kx = 0; kx < 4; ++kx) cm |= (int)((unsigned)(X - 2 + kx) >= (unsigned)a.Ws) << kx;
+
+  constexpr int PF_MAX = 2;  // (2 rows * 324 cols) / 640 threads, rounded up
+  uint4 pf[PF_MAX];
+  uint32_t pf_ok = 0;
+  const int pf_px = 2 * a.rc;
+  int pf_r[PF_MAX], pf_c[PF_MAX];
+#pragma unroll
+  for (int i = 0; i < PF_MAX; ++i) {
+    const int q = min(tid + nthreads * i, pf_px - 1);
+    pf_r[i] = q / a.rc;
+    pf_c[i] = q - pf_r[i] * a.rc;
+  }
+
+  float carry[2][16];
+#pragma unroll
+  for (int t = 0; t < 2; ++t)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) carry[t][k] = 0.f;
+
+  __syncthreads();
+  for (int py = pys; py < py1; ++py) {
+    const int Y0 = 2 * py;
+    const bool more = py + 1 < py1;
+    if (more) {
+      pf_ok = 0;
+#pragma unroll
+      for (int i = 0; i < PF_MAX; ++i) {
+        const int y = Y0 + 3 + pf_r[i];
+        const int x = pf_c[i] - 2;
+        const bool ok = tid + nthreads * i < pf_px && y < a.Hs && x >= 0 && x < a.Ws;
+        const size_t off = ok ? ((size_t)y * row_px + x) * 16 : 0;
+        pf[i] = *reinterpret_cast<const uint4*>(in_img + off);
+        pf_ok |= (uint32_t)ok << i;
+      }
+    }
+    f32x16 acc[2][2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r)
+#pragma unroll
+      for (int t = 0; t < 2; ++t) acc[r][t] = f32x16{};
+    int slot[5];
+#pragma unroll
+    for (int d = 0; d < 5; ++d) slot[d] = slot_of(Y0 - 2 + d);
+#pragma unroll
+    for (int tap = 0; tap < 16; ++tap) {
+      const int ky = tap >> 2, kx = tap & 3;
+      bf16x8 bx[2], aw[2][3];
+#pragma unroll
+      for (int r = 0; r < 2; ++r)
+        bx[r] = *reinterpret_cast<const bf16x8*>(sR + (((size_t)slot[r + ky] * 2 + h) * a.rc + X + kx) * 8);
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+#pragma unroll
+        for (int t = 0; t < 2; ++t)
+          aw[t][p] = *reinterpret_cast<const bf16x8*>(sW + (((tap * 3 + p) * 2 + h) * 64 + 32 * t + sig) * 8);
+      // small pieces first
+#pragma unroll
+      for (int p = 2; p >= 0; --p)
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+#pragma unroll
+          for (int t = 0; t < 2; ++t)
+            acc[r][t] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aw[t][p], bx[r], acc[r][t], 0, 0, 0);
+    }
+
+    // bias_eff (+ the edge term of the out-of-image taps) + ReLU, vertical max with the carried row
+    const bool row1_ok = Y0 + 1 < a.Hs;
+    int rm[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      rm[r] = 0;
+#pragma unroll
+      for (int ky = 0; ky < 4; ++ky) rm[r] |= (int)((unsigned)(Y0 + r - 2 + ky) >= (unsigned)a.Hs) << ky;
+    }
+    const float* ep0 = (rm[0] | cm) ? a.edge + (rm[0] * 16 + cm) * 64 + 16 * h : nullptr;
+    const float* ep1 = (rm[1] | cm) ? a.edge + (rm[1] * 16 + cm) * 64 + 16 * h : nullptr;
+    float vm[2][16];
+#pragma unroll
+    for (int t = 0; t < 2; ++t) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const float b = sBias[32 * t + 16 * h + k];
+        float v0 = acc[0][t][k] + b, v1 = acc[1][t][k] + b;
+        if (ep0) v0 += ep0[32 * t + k];  // border pixels only
+        if (ep1) v1 += ep1[32 * t + k];
+        const float p0 = fmaxf(v0, 0.f);
+        const float p1 = row1_ok ? fmaxf(v1, 0.f) : 0.f;
+        vm[t][k] = col_ok ? fmaxf(fmaxf(carry[t][k], p0), p1) : 0.f;
+        carry[t][k] = p1;
+      }
+    }
+    if (n == 31) {
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) sEdge[((wave * 2 + h) * 2 + t) * 16 + k] = vm[t][k];
+    }
+    __syncthreads();  // edges visible; every wave is done with ring rows 2py-2, 2py-1
+
+    if (more) {
+#pragma unroll
+      for (int i = 0; i < PF_MAX; ++i) {
+        if (tid + nthreads * i < pf_px) {
+          const uint4 v = ((pf_ok >> i) & 1u) ? pf[i] : make_uint4(0, 0, 0, 0);
+          store_px(pf_r[i] ? slot[1] : slot[0], pf_c[i], v);  // row Y0+3+r replaces row Y0-2+r
+        }
+      }
+    }
+    if (py >= py0) {
+      const int px = 16 * wave + (n >> 1);
+      const bool store = (n & 1) == 0 && px < a.Wp;
+      float* dst = a.out + (((size_t)img * a.Hp + py) * a.Wp + px) * 64 + 16 * h;
+#pragma unroll
+      for (int t = 0; t < 2; ++t)
+#pragma unroll
+        for (int k4 = 0; k4 < 4; ++k4) {
+          float o[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int k = 4 * k4 + e;
+            float left = __shfl_up(vm[t][k], 1);
+            const float right = __shfl_down(vm[t][k], 1);
+            if (n == 0) left = wave > 0 ? sEdge[(((wave - 1) * 2 + h) * 2 + t) * 16 + k] : 0.f;
+            o[e] = fmaxf(fmaxf(left, vm[t][k]), right);
+          }
+          if (store) *reinterpret_cast<float4*>(dst + 32 * t + 4 * k4) = make_float4(o[0], o[1], o[2], o[3]);
+        }
+    }
+    __syncthreads();  // ring refilled; edge reads done before the next pair overwrites them
+  }
+}
+
+// The same u8 stem in the f32 kernel's SIMD-balanced layout: 4 waves per block (one per SIMD;
+// 10 waves would sit 3/3/2/2 on the SIMDs of an MFMA-bound kernel), wave w = 32-channel tile
+// w & 1 of column tiles 5 (w >> 1) .. + 4 for both stem rows (10 accumulators, 512 registers).
+__global__ void __launch_bounds__(SF_THREADS) stem_pool_u8w4_kernel(StemPoolU8Args a) {
+  __shared__ __attribute__((aligned(16))) unsigned char sq_smem[16 * 3 * 2 * 64 * 16 + SP_RING * 2 * SF_RC * 16 + 64 * 4 +
+                                                               SF_WAVES * 2 * 16 * 4];
+  uint16_t* sW = reinterpret_cast<uint16_t*>(sq_smem);  // [16 taps][3 pieces][2 halves][64 cout][8]
+  uint16_t* sR = sW + 16 * 3 * 2 * 64 * 8;              // [5 slots][2 halves][SF_RC][8]
+  float* sBias = reinterpret_cast<float*>(sR + SP_RING * 2 * SF_RC * 8);  // [64]
+  float* sEdge = sBias + 64;                                              // [waves][2 h][16]
+
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int img = blockIdx.x / a.bands, band = blockIdx.x - img * a.bands;
+  const int py0 = band * a.band_rows;
+  const int py1 = min(a.Hp, py0 + a.band_rows);
+  if (py0 >= py1) return;
+  const int pys = py0 > 0 ? py0 - 1 : 0;
+  const size_t row_px = (size_t)a.Ws;
+  const uint8_t* in_img = a.in + (size_t)img * a.Hs * row_px * 16;
+
+  for (int q = tid; q < 3 * 64 * 16 * 2; q += SF_THREADS) {
+    const int half = q & 1, rest = q >> 1;
+    const int tap = rest & 15, pc = rest >> 4;
+    const int co = pc & 63, p = pc >> 6;
+    *reinterpret_cast<uint4*>(sW + (((tap * 3 + p) * 2 + half) * 64 + co) * 8) =
+        *reinterpret_cast<const uint4*>(a.w + (size_t)rest * 16 + half * 8);
+  }
+  if (tid < 64) sBias[tid] = a.bias[tid];
+
+  auto store_px = [&](int slot, int c, uint4 v) {
+    uint4 lo, hi;
+    u8x16_to_bf16(v, lo, hi);
+    *reinterpret_cast<uint4*>(sR + ((size_t)(slot * 2) * SF_RC + c) * 8) = lo;
+    *reinterpret_cast<uint4*>(sR + ((size_t)(slot * 2 + 1) * SF_RC + c) * 8) = hi;
+  };
+  auto slot_of = [](int y) { return (y + 2 * SP_RING) % SP_RING; };
+  for (int q = tid; q < SP_RING * SF_RC; q += SF_THREADS) {
+    const int r = q / SF_RC, c = q - r * SF_RC;
+    const int y = 2 * pys - 2 + r, x = c - 2;
+    uint4 v = make_uint4(0, 0, 0, 0);
+    if (y >= 0 && y < a.Hs && x >= 0 && x < a.Ws) v = *reinterpret_cast<const uint4*>(in_img + ((size_t)y * row_px + x) * 16);
+    store_px(slot_of(y), c, v);
+  }
+
+  const int n = lane & 31, h = lane >> 5;
+  const int t = wave & 1;
+  const int ct0 = SF_TILES * (wave >> 1);
+  const int sig = 16 * ((n >> 2) & 1) + (n & 3) + 4 * (n >> 3);
+  const int xcol = 32 * ct0 + n;
+
+  constexpr int PF_MAX = (2 * SF_RC + SF_THREADS - 1) / SF_THREADS;
+  uint4 pf[PF_MAX];
+  uint32_t pf_ok = 0;
+
+  float carry[SF_TILES][16];
+#pragma unroll
+  for (int i = 0; i < SF_TILES; ++i)
+#pragma unroll
+    for (int k = 0; k < 16; ++k) carry[i][k] = 0.f;
+
+  __syncthreads();
+  for (int py = pys; py < py1; ++py) {
+    const int Y0 = 2 * py;
+    const bool more = py + 1 < py1;
+    if (more) {
+      pf_ok = 0;
+#pragma unroll
+      for (int i = 0; i < PF_MAX; ++i) {
+        const int q = tid + SF_THREADS * i;
+        const int r = q / SF_RC, c = q - r * SF_RC;
+        const int y = Y0 + 3 + r, x = c - 2;
+        const bool ok = q < 2 * SF_RC && y < a.Hs && x >= 0 && x < a.Ws;
+        const size_t off = ok ? ((size_t)y * row_px + x) * 16 : 0;
+        pf[i] = *reinterpret_cast<const uint4*>(in_img + off);
+        pf_ok |= (uint32_t)ok << i;
+      }
+    }
+    f32x16 acc[SF_TILES][2];
+#pragma unroll
+    for (int i = 0; i < SF_TILES; ++i)
+#pragma unroll
+      for (int r = 0; r < 2; ++r) acc[i][r] = f32x16{};
+    int slot[5];
+#pragma unroll
+    for (int d = 0; d < 5; ++d) slot[d] = slot_of(Y0 - 2 + d);
+#pragma unroll
+    for (int tap = 0; tap < 16; ++tap) {
+      const int ky = tap >> 2, kx = tap & 3;
+      bf16x8 aw[3];
+#pragma unroll
+      for (int p = 0; p < 3; ++p)
+        aw[p] = *reinterpret_cast<const bf16x8*>(sW + (((tap * 3 + p) * 2 + h) * 64 + 32 * t + sig) * 8);
+#pragma unroll
+      for (int i = 0; i < SF_TILES; ++i) {
+        bf16x8 bx[2];
+#pragma unroll
+        for (int r = 0; r < 2; ++r)
+          bx[r] = *reinterpret_cast<const bf16x8*>(sR + (((size_t)slot[r + ky] * 2 + h) * SF_RC + xcol + 32 * i + kx) * 8);
+#pragma unroll
+        for (int p = 2; p >= 0; --p)
+#pragma unroll
+          for (int r = 0; r < 2; ++r) acc[i][r] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aw[p], bx[r], acc[i][r], 0, 0, 0);
+      }
+    }
+
+    const bool row1_ok = Y0 + 1 < a.Hs;
+    int rm[2];
+#pragma unroll
+    for (int r = 0; r < 2; ++r) {
+      rm[r] = 0;
+#pragma unroll
+      for (int ky = 0; ky < 4; ++ky) rm[r] |= (int)((unsigned)(Y0 + r - 2 + ky) >= (unsigned)a.Hs) << ky;
+    }
+#pragma unroll
+    for (int i = 0; i < SF_TILES; ++i) {
+      const int X = xcol + 32 * i;
+      const bool col_ok = X < a.Ws;
+      int cm = 0;
+#pragma unroll
+      for (int kx = 0; kx < 4; ++kx) cm |= (int)((unsigned)(X - 2 + kx) >= (unsigned)a.Ws) << kx;
+      const float* ep0 = (rm[0] | cm) ? a.edge + (rm[0] * 16 + cm) * 64 + 32 * t + 16 * h : nullptr;
+      const float* ep1 = (rm[1] | cm) ? a.edge + (rm[1] * 16 + cm) * 64 + 32 * t + 16 * h : nullptr;
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const float b = sBias[32 * t + 16 * h + k];
+        float v0 = acc[i][0][k] + b, v1 = acc[i][1][k] + b;
+        if (ep0) v0 += ep0[k];  // border pixels only
+        if (ep1) v1 += ep1[k];
+        const float p0 = fmaxf(v0, 0.f);
+        const float p1 = row1_ok ? fmaxf(v1, 0.f) : 0.f;
+        acc[i][0][k] = col_ok ? fmaxf(fmaxf(carry[i][k], p0), p1) : 0.f;
+        carry[i][k] = p1;
+      }
+    }
+    if (n == 31) {
+#pragma unroll
+      for (int k = 0; k < 16; ++k) sEdge[(wave * 2 + h) * 16 + k] = acc[SF_TILES - 1][0][k];
+    }
+    __syncthreads();
+
+    if (more) {
+#pragma unroll
+      for (int i = 0; i < PF_MAX; ++i) {
+        const int q = tid + SF_THREADS * i;
+        if (q < 2 * SF_RC) {
+          const int r = q / SF_RC, c = q - r * SF_RC;
+          store_px(slot_of(Y0 + 3 + r), c, ((pf_ok >> i) & 1u) ? pf[i] : make_uint4(0, 0, 0, 0));
+        }
+      }
+    }
+    if (py >= py0) {
+#pragma unroll
+      for (int i = 0; i < SF_TILES; ++i) {
+        const int px = 16 * (ct0 + i) + (n >> 1);
+        const bool store = (n & 1) == 0 && px < a.Wp;
+        float* dst = a.out + (((size_t)img * a.Hp + py) * a.Wp + px) * 64 + 32 * t + 16 * h;
+#pragma unroll
+        for (int k4 = 0; k4 < 4; ++k4) {
+          float o[4];
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int k = 4 * k4 + e;
+            float left = __shfl_up(acc[i][0][k], 1);
+            const float right = __shfl_down(acc[i][0][k], 1);
+            float prev;
+            if (i > 0)
+              prev = __shfl(acc[i - 1][0][k], (lane & 32) | 31);
+            else
+              prev = wave >= 2 ? sEdge[((wave - 2) * 2 + h) * 16 + k] : 0.f;
+            if (n == 0) left = prev;
+            o[e] = fmaxf(fmaxf(left, acc[i][0][k]), right);
+          }
+          if (store) *reinterpret_cast<float4*>(dst + 4 * k4) = make_float4(o[0], o[1], o[2], o[3]);
+        }
+      }
+    }
+    __syncthreads();
+  }
+}
+
 }  // namespace
 }  // namespace rmbx
 
@@ -503,6 +916,54 @@ extern "C" int rmbx_stem_s2d_conv_maxpool(const void* in, const void* weight, co
   const long long nblocks = (long long)N * a.bands;
   RMBX_CHECK_ARG(nblocks < (1ll << 31), "rmbx_stem_s2d_conv_maxpool: grid too large");
   hipLaunchKernelGGL(rmbx::stem_pool_kernel, dim3((unsigned)nblocks), dim3(64 * a.nct), 0, (hipStream_t)stream, a);
+  RMBX_CHECK_LAUNCH();
+  return RMBX_OK;
+}
+
+extern "C" int rmbx_stem_s2d_conv_maxpool_u8(const uint8_t* in, const void* w_planes, const float* bias,
+                                             const float* edge, float* out, int N, int Hs, int Ws, int band_rows,
+                                             void* stream) {
+  RMBX_CHECK_ARG(in && w_planes && bias && edge && out, "rmbx_stem_s2d_conv_maxpool_u8: null pointer");
+  RMBX_CHECK_ARG(N >= 0 && Hs > 0 && Ws > 0, "rmbx_stem_s2d_conv_maxpool_u8: bad geometry");
+  RMBX_CHECK_ARG(Ws <= 32 * rmbx::SP_MAX_WAVES, "rmbx_stem_s2d_conv_maxpool_u8: Ws=%d exceeds %d", Ws,
+                 32 * rmbx::SP_MAX_WAVES);
+  RMBX_CHECK_ARG((((uintptr_t)in | (uintptr_t)w_planes | (uintptr_t)edge | (uintptr_t)out) & 15) == 0,
+                 "rmbx_stem_s2d_conv_maxpool_u8: in/w_planes/edge/out must be 16-byte aligned");
+  if (N == 0) return RMBX_OK;
+  rmbx::StemPoolU8Args a;
+  a.in = in;
+  a.w = (const uint16_t*)w_planes;
+  a.bias = bias;
+  a.edge = edge;
+  a.out = out;
+  a.N = N;
+  a.Hs = Hs;
+  a.Ws = Ws;
+  a.Hp = (Hs - 1) / 2 + 1;
+  a.Wp = (Ws - 1) / 2 + 1;
+  a.nct = (Ws + 31) / 32;
+  a.rc = 32 * a.nct + 4;
+  RMBX_CHECK_ARG(2 * a.rc <= 2 * 64 * a.nct, "rmbx_stem_s2d_conv_maxpool_u8: prefetch does not fit");
+  // layout: 4 SIMD-balanced waves (default) or one wave per column tile (RMBX_STEM_U8_LAYOUT=10)
+  static const int layout = [] {
+    const char* e = getenv("RMBX_STEM_U8_LAYOUT");
+    return e ? atoi(e) : 4;
+  }();
+  if (band_rows <= 0) {
+    const int want_blocks = 512;
+    int bands = (want_blocks + N - 1) / N;
+    if (bands > a.Hp) bands = a.Hp;
+    band_rows = (a.Hp + bands - 1) / bands;
+  }
+  a.band_rows = band_rows;
+  a.bands = (a.Hp + band_rows - 1) / band_rows;
+  const long long nblocks = (long long)N * a.bands;
+  RMBX_CHECK_ARG(nblocks < (1ll << 31), "rmbx_stem_s2d_conv_maxpool_u8: grid too large");
+  if (layout == 10)
+    hipLaunchKernelGGL(rmbx::stem_pool_u8_kernel, dim3((unsigned)nblocks), dim3(64 * a.nct), 0, (hipStream_t)stream, a);
+  else
+    hipLaunchKernelGGL(rmbx::stem_pool_u8w4_kernel, dim3((unsigned)nblocks), dim3(rmbx::SF_THREADS), 0,
+                       (hipStream_t)stream, a);
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
 }

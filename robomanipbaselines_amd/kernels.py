@@ -704,6 +704,67 @@ def _stem_s2d_conv_maxpool_f32(x_s2d, w_packed, bias, band_rows=0):
     return out
 
 
+def pack_stem_u8(weight, bias, mean, std):
+    """Operands of rmbx_stem_s2d_conv_maxpool_u8 for the folded stem conv (weight [64, 3, 7, 7],
+    bias [64]) and the image normalisation x = (u / 255 - mean) / std: the three exact bf16 pieces
+    [3, 64, 16, 16] of W' = W / (255 std) (packed as pack_stem_s2d), bias_eff = bias - sum W mean/std
+    over every tap, and the edge table [16, 16, 64] of the mean/std term of the taps that fall
+    outside the image (row mask of ky x column mask of kx).  The mean terms are summed in f64."""
+    dev = weight.device
+    wp = pack_stem_s2d(weight.detach().double())  # [64, 4, 4, 16]
+    mean = torch.tensor(mean, dtype=torch.float64, device=dev)
+    std = torch.tensor(std, dtype=torch.float64, device=dev)
+    ch = torch.arange(16, device=dev)
+    valid = ch < 12
+    inv = torch.where(valid, 1.0 / (255.0 * std[ch % 3]), torch.zeros((), dtype=torch.float64, device=dev))
+    ms = torch.where(valid, mean[ch % 3] / std[ch % 3], torch.zeros((), dtype=torch.float64, device=dev))
+    wq = (wp * inv).float()
+    p0 = wq.bfloat16()
+    r = wq - p0.float()  # exact in f32
+    p1 = r.bfloat16()
+    p2 = (r - p1.float()).bfloat16()  # exact: <= 8 significant bits remain
+    planes = torch.stack([p0, p1, p2]).reshape(3, 64, 16, 16).contiguous()
+    g = (wp * ms).sum(-1)  # [64, 4, 4] mean term per tap
+    bias_eff = (bias.detach().double() - g.sum((1, 2))).float().contiguous()
+    bits = torch.arange(16, device=dev)
+    k4 = torch.arange(4, device=dev)
+    out_k = ((bits[:, None] >> k4[None, :]) & 1).bool()  # [mask, k]
+    sel = (out_k[:, None, :, None] | out_k[None, :, None, :]).double()  # [rm, cm, ky, kx]
+    edge = torch.einsum("abyx,cyx->abc", sel, g).float().contiguous()
+    return planes, bias_eff, edge
+
+
+def s2d_u8_normalize(x_u8, mean, std):
+    """The renderer's f32 space-to-depth policy image (policy_dtype 3) from its 8-bit form
+    (policy_dtype 4): ((u / 255) - mean[c]) / std[c] in f32 per channel (dy*2+dx)*3+c, pad 0."""
+    dev = x_u8.device
+    ch = torch.arange(16, device=dev)
+    m = torch.tensor(mean, dtype=torch.float32, device=dev)[ch % 3]
+    sd = torch.tensor(std, dtype=torch.float32, device=dev)[ch % 3]
+    x = (x_u8.float() / 255.0 - m) / sd
+    return torch.where(ch < 12, x, torch.zeros((), device=dev)).contiguous()
+
+
+def stem_s2d_conv_maxpool_u8(x_u8, planes, bias_eff, edge, band_rows=0):
+    """maxpool3x3/2/pad1(relu(conv1(x) + bias)) for x = (u / 255 - mean) / std on the 8-bit
+    space-to-depth image [n, Hs, Ws, 16] u8 (rmbx_render policy_dtype 4) -> channels_last
+    [n, 64, Hp, Wp] f32 (rmbx_stem_s2d_conv_maxpool_u8; operands from pack_stem_u8)."""
+    _chk(x_u8, torch.uint8, name="x_u8")
+    n, Hs, Ws, c16 = x_u8.shape
+    if c16 != 16:
+        raise ValueError("x_u8 must be [n, Hs, Ws, 16]")
+    if Ws > STEM_POOL_MAX_WS:
+        raise ValueError(f"stem_s2d_conv_maxpool_u8: Ws={Ws} exceeds {STEM_POOL_MAX_WS}")
+    _chk(planes, torch.bfloat16, (3, 64, 16, 16), "planes")
+    _chk(bias_eff, torch.float32, (64,), "bias_eff")
+    _chk(edge, torch.float32, (16, 16, 64), "edge")
+    Hp, Wp = (Hs - 1) // 2 + 1, (Ws - 1) // 2 + 1
+    out = torch.empty((n, 64, Hp, Wp), dtype=torch.float32, device=x_u8.device, memory_format=torch.channels_last)
+    N.call("rmbx_stem_s2d_conv_maxpool_u8", N.ptr(x_u8), N.ptr(planes), N.ptr(bias_eff), N.ptr(edge), N.ptr(out),
+           n, Hs, Ws, int(band_rows), N.stream_ptr())
+    return out
+
+
 # ------------------------------------------------------------------------------------------
 # Transformer attention
 # ------------------------------------------------------------------------------------------

@@ -337,14 +337,26 @@ class ActModel(nn.Module):
         [B, ncam, H/2, W/2, 16] (bf16) and runs the stem as an rmbx MFMA kernel."""
         return self._fused is not None
 
+    @property
+    def accepts_u8_s2d(self):
+        """The fp32 device form also takes the renderer's 8-bit space-to-depth images
+        [B, ncam, H/2, W/2, 16] u8 and folds the ImageNet normalisation into its f32 stem kernel
+        (rmbx_stem_s2d_conv_maxpool_u8); RMBX_STEM_U8=0 selects the f32 image instead."""
+        return (self._fused is not None and self._fused.stem.conv.weight.dtype == torch.float32
+                and os.environ.get("RMBX_STEM_U8", "1") != "0")
+
     def forward(self, qpos, image):
         B = qpos.shape[0]
         trunk = self._fused if self._fused is not None else self.backbone
         s2d = image.dim() == 5 and image.shape[-1] == 16
+        if image.dtype == torch.uint8 and not (s2d and self._fused is not None):
+            raise ValueError("ActModel: 8-bit images must be the space-to-depth form of the fused device model")
         feats, poss = [], []
         for c in range(image.shape[1]):
             x = image[:, c]
-            if s2d:
+            if image.dtype == torch.uint8:
+                f = self._input_proj(trunk.forward_s2d_u8(x.contiguous(), IMAGENET_MEAN, IMAGENET_STD))
+            elif s2d:
                 f = self._input_proj(trunk.forward_s2d(x.contiguous()))
             else:
                 if self._fused is not None:

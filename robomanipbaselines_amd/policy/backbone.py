@@ -267,6 +267,20 @@ class FusedResNet18Trunk(nn.Module):
         s = self.stem.conv_nobias(x)
         return self.blocks(K.nhwc_bias_relu_maxpool(s, self.stem.bias_f32()))
 
+    def forward_s2d_u8(self, x_u8, mean, std):
+        """The f32 trunk on the renderer's 8-bit space-to-depth image [n, H/2, W/2, 16] u8
+        (policy_dtype 4): the image normalisation x = (u / 255 - mean) / std is folded into the stem
+        (rmbx_stem_s2d_conv_maxpool_u8: exact bf16 integer pixels x three exact bf16 pieces of
+        W / (255 std), f32 accumulation, the mean term in the bias and the border edge table)."""
+        w = self.stem.conv.weight
+        if w.dtype != torch.float32 or w.shape[0] != 64 or x_u8.shape[2] > K.STEM_POOL_MAX_WS:
+            raise ValueError("forward_s2d_u8: needs the f32 64-channel stem and Ws <= STEM_POOL_MAX_WS")
+        key = (w.data_ptr(), w._version, self.stem.conv.bias.data_ptr(), tuple(mean), tuple(std))
+        if getattr(self, "_u8_key", None) != key:
+            self._u8_ops = K.pack_stem_u8(w, self.stem.conv.bias, mean, std)
+            self._u8_key = key
+        return self.blocks(K.stem_s2d_conv_maxpool_u8(x_u8, *self._u8_ops))
+
     def forward_s2d(self, x_s2d):
         """Same function on the renderer's 2x2 space-to-depth image [B, H/2, W/2, 16] (bf16 or
         f32): conv + bias + ReLU + max-pool in one rmbx MFMA kernel (rmbx_stem_s2d_conv_maxpool

@@ -91,9 +91,11 @@ class Renderer:
             assert depth.dtype == torch.float32 and tuple(depth.shape) == (n, H, W) and depth.is_contiguous()
         pdt = 0
         if policy is not None:
-            assert policy.is_contiguous() and policy.dtype in (torch.float32, torch.bfloat16)
+            assert policy.is_contiguous() and policy.dtype in (torch.float32, torch.bfloat16, torch.uint8)
             if tuple(policy.shape) == (n, H // 2, W // 2, 16):  # space-to-depth stem input
-                pdt = 2 if policy.dtype == torch.bfloat16 else 3
+                pdt = {torch.bfloat16: 2, torch.float32: 3, torch.uint8: 4}[policy.dtype]
+            elif policy.dtype == torch.uint8:
+                raise ValueError("a uint8 policy tensor must be the space-to-depth form [n, H/2, W/2, 16]")
             else:
                 assert tuple(policy.shape) == (n, 3, H, W)
                 pdt = 1 if policy.dtype == torch.bfloat16 else 0

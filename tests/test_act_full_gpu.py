@@ -56,11 +56,16 @@ def _inputs():
     out = []
     for _ in range(CALLS):
         state = torch.randn(N_ENV, 7, generator=g)
-        rgb = torch.rand(N_ENV, 1, 3, 480, 640, generator=g)
+        # 8-bit pixels as the renderer quantises them, normalised as it does (f32 ops)
+        u = (torch.rand(N_ENV, 1, 3, 480, 640, generator=g) * 255.0 + 0.5).floor().to(torch.uint8)
         m = torch.tensor(IMAGENET_MEAN).reshape(1, 1, 3, 1, 1)
         s = torch.tensor(IMAGENET_STD).reshape(1, 1, 3, 1, 1)
-        out.append((state, (rgb - m) / s))
+        out.append((state, (u.float() / 255.0 - m) / s))
+        _U8.append(u)
     return out
+
+
+_U8 = []  # the 8-bit images of _inputs(), in call order
 
 
 STATS = {"norm_config": {"type": "gaussian"}, "mean": np.linspace(-1.0, 1.0, 7), "std": np.full(7, 0.1)}
@@ -98,6 +103,14 @@ def test_act_production_config_fp32_within_1e4_and_bf16_error():
     err32 = np.abs(got - want).max()
     print(f"\nACT 4/7 480x640 fp32 device vs CPU: max |d chunk| {chunk_err:.3e}, max |d action| {err32:.3e}")
     assert err32 <= 1e-4, err32
+    # the rollout's fp32 path: the renderer's 8-bit space-to-depth frame, normalisation folded into
+    # the stem (rmbx_stem_s2d_conv_maxpool_u8)
+    assert dev32.accepts_u8_s2d
+    got_u8 = [dev32(s.to(DEV), K.image_to_s2d(u[:, 0].to(DEV))[:, None]) for (s, _), u in zip(inputs, _U8[-CALLS:])]
+    act_u8 = np.array(_ensemble_actions(got_u8))
+    err_u8 = np.abs(act_u8 - want).max()
+    print(f"ACT fp32 device (u8 stem) vs CPU: max |d action| {err_u8:.3e}")
+    assert err_u8 <= 1e-4, err_u8
 
     del dev32
     torch.cuda.empty_cache()

@@ -364,6 +364,74 @@ def test_stem_conv_maxpool_f32_matches_fp32_reference(n, H, W, band_rows):
     assert err <= 2e-5 * max(1.0, want.abs().max().item()), err
 
 
+@torch.no_grad()
+@pytest.mark.parametrize("n,H,W,band_rows", [(2, 48, 64, 0), (3, 480, 640, 0), (2, 480, 640, 7), (2, 46, 630, 5),
+                                             (1, 34, 90, 1), (2, 6, 8, 0)])
+def test_stem_conv_maxpool_u8_matches_fp32_reference(n, H, W, band_rows):
+    """rmbx_stem_s2d_conv_maxpool_u8 (normalisation folded into the stem, bf16 integer pixels x
+    three exact bf16 weight pieces) vs F.conv2d + bias + ReLU + max_pool2d in fp32 on the
+    normalised image x = (u / 255 - mean) / std the renderer would hand over (the border taps
+    exercise the edge table): within f32 rounding, and no worse than the f32 MFMA kernel against
+    an f64 reference on the CPU."""
+    from robomanipbaselines_amd import kernels as K
+
+    mean, std = (0.485, 0.456, 0.406), (0.229, 0.224, 0.225)
+    g = torch.Generator(device=DEV).manual_seed(17)
+    u = torch.randint(0, 256, (n, 3, H, W), device=DEV, generator=g, dtype=torch.int32).to(torch.uint8)
+    w = torch.randn(64, 3, 7, 7, device=DEV, generator=g) * 0.1
+    b = torch.randn(64, device=DEV, generator=g) * 0.5
+    m3 = torch.tensor(mean, device=DEV).reshape(1, 3, 1, 1)
+    s3 = torch.tensor(std, device=DEV).reshape(1, 3, 1, 1)
+    x = (u.float() / 255.0 - m3) / s3
+    us2d = K.image_to_s2d(u)
+    torch.testing.assert_close(K.s2d_u8_normalize(us2d, mean, std), K.image_to_s2d(x), rtol=0, atol=1e-6)
+    want = F.max_pool2d(F.relu(F.conv2d(x, w, b, 2, 3)), 3, 2, 1)
+    got = K.stem_s2d_conv_maxpool_u8(us2d, *K.pack_stem_u8(w, b, mean, std), band_rows=band_rows)
+    torch.cuda.synchronize()
+    assert got.shape == want.shape and got.dtype == torch.float32
+    assert got.is_contiguous(memory_format=torch.channels_last)
+    scale = max(1.0, want.abs().max().item())
+    err = (got - want).abs().max().item()
+    assert err <= 2e-5 * scale, err
+    if n * H * W <= 2 * 48 * 64:  # f64 CPU reference: the u8 form is as close as the f32 kernel
+        want64 = F.max_pool2d(F.relu(F.conv2d(x.cpu().double(), w.cpu().double(), b.cpu().double(), 2, 3)), 3, 2, 1)
+        f32k = K.stem_s2d_conv_maxpool(K.image_to_s2d(x), K.pack_stem_s2d(w), b, band_rows=band_rows)
+        e_u8 = (got.cpu().double() - want64).abs().max().item()
+        e_f32 = (f32k.cpu().double() - want64).abs().max().item()
+        assert e_u8 <= 3 * e_f32 + 1e-6 * scale, (e_u8, e_f32)
+
+
+def test_stem_conv_maxpool_u8_rejects_bad_operands():
+    from robomanipbaselines_amd import kernels as K
+
+    x = torch.zeros(1, 8, 8, 16, dtype=torch.uint8, device=DEV)
+    ops = K.pack_stem_u8(torch.zeros(64, 3, 7, 7, device=DEV), torch.zeros(64, device=DEV), (0, 0, 0), (1, 1, 1))
+    with pytest.raises(ValueError):
+        K.stem_s2d_conv_maxpool_u8(x.float(), *ops)
+    with pytest.raises(ValueError):
+        K.stem_s2d_conv_maxpool_u8(torch.zeros(1, 8, 400, 16, dtype=torch.uint8, device=DEV), *ops)
+
+
+def test_render_s2d_u8_layout_equals_rgb():
+    """rmbx_render policy_dtype 4 holds the rgb image's 8-bit values in the space-to-depth layout."""
+    from robomanipbaselines_amd import kernels as K
+    from robomanipbaselines_amd.envs.ur5e_cable import BatchedMujocoUR5eCableEnv
+
+    env = BatchedMujocoUR5eCableEnv(2, DEV)
+    env.reset()
+    H, W = env.renderer.height, env.renderer.width
+    rgb = torch.empty((2, H, W, 3), dtype=torch.uint8, device=DEV)
+    s2d = torch.empty((2, H // 2, W // 2, 16), dtype=torch.uint8, device=DEV)
+    f32 = torch.empty((2, H // 2, W // 2, 16), dtype=torch.float32, device=DEV)
+    mean, std = (0.485, 0.456, 0.406), (0.229, 0.224, 0.225)
+    env.render_images("front", rgb=rgb, policy=s2d, mean=mean, std=std)
+    env.render_images("front", policy=f32, mean=mean, std=std)
+    assert torch.equal(K.image_to_s2d(rgb.permute(0, 3, 1, 2)), s2d)
+    # the host restatement of the renderer's normalisation agrees to rounding (torch divides a
+    # tensor by a scalar through the reciprocal, the kernel divides)
+    torch.testing.assert_close(K.s2d_u8_normalize(s2d, mean, std), f32, rtol=0, atol=1e-6)
+
+
 def test_render_s2d_f32_layout_equals_standard():
     from robomanipbaselines_amd import kernels as K
     from robomanipbaselines_amd.envs.ur5e_cable import BatchedMujocoUR5eCableEnv
