@@ -105,19 +105,12 @@ __device__ __forceinline__ void wait_vm() {
 // cost; the result is not written), bit 4 = epilogue through LDS with 16-byte stores (needs
 // ldc % 4 == 0 and 16-B aligned C / res / bias rows), bit 5 = no A split (phase skip: the split's
 // VALU cost; truncated pieces, wrong values)
-template <bool CONV, int VAR = 0>
-__global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
+// one 256 x 128 output tile (linear tile index lin, see gemm_f32x6_kernel for the order)
+template <bool CONV, int VAR>
+__device__ __forceinline__ void gemm_tile(GemmArgs g, int lin, unsigned char* smem) {
   constexpr int GROUP = ((VAR >> 1) & 3) == 1 ? 4 : ((VAR >> 1) & 3) == 2 ? 16 : GM_GROUP;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * GM_STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 3, wn = wave >> 2;
-  const int lr = lane & 31, lh = lane >> 5;
-
-  // block -> tile: XCD-contiguous ranges (blocks bid, bid + 8, ... run on one XCD), then groups of
-  // GM_GROUP row tiles x all column tiles, row tile fastest
-  const int nblk = gridDim.x, bid = blockIdx.x;
-  const int xcd = bid & 7, q = nblk >> 3, r = nblk & 7;
-  int lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   if (g.batch > 1) {  // consecutive tiles of an XCD stay inside one batch item
     const int per_item = g.tiles_m * g.tiles_n;
     const int item = lin / per_item;
@@ -377,6 +370,29 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
   }
 }
 
+// block -> tiles: XCD-contiguous ranges of the linear tile index (blocks bid, bid + 8, ... run on
+// one XCD), inside them groups of GROUP row tiles x all column tiles, row tile fastest.  VAR bit 6
+// (64): persistent blocks -- a grid of one block per CU, block bid walks its XCD's range with
+// stride gridDim / 8 (no block launch per tile; the pipeline refills without a dispatch gap).
+template <bool CONV, int VAR = 0>
+__global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * GM_STAGE];
+  const int nblk = gridDim.x, bid = blockIdx.x;
+  if constexpr ((VAR & 64) != 0) {
+    const int total = g.tiles_m * g.tiles_n * (g.batch > 1 ? g.batch : 1);
+    const int xcd = bid & 7, q = total >> 3, r = total & 7;
+    const int start = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
+    const int cnt = q + (xcd < r ? 1 : 0);
+    for (int j = bid >> 3; j < cnt; j += nblk >> 3) {
+      gemm_tile<CONV, VAR>(g, start + j, smem);
+      __syncthreads();  // the next tile's prologue overwrites the LDS stages / epilogue image
+    }
+  } else {
+    const int xcd = bid & 7, q = nblk >> 3, r = nblk & 7;
+    gemm_tile<CONV, VAR>(g, (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3), smem);
+  }
+}
+
 // planes[p * n + i] = piece p of x[i] (x = x0 + x1 + x2, bf16 bits)
 __global__ void split_bf16x3_kernel(const float* __restrict__ x, uint16_t* __restrict__ planes, long long n) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
@@ -401,7 +417,19 @@ void launch_gemm(long long blocks, const GemmArgs& g, hipStream_t st) {
                       (g.batch <= 1 || g.c_bs % 4 == 0);
   int var = env_var >= 0 ? env_var : 16;
   if (!vec_ok) var &= ~16;
+  if (var & 64) {  // persistent: one block per CU (multiple of 8), when there are more tiles
+    static const int cus = [] {
+      int dev = 0, n = 0;
+      hipGetDevice(&dev);
+      hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
+      return n > 0 ? (n + 7) / 8 * 8 : 256;
+    }();
+    if (blocks > cus) blocks = cus;
+    else var &= ~64;
+  }
   switch (var) {
+    case 64: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 64>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
+    case 80: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 80>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
     case 1: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 1>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
     case 2: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 2>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
     case 4: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 4>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;

@@ -5,7 +5,8 @@ import sys
 
 import torch
 
-from robomanipbaselines_amd import kernels as K
+sys.path.insert(0, ".")
+from robomanipbaselines_amd import kernels as K  # noqa: E402
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 1024
 dev = "cuda"
