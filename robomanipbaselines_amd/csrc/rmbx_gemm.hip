@@ -105,10 +105,19 @@ __device__ __forceinline__ void wait_vm() {
 // cost; the result is not written), bit 4 = epilogue through LDS with 16-byte stores (needs
 // ldc % 4 == 0 and 16-B aligned C / res / bias rows), bit 5 = no A split (phase skip: the split's
 // VALU cost; truncated pieces, wrong values)
-// one 256 x 128 output tile (linear tile index lin, see gemm_f32x6_kernel for the order)
-// (tile origin of linear tile index lin: batch item pointers, first row, first column)
-template <int GROUP>
-__device__ __forceinline__ void tile_origin(GemmArgs& g, int lin, int& m0, int& n0) {
+template <bool CONV, int VAR = 0>
+__global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
+  constexpr int GROUP = ((VAR >> 1) & 3) == 1 ? 4 : ((VAR >> 1) & 3) == 2 ? 16 : GM_GROUP;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * GM_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 3, wn = wave >> 2;
+  const int lr = lane & 31, lh = lane >> 5;
+
+  // block -> tile: XCD-contiguous ranges (blocks bid, bid + 8, ... run on one XCD), then groups of
+  // GM_GROUP row tiles x all column tiles, row tile fastest
+  const int nblk = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q = nblk >> 3, r = nblk & 7;
+  int lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
   if (g.batch > 1) {  // consecutive tiles of an XCD stay inside one batch item
     const int per_item = g.tiles_m * g.tiles_n;
     const int item = lin / per_item;
@@ -121,22 +130,8 @@ __device__ __forceinline__ void tile_origin(GemmArgs& g, int lin, int& m0, int& 
   const int first_m = (lin / per_group) * GROUP;
   const int gsize = min(g.tiles_m - first_m, GROUP);
   const int in_group = lin - (lin / per_group) * per_group;
-  m0 = (first_m + in_group % gsize) * GM_BM;
-  n0 = (in_group / gsize) * GM_BN;
-}
-
-// VAR bit 7 (128, with 64, linear GEMMs): the first A step of the block's next tile (next_lin >= 0)
-// is loaded into Rpre before this tile's epilogue, and this tile starts from Rpre when have_pre
-template <bool CONV, int VAR>
-__device__ __forceinline__ void gemm_tile(GemmArgs g, int lin, unsigned char* smem, float4 (&Rpre)[4], bool have_pre,
-                                          int next_lin) {
-  constexpr int GROUP = ((VAR >> 1) & 3) == 1 ? 4 : ((VAR >> 1) & 3) == 2 ? 16 : GM_GROUP;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave & 3, wn = wave >> 2;
-  constexpr bool PRE = !CONV && (VAR & 192) == 192;
-  const float* const a_in = g.A;
-  int m0, n0;
-  tile_origin<GROUP>(g, lin, m0, n0);
+  const int tm = first_m + in_group % gsize, tn = in_group / gsize;
+  const int m0 = tm * GM_BM, n0 = tn * GM_BN;
 
   // LDS images: every plane row is 32 k = four 16-B slots (8 k each), physical slot =
   // logical ^ ((row >> 2) & 2): conflict-free for the 16x16x32 fragment reads (lane l reads row
@@ -291,13 +286,7 @@ __device__ __forceinline__ void gemm_tile(GemmArgs g, int lin, unsigned char* sm
   const int KT = g.K / GM_BK;
   float4 Ra[4], Rb[4];
   int oka, okb;
-  if (PRE && have_pre) {
-#pragma unroll
-    for (int i = 0; i < 4; ++i) Ra[i] = Rpre[i];
-    oka = 3;
-  } else {
-    oka = load_a(Ra, 0);
-  }
+  oka = load_a(Ra, 0);
   stage_b(0, 0);
   okb = load_a(Rb, min(1, KT - 1));
   store_a(Ra, oka, 0);
@@ -326,28 +315,6 @@ __device__ __forceinline__ void gemm_tile(GemmArgs g, int lin, unsigned char* sm
   for (int kt = 0; kt < KT; kt += 2) {
     step(kt, Rb, okb, Ra, oka);
     if (kt + 1 < KT) step(kt + 1, Ra, oka, Rb, okb);
-  }
-  if constexpr (PRE) {
-    if (next_lin >= 0) {  // the next tile's first A step, in flight under this tile's epilogue
-      int l = next_lin;
-      const float* An = a_in;
-      if (g.batch > 1) {
-        const int per_item = g.tiles_m * g.tiles_n;
-        const int item = l / per_item;
-        l -= item * per_item;
-        An += item * g.a_bs;
-      }
-      const int per_group = GROUP * g.tiles_n;
-      const int first_m = (l / per_group) * GROUP;
-      const int gsize = min(g.tiles_m - first_m, GROUP);
-      const int nm0 = (first_m + (l - (l / per_group) * per_group) % gsize) * GM_BM;
-      const float4* p0 = (const float4*)(An + (long long)min(nm0 + arow, g.M - 1) * g.lda + 8 * aq);
-      const float4* p1 = (const float4*)(An + (long long)min(nm0 + arow + 128, g.M - 1) * g.lda + 8 * aq);
-      Rpre[0] = p0[0];
-      Rpre[1] = p0[1];
-      Rpre[2] = p1[0];
-      Rpre[3] = p1[1];
-    }
   }
 
   if constexpr ((VAR & 16) != 0) {
@@ -410,33 +377,6 @@ __device__ __forceinline__ void gemm_tile(GemmArgs g, int lin, unsigned char* sm
   }
 }
 
-// block -> tiles: XCD-contiguous ranges of the linear tile index (blocks bid, bid + 8, ... run on
-// one XCD), inside them groups of GROUP row tiles x all column tiles, row tile fastest.  VAR bit 6
-// (64): persistent blocks -- a grid of one block per CU, block bid walks its XCD's range with
-// stride gridDim / 8 (no block launch per tile; the pipeline refills without a dispatch gap).
-template <bool CONV, int VAR = 0>
-__global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * GM_STAGE];
-  const int nblk = gridDim.x, bid = blockIdx.x;
-  if constexpr ((VAR & 64) != 0) {
-    const int total = g.tiles_m * g.tiles_n * (g.batch > 1 ? g.batch : 1);
-    const int xcd = bid & 7, q = total >> 3, r = total & 7;
-    const int start = xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q;
-    const int cnt = q + (xcd < r ? 1 : 0);
-    float4 Rpre[4];
-    for (int j = bid >> 3; j < cnt; j += nblk >> 3) {
-      const int jn = j + (nblk >> 3);
-      gemm_tile<CONV, VAR>(g, start + j, smem, Rpre, j != (bid >> 3), jn < cnt ? start + jn : -1);
-      __syncthreads();  // the next tile's prologue overwrites the LDS stages / epilogue image
-    }
-  } else {
-    const int xcd = bid & 7, q = nblk >> 3, r = nblk & 7;
-    float4 Rpre[4];
-    gemm_tile<CONV, VAR>(g, (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3), smem, Rpre, false,
-                         -1);
-  }
-}
-
 // planes[p * n + i] = piece p of x[i] (x = x0 + x1 + x2, bf16 bits)
 __global__ void split_bf16x3_kernel(const float* __restrict__ x, uint16_t* __restrict__ planes, long long n) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
@@ -461,20 +401,7 @@ void launch_gemm(long long blocks, const GemmArgs& g, hipStream_t st) {
                       (g.batch <= 1 || g.c_bs % 4 == 0);
   int var = env_var >= 0 ? env_var : 16;
   if (!vec_ok) var &= ~16;
-  if (var & 64) {  // persistent: one block per CU (multiple of 8), when there are more tiles
-    static const int cus = [] {
-      int dev = 0, n = 0;
-      hipGetDevice(&dev);
-      hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-      return n > 0 ? (n + 7) / 8 * 8 : 256;
-    }();
-    if (blocks > cus) blocks = cus;
-    else var &= ~(64 | 128);
-  }
   switch (var) {
-    case 64: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 64>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
-    case 80: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 80>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
-    case 208: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 208>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
     case 1: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 1>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
     case 2: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 2>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
     case 4: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 4>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
