@@ -702,6 +702,16 @@ __global__ void __launch_bounds__(SP_THREADS) stem_pool_u8_kernel(StemPoolU8Args
 // The same u8 stem in the f32 kernel's SIMD-balanced layout: 4 waves per block (one per SIMD;
 // 10 waves would sit 3/3/2/2 on the SIMDs of an MFMA-bound kernel), wave w = 32-channel tile
 // w & 1 of column tiles 5 (w >> 1) .. + 4 for both stem rows (10 accumulators, 512 registers).
+// the value of lane l - 1 / l + 1 by a DPP wave shift (one VALU move instead of an LDS permute;
+// gfx9 wave_shr:1 / wave_shl:1; the lanes without a neighbour are overridden by the caller)
+__device__ __forceinline__ float dpp_from_left(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float dpp_from_right(float x) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x130, 0xf, 0xf, false));
+}
+
+template <bool DPP>
 __global__ void __launch_bounds__(SF_THREADS) stem_pool_u8w4_kernel(StemPoolU8Args a) {
   __shared__ __attribute__((aligned(16))) unsigned char sq_smem[16 * 3 * 2 * 64 * 16 + SP_RING * 2 * SF_RC * 16 + 64 * 4 +
                                                                SF_WAVES * 2 * 16 * 4];
@@ -861,8 +871,8 @@ __global__ void __launch_bounds__(SF_THREADS) stem_pool_u8w4_kernel(StemPoolU8Ar
 #pragma unroll
           for (int e = 0; e < 4; ++e) {
             const int k = 4 * k4 + e;
-            float left = __shfl_up(acc[i][0][k], 1);
-            const float right = __shfl_down(acc[i][0][k], 1);
+            float left = DPP ? dpp_from_left(acc[i][0][k]) : __shfl_up(acc[i][0][k], 1);
+            const float right = DPP ? dpp_from_right(acc[i][0][k]) : __shfl_down(acc[i][0][k], 1);
             float prev;
             if (i > 0)
               prev = __shfl(acc[i - 1][0][k], (lane & 32) | 31);
@@ -949,6 +959,11 @@ extern "C" int rmbx_stem_s2d_conv_maxpool_u8(const uint8_t* in, const void* w_pl
     const char* e = getenv("RMBX_STEM_U8_LAYOUT");
     return e ? atoi(e) : 4;
   }();
+  // horizontal pool neighbours by DPP wave shifts (RMBX_STEM_U8_DPP=1) or LDS permutes (default)
+  static const bool dpp = [] {
+    const char* e = getenv("RMBX_STEM_U8_DPP");
+    return e && atoi(e) != 0;
+  }();
   if (band_rows <= 0) {
     const int want_blocks = 512;
     int bands = (want_blocks + N - 1) / N;
@@ -961,8 +976,11 @@ extern "C" int rmbx_stem_s2d_conv_maxpool_u8(const uint8_t* in, const void* w_pl
   RMBX_CHECK_ARG(nblocks < (1ll << 31), "rmbx_stem_s2d_conv_maxpool_u8: grid too large");
   if (layout == 10)
     hipLaunchKernelGGL(rmbx::stem_pool_u8_kernel, dim3((unsigned)nblocks), dim3(64 * a.nct), 0, (hipStream_t)stream, a);
+  else if (dpp)
+    hipLaunchKernelGGL(rmbx::stem_pool_u8w4_kernel<true>, dim3((unsigned)nblocks), dim3(rmbx::SF_THREADS), 0,
+                       (hipStream_t)stream, a);
   else
-    hipLaunchKernelGGL(rmbx::stem_pool_u8w4_kernel, dim3((unsigned)nblocks), dim3(rmbx::SF_THREADS), 0,
+    hipLaunchKernelGGL(rmbx::stem_pool_u8w4_kernel<false>, dim3((unsigned)nblocks), dim3(rmbx::SF_THREADS), 0,
                        (hipStream_t)stream, a);
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;

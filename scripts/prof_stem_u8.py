@@ -41,6 +41,6 @@ t32 = timeit(lambda: K.stem_s2d_conv_maxpool(x, wp, b))
 tu8 = timeit(lambda: K.stem_s2d_conv_maxpool_u8(u, *ops))
 fl = 2.0 * n * 240 * 320 * 64 * 147
 import os
-print(f"stem n={n} layout={os.environ.get('RMBX_STEM_U8_LAYOUT', 4)}: f32 kernel {t32:.3f} ms ({fl / t32 / 1e9:.1f} TF/s direct), u8 kernel {tu8:.3f} ms "
+print(f"stem n={n} layout={os.environ.get('RMBX_STEM_U8_LAYOUT', 4)} dpp={os.environ.get('RMBX_STEM_U8_DPP', 0)}: f32 kernel {t32:.3f} ms ({fl / t32 / 1e9:.1f} TF/s direct), u8 kernel {tu8:.3f} ms "
       f"({fl / tu8 / 1e9:.1f} TF/s direct, bf16 MFMA {3 * 2.0 * n * 240 * 320 * 64 * 256 / tu8 / 1e9:.0f} TF/s executed), "
       f"speedup {t32 / tu8:.2f}x, max rel diff {d:.2e}", flush=True)
