@@ -91,8 +91,9 @@ class BatchedRolloutBase:
                             help="environments stepped in lockstep (default: one per --world_idx_list entry, "
                                  "the episodes the reference runs one after another)")
         parser.add_argument("--device", type=str, default="cuda:0")
-        parser.add_argument("--precision", choices=["fp32", "bf16"], default="bf16",
-                            help="policy arithmetic: fp32 (parity mode) or bf16 (throughput mode)")
+        parser.add_argument("--precision", choices=["fp32", "bf16"], default="fp32",
+                            help="policy arithmetic: fp32 (the reference's precision, the default) or bf16 "
+                                 "(opt-in throughput mode, ~1e-3 action error)")
         parser.add_argument("--max_steps", type=int, default=None, help="hard cap on env-steps")
         parser.add_argument("--num_gpus", type=int, default=1,
                             help="shard the envs over this many GPUs of the node (bin/Rollout.py launches one "
@@ -202,9 +203,13 @@ class BatchedRolloutBase:
     image_norm = ((0.0, 0.0, 0.0), (1.0, 1.0, 1.0))
 
     def get_images(self, dtype):
-        """Render every policy camera straight into the normalised policy tensor [n,ncam,3,H,W]
-        (or, for a device policy that accepts it, the bf16 / f32 space-to-depth form
-        [n,ncam,H/2,W/2,16] its fused stem kernel reads)."""
+        """RolloutBase.get_images (:479-490): stack info["rgb_images"][camera] of every policy
+        camera -> CHW -> ToDtype(scale) (and the policy's image normalisation).  Fused: every
+        policy camera of the current state is rendered straight into the normalised policy tensor
+        [n,ncam,3,H,W] (or, for a device policy that accepts it, the bf16 / f32 / 8-bit
+        space-to-depth form [n,ncam,H/2,W/2,16] its fused stem kernel reads) -- the same values as
+        normalising info["rgb_images"] (tests/test_env_info_gpu.py), without the u8 frame round
+        trip through HBM."""
         H, W = self.env.renderer.height, self.env.renderer.width
         mean, std = self.image_norm
         # (the fused f32 stem kernel takes space-to-depth rows of at most STEM_POOL_MAX_WS: wider
@@ -423,13 +428,9 @@ class BatchedRolloutBase:
 
         if v is None:
             v = K.sched_view(self.sched)
-        H, W = self.env.renderer.height, self.env.renderer.width
-        frames = []
-        for cam in self.env.camera_names:
-            rgb = torch.empty((self.n, H, W, 3), dtype=torch.uint8, device=self.device)
-            self.env.render_images(cam, rgb=rgb)
-            frames.append(rgb)
-        image = torch.cat(frames, dim=2).cpu().numpy()
+        # cv2.hconcat(list(self.info["rgb_images"].values())): the envs are frozen at their last
+        # step, whose info this is
+        image = torch.cat([self.info["rgb_images"][cam] for cam in self.env.camera_names], dim=2).cpu().numpy()
         demo_name = self.env.demo_name
         os.makedirs(self.args.output_image_dir, exist_ok=True)
         for e in range(self.n):

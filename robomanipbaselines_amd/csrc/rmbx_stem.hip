@@ -470,11 +470,14 @@ __global__ void __launch_bounds__(SF_THREADS) stem_pool_f32_kernel(StemPoolF32Ar
 // ---------------------------------------------------------------------------------------------
 // f32-accurate form on the quantised image (rmbx_render policy_dtype 4): the pixels the policy
 // sees are x = (u / 255 - mean[c]) / std[c] with u an 8-bit integer (RolloutBase.py:479-490 +
-// the backbone's ImageNet normalisation), so
-//   conv(x)[co] = sum_in W'[co][tap][ch] u[tap][ch]  +  bias  -  sum_in W[co][tap][ch] mean/std
-// with W' = W / (255 std) and "in" = the taps inside the image.  u is exact in bf16 (<= 8
-// significant bits), W' is split exactly into three bf16 pieces (RNE at each level, as
-// rmbx_linear_f32x6), so the three piece products W'_p u are exact in the f32 accumulator:
+// the backbone's ImageNet normalisation), i.e. x = W'(u - 128) + c' with W' = 1 / (255 std) and
+// c' = (128 / 255 - mean) / std, so
+//   conv(x)[co] = sum_in W[co][tap][ch] W'[ch] (u - 128)[tap][ch]  +  bias  +  sum_in W c'
+// with "in" = the taps inside the image.  The pixels are CENTRED: the large mean term of the
+// uncentred form (sum W mean/std, ~2 per tap) no longer cancels against sum W' u, the constant
+// left (c' ~ 0.2) is 10x smaller and |u - 128| <= 128 is exact in bf16; W W' is split exactly
+// into three bf16 pieces (RNE at each level, as rmbx_linear_f32x6), so the three piece products
+// are exact in the f32 accumulator:
 // v_mfma_f32_32x32x16_bf16, 3 MFMAs of 32 cycles per 16-channel tap against 8 of 64 cycles for
 // the f32 kernel's 32x32x2_f32 (per k: 6 cycles vs 32).  The mean term is constant except where
 // taps fall outside the image: bias_eff = bias - (the term of all 16 taps) and edge[rm][cm][co]
@@ -497,19 +500,22 @@ struct StemPoolU8Args {
   int bands, band_rows;
 };
 
-// 16 u8 pixels channels -> two 16-B halves of bf16 integers (exact: <= 8 significant bits)
-__device__ __forceinline__ void u8x16_to_bf16(uint4 v, uint4& lo, uint4& hi) {
+// 16 u8 pixel channels -> two 16-B halves of the CENTRED bf16 integers u - 128 (exact: |u - 128|
+// <= 128 holds <= 8 significant bits); ok = false (outside the image): zeros, the conv's padding
+__device__ __forceinline__ void u8x16_to_bf16(uint4 v, bool ok, uint4& lo, uint4& hi) {
   uint32_t o[8];
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const uint32_t b0 = __float_as_uint((float)(w[i] & 0xffu)), b1 = __float_as_uint((float)((w[i] >> 8) & 0xffu));
-    const uint32_t b2 = __float_as_uint((float)((w[i] >> 16) & 0xffu)), b3 = __float_as_uint((float)(w[i] >> 24));
+    const uint32_t b0 = __float_as_uint((float)((int)(w[i] & 0xffu) - 128));
+    const uint32_t b1 = __float_as_uint((float)((int)((w[i] >> 8) & 0xffu) - 128));
+    const uint32_t b2 = __float_as_uint((float)((int)((w[i] >> 16) & 0xffu) - 128));
+    const uint32_t b3 = __float_as_uint((float)((int)(w[i] >> 24) - 128));
     o[2 * i] = (b0 >> 16) | (b1 & 0xffff0000u);
     o[2 * i + 1] = (b2 >> 16) | (b3 & 0xffff0000u);
   }
-  lo = make_uint4(o[0], o[1], o[2], o[3]);
-  hi = make_uint4(o[4], o[5], o[6], o[7]);
+  lo = ok ? make_uint4(o[0], o[1], o[2], o[3]) : make_uint4(0, 0, 0, 0);
+  hi = ok ? make_uint4(o[4], o[5], o[6], o[7]) : make_uint4(0, 0, 0, 0);
 }
 
 __global__ void __launch_bounds__(SP_THREADS) stem_pool_u8_kernel(StemPoolU8Args a) {
@@ -540,14 +546,14 @@ __global__ void __launch_bounds__(SP_THREADS) stem_pool_u8_kernel(StemPoolU8Args
   if (tid < 64) sBias[tid] = a.bias[tid];
 
   // s2d pixel (ring col c) of row y -> both halves; zero outside the image
+  auto px_ok = [&](int y, int c) { return y >= 0 && y < a.Hs && c - 2 >= 0 && c - 2 < a.Ws; };
   auto load_px = [&](int y, int c) -> uint4 {
-    const int x = c - 2;
-    if (y < 0 || y >= a.Hs || x < 0 || x >= a.Ws) return make_uint4(0, 0, 0, 0);
-    return *reinterpret_cast<const uint4*>(in_img + ((size_t)y * row_px + x) * 16);
+    if (!px_ok(y, c)) return make_uint4(0, 0, 0, 0);
+    return *reinterpret_cast<const uint4*>(in_img + ((size_t)y * row_px + c - 2) * 16);
   };
-  auto store_px = [&](int slot, int c, uint4 v) {
+  auto store_px = [&](int slot, int c, uint4 v, bool ok) {
     uint4 lo, hi;
-    u8x16_to_bf16(v, lo, hi);
+    u8x16_to_bf16(v, ok, lo, hi);
     *reinterpret_cast<uint4*>(sR + ((size_t)(slot * 2) * a.rc + c) * 8) = lo;
     *reinterpret_cast<uint4*>(sR + ((size_t)(slot * 2 + 1) * a.rc + c) * 8) = hi;
   };
@@ -555,7 +561,7 @@ __global__ void __launch_bounds__(SP_THREADS) stem_pool_u8_kernel(StemPoolU8Args
   for (int q = tid; q < SP_RING * a.rc; q += nthreads) {
     const int r = q / a.rc, c = q - r * a.rc;
     const int y = 2 * pys - 2 + r;
-    store_px(slot_of(y), c, load_px(y, c));
+    store_px(slot_of(y), c, load_px(y, c), px_ok(y, c));
   }
 
   const int n = lane & 31, h = lane >> 5;
@@ -670,8 +676,8 @@ __global__ void __launch_bounds__(SP_THREADS) stem_pool_u8_kernel(StemPoolU8Args
 #pragma unroll
       for (int i = 0; i < PF_MAX; ++i) {
         if (tid + nthreads * i < pf_px) {
-          const uint4 v = ((pf_ok >> i) & 1u) ? pf[i] : make_uint4(0, 0, 0, 0);
-          store_px(pf_r[i] ? slot[1] : slot[0], pf_c[i], v);  // row Y0+3+r replaces row Y0-2+r
+          // row Y0+3+r replaces row Y0-2+r
+          store_px(pf_r[i] ? slot[1] : slot[0], pf_c[i], pf[i], (pf_ok >> i) & 1u);
         }
       }
     }
@@ -738,9 +744,9 @@ __global__ void __launch_bounds__(SF_THREADS) stem_pool_u8w4_kernel(StemPoolU8Ar
   }
   if (tid < 64) sBias[tid] = a.bias[tid];
 
-  auto store_px = [&](int slot, int c, uint4 v) {
+  auto store_px = [&](int slot, int c, uint4 v, bool ok) {
     uint4 lo, hi;
-    u8x16_to_bf16(v, lo, hi);
+    u8x16_to_bf16(v, ok, lo, hi);
     *reinterpret_cast<uint4*>(sR + ((size_t)(slot * 2) * SF_RC + c) * 8) = lo;
     *reinterpret_cast<uint4*>(sR + ((size_t)(slot * 2 + 1) * SF_RC + c) * 8) = hi;
   };
@@ -749,8 +755,9 @@ __global__ void __launch_bounds__(SF_THREADS) stem_pool_u8w4_kernel(StemPoolU8Ar
     const int r = q / SF_RC, c = q - r * SF_RC;
     const int y = 2 * pys - 2 + r, x = c - 2;
     uint4 v = make_uint4(0, 0, 0, 0);
-    if (y >= 0 && y < a.Hs && x >= 0 && x < a.Ws) v = *reinterpret_cast<const uint4*>(in_img + ((size_t)y * row_px + x) * 16);
-    store_px(slot_of(y), c, v);
+    const bool ok = y >= 0 && y < a.Hs && x >= 0 && x < a.Ws;
+    if (ok) v = *reinterpret_cast<const uint4*>(in_img + ((size_t)y * row_px + x) * 16);
+    store_px(slot_of(y), c, v, ok);
   }
 
   const int n = lane & 31, h = lane >> 5;
@@ -855,7 +862,7 @@ __global__ void __launch_bounds__(SF_THREADS) stem_pool_u8w4_kernel(StemPoolU8Ar
         const int q = tid + SF_THREADS * i;
         if (q < 2 * SF_RC) {
           const int r = q / SF_RC, c = q - r * SF_RC;
-          store_px(slot_of(Y0 + 3 + r), c, ((pf_ok >> i) & 1u) ? pf[i] : make_uint4(0, 0, 0, 0));
+          store_px(slot_of(Y0 + 3 + r), c, pf[i], (pf_ok >> i) & 1u);
         }
       }
     }

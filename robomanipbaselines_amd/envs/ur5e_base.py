@@ -11,6 +11,8 @@ compiled scene, the initial arm/gripper pose, the body
 that modify_world moves per world index, and the reward kernel.
 """
 
+from collections.abc import Mapping
+
 import numpy as np
 import torch
 
@@ -69,6 +71,9 @@ class BatchedMujocoUR5eEnvBase:
         self.world_idx = np.zeros(self.num_envs, dtype=np.int64)
         # MuJoCo's bad-state resets (mj_checkAcc -> mj_resetData) per env
         self.bad_resets = torch.zeros(self.num_envs, dtype=torch.int32, device=self.device)
+        # the info dict's camera frames (_get_info): rendered on first access within an env-step
+        self._step_id = 0
+        self._frames = {}  # camera -> [step id, rgb u8 [n,H,W,3], depth f32 [n,H,W]]
 
     # -- reference API ----------------------------------------------------------------------
     def _setup_task(self):
@@ -127,7 +132,8 @@ class BatchedMujocoUR5eEnvBase:
             self.bad_resets[m] = 0
         e.forward()
         self.reward = self._get_reward()
-        return self._get_obs(), {}
+        self._step_id += 1
+        return self._get_obs(), self._get_info()  # _get_reset_info = _get_info (MujocoEnvBase.py:157-158)
 
     def step(self, action, active=None):
         """MujocoEnvBase.step (:82-97): ctrl = action; frame_skip x mj_step; obs; reward.
@@ -137,9 +143,41 @@ class BatchedMujocoUR5eEnvBase:
             e.ctrl.copy_(action)
         e.step(self.frame_skip, active=active)
         self._reset_bad_states()
+        self._step_id += 1
         obs = self._get_obs()
         self.reward = self._get_reward()
-        return obs, self.reward, False, False, {}
+        return obs, self.reward, False, False, self._get_info()
+
+    def _get_info(self):
+        """MujocoEnvBase._get_info (:103-155) for every env: info["rgb_images"][camera] u8
+        [n, H, W, 3] and info["depth_images"][camera] f32 [n, H, W] (the linearised camera depth,
+        :122-125) for every camera of the scene, device tensors.  The reference renders all
+        cameras on every step; here a camera is ray-cast (rgb and depth together) the first time
+        either of its images is read within an env-step and cached until the next one, so steps
+        whose images nobody reads cost nothing.  The tensors are the env's buffers: they hold this
+        env-step's frames until the next step renders the camera again (copy to keep them).
+        Tactile scenes add info["intensity_tactile"] (ur5e_pick.py)."""
+        if not self.camera_names:
+            return {}
+        return {"rgb_images": CameraImages(self, "rgb", self._step_id),
+                "depth_images": CameraImages(self, "depth", self._step_id)}
+
+    def _info_frame(self, camera_name, kind, step_id):
+        if step_id != self._step_id:
+            raise RuntimeError("info images of an earlier env-step: they are rendered on first access, copy "
+                               "them before the next step")
+        if camera_name not in self.camera_names:
+            raise KeyError(camera_name)
+        ent = self._frames.get(camera_name)
+        if ent is None:
+            n, H, W = self.num_envs, self.renderer.height, self.renderer.width
+            ent = [-1, torch.empty((n, H, W, 3), dtype=torch.uint8, device=self.device),
+                   torch.empty((n, H, W), dtype=torch.float32, device=self.device)]
+            self._frames[camera_name] = ent
+        if ent[0] != step_id:
+            self.render_images(camera_name, rgb=ent[1], depth=ent[2])
+            ent[0] = step_id
+        return ent[1] if kind == "rgb" else ent[2]
 
     def _reset_bad_states(self):
         """MuJoCo's divergence guard (mj_step -> mj_checkAcc -> mj_resetData, [ext] mujoco 3.1.6):
@@ -193,6 +231,22 @@ class BatchedMujocoUR5eEnvBase:
                              mean=mean, std=std)
         return rgb, depth, policy
 
+
+class CameraImages(Mapping):
+    """info["rgb_images"] / info["depth_images"] of one env-step: camera name -> [n, ...] device
+    tensor, rendered lazily (BatchedMujocoUR5eEnvBase._get_info)."""
+
+    def __init__(self, env, kind, step_id):
+        self._env, self._kind, self._step_id = env, kind, step_id
+
+    def __getitem__(self, camera_name):
+        return self._env._info_frame(camera_name, self._kind, self._step_id)
+
+    def __iter__(self):
+        return iter(self._env.camera_names)
+
+    def __len__(self):
+        return len(self._env.camera_names)
 
 
 def _mat2quat(R):

@@ -52,12 +52,12 @@ class BatchedMujocoUR5ePickEnv(BatchedMujocoUR5eEnvBase):
         self.tactile_enabled = bool(tactile)
         super().__init__(*args, **kw)
 
-    def step(self, action, active=None):
-        obs, reward, term, trunc, info = super().step(action, active=active)
+    def _get_info(self):
+        info = super()._get_info()
         if self.tactile_enabled:
             tac = self.tactile()
-            info = {"intensity_tactile": {name: tac[:, s] for s, name in enumerate(TACTILE_SITES)}}
-        return obs, reward, term, trunc, info
+            info["intensity_tactile"] = {name: tac[:, s] for s, name in enumerate(TACTILE_SITES)}
+        return info
 
     def _setup_task(self):
         a = self.arrays

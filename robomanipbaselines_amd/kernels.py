@@ -706,10 +706,11 @@ def _stem_s2d_conv_maxpool_f32(x_s2d, w_packed, bias, band_rows=0):
 
 def pack_stem_u8(weight, bias, mean, std):
     """Operands of rmbx_stem_s2d_conv_maxpool_u8 for the folded stem conv (weight [64, 3, 7, 7],
-    bias [64]) and the image normalisation x = (u / 255 - mean) / std: the three exact bf16 pieces
-    [3, 64, 16, 16] of W' = W / (255 std) (packed as pack_stem_s2d), bias_eff = bias - sum W mean/std
-    over every tap, and the edge table [16, 16, 64] of the mean/std term of the taps that fall
-    outside the image (row mask of ky x column mask of kx).  The mean terms are summed in f64."""
+    bias [64]) and the image normalisation x = (u / 255 - mean) / std = W'(u - 128) + c' (the kernel
+    reads the centred pixels u - 128): the three exact bf16 pieces [3, 64, 16, 16] of
+    W / (255 std) (packed as pack_stem_s2d), bias_eff = bias + sum W c' over every tap with
+    c' = (128 / 255 - mean) / std, and the edge table [16, 16, 64] removing the c' term of the taps
+    that fall outside the image (row mask of ky x column mask of kx).  Constants summed in f64."""
     dev = weight.device
     wp = pack_stem_s2d(weight.detach().double())  # [64, 4, 4, 16]
     mean = torch.tensor(mean, dtype=torch.float64, device=dev)
@@ -717,7 +718,9 @@ def pack_stem_u8(weight, bias, mean, std):
     ch = torch.arange(16, device=dev)
     valid = ch < 12
     inv = torch.where(valid, 1.0 / (255.0 * std[ch % 3]), torch.zeros((), dtype=torch.float64, device=dev))
-    ms = torch.where(valid, mean[ch % 3] / std[ch % 3], torch.zeros((), dtype=torch.float64, device=dev))
+    # -c' per channel: the constant of the centred pixels, negated (g below is subtracted)
+    ms = torch.where(valid, mean[ch % 3] / std[ch % 3] - 128.0 / (255.0 * std[ch % 3]),
+                     torch.zeros((), dtype=torch.float64, device=dev))
     wq = (wp * inv).float()
     p0 = wq.bfloat16()
     r = wq - p0.float()  # exact in f32

@@ -269,6 +269,10 @@ class ActModel(nn.Module):
         self.action_head = nn.Linear(d, action_dim)
         self.is_pad_head = nn.Linear(d, 1)
         self.prune_dead_decoder = False
+        # (mean, std) the 8-bit image path folds into its stem: the normalisation the float image
+        # paths receive from the renderer (ACTPolicy's ImageNet statistics; the rollout sets its own
+        # image_norm here, RolloutAct.setup_policy)
+        self.u8_image_norm = (IMAGENET_MEAN, IMAGENET_STD)
         self._fused = None
         self._pos_cache = {}
 
@@ -355,7 +359,7 @@ class ActModel(nn.Module):
         for c in range(image.shape[1]):
             x = image[:, c]
             if image.dtype == torch.uint8:
-                f = self._input_proj(trunk.forward_s2d_u8(x.contiguous(), IMAGENET_MEAN, IMAGENET_STD))
+                f = self._input_proj(trunk.forward_s2d_u8(x.contiguous(), *self.u8_image_norm))
             elif s2d:
                 f = self._input_proj(trunk.forward_s2d(x.contiguous()))
             else:

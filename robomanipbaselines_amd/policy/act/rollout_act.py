@@ -40,6 +40,8 @@ class RolloutAct(BatchedRolloutBase):
             # the reference's ACTPolicy checkpoint (or ActModel's own), strictly (RolloutBase.py:376-385)
             load_act_checkpoint(self.policy, self.args.checkpoint)
         self.policy.prune_dead_decoder = bool(self.args.act_prune_dead_decoder)
+        # the 8-bit stem folds in the same (mean, std) the renderer applies to float policy images
+        self.policy.u8_image_norm = tuple(tuple(float(v) for v in x) for x in self.image_norm)
         self.policy_dtype = torch.bfloat16 if self.args.precision == "bf16" else torch.float32
         if self.policy_dtype == torch.float32:
             # the reference's precision: IEEE fp32 convolutions and GEMMs, never a TF32-style

@@ -81,16 +81,15 @@ class RolloutDiffusionPolicy(BatchedRolloutBase):
         return self.state_buf
 
     def get_images(self, dtype):
-        H, W = self.env.renderer.height, self.env.renderer.width
-        if getattr(self, "_rgb", None) is None:
-            self._rgb = torch.empty((self.n, H, W, 3), dtype=torch.uint8, device=self.device)
+        """RolloutDiffusionPolicy.get_images (:111-143): info["rgb_images"][camera] of the last
+        env-step, resized / scaled / cropped on the device."""
         rw, rh = self.image_size
         cw, ch = self.crop_size
         crop = ((rh - ch) // 2, (rw - cw) // 2, ch, cw)
         imgs = []
         for cam in self.camera_names:
-            self.env.render_images(cam, rgb=self._rgb)
-            imgs.append(K.resize_crop_u8(self._rgb, (rw, rh), crop, a=2.0, b=-1.0, dtype=dtype))
+            rgb = self.info["rgb_images"][cam]
+            imgs.append(K.resize_crop_u8(rgb, (rw, rh), crop, a=2.0, b=-1.0, dtype=dtype))
         img = torch.stack(imgs, dim=1)  # [n, ncam, 3, ch, cw]
         if self.images_buf is None:
             self.images_buf = img[:, :, None].repeat(1, 1, self.n_obs_steps, 1, 1, 1)

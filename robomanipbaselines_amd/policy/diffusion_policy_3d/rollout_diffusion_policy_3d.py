@@ -62,15 +62,13 @@ class RolloutDiffusionPolicy3d(RolloutDiffusionPolicy):
         self.pointcloud_buf = None
 
     def get_pointcloud(self):
-        H, W = self.env.renderer.height, self.env.renderer.width
-        if getattr(self, "_rgb", None) is None:
-            self._rgb = torch.empty((self.n, H, W, 3), dtype=torch.uint8, device=self.device)
-            self._depth = torch.empty((self.n, H, W), dtype=torch.float32, device=self.device)
+        """RolloutDiffusionPolicy3d.get_pointcloud (:127-171): info["rgb_images"] and
+        info["depth_images"] of the first camera from the last env-step."""
         cam = self.camera_names[0]
-        self.env.render_images(cam, rgb=self._rgb, depth=self._depth)
+        rgb, depth = self.info["rgb_images"][cam], self.info["depth_images"][cam]
         rw, rh = self.image_size
-        rgb_s = K.resize_crop_u8(self._rgb, (rw, rh), None, dtype=torch.uint8)
-        depth_s = K.resize_f32(self._depth, (rw, rh))
+        rgb_s = K.resize_crop_u8(rgb, (rw, rh), None, dtype=torch.uint8)
+        depth_s = K.resize_f32(depth, (rw, rh))
         d = self.model_meta_info["data"]
         pc, self.pc_count, _ = K.pointcloud_fps(depth_s, rgb_s, self.env.get_camera_fovy(cam), self.num_points,
                                                 self.model_meta_info["pointcloud"], d["min_bound"], d["max_bound"])

@@ -36,6 +36,10 @@ class RolloutMlp(BatchedRolloutBase):
             sd = torch.load(self.args.checkpoint, map_location="cpu", weights_only=True)
             self.policy.load_state_dict(sd)
         self.policy_dtype = torch.bfloat16 if self.args.precision == "bf16" else torch.float32
+        if self.policy_dtype == torch.float32:
+            # the reference's precision: IEEE fp32 convolutions and GEMMs, no TF32-class mode
+            torch.backends.cudnn.allow_tf32 = False
+            torch.backends.cuda.matmul.allow_tf32 = False
         self.policy = self.policy.eval().requires_grad_(False)
         self.policy.fuse_backbone()
         torch.backends.cudnn.benchmark = True

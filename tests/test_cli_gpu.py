@@ -25,6 +25,11 @@ def test_autoeval_command_line(tmp_path, capsys):
                "--max_duration", "1.5"])
     out = capsys.readouterr().out
     assert ro.n == 3  # one env per listed world
+    # AutoEval passes no precision flag: the policy runs at the reference's precision (fp32)
+    import torch
+
+    assert ro.args.precision == "fp32" and ro.policy_dtype == torch.float32
+    assert all(p.dtype == torch.float32 for p in ro.policy.parameters())
     with open(res) as f:
         data = yaml.safe_load(f)
     assert set(data) == {"success", "reward", "duration"}

@@ -121,7 +121,8 @@ def test_rollout_dp3_pointcloud_and_actions():
     def spy(state, pc, **k):
         out = pa(state, pc, **k)
         rec.append((out.float().cpu().numpy().astype(np.float64), pc[:, -1].cpu().numpy(),
-                    ro._rgb.cpu().numpy(), ro._depth.cpu().numpy()))
+                    ro.info["rgb_images"][ro.camera_names[0]].cpu().numpy(),
+                    ro.info["depth_images"][ro.camera_names[0]].cpu().numpy()))
         return out
 
     ro.policy.predict_action = spy

@@ -1,0 +1,148 @@
+"""The env's `info` contract (envs/mujoco/MujocoEnvBase.py:82-97, 103-155): step() and reset()
+return info["rgb_images"][camera] (u8 [n, H, W, 3]) and info["depth_images"][camera] (f32
+[n, H, W], linearised camera depth) for EVERY camera of the scene, plus info["intensity_tactile"]
+on tactile scenes; reference-style plugins read them as RolloutBase.get_images does
+(common/base/RolloutBase.py:479-490).
+
+* every camera's info frames equal an explicit render of the same state;
+* a reference-shaped get_images over self.info (stack -> CHW -> ToDtype(scale) -> the policy's
+  normalisation, on the CPU) equals the fused policy tensor the in-tree plugins render straight
+  into (NCHW f32 for MLP, the 8-bit space-to-depth frame for the fp32 ACT);
+* frames are rendered once per camera and env-step, on first access, and a stale info refuses;
+* DP3's depth and DP's rgb come through info."""
+
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+DEV = "cuda:0"
+
+
+def _rollout(policy_cls, env="cable", argv=()):
+    if env == "cable":
+        from robomanipbaselines_amd.envs.operation.OperationMujocoUR5eCable import OperationMujocoUR5eCable as Op
+    else:
+        from robomanipbaselines_amd.envs.operation.OperationMujocoUR5ePick import OperationMujocoUR5ePick as Op
+
+    class Rollout(Op, policy_cls):
+        pass
+
+    return Rollout(argv=["--device", DEV, *argv])
+
+
+def _to_rollout_phase(ro, extra=0):
+    ro.reset()
+    ro._active = None
+    while ro.phase_idx < len(ro.pre_durations):
+        ro.step_once()
+    for _ in range(extra):
+        ro.step_once()
+
+
+def _reference_get_images(info, cams, mean, std):
+    """RolloutBase.get_images (:479-490) over the batch, CPU f32: [n, ncam, 3, H, W]."""
+    imgs = torch.stack([info["rgb_images"][c].cpu() for c in cams], dim=1)  # [n, ncam, H, W, 3]
+    x = imgs.permute(0, 1, 4, 2, 3).float() / 255.0
+    m = torch.tensor(mean, dtype=torch.float32).reshape(1, 1, 3, 1, 1)
+    s = torch.tensor(std, dtype=torch.float32).reshape(1, 1, 3, 1, 1)
+    return (x - m) / s
+
+
+@torch.no_grad()
+def test_info_frames_for_every_camera_equal_explicit_renders():
+    from robomanipbaselines_amd.policy.mlp.rollout_mlp import RolloutMlp
+
+    ro = _rollout(RolloutMlp, argv=["--num_envs", "3"])
+    _to_rollout_phase(ro, extra=2)
+    env, info = ro.env, ro.info
+    n, H, W = ro.n, env.renderer.height, env.renderer.width
+    assert set(info["rgb_images"]) == set(env.camera_names) == set(info["depth_images"])
+    assert len(env.camera_names) >= 2
+    for cam in env.camera_names:
+        rgb, depth = info["rgb_images"][cam], info["depth_images"][cam]
+        assert rgb.dtype == torch.uint8 and tuple(rgb.shape) == (n, H, W, 3)
+        assert depth.dtype == torch.float32 and tuple(depth.shape) == (n, H, W)
+        want_rgb = torch.empty_like(rgb)
+        want_depth = torch.empty_like(depth)
+        env.render_images(cam, rgb=want_rgb, depth=want_depth)
+        assert torch.equal(rgb, want_rgb), cam
+        assert torch.equal(depth, want_depth), cam
+        assert (depth > 0).all() and rgb.float().std() > 0
+    # the cameras see different views
+    a, b = env.camera_names[:2]
+    assert not torch.equal(info["rgb_images"][a], info["rgb_images"][b])
+
+
+@torch.no_grad()
+def test_info_frames_are_rendered_once_per_step_and_go_stale():
+    from robomanipbaselines_amd.policy.mlp.rollout_mlp import RolloutMlp
+
+    ro = _rollout(RolloutMlp, argv=["--num_envs", "2"])
+    ro.reset()
+    env = ro.env
+    calls = []
+    real = env.render_images
+    env.render_images = lambda cam, **k: calls.append(cam) or real(cam, **k)
+    info0 = ro.info  # reset() returns _get_info() as MujocoEnvBase._get_reset_info does
+    cam = env.camera_names[0]
+    x = info0["rgb_images"][cam]
+    y = info0["depth_images"][cam]  # rendered together with rgb
+    assert info0["rgb_images"][cam] is x and calls == [cam]
+    assert y.shape == x.shape[:3]
+    ro.step_once()
+    assert calls == [cam]  # a step whose images nobody reads renders nothing
+    with pytest.raises(RuntimeError):
+        info0["rgb_images"][cam]
+    with pytest.raises(KeyError):
+        ro.info["rgb_images"]["no_such_camera"]
+    ro.info["depth_images"][cam]
+    assert calls == [cam, cam]
+
+
+@torch.no_grad()
+def test_reference_shaped_get_images_equals_the_fused_policy_tensor_mlp():
+    from robomanipbaselines_amd.policy.mlp.rollout_mlp import RolloutMlp
+
+    ro = _rollout(RolloutMlp, argv=["--num_envs", "3"])
+    _to_rollout_phase(ro, extra=1)
+    fused = ro.get_images(torch.float32).cpu()  # rendered straight into [n, ncam, n_obs, 3, H, W]
+    want = _reference_get_images(ro.info, ro.camera_names, *ro.image_norm)
+    got = fused[:, :, -1]
+    assert got.shape == want.shape
+    # identical formula ((u / 255) - mean) / std in f32 on both sides
+    torch.testing.assert_close(got, want, rtol=0, atol=1e-6)
+
+
+@torch.no_grad()
+def test_reference_shaped_get_images_equals_the_fp32_act_u8_frame():
+    from robomanipbaselines_amd import kernels as K
+    from robomanipbaselines_amd.policy.act.rollout_act import RolloutAct
+
+    ro = _rollout(RolloutAct, argv=["--num_envs", "2", "--act_prune_dead_decoder"])
+    assert ro.policy_dtype == torch.float32  # the default precision
+    _to_rollout_phase(ro, extra=1)
+    frame = ro.get_images(torch.float32)  # the 8-bit space-to-depth frame the fp32 stem reads
+    assert frame.dtype == torch.uint8
+    cam = ro.camera_names[0]
+    rgb = ro.info["rgb_images"][cam]
+    assert torch.equal(frame[:, 0], K.image_to_s2d(rgb.permute(0, 3, 1, 2)))
+    # and its normalised values are the reference get_images' (the stem folds the same formula in)
+    want = _reference_get_images(ro.info, ro.camera_names, *ro.image_norm)[:, 0]
+    got = K.s2d_u8_normalize(frame[:, 0], *ro.image_norm).cpu()
+    torch.testing.assert_close(got, K.image_to_s2d(want), rtol=0, atol=1e-6)
+
+
+@torch.no_grad()
+def test_dp3_depth_and_tactile_come_through_info():
+    from robomanipbaselines_amd.policy.diffusion_policy_3d.rollout_diffusion_policy_3d import RolloutDiffusionPolicy3d
+
+    ro = _rollout(RolloutDiffusionPolicy3d, env="pick", argv=["--num_envs", "2", "--tactile"])
+    ro.reset()
+    assert set(ro.info["intensity_tactile"]) == {"left_tactile_sensor", "right_tactile_sensor"}
+    kinds = []
+    real = ro.env._info_frame
+    ro.env._info_frame = lambda cam, kind, sid: kinds.append((cam, kind)) or real(cam, kind, sid)
+    _to_rollout_phase(ro, extra=1)
+    cam = ro.camera_names[0]
+    assert (cam, "depth") in kinds and (cam, "rgb") in kinds
+    assert "intensity_tactile" in ro.info and "rgb_images" in ro.info

@@ -162,3 +162,42 @@ def test_conv2d_direct_f32_vs_f64(n, C, H, W, Cout, k, stride, pad, bias):
     ref = F.conv2d(x.double(), w.double(), None if b is None else b.double(), stride, pad)
     assert got.shape == ref.shape and got.is_contiguous(memory_format=torch.channels_last)
     assert _err(got.cpu(), ref) <= 1e-5
+
+
+@torch.no_grad()
+@pytest.mark.parametrize("M,N,K", [(5000, 3200, 512), (3000, 512, 3200), (300, 128, 32), (70000, 1536, 512),
+                                   (257, 384, 96)])
+def test_persistent_gemm_equals_per_tile_kernel(monkeypatch, M, N, K):
+    """The persistent form (default: one block per CU walks its tiles with the K pipeline running
+    across tile boundaries) computes every tile with the per-tile kernel's arithmetic: bit-identical
+    outputs, including ragged last row tiles, several tiles per block and K = one step."""
+    from robomanipbaselines_amd import kernels as K_
+
+    g = torch.Generator(device="cpu").manual_seed(M + N)
+    x = torch.randn(M, K, generator=g).to(DEV)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(DEV)
+    b = torch.randn(N, generator=g).to(DEV)
+    planes = K_.split_bf16x3(w)
+    monkeypatch.setenv("RMBX_GEMM_PERSIST", "1")
+    got = K_.linear_f32x6(x, planes, b, relu=True)
+    monkeypatch.setenv("RMBX_GEMM_PERSIST", "0")
+    want = K_.linear_f32x6(x, planes, b, relu=True)
+    torch.cuda.synchronize()
+    assert torch.equal(got, want)
+
+
+@torch.no_grad()
+def test_persistent_conv_gemm_equals_per_tile_kernel(monkeypatch):
+    from robomanipbaselines_amd import kernels as K_
+
+    g = torch.Generator(device="cpu").manual_seed(11)
+    x = torch.randn(9, 64, 37, 45, generator=g).to(DEV).contiguous(memory_format=torch.channels_last)
+    w = (torch.randn(128, 64, 3, 3, generator=g) / 24).to(DEV)
+    b = torch.randn(128, generator=g).to(DEV)
+    planes = K_.pack_conv_f32x6(w)
+    monkeypatch.setenv("RMBX_GEMM_PERSIST", "1")
+    got = K_.conv2d_f32x6(x, planes, b, (3, 3), 2, 1, relu=True)
+    monkeypatch.setenv("RMBX_GEMM_PERSIST", "0")
+    want = K_.conv2d_f32x6(x, planes, b, (3, 3), 2, 1, relu=True)
+    torch.cuda.synchronize()
+    assert torch.equal(got, want)

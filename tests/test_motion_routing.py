@@ -79,10 +79,19 @@ def test_golden_covers_every_trainable_key():
 
 
 def test_rejected_keys_raise_like_the_reference():
-    for skey, akey, err in G["rejected"]:
-        assert err == "ValueError"
-        with pytest.raises(ValueError):
-            state_key_codes([str(skey)])
+    # the golden records, per key pair, which stage the reference refused: get_state (the state
+    # key) and set_command_data (the action key), each run on its own
+    for skey, akey, serr, aerr in G["rejected"]:
+        assert (serr, aerr) in (("ValueError", ""), ("", "ValueError"))
+        if serr:
+            with pytest.raises(ValueError):
+                state_key_codes([str(skey)])
+        else:
+            state_key_codes([str(skey)])  # accepted by the reference: must not raise
+        if aerr:
+            with pytest.raises(ValueError):
+                action_key_codes([str(akey)])
+        else:
             action_key_codes([str(akey)])
     with pytest.raises(ValueError):
         state_key_codes(["no_such_key"])
@@ -195,3 +204,63 @@ def test_product_rollout_with_routed_keys(skeys, akeys):
     assert torch.isfinite(ro.q_cmd).all()
     # the rollout phase moved the arm command away from the last reach-phase IK result
     assert ro.rollout_time_idx > 0
+
+
+# -- hand-derived known answers for the pinocchio / Eigen arithmetic the golden cannot pin ------
+# (motion.npz was minted with these very helpers standing in for pinocchio, so the eef keys'
+# arithmetic is checked here against closed forms instead; parity vs pinocchio stays unpinned)
+
+def _rx(a):
+    c, s = np.cos(a), np.sin(a)
+    return np.array([[1, 0, 0], [0, c, -s], [0, s, c]])
+
+
+def _ry(a):
+    c, s = np.cos(a), np.sin(a)
+    return np.array([[c, 0, s], [0, 1, 0], [-s, 0, c]])
+
+
+def _rz(a):
+    c, s = np.cos(a), np.sin(a)
+    return np.array([[c, -s, 0], [s, c, 0], [0, 0, 1]])
+
+
+@pytest.mark.parametrize("a", [0.3, -1.2, np.pi / 2, 2.9])
+def test_rpy_to_matrix_single_axis_known_answers(a):
+    """pin.rpy.rpyToMatrix(r, p, y) = Rz(y) Ry(p) Rx(r) (MathUtils.get_se3_from_rel_pose :44-46)."""
+    np.testing.assert_allclose(motion.rpy_to_mat(a, 0.0, 0.0), _rx(a), atol=1e-15)
+    np.testing.assert_allclose(motion.rpy_to_mat(0.0, a, 0.0), _ry(a), atol=1e-15)
+    np.testing.assert_allclose(motion.rpy_to_mat(0.0, 0.0, a), _rz(a), atol=1e-15)
+    np.testing.assert_allclose(motion.rpy_to_mat(0.2, a, -0.7), _rz(-0.7) @ _ry(a) @ _rx(0.2), atol=1e-15)
+
+
+def test_quaternion_of_half_turns_takes_the_nonpositive_trace_branch():
+    """Eigen's matrix -> quaternion at trace -1 (half turns): the largest-diagonal branch."""
+    for R, want in ((np.diag([1.0, -1, -1]), [0, 1, 0, 0]), (np.diag([-1.0, 1, -1]), [0, 0, 1, 0]),
+                    (np.diag([-1.0, -1, 1]), [0, 0, 0, 1])):
+        np.testing.assert_array_equal(motion.quat_from_mat(R), want)
+    n = np.array([1.0, 1.0, 0.0]) / np.sqrt(2.0)  # half turn about (1, 1, 0)/sqrt(2): R = 2nn^T - I
+    q = motion.quat_from_mat(2.0 * np.outer(n, n) - np.eye(3))
+    np.testing.assert_allclose(q, [0.0, n[0], n[1], 0.0], atol=1e-15)
+    rng = np.random.default_rng(5)
+    for _ in range(50):  # toRotationMatrix inverts it (sign of q free)
+        R = motion.rpy_to_mat(*rng.uniform(-np.pi, np.pi, 3))
+        np.testing.assert_allclose(motion.mat_from_quat(*motion.quat_from_mat(R)), R, atol=1e-14)
+
+
+def test_relative_eef_command_composes_in_the_body_frame():
+    """set_command_eef_pose_rel (ArmManager.py:155-159): target = target * SE3(rpy, t), i.e.
+    p' = p + R t and R' = R Rr -- here with the IK step's input checked before it runs."""
+    P, q0 = G["placement"], G["q0"]
+    arm = motion.ArmCommand(P, q0)
+    R0, p0 = arm.R.copy(), arm.p.copy()
+    rel = np.array([0.01, -0.02, 0.03, 0.1, 0.0, 0.0])
+    seen = {}
+    real = motion.arm_ik.ik_step
+    motion.arm_ik.ik_step = lambda P_, q, R, p: seen.update(R=R.copy(), p=p.copy()) or q
+    try:
+        motion.set_command(["command_eef_pose_rel"], rel, False, arm, 0.0, 255.0)
+    finally:
+        motion.arm_ik.ik_step = real
+    np.testing.assert_allclose(seen["p"], p0 + R0 @ rel[:3], atol=1e-15)
+    np.testing.assert_allclose(seen["R"], R0 @ _rx(0.1), atol=1e-15)

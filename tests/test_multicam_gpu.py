@@ -68,12 +68,14 @@ def test_act_two_camera_policy_input_and_network():
     ref = ActModel(num_cams=2).eval()
     sd = {k: v.float().cpu() for k, v in ro.policy.state_dict().items() if not k.startswith("_fused.")}
     ref.load_state_dict(sd)
-    if images.dtype == torch.uint8:  # the fp32 rollout's 8-bit frame: the reference takes it normalised
-        from robomanipbaselines_amd import kernels as K
-
-        images = torch.stack([K.s2d_u8_normalize(images[:, i], *ro.image_norm) for i in range(2)], dim=1)
     imgs = images if images.dim() == 5 and images.shape[-1] != 16 else torch.stack(
-        [_s2d_to_nchw(images[:, i]) for i in range(2)], dim=1)
+        [_s2d_to_nchw(images[:, i].cpu()) for i in range(2)], dim=1)
+    if imgs.dtype == torch.uint8:
+        # the fp32 rollout's 8-bit frame: the reference's ToDtype(scale) + ImageNet normalisation,
+        # computed here on the CPU in f32 (independent of the product's kernels)
+        m = torch.tensor(ro.image_norm[0], dtype=torch.float32).reshape(1, 1, 3, 1, 1)
+        s = torch.tensor(ro.image_norm[1], dtype=torch.float32).reshape(1, 1, 3, 1, 1)
+        imgs = (imgs.cpu().float() / 255.0 - m) / s
     want = ref(state.float().cpu(), imgs.float().cpu())
     err = (out.cpu() - want).abs().max().item()
     print(f"\ntwo-camera ACT fp32 device vs CPU: max |d chunk| {err:.3e}")

@@ -392,13 +392,16 @@ def test_stem_conv_maxpool_u8_matches_fp32_reference(n, H, W, band_rows):
     assert got.is_contiguous(memory_format=torch.channels_last)
     scale = max(1.0, want.abs().max().item())
     err = (got - want).abs().max().item()
-    assert err <= 2e-5 * scale, err
+    print(f"\nu8 stem (centred pixels) vs f32 conv: max |d| {err:.3e} = {err / scale:.2e} relative")
+    # the centred form: within 5e-6 of the f32 conv (the uncentred form needed 2e-5)
+    assert err <= 5e-6 * scale, err
     if n * H * W <= 2 * 48 * 64:  # f64 CPU reference: the u8 form is as close as the f32 kernel
         want64 = F.max_pool2d(F.relu(F.conv2d(x.cpu().double(), w.cpu().double(), b.cpu().double(), 2, 3)), 3, 2, 1)
         f32k = K.stem_s2d_conv_maxpool(K.image_to_s2d(x), K.pack_stem_s2d(w), b, band_rows=band_rows)
         e_u8 = (got.cpu().double() - want64).abs().max().item()
         e_f32 = (f32k.cpu().double() - want64).abs().max().item()
-        assert e_u8 <= 3 * e_f32 + 1e-6 * scale, (e_u8, e_f32)
+        print(f"vs f64: u8 stem {e_u8:.3e}, f32 MFMA stem {e_f32:.3e}")
+        assert e_u8 <= 1.5 * e_f32 + 1e-7 * scale, (e_u8, e_f32)
 
 
 def test_stem_conv_maxpool_u8_rejects_bad_operands():

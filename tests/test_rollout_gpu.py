@@ -102,6 +102,8 @@ def test_rollout_act_temporal_ensemble_follows_reference_arithmetic():
 def test_mlp_fused_fp32_matches_reference_module():
     from robomanipbaselines_amd.policy.mlp.mlp_model import MlpModel
 
+    torch.backends.cudnn.allow_tf32 = False  # as RolloutMlp.setup_policy does in fp32
+    torch.backends.cuda.matmul.allow_tf32 = False
     torch.manual_seed(0)
     ref = MlpModel(7, 7, 1, n_obs_steps=2, n_action_steps=3).eval().requires_grad_(False)
     dev = MlpModel(7, 7, 1, n_obs_steps=2, n_action_steps=3).eval().requires_grad_(False)
@@ -115,4 +117,6 @@ def test_mlp_fused_fp32_matches_reference_module():
         want = ref(s, im)
         got = dev(s.to(DEV), im.to(DEV)).cpu()
     assert got.shape == (3, 3, 7)
-    assert (got - want).abs().max().item() <= 1e-3 * max(1.0, want.abs().max().item())
+    err = (got - want).abs().max().item()
+    print(f"\nMLP fused fp32 vs CPU module: max |d| {err:.3e} (scale {want.abs().max().item():.3e})")
+    assert err <= 1e-4 * max(1.0, want.abs().max().item())  # the north star's 1e-4 action bar

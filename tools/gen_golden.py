@@ -1100,14 +1100,18 @@ def gen_motion(importlib):
         op.model_meta_info = {"state": {"norm_config": {"type": "gaussian"}, "mean": np.zeros(7), "std": np.ones(7)}}
         op.device, op.args, op.rollout_time_idx = "cpu", types.SimpleNamespace(skip=3), 0
         op.obs = {"joint_pos": np.zeros(7), "joint_vel": np.zeros(7), "wrench": np.zeros(6)}
-        err = ""
+        # each stage on its own, so the fixture records WHICH key the reference refuses
+        serr = aerr = ""
         try:
             op.get_state()
+        except (ValueError, AttributeError) as ex:
+            serr = type(ex).__name__
+        try:
             op.policy_action = np.zeros(7)
             op.set_command_data()
         except (ValueError, AttributeError) as ex:
-            err = type(ex).__name__
-        rejected.append((skeys[0], akeys[0], err))
+            aerr = type(ex).__name__
+        rejected.append((skeys[0], akeys[0], serr, aerr))
     d["rejected"] = np.array(rejected, dtype="U40")
     d["cases"] = np.array(names, dtype="U32")
     np.savez_compressed(os.path.join(OUT, "motion.npz"), **d)
