@@ -48,7 +48,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (spec)
 MFMA_PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2500.0}  # MI355X_MICROARCH.md: F32 / BF16 MFMA dense
 GOLDEN = os.path.join(ROOT, "tests", "golden")
-CPU_WORKERS_MAX = 16  # the GPU box's CPU share per GPU
+CPU_WORKERS_MAX = 16  # fallback CPU share per GPU when the box does not export OMP_NUM_THREADS
 _T0 = time.time()
 
 
@@ -357,7 +357,13 @@ def cpu_baseline(args, skip=3):
     Rendering is excluded (the reference renders 3 cameras with MuJoCo's OpenGL renderer; there
     is no CPU renderer in this image)."""
     cores = len(os.sched_getaffinity(0))
-    P = max(1, min(cores, CPU_WORKERS_MAX))
+    # the box's CPU share: the GPU pool exports it to every command as OMP_NUM_THREADS / MAX_JOBS (16
+    # on a 1-GPU box, recorded in the line below); without it, CPU_WORKERS_MAX
+    share_env = {k: os.environ.get(k) for k in ("OMP_NUM_THREADS", "MAX_JOBS")}
+    cap = CPU_WORKERS_MAX
+    if (share_env["OMP_NUM_THREADS"] or "").isdigit() and int(share_env["OMP_NUM_THREADS"]) > 0:
+        cap = int(share_env["OMP_NUM_THREADS"])
+    P = max(1, min(cores, cap))
     t0 = time.time()
     progress(f"CPU baseline: {P} workers")
     thr = _spawn_workers("act", P, args.cpu_steps, 1)
@@ -370,6 +376,9 @@ def cpu_baseline(args, skip=3):
     share = max(1, cores // 8)
     return {"value": thr_value, "unit": "env-steps/s", "cores": P, "kind": "port",
             "cpu_model": cpu_model_name(), "host_cpus_visible": cores,
+            "cpu_share": {"workers": P, "env": share_env,
+                          "source": "the box's OMP_NUM_THREADS" if (share_env["OMP_NUM_THREADS"] or "").isdigit()
+                          else "CPU_WORKERS_MAX default"},
             "per_gpu_share": {"cores": share, "value": round(thr_value * share / P, 1),
                               "basis": f"linear extrapolation of the {P}-process measurement to visible/8 cores"},
             "whole_host": {"cores": cores, "value": round(thr_value * cores / P, 1),

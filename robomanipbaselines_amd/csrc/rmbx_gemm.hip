@@ -104,7 +104,8 @@ __device__ __forceinline__ void wait_vm() {
 // tiles per block group 8 (0), 4 (1), 16 (2), bit 3 = no output stores (phase skip: the epilogue's
 // cost; the result is not written), bit 4 = epilogue through LDS with 16-byte stores (needs
 // ldc % 4 == 0 and 16-B aligned C / res / bias rows), bit 5 = no A split (phase skip: the split's
-// VALU cost; truncated pieces, wrong values)
+// VALU cost; truncated pieces, wrong values), bit 6 = stagger: waves 4-7 split + store the next A
+// tile before their first MFMA half-step (see gemm_f32x6_persistent_kernel's STAGGER)
 template <bool CONV, int VAR = 0>
 __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
   constexpr int GROUP = ((VAR >> 1) & 3) == 1 ? 4 : ((VAR >> 1) & 3) == 2 ? 16 : GM_GROUP;
@@ -300,10 +301,12 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
                                          // hipcc's wait before the split stays counted
     bf16x8 b[4][3];
     read_b(b, buf);
+    const bool late = (VAR & 64) == 0 || wave < 4;
+    if (more && !late) store_a(Rcur, okcur, buf ^ 1);
     if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(1);
     half_step(buf, 0, b);
     if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(0);
-    if (more) store_a(Rcur, okcur, buf ^ 1);
+    if (more && late) store_a(Rcur, okcur, buf ^ 1);
     if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(1);
     half_step(buf, 1, b);
     if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(0);
@@ -378,7 +381,9 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// Persistent form (the default): one block per CU walks a sequence of output tiles and the K
+// Persistent form (RMBX_GEMM_PERSIST=1; measured 1-6 % SLOWER than the per-tile kernel on every ACT
+// shape, profiles/r4_gemm_persist_ab.log, so not the default): one block per CU walks a sequence of
+// output tiles and the K
 // pipeline runs on ACROSS tile boundaries -- the W DMA of the next tile's first K step and its A
 // loads are issued under the last MFMAs of the current tile, so a tile's prologue (first A loads,
 // first split, first DMA) is never exposed, and the epilogue's 16-byte stores drain under the next
@@ -416,7 +421,11 @@ __device__ __forceinline__ TileRef decode_tile(const GemmArgs& g, int lin) {
   return t;
 }
 
-template <bool CONV>
+// STAGGER: waves 4-7 (the partners of waves 0-3 on the four SIMDs) split + store the next A tile
+// BEFORE their first MFMA half-step instead of between the two halves, so that on every SIMD one
+// wave's VALU/LDS segment runs beside its partner's MFMAs instead of both waves idling the matrix
+// pipe at the same time (MI355X_MICROARCH.md, two waves per SIMD, item 9)
+template <bool CONV, bool STAGGER>
 __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_persistent_kernel(GemmArgs g) {
   __shared__ __attribute__((aligned(16))) unsigned char smem[2 * GM_STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -656,8 +665,10 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_persistent_kernel(Ge
     oknext = load_a(Rnext, min(s + 2, S - 1));  // unconditional, as gemm_f32x6_kernel
     bf16x8 b[4][3];
     read_b(b, buf);
+    const bool late = !STAGGER || wave < 4;
+    if (more && !late) store_a(Rcur, okcur, buf ^ 1);
     half_step(buf, 0, b);
-    if (more) store_a(Rcur, okcur, buf ^ 1);
+    if (more && late) store_a(Rcur, okcur, buf ^ 1);
     half_step(buf, 1, b);
     if (more) {
       wait_vm<4>();
@@ -707,18 +718,21 @@ int gemm_device_cus() {
 
 template <bool CONV>
 void launch_gemm(long long blocks, const GemmArgs& g, hipStream_t st) {
-  static const int env_var = [] {
-    const char* e = getenv("RMBX_GEMM_VAR");
-    return e ? atoi(e) : -1;
-  }();
-  // persistent blocks (one per CU) unless RMBX_GEMM_PERSIST=0 or a profiling variant is asked for
-  // (read per launch, so a test can compare both forms in one process)
+  // (the environment is read per launch, so a test or a profile can compare the forms in one process)
+  const char* ve = getenv("RMBX_GEMM_VAR");
+  const int env_var = ve ? atoi(ve) : -1;
+  // persistent blocks (one per CU) only with RMBX_GEMM_PERSIST=1: measured 1-6 % slower than one
+  // block per tile on every ACT shape (profiles/r4_gemm_persist_ab.log)
   const char* pe = getenv("RMBX_GEMM_PERSIST");
-  const bool persist = pe ? atoi(pe) != 0 : true;
+  const bool persist = pe ? atoi(pe) != 0 : false;
   if (persist && env_var < 0) {
     const int cus = gemm_device_cus();
     const long long grid = blocks < cus ? blocks : cus;
-    hipLaunchKernelGGL((gemm_f32x6_persistent_kernel<CONV>), dim3((unsigned)grid), dim3(GM_THREADS), 0, st, g);
+    const char* se = getenv("RMBX_GEMM_STAGGER");
+    if (se && atoi(se) != 0)
+      hipLaunchKernelGGL((gemm_f32x6_persistent_kernel<CONV, true>), dim3((unsigned)grid), dim3(GM_THREADS), 0, st, g);
+    else
+      hipLaunchKernelGGL((gemm_f32x6_persistent_kernel<CONV, false>), dim3((unsigned)grid), dim3(GM_THREADS), 0, st, g);
     return;
   }
   const bool vec_ok = g.ldc % 4 == 0 && ((uintptr_t)g.C | (uintptr_t)g.res | (uintptr_t)g.bias) % 16 == 0 &&
@@ -733,6 +747,7 @@ void launch_gemm(long long blocks, const GemmArgs& g, hipStream_t st) {
     case 16: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 16>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
     case 18: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 18>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
     case 48: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 48>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
+    case 80: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 80>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
     default: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 0>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g);
   }
 }

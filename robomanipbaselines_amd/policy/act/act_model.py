@@ -79,6 +79,36 @@ def _x6_linear(owner, name, x, w, b, relu=False):
     return K.linear_f32x6(x, _x6_planes(owner, name, w), b, relu=relu)
 
 
+def _x6_linear_padded(owner, name, x, w, b):
+    """F.linear(x, w, b) on rmbx_linear_f32x6 for shapes it does not take directly (N not a multiple
+    of 128, K not a multiple of 32: the proprio projection 7 -> 512, the action head 512 -> 7): W and
+    b zero-padded once (cached per weight storage and version), x zero-padded along K when needed,
+    the first N columns returned.  fp32-accurate like the other device GEMMs, and every row's
+    result is independent of the batch size (hipBLASLt chooses its algorithm by the row count, so
+    its last bits vary with the number of envs)."""
+    from ... import kernels as K
+
+    N, Kd = w.shape
+    Np, Kp = -(-N // 128) * 128, -(-Kd // 32) * 32
+    key = (w.data_ptr(), w._version, b.data_ptr(), Np, Kp)
+    cache = owner.__dict__.setdefault("_x6p", {})
+    ent = cache.get(name)
+    if ent is None or ent[0] != key:
+        wp = torch.zeros(Np, Kp, device=w.device, dtype=torch.float32)
+        wp[:N, :Kd] = w.detach()
+        bp = torch.zeros(Np, device=w.device, dtype=torch.float32)
+        bp[:N] = b.detach()
+        ent = (key, K.split_bf16x3(wp), bp)
+        cache[name] = ent
+    shp = x.shape
+    x2 = x.reshape(-1, Kd)
+    if Kp != Kd:
+        xp = torch.zeros(x2.shape[0], Kp, device=x.device, dtype=torch.float32)
+        xp[:, :Kd] = x2
+        x2 = xp
+    return K.linear_f32x6(x2, ent[1], ent[2])[:, :N].reshape(*shp[:-1], N)
+
+
 class MHA(nn.Module):
     """nn.MultiheadAttention-compatible parameters (in_proj_weight/bias, out_proj), batch-first
     compute through scaled_dot_product_attention."""
@@ -370,8 +400,15 @@ class ActModel(nn.Module):
             poss.append(self._pos(f.shape[2], f.shape[3], f.device, f.dtype))
         src = torch.cat(feats, dim=3).flatten(2).transpose(1, 2)  # [B, hw, d]
         pos = torch.cat(poss, dim=3).flatten(2).transpose(1, 2)  # [1, hw, d]
+        # fp32 device form: the two small linears and the final norm on rmbx kernels too, so every
+        # env's chunk is bit-identical whatever the batch (tests/test_act_batch_gpu.py)
+        dev_f32 = self._fused is not None and src.is_cuda and src.dtype == torch.float32 and F32_GEMM == "x6"
         latent = self.latent_out_proj(torch.zeros(B, self.latent_dim, device=qpos.device, dtype=src.dtype))
-        proprio = self.input_proj_robot_state(qpos.to(src.dtype))
+        if dev_f32:
+            p = self.input_proj_robot_state
+            proprio = _x6_linear_padded(self, "proprio", qpos.to(src.dtype).contiguous(), p.weight, p.bias)
+        else:
+            proprio = self.input_proj_robot_state(qpos.to(src.dtype))
         src = torch.cat([latent[:, None], proprio[:, None], src], dim=1)
         pos = torch.cat([self.additional_pos_embed.weight[None].to(src.dtype), pos], dim=1)
         mem = src
@@ -392,7 +429,17 @@ class ActModel(nn.Module):
             tgt, q = self.decoder_layers[i].forward_q(tgt, q, mem, qe, mem_pos, want_next_q=i + 1 < n_dec,
                                                       cross_kv=cross[i] if cross else None)
             if i == 0:
-                first = self.decoder_norm(tgt)  # intermediate[0] = norm(output of layer 0)
+                # intermediate[0] = norm(output of layer 0)
+                if dev_f32:
+                    from ... import kernels as K
+
+                    w, b = _LayerOps._norm_f32(self.decoder_norm)
+                    first = K.add_layernorm(tgt.contiguous(), None, w, b, self.decoder_norm.eps)
+                else:
+                    first = self.decoder_norm(tgt)
+        if dev_f32:
+            h = self.action_head
+            return _x6_linear_padded(self, "action_head", first.contiguous(), h.weight, h.bias)
         return self.action_head(first)
 
 

@@ -1,5 +1,6 @@
-"""A/B of the bf16x6 GEMM's persistent form (RMBX_GEMM_PERSIST=1, the default) against the per-tile
-kernel (=0) on the fp32 ACT shapes at 1024 envs, interleaved rounds in one process (HIP events).
+"""A/B of the bf16x6 GEMM forms on the fp32 ACT shapes at 1024 envs, interleaved rounds in one process
+(HIP events): the per-tile kernel (default), with the wave-4-7 stagger (RMBX_GEMM_VAR=80), the
+persistent form (RMBX_GEMM_PERSIST=1) and persistent + stagger (RMBX_GEMM_STAGGER=1).
 Prints ms per call and the executed bf16 MFMA rate as a fraction of the 2.5 PF dense peak."""
 
 import os
@@ -33,24 +34,37 @@ def main():
         b = torch.rand(Nd, device="cuda")
         p = K.split_bf16x3(w)
         out = torch.empty(Mm, Nd, device="cuda")
-        res = {"1": [], "0": []}
-        for mode in ("1", "0"):  # warm-up
-            os.environ["RMBX_GEMM_PERSIST"] = mode
+        # (RMBX_GEMM_PERSIST, RMBX_GEMM_STAGGER, RMBX_GEMM_VAR)
+        modes = {"t": ("0", "0", None), "ts": ("0", "0", "80"), "p": ("1", "0", None), "ps": ("1", "1", None)}
+
+        def setmode(m):
+            pe, st, var = modes[m]
+            os.environ["RMBX_GEMM_PERSIST"], os.environ["RMBX_GEMM_STAGGER"] = pe, st
+            if var is None:
+                os.environ.pop("RMBX_GEMM_VAR", None)
+            else:
+                os.environ["RMBX_GEMM_VAR"] = var
+
+        res = {m: [] for m in modes}
+        for mode in modes:  # warm-up
+            setmode(mode)
             K.linear_f32x6(x, p, b, out=out)
         torch.cuda.synchronize()
         for _ in range(5):
-            for mode in ("1", "0"):
-                os.environ["RMBX_GEMM_PERSIST"] = mode
+            for mode in modes:
+                setmode(mode)
                 res[mode].append(timeit(lambda: K.linear_f32x6(x, p, b, out=out)))
         fl = 2.0 * Mm * Kd * Nd
         line = f"{name:9s} M={Mm} K={Kd:5d} N={Nd:5d}:"
-        for mode, label in (("1", "persistent"), ("0", "per-tile")):
+        for mode, label in (("t", "per-tile"), ("ts", "per-tile+stagger"), ("p", "persistent"),
+                            ("ps", "persistent+stagger")):
             t = statistics.median(res[mode])
             line += f"  {label} {t:7.3f} ms ({6 * fl / t / 1e9 / 2500:5.3f} of bf16 peak, min {min(res[mode]):.3f})"
         print(line, flush=True)
         del x, w, out
         torch.cuda.empty_cache()
-    os.environ["RMBX_GEMM_PERSIST"] = "1"
+    os.environ["RMBX_GEMM_PERSIST"], os.environ["RMBX_GEMM_STAGGER"] = "0", "0"
+    os.environ.pop("RMBX_GEMM_VAR", None)
 
 
 if __name__ == "__main__":
