@@ -692,6 +692,254 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_persistent_kernel(Ge
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Wide tile (RMBX_GEMM_WIDE=1): the block owns 128 rows x 256 columns instead of 256 x 128, same
+// 8 waves of 64 x 64 (2 row x 4 column waves), same K step of 32 and two 72-KiB LDS stages (A:
+// 3 planes x 128 x 32, W: 3 planes x 256 x 32).  Per K step a thread splits 8 A values instead of
+// 16 (half the split VALU per MFMA), each A row is re-read by half as many column tiles (A is the
+// operand that streams from beyond L2: FFN1 re-reads its 0.63 GB A once per column tile), W --
+// pre-split, LDS-DMA, L2-resident -- twice as often.  N % 256 == 128 leaves the last column tile
+// half full: its waves 4-7 (columns 128-255) skip their MFMAs.  Bit-identical to the 256 x 128
+// kernel (same products, same K order per output).
+// ---------------------------------------------------------------------------------------------
+constexpr int GW_BM = 128, GW_BN = 256;
+constexpr int GW_A_PLANE = GW_BM * GM_BK * 2;           // 8 KiB
+constexpr int GW_B_PLANE = GW_BN * GM_BK * 2;           // 16 KiB
+constexpr int GW_A_BYTES = 3 * GW_A_PLANE;              // 24 KiB
+constexpr int GW_STAGE = GW_A_BYTES + 3 * GW_B_PLANE;   // 72 KiB
+static_assert(2 * GW_STAGE <= 160 * 1024, "wide GEMM stages");
+
+template <bool CONV, bool STAGGER>
+__global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_wide_kernel(GemmArgs g) {
+  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * GW_STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 1, wn = wave >> 1;  // waves 4-7 own columns 128-255
+
+  // block -> tile, as gemm_f32x6_kernel (XCD-contiguous ranges, groups of GM_GROUP row tiles x all
+  // column tiles, row tile fastest)
+  const int nblk = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q = nblk >> 3, r = nblk & 7;
+  int lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  if (g.batch > 1) {
+    const int per_item = g.tiles_m * g.tiles_n;
+    const int item = lin / per_item;
+    lin -= item * per_item;
+    g.A += item * g.a_bs;
+    g.W += item * g.w_bs;
+    g.C += item * g.c_bs;
+  }
+  const int per_group = GM_GROUP * g.tiles_n;
+  const int first_m = (lin / per_group) * GM_GROUP;
+  const int gsize = min(g.tiles_m - first_m, GM_GROUP);
+  const int in_group = lin - (lin / per_group) * per_group;
+  const int tm = first_m + in_group % gsize, tn = in_group / gsize;
+  const int m0 = tm * GW_BM, n0 = tn * GW_BN;
+  const bool wave_cols = n0 + wn * 64 < g.N;  // this wave's 64 columns exist (half tile at the end)
+
+  // A staging: thread -> row tid / 4, k quarter tid % 4 (8 f32); rows past M re-read row M - 1
+  const int aq = tid & 3, arow = tid >> 2;
+  const float* ag = g.A + (long long)min(m0 + arow, g.M - 1) * g.lda + 8 * aq;
+  const int aoff = arow * 64 + ((aq ^ ((arow >> 2) & 2)) << 4);
+  // W: 48 LDS-DMA pieces (16 per plane) of 16 rows x 64 B, wave w copies pieces 6w .. 6w + 5; rows
+  // past N (the half tile) re-read row N - 1
+  const uint16_t* bsrc[6];
+#pragma unroll
+  for (int t = 0; t < 6; ++t) {
+    const int i = wave * 6 + t, p = i >> 4;
+    const int row = (i & 15) * 16 + (lane >> 2);
+    const int sl = (lane & 3) ^ ((row >> 2) & 2);
+    bsrc[t] = g.W + p * g.wps + (long long)min(n0 + row, g.N - 1) * g.ldw + sl * 8;
+  }
+  auto stage_b = [&](int kt, int buf) {
+    unsigned char* base = smem + buf * GW_STAGE + GW_A_BYTES;
+#pragma unroll
+    for (int t = 0; t < 6; ++t) glds16(bsrc[t] + kt * GM_BK, base + (wave * 6 + t) * 1024);
+  };
+  long long cbase = 0;
+  int cy = 0, cx = 0;
+  if constexpr (CONV) {
+    const int m = min(m0 + arow, g.M - 1);
+    const int hw = g.oh * g.ow;
+    const int img = m / hw, rem = m - img * hw;
+    const int oy = rem / g.ow, ox = rem - oy * g.ow;
+    cy = oy * g.stride - g.pad;
+    cx = ox * g.stride - g.pad;
+    cbase = ((long long)(img * g.ih + cy) * g.iw + cx) * g.ic + 8 * aq;
+  }
+  auto load_a = [&](float4 (&R)[2], int kt) -> int {
+    if constexpr (!CONV) {
+      const float4* p0 = (const float4*)(ag + kt * GM_BK);
+      R[0] = p0[0];
+      R[1] = p0[1];
+      return 1;
+    } else {
+      const int k0 = kt * GM_BK;
+      const int tap = k0 / g.ic, c0 = k0 - tap * g.ic;
+      const int ky = tap / g.kw, kx = tap - ky * g.kw;
+      const bool v = (unsigned)(cy + ky) < (unsigned)g.ih && (unsigned)(cx + kx) < (unsigned)g.iw;
+      const float4* p = (const float4*)(g.A + (v ? cbase + (long long)(ky * g.iw + kx) * g.ic + c0 : 0));
+      R[0] = p[0];
+      R[1] = p[1];
+      return (int)v;
+    }
+  };
+  auto store_a = [&](const float4 (&Rin)[2], int ok, int buf) {
+    float4 R[2] = {Rin[0], Rin[1]};
+    if constexpr (CONV) {
+      if (!ok) R[0] = R[1] = make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+    uint32_t p0[4], p1[4], p2[4];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      split_pair(R[i].x, R[i].y, p0[2 * i], p1[2 * i], p2[2 * i]);
+      split_pair(R[i].z, R[i].w, p0[2 * i + 1], p1[2 * i + 1], p2[2 * i + 1]);
+    }
+    unsigned char* base = smem + buf * GW_STAGE;
+    *(uint4*)(base + aoff) = make_uint4(p0[0], p0[1], p0[2], p0[3]);
+    *(uint4*)(base + GW_A_PLANE + aoff) = make_uint4(p1[0], p1[1], p1[2], p1[3]);
+    *(uint4*)(base + 2 * GW_A_PLANE + aoff) = make_uint4(p2[0], p2[1], p2[2], p2[3]);
+  };
+
+  f32x4v acc[4][4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4v){0.f, 0.f, 0.f, 0.f};
+
+  const int fr = lane & 15, fs = lane >> 4;
+  auto frag_off = [&](int row) { return row * 64 + ((fs ^ ((row >> 2) & 2)) << 4); };
+  auto half_step = [&](int buf, int h, const bf16x8 (&b)[4][3]) {
+    const unsigned char* As = smem + buf * GW_STAGE;
+    bf16x8 a[2][3];
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int off = frag_off(wm * 64 + (2 * h + i) * 16 + fr);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) a[i][p] = *(const bf16x8*)(As + p * GW_A_PLANE + off);
+    }
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int nj = 0; nj < 4; ++nj) {
+        f32x4v c = acc[2 * h + i][nj];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][2], b[nj][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[nj][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[nj][2], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[nj][0], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[nj][1], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[nj][0], c, 0, 0, 0);
+        acc[2 * h + i][nj] = c;
+      }
+  };
+  auto read_b = [&](bf16x8 (&b)[4][3], int buf) {
+    const unsigned char* Bs = smem + buf * GW_STAGE + GW_A_BYTES;
+#pragma unroll
+    for (int nj = 0; nj < 4; ++nj) {
+      const int off = frag_off(wn * 64 + nj * 16 + fr);
+#pragma unroll
+      for (int p = 0; p < 3; ++p) b[nj][p] = *(const bf16x8*)(Bs + p * GW_B_PLANE + off);
+    }
+  };
+
+  // K steps as gemm_f32x6_kernel: W of kt + 1 by LDS-DMA (6 pieces per wave), A of kt + 2 into
+  // registers, A of kt + 1 split and stored between the two MFMA halves (before them for waves 4-7
+  // with STAGGER); vmcnt(2): the 2 A loads of kt + 2 may stay in flight
+  const int KT = g.K / GM_BK;
+  float4 Ra[2], Rb[2];
+  int oka, okb;
+  oka = load_a(Ra, 0);
+  stage_b(0, 0);
+  okb = load_a(Rb, min(1, KT - 1));
+  store_a(Ra, oka, 0);
+  wait_vm<2>();
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  auto step = [&](int kt, float4 (&Rcur)[2], int& okcur, float4 (&Rnext)[2], int& oknext) {
+    const int buf = kt & 1;
+    const bool more = kt + 1 < KT;
+    if (more) stage_b(kt + 1, buf ^ 1);
+    oknext = load_a(Rnext, min(kt + 2, KT - 1));
+    const bool late = !STAGGER || wave < 4;
+    if (more && !late) store_a(Rcur, okcur, buf ^ 1);
+    if (wave_cols) {
+      bf16x8 b[4][3];
+      read_b(b, buf);
+      half_step(buf, 0, b);
+      if (more && late) store_a(Rcur, okcur, buf ^ 1);
+      half_step(buf, 1, b);
+    } else if (more && late) {
+      store_a(Rcur, okcur, buf ^ 1);
+    }
+    if (more) {
+      wait_vm<2>();
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    }
+  };
+  for (int kt = 0; kt < KT; kt += 2) {
+    step(kt, Rb, okb, Ra, oka);
+    if (kt + 1 < KT) step(kt + 1, Ra, oka, Rb, okb);
+  }
+
+  // epilogue through LDS (as gemm_f32x6_kernel VAR 16): the wave's 64 x 64 tile row-major in its
+  // own 17 KiB of the idle stage buffers, then float4 rows, 16-byte stores
+  const bool vec_ok = g.ldc % 4 == 0 && ((uintptr_t)g.C | (uintptr_t)g.res | (uintptr_t)g.bias) % 16 == 0 &&
+                      (g.batch <= 1 || g.c_bs % 4 == 0);
+  if (!vec_ok) {
+    if (!wave_cols) return;
+#pragma unroll
+    for (int nj = 0; nj < 4; ++nj) {
+      const int n = n0 + wn * 64 + nj * 16 + fr;
+      const float bn = g.bias ? g.bias[n] : 0.f;
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        const int mb = m0 + wm * 64 + mi * 16 + 4 * fs;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int m = mb + e;
+          if (m < g.M) {
+            float v = acc[mi][nj][e] + bn;
+            if (g.res) v += g.res[(long long)m * g.ldc + n];
+            if (g.relu) v = fmaxf(v, 0.f);
+            g.C[(long long)m * g.ldc + n] = v;
+          }
+        }
+      }
+    }
+    return;
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  if (!wave_cols) return;
+  constexpr int PITCH = 68;
+  float* T = reinterpret_cast<float*>(smem) + wave * (64 * PITCH);
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int nj = 0; nj < 4; ++nj)
+#pragma unroll
+      for (int e = 0; e < 4; ++e) T[(mi * 16 + 4 * fs + e) * PITCH + nj * 16 + fr] = acc[mi][nj][e];
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  const int c4 = (lane & 15) * 4;
+  const int n = n0 + wn * 64 + c4;
+  float4 bn = make_float4(0.f, 0.f, 0.f, 0.f);
+  if (g.bias) bn = *(const float4*)(g.bias + n);
+#pragma unroll
+  for (int it = 0; it < 16; ++it) {
+    const int rr = it * 4 + (lane >> 4);
+    const int m = m0 + wm * 64 + rr;
+    if (m < g.M) {
+      float4 v = *(const float4*)(T + rr * PITCH + c4);
+      v.x += bn.x; v.y += bn.y; v.z += bn.z; v.w += bn.w;
+      if (g.res) {
+        const float4 rv = *(const float4*)(g.res + (long long)m * g.ldc + n);
+        v.x += rv.x; v.y += rv.y; v.z += rv.z; v.w += rv.w;
+      }
+      if (g.relu) {
+        v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+      }
+      *(float4*)(g.C + (long long)m * g.ldc + n) = v;
+    }
+  }
+}
+
 // planes[p * n + i] = piece p of x[i] (x = x0 + x1 + x2, bf16 bits)
 __global__ void split_bf16x3_kernel(const float* __restrict__ x, uint16_t* __restrict__ planes, long long n) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
@@ -721,6 +969,20 @@ void launch_gemm(long long blocks, const GemmArgs& g, hipStream_t st) {
   // (the environment is read per launch, so a test or a profile can compare the forms in one process)
   const char* ve = getenv("RMBX_GEMM_VAR");
   const int env_var = ve ? atoi(ve) : -1;
+  // the 128 x 256 tile (RMBX_GEMM_WIDE=1; RMBX_GEMM_STAGGER=1 adds the wave-4-7 stagger)
+  const char* we = getenv("RMBX_GEMM_WIDE");
+  if (we && atoi(we) != 0 && env_var < 0) {
+    GemmArgs w = g;
+    w.tiles_m = (g.M + GW_BM - 1) / GW_BM;
+    w.tiles_n = (g.N + GW_BN - 1) / GW_BN;
+    const long long wblocks = (long long)w.tiles_m * w.tiles_n * (g.batch > 1 ? g.batch : 1);
+    const char* se = getenv("RMBX_GEMM_STAGGER");
+    if (se && atoi(se) != 0)
+      hipLaunchKernelGGL((gemm_f32x6_wide_kernel<CONV, true>), dim3((unsigned)wblocks), dim3(GM_THREADS), 0, st, w);
+    else
+      hipLaunchKernelGGL((gemm_f32x6_wide_kernel<CONV, false>), dim3((unsigned)wblocks), dim3(GM_THREADS), 0, st, w);
+    return;
+  }
   // persistent blocks (one per CU) only with RMBX_GEMM_PERSIST=1: measured 1-6 % slower than one
   // block per tile on every ACT shape (profiles/r4_gemm_persist_ab.log)
   const char* pe = getenv("RMBX_GEMM_PERSIST");

@@ -34,12 +34,14 @@ def main():
         b = torch.rand(Nd, device="cuda")
         p = K.split_bf16x3(w)
         out = torch.empty(Mm, Nd, device="cuda")
-        # (RMBX_GEMM_PERSIST, RMBX_GEMM_STAGGER, RMBX_GEMM_VAR)
-        modes = {"t": ("0", "0", None), "ts": ("0", "0", "80"), "p": ("1", "0", None), "ps": ("1", "1", None)}
+        # (RMBX_GEMM_PERSIST, RMBX_GEMM_STAGGER, RMBX_GEMM_VAR, RMBX_GEMM_WIDE)
+        modes = {"t": ("0", "0", None, "0"), "ts": ("0", "0", "80", "0"), "p": ("1", "0", None, "0"),
+                 "ps": ("1", "1", None, "0"), "w": ("0", "0", None, "1"), "ws": ("0", "1", None, "1")}
 
         def setmode(m):
-            pe, st, var = modes[m]
+            pe, st, var, wide = modes[m]
             os.environ["RMBX_GEMM_PERSIST"], os.environ["RMBX_GEMM_STAGGER"] = pe, st
+            os.environ["RMBX_GEMM_WIDE"] = wide
             if var is None:
                 os.environ.pop("RMBX_GEMM_VAR", None)
             else:
@@ -57,13 +59,13 @@ def main():
         fl = 2.0 * Mm * Kd * Nd
         line = f"{name:9s} M={Mm} K={Kd:5d} N={Nd:5d}:"
         for mode, label in (("t", "per-tile"), ("ts", "per-tile+stagger"), ("p", "persistent"),
-                            ("ps", "persistent+stagger")):
+                            ("ps", "persistent+stagger"), ("w", "wide 128x256"), ("ws", "wide+stagger")):
             t = statistics.median(res[mode])
-            line += f"  {label} {t:7.3f} ms ({6 * fl / t / 1e9 / 2500:5.3f} of bf16 peak, min {min(res[mode]):.3f})"
+            line += f"\n    {label:20s} {t:7.3f} ms ({6 * fl / t / 1e9 / 2500:5.3f} of bf16 peak, min {min(res[mode]):.3f})"
         print(line, flush=True)
         del x, w, out
         torch.cuda.empty_cache()
-    os.environ["RMBX_GEMM_PERSIST"], os.environ["RMBX_GEMM_STAGGER"] = "0", "0"
+    os.environ["RMBX_GEMM_PERSIST"], os.environ["RMBX_GEMM_STAGGER"], os.environ["RMBX_GEMM_WIDE"] = "0", "0", "0"
     os.environ.pop("RMBX_GEMM_VAR", None)
 
 
