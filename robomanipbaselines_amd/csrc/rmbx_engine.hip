@@ -2250,9 +2250,7 @@ __device__ void sensors(Env& e, int ncon, int tid, double* cacc, double* cfrc, d
 // accumulation run on those register blocks with only one block column / vector staged in LDS.
 // The constraint Jacobian streams from the workspace (HBM/L2) through a 16-row LDS chunk.
 // ------------------------------------------------------------------------------------------
-#define SOLVER_THREADS 256  // the largest solver block (launch bound); the block may be 192 threads
-// (three waves, RMBX_SOLVER_THREADS=192): device loops stride by the launched size
-#define SOLVER_NT ((int)blockDim.x)
+#define SOLVER_THREADS 256
 #define MAX_NB 18  // nv <= 72
 #define MAX_NVP (4 * MAX_NB)
 #define RCHUNK 16
@@ -2490,7 +2488,7 @@ __device__ __forceinline__ void fwd4(const double* a, const double* inv, double*
 // the next diagonal block solves its block of y right after factoring it.
 __device__ void blk_cholesky_fwd(double* a, int bi, int bj, bool own, int NB, const double* b, SolverShared& S,
                                  int tid) {
-  for (int r = tid; r < 4 * NB; r += SOLVER_NT) S.acc[r] = b[r];
+  for (int r = tid; r < 4 * NB; r += SOLVER_THREADS) S.acc[r] = b[r];
   lds_sync();
   if (own && bi == 0 && bj == 0) {
     double inv[4];
@@ -2566,7 +2564,7 @@ __device__ void blk_solve_back(const double* a, int bi, int bj, bool own, int NB
     }
     lds_sync();
   }
-  for (int r = tid; r < 4 * NB; r += SOLVER_NT) x[r] = S.acc[r];
+  for (int r = tid; r < 4 * NB; r += SOLVER_THREADS) x[r] = S.acc[r];
   lds_sync();
 }
 
@@ -2574,7 +2572,7 @@ __device__ void blk_solve_back(const double* a, int bi, int bj, bool own, int NB
 __device__ void blk_solve(const double* a, int bi, int bj, bool own, int NB, const double* b,
                           double* x, SolverShared& S, int tid) {
   const int NVP = 4 * NB;
-  for (int r = tid; r < NVP; r += SOLVER_NT) S.acc[r] = b[r];
+  for (int r = tid; r < NVP; r += SOLVER_THREADS) S.acc[r] = b[r];
   lds_sync();
   // forward: y_j = L_jj^-1 (acc_j); acc_i -= L_ij y_j
   for (int j = 0; j < NB; j++) {
@@ -2626,7 +2624,7 @@ __device__ void blk_solve(const double* a, int bi, int bj, bool own, int NB, con
     }
     lds_sync();
   }
-  for (int r = tid; r < NVP; r += SOLVER_NT) x[r] = S.acc[r];
+  for (int r = tid; r < NVP; r += SOLVER_THREADS) x[r] = S.acc[r];
   lds_sync();
 }
 
@@ -2767,7 +2765,7 @@ __device__ void mass_tail(const SolverCtx& c, const double* x, double* y, Solver
   }
   lds_sync();
   subtree_sums(c, S);
-  for (int k = tid; k < 4 * c.NB; k += SOLVER_NT)
+  for (int k = tid; k < 4 * c.NB; k += SOLVER_THREADS)
     y[k] = k < c.nv ? dot6(S.cdof + 6 * k, S.bv + 6 * S.kb[k]) + m.dof_armature[k] * x[k] : 0.0;
   lds_sync();
   CPROF(30)
@@ -2785,7 +2783,7 @@ __device__ void jac_tmul(const SolverCtx& c, const double* w, double* out, Solve
   __syncthreads();  // w was written row-per-thread through global memory: full fence
   unsigned long long tp_ = c.prof ? stamp() : 0;
   // contact wrench about the origin = sum over the contact's rows of w_r (p x dir_r, dir_r)
-  for (int q = tid; q < c.ncon; q += SOLVER_NT) {
+  for (int q = tid; q < c.ncon; q += SOLVER_THREADS) {
     const int r0 = c.cefcadr[q];
     const int cnt = min(c.ccondim[q] == 1 ? 1 : 4, c.nefc - r0);
     double f[6] = {0, 0, 0, 0, 0, 0};
@@ -2798,7 +2796,7 @@ __device__ void jac_tmul(const SolverCtx& c, const double* w, double* out, Solve
 #pragma unroll
     for (int i = 0; i < 6; i++) cw[6 * q + i] = f[i];
   }
-  for (int i = tid; i < c.ne + c.nlim; i += SOLVER_NT) wst[i] = w[i];
+  for (int i = tid; i < c.ne + c.nlim; i += SOLVER_THREADS) wst[i] = w[i];
   lds_sync();
   CPROF(24)
   if (tid > 0 && tid < m.nbody) {
@@ -2825,7 +2823,7 @@ __device__ void jac_tmul(const SolverCtx& c, const double* w, double* out, Solve
   CPROF(25)
   subtree_sums(c, S);
   CPROF(26)
-  for (int k = tid; k < 4 * c.NB; k += SOLVER_NT) {
+  for (int k = tid; k < 4 * c.NB; k += SOLVER_THREADS) {
     double v = 0.0;
     if (k < c.nv) {
       v = dot6(S.cdof + 6 * k, S.bv + 6 * S.kb[k]);
@@ -2847,15 +2845,15 @@ __device__ void jac_tmul(const SolverCtx& c, const double* w, double* out, Solve
 // cost at x: sets jar (J x - aref), S.res, S.Mres; returns cost
 __device__ double solver_cost(const SolverCtx& c, const double* x, SolverShared& S) {
   const int tid = c.tid;
-  for (int k = tid; k < 4 * c.NB; k += SOLVER_NT) S.res[k] = k < c.nv ? x[k] - S.a0[k] : 0.0;
+  for (int k = tid; k < 4 * c.NB; k += SOLVER_THREADS) S.res[k] = k < c.nv ? x[k] - S.a0[k] : 0.0;
   lds_sync();
   body_vel(c, S.res, S);
   mass_tail(c, S.res, S.Mres, S);
   double part = 0;
-  for (int k = tid; k < c.nv; k += SOLVER_NT) part += S.res[k] * S.Mres[k];
+  for (int k = tid; k < c.nv; k += SOLVER_THREADS) part += S.res[k] * S.Mres[k];
   body_vel(c, x, S);
   double cpart = 0;
-  for (int r = tid; r < c.nefc; r += SOLVER_NT) {
+  for (int r = tid; r < c.nefc; r += SOLVER_THREADS) {
     const double jar = row_dot(c, r, S, x) - c.aref[r];
     c.jar[r] = jar;
     if (c.type[r] == 0 || jar < 0) cpart += 0.5 * c.D[r] * jar * jar;
@@ -2868,7 +2866,7 @@ __device__ double solver_cost(const SolverCtx& c, const double* x, SolverShared&
 __device__ double rows_cost(const SolverCtx& c, const double* x, SolverShared& S) {
   body_vel(c, x, S);
   double cpart = 0;
-  for (int r = c.tid; r < c.nefc; r += SOLVER_NT) {
+  for (int r = c.tid; r < c.nefc; r += SOLVER_THREADS) {
     const double jar = row_dot(c, r, S, x) - c.aref[r];
     c.jar[r] = jar;
     if (c.type[r] == 0 || jar < 0) cpart += 0.5 * c.D[r] * jar * jar;
@@ -2881,7 +2879,7 @@ __device__ double rows_cost(const SolverCtx& c, const double* x, SolverShared& S
 __device__ double solver_grad(const SolverCtx& c, int32_t* act_flags, SolverShared& S, bool* changed) {
   const int tid = c.tid, nv = c.nv, NVP = 4 * c.NB;
   int diff = 0;
-  for (int r = tid; r < c.nefc; r += SOLVER_NT) {
+  for (int r = tid; r < c.nefc; r += SOLVER_THREADS) {
     const double jar = c.jar[r];
     const int act = (c.type[r] == 0 || jar < 0) ? 1 : 0;
     c.wrow[r] = act ? c.D[r] * jar : 0.0;
@@ -2990,7 +2988,7 @@ __device__ void solver_hessian(const SolverCtx& c, const double* Mb, const int32
     if (!any) continue;  // uniform: every thread read the same flags
     // J_rk = [k on chain(b1)] cdof_k . rho1 + [k on chain(b2)] cdof_k . rho2 + dof terms; a
     // contact's two sides are exact negatives, so dofs on both chains give exactly 0
-    for (int e = tid; e < RCHUNK * NVP; e += SOLVER_NT) {
+    for (int e = tid; e < RCHUNK * NVP; e += SOLVER_THREADS) {
       const int rr = e / NVP, k = e - rr * NVP;
       double v = 0.0;
       const double w = S.jw[rr];
@@ -3096,28 +3094,28 @@ __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj,
   c.tid = tid;
   // qacc_smooth = M^-1 qfrc_smooth
   if (own) load_blockp(Mb, tid, a);
-  for (int k = tid; k < NVP; k += SOLVER_NT) S.tmp[k] = k < nv ? W(qfrc_smooth)[k] : 0.0;
+  for (int k = tid; k < NVP; k += SOLVER_THREADS) S.tmp[k] = k < nv ? W(qfrc_smooth)[k] : 0.0;
   lds_sync();
   blk_cholesky_fwd(a, bi, bj, own, NB, S.tmp, S, tid);
   blk_solve_back(a, bi, bj, own, NB, S.a0, S, tid);
   SPROF(8)
-  for (int k = tid; k < NVP; k += SOLVER_NT) S.tmp[k] = k < nv ? e.qacc_ws[k] : 0.0;
+  for (int k = tid; k < NVP; k += SOLVER_THREADS) S.tmp[k] = k < nv ? e.qacc_ws[k] : 0.0;
   lds_sync();
   // warm start vs smooth start (the smooth start has res = 0: only its rows cost anything)
   const double c_ws = solver_cost(c, S.tmp, S);
   double* jar_ws = W(efc_Js);  // (Js is dead until the first line search)
-  for (int r = tid; r < nefc; r += SOLVER_NT) jar_ws[r] = c.jar[r];
-  for (int k = tid; k < NVP; k += SOLVER_NT) S.Ms[k] = S.Mres[k];
+  for (int r = tid; r < nefc; r += SOLVER_THREADS) jar_ws[r] = c.jar[r];
+  for (int k = tid; k < NVP; k += SOLVER_THREADS) S.Ms[k] = S.Mres[k];
   lds_sync();
   const double c_sm = rows_cost(c, S.a0, S);
   const bool use_ws = c_ws < c_sm;
-  for (int k = tid; k < NVP; k += SOLVER_NT) {
+  for (int k = tid; k < NVP; k += SOLVER_THREADS) {
     S.a[k] = use_ws ? S.tmp[k] : S.a0[k];
     S.res[k] = use_ws ? S.res[k] : 0.0;
     S.Mres[k] = use_ws ? S.Ms[k] : 0.0;
   }
   if (use_ws)
-    for (int r = tid; r < nefc; r += SOLVER_NT) c.jar[r] = jar_ws[r];
+    for (int r = tid; r < nefc; r += SOLVER_THREADS) c.jar[r] = jar_ws[r];
   lds_sync();
   double cost = use_ws ? c_ws : c_sm;
   SPROF(9)
@@ -3142,14 +3140,14 @@ __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj,
       blk_solve(a, bi, bj, own, NB, S.grad, S.srch, S, tid);
     }
     SPROF(11)
-    for (int k = tid; k < NVP; k += SOLVER_NT) S.srch[k] = -S.srch[k];
+    for (int k = tid; k < NVP; k += SOLVER_THREADS) S.srch[k] = -S.srch[k];
     lds_sync();
     // J search (rows) and M search from one pass of body velocities of the search direction
     body_vel(c, S.srch, S);
-    for (int r = tid; r < nefc; r += SOLVER_NT) c.Js[r] = row_dot(c, r, S, S.srch);
+    for (int r = tid; r < nefc; r += SOLVER_THREADS) c.Js[r] = row_dot(c, r, S, S.srch);
     mass_tail(c, S.srch, S.Ms, S);
     double qp = 0, lp = 0;
-    for (int k = tid; k < nv; k += SOLVER_NT) {
+    for (int k = tid; k < nv; k += SOLVER_THREADS) {
       qp += S.srch[k] * S.Ms[k];
       lp += S.res[k] * S.Ms[k];
     }
@@ -3162,7 +3160,7 @@ __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj,
     for (int ls = 0; ls < m.ls_iterations; ls++) {
       double p1 = 0, p2 = 0;
       int changed = 0;
-      for (int r = tid; r < nefc; r += SOLVER_NT) {
+      for (int r = tid; r < nefc; r += SOLVER_THREADS) {
         const double js = c.Js[r], jr = c.jar[r];
         const double x = jr + alpha * js;
         if (c.type[r] == 0 || x < 0) {
@@ -3189,13 +3187,13 @@ __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj,
     // move along the search direction; res, M res and jar updated incrementally (as
     // mj_solNewton updates qacc, Ma and efc_Jaref)
     double part = 0, cpart = 0;
-    for (int k = tid; k < NVP; k += SOLVER_NT) {
+    for (int k = tid; k < NVP; k += SOLVER_THREADS) {
       S.a[k] += alpha * S.srch[k];
       S.res[k] += alpha * S.srch[k];
       S.Mres[k] += alpha * S.Ms[k];
       if (k < nv) part += S.res[k] * S.Mres[k];
     }
-    for (int r = tid; r < nefc; r += SOLVER_NT) {
+    for (int r = tid; r < nefc; r += SOLVER_THREADS) {
       const double jar = c.jar[r] + alpha * c.Js[r];
       c.jar[r] = jar;
       if (c.type[r] == 0 || jar < 0) cpart += 0.5 * c.D[r] * jar * jar;
@@ -3211,7 +3209,7 @@ __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj,
     }
   }
   // forces and qfrc_constraint = J^T f
-  for (int r = tid; r < nefc; r += SOLVER_NT) {
+  for (int r = tid; r < nefc; r += SOLVER_THREADS) {
     const double jar = c.jar[r];
     c.force[r] = (c.type[r] == 0 || jar < 0) ? -c.D[r] * jar : 0.0;
   }
@@ -3263,7 +3261,7 @@ __device__ void solver_sensors(Env& e, SolverShared& S, int ncon, int tree_round
     cross_force(v, Iv, vxIv);
     for (int i = 0; i < 6; i++) cfrc[6 * tid + i] = Ia[i] + vxIv[i];
   }
-  for (int c = tid; c < ncon; c += SOLVER_NT) {
+  for (int c = tid; c < ncon; c += SOLVER_THREADS) {
     double* o = cw + 6 * c;
     const int r0 = WI(con_efcadr)[c];
     if (r0 + (WI(con_condim)[c] == 1 ? 1 : 4) > e.L->nefc_max) {
@@ -3340,12 +3338,12 @@ __device__ void solver_integrate(Env& e, SolverShared& S, double* a, int bi, int
 #pragma unroll
     for (int q = 0; q < 16; q++) a[q] += hb[q];
   }
-  for (int k = tid; k < NVP; k += SOLVER_NT)
+  for (int k = tid; k < NVP; k += SOLVER_THREADS)
     S.tmp[k] = k < nv ? W(qfrc_smooth)[k] + W(qfrc_constraint)[k] : 0.0;
   lds_sync();
   // MuJoCo's divergence guard (mj_step -> mj_checkAcc) on the forward (constraint-solver) qacc
   bool bad = false;
-  for (int k = tid; k < nv; k += SOLVER_NT) {
+  for (int k = tid; k < nv; k += SOLVER_THREADS) {
     const double acc = W(qacc)[k];
     if (!isfinite(acc) || fabs(acc) > 1e10) bad = true;
   }
@@ -3358,12 +3356,12 @@ __device__ void solver_integrate(Env& e, SolverShared& S, double* a, int bi, int
     // the remaining substeps run from the reset state and the engine adds one masked substep
     // after the env-step (launch(): redo pass) for the envs that reset, so each env ends the
     // env-step with its full count of integrated substeps and MuJoCo's time.
-    for (int k = tid; k < m.nq; k += SOLVER_NT) e.qpos[k] = m.qpos0[k];
-    for (int k = tid; k < nv; k += SOLVER_NT) {
+    for (int k = tid; k < m.nq; k += SOLVER_THREADS) e.qpos[k] = m.qpos0[k];
+    for (int k = tid; k < nv; k += SOLVER_THREADS) {
       e.qvel[k] = 0.0;
       e.qacc_ws[k] = 0.0;
     }
-    for (int k = tid; k < m.nu; k += SOLVER_NT) e.ctrl[k] = 0.0;
+    for (int k = tid; k < m.nu; k += SOLVER_THREADS) e.ctrl[k] = 0.0;
     if (tid == 0) {
       e.time[0] = 0.0;
       e.stats[3] = sub;
@@ -3371,13 +3369,13 @@ __device__ void solver_integrate(Env& e, SolverShared& S, double* a, int bi, int
     __syncthreads();
     return;
   }
-  for (int k = tid; k < nv; k += SOLVER_NT) {
+  for (int k = tid; k < nv; k += SOLVER_THREADS) {
     const double acc = S.a[k];
     e.qvel[k] += h * acc;
     e.qacc_ws[k] = acc;
   }
   __syncthreads();  // the joint loop reads qvel joint-per-thread: full fence
-  for (int j = tid; j < m.njnt; j += SOLVER_NT) {
+  for (int j = tid; j < m.njnt; j += SOLVER_THREADS) {
     const int qa = m.jnt_qposadr[j], da = m.jnt_dofadr[j];
     if (m.jnt_type[j] == RMBX_JNT_FREE) {
       for (int i = 0; i < 3; i++) e.qpos[qa + i] += h * e.qvel[da + i];
@@ -3504,12 +3502,6 @@ __global__ void __launch_bounds__(SOLVER_THREADS, MINB) solver_kernel(KArgs args
   make_env(args, env, e);
   if (args.redo && e.stats[3] == 0) return;
   const int NB = (args.m.nv + 3) / 4;
-  // a three-wave block leaves the fourth wave's slots of the block reductions at zero (they add
-  // red[0] + red[1] + red[2] + red[3]); the owners of the packed 4x4 blocks must fit the block
-  if (tid == 0 && blockDim.x < 256) {
-    S.red[3] = S.red[7] = 0.0;
-    S.ired[3] = 0;
-  }
   int bi = 0, bj = 0;
   const bool own = tid < NB * (NB + 1) / 2;
   if (own) blk_coords(tid, &bi, &bj);
@@ -3517,22 +3509,22 @@ __global__ void __launch_bounds__(SOLVER_THREADS, MINB) solver_kernel(KArgs args
   PROF_BEGIN()
   const rmbx_model& m = args.m;
   // stage the dof axes, composite inertias and tree ranges the J-free row passes read
-  for (int k = tid; k < 6 * m.nv; k += SOLVER_NT) S.cdof[k] = W(cdof)[k];
-  for (int k = tid; k < 10 * m.nbody; k += SOLVER_NT) S.cinert[k] = W(cinert)[k];
-  for (int k = tid; k < m.nbody; k += SOLVER_NT) S.send[k] = (int16_t)args.subtree_end[k];
-  for (int k = tid; k < m.nv; k += SOLVER_NT) S.kb[k] = (int16_t)m.dof_body[k];
-  for (int k = tid; k < m.nbody; k += SOLVER_NT) S.par[k] = (int16_t)m.body_parent[k];
+  for (int k = tid; k < 6 * m.nv; k += SOLVER_THREADS) S.cdof[k] = W(cdof)[k];
+  for (int k = tid; k < 10 * m.nbody; k += SOLVER_THREADS) S.cinert[k] = W(cinert)[k];
+  for (int k = tid; k < m.nbody; k += SOLVER_THREADS) S.send[k] = (int16_t)args.subtree_end[k];
+  for (int k = tid; k < m.nv; k += SOLVER_THREADS) S.kb[k] = (int16_t)m.dof_body[k];
+  for (int k = tid; k < m.nbody; k += SOLVER_THREADS) S.par[k] = (int16_t)m.body_parent[k];
   if (tid < 6) S.bv[tid] = 0.0;  // the world body's velocity (row passes read it)
   const int ncon = WI(scal)[0], nefc = WI(scal)[1], ne = WI(scal)[2], nlim = WI(scal)[3];
   // per-launch row structure: contact bodies, equality rows, limit rows
   // (a body welded to the world moves with it: no dof sees its wrench and its velocity is
   // zero, so it is staged as the world body and the row passes skip it)
-  for (int q = tid; q < ncon; q += SOLVER_NT) {
+  for (int q = tid; q < ncon; q += SOLVER_THREADS) {
     const int b1 = WI(con_b1)[q], b2 = WI(con_b2)[q];
     S.ccb[q][0] = (int16_t)(m.body_weldid[b1] == 0 ? 0 : b1);
     S.ccb[q][1] = (int16_t)(m.body_weldid[b2] == 0 ? 0 : b2);
   }
-  for (int q = tid; q < ne; q += SOLVER_NT) {
+  for (int q = tid; q < ne; q += SOLVER_THREADS) {
     for (int i = 0; i < 12; i++) S.eqrho[q][i] = W(eqr_rho)[12 * q + i];
     for (int i = 0; i < 2; i++) {
       S.eqcoef[q][i] = W(eqr_coef)[2 * q + i];
@@ -3541,7 +3533,7 @@ __global__ void __launch_bounds__(SOLVER_THREADS, MINB) solver_kernel(KArgs args
       S.eqd[q][i] = (int16_t)WI(eqr_dof)[2 * q + i];
     }
   }
-  for (int i = tid; i < nlim; i += SOLVER_NT)
+  for (int i = tid; i < nlim; i += SOLVER_THREADS)
     S.lim[i] = (int16_t)(2 * WI(efc_obj)[ne + i] + (WI(efc_kind)[ne + i] >> 3));
   __syncthreads();
   // per-body wrench lists for J^T w (counted, scanned over bodies in wave 0, then filled)
@@ -3589,16 +3581,6 @@ static void launch_solver(int n_env, hipStream_t st, const KArgs& a) {
     const char* v = getenv("RMBX_SOLVER_MINB");
     return v ? atoi(v) : 4;
   }();
-  // RMBX_SOLVER_THREADS=192: three waves per env with the 3-waves-per-SIMD register budget (168
-  // VGPRs instead of 128: 46 spilled registers instead of 92) at the same 4 envs per CU
-  static const int nthr = [] {
-    const char* v = getenv("RMBX_SOLVER_THREADS");
-    return v ? atoi(v) : SOLVER_THREADS;
-  }();
-  if (nthr == 192 && ((a.m.nv + 3) / 4) * ((a.m.nv + 3) / 4 + 1) / 2 <= 192) {
-    hipLaunchKernelGGL(solver_kernel<3>, dim3(n_env), dim3(192), 0, st, a);
-    return;
-  }
   if (minb == 2)
     hipLaunchKernelGGL(solver_kernel<2>, dim3(n_env), dim3(SOLVER_THREADS), 0, st, a);
   else if (minb == 3)

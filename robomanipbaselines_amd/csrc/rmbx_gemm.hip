@@ -104,8 +104,10 @@ __device__ __forceinline__ void wait_vm() {
 // tiles per block group 8 (0), 4 (1), 16 (2), bit 3 = no output stores (phase skip: the epilogue's
 // cost; the result is not written), bit 4 = epilogue through LDS with 16-byte stores (needs
 // ldc % 4 == 0 and 16-B aligned C / res / bias rows), bit 5 = no A split (phase skip: the split's
-// VALU cost; truncated pieces, wrong values), bit 6 = stagger: waves 4-7 split + store the next A
-// tile before their first MFMA half-step (see gemm_f32x6_persistent_kernel's STAGGER)
+// VALU cost; truncated pieces, wrong values), bit 6 = stagger: waves 4-7 (the SIMD partners of
+// waves 0-3) split + store the next A tile before their first MFMA half-step instead of between
+// the halves (measured 3-7 % slower; so were a persistent one-block-per-CU form with the K pipeline
+// running across tiles and a 128 x 256 tile, profiles/r4_gemm_forms_ab.log)
 template <bool CONV, int VAR = 0>
 __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
   constexpr int GROUP = ((VAR >> 1) & 3) == 1 ? 4 : ((VAR >> 1) & 3) == 2 ? 16 : GM_GROUP;
@@ -380,566 +382,6 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// Persistent form (RMBX_GEMM_PERSIST=1; measured 1-6 % SLOWER than the per-tile kernel on every ACT
-// shape, profiles/r4_gemm_persist_ab.log, so not the default): one block per CU walks a sequence of
-// output tiles and the K
-// pipeline runs on ACROSS tile boundaries -- the W DMA of the next tile's first K step and its A
-// loads are issued under the last MFMAs of the current tile, so a tile's prologue (first A loads,
-// first split, first DMA) is never exposed, and the epilogue's 16-byte stores drain under the next
-// tile's MFMAs.  The epilogue transposes the accumulators through the stage buffer the last step
-// has just consumed (two halves of 32 rows per wave: 69.6 KiB), then one barrier before the
-// pipeline refills that buffer.  Tiles: the launch's tile list (XCD-grouped as above) is cut into
-// 8 contiguous ranges, one per XCD (blockIdx % 8), and the XCD's blocks take its tiles round-robin,
-// so the tiles in flight on one XCD at any time are neighbours sharing A rows and W columns in its
-// L2.  Same arithmetic and summation order as gemm_f32x6_kernel: bit-identical outputs.
-// ---------------------------------------------------------------------------------------------
-struct TileRef {
-  const float* A;
-  const uint16_t* W;
-  float* C;
-  int m0, n0;
-};
-
-__device__ __forceinline__ TileRef decode_tile(const GemmArgs& g, int lin) {
-  TileRef t{g.A, g.W, g.C, 0, 0};
-  if (g.batch > 1) {
-    const int per_item = g.tiles_m * g.tiles_n;
-    const int item = lin / per_item;
-    lin -= item * per_item;
-    t.A += item * g.a_bs;
-    t.W += item * g.w_bs;
-    t.C += item * g.c_bs;
-  }
-  const int per_group = GM_GROUP * g.tiles_n;
-  const int grp = lin / per_group;
-  const int first_m = grp * GM_GROUP;
-  const int gsize = min(g.tiles_m - first_m, GM_GROUP);
-  const int in_group = lin - grp * per_group;
-  t.m0 = (first_m + in_group % gsize) * GM_BM;
-  t.n0 = (in_group / gsize) * GM_BN;
-  return t;
-}
-
-// STAGGER: waves 4-7 (the partners of waves 0-3 on the four SIMDs) split + store the next A tile
-// BEFORE their first MFMA half-step instead of between the two halves, so that on every SIMD one
-// wave's VALU/LDS segment runs beside its partner's MFMAs instead of both waves idling the matrix
-// pipe at the same time (MI355X_MICROARCH.md, two waves per SIMD, item 9)
-template <bool CONV, bool STAGGER>
-__global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_persistent_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * GM_STAGE];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave & 3, wn = wave >> 2;
-
-  // this block's tiles: XCD x = blockIdx % 8 owns the contiguous range [lo, hi) of the tile list;
-  // its blocks (blockIdx / 8 = j of nbx) take lo + j, lo + j + nbx, ...
-  const int ntiles = g.tiles_m * g.tiles_n * (g.batch > 1 ? g.batch : 1);
-  const int nblk = gridDim.x, bid = blockIdx.x;
-  const int xcd = bid & 7, j = bid >> 3;
-  const int nbx = (nblk >> 3) + (xcd < (nblk & 7) ? 1 : 0);
-  const int per = ntiles >> 3, rem = ntiles & 7;
-  const int lo = xcd * per + min(xcd, rem);
-  const int hi = lo + per + (xcd < rem ? 1 : 0);
-  const int first = lo + j;
-  if (first >= hi) return;
-  const int my_tiles = (hi - first + nbx - 1) / nbx;
-  const int KT = g.K / GM_BK;
-  const int S = my_tiles * KT;  // K steps of this block, all tiles concatenated
-
-  // A staging as gemm_f32x6_kernel (rows arow, arow + 128; k quarter aq), for the tile of the
-  // step being loaded (A runs two steps ahead of the MFMAs, W one step)
-  const int aq = tid & 3, arow = tid >> 2;
-  const int aoff0 = arow * 64 + ((aq ^ ((arow >> 2) & 2)) << 4);
-  const int aoff1 = (arow + 128) * 64 + ((aq ^ (((arow + 128) >> 2) & 2)) << 4);
-  int a_tile = -1;
-  const float* ag0 = g.A;
-  const float* ag1 = g.A;
-  long long cbase[2] = {0, 0};
-  int cy[2] = {0, 0}, cx[2] = {0, 0};
-  auto set_a_tile = [&](int i) {
-    a_tile = i;
-    const TileRef t = decode_tile(g, first + i * nbx);
-    if constexpr (!CONV) {
-      ag0 = t.A + (long long)min(t.m0 + arow, g.M - 1) * g.lda + 8 * aq;
-      ag1 = t.A + (long long)min(t.m0 + arow + 128, g.M - 1) * g.lda + 8 * aq;
-    } else {
-#pragma unroll
-      for (int r2 = 0; r2 < 2; ++r2) {
-        const int m = min(t.m0 + arow + 128 * r2, g.M - 1);
-        const int hw = g.oh * g.ow;
-        const int img = m / hw, rm = m - img * hw;
-        const int oy = rm / g.ow, ox = rm - oy * g.ow;
-        cy[r2] = oy * g.stride - g.pad;
-        cx[r2] = ox * g.stride - g.pad;
-        cbase[r2] = ((long long)(img * g.ih + cy[r2]) * g.iw + cx[r2]) * g.ic + 8 * aq;
-      }
-    }
-  };
-  int w_tile = -1;
-  const uint16_t* bsrc[3] = {g.W, g.W, g.W};
-  auto set_w_tile = [&](int i) {
-    w_tile = i;
-    const TileRef t = decode_tile(g, first + i * nbx);
-#pragma unroll
-    for (int q = 0; q < 3; ++q) {
-      const int idx = wave * 3 + q, p = idx >> 3;
-      const int row = (idx & 7) * 16 + (lane >> 2);
-      const int sl = (lane & 3) ^ ((row >> 2) & 2);
-      bsrc[q] = t.W + p * g.wps + (long long)(t.n0 + row) * g.ldw + sl * 8;
-    }
-  };
-  auto stage_b = [&](int s, int buf) {
-    const int i = s / KT, kt = s - i * KT;
-    if (i != w_tile) set_w_tile(i);
-    unsigned char* base = smem + buf * GM_STAGE + GM_A_BYTES;
-#pragma unroll
-    for (int q = 0; q < 3; ++q) glds16(bsrc[q] + kt * GM_BK, base + (wave * 3 + q) * 1024);
-  };
-  auto load_a = [&](float4 (&R)[4], int s) -> int {
-    const int i = s / KT, kt = s - i * KT;
-    if (i != a_tile) set_a_tile(i);
-    if constexpr (!CONV) {
-      const float4* p0 = (const float4*)(ag0 + kt * GM_BK);
-      const float4* p1 = (const float4*)(ag1 + kt * GM_BK);
-      R[0] = p0[0];
-      R[1] = p0[1];
-      R[2] = p1[0];
-      R[3] = p1[1];
-      return 3;
-    } else {
-      const int k0 = kt * GM_BK;
-      const int tap = k0 / g.ic, c0 = k0 - tap * g.ic;
-      const int ky = tap / g.kw, kx = tap - ky * g.kw;
-      int ok = 0;
-#pragma unroll
-      for (int r2 = 0; r2 < 2; ++r2) {
-        const bool v = (unsigned)(cy[r2] + ky) < (unsigned)g.ih && (unsigned)(cx[r2] + kx) < (unsigned)g.iw;
-        const float4* p = (const float4*)(g.A + (v ? cbase[r2] + (long long)(ky * g.iw + kx) * g.ic + c0 : 0));
-        R[2 * r2] = p[0];
-        R[2 * r2 + 1] = p[1];
-        ok |= (int)v << r2;
-      }
-      return ok;
-    }
-  };
-  auto store_a = [&](const float4 (&Rin)[4], int ok, int buf) {
-    float4 R[4] = {Rin[0], Rin[1], Rin[2], Rin[3]};
-    if constexpr (CONV) {
-      const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
-      if (!(ok & 1)) R[0] = R[1] = z;
-      if (!(ok & 2)) R[2] = R[3] = z;
-    }
-    uint32_t p0[8], p1[8], p2[8];
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      split_pair(R[i].x, R[i].y, p0[2 * i], p1[2 * i], p2[2 * i]);
-      split_pair(R[i].z, R[i].w, p0[2 * i + 1], p1[2 * i + 1], p2[2 * i + 1]);
-    }
-    unsigned char* base = smem + buf * GM_STAGE;
-    *(uint4*)(base + aoff0) = make_uint4(p0[0], p0[1], p0[2], p0[3]);
-    *(uint4*)(base + GM_A_PLANE + aoff0) = make_uint4(p1[0], p1[1], p1[2], p1[3]);
-    *(uint4*)(base + 2 * GM_A_PLANE + aoff0) = make_uint4(p2[0], p2[1], p2[2], p2[3]);
-    *(uint4*)(base + aoff1) = make_uint4(p0[4], p0[5], p0[6], p0[7]);
-    *(uint4*)(base + GM_A_PLANE + aoff1) = make_uint4(p1[4], p1[5], p1[6], p1[7]);
-    *(uint4*)(base + 2 * GM_A_PLANE + aoff1) = make_uint4(p2[4], p2[5], p2[6], p2[7]);
-  };
-
-  f32x4v acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int jj = 0; jj < 4; ++jj) acc[i][jj] = (f32x4v){0.f, 0.f, 0.f, 0.f};
-
-  const int fr = lane & 15, fs = lane >> 4;
-  auto frag_off = [&](int row) { return row * 64 + ((fs ^ ((row >> 2) & 2)) << 4); };
-  auto half_step = [&](int buf, int h, const bf16x8 (&b)[4][3]) {
-    const unsigned char* As = smem + buf * GM_STAGE;
-    bf16x8 a[2][3];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int off = frag_off(wm * 64 + (2 * h + i) * 16 + fr);
-#pragma unroll
-      for (int p = 0; p < 3; ++p) a[i][p] = *(const bf16x8*)(As + p * GM_A_PLANE + off);
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int nj = 0; nj < 4; ++nj) {
-        f32x4v c = acc[2 * h + i][nj];
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][2], b[nj][0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[nj][1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[nj][2], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[nj][0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[nj][1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[nj][0], c, 0, 0, 0);
-        acc[2 * h + i][nj] = c;
-      }
-  };
-  auto read_b = [&](bf16x8 (&b)[4][3], int buf) {
-    const unsigned char* Bs = smem + buf * GM_STAGE + GM_A_BYTES;
-#pragma unroll
-    for (int nj = 0; nj < 4; ++nj) {
-      const int off = frag_off(wn * 64 + nj * 16 + fr);
-#pragma unroll
-      for (int p = 0; p < 3; ++p) b[nj][p] = *(const bf16x8*)(Bs + p * GM_B_PLANE + off);
-    }
-  };
-
-  // epilogue of tile i through the (consumed) stage buffer buf, 32 rows per wave per half:
-  // accumulators -> LDS rows (pitch 68 floats) -> float4 rows, 16-byte stores
-  constexpr int PITCH = 68;
-  static_assert(8 * 32 * PITCH * 4 <= GM_STAGE, "epilogue halves must fit one stage buffer");
-  const bool vec_ok = g.ldc % 4 == 0 && ((uintptr_t)g.C | (uintptr_t)g.res | (uintptr_t)g.bias) % 16 == 0 &&
-                      (g.batch <= 1 || g.c_bs % 4 == 0);
-  auto epilogue = [&](int i, int buf) {
-    const TileRef t = decode_tile(g, first + i * nbx);
-    if (!vec_ok) {  // scalar stores straight from the accumulators (no 16-B alignment)
-#pragma unroll
-      for (int nj = 0; nj < 4; ++nj) {
-        const int n = t.n0 + wn * 64 + nj * 16 + fr;
-        const float bn = g.bias ? g.bias[n] : 0.f;
-#pragma unroll
-        for (int mi = 0; mi < 4; ++mi) {
-          const int mb = t.m0 + wm * 64 + mi * 16 + 4 * fs;
-#pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int m = mb + e;
-            if (m < g.M) {
-              float v = acc[mi][nj][e] + bn;
-              if (g.res) v += g.res[(long long)m * g.ldc + n];
-              if (g.relu) v = fmaxf(v, 0.f);
-              t.C[(long long)m * g.ldc + n] = v;
-            }
-          }
-        }
-      }
-      return;
-    }
-    float* T = reinterpret_cast<float*>(smem + buf * GM_STAGE) + wave * (32 * PITCH);
-    const int c4 = (lane & 15) * 4;
-    const int n = t.n0 + wn * 64 + c4;
-    float4 bn = make_float4(0.f, 0.f, 0.f, 0.f);
-    if (g.bias) bn = *(const float4*)(g.bias + n);
-#pragma unroll
-    for (int hh = 0; hh < 2; ++hh) {
-#pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
-#pragma unroll
-        for (int nj = 0; nj < 4; ++nj)
-#pragma unroll
-          for (int e = 0; e < 4; ++e) T[(mi * 16 + 4 * fs + e) * PITCH + nj * 16 + fr] = acc[2 * hh + mi][nj][e];
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave reads only its own rows
-#pragma unroll
-      for (int it = 0; it < 8; ++it) {
-        const int r = it * 4 + (lane >> 4);
-        const int m = t.m0 + wm * 64 + hh * 32 + r;
-        float4 v = *(const float4*)(T + r * PITCH + c4);
-        if (m < g.M) {
-          v.x += bn.x; v.y += bn.y; v.z += bn.z; v.w += bn.w;
-          if (g.res) {
-            const float4 rv = *(const float4*)(g.res + (long long)m * g.ldc + n);
-            v.x += rv.x; v.y += rv.y; v.z += rv.z; v.w += rv.w;
-          }
-          if (g.relu) {
-            v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
-          }
-          *(float4*)(t.C + (long long)m * g.ldc + n) = v;
-        }
-      }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // reads done before the second half's writes
-    }
-  };
-
-  float4 Ra[4], Rb[4];
-  int oka, okb;
-  oka = load_a(Ra, 0);
-  stage_b(0, 0);
-  okb = load_a(Rb, min(1, S - 1));
-  store_a(Ra, oka, 0);
-  wait_vm<4>();
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  auto step = [&](int s, float4 (&Rcur)[4], int& okcur, float4 (&Rnext)[4], int& oknext) {
-    const int buf = s & 1;
-    const bool more = s + 1 < S;
-    if (more) stage_b(s + 1, buf ^ 1);
-    oknext = load_a(Rnext, min(s + 2, S - 1));  // unconditional, as gemm_f32x6_kernel
-    bf16x8 b[4][3];
-    read_b(b, buf);
-    const bool late = !STAGGER || wave < 4;
-    if (more && !late) store_a(Rcur, okcur, buf ^ 1);
-    half_step(buf, 0, b);
-    if (more && late) store_a(Rcur, okcur, buf ^ 1);
-    half_step(buf, 1, b);
-    if (more) {
-      wait_vm<4>();
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    }
-    const int i = s / KT;
-    if (s - i * KT == KT - 1) {  // the tile's last K step: epilogue through buffer buf (consumed)
-      if (!more) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-      epilogue(i, buf);
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-        for (int nj = 0; nj < 4; ++nj) acc[mi][nj] = (f32x4v){0.f, 0.f, 0.f, 0.f};
-      // every wave's epilogue reads of buf are done before step s + 1 refills it
-      if (more) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    }
-  };
-  for (int s = 0; s < S; s += 2) {
-    step(s, Rb, okb, Ra, oka);
-    if (s + 1 < S) step(s + 1, Ra, oka, Rb, okb);
-  }
-}
-
-// ---------------------------------------------------------------------------------------------
-// Wide tile (RMBX_GEMM_WIDE=1): the block owns 128 rows x 256 columns instead of 256 x 128, same
-// 8 waves of 64 x 64 (2 row x 4 column waves), same K step of 32 and two 72-KiB LDS stages (A:
-// 3 planes x 128 x 32, W: 3 planes x 256 x 32).  Per K step a thread splits 8 A values instead of
-// 16 (half the split VALU per MFMA), each A row is re-read by half as many column tiles (A is the
-// operand that streams from beyond L2: FFN1 re-reads its 0.63 GB A once per column tile), W --
-// pre-split, LDS-DMA, L2-resident -- twice as often.  N % 256 == 128 leaves the last column tile
-// half full: its waves 4-7 (columns 128-255) skip their MFMAs.  Bit-identical to the 256 x 128
-// kernel (same products, same K order per output).
-// ---------------------------------------------------------------------------------------------
-constexpr int GW_BM = 128, GW_BN = 256;
-constexpr int GW_A_PLANE = GW_BM * GM_BK * 2;           // 8 KiB
-constexpr int GW_B_PLANE = GW_BN * GM_BK * 2;           // 16 KiB
-constexpr int GW_A_BYTES = 3 * GW_A_PLANE;              // 24 KiB
-constexpr int GW_STAGE = GW_A_BYTES + 3 * GW_B_PLANE;   // 72 KiB
-static_assert(2 * GW_STAGE <= 160 * 1024, "wide GEMM stages");
-
-template <bool CONV, bool STAGGER>
-__global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_wide_kernel(GemmArgs g) {
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * GW_STAGE];
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int wm = wave & 1, wn = wave >> 1;  // waves 4-7 own columns 128-255
-
-  // block -> tile, as gemm_f32x6_kernel (XCD-contiguous ranges, groups of GM_GROUP row tiles x all
-  // column tiles, row tile fastest)
-  const int nblk = gridDim.x, bid = blockIdx.x;
-  const int xcd = bid & 7, q = nblk >> 3, r = nblk & 7;
-  int lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
-  if (g.batch > 1) {
-    const int per_item = g.tiles_m * g.tiles_n;
-    const int item = lin / per_item;
-    lin -= item * per_item;
-    g.A += item * g.a_bs;
-    g.W += item * g.w_bs;
-    g.C += item * g.c_bs;
-  }
-  const int per_group = GM_GROUP * g.tiles_n;
-  const int first_m = (lin / per_group) * GM_GROUP;
-  const int gsize = min(g.tiles_m - first_m, GM_GROUP);
-  const int in_group = lin - (lin / per_group) * per_group;
-  const int tm = first_m + in_group % gsize, tn = in_group / gsize;
-  const int m0 = tm * GW_BM, n0 = tn * GW_BN;
-  const bool wave_cols = n0 + wn * 64 < g.N;  // this wave's 64 columns exist (half tile at the end)
-
-  // A staging: thread -> row tid / 4, k quarter tid % 4 (8 f32); rows past M re-read row M - 1
-  const int aq = tid & 3, arow = tid >> 2;
-  const float* ag = g.A + (long long)min(m0 + arow, g.M - 1) * g.lda + 8 * aq;
-  const int aoff = arow * 64 + ((aq ^ ((arow >> 2) & 2)) << 4);
-  // W: 48 LDS-DMA pieces (16 per plane) of 16 rows x 64 B, wave w copies pieces 6w .. 6w + 5; rows
-  // past N (the half tile) re-read row N - 1
-  const uint16_t* bsrc[6];
-#pragma unroll
-  for (int t = 0; t < 6; ++t) {
-    const int i = wave * 6 + t, p = i >> 4;
-    const int row = (i & 15) * 16 + (lane >> 2);
-    const int sl = (lane & 3) ^ ((row >> 2) & 2);
-    bsrc[t] = g.W + p * g.wps + (long long)min(n0 + row, g.N - 1) * g.ldw + sl * 8;
-  }
-  auto stage_b = [&](int kt, int buf) {
-    unsigned char* base = smem + buf * GW_STAGE + GW_A_BYTES;
-#pragma unroll
-    for (int t = 0; t < 6; ++t) glds16(bsrc[t] + kt * GM_BK, base + (wave * 6 + t) * 1024);
-  };
-  long long cbase = 0;
-  int cy = 0, cx = 0;
-  if constexpr (CONV) {
-    const int m = min(m0 + arow, g.M - 1);
-    const int hw = g.oh * g.ow;
-    const int img = m / hw, rem = m - img * hw;
-    const int oy = rem / g.ow, ox = rem - oy * g.ow;
-    cy = oy * g.stride - g.pad;
-    cx = ox * g.stride - g.pad;
-    cbase = ((long long)(img * g.ih + cy) * g.iw + cx) * g.ic + 8 * aq;
-  }
-  auto load_a = [&](float4 (&R)[2], int kt) -> int {
-    if constexpr (!CONV) {
-      const float4* p0 = (const float4*)(ag + kt * GM_BK);
-      R[0] = p0[0];
-      R[1] = p0[1];
-      return 1;
-    } else {
-      const int k0 = kt * GM_BK;
-      const int tap = k0 / g.ic, c0 = k0 - tap * g.ic;
-      const int ky = tap / g.kw, kx = tap - ky * g.kw;
-      const bool v = (unsigned)(cy + ky) < (unsigned)g.ih && (unsigned)(cx + kx) < (unsigned)g.iw;
-      const float4* p = (const float4*)(g.A + (v ? cbase + (long long)(ky * g.iw + kx) * g.ic + c0 : 0));
-      R[0] = p[0];
-      R[1] = p[1];
-      return (int)v;
-    }
-  };
-  auto store_a = [&](const float4 (&Rin)[2], int ok, int buf) {
-    float4 R[2] = {Rin[0], Rin[1]};
-    if constexpr (CONV) {
-      if (!ok) R[0] = R[1] = make_float4(0.f, 0.f, 0.f, 0.f);
-    }
-    uint32_t p0[4], p1[4], p2[4];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      split_pair(R[i].x, R[i].y, p0[2 * i], p1[2 * i], p2[2 * i]);
-      split_pair(R[i].z, R[i].w, p0[2 * i + 1], p1[2 * i + 1], p2[2 * i + 1]);
-    }
-    unsigned char* base = smem + buf * GW_STAGE;
-    *(uint4*)(base + aoff) = make_uint4(p0[0], p0[1], p0[2], p0[3]);
-    *(uint4*)(base + GW_A_PLANE + aoff) = make_uint4(p1[0], p1[1], p1[2], p1[3]);
-    *(uint4*)(base + 2 * GW_A_PLANE + aoff) = make_uint4(p2[0], p2[1], p2[2], p2[3]);
-  };
-
-  f32x4v acc[4][4];
-#pragma unroll
-  for (int i = 0; i < 4; ++i)
-#pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4v){0.f, 0.f, 0.f, 0.f};
-
-  const int fr = lane & 15, fs = lane >> 4;
-  auto frag_off = [&](int row) { return row * 64 + ((fs ^ ((row >> 2) & 2)) << 4); };
-  auto half_step = [&](int buf, int h, const bf16x8 (&b)[4][3]) {
-    const unsigned char* As = smem + buf * GW_STAGE;
-    bf16x8 a[2][3];
-#pragma unroll
-    for (int i = 0; i < 2; ++i) {
-      const int off = frag_off(wm * 64 + (2 * h + i) * 16 + fr);
-#pragma unroll
-      for (int p = 0; p < 3; ++p) a[i][p] = *(const bf16x8*)(As + p * GW_A_PLANE + off);
-    }
-#pragma unroll
-    for (int i = 0; i < 2; ++i)
-#pragma unroll
-      for (int nj = 0; nj < 4; ++nj) {
-        f32x4v c = acc[2 * h + i][nj];
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][2], b[nj][0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[nj][1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[nj][2], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[nj][0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[nj][1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[nj][0], c, 0, 0, 0);
-        acc[2 * h + i][nj] = c;
-      }
-  };
-  auto read_b = [&](bf16x8 (&b)[4][3], int buf) {
-    const unsigned char* Bs = smem + buf * GW_STAGE + GW_A_BYTES;
-#pragma unroll
-    for (int nj = 0; nj < 4; ++nj) {
-      const int off = frag_off(wn * 64 + nj * 16 + fr);
-#pragma unroll
-      for (int p = 0; p < 3; ++p) b[nj][p] = *(const bf16x8*)(Bs + p * GW_B_PLANE + off);
-    }
-  };
-
-  // K steps as gemm_f32x6_kernel: W of kt + 1 by LDS-DMA (6 pieces per wave), A of kt + 2 into
-  // registers, A of kt + 1 split and stored between the two MFMA halves (before them for waves 4-7
-  // with STAGGER); vmcnt(2): the 2 A loads of kt + 2 may stay in flight
-  const int KT = g.K / GM_BK;
-  float4 Ra[2], Rb[2];
-  int oka, okb;
-  oka = load_a(Ra, 0);
-  stage_b(0, 0);
-  okb = load_a(Rb, min(1, KT - 1));
-  store_a(Ra, oka, 0);
-  wait_vm<2>();
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  auto step = [&](int kt, float4 (&Rcur)[2], int& okcur, float4 (&Rnext)[2], int& oknext) {
-    const int buf = kt & 1;
-    const bool more = kt + 1 < KT;
-    if (more) stage_b(kt + 1, buf ^ 1);
-    oknext = load_a(Rnext, min(kt + 2, KT - 1));
-    const bool late = !STAGGER || wave < 4;
-    if (more && !late) store_a(Rcur, okcur, buf ^ 1);
-    if (wave_cols) {
-      bf16x8 b[4][3];
-      read_b(b, buf);
-      half_step(buf, 0, b);
-      if (more && late) store_a(Rcur, okcur, buf ^ 1);
-      half_step(buf, 1, b);
-    } else if (more && late) {
-      store_a(Rcur, okcur, buf ^ 1);
-    }
-    if (more) {
-      wait_vm<2>();
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    }
-  };
-  for (int kt = 0; kt < KT; kt += 2) {
-    step(kt, Rb, okb, Ra, oka);
-    if (kt + 1 < KT) step(kt + 1, Ra, oka, Rb, okb);
-  }
-
-  // epilogue through LDS (as gemm_f32x6_kernel VAR 16): the wave's 64 x 64 tile row-major in its
-  // own 17 KiB of the idle stage buffers, then float4 rows, 16-byte stores
-  const bool vec_ok = g.ldc % 4 == 0 && ((uintptr_t)g.C | (uintptr_t)g.res | (uintptr_t)g.bias) % 16 == 0 &&
-                      (g.batch <= 1 || g.c_bs % 4 == 0);
-  if (!vec_ok) {
-    if (!wave_cols) return;
-#pragma unroll
-    for (int nj = 0; nj < 4; ++nj) {
-      const int n = n0 + wn * 64 + nj * 16 + fr;
-      const float bn = g.bias ? g.bias[n] : 0.f;
-#pragma unroll
-      for (int mi = 0; mi < 4; ++mi) {
-        const int mb = m0 + wm * 64 + mi * 16 + 4 * fs;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int m = mb + e;
-          if (m < g.M) {
-            float v = acc[mi][nj][e] + bn;
-            if (g.res) v += g.res[(long long)m * g.ldc + n];
-            if (g.relu) v = fmaxf(v, 0.f);
-            g.C[(long long)m * g.ldc + n] = v;
-          }
-        }
-      }
-    }
-    return;
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  if (!wave_cols) return;
-  constexpr int PITCH = 68;
-  float* T = reinterpret_cast<float*>(smem) + wave * (64 * PITCH);
-#pragma unroll
-  for (int mi = 0; mi < 4; ++mi)
-#pragma unroll
-    for (int nj = 0; nj < 4; ++nj)
-#pragma unroll
-      for (int e = 0; e < 4; ++e) T[(mi * 16 + 4 * fs + e) * PITCH + nj * 16 + fr] = acc[mi][nj][e];
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  const int c4 = (lane & 15) * 4;
-  const int n = n0 + wn * 64 + c4;
-  float4 bn = make_float4(0.f, 0.f, 0.f, 0.f);
-  if (g.bias) bn = *(const float4*)(g.bias + n);
-#pragma unroll
-  for (int it = 0; it < 16; ++it) {
-    const int rr = it * 4 + (lane >> 4);
-    const int m = m0 + wm * 64 + rr;
-    if (m < g.M) {
-      float4 v = *(const float4*)(T + rr * PITCH + c4);
-      v.x += bn.x; v.y += bn.y; v.z += bn.z; v.w += bn.w;
-      if (g.res) {
-        const float4 rv = *(const float4*)(g.res + (long long)m * g.ldc + n);
-        v.x += rv.x; v.y += rv.y; v.z += rv.z; v.w += rv.w;
-      }
-      if (g.relu) {
-        v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
-      }
-      *(float4*)(g.C + (long long)m * g.ldc + n) = v;
-    }
-  }
-}
-
 // planes[p * n + i] = piece p of x[i] (x = x0 + x1 + x2, bf16 bits)
 __global__ void split_bf16x3_kernel(const float* __restrict__ x, uint16_t* __restrict__ planes, long long n) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
@@ -954,49 +396,11 @@ __global__ void split_bf16x3_kernel(const float* __restrict__ x, uint16_t* __res
 // default: the LDS-transposed epilogue with 16-byte stores (VAR 16: 1.04-1.08x over 64 scalar
 // stores per lane, profiles/r3_gemm_var_sweep.log) whenever the output / residual / bias rows allow
 // 16-byte accesses; RMBX_GEMM_VAR overrides (profiling)
-int gemm_device_cus() {
-  static const int cus = [] {
-    int dev = 0, n = 0;
-    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
-      return 256;
-    return n > 0 ? n : 256;
-  }();
-  return cus;
-}
-
 template <bool CONV>
 void launch_gemm(long long blocks, const GemmArgs& g, hipStream_t st) {
   // (the environment is read per launch, so a test or a profile can compare the forms in one process)
   const char* ve = getenv("RMBX_GEMM_VAR");
   const int env_var = ve ? atoi(ve) : -1;
-  // the 128 x 256 tile (RMBX_GEMM_WIDE=1; RMBX_GEMM_STAGGER=1 adds the wave-4-7 stagger)
-  const char* we = getenv("RMBX_GEMM_WIDE");
-  if (we && atoi(we) != 0 && env_var < 0) {
-    GemmArgs w = g;
-    w.tiles_m = (g.M + GW_BM - 1) / GW_BM;
-    w.tiles_n = (g.N + GW_BN - 1) / GW_BN;
-    const long long wblocks = (long long)w.tiles_m * w.tiles_n * (g.batch > 1 ? g.batch : 1);
-    const char* se = getenv("RMBX_GEMM_STAGGER");
-    if (se && atoi(se) != 0)
-      hipLaunchKernelGGL((gemm_f32x6_wide_kernel<CONV, true>), dim3((unsigned)wblocks), dim3(GM_THREADS), 0, st, w);
-    else
-      hipLaunchKernelGGL((gemm_f32x6_wide_kernel<CONV, false>), dim3((unsigned)wblocks), dim3(GM_THREADS), 0, st, w);
-    return;
-  }
-  // persistent blocks (one per CU) only with RMBX_GEMM_PERSIST=1: measured 1-6 % slower than one
-  // block per tile on every ACT shape (profiles/r4_gemm_persist_ab.log)
-  const char* pe = getenv("RMBX_GEMM_PERSIST");
-  const bool persist = pe ? atoi(pe) != 0 : false;
-  if (persist && env_var < 0) {
-    const int cus = gemm_device_cus();
-    const long long grid = blocks < cus ? blocks : cus;
-    const char* se = getenv("RMBX_GEMM_STAGGER");
-    if (se && atoi(se) != 0)
-      hipLaunchKernelGGL((gemm_f32x6_persistent_kernel<CONV, true>), dim3((unsigned)grid), dim3(GM_THREADS), 0, st, g);
-    else
-      hipLaunchKernelGGL((gemm_f32x6_persistent_kernel<CONV, false>), dim3((unsigned)grid), dim3(GM_THREADS), 0, st, g);
-    return;
-  }
   const bool vec_ok = g.ldc % 4 == 0 && ((uintptr_t)g.C | (uintptr_t)g.res | (uintptr_t)g.bias) % 16 == 0 &&
                       (g.batch <= 1 || g.c_bs % 4 == 0);
   int var = env_var >= 0 ? env_var : 16;
