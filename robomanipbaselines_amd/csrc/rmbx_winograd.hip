@@ -320,7 +320,12 @@ __global__ void __launch_bounds__(WG_THREADS, 1) wino_f32_kernel(WinoArgs a) {
 // complementary SIMDs, with the loads issued mid-stream -- 6.42 vs 5.71 ms at 512 channels; four
 // groups including the U waves, 6.90 ms.)
 // LDS: U and V double buffered, 108 KiB.  Persistent blocks and the per-XCD output-channel block
-// as F(2x2).
+// as F(2x2).  Measured slower in round 4 (profiles/r4_wino4_padded_lds_ab.log,
+// r4_wino4_producer_consumer_ab.log): bank-conflict-free padded U / V images (64 ch 8.17 vs 7.66
+// ms: 33 % more U DMA per chunk, 150 KiB of LDS) and a 12-wave producer / consumer split (8 MFMA-only
+// waves, 4 waves moving U and transforming the windows; 1.26-1.36x slower, bit-identical: at 3 waves
+// per SIMD the 168-register budget spills the consumers and the U DMA of a chunk, issued by two
+// waves, lands too late for the barrier that publishes it).
 // =============================================================================================
 __device__ float g_wino_zero[4];  // zero-initialised: the pixels outside the image
 constexpr int W4_TILES = 32;
@@ -604,225 +609,6 @@ __global__ void __launch_bounds__(WG_THREADS, 1) wino4_f32_kernel(WinoArgs a) {
   }
 }
 
-// =============================================================================================
-// Producer / consumer form of the F(4x4) kernel (RMBX_WINO4_SPEC=1): 12 waves per block, the
-// eight MFMA waves (consumers, the same 64 output channels x 32 tiles and accumulator layout as
-// wino4_f32_kernel) issue nothing but their LDS operand reads, MFMAs and the unit epilogue; four
-// producer waves (two groups of two) do all the data movement.  In the interval between the
-// barriers that publish chunks c and c + 1, group (c + 1) & 1 transforms the windows of chunk c + 1
-// (loaded one interval earlier) into V buffer (c + 1) & 1, and group c & 1 moves U of chunk c + 1
-// into U buffer (c + 1) & 1 by LDS-DMA and then issues the window loads of chunk c + 2, which stay in
-// flight across the barrier (its s_waitcnt leaves those 36 loads outstanding).  Same products,
-// same order, bit-identical to wino4_f32_kernel.  12 waves = 3 per SIMD: 168 VGPRs per wave (the
-// consumer's 144 accumulators + operands; the producer's 36 window values + transform).
-// =============================================================================================
-constexpr int W4S_THREADS = 768;
-
-template <int PD>
-__global__ void __launch_bounds__(W4S_THREADS, 1) wino4s_f32_kernel(WinoArgs a) {
-  __shared__ __attribute__((aligned(16))) float smem[2 * W4_UCH + 2 * W4_VCH];  // sU[2], sV[2]
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-
-  const int G = gridDim.x;
-  const int xcd = blockIdx.x & 7;
-  const int cb = xcd % a.ncb;
-  const int per_cb = G / a.ncb;
-  const int r = (blockIdx.x >> 3) * (8 / a.ncb) + xcd / a.ncb;
-  if (r >= a.ntb) return;
-  const int nunits = (a.ntb - r + per_cb - 1) / per_cb;
-  const int nsteps = nunits << a.nk_log2;
-  auto tile_pos = [&](int t, int& img, int& ty, int& tx) {
-    const int q = t / a.tiles_x;
-    tx = t - q * a.tiles_x;
-    img = q / a.tiles_y;
-    ty = q - img * a.tiles_y;
-  };
-
-  if (wave >= 8) {
-    // ------------------------------------------------------------------ producers
-    const int ptid = tid - 512;
-    const int grp = ptid >> 7;          // group 0: waves 8-9, group 1: waves 10-11
-    const int gw = (ptid >> 6) & 1;     // wave within the group
-    const int lt = (ptid & 127) >> 2, lc = ptid & 3;
-    float xr[36];
-    uint32_t ld_mlo = 0, ld_mhi = 0;
-    int ld_unit = -1, ld_o0 = 0;
-    auto load_window = [&](int s) {
-      const int unit = s >> a.nk_log2;
-      const int k = s & (a.nk - 1);
-      if (unit != ld_unit) {
-        ld_unit = unit;
-        const int t = (r + unit * per_cb) * W4_TILES + lt;
-        const bool tok = t < a.ntiles;
-        int img, ty, tx;
-        tile_pos(tok ? t : a.ntiles - 1, img, ty, tx);
-        const int y0 = 4 * ty - 1, x0 = 4 * tx - 1;
-        ld_o0 = ((img * a.H + y0) * a.W + x0) * a.C + lc;
-        ld_mlo = ld_mhi = 0;
-#pragma unroll
-        for (int i = 0; i < 36; ++i) {
-          const int y = y0 + i / 6, x = x0 + i % 6;
-          const uint32_t bit = (uint32_t)(tok && y >= 0 && y < a.H && x >= 0 && x < a.W);
-          if (i < 32)
-            ld_mlo |= bit << i;
-          else
-            ld_mhi |= bit << (i - 32);
-        }
-      }
-      const float* base = a.in + ld_o0 + k * W4_KC;
-#pragma unroll
-      for (int i = 0; i < 36; ++i) {
-        const uint32_t bit = i < 32 ? (ld_mlo >> i) & 1u : (ld_mhi >> (i - 32)) & 1u;
-        const float* src = bit ? base + ((i / 6) * a.W + (i % 6)) * a.C : &g_wino_zero[0];
-        xr[i] = *src;
-      }
-    };
-    auto bt6 = [](float d0, float d1, float d2, float d3, float d4, float d5, float* v) {
-      v[0] = 4.f * d0 - 5.f * d2 + d4;
-      v[1] = (d3 + d4) - 4.f * (d1 + d2);
-      v[2] = (d4 - d3) + 4.f * (d1 - d2);
-      v[3] = (d4 - d2) + 2.f * (d3 - d1);
-      v[4] = (d4 - d2) - 2.f * (d3 - d1);
-      v[5] = 4.f * d1 - 5.f * d3 + d5;
-    };
-    auto transform = [&](int buf) {  // B^T down the columns in registers, then along the rows to LDS
-#pragma unroll
-      for (int x = 0; x < 6; ++x) {
-        float v[6];
-        bt6(xr[x], xr[6 + x], xr[12 + x], xr[18 + x], xr[24 + x], xr[30 + x], v);
-#pragma unroll
-        for (int y = 0; y < 6; ++y) xr[6 * y + x] = v[y];
-      }
-      float* vb = smem + 2 * W4_UCH + buf * W4_VCH + lt * W4_KC + lc;
-#pragma unroll
-      for (int y = 0; y < 6; ++y) {
-        float v[6];
-        bt6(xr[6 * y], xr[6 * y + 1], xr[6 * y + 2], xr[6 * y + 3], xr[6 * y + 4], xr[6 * y + 5], v);
-#pragma unroll
-        for (int x = 0; x < 6; ++x) vb[(6 * y + x) * (W4_TILES * W4_KC)] = v[x];
-      }
-    };
-    auto load_u = [&](int s) {  // the group's two waves: 18 lane-linear 1-KiB LDS-DMA pieces each
-      const int k = s & (a.nk - 1);
-      const float* ug = a.u + ((size_t)cb * a.nk + k) * W4_UCH + gw * 4608 + lane * 4;
-      float* ul = smem + (s & 1) * W4_UCH + gw * 4608;
-#pragma unroll
-      for (int j = 0; j < 18; ++j) glds16(ug + 256 * j, ul + 256 * j);
-    };
-    // prologue (before the barrier publishing chunk 0): group 0 stages chunk 0 (U, then the
-    // windows, transformed), group 1 issues the window loads of chunk 1
-    if (grp == 0) {
-      load_u(0);
-      load_window(0);
-      transform(0);
-      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else if (nsteps > 1) {
-      load_window(1);
-    }
-    lds_barrier();
-    for (int c = 0; c + 1 < nsteps; ++c) {
-      if (grp == ((c + 1) & 1)) {
-        transform((c + 1) & 1);  // the windows of chunk c + 1 (hipcc waits for them at first use)
-      } else {
-        load_u(c + 1);
-        if (c + 2 < nsteps) {
-          load_window(c + 2);
-          asm volatile("s_waitcnt vmcnt(36)" ::: "memory");  // U landed; the 36 window loads stay in flight
-        } else {
-          asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        }
-      }
-      lds_barrier();
-    }
-    return;
-  }
-
-  // -------------------------------------------------------------------- consumers
-  const int cq = wave & 3, tg = wave >> 2;
-  const int li = lane & 15, lq = lane >> 4;
-  f32x4 acc[36];
-#pragma unroll
-  for (int p = 0; p < 36; ++p) acc[p] = f32x4{};
-  lds_barrier();
-  int c = 0;
-  for (int unit = 0; unit < nunits; ++unit) {
-    for (int k = 0; k < a.nk; ++k, ++c) {
-      const int buf = c & 1;
-      const float* Ub = smem + buf * W4_UCH + cq * 64 + li * 4 + lq;
-      const float* Vb = smem + 2 * W4_UCH + buf * W4_VCH + tg * 64 + li * 4 + lq;
-      float ar[PD], br[PD];
-#pragma unroll
-      for (int j = 0; j < PD; ++j) {
-        ar[j] = Ub[j * (W4_COUT * W4_KC)];
-        br[j] = Vb[j * (W4_TILES * W4_KC)];
-      }
-#pragma unroll
-      for (int p = 0; p < 36; ++p) {
-        const float av = ar[p % PD], bv = br[p % PD];
-        if (p + PD < 36) {
-          ar[p % PD] = Ub[(p + PD) * (W4_COUT * W4_KC)];
-          br[p % PD] = Vb[(p + PD) * (W4_TILES * W4_KC)];
-        }
-        acc[p] = __builtin_amdgcn_mfma_f32_16x16x4f32(av, bv, acc[p], 0, 0, 0);
-      }
-      // the barrier that publishes chunk c + 1 (the unit's epilogue below then runs while the
-      // producers stage chunk c + 2)
-      if (c + 1 < nsteps) lds_barrier();
-    }
-    // Y = A^T M A (+ bias, + residual, ReLU) with the formulas of wino4_f32_kernel: lane (li, lq)
-    // holds channels 4 lq .. + 3 of its tile in each accumulator; the column pass runs in place in
-    // the accumulators, one channel at a time, so that few temporaries are live beside them
-    const int co0 = cb * W4_COUT + cq * 16 + 4 * lq;
-    const float4 b4f = *reinterpret_cast<const float4*>(a.bias + co0);
-    const f32x4 b4 = {b4f.x, b4f.y, b4f.z, b4f.w};
-    const int t_out = (r + unit * per_cb) * W4_TILES + tg * 16 + li;
-    const bool t_ok = t_out < a.ntiles;
-    int oimg, oty, otx;
-    tile_pos(t_ok ? t_out : a.ntiles - 1, oimg, oty, otx);
-#pragma unroll
-    for (int x = 0; x < 6; ++x) {  // (A^T M)[i][x] -> acc[6 i + x], i = 0..3
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float m0 = acc[x][e], m1 = acc[6 + x][e], m2 = acc[12 + x][e], m3 = acc[18 + x][e],
-                    m4 = acc[24 + x][e], m5 = acc[30 + x][e];
-        const float s12 = m1 + m2, d12 = m1 - m2, s34 = m3 + m4, d34 = m3 - m4;
-        acc[x][e] = m0 + s12 + s34;
-        acc[6 + x][e] = d12 + 2.f * d34;
-        acc[12 + x][e] = s12 + 4.f * s34;
-        acc[18 + x][e] = d12 + 8.f * d34 + m5;
-      }
-    }
-#pragma unroll
-    for (int i = 0; i < 4; ++i) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        f32x4 o;
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const float t0 = acc[6 * i][e], t1 = acc[6 * i + 1][e], t2 = acc[6 * i + 2][e], t3 = acc[6 * i + 3][e],
-                      t4 = acc[6 * i + 4][e], t5 = acc[6 * i + 5][e];
-          const float s12 = t1 + t2, d12 = t1 - t2, s34 = t3 + t4, d34 = t3 - t4;
-          o[e] = (q == 0 ? t0 + s12 + s34 : q == 1 ? d12 + 2.f * d34 : q == 2 ? s12 + 4.f * s34 : d12 + 8.f * d34 + t5) + b4[e];
-        }
-        const int yy = 4 * oty + i, xx = 4 * otx + q;
-        const bool ok = t_ok && yy < a.H && xx < a.W;
-        const int off = ok ? ((oimg * a.H + yy) * a.W + xx) * a.C + co0 : 0;
-        if (a.res) {
-          const float4 rv = *reinterpret_cast<const float4*>(a.res + off);
-          o += (f32x4){rv.x, rv.y, rv.z, rv.w};
-        }
-        if (a.relu) {
-#pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = o[e] > 0.f ? o[e] : (o[e] != o[e] ? o[e] : 0.f);
-        }
-        if (ok) *reinterpret_cast<float4*>(a.out + off) = make_float4(o[0], o[1], o[2], o[3]);
-      }
-    }
-#pragma unroll
-    for (int p = 0; p < 36; ++p) acc[p] = f32x4{};
-  }
-}
-
 int device_cus() {
   int dev = 0, cus = 0;
   if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
@@ -946,17 +732,6 @@ extern "C" int rmbx_conv3x3_winograd4_f32(const float* in, const float* u_packed
   RMBX_CHECK_ARG(a.dbg == 0 || var == rmbx::W4_DEFAULT_VAR,
                  "rmbx_conv3x3_winograd4_f32: RMBX_WINO_DBG needs RMBX_WINO4_VAR=%d", rmbx::W4_DEFAULT_VAR);
 #define RMBX_W4_LAUNCH(D, V) hipLaunchKernelGGL((rmbx::wino4_f32_kernel<D, V>), g, blk, 0, st, a)
-  // producer / consumer form (RMBX_WINO4_SPEC=1)
-  const char* spec_env = std::getenv("RMBX_WINO4_SPEC");
-  if (spec_env && std::atoi(spec_env) != 0 && a.dbg == 0) {
-    const int pd = std::atoi(spec_env) == 2 ? 1 : 4;  // operand prefetch distance (positions)
-    if (pd == 4)
-      hipLaunchKernelGGL((rmbx::wino4s_f32_kernel<4>), g, dim3(rmbx::W4S_THREADS), 0, st, a);
-    else
-      hipLaunchKernelGGL((rmbx::wino4s_f32_kernel<1>), g, dim3(rmbx::W4S_THREADS), 0, st, a);
-    RMBX_CHECK_LAUNCH();
-    return RMBX_OK;
-  }
   if (a.dbg == 0) {
     switch (var) {
       case 0: RMBX_W4_LAUNCH(0, 0); break;

@@ -131,28 +131,3 @@ def test_winograd4_multi_unit_matches_device_conv(n, C, H, W):
     got = _run4(x, w, b, r, True)
     err = (got - ref).abs().max().item()
     assert err <= 2e-5 * max(1.0, ref.abs().max().item()), err
-
-
-@torch.no_grad()
-@pytest.mark.parametrize("n,C,H,W,res,relu", [(3, 64, 30, 41, True, True), (2, 128, 17, 23, False, True),
-                                              (40, 64, 24, 32, True, True), (2, 256, 9, 11, True, False)])
-def test_winograd4_producer_consumer_form_equals_default(monkeypatch, n, C, H, W, res, relu):
-    """RMBX_WINO4_SPEC=1 (four producer waves move U and transform the windows, eight consumer
-    waves only run the MFMAs and the epilogue): the default kernel's products in the same order, so
-    the same output; several units per block and ragged tiles included."""
-    from robomanipbaselines_amd import kernels as K
-
-    g = torch.Generator(device="cpu").manual_seed(C * 7 + H)
-    cl = torch.channels_last
-    x = torch.randn(n, C, H, W, generator=g).to(DEV).contiguous(memory_format=cl)
-    w = (torch.randn(C, C, 3, 3, generator=g) / (9 * C) ** 0.5).to(DEV)
-    b = torch.randn(C, generator=g).to(DEV)
-    r = torch.randn(n, C, H, W, generator=g).to(DEV).contiguous(memory_format=cl) if res else None
-    u = K.pack_winograd4_f32(w)
-    monkeypatch.setenv("RMBX_WINO4_SPEC", "0")
-    want = K.conv3x3_winograd4_f32(x, u, b, relu=relu, res=r)
-    for spec in ("1", "2"):
-        monkeypatch.setenv("RMBX_WINO4_SPEC", spec)
-        got = K.conv3x3_winograd4_f32(x, u, b, relu=relu, res=r)
-        torch.cuda.synchronize()
-        torch.testing.assert_close(got, want, rtol=1e-6, atol=1e-6)
