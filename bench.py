@@ -111,10 +111,14 @@ def winograd_kernel_launches(shape, tile):
 def winograd_pmc_traffic(tile):
     """HBM counter bytes per conv call at 1024 frames, per layer shape, from the committed PMC
     passes (scripts/gpurun/wino_pmc.sh + tools/pmc_traffic.py --winograd); ({}, None) if absent."""
-    path = os.path.join(ROOT, "profiles", "r3_pmc_winograd4_traffic.json" if tile == "f4"
-                        else "r2_pmc_winograd_traffic_v1.json")
-    if not os.path.exists(path):
+    import glob
+
+    pat = "r*_pmc_winograd4_traffic.json" if tile == "f4" else "r*_pmc_winograd_traffic_v*.json"
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", pat)),
+                   key=lambda f: int(os.path.basename(f)[1:].split("_")[0]))
+    if not files:
         return {}, None
+    path = files[-1]
     with open(path) as f:
         d = json.load(f)
     layers = d.get("layers", {})
@@ -172,18 +176,27 @@ def gemm_pmc_traffic():
     """HBM counter bytes per gemm_f32x6 launch (mean over one fp32 ACT inference at 1024 envs) from the
     committed PMC passes (scripts/gpurun/gemm_pmc.sh + tools/pmc_traffic.py --gemm); (None, None) if
     absent."""
-    path = os.path.join(ROOT, "profiles", "r3_pmc_gemm_f32x6_traffic.json")
-    if not os.path.exists(path):
+    import glob
+
+    from robomanipbaselines_amd import kernels as K
+
+    # the newest committed profile of the form in use (r<round>_pmc_gemm_<form>_traffic.json)
+    form = "f16x3" if K.F32_PIECES == "f16x3" else "f32x6"
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", f"r*_pmc_gemm_{form}_traffic.json")),
+                   key=lambda f: int(os.path.basename(f)[1:].split("_")[0]))
+    if not files:
         return None, None
+    path = files[-1]
     with open(path) as f:
         d = json.load(f)
     return d.get("traffic_bytes_per_launch"), os.path.relpath(path, ROOT)
 
 
 def gemm_probe(ro):
-    """One infer_policy call of `ro` with HIP events around every rmbx fp32-accurate bf16x6 GEMM
-    launch (rmbx_linear_f32x6 / _batched / rmbx_conv2d_f32x6, the dominant policy kernel): executed
-    bf16 MFMA rate (six bf16 products per f32 product) against the bf16 dense peak."""
+    """One infer_policy call of `ro` with HIP events around every rmbx fp32-accurate GEMM launch
+    (rmbx_linear_f16x3 / _batched / rmbx_conv2d_f16x3, or their bf16x6 counterparts under
+    RMBX_F32_PIECES=bf16x6: the dominant policy kernel): executed MFMA rate (three f16 or six bf16
+    products per f32 product, both at the bf16 rate) against the bf16 dense peak."""
     from robomanipbaselines_amd import kernels as K
 
     K.GEMM_PROBE = probe = []
@@ -194,29 +207,35 @@ def gemm_probe(ro):
         K.GEMM_PROBE = None
     if not probe:
         return None
-    ms = flops = nbytes = 0.0
+    ms = flops = nbytes = executed = 0.0
     shapes = {}
-    for name, fl, nb, e0, e1 in probe:
+    kinds = set()
+    for name, fl, nb, products, e0, e1 in probe:
         dt = e0.elapsed_time(e1)
         ms += dt
         flops += fl
         nbytes += nb
+        executed += products * fl
+        kinds.add(products)
         L = shapes.setdefault(name, {"launches": 0, "ms": 0.0, "flops": 0.0})
         L["launches"] += 1
         L["ms"] += dt
         L["flops"] += fl
-    eq = flops / ms / 1e9  # fp32-equivalent TFLOP/s
-    ex = 6 * eq            # executed bf16 MFMA TFLOP/s
+    eq = flops / ms / 1e9      # fp32-equivalent TFLOP/s
+    ex = executed / ms / 1e9   # executed MFMA TFLOP/s
     traffic, src = gemm_pmc_traffic()
     n = len(probe)
+    form = ("f16x3: each f32 operand split into two f16 pieces (the low one scaled by 2^11), three piece products "
+            "on v_mfma_f32_16x16x32_f16" if kinds == {3} else
+            "bf16x6: each f32 operand split into three bf16 pieces, six piece products on v_mfma_f32_16x16x32_bf16"
+            if kinds == {6} else "mixed f16x3 / bf16x6")
     return {"bound": "mfma", "achieved": round(ex, 2), "peak": MFMA_PEAK_TFLOPS["bf16"], "unit": "TFLOP/s",
             "frac": ex / MFMA_PEAK_TFLOPS["bf16"], "traffic": None if traffic is None else round(traffic),
             "traffic_unit": "HBM bytes per launch, mean over the launches of one fp32 ACT inference at 1024 envs",
             "traffic_source": src,
             "algorithmic_bytes_per_launch": round(nbytes / len(probe)),
-            "kernel": "rmbx::gemm_f32x6_kernel (fp32-accurate GEMM / implicit-GEMM conv on v_mfma_f32_16x16x32_bf16: "
-                      "each f32 operand split into three bf16 pieces, six piece products, f32 accumulation)",
-            "flops": "executed bf16 MFMA FLOPs = 6 x the f32 problem's 2*M*N*K",
+            "kernel": f"rmbx::gemm_f32x6_kernel (fp32-accurate GEMM / implicit-GEMM conv, {form}, f32 accumulation)",
+            "flops": "executed MFMA FLOPs = products x the f32 problem's 2*M*N*K (3 for f16x3, 6 for bf16x6)",
             "achieved_fp32_equivalent": round(eq, 2), "f32_mfma_peak": MFMA_PEAK_TFLOPS["fp32"],
             "launches_per_inference": n, "avg_launch_us": round(1e3 * ms / n, 1),
             "ms_per_inference": round(ms, 3),

@@ -453,6 +453,26 @@ int rmbx_conv2d_direct_f32(const float* in, int N, int H, int W, int C, const fl
 /* planes[p * n + i] = bf16 piece p of x[i], x = x0 + x1 + x2 exactly (round-to-nearest-even at each
  * level): the weight form rmbx_linear_f32x6 reads. */
 int rmbx_split_bf16x3(const float* x, void* planes, long long n, void* stream);
+/* f16x3 form of the fp32-accurate GEMM (two f16 pieces per operand, three products on the f16
+ * matrix cores at the bf16 rate: half the MFMA work of bf16x6, error measured below hipBLASLt's f32
+ * GEMM against an f64 product).  rmbx_split_f16x2 packs an f32 weight w [N][K] (contiguous) as
+ * planes [2][N][K] f16 bits, hi = f16(w[n] s_n) and lo = f16((w[n] s_n - hi) 2^11), with s_n a power
+ * of two putting the row's max |w| in [2^13, 2^14), and scale[n] = 1 / s_n.  rmbx_linear_f16x3,
+ * rmbx_linear_f16x3_batched and rmbx_conv2d_f16x3 take the arguments of their f32x6 counterparts
+ * plus that scale (w_scale [N], 16-byte aligned for the vector epilogue; batched: item b reads
+ * w_scale + b * ws_bs); the activations are split in registers, a block whose |a| max lies outside
+ * [2^-6, 2^15] re-runs its tile on a power-of-two-scaled copy (f16's range, handled exactly). */
+int rmbx_split_f16x2(const float* w, int N, int K, void* planes, float* scale, void* stream);
+int rmbx_linear_f16x3(const float* a, long long lda, const void* w_planes, long long ldw, long long w_plane_stride,
+                      const float* w_scale, const float* bias, float* c, long long ldc, int M, int N, int K, int relu,
+                      void* stream);
+int rmbx_linear_f16x3_batched(const float* a, long long lda, long long a_bs, const void* w_planes, long long ldw,
+                              long long w_plane_stride, long long w_bs, const float* w_scale, long long ws_bs,
+                              const float* bias, float* c, long long ldc, long long c_bs, int batch, int M, int N,
+                              int K, int relu, void* stream);
+int rmbx_conv2d_f16x3(const float* in, int N, int H, int W, int C, const void* w_planes, const float* w_scale,
+                      const float* bias, const float* res, float* out, int Cout, int KH, int KW, int stride, int pad,
+                      int relu, void* stream);
 /* rmbx_attention_f32 with fp32-accurate products on the bf16 matrix cores: Q, K, V and the softmax
  * probabilities split into three bf16 pieces, six piece products per product accumulated in f32 (the
  * rmbx_linear_f32x6 scheme); same layouts, strides and output as rmbx_attention_f32. */

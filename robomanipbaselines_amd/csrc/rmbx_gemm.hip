@@ -29,27 +29,57 @@
 // XOR-swizzled by (row >> 2) & 2 so the fragment reads, the DMA pieces and the A stores are all
 // LDS-bank-conflict-free.  Blocks are mapped XCD-contiguously and in groups of 8 row tiles x all
 // column tiles, so the A rows and W columns an XCD streams stay in its L2.
+//
+// f16x3 form (PC = 2, rmbx_linear_f16x3 / _batched / rmbx_conv2d_f16x3): the same kernel with two
+// f16 pieces per operand (11 significant bits each) and three products on
+// v_mfma_f32_16x16x32_f16 (the bf16 rate):
+//
+//   x = hi + 2^-11 lo,  hi = f16(x), lo = f16((x - hi) 2^11)      (|x - hi - 2^-11 lo| <= 2^-22 |x|)
+//   a.b ~ hi_a hi_b + 2^-11 (hi_a lo_b + lo_a hi_b)                 (dropped term <= 2^-22 |ab|)
+//
+// (the split of Ootomo & Yokota, IJHPCA 2022: the low piece is carried scaled by 2^11 so it stays
+// in f16's normal range, and the two product groups accumulate in separate f32 accumulators,
+// joined as acc + 2^-11 cor in the epilogue).  Each piece product is exact in f32 (11 x 11 bits),
+// so the error is the f32 accumulation plus <= ~3 * 2^-22 relative per term: measured below
+// hipBLASLt's f32 GEMM against an f64 product at every tested shape (tests/test_gemm_gpu.py).
+// Three products instead of six: half the MFMA work of bf16x6.  f16's exponent range is the
+// price, handled exactly: W rows are scaled by a power of two at packing (rmbx_split_f16x2: row
+// max in [2^13, 2^14), the inverse applied per output column in the epilogue), and every block
+// tracks the largest |a| it split; a block whose tile max lies outside [2^-6, 2^15] (values that
+// would overflow f16 or sit in its subnormal range) runs its K loop again on a * 2^s with s
+// putting the max in [2^13, 2^14), and scales its result back by 2^-s (powers of two: exact).
 #include "rmbx_common.h"
 
 #include <cstdint>
 #include <cstdlib>
+#include <type_traits>
 
 namespace rmbx {
 namespace {
 
 typedef short bf16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x4v __attribute__((ext_vector_type(4)));
 typedef __bf16 bf16x2v __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x2v __attribute__((ext_vector_type(2)));
 typedef float f32x2v __attribute__((ext_vector_type(2)));
 
 constexpr int GM_BM = 256, GM_BN = 128, GM_BK = 32;
 constexpr int GM_THREADS = 512;
-constexpr int GM_A_PLANE = GM_BM * GM_BK * 2;            // 16 KiB per bf16 piece plane
+constexpr int GM_A_PLANE = GM_BM * GM_BK * 2;            // 16 KiB per 16-bit piece plane
 constexpr int GM_B_PLANE = GM_BN * GM_BK * 2;            // 8 KiB
-constexpr int GM_A_BYTES = 3 * GM_A_PLANE;               // 48 KiB
-constexpr int GM_STAGE = GM_A_BYTES + 3 * GM_B_PLANE;    // 72 KiB
 constexpr int GM_GROUP = 8;                              // row tiles per block group
-static_assert(2 * GM_STAGE <= 160 * 1024, "two K stages must fit the LDS of a CU");
+constexpr int GM_EPI_PITCH = 68;                         // LDS epilogue row pitch (floats)
+constexpr int GM_EPI_BYTES = 8 * 64 * GM_EPI_PITCH * 4;  // 136 KiB: eight 64 x 64 wave tiles
+// PC pieces per operand (3: bf16x6, 2: f16x3): one K stage = PC A planes + PC W planes
+template <int PC>
+constexpr int gm_stage() { return PC * (GM_A_PLANE + GM_B_PLANE); }  // 72 / 48 KiB
+// two stages, at least the epilogue tile; f16x3 adds 64 B for the block max of |a|
+template <int PC>
+constexpr int gm_smem() {
+  return (2 * gm_stage<PC>() > GM_EPI_BYTES ? 2 * gm_stage<PC>() : GM_EPI_BYTES) + (PC == 2 ? 64 : 0);
+}
+static_assert(gm_smem<3>() <= 160 * 1024 && gm_smem<2>() <= 160 * 1024, "the LDS of a CU");
 
 struct GemmArgs {
   const float* A;      // [M][lda]
@@ -66,6 +96,9 @@ struct GemmArgs {
   // batched GEMM (rmbx_linear_f32x6_batched): batch item b uses A + b a_bs, W + b w_bs, C + b c_bs
   int batch;
   long long a_bs, w_bs, c_bs;
+  // f16x3: per-output-column power-of-two weight scales [N] (item b: ws + b ws_bs)
+  const float* ws;
+  long long ws_bs;
 };
 
 __device__ __forceinline__ uint32_t pk_bf16(float x, float y) {
@@ -80,6 +113,19 @@ __device__ __forceinline__ void split_pair(float x, float y, uint32_t& p0, uint3
   p1 = pk_bf16(rx, ry);
   const float sx = rx - __uint_as_float(p1 << 16), sy = ry - __uint_as_float(p1 & 0xffff0000u);
   p2 = pk_bf16(sx, sy);
+}
+
+__device__ __forceinline__ uint32_t pk_f16(float x, float y) {
+  f32x2v v = {x, y};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, f16x2v));  // RNE
+}
+
+// (x, y) -> packed f16 pairs hi = f16(x), lo = f16((x - hi) 2^11): x = hi + 2^-11 lo to 2^-22 |x|
+// for 2^-14 <= |x| <= 65504
+__device__ __forceinline__ void split_f16_pair(float x, float y, uint32_t& h, uint32_t& l) {
+  h = pk_f16(x, y);
+  const f16x2v hv = __builtin_bit_cast(f16x2v, h);
+  l = pk_f16((x - (float)hv[0]) * 2048.f, (y - (float)hv[1]) * 2048.f);
 }
 
 // LDS-DMA of 16 bytes per lane: the wave's 64 x 16 B land contiguously at the wave-uniform LDS
@@ -108,13 +154,14 @@ __device__ __forceinline__ void wait_vm() {
 // waves 0-3) split + store the next A tile before their first MFMA half-step instead of between
 // the halves (measured 3-7 % slower; so were a persistent one-block-per-CU form with the K pipeline
 // running across tiles and a 128 x 256 tile, profiles/r4_gemm_forms_ab.log)
-template <bool CONV, int VAR = 0>
+template <bool CONV, int VAR = 0, int PC = 3>
 __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
+  static_assert(PC == 3 || PC == 2, "bf16x6 (3 pieces) or f16x3 (2 pieces)");
   constexpr int GROUP = ((VAR >> 1) & 3) == 1 ? 4 : ((VAR >> 1) & 3) == 2 ? 16 : GM_GROUP;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[2 * GM_STAGE];
+  constexpr int STAGE = gm_stage<PC>(), A_BYTES = PC * GM_A_PLANE;
+  __shared__ __attribute__((aligned(16))) unsigned char smem[gm_smem<PC>()];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 3, wn = wave >> 2;
-  const int lr = lane & 31, lh = lane >> 5;
 
   // block -> tile: XCD-contiguous ranges (blocks bid, bid + 8, ... run on one XCD), then groups of
   // GM_GROUP row tiles x all column tiles, row tile fastest
@@ -128,6 +175,7 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
     g.A += item * g.a_bs;
     g.W += item * g.w_bs;
     g.C += item * g.c_bs;
+    if (g.ws) g.ws += item * g.ws_bs;
   }
   const int per_group = GROUP * g.tiles_n;
   const int first_m = (lin / per_group) * GROUP;
@@ -140,26 +188,26 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
   // logical ^ ((row >> 2) & 2): conflict-free for the 16x16x32 fragment reads (lane l reads row
   // l%16, slot l/16), the LDS-DMA pieces and the A stores below.
   // A staging (registers): thread -> rows tid/4 and tid/4 + 128, k quarter tid%4 (8 f32 = 32 B
-  // each); the three pieces go to the three LDS planes [256 rows][32 k].  Rows past M re-read
-  // row M-1 (their outputs are not stored).
+  // each); the pieces go to the PC LDS planes [256 rows][32 k].  Rows past M re-read row M-1
+  // (their outputs are not stored).
   const int aq = tid & 3, arow = tid >> 2;
   const float* ag0 = g.A + (long long)min(m0 + arow, g.M - 1) * g.lda + 8 * aq;
   const float* ag1 = g.A + (long long)min(m0 + arow + 128, g.M - 1) * g.lda + 8 * aq;
   const int aoff0 = arow * 64 + ((aq ^ ((arow >> 2) & 2)) << 4);
   const int aoff1 = (arow + 128) * 64 + ((aq ^ (((arow + 128) >> 2) & 2)) << 4);
-  // W: LDS-DMA of 24 pieces (8 per plane) of 16 rows x 64 B, wave w copies pieces 3w..3w+2
-  const uint16_t* bsrc[3];
+  // W: LDS-DMA of 8 PC pieces (8 per plane) of 16 rows x 64 B, wave w copies pieces PC w..PC w+PC-1
+  const uint16_t* bsrc[PC];
 #pragma unroll
-  for (int t = 0; t < 3; ++t) {
-    const int i = wave * 3 + t, p = i >> 3;
+  for (int t = 0; t < PC; ++t) {
+    const int i = wave * PC + t, p = i >> 3;
     const int row = (i & 7) * 16 + (lane >> 2);
     const int sl = (lane & 3) ^ ((row >> 2) & 2);
     bsrc[t] = g.W + p * g.wps + (long long)(n0 + row) * g.ldw + sl * 8;
   }
   auto stage_b = [&](int kt, int buf) {
-    unsigned char* base = smem + buf * GM_STAGE + GM_A_BYTES;
+    unsigned char* base = smem + buf * STAGE + A_BYTES;
 #pragma unroll
-    for (int t = 0; t < 3; ++t) glds16(bsrc[t] + kt * GM_BK, base + (wave * 3 + t) * 1024);
+    for (int t = 0; t < PC; ++t) glds16(bsrc[t] + kt * GM_BK, base + (wave * PC + t) * 1024);
   };
   // convolution: each staged row's window origin (iy0, ix0) and its element offset in the input;
   // a K step of 32 lies inside one filter tap (C % 32 == 0), so a row's 8 channels are one
@@ -205,78 +253,120 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
       return ok;
     }
   };
-  auto store_a = [&](const float4 (&Rin)[4], int ok, int buf) {
+  // f16x3: the largest |a| this thread split (pass 0) and the pass-1 scale of a
+  float amax = 0.f, ascale = 1.f;
+  auto store_a = [&](const float4 (&Rin)[4], int ok, int buf, auto scaled) {
     float4 R[4] = {Rin[0], Rin[1], Rin[2], Rin[3]};
     if constexpr (CONV) {
       const float4 z = make_float4(0.f, 0.f, 0.f, 0.f);
       if (!(ok & 1)) R[0] = R[1] = z;
       if (!(ok & 2)) R[2] = R[3] = z;
     }
-    uint32_t p0[8], p1[8], p2[8];
+    unsigned char* base = smem + buf * STAGE;
+    if constexpr (PC == 2) {
+      uint32_t h[8], l[8];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      if constexpr ((VAR & 32) != 0) {  // phase skip: truncated bf16 pieces (realistic values, no split VALU)
-        p0[2 * i] = __builtin_amdgcn_perm(__float_as_uint(R[i].y), __float_as_uint(R[i].x), 0x07060302u);
-        p0[2 * i + 1] = __builtin_amdgcn_perm(__float_as_uint(R[i].w), __float_as_uint(R[i].z), 0x07060302u);
-        p1[2 * i] = p0[2 * i + 1];
-        p1[2 * i + 1] = p0[2 * i];
-        p2[2 * i] = p0[2 * i];
-        p2[2 * i + 1] = p0[2 * i + 1];
-      } else {
-        split_pair(R[i].x, R[i].y, p0[2 * i], p1[2 * i], p2[2 * i]);
-        split_pair(R[i].z, R[i].w, p0[2 * i + 1], p1[2 * i + 1], p2[2 * i + 1]);
+      for (int i = 0; i < 4; ++i) {
+        if constexpr (decltype(scaled)::value) {
+          R[i].x *= ascale;
+          R[i].y *= ascale;
+          R[i].z *= ascale;
+          R[i].w *= ascale;
+        } else {
+          amax = fmaxf(amax, fmaxf(fabsf(R[i].x), fabsf(R[i].y)));
+          amax = fmaxf(amax, fmaxf(fabsf(R[i].z), fabsf(R[i].w)));
+        }
+        split_f16_pair(R[i].x, R[i].y, h[2 * i], l[2 * i]);
+        split_f16_pair(R[i].z, R[i].w, h[2 * i + 1], l[2 * i + 1]);
       }
+      *(uint4*)(base + aoff0) = make_uint4(h[0], h[1], h[2], h[3]);
+      *(uint4*)(base + GM_A_PLANE + aoff0) = make_uint4(l[0], l[1], l[2], l[3]);
+      *(uint4*)(base + aoff1) = make_uint4(h[4], h[5], h[6], h[7]);
+      *(uint4*)(base + GM_A_PLANE + aoff1) = make_uint4(l[4], l[5], l[6], l[7]);
+    } else {
+      uint32_t p0[8], p1[8], p2[8];
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        if constexpr ((VAR & 32) != 0) {  // phase skip: truncated bf16 pieces (realistic values, no split VALU)
+          p0[2 * i] = __builtin_amdgcn_perm(__float_as_uint(R[i].y), __float_as_uint(R[i].x), 0x07060302u);
+          p0[2 * i + 1] = __builtin_amdgcn_perm(__float_as_uint(R[i].w), __float_as_uint(R[i].z), 0x07060302u);
+          p1[2 * i] = p0[2 * i + 1];
+          p1[2 * i + 1] = p0[2 * i];
+          p2[2 * i] = p0[2 * i];
+          p2[2 * i + 1] = p0[2 * i + 1];
+        } else {
+          split_pair(R[i].x, R[i].y, p0[2 * i], p1[2 * i], p2[2 * i]);
+          split_pair(R[i].z, R[i].w, p0[2 * i + 1], p1[2 * i + 1], p2[2 * i + 1]);
+        }
+      }
+      *(uint4*)(base + aoff0) = make_uint4(p0[0], p0[1], p0[2], p0[3]);
+      *(uint4*)(base + GM_A_PLANE + aoff0) = make_uint4(p1[0], p1[1], p1[2], p1[3]);
+      *(uint4*)(base + 2 * GM_A_PLANE + aoff0) = make_uint4(p2[0], p2[1], p2[2], p2[3]);
+      *(uint4*)(base + aoff1) = make_uint4(p0[4], p0[5], p0[6], p0[7]);
+      *(uint4*)(base + GM_A_PLANE + aoff1) = make_uint4(p1[4], p1[5], p1[6], p1[7]);
+      *(uint4*)(base + 2 * GM_A_PLANE + aoff1) = make_uint4(p2[4], p2[5], p2[6], p2[7]);
     }
-    unsigned char* base = smem + buf * GM_STAGE;
-    *(uint4*)(base + aoff0) = make_uint4(p0[0], p0[1], p0[2], p0[3]);
-    *(uint4*)(base + GM_A_PLANE + aoff0) = make_uint4(p1[0], p1[1], p1[2], p1[3]);
-    *(uint4*)(base + 2 * GM_A_PLANE + aoff0) = make_uint4(p2[0], p2[1], p2[2], p2[3]);
-    *(uint4*)(base + aoff1) = make_uint4(p0[4], p0[5], p0[6], p0[7]);
-    *(uint4*)(base + GM_A_PLANE + aoff1) = make_uint4(p1[4], p1[5], p1[6], p1[7]);
-    *(uint4*)(base + 2 * GM_A_PLANE + aoff1) = make_uint4(p2[4], p2[5], p2[6], p2[7]);
   };
 
-  // wave (wm, wn) owns rows 64 wm.., columns 64 wn..: 4 x 4 accumulators of 16 x 16
-  f32x4v acc[4][4];
+  // wave (wm, wn) owns rows 64 wm.., columns 64 wn..: 4 x 4 accumulators of 16 x 16 (f16x3: a
+  // second set for the 2^-11-scaled cross products)
+  f32x4v acc[4][4], cor[4][4];
+  auto zero_acc = [&]() {
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+    for (int i = 0; i < 4; ++i)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4v){0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < 4; ++j) {
+        acc[i][j] = (f32x4v){0.f, 0.f, 0.f, 0.f};
+        if constexpr (PC == 2) cor[i][j] = (f32x4v){0.f, 0.f, 0.f, 0.f};
+      }
+  };
+  zero_acc();
 
   // 16x16x32 fragments: lane l holds X_p[row l%16][k = 8 (l/16) + j], j = 0..7 (one 16-B slot)
   const int fr = lane & 15, fs = lane >> 4;
   auto frag_off = [&](int row) { return row * 64 + ((fs ^ ((row >> 2) & 2)) << 4); };
-  // half h of a K step: m-tiles 2h, 2h+1 against all four n-tiles (48 MFMAs, small terms first)
-  auto half_step = [&](int buf, int h, const bf16x8 (&b)[4][3]) {
-    const unsigned char* As = smem + buf * GM_STAGE;
-    bf16x8 a[2][3];
+  // half h of a K step: m-tiles 2h, 2h+1 against all four n-tiles (bf16x6: 48 MFMAs, small
+  // terms first; f16x3: 24)
+  auto half_step = [&](int buf, int h, const bf16x8 (&b)[4][PC]) {
+    const unsigned char* As = smem + buf * STAGE;
+    bf16x8 a[2][PC];
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int off = frag_off(wm * 64 + (2 * h + i) * 16 + fr);
 #pragma unroll
-      for (int p = 0; p < 3; ++p) a[i][p] = *(const bf16x8*)(As + p * GM_A_PLANE + off);
+      for (int p = 0; p < PC; ++p) a[i][p] = *(const bf16x8*)(As + p * GM_A_PLANE + off);
     }
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int nj = 0; nj < 4; ++nj) {
-        f32x4v c = acc[2 * h + i][nj];
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][2], b[nj][0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[nj][1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[nj][2], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[nj][0], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[nj][1], c, 0, 0, 0);
-        c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[nj][0], c, 0, 0, 0);
-        acc[2 * h + i][nj] = c;
+        if constexpr (PC == 2) {
+          const f16x8 ah = __builtin_bit_cast(f16x8, a[i][0]), al = __builtin_bit_cast(f16x8, a[i][1]);
+          const f16x8 bh = __builtin_bit_cast(f16x8, b[nj][0]), bl = __builtin_bit_cast(f16x8, b[nj][1]);
+          f32x4v c = cor[2 * h + i][nj];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, c, 0, 0, 0);
+          cor[2 * h + i][nj] = c;
+          acc[2 * h + i][nj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, acc[2 * h + i][nj], 0, 0, 0);
+        } else {
+          f32x4v c = acc[2 * h + i][nj];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][2], b[nj][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[nj][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[nj][2], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][1], b[nj][0], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[nj][1], c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][0], b[nj][0], c, 0, 0, 0);
+          acc[2 * h + i][nj] = c;
+        }
       }
   };
-  auto read_b = [&](bf16x8 (&b)[4][3], int buf) {
-    const unsigned char* Bs = smem + buf * GM_STAGE + GM_A_BYTES;
+  auto read_b = [&](bf16x8 (&b)[4][PC], int buf) {
+    const unsigned char* Bs = smem + buf * STAGE + A_BYTES;
 #pragma unroll
     for (int nj = 0; nj < 4; ++nj) {
       const int off = frag_off(wn * 64 + nj * 16 + fr);
 #pragma unroll
-      for (int p = 0; p < 3; ++p) b[nj][p] = *(const bf16x8*)(Bs + p * GM_B_PLANE + off);
+      for (int p = 0; p < PC; ++p) b[nj][p] = *(const bf16x8*)(Bs + p * GM_B_PLANE + off);
     }
   };
 
@@ -287,39 +377,73 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
   // stay in flight) retires the W DMA; hipcc's own wait before the split (for A of kt + 1) is at
   // least as strict.
   const int KT = g.K / GM_BK;
-  float4 Ra[4], Rb[4];
-  int oka, okb;
-  oka = load_a(Ra, 0);
-  stage_b(0, 0);
-  okb = load_a(Rb, min(1, KT - 1));
-  store_a(Ra, oka, 0);
-  wait_vm<4>();
-  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-  auto step = [&](int kt, float4 (&Rcur)[4], int& okcur, float4 (&Rnext)[4], int& oknext) {
-    const int buf = kt & 1;
-    const bool more = kt + 1 < KT;
-    if (more) stage_b(kt + 1, buf ^ 1);
-    oknext = load_a(Rnext, min(kt + 2, KT - 1));  // unconditional (a redundant reload at the end) so that
-                                         // hipcc's wait before the split stays counted
-    bf16x8 b[4][3];
-    read_b(b, buf);
-    const bool late = (VAR & 64) == 0 || wave < 4;
-    if (more && !late) store_a(Rcur, okcur, buf ^ 1);
-    if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(1);
-    half_step(buf, 0, b);
-    if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(0);
-    if (more && late) store_a(Rcur, okcur, buf ^ 1);
-    if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(1);
-    half_step(buf, 1, b);
-    if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(0);
-    if (more) {
-      wait_vm<4>();
-      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  auto k_loop = [&](auto scaled) {
+    float4 Ra[4], Rb[4];
+    int oka, okb;
+    oka = load_a(Ra, 0);
+    stage_b(0, 0);
+    okb = load_a(Rb, min(1, KT - 1));
+    store_a(Ra, oka, 0, scaled);
+    wait_vm<4>();
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    auto step = [&](int kt, float4 (&Rcur)[4], int& okcur, float4 (&Rnext)[4], int& oknext) {
+      const int buf = kt & 1;
+      const bool more = kt + 1 < KT;
+      if (more) stage_b(kt + 1, buf ^ 1);
+      oknext = load_a(Rnext, min(kt + 2, KT - 1));  // unconditional (a redundant reload at the end) so that
+                                                   // hipcc's wait before the split stays counted
+      bf16x8 b[4][PC];
+      read_b(b, buf);
+      const bool late = (VAR & 64) == 0 || wave < 4;
+      if (more && !late) store_a(Rcur, okcur, buf ^ 1, scaled);
+      if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(1);
+      half_step(buf, 0, b);
+      if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(0);
+      if (more && late) store_a(Rcur, okcur, buf ^ 1, scaled);
+      if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(1);
+      half_step(buf, 1, b);
+      if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(0);
+      if (more) {
+        wait_vm<4>();
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      }
+    };
+    for (int kt = 0; kt < KT; kt += 2) {
+      step(kt, Rb, okb, Ra, oka);
+      if (kt + 1 < KT) step(kt + 1, Ra, oka, Rb, okb);
     }
   };
-  for (int kt = 0; kt < KT; kt += 2) {
-    step(kt, Rb, okb, Ra, oka);
-    if (kt + 1 < KT) step(kt + 1, Ra, oka, Rb, okb);
+  k_loop(std::false_type{});
+
+  float post = 1.f;  // f16x3: 2^-s of a pass-1 block
+  if constexpr (PC == 2) {
+    // block max of |a| over the tile; outside [2^-6, 2^15] (f16 overflow / subnormal range) the
+    // block runs its K loop again on a * 2^s, max in [2^13, 2^14), and scales back by 2^-s.  A
+    // NaN never raises the max (fmaxf) and an infinite max is left to propagate as in f32.
+    float m = amax;
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+    float* red = reinterpret_cast<float*>(smem + gm_smem<PC>() - 64);
+    if (lane == 0) red[wave] = m;
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    float bm = red[0];
+#pragma unroll
+    for (int w = 1; w < 8; ++w) bm = fmaxf(bm, red[w]);
+    if ((bm > 32768.f || (bm > 0.f && bm < 0.015625f)) && bm <= 3.4e38f) {
+      int e;
+      frexpf(bm, &e);  // bm = f 2^e, f in [0.5, 1)
+      ascale = ldexpf(1.f, 14 - e);
+      post = ldexpf(1.f, e - 14);
+      zero_acc();
+      k_loop(std::true_type{});
+    }
+    // join the product groups: acc + 2^-11 cor, then undo the pass-1 scale (a power of two)
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) acc[i][j][e] = fmaf(cor[i][j][e], 0.00048828125f, acc[i][j][e]) * post;
   }
 
   if constexpr ((VAR & 16) != 0) {
@@ -328,7 +452,7 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
     // write 16 consecutive floats, rows 4 apart land on different banks), then reads it back as
     // float4 rows so every lane stores 16 contiguous bytes (16 stores per lane instead of 64)
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    constexpr int PITCH = 68;
+    constexpr int PITCH = GM_EPI_PITCH;
     float* T = reinterpret_cast<float*>(smem) + wave * (64 * PITCH);
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
@@ -341,12 +465,17 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
     const int n = n0 + wn * 64 + c4;
     float4 bn = make_float4(0.f, 0.f, 0.f, 0.f);
     if (g.bias) bn = *(const float4*)(g.bias + n);
+    float4 sn = make_float4(1.f, 1.f, 1.f, 1.f);
+    if constexpr (PC == 2) sn = *(const float4*)(g.ws + n);
 #pragma unroll
     for (int it = 0; it < 16; ++it) {
       const int r = it * 4 + (lane >> 4);
       const int m = m0 + wm * 64 + r;
       if (m < g.M) {
         float4 v = *(const float4*)(T + r * PITCH + c4);
+        if constexpr (PC == 2) {  // the weight row scales (powers of two: exact)
+          v.x *= sn.x; v.y *= sn.y; v.z *= sn.z; v.w *= sn.w;
+        }
         v.x += bn.x; v.y += bn.y; v.z += bn.z; v.w += bn.w;
         if (g.res) {
           const float4 rv = *(const float4*)(g.res + (long long)m * g.ldc + n);
@@ -365,6 +494,7 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
   for (int nj = 0; nj < 4; ++nj) {
     const int n = n0 + wn * 64 + nj * 16 + fr;
     const float bn = g.bias ? g.bias[n] : 0.f;
+    const float sn = PC == 2 ? g.ws[n] : 1.f;
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi) {
       const int mb = m0 + wm * 64 + mi * 16 + 4 * fs;
@@ -372,7 +502,9 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
       for (int e = 0; e < 4; ++e) {
         const int m = mb + e;
         if (!(VAR & 8) && m < g.M) {
-          float v = acc[mi][nj][e] + bn;
+          float v = acc[mi][nj][e];
+          if constexpr (PC == 2) v *= sn;
+          v += bn;
           if (g.res) v += g.res[(long long)m * g.ldc + n];
           if (g.relu) v = fmaxf(v, 0.f);
           g.C[(long long)m * g.ldc + n] = v;
@@ -393,28 +525,64 @@ __global__ void split_bf16x3_kernel(const float* __restrict__ x, uint16_t* __res
   }
 }
 
+// one block per weight row n: s = 2^(14 - e) with max_k |w[n][k]| = f 2^e (f in [0.5, 1)), so the
+// scaled row's max lies in [2^13, 2^14); planes [2][N][K] = f16 hi / lo pieces of w s, scale[n] =
+// 1 / s (an all-zero or non-finite row keeps s = 1)
+__global__ void __launch_bounds__(256) split_f16x2_kernel(const float* __restrict__ w, int K, long long plane,
+                                                          uint16_t* __restrict__ planes, float* __restrict__ scale) {
+  __shared__ float red[4];
+  const int n = blockIdx.x, tid = threadIdx.x;
+  const float* row = w + (long long)n * K;
+  float m = 0.f;
+  for (int k = tid; k < K; k += 256) m = fmaxf(m, fabsf(row[k]));
+#pragma unroll
+  for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
+  if ((tid & 63) == 0) red[tid >> 6] = m;
+  __syncthreads();
+  m = fmaxf(fmaxf(red[0], red[1]), fmaxf(red[2], red[3]));
+  int e = 14;
+  if (m > 0.f && m <= 3.4e38f) frexpf(m, &e);
+  const float s = ldexpf(1.f, 14 - e);
+  if (tid == 0) scale[n] = ldexpf(1.f, e - 14);
+  for (int k = tid; k < K; k += 256) {
+    uint32_t h, l;
+    split_f16_pair(row[k] * s, 0.f, h, l);
+    planes[(long long)n * K + k] = (uint16_t)(h & 0xffff);
+    planes[plane + (long long)n * K + k] = (uint16_t)(l & 0xffff);
+  }
+}
+
 // default: the LDS-transposed epilogue with 16-byte stores (VAR 16: 1.04-1.08x over 64 scalar
 // stores per lane, profiles/r3_gemm_var_sweep.log) whenever the output / residual / bias rows allow
-// 16-byte accesses; RMBX_GEMM_VAR overrides (profiling)
-template <bool CONV>
+// 16-byte accesses; RMBX_GEMM_VAR overrides the bf16x6 form (profiling)
+template <bool CONV, int PC>
 void launch_gemm(long long blocks, const GemmArgs& g, hipStream_t st) {
-  // (the environment is read per launch, so a test or a profile can compare the forms in one process)
-  const char* ve = getenv("RMBX_GEMM_VAR");
-  const int env_var = ve ? atoi(ve) : -1;
-  const bool vec_ok = g.ldc % 4 == 0 && ((uintptr_t)g.C | (uintptr_t)g.res | (uintptr_t)g.bias) % 16 == 0 &&
-                      (g.batch <= 1 || g.c_bs % 4 == 0);
-  int var = env_var >= 0 ? env_var : 16;
-  if (!vec_ok) var &= ~16;
-  switch (var) {
-    case 1: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 1>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
-    case 2: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 2>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
-    case 4: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 4>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
-    case 8: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 8>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
-    case 16: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 16>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
-    case 18: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 18>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
-    case 48: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 48>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
-    case 80: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 80>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
-    default: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 0>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g);
+  const bool vec_ok = g.ldc % 4 == 0 &&
+                      ((uintptr_t)g.C | (uintptr_t)g.res | (uintptr_t)g.bias | (uintptr_t)g.ws) % 16 == 0 &&
+                      (g.batch <= 1 || (g.c_bs % 4 == 0 && g.ws_bs % 4 == 0));
+  if constexpr (PC == 2) {
+    if (vec_ok)
+      hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 16, 2>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g);
+    else
+      hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 0, 2>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g);
+    return;
+  } else {
+    // (the environment is read per launch, so a test or a profile can compare the forms in one process)
+    const char* ve = getenv("RMBX_GEMM_VAR");
+    const int env_var = ve ? atoi(ve) : -1;
+    int var = env_var >= 0 ? env_var : 16;
+    if (!vec_ok) var &= ~16;
+    switch (var) {
+      case 1: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 1>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
+      case 2: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 2>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
+      case 4: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 4>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
+      case 8: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 8>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
+      case 16: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 16>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
+      case 18: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 18>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
+      case 48: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 48>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
+      case 80: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 80>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
+      default: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 0>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g);
+    }
   }
 }
 
@@ -431,73 +599,113 @@ extern "C" int rmbx_split_bf16x3(const float* x, void* planes, long long n, void
   return RMBX_OK;
 }
 
+namespace rmbx {
+namespace {
+// shared argument checks and launch of the linear / batched / conv entry points of both forms
+template <int PC>
+int linear_impl(const char* fn, const float* a, long long lda, long long a_bs, const void* w_planes, long long ldw,
+                long long wps, long long w_bs, const float* ws, long long ws_bs, const float* bias, float* c,
+                long long ldc, long long c_bs, int batch, int M, int N, int K, int relu, void* stream) {
+  RMBX_CHECK_ARG(a && w_planes && c && (PC == 3 || ws), "%s: null pointer", fn);
+  RMBX_CHECK_ARG(batch >= 1 && M >= 0 && N > 0 && K > 0, "%s: bad shape M=%d N=%d K=%d", fn, M, N, K);
+  RMBX_CHECK_ARG(N % GM_BN == 0, "%s: N=%d must be a multiple of %d", fn, N, GM_BN);
+  RMBX_CHECK_ARG(K % GM_BK == 0, "%s: K=%d must be a multiple of %d", fn, K, GM_BK);
+  RMBX_CHECK_ARG(lda >= K && lda % 4 == 0 && a_bs % 4 == 0 && ldc >= N && ldw >= K && ldw % 8 == 0 && wps % 8 == 0 &&
+                     w_bs % 8 == 0,
+                 "%s: bad strides lda=%lld ldc=%lld ldw=%lld wps=%lld", fn, lda, ldc, ldw, wps);
+  RMBX_CHECK_ARG(((uintptr_t)a | (uintptr_t)w_planes) % 16 == 0, "%s: operands must be 16-B aligned", fn);
+  if (M == 0) return RMBX_OK;
+  GemmArgs g{a, (const uint16_t*)w_planes, bias, c, lda, ldc, ldw, wps, M, N, K, relu ? 1 : 0,
+             (M + GM_BM - 1) / GM_BM, N / GM_BN, nullptr};
+  g.batch = batch;
+  g.a_bs = a_bs;
+  g.w_bs = w_bs;
+  g.c_bs = c_bs;
+  g.ws = ws;
+  g.ws_bs = ws_bs;
+  const long long blocks = (long long)g.tiles_m * g.tiles_n * batch;
+  RMBX_CHECK_ARG(blocks < (1ll << 31), "%s: too many tiles", fn);
+  launch_gemm<false, PC>(blocks, g, (hipStream_t)stream);
+  RMBX_CHECK_LAUNCH();
+  return RMBX_OK;
+}
+
+template <int PC>
+int conv_impl(const char* fn, const float* in, int N, int H, int W, int C, const void* w_planes, const float* ws,
+              const float* bias, const float* res, float* out, int Cout, int KH, int KW, int stride, int pad, int relu,
+              void* stream) {
+  RMBX_CHECK_ARG(in && w_planes && out && (PC == 3 || ws), "%s: null pointer", fn);
+  RMBX_CHECK_ARG(N >= 0 && H > 0 && W > 0 && KH > 0 && KW > 0 && stride > 0 && pad >= 0, "%s: bad geometry", fn);
+  RMBX_CHECK_ARG(C % GM_BK == 0, "%s: C=%d must be a multiple of %d", fn, C, GM_BK);
+  RMBX_CHECK_ARG(Cout % GM_BN == 0, "%s: Cout=%d must be a multiple of %d", fn, Cout, GM_BN);
+  RMBX_CHECK_ARG(((uintptr_t)in | (uintptr_t)w_planes) % 16 == 0, "%s: operands must be 16-B aligned", fn);
+  const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
+  RMBX_CHECK_ARG(Ho > 0 && Wo > 0, "%s: empty output", fn);
+  const long long M = (long long)N * Ho * Wo;
+  RMBX_CHECK_ARG(M < (1ll << 31) && (long long)N * H * W < (1ll << 31), "%s: too many pixels", fn);
+  if (M == 0) return RMBX_OK;
+  const int K = KH * KW * C;
+  GemmArgs g{in, (const uint16_t*)w_planes, bias, out, 0, Cout, K, (long long)Cout * K, (int)M, Cout, K,
+             relu ? 1 : 0, (int)((M + GM_BM - 1) / GM_BM), Cout / GM_BN, res, H, W, C, Ho, Wo, KW, stride, pad};
+  g.ws = ws;
+  const long long blocks = (long long)g.tiles_m * g.tiles_n;
+  RMBX_CHECK_ARG(blocks < (1ll << 31), "%s: too many tiles", fn);
+  launch_gemm<true, PC>(blocks, g, (hipStream_t)stream);
+  RMBX_CHECK_LAUNCH();
+  return RMBX_OK;
+}
+}  // namespace
+}  // namespace rmbx
+
 extern "C" int rmbx_linear_f32x6(const float* a, long long lda, const void* w_planes, long long ldw,
                                  long long w_plane_stride, const float* bias, float* c, long long ldc, int M, int N,
                                  int K, int relu, void* stream) {
-  RMBX_CHECK_ARG(a && w_planes && c, "rmbx_linear_f32x6: null pointer");
-  RMBX_CHECK_ARG(M >= 0 && N > 0 && K > 0, "rmbx_linear_f32x6: bad shape M=%d N=%d K=%d", M, N, K);
-  RMBX_CHECK_ARG(N % rmbx::GM_BN == 0, "rmbx_linear_f32x6: N=%d must be a multiple of %d", N, rmbx::GM_BN);
-  RMBX_CHECK_ARG(K % rmbx::GM_BK == 0, "rmbx_linear_f32x6: K=%d must be a multiple of %d", K, rmbx::GM_BK);
-  RMBX_CHECK_ARG(lda >= K && lda % 4 == 0 && ldc >= N && ldw >= K && ldw % 8 == 0 && w_plane_stride % 8 == 0,
-                 "rmbx_linear_f32x6: bad strides lda=%lld ldc=%lld ldw=%lld wps=%lld", lda, ldc, ldw, w_plane_stride);
-  RMBX_CHECK_ARG(((uintptr_t)a | (uintptr_t)w_planes) % 16 == 0, "rmbx_linear_f32x6: operands must be 16-B aligned");
-  if (M == 0) return RMBX_OK;
-  rmbx::GemmArgs g{a, (const uint16_t*)w_planes, bias, c, lda, ldc, ldw, w_plane_stride, M, N, K, relu ? 1 : 0,
-                   (M + rmbx::GM_BM - 1) / rmbx::GM_BM, N / rmbx::GM_BN, nullptr};
-  const long long blocks = (long long)g.tiles_m * g.tiles_n;
-  RMBX_CHECK_ARG(blocks < (1ll << 31), "rmbx_linear_f32x6: too many tiles");
-  rmbx::launch_gemm<false>(blocks, g, (hipStream_t)stream);
-  RMBX_CHECK_LAUNCH();
-  return RMBX_OK;
+  return rmbx::linear_impl<3>("rmbx_linear_f32x6", a, lda, 0, w_planes, ldw, w_plane_stride, 0, nullptr, 0, bias, c,
+                              ldc, 0, 1, M, N, K, relu, stream);
 }
 
 extern "C" int rmbx_linear_f32x6_batched(const float* a, long long lda, long long a_bs, const void* w_planes,
                                          long long ldw, long long w_plane_stride, long long w_bs, const float* bias,
                                          float* c, long long ldc, long long c_bs, int batch, int M, int N, int K,
                                          int relu, void* stream) {
-  RMBX_CHECK_ARG(a && w_planes && c, "rmbx_linear_f32x6_batched: null pointer");
-  RMBX_CHECK_ARG(batch >= 1 && M >= 0 && N > 0 && K > 0, "rmbx_linear_f32x6_batched: bad shape");
-  RMBX_CHECK_ARG(N % rmbx::GM_BN == 0 && K % rmbx::GM_BK == 0, "rmbx_linear_f32x6_batched: N=%d / K=%d not multiples of %d / %d",
-                 N, K, rmbx::GM_BN, rmbx::GM_BK);
-  RMBX_CHECK_ARG(lda >= K && lda % 4 == 0 && a_bs % 4 == 0 && ldc >= N && ldw >= K && ldw % 8 == 0 &&
-                     w_plane_stride % 8 == 0 && w_bs % 8 == 0,
-                 "rmbx_linear_f32x6_batched: bad strides");
-  RMBX_CHECK_ARG(((uintptr_t)a | (uintptr_t)w_planes) % 16 == 0, "rmbx_linear_f32x6_batched: operands must be 16-B aligned");
-  if (M == 0) return RMBX_OK;
-  rmbx::GemmArgs g{a, (const uint16_t*)w_planes, bias, c, lda, ldc, ldw, w_plane_stride, M, N, K, relu ? 1 : 0,
-                   (M + rmbx::GM_BM - 1) / rmbx::GM_BM, N / rmbx::GM_BN, nullptr};
-  g.batch = batch;
-  g.a_bs = a_bs;
-  g.w_bs = w_bs;
-  g.c_bs = c_bs;
-  const long long blocks = (long long)g.tiles_m * g.tiles_n * batch;
-  RMBX_CHECK_ARG(blocks < (1ll << 31), "rmbx_linear_f32x6_batched: too many tiles");
-  rmbx::launch_gemm<false>(blocks, g, (hipStream_t)stream);
-  RMBX_CHECK_LAUNCH();
-  return RMBX_OK;
+  return rmbx::linear_impl<3>("rmbx_linear_f32x6_batched", a, lda, a_bs, w_planes, ldw, w_plane_stride, w_bs, nullptr,
+                              0, bias, c, ldc, c_bs, batch, M, N, K, relu, stream);
 }
 
 extern "C" int rmbx_conv2d_f32x6(const float* in, int N, int H, int W, int C, const void* w_planes, const float* bias,
                                  const float* res, float* out, int Cout, int KH, int KW, int stride, int pad, int relu,
                                  void* stream) {
-  RMBX_CHECK_ARG(in && w_planes && out, "rmbx_conv2d_f32x6: null pointer");
-  RMBX_CHECK_ARG(N >= 0 && H > 0 && W > 0 && KH > 0 && KW > 0 && stride > 0 && pad >= 0,
-                 "rmbx_conv2d_f32x6: bad geometry");
-  RMBX_CHECK_ARG(C % rmbx::GM_BK == 0, "rmbx_conv2d_f32x6: C=%d must be a multiple of %d", C, rmbx::GM_BK);
-  RMBX_CHECK_ARG(Cout % rmbx::GM_BN == 0, "rmbx_conv2d_f32x6: Cout=%d must be a multiple of %d", Cout, rmbx::GM_BN);
-  RMBX_CHECK_ARG(((uintptr_t)in | (uintptr_t)w_planes) % 16 == 0, "rmbx_conv2d_f32x6: operands must be 16-B aligned");
-  const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
-  RMBX_CHECK_ARG(Ho > 0 && Wo > 0, "rmbx_conv2d_f32x6: empty output");
-  const long long M = (long long)N * Ho * Wo;
-  RMBX_CHECK_ARG(M < (1ll << 31) && (long long)N * H * W < (1ll << 31), "rmbx_conv2d_f32x6: too many pixels");
-  if (M == 0) return RMBX_OK;
-  const int K = KH * KW * C;
-  rmbx::GemmArgs g{in, (const uint16_t*)w_planes, bias, out, 0, Cout, K, (long long)Cout * K, (int)M, Cout, K,
-                   relu ? 1 : 0, (int)((M + rmbx::GM_BM - 1) / rmbx::GM_BM), Cout / rmbx::GM_BN, res,
-                   H, W, C, Ho, Wo, KW, stride, pad};
-  const long long blocks = (long long)g.tiles_m * g.tiles_n;
-  RMBX_CHECK_ARG(blocks < (1ll << 31), "rmbx_conv2d_f32x6: too many tiles");
-  rmbx::launch_gemm<true>(blocks, g, (hipStream_t)stream);
+  return rmbx::conv_impl<3>("rmbx_conv2d_f32x6", in, N, H, W, C, w_planes, nullptr, bias, res, out, Cout, KH, KW,
+                            stride, pad, relu, stream);
+}
+
+extern "C" int rmbx_split_f16x2(const float* w, int N, int K, void* planes, float* scale, void* stream) {
+  RMBX_CHECK_ARG(w && planes && scale && N >= 0 && K > 0, "rmbx_split_f16x2: bad arguments");
+  if (N == 0) return RMBX_OK;
+  hipLaunchKernelGGL(rmbx::split_f16x2_kernel, dim3((unsigned)N), dim3(256), 0, (hipStream_t)stream, w, K,
+                     (long long)N * K, (uint16_t*)planes, scale);
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
+}
+
+extern "C" int rmbx_linear_f16x3(const float* a, long long lda, const void* w_planes, long long ldw,
+                                 long long w_plane_stride, const float* w_scale, const float* bias, float* c,
+                                 long long ldc, int M, int N, int K, int relu, void* stream) {
+  return rmbx::linear_impl<2>("rmbx_linear_f16x3", a, lda, 0, w_planes, ldw, w_plane_stride, 0, w_scale, 0, bias, c,
+                              ldc, 0, 1, M, N, K, relu, stream);
+}
+
+extern "C" int rmbx_linear_f16x3_batched(const float* a, long long lda, long long a_bs, const void* w_planes,
+                                         long long ldw, long long w_plane_stride, long long w_bs, const float* w_scale,
+                                         long long ws_bs, const float* bias, float* c, long long ldc, long long c_bs,
+                                         int batch, int M, int N, int K, int relu, void* stream) {
+  return rmbx::linear_impl<2>("rmbx_linear_f16x3_batched", a, lda, a_bs, w_planes, ldw, w_plane_stride, w_bs, w_scale,
+                              ws_bs, bias, c, ldc, c_bs, batch, M, N, K, relu, stream);
+}
+
+extern "C" int rmbx_conv2d_f16x3(const float* in, int N, int H, int W, int C, const void* w_planes,
+                                 const float* w_scale, const float* bias, const float* res, float* out, int Cout,
+                                 int KH, int KW, int stride, int pad, int relu, void* stream) {
+  return rmbx::conv_impl<2>("rmbx_conv2d_f16x3", in, N, H, W, C, w_planes, w_scale, bias, res, out, Cout, KH, KW,
+                            stride, pad, relu, stream);
 }

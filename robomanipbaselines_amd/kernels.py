@@ -5,6 +5,7 @@ enqueued on the current torch stream.  Shape errors raise ValueError, as the ref
 MotionManager/DataKey do for bad keys (common/manager/MotionManager.py:36-39).
 """
 
+import os
 import numpy as np
 import torch
 
@@ -818,25 +819,33 @@ def attention_f32(q, k, v, heads, scale=None, x6=False):
 
 
 # ------------------------------------------------------------------------------------------
-# fp32-accurate linear layers on the bf16 matrix cores (rmbx_linear_f32x6)
+# fp32-accurate linear layers / convolutions on the matrix cores: f16x3 (rmbx_linear_f16x3, the
+# default) or bf16x6 (rmbx_linear_f32x6)
 # ------------------------------------------------------------------------------------------
 LINEAR_F32X6_BN, LINEAR_F32X6_BK = 128, 32
 
-# bench.py's GEMM probe: a list to which every rmbx_linear_f32x6(_batched) / rmbx_conv2d_f32x6 launch
-# appends (name, fp32-equivalent FLOPs, HIP events around it on the current stream); None = no events
+# the piece form pack_f32_weight produces (env RMBX_F32_PIECES): "f16x3" = two f16 pieces per
+# operand, three products (half the MFMA work); "bf16x6" = three bf16 pieces, six products
+F32_PIECES = os.environ.get("RMBX_F32_PIECES", "f16x3")
+if F32_PIECES not in ("f16x3", "bf16x6"):
+    raise ValueError(f"RMBX_F32_PIECES must be f16x3 or bf16x6, not {F32_PIECES!r}")
+
+# bench.py's GEMM probe: a list to which every fp32-accurate GEMM / conv launch appends (name,
+# fp32-equivalent FLOPs, algorithmic bytes, MFMA products per f32 product, HIP events around it on
+# the current stream); None = no events
 GEMM_PROBE = None
 
 
-def _gemm_launch(name, flops, nbytes, fn, *args):
-    """nbytes: the launch's algorithmic HBM bytes (f32 A in, the three bf16 W planes, f32 C out and
-    the residual if any)."""
+def _gemm_launch(name, flops, nbytes, products, fn, *args):
+    """nbytes: the launch's algorithmic HBM bytes (f32 A in, the W pieces, f32 C out and the
+    residual if any)."""
     if GEMM_PROBE is None:
         return N.call(fn, *args)
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     N.call(fn, *args)
     e1.record()
-    GEMM_PROBE.append((name, flops, nbytes, e0, e1))
+    GEMM_PROBE.append((name, flops, nbytes, products, e0, e1))
 
 
 def split_bf16x3(w):
@@ -848,22 +857,77 @@ def split_bf16x3(w):
     return planes
 
 
+class F16x3Planes:
+    """An f32 weight [N, K] in the f16x3 form (rmbx_split_f16x2): planes [2, N, K] f16 with
+    W[n] = scale[n] * (planes[0, n] + 2^-11 planes[1, n]) to 2^-22 relative, scale [N] f32 powers of
+    two.  planes[:, a:b] row slices (the fused MHA's q / k / v rows of in_proj) are supported."""
+
+    __slots__ = ("planes", "scale")
+
+    def __init__(self, planes, scale):
+        self.planes, self.scale = planes, scale
+
+    @property
+    def shape(self):
+        return self.planes.shape
+
+    @property
+    def device(self):
+        return self.planes.device
+
+    def __getitem__(self, idx):
+        if not (isinstance(idx, tuple) and len(idx) == 2 and idx[0] == slice(None) and isinstance(idx[1], slice)):
+            raise IndexError("F16x3Planes takes [:, a:b] row slices only")
+        return F16x3Planes(self.planes[idx], self.scale[idx[1]])
+
+
+def split_f16x2(w):
+    """w f32 [N, K] -> F16x3Planes (rmbx_split_f16x2: per-row power-of-two scale, f16 hi / lo)."""
+    _chk(w, torch.float32, name="w")
+    if w.dim() != 2:
+        raise ValueError("split_f16x2: w must be [N, K]")
+    w = w.contiguous()
+    n, k = w.shape
+    planes = torch.empty((2, n, k), dtype=torch.float16, device=w.device)
+    scale = torch.empty(n, dtype=torch.float32, device=w.device)
+    N.call("rmbx_split_f16x2", N.ptr(w), n, k, N.ptr(planes), N.ptr(scale), N.stream_ptr())
+    return F16x3Planes(planes, scale)
+
+
+def pack_f32_weight(w):
+    """An f32 weight [N, K] in the piece form of F32_PIECES: F16x3Planes or split_bf16x3 planes,
+    the W operand of linear_f32x6 / conv2d_f32x6."""
+    return split_f16x2(w) if F32_PIECES == "f16x3" else split_bf16x3(w)
+
+
+def _planes_nk(planes, what):
+    """(N, K, f16x3?) of a packed weight; raises on anything else."""
+    if isinstance(planes, F16x3Planes):
+        p = planes.planes
+        if p.dim() != 3 or p.shape[0] != 2 or p.dtype != torch.float16 or not p.is_cuda or p.stride(2) != 1:
+            raise ValueError(f"{what}: bad F16x3Planes")
+        return p.shape[1], p.shape[2], True
+    if (not isinstance(planes, torch.Tensor) or planes.dim() != 3 or planes.shape[0] != 3
+            or planes.dtype != torch.bfloat16 or not planes.is_cuda):
+        raise ValueError(f"{what}: planes must be a [3, N, K] bf16 device tensor from split_bf16x3 or F16x3Planes")
+    if planes.stride(2) != 1:
+        raise ValueError(f"{what}: planes rows must be contiguous")
+    return planes.shape[1], planes.shape[2], False
+
+
 def linear_f32x6_supported(x, n_out):
-    """Shapes rmbx_linear_f32x6 takes: f32 device input whose last dim (K) is a multiple of 32,
-    N a multiple of 128."""
+    """Shapes the fp32-accurate GEMM takes: f32 device input whose last dim (K) is a multiple of
+    32, N a multiple of 128."""
     return (x.is_cuda and x.dtype == torch.float32 and x.shape[-1] % LINEAR_F32X6_BK == 0
             and n_out % LINEAR_F32X6_BN == 0)
 
 
 def linear_f32x6(x, planes, bias=None, relu=False, out=None):
-    """relu?(x @ W^T + bias) with x f32 [..., K] and W given as split_bf16x3(W) [3, N, K] (or a row
-    slice planes[:, a:b] of one); f32 result [..., N] (rmbx_linear_f32x6).  x's rows may be strided
-    (last dim contiguous, row stride a multiple of 4 elements)."""
-    if planes.dim() != 3 or planes.shape[0] != 3 or planes.dtype != torch.bfloat16 or not planes.is_cuda:
-        raise ValueError("planes must be a [3, N, K] bf16 device tensor from split_bf16x3")
-    Nn, K = planes.shape[1], planes.shape[2]
-    if planes.stride(2) != 1:
-        raise ValueError("planes rows must be contiguous")
+    """relu?(x @ W^T + bias), fp32-accurate, with x f32 [..., K] and W = pack_f32_weight(W) (or a
+    row slice planes[:, a:b] of one): F16x3Planes -> rmbx_linear_f16x3, split_bf16x3 planes [3, N, K]
+    -> rmbx_linear_f32x6; f32 result [..., N].  x's rows may be strided (last dim contiguous, row
+    stride a multiple of 4 elements)."""
+    Nn, K, h3 = _planes_nk(planes, "linear_f32x6")
     if x.dtype != torch.float32 or not x.is_cuda or x.shape[-1] != K:
         raise ValueError(f"x must be an f32 device tensor [..., {K}]")
     x2 = x.reshape(-1, K)
@@ -876,19 +940,26 @@ def linear_f32x6(x, planes, bias=None, relu=False, out=None):
         out = torch.empty((M, Nn), dtype=torch.float32, device=x.device)
     elif out.dtype != torch.float32 or out.stride(-1) != 1 or out.shape != (M, Nn):
         raise ValueError("out must be an f32 [M, N] tensor with contiguous rows")
-    _gemm_launch(f"linear M={M} N={Nn} K={K}", 2.0 * M * Nn * K, 4 * M * K + 6 * Nn * K + 4 * M * Nn, "rmbx_linear_f32x6", N.ptr(x2), x2.stride(0),
-                 N.ptr(planes), planes.stride(1), planes.stride(0), N.ptr(bias), N.ptr(out), out.stride(0), M, Nn, K,
-                 1 if relu else 0, N.stream_ptr())
+    name, flops = f"linear M={M} N={Nn} K={K}", 2.0 * M * Nn * K
+    if h3:
+        p = planes.planes
+        _gemm_launch(name, flops, 4 * M * K + 4 * Nn * K + 4 * M * Nn, 3, "rmbx_linear_f16x3", N.ptr(x2), x2.stride(0),
+                     N.ptr(p), p.stride(1), p.stride(0), N.ptr(planes.scale), N.ptr(bias), N.ptr(out), out.stride(0),
+                     M, Nn, K, 1 if relu else 0, N.stream_ptr())
+    else:
+        _gemm_launch(name, flops, 4 * M * K + 6 * Nn * K + 4 * M * Nn, 6, "rmbx_linear_f32x6", N.ptr(x2), x2.stride(0),
+                     N.ptr(planes), planes.stride(1), planes.stride(0), N.ptr(bias), N.ptr(out), out.stride(0), M, Nn,
+                     K, 1 if relu else 0, N.stream_ptr())
     return out.view(*x.shape[:-1], Nn)
 
 
 def pack_conv_f32x6(weight):
-    """split_bf16x3 of a conv weight [Cout, C, KH, KW] laid out [Cout][KH][KW][C] (the k order of
-    rmbx_conv2d_f32x6): [3, Cout, KH*KW*C] bf16."""
+    """pack_f32_weight of a conv weight [Cout, C, KH, KW] laid out [Cout][KH][KW][C] (the k order of
+    the implicit-GEMM conv): F16x3Planes or [3, Cout, KH*KW*C] bf16."""
     if weight.dim() != 4:
         raise ValueError("pack_conv_f32x6: weight must be [Cout, C, KH, KW]")
     w = weight.detach().float().permute(0, 2, 3, 1).reshape(weight.shape[0], -1).contiguous()
-    return split_bf16x3(w)
+    return pack_f32_weight(w)
 
 
 def conv2d_f32x6_supported(cin, cout):
@@ -896,20 +967,21 @@ def conv2d_f32x6_supported(cin, cout):
 
 
 def conv2d_f32x6(x, planes, bias, kernel_size, stride=1, padding=0, relu=False, res=None):
-    """relu?(conv2d(x, w, stride, padding) + bias + res) by rmbx_conv2d_f32x6 (fp32-accurate bf16x6
-    implicit GEMM) with planes = pack_conv_f32x6(w); x f32 [N, C, H, W] channels_last; result
-    channels_last [N, Cout, Ho, Wo]."""
+    """relu?(conv2d(x, w, stride, padding) + bias + res) as one fp32-accurate implicit GEMM
+    (rmbx_conv2d_f16x3 / rmbx_conv2d_f32x6 by the form of planes = pack_conv_f32x6(w)); x f32
+    [N, C, H, W] channels_last; result channels_last [N, Cout, Ho, Wo]."""
     if x.dtype != torch.float32 or not x.is_cuda or x.dim() != 4:
         raise ValueError("conv2d_f32x6: x must be an f32 device tensor [N, C, H, W]")
     if not x.is_contiguous(memory_format=torch.channels_last):
         raise ValueError("conv2d_f32x6: x must be channels_last")
     n, c, h, w_ = x.shape
     kh, kw = (kernel_size, kernel_size) if isinstance(kernel_size, int) else kernel_size
-    if planes.dim() != 3 or planes.shape[0] != 3 or planes.shape[2] != kh * kw * c or planes.dtype != torch.bfloat16:
+    cout, kk, h3 = _planes_nk(planes, "conv2d_f32x6")
+    if kk != kh * kw * c:
         raise ValueError("conv2d_f32x6: planes must be pack_conv_f32x6(weight) for this input")
-    if not planes.is_contiguous():
+    pt = planes.planes if h3 else planes
+    if not pt.is_contiguous():
         raise ValueError("conv2d_f32x6: planes must be contiguous")
-    cout = planes.shape[1]
     if not conv2d_f32x6_supported(c, cout):
         raise ValueError(f"conv2d_f32x6: C={c} must be a multiple of 32 and Cout={cout} of 128")
     ho = (h + 2 * padding - kh) // stride + 1
@@ -920,10 +992,16 @@ def conv2d_f32x6(x, planes, bias, kernel_size, stride=1, padding=0, relu=False, 
     if res is not None:
         if res.shape != out.shape or res.dtype != torch.float32 or not res.is_contiguous(memory_format=torch.channels_last):
             raise ValueError("conv2d_f32x6: res must be a channels_last f32 tensor shaped like the output")
-    _gemm_launch(f"conv {kh}x{kw}/{stride} {c}->{cout} {h}x{w_}", 2.0 * n * ho * wo * cout * c * kh * kw,
-                 4 * n * h * w_ * c + 6 * cout * c * kh * kw + 4 * n * ho * wo * cout * (1 if res is None else 2),
-                 "rmbx_conv2d_f32x6", N.ptr(x), n, h, w_, c, N.ptr(planes), N.ptr(bias), N.ptr(res), N.ptr(out), cout,
-                 kh, kw, stride, padding, 1 if relu else 0, N.stream_ptr())
+    name = f"conv {kh}x{kw}/{stride} {c}->{cout} {h}x{w_}"
+    flops = 2.0 * n * ho * wo * cout * c * kh * kw
+    nbytes = 4 * n * h * w_ * c + (4 if h3 else 6) * cout * c * kh * kw + 4 * n * ho * wo * cout * (1 if res is None else 2)
+    if h3:
+        _gemm_launch(name, flops, nbytes, 3, "rmbx_conv2d_f16x3", N.ptr(x), n, h, w_, c, N.ptr(pt), N.ptr(planes.scale),
+                     N.ptr(bias), N.ptr(res), N.ptr(out), cout, kh, kw, stride, padding, 1 if relu else 0,
+                     N.stream_ptr())
+    else:
+        _gemm_launch(name, flops, nbytes, 6, "rmbx_conv2d_f32x6", N.ptr(x), n, h, w_, c, N.ptr(pt), N.ptr(bias),
+                     N.ptr(res), N.ptr(out), cout, kh, kw, stride, padding, 1 if relu else 0, N.stream_ptr())
     return out
 
 
@@ -931,30 +1009,31 @@ WINO_X6_CHANNELS = (256, 512)
 
 
 def pack_wino4_x6(weight):
-    """3x3 conv weight [Cout, C, 3, 3] -> split_bf16x3 of the Winograd F(4x4, 3x3) filter transform
-    U = G g G^T (f64 on the host, rounded once to f32) laid out [36 positions][Cout][C]:
-    [3, 36 * Cout, C] bf16 (the W operand of the 36 position GEMMs)."""
+    """3x3 conv weight [Cout, C, 3, 3] -> pack_f32_weight of the Winograd F(4x4, 3x3) filter
+    transform U = G g G^T (f64 on the host, rounded once to f32) laid out [36 positions][Cout][C]
+    (the W operand of the 36 position GEMMs; rows [36 Cout, C])."""
     if weight.dim() != 4 or tuple(weight.shape[2:]) != (3, 3):
         raise ValueError("pack_wino4_x6: weight must be [Cout, C, 3, 3]")
     co, ci = weight.shape[0], weight.shape[1]
     w = weight.detach().to("cpu", torch.float64)
     G = torch.tensor(_WINO4_G, dtype=torch.float64)
     U = torch.einsum("xa,oiab,yb->xyoi", G, w, G).reshape(36 * co, ci)
-    return split_bf16x3(U.to(torch.float32).to(weight.device).contiguous())
+    return pack_f32_weight(U.to(torch.float32).to(weight.device).contiguous())
 
 
 def conv3x3_wino4_x6(x, planes, bias, relu=False, res=None):
     """relu?(conv2d(x, w, stride 1, pad 1) + bias + res) as the explicit Winograd F(4x4, 3x3): input
-    transform pass (rmbx_wino4_input_f32), 36 fp32-accurate bf16x6 position GEMMs
-    (rmbx_linear_f32x6_batched, planes = pack_wino4_x6(w)), output transform pass with the epilogue
-    (rmbx_wino4_output_f32).  x f32 channels_last [N, C, H, W]."""
+    transform pass (rmbx_wino4_input_f32), 36 fp32-accurate position GEMMs (rmbx_linear_f16x3_batched
+    / rmbx_linear_f32x6_batched by the form of planes = pack_wino4_x6(w)), output transform pass
+    with the epilogue (rmbx_wino4_output_f32).  x f32 channels_last [N, C, H, W]."""
     _chk_nhwc(x, "x")
     if x.dtype != torch.float32:
         raise ValueError("conv3x3_wino4_x6: x must be f32")
     n, C, H, W = x.shape
-    if planes.dim() != 3 or planes.shape[0] != 3 or planes.shape[2] != C or planes.shape[1] % 36:
+    rows, kk, h3 = _planes_nk(planes, "conv3x3_wino4_x6")
+    if kk != C or rows % 36:
         raise ValueError("conv3x3_wino4_x6: planes must be pack_wino4_x6(weight) for this input")
-    co = planes.shape[1] // 36
+    co = rows // 36
     if not conv2d_f32x6_supported(C, co):
         raise ValueError(f"conv3x3_wino4_x6: C={C} must be a multiple of 32 and Cout={co} of 128")
     if bias is not None:
@@ -968,10 +1047,16 @@ def conv3x3_wino4_x6(x, planes, bias, relu=False, res=None):
     V = torch.empty((36, T, C), dtype=torch.float32, device=x.device)
     N.call("rmbx_wino4_input_f32", N.ptr(x), n, H, W, C, N.ptr(V), N.stream_ptr())
     M = torch.empty((36, T, co), dtype=torch.float32, device=x.device)
-    _gemm_launch(f"winograd x36 M={T} N={co} K={C}", 2.0 * 36 * T * co * C, 36 * (4 * T * C + 6 * co * C + 4 * T * co),
-                 "rmbx_linear_f32x6_batched", N.ptr(V), C,
-                 T * C, N.ptr(planes), planes.stride(1), planes.stride(0), co * C, None, N.ptr(M), co, T * co, 36, T,
-                 co, C, 0, N.stream_ptr())
+    name, flops = f"winograd x36 M={T} N={co} K={C}", 2.0 * 36 * T * co * C
+    if h3:
+        p = planes.planes
+        _gemm_launch(name, flops, 36 * (4 * T * C + 4 * co * C + 4 * T * co), 3, "rmbx_linear_f16x3_batched", N.ptr(V),
+                     C, T * C, N.ptr(p), p.stride(1), p.stride(0), co * C, N.ptr(planes.scale), co, None, N.ptr(M), co,
+                     T * co, 36, T, co, C, 0, N.stream_ptr())
+    else:
+        _gemm_launch(name, flops, 36 * (4 * T * C + 6 * co * C + 4 * T * co), 6, "rmbx_linear_f32x6_batched", N.ptr(V),
+                     C, T * C, N.ptr(planes), planes.stride(1), planes.stride(0), co * C, None, N.ptr(M), co, T * co,
+                     36, T, co, C, 0, N.stream_ptr())
     N.call("rmbx_wino4_output_f32", N.ptr(M), n, H, W, co, N.ptr(bias), N.ptr(res), N.ptr(out), 1 if relu else 0,
            N.stream_ptr())
     return out

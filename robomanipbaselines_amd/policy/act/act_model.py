@@ -43,9 +43,10 @@ def sine_pos_embed(h, w, num_pos_feats=256, temperature=10000, device=None, dtyp
     return torch.cat((pos_y, pos_x), dim=3).permute(0, 3, 1, 2).to(dtype)
 
 
-# f32 GEMMs of the fused device form: "x6" = rmbx_linear_f32x6 (each f32 operand split into three
-# bf16 pieces, six piece products on the bf16 matrix cores, f32 accumulation: the f32 GEMM error
-# class at 2.67x the f32 MFMA rate, tests/test_gemm_gpu.py), "blas" = hipBLASLt f32; env RMBX_F32_GEMM
+# f32 GEMMs of the fused device form: "x6" = the fp32-accurate rmbx GEMMs (kernels.pack_f32_weight:
+# f16x3 by default, two f16 pieces per operand and three products; or bf16x6, three bf16 pieces and six
+# products; both at the bf16 MFMA rate with f32 accumulation, the f32 GEMM error class,
+# tests/test_gemm_gpu.py), "blas" = hipBLASLt f32; env RMBX_F32_GEMM
 F32_GEMM = os.environ.get("RMBX_F32_GEMM", "x6")
 # f32 attention products: "x6" = rmbx_attention_f32x6 (bf16x6 pieces), "f32" = rmbx_attention_f32
 # (f32 MFMA); env RMBX_F32_ATTN
@@ -61,14 +62,14 @@ def _x6_ok(x, n_out):
 
 
 def _x6_planes(owner, name, w):
-    """split_bf16x3(w), cached on `owner` per weight storage and version."""
+    """pack_f32_weight(w) (the f16x3 or bf16x6 pieces), cached on `owner` per weight storage and version."""
     from ... import kernels as K
 
     key = (w.data_ptr(), w._version, tuple(w.shape))
     cache = owner.__dict__.setdefault("_x6", {})
     ent = cache.get(name)
     if ent is None or ent[0] != key:
-        ent = (key, K.split_bf16x3(w.detach().contiguous()))
+        ent = (key, K.pack_f32_weight(w.detach().contiguous()))
         cache[name] = ent
     return ent[1]
 
@@ -98,7 +99,7 @@ def _x6_linear_padded(owner, name, x, w, b):
         wp[:N, :Kd] = w.detach()
         bp = torch.zeros(Np, device=w.device, dtype=torch.float32)
         bp[:N] = b.detach()
-        ent = (key, K.split_bf16x3(wp), bp)
+        ent = (key, K.pack_f32_weight(wp), bp)
         cache[name] = ent
     shp = x.shape
     x2 = x.reshape(-1, Kd)

@@ -43,7 +43,7 @@ def _gemm(owner, name, x2, w2, bias):
         cache = owner.__dict__.setdefault("_x6", {})
         ent = cache.get(name)
         if ent is None or ent[0] != key:
-            ent = (key, K.split_bf16x3(w2.detach().contiguous()))
+            ent = (key, K.pack_f32_weight(w2.detach().contiguous()))
             cache[name] = ent
         return K.linear_f32x6(x2, ent[1], bias)
     return F.linear(x2, w2, bias)

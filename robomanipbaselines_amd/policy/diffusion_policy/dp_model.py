@@ -124,7 +124,7 @@ class SpatialSoftmax(nn.Module):
             wp[: c.out_channels] = w.detach().reshape(c.out_channels, -1)
             bp = torch.zeros(n_pad, dtype=torch.float32, device=w.device)
             bp[: c.out_channels] = c.bias.detach()
-            cache = (key, K.split_bf16x3(wp), bp)
+            cache = (key, K.pack_f32_weight(wp), bp)
             self.__dict__["_x6"] = cache
         B, C, H, W = f.shape
         y = K.linear_f32x6(f.permute(0, 2, 3, 1), cache[1], cache[2])[..., : c.out_channels]  # [B, H, W, kp]

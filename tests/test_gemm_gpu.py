@@ -1,10 +1,12 @@
-"""rmbx_linear_f32x6 (fp32-accurate GEMM on the bf16 matrix cores: both operands split into three
-bf16 pieces, six piece products accumulated in f32) against an f64 product of the same f32
-operands, beside the device's own f32 GEMM (hipBLASLt, the path it replaces in the fp32 ACT
-transformer).  The bar is the f32 GEMM error class: max |err| <= 4e-6 * max |ref|, and for the
-linear layers no worse than 2x hipBLASLt's f32 GEMM error on the same inputs (measured ~0.3-0.8e-6
-vs 1-2e-6).  rmbx_conv2d_f32x6 (the same kernel as an implicit-GEMM convolution) is held to the
-4e-6 bar against an f64 F.conv2d."""
+"""The fp32-accurate GEMMs on the matrix cores against an f64 product of the same f32 operands,
+beside the device's own f32 GEMM (hipBLASLt, the path they replace in the fp32 ACT transformer):
+rmbx_linear_f32x6 (bf16x6: both operands split into three bf16 pieces, six piece products
+accumulated in f32) and rmbx_linear_f16x3 (f16x3: two f16 pieces, the low one scaled by 2^11, three
+products; per-row power-of-two weight scales and a per-block re-run on a scaled copy for
+activations outside f16's comfortable range).  The bar is the f32 GEMM error class: max |err| <=
+4e-6 * max |ref|, and for the linear layers no worse than 2x hipBLASLt's f32 GEMM error on the same
+inputs (measured ~0.3-0.8e-6 vs 1-2e-6).  The implicit-GEMM convolutions (rmbx_conv2d_f16x3, the
+default packing, and rmbx_conv2d_f32x6) are held to the 4e-6 bar against an f64 F.conv2d."""
 
 import pytest
 import torch
@@ -35,18 +37,49 @@ def test_split_bf16x3_exact():
     assert (p[1].float().abs()[nz] <= p[0].float().abs()[nz] * 2.0 ** -8).all()
 
 
+def _pack(form):
+    from robomanipbaselines_amd import kernels as K_
+
+    return K_.split_bf16x3 if form == "bf16x6" else K_.split_f16x2
+
+
 @torch.no_grad()
+def test_split_f16x2_pieces_and_scales():
+    """W[n] = scale[n] (hi + 2^-11 lo) to 2^-22 of each element (2^-36 of the row max below f16's
+    normal range), scale[n] a power of two with the scaled row max in [2^13, 2^14); zero rows keep
+    scale 1."""
+    from robomanipbaselines_amd import kernels as K_
+
+    g = torch.Generator(device="cpu").manual_seed(1)
+    w = torch.randn(64, 300, generator=g) * torch.logspace(-20, 20, 64)[:, None]
+    w[5] = 0.0
+    w[6, :7] = torch.tensor([0.0, -0.0, 1e-30, 65504.0, -1e-5, 3.0, 1e-12])
+    p = K_.split_f16x2(w.to(DEV))
+    assert p.planes.shape == (2, 64, 300) and p.planes.dtype == torch.float16 and p.scale.shape == (64,)
+    hi, lo, sc = p.planes[0].double().cpu(), p.planes[1].double().cpu(), p.scale.double().cpu()
+    rec = sc[:, None] * (hi + lo / 2048)
+    wd = w.double()
+    rowmax = wd.abs().amax(1, keepdim=True)
+    assert ((rec - wd).abs() <= wd.abs() * 2.0 ** -22 + rowmax * 2.0 ** -36).all()
+    assert torch.equal(torch.log2(sc).round(), torch.log2(sc))  # powers of two
+    m = (hi.abs().amax(1))[rowmax[:, 0] > 0]
+    assert ((m >= 2 ** 13) & (m <= 2 ** 14)).all()
+    assert sc[5] == 1.0 and (rec[5] == 0).all()
+
+
+@torch.no_grad()
+@pytest.mark.parametrize("form", ["bf16x6", "f16x3"])
 @pytest.mark.parametrize("M,N,K,relu,bias", [(1, 128, 32, False, False), (1000, 384, 512, True, True),
                                              (257, 3200, 512, True, True), (3000, 512, 3200, False, True),
                                              (5000, 1536, 512, False, True)])
-def test_linear_f32x6_vs_f64(M, N, K, relu, bias):
+def test_linear_f32x6_vs_f64(form, M, N, K, relu, bias):
     from robomanipbaselines_amd import kernels as K_
 
     g = torch.Generator(device="cpu").manual_seed(M + N + K)
     x = torch.randn(M, K, generator=g).to(DEV)
     w = (torch.randn(N, K, generator=g) / K ** 0.5).to(DEV)
     b = torch.randn(N, generator=g).to(DEV) if bias else None
-    got = K_.linear_f32x6(x, K_.split_bf16x3(w), b, relu=relu)
+    got = K_.linear_f32x6(x, _pack(form)(w), b, relu=relu)
     ref = x.double() @ w.double().t()
     if bias:
         ref = ref + b.double()
@@ -61,7 +94,8 @@ def test_linear_f32x6_vs_f64(M, N, K, relu, bias):
 
 
 @torch.no_grad()
-def test_linear_f32x6_strided_rows_and_plane_slice():
+@pytest.mark.parametrize("form", ["bf16x6", "f16x3"])
+def test_linear_f32x6_strided_rows_and_plane_slice(form):
     """x as a column slice of a wider activation (row stride > K) and W as a row slice of a split
     in_proj_weight, as the fused MHA uses them."""
     from robomanipbaselines_amd import kernels as K_
@@ -71,21 +105,78 @@ def test_linear_f32x6_strided_rows_and_plane_slice():
     x = big[:, 512:1024]
     w = (torch.randn(1536, 512, generator=g) / 512 ** 0.5).to(DEV)
     b = torch.randn(1536, generator=g).to(DEV)
-    planes = K_.split_bf16x3(w)
+    planes = _pack(form)(w)
     got = K_.linear_f32x6(x, planes[:, 512:1024], b[512:1024])
     ref = x.double() @ w[512:1024].double().t() + b[512:1024].double()
     assert _err(got, ref) <= 4e-6
 
 
 @torch.no_grad()
-def test_linear_f32x6_rejects_bad_shapes():
+@pytest.mark.parametrize("form", ["bf16x6", "f16x3"])
+def test_linear_f32x6_rejects_bad_shapes(form):
     from robomanipbaselines_amd import kernels as K_
 
     x = torch.randn(8, 48, device=DEV)
     with pytest.raises((ValueError, RuntimeError)):
-        K_.linear_f32x6(x, K_.split_bf16x3(torch.randn(128, 48, device=DEV)))
+        K_.linear_f32x6(x, _pack(form)(torch.randn(128, 48, device=DEV)))
     with pytest.raises((ValueError, RuntimeError)):
-        K_.linear_f32x6(torch.randn(8, 64, device=DEV), K_.split_bf16x3(torch.randn(100, 64, device=DEV)))
+        K_.linear_f32x6(torch.randn(8, 64, device=DEV), _pack(form)(torch.randn(100, 64, device=DEV)))
+
+
+@torch.no_grad()
+@pytest.mark.parametrize("case", ["huge", "tiny", "mixed_blocks", "near_f16_max", "zero_rows"])
+def test_linear_f16x3_activation_range(case):
+    """f16's range is handled exactly: a 256-row block whose |a| max lies outside [2^-6, 2^15]
+    re-runs on a power-of-two-scaled copy.  Every block's rows stay in the f32 GEMM error class
+    relative to that block's own result scale, including activations far beyond f16's max
+    (65504) and far below its normal range."""
+    from robomanipbaselines_amd import kernels as K_
+
+    g = torch.Generator(device="cpu").manual_seed(11)
+    M, N, K = 1024, 256, 512
+    x = torch.randn(M, K, generator=g)
+    scale = {"huge": torch.full((M, 1), 1e7), "tiny": torch.full((M, 1), 1e-9),
+             "mixed_blocks": torch.tensor([1e6, 1e-7, 1.0, 3e4]).repeat_interleave(256)[:, None],
+             "near_f16_max": torch.full((M, 1), 32000.0 / 4.5), "zero_rows": torch.ones(M, 1)}[case]
+    x = x * scale
+    if case == "zero_rows":
+        x[::3] = 0.0
+    w = torch.randn(N, K, generator=g) / K ** 0.5
+    got = K_.linear_f32x6(x.to(DEV), K_.split_f16x2(w.to(DEV))).cpu().double()
+    ref = x.double() @ w.double().t()
+    assert torch.isfinite(got).all()
+    for blk in range(M // 256):
+        r = slice(256 * blk, 256 * blk + 256)
+        den = ref[r].abs().max()
+        if den == 0:
+            assert (got[r] == 0).all()
+            continue
+        assert ((got[r] - ref[r]).abs().max() / den).item() <= 4e-6, (case, blk)
+
+
+@torch.no_grad()
+def test_linear_f16x3_weight_range_and_non_finite_inputs():
+    """Weight rows from 1e-12 to 1e12 (per-row power-of-two scales) stay in the f32 error class per
+    output column; an inf / NaN activation makes its own output row non-finite as f32 does, and
+    leaves the other rows exact to the f32 class."""
+    from robomanipbaselines_amd import kernels as K_
+
+    g = torch.Generator(device="cpu").manual_seed(12)
+    M, N, K = 600, 256, 256
+    x = torch.randn(M, K, generator=g)
+    w = torch.randn(N, K, generator=g) * torch.logspace(-12, 12, N)[:, None]
+    got = K_.linear_f32x6(x.to(DEV), K_.split_f16x2(w.to(DEV))).cpu().double()
+    ref = x.double() @ w.double().t()
+    colmax = ref.abs().amax(0)
+    assert ((got - ref).abs().amax(0) / colmax).max().item() <= 4e-6
+    x[3, 7] = float("inf")
+    x[400, 9] = float("nan")
+    got = K_.linear_f32x6(x.to(DEV), K_.split_f16x2(w.to(DEV))).cpu().double()
+    base = (x @ w.t()).double()
+    assert torch.equal(torch.isfinite(got).all(1), torch.isfinite(base).all(1))
+    ok = torch.isfinite(base).all(1)
+    ref = x[ok].double() @ w.double().t()
+    assert ((got[ok] - ref).abs().amax(0) / ref.abs().amax(0)).max().item() <= 4e-6
 
 
 def _conv_ref(x, w, b, stride, pad, relu, res):
@@ -102,9 +193,11 @@ def _conv_ref(x, w, b, stride, pad, relu, res):
     (2, 256, 9, 11, 512, 3, 2, 1, True, False, True),
     (2, 64, 12, 16, 128, 3, 1, 1, True, True, True),      # stride 1 with a residual
 ])
-def test_conv2d_f32x6_vs_f64(n, C, H, W, Cout, k, stride, pad, relu, res, bias):
+@pytest.mark.parametrize("form", ["bf16x6", "f16x3"])
+def test_conv2d_f32x6_vs_f64(monkeypatch, form, n, C, H, W, Cout, k, stride, pad, relu, res, bias):
     from robomanipbaselines_amd import kernels as K_
 
+    monkeypatch.setattr(K_, "F32_PIECES", form)
     g = torch.Generator(device="cpu").manual_seed(n * 1000 + C + k)
     x = torch.randn(n, C, H, W, generator=g)
     w = torch.randn(Cout, C, k, k, generator=g) / (C * k * k) ** 0.5
@@ -182,3 +275,26 @@ def test_gemm_profiling_variants_equal_default(monkeypatch, M, N, K):
         got = K_.linear_f32x6(x, planes, b, relu=True)
         torch.cuda.synchronize()
         assert torch.equal(got, want), var
+
+
+@torch.no_grad()
+@pytest.mark.parametrize("form", ["bf16x6", "f16x3"])
+@pytest.mark.parametrize("n,C,H,W,Cout,res,relu", [(2, 256, 30, 40, 256, True, True), (3, 512, 15, 20, 512, False, True)])
+def test_winograd4_explicit_position_gemms_vs_f64(monkeypatch, form, n, C, H, W, Cout, res, relu):
+    """The explicit Winograd F(4x4) conv of the 256/512-channel layers (input transform, 36 batched
+    position GEMMs, output transform) in both piece forms against an f64 F.conv2d."""
+    from robomanipbaselines_amd import kernels as K_
+
+    monkeypatch.setattr(K_, "F32_PIECES", form)
+    g = torch.Generator(device="cpu").manual_seed(C + H)
+    x = torch.randn(n, C, H, W, generator=g).clamp_min(0)
+    w = torch.randn(Cout, C, 3, 3, generator=g) / (C * 9) ** 0.5
+    b = torch.randn(Cout, generator=g)
+    r = torch.randn(n, Cout, H, W, generator=g) if res else None
+    cl = torch.channels_last
+    planes = K_.pack_wino4_x6(w.to(DEV))
+    assert isinstance(planes, K_.F16x3Planes) == (form == "f16x3")
+    got = K_.conv3x3_wino4_x6(x.to(DEV).contiguous(memory_format=cl), planes, b.to(DEV), relu=relu,
+                              res=None if r is None else r.to(DEV).contiguous(memory_format=cl))
+    # Winograd's transforms add their own f32 rounding (~1e-6 relative at these sizes)
+    assert _err(got.cpu(), _conv_ref(x, w, b, 1, 1, relu, r)) <= 1e-5
