@@ -45,9 +45,11 @@
 // Three products instead of six: half the MFMA work of bf16x6.  f16's exponent range is the
 // price, handled exactly: W rows are scaled by a power of two at packing (rmbx_split_f16x2: row
 // max in [2^13, 2^14), the inverse applied per output column in the epilogue), and every block
-// tracks the largest |a| it split; a block whose tile max lies outside [2^-6, 2^15] (values that
-// would overflow f16 or sit in its subnormal range) runs its K loop again on a * 2^s with s
-// putting the max in [2^13, 2^14), and scales its result back by 2^-s (powers of two: exact).
+// tracks the largest |a| of each of its rows; a row whose max lies outside [2^-6, 2^15] (values
+// that would overflow f16 or sit in its subnormal range) is split again as a * 2^s with s putting
+// its max in [2^13, 2^14) and its result scaled back by 2^-s (powers of two: exact): the block
+// re-runs its K loop with the other rows at scale 1 (bit-identical to the first pass), so every
+// row's result depends on that row alone (batch invariance).
 #include "rmbx_common.h"
 
 #include <cstdint>
@@ -74,10 +76,10 @@ constexpr int GM_EPI_BYTES = 8 * 64 * GM_EPI_PITCH * 4;  // 136 KiB: eight 64 x 
 // PC pieces per operand (3: bf16x6, 2: f16x3): one K stage = PC A planes + PC W planes
 template <int PC>
 constexpr int gm_stage() { return PC * (GM_A_PLANE + GM_B_PLANE); }  // 72 / 48 KiB
-// two stages, at least the epilogue tile; f16x3 adds 64 B for the block max of |a|
+// two stages, at least the epilogue tile; f16x3 adds the rows' range scales (1 KiB) and 8 flags
 template <int PC>
 constexpr int gm_smem() {
-  return (2 * gm_stage<PC>() > GM_EPI_BYTES ? 2 * gm_stage<PC>() : GM_EPI_BYTES) + (PC == 2 ? 64 : 0);
+  return (2 * gm_stage<PC>() > GM_EPI_BYTES ? 2 * gm_stage<PC>() : GM_EPI_BYTES) + (PC == 2 ? 1024 + 64 : 0);
 }
 static_assert(gm_smem<3>() <= 160 * 1024 && gm_smem<2>() <= 160 * 1024, "the LDS of a CU");
 
@@ -253,8 +255,8 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
       return ok;
     }
   };
-  // f16x3: the largest |a| this thread split (pass 0) and the pass-1 scale of a
-  float amax = 0.f, ascale = 1.f;
+  // f16x3: the largest |a| this thread split of its two rows (pass 0) and the rows' pass-1 scales
+  float amax0 = 0.f, amax1 = 0.f, as0 = 1.f, as1 = 1.f;
   auto store_a = [&](const float4 (&Rin)[4], int ok, int buf, auto scaled) {
     float4 R[4] = {Rin[0], Rin[1], Rin[2], Rin[3]};
     if constexpr (CONV) {
@@ -268,13 +270,15 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
         if constexpr (decltype(scaled)::value) {
-          R[i].x *= ascale;
-          R[i].y *= ascale;
-          R[i].z *= ascale;
-          R[i].w *= ascale;
+          const float sc = i < 2 ? as0 : as1;
+          R[i].x *= sc;
+          R[i].y *= sc;
+          R[i].z *= sc;
+          R[i].w *= sc;
         } else {
-          amax = fmaxf(amax, fmaxf(fabsf(R[i].x), fabsf(R[i].y)));
-          amax = fmaxf(amax, fmaxf(fabsf(R[i].z), fabsf(R[i].w)));
+          float& am = i < 2 ? amax0 : amax1;
+          am = fmaxf(am, fmaxf(fabsf(R[i].x), fabsf(R[i].y)));
+          am = fmaxf(am, fmaxf(fabsf(R[i].z), fabsf(R[i].w)));
         }
         split_f16_pair(R[i].x, R[i].y, h[2 * i], l[2 * i]);
         split_f16_pair(R[i].z, R[i].w, h[2 * i + 1], l[2 * i + 1]);
@@ -415,35 +419,62 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
   };
   k_loop(std::false_type{});
 
-  float post = 1.f;  // f16x3: 2^-s of a pass-1 block
   if constexpr (PC == 2) {
-    // block max of |a| over the tile; outside [2^-6, 2^15] (f16 overflow / subnormal range) the
-    // block runs its K loop again on a * 2^s, max in [2^13, 2^14), and scales back by 2^-s.  A
-    // NaN never raises the max (fmaxf) and an infinite max is left to propagate as in f32.
-    float m = amax;
-#pragma unroll
-    for (int o = 32; o >= 1; o >>= 1) m = fmaxf(m, __shfl_xor(m, o));
-    float* red = reinterpret_cast<float*>(smem + gm_smem<PC>() - 64);
-    if (lane == 0) red[wave] = m;
+    // per-row range check: a row whose |a| max lies outside [2^-6, 2^15] (f16 overflow / subnormal
+    // range) is re-run on a * 2^s, max in [2^13, 2^14), and scaled back by 2^-s; a block with
+    // such a row runs its K loop again with every other row at scale 1, i.e. bit-identical to
+    // pass 0, so each row's result depends on its own values only.  A NaN never raises the max
+    // (fmaxf); an infinite max is left to propagate as in f32.
+    float m0 = amax0, m1 = amax1;
+    m0 = fmaxf(m0, __shfl_xor(m0, 1));  // the 4 lanes of a row (tid % 4 = k quarter)
+    m0 = fmaxf(m0, __shfl_xor(m0, 2));
+    m1 = fmaxf(m1, __shfl_xor(m1, 1));
+    m1 = fmaxf(m1, __shfl_xor(m1, 2));
+    float inv0 = 1.f, inv1 = 1.f;
+    auto row_scale = [](float m, float& sc, float& inv) {
+      if ((m > 32768.f || (m > 0.f && m < 0.015625f)) && m <= 3.4e38f) {
+        int e;
+        frexpf(m, &e);  // m = f 2^e, f in [0.5, 1)
+        sc = ldexpf(1.f, 14 - e);
+        inv = ldexpf(1.f, e - 14);
+        return true;
+      }
+      return false;
+    };
+    const bool need = row_scale(m0, as0, inv0) | row_scale(m1, as1, inv1);
+    float* rinv = reinterpret_cast<float*>(smem + gm_smem<PC>() - 1024 - 64);  // [256] rows' 2^-s
+    int* flag = reinterpret_cast<int*>(smem + gm_smem<PC>() - 64);
+    if (aq == 0) {
+      rinv[arow] = inv0;
+      rinv[arow + 128] = inv1;
+    }
+    const unsigned long long bal = __ballot(need);
+    if (lane == 0) flag[wave] = bal != 0ull;
     asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    float bm = red[0];
+    int any = 0;
 #pragma unroll
-    for (int w = 1; w < 8; ++w) bm = fmaxf(bm, red[w]);
-    if ((bm > 32768.f || (bm > 0.f && bm < 0.015625f)) && bm <= 3.4e38f) {
-      int e;
-      frexpf(bm, &e);  // bm = f 2^e, f in [0.5, 1)
-      ascale = ldexpf(1.f, 14 - e);
-      post = ldexpf(1.f, e - 14);
+    for (int w = 0; w < 8; ++w) any |= flag[w];
+    if (any) {
       zero_acc();
       k_loop(std::true_type{});
     }
-    // join the product groups: acc + 2^-11 cor, then undo the pass-1 scale (a power of two)
+    // join the product groups: acc + 2^-11 cor, then undo the rows' pass-1 scales (powers of two)
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
       for (int j = 0; j < 4; ++j)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) acc[i][j][e] = fmaf(cor[i][j][e], 0.00048828125f, acc[i][j][e]) * post;
+        for (int e = 0; e < 4; ++e) acc[i][j][e] = fmaf(cor[i][j][e], 0.00048828125f, acc[i][j][e]);
+    if (any) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const float inv = rinv[wm * 64 + i * 16 + 4 * fs + e];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[i][j][e] *= inv;
+        }
+    }
   }
 
   if constexpr ((VAR & 16) != 0) {

@@ -126,8 +126,8 @@ def test_linear_f32x6_rejects_bad_shapes(form):
 @torch.no_grad()
 @pytest.mark.parametrize("case", ["huge", "tiny", "mixed_blocks", "near_f16_max", "zero_rows"])
 def test_linear_f16x3_activation_range(case):
-    """f16's range is handled exactly: a 256-row block whose |a| max lies outside [2^-6, 2^15]
-    re-runs on a power-of-two-scaled copy.  Every block's rows stay in the f32 GEMM error class
+    """f16's range is handled exactly: a row whose |a| max lies outside [2^-6, 2^15] is re-run on a
+    power-of-two-scaled copy.  Every 256-row block of rows stays in the f32 GEMM error class
     relative to that block's own result scale, including activations far beyond f16's max
     (65504) and far below its normal range."""
     from robomanipbaselines_amd import kernels as K_
@@ -152,6 +152,27 @@ def test_linear_f16x3_activation_range(case):
             assert (got[r] == 0).all()
             continue
         assert ((got[r] - ref[r]).abs().max() / den).item() <= 4e-6, (case, blk)
+
+
+@torch.no_grad()
+def test_linear_f16x3_rows_independent_of_their_block():
+    """A row's f16x3 result is bitwise the same whether its 256-row block holds rows that need the
+    range re-run (1e8, 1e-9) or not: the re-run keeps in-range rows at scale 1."""
+    from robomanipbaselines_amd import kernels as K_
+
+    g = torch.Generator(device="cpu").manual_seed(13)
+    x = torch.randn(512, 512, generator=g)
+    x[5] *= 1e8
+    x[300] *= 1e-9
+    w = K_.split_f16x2((torch.randn(384, 512, generator=g) / 512 ** 0.5).to(DEV))
+    xd = x.to(DEV)
+    full = K_.linear_f32x6(xd, w)
+    keep = [i for i in range(512) if i not in (5, 300)]
+    alone = K_.linear_f32x6(xd[keep].contiguous(), w)
+    assert torch.equal(full[keep], alone)
+    for r in (5, 300):
+        one = K_.linear_f32x6(xd[r:r + 1].contiguous(), w)
+        assert torch.equal(full[r:r + 1], one)
 
 
 @torch.no_grad()
