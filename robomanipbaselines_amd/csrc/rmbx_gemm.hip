@@ -255,8 +255,11 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
       return ok;
     }
   };
-  // f16x3: the largest |a| this thread split of its two rows (pass 0) and the rows' pass-1 scales
-  float amax0 = 0.f, amax1 = 0.f, as0 = 1.f, as1 = 1.f;
+  // f16x3: the largest |a| this thread split of its two rows (pass 0; as f32 bit patterns with the
+  // sign cleared, whose unsigned order is the order of |a|, NaN above inf) and the rows' pass-1
+  // scales
+  uint32_t amax0 = 0, amax1 = 0;
+  float as0 = 1.f, as1 = 1.f;
   auto store_a = [&](const float4 (&Rin)[4], int ok, int buf, auto scaled) {
     float4 R[4] = {Rin[0], Rin[1], Rin[2], Rin[3]};
     if constexpr (CONV) {
@@ -276,9 +279,10 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
           R[i].z *= sc;
           R[i].w *= sc;
         } else {
-          float& am = i < 2 ? amax0 : amax1;
-          am = fmaxf(am, fmaxf(fabsf(R[i].x), fabsf(R[i].y)));
-          am = fmaxf(am, fmaxf(fabsf(R[i].z), fabsf(R[i].w)));
+          uint32_t& am = i < 2 ? amax0 : amax1;
+          constexpr uint32_t ABS = 0x7fffffffu;
+          am = max(am, max(__float_as_uint(R[i].x) & ABS, __float_as_uint(R[i].y) & ABS));
+          am = max(am, max(__float_as_uint(R[i].z) & ABS, __float_as_uint(R[i].w) & ABS));
         }
         split_f16_pair(R[i].x, R[i].y, h[2 * i], l[2 * i]);
         split_f16_pair(R[i].z, R[i].w, h[2 * i + 1], l[2 * i + 1]);
@@ -423,13 +427,14 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
     // per-row range check: a row whose |a| max lies outside [2^-6, 2^15] (f16 overflow / subnormal
     // range) is re-run on a * 2^s, max in [2^13, 2^14), and scaled back by 2^-s; a block with
     // such a row runs its K loop again with every other row at scale 1, i.e. bit-identical to
-    // pass 0, so each row's result depends on its own values only.  A NaN never raises the max
-    // (fmaxf); an infinite max is left to propagate as in f32.
-    float m0 = amax0, m1 = amax1;
-    m0 = fmaxf(m0, __shfl_xor(m0, 1));  // the 4 lanes of a row (tid % 4 = k quarter)
-    m0 = fmaxf(m0, __shfl_xor(m0, 2));
-    m1 = fmaxf(m1, __shfl_xor(m1, 1));
-    m1 = fmaxf(m1, __shfl_xor(m1, 2));
+    // pass 0, so each row's result depends on its own values only.  A row holding a NaN or an
+    // infinity is left to propagate them as in f32.
+    uint32_t b0 = amax0, b1 = amax1;
+    b0 = max(b0, (uint32_t)__shfl_xor((int)b0, 1));  // the 4 lanes of a row (tid % 4 = k quarter)
+    b0 = max(b0, (uint32_t)__shfl_xor((int)b0, 2));
+    b1 = max(b1, (uint32_t)__shfl_xor((int)b1, 1));
+    b1 = max(b1, (uint32_t)__shfl_xor((int)b1, 2));
+    const float m0 = __uint_as_float(b0), m1 = __uint_as_float(b1);  // NaN: no re-run
     float inv0 = 1.f, inv1 = 1.f;
     auto row_scale = [](float m, float& sc, float& inv) {
       if ((m > 32768.f || (m > 0.f && m < 0.015625f)) && m <= 3.4e38f) {

@@ -167,10 +167,17 @@ class _FusedConv(nn.Module):
         return (c.stride[0] == c.stride[1] and c.padding[0] == c.padding[1]
                 and K.conv2d_f32x6_supported(c.in_channels, c.out_channels))
 
+    # stride-1 3x3 convs whose output width is in this set run as the fp32-accurate implicit GEMM
+    # (x6 below, f16x3 pieces) instead of the fused f32 Winograd; env RMBX_S1_GEMM ("" = none)
+    S1_GEMM_CHANNELS = tuple(int(c) for c in os.environ.get("RMBX_S1_GEMM", "").split(",") if c)
+
+    def s1_gemm_ok(self):
+        return (self.conv.out_channels in self.S1_GEMM_CHANNELS and K.F32_PIECES == "f16x3" and self.x6_ok())
+
     def x6(self, x, relu, res=None, bias=True):
-        """f32 conv (+ bias) (+ res) (+ ReLU) as one rmbx_conv2d_f32x6 launch (fp32-accurate bf16x6
-        implicit GEMM, epilogue fused); bias=False: no bias.  The split weight is cached per
-        weight storage."""
+        """f32 conv (+ bias) (+ res) (+ ReLU) as one fp32-accurate implicit-GEMM launch
+        (rmbx_conv2d_f16x3 / rmbx_conv2d_f32x6 by kernels.F32_PIECES, epilogue fused); bias=False:
+        no bias, a tensor: that bias.  The packed weight is cached per weight storage."""
         c = self.conv
         w = c.weight
         key = (w.data_ptr(), w._version, w.device)
@@ -178,8 +185,17 @@ class _FusedConv(nn.Module):
         if cache is None or cache[0] != key:
             cache = (key, K.pack_conv_f32x6(w))
             self.__dict__["_x6"] = cache
-        return K.conv2d_f32x6(x, cache[1], self.bias_f32() if bias else None, c.kernel_size, c.stride[0],
-                              c.padding[0], relu=relu, res=res)
+        if isinstance(bias, torch.Tensor):
+            b = bias
+        else:
+            b = self.bias_f32() if bias else None
+        return K.conv2d_f32x6(x, cache[1], b, c.kernel_size, c.stride[0], c.padding[0], relu=relu, res=res)
+
+    def s1(self, x, relu, res=None, bias=None):
+        """A stride-1 3x3 conv of the f32 trunk: implicit GEMM (s1_gemm_ok) or fused Winograd."""
+        if self.s1_gemm_ok():
+            return self.x6(x, relu, res=res, bias=True if bias is None else bias)
+        return self.wino(x, relu, res=res, bias=bias)
 
     # bench.py's Winograd probe: a list to which wino() appends (shape, tile, HIP events around the
     # launch) on the current stream; None = no events
@@ -216,8 +232,8 @@ class _FusedBlock(nn.Module):
     def forward(self, x):
         if x.dtype == torch.float32 and self.F32_CONV == "winograd" and self.c2.wino_ok():
             if self.down is None and self.c1.wino_ok():
-                y = self.c1.wino(x, relu=True)
-                return self.c2.wino(y, relu=True, res=x)
+                y = self.c1.s1(x, relu=True)
+                return self.c2.s1(y, relu=True, res=x)
             if self.down is not None:
                 # stride-2 c1 and the 1x1 downsample: rmbx_conv2d_f32x6 (RMBX_F32_CONV_S2 = "x6",
                 # the default) or MIOpen + the epilogue pass ("miopen"); c2 (stride 1) adds the
@@ -228,7 +244,7 @@ class _FusedBlock(nn.Module):
                 else:
                     y = self.c1(x)
                     d = self.down.conv_nobias(x)
-                return self.c2.wino(y, relu=True, res=d, bias=self._bias_sum())
+                return self.c2.s1(y, relu=True, res=d, bias=self._bias_sum())
         if x.dtype == torch.bfloat16 and self.c2.conv.out_channels <= self.RMBX_CONV_MAX_COUT:
             y = self.c1.rmbx(x, relu=True)
             idt = x if self.down is None else self.down.rmbx(x, relu=False)
