@@ -207,6 +207,9 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
     bsrc[t] = g.W + p * g.wps + (long long)(n0 + row) * g.ldw + sl * 8;
   }
   auto stage_b = [&](int kt, int buf) {
+    if constexpr ((VAR & 512) != 0) {  // phase skip (timing only): no W DMA after the first stage
+      if (kt > 0) return;
+    }
     unsigned char* base = smem + buf * STAGE + A_BYTES;
 #pragma unroll
     for (int t = 0; t < PC; ++t) glds16(bsrc[t] + kt * GM_BK, base + (wave * PC + t) * 1024);
@@ -231,6 +234,9 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
   }
   // returns the in-image flags of the two rows (bit r)
   auto load_a = [&](float4 (&R)[4], int kt) -> int {
+    if constexpr ((VAR & 256) != 0) {  // phase skip (timing only): no A loads after the first two
+      if (kt > 1) return 3;
+    }
     if constexpr (!CONV) {
       const float4* p0 = (const float4*)(ag0 + kt * GM_BK);
       const float4* p1 = (const float4*)(ag1 + kt * GM_BK);
@@ -272,6 +278,13 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
       uint32_t h[8], l[8];
 #pragma unroll
       for (int i = 0; i < 4; ++i) {
+        if constexpr ((VAR & 32) != 0) {  // phase skip (timing only): raw bits, no split, no range check
+          h[2 * i] = __builtin_amdgcn_perm(__float_as_uint(R[i].y), __float_as_uint(R[i].x), 0x07060302u);
+          h[2 * i + 1] = __builtin_amdgcn_perm(__float_as_uint(R[i].w), __float_as_uint(R[i].z), 0x07060302u);
+          l[2 * i] = h[2 * i + 1];
+          l[2 * i + 1] = h[2 * i];
+          continue;
+        }
         if constexpr (decltype(scaled)::value) {
           const float sc = i < 2 ? as0 : as1;
           R[i].x *= sc;
@@ -597,10 +610,19 @@ void launch_gemm(long long blocks, const GemmArgs& g, hipStream_t st) {
                       ((uintptr_t)g.C | (uintptr_t)g.res | (uintptr_t)g.bias | (uintptr_t)g.ws) % 16 == 0 &&
                       (g.batch <= 1 || (g.c_bs % 4 == 0 && g.ws_bs % 4 == 0));
   if constexpr (PC == 2) {
-    if (vec_ok)
-      hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 16, 2>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g);
-    else
-      hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 0, 2>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g);
+    // RMBX_GEMM_VAR (profiling, linear only): 16 | phase skips 32 (no split), 256 (no A loads),
+    // 512 (no W DMA) -- wrong results, timing only
+    const char* ve = CONV ? nullptr : getenv("RMBX_GEMM_VAR");
+    const int var = ve && vec_ok ? atoi(ve) : (vec_ok ? 16 : 0);
+    switch (var) {
+      case 0: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 0, 2>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
+      case 48: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 48, 2>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
+      case 272: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 272, 2>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
+      case 528: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 528, 2>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
+      case 784: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 784, 2>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
+      case 816: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 816, 2>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
+      default: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 16, 2>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g);
+    }
     return;
   } else {
     // (the environment is read per launch, so a test or a profile can compare the forms in one process)

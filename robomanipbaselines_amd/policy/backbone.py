@@ -168,8 +168,11 @@ class _FusedConv(nn.Module):
                 and K.conv2d_f32x6_supported(c.in_channels, c.out_channels))
 
     # stride-1 3x3 convs whose output width is in this set run as the fp32-accurate implicit GEMM
-    # (x6 below, f16x3 pieces) instead of the fused f32 Winograd; env RMBX_S1_GEMM ("" = none)
-    S1_GEMM_CHANNELS = tuple(int(c) for c in os.environ.get("RMBX_S1_GEMM", "").split(",") if c)
+    # (x6 below, f16x3 pieces) instead of the fused f32 Winograd: at 128 channels (60 x 80, 1024
+    # frames) 5.1 vs 6.3 ms per conv, 18,559 vs 18,178 env-steps/s
+    # (profiles/r4_bench_s1gemm128_ab.log); the 64-channel layer needs N % 128 == 0 tiles, so it
+    # stays on the Winograd kernel; env RMBX_S1_GEMM ("" = none)
+    S1_GEMM_CHANNELS = tuple(int(c) for c in os.environ.get("RMBX_S1_GEMM", "128").split(",") if c)
 
     def s1_gemm_ok(self):
         return (self.conv.out_channels in self.S1_GEMM_CHANNELS and K.F32_PIECES == "f16x3" and self.x6_ok())
