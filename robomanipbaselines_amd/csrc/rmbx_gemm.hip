@@ -32,24 +32,27 @@
 //
 // f16x3 form (PC = 2, rmbx_linear_f16x3 / _batched / rmbx_conv2d_f16x3): the same kernel with two
 // f16 pieces per operand (11 significant bits each) and three products on
-// v_mfma_f32_16x16x32_f16 (the bf16 rate):
+// v_mfma_f32_16x16x32_f16 (the bf16 rate), all accumulated in one f32 accumulator:
 //
-//   x = hi + 2^-11 lo,  hi = f16(x), lo = f16((x - hi) 2^11)      (|x - hi - 2^-11 lo| <= 2^-22 |x|)
-//   a.b ~ hi_a hi_b + 2^-11 (hi_a lo_b + lo_a hi_b)                 (dropped term <= 2^-22 |ab|)
+//   W row n scaled by a power of two s_n (max |w s_n| in [2^13, 2^14)):
+//     w' = w s_n = hb + lb,          hb = f16(w'), lb = f16(w' - hb)
+//   a = ha + 2^-11 la,               ha = f16(a),  la = f16((a - ha) 2^11)
+//   a.w' ~ ha hb + ha lb + la (2^-11 hb)                         (dropped term <= 2^-22 |a w'|)
 //
-// (the split of Ootomo & Yokota, IJHPCA 2022: the low piece is carried scaled by 2^11 so it stays
-// in f16's normal range, and the two product groups accumulate in separate f32 accumulators,
-// joined as acc + 2^-11 cor in the epilogue).  Each piece product is exact in f32 (11 x 11 bits),
-// so the error is the f32 accumulation plus <= ~3 * 2^-22 relative per term: measured below
-// hipBLASLt's f32 GEMM against an f64 product at every tested shape (tests/test_gemm_gpu.py).
-// Three products instead of six: half the MFMA work of bf16x6.  f16's exponent range is the
-// price, handled exactly: W rows are scaled by a power of two at packing (rmbx_split_f16x2: row
-// max in [2^13, 2^14), the inverse applied per output column in the epilogue), and every block
-// tracks the largest |a| of each of its rows; a row whose max lies outside [2^-6, 2^15] (values
-// that would overflow f16 or sit in its subnormal range) is split again as a * 2^s with s putting
-// its max in [2^13, 2^14) and its result scaled back by 2^-s (powers of two: exact): the block
-// re-runs its K loop with the other rows at scale 1 (bit-identical to the first pass), so every
-// row's result depends on that row alone (batch invariance).
+// a's low piece is carried scaled by 2^11 so it stays in f16's normal range (the split of Ootomo &
+// Yokota, IJHPCA 2022), and the scale is undone on W's side: 2^-11 hb is formed in registers
+// (v_pk_mul_f16, exact for |hb| >= 2^-3, i.e. every element above 2^-16 of its row's max; smaller
+// ones round to f16 subnormals, 2^-38 of the row max), so the three products share one
+// accumulator.  Each piece product is exact in f32 (11 x 11 bits): the error is the f32
+// accumulation plus <= ~3 * 2^-22 relative per term, measured below hipBLASLt's f32 GEMM against
+// an f64 product at every tested shape (tests/test_gemm_gpu.py).  Three products instead of six:
+// half the MFMA work of bf16x6.  f16's exponent range is handled exactly: W by the row scales
+// (packed once, rmbx_split_f16x2; 1 / s_n applied per output column in the epilogue), a by a
+// per-row check: every block tracks the largest |a| of each of its rows, and a row whose max lies
+// outside [2^-6, 2^15] (values that would overflow f16 or sit in its subnormal range) is split
+// again as a 2^t with t putting its max in [2^13, 2^14), its result scaled back by 2^-t (powers
+// of two: exact): the block re-runs its K loop with the other rows at scale 1 (bit-identical to
+// the first pass), so every row's result depends on that row alone (batch invariance).
 #include "rmbx_common.h"
 
 #include <cstdint>
@@ -123,11 +126,18 @@ __device__ __forceinline__ uint32_t pk_f16(float x, float y) {
 }
 
 // (x, y) -> packed f16 pairs hi = f16(x), lo = f16((x - hi) 2^11): x = hi + 2^-11 lo to 2^-22 |x|
-// for 2^-14 <= |x| <= 65504
+// for 2^-14 <= |x| <= 65504 (the activation split)
 __device__ __forceinline__ void split_f16_pair(float x, float y, uint32_t& h, uint32_t& l) {
   h = pk_f16(x, y);
   const f16x2v hv = __builtin_bit_cast(f16x2v, h);
   l = pk_f16((x - (float)hv[0]) * 2048.f, (y - (float)hv[1]) * 2048.f);
+}
+
+// x -> hi = f16(x), lo = f16(x - hi) (the weight split, on rows scaled to max |x| in [2^13, 2^14))
+__device__ __forceinline__ void split_f16_w(float x, uint16_t& h, uint16_t& l) {
+  const _Float16 hv = (_Float16)x;
+  h = __builtin_bit_cast(uint16_t, hv);
+  l = __builtin_bit_cast(uint16_t, (_Float16)(x - (float)hv));
 }
 
 // LDS-DMA of 16 bytes per lane: the wave's 64 x 16 B land contiguously at the wave-uniform LDS
@@ -146,6 +156,27 @@ __device__ __forceinline__ void glds16(const void* gsrc, const void* lds_dst) {
 template <int N>
 __device__ __forceinline__ void wait_vm() {
   asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N) : "memory");
+}
+
+// 16-byte global load hidden from hipcc's wait insertion: the A staging loads and the W LDS-DMA
+// are all inline asm and counted by hand (hipcc does not count an asm LDS-DMA, and its own waits
+// for the register loads around it either drained the DMA at the top of every K step or pulled
+// the loads behind the MFMAs).  The destination is named "+v" by the wait that retires it
+// (wait_vm_regs), so nothing reads it before the data has landed.
+__device__ __forceinline__ void gload16(float4& r, const void* p) {
+  f32x4v v;
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=v"(v) : "v"(p) : "memory");
+  r = __builtin_bit_cast(float4, v);
+}
+template <int N>
+__device__ __forceinline__ void wait_vm_regs(float4 (&R)[4]) {
+  f32x4v v0 = __builtin_bit_cast(f32x4v, R[0]), v1 = __builtin_bit_cast(f32x4v, R[1]);
+  f32x4v v2 = __builtin_bit_cast(f32x4v, R[2]), v3 = __builtin_bit_cast(f32x4v, R[3]);
+  asm volatile("s_waitcnt vmcnt(%4)" : "+v"(v0), "+v"(v1), "+v"(v2), "+v"(v3) : "n"(N) : "memory");
+  R[0] = __builtin_bit_cast(float4, v0);
+  R[1] = __builtin_bit_cast(float4, v1);
+  R[2] = __builtin_bit_cast(float4, v2);
+  R[3] = __builtin_bit_cast(float4, v3);
 }
 
 // VAR (profiling, RMBX_GEMM_VAR): bit 0 = s_setprio(1) around each MFMA half-step, bits 1-2 = row
@@ -240,10 +271,10 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
     if constexpr (!CONV) {
       const float4* p0 = (const float4*)(ag0 + kt * GM_BK);
       const float4* p1 = (const float4*)(ag1 + kt * GM_BK);
-      R[0] = p0[0];
-      R[1] = p0[1];
-      R[2] = p1[0];
-      R[3] = p1[1];
+      gload16(R[0], p0);
+      gload16(R[1], p0 + 1);
+      gload16(R[2], p1);
+      gload16(R[3], p1 + 1);
       return 3;
     } else {
       const int k0 = kt * GM_BK;
@@ -254,8 +285,8 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
       for (int r2 = 0; r2 < 2; ++r2) {
         const bool v = (unsigned)(cy[r2] + ky) < (unsigned)g.ih && (unsigned)(cx[r2] + kx) < (unsigned)g.iw;
         const float4* p = (const float4*)(g.A + (v ? cbase[r2] + (long long)(ky * g.iw + kx) * g.ic + c0 : 0));
-        R[2 * r2] = p[0];
-        R[2 * r2 + 1] = p[1];
+        gload16(R[2 * r2], p);
+        gload16(R[2 * r2 + 1], p + 1);
         ok |= (int)v << r2;
       }
       return ok;
@@ -329,17 +360,13 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
     }
   };
 
-  // wave (wm, wn) owns rows 64 wm.., columns 64 wn..: 4 x 4 accumulators of 16 x 16 (f16x3: a
-  // second set for the 2^-11-scaled cross products)
-  f32x4v acc[4][4], cor[4][4];
+  // wave (wm, wn) owns rows 64 wm.., columns 64 wn..: 4 x 4 accumulators of 16 x 16
+  f32x4v acc[4][4];
   auto zero_acc = [&]() {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        acc[i][j] = (f32x4v){0.f, 0.f, 0.f, 0.f};
-        if constexpr (PC == 2) cor[i][j] = (f32x4v){0.f, 0.f, 0.f, 0.f};
-      }
+      for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4v){0.f, 0.f, 0.f, 0.f};
   };
   zero_acc();
 
@@ -348,7 +375,7 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
   auto frag_off = [&](int row) { return row * 64 + ((fs ^ ((row >> 2) & 2)) << 4); };
   // half h of a K step: m-tiles 2h, 2h+1 against all four n-tiles (bf16x6: 48 MFMAs, small
   // terms first; f16x3: 24)
-  auto half_step = [&](int buf, int h, const bf16x8 (&b)[4][PC]) {
+  auto half_step = [&](int buf, int h, const bf16x8 (&b)[4][PC], const f16x8 (&bs)[4]) {
     const unsigned char* As = smem + buf * STAGE;
     bf16x8 a[2][PC];
 #pragma unroll
@@ -364,11 +391,11 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
         if constexpr (PC == 2) {
           const f16x8 ah = __builtin_bit_cast(f16x8, a[i][0]), al = __builtin_bit_cast(f16x8, a[i][1]);
           const f16x8 bh = __builtin_bit_cast(f16x8, b[nj][0]), bl = __builtin_bit_cast(f16x8, b[nj][1]);
-          f32x4v c = cor[2 * h + i][nj];
-          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bh, c, 0, 0, 0);
+          f32x4v c = acc[2 * h + i][nj];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bs[nj], c, 0, 0, 0);  // small terms first
           c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bl, c, 0, 0, 0);
-          cor[2 * h + i][nj] = c;
-          acc[2 * h + i][nj] = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, acc[2 * h + i][nj], 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, bh, c, 0, 0, 0);
+          acc[2 * h + i][nj] = c;
         } else {
           f32x4v c = acc[2 * h + i][nj];
           c = __builtin_amdgcn_mfma_f32_16x16x32_bf16(a[i][2], b[nj][0], c, 0, 0, 0);
@@ -394,9 +421,9 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
   // K steps of 32, two LDS stages, one barrier per step.  Step kt computes stage kt while W of
   // kt + 1 arrives by LDS-DMA, A of kt + 1 (loaded during step kt - 1) is split and stored between
   // the step's two MFMA halves, and A of kt + 2 is loaded into registers.  Issue order per step:
-  // W DMA, then the A loads, so the counted wait at the end (vmcnt(4): the 4 A loads of kt + 2 may
-  // stay in flight) retires the W DMA; hipcc's own wait before the split (for A of kt + 1) is at
-  // least as strict.
+  // W DMA (PC pieces), then the 4 A loads; every step issues both (the last step's are redundant
+  // copies of the last K step into the idle stage), so the hand counts are fixed: the split waits
+  // for A of kt + 1 with vmcnt(PC + 4), the end of the step for the W DMA with vmcnt(4).
   const int KT = g.K / GM_BK;
   auto k_loop = [&](auto scaled) {
     float4 Ra[4], Rb[4];
@@ -404,35 +431,47 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
     oka = load_a(Ra, 0);
     stage_b(0, 0);
     okb = load_a(Rb, min(1, KT - 1));
+    wait_vm_regs<PC + 4>(Ra);
     store_a(Ra, oka, 0, scaled);
     wait_vm<4>();
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     auto step = [&](int kt, float4 (&Rcur)[4], int& okcur, float4 (&Rnext)[4], int& oknext) {
       const int buf = kt & 1;
       const bool more = kt + 1 < KT;
-      if (more) stage_b(kt + 1, buf ^ 1);
-      oknext = load_a(Rnext, min(kt + 2, KT - 1));  // unconditional (a redundant reload at the end) so that
-                                                   // hipcc's wait before the split stays counted
+      stage_b(min(kt + 1, KT - 1), buf ^ 1);
+      oknext = load_a(Rnext, min(kt + 2, KT - 1));
       bf16x8 b[4][PC];
       read_b(b, buf);
-      const bool late = (VAR & 64) == 0 || wave < 4;
-      if (more && !late) store_a(Rcur, okcur, buf ^ 1, scaled);
-      if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(1);
-      half_step(buf, 0, b);
-      if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(0);
-      if (more && late) store_a(Rcur, okcur, buf ^ 1, scaled);
-      if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(1);
-      half_step(buf, 1, b);
-      if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(0);
-      if (more) {
-        wait_vm<4>();
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      f16x8 bs[4];  // f16x3: 2^-11 hb (exact above f16's subnormal range)
+#pragma unroll
+      for (int nj = 0; nj < 4; ++nj) {
+        if constexpr (PC == 2) bs[nj] = __builtin_bit_cast(f16x8, b[nj][0]) * (_Float16)0.00048828125f;
       }
+      const bool late = (VAR & 64) == 0 || wave < 4;
+      if (!late) {
+        wait_vm_regs<PC + 4>(Rcur);
+        store_a(Rcur, okcur, buf ^ 1, scaled);
+      }
+      if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(1);
+      half_step(buf, 0, b, bs);
+      if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(0);
+      if (late) {
+        wait_vm_regs<PC + 4>(Rcur);
+        store_a(Rcur, okcur, buf ^ 1, scaled);
+      }
+      if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(1);
+      half_step(buf, 1, b, bs);
+      if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(0);
+      wait_vm<4>();
+      if (more) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     };
     for (int kt = 0; kt < KT; kt += 2) {
       step(kt, Rb, okb, Ra, oka);
       if (kt + 1 < KT) step(kt + 1, Ra, oka, Rb, okb);
     }
+    // drain the last step's redundant loads (their registers are free after this) and DMA
+    wait_vm_regs<0>(Ra);
+    wait_vm_regs<0>(Rb);
   };
   k_loop(std::false_type{});
 
@@ -476,13 +515,7 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
       zero_acc();
       k_loop(std::true_type{});
     }
-    // join the product groups: acc + 2^-11 cor, then undo the rows' pass-1 scales (powers of two)
-#pragma unroll
-    for (int i = 0; i < 4; ++i)
-#pragma unroll
-      for (int j = 0; j < 4; ++j)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) acc[i][j][e] = fmaf(cor[i][j][e], 0.00048828125f, acc[i][j][e]);
+    // undo the rows' pass-1 scales (powers of two)
     if (any) {
 #pragma unroll
       for (int i = 0; i < 4; ++i)
@@ -575,8 +608,8 @@ __global__ void split_bf16x3_kernel(const float* __restrict__ x, uint16_t* __res
 }
 
 // one block per weight row n: s = 2^(14 - e) with max_k |w[n][k]| = f 2^e (f in [0.5, 1)), so the
-// scaled row's max lies in [2^13, 2^14); planes [2][N][K] = f16 hi / lo pieces of w s, scale[n] =
-// 1 / s (an all-zero or non-finite row keeps s = 1)
+// scaled row's max lies in [2^13, 2^14); planes [2][N][K] = f16 hi = f16(w s), lo = f16(w s - hi),
+// scale[n] = 1 / s (an all-zero or non-finite row keeps s = 1)
 __global__ void __launch_bounds__(256) split_f16x2_kernel(const float* __restrict__ w, int K, long long plane,
                                                           uint16_t* __restrict__ planes, float* __restrict__ scale) {
   __shared__ float red[4];
@@ -594,10 +627,10 @@ __global__ void __launch_bounds__(256) split_f16x2_kernel(const float* __restric
   const float s = ldexpf(1.f, 14 - e);
   if (tid == 0) scale[n] = ldexpf(1.f, e - 14);
   for (int k = tid; k < K; k += 256) {
-    uint32_t h, l;
-    split_f16_pair(row[k] * s, 0.f, h, l);
-    planes[(long long)n * K + k] = (uint16_t)(h & 0xffff);
-    planes[plane + (long long)n * K + k] = (uint16_t)(l & 0xffff);
+    uint16_t h, l;
+    split_f16_w(row[k] * s, h, l);
+    planes[(long long)n * K + k] = h;
+    planes[plane + (long long)n * K + k] = l;
   }
 }
 

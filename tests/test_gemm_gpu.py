@@ -45,9 +45,9 @@ def _pack(form):
 
 @torch.no_grad()
 def test_split_f16x2_pieces_and_scales():
-    """W[n] = scale[n] (hi + 2^-11 lo) to 2^-22 of each element (2^-36 of the row max below f16's
-    normal range), scale[n] a power of two with the scaled row max in [2^13, 2^14); zero rows keep
-    scale 1."""
+    """W[n] = scale[n] (hi + lo) to 2^-22 of each element (2^-36 of the row max for elements below
+    2^-16 of it, whose low piece is an f16 subnormal), scale[n] a power of two with the scaled row
+    max in [2^13, 2^14); zero rows keep scale 1."""
     from robomanipbaselines_amd import kernels as K_
 
     g = torch.Generator(device="cpu").manual_seed(1)
@@ -57,7 +57,7 @@ def test_split_f16x2_pieces_and_scales():
     p = K_.split_f16x2(w.to(DEV))
     assert p.planes.shape == (2, 64, 300) and p.planes.dtype == torch.float16 and p.scale.shape == (64,)
     hi, lo, sc = p.planes[0].double().cpu(), p.planes[1].double().cpu(), p.scale.double().cpu()
-    rec = sc[:, None] * (hi + lo / 2048)
+    rec = sc[:, None] * (hi + lo)
     wd = w.double()
     rowmax = wd.abs().amax(1, keepdim=True)
     assert ((rec - wd).abs() <= wd.abs() * 2.0 ** -22 + rowmax * 2.0 ** -36).all()
