@@ -401,6 +401,12 @@ int rmbx_stem_s2d_conv_maxpool_f32(const float* in, const float* weight, const f
  * normalisation (RolloutBase.py:479-490, the ACT backbone's ImageNet Normalize). */
 int rmbx_stem_s2d_conv_maxpool_u8(const uint8_t* in, const void* w_planes, const float* bias, const float* edge,
                                   float* out, int N, int Hs, int Ws, int band_rows, void* stream);
+/* The same stem in the f16 form: w_planes [2 pieces][64][16 taps][16] f16 bits of W / (255 std) * 2^s
+ * (hi = f16(x), lo = f16(x - hi); one power of two for the whole bank, max in [2^13, 2^14)) and
+ * wscale = 2^-s: the integer pixels times the two pieces on the f16 matrix cores, one accumulator,
+ * scaled by wscale before bias_eff / edge (2 MFMAs per tap instead of 3; weights to 2^-22). */
+int rmbx_stem_s2d_conv_maxpool_u8h(const uint8_t* in, const void* w_planes, float wscale, const float* bias,
+                                   const float* edge, float* out, int N, int Hs, int Ws, int band_rows, void* stream);
 /* Multi-head attention forward, bf16: out[b][i][h*64 + d] = sum_j softmax_j(scale * q_i . k_j) v_j[d]
  * over the heads of q/k/v rows [b][row][h*64 .. h*64+63] (row/batch strides in elements, last dim
  * contiguous), f32 softmax and accumulation, head dim 64, Lk <= 320, no mask; out contiguous

@@ -62,6 +62,7 @@ SIGNATURES = {
     "rmbx_stem_s2d_conv_maxpool": (_c_int, [_c_p] * 4 + [_c_int] * 4 + [_c_p]),
     "rmbx_stem_s2d_conv_maxpool_f32": (_c_int, [_c_p] * 4 + [_c_int] * 4 + [_c_p]),
     "rmbx_stem_s2d_conv_maxpool_u8": (_c_int, [_c_p] * 5 + [_c_int] * 4 + [_c_p]),
+    "rmbx_stem_s2d_conv_maxpool_u8h": (_c_int, [_c_p, _c_p, ctypes.c_float] + [_c_p] * 3 + [_c_int] * 4 + [_c_p]),
     "rmbx_attention_bf16": (_c_int, [_c_p] * 4 + [_c_int] * 4 + [ctypes.c_longlong, _c_int] * 3 + [ctypes.c_float, _c_p]),
     "rmbx_attention_f32": (_c_int, [_c_p] * 4 + [_c_int] * 4 + [ctypes.c_longlong, _c_int] * 3 + [ctypes.c_float, _c_p]),
     "rmbx_attention_f32x6": (_c_int, [_c_p] * 4 + [_c_int] * 4 + [ctypes.c_longlong, _c_int] * 3 + [ctypes.c_float, _c_p]),

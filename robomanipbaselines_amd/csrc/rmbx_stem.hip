@@ -38,6 +38,8 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x8s __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2s __attribute__((ext_vector_type(2)));
 
 constexpr int SP_MAX_WAVES = 10;               // stem columns <= 320
 constexpr int SP_THREADS = 64 * SP_MAX_WAVES;  // launch bound
@@ -491,7 +493,8 @@ static_assert(SQ_LDS_BYTES <= 160 * 1024, "u8 stem+pool LDS must fit the 160 KiB
 
 struct StemPoolU8Args {
   const uint8_t* in;    // [N][Hs][Ws][16] u8
-  const uint16_t* w;    // [3 pieces][64][16 taps][16] bf16 bits
+  const uint16_t* w;    // [3 pieces][64][16 taps][16] bf16 bits (f16 form: [2 pieces] f16 bits)
+  float wscale;         // f16 form: the factor undoing the weights' power-of-two scale
   const float* bias;    // [64] bias_eff
   const float* edge;    // [16 rm][16 cm][64]
   float* out;           // [N][Hp][Wp][64]
@@ -717,12 +720,33 @@ __device__ __forceinline__ float dpp_from_right(float x) {
   return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x130, 0xf, 0xf, false));
 }
 
-template <bool DPP>
+// 16 u8 pixel channels -> two 16-B halves of the CENTRED f16 integers u - 128 (exact)
+__device__ __forceinline__ void u8x16_to_f16(uint4 v, bool ok, uint4& lo, uint4& hi) {
+  uint32_t o[8];
+  const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const f32x2 p0 = {(float)((int)(w[i] & 0xffu) - 128), (float)((int)((w[i] >> 8) & 0xffu) - 128)};
+    const f32x2 p1 = {(float)((int)((w[i] >> 16) & 0xffu) - 128), (float)((int)(w[i] >> 24) - 128)};
+    o[2 * i] = __builtin_bit_cast(uint32_t, __builtin_convertvector(p0, f16x2s));
+    o[2 * i + 1] = __builtin_bit_cast(uint32_t, __builtin_convertvector(p1, f16x2s));
+  }
+  lo = ok ? make_uint4(o[0], o[1], o[2], o[3]) : make_uint4(0, 0, 0, 0);
+  hi = ok ? make_uint4(o[4], o[5], o[6], o[7]) : make_uint4(0, 0, 0, 0);
+}
+
+// H2 (the default): the f16 form -- the integer pixels (exact in f16) times two f16 pieces of
+// W W' 2^s (hi = f16(x), lo = f16(x - hi), one power of two s for the whole filter bank putting
+// its max in [2^13, 2^14)), both products in one accumulator on v_mfma_f32_32x32x16_f16 and the
+// accumulator scaled by 2^-s before the bias: 2 MFMAs per tap and tile instead of 3, weights
+// represented to 2^-22 (the f16x3 GEMM's weight split, csrc/rmbx_gemm.hip)
+template <bool DPP, bool H2 = false>
 __global__ void __launch_bounds__(SF_THREADS) stem_pool_u8w4_kernel(StemPoolU8Args a) {
-  __shared__ __attribute__((aligned(16))) unsigned char sq_smem[16 * 3 * 2 * 64 * 16 + SP_RING * 2 * SF_RC * 16 + 64 * 4 +
-                                                               SF_WAVES * 2 * 16 * 4];
-  uint16_t* sW = reinterpret_cast<uint16_t*>(sq_smem);  // [16 taps][3 pieces][2 halves][64 cout][8]
-  uint16_t* sR = sW + 16 * 3 * 2 * 64 * 8;              // [5 slots][2 halves][SF_RC][8]
+  constexpr int NP = H2 ? 2 : 3;  // weight pieces
+  __shared__ __attribute__((aligned(16))) unsigned char sq_smem[16 * NP * 2 * 64 * 16 + SP_RING * 2 * SF_RC * 16 +
+                                                               64 * 4 + SF_WAVES * 2 * 16 * 4];
+  uint16_t* sW = reinterpret_cast<uint16_t*>(sq_smem);  // [16 taps][NP pieces][2 halves][64 cout][8]
+  uint16_t* sR = sW + 16 * NP * 2 * 64 * 8;             // [5 slots][2 halves][SF_RC][8]
   float* sBias = reinterpret_cast<float*>(sR + SP_RING * 2 * SF_RC * 8);  // [64]
   float* sEdge = sBias + 64;                                              // [waves][2 h][16]
 
@@ -735,18 +759,21 @@ __global__ void __launch_bounds__(SF_THREADS) stem_pool_u8w4_kernel(StemPoolU8Ar
   const size_t row_px = (size_t)a.Ws;
   const uint8_t* in_img = a.in + (size_t)img * a.Hs * row_px * 16;
 
-  for (int q = tid; q < 3 * 64 * 16 * 2; q += SF_THREADS) {
+  for (int q = tid; q < NP * 64 * 16 * 2; q += SF_THREADS) {
     const int half = q & 1, rest = q >> 1;
     const int tap = rest & 15, pc = rest >> 4;
     const int co = pc & 63, p = pc >> 6;
-    *reinterpret_cast<uint4*>(sW + (((tap * 3 + p) * 2 + half) * 64 + co) * 8) =
+    *reinterpret_cast<uint4*>(sW + (((tap * NP + p) * 2 + half) * 64 + co) * 8) =
         *reinterpret_cast<const uint4*>(a.w + (size_t)rest * 16 + half * 8);
   }
   if (tid < 64) sBias[tid] = a.bias[tid];
 
   auto store_px = [&](int slot, int c, uint4 v, bool ok) {
     uint4 lo, hi;
-    u8x16_to_bf16(v, ok, lo, hi);
+    if constexpr (H2)
+      u8x16_to_f16(v, ok, lo, hi);
+    else
+      u8x16_to_bf16(v, ok, lo, hi);
     *reinterpret_cast<uint4*>(sR + ((size_t)(slot * 2) * SF_RC + c) * 8) = lo;
     *reinterpret_cast<uint4*>(sR + ((size_t)(slot * 2 + 1) * SF_RC + c) * 8) = hi;
   };
@@ -804,10 +831,10 @@ __global__ void __launch_bounds__(SF_THREADS) stem_pool_u8w4_kernel(StemPoolU8Ar
 #pragma unroll
     for (int tap = 0; tap < 16; ++tap) {
       const int ky = tap >> 2, kx = tap & 3;
-      bf16x8 aw[3];
+      bf16x8 aw[NP];
 #pragma unroll
-      for (int p = 0; p < 3; ++p)
-        aw[p] = *reinterpret_cast<const bf16x8*>(sW + (((tap * 3 + p) * 2 + h) * 64 + 32 * t + sig) * 8);
+      for (int p = 0; p < NP; ++p)
+        aw[p] = *reinterpret_cast<const bf16x8*>(sW + (((tap * NP + p) * 2 + h) * 64 + 32 * t + sig) * 8);
 #pragma unroll
       for (int i = 0; i < SF_TILES; ++i) {
         bf16x8 bx[2];
@@ -815,9 +842,15 @@ __global__ void __launch_bounds__(SF_THREADS) stem_pool_u8w4_kernel(StemPoolU8Ar
         for (int r = 0; r < 2; ++r)
           bx[r] = *reinterpret_cast<const bf16x8*>(sR + (((size_t)slot[r + ky] * 2 + h) * SF_RC + xcol + 32 * i + kx) * 8);
 #pragma unroll
-        for (int p = 2; p >= 0; --p)
+        for (int p = NP - 1; p >= 0; --p)
 #pragma unroll
-          for (int r = 0; r < 2; ++r) acc[i][r] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aw[p], bx[r], acc[i][r], 0, 0, 0);
+          for (int r = 0; r < 2; ++r) {
+            if constexpr (H2)
+              acc[i][r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8s, aw[p]),
+                                                                  __builtin_bit_cast(f16x8s, bx[r]), acc[i][r], 0, 0, 0);
+            else
+              acc[i][r] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(aw[p], bx[r], acc[i][r], 0, 0, 0);
+          }
       }
     }
 
@@ -841,7 +874,14 @@ __global__ void __launch_bounds__(SF_THREADS) stem_pool_u8w4_kernel(StemPoolU8Ar
 #pragma unroll
       for (int k = 0; k < 16; ++k) {
         const float b = sBias[32 * t + 16 * h + k];
-        float v0 = acc[i][0][k] + b, v1 = acc[i][1][k] + b;
+        float v0, v1;
+        if constexpr (H2) {  // undo the weights' power of two (exact), then the bias
+          v0 = fmaf(acc[i][0][k], a.wscale, b);
+          v1 = fmaf(acc[i][1][k], a.wscale, b);
+        } else {
+          v0 = acc[i][0][k] + b;
+          v1 = acc[i][1][k] + b;
+        }
         if (ep0) v0 += ep0[k];  // border pixels only
         if (ep1) v1 += ep1[k];
         const float p0 = fmaxf(v0, 0.f);
@@ -937,9 +977,26 @@ extern "C" int rmbx_stem_s2d_conv_maxpool(const void* in, const void* weight, co
   return RMBX_OK;
 }
 
+namespace rmbx {
+int stem_u8_impl(const uint8_t* in, const void* w_planes, float wscale, bool h2, const float* bias, const float* edge,
+                 float* out, int N, int Hs, int Ws, int band_rows, void* stream);
+}  // namespace rmbx
+
 extern "C" int rmbx_stem_s2d_conv_maxpool_u8(const uint8_t* in, const void* w_planes, const float* bias,
                                              const float* edge, float* out, int N, int Hs, int Ws, int band_rows,
                                              void* stream) {
+  return rmbx::stem_u8_impl(in, w_planes, 1.f, false, bias, edge, out, N, Hs, Ws, band_rows, stream);
+}
+
+extern "C" int rmbx_stem_s2d_conv_maxpool_u8h(const uint8_t* in, const void* w_planes, float wscale, const float* bias,
+                                              const float* edge, float* out, int N, int Hs, int Ws, int band_rows,
+                                              void* stream) {
+  RMBX_CHECK_ARG(wscale > 0.f, "rmbx_stem_s2d_conv_maxpool_u8h: wscale must be positive");
+  return rmbx::stem_u8_impl(in, w_planes, wscale, true, bias, edge, out, N, Hs, Ws, band_rows, stream);
+}
+
+int rmbx::stem_u8_impl(const uint8_t* in, const void* w_planes, float wscale, bool h2, const float* bias,
+                       const float* edge, float* out, int N, int Hs, int Ws, int band_rows, void* stream) {
   RMBX_CHECK_ARG(in && w_planes && bias && edge && out, "rmbx_stem_s2d_conv_maxpool_u8: null pointer");
   RMBX_CHECK_ARG(N >= 0 && Hs > 0 && Ws > 0, "rmbx_stem_s2d_conv_maxpool_u8: bad geometry");
   RMBX_CHECK_ARG(Ws <= 32 * rmbx::SP_MAX_WAVES, "rmbx_stem_s2d_conv_maxpool_u8: Ws=%d exceeds %d", Ws,
@@ -950,6 +1007,7 @@ extern "C" int rmbx_stem_s2d_conv_maxpool_u8(const uint8_t* in, const void* w_pl
   rmbx::StemPoolU8Args a;
   a.in = in;
   a.w = (const uint16_t*)w_planes;
+  a.wscale = wscale;
   a.bias = bias;
   a.edge = edge;
   a.out = out;
@@ -982,7 +1040,10 @@ extern "C" int rmbx_stem_s2d_conv_maxpool_u8(const uint8_t* in, const void* w_pl
   a.bands = (a.Hp + band_rows - 1) / band_rows;
   const long long nblocks = (long long)N * a.bands;
   RMBX_CHECK_ARG(nblocks < (1ll << 31), "rmbx_stem_s2d_conv_maxpool_u8: grid too large");
-  if (layout == 10)
+  if (h2)
+    hipLaunchKernelGGL((rmbx::stem_pool_u8w4_kernel<true, true>), dim3((unsigned)nblocks), dim3(rmbx::SF_THREADS), 0,
+                       (hipStream_t)stream, a);
+  else if (layout == 10)
     hipLaunchKernelGGL(rmbx::stem_pool_u8_kernel, dim3((unsigned)nblocks), dim3(64 * a.nct), 0, (hipStream_t)stream, a);
   else if (dpp)
     hipLaunchKernelGGL(rmbx::stem_pool_u8w4_kernel<true>, dim3((unsigned)nblocks), dim3(rmbx::SF_THREADS), 0,

@@ -705,13 +705,25 @@ def _stem_s2d_conv_maxpool_f32(x_s2d, w_packed, bias, band_rows=0):
     return out
 
 
-def pack_stem_u8(weight, bias, mean, std):
-    """Operands of rmbx_stem_s2d_conv_maxpool_u8 for the folded stem conv (weight [64, 3, 7, 7],
-    bias [64]) and the image normalisation x = (u / 255 - mean) / std = W'(u - 128) + c' (the kernel
-    reads the centred pixels u - 128): the three exact bf16 pieces [3, 64, 16, 16] of
-    W / (255 std) (packed as pack_stem_s2d), bias_eff = bias + sum W c' over every tap with
-    c' = (128 / 255 - mean) / std, and the edge table [16, 16, 64] removing the c' term of the taps
-    that fall outside the image (row mask of ky x column mask of kx).  Constants summed in f64."""
+# piece form of the u8 stem's weights (env RMBX_STEM_U8_PIECES): "f16" = two f16 pieces of the
+# power-of-two-scaled bank on the f16 matrix cores (rmbx_stem_s2d_conv_maxpool_u8h, 2 MFMAs per
+# tap), "bf16" = three exact bf16 pieces (rmbx_stem_s2d_conv_maxpool_u8, 3 MFMAs per tap)
+STEM_U8_PIECES = os.environ.get("RMBX_STEM_U8_PIECES", "f16")
+
+
+def pack_stem_u8(weight, bias, mean, std, pieces=None):
+    """Operands of the u8 stem for the folded stem conv (weight [64, 3, 7, 7], bias [64]) and the
+    image normalisation x = (u / 255 - mean) / std = W'(u - 128) + c' (the kernel reads the
+    centred pixels u - 128): (planes, bias_eff, edge, wscale) with planes the pieces of
+    W / (255 std) (packed as pack_stem_s2d) -- "bf16": three exact bf16 pieces [3, 64, 16, 16],
+    wscale 1; "f16": two f16 pieces [2, 64, 16, 16] of the bank times 2^s (max in [2^13, 2^14),
+    hi = f16(x), lo = f16(x - hi), x represented to 2^-22) and wscale = 2^-s -- bias_eff = bias +
+    sum W c' over every tap with c' = (128 / 255 - mean) / std, and the edge table [16, 16, 64]
+    removing the c' term of the taps that fall outside the image (row mask of ky x column mask of
+    kx).  Constants summed in f64."""
+    pieces = STEM_U8_PIECES if pieces is None else pieces
+    if pieces not in ("f16", "bf16"):
+        raise ValueError(f"pack_stem_u8: pieces must be f16 or bf16, not {pieces!r}")
     dev = weight.device
     wp = pack_stem_s2d(weight.detach().double())  # [64, 4, 4, 16]
     mean = torch.tensor(mean, dtype=torch.float64, device=dev)
@@ -722,12 +734,23 @@ def pack_stem_u8(weight, bias, mean, std):
     # -c' per channel: the constant of the centred pixels, negated (g below is subtracted)
     ms = torch.where(valid, mean[ch % 3] / std[ch % 3] - 128.0 / (255.0 * std[ch % 3]),
                      torch.zeros((), dtype=torch.float64, device=dev))
-    wq = (wp * inv).float()
-    p0 = wq.bfloat16()
-    r = wq - p0.float()  # exact in f32
-    p1 = r.bfloat16()
-    p2 = (r - p1.float()).bfloat16()  # exact: <= 8 significant bits remain
-    planes = torch.stack([p0, p1, p2]).reshape(3, 64, 16, 16).contiguous()
+    if pieces == "bf16":
+        wq = (wp * inv).float()
+        p0 = wq.bfloat16()
+        r = wq - p0.float()  # exact in f32
+        p1 = r.bfloat16()
+        p2 = (r - p1.float()).bfloat16()  # exact: <= 8 significant bits remain
+        planes = torch.stack([p0, p1, p2]).reshape(3, 64, 16, 16).contiguous()
+        wscale = 1.0
+    else:
+        wq = wp * inv  # f64
+        m = float(wq.abs().max())
+        e = int(np.frexp(m)[1]) if m > 0 else 14
+        wq = wq * 2.0 ** (14 - e)  # exact; max in [2^13, 2^14)
+        hi = wq.half()
+        lo = (wq - hi.double()).half()
+        planes = torch.stack([hi, lo]).reshape(2, 64, 16, 16).contiguous()
+        wscale = 2.0 ** (e - 14)
     g = (wp * ms).sum(-1)  # [64, 4, 4] mean term per tap
     bias_eff = (bias.detach().double() - g.sum((1, 2))).float().contiguous()
     bits = torch.arange(16, device=dev)
@@ -735,7 +758,7 @@ def pack_stem_u8(weight, bias, mean, std):
     out_k = ((bits[:, None] >> k4[None, :]) & 1).bool()  # [mask, k]
     sel = (out_k[:, None, :, None] | out_k[None, :, None, :]).double()  # [rm, cm, ky, kx]
     edge = torch.einsum("abyx,cyx->abc", sel, g).float().contiguous()
-    return planes, bias_eff, edge
+    return planes, bias_eff, edge, wscale
 
 
 def s2d_u8_normalize(x_u8, mean, std):
@@ -749,23 +772,34 @@ def s2d_u8_normalize(x_u8, mean, std):
     return torch.where(ch < 12, x, torch.zeros((), device=dev)).contiguous()
 
 
-def stem_s2d_conv_maxpool_u8(x_u8, planes, bias_eff, edge, band_rows=0):
+def stem_s2d_conv_maxpool_u8(x_u8, planes, bias_eff, edge, wscale=1.0, band_rows=0):
     """maxpool3x3/2/pad1(relu(conv1(x) + bias)) for x = (u / 255 - mean) / std on the 8-bit
     space-to-depth image [n, Hs, Ws, 16] u8 (rmbx_render policy_dtype 4) -> channels_last
-    [n, 64, Hp, Wp] f32 (rmbx_stem_s2d_conv_maxpool_u8; operands from pack_stem_u8)."""
+    [n, 64, Hp, Wp] f32 (rmbx_stem_s2d_conv_maxpool_u8h for f16 planes, rmbx_stem_s2d_conv_maxpool_u8
+    for bf16 ones; operands from pack_stem_u8)."""
     _chk(x_u8, torch.uint8, name="x_u8")
     n, Hs, Ws, c16 = x_u8.shape
     if c16 != 16:
         raise ValueError("x_u8 must be [n, Hs, Ws, 16]")
     if Ws > STEM_POOL_MAX_WS:
         raise ValueError(f"stem_s2d_conv_maxpool_u8: Ws={Ws} exceeds {STEM_POOL_MAX_WS}")
-    _chk(planes, torch.bfloat16, (3, 64, 16, 16), "planes")
+    h2 = isinstance(planes, torch.Tensor) and planes.dtype == torch.float16
+    if h2:
+        _chk(planes, torch.float16, (2, 64, 16, 16), "planes")
+    else:
+        _chk(planes, torch.bfloat16, (3, 64, 16, 16), "planes")
     _chk(bias_eff, torch.float32, (64,), "bias_eff")
     _chk(edge, torch.float32, (16, 16, 64), "edge")
     Hp, Wp = (Hs - 1) // 2 + 1, (Ws - 1) // 2 + 1
     out = torch.empty((n, 64, Hp, Wp), dtype=torch.float32, device=x_u8.device, memory_format=torch.channels_last)
-    N.call("rmbx_stem_s2d_conv_maxpool_u8", N.ptr(x_u8), N.ptr(planes), N.ptr(bias_eff), N.ptr(edge), N.ptr(out),
-           n, Hs, Ws, int(band_rows), N.stream_ptr())
+    if h2:
+        N.call("rmbx_stem_s2d_conv_maxpool_u8h", N.ptr(x_u8), N.ptr(planes), float(wscale), N.ptr(bias_eff),
+               N.ptr(edge), N.ptr(out), n, Hs, Ws, int(band_rows), N.stream_ptr())
+    else:
+        if wscale != 1.0:
+            raise ValueError("stem_s2d_conv_maxpool_u8: bf16 planes take wscale 1")
+        N.call("rmbx_stem_s2d_conv_maxpool_u8", N.ptr(x_u8), N.ptr(planes), N.ptr(bias_eff), N.ptr(edge), N.ptr(out),
+               n, Hs, Ws, int(band_rows), N.stream_ptr())
     return out
 
 

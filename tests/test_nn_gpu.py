@@ -365,14 +365,16 @@ def test_stem_conv_maxpool_f32_matches_fp32_reference(n, H, W, band_rows):
 
 
 @torch.no_grad()
+@pytest.mark.parametrize("pieces", ["f16", "bf16"])
 @pytest.mark.parametrize("n,H,W,band_rows", [(2, 48, 64, 0), (3, 480, 640, 0), (2, 480, 640, 7), (2, 46, 630, 5),
                                              (1, 34, 90, 1), (2, 6, 8, 0)])
-def test_stem_conv_maxpool_u8_matches_fp32_reference(n, H, W, band_rows):
-    """rmbx_stem_s2d_conv_maxpool_u8 (normalisation folded into the stem, bf16 integer pixels x
-    three exact bf16 weight pieces) vs F.conv2d + bias + ReLU + max_pool2d in fp32 on the
-    normalised image x = (u / 255 - mean) / std the renderer would hand over (the border taps
-    exercise the edge table): within f32 rounding, and no worse than the f32 MFMA kernel against
-    an f64 reference on the CPU."""
+def test_stem_conv_maxpool_u8_matches_fp32_reference(pieces, n, H, W, band_rows):
+    """The u8 stem (normalisation folded into the stem, integer pixels x the weight pieces:
+    rmbx_stem_s2d_conv_maxpool_u8h with two f16 pieces of the power-of-two-scaled bank, the default,
+    and rmbx_stem_s2d_conv_maxpool_u8 with three exact bf16 pieces) vs F.conv2d + bias + ReLU +
+    max_pool2d in fp32 on the normalised image x = (u / 255 - mean) / std the renderer would hand
+    over (the border taps exercise the edge table): within f32 rounding, and no worse than the f32
+    MFMA kernel against an f64 reference on the CPU."""
     from robomanipbaselines_amd import kernels as K
 
     mean, std = (0.485, 0.456, 0.406), (0.229, 0.224, 0.225)
@@ -386,13 +388,15 @@ def test_stem_conv_maxpool_u8_matches_fp32_reference(n, H, W, band_rows):
     us2d = K.image_to_s2d(u)
     torch.testing.assert_close(K.s2d_u8_normalize(us2d, mean, std), K.image_to_s2d(x), rtol=0, atol=1e-6)
     want = F.max_pool2d(F.relu(F.conv2d(x, w, b, 2, 3)), 3, 2, 1)
-    got = K.stem_s2d_conv_maxpool_u8(us2d, *K.pack_stem_u8(w, b, mean, std), band_rows=band_rows)
+    ops = K.pack_stem_u8(w, b, mean, std, pieces=pieces)
+    assert ops[0].dtype == (torch.float16 if pieces == "f16" else torch.bfloat16)
+    got = K.stem_s2d_conv_maxpool_u8(us2d, *ops, band_rows=band_rows)
     torch.cuda.synchronize()
     assert got.shape == want.shape and got.dtype == torch.float32
     assert got.is_contiguous(memory_format=torch.channels_last)
     scale = max(1.0, want.abs().max().item())
     err = (got - want).abs().max().item()
-    print(f"\nu8 stem (centred pixels) vs f32 conv: max |d| {err:.3e} = {err / scale:.2e} relative")
+    print(f"\nu8 stem ({pieces} pieces) vs f32 conv: max |d| {err:.3e} = {err / scale:.2e} relative")
     # the centred form: within 5e-6 of the f32 conv (the uncentred form needed 2e-5)
     assert err <= 5e-6 * scale, err
     if n * H * W <= 2 * 48 * 64:  # f64 CPU reference: the u8 form is as close as the f32 kernel
