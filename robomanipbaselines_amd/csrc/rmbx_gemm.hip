@@ -72,19 +72,24 @@ typedef float f32x2v __attribute__((ext_vector_type(2)));
 constexpr int GM_BM = 256, GM_BN = 128, GM_BK = 32;
 constexpr int GM_THREADS = 512;
 constexpr int GM_A_PLANE = GM_BM * GM_BK * 2;            // 16 KiB per 16-bit piece plane
-constexpr int GM_B_PLANE = GM_BN * GM_BK * 2;            // 8 KiB
 constexpr int GM_GROUP = 8;                              // row tiles per block group
-constexpr int GM_EPI_PITCH = 68;                         // LDS epilogue row pitch (floats)
-constexpr int GM_EPI_BYTES = 8 * 64 * GM_EPI_PITCH * 4;  // 136 KiB: eight 64 x 64 wave tiles
-// PC pieces per operand (3: bf16x6, 2: f16x3): one K stage = PC A planes + PC W planes
-template <int PC>
-constexpr int gm_stage() { return PC * (GM_A_PLANE + GM_B_PLANE); }  // 72 / 48 KiB
+// PC pieces per operand (3: bf16x6, 2: f16x3), BN output columns per block (128, or 64 for the
+// f16x3 form's narrow layers): one K stage = PC A planes + PC W planes of BN x 32
+template <int BN>
+constexpr int gm_b_plane() { return BN * GM_BK * 2; }  // 8 KiB at BN = 128
+template <int PC, int BN = 128>
+constexpr int gm_stage() { return PC * (GM_A_PLANE + gm_b_plane<BN>()); }  // 72 / 48 / 40 KiB
+// the LDS epilogue: eight 64-row wave tiles of BN / 2 columns (+ 4 floats of row pitch)
+template <int BN>
+constexpr int gm_epi_bytes() { return 8 * 64 * (BN / 2 + 4) * 4; }
 // two stages, at least the epilogue tile; f16x3 adds the rows' range scales (1 KiB) and 8 flags
-template <int PC>
+template <int PC, int BN = 128>
 constexpr int gm_smem() {
-  return (2 * gm_stage<PC>() > GM_EPI_BYTES ? 2 * gm_stage<PC>() : GM_EPI_BYTES) + (PC == 2 ? 1024 + 64 : 0);
+  return (2 * gm_stage<PC, BN>() > gm_epi_bytes<BN>() ? 2 * gm_stage<PC, BN>() : gm_epi_bytes<BN>()) +
+         (PC == 2 ? 1024 + 64 : 0);
 }
-static_assert(gm_smem<3>() <= 160 * 1024 && gm_smem<2>() <= 160 * 1024, "the LDS of a CU");
+static_assert(gm_smem<3>() <= 160 * 1024 && gm_smem<2>() <= 160 * 1024 && gm_smem<2, 64>() <= 160 * 1024,
+              "the LDS of a CU");
 
 struct GemmArgs {
   const float* A;      // [M][lda]
@@ -187,12 +192,16 @@ __device__ __forceinline__ void wait_vm_regs(float4 (&R)[4]) {
 // waves 0-3) split + store the next A tile before their first MFMA half-step instead of between
 // the halves (measured 3-7 % slower; so were a persistent one-block-per-CU form with the K pipeline
 // running across tiles and a 128 x 256 tile, profiles/r4_gemm_forms_ab.log)
-template <bool CONV, int VAR = 0, int PC = 3>
+template <bool CONV, int VAR = 0, int PC = 3, int BN = 128>
 __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
   static_assert(PC == 3 || PC == 2, "bf16x6 (3 pieces) or f16x3 (2 pieces)");
+  static_assert(BN == 128 || (BN == 64 && PC == 2), "BN = 64 is the f16x3 form's narrow tile");
   constexpr int GROUP = ((VAR >> 1) & 3) == 1 ? 4 : ((VAR >> 1) & 3) == 2 ? 16 : GM_GROUP;
-  constexpr int STAGE = gm_stage<PC>(), A_BYTES = PC * GM_A_PLANE;
-  __shared__ __attribute__((aligned(16))) unsigned char smem[gm_smem<PC>()];
+  constexpr int STAGE = gm_stage<PC, BN>(), A_BYTES = PC * GM_A_PLANE, B_PLANE = gm_b_plane<BN>();
+  constexpr int NJ = BN / 32;             // 16-column accumulator tiles per wave (wave = 64 x BN / 2)
+  constexpr int WP = PC * BN / 128;       // W DMA pieces (16 rows x 64 B) per wave and K step
+  constexpr int PPP = BN / 16;            // pieces per W plane
+  __shared__ __attribute__((aligned(16))) unsigned char smem[gm_smem<PC, BN>()];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 3, wn = wave >> 2;
 
@@ -215,7 +224,7 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
   const int gsize = min(g.tiles_m - first_m, GROUP);
   const int in_group = lin - (lin / per_group) * per_group;
   const int tm = first_m + in_group % gsize, tn = in_group / gsize;
-  const int m0 = tm * GM_BM, n0 = tn * GM_BN;
+  const int m0 = tm * GM_BM, n0 = tn * BN;
 
   // LDS images: every plane row is 32 k = four 16-B slots (8 k each), physical slot =
   // logical ^ ((row >> 2) & 2): conflict-free for the 16x16x32 fragment reads (lane l reads row
@@ -228,12 +237,12 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
   const float* ag1 = g.A + (long long)min(m0 + arow + 128, g.M - 1) * g.lda + 8 * aq;
   const int aoff0 = arow * 64 + ((aq ^ ((arow >> 2) & 2)) << 4);
   const int aoff1 = (arow + 128) * 64 + ((aq ^ (((arow + 128) >> 2) & 2)) << 4);
-  // W: LDS-DMA of 8 PC pieces (8 per plane) of 16 rows x 64 B, wave w copies pieces PC w..PC w+PC-1
-  const uint16_t* bsrc[PC];
+  // W: LDS-DMA of 8 WP pieces (PPP per plane) of 16 rows x 64 B, wave w copies pieces WP w..WP w+WP-1
+  const uint16_t* bsrc[WP];
 #pragma unroll
-  for (int t = 0; t < PC; ++t) {
-    const int i = wave * PC + t, p = i >> 3;
-    const int row = (i & 7) * 16 + (lane >> 2);
+  for (int t = 0; t < WP; ++t) {
+    const int i = wave * WP + t, p = i / PPP;
+    const int row = (i % PPP) * 16 + (lane >> 2);
     const int sl = (lane & 3) ^ ((row >> 2) & 2);
     bsrc[t] = g.W + p * g.wps + (long long)(n0 + row) * g.ldw + sl * 8;
   }
@@ -243,7 +252,7 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
     }
     unsigned char* base = smem + buf * STAGE + A_BYTES;
 #pragma unroll
-    for (int t = 0; t < PC; ++t) glds16(bsrc[t] + kt * GM_BK, base + (wave * PC + t) * 1024);
+    for (int t = 0; t < WP; ++t) glds16(bsrc[t] + kt * GM_BK, base + (wave * WP + t) * 1024);
   };
   // convolution: each staged row's window origin (iy0, ix0) and its element offset in the input;
   // a K step of 32 lies inside one filter tap (C % 32 == 0), so a row's 8 channels are one
@@ -361,12 +370,12 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
   };
 
   // wave (wm, wn) owns rows 64 wm.., columns 64 wn..: 4 x 4 accumulators of 16 x 16
-  f32x4v acc[4][4];
+  f32x4v acc[4][NJ];
   auto zero_acc = [&]() {
 #pragma unroll
     for (int i = 0; i < 4; ++i)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) acc[i][j] = (f32x4v){0.f, 0.f, 0.f, 0.f};
+      for (int j = 0; j < NJ; ++j) acc[i][j] = (f32x4v){0.f, 0.f, 0.f, 0.f};
   };
   zero_acc();
 
@@ -375,7 +384,7 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
   auto frag_off = [&](int row) { return row * 64 + ((fs ^ ((row >> 2) & 2)) << 4); };
   // half h of a K step: m-tiles 2h, 2h+1 against all four n-tiles (bf16x6: 48 MFMAs, small
   // terms first; f16x3: 24)
-  auto half_step = [&](int buf, int h, const bf16x8 (&b)[4][PC], const f16x8 (&bs)[4]) {
+  auto half_step = [&](int buf, int h, const bf16x8 (&b)[NJ][PC], const f16x8 (&bs)[NJ]) {
     const unsigned char* As = smem + buf * STAGE;
     bf16x8 a[2][PC];
 #pragma unroll
@@ -387,7 +396,7 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
-      for (int nj = 0; nj < 4; ++nj) {
+      for (int nj = 0; nj < NJ; ++nj) {
         if constexpr (PC == 2) {
           const f16x8 ah = __builtin_bit_cast(f16x8, a[i][0]), al = __builtin_bit_cast(f16x8, a[i][1]);
           const f16x8 bh = __builtin_bit_cast(f16x8, b[nj][0]), bl = __builtin_bit_cast(f16x8, b[nj][1]);
@@ -408,22 +417,22 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
         }
       }
   };
-  auto read_b = [&](bf16x8 (&b)[4][PC], int buf) {
+  auto read_b = [&](bf16x8 (&b)[NJ][PC], int buf) {
     const unsigned char* Bs = smem + buf * STAGE + A_BYTES;
 #pragma unroll
-    for (int nj = 0; nj < 4; ++nj) {
-      const int off = frag_off(wn * 64 + nj * 16 + fr);
+    for (int nj = 0; nj < NJ; ++nj) {
+      const int off = frag_off(wn * (BN / 2) + nj * 16 + fr);
 #pragma unroll
-      for (int p = 0; p < PC; ++p) b[nj][p] = *(const bf16x8*)(Bs + p * GM_B_PLANE + off);
+      for (int p = 0; p < PC; ++p) b[nj][p] = *(const bf16x8*)(Bs + p * B_PLANE + off);
     }
   };
 
   // K steps of 32, two LDS stages, one barrier per step.  Step kt computes stage kt while W of
   // kt + 1 arrives by LDS-DMA, A of kt + 1 (loaded during step kt - 1) is split and stored between
   // the step's two MFMA halves, and A of kt + 2 is loaded into registers.  Issue order per step:
-  // W DMA (PC pieces), then the 4 A loads; every step issues both (the last step's are redundant
+  // W DMA (WP pieces), then the 4 A loads; every step issues both (the last step's are redundant
   // copies of the last K step into the idle stage), so the hand counts are fixed: the split waits
-  // for A of kt + 1 with vmcnt(PC + 4), the end of the step for the W DMA with vmcnt(4).
+  // for A of kt + 1 with vmcnt(WP + 4), the end of the step for the W DMA with vmcnt(4).
   const int KT = g.K / GM_BK;
   auto k_loop = [&](auto scaled) {
     float4 Ra[4], Rb[4];
@@ -431,7 +440,7 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
     oka = load_a(Ra, 0);
     stage_b(0, 0);
     okb = load_a(Rb, min(1, KT - 1));
-    wait_vm_regs<PC + 4>(Ra);
+    wait_vm_regs<WP + 4>(Ra);
     store_a(Ra, oka, 0, scaled);
     wait_vm<4>();
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -440,23 +449,23 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
       const bool more = kt + 1 < KT;
       stage_b(min(kt + 1, KT - 1), buf ^ 1);
       oknext = load_a(Rnext, min(kt + 2, KT - 1));
-      bf16x8 b[4][PC];
+      bf16x8 b[NJ][PC];
       read_b(b, buf);
-      f16x8 bs[4];  // f16x3: 2^-11 hb (exact above f16's subnormal range)
+      f16x8 bs[NJ];  // f16x3: 2^-11 hb (exact above f16's subnormal range)
 #pragma unroll
-      for (int nj = 0; nj < 4; ++nj) {
+      for (int nj = 0; nj < NJ; ++nj) {
         if constexpr (PC == 2) bs[nj] = __builtin_bit_cast(f16x8, b[nj][0]) * (_Float16)0.00048828125f;
       }
       const bool late = (VAR & 64) == 0 || wave < 4;
       if (!late) {
-        wait_vm_regs<PC + 4>(Rcur);
+        wait_vm_regs<WP + 4>(Rcur);
         store_a(Rcur, okcur, buf ^ 1, scaled);
       }
       if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(1);
       half_step(buf, 0, b, bs);
       if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(0);
       if (late) {
-        wait_vm_regs<PC + 4>(Rcur);
+        wait_vm_regs<WP + 4>(Rcur);
         store_a(Rcur, okcur, buf ^ 1, scaled);
       }
       if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(1);
@@ -499,8 +508,8 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
       return false;
     };
     const bool need = row_scale(m0, as0, inv0) | row_scale(m1, as1, inv1);
-    float* rinv = reinterpret_cast<float*>(smem + gm_smem<PC>() - 1024 - 64);  // [256] rows' 2^-s
-    int* flag = reinterpret_cast<int*>(smem + gm_smem<PC>() - 64);
+    float* rinv = reinterpret_cast<float*>(smem + gm_smem<PC, BN>() - 1024 - 64);  // [256] rows' 2^-s
+    int* flag = reinterpret_cast<int*>(smem + gm_smem<PC, BN>() - 64);
     if (aq == 0) {
       rinv[arow] = inv0;
       rinv[arow + 128] = inv1;
@@ -523,7 +532,7 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
         for (int e = 0; e < 4; ++e) {
           const float inv = rinv[wm * 64 + i * 16 + 4 * fs + e];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) acc[i][j][e] *= inv;
+          for (int j = 0; j < NJ; ++j) acc[i][j][e] *= inv;
         }
     }
   }
@@ -534,24 +543,25 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
     // write 16 consecutive floats, rows 4 apart land on different banks), then reads it back as
     // float4 rows so every lane stores 16 contiguous bytes (16 stores per lane instead of 64)
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    constexpr int PITCH = GM_EPI_PITCH;
+    constexpr int WC = BN / 2, PITCH = WC + 4;  // wave tile columns, row pitch
+    constexpr int LPR = WC / 4, RPI = 64 / LPR;  // lanes per row (4 columns each), rows per pass
     float* T = reinterpret_cast<float*>(smem) + wave * (64 * PITCH);
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-      for (int nj = 0; nj < 4; ++nj)
+      for (int nj = 0; nj < NJ; ++nj)
 #pragma unroll
         for (int e = 0; e < 4; ++e) T[(mi * 16 + 4 * fs + e) * PITCH + nj * 16 + fr] = acc[mi][nj][e];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave reads only its own tile
-    const int c4 = (lane & 15) * 4;                      // 4 columns of the 64
-    const int n = n0 + wn * 64 + c4;
+    const int c4 = (lane % LPR) * 4;                     // 4 columns of the WC
+    const int n = n0 + wn * WC + c4;
     float4 bn = make_float4(0.f, 0.f, 0.f, 0.f);
     if (g.bias) bn = *(const float4*)(g.bias + n);
     float4 sn = make_float4(1.f, 1.f, 1.f, 1.f);
     if constexpr (PC == 2) sn = *(const float4*)(g.ws + n);
 #pragma unroll
-    for (int it = 0; it < 16; ++it) {
-      const int r = it * 4 + (lane >> 4);
+    for (int it = 0; it < 64 / RPI; ++it) {
+      const int r = it * RPI + lane / LPR;
       const int m = m0 + wm * 64 + r;
       if (m < g.M) {
         float4 v = *(const float4*)(T + r * PITCH + c4);
@@ -573,8 +583,8 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
   }
   // epilogue: accumulator register e of lane l is C[row 4 (l/16) + e][col l%16] of its tile
 #pragma unroll
-  for (int nj = 0; nj < 4; ++nj) {
-    const int n = n0 + wn * 64 + nj * 16 + fr;
+  for (int nj = 0; nj < NJ; ++nj) {
+    const int n = n0 + wn * (BN / 2) + nj * 16 + fr;
     const float bn = g.bias ? g.bias[n] : 0.f;
     const float sn = PC == 2 ? g.ws[n] : 1.f;
 #pragma unroll
@@ -638,11 +648,18 @@ __global__ void __launch_bounds__(256) split_f16x2_kernel(const float* __restric
 // stores per lane, profiles/r3_gemm_var_sweep.log) whenever the output / residual / bias rows allow
 // 16-byte accesses; RMBX_GEMM_VAR overrides the bf16x6 form (profiling)
 template <bool CONV, int PC>
-void launch_gemm(long long blocks, const GemmArgs& g, hipStream_t st) {
+void launch_gemm(long long blocks, const GemmArgs& g, hipStream_t st, int bn = 128) {
   const bool vec_ok = g.ldc % 4 == 0 &&
                       ((uintptr_t)g.C | (uintptr_t)g.res | (uintptr_t)g.bias | (uintptr_t)g.ws) % 16 == 0 &&
                       (g.batch <= 1 || (g.c_bs % 4 == 0 && g.ws_bs % 4 == 0));
   if constexpr (PC == 2) {
+    if (bn == 64) {  // the narrow tile (N % 128 != 0): default epilogue forms only
+      if (vec_ok)
+        hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 16, 2, 64>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g);
+      else
+        hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 0, 2, 64>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g);
+      return;
+    }
     // RMBX_GEMM_VAR (profiling, linear only): 16 | phase skips 32 (no split), 256 (no A loads),
     // 512 (no W DMA) -- wrong results, timing only
     const char* ve = CONV ? nullptr : getenv("RMBX_GEMM_VAR");
@@ -699,7 +716,9 @@ int linear_impl(const char* fn, const float* a, long long lda, long long a_bs, c
                 long long ldc, long long c_bs, int batch, int M, int N, int K, int relu, void* stream) {
   RMBX_CHECK_ARG(a && w_planes && c && (PC == 3 || ws), "%s: null pointer", fn);
   RMBX_CHECK_ARG(batch >= 1 && M >= 0 && N > 0 && K > 0, "%s: bad shape M=%d N=%d K=%d", fn, M, N, K);
-  RMBX_CHECK_ARG(N % GM_BN == 0, "%s: N=%d must be a multiple of %d", fn, N, GM_BN);
+  // output columns per block: 128, or 64 for f16x3 layers narrower than a multiple of 128
+  const int bn = PC == 2 && N % GM_BN != 0 ? 64 : GM_BN;
+  RMBX_CHECK_ARG(N % bn == 0, "%s: N=%d must be a multiple of %d", fn, N, PC == 2 ? 64 : GM_BN);
   RMBX_CHECK_ARG(K % GM_BK == 0, "%s: K=%d must be a multiple of %d", fn, K, GM_BK);
   RMBX_CHECK_ARG(lda >= K && lda % 4 == 0 && a_bs % 4 == 0 && ldc >= N && ldw >= K && ldw % 8 == 0 && wps % 8 == 0 &&
                      w_bs % 8 == 0,
@@ -707,7 +726,7 @@ int linear_impl(const char* fn, const float* a, long long lda, long long a_bs, c
   RMBX_CHECK_ARG(((uintptr_t)a | (uintptr_t)w_planes) % 16 == 0, "%s: operands must be 16-B aligned", fn);
   if (M == 0) return RMBX_OK;
   GemmArgs g{a, (const uint16_t*)w_planes, bias, c, lda, ldc, ldw, wps, M, N, K, relu ? 1 : 0,
-             (M + GM_BM - 1) / GM_BM, N / GM_BN, nullptr};
+             (M + GM_BM - 1) / GM_BM, N / bn, nullptr};
   g.batch = batch;
   g.a_bs = a_bs;
   g.w_bs = w_bs;
@@ -716,7 +735,7 @@ int linear_impl(const char* fn, const float* a, long long lda, long long a_bs, c
   g.ws_bs = ws_bs;
   const long long blocks = (long long)g.tiles_m * g.tiles_n * batch;
   RMBX_CHECK_ARG(blocks < (1ll << 31), "%s: too many tiles", fn);
-  launch_gemm<false, PC>(blocks, g, (hipStream_t)stream);
+  launch_gemm<false, PC>(blocks, g, (hipStream_t)stream, bn);
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
 }
@@ -728,7 +747,8 @@ int conv_impl(const char* fn, const float* in, int N, int H, int W, int C, const
   RMBX_CHECK_ARG(in && w_planes && out && (PC == 3 || ws), "%s: null pointer", fn);
   RMBX_CHECK_ARG(N >= 0 && H > 0 && W > 0 && KH > 0 && KW > 0 && stride > 0 && pad >= 0, "%s: bad geometry", fn);
   RMBX_CHECK_ARG(C % GM_BK == 0, "%s: C=%d must be a multiple of %d", fn, C, GM_BK);
-  RMBX_CHECK_ARG(Cout % GM_BN == 0, "%s: Cout=%d must be a multiple of %d", fn, Cout, GM_BN);
+  const int bn = PC == 2 && Cout % GM_BN != 0 ? 64 : GM_BN;
+  RMBX_CHECK_ARG(Cout % bn == 0, "%s: Cout=%d must be a multiple of %d", fn, Cout, PC == 2 ? 64 : GM_BN);
   RMBX_CHECK_ARG(((uintptr_t)in | (uintptr_t)w_planes) % 16 == 0, "%s: operands must be 16-B aligned", fn);
   const int Ho = (H + 2 * pad - KH) / stride + 1, Wo = (W + 2 * pad - KW) / stride + 1;
   RMBX_CHECK_ARG(Ho > 0 && Wo > 0, "%s: empty output", fn);
@@ -737,11 +757,11 @@ int conv_impl(const char* fn, const float* in, int N, int H, int W, int C, const
   if (M == 0) return RMBX_OK;
   const int K = KH * KW * C;
   GemmArgs g{in, (const uint16_t*)w_planes, bias, out, 0, Cout, K, (long long)Cout * K, (int)M, Cout, K,
-             relu ? 1 : 0, (int)((M + GM_BM - 1) / GM_BM), Cout / GM_BN, res, H, W, C, Ho, Wo, KW, stride, pad};
+             relu ? 1 : 0, (int)((M + GM_BM - 1) / GM_BM), Cout / bn, res, H, W, C, Ho, Wo, KW, stride, pad};
   g.ws = ws;
   const long long blocks = (long long)g.tiles_m * g.tiles_n;
   RMBX_CHECK_ARG(blocks < (1ll << 31), "%s: too many tiles", fn);
-  launch_gemm<true, PC>(blocks, g, (hipStream_t)stream);
+  launch_gemm<true, PC>(blocks, g, (hipStream_t)stream, bn);
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
 }

@@ -949,11 +949,17 @@ def _planes_nk(planes, what):
     return planes.shape[1], planes.shape[2], False
 
 
+def _n_multiple(h3=None):
+    """Output-width granule of the fp32-accurate GEMM: 128, or 64 for the f16x3 form (its narrow
+    64-column tile)."""
+    return 64 if (F32_PIECES == "f16x3" if h3 is None else h3) else LINEAR_F32X6_BN
+
+
 def linear_f32x6_supported(x, n_out):
     """Shapes the fp32-accurate GEMM takes: f32 device input whose last dim (K) is a multiple of
-    32, N a multiple of 128."""
+    32, N a multiple of 128 (64 in the f16x3 form)."""
     return (x.is_cuda and x.dtype == torch.float32 and x.shape[-1] % LINEAR_F32X6_BK == 0
-            and n_out % LINEAR_F32X6_BN == 0)
+            and n_out % _n_multiple() == 0)
 
 
 def linear_f32x6(x, planes, bias=None, relu=False, out=None):
@@ -996,8 +1002,8 @@ def pack_conv_f32x6(weight):
     return pack_f32_weight(w)
 
 
-def conv2d_f32x6_supported(cin, cout):
-    return cin % LINEAR_F32X6_BK == 0 and cout % LINEAR_F32X6_BN == 0
+def conv2d_f32x6_supported(cin, cout, h3=None):
+    return cin % LINEAR_F32X6_BK == 0 and cout % _n_multiple(h3) == 0
 
 
 def conv2d_f32x6(x, planes, bias, kernel_size, stride=1, padding=0, relu=False, res=None):
@@ -1016,8 +1022,8 @@ def conv2d_f32x6(x, planes, bias, kernel_size, stride=1, padding=0, relu=False, 
     pt = planes.planes if h3 else planes
     if not pt.is_contiguous():
         raise ValueError("conv2d_f32x6: planes must be contiguous")
-    if not conv2d_f32x6_supported(c, cout):
-        raise ValueError(f"conv2d_f32x6: C={c} must be a multiple of 32 and Cout={cout} of 128")
+    if not conv2d_f32x6_supported(c, cout, h3):
+        raise ValueError(f"conv2d_f32x6: C={c} must be a multiple of 32 and Cout={cout} of {_n_multiple(h3)}")
     ho = (h + 2 * padding - kh) // stride + 1
     wo = (w_ + 2 * padding - kw) // stride + 1
     if bias is not None:
@@ -1068,8 +1074,8 @@ def conv3x3_wino4_x6(x, planes, bias, relu=False, res=None):
     if kk != C or rows % 36:
         raise ValueError("conv3x3_wino4_x6: planes must be pack_wino4_x6(weight) for this input")
     co = rows // 36
-    if not conv2d_f32x6_supported(C, co):
-        raise ValueError(f"conv3x3_wino4_x6: C={C} must be a multiple of 32 and Cout={co} of 128")
+    if not conv2d_f32x6_supported(C, co, h3):
+        raise ValueError(f"conv3x3_wino4_x6: C={C} must be a multiple of 32 and Cout={co} of {_n_multiple(h3)}")
     if bias is not None:
         _chk(bias, torch.float32, (co,), "bias")
     out = torch.empty((n, co, H, W), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)

@@ -319,3 +319,41 @@ def test_winograd4_explicit_position_gemms_vs_f64(monkeypatch, form, n, C, H, W,
                               res=None if r is None else r.to(DEV).contiguous(memory_format=cl))
     # Winograd's transforms add their own f32 rounding (~1e-6 relative at these sizes)
     assert _err(got.cpu(), _conv_ref(x, w, b, 1, 1, relu, r)) <= 1e-5
+
+
+@torch.no_grad()
+@pytest.mark.parametrize("M,N,K,relu", [(700, 64, 576, True), (1000, 192, 512, False), (257, 320, 96, True)])
+def test_linear_f16x3_narrow_tile_vs_f64(M, N, K, relu):
+    """The f16x3 form's 64-column tile (N % 128 != 0) against an f64 product, beside hipBLASLt f32."""
+    from robomanipbaselines_amd import kernels as K_
+
+    g = torch.Generator(device="cpu").manual_seed(M + N)
+    x = torch.randn(M, K, generator=g).to(DEV)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(DEV)
+    b = torch.randn(N, generator=g).to(DEV)
+    got = K_.linear_f32x6(x, K_.split_f16x2(w), b, relu=relu)
+    ref = x.double() @ w.double().t() + b.double()
+    base = F.linear(x, w, b)
+    if relu:
+        ref, base = ref.clamp_min(0), base.clamp_min(0)
+    e, e32 = _err(got, ref), _err(base, ref)
+    assert got.shape == (M, N) and (e <= 4e-6 and e <= 2 * e32 + 1e-7), (e, e32)
+
+
+@torch.no_grad()
+@pytest.mark.parametrize("n,H,W,res", [(3, 30, 41, True), (2, 120, 160, True), (4, 17, 23, False)])
+def test_conv2d_f16x3_64_channels_vs_f64(monkeypatch, n, H, W, res):
+    """The ResNet layer-1 conv shape (64 -> 64, 3x3, stride 1, bias + residual + ReLU) on the f16x3
+    implicit GEMM's 64-column tile against an f64 F.conv2d."""
+    from robomanipbaselines_amd import kernels as K_
+
+    monkeypatch.setattr(K_, "F32_PIECES", "f16x3")
+    g = torch.Generator(device="cpu").manual_seed(H * W)
+    x = torch.randn(n, 64, H, W, generator=g).clamp_min(0)
+    w = torch.randn(64, 64, 3, 3, generator=g) / (64 * 9) ** 0.5
+    b = torch.randn(64, generator=g)
+    r = torch.randn(n, 64, H, W, generator=g) if res else None
+    cl = torch.channels_last
+    got = K_.conv2d_f32x6(x.to(DEV).contiguous(memory_format=cl), K_.pack_conv_f32x6(w.to(DEV)), b.to(DEV), 3, 1, 1,
+                          relu=True, res=None if r is None else r.to(DEV).contiguous(memory_format=cl))
+    assert _err(got.cpu(), _conv_ref(x, w, b, 1, 1, True, r)) <= 4e-6
