@@ -170,8 +170,10 @@ class _FusedConv(nn.Module):
     # stride-1 3x3 convs whose output width is in this set run as the fp32-accurate implicit GEMM
     # (x6 below, f16x3 pieces) instead of the fused f32 Winograd: at 128 channels (60 x 80, 1024
     # frames) 5.1 vs 6.3 ms per conv, 18,559 vs 18,178 env-steps/s
-    # (profiles/r4_bench_s1gemm128_ab.log); the 64-channel layer needs N % 128 == 0 tiles, so it
-    # stays on the Winograd kernel; env RMBX_S1_GEMM ("" = none)
+    # (profiles/r4_bench_s1gemm128_ab.log); the 64-channel layer stays on the Winograd kernel: on
+    # the GEMM's 64-column tile it is 9.1 vs 7.7 ms per conv (18,366 vs 18,826 env-steps/s,
+    # profiles/r4_conv64_gemm_bn64_vs_winograd.log, r4_bench_s1gemm64_ab.log); env RMBX_S1_GEMM
+    # ("" = none)
     S1_GEMM_CHANNELS = tuple(int(c) for c in os.environ.get("RMBX_S1_GEMM", "128").split(",") if c)
 
     def s1_gemm_ok(self):
