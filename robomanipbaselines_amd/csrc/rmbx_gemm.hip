@@ -82,13 +82,14 @@ constexpr int gm_stage() { return PC * (GM_A_PLANE + gm_b_plane<BN>()); }  // 72
 // the LDS epilogue: eight 64-row wave tiles of BN / 2 columns (+ 4 floats of row pitch)
 template <int BN>
 constexpr int gm_epi_bytes() { return 8 * 64 * (BN / 2 + 4) * 4; }
-// two stages, at least the epilogue tile; f16x3 adds the rows' range scales (1 KiB) and 8 flags
-template <int PC, int BN = 128>
+// NS stages (2, or 3 for the f16x3 form: the W DMA two steps ahead), at least the epilogue tile;
+// f16x3 adds the rows' range scales (1 KiB) and 8 flags
+template <int PC, int BN = 128, int NS = 2>
 constexpr int gm_smem() {
-  return (2 * gm_stage<PC, BN>() > gm_epi_bytes<BN>() ? 2 * gm_stage<PC, BN>() : gm_epi_bytes<BN>()) +
+  return (NS * gm_stage<PC, BN>() > gm_epi_bytes<BN>() ? NS * gm_stage<PC, BN>() : gm_epi_bytes<BN>()) +
          (PC == 2 ? 1024 + 64 : 0);
 }
-static_assert(gm_smem<3>() <= 160 * 1024 && gm_smem<2>() <= 160 * 1024 && gm_smem<2, 64>() <= 160 * 1024,
+static_assert(gm_smem<3>() <= 160 * 1024 && gm_smem<2, 128, 3>() <= 160 * 1024 && gm_smem<2, 64, 3>() <= 160 * 1024,
               "the LDS of a CU");
 
 struct GemmArgs {
@@ -201,7 +202,11 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
   constexpr int NJ = BN / 32;             // 16-column accumulator tiles per wave (wave = 64 x BN / 2)
   constexpr int WP = PC * BN / 128;       // W DMA pieces (16 rows x 64 B) per wave and K step
   constexpr int PPP = BN / 16;            // pieces per W plane
-  __shared__ __attribute__((aligned(16))) unsigned char smem[gm_smem<PC, BN>()];
+  // LDS stages: 3 for f16x3 (the W DMA of step kt + 2 issued at step kt stays in flight across the
+  // barrier; VAR bit 10 forces 2, profiling), 2 for bf16x6 (72 KiB stages)
+  constexpr int NS = (PC == 2 && (VAR & 1024) == 0) ? 3 : 2;
+  constexpr int SMEM = gm_smem<PC, BN, NS>();
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int wm = wave & 3, wn = wave >> 2;
 
@@ -427,27 +432,38 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
     }
   };
 
-  // K steps of 32, two LDS stages, one barrier per step.  Step kt computes stage kt while W of
-  // kt + 1 arrives by LDS-DMA, A of kt + 1 (loaded during step kt - 1) is split and stored between
-  // the step's two MFMA halves, and A of kt + 2 is loaded into registers.  Issue order per step:
-  // W DMA (WP pieces), then the 4 A loads; every step issues both (the last step's are redundant
-  // copies of the last K step into the idle stage), so the hand counts are fixed: the split waits
-  // for A of kt + 1 with vmcnt(WP + 4), the end of the step for the W DMA with vmcnt(4).
+  // K steps of 32 over NS LDS stages, one barrier per step.  Step kt computes stage kt while W of
+  // kt + NS - 1 arrives by LDS-DMA, A of kt + 1 (loaded during step kt - 1) is split and stored
+  // between the step's two MFMA halves, and A of kt + 2 is loaded into registers.  Issue order
+  // per step: W DMA (WP pieces), then the 4 A loads; every step issues both (the last steps' are
+  // redundant copies of the last K step into idle stages), so the hand counts are fixed: the split
+  // waits for A of kt + 1 with vmcnt(WP + 4); the end of the step retires the DMA of stage kt + 1
+  // with vmcnt(4) (2 stages: it was issued this step) or vmcnt(WP + 4) (3 stages: issued the step
+  // before, so this step's DMA stays in flight across the barrier).
   const int KT = g.K / GM_BK;
+  constexpr int LEAD = NS - 1, END_WAIT = NS == 3 ? WP + 4 : 4;
+  auto stage_of = [](int k) { return NS == 2 ? (k & 1) : k % 3; };
   auto k_loop = [&](auto scaled) {
     float4 Ra[4], Rb[4];
     int oka, okb;
-    oka = load_a(Ra, 0);
-    stage_b(0, 0);
-    okb = load_a(Rb, min(1, KT - 1));
+    if constexpr (NS == 3) {
+      stage_b(0, 0);
+      oka = load_a(Ra, 0);
+      stage_b(min(1, KT - 1), 1);
+      okb = load_a(Rb, min(1, KT - 1));
+    } else {
+      oka = load_a(Ra, 0);
+      stage_b(0, 0);
+      okb = load_a(Rb, min(1, KT - 1));
+    }
     wait_vm_regs<WP + 4>(Ra);
     store_a(Ra, oka, 0, scaled);
-    wait_vm<4>();
+    wait_vm<END_WAIT>();
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     auto step = [&](int kt, float4 (&Rcur)[4], int& okcur, float4 (&Rnext)[4], int& oknext) {
-      const int buf = kt & 1;
+      const int buf = stage_of(kt), nbuf = stage_of(kt + 1);
       const bool more = kt + 1 < KT;
-      stage_b(min(kt + 1, KT - 1), buf ^ 1);
+      stage_b(min(kt + LEAD, KT - 1), stage_of(kt + LEAD));
       oknext = load_a(Rnext, min(kt + 2, KT - 1));
       bf16x8 b[NJ][PC];
       read_b(b, buf);
@@ -459,19 +475,19 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
       const bool late = (VAR & 64) == 0 || wave < 4;
       if (!late) {
         wait_vm_regs<WP + 4>(Rcur);
-        store_a(Rcur, okcur, buf ^ 1, scaled);
+        store_a(Rcur, okcur, nbuf, scaled);
       }
       if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(1);
       half_step(buf, 0, b, bs);
       if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(0);
       if (late) {
         wait_vm_regs<WP + 4>(Rcur);
-        store_a(Rcur, okcur, buf ^ 1, scaled);
+        store_a(Rcur, okcur, nbuf, scaled);
       }
       if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(1);
       half_step(buf, 1, b, bs);
       if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(0);
-      wait_vm<4>();
+      wait_vm<END_WAIT>();
       if (more) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
     };
     for (int kt = 0; kt < KT; kt += 2) {
@@ -508,8 +524,8 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
       return false;
     };
     const bool need = row_scale(m0, as0, inv0) | row_scale(m1, as1, inv1);
-    float* rinv = reinterpret_cast<float*>(smem + gm_smem<PC, BN>() - 1024 - 64);  // [256] rows' 2^-s
-    int* flag = reinterpret_cast<int*>(smem + gm_smem<PC, BN>() - 64);
+    float* rinv = reinterpret_cast<float*>(smem + SMEM - 1024 - 64);  // [256] rows' 2^-s
+    int* flag = reinterpret_cast<int*>(smem + SMEM - 64);
     if (aq == 0) {
       rinv[arow] = inv0;
       rinv[arow + 128] = inv1;
@@ -661,7 +677,7 @@ void launch_gemm(long long blocks, const GemmArgs& g, hipStream_t st, int bn = 1
       return;
     }
     // RMBX_GEMM_VAR (profiling, linear only): 16 | phase skips 32 (no split), 256 (no A loads),
-    // 512 (no W DMA) -- wrong results, timing only
+    // 512 (no W DMA) -- wrong results, timing only; 1040 = two LDS stages (same results)
     const char* ve = CONV ? nullptr : getenv("RMBX_GEMM_VAR");
     const int var = ve && vec_ok ? atoi(ve) : (vec_ok ? 16 : 0);
     switch (var) {
@@ -671,6 +687,7 @@ void launch_gemm(long long blocks, const GemmArgs& g, hipStream_t st, int bn = 1
       case 528: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 528, 2>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
       case 784: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 784, 2>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
       case 816: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 816, 2>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
+      case 1040: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 1040, 2>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g); break;
       default: hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 16, 2>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g);
     }
     return;

@@ -1,0 +1,10 @@
+#!/bin/bash
+# round 4 box k: f16x3 GEMM with three LDS stages (W DMA two steps ahead) -- tests, phase skips and
+# the two-stage A/B, f16x3 vs bf16x6, ACT parity, the default bench
+set -o pipefail
+cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+timeout -k 10 400 python -u -m pytest -x -v --timeout 200 --timeout-method thread tests/test_gemm_gpu.py > gpurun_out/r4_k_gemm_tests.log 2>&1 || exit 1
+timeout -k 10 300 python -u scripts/prof_gemm_h3_phases.py > gpurun_out/r4_k_gemm_phases.log 2>&1 || exit 1
+timeout -k 10 300 python -u scripts/prof_gemm_h3.py > gpurun_out/r4_k_gemm_h3_ab.log 2>&1 || exit 1
+timeout -k 10 600 python -u -m pytest -x -v -s --timeout 380 --timeout-method thread tests/test_act_batch_gpu.py tests/test_act_full_gpu.py > gpurun_out/r4_k_act_tests.log 2>&1 || exit 1
+timeout -k 10 600 python -u bench.py --no_cpu_baseline > gpurun_out/r4_k_bench.json.log 2> gpurun_out/r4_k_bench.err

@@ -1,6 +1,7 @@
 """Phase skips of the f16x3 GEMM (RMBX_GEMM_VAR; wrong results, timing only) on the ACT ffn1 /
 ffn2 / v-out shapes at 1024 envs, rounds interleaved in one process: 16 = default, 48 = no split
-VALU, 272 = no A loads, 528 = no W DMA, 784 = no A loads and no W DMA, 816 = none of the three."""
+VALU, 272 = no A loads, 528 = no W DMA, 784 = no A loads and no W DMA, 816 = none of the three,
+1040 = the two-LDS-stage schedule (same results)."""
 import os
 import sys
 
@@ -10,7 +11,7 @@ sys.path.insert(0, ".")
 from robomanipbaselines_amd import kernels as K  # noqa: E402
 
 M = 1024 * 302
-VARS = ["16", "48", "272", "528", "784", "816"]
+VARS = ["16", "1040", "48", "272", "528", "784", "816"]
 for name, Kd, Nd in (("ffn1", 512, 3200), ("ffn2", 3200, 512), ("v/out", 512, 512)):
     x = torch.randn(M, Kd, device="cuda")
     p = K.split_f16x2(torch.randn(Nd, Kd, device="cuda") / Kd ** 0.5)

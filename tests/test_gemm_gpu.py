@@ -357,3 +357,21 @@ def test_conv2d_f16x3_64_channels_vs_f64(monkeypatch, n, H, W, res):
     got = K_.conv2d_f32x6(x.to(DEV).contiguous(memory_format=cl), K_.pack_conv_f32x6(w.to(DEV)), b.to(DEV), 3, 1, 1,
                           relu=True, res=None if r is None else r.to(DEV).contiguous(memory_format=cl))
     assert _err(got.cpu(), _conv_ref(x, w, b, 1, 1, True, r)) <= 4e-6
+
+
+@torch.no_grad()
+@pytest.mark.parametrize("M,N,K", [(5000, 3200, 512), (3000, 512, 3200), (257, 384, 96)])
+def test_gemm_f16x3_two_stage_variant_equals_default(monkeypatch, M, N, K):
+    """The f16x3 kernel's two-LDS-stage schedule (RMBX_GEMM_VAR=1040, profiling) gives the default
+    three-stage schedule's output bit for bit."""
+    from robomanipbaselines_amd import kernels as K_
+
+    g = torch.Generator(device="cpu").manual_seed(M + 7 * N)
+    x = torch.randn(M, K, generator=g).to(DEV)
+    p = K_.split_f16x2((torch.randn(N, K, generator=g) / K ** 0.5).to(DEV))
+    b = torch.randn(N, generator=g).to(DEV)
+    want = K_.linear_f32x6(x, p, b, relu=True)
+    monkeypatch.setenv("RMBX_GEMM_VAR", "1040")
+    got = K_.linear_f32x6(x, p, b, relu=True)
+    torch.cuda.synchronize()
+    assert torch.equal(got, want)
