@@ -622,6 +622,354 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Producer / consumer form of the f16x3 kernel (256 x 128 tile): 12 waves, 3 per SIMD.  Waves 0-7
+// only read fragments and issue MFMAs (the layout above: 64 x 64 per wave, one accumulator set);
+// waves 8-11 (one per SIMD) produce the K steps two ahead into a ring of three 48-KiB LDS stages:
+// they load the A tile (thread -> rows r, r + 64, r + 128, r + 192 of k quarter q, 8 f32 each,
+// loaded one step before its split), split it into the two f16 planes, track each row's max |a|,
+// and move W by LDS-DMA (4 pieces per wave).  One barrier per K step for all 12 waves: after
+// barrier j + 1 the stage of step j + 1 is complete (its A was stored and its DMA retired by the
+// producers during step j), and the stage they write during step j (that of j + 2) was last read
+// in step j - 1.  The per-row range check and the re-run pass are the PC = 2 kernel's.
+constexpr int GP_THREADS = 768;
+template <bool CONV, bool VEC>
+__global__ void __launch_bounds__(GP_THREADS, 1) gemm_f16x3_pc_kernel(GemmArgs g) {
+  constexpr int NS = 3, BN = 128, NJ = 4;
+  constexpr int STAGE = gm_stage<2, BN>(), A_BYTES = 2 * GM_A_PLANE, B_PLANE = gm_b_plane<BN>();
+  constexpr int SMEM = gm_smem<2, BN, NS>();
+  constexpr int WPP = 4;  // W DMA pieces per producer wave and K step (16 per stage)
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const bool producer = wave >= 8;
+
+  // block -> tile (as gemm_f32x6_kernel)
+  const int nblk = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q8 = nblk >> 3, r8 = nblk & 7;
+  int lin = (xcd < r8 ? xcd * (q8 + 1) : r8 * (q8 + 1) + (xcd - r8) * q8) + (bid >> 3);
+  if (g.batch > 1) {
+    const int per_item = g.tiles_m * g.tiles_n;
+    const int item = lin / per_item;
+    lin -= item * per_item;
+    g.A += item * g.a_bs;
+    g.W += item * g.w_bs;
+    g.C += item * g.c_bs;
+    if (g.ws) g.ws += item * g.ws_bs;
+  }
+  const int per_group = GM_GROUP * g.tiles_n;
+  const int first_m = (lin / per_group) * GM_GROUP;
+  const int gsize = min(g.tiles_m - first_m, GM_GROUP);
+  const int in_group = lin - (lin / per_group) * per_group;
+  const int tm = first_m + in_group % gsize, tn = in_group / gsize;
+  const int m0 = tm * GM_BM, n0 = tn * BN;
+  const int KT = g.K / GM_BK;
+  auto stage_of = [](int k) { return k % 3; };
+
+  // ---- producer state: thread pt -> k quarter aq, rows prow + 64 i (i = 0..3)
+  const int pt = tid - 512, aq = pt & 3, prow = (pt >> 2) & 63;
+  const float* arow[4];
+  int aoff[4];
+  long long cbase[4] = {0, 0, 0, 0};
+  int cy[4] = {0, 0, 0, 0}, cx[4] = {0, 0, 0, 0};
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int r = prow + 64 * i, m = min(m0 + r, g.M - 1);
+    arow[i] = g.A + (long long)m * g.lda + 8 * aq;
+    aoff[i] = r * 64 + ((aq ^ ((r >> 2) & 2)) << 4);
+    if constexpr (CONV) {
+      const int hw = g.oh * g.ow;
+      const int img = m / hw, rem = m - img * hw;
+      const int oy = rem / g.ow, ox = rem - oy * g.ow;
+      cy[i] = oy * g.stride - g.pad;
+      cx[i] = ox * g.stride - g.pad;
+      cbase[i] = ((long long)(img * g.ih + cy[i]) * g.iw + cx[i]) * g.ic + 8 * aq;
+    }
+  }
+  const int pw = wave - 8;
+  const uint16_t* bsrc[WPP];
+#pragma unroll
+  for (int t = 0; t < WPP; ++t) {
+    const int i = pw * WPP + t, p = i >> 3;
+    const int row = (i & 7) * 16 + (lane >> 2);
+    const int sl = (lane & 3) ^ ((row >> 2) & 2);
+    bsrc[t] = g.W + p * g.wps + (long long)(n0 + row) * g.ldw + sl * 8;
+  }
+  auto dma_w = [&](int kt, int buf) {
+    unsigned char* base = smem + buf * STAGE + A_BYTES;
+#pragma unroll
+    for (int t = 0; t < WPP; ++t) glds16(bsrc[t] + kt * GM_BK, base + (pw * WPP + t) * 1024);
+  };
+  // 8 loads of 16 B: rows i = 0..3, two halves each; returns the rows' in-image flags (conv)
+  auto load_a = [&](float4 (&R)[8], int kt) -> int {
+    if constexpr (!CONV) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const float4* p = (const float4*)(arow[i] + kt * GM_BK);
+        gload16(R[2 * i], p);
+        gload16(R[2 * i + 1], p + 1);
+      }
+      return 15;
+    } else {
+      const int k0 = kt * GM_BK;
+      const int tap = k0 / g.ic, c0 = k0 - tap * g.ic;
+      const int ky = tap / g.kw, kx = tap - ky * g.kw;
+      int ok = 0;
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const bool v = (unsigned)(cy[i] + ky) < (unsigned)g.ih && (unsigned)(cx[i] + kx) < (unsigned)g.iw;
+        const float4* p = (const float4*)(g.A + (v ? cbase[i] + (long long)(ky * g.iw + kx) * g.ic + c0 : 0));
+        gload16(R[2 * i], p);
+        gload16(R[2 * i + 1], p + 1);
+        ok |= (int)v << i;
+      }
+      return ok;
+    }
+  };
+  auto wait_regs8 = [&](float4 (&R)[8]) {  // vmcnt(WPP + 8): this step's DMA and loads stay in flight
+    f32x4v v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = __builtin_bit_cast(f32x4v, R[i]);
+    asm volatile("s_waitcnt vmcnt(%8)"
+                 : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7])
+                 : "n"(WPP + 8)
+                 : "memory");
+#pragma unroll
+    for (int i = 0; i < 8; ++i) R[i] = __builtin_bit_cast(float4, v[i]);
+  };
+  auto drain_regs8 = [&](float4 (&R)[8]) {
+    f32x4v v[8];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) v[i] = __builtin_bit_cast(f32x4v, R[i]);
+    asm volatile("s_waitcnt vmcnt(0)"
+                 : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7])
+                 :
+                 : "memory");
+#pragma unroll
+    for (int i = 0; i < 8; ++i) R[i] = __builtin_bit_cast(float4, v[i]);
+  };
+  uint32_t amax[4] = {0, 0, 0, 0};
+  float asc[4] = {1.f, 1.f, 1.f, 1.f};
+  auto store_a = [&](const float4 (&Rin)[8], int ok, int buf, auto scaled) {
+    unsigned char* base = smem + buf * STAGE;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      float4 R0 = Rin[2 * i], R1 = Rin[2 * i + 1];
+      if constexpr (CONV) {
+        if (!((ok >> i) & 1)) R0 = R1 = make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+      if constexpr (decltype(scaled)::value) {
+        const float sc = asc[i];
+        R0.x *= sc; R0.y *= sc; R0.z *= sc; R0.w *= sc;
+        R1.x *= sc; R1.y *= sc; R1.z *= sc; R1.w *= sc;
+      } else {
+        constexpr uint32_t ABS = 0x7fffffffu;
+        uint32_t m = max(max(__float_as_uint(R0.x) & ABS, __float_as_uint(R0.y) & ABS),
+                         max(__float_as_uint(R0.z) & ABS, __float_as_uint(R0.w) & ABS));
+        m = max(m, max(max(__float_as_uint(R1.x) & ABS, __float_as_uint(R1.y) & ABS),
+                       max(__float_as_uint(R1.z) & ABS, __float_as_uint(R1.w) & ABS)));
+        amax[i] = max(amax[i], m);
+      }
+      uint32_t h[4], l[4];
+      split_f16_pair(R0.x, R0.y, h[0], l[0]);
+      split_f16_pair(R0.z, R0.w, h[1], l[1]);
+      split_f16_pair(R1.x, R1.y, h[2], l[2]);
+      split_f16_pair(R1.z, R1.w, h[3], l[3]);
+      *(uint4*)(base + aoff[i]) = make_uint4(h[0], h[1], h[2], h[3]);
+      *(uint4*)(base + GM_A_PLANE + aoff[i]) = make_uint4(l[0], l[1], l[2], l[3]);
+    }
+  };
+
+  // ---- consumer state (waves 0-7): wave (wm, wn) owns rows 64 wm.., columns 64 wn..
+  const int wm = wave & 3, wn = (wave >> 2) & 1;
+  const int fr = lane & 15, fs = lane >> 4;
+  auto frag_off = [&](int row) { return row * 64 + ((fs ^ ((row >> 2) & 2)) << 4); };
+  f32x4v acc[4][NJ];
+  auto zero_acc = [&]() {
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = (f32x4v){0.f, 0.f, 0.f, 0.f};
+  };
+  zero_acc();
+  auto consume = [&](int buf) {
+    const unsigned char* S = smem + buf * STAGE;
+    bf16x8 b[NJ][2];
+#pragma unroll
+    for (int nj = 0; nj < NJ; ++nj) {
+      const int off = frag_off(wn * 64 + nj * 16 + fr);
+      b[nj][0] = *(const bf16x8*)(S + A_BYTES + off);
+      b[nj][1] = *(const bf16x8*)(S + A_BYTES + B_PLANE + off);
+    }
+    f16x8 bs[NJ];
+#pragma unroll
+    for (int nj = 0; nj < NJ; ++nj) bs[nj] = __builtin_bit_cast(f16x8, b[nj][0]) * (_Float16)0.00048828125f;
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      const int off = frag_off(wm * 64 + mi * 16 + fr);
+      const f16x8 ah = __builtin_bit_cast(f16x8, *(const bf16x8*)(S + off));
+      const f16x8 al = __builtin_bit_cast(f16x8, *(const bf16x8*)(S + GM_A_PLANE + off));
+#pragma unroll
+      for (int nj = 0; nj < NJ; ++nj) {
+        f32x4v c = acc[mi][nj];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al, bs[nj], c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, __builtin_bit_cast(f16x8, b[nj][1]), c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah, __builtin_bit_cast(f16x8, b[nj][0]), c, 0, 0, 0);
+        acc[mi][nj] = c;
+      }
+    }
+  };
+
+  // one pass over K: KT + 1 barriers for every wave
+  auto k_pass = [&](auto scaled) {
+    if (producer) {
+      float4 Ra[8], Rb[8];
+      int oka, okb;
+      // prologue: K steps 0 and 1 into stages 0 and 1, A of step 2 in flight
+      dma_w(0, 0);
+      oka = load_a(Ra, 0);
+      dma_w(min(1, KT - 1), 1);
+      okb = load_a(Rb, min(1, KT - 1));
+      {
+        // A(0): younger = DMA(1) + A(1)
+        wait_regs8(Ra);
+        store_a(Ra, oka, 0, scaled);
+        drain_regs8(Rb);  // A(1) (and every DMA before it)
+        store_a(Rb, okb, 1, scaled);
+      }
+      oka = load_a(Ra, min(2, KT - 1));  // A(2)
+      asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      // step j: produce K step j + 2 (A loaded last step into Rcur) and load A(j + 3)
+      auto pstep = [&](int j, float4 (&Rcur)[8], int& okcur, float4 (&Rnext)[8], int& oknext) {
+        const int p = min(j + 2, KT - 1);
+        dma_w(p, stage_of(j + 2));
+        oknext = load_a(Rnext, min(j + 3, KT - 1));
+        wait_regs8(Rcur);  // A(j + 2): younger = DMA(j + 2) + A(j + 3)
+        store_a(Rcur, okcur, stage_of(j + 2), scaled);
+        // DMA(j + 1) (issued last step, older than A(j + 2)) retired by the same count
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      };
+      for (int j = 0; j < KT; j += 2) {
+        pstep(j, Ra, oka, Rb, okb);
+        if (j + 1 < KT) pstep(j + 1, Rb, okb, Ra, oka);
+      }
+      drain_regs8(Ra);
+      drain_regs8(Rb);
+    } else {
+      asm volatile("s_barrier" ::: "memory");
+      for (int j = 0; j < KT; ++j) {
+        consume(stage_of(j));
+        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+      }
+    }
+  };
+  k_pass(std::false_type{});
+
+  // per-row range check (producers hold the rows' maxima) and the re-run pass
+  float* rinv = reinterpret_cast<float*>(smem + SMEM - 1024 - 64);
+  int* flag = reinterpret_cast<int*>(smem + SMEM - 64);
+  {
+    bool need = false;
+    if (producer) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        uint32_t b = amax[i];
+        b = max(b, (uint32_t)__shfl_xor((int)b, 1));
+        b = max(b, (uint32_t)__shfl_xor((int)b, 2));
+        const float m = __uint_as_float(b);
+        float inv = 1.f;
+        if ((m > 32768.f || (m > 0.f && m < 0.015625f)) && m <= 3.4e38f) {
+          int e;
+          frexpf(m, &e);
+          asc[i] = ldexpf(1.f, 14 - e);
+          inv = ldexpf(1.f, e - 14);
+          need = true;
+        }
+        if (aq == 0) rinv[prow + 64 * i] = inv;
+      }
+    }
+    const unsigned long long bal = __ballot(need);
+    if (lane == 0) flag[wave] = bal != 0ull;
+    asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory");
+    int any = 0;
+#pragma unroll
+    for (int w = 8; w < 12; ++w) any |= flag[w];
+    if (any) {
+      zero_acc();
+      k_pass(std::true_type{});
+      if (!producer) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const float inv = rinv[wm * 64 + i * 16 + 4 * fs + e];
+#pragma unroll
+            for (int j = 0; j < NJ; ++j) acc[i][j][e] *= inv;
+          }
+      }
+    }
+  }
+
+  // epilogue (consumers; the producers only take part in the barrier)
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  if (producer) return;
+  if constexpr (VEC) {
+    constexpr int PITCH = 68;
+    float* T = reinterpret_cast<float*>(smem) + wave * (64 * PITCH);
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int nj = 0; nj < NJ; ++nj)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) T[(mi * 16 + 4 * fs + e) * PITCH + nj * 16 + fr] = acc[mi][nj][e];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const int c4 = (lane & 15) * 4;
+    const int n = n0 + wn * 64 + c4;
+    float4 bn = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (g.bias) bn = *(const float4*)(g.bias + n);
+    const float4 sn = *(const float4*)(g.ws + n);
+#pragma unroll
+    for (int it = 0; it < 16; ++it) {
+      const int r = it * 4 + (lane >> 4);
+      const int m = m0 + wm * 64 + r;
+      if (m < g.M) {
+        float4 v = *(const float4*)(T + r * PITCH + c4);
+        v.x *= sn.x; v.y *= sn.y; v.z *= sn.z; v.w *= sn.w;
+        v.x += bn.x; v.y += bn.y; v.z += bn.z; v.w += bn.w;
+        if (g.res) {
+          const float4 rv = *(const float4*)(g.res + (long long)m * g.ldc + n);
+          v.x += rv.x; v.y += rv.y; v.z += rv.z; v.w += rv.w;
+        }
+        if (g.relu) {
+          v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+        }
+        *(float4*)(g.C + (long long)m * g.ldc + n) = v;
+      }
+    }
+  } else {
+#pragma unroll
+    for (int nj = 0; nj < NJ; ++nj) {
+      const int n = n0 + wn * 64 + nj * 16 + fr;
+      const float bn = g.bias ? g.bias[n] : 0.f, sn = g.ws[n];
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        const int mb = m0 + wm * 64 + mi * 16 + 4 * fs;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int m = mb + e;
+          if (m < g.M) {
+            float v = acc[mi][nj][e];
+            v *= sn;  // as gemm_f32x6_kernel: scale, then bias (two roundings, no contraction)
+            v += bn;
+            if (g.res) v += g.res[(long long)m * g.ldc + n];
+            if (g.relu) v = fmaxf(v, 0.f);
+            g.C[(long long)m * g.ldc + n] = v;
+          }
+        }
+      }
+    }
+  }
+}
+
 // planes[p * n + i] = piece p of x[i] (x = x0 + x1 + x2, bf16 bits)
 __global__ void split_bf16x3_kernel(const float* __restrict__ x, uint16_t* __restrict__ planes, long long n) {
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
@@ -674,6 +1022,16 @@ void launch_gemm(long long blocks, const GemmArgs& g, hipStream_t st, int bn = 1
         hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 16, 2, 64>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g);
       else
         hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 0, 2, 64>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g);
+      return;
+    }
+    // producer / consumer form (RMBX_GEMM_PC=1; read per launch so a test can compare the forms)
+    const char* pce = getenv("RMBX_GEMM_PC");
+    const bool pc = pce && atoi(pce) != 0;
+    if (pc) {
+      if (vec_ok)
+        hipLaunchKernelGGL((gemm_f16x3_pc_kernel<CONV, true>), dim3((unsigned)blocks), dim3(GP_THREADS), 0, st, g);
+      else
+        hipLaunchKernelGGL((gemm_f16x3_pc_kernel<CONV, false>), dim3((unsigned)blocks), dim3(GP_THREADS), 0, st, g);
       return;
     }
     // RMBX_GEMM_VAR (profiling, linear only): 16 | phase skips 32 (no split), 256 (no A loads),

@@ -375,3 +375,43 @@ def test_gemm_f16x3_two_stage_variant_equals_default(monkeypatch, M, N, K):
     got = K_.linear_f32x6(x, p, b, relu=True)
     torch.cuda.synchronize()
     assert torch.equal(got, want)
+
+
+@torch.no_grad()
+@pytest.mark.parametrize("M,N,K,relu,scale", [(5000, 3200, 512, True, 1.0), (3000, 512, 3200, False, 1.0),
+                                              (257, 384, 96, True, 1.0), (700, 256, 512, False, 1e6)])
+def test_gemm_f16x3_producer_consumer_equals_default(monkeypatch, M, N, K, relu, scale):
+    """The producer / consumer f16x3 kernel (RMBX_GEMM_PC=1: 8 MFMA waves, 4 waves loading,
+    splitting and moving W) gives the default kernel's output bit for bit, the range re-run
+    included (scale 1e6)."""
+    from robomanipbaselines_amd import kernels as K_
+
+    g = torch.Generator(device="cpu").manual_seed(M + 3 * N)
+    x = (torch.randn(M, K, generator=g) * scale).to(DEV)
+    p = K_.split_f16x2((torch.randn(N, K, generator=g) / K ** 0.5).to(DEV))
+    b = torch.randn(N, generator=g).to(DEV)
+    monkeypatch.setenv("RMBX_GEMM_PC", "0")
+    want = K_.linear_f32x6(x, p, b, relu=relu)
+    monkeypatch.setenv("RMBX_GEMM_PC", "1")
+    got = K_.linear_f32x6(x, p, b, relu=relu)
+    torch.cuda.synchronize()
+    assert torch.equal(got, want)
+
+
+@torch.no_grad()
+def test_conv2d_f16x3_producer_consumer_equals_default(monkeypatch):
+    from robomanipbaselines_amd import kernels as K_
+
+    monkeypatch.setattr(K_, "F32_PIECES", "f16x3")
+    g = torch.Generator(device="cpu").manual_seed(5)
+    cl = torch.channels_last
+    x = torch.randn(3, 64, 37, 45, generator=g).clamp_min(0).to(DEV).contiguous(memory_format=cl)
+    w = K_.pack_conv_f32x6((torch.randn(128, 64, 3, 3, generator=g) / 24.0).to(DEV))
+    b = torch.randn(128, generator=g).to(DEV)
+    r = torch.randn(3, 128, 19, 23, generator=g).to(DEV).contiguous(memory_format=cl)
+    monkeypatch.setenv("RMBX_GEMM_PC", "0")
+    want = K_.conv2d_f32x6(x, w, b, 3, 2, 1, relu=True, res=r)
+    monkeypatch.setenv("RMBX_GEMM_PC", "1")
+    got = K_.conv2d_f32x6(x, w, b, 3, 2, 1, relu=True, res=r)
+    torch.cuda.synchronize()
+    assert torch.equal(got, want)
