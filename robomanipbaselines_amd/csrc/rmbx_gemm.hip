@@ -441,7 +441,10 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
   // with vmcnt(4) (2 stages: it was issued this step) or vmcnt(WP + 4) (3 stages: issued the step
   // before, so this step's DMA stays in flight across the barrier).
   const int KT = g.K / GM_BK;
-  constexpr int LEAD = NS - 1, END_WAIT = NS == 3 ? WP + 4 : 4;
+  // (the phase-skip variants issue fewer memory operations than the counts assume: they wait for
+  // everything instead, so no register is read or reused before its load has landed)
+  constexpr bool SKIPS = (VAR & (256 | 512)) != 0;
+  constexpr int LEAD = NS - 1, END_WAIT = SKIPS ? 0 : (NS == 3 ? WP + 4 : 4), SPLIT_WAIT = SKIPS ? 0 : WP + 4;
   auto stage_of = [](int k) { return NS == 2 ? (k & 1) : k % 3; };
   auto k_loop = [&](auto scaled) {
     float4 Ra[4], Rb[4];
@@ -456,7 +459,7 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
       stage_b(0, 0);
       okb = load_a(Rb, min(1, KT - 1));
     }
-    wait_vm_regs<WP + 4>(Ra);
+    wait_vm_regs<SPLIT_WAIT>(Ra);
     store_a(Ra, oka, 0, scaled);
     wait_vm<END_WAIT>();
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
@@ -474,14 +477,14 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
       }
       const bool late = (VAR & 64) == 0 || wave < 4;
       if (!late) {
-        wait_vm_regs<WP + 4>(Rcur);
+        wait_vm_regs<SPLIT_WAIT>(Rcur);
         store_a(Rcur, okcur, nbuf, scaled);
       }
       if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(1);
       half_step(buf, 0, b, bs);
       if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(0);
       if (late) {
-        wait_vm_regs<WP + 4>(Rcur);
+        wait_vm_regs<SPLIT_WAIT>(Rcur);
         store_a(Rcur, okcur, nbuf, scaled);
       }
       if constexpr (VAR & 1) __builtin_amdgcn_s_setprio(1);
