@@ -10,7 +10,11 @@ import os
 
 import numpy as np
 
-_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib", "librmbx.so")
+# RMBX_LIB_VARIANT=<name> loads _lib/librmbx_<name>.so instead (profiling A/Bs of build options
+# only; the product loads librmbx.so)
+_LIB_PATH = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_lib",
+                         f"librmbx_{os.environ['RMBX_LIB_VARIANT']}.so" if os.environ.get("RMBX_LIB_VARIANT")
+                         else "librmbx.so")
 
 _c_int = ctypes.c_int
 _c_p = ctypes.c_void_p

@@ -202,9 +202,10 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
   constexpr int NJ = BN / 32;             // 16-column accumulator tiles per wave (wave = 64 x BN / 2)
   constexpr int WP = PC * BN / 128;       // W DMA pieces (16 rows x 64 B) per wave and K step
   constexpr int PPP = BN / 16;            // pieces per W plane
-  // LDS stages: 3 for f16x3 (the W DMA of step kt + 2 issued at step kt stays in flight across the
-  // barrier; VAR bit 10 forces 2, profiling), 2 for bf16x6 (72 KiB stages)
-  constexpr int NS = (PC == 2 && (VAR & 1024) == 0) ? 3 : 2;
+  // LDS stages: 2; VAR bit 10 (f16x3, profiling) = 3 stages, the W DMA of step kt + 2 issued at step
+  // kt and left in flight across the barrier -- measured 1.02-1.08x slower than 2 stages
+  // (profiles/r4_gemm_f16x3_phase_skips.log)
+  constexpr int NS = (PC == 2 && (VAR & 1024) != 0) ? 3 : 2;
   constexpr int SMEM = gm_smem<PC, BN, NS>();
   __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -1038,7 +1039,7 @@ void launch_gemm(long long blocks, const GemmArgs& g, hipStream_t st, int bn = 1
       return;
     }
     // RMBX_GEMM_VAR (profiling, linear only): 16 | phase skips 32 (no split), 256 (no A loads),
-    // 512 (no W DMA) -- wrong results, timing only; 1040 = two LDS stages (same results)
+    // 512 (no W DMA) -- wrong results, timing only; 1040 = three LDS stages (same results)
     const char* ve = CONV ? nullptr : getenv("RMBX_GEMM_VAR");
     const int var = ve && vec_ok ? atoi(ve) : (vec_ok ? 16 : 0);
     switch (var) {

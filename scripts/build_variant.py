@@ -1,0 +1,16 @@
+"""Build a profiling variant of the library into robomanipbaselines_amd/_lib/librmbx_<name>.so
+(loaded with RMBX_LIB_VARIANT=<name>; the product loads librmbx.so).  Variants:
+  slp -- rmbx_gemm.hip without -fno-slp-vectorize (the SLP vectorizer's packed f32 split ops)."""
+import os
+import sys
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+from robomanipbaselines_amd import build as B  # noqa: E402
+
+name = sys.argv[1]
+if name == "slp":
+    B.FILE_FLAGS = {}
+else:
+    raise SystemExit(f"unknown variant {name}")
+B.LIB_PATH = os.path.join(B.LIB_DIR, f"librmbx_{name}.so")
+print(B.build())

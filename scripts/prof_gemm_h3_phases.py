@@ -1,7 +1,7 @@
 """Phase skips of the f16x3 GEMM (RMBX_GEMM_VAR; wrong results, timing only) on the ACT ffn1 /
 ffn2 / v-out shapes at 1024 envs, rounds interleaved in one process: 16 = default, 48 = no split
 VALU, 272 = no A loads, 528 = no W DMA, 784 = no A loads and no W DMA, 816 = none of the three,
-1040 = the two-LDS-stage schedule (same results)."""
+1040 = the three-LDS-stage schedule (same results)."""
 import os
 import sys
 

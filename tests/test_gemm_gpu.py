@@ -361,9 +361,9 @@ def test_conv2d_f16x3_64_channels_vs_f64(monkeypatch, n, H, W, res):
 
 @torch.no_grad()
 @pytest.mark.parametrize("M,N,K", [(5000, 3200, 512), (3000, 512, 3200), (257, 384, 96)])
-def test_gemm_f16x3_two_stage_variant_equals_default(monkeypatch, M, N, K):
-    """The f16x3 kernel's two-LDS-stage schedule (RMBX_GEMM_VAR=1040, profiling) gives the default
-    three-stage schedule's output bit for bit."""
+def test_gemm_f16x3_three_stage_variant_equals_default(monkeypatch, M, N, K):
+    """The f16x3 kernel's three-LDS-stage schedule (RMBX_GEMM_VAR=1040, profiling) gives the default
+    two-stage schedule's output bit for bit."""
     from robomanipbaselines_amd import kernels as K_
 
     g = torch.Generator(device="cpu").manual_seed(M + 7 * N)
