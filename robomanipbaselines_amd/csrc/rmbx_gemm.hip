@@ -79,9 +79,10 @@ template <int BN>
 constexpr int gm_b_plane() { return BN * GM_BK * 2; }  // 8 KiB at BN = 128
 template <int PC, int BN = 128>
 constexpr int gm_stage() { return PC * (GM_A_PLANE + gm_b_plane<BN>()); }  // 72 / 48 / 40 KiB
-// the LDS epilogue: eight 64-row wave tiles of BN / 2 columns (+ 4 floats of row pitch)
+// the LDS epilogue: eight 64-row wave tiles of min(BN / 2, 64) columns (+ 4 floats of row pitch;
+// the 256-wide tile transposes its 128 wave columns in two passes)
 template <int BN>
-constexpr int gm_epi_bytes() { return 8 * 64 * (BN / 2 + 4) * 4; }
+constexpr int gm_epi_bytes() { return 8 * 64 * ((BN / 2 < 64 ? BN / 2 : 64) + 4) * 4; }
 // NS stages (2, or 3 for the f16x3 form: the W DMA two steps ahead), at least the epilogue tile;
 // f16x3 adds the rows' range scales (1 KiB) and 8 flags
 template <int PC, int BN = 128, int NS = 2>
@@ -89,7 +90,8 @@ constexpr int gm_smem() {
   return (NS * gm_stage<PC, BN>() > gm_epi_bytes<BN>() ? NS * gm_stage<PC, BN>() : gm_epi_bytes<BN>()) +
          (PC == 2 ? 1024 + 64 : 0);
 }
-static_assert(gm_smem<3>() <= 160 * 1024 && gm_smem<2, 128, 3>() <= 160 * 1024 && gm_smem<2, 64, 3>() <= 160 * 1024,
+static_assert(gm_smem<3>() <= 160 * 1024 && gm_smem<2, 128, 3>() <= 160 * 1024 && gm_smem<2, 64, 3>() <= 160 * 1024 &&
+                  gm_smem<2, 256, 2>() <= 160 * 1024,
               "the LDS of a CU");
 
 struct GemmArgs {
@@ -196,7 +198,8 @@ __device__ __forceinline__ void wait_vm_regs(float4 (&R)[4]) {
 template <bool CONV, int VAR = 0, int PC = 3, int BN = 128>
 __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
   static_assert(PC == 3 || PC == 2, "bf16x6 (3 pieces) or f16x3 (2 pieces)");
-  static_assert(BN == 128 || (BN == 64 && PC == 2), "BN = 64 is the f16x3 form's narrow tile");
+  static_assert(BN == 128 || ((BN == 64 || BN == 256) && PC == 2), "BN = 64 / 256: the f16x3 form's tiles");
+  static_assert(BN != 256 || (VAR & 1024) == 0, "the 256-wide tile runs two stages");
   constexpr int GROUP = ((VAR >> 1) & 3) == 1 ? 4 : ((VAR >> 1) & 3) == 2 ? 16 : GM_GROUP;
   constexpr int STAGE = gm_stage<PC, BN>(), A_BYTES = PC * GM_A_PLANE, B_PLANE = gm_b_plane<BN>();
   constexpr int NJ = BN / 32;             // 16-column accumulator tiles per wave (wave = 64 x BN / 2)
@@ -469,6 +472,44 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
       const bool more = kt + 1 < KT;
       stage_b(min(kt + LEAD, KT - 1), stage_of(kt + LEAD));
       oknext = load_a(Rnext, min(kt + 2, KT - 1));
+      if constexpr (BN == 256) {
+        // the 256-wide tile (wave = 64 x 128, 4 x 8 accumulators): the wave's four A fragment
+        // pairs stay in registers for the step, the W fragments are read per column tile in two
+        // halves of four, the A split between them (registers: acc 128 + A 32 + one W tile 12)
+        const unsigned char* S = smem + buf * STAGE;
+        f16x8 ah[4], al[4];
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) {
+          const int off = frag_off(wm * 64 + mi * 16 + fr);
+          ah[mi] = __builtin_bit_cast(f16x8, *(const bf16x8*)(S + off));
+          al[mi] = __builtin_bit_cast(f16x8, *(const bf16x8*)(S + GM_A_PLANE + off));
+        }
+        auto wide_half = [&](int hh) {
+#pragma unroll
+          for (int q = 0; q < NJ / 2; ++q) {
+            const int nj = hh * (NJ / 2) + q;
+            const int off = frag_off(wn * (BN / 2) + nj * 16 + fr);
+            const f16x8 bh = __builtin_bit_cast(f16x8, *(const bf16x8*)(S + A_BYTES + off));
+            const f16x8 bl = __builtin_bit_cast(f16x8, *(const bf16x8*)(S + A_BYTES + B_PLANE + off));
+            const f16x8 bsc = bh * (_Float16)0.00048828125f;
+#pragma unroll
+            for (int mi = 0; mi < 4; ++mi) {
+              f32x4v c = acc[mi][nj];
+              c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[mi], bsc, c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[mi], bl, c, 0, 0, 0);
+              c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[mi], bh, c, 0, 0, 0);
+              acc[mi][nj] = c;
+            }
+          }
+        };
+        wide_half(0);
+        wait_vm_regs<SPLIT_WAIT>(Rcur);
+        store_a(Rcur, okcur, nbuf, scaled);
+        wide_half(1);
+        wait_vm<END_WAIT>();
+        if (more) asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+        return;
+      }
       bf16x8 b[NJ][PC];
       read_b(b, buf);
       f16x8 bs[NJ];  // f16x3: 2^-11 hb (exact above f16's subnormal range)
@@ -563,18 +604,22 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
     // write 16 consecutive floats, rows 4 apart land on different banks), then reads it back as
     // float4 rows so every lane stores 16 contiguous bytes (16 stores per lane instead of 64)
     asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-    constexpr int WC = BN / 2, PITCH = WC + 4;  // wave tile columns, row pitch
+    constexpr int WC = BN / 2 < 64 ? BN / 2 : 64, PITCH = WC + 4;  // columns per pass, row pitch
     constexpr int LPR = WC / 4, RPI = 64 / LPR;  // lanes per row (4 columns each), rows per pass
+    constexpr int NPASS = (BN / 2) / WC, NJP = NJ / NPASS;  // passes, accumulator columns per pass
     float* T = reinterpret_cast<float*>(smem) + wave * (64 * PITCH);
+#pragma unroll
+    for (int pass = 0; pass < NPASS; ++pass) {
+    if (pass > 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the last pass's reads are done
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi)
 #pragma unroll
-      for (int nj = 0; nj < NJ; ++nj)
+      for (int q = 0; q < NJP; ++q)
 #pragma unroll
-        for (int e = 0; e < 4; ++e) T[(mi * 16 + 4 * fs + e) * PITCH + nj * 16 + fr] = acc[mi][nj][e];
+        for (int e = 0; e < 4; ++e) T[(mi * 16 + 4 * fs + e) * PITCH + q * 16 + fr] = acc[mi][pass * NJP + q][e];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");  // the wave reads only its own tile
     const int c4 = (lane % LPR) * 4;                     // 4 columns of the WC
-    const int n = n0 + wn * WC + c4;
+    const int n = n0 + wn * (BN / 2) + pass * WC + c4;
     float4 bn = make_float4(0.f, 0.f, 0.f, 0.f);
     if (g.bias) bn = *(const float4*)(g.bias + n);
     float4 sn = make_float4(1.f, 1.f, 1.f, 1.f);
@@ -599,6 +644,7 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
         *(float4*)(g.C + (long long)m * g.ldc + n) = v;
       }
     }
+    }  // pass
     return;
   }
   // epilogue: accumulator register e of lane l is C[row 4 (l/16) + e][col l%16] of its tile
@@ -1028,6 +1074,13 @@ void launch_gemm(long long blocks, const GemmArgs& g, hipStream_t st, int bn = 1
         hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 0, 2, 64>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g);
       return;
     }
+    if (bn == 256) {  // the wide tile
+      if (vec_ok)
+        hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 16, 2, 256>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g);
+      else
+        hipLaunchKernelGGL((gemm_f32x6_kernel<CONV, 0, 2, 256>), dim3((unsigned)blocks), dim3(GM_THREADS), 0, st, g);
+      return;
+    }
     // producer / consumer form (RMBX_GEMM_PC=1; read per launch so a test can compare the forms)
     const char* pce = getenv("RMBX_GEMM_PC");
     const bool pc = pce && atoi(pce) != 0;
@@ -1095,9 +1148,36 @@ int linear_impl(const char* fn, const float* a, long long lda, long long a_bs, c
                 long long ldc, long long c_bs, int batch, int M, int N, int K, int relu, void* stream) {
   RMBX_CHECK_ARG(a && w_planes && c && (PC == 3 || ws), "%s: null pointer", fn);
   RMBX_CHECK_ARG(batch >= 1 && M >= 0 && N > 0 && K > 0, "%s: bad shape M=%d N=%d K=%d", fn, M, N, K);
-  // output columns per block: 128, or 64 for f16x3 layers narrower than a multiple of 128
+  // output columns per block: 128, or 64 for f16x3 layers narrower than a multiple of 128; the
+  // f16x3 wide tile (256, RMBX_GEMM_WIDE=1) takes the leading multiple of 256 columns and a second
+  // launch the 128 left over
   const int bn = PC == 2 && N % GM_BN != 0 ? 64 : GM_BN;
   RMBX_CHECK_ARG(N % bn == 0, "%s: N=%d must be a multiple of %d", fn, N, PC == 2 ? 64 : GM_BN);
+  if constexpr (PC == 2) {
+    const char* we = getenv("RMBX_GEMM_WIDE");
+    if (we && atoi(we) != 0 && bn == GM_BN && N >= 256 && batch == 1) {
+      const int n256 = N / 256 * 256;
+      RMBX_CHECK_ARG(K % GM_BK == 0, "%s: K=%d must be a multiple of %d", fn, K, GM_BK);
+      RMBX_CHECK_ARG(lda >= K && lda % 4 == 0 && ldc >= N && ldw >= K && ldw % 8 == 0 && wps % 8 == 0,
+                     "%s: bad strides lda=%lld ldc=%lld ldw=%lld wps=%lld", fn, lda, ldc, ldw, wps);
+      RMBX_CHECK_ARG(((uintptr_t)a | (uintptr_t)w_planes) % 16 == 0, "%s: operands must be 16-B aligned", fn);
+      if (M == 0) return RMBX_OK;
+      GemmArgs g{a, (const uint16_t*)w_planes, bias, c, lda, ldc, ldw, wps, M, n256, K, relu ? 1 : 0,
+                 (M + GM_BM - 1) / GM_BM, n256 / 256, nullptr};
+      g.batch = 1;
+      g.ws = ws;
+      launch_gemm<false, PC>((long long)g.tiles_m * g.tiles_n, g, (hipStream_t)stream, 256);
+      RMBX_CHECK_LAUNCH();
+      if (n256 == N) return RMBX_OK;
+      GemmArgs t{a, (const uint16_t*)w_planes + (long long)n256 * ldw, bias ? bias + n256 : nullptr, c + n256, lda, ldc,
+                 ldw, wps, M, N - n256, K, relu ? 1 : 0, (M + GM_BM - 1) / GM_BM, (N - n256) / GM_BN, nullptr};
+      t.batch = 1;
+      t.ws = ws + n256;
+      launch_gemm<false, PC>((long long)t.tiles_m * t.tiles_n, t, (hipStream_t)stream, GM_BN);
+      RMBX_CHECK_LAUNCH();
+      return RMBX_OK;
+    }
+  }
   RMBX_CHECK_ARG(K % GM_BK == 0, "%s: K=%d must be a multiple of %d", fn, K, GM_BK);
   RMBX_CHECK_ARG(lda >= K && lda % 4 == 0 && a_bs % 4 == 0 && ldc >= N && ldw >= K && ldw % 8 == 0 && wps % 8 == 0 &&
                      w_bs % 8 == 0,

@@ -415,3 +415,23 @@ def test_conv2d_f16x3_producer_consumer_equals_default(monkeypatch):
     got = K_.conv2d_f32x6(x, w, b, 3, 2, 1, relu=True, res=r)
     torch.cuda.synchronize()
     assert torch.equal(got, want)
+
+
+@torch.no_grad()
+@pytest.mark.parametrize("M,N,K,relu,scale", [(5000, 3200, 512, True, 1.0), (3000, 512, 3200, False, 1.0),
+                                              (1000, 1024, 512, True, 1.0), (700, 768, 96, False, 1e6)])
+def test_gemm_f16x3_wide_tile_equals_default(monkeypatch, M, N, K, relu, scale):
+    """The f16x3 kernel's 256-column tile (RMBX_GEMM_WIDE=1; N = 3200 as a 3072-column wide launch
+    plus a 128-column one) gives the default tile's output bit for bit, the range re-run included."""
+    from robomanipbaselines_amd import kernels as K_
+
+    g = torch.Generator(device="cpu").manual_seed(M + 11 * N)
+    x = (torch.randn(M, K, generator=g) * scale).to(DEV)
+    p = K_.split_f16x2((torch.randn(N, K, generator=g) / K ** 0.5).to(DEV))
+    b = torch.randn(N, generator=g).to(DEV)
+    monkeypatch.setenv("RMBX_GEMM_WIDE", "0")
+    want = K_.linear_f32x6(x, p, b, relu=relu)
+    monkeypatch.setenv("RMBX_GEMM_WIDE", "1")
+    got = K_.linear_f32x6(x, p, b, relu=relu)
+    torch.cuda.synchronize()
+    assert torch.equal(got, want)
