@@ -173,7 +173,7 @@ def winograd_probe(ro):
 
 
 def gemm_pmc_traffic():
-    """HBM counter bytes per gemm_f32x6 launch (mean over one fp32 ACT inference at 1024 envs) from the
+    """HBM counter bytes of the gemm_f32x6 dispatches of one fp32 ACT inference at 1024 envs, from the
     committed PMC passes (scripts/gpurun/gemm_pmc.sh + tools/pmc_traffic.py --gemm); (None, None) if
     absent."""
     import glob
@@ -189,7 +189,7 @@ def gemm_pmc_traffic():
     path = files[-1]
     with open(path) as f:
         d = json.load(f)
-    return d.get("traffic_bytes_per_launch"), os.path.relpath(path, ROOT)
+    return d["read_bytes_per_inference"] + d["write_bytes_per_inference"], os.path.relpath(path, ROOT)
 
 
 def gemm_probe(ro):
@@ -225,13 +225,16 @@ def gemm_probe(ro):
     ex = executed / ms / 1e9   # executed MFMA TFLOP/s
     traffic, src = gemm_pmc_traffic()
     n = len(probe)
+    if traffic is not None:
+        traffic /= n  # per GEMM call (one or two kernel dispatches: the 256-wide tile + a 128 remainder)
     form = ("f16x3: each f32 operand split into two f16 pieces (the low one scaled by 2^11), three piece products "
             "on v_mfma_f32_16x16x32_f16" if kinds == {3} else
             "bf16x6: each f32 operand split into three bf16 pieces, six piece products on v_mfma_f32_16x16x32_bf16"
             if kinds == {6} else "mixed f16x3 / bf16x6")
     return {"bound": "mfma", "achieved": round(ex, 2), "peak": MFMA_PEAK_TFLOPS["bf16"], "unit": "TFLOP/s",
             "frac": ex / MFMA_PEAK_TFLOPS["bf16"], "traffic": None if traffic is None else round(traffic),
-            "traffic_unit": "HBM bytes per launch, mean over the launches of one fp32 ACT inference at 1024 envs",
+            "traffic_unit": "HBM bytes per GEMM call (one op launch; N = 3200 runs as two kernel dispatches), mean over "
+                            "the calls of one fp32 ACT inference at 1024 envs",
             "traffic_source": src,
             "algorithmic_bytes_per_launch": round(nbytes / len(probe)),
             "kernel": f"rmbx::gemm_f32x6_kernel (fp32-accurate GEMM / implicit-GEMM conv, {form}, f32 accumulation)",

@@ -1142,42 +1142,47 @@ extern "C" int rmbx_split_bf16x3(const float* x, void* planes, long long n, void
 namespace rmbx {
 namespace {
 // shared argument checks and launch of the linear / batched / conv entry points of both forms
+// f16x3 dispatch: the leading multiple of 256 output columns on the 256-wide tile (A split once
+// per 256 columns instead of 128: 1.05-1.09x at the ACT shapes, bitwise equal,
+// profiles/r4_gemm_wide_ab.log), the 128 columns left over (N = 3200 = 3072 + 128) by a second
+// launch of the 128-wide tile; N % 128 != 0 runs the 64-wide tile.  RMBX_GEMM_WIDE=0 (read per
+// launch) keeps everything on the 128-wide tile.
+template <bool CONV>
+void launch_f16x3(const GemmArgs& g, hipStream_t st, int bn) {
+  const char* we = getenv("RMBX_GEMM_WIDE");
+  const bool wide = !(we && atoi(we) == 0);
+  const int n256 = g.N / 256 * 256;
+  const long long items = g.batch > 1 ? g.batch : 1;
+  if (!wide || bn != GM_BN || n256 == 0) {
+    launch_gemm<CONV, 2>((long long)g.tiles_m * g.tiles_n * items, g, st, bn);
+    return;
+  }
+  GemmArgs w = g;
+  w.N = n256;
+  w.tiles_n = n256 / 256;
+  launch_gemm<CONV, 2>((long long)w.tiles_m * w.tiles_n * items, w, st, 256);
+  if (n256 == g.N) return;
+  GemmArgs t = g;
+  t.W = g.W + (long long)n256 * g.ldw;
+  t.bias = g.bias ? g.bias + n256 : nullptr;
+  t.C = g.C + n256;
+  t.res = g.res ? g.res + n256 : nullptr;
+  t.ws = g.ws + n256;
+  t.N = g.N - n256;
+  t.tiles_n = t.N / GM_BN;
+  launch_gemm<CONV, 2>((long long)t.tiles_m * t.tiles_n * items, t, st, GM_BN);
+}
+
 template <int PC>
 int linear_impl(const char* fn, const float* a, long long lda, long long a_bs, const void* w_planes, long long ldw,
                 long long wps, long long w_bs, const float* ws, long long ws_bs, const float* bias, float* c,
                 long long ldc, long long c_bs, int batch, int M, int N, int K, int relu, void* stream) {
   RMBX_CHECK_ARG(a && w_planes && c && (PC == 3 || ws), "%s: null pointer", fn);
   RMBX_CHECK_ARG(batch >= 1 && M >= 0 && N > 0 && K > 0, "%s: bad shape M=%d N=%d K=%d", fn, M, N, K);
-  // output columns per block: 128, or 64 for f16x3 layers narrower than a multiple of 128; the
-  // f16x3 wide tile (256, RMBX_GEMM_WIDE=1) takes the leading multiple of 256 columns and a second
-  // launch the 128 left over
+  // output columns per block: 128, or 64 for f16x3 layers narrower than a multiple of 128 (the
+  // f16x3 form runs the leading multiple of 256 columns on its 256-wide tile, launch_f16x3)
   const int bn = PC == 2 && N % GM_BN != 0 ? 64 : GM_BN;
   RMBX_CHECK_ARG(N % bn == 0, "%s: N=%d must be a multiple of %d", fn, N, PC == 2 ? 64 : GM_BN);
-  if constexpr (PC == 2) {
-    const char* we = getenv("RMBX_GEMM_WIDE");
-    if (we && atoi(we) != 0 && bn == GM_BN && N >= 256 && batch == 1) {
-      const int n256 = N / 256 * 256;
-      RMBX_CHECK_ARG(K % GM_BK == 0, "%s: K=%d must be a multiple of %d", fn, K, GM_BK);
-      RMBX_CHECK_ARG(lda >= K && lda % 4 == 0 && ldc >= N && ldw >= K && ldw % 8 == 0 && wps % 8 == 0,
-                     "%s: bad strides lda=%lld ldc=%lld ldw=%lld wps=%lld", fn, lda, ldc, ldw, wps);
-      RMBX_CHECK_ARG(((uintptr_t)a | (uintptr_t)w_planes) % 16 == 0, "%s: operands must be 16-B aligned", fn);
-      if (M == 0) return RMBX_OK;
-      GemmArgs g{a, (const uint16_t*)w_planes, bias, c, lda, ldc, ldw, wps, M, n256, K, relu ? 1 : 0,
-                 (M + GM_BM - 1) / GM_BM, n256 / 256, nullptr};
-      g.batch = 1;
-      g.ws = ws;
-      launch_gemm<false, PC>((long long)g.tiles_m * g.tiles_n, g, (hipStream_t)stream, 256);
-      RMBX_CHECK_LAUNCH();
-      if (n256 == N) return RMBX_OK;
-      GemmArgs t{a, (const uint16_t*)w_planes + (long long)n256 * ldw, bias ? bias + n256 : nullptr, c + n256, lda, ldc,
-                 ldw, wps, M, N - n256, K, relu ? 1 : 0, (M + GM_BM - 1) / GM_BM, (N - n256) / GM_BN, nullptr};
-      t.batch = 1;
-      t.ws = ws + n256;
-      launch_gemm<false, PC>((long long)t.tiles_m * t.tiles_n, t, (hipStream_t)stream, GM_BN);
-      RMBX_CHECK_LAUNCH();
-      return RMBX_OK;
-    }
-  }
   RMBX_CHECK_ARG(K % GM_BK == 0, "%s: K=%d must be a multiple of %d", fn, K, GM_BK);
   RMBX_CHECK_ARG(lda >= K && lda % 4 == 0 && a_bs % 4 == 0 && ldc >= N && ldw >= K && ldw % 8 == 0 && wps % 8 == 0 &&
                      w_bs % 8 == 0,
@@ -1194,7 +1199,11 @@ int linear_impl(const char* fn, const float* a, long long lda, long long a_bs, c
   g.ws_bs = ws_bs;
   const long long blocks = (long long)g.tiles_m * g.tiles_n * batch;
   RMBX_CHECK_ARG(blocks < (1ll << 31), "%s: too many tiles", fn);
-  launch_gemm<false, PC>(blocks, g, (hipStream_t)stream, bn);
+  if constexpr (PC == 2) {
+    launch_f16x3<false>(g, (hipStream_t)stream, bn);
+  } else {
+    launch_gemm<false, PC>(blocks, g, (hipStream_t)stream, bn);
+  }
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
 }
@@ -1220,7 +1229,11 @@ int conv_impl(const char* fn, const float* in, int N, int H, int W, int C, const
   g.ws = ws;
   const long long blocks = (long long)g.tiles_m * g.tiles_n;
   RMBX_CHECK_ARG(blocks < (1ll << 31), "%s: too many tiles", fn);
-  launch_gemm<true, PC>(blocks, g, (hipStream_t)stream, bn);
+  if constexpr (PC == 2) {
+    launch_f16x3<true>(g, (hipStream_t)stream, bn);
+  } else {
+    launch_gemm<true, PC>(blocks, g, (hipStream_t)stream, bn);
+  }
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
 }

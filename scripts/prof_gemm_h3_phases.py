@@ -5,6 +5,7 @@ VALU, 272 = no A loads, 528 = no W DMA, 784 = no A loads and no W DMA, 816 = non
 import os
 import sys
 
+os.environ.setdefault("RMBX_GEMM_WIDE", "0")  # the variants compared are forms of the 128-wide tile
 import torch
 
 sys.path.insert(0, ".")

@@ -3,6 +3,7 @@ shapes at 1024 envs and a trunk conv, rounds interleaved in one process; outputs
 import os
 import sys
 
+os.environ.setdefault("RMBX_GEMM_WIDE", "0")  # the variants compared are forms of the 128-wide tile
 import torch
 
 sys.path.insert(0, ".")

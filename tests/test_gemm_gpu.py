@@ -370,6 +370,7 @@ def test_gemm_f16x3_three_stage_variant_equals_default(monkeypatch, M, N, K):
     x = torch.randn(M, K, generator=g).to(DEV)
     p = K_.split_f16x2((torch.randn(N, K, generator=g) / K ** 0.5).to(DEV))
     b = torch.randn(N, generator=g).to(DEV)
+    monkeypatch.setenv("RMBX_GEMM_WIDE", "0")  # the variants are forms of the 128-wide tile
     want = K_.linear_f32x6(x, p, b, relu=True)
     monkeypatch.setenv("RMBX_GEMM_VAR", "1040")
     got = K_.linear_f32x6(x, p, b, relu=True)
@@ -390,6 +391,7 @@ def test_gemm_f16x3_producer_consumer_equals_default(monkeypatch, M, N, K, relu,
     x = (torch.randn(M, K, generator=g) * scale).to(DEV)
     p = K_.split_f16x2((torch.randn(N, K, generator=g) / K ** 0.5).to(DEV))
     b = torch.randn(N, generator=g).to(DEV)
+    monkeypatch.setenv("RMBX_GEMM_WIDE", "0")  # the producer / consumer kernel is a 128-wide form
     monkeypatch.setenv("RMBX_GEMM_PC", "0")
     want = K_.linear_f32x6(x, p, b, relu=relu)
     monkeypatch.setenv("RMBX_GEMM_PC", "1")
@@ -409,6 +411,7 @@ def test_conv2d_f16x3_producer_consumer_equals_default(monkeypatch):
     w = K_.pack_conv_f32x6((torch.randn(128, 64, 3, 3, generator=g) / 24.0).to(DEV))
     b = torch.randn(128, generator=g).to(DEV)
     r = torch.randn(3, 128, 19, 23, generator=g).to(DEV).contiguous(memory_format=cl)
+    monkeypatch.setenv("RMBX_GEMM_WIDE", "0")
     monkeypatch.setenv("RMBX_GEMM_PC", "0")
     want = K_.conv2d_f32x6(x, w, b, 3, 2, 1, relu=True, res=r)
     monkeypatch.setenv("RMBX_GEMM_PC", "1")
@@ -421,8 +424,9 @@ def test_conv2d_f16x3_producer_consumer_equals_default(monkeypatch):
 @pytest.mark.parametrize("M,N,K,relu,scale", [(5000, 3200, 512, True, 1.0), (3000, 512, 3200, False, 1.0),
                                               (1000, 1024, 512, True, 1.0), (700, 768, 96, False, 1e6)])
 def test_gemm_f16x3_wide_tile_equals_default(monkeypatch, M, N, K, relu, scale):
-    """The f16x3 kernel's 256-column tile (RMBX_GEMM_WIDE=1; N = 3200 as a 3072-column wide launch
-    plus a 128-column one) gives the default tile's output bit for bit, the range re-run included."""
+    """The f16x3 kernel's 256-column tile (the default; N = 3200 as a 3072-column wide launch plus a
+    128-column one) gives the 128-column tile's output (RMBX_GEMM_WIDE=0) bit for bit, the range
+    re-run included."""
     from robomanipbaselines_amd import kernels as K_
 
     g = torch.Generator(device="cpu").manual_seed(M + 11 * N)
@@ -435,3 +439,56 @@ def test_gemm_f16x3_wide_tile_equals_default(monkeypatch, M, N, K, relu, scale):
     got = K_.linear_f32x6(x, p, b, relu=relu)
     torch.cuda.synchronize()
     assert torch.equal(got, want)
+
+
+@torch.no_grad()
+@pytest.mark.parametrize("n,C,H,W,Cout", [(2, 256, 30, 40, 256), (3, 128, 15, 21, 384)])
+def test_gemm_f16x3_wide_tile_batched_equals_narrow(monkeypatch, n, C, H, W, Cout):
+    """The batched f16x3 GEMM (the 36 Winograd position GEMMs) on the 256-wide tile -- with a
+    128-column remainder launch per item for Cout = 384 -- equals the 128-wide tile bit for bit."""
+    from robomanipbaselines_amd import kernels as K_
+
+    monkeypatch.setattr(K_, "F32_PIECES", "f16x3")
+    g = torch.Generator(device="cpu").manual_seed(n * C + Cout)
+    cl = torch.channels_last
+    x = torch.randn(n, C, H, W, generator=g).clamp_min(0).to(DEV).contiguous(memory_format=cl)
+    wt = (torch.randn(Cout, C, 3, 3, generator=g) / (9 * C) ** 0.5).to(DEV)
+    b = torch.randn(Cout, generator=g).to(DEV)
+    u = K_.pack_wino4_x6(wt)
+    outs = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("RMBX_GEMM_WIDE", v)
+        outs.append(K_.conv3x3_wino4_x6(x, u, b, relu=True))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    ref = _conv_ref(x, wt, b, 1, 1, True, None)
+    assert _err(outs[1], ref) < 2e-6
+
+
+@torch.no_grad()
+@pytest.mark.parametrize("n,C,H,W,Cout,k,stride,res", [(2, 128, 30, 40, 256, 3, 2, True), (3, 256, 15, 20, 512, 3, 2, False),
+                                                       (2, 64, 20, 24, 384, 1, 1, True)])
+def test_conv2d_f16x3_wide_tile_equals_narrow(monkeypatch, n, C, H, W, Cout, k, stride, res):
+    """Implicit-GEMM convs with Cout >= 256 on the 256-wide tile (the layer-3/4 stride-2 and 1x1
+    downsample convs; Cout = 384 adds a 128-column remainder launch with its residual offset) equal
+    the 128-wide tile bit for bit and the f64 conv to f32 accuracy."""
+    from robomanipbaselines_amd import kernels as K_
+
+    monkeypatch.setattr(K_, "F32_PIECES", "f16x3")
+    g = torch.Generator(device="cpu").manual_seed(n * C + Cout)
+    cl = torch.channels_last
+    pad = k // 2
+    x = torch.randn(n, C, H, W, generator=g).clamp_min(0).to(DEV).contiguous(memory_format=cl)
+    wt = (torch.randn(Cout, C, k, k, generator=g) / (C * k * k) ** 0.5).to(DEV)
+    b = torch.randn(Cout, generator=g).to(DEV)
+    Ho, Wo = (H + 2 * pad - k) // stride + 1, (W + 2 * pad - k) // stride + 1
+    r = torch.randn(n, Cout, Ho, Wo, generator=g).to(DEV).contiguous(memory_format=cl) if res else None
+    w = K_.pack_conv_f32x6(wt)
+    outs = []
+    for v in ("0", "1"):
+        monkeypatch.setenv("RMBX_GEMM_WIDE", v)
+        outs.append(K_.conv2d_f32x6(x, w, b, k, stride, pad, relu=True, res=r))
+    torch.cuda.synchronize()
+    assert torch.equal(outs[0], outs[1])
+    ref = _conv_ref(x, wt, b, stride, pad, True, r)
+    assert _err(outs[1], ref) < 2e-6
