@@ -485,6 +485,15 @@ int rmbx_conv2d_f16x3(const float* in, int N, int H, int W, int C, const void* w
 int rmbx_attention_f32x6(const float* q, const float* k, const float* v, float* out, int B, int heads, int Lq, int Lk,
                          long long q_bstride, int q_rstride, long long k_bstride, int k_rstride, long long v_bstride,
                          int v_rstride, float scale, void* stream);
+/* rmbx_attention_f32 with fp32-accurate products in the f16x3 form (rmbx_linear_f16x3's scheme): K, V
+ * split as h + 2^-11 l, Q and the probabilities (scaled by 2^14) as h + l, three f16 piece products per
+ * product accumulated in f32.  A block (one head of one batch item, up to 160 queries) whose |q|, |k|
+ * or |v| reaches 2^15, or with a head dimension whose max |v| lies in (0, 2^-6), is re-run on the
+ * rmbx_attention_f32x6 kernel.  redo: int32 workspace of at least B * heads * ceil(Lq / 32) entries
+ * (one flag per block, written here).  Replaces the same call site as rmbx_attention_f32. */
+int rmbx_attention_f16x3(const float* q, const float* k, const float* v, float* out, int* redo, int B, int heads,
+                         int Lq, int Lk, long long q_bstride, int q_rstride, long long k_bstride, int k_rstride,
+                         long long v_bstride, int v_rstride, float scale, void* stream);
 /* Residual add + LayerNorm over the last dim of [rows][D] rows (D <= 2048, multiple of 8 bf16 / 4
  * f32): out = LayerNorm(rnd(x + r)) * weight + bias (f32 weight/bias), r optional (NULL); replaces
  * the add + nn.LayerNorm pair of the ACT transformer's post-norm layers (third_party/act). */

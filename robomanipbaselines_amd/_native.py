@@ -70,6 +70,7 @@ SIGNATURES = {
     "rmbx_attention_bf16": (_c_int, [_c_p] * 4 + [_c_int] * 4 + [ctypes.c_longlong, _c_int] * 3 + [ctypes.c_float, _c_p]),
     "rmbx_attention_f32": (_c_int, [_c_p] * 4 + [_c_int] * 4 + [ctypes.c_longlong, _c_int] * 3 + [ctypes.c_float, _c_p]),
     "rmbx_attention_f32x6": (_c_int, [_c_p] * 4 + [_c_int] * 4 + [ctypes.c_longlong, _c_int] * 3 + [ctypes.c_float, _c_p]),
+    "rmbx_attention_f16x3": (_c_int, [_c_p] * 5 + [_c_int] * 4 + [ctypes.c_longlong, _c_int] * 3 + [ctypes.c_float, _c_p]),
     "rmbx_linear_f32x6": (_c_int, [_c_p, ctypes.c_longlong, _c_p, ctypes.c_longlong, ctypes.c_longlong, _c_p, _c_p,
                                    ctypes.c_longlong, _c_int, _c_int, _c_int, _c_int, _c_p]),
     "rmbx_conv2d_f32x6": (_c_int, [_c_p] + [_c_int] * 4 + [_c_p] * 4 + [_c_int] * 6 + [_c_p]),

@@ -26,6 +26,8 @@ typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
 typedef float f32x16 __attribute__((ext_vector_type(16)));
 typedef float f32x2 __attribute__((ext_vector_type(2)));
 typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
 
 constexpr int AT_MAX_WAVES = 5;  // waves per block (each walks 32-query groups)
 constexpr int AT_LK_MAX = 320;   // keys staged per block
@@ -242,6 +244,9 @@ struct AttnF32Args {
   int o_rstride;
   int heads, Lq, Lk, parts;
   float scale_log2;
+  // rmbx_attention_f16x3: per block, 1 = re-run on the bf16x6 kernel (written by the f16x3 kernel;
+  // the bf16x6 kernel then runs only the flagged blocks); null for the other kernels
+  int* redo = nullptr;
 };
 
 template <int DBG>
@@ -430,6 +435,7 @@ __device__ __forceinline__ int ax_pos_of_key(int k) {
 
 __global__ void __launch_bounds__(64 * AX_MAX_WAVES) attn_fwd_f32x6_kernel(AttnF32Args a) {
   __shared__ __attribute__((aligned(16))) uint16_t sA[2 * AX_BUF];
+  if (a.redo && a.redo[blockIdx.x] == 0) return;  // f16x3 re-run mode: only the flagged blocks
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nthreads = blockDim.x;
   const int bh = blockIdx.x / a.parts, part = blockIdx.x - bh * a.parts;
@@ -607,6 +613,237 @@ __global__ void __launch_bounds__(64 * AX_MAX_WAVES) attn_fwd_f32x6_kernel(AttnF
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// f16x3 form (rmbx_attention_f16x3, the fp32 policy's default since round 4): the f16x3 GEMM's
+// scheme (csrc/rmbx_gemm.hip) on the two products, three piece products each instead of six on
+// the f16 matrix cores (bf16 rate):
+//   S^T = K Q^T:  K (staged) = kh + 2^-11 kl with kh = f16(k), kl = f16((k - kh) 2^11); Q (registers)
+//                 = qh + ql with ql = f16(q - qh): S = kh qh + kh ql + kl (2^-11 qh)
+//   O^T += V^T P^T: V as K; P' = 2^14 exp2(...) (the power of two keeps every probability down to
+//                 2^-28 in f16's normal range; l sums the same P', so O = acc / l is unchanged)
+//                 = ph + pl: O' = vh ph + vh pl + vl (2^-11 ph)
+// Each piece product is exact in f32; the dropped kl ql / vl pl terms are 2^-22 relative.  f16's
+// range is checked per block: any |q|, |k|, |v| >= 2^15 (f16 overflow) or a head dimension whose
+// max |v| over the keys is in (0, 2^-6) (its values would sit near f16's subnormal floor) flags the
+// block, and rmbx_attention_f16x3 re-runs the flagged blocks on the bf16x6 kernel (f32's exponent
+// range), so every query's result depends only on its own block (one head of one batch item).
+// Layout of the bf16x6 kernel, two pieces per staged tile (16 KiB per buffer).
+// ---------------------------------------------------------------------------------------------
+constexpr int AH_PLANE = 32 * 64;      // f16 elements of one piece of a K or V^T tile
+constexpr int AH_BUF = 4 * AH_PLANE;   // K pieces then V^T pieces
+constexpr float AH_BIG = 32768.f;      // 2^15
+constexpr float AH_TINY = 0.015625f;   // 2^-6
+
+__device__ __forceinline__ uint32_t ah_pk(float x, float y) {
+  f32x2 v = {x, y};
+  return __builtin_bit_cast(uint32_t, __builtin_convertvector(v, f16x2));
+}
+__device__ __forceinline__ float ah_lo(uint32_t p) { return (float)__builtin_bit_cast(f16x2, p)[0]; }
+__device__ __forceinline__ float ah_hi(uint32_t p) { return (float)__builtin_bit_cast(f16x2, p)[1]; }
+// staged operand (K, V): h = f16(x), l = f16((x - h) 2^11)
+__device__ __forceinline__ void ah_split_a(float x, float y, uint32_t& h, uint32_t& l) {
+  h = ah_pk(x, y);
+  l = ah_pk((x - ah_lo(h)) * 2048.f, (y - ah_hi(h)) * 2048.f);
+}
+// register operand (Q, P'): h = f16(x), l = f16(x - h)
+__device__ __forceinline__ void ah_split_w(float x, float y, uint32_t& h, uint32_t& l) {
+  h = ah_pk(x, y);
+  l = ah_pk(x - ah_lo(h), y - ah_hi(h));
+}
+
+__global__ void __launch_bounds__(64 * AX_MAX_WAVES) attn_fwd_f16x3_kernel(AttnF32Args a) {
+  __shared__ __attribute__((aligned(16))) uint16_t sA[2 * AH_BUF];
+  __shared__ uint32_t sDim[64];  // per head dimension: max |v| over the keys (f32 bits)
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int nthreads = blockDim.x;
+  const int bh = blockIdx.x / a.parts, part = blockIdx.x - bh * a.parts;
+  const int b = bh / a.heads, hd = bh - b * a.heads;
+  const int r32 = lane & 31, kh = lane >> 5;
+  const int qi = (part * (nthreads >> 6) + wave) * 32 + r32;
+  const bool q_ok = qi < a.Lq;
+  const float* kbase = a.k + (size_t)b * a.k_bstride + hd * 64;
+  const float* vbase = a.v + (size_t)b * a.v_bstride + hd * 64;
+  const int nt = (a.Lk + 31) >> 5;
+  if (tid < 64) sDim[tid] = 0u;
+  float big = 0.f;  // this thread's max |q|, |k|, |v|
+
+  // Q pieces (B operand of S^T = K Q^T): dims 16 s + 8 kh .. +7 of query qi; fq[s][2] = 2^-11 qh
+  f16x8 fq[4][3];
+  {
+    const float* qp = a.q + (size_t)b * a.q_bstride + (size_t)(q_ok ? qi : 0) * a.q_rstride + hd * 64 + 8 * kh;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const float4 x0 = *reinterpret_cast<const float4*>(qp + 16 * s);
+      const float4 x1 = *reinterpret_cast<const float4*>(qp + 16 * s + 4);
+      big = fmaxf(big, fmaxf(fmaxf(fabsf(x0.x), fabsf(x0.y)), fmaxf(fabsf(x0.z), fabsf(x0.w))));
+      big = fmaxf(big, fmaxf(fmaxf(fabsf(x1.x), fabsf(x1.y)), fmaxf(fabsf(x1.z), fabsf(x1.w))));
+      uint32_t h[4], l[4];
+      ah_split_w(x0.x, x0.y, h[0], l[0]);
+      ah_split_w(x0.z, x0.w, h[1], l[1]);
+      ah_split_w(x1.x, x1.y, h[2], l[2]);
+      ah_split_w(x1.z, x1.w, h[3], l[3]);
+      fq[s][0] = __builtin_bit_cast(f16x8, make_uint4(h[0], h[1], h[2], h[3]));
+      fq[s][1] = __builtin_bit_cast(f16x8, make_uint4(l[0], l[1], l[2], l[3]));
+      fq[s][2] = fq[s][0] * (_Float16)0.00048828125f;
+    }
+  }
+
+  // staging: chunk q < 512 = K[key q/16][4 (q%16) ..], q >= 512 = V[key (q-512)/16][...]; the
+  // thread count is a multiple of 16, so a thread's V chunks all hold dims 4 (tid & 15) .. + 3
+  float4 st[AX_CH];
+  float vmax[4] = {0.f, 0.f, 0.f, 0.f};
+  auto load_tile = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < AX_CH; ++i) {
+      const int q = tid + nthreads * i;
+      const int qq = q & 511, key = 32 * t + (qq >> 4), quad = qq & 15;
+      const bool ok = q < 1024 && key < a.Lk;
+      const float* src = q < 512 ? kbase + (size_t)key * a.k_rstride : vbase + (size_t)key * a.v_rstride;
+      st[i] = ok ? *reinterpret_cast<const float4*>(src + 4 * quad) : make_float4(0.f, 0.f, 0.f, 0.f);
+    }
+  };
+  auto store_tile = [&](uint16_t* buf) {
+#pragma unroll
+    for (int i = 0; i < AX_CH; ++i) {
+      const int q = tid + nthreads * i;
+      if (q >= 1024) continue;
+      const int qq = q & 511, key = qq >> 4, quad = qq & 15;
+      const float ax = fabsf(st[i].x), ay = fabsf(st[i].y), az = fabsf(st[i].z), aw = fabsf(st[i].w);
+      big = fmaxf(big, fmaxf(fmaxf(ax, ay), fmaxf(az, aw)));
+      uint32_t h[2], l[2];
+      ah_split_a(st[i].x, st[i].y, h[0], l[0]);
+      ah_split_a(st[i].z, st[i].w, h[1], l[1]);
+      if (q < 512) {  // K: 4 dims = half a 16-byte chunk of the key row
+        const int off = key * 64 + (((quad >> 1) ^ ((key >> 1) & 7)) << 3) + 4 * (quad & 1);
+        *reinterpret_cast<uint2*>(buf + off) = make_uint2(h[0], h[1]);
+        *reinterpret_cast<uint2*>(buf + AH_PLANE + off) = make_uint2(l[0], l[1]);
+      } else {  // V^T: 4 dims of one key = one element in each of 4 rows
+        vmax[0] = fmaxf(vmax[0], ax);
+        vmax[1] = fmaxf(vmax[1], ay);
+        vmax[2] = fmaxf(vmax[2], az);
+        vmax[3] = fmaxf(vmax[3], aw);
+        const int pos = ax_pos_of_key(key);
+        const uint32_t pk[2][2] = {{h[0], h[1]}, {l[0], l[1]}};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int d = 4 * quad + e;
+          const int off = 2 * AH_PLANE + d * 32 + ((((pos >> 3) ^ ((d >> 2) & 3))) << 3) + (pos & 7);
+#pragma unroll
+          for (int pc = 0; pc < 2; ++pc)
+            buf[off + pc * AH_PLANE] = (uint16_t)((pk[pc][e >> 1] >> (16 * (e & 1))) & 0xffff);
+        }
+      }
+    }
+  };
+  load_tile(0);
+  store_tile(sA);
+  __syncthreads();
+
+  const float c = a.scale_log2;
+  const bool ragged = (a.Lk & 31) != 0;
+  const int d0 = at_sigma(r32), d1 = d0 + 32;
+  f32x16 acc0 = {}, acc1 = {};
+  float m_run = -INFINITY, l_run = 0.f;
+  for (int t = 0; t < nt; ++t) {
+    const uint16_t* buf = sA + (t & 1) * AH_BUF;
+    const bool more = t + 1 < nt;
+    if (more) load_tile(t + 1);
+    // S^T tile: three piece products per 16-dim step
+    f32x16 s = {};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int off = r32 * 64 + (((2 * ks + kh) ^ ((r32 >> 1) & 7)) << 3);
+      const f16x8 k0 = *reinterpret_cast<const f16x8*>(buf + off);
+      const f16x8 k1 = *reinterpret_cast<const f16x8*>(buf + AH_PLANE + off);
+      s = __builtin_amdgcn_mfma_f32_32x32x16_f16(k1, fq[ks][2], s, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_32x32x16_f16(k0, fq[ks][1], s, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_32x32x16_f16(k0, fq[ks][0], s, 0, 0, 0);
+    }
+    if (ragged && t == nt - 1) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (32 * t + 4 * kh + (j & 3) + 8 * (j >> 2) >= a.Lk) s[j] = -INFINITY;
+    }
+    float mx = s[0];
+#pragma unroll
+    for (int j = 1; j < 16; ++j) mx = fmaxf(mx, s[j]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const float m_new = fmaxf(m_run, mx);
+    if (__any(m_new != m_run)) {
+      const float alpha = exp2f((m_run - m_new) * c);  // first tile: exp2(-inf) = 0
+      l_run *= alpha;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        acc0[j] *= alpha;
+        acc1[j] *= alpha;
+      }
+      m_run = m_new;
+    }
+    const float mc = m_run * c;
+    // P' pieces: the B operand of O^T += V^T P'^T, k-step u from registers 8 u .. 8 u + 7
+    f16x8 fp[2][3];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      uint32_t h[4], l[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float pa = exp2f(fmaf(s[8 * u + 2 * e], c, -mc)) * 16384.f;
+        const float pb = exp2f(fmaf(s[8 * u + 2 * e + 1], c, -mc)) * 16384.f;
+        l_run += pa + pb;
+        ah_split_w(pa, pb, h[e], l[e]);
+      }
+      fp[u][0] = __builtin_bit_cast(f16x8, make_uint4(h[0], h[1], h[2], h[3]));
+      fp[u][1] = __builtin_bit_cast(f16x8, make_uint4(l[0], l[1], l[2], l[3]));
+      fp[u][2] = fp[u][0] * (_Float16)0.00048828125f;
+    }
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int cc = 2 * u + kh;
+      const int o0 = 2 * AH_PLANE + d0 * 32 + ((cc ^ ((d0 >> 2) & 3)) << 3);
+      const int o1 = 2 * AH_PLANE + d1 * 32 + ((cc ^ ((d1 >> 2) & 3)) << 3);
+      f16x8 v0[2], v1[2];
+#pragma unroll
+      for (int pc = 0; pc < 2; ++pc) {
+        v0[pc] = *reinterpret_cast<const f16x8*>(buf + o0 + pc * AH_PLANE);
+        v1[pc] = *reinterpret_cast<const f16x8*>(buf + o1 + pc * AH_PLANE);
+      }
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v0[1], fp[u][2], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v1[1], fp[u][2], acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v0[0], fp[u][1], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v1[0], fp[u][1], acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v0[0], fp[u][0], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v1[0], fp[u][0], acc1, 0, 0, 0);
+    }
+    if (more) store_tile(sA + ((t + 1) & 1) * AH_BUF);
+    __syncthreads();
+  }
+  // range check: the block re-runs on the bf16x6 kernel if any operand left f16's range
+#pragma unroll
+  for (int e = 0; e < 4; ++e)  // (|v| as u32 bits orders like the value)
+    if (vmax[e] > 0.f) atomicMax(&sDim[4 * (tid & 15) + e], __float_as_uint(vmax[e]));
+  __syncthreads();
+  // (fmaxf skips NaNs: NaN inputs are not flagged and propagate through the f16 pieces)
+  bool flag = big >= AH_BIG;
+  if (tid < 64) {
+    const float m = __uint_as_float(sDim[tid]);
+    flag = flag || (m > 0.f && m < AH_TINY);
+  }
+  const int any = __syncthreads_or(flag ? 1 : 0);
+  if (tid == 0) a.redo[blockIdx.x] = any;
+  if (any) return;
+  const float l_tot = l_run + __shfl_xor(l_run, 32);
+  if (!q_ok) return;
+  const float inv = 1.f / l_tot;
+  float* op = a.o + ((size_t)b * a.Lq + qi) * a.o_rstride + hd * 64 + 16 * kh;
+#pragma unroll
+  for (int q4 = 0; q4 < 4; ++q4) {
+    *reinterpret_cast<float4*>(op + 4 * q4) =
+        make_float4(acc0[4 * q4] * inv, acc0[4 * q4 + 1] * inv, acc0[4 * q4 + 2] * inv, acc0[4 * q4 + 3] * inv);
+    *reinterpret_cast<float4*>(op + 32 + 4 * q4) =
+        make_float4(acc1[4 * q4] * inv, acc1[4 * q4 + 1] * inv, acc1[4 * q4 + 2] * inv, acc1[4 * q4 + 3] * inv);
+  }
+}
+
 }  // namespace
 }  // namespace rmbx
 
@@ -737,6 +974,49 @@ extern "C" int rmbx_attention_f32x6(const float* q, const float* k, const float*
   a.parts = (ngroups + waves - 1) / waves;
   const long long nblocks = (long long)B * heads * a.parts;
   RMBX_CHECK_ARG(nblocks < (1ll << 31), "rmbx_attention_f32x6: grid too large");
+  hipLaunchKernelGGL(rmbx::attn_fwd_f32x6_kernel, dim3((unsigned)nblocks), dim3(64 * waves), 0, (hipStream_t)stream, a);
+  RMBX_CHECK_LAUNCH();
+  return RMBX_OK;
+}
+
+extern "C" int rmbx_attention_f16x3(const float* q, const float* k, const float* v, float* out, int* redo, int B,
+                                    int heads, int Lq, int Lk, long long q_bstride, int q_rstride, long long k_bstride,
+                                    int k_rstride, long long v_bstride, int v_rstride, float scale, void* stream) {
+  RMBX_CHECK_ARG(q && k && v && out && redo, "rmbx_attention_f16x3: null pointer");
+  RMBX_CHECK_ARG(B >= 0 && heads > 0 && Lq > 0 && Lk > 0, "rmbx_attention_f16x3: bad geometry");
+  RMBX_CHECK_ARG(scale > 0.f, "rmbx_attention_f16x3: scale must be positive");
+  RMBX_CHECK_ARG(q_rstride % 4 == 0 && k_rstride % 4 == 0 && v_rstride % 4 == 0 && q_bstride % 4 == 0 &&
+                     k_bstride % 4 == 0 && v_bstride % 4 == 0,
+                 "rmbx_attention_f16x3: strides must be multiples of 4 elements");
+  RMBX_CHECK_ARG((((uintptr_t)q | (uintptr_t)k | (uintptr_t)v | (uintptr_t)out) & 15) == 0,
+                 "rmbx_attention_f16x3: pointers must be 16-byte aligned");
+  if (B == 0) return RMBX_OK;
+  rmbx::AttnF32Args a;
+  a.q = q;
+  a.k = k;
+  a.v = v;
+  a.o = out;
+  a.q_bstride = q_bstride;
+  a.k_bstride = k_bstride;
+  a.v_bstride = v_bstride;
+  a.q_rstride = q_rstride;
+  a.k_rstride = k_rstride;
+  a.v_rstride = v_rstride;
+  a.o_rstride = heads * 64;
+  a.heads = heads;
+  a.Lq = Lq;
+  a.Lk = Lk;
+  a.scale_log2 = scale * 1.4426950408889634f;
+  a.redo = redo;
+  const int ngroups = (Lq + 31) / 32;
+  const int waves = ngroups >= rmbx::AX_MAX_WAVES ? rmbx::AX_MAX_WAVES : 4;
+  a.parts = (ngroups + waves - 1) / waves;
+  const long long nblocks = (long long)B * heads * a.parts;
+  RMBX_CHECK_ARG(nblocks < (1ll << 31), "rmbx_attention_f16x3: grid too large");
+  // the f16x3 pass, then the bf16x6 kernel over the same blocks: it returns at once for every block
+  // the first pass did not flag (redo[block] = 0), so both write each query once
+  hipLaunchKernelGGL(rmbx::attn_fwd_f16x3_kernel, dim3((unsigned)nblocks), dim3(64 * waves), 0, (hipStream_t)stream, a);
+  RMBX_CHECK_LAUNCH();
   hipLaunchKernelGGL(rmbx::attn_fwd_f32x6_kernel, dim3((unsigned)nblocks), dim3(64 * waves), 0, (hipStream_t)stream, a);
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;

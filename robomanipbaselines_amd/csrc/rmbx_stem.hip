@@ -740,7 +740,10 @@ __device__ __forceinline__ void u8x16_to_f16(uint4 v, bool ok, uint4& lo, uint4&
 // its max in [2^13, 2^14)), both products in one accumulator on v_mfma_f32_32x32x16_f16 and the
 // accumulator scaled by 2^-s before the bias: 2 MFMAs per tap and tile instead of 3, weights
 // represented to 2^-22 (the f16x3 GEMM's weight split, csrc/rmbx_gemm.hip)
-template <bool DPP, bool H2 = false>
+// VAR (profiling, RMBX_STEM_VAR; wrong results, timing only): bit 0 = no pool epilogue (one store
+// per lane keeps the accumulators live), bit 1 = no ring refill (no prefetch loads / conversions),
+// bit 2 = no MFMAs
+template <bool DPP, bool H2 = false, int VAR = 0>
 __global__ void __launch_bounds__(SF_THREADS) stem_pool_u8w4_kernel(StemPoolU8Args a) {
   constexpr int NP = H2 ? 2 : 3;  // weight pieces
   __shared__ __attribute__((aligned(16))) unsigned char sq_smem[16 * NP * 2 * 64 * 16 + SP_RING * 2 * SF_RC * 16 +
@@ -806,7 +809,7 @@ __global__ void __launch_bounds__(SF_THREADS) stem_pool_u8w4_kernel(StemPoolU8Ar
   __syncthreads();
   for (int py = pys; py < py1; ++py) {
     const int Y0 = 2 * py;
-    const bool more = py + 1 < py1;
+    const bool more = (VAR & 2) == 0 && py + 1 < py1;
     if (more) {
       pf_ok = 0;
 #pragma unroll
@@ -845,7 +848,9 @@ __global__ void __launch_bounds__(SF_THREADS) stem_pool_u8w4_kernel(StemPoolU8Ar
         for (int p = NP - 1; p >= 0; --p)
 #pragma unroll
           for (int r = 0; r < 2; ++r) {
-            if constexpr (H2)
+            if constexpr ((VAR & 4) != 0)
+              acc[i][r][p] += __uint_as_float(__builtin_bit_cast(uint4, aw[p]).x ^ __builtin_bit_cast(uint4, bx[r]).y);
+            else if constexpr (H2)
               acc[i][r] = __builtin_amdgcn_mfma_f32_32x32x16_f16(__builtin_bit_cast(f16x8s, aw[p]),
                                                                   __builtin_bit_cast(f16x8s, bx[r]), acc[i][r], 0, 0, 0);
             else
@@ -854,6 +859,27 @@ __global__ void __launch_bounds__(SF_THREADS) stem_pool_u8w4_kernel(StemPoolU8Ar
       }
     }
 
+    if constexpr ((VAR & 1) != 0) {
+      float sum = 0.f;
+#pragma unroll
+      for (int i = 0; i < SF_TILES; ++i)
+#pragma unroll
+        for (int k = 0; k < 16; ++k) sum += acc[i][0][k] + acc[i][1][k];
+      a.out[(((size_t)img * a.Hp + py) * a.Wp) * 64 + tid] = sum;
+      __syncthreads();
+      if (more) {
+#pragma unroll
+        for (int i = 0; i < PF_MAX; ++i) {
+          const int q = tid + SF_THREADS * i;
+          if (q < 2 * SF_RC) {
+            const int r = q / SF_RC, c = q - r * SF_RC;
+            store_px(slot_of(Y0 + 3 + r), c, pf[i], (pf_ok >> i) & 1u);
+          }
+        }
+      }
+      __syncthreads();
+      continue;
+    }
     const bool row1_ok = Y0 + 1 < a.Hs;
     int rm[2];
 #pragma unroll
@@ -1040,9 +1066,19 @@ int rmbx::stem_u8_impl(const uint8_t* in, const void* w_planes, float wscale, bo
   a.bands = (a.Hp + band_rows - 1) / band_rows;
   const long long nblocks = (long long)N * a.bands;
   RMBX_CHECK_ARG(nblocks < (1ll << 31), "rmbx_stem_s2d_conv_maxpool_u8: grid too large");
-  if (h2)
-    hipLaunchKernelGGL((rmbx::stem_pool_u8w4_kernel<true, true>), dim3((unsigned)nblocks), dim3(rmbx::SF_THREADS), 0,
-                       (hipStream_t)stream, a);
+  const char* ve = h2 ? getenv("RMBX_STEM_VAR") : nullptr;  // profiling phase skips (read per launch)
+  const int var = ve ? atoi(ve) : 0;
+  if (h2) {
+    const dim3 grid((unsigned)nblocks), blk(rmbx::SF_THREADS);
+    switch (var) {
+      case 1: hipLaunchKernelGGL((rmbx::stem_pool_u8w4_kernel<true, true, 1>), grid, blk, 0, (hipStream_t)stream, a); break;
+      case 2: hipLaunchKernelGGL((rmbx::stem_pool_u8w4_kernel<true, true, 2>), grid, blk, 0, (hipStream_t)stream, a); break;
+      case 3: hipLaunchKernelGGL((rmbx::stem_pool_u8w4_kernel<true, true, 3>), grid, blk, 0, (hipStream_t)stream, a); break;
+      case 4: hipLaunchKernelGGL((rmbx::stem_pool_u8w4_kernel<true, true, 4>), grid, blk, 0, (hipStream_t)stream, a); break;
+      case 6: hipLaunchKernelGGL((rmbx::stem_pool_u8w4_kernel<true, true, 6>), grid, blk, 0, (hipStream_t)stream, a); break;
+      default: hipLaunchKernelGGL((rmbx::stem_pool_u8w4_kernel<true, true>), grid, blk, 0, (hipStream_t)stream, a);
+    }
+  }
   else if (layout == 10)
     hipLaunchKernelGGL(rmbx::stem_pool_u8_kernel, dim3((unsigned)nblocks), dim3(64 * a.nct), 0, (hipStream_t)stream, a);
   else if (dpp)

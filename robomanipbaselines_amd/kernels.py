@@ -831,10 +831,15 @@ def attention_bf16(q, k, v, heads, scale=None):
     return out
 
 
-def attention_f32(q, k, v, heads, scale=None, x6=False):
-    """attention_bf16 in f32 (rmbx_attention_f32: exact f32 MFMA products, f32 online softmax; x6:
-    rmbx_attention_f32x6, the same products fp32-accurate on the bf16 matrix cores by three-piece
-    splits): f32 [B, L, heads * 64] views with a contiguous last dim -> contiguous [B, Lq, heads * 64]."""
+def attention_f32(q, k, v, heads, scale=None, x6=False, form=None):
+    """attention_bf16 in f32: f32 [B, L, heads * 64] views with a contiguous last dim -> contiguous
+    [B, Lq, heads * 64].  form "f32" (rmbx_attention_f32: exact f32 MFMA products, f32 online
+    softmax), "x6" (rmbx_attention_f32x6: the same products fp32-accurate on the bf16 matrix cores by
+    three-piece splits) or "f16x3" (rmbx_attention_f16x3: two f16 pieces, three products, blocks
+    outside f16's range re-run as x6); x=True is form "x6"."""
+    form = form or ("x6" if x6 else "f32")
+    if form not in ("f32", "x6", "f16x3"):
+        raise ValueError(f"attention_f32: unknown form {form!r}")
     for t, nm in ((q, "q"), (k, "k"), (v, "v")):
         if not isinstance(t, torch.Tensor) or not t.is_cuda or t.dtype != torch.float32 or t.dim() != 3:
             raise ValueError(f"{nm} must be an f32 [B, L, D] device tensor")
@@ -846,9 +851,15 @@ def attention_f32(q, k, v, heads, scale=None, x6=False):
         raise ValueError("k and v must be [B, Lk, D] like q")
     scale = 1.0 / 8.0 if scale is None else float(scale)
     out = torch.empty((B, Lq, D), dtype=torch.float32, device=q.device)
-    N.call("rmbx_attention_f32x6" if x6 else "rmbx_attention_f32", N.ptr(q), N.ptr(k), N.ptr(v), N.ptr(out), B,
-           heads, Lq, Lk, q.stride(0), q.stride(1), k.stride(0), k.stride(1), v.stride(0), v.stride(1), scale,
-           N.stream_ptr())
+    strides = (q.stride(0), q.stride(1), k.stride(0), k.stride(1), v.stride(0), v.stride(1), scale, N.stream_ptr())
+    if form == "f16x3":
+        # one re-run flag per block (blocks = B x heads x query parts <= B x heads x 32-query groups)
+        redo = torch.empty(max(1, B * heads * ((Lq + 31) // 32)), dtype=torch.int32, device=q.device)
+        N.call("rmbx_attention_f16x3", N.ptr(q), N.ptr(k), N.ptr(v), N.ptr(out), N.ptr(redo), B, heads, Lq, Lk,
+               *strides)
+    else:
+        N.call("rmbx_attention_f32x6" if form == "x6" else "rmbx_attention_f32", N.ptr(q), N.ptr(k), N.ptr(v),
+               N.ptr(out), B, heads, Lq, Lk, *strides)
     return out
 
 

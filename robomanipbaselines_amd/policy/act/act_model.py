@@ -48,9 +48,10 @@ def sine_pos_embed(h, w, num_pos_feats=256, temperature=10000, device=None, dtyp
 # products; both at the bf16 MFMA rate with f32 accumulation, the f32 GEMM error class,
 # tests/test_gemm_gpu.py), "blas" = hipBLASLt f32; env RMBX_F32_GEMM
 F32_GEMM = os.environ.get("RMBX_F32_GEMM", "x6")
-# f32 attention products: "x6" = rmbx_attention_f32x6 (bf16x6 pieces), "f32" = rmbx_attention_f32
-# (f32 MFMA); env RMBX_F32_ATTN
-F32_ATTN = os.environ.get("RMBX_F32_ATTN", "x6")
+# f32 attention products: "f16x3" = rmbx_attention_f16x3 (two f16 pieces, three products; blocks
+# outside f16's range re-run as x6), "x6" = rmbx_attention_f32x6 (bf16x6 pieces), "f32" =
+# rmbx_attention_f32 (f32 MFMA); env RMBX_F32_ATTN
+F32_ATTN = os.environ.get("RMBX_F32_ATTN", "f16x3")
 
 
 def _x6_ok(x, n_out):
@@ -173,7 +174,7 @@ class MHA(nn.Module):
         if self.fused_attention and qq.dtype == torch.float32 and hd == 64 and qq.is_cuda:
             from ... import kernels as K
 
-            return self._out_proj(K.attention_f32(qq, kk, vv, self.h, x6=F32_ATTN == "x6"))
+            return self._out_proj(K.attention_f32(qq, kk, vv, self.h, form=F32_ATTN))
         qq = qq.view(B, Lq, self.h, hd).transpose(1, 2)
         kk = kk.view(B, Lk, self.h, hd).transpose(1, 2)
         vv = vv.view(B, Lk, self.h, hd).transpose(1, 2)

@@ -8,3 +8,4 @@ timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_ou
 timeout -k 10 600 python -u bench.py > gpurun_out/r4_final_bench.json.log 2> gpurun_out/r4_final_bench.err || exit 1
 bash scripts/gpurun/r3_benchprof.sh r4final || exit 1
 bash scripts/gpurun/gemm_pmc.sh r4final || exit 1
+timeout -k 10 200 python -u scripts/prof_stem_phases.py > gpurun_out/r4_final_stem_phases.log 2>&1 || exit 1

@@ -1,0 +1,7 @@
+#!/bin/bash
+# f16x3 attention: its tests + the ACT-shape A/B, then the round-4 records (r4_final.sh)
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest -v --timeout 120 --timeout-method thread -m gpu tests/test_attention_gpu.py tests/test_gemm_gpu.py > gpurun_out/r4_q_attn_gemm_tests.log 2>&1 || exit 1
+timeout -k 10 200 python -u scripts/prof_attn_forms.py > gpurun_out/r4_q_attn_forms.log 2>&1 || exit 1
+bash scripts/gpurun/r4_final.sh

