@@ -30,6 +30,7 @@
 
 #include <cstdint>
 #include <cstdlib>
+#include <type_traits>
 
 namespace rmbx {
 namespace {
@@ -713,11 +714,12 @@ __global__ void __launch_bounds__(SP_THREADS) stem_pool_u8_kernel(StemPoolU8Args
 // w & 1 of column tiles 5 (w >> 1) .. + 4 for both stem rows (10 accumulators, 512 registers).
 // the value of lane l - 1 / l + 1 by a DPP wave shift (one VALU move instead of an LDS permute;
 // gfx9 wave_shr:1 / wave_shl:1; the lanes without a neighbour are overridden by the caller)
+// (bound_ctrl: a lane without a source reads 0 -- no separate zero-initialised destination)
 __device__ __forceinline__ float dpp_from_left(float x) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x138, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x138, 0xf, 0xf, true));
 }
 __device__ __forceinline__ float dpp_from_right(float x) {
-  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), 0x130, 0xf, 0xf, false));
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), 0x130, 0xf, 0xf, true));
 }
 
 // 16 u8 pixel channels -> two 16-B halves of the CENTRED f16 integers u - 128 (exact)
@@ -742,7 +744,11 @@ __device__ __forceinline__ void u8x16_to_f16(uint4 v, bool ok, uint4& lo, uint4&
 // represented to 2^-22 (the f16x3 GEMM's weight split, csrc/rmbx_gemm.hip)
 // VAR (profiling, RMBX_STEM_VAR; wrong results, timing only): bit 0 = no pool epilogue (one store
 // per lane keeps the accumulators live), bit 1 = no ring refill (no prefetch loads / conversions),
-// bit 2 = no MFMAs
+// bit 2 = no MFMAs.  Round 4 (profiles/r4_stem_u8h_phase_skips.log -> ..._epilogue_v2.log): the
+// pool epilogue cost more than the MFMAs (8.17 ms per 1024 frames, 3.55 without it); without its
+// per-element branches (edge terms behind one wave-uniform test per tile, the column mask as a bit
+// mask, the left neighbour by two readlanes instead of an LDS permute, DPP moves with bound_ctrl)
+// the kernel runs 5.62 ms.
 template <bool DPP, bool H2 = false, int VAR = 0>
 __global__ void __launch_bounds__(SF_THREADS) stem_pool_u8w4_kernel(StemPoolU8Args a) {
   constexpr int NP = H2 ? 2 : 3;  // weight pieces
@@ -753,7 +759,8 @@ __global__ void __launch_bounds__(SF_THREADS) stem_pool_u8w4_kernel(StemPoolU8Ar
   float* sBias = reinterpret_cast<float*>(sR + SP_RING * 2 * SF_RC * 8);  // [64]
   float* sEdge = sBias + 64;                                              // [waves][2 h][16]
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // (the wave index as a scalar: the tile / channel-half choices derived from it stay uniform)
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int img = blockIdx.x / a.bands, band = blockIdx.x - img * a.bands;
   const int py0 = band * a.band_rows;
   const int py1 = min(a.Hp, py0 + a.band_rows);
@@ -881,6 +888,12 @@ __global__ void __launch_bounds__(SF_THREADS) stem_pool_u8w4_kernel(StemPoolU8Ar
       continue;
     }
     const bool row1_ok = Y0 + 1 < a.Hs;
+    bool tile_edge[SF_TILES];  // wave-uniform: tile i holds a column within 2 of either image edge
+#pragma unroll
+    for (int i = 0; i < SF_TILES; ++i) {
+      const int X0 = 32 * (ct0 + i);
+      tile_edge[i] = X0 < 2 || X0 + 33 >= a.Ws;
+    }
     int rm[2];
 #pragma unroll
     for (int r = 0; r < 2; ++r) {
@@ -895,26 +908,43 @@ __global__ void __launch_bounds__(SF_THREADS) stem_pool_u8w4_kernel(StemPoolU8Ar
       int cm = 0;
 #pragma unroll
       for (int kx = 0; kx < 4; ++kx) cm |= (int)((unsigned)(X - 2 + kx) >= (unsigned)a.Ws) << kx;
-      const float* ep0 = (rm[0] | cm) ? a.edge + (rm[0] * 16 + cm) * 64 + 32 * t + 16 * h : nullptr;
-      const float* ep1 = (rm[1] | cm) ? a.edge + (rm[1] * 16 + cm) * 64 + 32 * t + 16 * h : nullptr;
+      // the mean term of the out-of-image taps: only rows near the image's top / bottom and the
+      // first / last column tiles have any (a wave-uniform test, no per-element exec masking); the
+      // edge table's entry (0, 0) is zero, so every lane reads a valid row
+      const int col_mask = col_ok ? -1 : 0;
+      const float* ep0 = a.edge + (rm[0] * 16 + cm) * 64 + 32 * t + 16 * h;
+      const float* ep1 = a.edge + (rm[1] * 16 + cm) * 64 + 32 * t + 16 * h;
+      auto pool_rows = [&](auto edge) {
 #pragma unroll
-      for (int k = 0; k < 16; ++k) {
-        const float b = sBias[32 * t + 16 * h + k];
-        float v0, v1;
-        if constexpr (H2) {  // undo the weights' power of two (exact), then the bias
-          v0 = fmaf(acc[i][0][k], a.wscale, b);
-          v1 = fmaf(acc[i][1][k], a.wscale, b);
-        } else {
-          v0 = acc[i][0][k] + b;
-          v1 = acc[i][1][k] + b;
+        for (int k = 0; k < 16; ++k) {
+          const float b = sBias[32 * t + 16 * h + k];
+          float v0, v1;
+          if constexpr (H2) {  // undo the weights' power of two (exact), then the bias
+            v0 = fmaf(acc[i][0][k], a.wscale, b);
+            v1 = fmaf(acc[i][1][k], a.wscale, b);
+          } else {
+            v0 = acc[i][0][k] + b;
+            v1 = acc[i][1][k] + b;
+          }
+          if constexpr (decltype(edge)::value) {  // + 0 where no tap is outside
+            v0 += ep0[k];
+            v1 += ep1[k];
+          }
+          const float p0 = fmaxf(v0, 0.f);
+          const float p1 = fmaxf(v1, 0.f);  // 0 for a missing second row (-inf, set above)
+          // columns past the image: 0 (a bit mask, not a select the compiler turns into a branch)
+          acc[i][0][k] = __int_as_float(__float_as_int(fmaxf(fmaxf(carry[i][k], p0), p1)) & col_mask);
+          carry[i][k] = p1;
         }
-        if (ep0) v0 += ep0[k];  // border pixels only
-        if (ep1) v1 += ep1[k];
-        const float p0 = fmaxf(v0, 0.f);
-        const float p1 = row1_ok ? fmaxf(v1, 0.f) : 0.f;
-        acc[i][0][k] = col_ok ? fmaxf(fmaxf(carry[i][k], p0), p1) : 0.f;
-        carry[i][k] = p1;
+      };
+      if (!row1_ok) {  // odd stem height: the last pool row has one stem row; -inf pools as 0
+#pragma unroll
+        for (int k = 0; k < 16; ++k) acc[i][1][k] = -INFINITY;
       }
+      if (rm[0] != 0 || rm[1] != 0 || tile_edge[i])
+        pool_rows(std::true_type{});
+      else
+        pool_rows(std::false_type{});
     }
     if (n == 31) {
 #pragma unroll
@@ -947,9 +977,11 @@ __global__ void __launch_bounds__(SF_THREADS) stem_pool_u8w4_kernel(StemPoolU8Ar
             float left = DPP ? dpp_from_left(acc[i][0][k]) : __shfl_up(acc[i][0][k], 1);
             const float right = DPP ? dpp_from_right(acc[i][0][k]) : __shfl_down(acc[i][0][k], 1);
             float prev;
-            if (i > 0)
-              prev = __shfl(acc[i - 1][0][k], (lane & 32) | 31);
-            else
+            if (i > 0) {  // lane 31 / 63 of the tile on the left (same channel half): two readlanes
+              const int x = __float_as_int(acc[i - 1][0][k]);
+              const int l31 = __builtin_amdgcn_readlane(x, 31), l63 = __builtin_amdgcn_readlane(x, 63);
+              prev = __int_as_float(l31 ^ ((l31 ^ l63) & -h));
+            } else
               prev = wave >= 2 ? sEdge[((wave - 2) * 2 + h) * 16 + k] : 0.f;
             if (n == 0) left = prev;
             o[e] = fmaxf(fmaxf(left, acc[i][0][k]), right);
