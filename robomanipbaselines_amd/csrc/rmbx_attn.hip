@@ -247,6 +247,7 @@ struct AttnF32Args {
   // rmbx_attention_f16x3: per block, 1 = re-run on the bf16x6 kernel (written by the f16x3 kernel;
   // the bf16x6 kernel then runs only the flagged blocks); null for the other kernels
   int* redo = nullptr;
+  int xcd_map = 0;  // f16x3 kernel: the parts of a head on one XCD (RMBX_ATTN_XCD=0 disables; A/B)
 };
 
 template <int DBG>
@@ -656,7 +657,18 @@ __global__ void __launch_bounds__(64 * AX_MAX_WAVES) attn_fwd_f16x3_kernel(AttnF
   __shared__ uint32_t sDim[64];  // per head dimension: max |v| over the keys (f32 bits)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nthreads = blockDim.x;
-  const int bh = blockIdx.x / a.parts, part = blockIdx.x - bh * a.parts;
+  // block -> (head, query part): the parts of one head on one XCD, one after the other (blocks
+  // bid and bid + 8 when parts = 2), so the second part's K / V reads hit that XCD's L2; the plain
+  // order when the heads do not divide into the 8 XCDs
+  int bh, part;
+  if (a.xcd_map && a.parts > 1 && (gridDim.x & (8 * a.parts - 1)) == 0 && (a.parts & (a.parts - 1)) == 0) {
+    const int j = blockIdx.x >> 3;
+    part = j & (a.parts - 1);
+    bh = (j / a.parts) * 8 + (blockIdx.x & 7);
+  } else {
+    bh = blockIdx.x / a.parts;
+    part = blockIdx.x - bh * a.parts;
+  }
   const int b = bh / a.heads, hd = bh - b * a.heads;
   const int r32 = lane & 31, kh = lane >> 5;
   const int qi = (part * (nthreads >> 6) + wave) * 32 + r32;
@@ -829,7 +841,7 @@ __global__ void __launch_bounds__(64 * AX_MAX_WAVES) attn_fwd_f16x3_kernel(AttnF
     flag = flag || (m > 0.f && m < AH_TINY);
   }
   const int any = __syncthreads_or(flag ? 1 : 0);
-  if (tid == 0) a.redo[blockIdx.x] = any;
+  if (tid == 0) a.redo[bh * a.parts + part] = any;  // the bf16x6 kernel's block order
   if (any) return;
   const float l_tot = l_run + __shfl_xor(l_run, 32);
   if (!q_ok) return;
@@ -1008,6 +1020,8 @@ extern "C" int rmbx_attention_f16x3(const float* q, const float* k, const float*
   a.Lk = Lk;
   a.scale_log2 = scale * 1.4426950408889634f;
   a.redo = redo;
+  const char* xe = std::getenv("RMBX_ATTN_XCD");  // read per launch (A/B in one process)
+  a.xcd_map = !(xe && std::atoi(xe) == 0);
   const int ngroups = (Lq + 31) / 32;
   const int waves = ngroups >= rmbx::AX_MAX_WAVES ? rmbx::AX_MAX_WAVES : 4;
   a.parts = (ngroups + waves - 1) / waves;

@@ -165,8 +165,9 @@ def test_attention_f16x3_strided_qkv_views():
 
 
 @torch.no_grad()
+@pytest.mark.parametrize("shape", [(3, 2, 100, 90), (4, 2, 302, 90)])  # 1 / 2 query parts per head
 @pytest.mark.parametrize("case", ["huge_q", "huge_k", "huge_v", "tiny_v_dim", "tiny_all", "zero_v_dim"])
-def test_attention_f16x3_range_and_block_independence(case):
+def test_attention_f16x3_range_and_block_independence(case, shape):
     """Out-of-f16-range inputs in ONE batch item (|q|, |k| or |v| >= 2^15, a head dimension of V
     whose max is below 2^-6, everything scaled by 1e-6) re-run that item's blocks on the bf16x6
     kernel: the result stays within f32 accuracy of f64 relative to each item's own output scale, the
@@ -175,7 +176,7 @@ def test_attention_f16x3_range_and_block_independence(case):
     from robomanipbaselines_amd import kernels as K
 
     g = torch.Generator(device=DEV).manual_seed(7)
-    B, H, Lq, Lk = 3, 2, 100, 90
+    B, H, Lq, Lk = shape
     D = H * 64
     q = torch.randn(B, Lq, D, device=DEV, generator=g)
     k = torch.randn(B, Lk, D, device=DEV, generator=g)
@@ -205,7 +206,9 @@ def test_attention_f16x3_range_and_block_independence(case):
         scale = want[b].abs().max().item()
         err = (got[b].double() - want[b]).abs().max().item() / scale
         assert err < 1e-6, (case, b, err)
-    assert torch.equal(got[0], base[0]) and torch.equal(got[2], base[2])
+    for b in range(B):
+        if b != 1:
+            assert torch.equal(got[b], base[b])
     if case in ("huge_q", "tiny_all"):
         assert torch.equal(got[1], x6[1]), case  # every block of item 1 re-ran on bf16x6
     if case in ("huge_k", "tiny_v_dim"):  # head 0 re-ran, head 1 kept its f16x3 result
