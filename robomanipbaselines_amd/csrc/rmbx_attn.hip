@@ -247,7 +247,7 @@ struct AttnF32Args {
   // rmbx_attention_f16x3: per block, 1 = re-run on the bf16x6 kernel (written by the f16x3 kernel;
   // the bf16x6 kernel then runs only the flagged blocks); null for the other kernels
   int* redo = nullptr;
-  int xcd_map = 0;  // f16x3 kernel: the parts of a head on one XCD (RMBX_ATTN_XCD=0 disables; A/B)
+  int xcd_map = 0;  // f16x3 kernel: the parts of a head on one XCD (RMBX_ATTN_XCD=1; not faster)
 };
 
 template <int DBG>
@@ -657,9 +657,9 @@ __global__ void __launch_bounds__(64 * AX_MAX_WAVES) attn_fwd_f16x3_kernel(AttnF
   __shared__ uint32_t sDim[64];  // per head dimension: max |v| over the keys (f32 bits)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nthreads = blockDim.x;
-  // block -> (head, query part): the parts of one head on one XCD, one after the other (blocks
-  // bid and bid + 8 when parts = 2), so the second part's K / V reads hit that XCD's L2; the plain
-  // order when the heads do not divide into the 8 XCDs
+  // block -> (head, query part): plain order, or (xcd_map) the parts of one head on one XCD, one
+  // after the other (blocks bid and bid + 8 when parts = 2) so the second part's K / V reads could
+  // hit that XCD's L2
   int bh, part;
   if (a.xcd_map && a.parts > 1 && (gridDim.x & (8 * a.parts - 1)) == 0 && (a.parts & (a.parts - 1)) == 0) {
     const int j = blockIdx.x >> 3;
@@ -1020,8 +1020,11 @@ extern "C" int rmbx_attention_f16x3(const float* q, const float* k, const float*
   a.Lk = Lk;
   a.scale_log2 = scale * 1.4426950408889634f;
   a.redo = redo;
-  const char* xe = std::getenv("RMBX_ATTN_XCD");  // read per launch (A/B in one process)
-  a.xcd_map = !(xe && std::atoi(xe) == 0);
+  // RMBX_ATTN_XCD=1 (read per launch): the query parts of a head paired on one XCD -- measured no
+  // faster (1.774 vs 1.756 ms encoder self-attention, profiles/r4_attention_xcd_pairing_ab.log):
+  // the kernel is not bound by its K / V reads
+  const char* xe = std::getenv("RMBX_ATTN_XCD");
+  a.xcd_map = xe && std::atoi(xe) != 0;
   const int ngroups = (Lq + 31) / 32;
   const int waves = ngroups >= rmbx::AX_MAX_WAVES ? rmbx::AX_MAX_WAVES : 4;
   a.parts = (ngroups + waves - 1) / waves;
