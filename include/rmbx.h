@@ -476,6 +476,14 @@ int rmbx_linear_f16x3_batched(const float* a, long long lda, long long a_bs, con
                               long long w_plane_stride, long long w_bs, const float* w_scale, long long ws_bs,
                               const float* bias, float* c, long long ldc, long long c_bs, int batch, int M, int N,
                               int K, int relu, void* stream);
+/* 3x3 / stride-1 / pad-1 rmbx_conv2d_f16x3 with each input pixel split once per output tile: the
+ * block stages the input patch of its 16 x 16 (Cout % 128 == 0) or 16 x 32 output tile for one
+ * 32-channel chunk as two f16 pieces in LDS, scaled per (tile, chunk) by a power of two, and all
+ * nine taps read it.  w_planes / w_scale: rmbx_split_f16x2 of the [Cout][3][3][C] filter (plane
+ * stride w_plane_stride elements); C % 32 == 0, Cout % 64 == 0; res / bias nullable; NHWC. */
+int rmbx_conv3x3_f16x3_patch(const float* in, int N, int H, int W, int C, const void* w_planes,
+                             long long w_plane_stride, const float* w_scale, const float* bias, const float* res,
+                             float* out, int Cout, int relu, void* stream);
 int rmbx_conv2d_f16x3(const float* in, int N, int H, int W, int C, const void* w_planes, const float* w_scale,
                       const float* bias, const float* res, float* out, int Cout, int KH, int KW, int stride, int pad,
                       int relu, void* stream);

@@ -1056,6 +1056,40 @@ def conv2d_f32x6(x, planes, bias, kernel_size, stride=1, padding=0, relu=False, 
     return out
 
 
+def conv3x3_f16x3_patch(x, planes, bias, relu=False, res=None):
+    """relu?(conv2d(x, w, stride 1, pad 1) + bias + res), fp32-accurate, by rmbx_conv3x3_f16x3_patch:
+    the f16x3 form with each input pixel split once per output tile (16 x 16 or 16 x 32 pixels,
+    the input patch of a 32-channel chunk staged in LDS for all nine taps) instead of once per tap.
+    planes = pack_conv_f32x6(w) in the f16x3 form (F16x3Planes [2, Cout, 9 C]); x f32 channels_last
+    [N, C, H, W] with C % 32 == 0, Cout % 64 == 0; result channels_last."""
+    if x.dtype != torch.float32 or not x.is_cuda or x.dim() != 4:
+        raise ValueError("conv3x3_f16x3_patch: x must be an f32 device tensor [N, C, H, W]")
+    if not x.is_contiguous(memory_format=torch.channels_last):
+        raise ValueError("conv3x3_f16x3_patch: x must be channels_last")
+    n, c, h, w_ = x.shape
+    cout, kk, h3 = _planes_nk(planes, "conv3x3_f16x3_patch")
+    if not h3:
+        raise ValueError("conv3x3_f16x3_patch: planes must be in the f16x3 form")
+    if kk != 9 * c or c % 32 or cout % 64:
+        raise ValueError(f"conv3x3_f16x3_patch: C={c} (multiple of 32), Cout={cout} (multiple of 64), "
+                         "planes = pack_conv_f32x6 of a 3x3 weight")
+    pt = planes.planes
+    if not pt.is_contiguous():
+        raise ValueError("conv3x3_f16x3_patch: planes must be contiguous")
+    if bias is not None:
+        _chk(bias, torch.float32, (cout,), "bias")
+    out = torch.empty((n, cout, h, w_), dtype=torch.float32, device=x.device, memory_format=torch.channels_last)
+    if res is not None:
+        if res.shape != out.shape or res.dtype != torch.float32 or not res.is_contiguous(memory_format=torch.channels_last):
+            raise ValueError("conv3x3_f16x3_patch: res must be a channels_last f32 tensor shaped like the output")
+    name = f"conv3x3p {c}->{cout} {h}x{w_}"
+    flops = 2.0 * n * h * w_ * cout * c * 9
+    nbytes = 4 * n * h * w_ * c + 4 * cout * c * 9 + 4 * n * h * w_ * cout * (1 if res is None else 2)
+    _gemm_launch(name, flops, nbytes, 3, "rmbx_conv3x3_f16x3_patch", N.ptr(x), n, h, w_, c, N.ptr(pt), pt.stride(0),
+                 N.ptr(planes.scale), N.ptr(bias), N.ptr(res), N.ptr(out), cout, 1 if relu else 0, N.stream_ptr())
+    return out
+
+
 WINO_X6_CHANNELS = (256, 512)
 
 

@@ -1,0 +1,6 @@
+#!/bin/bash
+# patch-staged f16x3 3x3 conv: tests, then the A/B against the Winograd / implicit-GEMM paths
+set -o pipefail
+cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
+timeout -k 10 300 python -u -m pytest -v --timeout 120 --timeout-method thread -m gpu tests/test_convp_gpu.py > gpurun_out/r4_u_convp_tests.log 2>&1 || exit 1
+timeout -k 10 300 python -u scripts/prof_convp.py > gpurun_out/r4_u_convp_ab.log 2>&1 || exit 1
