@@ -237,7 +237,8 @@ def gemm_probe(ro):
                             "the calls of one fp32 ACT inference at 1024 envs",
             "traffic_source": src,
             "algorithmic_bytes_per_launch": round(nbytes / len(probe)),
-            "kernel": f"rmbx::gemm_f32x6_kernel (fp32-accurate GEMM / implicit-GEMM conv, {form}, f32 accumulation)",
+            "kernel": f"rmbx::gemm_f32x6_kernel + rmbx::conv3x3p_f16x3_kernel (fp32-accurate GEMM / implicit-GEMM "
+                      f"and patch-staged 3x3 convs, {form}, f32 accumulation)",
             "flops": "executed MFMA FLOPs = products x the f32 problem's 2*M*N*K (3 for f16x3, 6 for bf16x6)",
             "achieved_fp32_equivalent": round(eq, 2), "f32_mfma_peak": MFMA_PEAK_TFLOPS["fp32"],
             "launches_per_inference": n, "avg_launch_us": round(1e3 * ms / n, 1),

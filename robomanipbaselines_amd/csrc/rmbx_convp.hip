@@ -80,7 +80,7 @@ __global__ void __launch_bounds__(CP_THREADS, 1) conv3x3p_f16x3_kernel(ConvPArgs
   constexpr int NWR = (2 * BN * 4) / CP_THREADS;               // W 16-B loads per thread
   constexpr int WN = BN / 64;                                   // waves across the channels
   __shared__ __attribute__((aligned(16))) unsigned char sP[2 * PLANE];
-  __shared__ __attribute__((aligned(16))) unsigned char sW[2 * 2 * WPLANE];
+  __shared__ __attribute__((aligned(16))) unsigned char sW[2 * 3 * 2 * WPLANE];  // [buf][kx][piece][row]
   __shared__ unsigned int sMax;
 
   const int tid = threadIdx.x, lane = tid & 63;
@@ -148,9 +148,11 @@ __global__ void __launch_bounds__(CP_THREADS, 1) conv3x3p_f16x3_kernel(ConvPArgs
     return 14 - e;
   };
 
-  // ---- W of K step (unit u, chunk c, tap): item q = tid + 512 i -> piece, row, 16-B slot
-  // (NWR = 1 or 2 named registers, not an array: hipcc kept a captured uint4 array in scratch)
-  uint4 wr0 = make_uint4(0, 0, 0, 0), wr1 = make_uint4(0, 0, 0, 0);
+  // ---- W of one filter row (unit u, chunk c, ky; its three taps kx): item q = tid + 512 i ->
+  // (kx, piece, row, 16-B slot); 3 NWR named registers (not an array: hipcc kept a captured
+  // uint4 array in scratch)
+  static_assert(NWR == 1 || NWR == 2, "BN = 64 or 128");
+  uint4 w00 = make_uint4(0, 0, 0, 0), w01 = w00, w10 = w00, w11 = w00, w20 = w00, w21 = w00;
   auto w_item = [&](int i, int& pc, int& n, int& sl) {
     const int q = tid + CP_THREADS * i;
     pc = q / (BN * 4);
@@ -158,27 +160,38 @@ __global__ void __launch_bounds__(CP_THREADS, 1) conv3x3p_f16x3_kernel(ConvPArgs
     n = rem >> 2;
     sl = rem & 3;
   };
-  auto load_w = [&](int u, int c, int tap) {
-    const int n0 = (u % a.ncb) * BN;
-    const uint16_t* base = a.w + (long long)n0 * K + tap * a.C + c * CP_KC;
+  auto w_src = [&](int u, int c, int ky, int kx, int i) {
     int pc, n, sl;
-    w_item(0, pc, n, sl);
-    wr0 = *reinterpret_cast<const uint4*>(base + pc * a.wps + (long long)n * K + 8 * sl);
+    w_item(i, pc, n, sl);
+    const int n0 = (u % a.ncb) * BN;
+    return reinterpret_cast<const uint4*>(a.w + pc * a.wps + (long long)(n0 + n) * K + (3 * ky + kx) * a.C +
+                                          c * CP_KC + 8 * sl);
+  };
+  auto load_w = [&](int u, int c, int ky) {
+    w00 = *w_src(u, c, ky, 0, 0);
+    w10 = *w_src(u, c, ky, 1, 0);
+    w20 = *w_src(u, c, ky, 2, 0);
     if constexpr (NWR == 2) {
-      w_item(1, pc, n, sl);
-      wr1 = *reinterpret_cast<const uint4*>(base + pc * a.wps + (long long)n * K + 8 * sl);
+      w01 = *w_src(u, c, ky, 0, 1);
+      w11 = *w_src(u, c, ky, 1, 1);
+      w21 = *w_src(u, c, ky, 2, 1);
     }
+  };
+  auto w_dst = [&](int buf, int kx, int i) {
+    int pc, n, sl;
+    w_item(i, pc, n, sl);
+    return reinterpret_cast<uint4*>(sW + ((buf * 3 + kx) * 2 + pc) * WPLANE + n * 64 + cp_slot(n, sl) * 16);
   };
   auto store_w = [&](int buf) {
-    int pc, n, sl;
-    w_item(0, pc, n, sl);
-    *reinterpret_cast<uint4*>(sW + (buf * 2 + pc) * WPLANE + n * 64 + cp_slot(n, sl) * 16) = wr0;
+    *w_dst(buf, 0, 0) = w00;
+    *w_dst(buf, 1, 0) = w10;
+    *w_dst(buf, 2, 0) = w20;
     if constexpr (NWR == 2) {
-      w_item(1, pc, n, sl);
-      *reinterpret_cast<uint4*>(sW + (buf * 2 + pc) * WPLANE + n * 64 + cp_slot(n, sl) * 16) = wr1;
+      *w_dst(buf, 0, 1) = w01;
+      *w_dst(buf, 1, 1) = w11;
+      *w_dst(buf, 2, 1) = w21;
     }
   };
-  static_assert(NWR == 1 || NWR == 2, "BN = 64 or 128");
 
   cp_f32x4 acc[4][4];
 #pragma unroll
@@ -187,8 +200,7 @@ __global__ void __launch_bounds__(CP_THREADS, 1) conv3x3p_f16x3_kernel(ConvPArgs
     for (int j = 0; j < 4; ++j) acc[i][j] = (cp_f32x4){0.f, 0.f, 0.f, 0.f};
 
   // MFMAs of one tap: A fragments from the patch at (ky, kx), B from W buffer wb
-  auto mfma_tap = [&](int tap, int wb) {
-    const int ky = tap / 3, kx = tap - 3 * ky;
+  auto mfma_tap = [&](int ky, int kx, int wb) {
     cp_f16x8 ah[4], al[4];
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi) {
@@ -203,8 +215,8 @@ __global__ void __launch_bounds__(CP_THREADS, 1) conv3x3p_f16x3_kernel(ConvPArgs
     for (int nj = 0; nj < 4; ++nj) {
       const int n = wn * 64 + nj * 16 + fr;
       const int off = n * 64 + cp_slot(n, fs) * 16;
-      const cp_f16x8 bh = *reinterpret_cast<const cp_f16x8*>(sW + (wb * 2) * WPLANE + off);
-      const cp_f16x8 bl = *reinterpret_cast<const cp_f16x8*>(sW + (wb * 2 + 1) * WPLANE + off);
+      const cp_f16x8 bh = *reinterpret_cast<const cp_f16x8*>(sW + ((wb * 3 + kx) * 2) * WPLANE + off);
+      const cp_f16x8 bl = *reinterpret_cast<const cp_f16x8*>(sW + ((wb * 3 + kx) * 2 + 1) * WPLANE + off);
       const cp_f16x8 bs = bh * (_Float16)0.00048828125f;  // 2^-11 hb (exact above f16's subnormals)
 #pragma unroll
       for (int mi = 0; mi < 4; ++mi) {
@@ -217,31 +229,45 @@ __global__ void __launch_bounds__(CP_THREADS, 1) conv3x3p_f16x3_kernel(ConvPArgs
     }
   };
 
+  // epilogue of a unit: per 16-pixel row segment, the 16 residual loads of a lane are issued
+  // together (past-the-image pixels read a clamped in-range address and skip the store)
   auto epilogue = [&](int u, int t) {
     int img, oy0, ox0, n0;
     unit_geo(u, img, oy0, ox0, n0);
+    float sn[4], bb[4];
 #pragma unroll
     for (int nj = 0; nj < 4; ++nj) {
       const int n = n0 + wn * 64 + nj * 16 + fr;
-      const float sn = a.ws[n];
-      const float b = a.bias ? a.bias[n] : 0.f;
+      sn[nj] = a.ws[n];
+      bb[nj] = a.bias ? a.bias[n] : 0.f;
+    }
 #pragma unroll
-      for (int mi = 0; mi < 4; ++mi) {
+    for (int mi = 0; mi < 4; ++mi) {
+      long long idx[4];
+      bool ok[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const int p = wm * 64 + mi * 16 + 4 * fs + e;
+        const int ty = p / TW, tx = p - ty * TW;
+        const int y = oy0 + ty, x = ox0 + tx;
+        ok[e] = y < a.H && x < a.W;
+        idx[e] = ok[e] ? (((long long)img * a.H + y) * a.W + x) * a.Cout + n0 + wn * 64 + fr : 0;
+      }
+      float rv[4][4];
+#pragma unroll
+      for (int nj = 0; nj < 4; ++nj)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) rv[nj][e] = a.res ? a.res[idx[e] + nj * 16] : 0.f;
+#pragma unroll
+      for (int nj = 0; nj < 4; ++nj)
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
-          const int p = wm * 64 + mi * 16 + 4 * fs + e;
-          const int ty = p / TW, tx = p - ty * TW;
-          const int y = oy0 + ty, x = ox0 + tx;
-          if (y < a.H && x < a.W) {
-            const long long idx = (((long long)img * a.H + y) * a.W + x) * a.Cout + n;
-            float v = t == CP_TNONE ? 0.f : ldexpf(acc[mi][nj][e] * sn, -t);
-            v += b;
-            if (a.res) v += a.res[idx];
-            if (a.relu) v = fmaxf(v, 0.f);
-            a.out[idx] = v;
-          }
+          float v = t == CP_TNONE ? 0.f : ldexpf(acc[mi][nj][e] * sn[nj], -t);
+          v += bb[nj];
+          v += rv[nj][e];
+          if (a.relu) v = fmaxf(v, 0.f);
+          if (ok[e]) a.out[idx[e] + nj * 16] = v;
         }
-      }
     }
   };
 
@@ -251,7 +277,7 @@ __global__ void __launch_bounds__(CP_THREADS, 1) conv3x3p_f16x3_kernel(ConvPArgs
   if (u >= a.units) return;
   if (tid == 0) sMax = 0u;
   load_patch(u, 0);
-  load_w(u, 0, 0);
+  load_w(u, 0, 0);  // filter row ky = 0
   __syncthreads();
   atomicMax(&sMax, __float_as_uint(patch_max()));
   __syncthreads();
@@ -269,15 +295,19 @@ __global__ void __launch_bounds__(CP_THREADS, 1) conv3x3p_f16x3_kernel(ConvPArgs
     const int c_next = last_chunk ? 0 : c + 1;
     const bool more = u_next < a.units;
 #pragma unroll 1
-    for (int tap = 0; tap < 9; ++tap) {
-      if (tap == 0 && more) load_patch(u_next, c_next);
-      // W of the next K step, loaded and stored unconditionally (after the last step: a redundant
-      // copy of this step's W into the idle buffer) so the staging registers stay registers
-      const int wu = tap < 8 || !more ? u : u_next, wc = tap < 8 || !more ? c : c_next;
-      const int wt = tap < 8 ? tap + 1 : (more ? 0 : 8);
-      load_w(wu, wc, wt);
-      mfma_tap(tap, wb);
-      if (tap == 4 && more) atomicMax(&sMax, __float_as_uint(patch_max()));
+    for (int ky = 0; ky < 3; ++ky) {
+      if (ky == 0 && more) load_patch(u_next, c_next);
+      // W of the next filter row, loaded and stored unconditionally (after the last row: a
+      // redundant copy of this row into the idle buffer) so the staging registers stay registers
+      const int wu = ky < 2 || !more ? u : u_next, wc = ky < 2 || !more ? c : c_next;
+      const int wk = ky < 2 ? ky + 1 : (more ? 0 : 2);
+      load_w(wu, wc, wk);
+      // keep the loads ahead of the MFMAs (left alone, the scheduler sinks them behind the MFMA
+      // stream, and their latency is exposed at the end of every step)
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int kx = 0; kx < 3; ++kx) mfma_tap(ky, kx, wb);
+      if (ky == 1 && more) atomicMax(&sMax, __float_as_uint(patch_max()));
       store_w(wb ^ 1);
       __syncthreads();
       wb ^= 1;

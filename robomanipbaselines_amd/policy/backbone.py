@@ -179,6 +179,19 @@ class _FusedConv(nn.Module):
     def s1_gemm_ok(self):
         return (self.conv.out_channels in self.S1_GEMM_CHANNELS and K.F32_PIECES == "f16x3" and self.x6_ok())
 
+    # stride-1 3x3 convs whose output width is in this set run on the patch-staged f16x3 conv
+    # (rmbx_conv3x3_f16x3_patch: each input pixel split once per output tile instead of once per
+    # tap) -- 64 channels at 120 x 160, 1024 frames: 6.86 ms vs 7.70 for the fused Winograd (and
+    # 10x closer to f64); 128 channels at 60 x 80: 4.93 vs 5.34 ms for the implicit GEMM
+    # (profiles/r4_conv3x3_patch_ab.log); env RMBX_S1_PATCH ("" = none)
+    S1_PATCH_CHANNELS = tuple(int(c) for c in os.environ.get("RMBX_S1_PATCH", "64,128").split(",") if c)
+
+    def s1_patch_ok(self):
+        c = self.conv
+        return (c.out_channels in self.S1_PATCH_CHANNELS and K.F32_PIECES == "f16x3" and c.in_channels % 32 == 0
+                and c.out_channels % 64 == 0 and tuple(c.kernel_size) == (3, 3) and tuple(c.stride) == (1, 1)
+                and tuple(c.padding) == (1, 1) and tuple(c.dilation) == (1, 1) and c.groups == 1)
+
     def x6(self, x, relu, res=None, bias=True):
         """f32 conv (+ bias) (+ res) (+ ReLU) as one fp32-accurate implicit-GEMM launch
         (rmbx_conv2d_f16x3 / rmbx_conv2d_f32x6 by kernels.F32_PIECES, epilogue fused); bias=False:
@@ -197,7 +210,17 @@ class _FusedConv(nn.Module):
         return K.conv2d_f32x6(x, cache[1], b, c.kernel_size, c.stride[0], c.padding[0], relu=relu, res=res)
 
     def s1(self, x, relu, res=None, bias=None):
-        """A stride-1 3x3 conv of the f32 trunk: implicit GEMM (s1_gemm_ok) or fused Winograd."""
+        """A stride-1 3x3 conv of the f32 trunk: patch-staged f16x3 conv (s1_patch_ok), implicit
+        GEMM (s1_gemm_ok) or fused Winograd."""
+        if self.s1_patch_ok():
+            w = self.conv.weight
+            key = (w.data_ptr(), w._version, w.device)
+            cache = self.__dict__.get("_x6")
+            if cache is None or cache[0] != key:
+                cache = (key, K.pack_conv_f32x6(w))
+                self.__dict__["_x6"] = cache
+            b = self.bias_f32() if bias is None else bias
+            return K.conv3x3_f16x3_patch(x, cache[1], b, relu=relu, res=res)
         if self.s1_gemm_ok():
             return self.x6(x, relu, res=res, bias=True if bias is None else bias)
         return self.wino(x, relu, res=res, bias=bias)
