@@ -70,7 +70,10 @@ __device__ __forceinline__ void cp_split(float x, float y, uint32_t& h, uint32_t
 }
 __device__ __forceinline__ int cp_slot(int r, int s) { return s ^ ((r >> 1) & 3); }
 
-template <int TW, int BN>
+// VAR (profiling, RMBX_CONVP_VAR; wrong results, timing only): bit 0 = no epilogue (one store per
+// lane keeps the accumulators live), bit 1 = no patch re-staging (the first patch is reused), bit 2
+// = no W staging (the first W row is reused)
+template <int TW, int BN, int VAR = 0>
 __global__ void __launch_bounds__(CP_THREADS, 1) conv3x3p_f16x3_kernel(ConvPArgs a) {
   static_assert(TW * CP_TH * BN == 256 * 128, "a block computes 32768 outputs");
   constexpr int PW = TW + 2, PP = (CP_TH + 2) * PW;       // patch width, pixels
@@ -229,45 +232,75 @@ __global__ void __launch_bounds__(CP_THREADS, 1) conv3x3p_f16x3_kernel(ConvPArgs
     }
   };
 
-  // epilogue of a unit: per 16-pixel row segment, the 16 residual loads of a lane are issued
-  // together (past-the-image pixels read a clamped in-range address and skip the store)
+  // epilogue of a unit: each 4 x 4 block of an accumulator (4 pixels x 4 channels over 4 lanes) is
+  // transposed across its lane quad by two DPP exchanges, so a lane holds 4 consecutive channels of
+  // one pixel: 16-B residual loads and stores (past-the-image pixels read a clamped address and
+  // skip the store)
   auto epilogue = [&](int u, int t) {
+    if constexpr ((VAR & 1) != 0) {
+      float sum = 0.f;
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int nj = 0; nj < 4; ++nj) sum += acc[mi][nj][0] + acc[mi][nj][1] + acc[mi][nj][2] + acc[mi][nj][3];
+      a.out[(long long)(u % 4096) * CP_THREADS + tid] = sum;
+      return;
+    }
     int img, oy0, ox0, n0;
     unit_geo(u, img, oy0, ox0, n0);
-    float sn[4], bb[4];
+    const int j = fr & 3, q = fr >> 2;  // lane in its quad, quad of 4 channels
+    float4 sn[4], bb[4];
 #pragma unroll
     for (int nj = 0; nj < 4; ++nj) {
-      const int n = n0 + wn * 64 + nj * 16 + fr;
-      sn[nj] = a.ws[n];
-      bb[nj] = a.bias ? a.bias[n] : 0.f;
+      const int n = n0 + wn * 64 + nj * 16 + 4 * q;
+      sn[nj] = *reinterpret_cast<const float4*>(a.ws + n);
+      bb[nj] = a.bias ? *reinterpret_cast<const float4*>(a.bias + n) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
+    auto xchg = [](float x, int ctrl) {
+      return __int_as_float(ctrl == 1 ? __builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xf, 0xf, false)
+                                      : __builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xf, 0xf, false));
+    };
 #pragma unroll
     for (int mi = 0; mi < 4; ++mi) {
-      long long idx[4];
-      bool ok[4];
-#pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const int p = wm * 64 + mi * 16 + 4 * fs + e;
-        const int ty = p / TW, tx = p - ty * TW;
-        const int y = oy0 + ty, x = ox0 + tx;
-        ok[e] = y < a.H && x < a.W;
-        idx[e] = ok[e] ? (((long long)img * a.H + y) * a.W + x) * a.Cout + n0 + wn * 64 + fr : 0;
-      }
-      float rv[4][4];
+      const int p = wm * 64 + mi * 16 + 4 * fs + j;  // this lane's pixel after the transpose
+      const int ty = p / TW, tx = p - ty * TW;
+      const int y = oy0 + ty, x = ox0 + tx;
+      const bool ok = y < a.H && x < a.W;
+      const long long pix = ok ? ((long long)img * a.H + y) * a.W + x : 0;
+      float4 rv[4];
 #pragma unroll
       for (int nj = 0; nj < 4; ++nj)
+        rv[nj] = a.res ? *reinterpret_cast<const float4*>(a.res + pix * a.Cout + n0 + wn * 64 + nj * 16 + 4 * q)
+                       : make_float4(0.f, 0.f, 0.f, 0.f);
 #pragma unroll
-        for (int e = 0; e < 4; ++e) rv[nj][e] = a.res ? a.res[idx[e] + nj * 16] : 0.f;
-#pragma unroll
-      for (int nj = 0; nj < 4; ++nj)
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          float v = t == CP_TNONE ? 0.f : ldexpf(acc[mi][nj][e] * sn[nj], -t);
-          v += bb[nj];
-          v += rv[nj][e];
-          if (a.relu) v = fmaxf(v, 0.f);
-          if (ok[e]) a.out[idx[e] + nj * 16] = v;
+      for (int nj = 0; nj < 4; ++nj) {
+        float v0 = acc[mi][nj][0], v1 = acc[mi][nj][1], v2 = acc[mi][nj][2], v3 = acc[mi][nj][3];
+        {  // 2 x 2 blocks transposed with the lane j ^ 1
+          const bool odd = j & 1;
+          const float ra = xchg(odd ? v0 : v1, 1), rb = xchg(odd ? v2 : v3, 1);
+          if (odd) { v0 = ra; v2 = rb; } else { v1 = ra; v3 = rb; }
         }
+        {  // off-diagonal 2 x 2 blocks swapped with the lane j ^ 2
+          const bool hi = j & 2;
+          const float ra = xchg(hi ? v0 : v2, 2), rb = xchg(hi ? v1 : v3, 2);
+          if (hi) { v0 = ra; v1 = rb; } else { v2 = ra; v3 = rb; }
+        }
+        const float sc[4] = {sn[nj].x, sn[nj].y, sn[nj].z, sn[nj].w};
+        const float bs[4] = {bb[nj].x, bb[nj].y, bb[nj].z, bb[nj].w};
+        const float rs[4] = {rv[nj].x, rv[nj].y, rv[nj].z, rv[nj].w};
+        float o[4] = {v0, v1, v2, v3};
+#pragma unroll
+        for (int c = 0; c < 4; ++c) {
+          float v = t == CP_TNONE ? 0.f : ldexpf(o[c] * sc[c], -t);
+          v += bs[c];
+          v += rs[c];
+          if (a.relu) v = fmaxf(v, 0.f);
+          o[c] = v;
+        }
+        if (ok)
+          *reinterpret_cast<float4*>(a.out + pix * a.Cout + n0 + wn * 64 + nj * 16 + 4 * q) =
+              make_float4(o[0], o[1], o[2], o[3]);
+      }
     }
   };
 
@@ -296,19 +329,19 @@ __global__ void __launch_bounds__(CP_THREADS, 1) conv3x3p_f16x3_kernel(ConvPArgs
     const bool more = u_next < a.units;
 #pragma unroll 1
     for (int ky = 0; ky < 3; ++ky) {
-      if (ky == 0 && more) load_patch(u_next, c_next);
+      if ((VAR & 2) == 0 && ky == 0 && more) load_patch(u_next, c_next);
       // W of the next filter row, loaded and stored unconditionally (after the last row: a
       // redundant copy of this row into the idle buffer) so the staging registers stay registers
       const int wu = ky < 2 || !more ? u : u_next, wc = ky < 2 || !more ? c : c_next;
       const int wk = ky < 2 ? ky + 1 : (more ? 0 : 2);
-      load_w(wu, wc, wk);
+      if constexpr ((VAR & 4) == 0) load_w(wu, wc, wk);
       // keep the loads ahead of the MFMAs (left alone, the scheduler sinks them behind the MFMA
       // stream, and their latency is exposed at the end of every step)
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int kx = 0; kx < 3; ++kx) mfma_tap(ky, kx, wb);
       if (ky == 1 && more) atomicMax(&sMax, __float_as_uint(patch_max()));
-      store_w(wb ^ 1);
+      if constexpr ((VAR & 4) == 0) store_w(wb ^ 1);
       __syncthreads();
       wb ^= 1;
     }
@@ -319,7 +352,7 @@ __global__ void __launch_bounds__(CP_THREADS, 1) conv3x3p_f16x3_kernel(ConvPArgs
     // every wave is past the chunk's MFMAs: replace the patch with the next stage's
     const int tc = chunk_t(sMax);
     const int t_next = last_chunk ? tc : min(t_cur, tc);
-    store_patch(t_next == CP_TNONE ? 0 : t_next);
+    if constexpr ((VAR & 2) == 0) store_patch(t_next == CP_TNONE ? 0 : t_next);
     if (last_chunk) {
       epilogue(u, t_cur);
 #pragma unroll
@@ -345,6 +378,8 @@ __global__ void __launch_bounds__(CP_THREADS, 1) conv3x3p_f16x3_kernel(ConvPArgs
 
 template <int TW, int BN>
 int launch_convp(const ConvPArgs& base, hipStream_t st) {
+  const char* ve = std::getenv("RMBX_CONVP_VAR");  // profiling phase skips (read per launch)
+  const int var = ve ? std::atoi(ve) : 0;
   ConvPArgs a = base;
   a.tiles_x = (a.W + TW - 1) / TW;
   a.tiles_y = (a.H + CP_TH - 1) / CP_TH;
@@ -357,7 +392,13 @@ int launch_convp(const ConvPArgs& base, hipStream_t st) {
   RMBX_CHECK_HIP(hipGetDevice(&dev));
   RMBX_CHECK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
   const int grid = a.units < cus ? a.units : cus;
-  hipLaunchKernelGGL((conv3x3p_f16x3_kernel<TW, BN>), dim3(grid), dim3(CP_THREADS), 0, st, a);
+  switch (var) {
+    case 1: hipLaunchKernelGGL((conv3x3p_f16x3_kernel<TW, BN, 1>), dim3(grid), dim3(CP_THREADS), 0, st, a); break;
+    case 2: hipLaunchKernelGGL((conv3x3p_f16x3_kernel<TW, BN, 2>), dim3(grid), dim3(CP_THREADS), 0, st, a); break;
+    case 4: hipLaunchKernelGGL((conv3x3p_f16x3_kernel<TW, BN, 4>), dim3(grid), dim3(CP_THREADS), 0, st, a); break;
+    case 7: hipLaunchKernelGGL((conv3x3p_f16x3_kernel<TW, BN, 7>), dim3(grid), dim3(CP_THREADS), 0, st, a); break;
+    default: hipLaunchKernelGGL((conv3x3p_f16x3_kernel<TW, BN>), dim3(grid), dim3(CP_THREADS), 0, st, a);
+  }
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
 }
