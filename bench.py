@@ -193,10 +193,11 @@ def gemm_pmc_traffic():
 
 
 def gemm_probe(ro):
-    """One infer_policy call of `ro` with HIP events around every rmbx fp32-accurate GEMM launch
+    """One infer_policy call of `ro` with HIP events around every fp32-accurate GEMM launch
     (rmbx_linear_f16x3 / _batched / rmbx_conv2d_f16x3, or their bf16x6 counterparts under
-    RMBX_F32_PIECES=bf16x6: the dominant policy kernel): executed MFMA rate (three f16 or six bf16
-    products per f32 product, both at the bf16 rate) against the bf16 dense peak."""
+    RMBX_F32_PIECES=bf16x6: the dominant policy kernel) and every patch-staged 3x3 conv
+    (rmbx_conv3x3_f16x3_patch): executed MFMA rate (three f16 or six bf16 products per f32 product,
+    both at the bf16 rate) against the bf16 dense peak.  Returns (GEMM line, patch-conv line)."""
     from robomanipbaselines_amd import kernels as K
 
     K.GEMM_PROBE = probe = []
@@ -205,6 +206,12 @@ def gemm_probe(ro):
         torch.cuda.synchronize()
     finally:
         K.GEMM_PROBE = None
+    gemm = [e for e in probe if not e[0].startswith("conv3x3p")]
+    patch = [e for e in probe if e[0].startswith("conv3x3p")]
+    return _probe_line(gemm, True), _probe_line(patch, False)
+
+
+def _probe_line(probe, is_gemm):
     if not probe:
         return None
     ms = flops = nbytes = executed = 0.0
@@ -223,22 +230,23 @@ def gemm_probe(ro):
         L["flops"] += fl
     eq = flops / ms / 1e9      # fp32-equivalent TFLOP/s
     ex = executed / ms / 1e9   # executed MFMA TFLOP/s
-    traffic, src = gemm_pmc_traffic()
     n = len(probe)
+    traffic, src = gemm_pmc_traffic() if is_gemm else (None, None)
     if traffic is not None:
         traffic /= n  # per GEMM call (one or two kernel dispatches: the 256-wide tile + a 128 remainder)
     form = ("f16x3: each f32 operand split into two f16 pieces (the low one scaled by 2^11), three piece products "
             "on v_mfma_f32_16x16x32_f16" if kinds == {3} else
             "bf16x6: each f32 operand split into three bf16 pieces, six piece products on v_mfma_f32_16x16x32_bf16"
             if kinds == {6} else "mixed f16x3 / bf16x6")
+    kernel = (f"rmbx::gemm_f32x6_kernel (fp32-accurate GEMM / implicit-GEMM conv, {form}, f32 accumulation)" if is_gemm
+              else f"rmbx::conv3x3p_f16x3_kernel (patch-staged 3x3 / stride-1 conv, {form}, f32 accumulation)")
     return {"bound": "mfma", "achieved": round(ex, 2), "peak": MFMA_PEAK_TFLOPS["bf16"], "unit": "TFLOP/s",
             "frac": ex / MFMA_PEAK_TFLOPS["bf16"], "traffic": None if traffic is None else round(traffic),
-            "traffic_unit": "HBM bytes per GEMM call (one op launch; N = 3200 runs as two kernel dispatches), mean over "
-                            "the calls of one fp32 ACT inference at 1024 envs",
+            "traffic_unit": ("HBM bytes per GEMM call (one op launch; N = 3200 runs as two kernel dispatches), mean "
+                             "over the calls of one fp32 ACT inference at 1024 envs" if is_gemm else None),
             "traffic_source": src,
-            "algorithmic_bytes_per_launch": round(nbytes / len(probe)),
-            "kernel": f"rmbx::gemm_f32x6_kernel + rmbx::conv3x3p_f16x3_kernel (fp32-accurate GEMM / implicit-GEMM "
-                      f"and patch-staged 3x3 convs, {form}, f32 accumulation)",
+            "algorithmic_bytes_per_launch": round(nbytes / n),
+            "kernel": kernel,
             "flops": "executed MFMA FLOPs = products x the f32 problem's 2*M*N*K (3 for f16x3, 6 for bf16x6)",
             "achieved_fp32_equivalent": round(eq, 2), "f32_mfma_peak": MFMA_PEAK_TFLOPS["fp32"],
             "launches_per_inference": n, "avg_launch_us": round(1e3 * ms / n, 1),
@@ -636,9 +644,10 @@ def rank_main(args):
         # whole batched infer_policy call (render + preprocessing + ACT), all kernels on the stream
         # the whole batched infer_policy call (render + preprocessing + ACT) at the direct-algorithm
         # FLOPs of the f32 problem: informational, no roofline fraction -- the stride-1 convs run as
-        # Winograd (fewer products) and the GEMMs as bf16x6 f32 emulation (six bf16 products per f32
-        # product at 16x the f32 MFMA rate), so this rate can exceed the f32 MFMA peak; the
-        # kernel-level fractions are roofline (bf16x6 GEMM), roofline_winograd, roofline_physics
+        # Winograd (fewer products) and the GEMMs / convs as f16x3 f32 emulation (three f16 products
+        # per f32 product at 16x the f32 MFMA rate), so this rate can exceed the f32 MFMA peak; the
+        # kernel-level fractions are roofline (f16x3 GEMM), roofline_conv3x3 (patch-staged convs),
+        # roofline_winograd, roofline_physics
         result["roofline_policy"] = {"achieved_direct_fp32_equivalent": round(pol_tf, 2), "unit": "TFLOP/s",
                                      "f32_mfma_peak": MFMA_PEAK_TFLOPS["fp32"], "bf16_mfma_peak": MFMA_PEAK_TFLOPS["bf16"],
                                      "dtype": args.precision, "algorithmic_flops_per_inference": pol_flops,
@@ -649,7 +658,9 @@ def rank_main(args):
             wp = winograd_probe(groups[0])
             if wp is not None:
                 result["roofline_winograd"] = wp
-            gp = gemm_probe(groups[0])
+            gp, cp = gemm_probe(groups[0])
+            if cp is not None:
+                result["roofline_conv3x3"] = cp
             if gp is not None:
                 # the dominant kernel of the step: the physics line stays as
                 # roofline_physics, the fused Winograd conv as roofline_winograd

@@ -75,14 +75,14 @@ def winograd(a):
 
 
 def gemm(a):
-    """--gemm: the gemm_f32x6_kernel / conv3x3p_f16x3_kernel launches of the SECOND fp32 ACT inference of
+    """--gemm: the gemm_f32x6_kernel launches of the SECOND fp32 ACT inference of
     scripts/prof_act_gemm_pmc.py (dispatch order), scaled by the 16-B-lane factors (its global loads
     are dwordx4 and LDS-DMA of 16 B per lane): HBM bytes per launch, mean over the inference."""
     def per_launch(path):
         rows = sorted((int(r["Dispatch_Id"]), r["Kernel_Name"], float(r["Counter_Value"]) * 1024.0,
                        (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3) for r in csv.DictReader(open(path)))
         cal = [v for _, n, v, _ in rows if n.startswith("calib_f32x4")]
-        g = [(v, us) for _, n, v, us in rows if "gemm_f32x6" in n or "conv3x3p_f16x3" in n]
+        g = [(v, us) for _, n, v, us in rows if "gemm_f32x6" in n]
         assert len(g) % 2 == 0, len(g)
         return g[len(g) // 2:], statistics.median(cal)
     fetch, cf = per_launch(os.path.join(a.dir, "pmc_fetch", "run_counter_collection.csv"))
