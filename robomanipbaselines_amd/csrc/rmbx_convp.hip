@@ -73,9 +73,14 @@ __device__ __forceinline__ int cp_slot(int r, int s) { return s ^ ((r >> 1) & 3)
 // VAR (profiling, RMBX_CONVP_VAR; wrong results, timing only): bit 0 = no epilogue (one store per
 // lane keeps the accumulators live), bit 1 = no patch re-staging (the first patch is reused), bit 2
 // = no W staging (the first W row is reused)
-template <int TW, int BN, int VAR = 0>
-__global__ void __launch_bounds__(CP_THREADS, 1) conv3x3p_f16x3_kernel(ConvPArgs a) {
-  static_assert(TW * CP_TH * BN == 256 * 128, "a block computes 32768 outputs");
+// Template: TW tile width, BN output channels per block, MI 16-pixel row segments per wave (a wave
+// owns 16 MI pixels x 64 channels), WG taps per W staging group (3: one filter row per barrier, 1:
+// one tap), MINB blocks per CU (2: 4 waves per SIMD, 128 registers).
+template <int TW, int BN, int MI, int WG, int MINB, int VAR = 0>
+__device__ __forceinline__ void conv3x3p_body(const ConvPArgs& a) {
+  static_assert((TW / MI) * (BN / 64) == CP_THREADS / 64, "8 waves of 16 MI pixels x 64 channels");
+  static_assert(WG == 1 || WG == 3, "a W group is one tap or one filter row");
+  constexpr int NG = 9 / WG;  // W groups (barriers) per chunk
   constexpr int PW = TW + 2, PP = (CP_TH + 2) * PW;       // patch width, pixels
   constexpr int PLANE = PP * 64;                          // bytes of one patch piece
   constexpr int WPLANE = BN * 64;                         // bytes of one W piece
@@ -83,12 +88,12 @@ __global__ void __launch_bounds__(CP_THREADS, 1) conv3x3p_f16x3_kernel(ConvPArgs
   constexpr int NWR = (2 * BN * 4) / CP_THREADS;               // W 16-B loads per thread
   constexpr int WN = BN / 64;                                   // waves across the channels
   __shared__ __attribute__((aligned(16))) unsigned char sP[2 * PLANE];
-  __shared__ __attribute__((aligned(16))) unsigned char sW[2 * 3 * 2 * WPLANE];  // [buf][kx][piece][row]
+  __shared__ __attribute__((aligned(16))) unsigned char sW[2 * WG * 2 * WPLANE];  // [buf][tap in group][piece][row]
   __shared__ unsigned int sMax;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / WN, wn = wave - wm * WN;  // 64-pixel slab, 64-channel column block
+  const int wm = wave / WN, wn = wave - wm * WN;  // 16 MI-pixel slab, 64-channel column block
   const int fr = lane & 15, fs = lane >> 4;
   const int K = 9 * a.C, nchunk = a.C / CP_KC;
 
@@ -151,9 +156,9 @@ __global__ void __launch_bounds__(CP_THREADS, 1) conv3x3p_f16x3_kernel(ConvPArgs
     return 14 - e;
   };
 
-  // ---- W of one filter row (unit u, chunk c, ky; its three taps kx): item q = tid + 512 i ->
-  // (kx, piece, row, 16-B slot); 3 NWR named registers (not an array: hipcc kept a captured
-  // uint4 array in scratch)
+  // ---- W of one staging group (unit u, chunk c, group g: taps WG g .. WG g + WG - 1): item
+  // q = tid + 512 i -> (piece, row, 16-B slot) of each tap; named registers (not an array: hipcc
+  // kept a captured uint4 array in scratch)
   static_assert(NWR == 1 || NWR == 2, "BN = 64 or 128");
   uint4 w00 = make_uint4(0, 0, 0, 0), w01 = w00, w10 = w00, w11 = w00, w20 = w00, w21 = w00;
   auto w_item = [&](int i, int& pc, int& n, int& sl) {
@@ -163,51 +168,56 @@ __global__ void __launch_bounds__(CP_THREADS, 1) conv3x3p_f16x3_kernel(ConvPArgs
     n = rem >> 2;
     sl = rem & 3;
   };
-  auto w_src = [&](int u, int c, int ky, int kx, int i) {
+  auto w_src = [&](int u, int c, int tap, int i) {
     int pc, n, sl;
     w_item(i, pc, n, sl);
     const int n0 = (u % a.ncb) * BN;
-    return reinterpret_cast<const uint4*>(a.w + pc * a.wps + (long long)(n0 + n) * K + (3 * ky + kx) * a.C +
-                                          c * CP_KC + 8 * sl);
+    return reinterpret_cast<const uint4*>(a.w + pc * a.wps + (long long)(n0 + n) * K + tap * a.C + c * CP_KC +
+                                          8 * sl);
   };
-  auto load_w = [&](int u, int c, int ky) {
-    w00 = *w_src(u, c, ky, 0, 0);
-    w10 = *w_src(u, c, ky, 1, 0);
-    w20 = *w_src(u, c, ky, 2, 0);
-    if constexpr (NWR == 2) {
-      w01 = *w_src(u, c, ky, 0, 1);
-      w11 = *w_src(u, c, ky, 1, 1);
-      w21 = *w_src(u, c, ky, 2, 1);
+  auto load_w = [&](int u, int c, int g) {
+    w00 = *w_src(u, c, WG * g, 0);
+    if constexpr (NWR == 2) w01 = *w_src(u, c, WG * g, 1);
+    if constexpr (WG == 3) {
+      w10 = *w_src(u, c, WG * g + 1, 0);
+      w20 = *w_src(u, c, WG * g + 2, 0);
+      if constexpr (NWR == 2) {
+        w11 = *w_src(u, c, WG * g + 1, 1);
+        w21 = *w_src(u, c, WG * g + 2, 1);
+      }
     }
   };
-  auto w_dst = [&](int buf, int kx, int i) {
+  auto w_dst = [&](int buf, int k, int i) {
     int pc, n, sl;
     w_item(i, pc, n, sl);
-    return reinterpret_cast<uint4*>(sW + ((buf * 3 + kx) * 2 + pc) * WPLANE + n * 64 + cp_slot(n, sl) * 16);
+    return reinterpret_cast<uint4*>(sW + ((buf * WG + k) * 2 + pc) * WPLANE + n * 64 + cp_slot(n, sl) * 16);
   };
   auto store_w = [&](int buf) {
     *w_dst(buf, 0, 0) = w00;
-    *w_dst(buf, 1, 0) = w10;
-    *w_dst(buf, 2, 0) = w20;
-    if constexpr (NWR == 2) {
-      *w_dst(buf, 0, 1) = w01;
-      *w_dst(buf, 1, 1) = w11;
-      *w_dst(buf, 2, 1) = w21;
+    if constexpr (NWR == 2) *w_dst(buf, 0, 1) = w01;
+    if constexpr (WG == 3) {
+      *w_dst(buf, 1, 0) = w10;
+      *w_dst(buf, 2, 0) = w20;
+      if constexpr (NWR == 2) {
+        *w_dst(buf, 1, 1) = w11;
+        *w_dst(buf, 2, 1) = w21;
+      }
     }
   };
 
-  cp_f32x4 acc[4][4];
+  cp_f32x4 acc[MI][4];
 #pragma unroll
-  for (int i = 0; i < 4; ++i)
+  for (int i = 0; i < MI; ++i)
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[i][j] = (cp_f32x4){0.f, 0.f, 0.f, 0.f};
 
   // MFMAs of one tap: A fragments from the patch at (ky, kx), B from W buffer wb
-  auto mfma_tap = [&](int ky, int kx, int wb) {
-    cp_f16x8 ah[4], al[4];
+  auto mfma_tap = [&](int tap, int k, int wb) {  // tap (ky, kx); W at slot k of buffer wb
+    const int ky = tap / 3, kx = tap - 3 * ky;
+    cp_f16x8 ah[MI], al[MI];
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi) {
-      const int p0 = wm * 64 + mi * 16;  // first pixel of this 16-pixel row segment
+    for (int mi = 0; mi < MI; ++mi) {
+      const int p0 = wm * 16 * MI + mi * 16;  // first pixel of this 16-pixel row segment
       const int ty = p0 / TW, tx = p0 - ty * TW;
       const int pp = (ty + ky) * PW + tx + fr + kx;
       const int off = pp * 64 + cp_slot(pp, fs) * 16;
@@ -218,11 +228,11 @@ __global__ void __launch_bounds__(CP_THREADS, 1) conv3x3p_f16x3_kernel(ConvPArgs
     for (int nj = 0; nj < 4; ++nj) {
       const int n = wn * 64 + nj * 16 + fr;
       const int off = n * 64 + cp_slot(n, fs) * 16;
-      const cp_f16x8 bh = *reinterpret_cast<const cp_f16x8*>(sW + ((wb * 3 + kx) * 2) * WPLANE + off);
-      const cp_f16x8 bl = *reinterpret_cast<const cp_f16x8*>(sW + ((wb * 3 + kx) * 2 + 1) * WPLANE + off);
+      const cp_f16x8 bh = *reinterpret_cast<const cp_f16x8*>(sW + ((wb * WG + k) * 2) * WPLANE + off);
+      const cp_f16x8 bl = *reinterpret_cast<const cp_f16x8*>(sW + ((wb * WG + k) * 2 + 1) * WPLANE + off);
       const cp_f16x8 bs = bh * (_Float16)0.00048828125f;  // 2^-11 hb (exact above f16's subnormals)
 #pragma unroll
-      for (int mi = 0; mi < 4; ++mi) {
+      for (int mi = 0; mi < MI; ++mi) {
         cp_f32x4 c = acc[mi][nj];
         c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[mi], bs, c, 0, 0, 0);
         c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[mi], bl, c, 0, 0, 0);
@@ -240,7 +250,7 @@ __global__ void __launch_bounds__(CP_THREADS, 1) conv3x3p_f16x3_kernel(ConvPArgs
     if constexpr ((VAR & 1) != 0) {
       float sum = 0.f;
 #pragma unroll
-      for (int mi = 0; mi < 4; ++mi)
+      for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
         for (int nj = 0; nj < 4; ++nj) sum += acc[mi][nj][0] + acc[mi][nj][1] + acc[mi][nj][2] + acc[mi][nj][3];
       a.out[(long long)(u % 4096) * CP_THREADS + tid] = sum;
@@ -261,8 +271,8 @@ __global__ void __launch_bounds__(CP_THREADS, 1) conv3x3p_f16x3_kernel(ConvPArgs
                                       : __builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xf, 0xf, false));
     };
 #pragma unroll
-    for (int mi = 0; mi < 4; ++mi) {
-      const int p = wm * 64 + mi * 16 + 4 * fs + j;  // this lane's pixel after the transpose
+    for (int mi = 0; mi < MI; ++mi) {
+      const int p = wm * 16 * MI + mi * 16 + 4 * fs + j;  // this lane's pixel after the transpose
       const int ty = p / TW, tx = p - ty * TW;
       const int y = oy0 + ty, x = ox0 + tx;
       const bool ok = y < a.H && x < a.W;
@@ -310,7 +320,7 @@ __global__ void __launch_bounds__(CP_THREADS, 1) conv3x3p_f16x3_kernel(ConvPArgs
   if (u >= a.units) return;
   if (tid == 0) sMax = 0u;
   load_patch(u, 0);
-  load_w(u, 0, 0);  // filter row ky = 0
+  load_w(u, 0, 0);  // group 0
   __syncthreads();
   atomicMax(&sMax, __float_as_uint(patch_max()));
   __syncthreads();
@@ -328,19 +338,19 @@ __global__ void __launch_bounds__(CP_THREADS, 1) conv3x3p_f16x3_kernel(ConvPArgs
     const int c_next = last_chunk ? 0 : c + 1;
     const bool more = u_next < a.units;
 #pragma unroll 1
-    for (int ky = 0; ky < 3; ++ky) {
-      if ((VAR & 2) == 0 && ky == 0 && more) load_patch(u_next, c_next);
-      // W of the next filter row, loaded and stored unconditionally (after the last row: a
-      // redundant copy of this row into the idle buffer) so the staging registers stay registers
-      const int wu = ky < 2 || !more ? u : u_next, wc = ky < 2 || !more ? c : c_next;
-      const int wk = ky < 2 ? ky + 1 : (more ? 0 : 2);
-      if constexpr ((VAR & 4) == 0) load_w(wu, wc, wk);
+    for (int g = 0; g < NG; ++g) {
+      if ((VAR & 2) == 0 && g == 0 && more) load_patch(u_next, c_next);
+      // W of the next group, loaded and stored unconditionally (after the last group: a redundant
+      // copy of this group into the idle buffer) so the staging registers stay registers
+      const int wu = g < NG - 1 || !more ? u : u_next, wc = g < NG - 1 || !more ? c : c_next;
+      const int wg = g < NG - 1 ? g + 1 : (more ? 0 : g);
+      if constexpr ((VAR & 4) == 0) load_w(wu, wc, wg);
       // keep the loads ahead of the MFMAs (left alone, the scheduler sinks them behind the MFMA
       // stream, and their latency is exposed at the end of every step)
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int kx = 0; kx < 3; ++kx) mfma_tap(ky, kx, wb);
-      if (ky == 1 && more) atomicMax(&sMax, __float_as_uint(patch_max()));
+      for (int k = 0; k < WG; ++k) mfma_tap(WG * g + k, k, wb);
+      if (g == NG / 2 && more) atomicMax(&sMax, __float_as_uint(patch_max()));
       if constexpr ((VAR & 4) == 0) store_w(wb ^ 1);
       __syncthreads();
       wb ^= 1;
@@ -356,13 +366,13 @@ __global__ void __launch_bounds__(CP_THREADS, 1) conv3x3p_f16x3_kernel(ConvPArgs
     if (last_chunk) {
       epilogue(u, t_cur);
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j) acc[i][j] = (cp_f32x4){0.f, 0.f, 0.f, 0.f};
     } else if (t_next != t_cur) {  // the chunk needs a smaller scale: rescale the sum so far (exact)
       const int d = t_cur == CP_TNONE ? -200 : t_next - t_cur;
 #pragma unroll
-      for (int i = 0; i < 4; ++i)
+      for (int i = 0; i < MI; ++i)
 #pragma unroll
         for (int j = 0; j < 4; ++j)
 #pragma unroll
@@ -376,7 +386,18 @@ __global__ void __launch_bounds__(CP_THREADS, 1) conv3x3p_f16x3_kernel(ConvPArgs
   }
 }
 
-template <int TW, int BN>
+// one block per CU (up to 256 registers per lane) / two blocks per CU (128: four waves per SIMD)
+template <int TW, int BN, int MI, int WG, int VAR>
+__global__ void __launch_bounds__(CP_THREADS, 1) conv3x3p_f16x3_kernel(ConvPArgs a) {
+  conv3x3p_body<TW, BN, MI, WG, 1, VAR>(a);
+}
+template <int TW, int BN, int MI, int WG, int VAR>
+__global__ void __launch_bounds__(CP_THREADS, 4)  // (hipcc: the second argument is waves per SIMD)
+conv3x3p2_f16x3_kernel(ConvPArgs a) {
+  conv3x3p_body<TW, BN, MI, WG, 2, VAR>(a);
+}
+
+template <int TW, int BN, int MI, int WG, int MINB>
 int launch_convp(const ConvPArgs& base, hipStream_t st) {
   const char* ve = std::getenv("RMBX_CONVP_VAR");  // profiling phase skips (read per launch)
   const int var = ve ? std::atoi(ve) : 0;
@@ -391,14 +412,20 @@ int launch_convp(const ConvPArgs& base, hipStream_t st) {
   int dev = 0, cus = 0;
   RMBX_CHECK_HIP(hipGetDevice(&dev));
   RMBX_CHECK_HIP(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
-  const int grid = a.units < cus ? a.units : cus;
+  const int grid = a.units < MINB * cus ? a.units : MINB * cus;
+#define RMBX_CP_LAUNCH(V)                                                                                       \
+  if constexpr (MINB == 2)                                                                                      \
+    hipLaunchKernelGGL((conv3x3p2_f16x3_kernel<TW, BN, MI, WG, V>), dim3(grid), dim3(CP_THREADS), 0, st, a); \
+  else                                                                                                          \
+    hipLaunchKernelGGL((conv3x3p_f16x3_kernel<TW, BN, MI, WG, V>), dim3(grid), dim3(CP_THREADS), 0, st, a)
   switch (var) {
-    case 1: hipLaunchKernelGGL((conv3x3p_f16x3_kernel<TW, BN, 1>), dim3(grid), dim3(CP_THREADS), 0, st, a); break;
-    case 2: hipLaunchKernelGGL((conv3x3p_f16x3_kernel<TW, BN, 2>), dim3(grid), dim3(CP_THREADS), 0, st, a); break;
-    case 4: hipLaunchKernelGGL((conv3x3p_f16x3_kernel<TW, BN, 4>), dim3(grid), dim3(CP_THREADS), 0, st, a); break;
-    case 7: hipLaunchKernelGGL((conv3x3p_f16x3_kernel<TW, BN, 7>), dim3(grid), dim3(CP_THREADS), 0, st, a); break;
-    default: hipLaunchKernelGGL((conv3x3p_f16x3_kernel<TW, BN>), dim3(grid), dim3(CP_THREADS), 0, st, a);
+    case 1: RMBX_CP_LAUNCH(1); break;
+    case 2: RMBX_CP_LAUNCH(2); break;
+    case 4: RMBX_CP_LAUNCH(4); break;
+    case 7: RMBX_CP_LAUNCH(7); break;
+    default: RMBX_CP_LAUNCH(0);
   }
+#undef RMBX_CP_LAUNCH
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
 }
@@ -433,7 +460,13 @@ extern "C" int rmbx_conv3x3_f16x3_patch(const float* in, int N, int H, int W, in
   a.C = C;
   a.Cout = Cout;
   a.relu = relu ? 1 : 0;
-  // 512 x 64 tiles (16 x 32 pixels) when the output channels are not a multiple of 128
-  if (Cout % 128 == 0) return rmbx::launch_convp<16, 128>(a, (hipStream_t)stream);
-  return rmbx::launch_convp<32, 64>(a, (hipStream_t)stream);
+  // RMBX_CONVP_CFG (read per launch): 0 = one block per CU (16 x 16 tiles x 128 channels, or 16 x
+  // 32 x 64 when Cout % 128 != 0; a filter row of W per barrier), 1 = two blocks per CU (16 x 16 x 64,
+  // 32 pixels x 64 channels per wave, one tap of W per barrier: one block's epilogue and patch
+  // staging under the other's MFMAs)
+  const char* ce = std::getenv("RMBX_CONVP_CFG");
+  const int cfg = ce ? std::atoi(ce) : 0;
+  if (cfg == 1) return rmbx::launch_convp<16, 64, 2, 1, 2>(a, (hipStream_t)stream);
+  if (Cout % 128 == 0) return rmbx::launch_convp<16, 128, 4, 3, 1>(a, (hipStream_t)stream);
+  return rmbx::launch_convp<32, 64, 4, 3, 1>(a, (hipStream_t)stream);
 }

@@ -2,6 +2,7 @@
 backbone's stride-1 shapes, 1024 frames: 64 channels at 120 x 160 vs the fused f32 Winograd
 F(4x4) and the f16x3 implicit GEMM; 128 channels at 60 x 80 vs the implicit GEMM.  Rounds
 interleaved in one process, HIP events; error of each vs f64 on 2 frames."""
+import os
 import sys
 
 import torch
@@ -32,7 +33,12 @@ with torch.no_grad():
         b = torch.randn(C, device=dev, generator=g)
         r = torch.randn(n, C, H, W, device=dev, generator=g).contiguous(memory_format=torch.channels_last)
         p = K.pack_conv_f32x6(w)
-        ops = {"patch": lambda: K.conv3x3_f16x3_patch(x, p, b, relu=True, res=r),
+        def patch_cfg(cfg):
+            def f():
+                os.environ["RMBX_CONVP_CFG"] = cfg
+                return K.conv3x3_f16x3_patch(x, p, b, relu=True, res=r)
+            return f
+        ops = {"patch": patch_cfg("0"), "patch2": patch_cfg("1"),
                "gemm": lambda: K.conv2d_f32x6(x, p, b, 3, 1, 1, relu=True, res=r)}
         if C == 64:
             u = K.pack_winograd4_f32(w) if hasattr(K, "pack_winograd4_f32") else None
