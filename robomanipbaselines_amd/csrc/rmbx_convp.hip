@@ -270,46 +270,57 @@ __device__ __forceinline__ void conv3x3p_body(const ConvPArgs& a) {
       return __int_as_float(ctrl == 1 ? __builtin_amdgcn_mov_dpp(__float_as_int(x), 0xB1, 0xf, 0xf, false)
                                       : __builtin_amdgcn_mov_dpp(__float_as_int(x), 0x4E, 0xf, 0xf, false));
     };
+    // the residual loads of two row segments at a time (two memory round trips per unit instead
+    // of one per segment; all four at once spills the 16 x 32-pixel configuration)
 #pragma unroll
-    for (int mi = 0; mi < MI; ++mi) {
-      const int p = wm * 16 * MI + mi * 16 + 4 * fs + j;  // this lane's pixel after the transpose
-      const int ty = p / TW, tx = p - ty * TW;
-      const int y = oy0 + ty, x = ox0 + tx;
-      const bool ok = y < a.H && x < a.W;
-      const long long pix = ok ? ((long long)img * a.H + y) * a.W + x : 0;
-      float4 rv[4];
+    for (int m2 = 0; m2 < MI; m2 += 2) {
+      long long pix[2];
+      bool ok[2];
+      float4 rv[2][4];
 #pragma unroll
-      for (int nj = 0; nj < 4; ++nj)
-        rv[nj] = a.res ? *reinterpret_cast<const float4*>(a.res + pix * a.Cout + n0 + wn * 64 + nj * 16 + 4 * q)
-                       : make_float4(0.f, 0.f, 0.f, 0.f);
+      for (int h = 0; h < 2; ++h) {
+        const int p = wm * 16 * MI + (m2 + h) * 16 + 4 * fs + j;  // this lane's pixel after the transpose
+        const int ty = p / TW, tx = p - ty * TW;
+        const int y = oy0 + ty, x = ox0 + tx;
+        ok[h] = y < a.H && x < a.W;
+        pix[h] = ok[h] ? ((long long)img * a.H + y) * a.W + x : 0;
 #pragma unroll
-      for (int nj = 0; nj < 4; ++nj) {
-        float v0 = acc[mi][nj][0], v1 = acc[mi][nj][1], v2 = acc[mi][nj][2], v3 = acc[mi][nj][3];
-        {  // 2 x 2 blocks transposed with the lane j ^ 1
-          const bool odd = j & 1;
-          const float ra = xchg(odd ? v0 : v1, 1), rb = xchg(odd ? v2 : v3, 1);
-          if (odd) { v0 = ra; v2 = rb; } else { v1 = ra; v3 = rb; }
+        for (int nj = 0; nj < 4; ++nj)
+          rv[h][nj] = a.res ? *reinterpret_cast<const float4*>(a.res + pix[h] * a.Cout + n0 + wn * 64 + nj * 16 + 4 * q)
+                            : make_float4(0.f, 0.f, 0.f, 0.f);
+      }
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const int mi = m2 + h;
+#pragma unroll
+        for (int nj = 0; nj < 4; ++nj) {
+          float v0 = acc[mi][nj][0], v1 = acc[mi][nj][1], v2 = acc[mi][nj][2], v3 = acc[mi][nj][3];
+          {  // 2 x 2 blocks transposed with the lane j ^ 1
+            const bool odd = j & 1;
+            const float ra = xchg(odd ? v0 : v1, 1), rb = xchg(odd ? v2 : v3, 1);
+            if (odd) { v0 = ra; v2 = rb; } else { v1 = ra; v3 = rb; }
+          }
+          {  // off-diagonal 2 x 2 blocks swapped with the lane j ^ 2
+            const bool hi = j & 2;
+            const float ra = xchg(hi ? v0 : v2, 2), rb = xchg(hi ? v1 : v3, 2);
+            if (hi) { v0 = ra; v1 = rb; } else { v2 = ra; v3 = rb; }
+          }
+          const float sc[4] = {sn[nj].x, sn[nj].y, sn[nj].z, sn[nj].w};
+          const float bs[4] = {bb[nj].x, bb[nj].y, bb[nj].z, bb[nj].w};
+          const float rs[4] = {rv[h][nj].x, rv[h][nj].y, rv[h][nj].z, rv[h][nj].w};
+          float o[4] = {v0, v1, v2, v3};
+#pragma unroll
+          for (int c = 0; c < 4; ++c) {
+            float v = t == CP_TNONE ? 0.f : ldexpf(o[c] * sc[c], -t);
+            v += bs[c];
+            v += rs[c];
+            if (a.relu) v = fmaxf(v, 0.f);
+            o[c] = v;
+          }
+          if (ok[h])
+            *reinterpret_cast<float4*>(a.out + pix[h] * a.Cout + n0 + wn * 64 + nj * 16 + 4 * q) =
+                make_float4(o[0], o[1], o[2], o[3]);
         }
-        {  // off-diagonal 2 x 2 blocks swapped with the lane j ^ 2
-          const bool hi = j & 2;
-          const float ra = xchg(hi ? v0 : v2, 2), rb = xchg(hi ? v1 : v3, 2);
-          if (hi) { v0 = ra; v1 = rb; } else { v2 = ra; v3 = rb; }
-        }
-        const float sc[4] = {sn[nj].x, sn[nj].y, sn[nj].z, sn[nj].w};
-        const float bs[4] = {bb[nj].x, bb[nj].y, bb[nj].z, bb[nj].w};
-        const float rs[4] = {rv[nj].x, rv[nj].y, rv[nj].z, rv[nj].w};
-        float o[4] = {v0, v1, v2, v3};
-#pragma unroll
-        for (int c = 0; c < 4; ++c) {
-          float v = t == CP_TNONE ? 0.f : ldexpf(o[c] * sc[c], -t);
-          v += bs[c];
-          v += rs[c];
-          if (a.relu) v = fmaxf(v, 0.f);
-          o[c] = v;
-        }
-        if (ok)
-          *reinterpret_cast<float4*>(a.out + pix * a.Cout + n0 + wn * 64 + nj * 16 + 4 * q) =
-              make_float4(o[0], o[1], o[2], o[3]);
       }
     }
   };
