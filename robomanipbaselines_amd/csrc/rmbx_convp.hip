@@ -134,28 +134,6 @@ __device__ __forceinline__ void conv3x3p_body(const ConvPArgs& a) {
       m = fmaxf(m, fmaxf(fmaxf(fabsf(pr[i].x), fabsf(pr[i].y)), fmaxf(fabsf(pr[i].z), fabsf(pr[i].w))));
     return m;
   };
-  // split the staged patch in its registers (pr[i] then holds {h0, h1, l0, l1} as bits), so that
-  // only the LDS stores are left for the chunk boundary
-  auto split_patch = [&](int t) {
-#pragma unroll
-    for (int i = 0; i < NPR; ++i) {
-      uint32_t h0, l0, h1, l1;
-      cp_split(ldexpf(pr[i].x, t), ldexpf(pr[i].y, t), h0, l0);
-      cp_split(ldexpf(pr[i].z, t), ldexpf(pr[i].w, t), h1, l1);
-      pr[i] = make_float4(__uint_as_float(h0), __uint_as_float(h1), __uint_as_float(l0), __uint_as_float(l1));
-    }
-  };
-  auto store_split = [&]() {
-#pragma unroll
-    for (int i = 0; i < NPR; ++i) {
-      const int q = tid + CP_THREADS * i;
-      if (q >= PP * 8) break;
-      const int p = q >> 3, q8 = q & 7;
-      const int off = p * 64 + cp_slot(p, q8 >> 1) * 16 + (q8 & 1) * 8;
-      *reinterpret_cast<uint2*>(sP + off) = make_uint2(__float_as_uint(pr[i].x), __float_as_uint(pr[i].y));
-      *reinterpret_cast<uint2*>(sP + PLANE + off) = make_uint2(__float_as_uint(pr[i].z), __float_as_uint(pr[i].w));
-    }
-  };
   auto store_patch = [&](int t) {
 #pragma unroll
     for (int i = 0; i < NPR; ++i) {
@@ -370,7 +348,6 @@ __device__ __forceinline__ void conv3x3p_body(const ConvPArgs& a) {
     const int u_next = last_chunk ? u + G : u;
     const int c_next = last_chunk ? 0 : c + 1;
     const bool more = u_next < a.units;
-    int t_next = t_cur;  // the next stage's scale exponent (set in the last group)
 #pragma unroll 1
     for (int g = 0; g < NG; ++g) {
       if ((VAR & 2) == 0 && g == 0 && more) load_patch(u_next, c_next);
@@ -384,13 +361,6 @@ __device__ __forceinline__ void conv3x3p_body(const ConvPArgs& a) {
       __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int k = 0; k < WG; ++k) mfma_tap(WG * g + k, k, wb);
-      if ((VAR & 2) == 0 && g == NG - 1 && more) {
-        // the next stage's scale (its max was reduced at group NG / 2, published by that group's
-        // barrier) and its split, under the other waves' MFMAs; stored after the final barrier
-        const int tc = chunk_t(sMax);
-        t_next = last_chunk ? tc : min(t_cur, tc);
-        split_patch(t_next == CP_TNONE ? 0 : t_next);
-      }
       if (g == NG / 2 && more) atomicMax(&sMax, __float_as_uint(patch_max()));
       if constexpr ((VAR & 4) == 0) store_w(wb ^ 1);
       __syncthreads();
@@ -401,7 +371,9 @@ __device__ __forceinline__ void conv3x3p_body(const ConvPArgs& a) {
       break;
     }
     // every wave is past the chunk's MFMAs: replace the patch with the next stage's
-    if constexpr ((VAR & 2) == 0) store_split();
+    const int tc = chunk_t(sMax);
+    const int t_next = last_chunk ? tc : min(t_cur, tc);
+    if constexpr ((VAR & 2) == 0) store_patch(t_next == CP_TNONE ? 0 : t_next);
     if (last_chunk) {
       epilogue(u, t_cur);
 #pragma unroll
