@@ -24,7 +24,9 @@
 // W of the next step is loaded into registers under this step's MFMAs and stored to the other W
 // buffer after them; the next chunk's patch (a 32-channel chunk of the tile, or the next unit's
 // first) is loaded under the chunk's first taps, its max reduced in LDS mid-chunk, and it is
-// split and stored after the chunk's last MFMAs (one extra barrier per chunk).
+// split and stored after the chunk's last MFMAs (one extra barrier per chunk; splitting it in
+// registers during the chunk's last W group instead was slower: the VALU beside the MFMAs costs
+// more than it hides, profiles/r4_conv3x3_patch_presplit_ab.log).
 // LDS images: patch [2 pieces][pixel][4 x 16-B slots of 8 channels], W [2 buffers][2 pieces][BN
 // rows][4 slots]; 16-B slot s of row / pixel r at s ^ ((r >> 1) & 3): the 16-lane groups of every
 // fragment read cover all 64 banks.
