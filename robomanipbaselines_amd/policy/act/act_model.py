@@ -400,8 +400,9 @@ class ActModel(nn.Module):
                 f = self._input_proj(trunk(x))  # [B, d, h, w]
             feats.append(f)
             poss.append(self._pos(f.shape[2], f.shape[3], f.device, f.dtype))
-        src = torch.cat(feats, dim=3).flatten(2).transpose(1, 2)  # [B, hw, d]
-        pos = torch.cat(poss, dim=3).flatten(2).transpose(1, 2)  # [1, hw, d]
+        # (one camera: no concatenation copy of the feature map)
+        src = (feats[0] if len(feats) == 1 else torch.cat(feats, dim=3)).flatten(2).transpose(1, 2)  # [B, hw, d]
+        pos = (poss[0] if len(poss) == 1 else torch.cat(poss, dim=3)).flatten(2).transpose(1, 2)  # [1, hw, d]
         # fp32 device form: the two small linears and the final norm on rmbx kernels too, so every
         # env's chunk is bit-identical whatever the batch (tests/test_act_batch_gpu.py)
         dev_f32 = self._fused is not None and src.is_cuda and src.dtype == torch.float32 and F32_GEMM == "x6"
@@ -419,10 +420,11 @@ class ActModel(nn.Module):
         q = src + pos
         n_enc = len(self.encoder_layers)
         for i, layer in enumerate(self.encoder_layers):
-            mem, q = layer.forward_q(mem, q, pos, want_next_q=i + 1 < n_enc)
+            # the last layer's (out, out + pos) pass also yields the decoder's memory keys mem + pos
+            mem, q = layer.forward_q(mem, q, pos, want_next_q=True)
         qe = self.query_embed.weight[None].to(src.dtype)
         tgt = torch.zeros(B, self.num_queries, mem.shape[2], device=mem.device, dtype=mem.dtype)
-        mem_pos = mem + pos
+        mem_pos = q if q is not None else mem + pos
         q = tgt + qe
         first = None
         n_dec = 1 if self.prune_dead_decoder else len(self.decoder_layers)
