@@ -172,6 +172,20 @@ def winograd_probe(ro):
                                     "TFLOPs": round(L["flops"] / L["ms"] / 1e9, 2)} for c, L in sorted(layers.items())}}
 
 
+def convp_pmc_traffic():
+    """HBM counter bytes of the patch-staged conv dispatches of one fp32 ACT inference at 1024 envs
+    (the same gemm_pmc.sh passes, tools/pmc_traffic.py --convp); (None, None) if absent."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_pmc_conv3x3p_traffic.json")),
+                   key=lambda f: int(os.path.basename(f)[1:].split("_")[0]))
+    if not files:
+        return None, None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    return d["read_bytes_per_inference"] + d["write_bytes_per_inference"], os.path.relpath(files[-1], ROOT)
+
+
 def gemm_pmc_traffic():
     """HBM counter bytes of the gemm_f32x6 dispatches of one fp32 ACT inference at 1024 envs, from the
     committed PMC passes (scripts/gpurun/gemm_pmc.sh + tools/pmc_traffic.py --gemm); (None, None) if
@@ -231,9 +245,9 @@ def _probe_line(probe, is_gemm):
     eq = flops / ms / 1e9      # fp32-equivalent TFLOP/s
     ex = executed / ms / 1e9   # executed MFMA TFLOP/s
     n = len(probe)
-    traffic, src = gemm_pmc_traffic() if is_gemm else (None, None)
+    traffic, src = gemm_pmc_traffic() if is_gemm else convp_pmc_traffic()
     if traffic is not None:
-        traffic /= n  # per GEMM call (one or two kernel dispatches: the 256-wide tile + a 128 remainder)
+        traffic /= n  # per call (a GEMM call is one or two kernel dispatches: the 256-wide tile + a 128 remainder)
     form = ("f16x3: each f32 operand split into two f16 pieces (the low one scaled by 2^11), three piece products "
             "on v_mfma_f32_16x16x32_f16" if kinds == {3} else
             "bf16x6: each f32 operand split into three bf16 pieces, six piece products on v_mfma_f32_16x16x32_bf16"
@@ -243,7 +257,8 @@ def _probe_line(probe, is_gemm):
     return {"bound": "mfma", "achieved": round(ex, 2), "peak": MFMA_PEAK_TFLOPS["bf16"], "unit": "TFLOP/s",
             "frac": ex / MFMA_PEAK_TFLOPS["bf16"], "traffic": None if traffic is None else round(traffic),
             "traffic_unit": ("HBM bytes per GEMM call (one op launch; N = 3200 runs as two kernel dispatches), mean "
-                             "over the calls of one fp32 ACT inference at 1024 envs" if is_gemm else None),
+                             "over the calls of one fp32 ACT inference at 1024 envs" if is_gemm else
+                             "HBM bytes per conv call, mean over the calls of one fp32 ACT inference at 1024 envs"),
             "traffic_source": src,
             "algorithmic_bytes_per_launch": round(nbytes / n),
             "kernel": kernel,

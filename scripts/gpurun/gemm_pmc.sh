@@ -1,5 +1,6 @@
 #!/bin/bash
-# HBM traffic of the f32x6 GEMM kernel over one fp32 ACT inference: FETCH_SIZE and WRITE_SIZE passes
+# HBM traffic of the fp32-accurate GEMM kernel and the patch-staged convs over one fp32 ACT inference:
+# FETCH_SIZE and WRITE_SIZE passes (tools/pmc_traffic.py --gemm / --convp reduce them)
 # usage: bash scripts/gpurun/gemm_pmc.sh <tag>
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out/gemm_pmc_$1 scripts/_build &&
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O2 -shared -fPIC scripts/pmc_calib.hip -o scripts/_build/libpmc_calib.so &&

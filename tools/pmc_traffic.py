@@ -74,7 +74,7 @@ def winograd(a):
     print(json.dumps(out, indent=1))
 
 
-def gemm(a):
+def gemm(a, pattern="gemm_f32x6", kernel="rmbx::gemm_f32x6_kernel"):
     """--gemm: the gemm_f32x6_kernel launches of the SECOND fp32 ACT inference of
     scripts/prof_act_gemm_pmc.py (dispatch order), scaled by the 16-B-lane factors (its global loads
     are dwordx4 and LDS-DMA of 16 B per lane): HBM bytes per launch, mean over the inference."""
@@ -82,7 +82,7 @@ def gemm(a):
         rows = sorted((int(r["Dispatch_Id"]), r["Kernel_Name"], float(r["Counter_Value"]) * 1024.0,
                        (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3) for r in csv.DictReader(open(path)))
         cal = [v for _, n, v, _ in rows if n.startswith("calib_f32x4")]
-        g = [(v, us) for _, n, v, us in rows if "gemm_f32x6" in n]
+        g = [(v, us) for _, n, v, us in rows if pattern in n]
         assert len(g) % 2 == 0, len(g)
         return g[len(g) // 2:], statistics.median(cal)
     fetch, cf = per_launch(os.path.join(a.dir, "pmc_fetch", "run_counter_collection.csv"))
@@ -92,7 +92,7 @@ def gemm(a):
     rd = sum(v for v, _ in fetch) * rf
     wr = sum(v for v, _ in write) * wf
     n = len(fetch)
-    out = {"calibration": {"x16_read_factor": rf, "x16_write_factor": wf}, "kernel": "rmbx::gemm_f32x6_kernel",
+    out = {"calibration": {"x16_read_factor": rf, "x16_write_factor": wf}, "kernel": kernel,
            "launches_per_inference": n, "read_bytes_per_inference": rd, "write_bytes_per_inference": wr,
            "traffic_bytes_per_launch": (rd + wr) / n,
            "us_per_inference_under_pmc": sum(t for _, t in fetch),
@@ -107,6 +107,8 @@ def main():
     p = argparse.ArgumentParser()
     p.add_argument("--winograd", action="store_true", help="reduce scripts/gpurun/wino_pmc.sh output")
     p.add_argument("--gemm", action="store_true", help="reduce scripts/gpurun/gemm_pmc.sh output")
+    p.add_argument("--convp", action="store_true",
+                   help="the patch-staged conv dispatches of the same scripts/gpurun/gemm_pmc.sh output")
     p.add_argument("--frames", type=int, default=1024, help="--winograd: frames per call")
     p.add_argument("dir")
     p.add_argument("--out", required=True)
@@ -118,6 +120,8 @@ def main():
         return winograd(a)
     if a.gemm:
         return gemm(a)
+    if a.convp:
+        return gemm(a, "conv3x3p_f16x3", "rmbx::conv3x3p_f16x3_kernel")
     fetch, nf, dur = medians(os.path.join(a.dir, "pmc_fetch", "run_counter_collection.csv"))
     write, nw, _ = medians(os.path.join(a.dir, "pmc_write", "run_counter_collection.csv"))
     cal = {
