@@ -1026,7 +1026,13 @@ extern "C" int rmbx_attention_f16x3(const float* q, const float* k, const float*
   const char* xe = std::getenv("RMBX_ATTN_XCD");
   a.xcd_map = xe && std::atoi(xe) != 0;
   const int ngroups = (Lq + 31) / 32;
-  const int waves = ngroups >= rmbx::AX_MAX_WAVES ? rmbx::AX_MAX_WAVES : 4;
+  // waves per block (RMBX_ATTN_WAVES, read per launch): 5 = up to five 32-query groups per block
+  // (302 queries: 2 parts; one 5-wave block per CU at 215 registers, so one SIMD carries two
+  // waves and three carry one), 4 = four groups (3 parts, two 4-wave blocks per CU: two waves
+  // on every SIMD)
+  const char* we = std::getenv("RMBX_ATTN_WAVES");
+  const int wsel = we ? std::atoi(we) : 5;
+  const int waves = (wsel == 5 && ngroups >= rmbx::AX_MAX_WAVES) ? rmbx::AX_MAX_WAVES : 4;
   a.parts = (ngroups + waves - 1) / waves;
   const long long nblocks = (long long)B * heads * a.parts;
   RMBX_CHECK_ARG(nblocks < (1ll << 31), "rmbx_attention_f16x3: grid too large");
