@@ -1026,12 +1026,13 @@ extern "C" int rmbx_attention_f16x3(const float* q, const float* k, const float*
   const char* xe = std::getenv("RMBX_ATTN_XCD");
   a.xcd_map = xe && std::atoi(xe) != 0;
   const int ngroups = (Lq + 31) / 32;
-  // waves per block (RMBX_ATTN_WAVES, read per launch): 5 = up to five 32-query groups per block
-  // (302 queries: 2 parts; one 5-wave block per CU at 215 registers, so one SIMD carries two
-  // waves and three carry one), 4 = four groups (3 parts, two 4-wave blocks per CU: two waves
-  // on every SIMD)
+  // waves per block (RMBX_ATTN_WAVES, read per launch): 4 (default) = four 32-query groups per
+  // block (302 queries: 3 parts; two 4-wave blocks per CU at 215 registers: two waves on every
+  // SIMD), 5 = up to five groups (2 parts; one 5-wave block per CU, so one SIMD carries two waves
+  // and three carry one): 1.41 vs 1.75 ms encoder self-attention at 1024 envs
+  // (profiles/r4_attention_waves_ab.log)
   const char* we = std::getenv("RMBX_ATTN_WAVES");
-  const int wsel = we ? std::atoi(we) : 5;
+  const int wsel = we ? std::atoi(we) : 4;
   const int waves = (wsel == 5 && ngroups >= rmbx::AX_MAX_WAVES) ? rmbx::AX_MAX_WAVES : 4;
   a.parts = (ngroups + waves - 1) / waves;
   const long long nblocks = (long long)B * heads * a.parts;

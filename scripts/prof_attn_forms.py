@@ -1,6 +1,6 @@
 """ACT attention at 1024 envs (encoder self-attention 302 x 302 and decoder cross-attention 100 x 302,
-8 heads): rmbx_attention_f16x3 vs rmbx_attention_f32x6, and the f16x3 kernel with 4-wave blocks
-(RMBX_ATTN_WAVES=4, "f16x3-w4"); rounds interleaved in one process; error of each
+8 heads): rmbx_attention_f16x3 vs rmbx_attention_f32x6, and the f16x3 kernel with 5-wave blocks
+(RMBX_ATTN_WAVES=5, "f16x3-w5"); rounds interleaved in one process; error of each
 vs an f64 reference on 16 envs."""
 import os
 import sys
@@ -42,16 +42,16 @@ with torch.no_grad():
         want = ref64(q[:16], k[:16], v[:16], 8)
         errs = {f: (K.attention_f32(q[:16], k[:16], v[:16], 8, form=f).double() - want).abs().max().item()
                 for f in ("f16x3", "x6")}
-        ts = {f: [] for f in ("f16x3", "f16x3-w4", "x6")}
+        ts = {f: [] for f in ("f16x3", "f16x3-w5", "x6")}
         for _ in range(3):
             for f in ts:
-                os.environ["RMBX_ATTN_WAVES"] = "4" if f == "f16x3-w4" else "5"
+                os.environ["RMBX_ATTN_WAVES"] = "5" if f == "f16x3-w5" else "4"
                 ff = f.split("-")[0]
                 K.attention_f32(q, k, v, 8, form=ff)
                 torch.cuda.synchronize()
                 ts[f].append(timeit(lambda: K.attention_f32(q, k, v, 8, form=ff)))
         os.environ.pop("RMBX_ATTN_WAVES")
-        print(f"{name}: f16x3 {min(ts['f16x3']):.3f} ms (err {errs['f16x3']:.2e}) | f16x3-w4 "
-              f"{min(ts['f16x3-w4']):.3f} ms | x6 {min(ts['x6']):.3f} ms (err {errs['x6']:.2e}) | "
+        print(f"{name}: f16x3 {min(ts['f16x3']):.3f} ms (err {errs['f16x3']:.2e}) | f16x3-w5 "
+              f"{min(ts['f16x3-w5']):.3f} ms | x6 {min(ts['x6']):.3f} ms (err {errs['x6']:.2e}) | "
               f"speedup {min(ts['x6']) / min(ts['f16x3']):.2f}x", flush=True)
         del q, k, v
