@@ -723,15 +723,19 @@ __device__ __forceinline__ float dpp_from_right(float x) {
 }
 
 // 16 u8 pixel channels -> two 16-B halves of the CENTRED f16 integers u - 128 (exact)
+// (two bytes at a time: v_perm_b32 places each byte under the f16 exponent of 1024 -- 0x6400 | u is
+// 1024 + u exactly -- and one packed f16 subtract of 1152 leaves u - 128, exact; two instructions
+// per pair instead of the extract / convert / round chain)
 __device__ __forceinline__ void u8x16_to_f16(uint4 v, bool ok, uint4& lo, uint4& hi) {
   uint32_t o[8];
   const uint32_t w[4] = {v.x, v.y, v.z, v.w};
+  const f16x2s off = {(_Float16)1152.0f, (_Float16)1152.0f};
 #pragma unroll
   for (int i = 0; i < 4; ++i) {
-    const f32x2 p0 = {(float)((int)(w[i] & 0xffu) - 128), (float)((int)((w[i] >> 8) & 0xffu) - 128)};
-    const f32x2 p1 = {(float)((int)((w[i] >> 16) & 0xffu) - 128), (float)((int)(w[i] >> 24) - 128)};
-    o[2 * i] = __builtin_bit_cast(uint32_t, __builtin_convertvector(p0, f16x2s));
-    o[2 * i + 1] = __builtin_bit_cast(uint32_t, __builtin_convertvector(p1, f16x2s));
+    const uint32_t e0 = __builtin_amdgcn_perm(0x64646464u, w[i], 0x04010400u);  // {0x64 b1, 0x64 b0}
+    const uint32_t e1 = __builtin_amdgcn_perm(0x64646464u, w[i], 0x04030402u);  // {0x64 b3, 0x64 b2}
+    o[2 * i] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(f16x2s, e0) - off);
+    o[2 * i + 1] = __builtin_bit_cast(uint32_t, __builtin_bit_cast(f16x2s, e1) - off);
   }
   lo = ok ? make_uint4(o[0], o[1], o[2], o[3]) : make_uint4(0, 0, 0, 0);
   hi = ok ? make_uint4(o[4], o[5], o[6], o[7]) : make_uint4(0, 0, 0, 0);
