@@ -206,7 +206,12 @@ struct RenderArgs {
   int dbg;     // diagnostic (RMBX_RENDER_DBG; 0 in production): 1 no ray loop, 2 no stores, 4 test counts, 8 sphere bounds only
 };
 
-__global__ void __launch_bounds__(256) render_kernel(RenderArgs a) {
+// RMBX_RENDER_MINW: minimum waves per SIMD the register allocation targets (4 = 98 registers; 5 =
+// 94, no spills; a build option for the A/B, scripts/build_variant.py render5)
+#ifndef RMBX_RENDER_MINW
+#define RMBX_RENDER_MINW 1
+#endif
+__global__ void __launch_bounds__(256, RMBX_RENDER_MINW) render_kernel(RenderArgs a) {
   __shared__ PrimCam prims[MAX_PRIM];
   __shared__ int order[MAX_PRIM];        // the block's primitives sorted front to back, once
   __shared__ int tile_sorted[MAX_PRIM];  // the tile's survivors in that order
