@@ -206,10 +206,12 @@ struct RenderArgs {
   int dbg;     // diagnostic (RMBX_RENDER_DBG; 0 in production): 1 no ray loop, 2 no stores, 4 test counts, 8 sphere bounds only
 };
 
-// RMBX_RENDER_MINW: minimum waves per SIMD the register allocation targets (4 = 98 registers; 5 =
-// 94, no spills; a build option for the A/B, scripts/build_variant.py render5)
+// RMBX_RENDER_MINW: minimum waves per SIMD the register allocation targets: 5 (default; 94
+// registers, no spills) -- 6.55 vs 7.43 ms per 1024-env 8-bit frame at the unconstrained 98
+// registers / 4 waves, identical images (profiles/r4_render_waves_ab.log); build options for the
+// A/Bs: scripts/build_variant.py render4 / render6
 #ifndef RMBX_RENDER_MINW
-#define RMBX_RENDER_MINW 1
+#define RMBX_RENDER_MINW 5
 #endif
 __global__ void __launch_bounds__(256, RMBX_RENDER_MINW) render_kernel(RenderArgs a) {
   __shared__ PrimCam prims[MAX_PRIM];

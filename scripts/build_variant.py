@@ -1,7 +1,8 @@
 """Build a profiling variant of the library into robomanipbaselines_amd/_lib/librmbx_<name>.so
 (loaded with RMBX_LIB_VARIANT=<name>; the product loads librmbx.so).  Variants:
   slp -- rmbx_gemm.hip without -fno-slp-vectorize (the SLP vectorizer's packed f32 split ops);
-  render5 -- rmbx_render.hip with its registers capped for 5 waves per SIMD."""
+  render4 / render6 -- rmbx_render.hip with its registers for 4 (unconstrained) / 6 waves per SIMD
+  (the default build targets 5)."""
 import os
 import sys
 
@@ -11,8 +12,8 @@ from robomanipbaselines_amd import build as B  # noqa: E402
 name = sys.argv[1]
 if name == "slp":
     B.FILE_FLAGS = {}
-elif name == "render5":
-    B.FILE_FLAGS = dict(B.FILE_FLAGS, **{"rmbx_render.hip": ["-DRMBX_RENDER_MINW=5"]})
+elif name in ("render4", "render6"):
+    B.FILE_FLAGS = dict(B.FILE_FLAGS, **{"rmbx_render.hip": [f"-DRMBX_RENDER_MINW={1 if name == 'render4' else 6}"]})
 else:
     raise SystemExit(f"unknown variant {name}")
 B.LIB_PATH = os.path.join(B.LIB_DIR, f"librmbx_{name}.so")
