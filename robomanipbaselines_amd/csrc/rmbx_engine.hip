@@ -39,6 +39,7 @@ struct Layout {
   size_t con_pos, con_frame, con_dist, con_mu;
   size_t con_tmp;  // collision stage: 4 candidate contacts (pos, normal, dist) per survivor
   size_t hsave;    // solver: Hessian blocks of the last build (incremental updates)
+  size_t fsave;    // solver: Cholesky factor blocks of the last build (reused while the active set holds)
   size_t efc_pos, efc_aref, efc_D, efc_sqD, efc_R, efc_force, efc_jar, efc_Js, efc_vel, efc_tmp;
   size_t efc_rho;  // contact rows: (p x dir, dir), J_r = efc_rho . (V_b2 - V_b1)
   size_t eqr_rho, eqr_coef;  // equality rows: 2 body-side 6-vectors, 2 dof coefficients
@@ -2308,6 +2309,16 @@ struct SolverShared {
   int16_t kb[MAX_NVP];         // dof -> body
 };
 
+// a value the compiler cannot see through (so addresses derived from it are not hoisted out of
+// the loop it is read in); RMBX_SOLVER_HOIST restores the hoisting for the A/B
+// (scripts/build_variant.py hoist)
+__device__ __forceinline__ int opaque_int(int v) {
+#ifndef RMBX_SOLVER_HOIST
+  asm volatile("" : "+v"(v));
+#endif
+  return v;
+}
+
 // X[6b..] <- sum of the increments X over the path world .. b (solver block; parents from LDS)
 __device__ void tree_prefix6_s(SolverShared& S, int nbody, int rounds, double* X, int b) {
   if (b < nbody) S.anc[b] = b == 0 ? -1 : S.par[b];
@@ -2729,11 +2740,18 @@ __device__ __forceinline__ void subtree_sums(const SolverCtx& c, SolverShared& S
     double x[6];
 #pragma unroll
     for (int i = 0; i < 6; i++) x[i] = (b > 0 && b < nb) ? S.bf[6 * b + i] : 0.0;  // (world: unused)
+    // source lanes from an opaque copy of the lane index: __shfl_up's six lane-address
+    // computations are otherwise hoisted to the kernel top and spilled at 128 registers
+    const int lane = opaque_int(b);
 #pragma unroll
     for (int off = 1; off < 64; off <<= 1) {
+      const int src = (lane - off) << 2;  // (b < off: a wrapped lane, discarded below)
 #pragma unroll
       for (int i = 0; i < 6; i++) {
-        const double y = __shfl_up(x[i], off, 64);
+        const unsigned long long u = __double_as_longlong(x[i]);
+        const int lo = __builtin_amdgcn_ds_bpermute(src, (int)u);
+        const int hi = __builtin_amdgcn_ds_bpermute(src, (int)(u >> 32));
+        const double y = __longlong_as_double(((unsigned long long)(unsigned)hi << 32) | (unsigned)lo);
         if (b >= off) x[i] += y;
       }
     }
@@ -2904,6 +2922,7 @@ __device__ double solver_grad(const SolverCtx& c, int32_t* act_flags, SolverShar
 // starts from M; later ones start from the previous H (saved in the workspace) and only add /
 // subtract the rows whose active flag changed since (hess_flags), skipping chunks without such
 // rows -- MuJoCo's Newton solver updates its Hessian incrementally in the same way.
+
 __device__ void solver_hessian(const SolverCtx& c, const double* Mb, const int32_t* act_flags, int32_t* hess_flags,
                                double* hsave, bool incremental, double* a, int bi, int bj, bool own,
                                SolverShared& S) {
@@ -3053,8 +3072,9 @@ __device__ void solver_hessian(const SolverCtx& c, const double* Mb, const int32
   }
 
 __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj, bool own,
-                             int ncon, int nefc, int ne, int nlim, int tree_rounds, int tid,
+                             int ncon, int nefc, int ne, int nlim, int tree_rounds, int tid_,
                              unsigned long long* prof) {
+  const int tid = tid_;
   const rmbx_model& m = *e.m;
   unsigned long long tp = prof ? stamp() : 0;
   const int nv = m.nv, NB = (nv + 3) / 4, NVP = 4 * NB;
@@ -3124,8 +3144,14 @@ __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj,
   // The Hessian depends only on the active row set: it is rebuilt and refactorised only when
   // that set changed since the last factorisation (identical matrix otherwise).
   int32_t* act_flags = WI(efc_act);
+  double* fsave = W(fsave);
   bool have_factor = false;
   for (it = 0; it < m.solver_iterations; it++) {
+    // the thread index, re-read opaquely each iteration: otherwise the compiler hoists ~20
+    // per-lane 64-bit row/dof addresses (base + 8 tid) out of the loop and, at 128 registers,
+    // spills them and reloads them every iteration (one add each to recompute)
+    const int tid = opaque_int(tid_);
+    c.tid = tid;
     bool changed;
     const double gn = solver_grad(c, act_flags, S, &changed);
     SPROF(10)
@@ -3135,8 +3161,19 @@ __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj,
       SPROF(15)
       blk_cholesky_fwd(a, bi, bj, own, NB, S.grad, S, tid);
       blk_solve_back(a, bi, bj, own, NB, S.srch, S, tid);
+      // the factor goes to the workspace (one 128-B store per owned block) instead of staying
+      // live in registers across the row passes and line search, where the compiler spilled it
+      // (with 14 more registers) for all 256 lanes every iteration
+      if (own) {
+#pragma unroll
+        for (int q = 0; q < 16; q++) fsave[16 * tid + q] = a[q];
+      }
       have_factor = true;
     } else {
+      if (own) {
+#pragma unroll
+        for (int q = 0; q < 16; q++) a[q] = fsave[16 * tid + q];
+      }
       blk_solve(a, bi, bj, own, NB, S.grad, S.srch, S, tid);
     }
     SPROF(11)
@@ -3160,7 +3197,7 @@ __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj,
     for (int ls = 0; ls < m.ls_iterations; ls++) {
       double p1 = 0, p2 = 0;
       int changed = 0;
-      for (int r = tid; r < nefc; r += SOLVER_THREADS) {
+      for (int r = opaque_int(tid); r < nefc; r += SOLVER_THREADS) {
         const double js = c.Js[r], jr = c.jar[r];
         const double x = jr + alpha * js;
         if (c.type[r] == 0 || x < 0) {
@@ -3187,13 +3224,13 @@ __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj,
     // move along the search direction; res, M res and jar updated incrementally (as
     // mj_solNewton updates qacc, Ma and efc_Jaref)
     double part = 0, cpart = 0;
-    for (int k = tid; k < NVP; k += SOLVER_THREADS) {
+    for (int k = opaque_int(tid); k < NVP; k += SOLVER_THREADS) {
       S.a[k] += alpha * S.srch[k];
       S.res[k] += alpha * S.srch[k];
       S.Mres[k] += alpha * S.Ms[k];
       if (k < nv) part += S.res[k] * S.Mres[k];
     }
-    for (int r = tid; r < nefc; r += SOLVER_THREADS) {
+    for (int r = opaque_int(tid); r < nefc; r += SOLVER_THREADS) {
       const double jar = c.jar[r] + alpha * c.Js[r];
       c.jar[r] = jar;
       if (c.type[r] == 0 || jar < 0) cpart += 0.5 * c.D[r] * jar * jar;
@@ -3636,6 +3673,7 @@ static Layout make_layout(const rmbx_model& m) {
   const int ne = L.nefc_max;
   L.neqr_max = 6 * m.neq > 0 ? 6 * m.neq : 1;
   L.hsave = take(16 * (size_t)(nb4 * (nb4 + 1) / 2));
+  L.fsave = take(16 * (size_t)(nb4 * (nb4 + 1) / 2));
   L.efc_pos = take(ne);
   L.efc_aref = take(ne);
   L.efc_D = take(ne);

@@ -206,12 +206,14 @@ struct RenderArgs {
   int dbg;     // diagnostic (RMBX_RENDER_DBG; 0 in production): 1 no ray loop, 2 no stores, 4 test counts, 8 sphere bounds only
 };
 
-// RMBX_RENDER_MINW: minimum waves per SIMD the register allocation targets: 5 (default; 94
-// registers, no spills) -- 6.55 vs 7.43 ms per 1024-env 8-bit frame at the unconstrained 98
-// registers / 4 waves, identical images (profiles/r4_render_waves_ab.log); build options for the
-// A/Bs: scripts/build_variant.py render4 / render6
+// RMBX_RENDER_MINW: minimum waves per SIMD the register allocation targets: 8 (default; 64
+// registers, 136 B/lane of spilled set-up values, none in the ray loop's hot path) -- per
+// 1024-env 8-bit frame 5.74-5.79 ms vs 6.46 at 5 waves (94 registers, no spills), 6.06 at 6,
+// 5.82 at 7 and 7.35-7.44 unconstrained (98 registers, 4 waves); identical images
+// (profiles/r4_render_waves_ab.log); the other targets are build options for the A/B
+// (scripts/build_variant.py render4 .. render7)
 #ifndef RMBX_RENDER_MINW
-#define RMBX_RENDER_MINW 5
+#define RMBX_RENDER_MINW 8
 #endif
 __global__ void __launch_bounds__(256, RMBX_RENDER_MINW) render_kernel(RenderArgs a) {
   __shared__ PrimCam prims[MAX_PRIM];

@@ -25,7 +25,7 @@ def medians(path):
     vals = collections.defaultdict(list)
     dur = collections.defaultdict(list)
     for r in csv.DictReader(open(path)):
-        name = r["Kernel_Name"].split("(")[0]
+        name = r["Kernel_Name"].split("(")[0].removeprefix("void ")
         vals[name].append(float(r["Counter_Value"]) * 1024.0)  # counters report KiB
         dur[name].append((int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3)
     return ({k: statistics.median(v) for k, v in vals.items()}, {k: len(v) for k, v in vals.items()},
@@ -112,7 +112,7 @@ def main():
     p.add_argument("--frames", type=int, default=1024, help="--winograd: frames per call")
     p.add_argument("dir")
     p.add_argument("--out", required=True)
-    p.add_argument("--kernels", nargs="+", default=["rmbx::front_kernel", "rmbx::solver_kernel"])
+    p.add_argument("--kernels", nargs="+", default=["rmbx::front_kernel<false>", "rmbx::solver_kernel<4>"])
     p.add_argument("--launches_per_unit", type=int, default=8, help="launches of each kernel per env-step")
     p.add_argument("--units", type=int, default=1024, help="envs per launch")
     a = p.parse_args()
