@@ -2284,7 +2284,10 @@ struct SolverShared {
   double jw[RCHUNK];           // chunk row weights sqrt(D) (active rows)
   double jsg[RCHUNK];          // chunk row signs (incremental Hessian: +1 added, -1 removed)
   double bv[6 * MAX_BODY];     // body velocities of a dof vector / subtree sums (sensors: cacc)
-  double bf[6 * MAX_BODY];     // body forces (sensors: cfrc)
+  union {
+    double bf[6 * MAX_BODY];     // body forces (sensors: cfrc)
+    int16_t hsel[12 * MAX_BODY]; // Hessian build: the rows it adds / takes back, row order (bit 15: take back)
+  };
   double cdof[6 * MAX_NVP];    // motion axes of the dofs (from the front kernel)
   double cinert[10 * MAX_BODY];
   double red[8];
@@ -2937,25 +2940,46 @@ __device__ void solver_hessian(const SolverCtx& c, const double* Mb, const int32
       load_blockp(Mb, tid, a);
     }
   }
-  for (int r0 = 0; r0 < c.nefc; r0 += RCHUNK) {
-    const int nr = min(RCHUNK, c.nefc - r0);
+  // select the rows this build adds (active now; an incremental build: newly active) or takes
+  // back (an incremental build: no longer active) -- one pass over all rows, a block-wide ballot
+  // scan into S.hsel in row order -- so the chunks below only describe and expand selected rows
+  // (an incremental build after a small active-set change is one chunk, not nefc / RCHUNK)
+  int nsel = 0;
+  for (int base = 0; base < c.nefc; base += SOLVER_THREADS) {
+    const int r = base + tid;
+    bool sel = false, back = false;
+    if (r < c.nefc) {
+      const int act = act_flags[r];
+      if (incremental) {
+        sel = act != hess_flags[r];
+        back = !act;
+      } else {
+        sel = act != 0;
+      }
+      hess_flags[r] = act;
+    }
+    const unsigned long long bal = __ballot(sel);
+    const int wv = tid >> 6;
+    lds_sync();
+    if ((tid & 63) == 0) S.ired[wv] = __popcll(bal);
+    lds_sync();
+    int off = nsel;
+    for (int q = 0; q < wv; q++) off += S.ired[q];
+    if (sel) S.hsel[off + __popcll(bal & ((1ull << (tid & 63)) - 1))] = (int16_t)(back ? (r | 0x8000) : r);
+    nsel += S.ired[0] + S.ired[1] + S.ired[2] + S.ired[3];
+  }
+  for (int s0 = 0; s0 < nsel; s0 += RCHUNK) {
+    const int nr = min(RCHUNK, nsel - s0);
     lds_sync();
     if (tid < RCHUNK) {
       double w = 0.0, sg = 1.0;
       if (tid < nr) {
-        const int r = r0 + tid;
-        const int act = act_flags[r];
+        const int hs = (uint16_t)S.hsel[s0 + tid];
+        const int r = hs & 0x7fff;
         const double Dr = c.sqD[r];
         const int kd = c.kind[r], o = c.obj[r];
-        if (incremental) {
-          if (act != hess_flags[r]) {
-            w = Dr;
-            sg = act ? 1.0 : -1.0;
-          }
-        } else if (act) {
-          w = Dr;
-        }
-        hess_flags[r] = act;
+        w = Dr;
+        sg = (hs & 0x8000) ? -1.0 : 1.0;
         if (w != 0.0) {
           // describe row r: sides (body, 6-vector) and dof terms
           const int k = kd & 7, sub = kd >> 3;
