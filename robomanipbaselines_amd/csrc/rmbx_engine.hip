@@ -2976,8 +2976,12 @@ __device__ void solver_hessian(const SolverCtx& c, const double* Mb, const int32
       if (tid < nr) {
         const int hs = (uint16_t)S.hsel[s0 + tid];
         const int r = hs & 0x7fff;
+        // every row's loads in one round trip: the contact 6-vector is loaded whatever the row's
+        // kind (efc_rho has 6 slots per row; unused for the other kinds)
         const double Dr = c.sqD[r];
         const int kd = c.kind[r], o = c.obj[r];
+        const double2* src2 = reinterpret_cast<const double2*>(c.rho + 6 * (size_t)r);
+        const double2 q0 = src2[0], q1 = src2[1], q2 = src2[2];
         w = Dr;
         sg = (hs & 0x8000) ? -1.0 : 1.0;
         if (w != 0.0) {
@@ -2987,11 +2991,11 @@ __device__ void solver_hessian(const SolverCtx& c, const double* Mb, const int32
           int b1 = 0, b2 = 0, d1 = -1, d2 = -1;
           double c1 = 0, c2 = 0;
           if (k == ROW_CONTACT) {
-            const double* src = c.rho + 6 * (size_t)r;
+            const double src[6] = {q0.x, q0.y, q1.x, q1.y, q2.x, q2.y};
+#pragma unroll
             for (int i = 0; i < 6; i++) {
-              const double v = src[i];
-              rho[6 + i] = v;
-              rho[i] = -v;
+              rho[6 + i] = src[i];
+              rho[i] = -src[i];
             }
             b1 = S.ccb[o][0];
             b2 = S.ccb[o][1];
