@@ -3209,7 +3209,19 @@ __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj,
     lds_sync();
     // J search (rows) and M search from one pass of body velocities of the search direction
     body_vel(c, S.srch, S);
-    for (int r = tid; r < nefc; r += SOLVER_THREADS) c.Js[r] = row_dot(c, r, S, S.srch);
+    // the thread's first row (r = tid) is carried in registers through the line search and the
+    // move (J search, J a - aref, D, equality flag): the per-step passes re-read only rows past 256
+    double js0 = 0, jr0 = 0, d0 = 0;
+    bool eq0 = false;
+    const bool row0 = tid < nefc;
+    if (row0) {
+      js0 = row_dot(c, tid, S, S.srch);
+      c.Js[tid] = js0;
+      jr0 = c.jar[tid];
+      d0 = c.D[tid];
+      eq0 = c.type[tid] == 0;
+    }
+    for (int r = tid + SOLVER_THREADS; r < nefc; r += SOLVER_THREADS) c.Js[r] = row_dot(c, r, S, S.srch);
     mass_tail(c, S.srch, S.Ms, S);
     double qp = 0, lp = 0;
     for (int k = tid; k < nv; k += SOLVER_THREADS) {
@@ -3225,7 +3237,15 @@ __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj,
     for (int ls = 0; ls < m.ls_iterations; ls++) {
       double p1 = 0, p2 = 0;
       int changed = 0;
-      for (int r = opaque_int(tid); r < nefc; r += SOLVER_THREADS) {
+      if (row0) {
+        const double x = jr0 + alpha * js0;
+        if (eq0 || x < 0) {
+          p1 += d0 * x * js0;
+          p2 += d0 * js0 * js0;
+        }
+        if (tid >= ne) changed |= ((jr0 + prev * js0 < 0) != (x < 0));
+      }
+      for (int r = opaque_int(tid) + SOLVER_THREADS; r < nefc; r += SOLVER_THREADS) {
         const double js = c.Js[r], jr = c.jar[r];
         const double x = jr + alpha * js;
         if (c.type[r] == 0 || x < 0) {
@@ -3258,7 +3278,12 @@ __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj,
       S.Mres[k] += alpha * S.Ms[k];
       if (k < nv) part += S.res[k] * S.Mres[k];
     }
-    for (int r = opaque_int(tid); r < nefc; r += SOLVER_THREADS) {
+    if (row0) {
+      const double jar = jr0 + alpha * js0;
+      c.jar[tid] = jar;
+      if (eq0 || jar < 0) cpart += 0.5 * d0 * jar * jar;
+    }
+    for (int r = opaque_int(tid) + SOLVER_THREADS; r < nefc; r += SOLVER_THREADS) {
       const double jar = c.jar[r] + alpha * c.Js[r];
       c.jar[r] = jar;
       if (c.type[r] == 0 || jar < 0) cpart += 0.5 * c.D[r] * jar * jar;
