@@ -2976,12 +2976,8 @@ __device__ void solver_hessian(const SolverCtx& c, const double* Mb, const int32
       if (tid < nr) {
         const int hs = (uint16_t)S.hsel[s0 + tid];
         const int r = hs & 0x7fff;
-        // every row's loads in one round trip: the contact 6-vector is loaded whatever the row's
-        // kind (efc_rho has 6 slots per row; unused for the other kinds)
         const double Dr = c.sqD[r];
         const int kd = c.kind[r], o = c.obj[r];
-        const double2* src2 = reinterpret_cast<const double2*>(c.rho + 6 * (size_t)r);
-        const double2 q0 = src2[0], q1 = src2[1], q2 = src2[2];
         w = Dr;
         sg = (hs & 0x8000) ? -1.0 : 1.0;
         if (w != 0.0) {
@@ -2991,11 +2987,11 @@ __device__ void solver_hessian(const SolverCtx& c, const double* Mb, const int32
           int b1 = 0, b2 = 0, d1 = -1, d2 = -1;
           double c1 = 0, c2 = 0;
           if (k == ROW_CONTACT) {
-            const double src[6] = {q0.x, q0.y, q1.x, q1.y, q2.x, q2.y};
-#pragma unroll
+            const double* src = c.rho + 6 * (size_t)r;
             for (int i = 0; i < 6; i++) {
-              rho[6 + i] = src[i];
-              rho[i] = -src[i];
+              const double v = src[i];
+              rho[6 + i] = v;
+              rho[i] = -v;
             }
             b1 = S.ccb[o][0];
             b2 = S.ccb[o][1];
@@ -3209,19 +3205,7 @@ __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj,
     lds_sync();
     // J search (rows) and M search from one pass of body velocities of the search direction
     body_vel(c, S.srch, S);
-    // the thread's first row (r = tid) is carried in registers through the line search and the
-    // move (J search, J a - aref, D, equality flag): the per-step passes re-read only rows past 256
-    double js0 = 0, jr0 = 0, d0 = 0;
-    bool eq0 = false;
-    const bool row0 = tid < nefc;
-    if (row0) {
-      js0 = row_dot(c, tid, S, S.srch);
-      c.Js[tid] = js0;
-      jr0 = c.jar[tid];
-      d0 = c.D[tid];
-      eq0 = c.type[tid] == 0;
-    }
-    for (int r = tid + SOLVER_THREADS; r < nefc; r += SOLVER_THREADS) c.Js[r] = row_dot(c, r, S, S.srch);
+    for (int r = tid; r < nefc; r += SOLVER_THREADS) c.Js[r] = row_dot(c, r, S, S.srch);
     mass_tail(c, S.srch, S.Ms, S);
     double qp = 0, lp = 0;
     for (int k = tid; k < nv; k += SOLVER_THREADS) {
@@ -3237,15 +3221,7 @@ __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj,
     for (int ls = 0; ls < m.ls_iterations; ls++) {
       double p1 = 0, p2 = 0;
       int changed = 0;
-      if (row0) {
-        const double x = jr0 + alpha * js0;
-        if (eq0 || x < 0) {
-          p1 += d0 * x * js0;
-          p2 += d0 * js0 * js0;
-        }
-        if (tid >= ne) changed |= ((jr0 + prev * js0 < 0) != (x < 0));
-      }
-      for (int r = opaque_int(tid) + SOLVER_THREADS; r < nefc; r += SOLVER_THREADS) {
+      for (int r = opaque_int(tid); r < nefc; r += SOLVER_THREADS) {
         const double js = c.Js[r], jr = c.jar[r];
         const double x = jr + alpha * js;
         if (c.type[r] == 0 || x < 0) {
@@ -3278,12 +3254,7 @@ __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj,
       S.Mres[k] += alpha * S.Ms[k];
       if (k < nv) part += S.res[k] * S.Mres[k];
     }
-    if (row0) {
-      const double jar = jr0 + alpha * js0;
-      c.jar[tid] = jar;
-      if (eq0 || jar < 0) cpart += 0.5 * d0 * jar * jar;
-    }
-    for (int r = opaque_int(tid) + SOLVER_THREADS; r < nefc; r += SOLVER_THREADS) {
+    for (int r = opaque_int(tid); r < nefc; r += SOLVER_THREADS) {
       const double jar = c.jar[r] + alpha * c.Js[r];
       c.jar[r] = jar;
       if (c.type[r] == 0 || jar < 0) cpart += 0.5 * c.D[r] * jar * jar;

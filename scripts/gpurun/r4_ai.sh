@@ -5,7 +5,7 @@
 set -o pipefail
 cd /tmp && export TMPDIR=/tmp && cd $GRAFT_REPO_ROOT && mkdir -p gpurun_out
 timeout -k 10 600 python -u -m pytest -x -v --timeout 200 --timeout-method thread -m gpu tests/test_engine_gpu.py tests/test_insert_gpu.py tests/test_pick_gpu.py tests/test_bad_state_gpu.py > gpurun_out/r4_ai_engine_tests.log 2>&1 || exit 1
-for v in "" at-2b03d30 "" at-2b03d30; do
+for v in "" at-c2204b2 at-2b03d30 "" at-c2204b2 at-2b03d30; do
   echo "== variant $v" >> gpurun_out/r4_ai_solver_ab.log
   RMBX_LIB_VARIANT=$v timeout -k 10 200 python3 -u scripts/prof_physics.py 1024 >> gpurun_out/r4_ai_solver_ab.log 2>&1 || exit 1
 done
