@@ -652,12 +652,7 @@ __device__ __forceinline__ void ah_split_w(float x, float y, uint32_t& h, uint32
   l = ah_pk(x - ah_lo(h), y - ah_hi(h));
 }
 
-// RMBX_ATTN_F16X3_MINW: register target in waves per SIMD (1: unconstrained, 215 registers = 2
-// waves); a build option for the occupancy A/B (scripts/build_variant.py attn3)
-#ifndef RMBX_ATTN_F16X3_MINW
-#define RMBX_ATTN_F16X3_MINW 1
-#endif
-__global__ void __launch_bounds__(64 * AX_MAX_WAVES, RMBX_ATTN_F16X3_MINW) attn_fwd_f16x3_kernel(AttnF32Args a) {
+__global__ void __launch_bounds__(64 * AX_MAX_WAVES) attn_fwd_f16x3_kernel(AttnF32Args a) {
   __shared__ __attribute__((aligned(16))) uint16_t sA[2 * AH_BUF];
   __shared__ uint32_t sDim[64];  // per head dimension: max |v| over the keys (f32 bits)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -709,18 +704,10 @@ __global__ void __launch_bounds__(64 * AX_MAX_WAVES, RMBX_ATTN_F16X3_MINW) attn_
   // thread count is a multiple of 16, so a thread's V chunks all hold dims 4 (tid & 15) .. + 3
   float4 st[AX_CH];
   float vmax[4] = {0.f, 0.f, 0.f, 0.f};
-  // the staging offsets depend on tid only: from an opaque copy read per tile, so they are
-  // recomputed in the loop instead of hoisted out of it (and spilled when the registers are capped)
-  auto opaque_tid = [&]() {
-    int v = tid;
-    asm volatile("" : "+v"(v));
-    return v;
-  };
   auto load_tile = [&](int t) {
-    const int tq = opaque_tid();
 #pragma unroll
     for (int i = 0; i < AX_CH; ++i) {
-      const int q = tq + nthreads * i;
+      const int q = tid + nthreads * i;
       const int qq = q & 511, key = 32 * t + (qq >> 4), quad = qq & 15;
       const bool ok = q < 1024 && key < a.Lk;
       const float* src = q < 512 ? kbase + (size_t)key * a.k_rstride : vbase + (size_t)key * a.v_rstride;
@@ -728,10 +715,9 @@ __global__ void __launch_bounds__(64 * AX_MAX_WAVES, RMBX_ATTN_F16X3_MINW) attn_
     }
   };
   auto store_tile = [&](uint16_t* buf) {
-    const int tq = opaque_tid();
 #pragma unroll
     for (int i = 0; i < AX_CH; ++i) {
-      const int q = tq + nthreads * i;
+      const int q = tid + nthreads * i;
       if (q >= 1024) continue;
       const int qq = q & 511, key = qq >> 4, quad = qq & 15;
       const float ax = fabsf(st[i].x), ay = fabsf(st[i].y), az = fabsf(st[i].z), aw = fabsf(st[i].w);

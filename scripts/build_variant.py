@@ -5,7 +5,6 @@
   SIMD (the default build targets 8);
   hoist -- rmbx_engine.hip with the solver's per-iteration addresses hoisted out of the Newton loop
   (RMBX_SOLVER_HOIST: the round-3 code generation, spilled at 128 registers);
-  attn3 -- rmbx_attn.hip's f16x3 kernel compiled for 3 waves per SIMD (168 registers);
   at-<rev> -- every csrc/*.hip source as of git revision <rev> (headers from the working tree): the
   A/B of a kernel change against the commit before it, on one box."""
 import os
@@ -23,8 +22,6 @@ elif name in ("render4", "render5", "render6", "render7"):
     B.FILE_FLAGS = dict(B.FILE_FLAGS, **{"rmbx_render.hip": [f"-DRMBX_RENDER_MINW={w}"]})
 elif name == "hoist":
     B.FILE_FLAGS = dict(B.FILE_FLAGS, **{"rmbx_engine.hip": ["-DRMBX_SOLVER_HOIST"]})
-elif name == "attn3":
-    B.FILE_FLAGS = dict(B.FILE_FLAGS, **{"rmbx_attn.hip": ["-DRMBX_ATTN_F16X3_MINW=3"]})
 elif name.startswith("at-"):
     rev = name[3:]
     tmp = os.path.join("/tmp", f"rmbx_src_{rev}")
