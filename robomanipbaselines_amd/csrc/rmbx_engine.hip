@@ -39,7 +39,6 @@ struct Layout {
   size_t con_pos, con_frame, con_dist, con_mu;
   size_t con_tmp;  // collision stage: 4 candidate contacts (pos, normal, dist) per survivor
   size_t hsave;    // solver: Hessian blocks of the last build (incremental updates)
-  size_t fsave;    // solver: Cholesky factor blocks of the last build (reused while the active set holds)
   size_t efc_pos, efc_aref, efc_D, efc_sqD, efc_R, efc_force, efc_jar, efc_Js, efc_vel, efc_tmp;
   size_t efc_rho;  // contact rows: (p x dir, dir), J_r = efc_rho . (V_b2 - V_b1)
   size_t eqr_rho, eqr_coef;  // equality rows: 2 body-side 6-vectors, 2 dof coefficients
@@ -3168,7 +3167,7 @@ __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj,
   // The Hessian depends only on the active row set: it is rebuilt and refactorised only when
   // that set changed since the last factorisation (identical matrix otherwise).
   int32_t* act_flags = WI(efc_act);
-  double* fsave = W(fsave);
+  const double* hsave_ = W(hsave);
   bool have_factor = false;
   for (it = 0; it < m.solver_iterations; it++) {
     // the thread index, re-read opaquely each iteration: otherwise the compiler hoists ~20
@@ -3185,20 +3184,18 @@ __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj,
       SPROF(15)
       blk_cholesky_fwd(a, bi, bj, own, NB, S.grad, S, tid);
       blk_solve_back(a, bi, bj, own, NB, S.srch, S, tid);
-      // the factor goes to the workspace (one 128-B store per owned block) instead of staying
-      // live in registers across the row passes and line search, where the compiler spilled it
-      // (with 14 more registers) for all 256 lanes every iteration
-      if (own) {
-#pragma unroll
-        for (int q = 0; q < 16; q++) fsave[16 * tid + q] = a[q];
-      }
       have_factor = true;
     } else {
+      // the active set held: the same Hessian, refactored from its workspace copy (bit-identical
+      // factor) -- the factor is not kept live in registers across the row passes and line search
+      // (the compiler spilled it for all 256 lanes every iteration) nor saved after every build
+      // (a 19.6 KB write per build that the usual two-iteration solve never reads back)
       if (own) {
 #pragma unroll
-        for (int q = 0; q < 16; q++) a[q] = fsave[16 * tid + q];
+        for (int q = 0; q < 16; q++) a[q] = hsave_[16 * tid + q];
       }
-      blk_solve(a, bi, bj, own, NB, S.grad, S.srch, S, tid);
+      blk_cholesky_fwd(a, bi, bj, own, NB, S.grad, S, tid);
+      blk_solve_back(a, bi, bj, own, NB, S.srch, S, tid);
     }
     SPROF(11)
     for (int k = tid; k < NVP; k += SOLVER_THREADS) S.srch[k] = -S.srch[k];
@@ -3697,7 +3694,6 @@ static Layout make_layout(const rmbx_model& m) {
   const int ne = L.nefc_max;
   L.neqr_max = 6 * m.neq > 0 ? 6 * m.neq : 1;
   L.hsave = take(16 * (size_t)(nb4 * (nb4 + 1) / 2));
-  L.fsave = take(16 * (size_t)(nb4 * (nb4 + 1) / 2));
   L.efc_pos = take(ne);
   L.efc_aref = take(ne);
   L.efc_D = take(ne);
