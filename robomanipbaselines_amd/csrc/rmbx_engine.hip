@@ -2955,7 +2955,7 @@ __device__ void solver_hessian(const SolverCtx& c, const double* Mb, const int32
       } else {
         sel = act != 0;
       }
-      hess_flags[r] = act;
+      if (!incremental) hess_flags[r] = act;
     }
     const unsigned long long bal = __ballot(sel);
     const int wv = tid >> 6;
@@ -3079,7 +3079,7 @@ __device__ void solver_hessian(const SolverCtx& c, const double* Mb, const int32
       }
     }
   }
-  if (own) {
+  if (own && !incremental) {
 #pragma unroll
     for (int q = 0; q < 16; q++) hsave[16 * tid + q] = a[q];
   }
@@ -3164,10 +3164,7 @@ __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj,
   SPROF(9)
   const double scale = 1.0 / (m.meaninertia * (nv > 1 ? nv : 1));
   int it;
-  // The Hessian depends only on the active row set: it is rebuilt and refactorised only when
-  // that set changed since the last factorisation (identical matrix otherwise).
   int32_t* act_flags = WI(efc_act);
-  const double* hsave_ = W(hsave);
   bool have_factor = false;
   for (it = 0; it < m.solver_iterations; it++) {
     // the thread index, re-read opaquely each iteration: otherwise the compiler hoists ~20
@@ -3179,24 +3176,20 @@ __device__ int solver_newton(Env& e, SolverShared& S, double* a, int bi, int bj,
     const double gn = solver_grad(c, act_flags, S, &changed);
     SPROF(10)
     if (scale * sqrt(gn) < m.solver_tolerance) break;
-    if (changed || !have_factor) {
-      solver_hessian(c, Mb, act_flags, WI(efc_hact), W(hsave), have_factor, a, bi, bj, own, S);
-      SPROF(15)
-      blk_cholesky_fwd(a, bi, bj, own, NB, S.grad, S, tid);
-      blk_solve_back(a, bi, bj, own, NB, S.srch, S, tid);
-      have_factor = true;
-    } else {
-      // the active set held: the same Hessian, refactored from its workspace copy (bit-identical
-      // factor) -- the factor is not kept live in registers across the row passes and line search
-      // (the compiler spilled it for all 256 lanes every iteration) nor saved after every build
-      // (a 19.6 KB write per build that the usual two-iteration solve never reads back)
-      if (own) {
-#pragma unroll
-        for (int q = 0; q < 16; q++) a[q] = hsave_[16 * tid + q];
-      }
-      blk_cholesky_fwd(a, bi, bj, own, NB, S.grad, S, tid);
-      blk_solve_back(a, bi, bj, own, NB, S.srch, S, tid);
-    }
+    // H = M + J^T D J over the active rows: built in full at the first iteration (saved with its
+    // row set), later as that saved matrix +/- the rows whose activity differs from its set (the
+    // net change: a row that came and went is never touched; with the usual two iterations the
+    // same sums as a chain of increments). No copy of the factor is kept: when the active set did
+    // not change (rare) the same net change is applied again -- a bit-identical matrix -- and
+    // refactored, instead of a 19.6 KB factor write after every build that is almost never read.
+    // (With one code path after the gradient the solver also compiles without spills at 128
+    // registers: the separate reuse-the-factor solve was the last register peak.)
+    (void)changed;
+    solver_hessian(c, Mb, act_flags, WI(efc_hact), W(hsave), have_factor, a, bi, bj, own, S);
+    SPROF(15)
+    blk_cholesky_fwd(a, bi, bj, own, NB, S.grad, S, tid);
+    blk_solve_back(a, bi, bj, own, NB, S.srch, S, tid);
+    have_factor = true;
     SPROF(11)
     for (int k = tid; k < NVP; k += SOLVER_THREADS) S.srch[k] = -S.srch[k];
     lds_sync();
