@@ -38,7 +38,7 @@ struct Layout {
   size_t ten_len, ten_vel;
   size_t con_pos, con_frame, con_dist, con_mu;
   size_t con_tmp;  // collision stage: 4 candidate contacts (pos, normal, dist) per survivor
-  size_t hsave;    // solver: Hessian blocks of the last build (incremental updates)
+  size_t hsave;    // solver: Hessian blocks of the substep's full build (net-change updates)
   size_t efc_pos, efc_aref, efc_D, efc_sqD, efc_R, efc_force, efc_jar, efc_Js, efc_vel, efc_tmp;
   size_t efc_rho;  // contact rows: (p x dir, dir), J_r = efc_rho . (V_b2 - V_b1)
   size_t eqr_rho, eqr_coef;  // equality rows: 2 body-side 6-vectors, 2 dof coefficients
@@ -2921,9 +2921,10 @@ __device__ double solver_grad(const SolverCtx& c, int32_t* act_flags, SolverShar
 
 // Hessian blocks a = M + J^T D_act J (active rows only), in RCHUNK-row chunks of J computed in
 // LDS from the row descriptions and cdof (scaled by sqrt(D)).  The first build of a substep
-// starts from M; later ones start from the previous H (saved in the workspace) and only add /
-// subtract the rows whose active flag changed since (hess_flags), skipping chunks without such
-// rows -- MuJoCo's Newton solver updates its Hessian incrementally in the same way.
+// starts from M and saves H with its row set (hsave, hess_flags); later ones start from that
+// saved H and only add / subtract the rows whose active flag differs from that set (the net
+// change; neither the copy nor the set is rewritten) -- MuJoCo's Newton solver likewise updates
+// its Hessian incrementally instead of rebuilding it.
 
 __device__ void solver_hessian(const SolverCtx& c, const double* Mb, const int32_t* act_flags, int32_t* hess_flags,
                                double* hsave, bool incremental, double* a, int bi, int bj, bool own,
