@@ -2930,7 +2930,6 @@ __device__ void solver_hessian(const SolverCtx& c, const double* Mb, const int32
                                double* hsave, bool incremental, double* a, int bi, int bj, bool own,
                                SolverShared& S) {
   const int tid = c.tid, nv = c.nv, NVP = 4 * c.NB;
-  const unsigned nvp_magic = ((1u << 20) + NVP - 1) / NVP;  // ceil(2^20 / NVP)
   __syncthreads();  // act_flags were written row-per-thread through global memory: full fence
   unsigned long long tp_ = c.prof ? stamp() : 0;
   if (own) {
@@ -3033,8 +3032,7 @@ __device__ void solver_hessian(const SolverCtx& c, const double* Mb, const int32
     // J_rk = [k on chain(b1)] cdof_k . rho1 + [k on chain(b2)] cdof_k . rho2 + dof terms; a
     // contact's two sides are exact negatives, so dofs on both chains give exactly 0
     for (int e = tid; e < RCHUNK * NVP; e += SOLVER_THREADS) {
-      // e / NVP by a multiply-shift: exact for e < 2^20 / NVP (here e < RCHUNK * NVP <= 1152)
-      const int rr = (int)(((unsigned)e * nvp_magic) >> 20), k = e - rr * NVP;
+      const int rr = e / NVP, k = e - rr * NVP;
       double v = 0.0;
       const double w = S.jw[rr];
       if (rr < nr && k < nv && w != 0.0) {
