@@ -485,16 +485,40 @@ def timed_run(groups, args, dist):
     markers = os.environ.get("RMBX_TRACE_MARKERS") == "1"  # scripts/trace_window.py --marker spin_kernel
     if markers:
         torch.cuda._sleep(1000)
+    # per-phase split of the timed steps (one group: its marks are one stream's timeline)
+    from robomanipbaselines_amd.common.phase_timer import PhaseTimer
+
+    timer = PhaseTimer() if len(groups) == 1 else None
+    if timer is not None:
+        groups[0].attach_phase_timer(timer)
     torch.cuda.synchronize()
     t0 = time.time()
     for _ in range(args.steps):
         for ro, st in zip(groups, streams):
             with torch.cuda.stream(st):
                 ro.step_once()
+    if timer is not None:
+        timer.mark("end")
     torch.cuda.synchronize()
     if dist:
         tdist.barrier()
     elapsed = time.time() - t0
+    phases = None
+    if timer is not None:
+        groups[0].attach_phase_timer(None)
+        seg, window = timer.summary()
+        seg.pop("end", None)
+        infers = sum(1 for (lab, _), (nxt, _) in zip(timer.marks, timer.marks[1:]) if lab == "policy" and nxt == "render")
+        phases = {"ms_per_env_step": {k: round(v / args.steps, 3) for k, v in sorted(seg.items())},
+                  "gpu_window_ms_per_env_step": round(window / args.steps, 3),
+                  "wall_ms_per_env_step": round(1e3 * elapsed / args.steps, 3),
+                  "accounted_frac": round(window / (1e3 * elapsed), 4),
+                  "inferences_in_window": infers,
+                  "note": "HIP events at the phase boundaries of every timed env-step on the rollout's stream: "
+                          "render = rmbx_render of the policy camera, policy = infer_policy minus the render "
+                          "(state, ACT, temporal ensemble), physics = rmbx_engine_step (8 substeps), glue = "
+                          "the rest (command routing, obs, reward, schedule); a window of K steps holds "
+                          "ceil or floor of K/skip inferences depending on the phase of rollout_time_idx"}
     if markers:
         torch.cuda._sleep(1000)
         torch.cuda.synchronize()
@@ -537,7 +561,7 @@ def timed_run(groups, args, dist):
         t = torch.tensor([elapsed], dtype=torch.float64, device=groups[0].device)
         tdist.all_reduce(t, op=tdist.ReduceOp.MAX)
         elapsed = float(t.item())
-    return elapsed, np.array(phys), np.array(infer), np.array(infer_full)
+    return elapsed, np.array(phys), np.array(infer), np.array(infer_full), phases
 
 
 @torch.no_grad()
@@ -595,7 +619,7 @@ def rank_main(args):
 
     groups = make_groups(args.precision)
     ro = groups[0]
-    elapsed, phys, infer, infer_full = timed_run(groups, args, dist)
+    elapsed, phys, infer, infer_full, phases = timed_run(groups, args, dist)
     value = total * args.steps / elapsed
     if dist:
         # RCCL all-gather of per-env episode records (success, reward, duration, steps)
@@ -631,7 +655,8 @@ def rank_main(args):
         "config": {"workload": f"MujocoUR5eCable x{total} ({n} per GPU), ACT (ResNet-18 + transformer 4/7 layers, "
                                f"chunk 100, skip 3, temporal ensembling), {args.precision} policy, RolloutPhase hot loop",
                    "num_envs_per_gpu": n, "total_envs": total,
-                   "parallelism": f"env-sharded x{world}, RCCL all-gather of results",
+                   "parallelism": (f"env-sharded x{world}, RCCL all-gather of results" if world > 1
+                                   else "single GPU (no collective)"),
                    "env_groups": G,
                    "act_decoder_layers_run": 7 if args.act_full_decoder else 1},
         "policy_inference_us_per_call": round(1e6 * float(infer.mean()), 1) if len(infer) else None,
@@ -653,6 +678,8 @@ def rank_main(args):
                           "algorithmic_flops_per_substep": round(fl_sub)},
         "contacts_mean": ncon, "constraint_rows_mean": nefc, "newton_iters_mean": iters,
     }
+    if phases is not None:
+        result["phases"] = phases
     if len(infer):
         pol_tf = groups[0].n * pol_flops / float(infer.mean()) / 1e12
         peak = MFMA_PEAK_TFLOPS[args.precision]
@@ -697,7 +724,7 @@ def rank_main(args):
         del groups, ro, eng
         torch.cuda.empty_cache()
         groups16 = make_groups("bf16")
-        el16, _, inf16, _ = timed_run(groups16, args, dist)
+        el16, _, inf16, _, phases16 = timed_run(groups16, args, dist)
         ro32 = make_rollout(args, dev, "fp32", 16, g0)  # same weights (seeded), its own 16-env frame
         err_abs, err_rel = bf16_action_error(ro32, groups16[0])
         result["secondary_bf16"] = {
@@ -705,6 +732,7 @@ def rank_main(args):
             "ms_per_step": round(1e3 * el16 / args.steps, 3), "dtype": "f64 physics + bf16 policy",
             "policy_inference_us_per_call": round(1e6 * float(inf16.mean()), 1) if len(inf16) else None,
             "max_abs_action_err_vs_fp32": err_abs, "chunk_rel_l2_err_vs_fp32": err_rel,
+            "phases_ms_per_env_step": None if phases16 is None else phases16["ms_per_env_step"],
             "note": "throughput mode, NOT reference precision: same workload with the ACT policy in bf16; "
                     "action error measured on the first 16 envs' frame (same weights, same inputs)"}
         if len(inf16):

@@ -65,6 +65,17 @@ class BatchedRolloutBase:
         self._infer_events = []
         self.datetime_now = datetime.datetime.now()
         self._active = None  # optional caller override of the per-env step mask
+        self.phase_timer = None  # optional PhaseTimer (common/phase_timer.py): bench.py's per-phase split
+
+    def attach_phase_timer(self, timer):
+        """Record HIP events at the policy / render / physics / glue boundaries of every env-step
+        (None detaches)."""
+        self.phase_timer = timer
+        self.env.phase_timer = timer
+
+    def _mark(self, label):
+        if self.phase_timer is not None:
+            self.phase_timer.mark(label)
 
     # -- arguments (RolloutBase.setup_args :165-284 + batching flags) --------------------------
     def setup_args(self, parser=None, argv=None):
@@ -224,12 +235,14 @@ class BatchedRolloutBase:
         if getattr(self, "_img", None) is None or self._img.dtype != dtype or tuple(self._img.shape[2:]) != shape:
             self._img = torch.empty((self.n, len(self.camera_names)) + shape, dtype=dtype, device=self.device)
             self._img_cam = [torch.empty((self.n,) + shape, dtype=dtype, device=self.device) for _ in self.camera_names]
+        self._mark("render")
         if len(self.camera_names) == 1:
             self.env.render_images(self.camera_names[0], policy=self._img.view((self.n,) + shape), mean=mean, std=std)
-            return self._img
-        for i, cam in enumerate(self.camera_names):
-            self.env.render_images(cam, policy=self._img_cam[i], mean=mean, std=std)
-            self._img[:, i].copy_(self._img_cam[i])
+        else:
+            for i, cam in enumerate(self.camera_names):
+                self.env.render_images(cam, policy=self._img_cam[i], mean=mean, std=std)
+                self._img[:, i].copy_(self._img_cam[i])
+        self._mark("policy")
         return self._img
 
     # -- command routing (MotionManager / ArmManager) ------------------------------------------
@@ -320,9 +333,11 @@ class BatchedRolloutBase:
         loop never waits on the device; wall clock on a CPU device."""
         if self.device.type == "cuda":
             e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            self._mark("policy")
             e0.record()
             self.infer_policy()
             e1.record()
+            self._mark("glue")
             self._infer_events.append((e0, e1))
         else:
             t0 = time.time()
@@ -357,6 +372,7 @@ class BatchedRolloutBase:
             self.rollout_time_idx += 1
 
     def step_once(self):
+        self._mark("glue")
         self._pre_update()
         active = self._active if self._active is not None else self._step_mask
         self.obs, self.reward, _, _, self.info = self.env.step(self.env_action(), active=active)

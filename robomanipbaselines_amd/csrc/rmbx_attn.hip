@@ -623,11 +623,17 @@ __global__ void __launch_bounds__(64 * AX_MAX_WAVES) attn_fwd_f32x6_kernel(AttnF
 //   O^T += V^T P^T: V as K; P' = 2^14 exp2(...) (the power of two keeps every probability down to
 //                 2^-28 in f16's normal range; l sums the same P', so O = acc / l is unchanged)
 //                 = ph + pl: O' = vh ph + vh pl + vl (2^-11 ph)
-// Each piece product is exact in f32; the dropped kl ql / vl pl terms are 2^-22 relative.  f16's
-// range is checked per block: any |q|, |k|, |v| >= 2^15 (f16 overflow) or a head dimension whose
-// max |v| over the keys is in (0, 2^-6) (its values would sit near f16's subnormal floor) flags the
-// block, and rmbx_attention_f16x3 re-runs the flagged blocks on the bf16x6 kernel (f32's exponent
-// range), so every query's result depends only on its own block (one head of one batch item).
+// Each piece product is exact in f32; the dropped kl ql / vl pl terms are 2^-22 relative.  Q is
+// scaled per query by a power of two 2^t putting the query's max |q| (over the head's 64 dims) in
+// [2^13, 2^14) before the split, so its pieces stay in f16's normal range whatever the query's
+// magnitude (an unscaled ql = f16(q - qh) is subnormal for every |q| < 2^-3, an absolute error floor
+// of 2^-25 per element); the softmax undoes the scale exactly through the per-query log2 factor
+// c 2^-t (S' = 2^t S, exp2((S' - m') c 2^-t) = exp2((S - m) c)).  f16's range of the staged
+// operands is checked per block: any |k|, |v| >= 2^15 (f16 overflow), a max |k| over the block in
+// (0, 2^-6), a head dimension whose max |v| over the keys is in (0, 2^-6) (their values would sit
+// near f16's subnormal floor), or a non-finite query flags the block, and rmbx_attention_f16x3
+// re-runs the flagged blocks on the bf16x6 kernel (f32's exponent range), so every query's result
+// depends only on its own block (one head of one batch item).
 // Layout of the bf16x6 kernel, two pieces per staged tile (16 KiB per buffer).
 // ---------------------------------------------------------------------------------------------
 constexpr int AH_PLANE = 32 * 64;      // f16 elements of one piece of a K or V^T tile
@@ -655,6 +661,7 @@ __device__ __forceinline__ void ah_split_w(float x, float y, uint32_t& h, uint32
 __global__ void __launch_bounds__(64 * AX_MAX_WAVES) attn_fwd_f16x3_kernel(AttnF32Args a) {
   __shared__ __attribute__((aligned(16))) uint16_t sA[2 * AH_BUF];
   __shared__ uint32_t sDim[64];  // per head dimension: max |v| over the keys (f32 bits)
+  __shared__ uint32_t sKmax;     // max |k| over the block (f32 bits)
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int nthreads = blockDim.x;
   // block -> (head, query part): plain order, or (xcd_map) the parts of one head on one XCD, one
@@ -677,23 +684,47 @@ __global__ void __launch_bounds__(64 * AX_MAX_WAVES) attn_fwd_f16x3_kernel(AttnF
   const float* vbase = a.v + (size_t)b * a.v_bstride + hd * 64;
   const int nt = (a.Lk + 31) >> 5;
   if (tid < 64) sDim[tid] = 0u;
-  float big = 0.f;  // this thread's max |q|, |k|, |v|
+  if (tid == 0) sKmax = 0u;
+  float big = 0.f;   // this thread's max |k|, |v| (and inf for a non-finite query)
+  float kmx = 0.f;   // this thread's max |k|
 
-  // Q pieces (B operand of S^T = K Q^T): dims 16 s + 8 kh .. +7 of query qi; fq[s][2] = 2^-11 qh
+  // Q pieces (B operand of S^T = K Q^T): dims 16 s + 8 kh .. +7 of query qi, scaled by the query's
+  // power of two 2^t (max |q| into [2^13, 2^14)); fq[s][2] = 2^-11 qh
   f16x8 fq[4][3];
+  float c = a.scale_log2;  // this query's log2-domain softmax factor: scale_log2 2^-t
   {
     const float* qp = a.q + (size_t)b * a.q_bstride + (size_t)(q_ok ? qi : 0) * a.q_rstride + hd * 64 + 8 * kh;
+    float4 x[4][2];
+    float qm = 0.f;
 #pragma unroll
     for (int s = 0; s < 4; ++s) {
-      const float4 x0 = *reinterpret_cast<const float4*>(qp + 16 * s);
-      const float4 x1 = *reinterpret_cast<const float4*>(qp + 16 * s + 4);
-      big = fmaxf(big, fmaxf(fmaxf(fabsf(x0.x), fabsf(x0.y)), fmaxf(fabsf(x0.z), fabsf(x0.w))));
-      big = fmaxf(big, fmaxf(fmaxf(fabsf(x1.x), fabsf(x1.y)), fmaxf(fabsf(x1.z), fabsf(x1.w))));
+      x[s][0] = *reinterpret_cast<const float4*>(qp + 16 * s);
+      x[s][1] = *reinterpret_cast<const float4*>(qp + 16 * s + 4);
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+        qm = fmaxf(qm, fmaxf(fmaxf(fabsf(x[s][u].x), fabsf(x[s][u].y)), fmaxf(fabsf(x[s][u].z), fabsf(x[s][u].w))));
+    }
+    qm = fmaxf(qm, __shfl_xor(qm, 32));  // the other 32 dims of the query
+    int t = 0;
+    if (qm > 0.f && qm < INFINITY) {
+      int e;
+      frexpf(qm, &e);  // qm in [2^(e-1), 2^e)
+      t = 14 - e;
+      t = t < -100 ? -100 : (t > 100 ? 100 : t);  // (keeps c 2^-t a normal f32)
+    } else if (qm == INFINITY) {
+      big = INFINITY;  // a non-finite query: the block re-runs on bf16x6
+    }
+    c = ldexpf(c, -t);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
       uint32_t h[4], l[4];
-      ah_split_w(x0.x, x0.y, h[0], l[0]);
-      ah_split_w(x0.z, x0.w, h[1], l[1]);
-      ah_split_w(x1.x, x1.y, h[2], l[2]);
-      ah_split_w(x1.z, x1.w, h[3], l[3]);
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const float4 y = make_float4(ldexpf(x[s][u].x, t), ldexpf(x[s][u].y, t), ldexpf(x[s][u].z, t),
+                                     ldexpf(x[s][u].w, t));
+        ah_split_w(y.x, y.y, h[2 * u], l[2 * u]);
+        ah_split_w(y.z, y.w, h[2 * u + 1], l[2 * u + 1]);
+      }
       fq[s][0] = __builtin_bit_cast(f16x8, make_uint4(h[0], h[1], h[2], h[3]));
       fq[s][1] = __builtin_bit_cast(f16x8, make_uint4(l[0], l[1], l[2], l[3]));
       fq[s][2] = fq[s][0] * (_Float16)0.00048828125f;
@@ -726,6 +757,7 @@ __global__ void __launch_bounds__(64 * AX_MAX_WAVES) attn_fwd_f16x3_kernel(AttnF
       ah_split_a(st[i].x, st[i].y, h[0], l[0]);
       ah_split_a(st[i].z, st[i].w, h[1], l[1]);
       if (q < 512) {  // K: 4 dims = half a 16-byte chunk of the key row
+        kmx = fmaxf(kmx, fmaxf(fmaxf(ax, ay), fmaxf(az, aw)));
         const int off = key * 64 + (((quad >> 1) ^ ((key >> 1) & 7)) << 3) + 4 * (quad & 1);
         *reinterpret_cast<uint2*>(buf + off) = make_uint2(h[0], h[1]);
         *reinterpret_cast<uint2*>(buf + AH_PLANE + off) = make_uint2(l[0], l[1]);
@@ -751,7 +783,6 @@ __global__ void __launch_bounds__(64 * AX_MAX_WAVES) attn_fwd_f16x3_kernel(AttnF
   store_tile(sA);
   __syncthreads();
 
-  const float c = a.scale_log2;
   const bool ragged = (a.Lk & 31) != 0;
   const int d0 = at_sigma(r32), d1 = d0 + 32;
   f32x16 acc0 = {}, acc1 = {};
@@ -833,12 +864,17 @@ __global__ void __launch_bounds__(64 * AX_MAX_WAVES) attn_fwd_f16x3_kernel(AttnF
 #pragma unroll
   for (int e = 0; e < 4; ++e)  // (|v| as u32 bits orders like the value)
     if (vmax[e] > 0.f) atomicMax(&sDim[4 * (tid & 15) + e], __float_as_uint(vmax[e]));
+  if (kmx > 0.f) atomicMax(&sKmax, __float_as_uint(kmx));
   __syncthreads();
   // (fmaxf skips NaNs: NaN inputs are not flagged and propagate through the f16 pieces)
   bool flag = big >= AH_BIG;
   if (tid < 64) {
     const float m = __uint_as_float(sDim[tid]);
     flag = flag || (m > 0.f && m < AH_TINY);
+  }
+  if (tid == 0) {
+    const float km = __uint_as_float(sKmax);
+    flag = flag || (km > 0.f && km < AH_TINY);
   }
   const int any = __syncthreads_or(flag ? 1 : 0);
   if (tid == 0) a.redo[bh * a.parts + part] = any;  // the bf16x6 kernel's block order

@@ -457,6 +457,9 @@ extern "C" int rmbx_conv3x3_f16x3_patch(const float* in, int N, int H, int W, in
                  "rmbx_conv3x3_f16x3_patch: bad plane stride %lld", w_plane_stride);
   RMBX_CHECK_ARG((((uintptr_t)in | (uintptr_t)w_planes) & 15) == 0,
                  "rmbx_conv3x3_f16x3_patch: in / w_planes must be 16-byte aligned");
+  // the epilogue reads w_scale / bias / res and writes out as float4 (no scalar fallback)
+  RMBX_CHECK_ARG((((uintptr_t)out | (uintptr_t)res | (uintptr_t)bias | (uintptr_t)w_scale) & 15) == 0,
+                 "rmbx_conv3x3_f16x3_patch: out / res / bias / w_scale must be 16-byte aligned");
   RMBX_CHECK_ARG((long long)N * H * W * (C > Cout ? C : Cout) < (1ll << 40), "rmbx_conv3x3_f16x3_patch: too large");
   if (N == 0) return RMBX_OK;
   rmbx::ConvPArgs a{};

@@ -2260,6 +2260,10 @@ __device__ void sensors(Env& e, int ncon, int tid, double* cacc, double* cfrc, d
 #define MAX_CON 208  // contacts (J^T w: one wrench per contact in S.cw)
 #define EQ_TAG 1024
 static_assert(NEQR + MAX_LIM <= RCHUNK * 12, "J^T w stages the equality/limit row weights in S.jrho");
+// capacity of the Hessian build's row-selection list: every constraint row can be selected once,
+// and nefc_max = 4 max_contacts + 6 neq + 2 njnt + 8 (make_layout) with max_contacts <= MAX_CON,
+// neq <= NEQR (each equality has >= 1 row) and 2 njnt <= MAX_LIM (checked at create)
+#define HSEL_CAP (4 * MAX_CON + 6 * NEQR + MAX_LIM + 8)
 
 struct SolverShared {
   double Lcol[MAX_NB][16];  // Cholesky: current block column, by block row
@@ -2285,7 +2289,7 @@ struct SolverShared {
   double bv[6 * MAX_BODY];     // body velocities of a dof vector / subtree sums (sensors: cacc)
   union {
     double bf[6 * MAX_BODY];     // body forces (sensors: cfrc)
-    int16_t hsel[12 * MAX_BODY]; // Hessian build: the rows it adds / takes back, row order (bit 15: take back)
+    int16_t hsel[HSEL_CAP];      // Hessian build: the rows it adds / takes back, row order (bit 15: take back)
   };
   double cdof[6 * MAX_NVP];    // motion axes of the dofs (from the front kernel)
   double cinert[10 * MAX_BODY];
@@ -2310,6 +2314,8 @@ struct SolverShared {
   int16_t send[MAX_BODY];      // end of each body's DFS subtree id range
   int16_t kb[MAX_NVP];         // dof -> body
 };
+static_assert(sizeof(int16_t) * HSEL_CAP <= sizeof(double) * 6 * MAX_BODY,
+              "the Hessian row-selection list must fit inside its union partner bf");
 
 // a value the compiler cannot see through (so addresses derived from it are not hoisted out of
 // the loop it is read in); RMBX_SOLVER_HOIST restores the hoisting for the A/B
@@ -3804,6 +3810,9 @@ int rmbx_engine_create(const struct rmbx_model* model, int n_env, rmbx_engine** 
     const int p = h.body_parent[b];
     RMBX_CHECK_ARG(b < subtree_end[p], "bodies are not in DFS preorder (body %d outside its parent's range)", b);
   }
+  RMBX_CHECK_ARG(make_layout(h).nefc_max <= HSEL_CAP,
+                 "nefc_max=%d exceeds the solver's Hessian row-selection capacity (%d)", make_layout(h).nefc_max,
+                 HSEL_CAP);
   rmbx_engine* eng = new rmbx_engine();
   {
     int maxd = 0;
@@ -3946,6 +3955,7 @@ int rmbx_engine_ws_offset(const rmbx_engine* eng, const char* name, size_t* offs
       {"sxpos", L.sxpos, 3 * (size_t)m.nsite},
       {"con_pos", L.con_pos, 3 * (size_t)m.max_contacts},
       {"con_dist", L.con_dist, (size_t)m.max_contacts},
+      {"con_frame", L.con_frame, 9 * (size_t)m.max_contacts},
       {"efc_force", L.efc_force, (size_t)L.nefc_max},
       {"efc_D", L.efc_D, (size_t)L.nefc_max},
       {"hsave", L.hsave, 16 * (size_t)(((nv + 3) / 4) * ((nv + 3) / 4 + 1) / 2)},
@@ -3953,6 +3963,7 @@ int rmbx_engine_ws_offset(const rmbx_engine* eng, const char* name, size_t* offs
       // int32 arrays: offsets in int32 units from the workspace start (2 per double)
       {"con_b1", 2 * L.ints + L.con_b1, (size_t)m.max_contacts},
       {"con_b2", 2 * L.ints + L.con_b2, (size_t)m.max_contacts},
+      {"con_pair", 2 * L.ints + L.con_pair, (size_t)m.max_contacts},
       {"efc_hact", 2 * L.ints + L.efc_hact, (size_t)L.nefc_max},
       {"efc_act", 2 * L.ints + L.efc_act, (size_t)L.nefc_max},
   };

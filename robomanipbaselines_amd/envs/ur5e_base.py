@@ -74,6 +74,7 @@ class BatchedMujocoUR5eEnvBase:
         # the info dict's camera frames (_get_info): rendered on first access within an env-step
         self._step_id = 0
         self._frames = {}  # camera -> [step id, rgb u8 [n,H,W,3], depth f32 [n,H,W]]
+        self.phase_timer = None  # optional PhaseTimer: marks the physics segment of step()
 
     # -- reference API ----------------------------------------------------------------------
     def _setup_task(self):
@@ -87,6 +88,9 @@ class BatchedMujocoUR5eEnvBase:
         bp = self.engine.body_pos
         bp[:, self._world_body, :] = torch.tensor(pos, dtype=torch.float64, device=self.device)
         self.world_idx = world_idx
+        # the world changed: an earlier step's lazily rendered info frames would show it, so they
+        # become stale (reading them raises, as after the next step)
+        self._step_id += 1
         return world_idx
 
     def _world_positions(self, world_idx, cumulative_idx):
@@ -141,7 +145,11 @@ class BatchedMujocoUR5eEnvBase:
         e = self.engine
         if action is not None:
             e.ctrl.copy_(action)
+        if self.phase_timer is not None:
+            self.phase_timer.mark("physics")
         e.step(self.frame_skip, active=active)
+        if self.phase_timer is not None:
+            self.phase_timer.mark("glue")
         self._reset_bad_states()
         self._step_id += 1
         obs = self._get_obs()

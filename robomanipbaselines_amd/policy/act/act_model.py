@@ -92,7 +92,7 @@ def _x6_linear_padded(owner, name, x, w, b):
 
     N, Kd = w.shape
     Np, Kp = -(-N // 128) * 128, -(-Kd // 32) * 32
-    key = (w.data_ptr(), w._version, b.data_ptr(), Np, Kp)
+    key = (w.data_ptr(), w._version, b.data_ptr(), b._version, Np, Kp)
     cache = owner.__dict__.setdefault("_x6p", {})
     ent = cache.get(name)
     if ent is None or ent[0] != key:

@@ -319,7 +319,8 @@ class FusedResNet18Trunk(nn.Module):
         w = self.stem.conv.weight
         if w.dtype != torch.float32 or w.shape[0] != 64 or x_u8.shape[2] > K.STEM_POOL_MAX_WS:
             raise ValueError("forward_s2d_u8: needs the f32 64-channel stem and Ws <= STEM_POOL_MAX_WS")
-        key = (w.data_ptr(), w._version, self.stem.conv.bias.data_ptr(), tuple(mean), tuple(std))
+        b = self.stem.conv.bias
+        key = (w.data_ptr(), w._version, b.data_ptr(), b._version, tuple(mean), tuple(std))
         if getattr(self, "_u8_key", None) != key:
             self._u8_ops = K.pack_stem_u8(w, self.stem.conv.bias, mean, std)
             self._u8_key = key

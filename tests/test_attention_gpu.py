@@ -166,13 +166,16 @@ def test_attention_f16x3_strided_qkv_views():
 
 @torch.no_grad()
 @pytest.mark.parametrize("shape", [(3, 2, 100, 90), (4, 2, 302, 90)])  # 1 / 2 query parts per head
-@pytest.mark.parametrize("case", ["huge_q", "huge_k", "huge_v", "tiny_v_dim", "tiny_all", "zero_v_dim"])
+@pytest.mark.parametrize("case", ["huge_q", "huge_k", "huge_v", "tiny_v_dim", "tiny_all", "zero_v_dim", "tiny_q",
+                                  "tiny_k"])
 def test_attention_f16x3_range_and_block_independence(case, shape):
-    """Out-of-f16-range inputs in ONE batch item (|q|, |k| or |v| >= 2^15, a head dimension of V
-    whose max is below 2^-6, everything scaled by 1e-6) re-run that item's blocks on the bf16x6
+    """Out-of-f16-range inputs in ONE batch item (|k| or |v| >= 2^15, a max |k| or a head dimension
+    of V whose max is below 2^-6, everything scaled by 1e-6) re-run that item's blocks on the bf16x6
     kernel: the result stays within f32 accuracy of f64 relative to each item's own output scale, the
     re-run blocks equal the bf16x6 kernel bit for bit, and the other items are bit-identical to a run
-    without the odd item."""
+    without the odd item.  Queries of any magnitude stay on the f16x3 kernel (each query is scaled by
+    a power of two before the split): tiny queries against large keys (S of order 1, so the
+    softmax sees the queries' low bits) keep f32 accuracy without a re-run."""
     from robomanipbaselines_amd import kernels as K
 
     g = torch.Generator(device=DEV).manual_seed(7)
@@ -198,6 +201,12 @@ def test_attention_f16x3_range_and_block_independence(case, shape):
         v[1] *= 1e-6
     elif case == "zero_v_dim":
         v[1, :, 3] = 0.0
+    elif case == "tiny_q":  # every |q| < 2^-3: an unscaled low piece would be subnormal
+        q[1] *= 1e-3
+        k[1] *= 100.0
+    elif case == "tiny_k":  # |k| ~ 1e-6 against large queries: re-run (kh would be subnormal)
+        k[1] *= 1e-6
+        q[1] *= 1e5
     got = K.attention_f32(q, k, v, H, form="f16x3")
     x6 = K.attention_f32(q, k, v, H, form="x6")
     want = _ref64(q, k, v, H)
@@ -209,8 +218,10 @@ def test_attention_f16x3_range_and_block_independence(case, shape):
     for b in range(B):
         if b != 1:
             assert torch.equal(got[b], base[b])
-    if case in ("huge_q", "tiny_all"):
-        assert torch.equal(got[1], x6[1]), case  # every block of item 1 re-ran on bf16x6
+    if case in ("huge_q", "tiny_all", "tiny_k"):
+        assert torch.equal(got[1], x6[1]), case  # every block of item 1 re-ran on bf16x6 (tiny |k|)
+    if case == "tiny_q":  # no re-run: item 1 is the f16x3 kernel's own result
+        assert not torch.equal(got[1], x6[1])
     if case in ("huge_k", "tiny_v_dim"):  # head 0 re-ran, head 1 kept its f16x3 result
         assert torch.equal(got[1, :, :64], x6[1, :, :64])
         assert torch.equal(got[1, :, 64:], base[1, :, 64:])

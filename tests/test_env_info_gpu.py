@@ -11,6 +11,7 @@ on tactile scenes; reference-style plugins read them as RolloutBase.get_images d
 * frames are rendered once per camera and env-step, on first access, and a stale info refuses;
 * DP3's depth and DP's rgb come through info."""
 
+import numpy as np
 import pytest
 import torch
 
@@ -97,6 +98,11 @@ def test_info_frames_are_rendered_once_per_step_and_go_stale():
         ro.info["rgb_images"]["no_such_camera"]
     ro.info["depth_images"][cam]
     assert calls == [cam, cam]
+    # modify_world changes the scene: the step's info frames go stale rather than show the new world
+    info1 = ro.info
+    env.modify_world(world_idx=np.array([1, 2]))
+    with pytest.raises(RuntimeError):
+        info1["rgb_images"][cam]
 
 
 @torch.no_grad()
