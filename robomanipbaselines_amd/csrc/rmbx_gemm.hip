@@ -205,6 +205,14 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
   constexpr int NJ = BN / 32;             // 16-column accumulator tiles per wave (wave = 64 x BN / 2)
   constexpr int WP = PC * BN / 128;       // W DMA pieces (16 rows x 64 B) per wave and K step
   constexpr int PPP = BN / 16;            // pieces per W plane
+  // Memory operations issued per K step, the counts every hand-written vmcnt below is derived from
+  // (the A loads and the W LDS-DMA are inline asm, invisible to hipcc's own wait insertion): stage_b
+  // issues W_OPS LDS-DMAs (one glds16 per W piece it owns), load_a issues A_OPS 16-byte loads (two
+  // per staged row, two rows).  Both loops below run exactly to these bounds on every path (linear
+  // and conv, BN 64 / 128 / 256, both range passes, the K tail, whose redundant copies keep the count
+  // fixed), so a wait computed from them cannot drift from what was issued.
+  constexpr int W_OPS = WP, A_OPS = 4, A_ROWS = 2;
+  static_assert(A_OPS == 2 * A_ROWS, "two 16-byte loads (8 f32 of one k quarter) per staged row");
   // LDS stages: 2; VAR bit 10 (f16x3, profiling) = 3 stages, the W DMA of step kt + 2 issued at step
   // kt and left in flight across the barrier -- measured 1.02-1.08x slower than 2 stages
   // (profiles/r4_gemm_f16x3_phase_skips.log)
@@ -261,7 +269,7 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
     }
     unsigned char* base = smem + buf * STAGE + A_BYTES;
 #pragma unroll
-    for (int t = 0; t < WP; ++t) glds16(bsrc[t] + kt * GM_BK, base + (wave * WP + t) * 1024);
+    for (int t = 0; t < W_OPS; ++t) glds16(bsrc[t] + kt * GM_BK, base + (wave * WP + t) * 1024);
   };
   // convolution: each staged row's window origin (iy0, ix0) and its element offset in the input;
   // a K step of 32 lies inside one filter tap (C % 32 == 0), so a row's 8 channels are one
@@ -287,12 +295,9 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
       if (kt > 1) return 3;
     }
     if constexpr (!CONV) {
-      const float4* p0 = (const float4*)(ag0 + kt * GM_BK);
-      const float4* p1 = (const float4*)(ag1 + kt * GM_BK);
-      gload16(R[0], p0);
-      gload16(R[1], p0 + 1);
-      gload16(R[2], p1);
-      gload16(R[3], p1 + 1);
+      const float4* p[A_ROWS] = {(const float4*)(ag0 + kt * GM_BK), (const float4*)(ag1 + kt * GM_BK)};
+#pragma unroll
+      for (int j = 0; j < A_OPS; ++j) gload16(R[j], p[j >> 1] + (j & 1));
       return 3;
     } else {
       const int k0 = kt * GM_BK;
@@ -300,11 +305,11 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
       const int ky = tap / g.kw, kx = tap - ky * g.kw;
       int ok = 0;
 #pragma unroll
-      for (int r2 = 0; r2 < 2; ++r2) {
+      for (int r2 = 0; r2 < A_ROWS; ++r2) {
         const bool v = (unsigned)(cy[r2] + ky) < (unsigned)g.ih && (unsigned)(cx[r2] + kx) < (unsigned)g.iw;
         const float4* p = (const float4*)(g.A + (v ? cbase[r2] + (long long)(ky * g.iw + kx) * g.ic + c0 : 0));
-        gload16(R[2 * r2], p);
-        gload16(R[2 * r2 + 1], p + 1);
+#pragma unroll
+        for (int j = 0; j < A_OPS / A_ROWS; ++j) gload16(R[(A_OPS / A_ROWS) * r2 + j], p + j);
         ok |= (int)v << r2;
       }
       return ok;
@@ -445,10 +450,25 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f32x6_kernel(GemmArgs g) {
   // with vmcnt(4) (2 stages: it was issued this step) or vmcnt(WP + 4) (3 stages: issued the step
   // before, so this step's DMA stays in flight across the barrier).
   const int KT = g.K / GM_BK;
-  // (the phase-skip variants issue fewer memory operations than the counts assume: they wait for
-  // everything instead, so no register is read or reused before its load has landed)
+  // The waits, from the per-step counts (vmcnt retires in issue order):
+  //   SPLIT_WAIT: A of kt + 1 was loaded during the step before; issued after it are this step's W
+  //     DMA and A loads, so <= W_OPS + A_OPS outstanding means it has landed (prologue likewise:
+  //     Ra, then the stage-0 / stage-1 DMA and Rb);
+  //   END_WAIT: the DMA of stage kt + 1 -- issued this step (2 stages: only this step's A loads
+  //     follow it) or the step before (3 stages: this step's DMA and A loads follow it).
+  // Round-4 fault (HSA_STATUS_ERROR_MEMORY_APERTURE_VIOLATION in gemm_f32x6_kernel<false, 528, 2,
+  // 128>, gpurun_out/r4_l_gemm_phases.log): the VAR & 512 phase skip issues no W DMA after the first
+  // stage, i.e. 4 operations per step where the literal waits assumed 6, so vmcnt(6) let the last two
+  // A loads of Rcur still be in flight when store_a consumed Rcur; hipcc, which sees the asm outputs
+  // as written at issue and Rcur dead after store_a, re-allocated those VGPRs -- to 64-bit load
+  // addresses among others -- and the late data landing in them turned the next loads' addresses
+  // out of range.  The phase-skip variants issue a varying count, so they wait for everything.
   constexpr bool SKIPS = (VAR & (256 | 512)) != 0;
-  constexpr int LEAD = NS - 1, END_WAIT = SKIPS ? 0 : (NS == 3 ? WP + 4 : 4), SPLIT_WAIT = SKIPS ? 0 : WP + 4;
+  constexpr int LEAD = NS - 1;
+  constexpr int SPLIT_WAIT = SKIPS ? 0 : W_OPS + A_OPS;
+  constexpr int END_WAIT = SKIPS ? 0 : (NS == 3 ? W_OPS + A_OPS : A_OPS);
+  static_assert(SPLIT_WAIT <= 63 && END_WAIT <= 63, "vmcnt holds 6 bits on gfx950");
+  static_assert(SKIPS || (END_WAIT < SPLIT_WAIT || NS == 3), "a stage's DMA is retired after the A split");
   auto stage_of = [](int k) { return NS == 2 ? (k & 1) : k % 3; };
   auto k_loop = [&](auto scaled) {
     float4 Ra[4], Rb[4];
@@ -689,6 +709,7 @@ __global__ void __launch_bounds__(GP_THREADS, 1) gemm_f16x3_pc_kernel(GemmArgs g
   constexpr int STAGE = gm_stage<2, BN>(), A_BYTES = 2 * GM_A_PLANE, B_PLANE = gm_b_plane<BN>();
   constexpr int SMEM = gm_smem<2, BN, NS>();
   constexpr int WPP = 4;  // W DMA pieces per producer wave and K step (16 per stage)
+  constexpr int PA_OPS = 8;  // 16-byte A loads per producer thread and K step (load_a: 4 rows x 2)
   __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const bool producer = wave >= 8;
@@ -775,13 +796,14 @@ __global__ void __launch_bounds__(GP_THREADS, 1) gemm_f16x3_pc_kernel(GemmArgs g
       return ok;
     }
   };
-  auto wait_regs8 = [&](float4 (&R)[8]) {  // vmcnt(WPP + 8): this step's DMA and loads stay in flight
+  static_assert(WPP + PA_OPS <= 63, "vmcnt holds 6 bits on gfx950");
+  auto wait_regs8 = [&](float4 (&R)[8]) {  // vmcnt(WPP + PA_OPS): this step's DMA and loads stay in flight
     f32x4v v[8];
 #pragma unroll
     for (int i = 0; i < 8; ++i) v[i] = __builtin_bit_cast(f32x4v, R[i]);
     asm volatile("s_waitcnt vmcnt(%8)"
                  : "+v"(v[0]), "+v"(v[1]), "+v"(v[2]), "+v"(v[3]), "+v"(v[4]), "+v"(v[5]), "+v"(v[6]), "+v"(v[7])
-                 : "n"(WPP + 8)
+                 : "n"(WPP + PA_OPS)
                  : "memory");
 #pragma unroll
     for (int i = 0; i < 8; ++i) R[i] = __builtin_bit_cast(float4, v[i]);
