@@ -31,7 +31,7 @@ extern "C" {
 #define RMBX_ERR_HIP -2   /* HIP runtime failure (maps to Python RuntimeError) */
 #define RMBX_ERR_STATE -3 /* engine used in a wrong state */
 
-#define RMBX_ABI_VERSION 1
+#define RMBX_ABI_VERSION 2
 
 /* ---------------------------------------------------------------------------------------------
  * Library
@@ -319,6 +319,37 @@ int rmbx_render(const rmbx_camera* cam, const int32_t* prim_i32, const float* pr
                 const double* xquat, int ngeom, int nbody, uint8_t* rgb, float* depth,
                 void* policy_img, int policy_dtype, const uint8_t* active, int n_env,
                 void* stream);
+
+/* The scene with its visual meshes (the reference renders every class="visual" mesh geom,
+ * envs/mujoco/MujocoEnvBase.py:103-126, through MuJoCo's OpenGL viewer).  Device tables:
+ * prim_i32 [nprim][4] = (geom id, type, -, -) and prim_f32 [nprim][8] = (size3, rgb3, -, -) as for
+ * rmbx_render (the analytic primitives); mesh_tri f32 [ntri][16] = the visual meshes' triangles in
+ * their body frames, (v0, e1 = v1 - v0, e2 = v2 - v0, unit face normal, tag = (mesh slot << 16) |
+ * geom id as int32 bits, rgb), mjcf/rmesh.py builds them; per mesh slot (a body with visual
+ * meshes) mesh_body [nmesh] its body id and mesh_rad [nmesh] its triangles' bounding radius about
+ * the body origin.  vis: caller-provided device workspace u64 [n_env][H][W] (16-byte aligned),
+ * cleared and filled on the stream with each pixel's nearest triangle (depth bits << 32 | index);
+ * big: caller-provided device workspace u64 [1 + 2^20] (a queue of triangles whose projection
+ * spans many pixels, covered by a whole workgroup each);
+ * triangle hits nearer than cam->znear are clipped (OpenGL's near plane).  hit_geom (optional)
+ * [n][H][W] receives the geom id of each pixel's surface, -1 for the background; the other
+ * arguments and outputs are rmbx_render's.  rmbx_render is this call without meshes. */
+typedef struct rmbx_scene_tables {
+  const int32_t* prim_i32;
+  const float* prim_f32;
+  int32_t nprim;
+  int32_t ntri, nmesh;
+  const float* mesh_tri;
+  const int32_t* mesh_body;
+  const float* mesh_rad;
+  unsigned long long* vis;
+  unsigned long long* big;
+} rmbx_scene_tables;
+
+int rmbx_render_scene(const rmbx_camera* cam, const rmbx_scene_tables* scene, const double* gxpos,
+                      const double* gxmat, const double* xpos, const double* xquat, int ngeom,
+                      int nbody, uint8_t* rgb, float* depth, int32_t* hit_geom, void* policy_img,
+                      int policy_dtype, const uint8_t* active, int n_env, void* stream);
 
 /* ---------------------------------------------------------------------------------------------
  * Policy vision-trunk epilogues (ResNet-18 with frozen BN folded into the convs), NHWC.

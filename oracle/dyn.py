@@ -32,6 +32,8 @@ def _load(flops=False):
         lib.orc_set_body_pos.argtypes = [vp, ip, vp]
         lib.orc_get_xpos.argtypes = [vp, vp, vp]
         lib.orc_get_efc.argtypes = [vp, vp, vp]
+        lib.orc_get_efc_force.argtypes = [vp, vp]
+        lib.orc_get_solver_trace.argtypes = [vp, vp, vp, vp]
         lib.orc_get_geom.argtypes = [vp, vp, vp]
         lib.orc_get_sensor.argtypes = [vp, vp]
         lib.orc_get_M.argtypes = [vp, vp]
@@ -139,6 +141,22 @@ class OracleEnv:
         if n:
             self.lib.orc_get_efc(self.h, J.ctypes.data, D.ctypes.data)
         return J, D
+
+    def efc_force(self):
+        """Constraint forces [nefc] of the last forward / step (zero on inactive rows)."""
+        f = np.zeros(self.nefc())
+        if len(f):
+            self.lib.orc_get_efc_force(self.h, f.ctypes.data)
+        return f
+
+    def solver_trace(self):
+        """(scaled gradient norms, scaled cost improvements, kink distances) per Newton iteration
+        of the last solve, up to the stopping one (MuJoCo's two tolerance tests); the kink
+        distance is min |jar| / max |jar| over the inequality rows at the iteration's start."""
+        g, i, k = np.zeros(128), np.zeros(128), np.zeros(128)
+        self.lib.orc_get_solver_trace(self.h, g.ctypes.data, i.ctypes.data, k.ctypes.data)
+        n = int(np.sum(g >= 0))
+        return g[:n], i[: int(np.sum(i >= 0))], k[:n]
 
     def solver_iter(self):
         return self.lib.orc_solver_iter(self.h)

@@ -57,6 +57,7 @@ typedef struct {
   int* efc_type; /* 0 equality, 1 inequality */
   double sensordata[6];
   int solver_iter;
+  double trace_grad[128], trace_impr[128], trace_kink[128];  /* per Newton iteration: scaled |grad| and improvement (-1: not reached) */
   int bad;     /* substep of the last divergence reset (orc_step) */
   int substep; /* 1-based substep being integrated */
 } Data;
@@ -906,8 +907,12 @@ static int col_box_box(const double* ca, const double* Ra, const double* ha, con
     }
     for (int k = 0; k < 3; k++) {
       double ua[3] = {Ra[k], Ra[3 + k], Ra[6 + k]}, ub[3] = {Rb[k], Rb[3 + k], Rb[6 + k]};
-      double sa2 = dot3(ua, n) >= 0 ? ha[k] : -ha[k];
-      double sb2 = dot3(ub, neg) >= 0 ? hb[k] : -hb[k];
+      /* the extent's end facing the other box, or its centre when the axis is perpendicular to n
+         within 1e-9 (a parallel face / edge: every point along it supports; a ~1e-17 dot product
+         would otherwise pick an end by rounding) */
+      const double da = dot3(ua, n), db = dot3(ub, neg);
+      double sa2 = fabs(da) < 1e-9 ? 0.0 : (da > 0 ? ha[k] : -ha[k]);
+      double sb2 = fabs(db) < 1e-9 ? 0.0 : (db > 0 ? hb[k] : -hb[k]);
       for (int i = 0; i < 3; i++) {
         pa[i] += ua[i] * sa2;
         pb[i] += ub[i] * sb2;
@@ -1827,6 +1832,7 @@ static void solve(Data* d) {
   }
   double scale = 1.0 / (m->meaninertia * (nv > 1 ? nv : 1));
   int it;
+  for (int k = 0; k < 128; k++) d->trace_grad[k] = d->trace_impr[k] = d->trace_kink[k] = -1.0;
   for (it = 0; it < m->solver_iterations; it++) {
     /* gradient: M (a - a0) - J^T f, f = -D jar on active rows (res/tmpv2 set by eval_cost) */
     for (int k = 0; k < nv; k++) d->grad[k] = d->tmpv2[k];
@@ -1840,6 +1846,18 @@ static void solve(Data* d) {
     }
     double gn = 0;
     for (int k = 0; k < nv; k++) gn += d->grad[k] * d->grad[k];
+    if (it < 128) {
+      d->trace_grad[it] = scale * sqrt(gn);
+      /* nearest inequality row to its kink (jar = 0), relative to the largest |jar|: an exact line
+         search often stops at a kink, where the row's side is decided by rounding */
+      double mn = 1e300, mx = 0;
+      for (int r = d->ne; r < nefc; r++) {
+        const double x = fabs(d->efc_jar[r]);
+        if (x > 0) mn = x < mn ? x : mn;  /* (an exact 0 is no rounding question) */
+        mx = x > mx ? x : mx;
+      }
+      d->trace_kink[it] = mx > 0 ? mn / mx : 1.0;
+    }
     if (scale * sqrt(gn) < m->solver_tolerance) break;
     /* Hessian H = M + J^T D_active J */
     memcpy(d->H, d->M, sizeof(double) * nv * nv);
@@ -1917,6 +1935,7 @@ static void solve(Data* d) {
       if (d->efc_type[r] == 0 || jar < 0) newcost += 0.5 * d->efc_D[r] * jar * jar;
     }
     double improvement = scale * (cost - newcost);
+    if (it < 128) d->trace_impr[it] = improvement;
     cost = newcost;
     if (improvement < m->solver_tolerance) {
       it++;
@@ -2138,9 +2157,23 @@ void orc_get_efc(void* p, double* J, double* D) {
   if (J) memcpy(J, d->J, sizeof(double) * (size_t)d->nefc * d->m->nv);
   if (D) memcpy(D, d->efc_D, sizeof(double) * (size_t)d->nefc);
 }
+/* constraint forces of the last forward / step (row order as orc_get_efc): the active set is the
+   rows with a nonzero force */
+void orc_get_efc_force(void* p, double* force) {
+  Data* d = (Data*)p;
+  memcpy(force, d->efc_force, sizeof(double) * (size_t)d->nefc);
+}
 int orc_ncon(void* p) { return ((Data*)p)->ncon; }
 int orc_nefc(void* p) { return ((Data*)p)->nefc; }
 int orc_solver_iter(void* p) { return ((Data*)p)->solver_iter; }
+/* the last solve's per-iteration stopping quantities (scaled gradient norm, scaled cost
+   improvement; -1 where the iteration did not reach that test), 128 entries each */
+void orc_get_solver_trace(void* p, double* grad, double* impr, double* kink) {
+  Data* d = (Data*)p;
+  memcpy(grad, d->trace_grad, sizeof(d->trace_grad));
+  memcpy(impr, d->trace_impr, sizeof(d->trace_impr));
+  if (kink) memcpy(kink, d->trace_kink, sizeof(d->trace_kink));
+}
 void orc_get_contacts(void* p, double* pos, double* frame, double* dist, int* pair) {
   Data* d = (Data*)p;
   int n = d->ncon;

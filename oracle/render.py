@@ -1,0 +1,136 @@
+"""ORACLE -- test infrastructure only.  ctypes wrapper of oracle/render_oracle.c: a brute-force f64
+ray caster restating the batched renderer (csrc/rmbx_render.hip) that replaces the camera renders of
+envs/mujoco/MujocoEnvBase.py:103-126.  Build with `make -C oracle`.
+
+The drawn geoms are selected here from the compiled scene arrays by the renderer's documented
+rules, restated (not imported from the product): MuJoCo's default visible groups 0-2; plane,
+sphere, capsule, cylinder and box geoms as they are in their geom frames; the visual mesh geoms as
+their render triangles (robomanipbaselines_amd/mjcf/rmesh.py stores each body's meshes in the
+body frame at the documented 1 mm level of detail, every triangle with its geom id and colour); a mesh geom whose file is missing from the
+checkout as its bounding box.  The camera pose is MuJoCo's: body frame x camera offset
+(mj_kinematics' cam_xpos / cam_xmat), looking along the camera's -z.
+"""
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_DIR = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_DIR, "_build", "librmbx_render_oracle.so")
+_lib = None
+
+
+class _Prim(ctypes.Structure):
+    _fields_ = [("geom", ctypes.c_int32), ("type", ctypes.c_int32), ("tri0", ctypes.c_int32), ("ntri", ctypes.c_int32),
+                ("size", ctypes.c_double * 3), ("rgb", ctypes.c_double * 3), ("pos", ctypes.c_double * 3),
+                ("R", ctypes.c_double * 9)]
+
+
+def _load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB):
+            subprocess.run(["make", "-C", _DIR], check=True, capture_output=True)
+        _lib = ctypes.CDLL(_LIB)
+        vp, ip, dp = ctypes.c_void_p, ctypes.c_int, ctypes.c_double
+        _lib.orc_render_rays.argtypes = [vp, ip, vp, vp, vp, dp, ip, ip, dp, vp, ip, vp, vp, vp, vp]
+    return _lib
+
+
+def _quat2mat(q):
+    w, x, y, z = q
+    return np.array([[1 - 2 * (y * y + z * z), 2 * (x * y - w * z), 2 * (x * z + w * y)],
+                     [2 * (x * y + w * z), 1 - 2 * (x * x + z * z), 2 * (y * z - w * x)],
+                     [2 * (x * z - w * y), 2 * (y * z + w * x), 1 - 2 * (x * x + y * y)]])
+
+
+def scene_prims(arrays):
+    """The drawn surfaces: [("geom", g, prim) | ("body", b, prim)] (see the module docstring);
+    frames are filled per env by cast()."""
+    gt, gg = arrays["geom_type"], arrays["geom_group"]
+    ct, cs, size, rgba = arrays["geom_ctype"], arrays["geom_csize"], arrays["geom_size"], arrays["geom_rgba"]
+    meshed = set(int(g) for g in arrays.get("rmesh_geoms", []))
+    out = []
+    for g in range(len(gt)):
+        if gg[g] > 2 or int(g) in meshed:
+            continue
+        t = int(gt[g])
+        p = _Prim()
+        p.geom = g
+        for i in range(3):
+            p.rgb[i] = float(rgba[g][i])
+        if t in (0, 2, 3, 5, 6):
+            p.type = t
+            for i in range(3):
+                p.size[i] = float(size[g][i])
+        elif t == 7 and ct[g] < 0 and np.any(cs[g][:3] > 0):
+            p.type = 6  # mesh file missing from the checkout: its bounding box
+            for i in range(3):
+                p.size[i] = float(cs[g][i])
+        else:
+            continue
+        out.append(("geom", g, p))
+    if "rmesh_body" in arrays:
+        tri = arrays["rmesh_tri"]
+        for k, b in enumerate(arrays["rmesh_body"]):
+            a, n = int(arrays["rmesh_tri_adr"][k]), int(arrays["rmesh_tri_num"][k])
+            tr = tri[a: a + n].astype(np.float64)
+            verts = np.concatenate([tr[:, 0:3], tr[:, 0:3] + tr[:, 3:6], tr[:, 0:3] + tr[:, 6:9]])
+            p = _Prim()
+            p.geom, p.type, p.tri0, p.ntri = -1, 7, a, n
+            p.size[0] = float(np.linalg.norm(verts, axis=1).max()) * (1 + 1e-9)  # bounding sphere
+            out.append(("body", int(b), p))
+    return out
+
+
+def camera_pose(arrays, cam_name, xpos, xquat):
+    """(R [3, 3] with columns = camera axes in world, p [3]) of a scene camera for one env."""
+    names = [str(x) for x in arrays["names_cam"]]
+    i = names.index(cam_name)
+    b = int(arrays["cam_body"][i])
+    Rb = _quat2mat(np.asarray(xquat[b], np.float64))
+    R = Rb @ _quat2mat(np.asarray(arrays["cam_quat"][i], np.float64))
+    p = np.asarray(xpos[b], np.float64) + Rb @ np.asarray(arrays["cam_pos"][i], np.float64)
+    return R, p
+
+
+def cast(arrays, prims, gxpos, gxmat, xpos, xquat, cam_name, width, height, pix, second=False):
+    """Rays of one env through the continuous pixel coordinates pix [n, 2] (x, y; centres at +0.5):
+    (geom id [n] (-1: background), camera depth [n], shaded colour [n, 3] in [0, 1]); with
+    second=True also the depth of the nearest hit of any other geom [n] (inf if none)."""
+    lib = _load()
+    gm_all = np.asarray(gxmat, np.float64).reshape(-1, 9)
+    plist = []
+    for kind, idx, pr in prims:
+        if kind == "geom":
+            pos, Rm = np.asarray(gxpos[idx], np.float64), gm_all[idx]
+        else:
+            pos, Rm = np.asarray(xpos[idx], np.float64), _quat2mat(np.asarray(xquat[idx], np.float64)).reshape(-1)
+        for i in range(3):
+            pr.pos[i] = float(pos[i])
+        for i in range(9):
+            pr.R[i] = float(Rm[i])
+        plist.append(pr)
+    R, p = camera_pose(arrays, cam_name, xpos, xquat)
+    i = [str(x) for x in arrays["names_cam"]].index(cam_name)
+    znear = float(arrays["_znear"]) * float(arrays["_extent"])
+    parr = (_Prim * len(plist))(*plist)
+    pix = np.ascontiguousarray(pix, np.float64)
+    n = len(pix)
+    geom, depth, rgb, depth2 = np.zeros(n, np.int32), np.zeros(n), np.zeros((n, 3)), np.zeros(n)
+    tri = np.ascontiguousarray(arrays["rmesh_tri"] if "rmesh_tri" in arrays else np.zeros((1, 16), np.float32),
+                               np.float32)
+    Rf = np.ascontiguousarray(R.reshape(-1))
+    lib.orc_render_rays(ctypes.cast(parr, ctypes.c_void_p), len(plist), tri.ctypes.data, Rf.ctypes.data, p.ctypes.data,
+                        float(arrays["cam_fovy"][i]), int(width), int(height), znear, pix.ctypes.data, n,
+                        geom.ctypes.data, depth.ctypes.data, rgb.ctypes.data, depth2.ctypes.data)
+    if second:
+        return geom, depth, rgb, np.where(depth2 >= 1e300, np.inf, depth2)
+    return geom, depth, rgb
+
+
+def to_u8(rgb):
+    """The renderer's 8-bit rounding of a shaded colour: (uint8)(c * 255 + 0.5)."""
+    return np.floor(np.asarray(rgb) * 255.0 + 0.5).astype(np.uint8)

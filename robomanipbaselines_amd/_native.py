@@ -56,6 +56,8 @@ SIGNATURES = {
                             + [_c_int, _c_p]),
     "rmbx_render": (_c_int, [_c_p, _c_p, _c_p, _c_int, _c_p, _c_p, _c_p, _c_p, _c_int, _c_int, _c_p, _c_p, _c_p,
                              _c_int, _c_p, _c_int, _c_p]),
+    "rmbx_render_scene": (_c_int, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_int, _c_int, _c_p, _c_p, _c_p, _c_p,
+                                   _c_int, _c_p, _c_int, _c_p]),
     "rmbx_nhwc_bias_act": (_c_int, [_c_p] * 5 + [_c_sz, _c_int, _c_int, _c_int, _c_p]),
     "rmbx_nhwc_bias_relu_maxpool": (_c_int, [_c_p] * 3 + [_c_int] * 5 + [_c_p]),
     "rmbx_conv2d_nhwc": (_c_int, [_c_p] * 5 + [_c_int] * 10 + [_c_p]),
@@ -108,6 +110,14 @@ class Camera(ctypes.Structure):
                 ("fovy_deg", ctypes.c_float), ("pos", ctypes.c_double * 3), ("quat", ctypes.c_double * 4),
                 ("znear", ctypes.c_float), ("zfar", ctypes.c_float), ("mean", ctypes.c_float * 3),
                 ("std", ctypes.c_float * 3)]
+
+
+class SceneTables(ctypes.Structure):
+    """ctypes mirror of rmbx_scene_tables (include/rmbx.h)."""
+
+    _fields_ = [("prim_i32", _c_p), ("prim_f32", _c_p), ("nprim", ctypes.c_int32), ("ntri", ctypes.c_int32),
+                ("nmesh", ctypes.c_int32), ("mesh_tri", _c_p), ("mesh_body", _c_p), ("mesh_rad", _c_p), ("vis", _c_p),
+                ("big", _c_p)]
 
 
 class EnvBuffers(ctypes.Structure):

@@ -900,8 +900,14 @@ __device__ int col_box_box(const double* ca, const double* Ra, const double* ha,
     }
     for (int k = 0; k < 3; k++) {
       const double ua[3] = {Ra[k], Ra[3 + k], Ra[6 + k]}, ub[3] = {Rb[k], Rb[3 + k], Rb[6 + k]};
-      const double sa2 = dot3(ua, n) >= 0 ? ha[k] : -ha[k];
-      const double sb2 = dot3(ub, neg) >= 0 ? hb[k] : -hb[k];
+      // support coordinate along each box axis: the extent's end facing the other box, or its
+      // centre when the axis is perpendicular to n within 1e-9 (a face or edge parallel to the
+      // contact plane: every point along it is a support point, and the sign of a ~1e-17 dot
+      // product would pick an end by rounding -- the engine and the oracle then put the contact
+      // a half extent apart)
+      const double da = dot3(ua, n), db = dot3(ub, neg);
+      const double sa2 = fabs(da) < 1e-9 ? 0.0 : (da > 0 ? ha[k] : -ha[k]);
+      const double sb2 = fabs(db) < 1e-9 ? 0.0 : (db > 0 ? hb[k] : -hb[k]);
       for (int i = 0; i < 3; i++) {
         pa[i] += ua[i] * sa2;
         pb[i] += ub[i] * sb2;

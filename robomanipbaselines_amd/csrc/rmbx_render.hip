@@ -1,14 +1,26 @@
-// Batched camera rendering by ray casting scene primitives (gfx950).
+// Batched camera rendering of the scene primitives and the visual meshes (gfx950).
 //
 // Replaces the per-env, per-camera OpenGL OffScreenViewer rgb + depth renders of
-// envs/mujoco/MujocoEnvBase.py:112-126.  One 256-thread workgroup renders a 16x16 pixel tile of
-// one env: the workgroup transforms that env's primitives into the camera frame into LDS,
-// culls them against the tile's view frustum slice (projected bounding spheres), and every lane
-// casts its pixel's ray against the surviving list.  Shading: ambient + headlight + one
-// directional light (the scene's <light> and MuJoCo's default headlight), material colour only
-// (textures are not sampled).  Outputs are written once per pixel: u8 HWC RGB, f32 linear
-// depth, and/or the policy input tensor (CHW, ImageNet-normalised, bf16 or f32) fused so the
-// policy never re-reads the u8 image.
+// envs/mujoco/MujocoEnvBase.py:112-126.  Two passes per camera:
+//   1. visibility of the visual meshes (the UR5e / Robotiq / D435i `class="visual"` geoms,
+//      mjcf/rmesh.py): one thread per (env, triangle) transforms the triangle into the camera frame
+//      (its body's pose, one transform per env and body in LDS), finds the pixel centres its
+//      projection covers (clipped at the camera's znear, as OpenGL's near plane), intersects each of
+//      those pixels' camera rays with it (the same ray-triangle test as a ray caster, so depth and
+//      coverage are the ray's) and keeps the nearest per pixel with a 64-bit atomic min of
+//      (depth bits, triangle) in a caller-provided visibility buffer.  Meshes are many small
+//      triangles: projecting each triangle once costs far less than tracing each pixel's ray
+//      through a hierarchy of them;
+//   2. one 256-thread workgroup per 16x16 pixel tile of one env ray-casts the analytic primitives:
+//      the env's primitives in the camera frame in LDS, culled against the tile's frustum slice
+//      (bounding spheres and projected boxes), sorted front to back by a depth bound; every lane
+//      starts from its pixel's mesh hit and casts its ray against the surviving primitives, stopping
+//      at the first whose bound lies behind its nearest hit.
+// Shading: ambient + headlight + one directional light (the scene's <light> and MuJoCo's default
+// headlight), material colour only, flat-shaded triangles (textures are not sampled).  Outputs are
+// written once per pixel: u8 HWC RGB, f32 linear depth, the hit geom id, and/or the policy input
+// tensor (CHW, ImageNet-normalised, bf16 or f32, or the space-to-depth forms) fused so the policy
+// never re-reads the u8 image.
 
 #include <hip/hip_bf16.h>
 
@@ -22,6 +34,8 @@ namespace rmbx {
 
 #define RENDER_TILE 16
 #define MAX_PRIM 128
+#define MAX_MESH 64  // bodies with render meshes
+#define VIS_EMPTY 0xffffffffffffffffull
 
 struct PrimCam {
   float c[3];    // centre in camera frame
@@ -32,6 +46,8 @@ struct PrimCam {
   float rad;   // bounding radius (0 = unbounded)
   float zmin;  // lower bound of any hit's depth (camera z) in the image; -1e30 if unbounded
   float ol[3];  // the camera (ray origin) in the primitive's local frame: R^T (0 - c)
+  float sx_lo, sx_hi, sy_lo, sy_hi;  // image-plane slopes (x / -z, y / -z) bounding the primitive's
+                                     // box (projected corners; unbounded when a corner is not in front)
 };
 
 __device__ __forceinline__ float dot3f(const float* a, const float* b) {
@@ -190,6 +206,13 @@ struct RenderArgs {
   const int32_t* prim_i32;
   const float* prim_f32;
   int nprim;
+  const float* mesh_tri;      // [ntri][16]: v0, e1, e2, n, tag = (mesh slot << 16) | geom (int bits), rgb
+  int ntri, nmesh;
+  const int32_t* mesh_body;   // [nmesh] body of each mesh slot
+  const float* mesh_rad;      // [nmesh] bounding radius of the slot's triangles about the body origin
+  unsigned long long* vis;    // [n][H][W] nearest mesh hit (depth bits << 32 | triangle), VIS_EMPTY: none
+  unsigned long long* big;    // [1 + BIG_CAP]: count, then queued (env << 32 | triangle) entries
+  int32_t* hit_geom;          // optional [n][H][W]: geom id of the pixel's surface (-1: background)
   const double* gxpos;
   const double* gxmat;
   const double* xpos;
@@ -206,6 +229,211 @@ struct RenderArgs {
   int dbg;     // diagnostic (RMBX_RENDER_DBG; 0 in production): 1 no ray loop, 2 no stores, 4 test counts, 8 sphere bounds only
 };
 
+// camera pose of env `env` in world: R (columns = camera axes), p
+__device__ __forceinline__ void camera_frame(const RenderArgs& a, int env, CamFrame& cf) {
+  double Rb[9], Rc[9], R[9], t[3];
+  const double* bq = a.xquat + ((size_t)env * a.nbody + a.cam.body) * 4;
+  const double* bp = a.xpos + ((size_t)env * a.nbody + a.cam.body) * 3;
+  quat2mat(bq, Rb);
+  quat2mat(a.cam.quat, Rc);
+  matmul3(Rb, Rc, R);
+  matvec3(Rb, a.cam.pos, t);
+  for (int i = 0; i < 9; i++) cf.R[i] = (float)R[i];
+  for (int i = 0; i < 3; i++) cf.p[i] = (float)(bp[i] + t[i]);
+}
+
+// a mesh slot's body frame in the camera frame: R = Rcam^T Rbody (row-major), c = Rcam^T (x - pcam)
+__device__ __forceinline__ void mesh_frame(const RenderArgs& a, int env, int k, const CamFrame& cf, float* R,
+                                           float* c) {
+  const int b = a.mesh_body[k];
+  double Rb[9];
+  quat2mat(a.xquat + ((size_t)env * a.nbody + b) * 4, Rb);
+  const double* bp = a.xpos + ((size_t)env * a.nbody + b) * 3;
+  const float dw[3] = {(float)bp[0] - cf.p[0], (float)bp[1] - cf.p[1], (float)bp[2] - cf.p[2]};
+  for (int i = 0; i < 3; i++) {
+    c[i] = cf.R[i] * dw[0] + cf.R[3 + i] * dw[1] + cf.R[6 + i] * dw[2];
+    for (int k2 = 0; k2 < 3; k2++)
+      R[3 * i + k2] = cf.R[i] * (float)Rb[k2] + cf.R[3 + i] * (float)Rb[3 + k2] + cf.R[6 + i] * (float)Rb[6 + k2];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Pass 1: mesh visibility.  Block = 256 consecutive triangles of one env; blocks are laid out so
+// each XCD (blocks bid = xcd mod 8) walks a contiguous range of triangle chunks for all envs, the
+// chunk outer and the env inner, keeping its chunks' 16 KiB of triangles in its L2.  A triangle
+// whose projection spans more than RASTER_SMALL pixel centres (close to the camera) is queued and
+// covered by a whole block in the second visibility kernel instead of by one thread.
+// ---------------------------------------------------------------------------------------------
+#define RASTER_THREADS 256
+#define RASTER_SMALL 64      // pixel centres one thread covers itself
+#define BIG_CAP (1 << 20)    // queued large triangles (beyond: covered by their own thread)
+
+struct TriCam {
+  float v0[3], e1[3], e2[3];  // the triangle in the camera frame
+  int x0, x1, y0, y1;         // the pixel centres its projection can cover (inclusive; empty if x0 > x1)
+};
+
+// the triangle in the camera frame and the range of pixel centres it can cover: its vertices in
+// front of the near plane and the points where its edges cross it, projected to image-plane slopes
+__device__ __forceinline__ void tri_setup(const RenderArgs& a, const float4* tp, const float* R, const float* c,
+                                          float tanh_, float aspect, TriCam& T) {
+  const float4 A = tp[0], B = tp[1], C = tp[2];
+  const float l0[3] = {A.x, A.y, A.z}, l1[3] = {A.w, B.x, B.y}, l2[3] = {B.z, B.w, C.x};
+  for (int i = 0; i < 3; i++) {
+    T.v0[i] = c[i] + R[3 * i] * l0[0] + R[3 * i + 1] * l0[1] + R[3 * i + 2] * l0[2];
+    T.e1[i] = R[3 * i] * l1[0] + R[3 * i + 1] * l1[1] + R[3 * i + 2] * l1[2];
+    T.e2[i] = R[3 * i] * l2[0] + R[3 * i + 1] * l2[1] + R[3 * i + 2] * l2[2];
+  }
+  const int W = a.cam.width, H = a.cam.height;
+  const float znear = a.cam.znear;
+  const float P[3][3] = {{T.v0[0], T.v0[1], T.v0[2]},
+                         {T.v0[0] + T.e1[0], T.v0[1] + T.e1[1], T.v0[2] + T.e1[2]},
+                         {T.v0[0] + T.e2[0], T.v0[1] + T.e2[1], T.v0[2] + T.e2[2]}};
+  float xl = 1e30f, xh = -1e30f, yl = 1e30f, yh = -1e30f;
+  int nin = 0;
+  for (int u = 0; u < 3; u++) {
+    const float zu = -P[u][2];
+    if (zu >= znear) {
+      ++nin;
+      const float iz = 1.f / zu;
+      xl = fminf(xl, P[u][0] * iz);
+      xh = fmaxf(xh, P[u][0] * iz);
+      yl = fminf(yl, P[u][1] * iz);
+      yh = fmaxf(yh, P[u][1] * iz);
+    }
+    const int w = (u + 1) % 3;
+    const float zw = -P[w][2];
+    if ((zu >= znear) != (zw >= znear)) {  // the edge crosses the near plane
+      const float s = (znear - zu) / (zw - zu);
+      const float x = P[u][0] + s * (P[w][0] - P[u][0]), y = P[u][1] + s * (P[w][1] - P[u][1]);
+      const float iz = 1.f / znear;
+      xl = fminf(xl, x * iz);
+      xh = fmaxf(xh, x * iz);
+      yl = fminf(yl, y * iz);
+      yh = fmaxf(yh, y * iz);
+    }
+  }
+  T.x0 = 1;
+  T.x1 = 0;
+  T.y0 = T.y1 = 0;
+  if (nin == 0) return;  // entirely in front of the camera's near plane: clipped
+  // pixel-centre ranges: the centre of column px has slope ((px + 0.5) 2 / W - 1) tanh aspect; a
+  // hair wider than the projection (the ray test decides coverage)
+  const float fx = 0.5f * W / (tanh_ * aspect), fy = 0.5f * H / tanh_, eps = 1e-3f;
+  const float cx0 = fmaxf(xl * fx + 0.5f * W - 0.5f - eps, -1.f), cx1 = fminf(xh * fx + 0.5f * W - 0.5f + eps, (float)W);
+  const float cy0 = fmaxf(0.5f * H - yh * fy - 0.5f - eps, -1.f), cy1 = fminf(0.5f * H - yl * fy - 0.5f + eps, (float)H);
+  T.x0 = max((int)ceilf(cx0), 0);
+  T.x1 = min((int)floorf(cx1), W - 1);
+  T.y0 = max((int)ceilf(cy0), 0);
+  T.y1 = min((int)floorf(cy1), H - 1);
+}
+
+// one pixel centre: its camera ray (origin 0) against the triangle (Moller-Trumbore); the nearest
+// hit per pixel is kept by an atomic min of (depth bits << 32 | triangle index)
+__device__ __forceinline__ void tri_cover(const RenderArgs& a, const TriCam& T, unsigned j, int px, int py,
+                                          float tanh_, float aspect, unsigned long long* vis) {
+  const int W = a.cam.width, H = a.cam.height;
+  const float d[3] = {((2.0f * (px + 0.5f) / W) - 1.0f) * tanh_ * aspect, (1.0f - 2.0f * (py + 0.5f) / H) * tanh_,
+                      -1.0f};
+  const float* e1 = T.e1;
+  const float* e2 = T.e2;
+  const float p[3] = {d[1] * e2[2] - d[2] * e2[1], d[2] * e2[0] - d[0] * e2[2], d[0] * e2[1] - d[1] * e2[0]};
+  const float det = e1[0] * p[0] + e1[1] * p[1] + e1[2] * p[2];
+  if (fabsf(det) < 1e-30f) return;
+  const float id = 1.0f / det;
+  const float s[3] = {-T.v0[0], -T.v0[1], -T.v0[2]};
+  const float uu = (s[0] * p[0] + s[1] * p[1] + s[2] * p[2]) * id;
+  if (uu < 0.f || uu > 1.f) return;
+  const float qv[3] = {s[1] * e1[2] - s[2] * e1[1], s[2] * e1[0] - s[0] * e1[2], s[0] * e1[1] - s[1] * e1[0]};
+  const float vv = (d[0] * qv[0] + d[1] * qv[1] + d[2] * qv[2]) * id;
+  if (vv < 0.f || uu + vv > 1.f) return;
+  const float t = (e2[0] * qv[0] + e2[1] * qv[1] + e2[2] * qv[2]) * id;
+  if (!(t > a.cam.znear)) return;
+  atomicMin(vis + (size_t)py * W + px, ((unsigned long long)__float_as_uint(t) << 32) | j);
+}
+
+__device__ __forceinline__ void mesh_frames_block(const RenderArgs& a, int env, CamFrame& cf, float (*mR)[9],
+                                                  float (*mc)[3], int* mvis, float tanh_, float aspect) {
+  const int tid = threadIdx.x;
+  if (tid == 0) camera_frame(a, env, cf);
+  __syncthreads();
+  if (tid < a.nmesh) {
+    mesh_frame(a, env, tid, cf, mR[tid], mc[tid]);
+    // the slot's bounding sphere against the view frustum (behind the near plane or outside an
+    // image edge: none of its triangles can cover a pixel)
+    const float rad = a.mesh_rad[tid], z = -mc[tid][2];
+    bool v = z + rad > a.cam.znear;
+    const float sx = tanh_ * aspect, sy = tanh_;
+    const float nx = rsqrtf(1.f + sx * sx), ny = rsqrtf(1.f + sy * sy);
+    if (v && (mc[tid][0] - sx * z) * nx > rad) v = false;
+    if (v && (-mc[tid][0] - sx * z) * nx > rad) v = false;
+    if (v && (mc[tid][1] - sy * z) * ny > rad) v = false;
+    if (v && (-mc[tid][1] - sy * z) * ny > rad) v = false;
+    mvis[tid] = v;
+  }
+  __syncthreads();
+}
+
+__global__ void __launch_bounds__(RASTER_THREADS) raster_kernel(RenderArgs a, int chunks) {
+  __shared__ CamFrame cf;
+  __shared__ float mR[MAX_MESH][9], mc[MAX_MESH][3];
+  __shared__ int mvis[MAX_MESH];
+  const int nblk = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q = nblk >> 3, r = nblk & 7;
+  const int lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int chunk = lin / a.n_env, env = lin - chunk * a.n_env;
+  if (chunk >= chunks) return;
+  if (a.active && !a.active[env]) return;
+  const float tanh_ = tanf(0.5f * a.cam.fovy_deg * 3.14159265358979f / 180.0f);
+  const float aspect = (float)a.cam.width / (float)a.cam.height;
+  mesh_frames_block(a, env, cf, mR, mc, mvis, tanh_, aspect);
+  const int j = chunk * RASTER_THREADS + threadIdx.x;
+  if (j >= a.ntri) return;
+  const float4* tp = reinterpret_cast<const float4*>(a.mesh_tri) + 4 * (size_t)j;
+  const int k = __float_as_int(tp[3].x) >> 16;
+  if (k < 0 || k >= a.nmesh || !mvis[k]) return;
+  TriCam T;
+  tri_setup(a, tp, mR[k], mc[k], tanh_, aspect, T);
+  if (T.x0 > T.x1 || T.y0 > T.y1) return;
+  const int span = (T.x1 - T.x0 + 1) * (T.y1 - T.y0 + 1);
+  if (span > RASTER_SMALL) {  // a large projection: queued for a whole block, when the queue has room
+    const unsigned long long slot = atomicAdd(a.big, 1ull);
+    if (slot < BIG_CAP) {
+      a.big[1 + slot] = ((unsigned long long)env << 32) | (unsigned)j;
+      return;
+    }
+  }
+  unsigned long long* vis = a.vis + (size_t)env * a.cam.width * a.cam.height;
+  for (int py = T.y0; py <= T.y1; ++py)
+    for (int px = T.x0; px <= T.x1; ++px) tri_cover(a, T, (unsigned)j, px, py, tanh_, aspect, vis);
+}
+
+// the queued large triangles: one block per entry (grid-stride over the queue), the block's threads
+// over the triangle's pixel centres
+__global__ void __launch_bounds__(RASTER_THREADS) raster_big_kernel(RenderArgs a) {
+  __shared__ CamFrame cf;
+  __shared__ float mR[MAX_MESH][9], mc[MAX_MESH][3];
+  __shared__ int mvis[MAX_MESH];
+  const unsigned long long nq = min(*(volatile const unsigned long long*)a.big, (unsigned long long)BIG_CAP);
+  const float tanh_ = tanf(0.5f * a.cam.fovy_deg * 3.14159265358979f / 180.0f);
+  const float aspect = (float)a.cam.width / (float)a.cam.height;
+  for (unsigned long long e = blockIdx.x; e < nq; e += gridDim.x) {
+    const unsigned long long ent = a.big[1 + e];
+    const int env = (int)(ent >> 32);
+    const unsigned j = (unsigned)ent;
+    __syncthreads();  // the previous entry's frames are no longer read
+    mesh_frames_block(a, env, cf, mR, mc, mvis, tanh_, aspect);
+    const float4* tp = reinterpret_cast<const float4*>(a.mesh_tri) + 4 * (size_t)j;
+    const int k = __float_as_int(tp[3].x) >> 16;
+    TriCam T;
+    tri_setup(a, tp, mR[k], mc[k], tanh_, aspect, T);
+    const int nx = T.x1 - T.x0 + 1, ny = T.y1 - T.y0 + 1;
+    unsigned long long* vis = a.vis + (size_t)env * a.cam.width * a.cam.height;
+    for (int i = threadIdx.x; i < nx * ny; i += RASTER_THREADS)
+      tri_cover(a, T, j, T.x0 + i % nx, T.y0 + i / nx, tanh_, aspect, vis);
+  }
+}
+
 // RMBX_RENDER_MINW: minimum waves per SIMD the register allocation targets: 8 (default; 64
 // registers, 136 B/lane of spilled set-up values, none in the ray loop's hot path) -- per
 // 1024-env 8-bit frame 5.74-5.79 ms vs 6.46 at 5 waves (94 registers, no spills), 6.06 at 6,
@@ -215,12 +443,14 @@ struct RenderArgs {
 #ifndef RMBX_RENDER_MINW
 #define RMBX_RENDER_MINW 8
 #endif
+template <bool VIS>
 __global__ void __launch_bounds__(256, RMBX_RENDER_MINW) render_kernel(RenderArgs a) {
   __shared__ PrimCam prims[MAX_PRIM];
   __shared__ int order[MAX_PRIM];        // the block's primitives sorted front to back, once
   __shared__ int tile_sorted[MAX_PRIM];  // the tile's survivors in that order
   __shared__ int wcount[4];
   __shared__ CamFrame cf;
+  __shared__ float mR[VIS ? MAX_MESH : 1][9];  // mesh slots' body rotations in the camera frame
   const int ntiles = a.tiles_x * a.tiles_y;
   const int env = blockIdx.x / a.groups;
   const int grp = blockIdx.x % a.groups;
@@ -232,19 +462,14 @@ __global__ void __launch_bounds__(256, RMBX_RENDER_MINW) render_kernel(RenderArg
   const float aspect = (float)W / (float)H;
   // cosine of the widest ray (image corner) against the view axis
   const float cos_max = rsqrtf(1.0f + tanh_ * tanh_ * (1.0f + aspect * aspect));
-  if (tid == 0) {
-    // camera pose in world
-    double Rb[9], Rc[9], R[9], t[3];
-    const double* bq = a.xquat + ((size_t)env * a.nbody + a.cam.body) * 4;
-    const double* bp = a.xpos + ((size_t)env * a.nbody + a.cam.body) * 3;
-    quat2mat(bq, Rb);
-    quat2mat(a.cam.quat, Rc);
-    matmul3(Rb, Rc, R);
-    matvec3(Rb, a.cam.pos, t);
-    for (int i = 0; i < 9; i++) cf.R[i] = (float)R[i];
-    for (int i = 0; i < 3; i++) cf.p[i] = (float)(bp[i] + t[i]);
-  }
+  if (tid == 0) camera_frame(a, env, cf);
   __syncthreads();
+  if constexpr (VIS) {
+    if (tid < a.nmesh) {
+      float c[3];
+      mesh_frame(a, env, tid, cf, mR[tid], c);
+    }
+  }
   // the env's primitives in the camera frame, once per block (the block then renders a range
   // of tiles of this env)
   const int np = a.nprim < MAX_PRIM ? a.nprim : MAX_PRIM;
@@ -282,6 +507,42 @@ __global__ void __launch_bounds__(256, RMBX_RENDER_MINW) render_kernel(RenderArg
     P.rad = rad;
     P.zmin = (type == RMBX_GEOM_PLANE || rad <= 0) ? -1e30f : (-P.c[2] - rad);
     for (int i = 0; i < 3; i++) P.ol[i] = -(P.R[i] * P.c[0] + P.R[3 + i] * P.c[1] + P.R[6 + i] * P.c[2]);
+    // screen-space bound: the 8 corners of the primitive's box in its frame, projected (tighter
+    // than the bounding sphere for long thin primitives)
+    P.sx_lo = P.sy_lo = -1e30f;
+    P.sx_hi = P.sy_hi = 1e30f;
+    if (type != RMBX_GEOM_PLANE && rad > 0) {
+      float bh[3] = {rad, rad, rad};
+      if (type == RMBX_GEOM_BOX) {
+        bh[0] = f[0]; bh[1] = f[1]; bh[2] = f[2];
+      } else if (type == RMBX_GEOM_CAPSULE) {
+        bh[0] = bh[1] = f[0]; bh[2] = f[0] + f[1];
+      } else if (type == RMBX_GEOM_CYLINDER) {
+        bh[0] = bh[1] = f[0]; bh[2] = f[1];
+      }
+      float xl = 1e30f, xh = -1e30f, yl = 1e30f, yh = -1e30f;
+      bool front = true;
+      for (int v = 0; v < 8; v++) {
+        const float l[3] = {(v & 1) ? bh[0] : -bh[0], (v & 2) ? bh[1] : -bh[1], (v & 4) ? bh[2] : -bh[2]};
+        float qc[3];
+        for (int i = 0; i < 3; i++) qc[i] = P.c[i] + P.R[3 * i] * l[0] + P.R[3 * i + 1] * l[1] + P.R[3 * i + 2] * l[2];
+        if (-qc[2] < 1e-3f) {
+          front = false;
+          break;
+        }
+        const float iz = 1.0f / -qc[2];
+        xl = fminf(xl, qc[0] * iz);
+        xh = fmaxf(xh, qc[0] * iz);
+        yl = fminf(yl, qc[1] * iz);
+        yh = fmaxf(yh, qc[1] * iz);
+      }
+      if (front) {
+        P.sx_lo = xl - 1e-5f;
+        P.sx_hi = xh + 1e-5f;
+        P.sy_lo = yl - 1e-5f;
+        P.sy_hi = yh + 1e-5f;
+      }
+    }
     if (!(a.dbg & 8) && type != RMBX_GEOM_PLANE) {
       // tighter bound for large primitives (the 10 m walls, the table): every hit point lies at
       // least the camera-to-primitive distance r away, so its camera depth is >= r * cos_max
@@ -352,6 +613,8 @@ __global__ void __launch_bounds__(256, RMBX_RENDER_MINW) render_kernel(RenderArg
         if ((P.c[1] - y_lo * z) * ny_lo < -rad) keep = false;
         if ((y_hi * z - P.c[1]) * ny_hi < -rad) keep = false;
       }
+      // the projected box against the tile's slope rectangle
+      if (P.sx_hi < x_lo || P.sx_lo > x_hi || P.sy_hi < y_lo || P.sy_lo > y_hi) keep = false;
     }
   }
   // compact the survivors in sorted order: ballot per wave, wave offsets through LDS
@@ -367,8 +630,27 @@ __global__ void __launch_bounds__(256, RMBX_RENDER_MINW) render_kernel(RenderArg
   if (px < W && py < H) {
   const float d[3] = {((2.0f * (px + 0.5f) / W) - 1.0f) * tanh_ * aspect,
                       (1.0f - 2.0f * (py + 0.5f) / H) * tanh_, -1.0f};
-  float best = 1e30f, bn[3] = {0, 0, 1};
-  int bp = -1;
+  float best = 1e30f, bn[3] = {0, 0, 1}, brgb[3] = {0.f, 0.f, 0.f};
+  int bp = -1, bgeom = -1;  // the winning primitive / surface geom (-2: a primitive, resolved below)
+  const size_t pix = (size_t)py * W + px;
+  const size_t hw = (size_t)H * W;
+  if constexpr (VIS) {
+    // the pixel's nearest mesh triangle from the visibility pass
+    const unsigned long long key = a.vis[(size_t)env * hw + pix];
+    if (key != VIS_EMPTY) {
+      const unsigned j = (unsigned)key;
+      const float4* tp = reinterpret_cast<const float4*>(a.mesh_tri) + 4 * (size_t)j;
+      const float4 C = tp[2], D = tp[3];
+      const int tag = __float_as_int(D.x), k = tag >> 16;
+      best = __uint_as_float((unsigned)(key >> 32));
+      bgeom = tag & 0xffff;
+      brgb[0] = D.y;
+      brgb[1] = D.z;
+      brgb[2] = D.w;
+      const float nl[3] = {C.y, C.z, C.w};
+      for (int i = 0; i < 3; i++) bn[i] = mR[k][3 * i] * nl[0] + mR[k][3 * i + 1] * nl[1] + mR[k][3 * i + 2] * nl[2];
+    }
+  }
   const int cnt = tile_cnt;
   int ntest = 0;
   for (int k = 0; k < ((a.dbg & 1) ? 0 : cnt); k++) {
@@ -387,21 +669,27 @@ __global__ void __launch_bounds__(256, RMBX_RENDER_MINW) render_kernel(RenderArg
       case RMBX_GEOM_BOX: h = hit_box(o_l, d_l, P.s, &t, nl); break;
       default: break;
     }
-    if (h && (t < best || (t == best && p < bp))) {
+    if (h && (t < best || (t == best && bp >= 0 && p < bp))) {
       best = t;
       bp = p;
+      bgeom = -2;
       // normal back to camera frame
       for (int i = 0; i < 3; i++) bn[i] = P.R[3 * i] * nl[0] + P.R[3 * i + 1] * nl[1] + P.R[3 * i + 2] * nl[2];
     }
   }
+  if (bgeom == -2) {  // a primitive won: its geom and material colour
+    bgeom = a.prim_i32[4 * bp];
+    brgb[0] = prims[bp].rgb[0];
+    brgb[1] = prims[bp].rgb[1];
+    brgb[2] = prims[bp].rgb[2];
+  }
   float col[3];
   float depth = a.cam.zfar;
-  if (bp < 0) {
+  if (bgeom < 0) {
     col[0] = 0.9f;  // skybox gradient colour of env_ur5e_common.xml
     col[1] = 1.0f;
     col[2] = 1.0f;
   } else {
-    const PrimCam& P = prims[bp];
     const float inv = rsqrtf(dot3f(d, d));
     const float vd[3] = {d[0] * inv, d[1] * inv, d[2] * inv};
     float ndv = -(bn[0] * vd[0] + bn[1] * vd[1] + bn[2] * vd[2]);
@@ -416,11 +704,9 @@ __global__ void __launch_bounds__(256, RMBX_RENDER_MINW) render_kernel(RenderArg
     float ndl = -(bn[0] * Ld[0] + bn[1] * Ld[1] + bn[2] * Ld[2]);
     ndl = ndl > 0 ? ndl : 0;
     const float shade = 0.1f + 0.6f * ndv + 0.3f * ndl;
-    for (int i = 0; i < 3; i++) col[i] = fminf(P.rgb[i] * shade, 1.0f);
+    for (int i = 0; i < 3; i++) col[i] = fminf(brgb[i] * shade, 1.0f);
     depth = best;  // d has unit -z component: t is the camera-z distance
   }
-  const size_t pix = (size_t)py * W + px;
-  const size_t hw = (size_t)H * W;
   const bool do_store = !(a.dbg & 2) || col[0] == 12345.f;  // (diagnostic: keep the shading live)
   uint8_t u[3];
   for (int i = 0; i < 3; i++) u[i] = (uint8_t)(col[i] * 255.0f + 0.5f);
@@ -431,6 +717,7 @@ __global__ void __launch_bounds__(256, RMBX_RENDER_MINW) render_kernel(RenderArg
     o[2] = u[2];
   }
   if (a.depth && do_store) a.depth[(size_t)env * hw + pix] = (a.dbg & 4) ? (float)(ntest + 1000 * cnt) : depth;
+  if (a.hit_geom && do_store) a.hit_geom[(size_t)env * hw + pix] = bgeom;
   if (a.policy && do_store) {
     if (a.policy_dtype == 2) {
       // 2x2 space-to-depth [n][H/2][W/2][16]: channel (dy*2+dx)*3+c, 12..15 zero
@@ -476,13 +763,13 @@ __global__ void __launch_bounds__(256, RMBX_RENDER_MINW) render_kernel(RenderArg
 
 }  // namespace rmbx
 
-extern "C" int rmbx_render(const rmbx_camera* cam, const int32_t* prim_i32, const float* prim_f32,
-                           int nprim, const double* gxpos, const double* gxmat, const double* xpos,
-                           const double* xquat, int ngeom, int nbody, uint8_t* rgb, float* depth,
-                           void* policy_img, int policy_dtype, const uint8_t* active, int n_env,
-                           void* stream) {
-  RMBX_CHECK_ARG(cam && prim_i32 && prim_f32 && gxpos && gxmat && xpos && xquat, "NULL argument");
-  RMBX_CHECK_ARG(nprim > 0 && nprim <= MAX_PRIM, "nprim=%d outside [1, %d]", nprim, MAX_PRIM);
+extern "C" int rmbx_render_scene(const rmbx_camera* cam, const rmbx_scene_tables* scene, const double* gxpos,
+                                 const double* gxmat, const double* xpos, const double* xquat, int ngeom,
+                                 int nbody, uint8_t* rgb, float* depth, int32_t* hit_geom, void* policy_img,
+                                 int policy_dtype, const uint8_t* active, int n_env, void* stream) {
+  RMBX_CHECK_ARG(cam && scene && scene->prim_i32 && scene->prim_f32 && gxpos && gxmat && xpos && xquat,
+                 "NULL argument");
+  RMBX_CHECK_ARG(scene->nprim > 0 && scene->nprim <= MAX_PRIM, "nprim=%d outside [1, %d]", scene->nprim, MAX_PRIM);
   RMBX_CHECK_ARG(cam->width > 0 && cam->height > 0 && cam->width <= 8192 && cam->height <= 8192,
                  "bad image size %dx%d", cam->width, cam->height);
   RMBX_CHECK_ARG(cam->body >= 0 && cam->body < nbody, "bad camera body %d", cam->body);
@@ -490,12 +777,26 @@ extern "C" int rmbx_render(const rmbx_camera* cam, const int32_t* prim_i32, cons
                  "policy_dtype must be 0 (f32), 1 (bf16), 2 (bf16 s2d), 3 (f32 s2d) or 4 (u8 s2d)");
   RMBX_CHECK_ARG(policy_dtype < 2 || (cam->width % 2 == 0 && cam->height % 2 == 0),
                  "space-to-depth policy output needs an even image size");
+  const bool meshes = scene->ntri > 0;
+  RMBX_CHECK_ARG(scene->ntri >= 0 && scene->ntri < (1 << 26) && scene->nmesh >= 0 && scene->nmesh <= MAX_MESH,
+                 "bad mesh sizes (ntri=%d, nmesh=%d, at most %d mesh bodies)", scene->ntri, scene->nmesh, MAX_MESH);
+  RMBX_CHECK_ARG(!meshes || (scene->mesh_tri && scene->mesh_body && scene->mesh_rad && scene->vis && scene->big &&
+                             scene->nmesh > 0 && (((uintptr_t)scene->mesh_tri | (uintptr_t)scene->vis) & 15) == 0),
+                 "meshes need mesh_tri / mesh_body / mesh_rad / vis (16-byte aligned) / big and nmesh > 0");
   if (n_env == 0) return RMBX_OK;
   rmbx::RenderArgs a;
   a.cam = *cam;
-  a.prim_i32 = prim_i32;
-  a.prim_f32 = prim_f32;
-  a.nprim = nprim;
+  a.prim_i32 = scene->prim_i32;
+  a.prim_f32 = scene->prim_f32;
+  a.nprim = scene->nprim;
+  a.mesh_tri = scene->mesh_tri;
+  a.ntri = meshes ? scene->ntri : 0;
+  a.nmesh = meshes ? scene->nmesh : 0;
+  a.mesh_body = scene->mesh_body;
+  a.mesh_rad = scene->mesh_rad;
+  a.vis = meshes ? scene->vis : nullptr;
+  a.big = meshes ? scene->big : nullptr;
+  a.hit_geom = hit_geom;
   a.gxpos = gxpos;
   a.gxmat = gxmat;
   a.xpos = xpos;
@@ -515,8 +816,36 @@ extern "C" int rmbx_render(const rmbx_camera* cam, const int32_t* prim_i32, cons
   a.dbg = dbg_env ? std::atoi(dbg_env) : 0;
   const size_t nblocks = (size_t)n_env * a.groups;
   RMBX_CHECK_ARG(nblocks < (1ull << 31), "grid too large");
-  hipLaunchKernelGGL(rmbx::render_kernel, dim3((unsigned)nblocks), dim3(256), 0,
-                     reinterpret_cast<hipStream_t>(stream), a);
+  hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (meshes) {
+    // pass 1: the meshes' nearest triangle per pixel into the (cleared) visibility buffer
+    const size_t hw = (size_t)cam->width * cam->height;
+    RMBX_CHECK_HIP(hipMemsetAsync(scene->vis, 0xff, (size_t)n_env * hw * sizeof(unsigned long long), st));
+    RMBX_CHECK_HIP(hipMemsetAsync(scene->big, 0, sizeof(unsigned long long), st));
+    const int chunks = (scene->ntri + RASTER_THREADS - 1) / RASTER_THREADS;
+    const size_t rblocks = (size_t)chunks * n_env;
+    RMBX_CHECK_ARG(rblocks < (1ull << 31), "raster grid too large");
+    hipLaunchKernelGGL(rmbx::raster_kernel, dim3((unsigned)rblocks), dim3(RASTER_THREADS), 0, st, a, chunks);
+    RMBX_CHECK_LAUNCH();
+    hipLaunchKernelGGL(rmbx::raster_big_kernel, dim3(2048), dim3(RASTER_THREADS), 0, st, a);
+    RMBX_CHECK_LAUNCH();
+    hipLaunchKernelGGL(rmbx::render_kernel<true>, dim3((unsigned)nblocks), dim3(256), 0, st, a);
+  } else {
+    hipLaunchKernelGGL(rmbx::render_kernel<false>, dim3((unsigned)nblocks), dim3(256), 0, st, a);
+  }
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
+}
+
+extern "C" int rmbx_render(const rmbx_camera* cam, const int32_t* prim_i32, const float* prim_f32,
+                           int nprim, const double* gxpos, const double* gxmat, const double* xpos,
+                           const double* xquat, int ngeom, int nbody, uint8_t* rgb, float* depth,
+                           void* policy_img, int policy_dtype, const uint8_t* active, int n_env,
+                           void* stream) {
+  rmbx_scene_tables sc{};
+  sc.prim_i32 = prim_i32;
+  sc.prim_f32 = prim_f32;
+  sc.nprim = nprim;
+  return rmbx_render_scene(cam, &sc, gxpos, gxmat, xpos, xquat, ngeom, nbody, rgb, depth, nullptr, policy_img,
+                           policy_dtype, active, n_env, stream);
 }

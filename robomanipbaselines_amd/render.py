@@ -1,10 +1,14 @@
-"""Batched camera rendering front end (C ABI rmbx_render).
+"""Batched camera rendering front end (C ABI rmbx_render_scene).
 
-Builds the primitive table of a compiled scene and renders one camera for all envs of a
-PhysicsEngine.  Visual meshes are drawn through their body's collision primitives (capsules,
-mesh bounding boxes) in the mesh's material colour; primitive visual geoms are drawn as they
-are; textures are not sampled (documented substitution: images are not pixel-identical to
-MuJoCo's OpenGL renderer).
+Builds the drawing tables of a compiled scene and renders one camera for all envs of a
+PhysicsEngine.  The geoms MuJoCo draws by default (groups 0-2) are drawn: primitive geoms as they
+are (ray cast), visual mesh geoms as their triangles (scenes compiled with render meshes,
+mjcf/rmesh.py: vertex-clustered at 1 mm, grouped per body; rasterised into a per-pixel visibility
+buffer first), a mesh whose file is missing from the reference checkout as its bounding box;
+material colours, flat-shaded triangles, textures are not sampled (documented substitution: images
+are not pixel-identical to MuJoCo's OpenGL renderer).  Assets packed without
+render meshes fall back to the round-3 form (visual meshes drawn through their body's collision
+primitives).
 """
 
 import ctypes
@@ -20,6 +24,34 @@ IMAGENET_STD = (0.229, 0.224, 0.225)
 
 
 def build_prims(arrays):
+    """(prim_i32 [nprim, 4], prim_f32 [nprim, 8]) of the scene (include/rmbx.h rmbx_scene_tables)."""
+    if "rmesh_body" in arrays:
+        return _build_prims_meshes(arrays)
+    return _build_prims_substitutes(arrays)
+
+
+def _build_prims_meshes(arrays):
+    """Every geom of groups 0-2 except the visual meshes with render triangles (drawn by the
+    visibility pass): primitives as they are, a mesh whose file is missing from the checkout as its
+    bounding box."""
+    gt, gg = arrays["geom_type"], arrays["geom_group"]
+    ct, cs, size, rgba = arrays["geom_ctype"], arrays["geom_csize"], arrays["geom_size"], arrays["geom_rgba"]
+    meshed = set(int(g) for g in arrays["rmesh_geoms"])
+    pi, pf = [], []
+    for g in range(len(gt)):
+        t = int(gt[g])
+        if gg[g] > 2 or g in meshed:
+            continue
+        if t in (C.GEOM_PLANE, C.GEOM_SPHERE, C.GEOM_CAPSULE, C.GEOM_CYLINDER, C.GEOM_BOX):
+            pi.append([g, t, 0, 0])
+            pf.append(list(size[g][:3]) + list(rgba[g][:3]) + [0, 0])
+        elif t == C.GEOM_MESH and ct[g] < 0 and np.any(cs[g][:3] > 0):
+            pi.append([g, C.GEOM_BOX, 0, 0])  # missing mesh file: its bounding box
+            pf.append(list(cs[g][:3]) + list(rgba[g][:3]) + [0, 0])
+    return np.array(pi, np.int32), np.array(pf, np.float32)
+
+
+def _build_prims_substitutes(arrays):
     gt, gb, gg = arrays["geom_type"], arrays["geom_body"], arrays["geom_group"]
     ct, cs, size, rgba = arrays["geom_ctype"], arrays["geom_csize"], arrays["geom_size"], arrays["geom_rgba"]
     mesh_color = {}
@@ -54,6 +86,22 @@ class Renderer:
         self.nprim = len(pi)
         self.prim_i32 = torch.tensor(pi, device=device)
         self.prim_f32 = torch.tensor(pf, device=device)
+        self.device = torch.device(device)
+        if "rmesh_body" in arrays:
+            self.mesh_tri = torch.tensor(arrays["rmesh_tri"], dtype=torch.float32, device=device).contiguous()
+            self.mesh_body = torch.tensor(arrays["rmesh_body"], dtype=torch.int32, device=device)
+            self.mesh_rad = torch.tensor(arrays["rmesh_rad"], dtype=torch.float32, device=device)
+        else:
+            self.mesh_tri = self.mesh_body = self.mesh_rad = None
+        self._vis = None  # visibility workspace u64 [n, H, W], allocated at the first render
+        self._big = None  # large-triangle queue u64 [1 + 2^20]
+        sc = N.SceneTables()
+        sc.prim_i32, sc.prim_f32, sc.nprim = self.prim_i32.data_ptr(), self.prim_f32.data_ptr(), self.nprim
+        if self.mesh_tri is not None:
+            sc.ntri, sc.nmesh = self.mesh_tri.shape[0], self.mesh_body.shape[0]
+            sc.mesh_tri, sc.mesh_body, sc.mesh_rad = (self.mesh_tri.data_ptr(), self.mesh_body.data_ptr(),
+                                                      self.mesh_rad.data_ptr())
+        self._scene = sc
         self.width, self.height = width, height
         self.cam_names = [str(x) for x in arrays["names_cam"]]
         self.znear = float(arrays["_znear"]) * float(arrays["_extent"])
@@ -76,9 +124,11 @@ class Renderer:
             c.std[k] = IMAGENET_STD[k]
         return c
 
-    def render(self, engine, camera_name, rgb=None, depth=None, policy=None, active=None, mean=None, std=None):
+    def render(self, engine, camera_name, rgb=None, depth=None, policy=None, active=None, mean=None, std=None,
+               hit_geom=None):
         """Render `camera_name` for every env of `engine` into the given (optional) tensors:
-        rgb u8 [n,H,W,3], depth f32 [n,H,W], policy bf16/f32 [n,3,H,W]."""
+        rgb u8 [n,H,W,3], depth f32 [n,H,W], policy bf16/f32 [n,3,H,W], hit_geom i32 [n,H,W] (the
+        geom id of each pixel's surface, -1 for the background)."""
         cam = self.camera(camera_name)
         if mean is not None:
             for k in range(3):
@@ -99,7 +149,14 @@ class Renderer:
             else:
                 assert tuple(policy.shape) == (n, 3, H, W)
                 pdt = 1 if policy.dtype == torch.bfloat16 else 0
-        N.call("rmbx_render", ctypes.byref(cam), N.ptr(self.prim_i32), N.ptr(self.prim_f32), self.nprim,
+        if hit_geom is not None:
+            assert hit_geom.dtype == torch.int32 and tuple(hit_geom.shape) == (n, H, W) and hit_geom.is_contiguous()
+        if self.mesh_tri is not None:
+            if self._vis is None or self._vis.shape[0] < n * H * W:
+                self._vis = torch.empty(n * H * W, dtype=torch.int64, device=self.device)
+                self._big = torch.empty(1 + (1 << 20), dtype=torch.int64, device=self.device)
+            self._scene.vis, self._scene.big = self._vis.data_ptr(), self._big.data_ptr()
+        N.call("rmbx_render_scene", ctypes.byref(cam), ctypes.byref(self._scene),
                N.ptr(engine.gxpos), N.ptr(engine.gxmat), N.ptr(engine.xpos), N.ptr(engine.xquat),
-               engine.ngeom, engine.nbody, N.ptr(rgb), N.ptr(depth), N.ptr(policy), pdt, N.ptr(active), n,
-               N.stream_ptr())
+               engine.ngeom, engine.nbody, N.ptr(rgb), N.ptr(depth), N.ptr(hit_geom), N.ptr(policy), pdt,
+               N.ptr(active), n, N.stream_ptr())

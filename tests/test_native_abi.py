@@ -30,7 +30,7 @@ def test_signatures_cover_only_declared():
 
 def test_abi_version_and_errors():
     lib = N.load()
-    assert lib.rmbx_abi_version() == 1
+    assert lib.rmbx_abi_version() == 2
     cnt = ctypes.c_int(-5)
     assert lib.rmbx_device_count(ctypes.byref(cnt)) == 0
     assert cnt.value >= 0

@@ -6,6 +6,9 @@ import sys
 sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
 from robomanipbaselines_amd import model as MD  # noqa: E402
 from robomanipbaselines_amd.mjcf import compiler as C  # noqa: E402
+from robomanipbaselines_amd.mjcf import rmesh as MB  # noqa: E402
+
+RENDER_MESH_CELL = 1e-3  # m: vertex-clustering grid of the render meshes (mjcf/rmesh.py)
 
 REF_ENVS = "/root/reference/robo_manip_baselines/envs/assets/mujoco/envs"
 SCENES = {"ur5e_cable": os.path.join(REF_ENVS, "ur5e", "env_ur5e_cable.xml"),
@@ -50,6 +53,8 @@ if __name__ == "__main__":
         M = C.compile_mjcf(path, **OPTIONS.get(name, {}))
         arrays = MD.pack(M, **PACK_OPTIONS.get(name, {}))
         add_arm_ik(M, arrays)
+        # render meshes: the visual mesh geoms' triangles per body (1 mm vertex clustering)
+        arrays.update(MB.render_meshes(M.geoms, cell=RENDER_MESH_CELL))
         out = os.path.join(MD.ASSET_DIR, name + ".npz")
         MD.save(arrays, out)
         print(name, "nq", M.nq, "nv", M.nv, "pairs", len(M.pairs), "->", out, os.path.getsize(out), "bytes")
