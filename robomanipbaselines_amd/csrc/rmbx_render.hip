@@ -211,7 +211,9 @@ struct RenderArgs {
   const int32_t* mesh_body;   // [nmesh] body of each mesh slot
   const float* mesh_rad;      // [nmesh] bounding radius of the slot's triangles about the body origin
   unsigned long long* vis;    // [n][H][W] nearest mesh hit (depth bits << 32 | triangle), VIS_EMPTY: none
-  unsigned long long* big;    // [1 + BIG_CAP]: count, then queued (env << 32 | triangle) entries
+  unsigned long long* big;    // [1 + big_cap]: count, then queued (env << 32 | triangle) entries
+  long long big_cap;
+  uint8_t* tflag;             // [n][tiles]: 1 where the visibility pass wrote a pixel of the tile
   int32_t* hit_geom;          // optional [n][H][W]: geom id of the pixel's surface (-1: background)
   const double* gxpos;
   const double* gxmat;
@@ -231,6 +233,7 @@ struct RenderArgs {
 
 // camera pose of env `env` in world: R (columns = camera axes), p
 __device__ __forceinline__ void camera_frame(const RenderArgs& a, int env, CamFrame& cf) {
+#pragma clang fp contract(off)  // bit-identical in every kernel it is inlined into
   double Rb[9], Rc[9], R[9], t[3];
   const double* bq = a.xquat + ((size_t)env * a.nbody + a.cam.body) * 4;
   const double* bp = a.xpos + ((size_t)env * a.nbody + a.cam.body) * 3;
@@ -245,6 +248,7 @@ __device__ __forceinline__ void camera_frame(const RenderArgs& a, int env, CamFr
 // a mesh slot's body frame in the camera frame: R = Rcam^T Rbody (row-major), c = Rcam^T (x - pcam)
 __device__ __forceinline__ void mesh_frame(const RenderArgs& a, int env, int k, const CamFrame& cf, float* R,
                                            float* c) {
+#pragma clang fp contract(off)
   const int b = a.mesh_body[k];
   double Rb[9];
   quat2mat(a.xquat + ((size_t)env * a.nbody + b) * 4, Rb);
@@ -266,7 +270,6 @@ __device__ __forceinline__ void mesh_frame(const RenderArgs& a, int env, int k, 
 // ---------------------------------------------------------------------------------------------
 #define RASTER_THREADS 256
 #define RASTER_SMALL 64      // pixel centres one thread covers itself
-#define BIG_CAP (1 << 20)    // queued large triangles (beyond: covered by their own thread)
 
 struct TriCam {
   float v0[3], e1[3], e2[3];  // the triangle in the camera frame
@@ -277,6 +280,9 @@ struct TriCam {
 // front of the near plane and the points where its edges cross it, projected to image-plane slopes
 __device__ __forceinline__ void tri_setup(const RenderArgs& a, const float4* tp, const float* R, const float* c,
                                           float tanh_, float aspect, TriCam& T) {
+  // no FMA contraction here and in tri_cover: a triangle covered by raster_kernel and one covered by
+  // raster_big_kernel must give bit-identical depths whichever kernel (and inlining) computed them
+#pragma clang fp contract(off)
   const float4 A = tp[0], B = tp[1], C = tp[2];
   const float l0[3] = {A.x, A.y, A.z}, l1[3] = {A.w, B.x, B.y}, l2[3] = {B.z, B.w, C.x};
   for (int i = 0; i < 3; i++) {
@@ -331,7 +337,8 @@ __device__ __forceinline__ void tri_setup(const RenderArgs& a, const float4* tp,
 // one pixel centre: its camera ray (origin 0) against the triangle (Moller-Trumbore); the nearest
 // hit per pixel is kept by an atomic min of (depth bits << 32 | triangle index)
 __device__ __forceinline__ void tri_cover(const RenderArgs& a, const TriCam& T, unsigned j, int px, int py,
-                                          float tanh_, float aspect, unsigned long long* vis) {
+                                          float tanh_, float aspect, unsigned long long* vis, uint8_t* tflag) {
+#pragma clang fp contract(off)
   const int W = a.cam.width, H = a.cam.height;
   const float d[3] = {((2.0f * (px + 0.5f) / W) - 1.0f) * tanh_ * aspect, (1.0f - 2.0f * (py + 0.5f) / H) * tanh_,
                       -1.0f};
@@ -350,6 +357,7 @@ __device__ __forceinline__ void tri_cover(const RenderArgs& a, const TriCam& T, 
   const float t = (e2[0] * qv[0] + e2[1] * qv[1] + e2[2] * qv[2]) * id;
   if (!(t > a.cam.znear)) return;
   atomicMin(vis + (size_t)py * W + px, ((unsigned long long)__float_as_uint(t) << 32) | j);
+  tflag[(py / RENDER_TILE) * a.tiles_x + px / RENDER_TILE] = 1;  // (every writer stores the same 1)
 }
 
 __device__ __forceinline__ void mesh_frames_block(const RenderArgs& a, int env, CamFrame& cf, float (*mR)[9],
@@ -398,14 +406,15 @@ __global__ void __launch_bounds__(RASTER_THREADS) raster_kernel(RenderArgs a, in
   const int span = (T.x1 - T.x0 + 1) * (T.y1 - T.y0 + 1);
   if (span > RASTER_SMALL) {  // a large projection: queued for a whole block, when the queue has room
     const unsigned long long slot = atomicAdd(a.big, 1ull);
-    if (slot < BIG_CAP) {
+    if (slot < (unsigned long long)a.big_cap) {
       a.big[1 + slot] = ((unsigned long long)env << 32) | (unsigned)j;
       return;
     }
   }
   unsigned long long* vis = a.vis + (size_t)env * a.cam.width * a.cam.height;
+  uint8_t* tflag = a.tflag + (size_t)env * a.tiles_x * a.tiles_y;
   for (int py = T.y0; py <= T.y1; ++py)
-    for (int px = T.x0; px <= T.x1; ++px) tri_cover(a, T, (unsigned)j, px, py, tanh_, aspect, vis);
+    for (int px = T.x0; px <= T.x1; ++px) tri_cover(a, T, (unsigned)j, px, py, tanh_, aspect, vis, tflag);
 }
 
 // the queued large triangles: one block per entry (grid-stride over the queue), the block's threads
@@ -414,23 +423,31 @@ __global__ void __launch_bounds__(RASTER_THREADS) raster_big_kernel(RenderArgs a
   __shared__ CamFrame cf;
   __shared__ float mR[MAX_MESH][9], mc[MAX_MESH][3];
   __shared__ int mvis[MAX_MESH];
-  const unsigned long long nq = min(*(volatile const unsigned long long*)a.big, (unsigned long long)BIG_CAP);
+  const unsigned long long nq = min(*(volatile const unsigned long long*)a.big, (unsigned long long)a.big_cap);
   const float tanh_ = tanf(0.5f * a.cam.fovy_deg * 3.14159265358979f / 180.0f);
   const float aspect = (float)a.cam.width / (float)a.cam.height;
-  for (unsigned long long e = blockIdx.x; e < nq; e += gridDim.x) {
+  // a contiguous range of entries per block: a raster wave queues its triangles in one run of
+  // slots, all of one env, so the frames are recomputed only where the env changes
+  const unsigned long long e0 = nq * blockIdx.x / gridDim.x, e1 = nq * (blockIdx.x + 1) / gridDim.x;
+  int cur = -1;
+  for (unsigned long long e = e0; e < e1; ++e) {
     const unsigned long long ent = a.big[1 + e];
     const int env = (int)(ent >> 32);
     const unsigned j = (unsigned)ent;
-    __syncthreads();  // the previous entry's frames are no longer read
-    mesh_frames_block(a, env, cf, mR, mc, mvis, tanh_, aspect);
+    if (env != cur) {  // (block-uniform: every thread read the same entry)
+      __syncthreads();  // the previous env's frames are no longer read
+      mesh_frames_block(a, env, cf, mR, mc, mvis, tanh_, aspect);
+      cur = env;
+    }
     const float4* tp = reinterpret_cast<const float4*>(a.mesh_tri) + 4 * (size_t)j;
     const int k = __float_as_int(tp[3].x) >> 16;
     TriCam T;
     tri_setup(a, tp, mR[k], mc[k], tanh_, aspect, T);
     const int nx = T.x1 - T.x0 + 1, ny = T.y1 - T.y0 + 1;
     unsigned long long* vis = a.vis + (size_t)env * a.cam.width * a.cam.height;
+    uint8_t* tflag = a.tflag + (size_t)env * a.tiles_x * a.tiles_y;
     for (int i = threadIdx.x; i < nx * ny; i += RASTER_THREADS)
-      tri_cover(a, T, j, T.x0 + i % nx, T.y0 + i / nx, tanh_, aspect, vis);
+      tri_cover(a, T, j, T.x0 + i % nx, T.y0 + i / nx, tanh_, aspect, vis, tflag);
   }
 }
 
@@ -625,6 +642,11 @@ __global__ void __launch_bounds__(256, RMBX_RENDER_MINW) render_kernel(RenderArg
   for (int w = 0; w < (tid >> 6); ++w) base += wcount[w];
   if (keep) tile_sorted[base + __popcll(kb & ((1ull << (tid & 63)) - 1))] = p_cull;
   const int tile_cnt = wcount[0] + wcount[1] + wcount[2] + wcount[3];
+  // did the visibility pass write a pixel of this tile? (the flag is consumed: cleared below, after
+  // every lane has read it, with the pixels' keys, so the workspace is back to empty for the next
+  // call without a clearing pass)
+  bool tile_vis = false;
+  if constexpr (VIS) tile_vis = a.tflag[(size_t)env * ntiles + tile] != 0;
   __syncthreads();
   const int px = tx0 + (tid % RENDER_TILE), py = ty0 + (tid / RENDER_TILE);
   if (px < W && py < H) {
@@ -636,8 +658,9 @@ __global__ void __launch_bounds__(256, RMBX_RENDER_MINW) render_kernel(RenderArg
   const size_t hw = (size_t)H * W;
   if constexpr (VIS) {
     // the pixel's nearest mesh triangle from the visibility pass
-    const unsigned long long key = a.vis[(size_t)env * hw + pix];
+    const unsigned long long key = tile_vis ? a.vis[(size_t)env * hw + pix] : VIS_EMPTY;
     if (key != VIS_EMPTY) {
+      a.vis[(size_t)env * hw + pix] = VIS_EMPTY;
       const unsigned j = (unsigned)key;
       const float4* tp = reinterpret_cast<const float4*>(a.mesh_tri) + 4 * (size_t)j;
       const float4 C = tp[2], D = tp[3];
@@ -758,6 +781,7 @@ __global__ void __launch_bounds__(256, RMBX_RENDER_MINW) render_kernel(RenderArg
   }
   }  // pixel
   __syncthreads();
+  if (VIS && tid == 0 && tile_vis) a.tflag[(size_t)env * ntiles + tile] = 0;
   }  // tiles
 }
 
@@ -781,8 +805,10 @@ extern "C" int rmbx_render_scene(const rmbx_camera* cam, const rmbx_scene_tables
   RMBX_CHECK_ARG(scene->ntri >= 0 && scene->ntri < (1 << 26) && scene->nmesh >= 0 && scene->nmesh <= MAX_MESH,
                  "bad mesh sizes (ntri=%d, nmesh=%d, at most %d mesh bodies)", scene->ntri, scene->nmesh, MAX_MESH);
   RMBX_CHECK_ARG(!meshes || (scene->mesh_tri && scene->mesh_body && scene->mesh_rad && scene->vis && scene->big &&
+                             scene->tflag &&
                              scene->nmesh > 0 && (((uintptr_t)scene->mesh_tri | (uintptr_t)scene->vis) & 15) == 0),
                  "meshes need mesh_tri / mesh_body / mesh_rad / vis (16-byte aligned) / big and nmesh > 0");
+  RMBX_CHECK_ARG(!meshes || scene->big_cap >= 0, "bad big_cap %lld", (long long)scene->big_cap);
   if (n_env == 0) return RMBX_OK;
   rmbx::RenderArgs a;
   a.cam = *cam;
@@ -796,6 +822,8 @@ extern "C" int rmbx_render_scene(const rmbx_camera* cam, const rmbx_scene_tables
   a.mesh_rad = scene->mesh_rad;
   a.vis = meshes ? scene->vis : nullptr;
   a.big = meshes ? scene->big : nullptr;
+  a.big_cap = meshes ? scene->big_cap : 0;
+  a.tflag = meshes ? scene->tflag : nullptr;
   a.hit_geom = hit_geom;
   a.gxpos = gxpos;
   a.gxmat = gxmat;
@@ -818,9 +846,8 @@ extern "C" int rmbx_render_scene(const rmbx_camera* cam, const rmbx_scene_tables
   RMBX_CHECK_ARG(nblocks < (1ull << 31), "grid too large");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
   if (meshes) {
-    // pass 1: the meshes' nearest triangle per pixel into the (cleared) visibility buffer
-    const size_t hw = (size_t)cam->width * cam->height;
-    RMBX_CHECK_HIP(hipMemsetAsync(scene->vis, 0xff, (size_t)n_env * hw * sizeof(unsigned long long), st));
+    // pass 1: the meshes' nearest triangle per pixel into the visibility buffer (empty on entry:
+    // the ray-cast pass clears every key and tile flag it consumes)
     RMBX_CHECK_HIP(hipMemsetAsync(scene->big, 0, sizeof(unsigned long long), st));
     const int chunks = (scene->ntri + RASTER_THREADS - 1) / RASTER_THREADS;
     const size_t rblocks = (size_t)chunks * n_env;

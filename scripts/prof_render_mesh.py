@@ -22,6 +22,7 @@ hit = torch.empty((n, H, W), dtype=torch.int32, device="cuda:0")
 cam = env.renderer.cam_names[0]
 base = {k: v for k, v in env.arrays.items() if not k.startswith("rmesh_")}
 variants_only = os.environ.get("RENDER_ONLY_ASSET") == "1"
+cams = env.renderer.cam_names if os.environ.get("RENDER_ALL_CAMS") == "1" else [cam]
 variants = [("meshes 1 mm (asset)", env.renderer)]
 if not variants_only:
     variants.append(("substitutes (no meshes)", Renderer(base, "cuda:0")))
@@ -30,7 +31,7 @@ for f in ([] if variants_only else sorted(glob.glob(os.path.join(os.path.dirname
         arr = dict(base, **{k: z[k] for k in z.files})
     variants.append((os.path.basename(f), Renderer(arr, "cuda:0")))
 mesh_geoms = torch.tensor(env.arrays["rmesh_geoms"], device="cuda:0")
-for name, r in variants:
+for name, r, cam in [(nm, r, c) for nm, r in variants for c in cams]:
     def run():
         r.render(env.engine, cam, policy=u8)
     run()
@@ -46,5 +47,5 @@ for name, r in variants:
         best = min(best, a.elapsed_time(b) / 3)
     r.render(env.engine, cam, hit_geom=hit)
     frac = torch.isin(hit, mesh_geoms).float().mean().item()
-    print(f"{name}: {best:.3f} ms per {n}-env call, mesh pixels {frac:.3f}, tris "
+    print(f"{name} [{cam}]: {best:.3f} ms per {n}-env call, mesh pixels {frac:.3f}, tris "
           f"{0 if r.mesh_tri is None else r.mesh_tri.shape[0]}", flush=True)
