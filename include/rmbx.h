@@ -331,14 +331,9 @@ int rmbx_render(const rmbx_camera* cam, const int32_t* prim_i32, const float* pr
  * all ones (empty) on entry, filled with each pixel's nearest triangle (depth bits << 32 | index)
  * and left empty again by the call; tflag: u8 [n_env][tiles of 16x16 pixels], zero on entry and
  * on return (the tiles the visibility pass wrote);
- * big: caller-provided device workspace u64 [1 + big_cap] (a queue of triangles whose projection
- * spans many pixels, covered by a whole workgroup each; a triangle beyond the capacity is covered
- * by its own thread, with identical results, only slower -- about 2.5k entries per env are used by
- * the close-up wrist camera of the UR5e scenes, RMBX_RENDER_BIG_PER_ENV per env is ample);
  * triangle hits nearer than cam->znear are clipped (OpenGL's near plane).  hit_geom (optional)
  * [n][H][W] receives the geom id of each pixel's surface, -1 for the background; the other
  * arguments and outputs are rmbx_render's.  rmbx_render is this call without meshes. */
-#define RMBX_RENDER_BIG_PER_ENV 8192
 typedef struct rmbx_scene_tables {
   const int32_t* prim_i32;
   const float* prim_f32;
@@ -348,8 +343,6 @@ typedef struct rmbx_scene_tables {
   const int32_t* mesh_body;
   const float* mesh_rad;
   unsigned long long* vis;
-  unsigned long long* big;
-  int64_t big_cap;
   uint8_t* tflag;
 } rmbx_scene_tables;
 

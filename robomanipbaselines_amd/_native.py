@@ -117,7 +117,7 @@ class SceneTables(ctypes.Structure):
 
     _fields_ = [("prim_i32", _c_p), ("prim_f32", _c_p), ("nprim", ctypes.c_int32), ("ntri", ctypes.c_int32),
                 ("nmesh", ctypes.c_int32), ("mesh_tri", _c_p), ("mesh_body", _c_p), ("mesh_rad", _c_p), ("vis", _c_p),
-                ("big", _c_p), ("big_cap", ctypes.c_int64), ("tflag", _c_p)]
+                ("tflag", _c_p)]
 
 
 class EnvBuffers(ctypes.Structure):

@@ -211,8 +211,6 @@ struct RenderArgs {
   const int32_t* mesh_body;   // [nmesh] body of each mesh slot
   const float* mesh_rad;      // [nmesh] bounding radius of the slot's triangles about the body origin
   unsigned long long* vis;    // [n][H][W] nearest mesh hit (depth bits << 32 | triangle), VIS_EMPTY: none
-  unsigned long long* big;    // [1 + big_cap]: count, then queued (env << 32 | triangle) entries
-  long long big_cap;
   uint8_t* tflag;             // [n][tiles]: 1 where the visibility pass wrote a pixel of the tile
   int32_t* hit_geom;          // optional [n][H][W]: geom id of the pixel's surface (-1: background)
   const double* gxpos;
@@ -265,23 +263,29 @@ __device__ __forceinline__ void mesh_frame(const RenderArgs& a, int env, int k, 
 // Pass 1: mesh visibility.  Block = 256 consecutive triangles of one env; blocks are laid out so
 // each XCD (blocks bid = xcd mod 8) walks a contiguous range of triangle chunks for all envs, the
 // chunk outer and the env inner, keeping its chunks' 16 KiB of triangles in its L2.  A triangle
-// whose projection spans more than RASTER_SMALL pixel centres (close to the camera) is queued and
-// covered by a whole block in the second visibility kernel instead of by one thread.
+// whose projection spans more than RASTER_SMALL pixel centres is covered by its whole wave.
 // ---------------------------------------------------------------------------------------------
 #define RASTER_THREADS 256
-#define RASTER_SMALL 64      // pixel centres one thread covers itself
+#ifndef RASTER_SMALL
+#define RASTER_SMALL 32  // pixel centres a lane covers itself (larger: its wave); 2-32 A/B: profiles/r5_render_raster_small_ab.log
+#endif
 
 struct TriCam {
   float v0[3], e1[3], e2[3];  // the triangle in the camera frame
   int x0, x1, y0, y1;         // the pixel centres its projection can cover (inclusive; empty if x0 > x1)
+  // the projection's edges (the near-plane-clipped polygon: 3 or 4 edges) as pixel-space half
+  // planes ea x + eb y + ec >= 0 (unit normals, a tolerance folded into ec): a cheap conservative
+  // reject before the ray test, which alone decides coverage
+  float ea[4], eb[4], ec[4];
 };
 
-// the triangle in the camera frame and the range of pixel centres it can cover: its vertices in
-// front of the near plane and the points where its edges cross it, projected to image-plane slopes
+// the triangle in the camera frame, its near-plane-clipped projection (vertices in front of the
+// near plane and the points where edges cross it) in pixel coordinates, the range of pixel centres
+// that projection can cover and its edges
 __device__ __forceinline__ void tri_setup(const RenderArgs& a, const float4* tp, const float* R, const float* c,
                                           float tanh_, float aspect, TriCam& T) {
-  // no FMA contraction here and in tri_cover: a triangle covered by raster_kernel and one covered by
-  // raster_big_kernel must give bit-identical depths whichever kernel (and inlining) computed them
+  // no FMA contraction here and in tri_cover: a triangle's depths must be bit-identical whichever
+  // path covered it (its own lane or its wave) and however the compiler inlined it
 #pragma clang fp contract(off)
   const float4 A = tp[0], B = tp[1], C = tp[2];
   const float l0[3] = {A.x, A.y, A.z}, l1[3] = {A.w, B.x, B.y}, l2[3] = {B.z, B.w, C.x};
@@ -292,46 +296,72 @@ __device__ __forceinline__ void tri_setup(const RenderArgs& a, const float4* tp,
   }
   const int W = a.cam.width, H = a.cam.height;
   const float znear = a.cam.znear;
+  const float fx = 0.5f * W / (tanh_ * aspect), fy = 0.5f * H / tanh_;
   const float P[3][3] = {{T.v0[0], T.v0[1], T.v0[2]},
                          {T.v0[0] + T.e1[0], T.v0[1] + T.e1[1], T.v0[2] + T.e1[2]},
                          {T.v0[0] + T.e2[0], T.v0[1] + T.e2[1], T.v0[2] + T.e2[2]}};
-  float xl = 1e30f, xh = -1e30f, yl = 1e30f, yh = -1e30f;
-  int nin = 0;
+  // the clipped polygon in pixel coordinates (pixel centre (px, py) at (px + 0.5, py + 0.5))
+  float X[4], Y[4];
+  int n = 0;
+#pragma unroll
   for (int u = 0; u < 3; u++) {
-    const float zu = -P[u][2];
-    if (zu >= znear) {
-      ++nin;
-      const float iz = 1.f / zu;
-      xl = fminf(xl, P[u][0] * iz);
-      xh = fmaxf(xh, P[u][0] * iz);
-      yl = fminf(yl, P[u][1] * iz);
-      yh = fmaxf(yh, P[u][1] * iz);
-    }
     const int w = (u + 1) % 3;
-    const float zw = -P[w][2];
+    const float zu = -P[u][2], zw = -P[w][2];
+    if (zu >= znear) {
+      const float iz = 1.f / zu;
+      X[n] = P[u][0] * iz * fx + 0.5f * W;
+      Y[n] = 0.5f * H - P[u][1] * iz * fy;
+      ++n;
+    }
     if ((zu >= znear) != (zw >= znear)) {  // the edge crosses the near plane
       const float s = (znear - zu) / (zw - zu);
       const float x = P[u][0] + s * (P[w][0] - P[u][0]), y = P[u][1] + s * (P[w][1] - P[u][1]);
       const float iz = 1.f / znear;
-      xl = fminf(xl, x * iz);
-      xh = fmaxf(xh, x * iz);
-      yl = fminf(yl, y * iz);
-      yh = fmaxf(yh, y * iz);
+      X[n] = x * iz * fx + 0.5f * W;
+      Y[n] = 0.5f * H - y * iz * fy;
+      ++n;
     }
   }
   T.x0 = 1;
   T.x1 = 0;
   T.y0 = T.y1 = 0;
-  if (nin == 0) return;  // entirely in front of the camera's near plane: clipped
-  // pixel-centre ranges: the centre of column px has slope ((px + 0.5) 2 / W - 1) tanh aspect; a
-  // hair wider than the projection (the ray test decides coverage)
-  const float fx = 0.5f * W / (tanh_ * aspect), fy = 0.5f * H / tanh_, eps = 1e-3f;
-  const float cx0 = fmaxf(xl * fx + 0.5f * W - 0.5f - eps, -1.f), cx1 = fminf(xh * fx + 0.5f * W - 0.5f + eps, (float)W);
-  const float cy0 = fmaxf(0.5f * H - yh * fy - 0.5f - eps, -1.f), cy1 = fminf(0.5f * H - yl * fy - 0.5f + eps, (float)H);
-  T.x0 = max((int)ceilf(cx0), 0);
-  T.x1 = min((int)floorf(cx1), W - 1);
-  T.y0 = max((int)ceilf(cy0), 0);
-  T.y1 = min((int)floorf(cy1), H - 1);
+  if (n < 3) return;  // entirely in front of the camera's near plane: clipped
+  if (n == 3) {
+    X[3] = X[2];
+    Y[3] = Y[2];
+  }
+  float xl = fminf(fminf(X[0], X[1]), fminf(X[2], X[3])), xh = fmaxf(fmaxf(X[0], X[1]), fmaxf(X[2], X[3]));
+  float yl = fminf(fminf(Y[0], Y[1]), fminf(Y[2], Y[3])), yh = fmaxf(fmaxf(Y[0], Y[1]), fmaxf(Y[2], Y[3]));
+  // pixel-centre ranges a hair wider than the projection
+  const float eps = 1e-3f;
+  T.x0 = max((int)ceilf(fmaxf(xl - 0.5f - eps, -1.f)), 0);
+  T.x1 = min((int)floorf(fminf(xh - 0.5f + eps, (float)W)), W - 1);
+  T.y0 = max((int)ceilf(fmaxf(yl - 0.5f - eps, -1.f)), 0);
+  T.y1 = min((int)floorf(fminf(yh - 0.5f + eps, (float)H)), H - 1);
+  // edges: inside is where every unit-normal edge function is >= -tol, oriented by the polygon's
+  // signed area; tol = 0.02 px plus the rounding of the edge function at this coordinate magnitude
+  float area2 = 0.f;
+#pragma unroll
+  for (int i = 0; i < 4; i++) area2 += X[i] * Y[(i + 1) & 3] - X[(i + 1) & 3] * Y[i];
+  const float orient = area2 >= 0.f ? -1.f : 1.f;
+  const float mag = fmaxf(fmaxf(fabsf(xl), fabsf(xh)), fmaxf(fabsf(yl), fabsf(yh))) + (float)(W + H);
+#pragma unroll
+  for (int i = 0; i < 4; i++) {
+    const int k = (i + 1) & 3;
+    const float dx = X[k] - X[i], dy = Y[k] - Y[i];
+    const float len = sqrtf(dx * dx + dy * dy);
+    if (!(len > 1e-6f * mag)) {  // a collapsed edge (or the repeated vertex of a triangle): no constraint
+      T.ea[i] = 0.f;
+      T.eb[i] = 0.f;
+      T.ec[i] = 1.f;
+      continue;
+    }
+    const float il = orient / len;
+    // E(x, y) = (x - Xi) dy - (y - Yi) dx, negative inside for a positive area
+    T.ea[i] = dy * il;
+    T.eb[i] = -dx * il;
+    T.ec[i] = (Y[i] * dx - X[i] * dy) * il + 0.02f + 4e-6f * mag;
+  }
 }
 
 // one pixel centre: its camera ray (origin 0) against the triangle (Moller-Trumbore); the nearest
@@ -340,14 +370,22 @@ __device__ __forceinline__ void tri_cover(const RenderArgs& a, const TriCam& T, 
                                           float tanh_, float aspect, unsigned long long* vis, uint8_t* tflag) {
 #pragma clang fp contract(off)
   const int W = a.cam.width, H = a.cam.height;
-  const float d[3] = {((2.0f * (px + 0.5f) / W) - 1.0f) * tanh_ * aspect, (1.0f - 2.0f * (py + 0.5f) / H) * tanh_,
-                      -1.0f};
+  {
+    const float cx = px + 0.5f, cy = py + 0.5f;
+    bool in = true;
+#pragma unroll
+    for (int i = 0; i < 4; i++) in = in && (T.ea[i] * cx + T.eb[i] * cy + T.ec[i] >= 0.f);
+    if (!in) return;  // outside the projection (conservatively): the ray cannot hit the triangle
+  }
+  // the pixel centre's ray (slopes by multiplication: no division per pixel)
+  const float sx = tanh_ * aspect, sy = tanh_;
+  const float d[3] = {(px + 0.5f) * (2.0f * sx / W) - sx, sy - (py + 0.5f) * (2.0f * sy / H), -1.0f};
   const float* e1 = T.e1;
   const float* e2 = T.e2;
   const float p[3] = {d[1] * e2[2] - d[2] * e2[1], d[2] * e2[0] - d[0] * e2[2], d[0] * e2[1] - d[1] * e2[0]};
   const float det = e1[0] * p[0] + e1[1] * p[1] + e1[2] * p[2];
   if (fabsf(det) < 1e-30f) return;
-  const float id = 1.0f / det;
+  const float id = __builtin_amdgcn_rcpf(det);  // (1 ulp; the barycentric bounds and depth tolerate it)
   const float s[3] = {-T.v0[0], -T.v0[1], -T.v0[2]};
   const float uu = (s[0] * p[0] + s[1] * p[1] + s[2] * p[2]) * id;
   if (uu < 0.f || uu > 1.f) return;
@@ -356,7 +394,15 @@ __device__ __forceinline__ void tri_cover(const RenderArgs& a, const TriCam& T, 
   if (vv < 0.f || uu + vv > 1.f) return;
   const float t = (e2[0] * qv[0] + e2[1] * qv[1] + e2[2] * qv[2]) * id;
   if (!(t > a.cam.znear)) return;
-  atomicMin(vis + (size_t)py * W + px, ((unsigned long long)__float_as_uint(t) << 32) | j);
+  unsigned long long* slot = vis + (size_t)py * W + px;
+  const unsigned long long key = ((unsigned long long)__float_as_uint(t) << 32) | j;
+  // the key only ever decreases, so a value read earlier (older) that is already <= key proves the
+  // atomic would not change it: skip it (most covered pixels of a mesh are overdrawn)
+  if (a.dbg & 8) {  // (timing probe: the ray tests without the visibility writes)
+    if (t == 12345.f) *slot = key;
+    return;
+  }
+  if (__hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) > key) atomicMin(slot, key);
   tflag[(py / RENDER_TILE) * a.tiles_x + px / RENDER_TILE] = 1;  // (every writer stores the same 1)
 }
 
@@ -395,59 +441,61 @@ __global__ void __launch_bounds__(RASTER_THREADS) raster_kernel(RenderArgs a, in
   const float tanh_ = tanf(0.5f * a.cam.fovy_deg * 3.14159265358979f / 180.0f);
   const float aspect = (float)a.cam.width / (float)a.cam.height;
   mesh_frames_block(a, env, cf, mR, mc, mvis, tanh_, aspect);
+  if (a.dbg & 2) return;  // (timing probe: the per-block frames only)
+  // every lane stays to the end (the wave's pixel work is shared by all 64 lanes below)
   const int j = chunk * RASTER_THREADS + threadIdx.x;
-  if (j >= a.ntri) return;
-  const float4* tp = reinterpret_cast<const float4*>(a.mesh_tri) + 4 * (size_t)j;
-  const int k = __float_as_int(tp[3].x) >> 16;
-  if (k < 0 || k >= a.nmesh || !mvis[k]) return;
   TriCam T;
-  tri_setup(a, tp, mR[k], mc[k], tanh_, aspect, T);
-  if (T.x0 > T.x1 || T.y0 > T.y1) return;
-  const int span = (T.x1 - T.x0 + 1) * (T.y1 - T.y0 + 1);
-  if (span > RASTER_SMALL) {  // a large projection: queued for a whole block, when the queue has room
-    const unsigned long long slot = atomicAdd(a.big, 1ull);
-    if (slot < (unsigned long long)a.big_cap) {
-      a.big[1 + slot] = ((unsigned long long)env << 32) | (unsigned)j;
-      return;
-    }
-  }
-  unsigned long long* vis = a.vis + (size_t)env * a.cam.width * a.cam.height;
-  uint8_t* tflag = a.tflag + (size_t)env * a.tiles_x * a.tiles_y;
-  for (int py = T.y0; py <= T.y1; ++py)
-    for (int px = T.x0; px <= T.x1; ++px) tri_cover(a, T, (unsigned)j, px, py, tanh_, aspect, vis, tflag);
-}
-
-// the queued large triangles: one block per entry (grid-stride over the queue), the block's threads
-// over the triangle's pixel centres
-__global__ void __launch_bounds__(RASTER_THREADS) raster_big_kernel(RenderArgs a) {
-  __shared__ CamFrame cf;
-  __shared__ float mR[MAX_MESH][9], mc[MAX_MESH][3];
-  __shared__ int mvis[MAX_MESH];
-  const unsigned long long nq = min(*(volatile const unsigned long long*)a.big, (unsigned long long)a.big_cap);
-  const float tanh_ = tanf(0.5f * a.cam.fovy_deg * 3.14159265358979f / 180.0f);
-  const float aspect = (float)a.cam.width / (float)a.cam.height;
-  // a contiguous range of entries per block: a raster wave queues its triangles in one run of
-  // slots, all of one env, so the frames are recomputed only where the env changes
-  const unsigned long long e0 = nq * blockIdx.x / gridDim.x, e1 = nq * (blockIdx.x + 1) / gridDim.x;
-  int cur = -1;
-  for (unsigned long long e = e0; e < e1; ++e) {
-    const unsigned long long ent = a.big[1 + e];
-    const int env = (int)(ent >> 32);
-    const unsigned j = (unsigned)ent;
-    if (env != cur) {  // (block-uniform: every thread read the same entry)
-      __syncthreads();  // the previous env's frames are no longer read
-      mesh_frames_block(a, env, cf, mR, mc, mvis, tanh_, aspect);
-      cur = env;
-    }
+  T.x0 = 1;
+  T.x1 = T.y0 = T.y1 = 0;
+  if (j < a.ntri) {
     const float4* tp = reinterpret_cast<const float4*>(a.mesh_tri) + 4 * (size_t)j;
     const int k = __float_as_int(tp[3].x) >> 16;
-    TriCam T;
-    tri_setup(a, tp, mR[k], mc[k], tanh_, aspect, T);
-    const int nx = T.x1 - T.x0 + 1, ny = T.y1 - T.y0 + 1;
-    unsigned long long* vis = a.vis + (size_t)env * a.cam.width * a.cam.height;
-    uint8_t* tflag = a.tflag + (size_t)env * a.tiles_x * a.tiles_y;
-    for (int i = threadIdx.x; i < nx * ny; i += RASTER_THREADS)
-      tri_cover(a, T, j, T.x0 + i % nx, T.y0 + i / nx, tanh_, aspect, vis, tflag);
+    if (k >= 0 && k < a.nmesh && mvis[k]) tri_setup(a, tp, mR[k], mc[k], tanh_, aspect, T);
+  }
+  const bool live = T.x0 <= T.x1 && T.y0 <= T.y1 && !(a.dbg & 4);  // (dbg 4, timing probe: set-up only)
+  if ((a.dbg & 4) && T.x0 == -12345) a.vis[0] = 0;  // (keeps the probe's set-up alive)
+  const int nx = T.x1 - T.x0 + 1;
+  const int span = live ? nx * (T.y1 - T.y0 + 1) : 0;
+  unsigned long long* vis = a.vis + (size_t)env * a.cam.width * a.cam.height;
+  uint8_t* tflag = a.tflag + (size_t)env * a.tiles_x * a.tiles_y;
+  // A small projection (most: a 1 mm-LOD triangle spans a few pixels) is covered by its own lane;
+  // the wave's larger ones one after the other by all 64 lanes, the triangle broadcast from its lane
+  // by readlane.  (Dealing all of the wave's pixel centres out evenly over the lanes -- a scan and a
+  // max-scan through LDS per 64 centres -- measured 2x slower: latency-bound LDS round trips.)
+  if (live && span <= RASTER_SMALL)
+    for (int py = T.y0; py <= T.y1; ++py)
+      for (int px = T.x0; px <= T.x1; ++px) tri_cover(a, T, (unsigned)j, px, py, tanh_, aspect, vis, tflag);
+  unsigned long long bigs = __ballot(live && span > RASTER_SMALL);
+  const int lane = threadIdx.x & 63;
+  while (bigs) {
+    const int l = __builtin_ctzll(bigs);
+    bigs &= bigs - 1;
+    TriCam B;
+    for (int i = 0; i < 3; i++) {
+      B.v0[i] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(T.v0[i]), l));
+      B.e1[i] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(T.e1[i]), l));
+      B.e2[i] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(T.e2[i]), l));
+    }
+    for (int i = 0; i < 4; i++) {
+      B.ea[i] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(T.ea[i]), l));
+      B.eb[i] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(T.eb[i]), l));
+      B.ec[i] = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(T.ec[i]), l));
+    }
+    const int bx0 = __builtin_amdgcn_readlane(T.x0, l), by0 = __builtin_amdgcn_readlane(T.y0, l);
+    const int bnx = __builtin_amdgcn_readlane(nx, l), np = __builtin_amdgcn_readlane(span, l);
+    const unsigned jb = (unsigned)__builtin_amdgcn_readlane(j, l);
+    // lane i walks centres i, i + 64, ...: row and column stepped (64 = q nx + r), no division
+    const int q = 64 / bnx, r = 64 - q * bnx;
+    int yy = lane / bnx, xx = lane - yy * bnx;
+    for (int i = lane; i < np; i += 64) {
+      tri_cover(a, B, jb, bx0 + xx, by0 + yy, tanh_, aspect, vis, tflag);
+      xx += r;
+      yy += q;
+      if (xx >= bnx) {
+        xx -= bnx;
+        ++yy;
+      }
+    }
   }
 }
 
@@ -804,11 +852,10 @@ extern "C" int rmbx_render_scene(const rmbx_camera* cam, const rmbx_scene_tables
   const bool meshes = scene->ntri > 0;
   RMBX_CHECK_ARG(scene->ntri >= 0 && scene->ntri < (1 << 26) && scene->nmesh >= 0 && scene->nmesh <= MAX_MESH,
                  "bad mesh sizes (ntri=%d, nmesh=%d, at most %d mesh bodies)", scene->ntri, scene->nmesh, MAX_MESH);
-  RMBX_CHECK_ARG(!meshes || (scene->mesh_tri && scene->mesh_body && scene->mesh_rad && scene->vis && scene->big &&
+  RMBX_CHECK_ARG(!meshes || (scene->mesh_tri && scene->mesh_body && scene->mesh_rad && scene->vis &&
                              scene->tflag &&
                              scene->nmesh > 0 && (((uintptr_t)scene->mesh_tri | (uintptr_t)scene->vis) & 15) == 0),
-                 "meshes need mesh_tri / mesh_body / mesh_rad / vis (16-byte aligned) / big and nmesh > 0");
-  RMBX_CHECK_ARG(!meshes || scene->big_cap >= 0, "bad big_cap %lld", (long long)scene->big_cap);
+                 "meshes need mesh_tri / mesh_body / mesh_rad / vis (16-byte aligned) / tflag and nmesh > 0");
   if (n_env == 0) return RMBX_OK;
   rmbx::RenderArgs a;
   a.cam = *cam;
@@ -821,8 +868,6 @@ extern "C" int rmbx_render_scene(const rmbx_camera* cam, const rmbx_scene_tables
   a.mesh_body = scene->mesh_body;
   a.mesh_rad = scene->mesh_rad;
   a.vis = meshes ? scene->vis : nullptr;
-  a.big = meshes ? scene->big : nullptr;
-  a.big_cap = meshes ? scene->big_cap : 0;
   a.tflag = meshes ? scene->tflag : nullptr;
   a.hit_geom = hit_geom;
   a.gxpos = gxpos;
@@ -848,13 +893,10 @@ extern "C" int rmbx_render_scene(const rmbx_camera* cam, const rmbx_scene_tables
   if (meshes) {
     // pass 1: the meshes' nearest triangle per pixel into the visibility buffer (empty on entry:
     // the ray-cast pass clears every key and tile flag it consumes)
-    RMBX_CHECK_HIP(hipMemsetAsync(scene->big, 0, sizeof(unsigned long long), st));
     const int chunks = (scene->ntri + RASTER_THREADS - 1) / RASTER_THREADS;
     const size_t rblocks = (size_t)chunks * n_env;
     RMBX_CHECK_ARG(rblocks < (1ull << 31), "raster grid too large");
     hipLaunchKernelGGL(rmbx::raster_kernel, dim3((unsigned)rblocks), dim3(RASTER_THREADS), 0, st, a, chunks);
-    RMBX_CHECK_LAUNCH();
-    hipLaunchKernelGGL(rmbx::raster_big_kernel, dim3(2048), dim3(RASTER_THREADS), 0, st, a);
     RMBX_CHECK_LAUNCH();
     hipLaunchKernelGGL(rmbx::render_kernel<true>, dim3((unsigned)nblocks), dim3(256), 0, st, a);
   } else {

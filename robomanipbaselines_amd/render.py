@@ -21,7 +21,6 @@ from .mjcf import compiler as C
 
 IMAGENET_MEAN = (0.485, 0.456, 0.406)
 IMAGENET_STD = (0.229, 0.224, 0.225)
-BIG_PER_ENV = 8192  # RMBX_RENDER_BIG_PER_ENV (include/rmbx.h): large-triangle queue entries per env
 
 
 def build_prims(arrays):
@@ -95,7 +94,6 @@ class Renderer:
         else:
             self.mesh_tri = self.mesh_body = self.mesh_rad = None
         self._vis = None  # visibility workspace u64 [n, H, W], allocated at the first render
-        self._big = None  # large-triangle queue u64 [1 + RMBX_RENDER_BIG_PER_ENV n]
         self._tflag = None  # tiles the visibility pass wrote, u8 [n, tiles]
         sc = N.SceneTables()
         sc.prim_i32, sc.prim_f32, sc.nprim = self.prim_i32.data_ptr(), self.prim_f32.data_ptr(), self.nprim
@@ -155,15 +153,11 @@ class Renderer:
             assert hit_geom.dtype == torch.int32 and tuple(hit_geom.shape) == (n, H, W) and hit_geom.is_contiguous()
         if self.mesh_tri is not None:
             ntiles = -(-H // 16) * -(-W // 16)
-            if (self._vis is None or self._vis.shape[0] < n * H * W or self._tflag.shape[0] < n * ntiles
-                    or self._big.shape[0] < 1 + BIG_PER_ENV * n):
+            if self._vis is None or self._vis.shape[0] < n * H * W or self._tflag.shape[0] < n * ntiles:
                 # empty on entry to every call (the call leaves them so): all-ones keys, zero flags
                 self._vis = torch.full((n * H * W,), -1, dtype=torch.int64, device=self.device)
                 self._tflag = torch.zeros(n * ntiles, dtype=torch.uint8, device=self.device)
-                self._big = torch.empty(1 + BIG_PER_ENV * n, dtype=torch.int64, device=self.device)
-            self._scene.vis, self._scene.big = self._vis.data_ptr(), self._big.data_ptr()
-            self._scene.big_cap = self._big.shape[0] - 1
-            self._scene.tflag = self._tflag.data_ptr()
+            self._scene.vis, self._scene.tflag = self._vis.data_ptr(), self._tflag.data_ptr()
         N.call("rmbx_render_scene", ctypes.byref(cam), ctypes.byref(self._scene),
                N.ptr(engine.gxpos), N.ptr(engine.gxmat), N.ptr(engine.xpos), N.ptr(engine.xquat),
                engine.ngeom, engine.nbody, N.ptr(rgb), N.ptr(depth), N.ptr(hit_geom), N.ptr(policy), pdt,

@@ -3,6 +3,7 @@
   slp -- rmbx_gemm.hip without -fno-slp-vectorize (the SLP vectorizer's packed f32 split ops);
   render4 .. render7 -- rmbx_render.hip with its registers for 4 (unconstrained) .. 7 waves per
   SIMD (the default build targets 8);
+  rsmall<N> -- rmbx_render.hip with RASTER_SMALL = N (pixel centres a lane covers itself);
   hoist -- rmbx_engine.hip with the solver's per-iteration addresses hoisted out of the Newton loop
   (RMBX_SOLVER_HOIST: the round-3 code generation, spilled at 128 registers);
   at-<rev> -- every csrc/*.hip source as of git revision <rev> (headers from the working tree): the
@@ -20,6 +21,8 @@ if name == "slp":
 elif name in ("render4", "render5", "render6", "render7"):
     w = 1 if name == "render4" else int(name[-1])
     B.FILE_FLAGS = dict(B.FILE_FLAGS, **{"rmbx_render.hip": [f"-DRMBX_RENDER_MINW={w}"]})
+elif name.startswith("rsmall"):
+    B.FILE_FLAGS = dict(B.FILE_FLAGS, **{"rmbx_render.hip": [f"-DRASTER_SMALL={int(name[6:])}"]})
 elif name == "hoist":
     B.FILE_FLAGS = dict(B.FILE_FLAGS, **{"rmbx_engine.hip": ["-DRMBX_SOLVER_HOIST"]})
 elif name.startswith("at-"):

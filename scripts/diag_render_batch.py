@@ -30,7 +30,6 @@ for cam in big.camera_names:
         depth = torch.empty((n, H, W), dtype=torch.float32, device=dev)
         hit = torch.empty((n, H, W), dtype=torch.int32, device=dev)
         env.renderer.render(env.engine, cam, rgb=rgb, depth=depth, hit_geom=hit)
-        print(f"{cam} {tag}: queued large triangles {int(env.renderer._big[0])}", flush=True)
         out[tag] = (rgb[:512].clone(), depth[:512].clone(), hit[:512].clone())
     for a_, b_ in (("b1", "b2"), ("b1", "s")):
         dr = (out[a_][0] != out[b_][0]).any(-1)
