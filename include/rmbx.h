@@ -507,6 +507,17 @@ int rmbx_linear_f16x3_batched(const float* a, long long lda, long long a_bs, con
                               long long w_plane_stride, long long w_bs, const float* w_scale, long long ws_bs,
                               const float* bias, float* c, long long ldc, long long c_bs, int batch, int M, int N,
                               int K, int relu, void* stream);
+/* rmbx_linear_f16x3 with the activations already split by their producer (rmbx_add_layernorm_split):
+ * a_planes [2][M][K] f16 bits (plane stride a_plane_stride, row stride lda elements, both multiples
+ * of 8) with a[m] = a_rinv[m] (hi + lo), hi = f16(a[m] 2^t_m), lo = f16(a[m] 2^t_m - hi), 2^t_m putting
+ * the row's max |a| in [2^13, 2^14) and a_rinv[m] = 2^-t_m.  Both operands move by LDS-DMA, no split
+ * or range pass in the GEMM.  c = relu?(a . w^T + bias + res) (bias / res nullable, res [M][ldc]);
+ * N % 128 == 0, K % 32 == 0, 16-byte aligned operands, ldc % 4 == 0.  Replaces the same nn.Linear
+ * call sites as rmbx_linear_f16x3 (ACT transformer in-projections and FFN, third_party/act). */
+int rmbx_linear_f16x3_presplit(const void* a_planes, long long lda, long long a_plane_stride, const float* a_rinv,
+                               const void* w_planes, long long ldw, long long w_plane_stride, const float* w_scale,
+                               const float* bias, const float* res, float* c, long long ldc, int M, int N, int K,
+                               int relu, void* stream);
 /* 3x3 / stride-1 / pad-1 rmbx_conv2d_f16x3 with each input pixel split once per output tile: the
  * block stages the input patch of its 16 x 16 (Cout % 128 == 0) or 16 x 32 output tile for one
  * 32-channel chunk as two f16 pieces in LDS, scaled per (tile, chunk) by a power of two, and all
@@ -544,6 +555,14 @@ int rmbx_add_layernorm(const void* x, const void* r, const float* weight, const 
 int rmbx_add_layernorm_pos(const void* x, const void* r, const float* weight, const float* bias, void* out,
                            const void* pos, int pos_rows, void* out_pos, int rows, int D, float eps, int dtype,
                            void* stream);
+/* f32 rmbx_add_layernorm_pos that also emits its outputs in rmbx_linear_f16x3_presplit's A form:
+ * y = LayerNorm(rnd(x + r)) (out f32, nullable), y_planes [2][rows][D] + y_rinv [rows] (nullable
+ * together), y + pos[row % pos_rows] (out_pos f32 and pos_planes + pos_rinv, each nullable; pos
+ * needed if either is set); every row's scale from that row alone (batch-invariant).  D % 4 == 0,
+ * 8-byte aligned planes. */
+int rmbx_add_layernorm_split(const float* x, const float* r, const float* weight, const float* bias, float* out,
+                             void* y_planes, float* y_rinv, const float* pos, int pos_rows, float* out_pos,
+                             void* pos_planes, float* pos_rinv, int rows, int D, float eps, void* stream);
 /* out [N][Ho][Wo][C] = maxpool3x3s2p1(relu(rnd(x + bias))), Ho = (H-1)/2+1, Wo = (W-1)/2+1. */
 int rmbx_nhwc_bias_relu_maxpool(const void* x, const float* bias, void* out, int N, int H, int W,
                                 int C, int dtype, void* stream);

@@ -1080,6 +1080,331 @@ __global__ void __launch_bounds__(256) split_f16x2_kernel(const float* __restric
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// Pre-split A form of the f16x3 kernel (rmbx_linear_f16x3_presplit): A arrives already split by its
+// producer (rmbx_add_layernorm_split: each row scaled by a power of two 2^t_m with its max |a| in
+// [2^13, 2^14), a' = a 2^t_m = ha + la, ha = f16(a'), la = f16(a' - ha) -- the weight rows' split),
+// as two f16 planes [M][K] and the rows' 2^-t_m.  Both operands then move by LDS-DMA
+// (global_load_lds_dwordx4, the W pieces' layout and swizzle for A too): no A registers, no split,
+// no per-row range check or re-run pass (the producer chose each row's scale), and the three
+// products take the raw pieces, a'.w' ~ ha hb + ha lb + la hb (dropped term <= 2^-22 |a' w'|,
+// pieces below 2^-16 of their row's max are f16 subnormals, as for W).  The epilogue applies
+// 2^-t_m 1 / s_n (powers of two: exact), then bias / residual / ReLU.  Two LDS stages: step kt
+// computes stage kt while the DMA of kt + 1 is in flight, one barrier per step.  Tile 256 x BN,
+// 8 waves (wave = 64 x BN / 2), the same XCD / group mapping as gemm_f32x6_kernel.
+// N % 256 == 128 (FFN1's 3200 columns): the last column tile's second half is dead -- its waves
+// skip the fragment reads and MFMAs, its W rows re-read row N - 1, nothing is stored -- so every
+// column tile of a row band runs in one launch and the band's A is fetched once into the XCD's L2
+// (a separate 128-wide launch re-read all of A for 4 % of the work).  GROUP row tiles per block
+// group (the rasterisation: all column tiles of GROUP row tiles, row tile fastest).
+// VAR (profiling phase skips, RMBX_PRESPLIT_VAR; wrong results, timing only): bit 0 = no DMA after
+// the first stage, bit 1 = no fragment reads / MFMAs, bit 2 = no output stores
+template <int BN, int GROUP, int VAR = 0>
+__global__ void __launch_bounds__(GM_THREADS, 1) gemm_f16x3_presplit_kernel(GemmArgs g, const uint16_t* __restrict__ Ap,
+                                                                           long long aps, long long ldah,
+                                                                           const float* __restrict__ arinv) {
+  static_assert(BN == 128 || BN == 256, "the 128- and 256-wide tiles");
+  constexpr int NJ = BN / 32;                                 // 16-column accumulator tiles per wave
+  constexpr int A_PIECES = 2 * (GM_BM / 16), B_PIECES = 2 * (BN / 16);  // 16 rows x 64 B per piece
+  constexpr int PIECES = A_PIECES + B_PIECES, PW = PIECES / 8;          // per wave and K step
+  static_assert(PIECES % 8 == 0, "pieces split evenly over the 8 waves");
+  constexpr int A_BYTES = 2 * GM_A_PLANE, B_PLANE = gm_b_plane<BN>(), STAGE = A_BYTES + 2 * B_PLANE;
+  constexpr int EPI = gm_epi_bytes<BN>();
+  constexpr int SMEM = 2 * STAGE > EPI ? 2 * STAGE : EPI;
+  static_assert(SMEM <= 160 * 1024, "the LDS of a CU");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 3, wn = wave >> 2;
+  const int nblk = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q = nblk >> 3, r = nblk & 7;
+  const int lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int per_group = GROUP * g.tiles_n;
+  const int first_m = (lin / per_group) * GROUP;
+  const int gsize = min(g.tiles_m - first_m, GROUP);
+  const int in_group = lin - (lin / per_group) * per_group;
+  const int tm = first_m + in_group % gsize, tn = in_group / gsize;
+  const int m0 = tm * GM_BM, n0 = tn * BN;
+  const bool dead = n0 + wn * (BN / 2) >= g.N;  // (wave-uniform) the half tile past N
+
+  // the wave's DMA pieces: piece i < A_PIECES is A plane i / 16, rows 16 (i % 16)..; the rest W
+  // plane, rows as in gemm_f32x6_kernel.  Lane l moves row (l / 4) of the piece, logical 8-k slot
+  // (l % 4) ^ ((row >> 2) & 2) to physical slot l % 4 (the fragment reads' swizzle).  A rows past M
+  // re-read row M - 1 (their outputs are not stored).
+  const uint16_t* src[PW];
+  int dst[PW];
+#pragma unroll
+  for (int t = 0; t < PW; ++t) {
+    const int i = wave * PW + t;
+    if (i < A_PIECES) {
+      const int p = i / (GM_BM / 16), row = (i % (GM_BM / 16)) * 16 + (lane >> 2);
+      const int sl = (lane & 3) ^ ((row >> 2) & 2);
+      src[t] = Ap + p * aps + (long long)min(m0 + row, g.M - 1) * ldah + sl * 8;
+      dst[t] = p * GM_A_PLANE + (i % (GM_BM / 16)) * 1024;
+    } else {
+      const int j = i - A_PIECES, p = j / (BN / 16), row = (j % (BN / 16)) * 16 + (lane >> 2);
+      const int sl = (lane & 3) ^ ((row >> 2) & 2);
+      src[t] = g.W + p * g.wps + (long long)min(n0 + row, g.N - 1) * g.ldw + sl * 8;
+      dst[t] = A_BYTES + p * B_PLANE + (j % (BN / 16)) * 1024;
+    }
+  }
+  auto stage = [&](int kt, int buf) {
+#pragma unroll
+    for (int t = 0; t < PW; ++t) glds16(src[t] + kt * GM_BK, smem + buf * STAGE + dst[t]);
+  };
+
+  f32x4v acc[4][NJ];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = (f32x4v){0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fs = lane >> 4;
+  auto frag_off = [&](int row) { return row * 64 + ((fs ^ ((row >> 2) & 2)) << 4); };
+
+  const int KT = g.K / GM_BK;
+  stage(0, 0);
+  wait_vm<0>();
+  asm volatile("s_barrier" ::: "memory");
+  for (int kt = 0; kt < KT; ++kt) {
+    const int buf = kt & 1;
+    // the next stage's DMA (its buffer was last read in step kt - 1, which the barrier closed)
+    if (kt + 1 < KT && !(VAR & 1)) stage(kt + 1, buf ^ 1);
+    const unsigned char* S = smem + buf * STAGE;
+    f16x8 ah[4], al[4];
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) {
+      const int off = frag_off(wm * 64 + mi * 16 + fr);
+      ah[mi] = *(const f16x8*)(S + off);
+      al[mi] = *(const f16x8*)(S + GM_A_PLANE + off);
+    }
+    if (!dead && !(VAR & 2))
+#pragma unroll
+    for (int nj = 0; nj < NJ; ++nj) {
+      const int off = frag_off(wn * (BN / 2) + nj * 16 + fr);
+      const f16x8 bh = *(const f16x8*)(S + A_BYTES + off);
+      const f16x8 bl = *(const f16x8*)(S + A_BYTES + B_PLANE + off);
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        f32x4v c = acc[mi][nj];
+        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[mi], bh, c, 0, 0, 0);  // small terms first
+        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[mi], bl, c, 0, 0, 0);
+        c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[mi], bh, c, 0, 0, 0);
+        acc[mi][nj] = c;
+      }
+    }
+    wait_vm<0>();  // the next stage has landed
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+
+  // epilogue through LDS (each wave's 64 x BN/2 tile in passes of 64 columns, row pitch 68 floats),
+  // then 16-byte stores: C = acc 2^-t_m / s_n + bias (+ res) (ReLU)
+  constexpr int WC = 64, PITCH = WC + 4, LPR = WC / 4, RPI = 64 / LPR;
+  constexpr int NPASS = (BN / 2) / WC, NJP = NJ / NPASS;
+  float* T = reinterpret_cast<float*>(smem) + wave * (64 * PITCH);
+  if (dead) return;  // (after the K loop's last barrier: no block-wide synchronisation follows)
+#pragma unroll
+  for (int pass = 0; pass < NPASS; ++pass) {
+    if (pass > 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int qq = 0; qq < NJP; ++qq)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) T[(mi * 16 + 4 * fs + e) * PITCH + qq * 16 + fr] = acc[mi][pass * NJP + qq][e];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const int c4 = (lane % LPR) * 4;
+    const int n = n0 + wn * (BN / 2) + pass * WC + c4;
+    float4 bn = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (g.bias) bn = *(const float4*)(g.bias + n);
+    const float4 sn = *(const float4*)(g.ws + n);
+#pragma unroll
+    for (int it = 0; it < 64 / RPI; ++it) {
+      const int rr = it * RPI + lane / LPR;
+      const int m = m0 + wm * 64 + rr;
+      if (m < g.M) {
+        float4 v = *(const float4*)(T + rr * PITCH + c4);
+        const float rs = arinv[m];
+        v.x *= rs * sn.x; v.y *= rs * sn.y; v.z *= rs * sn.z; v.w *= rs * sn.w;
+        v.x += bn.x; v.y += bn.y; v.z += bn.z; v.w += bn.w;
+        if (g.res) {
+          const float4 rv = *(const float4*)(g.res + (long long)m * g.ldc + n);
+          v.x += rv.x; v.y += rv.y; v.z += rv.z; v.w += rv.w;
+        }
+        if (g.relu) {
+          v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+        }
+        if (!(VAR & 4)) *(float4*)(g.C + (long long)m * g.ldc + n) = v;
+      }
+    }
+  }
+}
+
+// Three-ring form of the pre-split kernel (the default; RMBX_PRESPLIT_FORM=2 selects the two-stage
+// form above): the 256 x 256 tile's K steps move by LDS-DMA into an A ring of three stages and a W
+// ring of two (3 x 32 + 2 x 32 KiB = all 160 KiB of the CU's LDS), so the A pieces of step kt + 2 and
+// the W pieces of step kt + 1 are in flight while step kt computes -- half again the bytes in
+// flight of two full stages, and the DMA's L2 latency (~1.4 us per 64 KiB step measured with the
+// MFMAs skipped) is what the two-stage form could not hide.  The eight DMA issues of a wave are
+// spread over its eight column-tile MFMA groups instead of bunched at the step's start.  Per step,
+// in issue order: W(kt + 1), then A(kt + 2); the step ends waiting until at most the A(kt + 2)
+// pieces are outstanding, which retires A(kt + 1) (issued the step before) and W(kt + 1).
+template <int GROUP, int VAR = 0>
+__global__ void __launch_bounds__(GM_THREADS, 1) gemm_f16x3_presplit3_kernel(GemmArgs g, const uint16_t* __restrict__ Ap,
+                                                                            long long aps, long long ldah,
+                                                                            const float* __restrict__ arinv) {
+  constexpr int BN = 256, NJ = 8;
+  constexpr int A_STAGE = 2 * GM_A_PLANE, B_PLANE = gm_b_plane<BN>(), W_STAGE = 2 * B_PLANE;  // 32 KiB each
+  constexpr int W_RING = 3 * A_STAGE;
+  constexpr int SMEM = 3 * A_STAGE + 2 * W_STAGE;
+  static_assert(SMEM == 160 * 1024 && gm_epi_bytes<BN>() <= SMEM, "the LDS of a CU");
+  constexpr int APW = 2 * (GM_BM / 16) / 8, WPW = 2 * (BN / 16) / 8;  // DMA pieces per wave and step
+  static_assert(APW == 4 && WPW == 4 && APW + WPW == NJ, "one DMA issue per column-tile MFMA group");
+  __shared__ __attribute__((aligned(16))) unsigned char smem[SMEM];
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave & 3, wn = wave >> 2;
+  const int nblk = gridDim.x, bid = blockIdx.x;
+  const int xcd = bid & 7, q = nblk >> 3, r = nblk & 7;
+  const int lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  const int per_group = GROUP * g.tiles_n;
+  const int first_m = (lin / per_group) * GROUP;
+  const int gsize = min(g.tiles_m - first_m, GROUP);
+  const int in_group = lin - (lin / per_group) * per_group;
+  const int tm = first_m + in_group % gsize, tn = in_group / gsize;
+  const int m0 = tm * GM_BM, n0 = tn * BN;
+  const bool dead = n0 + wn * (BN / 2) >= g.N;  // (wave-uniform) the half tile past N
+
+  // the wave's pieces (16 rows x 64 B; lane l moves row l / 4, logical slot (l % 4) ^ ((row >> 2) & 2)
+  // to physical slot l % 4): A pieces 4 wave .. 4 wave + 3 of the 32 (plane i / 16), W likewise
+  const uint16_t* asrc[APW];
+  const uint16_t* wsrc[WPW];
+  int adst[APW], wdst[WPW];
+#pragma unroll
+  for (int t = 0; t < APW; ++t) {
+    const int i = wave * APW + t, p = i / 16, rb = i % 16, row = rb * 16 + (lane >> 2);
+    const int sl = (lane & 3) ^ ((row >> 2) & 2);
+    asrc[t] = Ap + p * aps + (long long)min(m0 + row, g.M - 1) * ldah + sl * 8;
+    adst[t] = p * GM_A_PLANE + rb * 1024;
+  }
+#pragma unroll
+  for (int t = 0; t < WPW; ++t) {
+    const int i = wave * WPW + t, p = i / 16, rb = i % 16, row = rb * 16 + (lane >> 2);
+    const int sl = (lane & 3) ^ ((row >> 2) & 2);
+    wsrc[t] = g.W + p * g.wps + (long long)min(n0 + row, g.N - 1) * g.ldw + sl * 8;
+    wdst[t] = W_RING + p * B_PLANE + rb * 1024;
+  }
+  auto dma_a = [&](int t, int kt) {
+    if constexpr ((VAR & 1) == 0) glds16(asrc[t] + kt * GM_BK, smem + (kt % 3) * A_STAGE + adst[t]);
+  };
+  auto dma_w = [&](int t, int kt) {
+    if constexpr ((VAR & 1) == 0) glds16(wsrc[t] + kt * GM_BK, smem + (kt & 1) * W_STAGE + wdst[t]);
+  };
+
+  f32x4v acc[4][NJ];
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = (f32x4v){0.f, 0.f, 0.f, 0.f};
+  const int fr = lane & 15, fs = lane >> 4;
+  auto frag_off = [&](int row) { return row * 64 + ((fs ^ ((row >> 2) & 2)) << 4); };
+
+  const int KT = g.K / GM_BK;
+  // prologue: W(0), A(0), A(1)
+#pragma unroll
+  for (int t = 0; t < WPW; ++t) glds16(wsrc[t], smem + wdst[t]);
+#pragma unroll
+  for (int t = 0; t < APW; ++t) glds16(asrc[t], smem + adst[t]);
+  if (KT > 1) {
+#pragma unroll
+    for (int t = 0; t < APW; ++t) glds16(asrc[t] + GM_BK, smem + A_STAGE + adst[t]);
+    wait_vm<APW>();
+  } else {
+    wait_vm<0>();
+  }
+  asm volatile("s_barrier" ::: "memory");
+  for (int kt = 0; kt < KT; ++kt) {
+    const bool w_next = kt + 1 < KT, a_next = kt + 2 < KT;
+    const unsigned char* SA = smem + (kt % 3) * A_STAGE;
+    const unsigned char* SW = smem + W_RING + (kt & 1) * W_STAGE;
+    f16x8 ah[4], al[4];
+    if (!dead && !(VAR & 2)) {
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi) {
+        const int off = frag_off(wm * 64 + mi * 16 + fr);
+        ah[mi] = *(const f16x8*)(SA + off);
+        al[mi] = *(const f16x8*)(SA + GM_A_PLANE + off);
+      }
+    }
+#pragma unroll
+    for (int nj = 0; nj < NJ; ++nj) {
+      // one DMA issue per group: W(kt + 1) pieces first, then A(kt + 2)
+      if (nj < WPW) {
+        if (w_next) dma_w(nj, kt + 1);
+      } else {
+        if (a_next) dma_a(nj - WPW, kt + 2);
+      }
+      if (!dead && !(VAR & 2)) {
+        const int off = frag_off(wn * (BN / 2) + nj * 16 + fr);
+        const f16x8 bh = *(const f16x8*)(SW + off);
+        const f16x8 bl = *(const f16x8*)(SW + B_PLANE + off);
+#pragma unroll
+        for (int mi = 0; mi < 4; ++mi) {
+          f32x4v c = acc[mi][nj];
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(al[mi], bh, c, 0, 0, 0);  // small terms first
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[mi], bl, c, 0, 0, 0);
+          c = __builtin_amdgcn_mfma_f32_16x16x32_f16(ah[mi], bh, c, 0, 0, 0);
+          acc[mi][nj] = c;
+        }
+      }
+    }
+    if (a_next)
+      wait_vm<APW>();  // A(kt + 2) may stay in flight
+    else
+      wait_vm<0>();
+    asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+  }
+
+  // epilogue through LDS (each wave's 64 x 128 tile in two passes of 64 columns, row pitch 68
+  // floats), then 16-byte stores: C = acc 2^-t_m / s_n + bias (+ res) (ReLU)
+  constexpr int WC = 64, PITCH = WC + 4, LPR = WC / 4, RPI = 64 / LPR;
+  constexpr int NPASS = (BN / 2) / WC, NJP = NJ / NPASS;
+  float* T = reinterpret_cast<float*>(smem) + wave * (64 * PITCH);
+  if (dead) return;  // (after the K loop's last barrier: no block-wide synchronisation follows)
+#pragma unroll
+  for (int pass = 0; pass < NPASS; ++pass) {
+    if (pass > 0) asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+      for (int qq = 0; qq < NJP; ++qq)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) T[(mi * 16 + 4 * fs + e) * PITCH + qq * 16 + fr] = acc[mi][pass * NJP + qq][e];
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    const int c4 = (lane % LPR) * 4;
+    const int n = n0 + wn * (BN / 2) + pass * WC + c4;
+    float4 bn = make_float4(0.f, 0.f, 0.f, 0.f);
+    if (g.bias) bn = *(const float4*)(g.bias + n);
+    const float4 sn = *(const float4*)(g.ws + n);
+#pragma unroll
+    for (int it = 0; it < 64 / RPI; ++it) {
+      const int rr = it * RPI + lane / LPR;
+      const int m = m0 + wm * 64 + rr;
+      if (m < g.M) {
+        float4 v = *(const float4*)(T + rr * PITCH + c4);
+        const float rs = arinv[m];
+        v.x *= rs * sn.x; v.y *= rs * sn.y; v.z *= rs * sn.z; v.w *= rs * sn.w;
+        v.x += bn.x; v.y += bn.y; v.z += bn.z; v.w += bn.w;
+        if (g.res) {
+          const float4 rv = *(const float4*)(g.res + (long long)m * g.ldc + n);
+          v.x += rv.x; v.y += rv.y; v.z += rv.z; v.w += rv.w;
+        }
+        if (g.relu) {
+          v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+        }
+        if (!(VAR & 4)) *(float4*)(g.C + (long long)m * g.ldc + n) = v;
+      }
+    }
+  }
+}
+
 // default: the LDS-transposed epilogue with 16-byte stores (VAR 16: 1.04-1.08x over 64 scalar
 // stores per lane, profiles/r3_gemm_var_sweep.log) whenever the output / residual / bias rows allow
 // 16-byte accesses; RMBX_GEMM_VAR overrides the bf16x6 form (profiling)
@@ -1313,4 +1638,73 @@ extern "C" int rmbx_conv2d_f16x3(const float* in, int N, int H, int W, int C, co
                                  int KH, int KW, int stride, int pad, int relu, void* stream) {
   return rmbx::conv_impl<2>("rmbx_conv2d_f16x3", in, N, H, W, C, w_planes, w_scale, bias, res, out, Cout, KH, KW,
                             stride, pad, relu, stream);
+}
+
+extern "C" int rmbx_linear_f16x3_presplit(const void* a_planes, long long lda, long long a_plane_stride,
+                                          const float* a_rinv, const void* w_planes, long long ldw,
+                                          long long w_plane_stride, const float* w_scale, const float* bias,
+                                          const float* res, float* c, long long ldc, int M, int N, int K, int relu,
+                                          void* stream) {
+  const char* fn = "rmbx_linear_f16x3_presplit";
+  RMBX_CHECK_ARG(a_planes && a_rinv && w_planes && w_scale && c, "%s: null pointer", fn);
+  RMBX_CHECK_ARG(M >= 0 && N > 0 && K > 0 && N % rmbx::GM_BN == 0 && K % rmbx::GM_BK == 0,
+                 "%s: bad shape M=%d N=%d K=%d (N %% 128, K %% 32)", fn, M, N, K);
+  RMBX_CHECK_ARG(lda >= K && lda % 8 == 0 && a_plane_stride % 8 == 0 && ldw >= K && ldw % 8 == 0 &&
+                     w_plane_stride % 8 == 0 && ldc >= N && ldc % 4 == 0,
+                 "%s: bad strides lda=%lld ldw=%lld ldc=%lld", fn, lda, ldw, ldc);
+  RMBX_CHECK_ARG(((uintptr_t)a_planes | (uintptr_t)w_planes | (uintptr_t)c | (uintptr_t)bias | (uintptr_t)res |
+                  (uintptr_t)w_scale) % 16 == 0,
+                 "%s: operands must be 16-B aligned", fn);
+  RMBX_CHECK_ARG((long long)M * lda + a_plane_stride < (1ll << 62), "%s: too large", fn);
+  if (M == 0) return RMBX_OK;
+  rmbx::GemmArgs g{nullptr, (const uint16_t*)w_planes, bias, c, 0, ldc, ldw, w_plane_stride, M, N, K, relu ? 1 : 0,
+                   (M + rmbx::GM_BM - 1) / rmbx::GM_BM, 0, res};
+  g.batch = 1;
+  g.ws = w_scale;
+  hipStream_t st = (hipStream_t)stream;
+  const uint16_t* ap = (const uint16_t*)a_planes;
+  // every column tile on the 256-wide tile (N % 256 == 128: the last one half dead); RMBX_PRESPLIT_GROUP
+  // (profiling, read per launch) = row tiles per block group, 8 by default
+  g.tiles_n = (N + 255) / 256;
+  const long long blocks = (long long)g.tiles_m * g.tiles_n;
+  RMBX_CHECK_ARG(blocks < (1ll << 31), "%s: too many tiles", fn);
+  const char* ge = getenv("RMBX_PRESPLIT_GROUP");
+  const int grp = ge ? atoi(ge) : 8;
+  const char* ve = getenv("RMBX_PRESPLIT_VAR");
+  const int var = ve ? atoi(ve) : 0;
+  const char* fe = getenv("RMBX_PRESPLIT_FORM");
+  const bool form2 = fe && atoi(fe) == 2;
+  if (!form2) {  // the three-ring form (default)
+    switch (var) {
+      case 0: hipLaunchKernelGGL((rmbx::gemm_f16x3_presplit3_kernel<8, 0>), dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0, st, g, ap, a_plane_stride, lda, a_rinv); break;
+      case 1: hipLaunchKernelGGL((rmbx::gemm_f16x3_presplit3_kernel<8, 1>), dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0, st, g, ap, a_plane_stride, lda, a_rinv); break;
+      case 2: hipLaunchKernelGGL((rmbx::gemm_f16x3_presplit3_kernel<8, 2>), dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0, st, g, ap, a_plane_stride, lda, a_rinv); break;
+      case 4: hipLaunchKernelGGL((rmbx::gemm_f16x3_presplit3_kernel<8, 4>), dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0, st, g, ap, a_plane_stride, lda, a_rinv); break;
+      case 5: hipLaunchKernelGGL((rmbx::gemm_f16x3_presplit3_kernel<8, 5>), dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0, st, g, ap, a_plane_stride, lda, a_rinv); break;
+      case 6: hipLaunchKernelGGL((rmbx::gemm_f16x3_presplit3_kernel<8, 6>), dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0, st, g, ap, a_plane_stride, lda, a_rinv); break;
+      default: RMBX_CHECK_ARG(false, "%s: RMBX_PRESPLIT_VAR %d", fn, var);
+    }
+    RMBX_CHECK_LAUNCH();
+    return RMBX_OK;
+  }
+  if (var != 0) {  // profiling phase skips at the default group
+    switch (var) {
+      case 1: hipLaunchKernelGGL((rmbx::gemm_f16x3_presplit_kernel<256, 8, 1>), dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0, st, g, ap, a_plane_stride, lda, a_rinv); break;
+      case 2: hipLaunchKernelGGL((rmbx::gemm_f16x3_presplit_kernel<256, 8, 2>), dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0, st, g, ap, a_plane_stride, lda, a_rinv); break;
+      case 4: hipLaunchKernelGGL((rmbx::gemm_f16x3_presplit_kernel<256, 8, 4>), dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0, st, g, ap, a_plane_stride, lda, a_rinv); break;
+      case 5: hipLaunchKernelGGL((rmbx::gemm_f16x3_presplit_kernel<256, 8, 5>), dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0, st, g, ap, a_plane_stride, lda, a_rinv); break;
+      case 6: hipLaunchKernelGGL((rmbx::gemm_f16x3_presplit_kernel<256, 8, 6>), dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0, st, g, ap, a_plane_stride, lda, a_rinv); break;
+      default: RMBX_CHECK_ARG(false, "%s: RMBX_PRESPLIT_VAR %d", fn, var);
+    }
+    RMBX_CHECK_LAUNCH();
+    return RMBX_OK;
+  }
+  switch (grp) {
+    case 2: hipLaunchKernelGGL((rmbx::gemm_f16x3_presplit_kernel<256, 2>), dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0, st, g, ap, a_plane_stride, lda, a_rinv); break;
+    case 4: hipLaunchKernelGGL((rmbx::gemm_f16x3_presplit_kernel<256, 4>), dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0, st, g, ap, a_plane_stride, lda, a_rinv); break;
+    case 16: hipLaunchKernelGGL((rmbx::gemm_f16x3_presplit_kernel<256, 16>), dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0, st, g, ap, a_plane_stride, lda, a_rinv); break;
+    default: hipLaunchKernelGGL((rmbx::gemm_f16x3_presplit_kernel<256, 8>), dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0, st, g, ap, a_plane_stride, lda, a_rinv);
+  }
+  RMBX_CHECK_LAUNCH();
+  return RMBX_OK;
 }

@@ -16,6 +16,7 @@
 #include "rmbx_common.h"
 
 #include <cstdint>
+#include <type_traits>
 
 namespace rmbx {
 namespace {
@@ -225,20 +226,30 @@ extern "C" int rmbx_nhwc_bias_relu_maxpool(const void* x, const float* bias, voi
 namespace rmbx {
 namespace {
 
+// optional pre-split outputs (f32 only, rmbx_add_layernorm_split): planes u16 [2][rows][D]
+struct LnSplit {
+  uint16_t* y_planes;
+  float* y_rinv;
+  uint16_t* pos_planes;
+  float* pos_rinv;
+  int rows;
+};
+
 template <class T, int PER>
 __global__ void __launch_bounds__(256) add_layernorm_kernel(const typename T::vec_t* __restrict__ x,
                                                             const typename T::vec_t* __restrict__ r,
                                                             const float* __restrict__ w, const float* __restrict__ b,
                                                             typename T::vec_t* __restrict__ out, int rows, int D,
                                                             float eps, const typename T::vec_t* __restrict__ pos,
-                                                            int pos_rows, typename T::vec_t* __restrict__ out_pos) {
+                                                            int pos_rows, typename T::vec_t* __restrict__ out_pos,
+                                                            LnSplit sp) {
   constexpr int V = T::VEC;
   const int lane = threadIdx.x & 63;
   const int row = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (row >= rows) return;
   const int nvec = D / V;
   const size_t base = (size_t)row * nvec;
-  float s[PER][V];
+  float s[PER][V], s2[PER][V];
   float sum = 0.f;
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
@@ -279,6 +290,7 @@ __global__ void __launch_bounds__(256) add_layernorm_kernel(const typename T::ve
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) var += __shfl_xor(var, off);
   const float rstd = rsqrtf(var / (float)D + eps);
+  float ymax = 0.f, pmax = 0.f;  // f32 split outputs: the rows' max |y| and max |y + pos|
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
     const int v = lane + q * 64;
@@ -290,18 +302,73 @@ __global__ void __launch_bounds__(256) add_layernorm_kernel(const typename T::ve
         y[k] = (s[q][k] - mean) * rstd * w[c] + b[c];
       }
       const typename T::vec_t yv = T::pack(y);
-      out[base + v] = yv;
-      if (out_pos) {
+      if (out) out[base + v] = yv;
+      float yr[V];
+      T::unpack(yv, yr);
+      if (sp.y_planes) {
+#pragma unroll
+        for (int k = 0; k < V; ++k) ymax = fmaxf(ymax, fabsf(yr[k]));
+      }
+      if (out_pos || sp.pos_planes) {
         // the next attention's query input: rnd(y + pos[row % pos_rows]) on the rounded y, as the
         // separate `x + pos` of the unfused module computes it
-        float yr[V], pv[V];
-        T::unpack(yv, yr);
+        float pv[V];
         T::unpack(pos[(size_t)(row % pos_rows) * nvec + v], pv);
 #pragma unroll
         for (int k = 0; k < V; ++k) yr[k] = yr[k] + pv[k];
-        out_pos[base + v] = T::pack(yr);
+        const typename T::vec_t pvv = T::pack(yr);
+        if (out_pos) out_pos[base + v] = pvv;
+        if (sp.pos_planes) {
+          T::unpack(pvv, yr);
+#pragma unroll
+          for (int k = 0; k < V; ++k) pmax = fmaxf(pmax, fabsf(yr[k]));
+        }
+      }
+      // keep the (rounded) values for the split pass: y in s, y + pos in s2
+      {
+        float t[V];
+        T::unpack(yv, t);
+#pragma unroll
+        for (int k = 0; k < V; ++k) s[q][k] = t[k];
+      }
+      if (sp.pos_planes) {
+#pragma unroll
+        for (int k = 0; k < V; ++k) s2[q][k] = yr[k];
       }
     }
+  }
+  if constexpr (std::is_same<T, F32>::value) {
+    // the f16x3 GEMM's pre-split A (rmbx_linear_f16x3_presplit): a' = a 2^t with the row's max |a'|
+    // in [2^13, 2^14), hi = f16(a'), lo = f16(a' - hi), and 2^-t per row
+    auto split_row = [&](float (*vals)[V], float mx, uint16_t* planes, float* rinv) {
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+      int e = 14;
+      if (mx > 0.f && mx <= 3.4e38f) frexpf(mx, &e);  // mx = f 2^e, f in [0.5, 1); NaN / inf: scale 1
+      const float sc = ldexpf(1.f, 14 - e);
+      if (lane == 0) rinv[row] = ldexpf(1.f, e - 14);
+      const size_t plane = (size_t)sp.rows * D;
+#pragma unroll
+      for (int q = 0; q < PER; ++q) {
+        const int v = lane + q * 64;
+        if (v < nvec) {
+          uint16_t h[V], l[V];
+#pragma unroll
+          for (int k = 0; k < V; ++k) {
+            const float a = vals[q][k] * sc;
+            const _Float16 hv = (_Float16)a;
+            h[k] = __builtin_bit_cast(uint16_t, hv);
+            l[k] = __builtin_bit_cast(uint16_t, (_Float16)(a - (float)hv));
+          }
+          static_assert(V == 4, "f32 rows move as float4");
+          const size_t o = (size_t)row * D + (size_t)v * V;
+          *(uint2*)(planes + o) = make_uint2(h[0] | ((uint32_t)h[1] << 16), h[2] | ((uint32_t)h[3] << 16));
+          *(uint2*)(planes + plane + o) = make_uint2(l[0] | ((uint32_t)l[1] << 16), l[2] | ((uint32_t)l[3] << 16));
+        }
+      }
+    };
+    if (sp.y_planes) split_row(s, ymax, sp.y_planes, sp.y_rinv);
+    if (sp.pos_planes) split_row(s2, pmax, sp.pos_planes, sp.pos_rinv);
   }
 }
 
@@ -317,12 +384,14 @@ extern "C" int rmbx_add_layernorm(const void* x, const void* r, const float* wei
   return rmbx_add_layernorm_pos(x, r, weight, bias, out, nullptr, 0, nullptr, rows, D, eps, dtype, stream);
 }
 
-extern "C" int rmbx_add_layernorm_pos(const void* x, const void* r, const float* weight, const float* bias, void* out,
-                                      const void* pos, int pos_rows, void* out_pos, int rows, int D, float eps,
-                                      int dtype, void* stream) {
-  RMBX_CHECK_ARG(!out_pos || (pos && pos_rows > 0), "rmbx_add_layernorm_pos: out_pos needs pos and pos_rows > 0");
+namespace {
+int add_layernorm_impl(const void* x, const void* r, const float* weight, const float* bias, void* out,
+                       const void* pos, int pos_rows, void* out_pos, int rows, int D, float eps, int dtype,
+                       void* stream, rmbx::LnSplit sp) {
+  RMBX_CHECK_ARG(!(out_pos || sp.pos_planes) || (pos && pos_rows > 0),
+                 "rmbx_add_layernorm_pos: out_pos needs pos and pos_rows > 0");
   RMBX_CHECK_ARG(((uintptr_t)pos | (uintptr_t)out_pos) % 16 == 0, "rmbx_add_layernorm_pos: unaligned");
-  RMBX_CHECK_ARG(x && weight && bias && out, "rmbx_add_layernorm: null pointer");
+  RMBX_CHECK_ARG(x && weight && bias && (out || sp.y_planes || sp.pos_planes), "rmbx_add_layernorm: null pointer");
   RMBX_CHECK_ARG(dtype == 0 || dtype == 1, "rmbx_add_layernorm: dtype must be 0 (f32) or 1 (bf16)");
   const int vec = dtype == 1 ? 8 : 4;
   RMBX_CHECK_ARG(D > 0 && D % vec == 0 && D <= 2048, "rmbx_add_layernorm: D=%d must be a multiple of %d, <= 2048",
@@ -336,33 +405,52 @@ extern "C" int rmbx_add_layernorm_pos(const void* x, const void* r, const float*
     if (nvec <= 64)
       hipLaunchKernelGGL((rmbx::add_layernorm_kernel<rmbx::BF16, 1>), dim3(grid), dim3(256), 0, s, (const uint4*)x,
                          (const uint4*)r, weight, bias, (uint4*)out, rows, D, eps, (const uint4*)pos, pos_rows,
-                         (uint4*)out_pos);
+                         (uint4*)out_pos, sp);
     else if (nvec <= 128)
       hipLaunchKernelGGL((rmbx::add_layernorm_kernel<rmbx::BF16, 2>), dim3(grid), dim3(256), 0, s, (const uint4*)x,
                          (const uint4*)r, weight, bias, (uint4*)out, rows, D, eps, (const uint4*)pos, pos_rows,
-                         (uint4*)out_pos);
+                         (uint4*)out_pos, sp);
     else
       hipLaunchKernelGGL((rmbx::add_layernorm_kernel<rmbx::BF16, 4>), dim3(grid), dim3(256), 0, s, (const uint4*)x,
                          (const uint4*)r, weight, bias, (uint4*)out, rows, D, eps, (const uint4*)pos, pos_rows,
-                         (uint4*)out_pos);
+                         (uint4*)out_pos, sp);
   } else {
     if (nvec <= 64)
       hipLaunchKernelGGL((rmbx::add_layernorm_kernel<rmbx::F32, 1>), dim3(grid), dim3(256), 0, s, (const float4*)x,
                          (const float4*)r, weight, bias, (float4*)out, rows, D, eps, (const float4*)pos, pos_rows,
-                         (float4*)out_pos);
+                         (float4*)out_pos, sp);
     else if (nvec <= 128)
       hipLaunchKernelGGL((rmbx::add_layernorm_kernel<rmbx::F32, 2>), dim3(grid), dim3(256), 0, s, (const float4*)x,
                          (const float4*)r, weight, bias, (float4*)out, rows, D, eps, (const float4*)pos, pos_rows,
-                         (float4*)out_pos);
+                         (float4*)out_pos, sp);
     else if (nvec <= 256)
       hipLaunchKernelGGL((rmbx::add_layernorm_kernel<rmbx::F32, 4>), dim3(grid), dim3(256), 0, s, (const float4*)x,
                          (const float4*)r, weight, bias, (float4*)out, rows, D, eps, (const float4*)pos, pos_rows,
-                         (float4*)out_pos);
+                         (float4*)out_pos, sp);
     else
       hipLaunchKernelGGL((rmbx::add_layernorm_kernel<rmbx::F32, 8>), dim3(grid), dim3(256), 0, s, (const float4*)x,
                          (const float4*)r, weight, bias, (float4*)out, rows, D, eps, (const float4*)pos, pos_rows,
-                         (float4*)out_pos);
+                         (float4*)out_pos, sp);
   }
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
+}
+}  // namespace
+
+extern "C" int rmbx_add_layernorm_pos(const void* x, const void* r, const float* weight, const float* bias, void* out,
+                                      const void* pos, int pos_rows, void* out_pos, int rows, int D, float eps,
+                                      int dtype, void* stream) {
+  return add_layernorm_impl(x, r, weight, bias, out, pos, pos_rows, out_pos, rows, D, eps, dtype, stream,
+                            rmbx::LnSplit{nullptr, nullptr, nullptr, nullptr, rows});
+}
+
+extern "C" int rmbx_add_layernorm_split(const float* x, const float* r, const float* weight, const float* bias,
+                                        float* out, void* y_planes, float* y_rinv, const float* pos, int pos_rows,
+                                        float* out_pos, void* pos_planes, float* pos_rinv, int rows, int D, float eps,
+                                        void* stream) {
+  RMBX_CHECK_ARG(!y_planes == !y_rinv && !pos_planes == !pos_rinv, "rmbx_add_layernorm_split: planes need their rinv");
+  RMBX_CHECK_ARG(D % 4 == 0 && ((uintptr_t)y_planes | (uintptr_t)pos_planes) % 8 == 0,
+                 "rmbx_add_layernorm_split: D %% 4 and 8-byte aligned planes");
+  return add_layernorm_impl(x, r, weight, bias, out, pos, pos_rows, out_pos, rows, D, eps, 0, stream,
+                            rmbx::LnSplit{(uint16_t*)y_planes, y_rinv, (uint16_t*)pos_planes, pos_rinv, rows});
 }

@@ -499,6 +499,59 @@ def add_layernorm_pos(x, r, weight, bias, pos, eps=1e-5):
     return out, out_pos
 
 
+class PresplitRows:
+    """An f32 activation [M, K] in the pre-split A form of rmbx_linear_f16x3_presplit (written by
+    rmbx_add_layernorm_split): planes [2, M, K] f16, a[m] = rinv[m] * (planes[0, m] + planes[1, m])
+    to 2^-22 relative, rinv [M] f32 powers of two."""
+
+    __slots__ = ("planes", "rinv")
+
+    def __init__(self, planes, rinv):
+        self.planes, self.rinv = planes, rinv
+
+
+# the pre-split A path (env RMBX_GEMM_PRESPLIT=0 turns it off: the LayerNorms then emit f32 only and
+# every GEMM splits its A in registers)
+GEMM_PRESPLIT = os.environ.get("RMBX_GEMM_PRESPLIT", "1") != "0"
+
+
+def add_layernorm_split(x, r, weight, bias, eps=1e-5, pos=None, split_y=True, split_pos=True):
+    """add_layernorm(_pos) of f32 rows that also attaches the pre-split A form to its outputs:
+    returns y (and y + pos when pos is given), each an f32 tensor carrying `.rmbx_split`
+    (PresplitRows) when requested -- the form linear_f32x6 then reads (rmbx_add_layernorm_split)."""
+    if x.dtype != torch.float32 or not x.is_cuda or not x.is_contiguous():
+        raise ValueError("x must be a contiguous f32 device tensor")
+    D = x.shape[-1]
+    if r is not None and (r.shape != x.shape or r.dtype != x.dtype or not r.is_contiguous()):
+        raise ValueError("r must match x")
+    _chk(weight, torch.float32, (D,), "weight")
+    _chk(bias, torch.float32, (D,), "bias")
+    rows = x.numel() // D
+    y = torch.empty_like(x)
+    ys = PresplitRows(torch.empty((2, rows, D), dtype=torch.float16, device=x.device),
+                      torch.empty(rows, dtype=torch.float32, device=x.device)) if split_y else None
+    yp = ps = pos2 = None
+    if pos is not None:
+        pos2 = pos.reshape(-1, D)
+        if pos2.dtype != x.dtype or not pos2.is_contiguous() or not pos2.is_cuda:
+            raise ValueError("pos must be a contiguous device tensor of x's dtype")
+        if x.dim() < 2 or x.shape[-2] % pos2.shape[0] != 0:
+            raise ValueError("pos rows must divide the sequence length")
+        yp = torch.empty_like(x)
+        if split_pos:
+            ps = PresplitRows(torch.empty((2, rows, D), dtype=torch.float16, device=x.device),
+                              torch.empty(rows, dtype=torch.float32, device=x.device))
+    N.call("rmbx_add_layernorm_split", N.ptr(x), N.ptr(r), N.ptr(weight), N.ptr(bias), N.ptr(y),
+           N.ptr(ys.planes if ys else None), N.ptr(ys.rinv if ys else None), N.ptr(pos2),
+           pos2.shape[0] if pos2 is not None else 0, N.ptr(yp), N.ptr(ps.planes if ps else None),
+           N.ptr(ps.rinv if ps else None), rows, D, float(eps), N.stream_ptr())
+    if ys is not None:
+        y.rmbx_split = ys
+    if ps is not None:
+        yp.rmbx_split = ps
+    return (y, yp) if pos is not None else y
+
+
 def conv2d_nhwc(x, weight, bias, stride=1, padding=0, relu=False, res=None):
     """relu?(conv2d(x, weight) + bias + res) by rmbx_conv2d_nhwc (bf16) / rmbx_conv2d_nhwc_f32
     (f32: the 3x3 / stride-1 / pad-1 conv with Cin = Cout = 64 only): x channels_last
@@ -992,7 +1045,15 @@ def linear_f32x6(x, planes, bias=None, relu=False, out=None):
     elif out.dtype != torch.float32 or out.stride(-1) != 1 or out.shape != (M, Nn):
         raise ValueError("out must be an f32 [M, N] tensor with contiguous rows")
     name, flops = f"linear M={M} N={Nn} K={K}", 2.0 * M * Nn * K
-    if h3:
+    sp = getattr(x, "rmbx_split", None)
+    if h3 and sp is not None and Nn % LINEAR_F32X6_BN == 0 and sp.planes.shape[1] == M and sp.planes.shape[2] == K:
+        # the producer's pre-split rows (add_layernorm_split): both operands by LDS-DMA
+        p, ap = planes.planes, sp.planes
+        _gemm_launch(name + " presplit", flops, 4 * M * K + 4 * Nn * K + 4 * M * Nn, 3, "rmbx_linear_f16x3_presplit",
+                     N.ptr(ap), ap.stride(1), ap.stride(0), N.ptr(sp.rinv), N.ptr(p), p.stride(1), p.stride(0),
+                     N.ptr(planes.scale), N.ptr(bias), None, N.ptr(out), out.stride(0), M, Nn, K, 1 if relu else 0,
+                     N.stream_ptr())
+    elif h3:
         p = planes.planes
         _gemm_launch(name, flops, 4 * M * K + 4 * Nn * K + 4 * M * Nn, 3, "rmbx_linear_f16x3", N.ptr(x2), x2.stride(0),
                      N.ptr(p), p.stride(1), p.stride(0), N.ptr(planes.scale), N.ptr(bias), N.ptr(out), out.stride(0),

@@ -209,11 +209,23 @@ class _LayerOps(nn.Module):
             norm.__dict__["_f32"] = cache
         return cache[1], cache[2]
 
+    @staticmethod
+    def _presplit(x):
+        """Emit the LayerNorm outputs in the pre-split A form too (f32 device rows feeding f16x3
+        GEMMs): the QK / V / FFN1 / cross-attention projections then load pieces instead of
+        splitting in registers (kernels.add_layernorm_split, rmbx_linear_f16x3_presplit)."""
+        from ... import kernels as K
+
+        return (x.dtype == torch.float32 and F32_GEMM == "x6" and K.F32_PIECES == "f16x3" and K.GEMM_PRESPLIT
+                and x.shape[-1] % 4 == 0)
+
     def addnorm(self, norm, x, r):
         if self.fused:
             from ... import kernels as K
 
             w, b = self._norm_f32(norm)
+            if self._presplit(x):
+                return K.add_layernorm_split(x.contiguous(), r.contiguous(), w, b, norm.eps)
             return K.add_layernorm(x.contiguous(), r.contiguous(), w, b, norm.eps)
         return norm(x + r)
 
@@ -224,6 +236,11 @@ class _LayerOps(nn.Module):
             from ... import kernels as K
 
             w, b = self._norm_f32(norm)
+            if self._presplit(x):
+                # (y + pos feeds the next QK / cross-attention projections; y itself only the V
+                # projection, N = 512, whose gain does not pay for writing its pieces)
+                return K.add_layernorm_split(x.contiguous(), r.contiguous(), w, b, norm.eps, pos=pos.contiguous(),
+                                             split_y=False)
             return K.add_layernorm_pos(x.contiguous(), r.contiguous(), w, b, pos.contiguous(), norm.eps)
         y = norm(x + r)
         return y, y + pos

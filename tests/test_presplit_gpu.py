@@ -1,0 +1,135 @@
+"""The pre-split A path of the f16x3 GEMM: rmbx_add_layernorm_split (the ACT transformer's residual
+add + LayerNorm that also emits its output rows as f16 pieces with a per-row power-of-two scale) and
+rmbx_linear_f16x3_presplit (the GEMM loading those pieces by LDS-DMA instead of splitting f32 rows in
+registers).  The LayerNorm outputs must be bitwise those of rmbx_add_layernorm(_pos); the pieces must
+reconstruct the rows to 2^-22 of each element (2^-36 of the row max for elements below 2^-16 of it,
+whose low piece is an f16 subnormal) with the scaled row max in [2^13, 2^14); the GEMM is held to the
+f32 GEMM error class of tests/test_gemm_gpu.py (max |err| <= 4e-6 max |ref| against an f64 product and
+no worse than 2x hipBLASLt's f32 GEMM + 1e-7), on the ACT shapes (N = 3200 runs its last 128 columns
+on the narrow tile), ragged M, bias / residual / ReLU, and rows of extreme range."""
+
+import pytest
+import torch
+import torch.nn.functional as F
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda:0"
+
+
+def _err(got, ref):
+    return ((got.double() - ref).abs().max() / ref.abs().max()).item()
+
+
+def _rows(M, D, seed, extreme=False):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    x = torch.randn(M, D, generator=g)
+    r = torch.randn(M, D, generator=g)
+    if extreme:  # rows whose LayerNorm output spans a wide range (weights of very different sizes)
+        r[: M // 2] *= 0.0
+    return x.to(DEV), r.to(DEV)
+
+
+def _check_pieces(sp, y):
+    hi, lo = sp.planes[0].double(), sp.planes[1].double()
+    rinv = sp.rinv.double()
+    rec = rinv[:, None] * (hi + lo)
+    yd = y.double().reshape(rec.shape)
+    rowmax = yd.abs().amax(1, keepdim=True)
+    assert ((rec - yd).abs() <= yd.abs() * 2.0 ** -22 + rowmax * 2.0 ** -36).all()
+    assert torch.equal(torch.log2(rinv).round(), torch.log2(rinv))  # powers of two
+    m = hi.abs().amax(1)[rowmax[:, 0] > 0]
+    assert ((m >= 2 ** 13) & (m <= 2 ** 14)).all()
+
+
+@torch.no_grad()
+@pytest.mark.parametrize("M,D,extreme", [(1, 512, False), (1001, 512, False), (300, 512, True), (64, 2048, False)])
+def test_layernorm_split_outputs_and_pieces(M, D, extreme):
+    from robomanipbaselines_amd import kernels as K
+
+    x, r = _rows(M, D, M + D, extreme)
+    g = torch.Generator(device="cpu").manual_seed(3)
+    w = (torch.rand(D, generator=g) * 2.0 ** torch.randint(-12, 12, (D,), generator=g).float()).to(DEV)
+    b = torch.randn(D, generator=g).to(DEV) * 1e-3
+    pos = torch.randn(M, D, generator=g).to(DEV)
+    y_ref = K.add_layernorm(x, r, w, b, 1e-5)
+    y_ref2, yp_ref = K.add_layernorm_pos(x.view(1, M, D), r.view(1, M, D), w, b, pos, 1e-5)
+    y = K.add_layernorm_split(x, r, w, b, 1e-5)
+    y2, yp = K.add_layernorm_split(x.view(1, M, D), r.view(1, M, D), w, b, 1e-5, pos=pos)
+    assert torch.equal(y, y_ref) and torch.equal(y2, y_ref2) and torch.equal(yp, yp_ref)
+    _check_pieces(y.rmbx_split, y)
+    _check_pieces(y2.rmbx_split, y2)
+    _check_pieces(yp.rmbx_split, yp)
+    # a row's pieces and scale depend on that row alone (batch invariance)
+    y_one = K.add_layernorm_split(x[M // 2:M // 2 + 1].contiguous(), r[M // 2:M // 2 + 1].contiguous(), w, b, 1e-5)
+    assert torch.equal(y_one.rmbx_split.planes[:, 0], y.rmbx_split.planes[:, M // 2])
+    assert torch.equal(y_one.rmbx_split.rinv[0], y.rmbx_split.rinv[M // 2])
+
+
+@torch.no_grad()
+@pytest.mark.parametrize("M,N,K,relu,bias,res", [(1, 128, 512, False, False, False), (1000, 3200, 512, True, True, False),
+                                                 (2500, 1024, 512, False, True, False), (777, 512, 512, False, True, True),
+                                                 (300, 384, 64, True, False, True)])
+def test_presplit_linear_vs_f64(M, N, K, relu, bias, res):
+    from robomanipbaselines_amd import kernels as K_
+
+    x, r = _rows(M, K, M + N)
+    g = torch.Generator(device="cpu").manual_seed(N + K)
+    lw = (1.0 + torch.rand(K, generator=g)).to(DEV)
+    lb = (0.1 * torch.randn(K, generator=g)).to(DEV)
+    a = K_.add_layernorm_split(x, r, lw, lb, 1e-5)
+    assert hasattr(a, "rmbx_split")
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(DEV)
+    b = torch.randn(N, generator=g).to(DEV) if bias else None
+    rr = torch.randn(M, N, generator=g).to(DEV) if res else None
+    planes = K_.split_f16x2(w)
+    out = torch.empty(M, N, device=DEV)
+    sp = a.rmbx_split
+    K_.N.call("rmbx_linear_f16x3_presplit", K_.N.ptr(sp.planes), sp.planes.stride(1), sp.planes.stride(0),
+              K_.N.ptr(sp.rinv), K_.N.ptr(planes.planes), planes.planes.stride(1), planes.planes.stride(0),
+              K_.N.ptr(planes.scale), K_.N.ptr(b), K_.N.ptr(rr), K_.N.ptr(out), out.stride(0), M, N, K,
+              1 if relu else 0, K_.N.stream_ptr())
+    ref = a.double() @ w.double().t()
+    base = F.linear(a, w, b)
+    if bias:
+        ref = ref + b.double()
+    if res:
+        ref = ref + rr.double()
+        base = base + rr
+    if relu:
+        ref = ref.clamp_min(0)
+        base = base.clamp_min(0)
+    e, e32 = _err(out, ref), _err(base, ref)
+    assert torch.isfinite(out).all()
+    assert e <= 4e-6 and e <= 2 * e32 + 1e-7, (e, e32)
+    # linear_f32x6 takes the pre-split path for the LayerNorm's output, and agrees with the
+    # in-register split of the same f32 rows to the same bar
+    if not res:
+        got = K_.linear_f32x6(a, planes, b, relu=relu)
+        plain = K_.linear_f32x6(a.clone(), planes, b, relu=relu)  # (a clone carries no pieces)
+        assert _err(got, ref) <= 4e-6 and _err(plain, ref) <= 4e-6
+        assert torch.equal(got, out)
+
+
+@torch.no_grad()
+def test_presplit_rows_of_extreme_range():
+    """Rows with max |a| far outside f16's range (1e-20, 1e20) and an all-zero row: the per-row scale
+    keeps every row at f32 accuracy relative to its own magnitude."""
+    from robomanipbaselines_amd import kernels as K_
+
+    M, N, K = 6, 256, 512
+    g = torch.Generator(device="cpu").manual_seed(11)
+    x = torch.randn(M, K, generator=g)
+    scale = torch.tensor([1e-20, 1e20, 1.0, 0.0, 3e-5, 7e4])
+    lw = torch.ones(K)
+    # LayerNorm output ~N(0, 1) per row, then scaled per row by the weight: one launch per row scale
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(DEV)
+    planes = K_.split_f16x2(w)
+    for i, s in enumerate(scale.tolist()):
+        a = K_.add_layernorm_split(x[i:i + 1].to(DEV), None, (lw * s).to(DEV), torch.zeros(K, device=DEV), 1e-5)
+        got = K_.linear_f32x6(a, planes, None)
+        ref = a.double() @ w.double().t()
+        if s == 0.0:
+            assert (got == 0).all()
+        else:
+            assert _err(got, ref) <= 4e-6, (s, _err(got, ref))
