@@ -1673,7 +1673,8 @@ extern "C" int rmbx_linear_f16x3_presplit(const void* a_planes, long long lda, l
   const char* ve = getenv("RMBX_PRESPLIT_VAR");
   const int var = ve ? atoi(ve) : 0;
   const char* fe = getenv("RMBX_PRESPLIT_FORM");
-  const bool form2 = fe && atoi(fe) == 2;
+  const int form = fe ? atoi(fe) : 3;
+  const bool form2 = form == 2;
   if (!form2) {  // the three-ring form (default)
     switch (var) {
       case 0: hipLaunchKernelGGL((rmbx::gemm_f16x3_presplit3_kernel<8, 0>), dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0, st, g, ap, a_plane_stride, lda, a_rinv); break;

@@ -41,10 +41,12 @@ for name, N in (("qk", 1024), ("v/out", 512), ("ffn1", 3200)):
     ref = out.clone()
     os.environ["RMBX_PRESPLIT_FORM"] = "3"
     t2 = timeit(lambda: K.linear_f32x6(a, p, b, out=out))
+    eq = torch.equal(ref, out)
+    os.environ["RMBX_PRESPLIT_FORM"] = "3"
     fl = 3 * 2.0 * M * N * 512
     print(f"{name:6s} M={M} N={N} K=512: in-register split {t0:.3f} ms ({fl / t0 / 1e9 / 2500:.3f}) | "
           f"pre-split 2 stages {t1:.3f} ms ({fl / t1 / 1e9 / 2500:.3f}) | 3 rings {t2:.3f} ms "
-          f"({fl / t2 / 1e9 / 2500:.3f}) | equal {torch.equal(ref, out)}", flush=True)
+          f"({fl / t2 / 1e9 / 2500:.3f}) | equal {eq}", flush=True)
 for grp in ("2", "4", "8", "16"):
     os.environ["RMBX_PRESPLIT_GROUP"] = grp
     for name, N in (("qk", 1024), ("ffn1", 3200)):

@@ -5,8 +5,8 @@ registers).  The LayerNorm outputs must be bitwise those of rmbx_add_layernorm(_
 reconstruct the rows to 2^-22 of each element (2^-36 of the row max for elements below 2^-16 of it,
 whose low piece is an f16 subnormal) with the scaled row max in [2^13, 2^14); the GEMM is held to the
 f32 GEMM error class of tests/test_gemm_gpu.py (max |err| <= 4e-6 max |ref| against an f64 product and
-no worse than 2x hipBLASLt's f32 GEMM + 1e-7), on the ACT shapes (N = 3200 runs its last 128 columns
-on the narrow tile), ragged M, bias / residual / ReLU, and rows of extreme range."""
+no worse than 2x hipBLASLt's f32 GEMM + 1e-7), on the ACT shapes (N = 3200: the last 256-wide column
+tile half dead), ragged M, bias / residual / ReLU, and rows of extreme range."""
 
 import pytest
 import torch
@@ -133,3 +133,28 @@ def test_presplit_rows_of_extreme_range():
             assert (got == 0).all()
         else:
             assert _err(got, ref) <= 4e-6, (s, _err(got, ref))
+
+
+@torch.no_grad()
+@pytest.mark.parametrize("M,N,relu,bias", [(1, 256, False, True), (1000, 3200, True, True), (70000, 1024, False, True),
+                                           (5000, 384, True, False)])
+def test_presplit_forms_equal(M, N, relu, bias, monkeypatch):
+    """The two-stage and three-ring (default) forms of rmbx_linear_f16x3_presplit compute the same
+    sums in the same order: bitwise equal outputs."""
+    from robomanipbaselines_amd import kernels as K_
+
+    x, r = _rows(M, 512, M + N + 1)
+    a = K_.add_layernorm_split(x, r, torch.ones(512, device=DEV), torch.zeros(512, device=DEV), 1e-5)
+    g = torch.Generator(device="cpu").manual_seed(N)
+    w = (torch.randn(N, 512, generator=g) / 512 ** 0.5).to(DEV)
+    b = torch.randn(N, generator=g).to(DEV) if bias else None
+    planes = K_.split_f16x2(w)
+    outs = {}
+    for form in ("2", "3"):
+        monkeypatch.setenv("RMBX_PRESPLIT_FORM", form)
+        outs[form] = K_.linear_f32x6(a, planes, b, relu=relu).clone()
+    assert torch.equal(outs["2"], outs["3"])
+    ref = a.double() @ w.double().t() + (b.double() if bias else 0)
+    if relu:
+        ref = ref.clamp_min(0)
+    assert _err(outs["3"], ref) <= 4e-6
