@@ -252,11 +252,13 @@ def _probe_line(probe, is_gemm):
             "on v_mfma_f32_16x16x32_f16" if kinds == {3} else
             "bf16x6: each f32 operand split into three bf16 pieces, six piece products on v_mfma_f32_16x16x32_bf16"
             if kinds == {6} else "mixed f16x3 / bf16x6")
-    kernel = (f"rmbx::gemm_f32x6_kernel (fp32-accurate GEMM / implicit-GEMM conv, {form}, f32 accumulation)" if is_gemm
+    kernel = (f"rmbx::gemm_f32x6_kernel + rmbx::gemm_f16x3_presplit3_kernel (fp32-accurate GEMM / implicit-GEMM conv, "
+              f"{form}, f32 accumulation; the pre-split form loads the LayerNorm-split A pieces by LDS-DMA)" if is_gemm
               else f"rmbx::conv3x3p_f16x3_kernel (patch-staged 3x3 / stride-1 conv, {form}, f32 accumulation)")
     return {"bound": "mfma", "achieved": round(ex, 2), "peak": MFMA_PEAK_TFLOPS["bf16"], "unit": "TFLOP/s",
             "frac": ex / MFMA_PEAK_TFLOPS["bf16"], "traffic": None if traffic is None else round(traffic),
-            "traffic_unit": ("HBM bytes per GEMM call (one op launch; N = 3200 runs as two kernel dispatches), mean "
+            "traffic_unit": ("HBM bytes per GEMM call (one op launch; N = 3200 on the in-register form runs as two kernel "
+                             "dispatches), mean "
                              "over the calls of one fp32 ACT inference at 1024 envs" if is_gemm else
                              "HBM bytes per conv call, mean over the calls of one fp32 ACT inference at 1024 envs"),
             "traffic_source": src,

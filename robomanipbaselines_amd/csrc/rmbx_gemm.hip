@@ -1399,7 +1399,12 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f16x3_presplit3_kernel(Gem
         if (g.relu) {
           v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
         }
-        if (!(VAR & 4)) *(float4*)(g.C + (long long)m * g.ldc + n) = v;
+        if constexpr ((VAR & 8) != 0) {  // (profiling) non-temporal output stores
+          const f32x4v vv = {v.x, v.y, v.z, v.w};
+          __builtin_nontemporal_store(vv, (f32x4v*)(g.C + (long long)m * g.ldc + n));
+        } else if (!(VAR & 4)) {
+          *(float4*)(g.C + (long long)m * g.ldc + n) = v;
+        }
       }
     }
   }
@@ -1683,6 +1688,7 @@ extern "C" int rmbx_linear_f16x3_presplit(const void* a_planes, long long lda, l
       case 4: hipLaunchKernelGGL((rmbx::gemm_f16x3_presplit3_kernel<8, 4>), dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0, st, g, ap, a_plane_stride, lda, a_rinv); break;
       case 5: hipLaunchKernelGGL((rmbx::gemm_f16x3_presplit3_kernel<8, 5>), dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0, st, g, ap, a_plane_stride, lda, a_rinv); break;
       case 6: hipLaunchKernelGGL((rmbx::gemm_f16x3_presplit3_kernel<8, 6>), dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0, st, g, ap, a_plane_stride, lda, a_rinv); break;
+      case 8: hipLaunchKernelGGL((rmbx::gemm_f16x3_presplit3_kernel<8, 8>), dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0, st, g, ap, a_plane_stride, lda, a_rinv); break;
       default: RMBX_CHECK_ARG(false, "%s: RMBX_PRESPLIT_VAR %d", fn, var);
     }
     RMBX_CHECK_LAUNCH();

@@ -56,8 +56,9 @@ for grp in ("2", "4", "8", "16"):
         t1 = timeit(lambda: K.linear_f32x6(a, p, None, out=out))
         print(f"group {grp:>2s} {name:5s}: pre-split {t1:.3f} ms ({3 * 2.0 * M * N * 512 / t1 / 1e9 / 2500:.3f})", flush=True)
 os.environ["RMBX_PRESPLIT_GROUP"] = "8"
-# phase skips (timing only, the three-ring form): 1 = no DMA after the prologue, 2 = no MFMAs, 4 = no stores
-for var in ("1", "2", "4", "5", "6"):
+# phase skips (timing only, the three-ring form): 1 = no DMA after the prologue, 2 = no MFMAs, 4 = no stores;
+# 8 = non-temporal output stores (same results)
+for var in ("1", "2", "4", "5", "6", "8"):
     os.environ["RMBX_PRESPLIT_VAR"] = var
     for name, N in (("qk", 1024), ("ffn1", 3200)):
         w = torch.randn(N, 512, device=dev) / 512 ** 0.5

@@ -74,7 +74,7 @@ def winograd(a):
     print(json.dumps(out, indent=1))
 
 
-def gemm(a, pattern="gemm_f32x6", kernel="rmbx::gemm_f32x6_kernel"):
+def gemm(a, pattern=("gemm_f32x6", "gemm_f16x3_presplit"), kernel="rmbx::gemm_f32x6_kernel + rmbx::gemm_f16x3_presplit3_kernel"):
     """--gemm: the gemm_f32x6_kernel launches of the SECOND fp32 ACT inference of
     scripts/prof_act_gemm_pmc.py (dispatch order), scaled by the 16-B-lane factors (its global loads
     are dwordx4 and LDS-DMA of 16 B per lane): HBM bytes per launch, mean over the inference."""
@@ -82,7 +82,8 @@ def gemm(a, pattern="gemm_f32x6", kernel="rmbx::gemm_f32x6_kernel"):
         rows = sorted((int(r["Dispatch_Id"]), r["Kernel_Name"], float(r["Counter_Value"]) * 1024.0,
                        (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3) for r in csv.DictReader(open(path)))
         cal = [v for _, n, v, _ in rows if n.startswith("calib_f32x4")]
-        g = [(v, us) for _, n, v, us in rows if pattern in n]
+        pats = (pattern,) if isinstance(pattern, str) else pattern
+        g = [(v, us) for _, n, v, us in rows if any(q in n for q in pats)]
         assert len(g) % 2 == 0, len(g)
         return g[len(g) // 2:], statistics.median(cal)
     fetch, cf = per_launch(os.path.join(a.dir, "pmc_fetch", "run_counter_collection.csv"))
