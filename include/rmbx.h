@@ -518,6 +518,17 @@ int rmbx_linear_f16x3_presplit(const void* a_planes, long long lda, long long a_
                                const void* w_planes, long long ldw, long long w_plane_stride, const float* w_scale,
                                const float* bias, const float* res, float* c, long long ldc, int M, int N, int K,
                                int relu, void* stream);
+/* rmbx_linear_f16x3_presplit whose outputs c = relu?(a . w^T + bias) leave in the same pre-split
+ * form (the next GEMM's A): out_planes [2][M][ldo] f16 bits (plane stride out_plane_stride), row m
+ * scaled by 2^u_m with B_m (1 + 2^-10) in [2^13, 2^14), B_m = a_norm[m] w_norm_max + b_abs_max an
+ * upper bound of the row's |c| (a_norm: upper bounds of the A rows' 2-norms, rmbx_add_layernorm_split;
+ * w_norm_max >= max_n |w_n|_2, b_abs_max >= max |bias|), out_rinv[m] = 2^-u_m.  Replaces ACT's FFN
+ * first Linear + ReLU (its output only feeds the second Linear). */
+int rmbx_linear_f16x3_presplit_split(const void* a_planes, long long lda, long long a_plane_stride, const float* a_rinv,
+                                     const float* a_norm, const void* w_planes, long long ldw, long long w_plane_stride,
+                                     const float* w_scale, float w_norm_max, float b_abs_max, const float* bias,
+                                     int relu, void* out_planes, long long ldo, long long out_plane_stride,
+                                     float* out_rinv, int M, int N, int K, void* stream);
 /* 3x3 / stride-1 / pad-1 rmbx_conv2d_f16x3 with each input pixel split once per output tile: the
  * block stages the input patch of its 16 x 16 (Cout % 128 == 0) or 16 x 32 output tile for one
  * 32-channel chunk as two f16 pieces in LDS, scaled per (tile, chunk) by a power of two, and all
@@ -557,12 +568,15 @@ int rmbx_add_layernorm_pos(const void* x, const void* r, const float* weight, co
                            void* stream);
 /* f32 rmbx_add_layernorm_pos that also emits its outputs in rmbx_linear_f16x3_presplit's A form:
  * y = LayerNorm(rnd(x + r)) (out f32, nullable), y_planes [2][rows][D] + y_rinv [rows] (nullable
- * together), y + pos[row % pos_rows] (out_pos f32 and pos_planes + pos_rinv, each nullable; pos
- * needed if either is set); every row's scale from that row alone (batch-invariant).  D % 4 == 0,
- * 8-byte aligned planes. */
+ * together), y_norm [rows] (nullable) an upper bound of each row's |y|_2 (the f32 norm times
+ * 1 + 2^-12; rmbx_linear_f16x3_presplit_split bounds the next GEMM's outputs with it), y +
+ * pos[row % pos_rows] (out_pos f32 and pos_planes + pos_rinv, each nullable; pos needed if either
+ * is set); every row's values from that row alone (batch-invariant).  D % 4 == 0, 8-byte aligned
+ * planes. */
 int rmbx_add_layernorm_split(const float* x, const float* r, const float* weight, const float* bias, float* out,
-                             void* y_planes, float* y_rinv, const float* pos, int pos_rows, float* out_pos,
-                             void* pos_planes, float* pos_rinv, int rows, int D, float eps, void* stream);
+                             void* y_planes, float* y_rinv, float* y_norm, const float* pos, int pos_rows,
+                             float* out_pos, void* pos_planes, float* pos_rinv, int rows, int D, float eps,
+                             void* stream);
 /* out [N][Ho][Wo][C] = maxpool3x3s2p1(relu(rnd(x + bias))), Ho = (H-1)/2+1, Wo = (W-1)/2+1. */
 int rmbx_nhwc_bias_relu_maxpool(const void* x, const float* bias, void* out, int N, int H, int W,
                                 int C, int dtype, void* stream);

@@ -1247,10 +1247,26 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f16x3_presplit_kernel(Gemm
 // spread over its eight column-tile MFMA groups instead of bunched at the step's start.  Per step,
 // in issue order: W(kt + 1), then A(kt + 2); the step ends waiting until at most the A(kt + 2)
 // pieces are outstanding, which retires A(kt + 1) (issued the step before) and W(kt + 1).
-template <int GROUP, int VAR = 0>
+// SPLIT_OUT (rmbx_linear_f16x3_presplit_split): the outputs leave in the same pre-split form, for the
+// next GEMM to load by DMA -- row m scaled by 2^u_m from a bound of its values, |c[m][n]| <=
+// B_m = |a_m|_2 max_n |w_n|_2 + max |bias| (Cauchy-Schwarz on the f32 product; a_norm from the
+// producing LayerNorm), 2^u_m putting B_m (1 + 2^-10) in [2^13, 2^14): hi = f16(c 2^u_m),
+// lo = f16(c 2^u_m - hi), and out_rinv[m] = 2^-u_m.  The bound is loose by the ratio of B_m to the
+// row's true max (a few bits for the ACT layers); elements below 2^-16 of B_m keep their low piece
+// as an f16 subnormal, an absolute error <= 2^-38 B_m.
+struct PresplitOut {
+  uint16_t* planes;      // [2][M][ldo] f16 bits
+  long long ldo, ps;     // row stride, plane stride (elements)
+  float* rinv;           // [M]
+  const float* a_norm;   // [M] upper bounds of the A rows' 2-norms
+  float w_norm_max, b_abs_max;
+};
+
+template <int GROUP, int VAR = 0, bool SPLIT_OUT = false>
 __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f16x3_presplit3_kernel(GemmArgs g, const uint16_t* __restrict__ Ap,
                                                                             long long aps, long long ldah,
-                                                                            const float* __restrict__ arinv) {
+                                                                            const float* __restrict__ arinv,
+                                                                            PresplitOut po = PresplitOut{}) {
   constexpr int BN = 256, NJ = 8;
   constexpr int A_STAGE = 2 * GM_A_PLANE, B_PLANE = gm_b_plane<BN>(), W_STAGE = 2 * B_PLANE;  // 32 KiB each
   constexpr int W_RING = 3 * A_STAGE;
@@ -1398,6 +1414,26 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f16x3_presplit3_kernel(Gem
         }
         if (g.relu) {
           v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
+        }
+        if constexpr (SPLIT_OUT) {
+          const float B = (po.a_norm[m] * po.w_norm_max + po.b_abs_max) * (1.f + 0.0009765625f);
+          int e = 14;
+          if (B > 0.f && B <= 3.4e38f) frexpf(B, &e);  // B = f 2^e, f in [0.5, 1); NaN / inf: scale 1
+          const float sc = ldexpf(1.f, 14 - e);
+          if (n == 0) po.rinv[m] = ldexpf(1.f, e - 14);
+          const float x4[4] = {v.x * sc, v.y * sc, v.z * sc, v.w * sc};
+          uint32_t hw[2], lw[2];
+#pragma unroll
+          for (int k = 0; k < 2; ++k) {
+            const _Float16 h0 = (_Float16)x4[2 * k], h1 = (_Float16)x4[2 * k + 1];
+            const _Float16 l0 = (_Float16)(x4[2 * k] - (float)h0), l1 = (_Float16)(x4[2 * k + 1] - (float)h1);
+            hw[k] = __builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+            lw[k] = __builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
+          }
+          uint16_t* o = po.planes + (long long)m * po.ldo + n;
+          *(uint2*)o = make_uint2(hw[0], hw[1]);
+          *(uint2*)(o + po.ps) = make_uint2(lw[0], lw[1]);
+          continue;
         }
         if constexpr ((VAR & 8) != 0) {  // (profiling) non-temporal output stores
           const f32x4v vv = {v.x, v.y, v.z, v.w};
@@ -1712,6 +1748,38 @@ extern "C" int rmbx_linear_f16x3_presplit(const void* a_planes, long long lda, l
     case 16: hipLaunchKernelGGL((rmbx::gemm_f16x3_presplit_kernel<256, 16>), dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0, st, g, ap, a_plane_stride, lda, a_rinv); break;
     default: hipLaunchKernelGGL((rmbx::gemm_f16x3_presplit_kernel<256, 8>), dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0, st, g, ap, a_plane_stride, lda, a_rinv);
   }
+  RMBX_CHECK_LAUNCH();
+  return RMBX_OK;
+}
+
+extern "C" int rmbx_linear_f16x3_presplit_split(const void* a_planes, long long lda, long long a_plane_stride,
+                                                const float* a_rinv, const float* a_norm, const void* w_planes,
+                                                long long ldw, long long w_plane_stride, const float* w_scale,
+                                                float w_norm_max, float b_abs_max, const float* bias, int relu,
+                                                void* out_planes, long long ldo, long long out_plane_stride,
+                                                float* out_rinv, int M, int N, int K, void* stream) {
+  const char* fn = "rmbx_linear_f16x3_presplit_split";
+  RMBX_CHECK_ARG(a_planes && a_rinv && a_norm && w_planes && w_scale && out_planes && out_rinv, "%s: null pointer", fn);
+  RMBX_CHECK_ARG(M >= 0 && N > 0 && K > 0 && N % rmbx::GM_BN == 0 && K % rmbx::GM_BK == 0,
+                 "%s: bad shape M=%d N=%d K=%d (N %% 128, K %% 32)", fn, M, N, K);
+  RMBX_CHECK_ARG(lda >= K && lda % 8 == 0 && a_plane_stride % 8 == 0 && ldw >= K && ldw % 8 == 0 &&
+                     w_plane_stride % 8 == 0 && ldo >= N && ldo % 4 == 0 && out_plane_stride % 4 == 0 &&
+                     out_plane_stride >= (long long)M * ldo,
+                 "%s: bad strides lda=%lld ldw=%lld ldo=%lld", fn, lda, ldw, ldo);
+  RMBX_CHECK_ARG(((uintptr_t)a_planes | (uintptr_t)w_planes | (uintptr_t)bias | (uintptr_t)w_scale) % 16 == 0 &&
+                     (uintptr_t)out_planes % 8 == 0,
+                 "%s: operands must be 16-B aligned (out_planes 8-B)", fn);
+  RMBX_CHECK_ARG(w_norm_max >= 0.f && b_abs_max >= 0.f, "%s: bad bounds", fn);
+  if (M == 0) return RMBX_OK;
+  rmbx::GemmArgs g{nullptr, (const uint16_t*)w_planes, bias, nullptr, 0, 0, ldw, w_plane_stride, M, N, K,
+                   relu ? 1 : 0, (M + rmbx::GM_BM - 1) / rmbx::GM_BM, (N + 255) / 256, nullptr};
+  g.batch = 1;
+  g.ws = w_scale;
+  const long long blocks = (long long)g.tiles_m * g.tiles_n;
+  RMBX_CHECK_ARG(blocks < (1ll << 31), "%s: too many tiles", fn);
+  rmbx::PresplitOut po{(uint16_t*)out_planes, ldo, out_plane_stride, out_rinv, a_norm, w_norm_max, b_abs_max};
+  hipLaunchKernelGGL((rmbx::gemm_f16x3_presplit3_kernel<8, 0, true>), dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0,
+                     (hipStream_t)stream, g, (const uint16_t*)a_planes, a_plane_stride, lda, a_rinv, po);
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
 }

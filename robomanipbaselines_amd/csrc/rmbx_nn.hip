@@ -233,6 +233,7 @@ struct LnSplit {
   uint16_t* pos_planes;
   float* pos_rinv;
   int rows;
+  float* y_norm;  // an upper bound of each row's Euclidean norm |y|_2 (nullable)
 };
 
 template <class T, int PER>
@@ -290,7 +291,7 @@ __global__ void __launch_bounds__(256) add_layernorm_kernel(const typename T::ve
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) var += __shfl_xor(var, off);
   const float rstd = rsqrtf(var / (float)D + eps);
-  float ymax = 0.f, pmax = 0.f;  // f32 split outputs: the rows' max |y| and max |y + pos|
+  float ymax = 0.f, pmax = 0.f, ysq = 0.f;  // f32 split outputs: the rows' max |y|, max |y + pos|, sum y^2
 #pragma unroll
   for (int q = 0; q < PER; ++q) {
     const int v = lane + q * 64;
@@ -308,6 +309,10 @@ __global__ void __launch_bounds__(256) add_layernorm_kernel(const typename T::ve
       if (sp.y_planes) {
 #pragma unroll
         for (int k = 0; k < V; ++k) ymax = fmaxf(ymax, fabsf(yr[k]));
+      }
+      if (sp.y_norm) {
+#pragma unroll
+        for (int k = 0; k < V; ++k) ysq += yr[k] * yr[k];
       }
       if (out_pos || sp.pos_planes) {
         // the next attention's query input: rnd(y + pos[row % pos_rows]) on the rounded y, as the
@@ -367,6 +372,13 @@ __global__ void __launch_bounds__(256) add_layernorm_kernel(const typename T::ve
         }
       }
     };
+    if (sp.y_norm) {
+      // |y|_2 from an f32 sum of squares: relative rounding <= ~D 2^-24, covered 2^-12 over
+      float q = ysq;
+#pragma unroll
+      for (int off = 32; off > 0; off >>= 1) q += __shfl_xor(q, off);
+      if (lane == 0) sp.y_norm[row] = sqrtf(q) * (1.f + 0.000244140625f);
+    }
     if (sp.y_planes) split_row(s, ymax, sp.y_planes, sp.y_rinv);
     if (sp.pos_planes) split_row(s2, pmax, sp.pos_planes, sp.pos_rinv);
   }
@@ -441,16 +453,16 @@ extern "C" int rmbx_add_layernorm_pos(const void* x, const void* r, const float*
                                       const void* pos, int pos_rows, void* out_pos, int rows, int D, float eps,
                                       int dtype, void* stream) {
   return add_layernorm_impl(x, r, weight, bias, out, pos, pos_rows, out_pos, rows, D, eps, dtype, stream,
-                            rmbx::LnSplit{nullptr, nullptr, nullptr, nullptr, rows});
+                            rmbx::LnSplit{nullptr, nullptr, nullptr, nullptr, rows, nullptr});
 }
 
 extern "C" int rmbx_add_layernorm_split(const float* x, const float* r, const float* weight, const float* bias,
-                                        float* out, void* y_planes, float* y_rinv, const float* pos, int pos_rows,
-                                        float* out_pos, void* pos_planes, float* pos_rinv, int rows, int D, float eps,
-                                        void* stream) {
+                                        float* out, void* y_planes, float* y_rinv, float* y_norm, const float* pos,
+                                        int pos_rows, float* out_pos, void* pos_planes, float* pos_rinv, int rows, int D,
+                                        float eps, void* stream) {
   RMBX_CHECK_ARG(!y_planes == !y_rinv && !pos_planes == !pos_rinv, "rmbx_add_layernorm_split: planes need their rinv");
   RMBX_CHECK_ARG(D % 4 == 0 && ((uintptr_t)y_planes | (uintptr_t)pos_planes) % 8 == 0,
                  "rmbx_add_layernorm_split: D %% 4 and 8-byte aligned planes");
   return add_layernorm_impl(x, r, weight, bias, out, pos, pos_rows, out_pos, rows, D, eps, 0, stream,
-                            rmbx::LnSplit{(uint16_t*)y_planes, y_rinv, (uint16_t*)pos_planes, pos_rinv, rows});
+                            rmbx::LnSplit{(uint16_t*)y_planes, y_rinv, (uint16_t*)pos_planes, pos_rinv, rows, y_norm});
 }

@@ -226,7 +226,8 @@ struct RenderArgs {
   int n_env;
   int tiles_x, tiles_y;
   int groups;  // blocks per env (each renders a contiguous range of tiles)
-  int dbg;     // diagnostic (RMBX_RENDER_DBG; 0 in production): 1 no ray loop, 2 no stores, 4 test counts, 8 sphere bounds only
+  int dbg;     // diagnostic (RMBX_RENDER_DBG; 0 in production): 1 no ray loop, 2 no stores, 4 test counts, 8 sphere
+               // bounds only; visibility-pass timing probes: 16 frames only, 32 + set-up, 64 + ray tests, no writes
 };
 
 // camera pose of env `env` in world: R (columns = camera axes), p
@@ -398,7 +399,7 @@ __device__ __forceinline__ void tri_cover(const RenderArgs& a, const TriCam& T, 
   const unsigned long long key = ((unsigned long long)__float_as_uint(t) << 32) | j;
   // the key only ever decreases, so a value read earlier (older) that is already <= key proves the
   // atomic would not change it: skip it (most covered pixels of a mesh are overdrawn)
-  if (a.dbg & 8) {  // (timing probe: the ray tests without the visibility writes)
+  if (a.dbg & 64) {  // (timing probe: the ray tests without the visibility writes)
     if (t == 12345.f) *slot = key;
     return;
   }
@@ -441,7 +442,7 @@ __global__ void __launch_bounds__(RASTER_THREADS) raster_kernel(RenderArgs a, in
   const float tanh_ = tanf(0.5f * a.cam.fovy_deg * 3.14159265358979f / 180.0f);
   const float aspect = (float)a.cam.width / (float)a.cam.height;
   mesh_frames_block(a, env, cf, mR, mc, mvis, tanh_, aspect);
-  if (a.dbg & 2) return;  // (timing probe: the per-block frames only)
+  if (a.dbg & 16) return;  // (timing probe: the per-block frames only)
   // every lane stays to the end (the wave's pixel work is shared by all 64 lanes below)
   const int j = chunk * RASTER_THREADS + threadIdx.x;
   TriCam T;
@@ -452,8 +453,8 @@ __global__ void __launch_bounds__(RASTER_THREADS) raster_kernel(RenderArgs a, in
     const int k = __float_as_int(tp[3].x) >> 16;
     if (k >= 0 && k < a.nmesh && mvis[k]) tri_setup(a, tp, mR[k], mc[k], tanh_, aspect, T);
   }
-  const bool live = T.x0 <= T.x1 && T.y0 <= T.y1 && !(a.dbg & 4);  // (dbg 4, timing probe: set-up only)
-  if ((a.dbg & 4) && T.x0 == -12345) a.vis[0] = 0;  // (keeps the probe's set-up alive)
+  const bool live = T.x0 <= T.x1 && T.y0 <= T.y1 && !(a.dbg & 32);  // (dbg 32, timing probe: set-up only)
+  if ((a.dbg & 32) && T.x0 == -12345) a.vis[0] = 0;  // (keeps the probe's set-up alive)
   const int nx = T.x1 - T.x0 + 1;
   const int span = live ? nx * (T.y1 - T.y0 + 1) : 0;
   unsigned long long* vis = a.vis + (size_t)env * a.cam.width * a.cam.height;

@@ -501,13 +501,14 @@ def add_layernorm_pos(x, r, weight, bias, pos, eps=1e-5):
 
 class PresplitRows:
     """An f32 activation [M, K] in the pre-split A form of rmbx_linear_f16x3_presplit (written by
-    rmbx_add_layernorm_split): planes [2, M, K] f16, a[m] = rinv[m] * (planes[0, m] + planes[1, m])
-    to 2^-22 relative, rinv [M] f32 powers of two."""
+    rmbx_add_layernorm_split or rmbx_linear_f16x3_presplit_split): planes [2, M, K] f16, a[m] =
+    rinv[m] * (planes[0, m] + planes[1, m]) to 2^-22 relative, rinv [M] f32 powers of two; norm [M]
+    (optional) an upper bound of each row's |a|_2."""
 
-    __slots__ = ("planes", "rinv")
+    __slots__ = ("planes", "rinv", "norm")
 
-    def __init__(self, planes, rinv):
-        self.planes, self.rinv = planes, rinv
+    def __init__(self, planes, rinv, norm=None):
+        self.planes, self.rinv, self.norm = planes, rinv, norm
 
 
 # the pre-split A path (env RMBX_GEMM_PRESPLIT=0 turns it off: the LayerNorms then emit f32 only and
@@ -515,7 +516,7 @@ class PresplitRows:
 GEMM_PRESPLIT = os.environ.get("RMBX_GEMM_PRESPLIT", "1") != "0"
 
 
-def add_layernorm_split(x, r, weight, bias, eps=1e-5, pos=None, split_y=True, split_pos=True):
+def add_layernorm_split(x, r, weight, bias, eps=1e-5, pos=None, split_y=True, split_pos=True, y_norm=False):
     """add_layernorm(_pos) of f32 rows that also attaches the pre-split A form to its outputs:
     returns y (and y + pos when pos is given), each an f32 tensor carrying `.rmbx_split`
     (PresplitRows) when requested -- the form linear_f32x6 then reads (rmbx_add_layernorm_split)."""
@@ -529,7 +530,8 @@ def add_layernorm_split(x, r, weight, bias, eps=1e-5, pos=None, split_y=True, sp
     rows = x.numel() // D
     y = torch.empty_like(x)
     ys = PresplitRows(torch.empty((2, rows, D), dtype=torch.float16, device=x.device),
-                      torch.empty(rows, dtype=torch.float32, device=x.device)) if split_y else None
+                      torch.empty(rows, dtype=torch.float32, device=x.device),
+                      torch.empty(rows, dtype=torch.float32, device=x.device) if y_norm else None) if split_y else None
     yp = ps = pos2 = None
     if pos is not None:
         pos2 = pos.reshape(-1, D)
@@ -542,7 +544,7 @@ def add_layernorm_split(x, r, weight, bias, eps=1e-5, pos=None, split_y=True, sp
             ps = PresplitRows(torch.empty((2, rows, D), dtype=torch.float16, device=x.device),
                               torch.empty(rows, dtype=torch.float32, device=x.device))
     N.call("rmbx_add_layernorm_split", N.ptr(x), N.ptr(r), N.ptr(weight), N.ptr(bias), N.ptr(y),
-           N.ptr(ys.planes if ys else None), N.ptr(ys.rinv if ys else None), N.ptr(pos2),
+           N.ptr(ys.planes if ys else None), N.ptr(ys.rinv if ys else None), N.ptr(ys.norm if ys else None), N.ptr(pos2),
            pos2.shape[0] if pos2 is not None else 0, N.ptr(yp), N.ptr(ps.planes if ps else None),
            N.ptr(ps.rinv if ps else None), rows, D, float(eps), N.stream_ptr())
     if ys is not None:
@@ -550,6 +552,53 @@ def add_layernorm_split(x, r, weight, bias, eps=1e-5, pos=None, split_y=True, sp
     if ps is not None:
         yp.rmbx_split = ps
     return (y, yp) if pos is not None else y
+
+
+def weight_bounds(w, b):
+    """(max_n |w_n|_2, max |b|) of an f32 weight [N, K] and bias [N], rounded up to f32 upper bounds
+    (computed in f64): the output bound of linear_presplit_split."""
+    wn = float(w.detach().double().norm(dim=1).max()) if w.numel() else 0.0
+    bm = float(b.detach().double().abs().max()) if b is not None and b.numel() else 0.0
+    up = 1.0 + 2.0 ** -20
+    return wn * up, bm * up
+
+
+def linear_presplit_split(xs, planes, bias, bounds, relu=False):
+    """relu?(x @ W^T + bias) from pre-split rows xs (PresplitRows with norm bounds) to pre-split rows
+    (rmbx_linear_f16x3_presplit_split): the FFN's first Linear, whose output only feeds the second.
+    bounds = weight_bounds(W, bias)."""
+    Nn, K, h3 = _planes_nk(planes, "linear_presplit_split")
+    if not h3 or xs.norm is None or xs.planes.shape[2] != K:
+        raise ValueError("linear_presplit_split: f16x3 planes and pre-split rows with norm bounds of width K")
+    M = xs.planes.shape[1]
+    if bias is not None:
+        _chk(bias, torch.float32, (Nn,), "bias")
+    out = PresplitRows(torch.empty((2, M, Nn), dtype=torch.float16, device=xs.planes.device),
+                       torch.empty(M, dtype=torch.float32, device=xs.planes.device))
+    p, ap, op = planes.planes, xs.planes, out.planes
+    _gemm_launch(f"linear M={M} N={Nn} K={K} presplit->split", 2.0 * M * Nn * K, 4 * M * K + 4 * Nn * K + 4 * M * Nn, 3,
+                 "rmbx_linear_f16x3_presplit_split", N.ptr(ap), ap.stride(1), ap.stride(0), N.ptr(xs.rinv),
+                 N.ptr(xs.norm), N.ptr(p), p.stride(1), p.stride(0), N.ptr(planes.scale), float(bounds[0]),
+                 float(bounds[1]), N.ptr(bias), 1 if relu else 0, N.ptr(op), op.stride(1), op.stride(0),
+                 N.ptr(out.rinv), M, Nn, K, N.stream_ptr())
+    return out
+
+
+def linear_presplit(xs, planes, bias=None, relu=False):
+    """relu?(x @ W^T + bias) f32 [M, N] from pre-split rows xs (rmbx_linear_f16x3_presplit)."""
+    Nn, K, h3 = _planes_nk(planes, "linear_presplit")
+    if not h3 or xs.planes.shape[2] != K or Nn % LINEAR_F32X6_BN != 0:
+        raise ValueError("linear_presplit: f16x3 planes, N % 128 == 0 and pre-split rows of width K")
+    M = xs.planes.shape[1]
+    if bias is not None:
+        _chk(bias, torch.float32, (Nn,), "bias")
+    out = torch.empty((M, Nn), dtype=torch.float32, device=xs.planes.device)
+    p, ap = planes.planes, xs.planes
+    _gemm_launch(f"linear M={M} N={Nn} K={K} presplit", 2.0 * M * Nn * K, 4 * M * K + 4 * Nn * K + 4 * M * Nn, 3,
+                 "rmbx_linear_f16x3_presplit", N.ptr(ap), ap.stride(1), ap.stride(0), N.ptr(xs.rinv), N.ptr(p),
+                 p.stride(1), p.stride(0), N.ptr(planes.scale), N.ptr(bias), None, N.ptr(out), out.stride(0), M, Nn, K,
+                 1 if relu else 0, N.stream_ptr())
+    return out
 
 
 def conv2d_nhwc(x, weight, bias, stride=1, padding=0, relu=False, res=None):

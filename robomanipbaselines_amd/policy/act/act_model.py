@@ -190,6 +190,21 @@ class _LayerOps(nn.Module):
     fused = False
 
     def ffn(self, x):
+        sp = getattr(x, "rmbx_split", None)
+        if (self.fused and sp is not None and sp.norm is not None and self.linear1.out_features % 128 == 0
+                and self.linear2.out_features % 128 == 0):
+            # the LayerNorm's pre-split rows in, the hidden layer kept in the pre-split form (scaled per
+            # row by a Cauchy-Schwarz bound of its values): neither GEMM splits in registers
+            from ... import kernels as K
+
+            l1, l2 = self.linear1, self.linear2
+            key = (l1.weight.data_ptr(), l1.weight._version, l1.bias.data_ptr(), l1.bias._version)
+            cache = self.__dict__.get("_ffn_bounds")
+            if cache is None or cache[0] != key:
+                cache = (key, K.weight_bounds(l1.weight, l1.bias))
+                self.__dict__["_ffn_bounds"] = cache
+            hs = K.linear_presplit_split(sp, _x6_planes(self, "linear1", l1.weight), l1.bias, cache[1], relu=True)
+            return K.linear_presplit(hs, _x6_planes(self, "linear2", l2.weight), l2.bias).view(*x.shape[:-1], -1)
         if self.fused and _x6_ok(x, self.linear1.out_features) and self.linear2.out_features % 128 == 0:
             h = _x6_linear(self, "linear1", x, self.linear1.weight, self.linear1.bias, relu=True)
             return _x6_linear(self, "linear2", h, self.linear2.weight, self.linear2.bias)
@@ -225,7 +240,7 @@ class _LayerOps(nn.Module):
 
             w, b = self._norm_f32(norm)
             if self._presplit(x):
-                return K.add_layernorm_split(x.contiguous(), r.contiguous(), w, b, norm.eps)
+                return K.add_layernorm_split(x.contiguous(), r.contiguous(), w, b, norm.eps, y_norm=True)
             return K.add_layernorm(x.contiguous(), r.contiguous(), w, b, norm.eps)
         return norm(x + r)
 

@@ -1,5 +1,5 @@
 """Timing probe (GPU) of the mesh visibility pass: per camera, the raster kernel's time with
-RMBX_RENDER_DBG probes -- 2: per-block frames only, 4: + triangle set-up, 8: + ray tests without
+RMBX_RENDER_DBG probes -- 16: per-block frames only, 32: + triangle set-up, 64: + ray tests without
 the visibility writes, 0: the full pass (frames wrong under a probe; timing only)."""
 import os
 import sys
@@ -15,7 +15,7 @@ env.reset()
 H, W = env.renderer.height, env.renderer.width
 u8 = torch.empty((n, H // 2, W // 2, 16), dtype=torch.uint8, device="cuda:0")
 for cam in env.renderer.cam_names:
-    for dbg in ("2", "4", "8", "0"):
+    for dbg in ("16", "32", "64", "0"):
         os.environ["RMBX_RENDER_DBG"] = dbg
         env.renderer.render(env.engine, cam, policy=u8)
         torch.cuda.synchronize()
