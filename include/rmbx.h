@@ -523,7 +523,8 @@ int rmbx_linear_f16x3_presplit(const void* a_planes, long long lda, long long a_
  * scaled by 2^u_m with B_m (1 + 2^-10) in [2^13, 2^14), B_m = a_norm[m] w_norm_max + b_abs_max an
  * upper bound of the row's |c| (a_norm: upper bounds of the A rows' 2-norms, rmbx_add_layernorm_split;
  * w_norm_max >= max_n |w_n|_2, b_abs_max >= max |bias|), out_rinv[m] = 2^-u_m.  Replaces ACT's FFN
- * first Linear + ReLU (its output only feeds the second Linear). */
+ * first Linear + ReLU (its output only feeds the second Linear).  ldo and out_plane_stride % 8 == 0,
+ * 16-byte aligned operands. */
 int rmbx_linear_f16x3_presplit_split(const void* a_planes, long long lda, long long a_plane_stride, const float* a_rinv,
                                      const float* a_norm, const void* w_planes, long long ldw, long long w_plane_stride,
                                      const float* w_scale, float w_norm_max, float b_abs_max, const float* bias,

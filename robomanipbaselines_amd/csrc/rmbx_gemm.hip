@@ -1394,6 +1394,54 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f16x3_presplit3_kernel(Gem
 #pragma unroll
         for (int e = 0; e < 4; ++e) T[(mi * 16 + 4 * fs + e) * PITCH + qq * 16 + fr] = acc[mi][pass * NJP + qq][e];
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    if constexpr (SPLIT_OUT) {
+      // pre-split output: 8 columns per lane (16-byte stores of each piece plane), 8 rows per round
+      const int c8 = (lane & 7) * 8;
+      const int n = n0 + wn * (BN / 2) + pass * WC + c8;
+      float sn8[8], bn8[8];
+#pragma unroll
+      for (int h = 0; h < 2; ++h) {
+        const float4 s4 = *(const float4*)(g.ws + n + 4 * h);
+        const float4 b4 = g.bias ? *(const float4*)(g.bias + n + 4 * h) : make_float4(0.f, 0.f, 0.f, 0.f);
+        sn8[4 * h] = s4.x; sn8[4 * h + 1] = s4.y; sn8[4 * h + 2] = s4.z; sn8[4 * h + 3] = s4.w;
+        bn8[4 * h] = b4.x; bn8[4 * h + 1] = b4.y; bn8[4 * h + 2] = b4.z; bn8[4 * h + 3] = b4.w;
+      }
+#pragma unroll
+      for (int it = 0; it < 8; ++it) {
+        const int rr = it * 8 + (lane >> 3);
+        const int m = m0 + wm * 64 + rr;
+        if (m < g.M) {
+          const float4 v0 = *(const float4*)(T + rr * PITCH + c8), v1 = *(const float4*)(T + rr * PITCH + c8 + 4);
+          const float vv[8] = {v0.x, v0.y, v0.z, v0.w, v1.x, v1.y, v1.z, v1.w};
+          const float rs = arinv[m];
+          const float B = (po.a_norm[m] * po.w_norm_max + po.b_abs_max) * (1.f + 0.0009765625f);
+          int e = 14;
+          if (B > 0.f && B <= 3.4e38f) frexpf(B, &e);  // B = f 2^e, f in [0.5, 1); NaN / inf: scale 1
+          const float sc = ldexpf(1.f, 14 - e);
+          if (n == 0) po.rinv[m] = ldexpf(1.f, e - 14);
+          uint32_t hw[4], lw[4];
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            float x0 = vv[2 * k] * (rs * sn8[2 * k]) + bn8[2 * k];
+            float x1 = vv[2 * k + 1] * (rs * sn8[2 * k + 1]) + bn8[2 * k + 1];
+            if (g.relu) {
+              x0 = fmaxf(x0, 0.f);
+              x1 = fmaxf(x1, 0.f);
+            }
+            x0 *= sc;
+            x1 *= sc;
+            const _Float16 h0 = (_Float16)x0, h1 = (_Float16)x1;
+            const _Float16 l0 = (_Float16)(x0 - (float)h0), l1 = (_Float16)(x1 - (float)h1);
+            hw[k] = __builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+            lw[k] = __builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
+          }
+          uint16_t* o = po.planes + (long long)m * po.ldo + n;
+          *(uint4*)o = make_uint4(hw[0], hw[1], hw[2], hw[3]);
+          *(uint4*)(o + po.ps) = make_uint4(lw[0], lw[1], lw[2], lw[3]);
+        }
+      }
+      continue;
+    }
     const int c4 = (lane % LPR) * 4;
     const int n = n0 + wn * (BN / 2) + pass * WC + c4;
     float4 bn = make_float4(0.f, 0.f, 0.f, 0.f);
@@ -1414,26 +1462,6 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f16x3_presplit3_kernel(Gem
         }
         if (g.relu) {
           v.x = fmaxf(v.x, 0.f); v.y = fmaxf(v.y, 0.f); v.z = fmaxf(v.z, 0.f); v.w = fmaxf(v.w, 0.f);
-        }
-        if constexpr (SPLIT_OUT) {
-          const float B = (po.a_norm[m] * po.w_norm_max + po.b_abs_max) * (1.f + 0.0009765625f);
-          int e = 14;
-          if (B > 0.f && B <= 3.4e38f) frexpf(B, &e);  // B = f 2^e, f in [0.5, 1); NaN / inf: scale 1
-          const float sc = ldexpf(1.f, 14 - e);
-          if (n == 0) po.rinv[m] = ldexpf(1.f, e - 14);
-          const float x4[4] = {v.x * sc, v.y * sc, v.z * sc, v.w * sc};
-          uint32_t hw[2], lw[2];
-#pragma unroll
-          for (int k = 0; k < 2; ++k) {
-            const _Float16 h0 = (_Float16)x4[2 * k], h1 = (_Float16)x4[2 * k + 1];
-            const _Float16 l0 = (_Float16)(x4[2 * k] - (float)h0), l1 = (_Float16)(x4[2 * k + 1] - (float)h1);
-            hw[k] = __builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
-            lw[k] = __builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
-          }
-          uint16_t* o = po.planes + (long long)m * po.ldo + n;
-          *(uint2*)o = make_uint2(hw[0], hw[1]);
-          *(uint2*)(o + po.ps) = make_uint2(lw[0], lw[1]);
-          continue;
         }
         if constexpr ((VAR & 8) != 0) {  // (profiling) non-temporal output stores
           const f32x4v vv = {v.x, v.y, v.z, v.w};
@@ -1763,12 +1791,12 @@ extern "C" int rmbx_linear_f16x3_presplit_split(const void* a_planes, long long 
   RMBX_CHECK_ARG(M >= 0 && N > 0 && K > 0 && N % rmbx::GM_BN == 0 && K % rmbx::GM_BK == 0,
                  "%s: bad shape M=%d N=%d K=%d (N %% 128, K %% 32)", fn, M, N, K);
   RMBX_CHECK_ARG(lda >= K && lda % 8 == 0 && a_plane_stride % 8 == 0 && ldw >= K && ldw % 8 == 0 &&
-                     w_plane_stride % 8 == 0 && ldo >= N && ldo % 4 == 0 && out_plane_stride % 4 == 0 &&
+                     w_plane_stride % 8 == 0 && ldo >= N && ldo % 8 == 0 && out_plane_stride % 8 == 0 &&
                      out_plane_stride >= (long long)M * ldo,
                  "%s: bad strides lda=%lld ldw=%lld ldo=%lld", fn, lda, ldw, ldo);
-  RMBX_CHECK_ARG(((uintptr_t)a_planes | (uintptr_t)w_planes | (uintptr_t)bias | (uintptr_t)w_scale) % 16 == 0 &&
-                     (uintptr_t)out_planes % 8 == 0,
-                 "%s: operands must be 16-B aligned (out_planes 8-B)", fn);
+  RMBX_CHECK_ARG(((uintptr_t)a_planes | (uintptr_t)w_planes | (uintptr_t)bias | (uintptr_t)w_scale |
+                  (uintptr_t)out_planes) % 16 == 0,
+                 "%s: operands must be 16-B aligned", fn);
   RMBX_CHECK_ARG(w_norm_max >= 0.f && b_abs_max >= 0.f, "%s: bad bounds", fn);
   if (M == 0) return RMBX_OK;
   rmbx::GemmArgs g{nullptr, (const uint16_t*)w_planes, bias, nullptr, 0, 0, ldw, w_plane_stride, M, N, K,
