@@ -479,6 +479,10 @@ int rmbx_linear_f32x6_batched(const float* a, long long lda, long long a_bs, con
  * B^T d B of every 6x6 input window (in NHWC [N][H][W][C], T = N * ceil(H/4) * ceil(W/4) tiles), and
  * out NHWC = relu?(A^T M A + bias + res) from the position GEMM results M[36][T][C]. */
 int rmbx_wino4_input_f32(const float* in, int N, int H, int W, int C, float* V, void* stream);
+/* rmbx_wino4_input_f32 emitting V in rmbx_linear_f16x3_presplit's A form: V_planes [2][36][T][C] f16
+ * bits, each tile's 36 x C values scaled by one power of two (max in [2^13, 2^14)), rinv [T] = the
+ * inverse scales (the same for the tile's 36 position rows).  C <= 512. */
+int rmbx_wino4_input_split(const float* in, int N, int H, int W, int C, void* V_planes, float* rinv, void* stream);
 int rmbx_wino4_output_f32(const float* M, int N, int H, int W, int C, const float* bias, const float* res, float* out,
                           int relu, void* stream);
 /* Direct f32 convolution for few input channels (the 3-channel 7x7 / stride-2 stem of the diffusion
@@ -530,6 +534,14 @@ int rmbx_linear_f16x3_presplit_split(const void* a_planes, long long lda, long l
                                      const float* w_scale, float w_norm_max, float b_abs_max, const float* bias,
                                      int relu, void* out_planes, long long ldo, long long out_plane_stride,
                                      float* out_rinv, int M, int N, int K, void* stream);
+/* rmbx_linear_f16x3_presplit over `batch` items: item b reads a_planes + b a_bs, a_rinv + b r_bs,
+ * w_planes + b w_bs, w_scale + b ws_bs and writes c + b c_bs (bias shared, no residual).  The 36
+ * Winograd position GEMMs of rmbx_wino4_input_split's output. */
+int rmbx_linear_f16x3_presplit_batched(const void* a_planes, long long lda, long long a_plane_stride, long long a_bs,
+                                       const float* a_rinv, long long r_bs, const void* w_planes, long long ldw,
+                                       long long w_plane_stride, long long w_bs, const float* w_scale, long long ws_bs,
+                                       const float* bias, float* c, long long ldc, long long c_bs, int batch, int M,
+                                       int N, int K, int relu, void* stream);
 /* 3x3 / stride-1 / pad-1 rmbx_conv2d_f16x3 with each input pixel split once per output tile: the
  * block stages the input patch of its 16 x 16 (Cout % 128 == 0) or 16 x 32 output tile for one
  * 32-channel chunk as two f16 pieces in LDS, scaled per (tile, chunk) by a power of two, and all

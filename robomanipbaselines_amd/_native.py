@@ -98,6 +98,12 @@ SIGNATURES = {
                                                   ctypes.c_longlong, ctypes.c_longlong, _c_p, ctypes.c_float,
                                                   ctypes.c_float, _c_p, _c_int, _c_p, ctypes.c_longlong,
                                                   ctypes.c_longlong, _c_p, _c_int, _c_int, _c_int, _c_p]),
+    "rmbx_linear_f16x3_presplit_batched": (_c_int, [_c_p, ctypes.c_longlong, ctypes.c_longlong, ctypes.c_longlong, _c_p,
+                                                    ctypes.c_longlong, _c_p, ctypes.c_longlong, ctypes.c_longlong,
+                                                    ctypes.c_longlong, _c_p, ctypes.c_longlong, _c_p, _c_p,
+                                                    ctypes.c_longlong, ctypes.c_longlong, _c_int, _c_int, _c_int, _c_int,
+                                                    _c_int, _c_p]),
+    "rmbx_wino4_input_split": (_c_int, [_c_p, _c_int, _c_int, _c_int, _c_int, _c_p, _c_p, _c_p]),
     "rmbx_linear_f16x3_presplit": (_c_int, [_c_p, ctypes.c_longlong, ctypes.c_longlong, _c_p, _c_p, ctypes.c_longlong,
                                             ctypes.c_longlong, _c_p, _c_p, _c_p, _c_p, ctypes.c_longlong, _c_int, _c_int,
                                             _c_int, _c_int, _c_p]),

@@ -1266,7 +1266,8 @@ template <int GROUP, int VAR = 0, bool SPLIT_OUT = false>
 __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f16x3_presplit3_kernel(GemmArgs g, const uint16_t* __restrict__ Ap,
                                                                             long long aps, long long ldah,
                                                                             const float* __restrict__ arinv,
-                                                                            PresplitOut po = PresplitOut{}) {
+                                                                            PresplitOut po = PresplitOut{},
+                                                                            long long a_bs = 0, long long r_bs = 0) {
   constexpr int BN = 256, NJ = 8;
   constexpr int A_STAGE = 2 * GM_A_PLANE, B_PLANE = gm_b_plane<BN>(), W_STAGE = 2 * B_PLANE;  // 32 KiB each
   constexpr int W_RING = 3 * A_STAGE;
@@ -1279,7 +1280,17 @@ __global__ void __launch_bounds__(GM_THREADS, 1) gemm_f16x3_presplit3_kernel(Gem
   const int wm = wave & 3, wn = wave >> 2;
   const int nblk = gridDim.x, bid = blockIdx.x;
   const int xcd = bid & 7, q = nblk >> 3, r = nblk & 7;
-  const int lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  int lin = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + (bid >> 3);
+  if (g.batch > 1) {  // (rmbx_linear_f16x3_presplit_batched) consecutive tiles of an XCD stay in one item
+    const int per_item = g.tiles_m * g.tiles_n;
+    const int item = lin / per_item;
+    lin -= item * per_item;
+    Ap += item * a_bs;
+    arinv += item * r_bs;
+    g.W += item * g.w_bs;
+    g.C += item * g.c_bs;
+    g.ws += item * g.ws_bs;
+  }
   const int per_group = GROUP * g.tiles_n;
   const int first_m = (lin / per_group) * GROUP;
   const int gsize = min(g.tiles_m - first_m, GROUP);
@@ -1808,6 +1819,40 @@ extern "C" int rmbx_linear_f16x3_presplit_split(const void* a_planes, long long 
   rmbx::PresplitOut po{(uint16_t*)out_planes, ldo, out_plane_stride, out_rinv, a_norm, w_norm_max, b_abs_max};
   hipLaunchKernelGGL((rmbx::gemm_f16x3_presplit3_kernel<8, 0, true>), dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0,
                      (hipStream_t)stream, g, (const uint16_t*)a_planes, a_plane_stride, lda, a_rinv, po);
+  RMBX_CHECK_LAUNCH();
+  return RMBX_OK;
+}
+
+extern "C" int rmbx_linear_f16x3_presplit_batched(const void* a_planes, long long lda, long long a_plane_stride,
+                                                  long long a_bs, const float* a_rinv, long long r_bs,
+                                                  const void* w_planes, long long ldw, long long w_plane_stride,
+                                                  long long w_bs, const float* w_scale, long long ws_bs,
+                                                  const float* bias, float* c, long long ldc, long long c_bs,
+                                                  int batch, int M, int N, int K, int relu, void* stream) {
+  const char* fn = "rmbx_linear_f16x3_presplit_batched";
+  RMBX_CHECK_ARG(a_planes && a_rinv && w_planes && w_scale && c && batch >= 1, "%s: null pointer / batch", fn);
+  RMBX_CHECK_ARG(M >= 0 && N > 0 && K > 0 && N % rmbx::GM_BN == 0 && K % rmbx::GM_BK == 0,
+                 "%s: bad shape M=%d N=%d K=%d (N %% 128, K %% 32)", fn, M, N, K);
+  RMBX_CHECK_ARG(lda >= K && lda % 8 == 0 && a_plane_stride % 8 == 0 && a_bs % 8 == 0 && ldw >= K && ldw % 8 == 0 &&
+                     w_plane_stride % 8 == 0 && w_bs % 8 == 0 && ws_bs % 4 == 0 && ldc >= N && ldc % 4 == 0 &&
+                     c_bs % 4 == 0 && r_bs >= 0,
+                 "%s: bad strides", fn);
+  RMBX_CHECK_ARG(((uintptr_t)a_planes | (uintptr_t)w_planes | (uintptr_t)c | (uintptr_t)bias | (uintptr_t)w_scale) % 16 ==
+                     0,
+                 "%s: operands must be 16-B aligned", fn);
+  if (M == 0) return RMBX_OK;
+  rmbx::GemmArgs g{nullptr, (const uint16_t*)w_planes, bias, c, 0, ldc, ldw, w_plane_stride, M, N, K, relu ? 1 : 0,
+                   (M + rmbx::GM_BM - 1) / rmbx::GM_BM, (N + 255) / 256, nullptr};
+  g.batch = batch;
+  g.w_bs = w_bs;
+  g.c_bs = c_bs;
+  g.ws = w_scale;
+  g.ws_bs = ws_bs;
+  const long long blocks = (long long)g.tiles_m * g.tiles_n * batch;
+  RMBX_CHECK_ARG(blocks < (1ll << 31), "%s: too many tiles", fn);
+  hipLaunchKernelGGL((rmbx::gemm_f16x3_presplit3_kernel<8, 0, false>), dim3((unsigned)blocks), dim3(rmbx::GM_THREADS), 0,
+                     (hipStream_t)stream, g, (const uint16_t*)a_planes, a_plane_stride, lda, a_rinv, rmbx::PresplitOut{},
+                     a_bs, r_bs);
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
 }

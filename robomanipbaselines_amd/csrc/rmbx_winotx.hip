@@ -81,6 +81,82 @@ __global__ void __launch_bounds__(256) wino4_input_kernel(const float* __restric
   }
 }
 
+// Input transform emitting the position GEMMs' A in the pre-split form (rmbx_linear_f16x3_presplit
+// _batched): block = one tile, thread = channels tid, tid + 256, ...; the tile's 36 x C transformed
+// values are scaled by one power of two 2^t putting their max |v| in [2^13, 2^14) (a block max
+// reduction), hi = f16(v 2^t), lo = f16(v 2^t - hi) into planes [2][36][T][C], rinv[t] = 2^-t.  One
+// scale per tile for all 36 positions: a position whose values are far below the tile's max keeps
+// its pieces exact to 2^-38 of that max (f16 subnormal low pieces below 2^-16 of it), well inside
+// the transform's own rounding.  The scale comes from the tile's own inputs (batch-invariant).
+__global__ void __launch_bounds__(256) wino4_input_split_kernel(const float* __restrict__ in, uint16_t* __restrict__ Vp,
+                                                                float* __restrict__ rinv, int H, int W, int C,
+                                                                int ty_n, int tx_n, long long T) {
+  // thread = two adjacent channels 2 tid, 2 tid + 1 (8-byte loads, 4-byte piece stores); C = 2 blockDim
+  __shared__ float red[4];
+  const long long t = blockIdx.x;
+  const int tx = (int)(t % tx_n);
+  const long long q = t / tx_n;
+  const int ty = (int)(q % ty_n);
+  const long long img = q / ty_n;
+  const int y0 = 4 * ty - 1, x0 = 4 * tx - 1;
+  const int c = 2 * threadIdx.x;
+  const float* base = in + img * H * (long long)W * C + c;
+  float v[2][36];
+  float mx = 0.f;
+  {
+    float d[2][6][6];
+#pragma unroll
+    for (int i = 0; i < 6; ++i)
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        const int y = y0 + i, x = x0 + j;
+        float2 dv = make_float2(0.f, 0.f);
+        if ((unsigned)y < (unsigned)H && (unsigned)x < (unsigned)W) dv = *(const float2*)(base + ((long long)y * W + x) * C);
+        d[0][i][j] = dv.x;
+        d[1][i][j] = dv.y;
+      }
+#pragma unroll
+    for (int k = 0; k < 2; ++k) {
+      float r[6][6];
+#pragma unroll
+      for (int i = 0; i < 6; ++i) bt6(d[k][i], r[i]);
+#pragma unroll
+      for (int j = 0; j < 6; ++j) {
+        float col[6], vv[6];
+#pragma unroll
+        for (int i = 0; i < 6; ++i) col[i] = r[i][j];
+        bt6(col, vv);
+#pragma unroll
+        for (int i = 0; i < 6; ++i) {
+          v[k][i * 6 + j] = vv[i];
+          mx = fmaxf(mx, fabsf(vv[i]));
+        }
+      }
+    }
+  }
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off));
+  const int nw = (blockDim.x + 63) >> 6;
+  if ((threadIdx.x & 63) == 0) red[threadIdx.x >> 6] = mx;
+  __syncthreads();
+  mx = red[0];
+  for (int w = 1; w < nw; ++w) mx = fmaxf(mx, red[w]);
+  int e = 14;
+  if (mx > 0.f && mx <= 3.4e38f) frexpf(mx, &e);  // NaN / inf: scale 1, propagated
+  const float sc = ldexpf(1.f, 14 - e);
+  if (threadIdx.x == 0) rinv[t] = ldexpf(1.f, e - 14);
+  const long long ps = T * C, plane = 36 * ps;
+  uint32_t* o = reinterpret_cast<uint32_t*>(Vp + t * C + c);
+#pragma unroll
+  for (int p = 0; p < 36; ++p) {
+    const float a0 = v[0][p] * sc, a1 = v[1][p] * sc;
+    const _Float16 h0 = (_Float16)a0, h1 = (_Float16)a1;
+    const _Float16 l0 = (_Float16)(a0 - (float)h0), l1 = (_Float16)(a1 - (float)h1);
+    o[p * ps / 2] = __builtin_bit_cast(uint16_t, h0) | ((uint32_t)__builtin_bit_cast(uint16_t, h1) << 16);
+    o[(plane + p * ps) / 2] = __builtin_bit_cast(uint16_t, l0) | ((uint32_t)__builtin_bit_cast(uint16_t, l1) << 16);
+  }
+}
+
 __global__ void __launch_bounds__(256) wino4_output_kernel(const float* __restrict__ M, const float* __restrict__ bias,
                                                            const float* __restrict__ res, float* __restrict__ out,
                                                            int H, int W, int C, int ty_n, int tx_n, long long T,
@@ -137,6 +213,21 @@ extern "C" int rmbx_wino4_input_f32(const float* in, int N, int H, int W, int C,
   const long long n = T * C;
   hipLaunchKernelGGL(rmbx::wino4_input_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
                      in, V, H, W, C, ty, tx, T);
+  RMBX_CHECK_LAUNCH();
+  return RMBX_OK;
+}
+
+extern "C" int rmbx_wino4_input_split(const float* in, int N, int H, int W, int C, void* V_planes, float* rinv,
+                                      void* stream) {
+  RMBX_CHECK_ARG(in && V_planes && rinv && N >= 0 && H > 0 && W > 0 && C > 0 && C <= 512 && C % 2 == 0,
+                 "rmbx_wino4_input_split: bad arguments (C even, <= 512)");
+  RMBX_CHECK_ARG(((uintptr_t)in % 8) == 0 && ((uintptr_t)V_planes % 4) == 0, "rmbx_wino4_input_split: unaligned");
+  const int ty = (H + 3) / 4, tx = (W + 3) / 4;
+  const long long T = (long long)N * ty * tx;
+  if (T == 0) return RMBX_OK;
+  RMBX_CHECK_ARG(T < (1ll << 31), "rmbx_wino4_input_split: too many tiles");
+  hipLaunchKernelGGL(rmbx::wino4_input_split_kernel, dim3((unsigned)T), dim3(C / 2), 0, (hipStream_t)stream, in,
+                     (uint16_t*)V_planes, rinv, H, W, C, ty, tx, T);
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
 }

@@ -1239,10 +1239,23 @@ def conv3x3_wino4_x6(x, planes, bias, relu=False, res=None):
         if tuple(res.shape) != tuple(out.shape) or res.dtype != torch.float32:
             raise ValueError("res must match the output")
     T = n * ((H + 3) // 4) * ((W + 3) // 4)
-    V = torch.empty((36, T, C), dtype=torch.float32, device=x.device)
-    N.call("rmbx_wino4_input_f32", N.ptr(x), n, H, W, C, N.ptr(V), N.stream_ptr())
     M = torch.empty((36, T, co), dtype=torch.float32, device=x.device)
     name, flops = f"winograd x36 M={T} N={co} K={C}", 2.0 * 36 * T * co * C
+    if h3 and GEMM_PRESPLIT and C <= 512 and co % LINEAR_F32X6_BN == 0:
+        # the input transform writes the position GEMMs' A pre-split (one power-of-two scale per tile)
+        Vp = torch.empty((2, 36, T, C), dtype=torch.float16, device=x.device)
+        rinv = torch.empty(T, dtype=torch.float32, device=x.device)
+        N.call("rmbx_wino4_input_split", N.ptr(x), n, H, W, C, N.ptr(Vp), N.ptr(rinv), N.stream_ptr())
+        p = planes.planes
+        _gemm_launch(name + " presplit", flops, 36 * (4 * T * C + 4 * co * C + 4 * T * co), 3,
+                     "rmbx_linear_f16x3_presplit_batched", N.ptr(Vp), C, Vp.stride(0), T * C, N.ptr(rinv), 0, N.ptr(p),
+                     p.stride(1), p.stride(0), co * C, N.ptr(planes.scale), co, None, N.ptr(M), co, T * co, 36, T, co, C,
+                     0, N.stream_ptr())
+        N.call("rmbx_wino4_output_f32", N.ptr(M), n, H, W, co, N.ptr(bias), N.ptr(res), N.ptr(out), 1 if relu else 0,
+               N.stream_ptr())
+        return out
+    V = torch.empty((36, T, C), dtype=torch.float32, device=x.device)
+    N.call("rmbx_wino4_input_f32", N.ptr(x), n, H, W, C, N.ptr(V), N.stream_ptr())
     if h3:
         p = planes.planes
         _gemm_launch(name, flops, 36 * (4 * T * C + 4 * co * C + 4 * T * co), 3, "rmbx_linear_f16x3_batched", N.ptr(V),

@@ -193,3 +193,44 @@ def test_ffn_chain_in_presplit_form(M, scale):
     base = F.linear(F.linear(a, w1, b1).clamp_min(0), w2, b2)
     e, e32 = _err(out, ref), _err(base, ref)
     assert e <= 4e-6 and e <= 2 * e32 + 1e-7, (e, e32)
+
+
+@torch.no_grad()
+@pytest.mark.parametrize("n,C,H,W,res,relu", [(2, 256, 30, 40, True, True), (3, 512, 15, 20, False, True),
+                                              (1, 256, 7, 9, True, False)])
+def test_winograd_presplit_vs_f64_and_batch_invariance(monkeypatch, n, C, H, W, res, relu):
+    """The explicit Winograd conv with the input transform emitting the position GEMMs' A pre-split
+    (rmbx_wino4_input_split, one scale per tile) and the 36 batched pre-split GEMMs: within the
+    Winograd bar of an f64 conv (1e-5, as the in-register form, checked beside it), and an image's
+    output does not depend on the other images of the batch (bitwise)."""
+    from robomanipbaselines_amd import kernels as K_
+
+    g = torch.Generator(device="cpu").manual_seed(C + H + 1)
+    x = torch.randn(n, C, H, W, generator=g).clamp_min(0)
+    x[0] *= 1e-3  # images of very different magnitude share the batch
+    w = torch.randn(C, C, 3, 3, generator=g) / (C * 9) ** 0.5
+    b = torch.randn(C, generator=g)
+    r = torch.randn(n, C, H, W, generator=g) if res else None
+    cl = torch.channels_last
+    planes = K_.pack_wino4_x6(w.to(DEV))
+    xd = x.to(DEV).contiguous(memory_format=cl)
+    rd = None if r is None else r.to(DEV).contiguous(memory_format=cl)
+    monkeypatch.setattr(K_, "GEMM_PRESPLIT", True)
+    got = K_.conv3x3_wino4_x6(xd, planes, b.to(DEV), relu=relu, res=rd)
+    monkeypatch.setattr(K_, "GEMM_PRESPLIT", False)
+    plain = K_.conv3x3_wino4_x6(xd, planes, b.to(DEV), relu=relu, res=rd)
+    ref = F.conv2d(x.double(), w.double(), b.double(), 1, 1)
+    if r is not None:
+        ref = ref + r.double()
+    if relu:
+        ref = ref.clamp_min(0)
+    scale = ref.abs().max()
+    for i in range(n):  # per image (the images' magnitudes differ by 1e3)
+        si = ref[i].abs().max()
+        assert ((got[i].cpu().double() - ref[i]).abs().max() / si).item() <= 1e-5, i
+        assert ((plain[i].cpu().double() - ref[i]).abs().max() / si).item() <= 1e-5, i
+    assert ((got.cpu().double() - ref).abs().max() / scale).item() <= 1e-5
+    monkeypatch.setattr(K_, "GEMM_PRESPLIT", True)
+    last = K_.conv3x3_wino4_x6(xd[n - 1:].contiguous(memory_format=cl), planes, b.to(DEV), relu=relu,
+                               res=None if rd is None else rd[n - 1:].contiguous(memory_format=cl))
+    assert torch.equal(last[0], got[n - 1])
