@@ -658,6 +658,9 @@ __device__ __forceinline__ void ah_split_w(float x, float y, uint32_t& h, uint32
   l = ah_pk(x - ah_lo(h), y - ah_hi(h));
 }
 
+// DBG (profiling phase skips, RMBX_ATTN_F16_DBG; wrong results, timing only): 1 = no V^T staging
+// stores, 2 = no S^T MFMAs, 4 = no softmax (fixed P'), 8 = no PV MFMAs, 16 = no K / V tile loads
+template <int DBG>
 __global__ void __launch_bounds__(64 * AX_MAX_WAVES) attn_fwd_f16x3_kernel(AttnF32Args a) {
   __shared__ __attribute__((aligned(16))) uint16_t sA[2 * AH_BUF];
   __shared__ uint32_t sDim[64];  // per head dimension: max |v| over the keys (f32 bits)
@@ -740,7 +743,7 @@ __global__ void __launch_bounds__(64 * AX_MAX_WAVES) attn_fwd_f16x3_kernel(AttnF
     for (int i = 0; i < AX_CH; ++i) {
       const int q = tid + nthreads * i;
       const int qq = q & 511, key = 32 * t + (qq >> 4), quad = qq & 15;
-      const bool ok = q < 1024 && key < a.Lk;
+      const bool ok = q < 1024 && key < a.Lk && ((DBG & 16) == 0 || t == 0);
       const float* src = q < 512 ? kbase + (size_t)key * a.k_rstride : vbase + (size_t)key * a.v_rstride;
       st[i] = ok ? *reinterpret_cast<const float4*>(src + 4 * quad) : make_float4(0.f, 0.f, 0.f, 0.f);
     }
@@ -761,7 +764,7 @@ __global__ void __launch_bounds__(64 * AX_MAX_WAVES) attn_fwd_f16x3_kernel(AttnF
         const int off = key * 64 + (((quad >> 1) ^ ((key >> 1) & 7)) << 3) + 4 * (quad & 1);
         *reinterpret_cast<uint2*>(buf + off) = make_uint2(h[0], h[1]);
         *reinterpret_cast<uint2*>(buf + AH_PLANE + off) = make_uint2(l[0], l[1]);
-      } else {  // V^T: 4 dims of one key = one element in each of 4 rows
+      } else if ((DBG & 1) == 0) {  // V^T: 4 dims of one key = one element in each of 4 rows
         vmax[0] = fmaxf(vmax[0], ax);
         vmax[1] = fmaxf(vmax[1], ay);
         vmax[2] = fmaxf(vmax[2], az);
@@ -798,9 +801,13 @@ __global__ void __launch_bounds__(64 * AX_MAX_WAVES) attn_fwd_f16x3_kernel(AttnF
       const int off = r32 * 64 + (((2 * ks + kh) ^ ((r32 >> 1) & 7)) << 3);
       const f16x8 k0 = *reinterpret_cast<const f16x8*>(buf + off);
       const f16x8 k1 = *reinterpret_cast<const f16x8*>(buf + AH_PLANE + off);
-      s = __builtin_amdgcn_mfma_f32_32x32x16_f16(k1, fq[ks][2], s, 0, 0, 0);
-      s = __builtin_amdgcn_mfma_f32_32x32x16_f16(k0, fq[ks][1], s, 0, 0, 0);
-      s = __builtin_amdgcn_mfma_f32_32x32x16_f16(k0, fq[ks][0], s, 0, 0, 0);
+      if constexpr ((DBG & 2) != 0) {
+        s[ks] += (float)k0[0] + (float)k1[0];
+      } else {
+        s = __builtin_amdgcn_mfma_f32_32x32x16_f16(k1, fq[ks][2], s, 0, 0, 0);
+        s = __builtin_amdgcn_mfma_f32_32x32x16_f16(k0, fq[ks][1], s, 0, 0, 0);
+        s = __builtin_amdgcn_mfma_f32_32x32x16_f16(k0, fq[ks][0], s, 0, 0, 0);
+      }
     }
     if (ragged && t == nt - 1) {
 #pragma unroll
@@ -808,11 +815,13 @@ __global__ void __launch_bounds__(64 * AX_MAX_WAVES) attn_fwd_f16x3_kernel(AttnF
         if (32 * t + 4 * kh + (j & 3) + 8 * (j >> 2) >= a.Lk) s[j] = -INFINITY;
     }
     float mx = s[0];
+    if constexpr ((DBG & 4) == 0) {
 #pragma unroll
-    for (int j = 1; j < 16; ++j) mx = fmaxf(mx, s[j]);
-    mx = fmaxf(mx, __shfl_xor(mx, 32));
+      for (int j = 1; j < 16; ++j) mx = fmaxf(mx, s[j]);
+      mx = fmaxf(mx, __shfl_xor(mx, 32));
+    }
     const float m_new = fmaxf(m_run, mx);
-    if (__any(m_new != m_run)) {
+    if ((DBG & 4) == 0 && __any(m_new != m_run)) {
       const float alpha = exp2f((m_run - m_new) * c);  // first tile: exp2(-inf) = 0
       l_run *= alpha;
 #pragma unroll
@@ -830,6 +839,11 @@ __global__ void __launch_bounds__(64 * AX_MAX_WAVES) attn_fwd_f16x3_kernel(AttnF
       uint32_t h[4], l[4];
 #pragma unroll
       for (int e = 0; e < 4; ++e) {
+        if constexpr ((DBG & 4) != 0) {
+          h[e] = __float_as_uint(s[8 * u + 2 * e]);
+          l[e] = __float_as_uint(s[8 * u + 2 * e + 1]);
+          continue;
+        }
         const float pa = exp2f(fmaf(s[8 * u + 2 * e], c, -mc)) * 16384.f;
         const float pb = exp2f(fmaf(s[8 * u + 2 * e + 1], c, -mc)) * 16384.f;
         l_run += pa + pb;
@@ -849,6 +863,11 @@ __global__ void __launch_bounds__(64 * AX_MAX_WAVES) attn_fwd_f16x3_kernel(AttnF
       for (int pc = 0; pc < 2; ++pc) {
         v0[pc] = *reinterpret_cast<const f16x8*>(buf + o0 + pc * AH_PLANE);
         v1[pc] = *reinterpret_cast<const f16x8*>(buf + o1 + pc * AH_PLANE);
+      }
+      if constexpr ((DBG & 8) != 0) {
+        acc0[u] += (float)v0[1][0] + (float)v0[0][0] + (float)fp[u][0][0] + (float)fp[u][1][0] + (float)fp[u][2][0];
+        acc1[u] += (float)v1[1][0] + (float)v1[0][0];
+        continue;
       }
       acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v0[1], fp[u][2], acc0, 0, 0, 0);
       acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v1[1], fp[u][2], acc1, 0, 0, 0);
@@ -1075,7 +1094,20 @@ extern "C" int rmbx_attention_f16x3(const float* q, const float* k, const float*
   RMBX_CHECK_ARG(nblocks < (1ll << 31), "rmbx_attention_f16x3: grid too large");
   // the f16x3 pass, then the bf16x6 kernel over the same blocks: it returns at once for every block
   // the first pass did not flag (redo[block] = 0), so both write each query once
-  hipLaunchKernelGGL(rmbx::attn_fwd_f16x3_kernel, dim3((unsigned)nblocks), dim3(64 * waves), 0, (hipStream_t)stream, a);
+  const char* de = std::getenv("RMBX_ATTN_F16_DBG");  // profiling phase skips (read per launch)
+  const int dbg = de ? std::atoi(de) : 0;
+  const dim3 g((unsigned)nblocks), blk(64 * waves);
+  switch (dbg) {
+    case 0: hipLaunchKernelGGL(rmbx::attn_fwd_f16x3_kernel<0>, g, blk, 0, (hipStream_t)stream, a); break;
+    case 1: hipLaunchKernelGGL(rmbx::attn_fwd_f16x3_kernel<1>, g, blk, 0, (hipStream_t)stream, a); break;
+    case 2: hipLaunchKernelGGL(rmbx::attn_fwd_f16x3_kernel<2>, g, blk, 0, (hipStream_t)stream, a); break;
+    case 4: hipLaunchKernelGGL(rmbx::attn_fwd_f16x3_kernel<4>, g, blk, 0, (hipStream_t)stream, a); break;
+    case 8: hipLaunchKernelGGL(rmbx::attn_fwd_f16x3_kernel<8>, g, blk, 0, (hipStream_t)stream, a); break;
+    case 16: hipLaunchKernelGGL(rmbx::attn_fwd_f16x3_kernel<16>, g, blk, 0, (hipStream_t)stream, a); break;
+    case 10: hipLaunchKernelGGL(rmbx::attn_fwd_f16x3_kernel<10>, g, blk, 0, (hipStream_t)stream, a); break;
+    case 15: hipLaunchKernelGGL(rmbx::attn_fwd_f16x3_kernel<15>, g, blk, 0, (hipStream_t)stream, a); break;
+    default: RMBX_CHECK_ARG(false, "rmbx_attention_f16x3: RMBX_ATTN_F16_DBG=%d not instantiated", dbg);
+  }
   RMBX_CHECK_LAUNCH();
   hipLaunchKernelGGL(rmbx::attn_fwd_f32x6_kernel, dim3((unsigned)nblocks), dim3(64 * waves), 0, (hipStream_t)stream, a);
   RMBX_CHECK_LAUNCH();
