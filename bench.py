@@ -225,6 +225,25 @@ def gemm_probe(ro):
     return _probe_line(gemm, True), _probe_line(patch, False)
 
 
+def gemm_library_ceiling():
+    """The vendor library's f16 GEMM running the same MFMA work as the f16x3 form (K tripled, f32 out)
+    at the ACT shapes, from the latest committed calibration (scripts/prof_blas_f16_ceiling.py ->
+    profiles/r<round>_blas_f16_ceiling.json): {"source", "hipblaslt_frac": {shape: fraction of the
+    dense peak}} or None."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_blas_f16_ceiling.json")))
+    if not files:
+        return None
+    with open(files[-1]) as f:
+        d = json.load(f)
+    lt = d.get("libraries", {}).get("hipblaslt", {})
+    return {"source": os.path.relpath(files[-1], ROOT),
+            "hipblaslt_frac": {k: v["frac_f32_out"] for k, v in lt.items()},
+            "note": "hipBLASLt f16 GEMM over [ah, ah, al] x [wh, wl, 2^-11 wh] (the same MFMA work as f16x3), f32 out, "
+                    "same chip; the per_shape table above is this kernel at those shapes"}
+
+
 def _probe_line(probe, is_gemm):
     if not probe:
         return None
@@ -269,7 +288,8 @@ def _probe_line(probe, is_gemm):
             "launches_per_inference": n, "avg_launch_us": round(1e3 * ms / n, 1),
             "ms_per_inference": round(ms, 3),
             "per_shape": {k: {"launches": L["launches"], "ms": round(L["ms"], 3),
-                              "fp32_equiv_TFLOPs": round(L["flops"] / L["ms"] / 1e9, 1)} for k, L in shapes.items()}}
+                              "fp32_equiv_TFLOPs": round(L["flops"] / L["ms"] / 1e9, 1)} for k, L in shapes.items()},
+            "library_ceiling": gemm_library_ceiling() if is_gemm else None}
 
 
 def policy_flops_per_inference(full_decoder):
