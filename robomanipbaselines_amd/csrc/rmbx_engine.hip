@@ -310,9 +310,12 @@ __device__ void kinematics(Env& e, int lane, int* s_anc) {
 // front-kernel LDS map (doubles): xpos 3nb | xquat 4nb | xmat 9nb | cvel 6nb | cacc 6nb |
 // cfrc 6nb | cdofdot 6nv | cinert 10nb | cdof 6nv | crb 10nb
 __host__ __device__ __forceinline__ size_t front_lds_doubles(int nb, int nv) { return 54 * (size_t)nb + 12 * (size_t)nv; }
+// front kernel LDS: [0, 16 nb) xpos / xquat / xmat; [16 nb, 34 nb + 6 nv) cvel, cacc, cfrc, cdofdot;
+// cinert [10 nb]; crb [10 nb] (dead once the mass matrix is written); cdof [6 nv] (live to the end)
+// last, so everything from 16 nb up to cdof is one region the collision stage can reuse
 #define LDS_CINERT(e) ((e).sh + 34 * (e).m->nbody + 6 * (e).m->nv)
-#define LDS_CDOF(e) (LDS_CINERT(e) + 10 * (e).m->nbody)
-#define LDS_CRB(e) (LDS_CDOF(e) + 6 * (e).m->nv)
+#define LDS_CRB(e) (LDS_CINERT(e) + 10 * (e).m->nbody)
+#define LDS_CDOF(e) (LDS_CRB(e) + 10 * (e).m->nbody)
 
 __device__ void com_pos_crb(Env& e, int lane, const int32_t* subtree_end) {
   const rmbx_model& m = *e.m;
@@ -1606,9 +1609,11 @@ __host__ __device__ __forceinline__ size_t collision_lds_doubles(int ngeom, int 
   return 8 * (size_t)ngeom + (size_t)collision_cap(npair) + 2 + runs;
 }
 __host__ __device__ __forceinline__ size_t collision_lds_free_doubles(int nb, int nv) {
-  return 28 * (size_t)nb + 6 * (size_t)nv;  // cvel, cacc, cfrc, cdofdot, cinert
+  return 38 * (size_t)nb + 6 * (size_t)nv;  // cvel, cacc, cfrc, cdofdot, cinert, crb
 }
-// (cdof, still live, follows the free region: a model that does not fit takes its own space)
+// (cdof, still live, follows the free region: a model that does not fit takes its own space.  The
+// cable scene's collision scratch, 2,366 doubles, fits the 2,498 of this region: 29.6 KiB of LDS
+// per env instead of 48.1, so four envs per CU and all 1,024 in one round of blocks)
 static inline size_t front_kernel_lds_bytes(const rmbx_model& h, int nprun) {
   const size_t need = collision_lds_doubles(h.ngeom, h.npair, h.nbody, nprun);
   const size_t extra = need <= collision_lds_free_doubles(h.nbody, h.nv) ? 0 : need;
