@@ -310,9 +310,9 @@ __device__ void kinematics(Env& e, int lane, int* s_anc) {
 // front-kernel LDS map (doubles): xpos 3nb | xquat 4nb | xmat 9nb | cvel 6nb | cacc 6nb |
 // cfrc 6nb | cdofdot 6nv | cinert 10nb | cdof 6nv | crb 10nb
 __host__ __device__ __forceinline__ size_t front_lds_doubles(int nb, int nv) { return 54 * (size_t)nb + 12 * (size_t)nv; }
-// front kernel LDS: [0, 16 nb) xpos / xquat / xmat; [16 nb, 34 nb + 6 nv) cvel, cacc, cfrc, cdofdot;
-// cinert [10 nb]; crb [10 nb] (dead once the mass matrix is written); cdof [6 nv] (live to the end)
-// last, so everything from 16 nb up to cdof is one region the collision stage can reuse
+// front kernel LDS: [0, 16 nb) xpos / xquat / xmat (live to the end); [16 nb, 34 nb + 6 nv) cvel,
+// cacc, cfrc, cdofdot; cinert [10 nb]; crb [10 nb] (dead once the mass matrix is written); cdof
+// [6 nv] -- all of [16 nb, ...) dead after the velocity stage and reused by the collision stage
 #define LDS_CINERT(e) ((e).sh + 34 * (e).m->nbody + 6 * (e).m->nv)
 #define LDS_CRB(e) (LDS_CINERT(e) + 10 * (e).m->nbody)
 #define LDS_CDOF(e) (LDS_CRB(e) + 10 * (e).m->nbody)
@@ -1608,23 +1608,24 @@ __host__ __device__ __forceinline__ size_t collision_lds_doubles(int ngeom, int 
   const size_t runs = nprun > 0 ? 6 * (size_t)nbody + 65 : 0;
   return 8 * (size_t)ngeom + (size_t)collision_cap(npair) + 2 + runs;
 }
-__host__ __device__ __forceinline__ size_t collision_lds_free_doubles(int nb, int nv) {
-  return 38 * (size_t)nb + 6 * (size_t)nv;  // cvel, cacc, cfrc, cdofdot, cinert, crb
+// The collision scratch starts at 16 nb: everything above the body frames (cvel, cacc, cfrc,
+// cdofdot, cinert, crb, cdof) is dead once the velocity stage has copied it out, and a model whose
+// scratch is larger runs past the end of that region.  The cable scene's 2,366 doubles fit in
+// the 2,906 there: 29.6 KiB of LDS per env instead of 48.1, so four envs per CU and all 1,024 in
+// one round of blocks; the Pick scene's 5,085 take it to 45.1 KiB (three envs per CU, was 61.5: two)
+__host__ __device__ __forceinline__ size_t front_kernel_lds_doubles(int nb, int nv, size_t need) {
+  const size_t front = front_lds_doubles(nb, nv), coll = 16 * (size_t)nb + need;
+  return front > coll ? front : coll;
 }
-// (cdof, still live, follows the free region: a model that does not fit takes its own space.  The
-// cable scene's collision scratch, 2,366 doubles, fits the 2,498 of this region: 29.6 KiB of LDS
-// per env instead of 48.1, so four envs per CU and all 1,024 in one round of blocks)
 static inline size_t front_kernel_lds_bytes(const rmbx_model& h, int nprun) {
   const size_t need = collision_lds_doubles(h.ngeom, h.npair, h.nbody, nprun);
-  const size_t extra = need <= collision_lds_free_doubles(h.nbody, h.nv) ? 0 : need;
-  return (front_lds_doubles(h.nbody, h.nv) + extra) * sizeof(double);
+  return front_kernel_lds_doubles(h.nbody, h.nv, need) * sizeof(double);
 }
 __device__ __forceinline__ CollisionLds collision_lds(const Env& e, const PairRuns& pr) {
   const rmbx_model& m = *e.m;
   CollisionLds cl;
-  const bool fits = collision_lds_doubles(m.ngeom, m.npair, m.nbody, pr.n) <= collision_lds_free_doubles(m.nbody, m.nv);
   const int cap = collision_cap(m.npair);
-  cl.geom = fits ? e.sh + 16 * m.nbody : e.sh + front_lds_doubles(m.nbody, m.nv);
+  cl.geom = e.sh + 16 * m.nbody;  // (front_kernel_lds_bytes sized the LDS for it)
   cl.spair = reinterpret_cast<int32_t*>(cl.geom + 8 * m.ngeom);
   cl.list = reinterpret_cast<int16_t*>(cl.spair + cap);
   cl.count = reinterpret_cast<uint8_t*>(cl.list + cap);
