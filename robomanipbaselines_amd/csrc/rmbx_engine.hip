@@ -85,6 +85,7 @@ struct rmbx_engine {
   int n_env;
   rmbx_env_buffers bufs;
   bool bound;
+  size_t front_lds;  // dynamic LDS of a front-kernel launch (front_launch_lds)
 };
 
 namespace rmbx {
@@ -3750,6 +3751,8 @@ static Layout make_layout(const rmbx_model& m) {
 
 using namespace rmbx;
 
+static size_t front_launch_lds(const rmbx_engine* eng);
+
 // ------------------------------------------------------------------------------------------
 // C ABI
 // ------------------------------------------------------------------------------------------
@@ -3926,6 +3929,7 @@ int rmbx_engine_create(const struct rmbx_model* model, int n_env, rmbx_engine** 
     return st;
   }
   eng->L = make_layout(h);
+  eng->front_lds = front_launch_lds(eng);
   *out = eng;
   return RMBX_OK;
 }
@@ -4003,6 +4007,41 @@ int rmbx_engine_bind(rmbx_engine* eng, const rmbx_env_buffers* bufs) {
   return RMBX_OK;
 }
 
+// Dynamic LDS of a front-kernel launch: the model's need, padded so the n_env blocks spread
+// evenly over their rounds of blocks.  With k envs fitting a CU (LDS- or register-bound) the launch
+// takes R = ceil(n_env / (k CUs)) rounds; asking for LDS that admits only ceil(n_env / (R CUs)) per
+// CU gives every CU the same count in every round (otherwise the dispatcher may stack k on some
+// CUs and leave others short, or run a last round of a few envs alone).  RMBX_FRONT_BALANCE=0: the
+// plain need.
+static size_t front_launch_lds(const rmbx_engine* eng) {
+  const size_t need = front_kernel_lds_bytes(eng->host, eng->nprun);
+  const char* be = std::getenv("RMBX_FRONT_BALANCE");
+  if (be && std::atoi(be) == 0) return need;
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+      cus <= 0)
+    return need;
+  hipFuncAttributes fa{};
+  const void* fn = eng->nprun > 0 ? reinterpret_cast<const void*>(&front_kernel<true>)
+                                  : reinterpret_cast<const void*>(&front_kernel<false>);
+  if (hipFuncGetAttributes(&fa, fn) != hipSuccess) return need;
+  const size_t cu_lds = 160 * 1024, stat = fa.sharedSizeBytes;
+  const int regs = fa.numRegs > 0 ? fa.numRegs : 256;
+  const int k_reg = 4 * (512 / (((regs + 7) / 8) * 8));  // one wave per env, four SIMDs
+  int k = (int)(cu_lds / (need + stat));
+  if (k > k_reg) k = k_reg;
+  if (k < 2) return need;
+  const long long n = eng->n_env;
+  const long long R = (n + (long long)k * cus - 1) / ((long long)k * cus);
+  const int occ = (int)((n + R * cus - 1) / (R * cus));
+  if (occ >= k || occ < 1) return need;
+  size_t dyn = cu_lds / occ - stat;
+  if (dyn > 65536) dyn = 65536;
+  dyn &= ~(size_t)15;
+  if (dyn < need || (int)(cu_lds / (dyn + stat)) != occ) return need;
+  return dyn;
+}
+
 static int launch(rmbx_engine* eng, int nsub, int integ, const uint8_t* active, void* stream,
                   unsigned long long* prof = nullptr) {
   if (!eng->bound) {
@@ -4031,7 +4070,7 @@ static int launch(rmbx_engine* eng, int nsub, int integ, const uint8_t* active, 
   const int reps = integ ? nsub : 1;
   for (int s = 0; s < reps; s++) {
     a.sub = s + 1;
-    const size_t front_lds = front_kernel_lds_bytes(eng->host, eng->nprun);
+    const size_t front_lds = eng->front_lds;
     if (eng->nprun > 0)
       hipLaunchKernelGGL(front_kernel<true>, dim3(eng->n_env), dim3(64), front_lds, st, a);
     else
@@ -4046,7 +4085,7 @@ static int launch(rmbx_engine* eng, int nsub, int integ, const uint8_t* active, 
     a.sub = nsub + 1;
     a.redo = 1;
     a.prof = nullptr;
-    const size_t front_lds = front_kernel_lds_bytes(eng->host, eng->nprun);
+    const size_t front_lds = eng->front_lds;
     if (eng->nprun > 0)
       hipLaunchKernelGGL(front_kernel<true>, dim3(eng->n_env), dim3(64), front_lds, st, a);
     else
