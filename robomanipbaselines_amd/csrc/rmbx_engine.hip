@@ -1424,13 +1424,16 @@ enum { CLS_PLANE = 0, CLS_SPH_SPH, CLS_SPH_CAP, CLS_SPH_BOX, CLS_CAP_CAP, CLS_CA
 
 // Broadphase record of one geom in LDS (8 doubles): centre, AABB half-extent (a plane: its
 // normal), bounding radius, type.
-__device__ void geom_record(const Env& e, int g, double* r) {
+// broadphase record of geom g: center [3], half-extents (plane: normal) [3], rbound; the type goes to
+// a byte array beside the records (gtype)
+constexpr int GREC = 7;
+__device__ void geom_record(const Env& e, int g, double* r, uint8_t* gtype) {
   const rmbx_model& m = *e.m;
   const double* c = e.gxpos + 3 * g;
   const double* R = e.gxmat + 9 * g;
   const double* s = m.geom_csize + 3 * g;
   const int t = m.geom_ctype[g];
-  double x[8];
+  double x[GREC];
   for (int i = 0; i < 3; i++) {
     x[i] = c[i];
     if (t == RMBX_GEOM_PLANE)
@@ -1443,19 +1446,19 @@ __device__ void geom_record(const Env& e, int g, double* r) {
       x[3 + i] = fabs(R[3 * i]) * s[0] + fabs(R[3 * i + 1]) * s[1] + fabs(R[3 * i + 2]) * s[2];
   }
   x[6] = m.geom_rbound[g];
-  x[7] = (double)t;
-  for (int i = 0; i < 8; i++) r[i] = x[i];
+  for (int i = 0; i < GREC; i++) r[i] = x[i];
+  gtype[g] = (uint8_t)t;
 }
 
 // broadphase of pair p (geoms g1, g2, records in LDS); returns its narrow-phase class, or -1
 // when it cannot touch (or the type combination has no collider: no contacts)
-__device__ int pair_class(const double* grec, int g1, int g2, double margin) {
-  double r1[8], r2[8];
-  for (int i = 0; i < 8; i++) {
-    r1[i] = grec[8 * g1 + i];
-    r2[i] = grec[8 * g2 + i];
+__device__ int pair_class(const double* grec, const uint8_t* gtype, int g1, int g2, double margin) {
+  double r1[GREC], r2[GREC];
+  for (int i = 0; i < GREC; i++) {
+    r1[i] = grec[GREC * g1 + i];
+    r2[i] = grec[GREC * g2 + i];
   }
-  const int t1 = (int)r1[7], t2 = (int)r2[7];
+  const int t1 = gtype[g1], t2 = gtype[g2];
   if (t1 == RMBX_GEOM_PLANE || t2 == RMBX_GEOM_PLANE) {
     const double* rp = t1 == RMBX_GEOM_PLANE ? r1 : r2;
     const double* ro = t1 == RMBX_GEOM_PLANE ? r2 : r1;
@@ -1592,8 +1595,9 @@ struct PairRuns {
   const int32_t* body_cgeom;  // [nbody][2] first collision geom of the body, count
 };
 struct CollisionLds {
-  double* geom;
-  int32_t* spair;
+  double* geom;      // [ngeom][GREC] broadphase records
+  uint8_t* gtype;    // [ngeom] geom types
+  uint16_t* spair;   // survivors' pair indices (npair <= 65535, checked at engine creation)
   int16_t* list;
   uint8_t* count;
   uint8_t* scls;
@@ -1604,16 +1608,19 @@ struct CollisionLds {
 __host__ __device__ __forceinline__ int collision_cap(int npair) {
   return npair < RMBX_MAX_CANDIDATES ? npair : RMBX_MAX_CANDIDATES;
 }
+// doubles of the survivor arrays: spair (2 B), list (2 B), count (1 B), scls (1 B) per survivor
+__host__ __device__ __forceinline__ size_t collision_surv_doubles(int cap) { return (6 * (size_t)cap + 7) / 8 + 1; }
 __host__ __device__ __forceinline__ size_t collision_lds_doubles(int ngeom, int npair, int nbody, int nprun) {
-  // 8 bytes per survivor; two-level: 6 doubles per body + 129 int32 of run-chunk bookkeeping
+  // GREC doubles + a type byte per geom; 6 bytes per survivor; two-level: 6 doubles per body + 129
+  // int32 of run-chunk bookkeeping
   const size_t runs = nprun > 0 ? 6 * (size_t)nbody + 65 : 0;
-  return 8 * (size_t)ngeom + (size_t)collision_cap(npair) + 2 + runs;
+  return GREC * (size_t)ngeom + ((size_t)ngeom + 7) / 8 + collision_surv_doubles(collision_cap(npair)) + runs;
 }
 // The collision scratch starts at 16 nb: everything above the body frames (cvel, cacc, cfrc,
 // cdofdot, cinert, crb, cdof) is dead once the velocity stage has copied it out, and a model whose
-// scratch is larger runs past the end of that region.  The cable scene's 2,366 doubles fit in
+// scratch is larger runs past the end of that region.  The cable scene's 1,891 doubles fit in
 // the 2,906 there: 29.6 KiB of LDS per env instead of 48.1, so four envs per CU and all 1,024 in
-// one round of blocks; the Pick scene's 5,085 take it to 45.1 KiB (three envs per CU, was 61.5: two)
+// one round of blocks; the Pick scene's 4,276 take it to 38.8 KiB (four envs per CU, was 61.5: two)
 __host__ __device__ __forceinline__ size_t front_kernel_lds_doubles(int nb, int nv, size_t need) {
   const size_t front = front_lds_doubles(nb, nv), coll = 16 * (size_t)nb + need;
   return front > coll ? front : coll;
@@ -1627,12 +1634,13 @@ __device__ __forceinline__ CollisionLds collision_lds(const Env& e, const PairRu
   CollisionLds cl;
   const int cap = collision_cap(m.npair);
   cl.geom = e.sh + 16 * m.nbody;  // (front_kernel_lds_bytes sized the LDS for it)
-  cl.spair = reinterpret_cast<int32_t*>(cl.geom + 8 * m.ngeom);
+  cl.gtype = reinterpret_cast<uint8_t*>(cl.geom + GREC * m.ngeom);
+  double* sv = cl.geom + GREC * m.ngeom + (m.ngeom + 7) / 8;
+  cl.spair = reinterpret_cast<uint16_t*>(sv);
   cl.list = reinterpret_cast<int16_t*>(cl.spair + cap);
   cl.count = reinterpret_cast<uint8_t*>(cl.list + cap);
   cl.scls = cl.count + cap;
-  // (cap + 2 doubles hold spair, list, count, scls: 8 bytes per survivor)
-  cl.bbox = cl.geom + 8 * m.ngeom + cap + 2;
+  cl.bbox = sv + collision_surv_doubles(cap);
   cl.run_pre = reinterpret_cast<int32_t*>(cl.bbox + 6 * m.nbody);
   cl.run_id = cl.run_pre + 65;
   return cl;
@@ -1652,9 +1660,9 @@ __device__ __forceinline__ int broadphase_runs(const Env& e, int lane, const Col
     bool inf = false;
     const int g0 = pr.body_cgeom[2 * b], gn = pr.body_cgeom[2 * b + 1];
     for (int g = g0; g < g0 + gn; g++) {
-      const double* r = cl.geom + 8 * g;
+      const double* r = cl.geom + GREC * g;
       if (m.geom_ctype[g] < 0) continue;  // visual only
-      if ((int)r[7] == RMBX_GEOM_PLANE) {
+      if (cl.gtype[g] == RMBX_GEOM_PLANE) {
         inf = true;
         continue;
       }
@@ -1714,12 +1722,12 @@ __device__ __forceinline__ int broadphase_runs(const Env& e, int lane, const Col
             hi = mid;
         }
         p = pr.start[cl.run_id[lo]] + (i - cl.run_pre[lo]);
-        c = pair_class(cl.geom, m.pair_geom1[p], m.pair_geom2[p], m.pair_margin[p]);
+        c = pair_class(cl.geom, cl.gtype, m.pair_geom1[p], m.pair_geom2[p], m.pair_margin[p]);
       }
       const unsigned long long mk = __ballot(c >= 0);
       const int idx = nsurv + __popcll(mk & below);
       if (c >= 0 && idx < cap) {
-        cl.spair[idx] = p;
+        cl.spair[idx] = (uint16_t)p;
         cl.scls[idx] = (uint8_t)c;
       }
       nsurv += __popcll(mk);
@@ -1742,7 +1750,7 @@ __device__ int collision(Env& e, int lane, const CollisionLds& cl, const PairRun
   const int np = m.npair;
   const int cap = collision_cap(np);
   const unsigned long long below = (1ull << lane) - 1;
-  for (int g = lane; g < m.ngeom; g += 64) geom_record(e, g, cl.geom + 8 * g);
+  for (int g = lane; g < m.ngeom; g += 64) geom_record(e, g, cl.geom + GREC * g, cl.gtype);
   sync();
   SUBPROF(16)
   int nsurv = 0;
@@ -1766,11 +1774,11 @@ __device__ int collision(Env& e, int lane, const CollisionLds& cl, const PairRun
         g2n = m.pair_geom2[p + 64];
         mn = m.pair_margin[p + 64];
       }
-      const int c = p < np ? pair_class(cl.geom, g1, g2, mg) : -1;
+      const int c = p < np ? pair_class(cl.geom, cl.gtype, g1, g2, mg) : -1;
       const unsigned long long mk = __ballot(c >= 0);
       const int idx = nsurv + __popcll(mk & below);
       if (c >= 0 && idx < cap) {
-        cl.spair[idx] = p;
+        cl.spair[idx] = (uint16_t)p;
         cl.scls[idx] = (uint8_t)c;
       }
       nsurv += __popcll(mk);
@@ -3804,6 +3812,7 @@ int rmbx_engine_create(const struct rmbx_model* model, int n_env, rmbx_engine** 
   int nprun = (int)prun_margin.size();
   prun_start.push_back(h.npair);
   if (nprun == 0 || h.npair < 4 * nprun || front_kernel_lds_bytes(h, nprun) > 65536) nprun = 0;
+  RMBX_CHECK_ARG(h.npair <= 65535, "the collision stage indexes pairs in 16 bits (npair=%d)", h.npair);
   RMBX_CHECK_ARG(front_kernel_lds_bytes(h, nprun) <= 65536,
                  "model too large for the front kernel's LDS (nbody=%d nv=%d ngeom=%d npair=%d)", h.nbody,
                  h.nv, h.ngeom, h.npair);
