@@ -1574,12 +1574,38 @@ namespace {
 // profiles/r4_gemm_wide_ab.log), the 128 columns left over (N = 3200 = 3072 + 128) by a second
 // launch of the 128-wide tile; N % 128 != 0 runs the 64-wide tile.  RMBX_GEMM_WIDE=0 (read per
 // launch) keeps everything on the 128-wide tile.
+// Small grids (fewer blocks than CUs at one block per CU, e.g. the DiffusionPolicy UNet's
+// 32,768 x 256 layers: 128 wide tiles) take the 128- or 64-wide tile instead, so every CU gets a
+// block (same per-element K order: bitwise-equal results); RMBX_GEMM_FILL=0 (read per launch) keeps
+// the width rule above.
+static int gemm_cus() {
+  static const int cus = [] {
+    int dev = 0, n = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return n > 0 ? n : 256;
+  }();
+  return cus;
+}
 template <bool CONV>
 void launch_f16x3(const GemmArgs& g, hipStream_t st, int bn) {
   const char* we = getenv("RMBX_GEMM_WIDE");
   const bool wide = !(we && atoi(we) == 0);
   const int n256 = g.N / 256 * 256;
   const long long items = g.batch > 1 ? g.batch : 1;
+  const char* fe = getenv("RMBX_GEMM_FILL");
+  if (!(fe && atoi(fe) == 0) && bn == GM_BN) {
+    const long long cus = gemm_cus();
+    const long long wide_blocks = (long long)g.tiles_m * (g.N / 256 + (g.N % 256 ? 1 : 0)) * items;
+    if (wide_blocks < cus) {
+      int nb = GM_BN;
+      if ((long long)g.tiles_m * (g.N / GM_BN) * items < cus && g.N % 64 == 0) nb = 64;
+      GemmArgs t = g;
+      t.tiles_n = g.N / nb;
+      launch_gemm<CONV, 2>((long long)t.tiles_m * t.tiles_n * items, t, st, nb);
+      return;
+    }
+  }
   if (!wide || bn != GM_BN || n256 == 0) {
     launch_gemm<CONV, 2>((long long)g.tiles_m * g.tiles_n * items, g, st, bn);
     return;

@@ -492,3 +492,24 @@ def test_conv2d_f16x3_wide_tile_equals_narrow(monkeypatch, n, C, H, W, Cout, k, 
     assert torch.equal(outs[0], outs[1])
     ref = _conv_ref(x, wt, b, stride, pad, True, r)
     assert _err(outs[1], ref) < 2e-6
+
+
+@pytest.mark.parametrize("M,N,K", [(32768, 256, 2560), (4096, 512, 1024), (1024, 192, 256)])
+def test_linear_f16x3_small_grid_tiles_bitwise(monkeypatch, M, N, K):
+    """Grids with fewer wide tiles than CUs run the 128- / 64-wide tile (launch_f16x3); the per-element
+    K order is the tile width's invariant, so the outputs equal the wide-tile rule's bitwise
+    (RMBX_GEMM_FILL=0) and stay within the f16x3 bar against f64."""
+    from robomanipbaselines_amd import kernels as K_
+
+    g = torch.Generator().manual_seed(M + N)
+    x = torch.randn(M, K, generator=g).to(DEV)
+    w = (torch.randn(N, K, generator=g) / K ** 0.5).to(DEV)
+    b = torch.randn(N, generator=g).to(DEV)
+    planes = K_.split_f16x2(w)
+    got = K_.linear_f32x6(x, planes, b)
+    monkeypatch.setenv("RMBX_GEMM_FILL", "0")
+    ref = K_.linear_f32x6(x, planes, b)
+    assert torch.equal(got, ref)
+    want = x.double() @ w.double().t() + b.double()
+    err = _err(got, want)  # max |err| / max |ref|: the file's f32 GEMM bar
+    assert err < 4e-6, err
