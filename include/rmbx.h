@@ -213,6 +213,10 @@ typedef struct rmbx_env_buffers {
   void* workspace;    /* engine scratch, rmbx_engine_workspace_bytes() bytes */
 } rmbx_env_buffers;
 
+/* Model limits checked here (RMBX_ERR_ARG otherwise): npair <= 65535 (the collision stage indexes
+ * pairs in 16 bits) and the front kernel's LDS (body frames + the collision scratch) <= 64 KiB.
+ * The front kernel's launch LDS is sized here for n_env (padded so the envs spread evenly over the
+ * CUs and rounds of blocks; RMBX_FRONT_BALANCE=0 in the environment at creation: the plain need). */
 int rmbx_engine_create(const struct rmbx_model* model, int n_env, rmbx_engine** out);
 int rmbx_engine_destroy(rmbx_engine* eng);
 int rmbx_engine_workspace_bytes(const rmbx_engine* eng, size_t* bytes);
