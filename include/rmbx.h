@@ -575,6 +575,11 @@ int rmbx_attention_f16x3(const float* q, const float* k, const float* v, float* 
 /* Residual add + LayerNorm over the last dim of [rows][D] rows (D <= 2048, multiple of 8 bf16 / 4
  * f32): out = LayerNorm(rnd(x + r)) * weight + bias (f32 weight/bias), r optional (NULL); replaces
  * the add + nn.LayerNorm pair of the ACT transformer's post-norm layers (third_party/act). */
+/* GroupNorm(groups, C) over x [B][C][T] f32 with the affine (weight, bias [C]), then Mish when
+ * mish != 0 (the DiffusionPolicy / DP3 UNet's Conv1dBlock: policy/diffusion/unet1d.py); out may
+ * alias x. */
+int rmbx_groupnorm_act(const float* x, const float* weight, const float* bias, float* out, int B, int C, int T,
+                       int groups, float eps, int mish, void* stream);
 int rmbx_add_layernorm(const void* x, const void* r, const float* weight, const float* bias, void* out,
                        int rows, int D, float eps, int dtype, void* stream);
 /* rmbx_add_layernorm that also writes out_pos = rnd(out + pos[row % pos_rows]) (pos [pos_rows][D] in

@@ -93,6 +93,7 @@ SIGNATURES = {
                                  + [_c_int, _c_int, _c_p]),
     "rmbx_conv2d_f16x3": (_c_int, [_c_p] + [_c_int] * 4 + [_c_p] * 5 + [_c_int] * 6 + [_c_p]),
     "rmbx_add_layernorm": (_c_int, [_c_p] * 5 + [_c_int, _c_int, ctypes.c_float, _c_int, _c_p]),
+    "rmbx_groupnorm_act": (_c_int, [_c_p] * 4 + [_c_int] * 4 + [ctypes.c_float, _c_int, _c_p]),
     "rmbx_add_layernorm_split": (_c_int, [_c_p] * 9 + [_c_int, _c_p, _c_p, _c_p, _c_int, _c_int, ctypes.c_float, _c_p]),
     "rmbx_linear_f16x3_presplit_split": (_c_int, [_c_p, ctypes.c_longlong, ctypes.c_longlong, _c_p, _c_p, _c_p,
                                                   ctypes.c_longlong, ctypes.c_longlong, _c_p, ctypes.c_float,

@@ -466,3 +466,75 @@ extern "C" int rmbx_add_layernorm_split(const float* x, const float* r, const fl
   return add_layernorm_impl(x, r, weight, bias, out, pos, pos_rows, out_pos, rows, D, eps, 0, stream,
                             rmbx::LnSplit{(uint16_t*)y_planes, y_rinv, (uint16_t*)pos_planes, pos_rinv, rows, y_norm});
 }
+
+// ---------------------------------------------------------------------------------------------
+// GroupNorm (+ Mish) of the DiffusionPolicy / DP3 UNet's Conv1dBlock (nn.GroupNorm(G, C) ->
+// nn.Mish() after each Conv1d, policy/diffusion/unet1d.py; the reference's diffusion_policy
+// ConditionalUnet1D, third_party [absent]) on [B][C][T] f32: the channels of a group are one
+// contiguous span of (C / G) T values, so one 256-thread block per (b, g) reduces it (sum, then
+// the sum of squared deviations: two passes over the span, which stays in L1 / L2), and writes
+// y = (x - mean) rstd gamma_c + beta_c, optionally mish(y) = y tanh(log1p(exp y)) (torch's form).
+// One read pass more than the statistics need, against torch's moments kernel + affine kernel +
+// Mish kernel (three reads, two writes).
+// ---------------------------------------------------------------------------------------------
+namespace rmbx {
+namespace {
+
+__device__ __forceinline__ float gn_block_sum(float v, float* red) {
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o);
+  const int wave = threadIdx.x >> 6;
+  __syncthreads();  // (red is reused by the next reduction)
+  if ((threadIdx.x & 63) == 0) red[wave] = v;
+  __syncthreads();
+  return red[0] + red[1] + red[2] + red[3];
+}
+
+template <bool MISH>
+__global__ void __launch_bounds__(256) groupnorm_act_kernel(const float* __restrict__ x, const float* __restrict__ w,
+                                                            const float* __restrict__ b, float* __restrict__ y, int C,
+                                                            int T, int G, float eps) {
+  __shared__ float red[4];
+  const int bg = blockIdx.x, g = bg % G, cg = C / G;
+  const int E = cg * T, tid = threadIdx.x;
+  const float* xs = x + (long long)bg * E;
+  float* ys = y + (long long)bg * E;
+  float s = 0.f;
+  for (int i = tid; i < E; i += 256) s += xs[i];
+  const float mean = gn_block_sum(s, red) / (float)E;
+  float q = 0.f;
+  for (int i = tid; i < E; i += 256) {
+    const float d = xs[i] - mean;
+    q += d * d;
+  }
+  const float var = gn_block_sum(q, red) / (float)E;
+  const float rstd = 1.f / sqrtf(var + eps);
+  for (int i = tid; i < E; i += 256) {
+    const int c = g * cg + i / T;
+    float v = (xs[i] - mean) * rstd * w[c] + b[c];
+    if constexpr (MISH) v = v * tanhf(log1pf(expf(v)));
+    ys[i] = v;
+  }
+}
+
+}  // namespace
+}  // namespace rmbx
+
+extern "C" int rmbx_groupnorm_act(const float* x, const float* weight, const float* bias, float* out, int B, int C,
+                                  int T, int groups, float eps, int mish, void* stream) {
+  RMBX_CHECK_ARG(x && weight && bias && out, "rmbx_groupnorm_act: null pointer");
+  RMBX_CHECK_ARG(B >= 0 && C > 0 && T > 0 && groups > 0 && C % groups == 0,
+                 "rmbx_groupnorm_act: bad shape B=%d C=%d T=%d groups=%d", B, C, T, groups);
+  RMBX_CHECK_ARG(eps >= 0.f, "rmbx_groupnorm_act: eps must be >= 0");
+  const long long nblocks = (long long)B * groups;
+  RMBX_CHECK_ARG(nblocks < (1ll << 31) && (long long)(C / groups) * T < (1ll << 31), "rmbx_groupnorm_act: too large");
+  if (B == 0) return RMBX_OK;
+  if (mish)
+    hipLaunchKernelGGL(rmbx::groupnorm_act_kernel<true>, dim3((unsigned)nblocks), dim3(256), 0, (hipStream_t)stream, x,
+                       weight, bias, out, C, T, groups, eps);
+  else
+    hipLaunchKernelGGL(rmbx::groupnorm_act_kernel<false>, dim3((unsigned)nblocks), dim3(256), 0, (hipStream_t)stream, x,
+                       weight, bias, out, C, T, groups, eps);
+  RMBX_CHECK_LAUNCH();
+  return RMBX_OK;
+}

@@ -477,6 +477,23 @@ def add_layernorm(x, r, weight, bias, eps=1e-5, out=None):
     return out
 
 
+def groupnorm_act(x, weight, bias, groups, eps=1e-5, mish=True, out=None):
+    """GroupNorm(groups) over x [B, C, T] (contiguous f32 device tensor) with the affine, then Mish
+    (rmbx_groupnorm_act): the UNet Conv1dBlock's norm + activation in one pass."""
+    if x.dtype != torch.float32 or not x.is_cuda or not x.is_contiguous() or x.dim() != 3:
+        raise ValueError("x must be a contiguous f32 device tensor [B, C, T]")
+    B, C, T = x.shape
+    if C % groups != 0:
+        raise ValueError(f"C={C} is not a multiple of groups={groups}")
+    _chk(weight, torch.float32, (C,), "weight")
+    _chk(bias, torch.float32, (C,), "bias")
+    if out is None:
+        out = torch.empty_like(x)
+    N.call("rmbx_groupnorm_act", N.ptr(x), N.ptr(weight), N.ptr(bias), N.ptr(out), B, C, T, int(groups), float(eps),
+           1 if mish else 0, N.stream_ptr())
+    return out
+
+
 def add_layernorm_pos(x, r, weight, bias, pos, eps=1e-5):
     """(y, y + pos) with y = LayerNorm(rnd(x + r)) in one pass (rmbx_add_layernorm_pos); pos
     [P, D] (or [1, P, D]) in x's dtype, broadcast over the leading dims row-wise (row % P)."""

@@ -12,6 +12,7 @@ captured with the scheduler-step kernels in one HIP graph (see dp_model.Diffusio
 """
 
 import math
+import os
 
 import torch
 import torch.nn as nn
@@ -78,6 +79,10 @@ def conv_transpose1d_gemm(x, conv):
     return y.transpose(1, 2).contiguous()
 
 
+# the fp32 device UNet's GroupNorm + Mish as one rmbx pass (RMBX_UNET_FUSED_GN=0: torch's ops)
+UNET_FUSED_GN = os.environ.get("RMBX_UNET_FUSED_GN", "1") != "0"
+
+
 def _device_form(x):
     return x.is_cuda and x.dtype in (torch.bfloat16, torch.float16, torch.float32)
 
@@ -104,7 +109,15 @@ class Conv1dBlock(nn.Module):
 
     def forward(self, x):
         conv, norm, act = self.block
-        return act(norm(run_conv(conv, x)))
+        y = run_conv(conv, x)
+        if (y.is_cuda and y.dtype == torch.float32 and y.dim() == 3 and norm.affine and UNET_FUSED_GN
+                and norm.weight.dtype == torch.float32):
+            from ... import kernels as K
+
+            # GroupNorm + Mish in one pass (rmbx_groupnorm_act), in place on the conv output
+            return K.groupnorm_act(y.contiguous(), norm.weight, norm.bias, norm.num_groups, norm.eps, mish=True,
+                                   out=y if y.is_contiguous() else None)
+        return act(norm(y))
 
 
 class ConditionalResidualBlock1D(nn.Module):
