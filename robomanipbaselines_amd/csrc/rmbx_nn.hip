@@ -490,6 +490,7 @@ __device__ __forceinline__ float gn_block_sum(float v, float* red) {
   return red[0] + red[1] + red[2] + red[3];
 }
 
+constexpr int GN_REG = 8;  // values per thread held in registers (spans up to 2048)
 template <bool MISH>
 __global__ void __launch_bounds__(256) groupnorm_act_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                             const float* __restrict__ b, float* __restrict__ y, int C,
@@ -499,6 +500,36 @@ __global__ void __launch_bounds__(256) groupnorm_act_kernel(const float* __restr
   const int E = cg * T, tid = threadIdx.x;
   const float* xs = x + (long long)bg * E;
   float* ys = y + (long long)bg * E;
+  if (E <= 256 * GN_REG) {  // the UNet's spans (512-2048 values): one read, the values kept in registers
+    float v[GN_REG];
+    float s = 0.f;
+#pragma unroll
+    for (int k = 0; k < GN_REG; ++k) {
+      const int i = tid + 256 * k;
+      v[k] = i < E ? xs[i] : 0.f;
+      s += v[k];
+    }
+    const float mean = gn_block_sum(s, red) / (float)E;
+    float q = 0.f;
+#pragma unroll
+    for (int k = 0; k < GN_REG; ++k) {
+      const int i = tid + 256 * k;
+      const float d = i < E ? v[k] - mean : 0.f;
+      q += d * d;
+    }
+    const float rstd = 1.f / sqrtf(gn_block_sum(q, red) / (float)E + eps);
+#pragma unroll
+    for (int k = 0; k < GN_REG; ++k) {
+      const int i = tid + 256 * k;
+      if (i < E) {
+        const int c = g * cg + i / T;
+        float o = (v[k] - mean) * rstd * w[c] + b[c];
+        if constexpr (MISH) o = o * tanhf(log1pf(expf(o)));
+        ys[i] = o;
+      }
+    }
+    return;
+  }
   float s = 0.f;
   for (int i = tid; i < E; i += 256) s += xs[i];
   const float mean = gn_block_sum(s, red) / (float)E;

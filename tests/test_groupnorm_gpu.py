@@ -1,5 +1,5 @@
 """rmbx_groupnorm_act (the DiffusionPolicy / DP3 UNet Conv1dBlock's GroupNorm + Mish in one pass)
-against torch's group_norm + mish in f64 on the same f32 inputs: within the f32 error class
+against torch's group_norm + mish in f64 on the same f32 inputs: within the f32 error class (the register-resident path for spans up to 2,048 values and the three-pass one above)
 (1e-5 absolute on unit-scale outputs; torch's own f32 ops measured ~1e-6), with and without the
 Mish, in place, and at the UNet's shapes (B = 2048, C 256-1024, T 16 / 8 / 4)."""
 
@@ -12,7 +12,7 @@ DEV = "cuda:0"
 
 
 @pytest.mark.parametrize("B,C,T,G", [(2048, 256, 16, 8), (2048, 1024, 4, 8), (2048, 512, 8, 8), (7, 64, 5, 8),
-                                     (3, 96, 33, 4)])
+                                     (3, 96, 33, 4), (2, 64, 300, 2)])
 @pytest.mark.parametrize("mish", [True, False])
 def test_groupnorm_act_vs_f64(B, C, T, G, mish):
     from robomanipbaselines_amd import kernels as K
