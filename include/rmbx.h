@@ -576,8 +576,9 @@ int rmbx_attention_f16x3(const float* q, const float* k, const float* v, float* 
  * f32): out = LayerNorm(rnd(x + r)) * weight + bias (f32 weight/bias), r optional (NULL); replaces
  * the add + nn.LayerNorm pair of the ACT transformer's post-norm layers (third_party/act). */
 /* GroupNorm(groups, C) over x [B][C][T] f32 with the affine (weight, bias [C]), then Mish when
- * mish != 0 (the DiffusionPolicy / DP3 UNet's Conv1dBlock: policy/diffusion/unet1d.py); out may
- * alias x. */
+ * mish & 1 (the DiffusionPolicy / DP3 UNet's Conv1dBlock: policy/diffusion/unet1d.py); mish & 2:
+ * x is laid out [B][T][C] (the conv GEMM's rows; out is [B][C][T] either way).  out may alias x
+ * only without bit 1. */
 int rmbx_groupnorm_act(const float* x, const float* weight, const float* bias, float* out, int B, int C, int T,
                        int groups, float eps, int mish, void* stream);
 int rmbx_add_layernorm(const void* x, const void* r, const float* weight, const float* bias, void* out,

@@ -474,6 +474,8 @@ extern "C" int rmbx_add_layernorm_split(const float* x, const float* r, const fl
 // contiguous span of (C / G) T values, so one 256-thread block per (b, g) reduces it (sum, then
 // the sum of squared deviations: two passes over the span, which stays in L1 / L2), and writes
 // y = (x - mean) rstd gamma_c + beta_c, optionally mish(y) = y tanh(log1p(exp y)) (torch's form).
+// The input may also be the conv GEMM's [B][T][C] rows (flags bit 1): the transpose to [B][C][T]
+// then happens in this pass instead of a separate copy.
 // One read pass more than the statistics need, against torch's moments kernel + affine kernel +
 // Mish kernel (three reads, two writes).
 // ---------------------------------------------------------------------------------------------
@@ -491,14 +493,28 @@ __device__ __forceinline__ float gn_block_sum(float v, float* red) {
 }
 
 constexpr int GN_REG = 8;  // values per thread held in registers (spans up to 2048)
-template <bool MISH>
+// TIN: x is [B][T][C] (the conv GEMM's output rows; element i of a (b, g) span read t-major, i = t cg + c,
+// so a wave's loads are contiguous channels); y is [B][C][T] either way
+template <bool MISH, bool TIN>
 __global__ void __launch_bounds__(256) groupnorm_act_kernel(const float* __restrict__ x, const float* __restrict__ w,
                                                             const float* __restrict__ b, float* __restrict__ y, int C,
                                                             int T, int G, float eps) {
   __shared__ float red[4];
   const int bg = blockIdx.x, g = bg % G, cg = C / G;
   const int E = cg * T, tid = threadIdx.x;
-  const float* xs = x + (long long)bg * E;
+  const long long bb = bg / G;
+  // element i of the span: channel c, time t, its input offset; the output offset is c T + t
+  auto at = [&](int i, int& c, int& t) -> long long {
+    if constexpr (TIN) {
+      t = i / cg;
+      c = i - t * cg;
+      return (bb * T + t) * C + g * cg + c;
+    } else {
+      c = i / T;
+      t = i - c * T;
+      return (long long)bg * E + i;
+    }
+  };
   float* ys = y + (long long)bg * E;
   if (E <= 256 * GN_REG) {  // the UNet's spans (512-2048 values): one read, the values kept in registers
     float v[GN_REG];
@@ -506,7 +522,8 @@ __global__ void __launch_bounds__(256) groupnorm_act_kernel(const float* __restr
 #pragma unroll
     for (int k = 0; k < GN_REG; ++k) {
       const int i = tid + 256 * k;
-      v[k] = i < E ? xs[i] : 0.f;
+      int c, t;
+      v[k] = i < E ? x[at(i, c, t)] : 0.f;
       s += v[k];
     }
     const float mean = gn_block_sum(s, red) / (float)E;
@@ -522,29 +539,35 @@ __global__ void __launch_bounds__(256) groupnorm_act_kernel(const float* __restr
     for (int k = 0; k < GN_REG; ++k) {
       const int i = tid + 256 * k;
       if (i < E) {
-        const int c = g * cg + i / T;
-        float o = (v[k] - mean) * rstd * w[c] + b[c];
+        int c, t;
+        at(i, c, t);
+        float o = (v[k] - mean) * rstd * w[g * cg + c] + b[g * cg + c];
         if constexpr (MISH) o = o * tanhf(log1pf(expf(o)));
-        ys[i] = o;
+        ys[c * T + t] = o;
       }
     }
     return;
   }
   float s = 0.f;
-  for (int i = tid; i < E; i += 256) s += xs[i];
+  for (int i = tid; i < E; i += 256) {
+    int c, t;
+    s += x[at(i, c, t)];
+  }
   const float mean = gn_block_sum(s, red) / (float)E;
   float q = 0.f;
   for (int i = tid; i < E; i += 256) {
-    const float d = xs[i] - mean;
+    int c, t;
+    const float d = x[at(i, c, t)] - mean;
     q += d * d;
   }
   const float var = gn_block_sum(q, red) / (float)E;
   const float rstd = 1.f / sqrtf(var + eps);
   for (int i = tid; i < E; i += 256) {
-    const int c = g * cg + i / T;
-    float v = (xs[i] - mean) * rstd * w[c] + b[c];
+    int c, t;
+    const long long off = at(i, c, t);
+    float v = (x[off] - mean) * rstd * w[g * cg + c] + b[g * cg + c];
     if constexpr (MISH) v = v * tanhf(log1pf(expf(v)));
-    ys[i] = v;
+    ys[c * T + t] = v;
   }
 }
 
@@ -560,12 +583,15 @@ extern "C" int rmbx_groupnorm_act(const float* x, const float* weight, const flo
   const long long nblocks = (long long)B * groups;
   RMBX_CHECK_ARG(nblocks < (1ll << 31) && (long long)(C / groups) * T < (1ll << 31), "rmbx_groupnorm_act: too large");
   if (B == 0) return RMBX_OK;
-  if (mish)
-    hipLaunchKernelGGL(rmbx::groupnorm_act_kernel<true>, dim3((unsigned)nblocks), dim3(256), 0, (hipStream_t)stream, x,
-                       weight, bias, out, C, T, groups, eps);
-  else
-    hipLaunchKernelGGL(rmbx::groupnorm_act_kernel<false>, dim3((unsigned)nblocks), dim3(256), 0, (hipStream_t)stream, x,
-                       weight, bias, out, C, T, groups, eps);
+  RMBX_CHECK_ARG(!(mish & 2) || x != out, "rmbx_groupnorm_act: a time-major input cannot alias the output");
+  const dim3 grid((unsigned)nblocks), blk(256);
+  hipStream_t st = (hipStream_t)stream;
+  switch (mish & 3) {
+    case 0: hipLaunchKernelGGL((rmbx::groupnorm_act_kernel<false, false>), grid, blk, 0, st, x, weight, bias, out, C, T, groups, eps); break;
+    case 1: hipLaunchKernelGGL((rmbx::groupnorm_act_kernel<true, false>), grid, blk, 0, st, x, weight, bias, out, C, T, groups, eps); break;
+    case 2: hipLaunchKernelGGL((rmbx::groupnorm_act_kernel<false, true>), grid, blk, 0, st, x, weight, bias, out, C, T, groups, eps); break;
+    default: hipLaunchKernelGGL((rmbx::groupnorm_act_kernel<true, true>), grid, blk, 0, st, x, weight, bias, out, C, T, groups, eps);
+  }
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
 }

@@ -477,20 +477,26 @@ def add_layernorm(x, r, weight, bias, eps=1e-5, out=None):
     return out
 
 
-def groupnorm_act(x, weight, bias, groups, eps=1e-5, mish=True, out=None):
+def groupnorm_act(x, weight, bias, groups, eps=1e-5, mish=True, out=None, time_major=False):
     """GroupNorm(groups) over x [B, C, T] (contiguous f32 device tensor) with the affine, then Mish
-    (rmbx_groupnorm_act): the UNet Conv1dBlock's norm + activation in one pass."""
+    (rmbx_groupnorm_act): the UNet Conv1dBlock's norm + activation in one pass.  time_major: x is
+    [B, T, C] (the conv GEMM's rows) and the result [B, C, T] (the transpose folded into the pass)."""
     if x.dtype != torch.float32 or not x.is_cuda or not x.is_contiguous() or x.dim() != 3:
         raise ValueError("x must be a contiguous f32 device tensor [B, C, T]")
-    B, C, T = x.shape
+    if time_major:
+        B, T, C = x.shape
+    else:
+        B, C, T = x.shape
     if C % groups != 0:
         raise ValueError(f"C={C} is not a multiple of groups={groups}")
     _chk(weight, torch.float32, (C,), "weight")
     _chk(bias, torch.float32, (C,), "bias")
     if out is None:
-        out = torch.empty_like(x)
+        out = torch.empty((B, C, T), device=x.device, dtype=x.dtype)
+    elif time_major and out.data_ptr() == x.data_ptr():
+        raise ValueError("a time-major input cannot be normalised in place")
     N.call("rmbx_groupnorm_act", N.ptr(x), N.ptr(weight), N.ptr(bias), N.ptr(out), B, C, T, int(groups), float(eps),
-           1 if mish else 0, N.stream_ptr())
+           (1 if mish else 0) | (2 if time_major else 0), N.stream_ptr())
     return out
 
 

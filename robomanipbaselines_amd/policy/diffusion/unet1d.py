@@ -50,7 +50,7 @@ def _gemm(owner, name, x2, w2, bias):
     return F.linear(x2, w2, bias)
 
 
-def conv1d_gemm(x, conv):
+def conv1d_gemm(x, conv, rows=False):
     """Conv1d as one GEMM: the k-tap windows of x [B, C, T] (padding, stride) unfolded to
     [B*To, C*k] rows times the weight viewed [Cout, C*k] (hipBLASLt), -> [B, Cout, To].  At
     rollout batch sizes the trajectories are short (T = horizon, 16) and wide (C up to 2048), a
@@ -61,6 +61,8 @@ def conv1d_gemm(x, conv):
     To = cols.shape[2]
     cols = cols.permute(0, 2, 1, 3).reshape(B * To, C * k)
     y = _gemm(conv, "w", cols, conv.weight.reshape(conv.out_channels, C * k), conv.bias)
+    if rows:  # [B, To, Cout] as the GEMM wrote it (the caller transposes)
+        return y.view(B, To, -1)
     return y.view(B, To, -1).transpose(1, 2).contiguous()
 
 
@@ -81,6 +83,8 @@ def conv_transpose1d_gemm(x, conv):
 
 # the fp32 device UNet's GroupNorm + Mish as one rmbx pass (RMBX_UNET_FUSED_GN=0: torch's ops)
 UNET_FUSED_GN = os.environ.get("RMBX_UNET_FUSED_GN", "1") != "0"
+# ... reading the conv GEMM's [B, T, C] rows (RMBX_UNET_GN_ROWS=0: after the transpose copy, in place)
+UNET_GN_ROWS = os.environ.get("RMBX_UNET_GN_ROWS", "1") != "0"
 
 
 def _device_form(x):
@@ -109,15 +113,19 @@ class Conv1dBlock(nn.Module):
 
     def forward(self, x):
         conv, norm, act = self.block
-        y = run_conv(conv, x)
-        if (y.is_cuda and y.dtype == torch.float32 and y.dim() == 3 and norm.affine and UNET_FUSED_GN
-                and norm.weight.dtype == torch.float32):
+        if (x.is_cuda and x.dtype == torch.float32 and x.dim() == 3 and norm.affine and UNET_FUSED_GN
+                and norm.weight.dtype == torch.float32 and isinstance(conv, nn.Conv1d)):
             from ... import kernels as K
 
-            # GroupNorm + Mish in one pass (rmbx_groupnorm_act), in place on the conv output
-            return K.groupnorm_act(y.contiguous(), norm.weight, norm.bias, norm.num_groups, norm.eps, mish=True,
-                                   out=y if y.is_contiguous() else None)
-        return act(norm(y))
+            # the conv GEMM's [B, T, C] rows straight into GroupNorm + Mish (rmbx_groupnorm_act), which
+            # writes [B, C, T]: no transpose copy, one pass for norm + activation
+            if UNET_GN_ROWS:
+                rows = conv1d_gemm(x, conv, rows=True).contiguous()
+                return K.groupnorm_act(rows, norm.weight, norm.bias, norm.num_groups, norm.eps, mish=True,
+                                       time_major=True)
+            y = run_conv(conv, x)
+            return K.groupnorm_act(y, norm.weight, norm.bias, norm.num_groups, norm.eps, mish=True, out=y)
+        return act(norm(run_conv(conv, x)))
 
 
 class ConditionalResidualBlock1D(nn.Module):

@@ -32,6 +32,21 @@ def test_groupnorm_act_vs_f64(B, C, T, G, mish):
     assert err <= 4 * (t32.double() - ref).abs().max().item() + 2e-6
 
 
+@pytest.mark.parametrize("B,C,T,G", [(2048, 256, 16, 8), (2048, 1024, 4, 8), (2, 64, 300, 2)])
+def test_groupnorm_act_time_major_input(B, C, T, G):
+    """The conv GEMM's [B, T, C] rows in, [B, C, T] out: the same values as the [B, C, T] input."""
+    from robomanipbaselines_amd import kernels as K
+
+    g = torch.Generator().manual_seed(B + T)
+    x = (2.0 * torch.randn(B, C, T, generator=g)).to(DEV)
+    w = (0.5 + torch.rand(C, generator=g)).to(DEV)
+    b = (0.2 * torch.randn(C, generator=g)).to(DEV)
+    got = K.groupnorm_act(x.transpose(1, 2).contiguous(), w, b, G, 1e-5, time_major=True)
+    assert got.shape == (B, C, T)
+    ref = F.mish(F.group_norm(x.double(), G, w.double(), b.double(), 1e-5))
+    assert (got.double() - ref).abs().max().item() < 1e-5
+
+
 def test_groupnorm_act_in_place_and_checks():
     from robomanipbaselines_amd import kernels as K
 
