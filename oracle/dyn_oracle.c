@@ -905,14 +905,18 @@ static int col_box_box(const double* ca, const double* Ra, const double* ha, con
       pa[i] = ca[i];
       pb[i] = cb[i];
     }
+    int fa = -1, fb = -1, nfa = 0, nfb = 0; /* the box axes parallel to the contact plane */
     for (int k = 0; k < 3; k++) {
       double ua[3] = {Ra[k], Ra[3 + k], Ra[6 + k]}, ub[3] = {Rb[k], Rb[3 + k], Rb[6 + k]};
       /* the extent's end facing the other box, or its centre when the axis is perpendicular to n
          within 1e-9 (a parallel face / edge: every point along it supports; a ~1e-17 dot product
          would otherwise pick an end by rounding) */
       const double da = dot3(ua, n), db = dot3(ub, neg);
-      double sa2 = fabs(da) < 1e-9 ? 0.0 : (da > 0 ? ha[k] : -ha[k]);
-      double sb2 = fabs(db) < 1e-9 ? 0.0 : (db > 0 ? hb[k] : -hb[k]);
+      const int pa_free = fabs(da) < 1e-9, pb_free = fabs(db) < 1e-9;
+      double sa2 = pa_free ? 0.0 : (da > 0 ? ha[k] : -ha[k]);
+      double sb2 = pb_free ? 0.0 : (db > 0 ? hb[k] : -hb[k]);
+      if (pa_free) { fa = k; ++nfa; }
+      if (pb_free) { fb = k; ++nfb; }
       for (int i = 0; i < 3; i++) {
         pa[i] += ua[i] * sa2;
         pb[i] += ub[i] * sb2;
@@ -922,6 +926,26 @@ static int col_box_box(const double* ca, const double* Ra, const double* ha, con
     (void)sb_;
     double dist = dot3(n, pb) - dot3(n, pa);
     if (dist >= margin) return 0;
+    if (nfa == 1 && nfb == 1) {
+      /* edge against edge: closest points of the two support segments pa + s ua (|s| <= ha) and
+         pb + t ub (|t| <= hb), clamped (crossed edges touch where they cross) */
+      const double ua[3] = {Ra[fa], Ra[3 + fa], Ra[6 + fa]}, ub[3] = {Rb[fb], Rb[3 + fb], Rb[6 + fb]};
+      const double w[3] = {pa[0] - pb[0], pa[1] - pb[1], pa[2] - pb[2]};
+      const double b = dot3(ua, ub), d = dot3(ua, w), e = dot3(ub, w);
+      const double den = 1.0 - b * b;
+      if (den > 1e-12) { /* (parallel edges keep the centres) */
+        double sv = (b * e - d) / den;
+        sv = sv < -ha[fa] ? -ha[fa] : (sv > ha[fa] ? ha[fa] : sv);
+        double tv = e + sv * b;
+        tv = tv < -hb[fb] ? -hb[fb] : (tv > hb[fb] ? hb[fb] : tv);
+        sv = tv * b - d;
+        sv = sv < -ha[fa] ? -ha[fa] : (sv > ha[fa] ? ha[fa] : sv);
+        for (int i = 0; i < 3; i++) {
+          pa[i] += ua[i] * sv;
+          pb[i] += ub[i] * tv;
+        }
+      }
+    }
     for (int i = 0; i < 3; i++) {
       out[0].n[i] = n[i];
       out[0].pos[i] = 0.5 * (pa[i] + pb[i]);

@@ -902,6 +902,7 @@ __device__ int col_box_box(const double* ca, const double* Ra, const double* ha,
       pa[i] = ca[i];
       pb[i] = cb[i];
     }
+    int fa = -1, fb = -1, nfa = 0, nfb = 0;  // the box axes parallel to the contact plane
     for (int k = 0; k < 3; k++) {
       const double ua[3] = {Ra[k], Ra[3 + k], Ra[6 + k]}, ub[3] = {Rb[k], Rb[3 + k], Rb[6 + k]};
       // support coordinate along each box axis: the extent's end facing the other box, or its
@@ -910,8 +911,11 @@ __device__ int col_box_box(const double* ca, const double* Ra, const double* ha,
       // product would pick an end by rounding -- the engine and the oracle then put the contact
       // a half extent apart)
       const double da = dot3(ua, n), db = dot3(ub, neg);
-      const double sa2 = fabs(da) < 1e-9 ? 0.0 : (da > 0 ? ha[k] : -ha[k]);
-      const double sb2 = fabs(db) < 1e-9 ? 0.0 : (db > 0 ? hb[k] : -hb[k]);
+      const bool pa_free = fabs(da) < 1e-9, pb_free = fabs(db) < 1e-9;
+      const double sa2 = pa_free ? 0.0 : (da > 0 ? ha[k] : -ha[k]);
+      const double sb2 = pb_free ? 0.0 : (db > 0 ? hb[k] : -hb[k]);
+      if (pa_free) { fa = k; ++nfa; }
+      if (pb_free) { fb = k; ++nfb; }
       for (int i = 0; i < 3; i++) {
         pa[i] += ua[i] * sa2;
         pb[i] += ub[i] * sb2;
@@ -919,6 +923,27 @@ __device__ int col_box_box(const double* ca, const double* Ra, const double* ha,
     }
     const double dist = dot3(n, pb) - dot3(n, pa);
     if (dist >= margin) return 0;
+    if (nfa == 1 && nfb == 1) {
+      // edge against edge: the closest points of the two support edges (segments pa + s ua,
+      // |s| <= ha, and pb + t ub, |t| <= hb; both lie in planes normal to n), clamped to the
+      // segments -- for crossed edges the contact sits where they cross, not at their centres
+      const double ua[3] = {Ra[fa], Ra[3 + fa], Ra[6 + fa]}, ub[3] = {Rb[fb], Rb[3 + fb], Rb[6 + fb]};
+      const double w[3] = {pa[0] - pb[0], pa[1] - pb[1], pa[2] - pb[2]};
+      const double b = dot3(ua, ub), d = dot3(ua, w), e = dot3(ub, w);
+      const double den = 1.0 - b * b;
+      if (den > 1e-12) {  // (parallel edges keep the centres)
+        double sv = (b * e - d) / den;
+        sv = sv < -ha[fa] ? -ha[fa] : (sv > ha[fa] ? ha[fa] : sv);
+        double tv = e + sv * b;
+        tv = tv < -hb[fb] ? -hb[fb] : (tv > hb[fb] ? hb[fb] : tv);
+        sv = tv * b - d;
+        sv = sv < -ha[fa] ? -ha[fa] : (sv > ha[fa] ? ha[fa] : sv);
+        for (int i = 0; i < 3; i++) {
+          pa[i] += ua[i] * sv;
+          pb[i] += ub[i] * tv;
+        }
+      }
+    }
     for (int i = 0; i < 3; i++) {
       out[0].n[i] = n[i];
       out[0].pos[i] = 0.5 * (pa[i] + pb[i]);

@@ -493,8 +493,12 @@ def groupnorm_act(x, weight, bias, groups, eps=1e-5, mish=True, out=None, time_m
     _chk(bias, torch.float32, (C,), "bias")
     if out is None:
         out = torch.empty((B, C, T), device=x.device, dtype=x.dtype)
-    elif time_major and out.data_ptr() == x.data_ptr():
-        raise ValueError("a time-major input cannot be normalised in place")
+    else:
+        _chk(out, torch.float32, (B, C, T), "out")
+        if out.device != x.device:
+            raise ValueError(f"out must be on {x.device} (got {out.device})")
+        if time_major and out.data_ptr() == x.data_ptr():
+            raise ValueError("a time-major input cannot be normalised in place")
     N.call("rmbx_groupnorm_act", N.ptr(x), N.ptr(weight), N.ptr(bias), N.ptr(out), B, C, T, int(groups), float(eps),
            (1 if mish else 0) | (2 if time_major else 0), N.stream_ptr())
     return out
@@ -528,10 +532,26 @@ class PresplitRows:
     rinv[m] * (planes[0, m] + planes[1, m]) to 2^-22 relative, rinv [M] f32 powers of two; norm [M]
     (optional) an upper bound of each row's |a|_2."""
 
-    __slots__ = ("planes", "rinv", "norm")
+    __slots__ = ("planes", "rinv", "norm", "_src")
 
     def __init__(self, planes, rinv, norm=None):
         self.planes, self.rinv, self.norm = planes, rinv, norm
+        self._src = None
+
+    def bind(self, t):
+        """Record the f32 tensor these pieces were written beside (its storage and version)."""
+        self._src = (t.data_ptr(), t._version)
+
+    def valid_for(self, t):
+        """True while `t` is that tensor (or a view of it) unchanged since the pieces were written: an
+        in-place change of the f32 rows bumps the version and retires the pieces."""
+        return self._src is not None and self._src == (t.data_ptr(), t._version)
+
+
+def presplit_of(x):
+    """The pre-split A form attached to x by its producer, if it still describes x's values."""
+    sp = getattr(x, "rmbx_split", None)
+    return sp if sp is not None and sp.valid_for(x) else None
 
 
 # the pre-split A path (env RMBX_GEMM_PRESPLIT=0 turns it off: the LayerNorms then emit f32 only and
@@ -571,8 +591,10 @@ def add_layernorm_split(x, r, weight, bias, eps=1e-5, pos=None, split_y=True, sp
            pos2.shape[0] if pos2 is not None else 0, N.ptr(yp), N.ptr(ps.planes if ps else None),
            N.ptr(ps.rinv if ps else None), rows, D, float(eps), N.stream_ptr())
     if ys is not None:
+        ys.bind(y)
         y.rmbx_split = ys
     if ps is not None:
+        ps.bind(yp)
         yp.rmbx_split = ps
     return (y, yp) if pos is not None else y
 
@@ -1117,7 +1139,7 @@ def linear_f32x6(x, planes, bias=None, relu=False, out=None):
     elif out.dtype != torch.float32 or out.stride(-1) != 1 or out.shape != (M, Nn):
         raise ValueError("out must be an f32 [M, N] tensor with contiguous rows")
     name, flops = f"linear M={M} N={Nn} K={K}", 2.0 * M * Nn * K
-    sp = getattr(x, "rmbx_split", None)
+    sp = presplit_of(x)
     if h3 and sp is not None and Nn % LINEAR_F32X6_BN == 0 and sp.planes.shape[1] == M and sp.planes.shape[2] == K:
         # the producer's pre-split rows (add_layernorm_split): both operands by LDS-DMA
         p, ap = planes.planes, sp.planes

@@ -190,13 +190,14 @@ class _LayerOps(nn.Module):
     fused = False
 
     def ffn(self, x):
-        sp = getattr(x, "rmbx_split", None)
-        if (self.fused and sp is not None and sp.norm is not None and self.linear1.out_features % 128 == 0
-                and self.linear2.out_features % 128 == 0):
+        from ... import kernels as K
+
+        sp = K.presplit_of(x) if self.fused else None
+        if (sp is not None and sp.norm is not None and _x6_ok(x, self.linear1.out_features)
+                and self.linear1.out_features % 128 == 0 and self.linear2.out_features % 128 == 0
+                and self.linear1.out_features % K.LINEAR_F32X6_BK == 0):
             # the LayerNorm's pre-split rows in, the hidden layer kept in the pre-split form (scaled per
             # row by a Cauchy-Schwarz bound of its values): neither GEMM splits in registers
-            from ... import kernels as K
-
             l1, l2 = self.linear1, self.linear2
             key = (l1.weight.data_ptr(), l1.weight._version, l1.bias.data_ptr(), l1.bias._version)
             cache = self.__dict__.get("_ffn_bounds")
@@ -231,8 +232,10 @@ class _LayerOps(nn.Module):
         splitting in registers (kernels.add_layernorm_split, rmbx_linear_f16x3_presplit)."""
         from ... import kernels as K
 
+        # (the pieces feed only the f16x3 GEMMs, which take K % LINEAR_F32X6_BK == 0: other widths keep
+        # the plain LayerNorm and the GEMM / library path that fits them)
         return (x.dtype == torch.float32 and F32_GEMM == "x6" and K.F32_PIECES == "f16x3" and K.GEMM_PRESPLIT
-                and x.shape[-1] % 4 == 0)
+                and x.is_cuda and x.shape[-1] % K.LINEAR_F32X6_BK == 0)
 
     def addnorm(self, norm, x, r):
         if self.fused:

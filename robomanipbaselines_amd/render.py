@@ -158,7 +158,16 @@ class Renderer:
                 self._vis = torch.full((n * H * W,), -1, dtype=torch.int64, device=self.device)
                 self._tflag = torch.zeros(n * ntiles, dtype=torch.uint8, device=self.device)
             self._scene.vis, self._scene.tflag = self._vis.data_ptr(), self._tflag.data_ptr()
-        N.call("rmbx_render_scene", ctypes.byref(cam), ctypes.byref(self._scene),
-               N.ptr(engine.gxpos), N.ptr(engine.gxmat), N.ptr(engine.xpos), N.ptr(engine.xquat),
-               engine.ngeom, engine.nbody, N.ptr(rgb), N.ptr(depth), N.ptr(hit_geom), N.ptr(policy), pdt,
-               N.ptr(active), n, N.stream_ptr())
+        try:
+            N.call("rmbx_render_scene", ctypes.byref(cam), ctypes.byref(self._scene),
+                   N.ptr(engine.gxpos), N.ptr(engine.gxmat), N.ptr(engine.xpos), N.ptr(engine.xquat),
+                   engine.ngeom, engine.nbody, N.ptr(rgb), N.ptr(depth), N.ptr(hit_geom), N.ptr(policy), pdt,
+                   N.ptr(active), n, N.stream_ptr())
+        except BaseException:
+            # the ray-cast pass is what empties the workspaces again: if the call failed after the
+            # visibility pass wrote them (or was interrupted between the launches), empty them here
+            # so no later frame of this Renderer sees stale mesh hits
+            if self._vis is not None:
+                self._vis.fill_(-1)
+                self._tflag.zero_()
+            raise

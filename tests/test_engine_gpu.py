@@ -4,8 +4,9 @@ iteration count and final active set per env, test_solver_takes_the_oracles_newt
 solver-side bars sit at the measured deviations, not at the solver tolerance: kinematics / mass
 matrix / bias forces 1e-10 relative; qacc 1e-9 relative to |qacc| + 1 (measured <= 2.3e-10),
 constraint forces and sensors 1e-11 (measured 1.3e-12 / 4.1e-13); one substep: qvel 1e-10 relative
-(measured 9.7e-12), qpos 1e-12 absolute (6.7e-14); bounded-horizon trajectories 1e-4 (chaotic
-contact dynamics amplify rounding over 200 substeps)."""
+(measured 9.7e-12), qpos 1e-12 absolute (6.7e-14); trajectories of all 69 qpos over 100 env-steps
+(800 substeps) 1e-9 (measured 3.1e-12; the divergence curve profiles/r6_divergence_cable.json shows
+no growth over that horizon, scripts/diag_divergence.py)."""
 
 import numpy as np
 import pytest
@@ -25,6 +26,8 @@ BAR_FORCE = 1e-11
 BAR_SENSOR = 1e-11
 BAR_QVEL1 = 1e-10
 BAR_QPOS1 = 1e-12
+# all 69 qpos over 100 env-steps from identical states (measured 3.1e-12, profiles/r6_divergence_cable.json)
+BAR_TRAJ_ALL = 1e-9
 
 
 def _states(arrays, n, seed=0, warm_steps=(0, 10, 40, 80)):
@@ -105,8 +108,11 @@ def test_one_substep_matches_oracle(arrays):
 
 
 def test_trajectory_bounded_horizon(arrays):
-    """25 env-steps (200 substeps, 0.8 s) under a fixed ctrl: joint trajectories within 1e-4."""
-    states = _states(arrays, 3, seed=2, warm_steps=(5,))
+    """16 envs, 100 env-steps (800 substeps, 3.2 s) under fixed ctrls from identical states: every
+    qpos -- arm, gripper linkage, the 48 cable hinges and the cable's free joint -- within the north
+    star's 1e-4, and within BAR_TRAJ_ALL (the divergence curve of these seeded states,
+    profiles/r6_divergence_cable.json: 3.1e-12 at worst over the 100 env-steps, no growth trend)."""
+    states = _states(arrays, 16, seed=2, warm_steps=(0, 5, 10, 40))
     eng = PhysicsEngine(arrays, len(states), DEV)
     _load(eng, states)
     orc = []
@@ -114,13 +120,16 @@ def test_trajectory_bounded_horizon(arrays):
         o = OracleEnv(arrays)
         o.set_state(t, qp, qv, qa, c)
         orc.append(o)
-    for step in range(25):
+    worst = 0.0
+    for step in range(100):
         eng.step(8)
         for o in orc:
-            o.step(8)
-    qpos = eng.qpos.cpu().numpy()
-    for i, o in enumerate(orc):
-        np.testing.assert_allclose(qpos[i][:14], o.state()[1][:14], rtol=0, atol=1e-4)
+            assert o.step(8) == 0
+        qpos = eng.qpos.cpu().numpy()
+        d = max(np.abs(qpos[i] - o.state()[1]).max() for i, o in enumerate(orc))
+        worst = max(worst, d)
+        assert d <= 1e-4 and d <= BAR_TRAJ_ALL, (step, d)
+    print(f"\n100 env-steps x 16 envs: max |d qpos| over all {eng.nq} coordinates {worst:.2e}")
     assert int(eng.stats[:, 3].sum()) == 0
 
 

@@ -59,3 +59,8 @@ def test_groupnorm_act_in_place_and_checks():
     assert out.data_ptr() == y.data_ptr() and torch.equal(out, want)
     with pytest.raises(ValueError):
         K.groupnorm_act(torch.randn(2, 12, 4, device=DEV), torch.ones(12, device=DEV), torch.zeros(12, device=DEV), 8)
+    # a caller-supplied out of the wrong shape, dtype or layout is rejected before the launch
+    for bad in (torch.empty(16, 128, 8, device=DEV), torch.empty(16, 128, 16, device=DEV, dtype=torch.float64),
+                torch.empty(16, 16, 128, device=DEV).transpose(1, 2)):
+        with pytest.raises(ValueError):
+            K.groupnorm_act(x, w, b, 8, out=bad)

@@ -239,3 +239,46 @@ def test_engine_matches_oracle_on_known_answer_models(name, q0, v0, ctrl, steps)
     qe, ve = _EngineRun(a, *args).run(steps)
     np.testing.assert_allclose(qe, qo, rtol=0, atol=1e-10)
     np.testing.assert_allclose(ve, vo, rtol=0, atol=1e-9)
+
+
+# tests/kat/box_edges.xml: A's top edge (y = 0, z = 0.2 + 0.05 sqrt 2) crossed by B's bottom edge
+# (x = 0), B lowered 1 mm into it
+BOX_EDGE_TOP = 0.2 + 0.05 * np.sqrt(2.0)
+
+
+def _box_edge_contact(kind):
+    a = _arrays("box_edges")
+    if kind == "oracle":
+        from oracle.dyn import OracleEnv
+
+        o = OracleEnv(a)
+        o.set_state(0.0, a["qpos0"].copy(), np.zeros(o.nv), np.zeros(o.nv), np.zeros(1))
+        o.forward()
+        c = o.contacts()
+        return c["pos"], c["dist"], c["frame"][:, 0]
+    import torch
+
+    from robomanipbaselines_amd.engine import PhysicsEngine
+
+    e = PhysicsEngine(a, 2, "cuda:0")
+    e.qpos.copy_(torch.tensor(np.tile(a["qpos0"], (2, 1))))
+    e.forward()
+    torch.cuda.synchronize()
+    ncon = int(e.stats[0, 0])
+    pos = e.ws("con_pos").cpu().numpy()[0, : 3 * ncon].reshape(ncon, 3)
+    assert np.array_equal(e.ws("con_pos").cpu().numpy()[0], e.ws("con_pos").cpu().numpy()[1])
+    return pos, None, None
+
+
+@pytest.mark.parametrize("kind", KINDS)
+def test_crossed_box_edges_touch_where_they_cross(kind):
+    """Box-box edge-on-edge contact (the support-point tie-break, pinned from first
+    principles instead of by the restated oracle): one contact, at the crossing point (0, 0) of the
+    two edges, halfway between them in z, 1 mm deep, normal along z -- not at the midpoint of the
+    two boxes' centres (0.015, 0.01), where a centre-of-support rule would put it."""
+    pos, dist, normal = _box_edge_contact(kind)
+    assert pos.shape == (1, 3)
+    np.testing.assert_allclose(pos[0], [0.0, 0.0, BOX_EDGE_TOP - 0.0005], rtol=0, atol=1e-12)
+    if dist is not None:
+        np.testing.assert_allclose(dist, [-0.001], rtol=0, atol=1e-12)
+        np.testing.assert_allclose(np.abs(normal[0]), [0.0, 0.0, 1.0], rtol=0, atol=1e-12)

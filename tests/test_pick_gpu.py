@@ -3,8 +3,8 @@ convex-hull collisions for the scanned objects, basket, bin and gripper meshes) 
 engine against the C oracle, and the synthetic tactile channel (envs/ur5e_pick.py) against a
 numpy restatement of its definition on the oracle's own contacts.
 
-Bars as in test_engine_gpu.py: forward (contact set, constraint rows, qacc 1e-6 relative to
-|qacc|+1), one env-step of 16 substeps qpos 1e-8, a bounded horizon 1e-4 on the arm/gripper."""
+Bars as in test_engine_gpu.py: forward (contact set, constraint rows, qacc 1e-9 relative to
+|qacc|+1), one env-step of 16 substeps qpos 1e-8, every qpos over a 50-env-step horizon (16 envs)."""
 
 import numpy as np
 import pytest
@@ -14,6 +14,8 @@ from robomanipbaselines_amd.envs.ur5e_pick import PICK_INIT_QPOS, TACTILE_INTERV
 
 DEV = "cuda:0"
 FRAME_SKIP = 16
+BAR_QACC = 1e-9  # the Cable scene's bar (tests/test_engine_gpu.py; measured 3.6e-10)
+BAR_TRAJ_ALL = 1e-10  # all qpos over 50 env-steps (measured 2.2e-14, profiles/r6_divergence_pick.json)
 
 
 @pytest.fixture(scope="module")
@@ -103,6 +105,20 @@ def _engine_from(arrays, orcs):
     return eng
 
 
+def _engine_from_states(arrays, states):
+    import torch
+
+    from robomanipbaselines_amd.engine import PhysicsEngine
+
+    eng = PhysicsEngine(arrays, len(states), DEV)
+    eng.time.copy_(torch.tensor([s[0] for s in states], dtype=torch.float64))
+    eng.qpos.copy_(torch.tensor(np.array([s[1] for s in states])))
+    eng.qvel.copy_(torch.tensor(np.array([s[2] for s in states])))
+    eng.qacc_ws.copy_(torch.tensor(np.array([s[3] for s in states])))
+    eng.ctrl.copy_(torch.tensor(np.array([s[4] for s in states])))
+    return eng
+
+
 def _orcs(arrays):
     out = []
     for grip, steps in ((0.0, 0), (0.0, 10), (255.0, 20), (120.0, 30)):
@@ -123,6 +139,7 @@ def test_pick_forward_matches_oracle(arrays):
     stats = eng.stats.cpu().numpy()
     qacc = eng.ws("qacc").cpu().numpy()
     xpos = eng.xpos.cpu().numpy()
+    worst = 0.0
     for i, o in enumerate(orcs):
         o.forward()
         np.testing.assert_allclose(xpos[i], o.xpos()[0], rtol=0, atol=1e-12)
@@ -130,29 +147,58 @@ def test_pick_forward_matches_oracle(arrays):
         assert stats[i, 1] == o.nefc(), "constraint rows"
         v = o.vecs()
         scale = np.abs(v["qacc"]).max() + 1.0
-        np.testing.assert_allclose(qacc[i], v["qacc"], rtol=0, atol=1e-6 * scale)
+        worst = max(worst, np.abs(qacc[i] - v["qacc"]).max() / scale)
+    print(f"\nPick forward: max |d qacc| / (max |qacc| + 1) = {worst:.2e}")
+    assert worst <= BAR_QACC, worst
+
+
+def horizon_states(arrays, n=16):
+    """Seeded Pick states for the horizon test and its divergence curve (scripts/diag_divergence.py):
+    gripper open / closed / half-closed, arm ctrl offsets, 0-30 env-steps settled in the oracle."""
+    from oracle.dyn import OracleEnv
+
+    rng = np.random.default_rng(4)
+    out = []
+    for i in range(n):
+        o = OracleEnv(arrays)
+        q = arrays["qpos0"].copy()
+        q[:14] = PICK_INIT_QPOS
+        grip = (0.0, 0.0, 255.0, 120.0)[i % 4]
+        ctrl = np.r_[PICK_INIT_QPOS[:6] + rng.normal(0, 0.03, 6), grip]
+        o.set_state(0.0, q, np.zeros(o.nv), np.zeros(o.nv), ctrl)
+        for _ in range((0, 10, 20, 30)[(i // 4) % 4]):
+            assert o.step(FRAME_SKIP) == 0
+        t, qp, qv, qa = o.state()
+        out.append((t, qp, qv, qa, ctrl))
+    return out
 
 
 @pytest.mark.gpu
 def test_pick_env_step_and_horizon_match_oracle(arrays):
-    import torch
+    """One env-step of 16 substeps within 1e-8, then 16 envs over 50 env-steps (800 substeps): every
+    qpos (arm, gripper, the free objects) within the north star's 1e-4 and within BAR_TRAJ_ALL (the
+    seeded states' divergence curve, profiles/r6_divergence_pick.json: 2.2e-14 at worst)."""
+    from oracle.dyn import OracleEnv
 
-    orcs = _orcs(arrays)
-    eng = _engine_from(arrays, orcs)
-    eng.step(FRAME_SKIP)
-    torch.cuda.synchronize()
-    q1 = eng.qpos.cpu().numpy()
-    for i, o in enumerate(orcs):
-        assert o.step(FRAME_SKIP) == 0
-        np.testing.assert_allclose(q1[i], o.state()[1], rtol=0, atol=1e-8)
-    for _ in range(9):
+    states = horizon_states(arrays)
+    eng = _engine_from_states(arrays, states)
+    orcs = []
+    for (t, qp, qv, qa, c) in states:
+        o = OracleEnv(arrays)
+        o.set_state(t, qp, qv, qa, c)
+        orcs.append(o)
+    worst = 0.0
+    for step in range(50):
         eng.step(FRAME_SKIP)
         for o in orcs:
-            o.step(FRAME_SKIP)
-    torch.cuda.synchronize()
-    q = eng.qpos.cpu().numpy()
-    for i, o in enumerate(orcs):
-        np.testing.assert_allclose(q[i][:14], o.state()[1][:14], rtol=0, atol=1e-4)
+            assert o.step(FRAME_SKIP) == 0
+        q = eng.qpos.cpu().numpy()
+        d = max(np.abs(q[i] - o.state()[1]).max() for i, o in enumerate(orcs))
+        if step == 0:
+            assert d <= 1e-8, d
+        worst = max(worst, d)
+        assert d <= 1e-4 and d <= BAR_TRAJ_ALL, (step, d)
+    print(f"\nPick 50 env-steps x 16 envs: max |d qpos| over all {eng.nq} coordinates {worst:.2e}")
     assert int(eng.stats[:, 3].sum()) == 0
     np.testing.assert_allclose(eng.time.cpu().numpy(), [o.state()[0] for o in orcs], rtol=0, atol=1e-12)
 

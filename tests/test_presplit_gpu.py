@@ -17,6 +17,10 @@ pytestmark = pytest.mark.gpu
 DEV = "cuda:0"
 
 
+# the pre-split FFN chain against an f64 chain (max |err| / max |ref|): worst measured case 1.46e-6
+BAR_FFN_CHAIN = 1.6e-6
+
+
 def _err(got, ref):
     return ((got.double() - ref).abs().max() / ref.abs().max()).item()
 
@@ -190,12 +194,13 @@ def test_ffn_chain_in_presplit_form(M, scale):
     assert _err(rec, h_ref) <= 4e-6
     out = K_.linear_presplit(hs, K_.split_f16x2(w2), b2)
     ref = h_ref @ w2.double().t() + b2.double()
-    base = F.linear(F.linear(a, w1, b1).clamp_min(0), w2, b2)
-    e, e32 = _err(out, ref), _err(base, ref)
-    # (the library chain's own error is not a fixed number: for the 1e-12 rows it measured 1.8e-7 on
-    # one box and 5.6e-7 on another with the same inputs, its kernel choice differing, while this
-    # path's is 5.49e-7 on both -- profiles/r5_ffn_presplit_err.log; hence 3x + 2e-7, not 2x + 1e-7)
-    assert e <= 4e-6 and e <= 3 * e32 + 2e-7, (e, e32)
+    e = _err(out, ref)
+    # anchored on the f64 chain alone: this path is deterministic (fixed summation order, no
+    # library kernel choice), and its error on these seeded cases is the same on every box --
+    # 1.46e-6 / 5.49e-7 / 1.45e-6 for the 1.0 / 1e-12 / 3e6 rows (profiles/r5_ffn_presplit_err.log),
+    # against 2.1e-6 / 5.6e-7 / 2.0e-6 for the library f32 chain; the bar sits just above the worst
+    print(f"\nFFN chain pre-split vs f64: {e:.3e}")
+    assert e <= BAR_FFN_CHAIN, e
 
 
 @torch.no_grad()
@@ -237,3 +242,24 @@ def test_winograd_presplit_vs_f64_and_batch_invariance(monkeypatch, n, C, H, W, 
     last = K_.conv3x3_wino4_x6(xd[n - 1:].contiguous(memory_format=cl), planes, b.to(DEV), relu=relu,
                                res=None if rd is None else rd[n - 1:].contiguous(memory_format=cl))
     assert torch.equal(last[0], got[n - 1])
+
+
+@torch.no_grad()
+def test_stale_pieces_are_not_used_after_an_in_place_change():
+    """The pieces a LayerNorm attaches describe its f32 output only until that output changes: after an
+    in-place update the GEMM must split the new values in registers, giving exactly what
+    it gives for a fresh tensor holding them."""
+    from robomanipbaselines_amd import kernels as K_
+
+    x, r = _rows(512, 512, 3)
+    a = K_.add_layernorm_split(x, r, torch.ones(512, device=DEV), torch.zeros(512, device=DEV), 1e-5)
+    assert K_.presplit_of(a) is a.rmbx_split
+    g = torch.Generator(device="cpu").manual_seed(9)
+    w = (torch.randn(256, 512, generator=g) / 512 ** 0.5).to(DEV)
+    planes = K_.split_f16x2(w)
+    a.mul_(3.0).add_(0.25)
+    assert K_.presplit_of(a) is None
+    got = K_.linear_f32x6(a, planes, None)
+    want = K_.linear_f32x6(a.clone(), planes, None)
+    assert torch.equal(got, want)
+    assert _err(got, a.double() @ w.double().t()) <= 4e-6

@@ -106,3 +106,35 @@ def test_renderer_matches_the_brute_force_oracle_on_every_camera():
             if cam == "front":
                 assert mesh_frac > 0.01, (cam, e, mesh_frac)  # the arm's meshes are in the policy view
     print("\n" + "\n".join(report))
+
+
+@torch.no_grad()
+def test_rerender_after_motion_equals_a_fresh_renderer():
+    """The visibility workspaces come back empty after every call (the ray-cast pass consumes every
+    key and tile flag it reads): a Renderer that drew a camera, then draws it again after the arm has
+    moved, produces bitwise the frame a fresh Renderer draws of the new state -- no stale mesh hits
+    of the first frame survive -- on every camera."""
+    from robomanipbaselines_amd.render import Renderer
+
+    env = _env_states()
+    eng, rnd = env.engine, env.renderer
+    n, H, W = eng.n_env, rnd.height, rnd.width
+
+    def frame(r, cam):
+        rgb = torch.empty((n, H, W, 3), dtype=torch.uint8, device=DEV)
+        depth = torch.empty((n, H, W), dtype=torch.float32, device=DEV)
+        hit = torch.empty((n, H, W), dtype=torch.int32, device=DEV)
+        r.render(eng, cam, rgb=rgb, depth=depth, hit_geom=hit)
+        return rgb, depth, hit
+
+    for cam in env.camera_names:
+        before = frame(rnd, cam)
+        q = eng.qpos.clone()
+        q[:, :6] += torch.tensor([0.3, 0.2, -0.25, 0.4, -0.3, 0.5], dtype=torch.float64, device=DEV)
+        eng.qpos.copy_(q)
+        eng.forward()
+        again = frame(rnd, cam)
+        fresh = frame(Renderer(env.arrays, DEV, width=W, height=H), cam)
+        for a, b in zip(again, fresh):
+            assert torch.equal(a, b), cam
+        assert not torch.equal(before[2], again[2]), cam  # the arm moved in the frame
