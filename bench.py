@@ -48,6 +48,7 @@ HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: HBM3E 8 TB/s (spec)
 FP64_PEAK_TFLOPS = 78.6  # MI355X FP64 vector (spec)
 MFMA_PEAK_TFLOPS = {"fp32": 157.3, "bf16": 2500.0}  # MI355X_MICROARCH.md: F32 / BF16 MFMA dense
 GOLDEN = os.path.join(ROOT, "tests", "golden")
+C3_PER_RANK = 512  # BASELINE.json configs[2]: 4096 envs over 8 GPUs
 CPU_WORKERS_MAX = 16  # fallback CPU share per GPU when the box does not export OMP_NUM_THREADS
 _T0 = time.time()
 
@@ -312,6 +313,7 @@ def parse(argv=None):
                         "(measured: no gain at 1024 envs, DESIGN.md section 5)")
     p.add_argument("--no_bf16_secondary", action="store_true")
     p.add_argument("--no_cpu_baseline", action="store_true")
+    p.add_argument("--no_c3_per_rank", action="store_true", help="skip the 512-env configs[2] per-rank line")
     p.add_argument("--act_full_decoder", action="store_true", help="also run the dead decoder layers 1..6")
     p.add_argument("--cpu_steps", type=int, default=60, help="timed env-steps per CPU throughput worker")
     p.add_argument("--cpu_latency_steps", type=int, default=150, help="timed env-steps of the 1-env latency leg")
@@ -742,6 +744,30 @@ def rank_main(args):
             "value_estimate": round(total / (elapsed / args.steps + extra), 1), "unit": "env-steps/s",
             "note": "the same step with decoder layers 1..6 computed too (their output is never read): "
                     "timed value with the per-env-step policy time replaced by the measured 7-layer call"}
+    if world == 1 and not strong and args.precision == "fp32" and n > C3_PER_RANK and not args.no_c3_per_rank:
+        # BASELINE.json configs[2] (4096 envs over 8 GPUs) runs 512 envs per rank with no data-path
+        # collective: its per-rank workload measured here, same loop and window, on this one GPU
+        del groups, ro, eng
+        torch.cuda.empty_cache()
+        g3 = [make_rollout(args, dev, "fp32", C3_PER_RANK, 0)]
+        el3, ph3, inf3, _, phases3 = timed_run(g3, args, False)
+        v3 = C3_PER_RANK * args.steps / el3
+        result["c3_per_rank"] = {
+            "value": round(v3, 1), "unit": "env-steps/s", "num_envs": C3_PER_RANK,
+            "ms_per_step": round(1e3 * el3 / args.steps, 3),
+            "physics_kernel_ms": round(float(ph3.mean()), 3),
+            "policy_inference_us_per_call": round(1e6 * float(inf3.mean()), 1) if len(inf3) else None,
+            "phases": phases3,
+            "projection_8gpu": {"value": round(8 * v3, 1), "unit": "env-steps/s",
+                                "basis": "8 x this per-rank rate: the ranks share no data-path collective (one "
+                                         "all-gather of episode records after the loop), so configs[2] is 8 "
+                                         "independent copies of this workload; an estimate, not a measurement"},
+            "note": "BASELINE.json configs[2]'s per-rank workload (4096 envs / 8 GPUs): the same fp32 ACT loop, "
+                    "steps and warm-up as `value`, 512 envs on one GPU; the physics solver runs two blocks per "
+                    "CU at this size (csrc/rmbx_engine.hip solver_minb_for)"}
+        del g3
+        torch.cuda.empty_cache()
+        groups = ro = eng = None
     if args.precision == "fp32" and not args.no_bf16_secondary:
         del groups, ro, eng
         torch.cuda.empty_cache()

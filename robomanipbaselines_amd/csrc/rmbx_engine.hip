@@ -86,6 +86,7 @@ struct rmbx_engine {
   rmbx_env_buffers bufs;
   bool bound;
   size_t front_lds;  // dynamic LDS of a front-kernel launch (front_launch_lds)
+  int solver_minb;   // solver blocks per CU of this batch size (solver_minb_for)
 };
 
 namespace rmbx {
@@ -3678,13 +3679,23 @@ __global__ void __launch_bounds__(SOLVER_THREADS, MINB) solver_kernel(KArgs args
   PROF(7)
 }
 
-// solver blocks resident per CU (launch bound): 4 (<= 128 VGPRs, spills) by default;
-// RMBX_SOLVER_MINB = 3 / 2 for the register-budget measurement (scripts/prof_physics.py)
-static void launch_solver(int n_env, hipStream_t st, const KArgs& a) {
-  static const int minb = [] {
-    const char* v = getenv("RMBX_SOLVER_MINB");
-    return v ? atoi(v) : 4;
-  }();
+// solver blocks resident per CU (launch bound): 4 (<= 128 VGPRs) when the batch needs more than two
+// envs per CU -- 1,024 envs run in one round of blocks only at that occupancy -- and 2 (up to 256
+// VGPRs: 28 % fewer cycles per env, profiles/r3_solver_occupancy_minb.log) when every env already
+// fits in one round at two per CU (C3's 512 envs per GPU).  Same source, same arithmetic: states
+// are bitwise equal either way (tests/test_shard_gpu.py runs 512-env shards against 1,024 envs).
+// RMBX_SOLVER_MINB = 2 / 3 / 4 forces one (scripts/prof_physics.py).
+static int solver_minb_for(int n_env) {
+  const char* v = getenv("RMBX_SOLVER_MINB");
+  if (v) return atoi(v);
+  int dev = 0, cus = 0;
+  if (hipGetDevice(&dev) != hipSuccess ||
+      hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess || cus <= 0)
+    return 4;
+  return n_env <= 2 * cus ? 2 : 4;
+}
+
+static void launch_solver(int minb, int n_env, hipStream_t st, const KArgs& a) {
   if (minb == 2)
     hipLaunchKernelGGL(solver_kernel<2>, dim3(n_env), dim3(SOLVER_THREADS), 0, st, a);
   else if (minb == 3)
@@ -3964,6 +3975,7 @@ int rmbx_engine_create(const struct rmbx_model* model, int n_env, rmbx_engine** 
   }
   eng->L = make_layout(h);
   eng->front_lds = front_launch_lds(eng);
+  eng->solver_minb = solver_minb_for(n_env);
   *out = eng;
   return RMBX_OK;
 }
@@ -4110,7 +4122,7 @@ static int launch(rmbx_engine* eng, int nsub, int integ, const uint8_t* active, 
     else
       hipLaunchKernelGGL(front_kernel<false>, dim3(eng->n_env), dim3(64), front_lds, st, a);
     RMBX_CHECK_LAUNCH();
-    launch_solver(eng->n_env, st, a);
+    launch_solver(eng->solver_minb, eng->n_env, st, a);
     RMBX_CHECK_LAUNCH();
   }
   if (integ) {
@@ -4125,7 +4137,7 @@ static int launch(rmbx_engine* eng, int nsub, int integ, const uint8_t* active, 
     else
       hipLaunchKernelGGL(front_kernel<false>, dim3(eng->n_env), dim3(64), front_lds, st, a);
     RMBX_CHECK_LAUNCH();
-    launch_solver(eng->n_env, st, a);
+    launch_solver(eng->solver_minb, eng->n_env, st, a);
     RMBX_CHECK_LAUNCH();
   }
   return RMBX_OK;
