@@ -348,7 +348,36 @@ typedef struct rmbx_scene_tables {
   const float* mesh_rad;
   unsigned long long* vis;
   uint8_t* tflag;
+  /* materials (optional; geom_matinfo NULL: flat material colours, no specular term, background
+   * (0.9, 1, 1) -- the round-5 shading).  Indexed by geom id: geom_texid [ngeom] the texture of
+   * the geom's material (-1: none; primitives only), geom_matinfo [ngeom][6] = (specular,
+   * shininess, texrepeat x, y, texuniform, emission) of MuJoCo's <material>
+   * (envs/assets/mujoco/envs/ur5e/env_ur5e_common.xml:13-25); textures tex_desc [ntex][4] =
+   * (type 0 "2d" / 1 "cube", height, width, first texel), texels tex_rgba as RGBA8 words (R in the
+   * low byte, rows in file order), each texture followed by its box-filtered mip levels, whose
+   * first texels tex_level_adr lists (relative to the texture's; level l
+   * max(H >> l, 1) x max(W >> l, 1) down to 1 x 1, texel = (sum of the 2 x 2 texels above, rows /
+   * columns clamped, + 2) / 4); sky_rgb = the gradient skybox's rgb1 (up), rgb2 (down).
+   * Sampling (trilinear as GL_LINEAR_MIPMAP_LINEAR with an isotropic footprint: level of detail
+   * log2(t pix / max(n.v, 1e-3) x density), t the camera depth, pix = 2 tan(fovy / 2) / height, the
+   * density in base texels per metre -- 2d: max(rx W, ry H) per metre of repeat, cube: max(W, H) /
+   * (2 |major axis coordinate|); bilinear per level, texel centres at +0.5): 2d from the hit's
+   * local (x, y), repeated
+   * texrepeat times over the geom's (2 size_x, 2 size_y) extent, or per metre when texuniform or
+   * the plane is infinite; cube from the local hit point (divided by the geom's half extents when
+   * texuniform) as a cube-map direction, the same image on all six faces, OpenGL's face
+   * orientation, clamped at the face edges.  Shading: material colour x texture x (0.1 ambient +
+   * 0.6 headlight |n.v| + 0.3 max(0, n.z) + emission) + specular x 0.3 x max(0, n.h)^(128
+   * shininess) for the directional light (world +z towards it, h the half vector), clamped at 1. */
+  const int32_t* geom_texid;
+  const float* geom_matinfo;
+  const uint32_t* tex_rgba;
+  const int32_t* tex_desc;
+  const int32_t* tex_level_adr; /* [ntex][RMBX_TEX_LEVELS]: first texel of each mip level */
+  int32_t ntex;
+  float sky_rgb[6];
 } rmbx_scene_tables;
+#define RMBX_TEX_LEVELS 16 /* mip levels per texture (images up to 32768 texels wide) */
 
 int rmbx_render_scene(const rmbx_camera* cam, const rmbx_scene_tables* scene, const double* gxpos,
                       const double* gxmat, const double* xpos, const double* xquat, int ngeom,

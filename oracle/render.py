@@ -28,6 +28,63 @@ class _Prim(ctypes.Structure):
                 ("R", ctypes.c_double * 9)]
 
 
+class _Materials(ctypes.Structure):
+    _fields_ = [("geom_texid", ctypes.c_void_p), ("geom_matinfo", ctypes.c_void_p), ("tex_rgb", ctypes.c_void_p),
+                ("tex_desc", ctypes.c_void_p), ("sky", ctypes.c_double * 6)]
+
+
+def _pyramid(img):
+    """The mip levels of the renderer's contract (include/rmbx.h rmbx_scene_tables), restated:
+    level l of an H x W image is max(H >> l, 1) x max(W >> l, 1) down to 1 x 1, each texel the
+    rounded mean (+ 2, // 4) of the 2 x 2 texels of the level above, indices clamped at its edge."""
+    H, W = img.shape[:2]
+    levels = [np.asarray(img, np.int64)]
+    for l in range(1, max(H, W).bit_length()):
+        up = levels[-1]
+        ys = np.minimum(np.arange(2 * max(H >> l, 1)), up.shape[0] - 1)
+        xs = np.minimum(np.arange(2 * max(W >> l, 1)), up.shape[1] - 1)
+        q = up[ys][:, xs]
+        levels.append((q[0::2, 0::2] + q[0::2, 1::2] + q[1::2, 0::2] + q[1::2, 1::2] + 2) // 4)
+    return levels
+
+
+_MATERIALS = {}
+
+
+def materials(arrays):
+    """(orc_materials struct, the arrays it points into) of a scene compiled with its materials
+    (compiler.visual_arrays), or (None, None): the renderer's material tables restated from the
+    compiled arrays -- texture per geom, (specular, shininess, texrepeat, texuniform, emission),
+    the decoded texture images with their mip pyramids, the gradient skybox.  Cached per arrays
+    object (keep it unchanged once cast)."""
+    if "geom_matinfo" not in arrays:
+        return None, None
+    key = (id(arrays), id(arrays["tex_rgb"]), id(arrays["geom_matinfo"]), id(arrays["geom_texid"]))
+    if key not in _MATERIALS:
+        _MATERIALS[key] = _materials(arrays)
+    return _MATERIALS[key]
+
+
+def _materials(arrays):
+    desc = np.zeros((max(1, len(arrays["tex_type"])), 4), np.int32)
+    texels, adr = [], 0
+    for i in range(len(arrays["tex_type"])):
+        h, w = (int(x) for x in arrays["tex_size"][i])
+        a0 = int(arrays["tex_adr"][i])
+        desc[i] = (int(arrays["tex_type"][i]), h, w, adr)
+        for lv in _pyramid(np.asarray(arrays["tex_rgb"][a0:a0 + h * w], np.int64).reshape(h, w, 3)):
+            texels.append(lv.reshape(-1, 3))
+            adr += lv.shape[0] * lv.shape[1]
+    keep = [np.ascontiguousarray(arrays["geom_texid"], np.int32),
+            np.ascontiguousarray(arrays["geom_matinfo"], np.float32),
+            np.ascontiguousarray(np.concatenate(texels), np.uint8) if texels else np.zeros((1, 3), np.uint8), desc]
+    m = _Materials()
+    m.geom_texid, m.geom_matinfo, m.tex_rgb, m.tex_desc = (k.ctypes.data for k in keep)
+    for i, v in enumerate(np.asarray(arrays["sky_rgb"], np.float64).reshape(-1)):
+        m.sky[i] = float(v)
+    return m, keep
+
+
 def _load():
     global _lib
     if _lib is None:
@@ -35,7 +92,7 @@ def _load():
             subprocess.run(["make", "-C", _DIR], check=True, capture_output=True)
         _lib = ctypes.CDLL(_LIB)
         vp, ip, dp = ctypes.c_void_p, ctypes.c_int, ctypes.c_double
-        _lib.orc_render_rays.argtypes = [vp, ip, vp, vp, vp, dp, ip, ip, dp, vp, ip, vp, vp, vp, vp]
+        _lib.orc_render_rays.argtypes = [vp, ip, vp, vp, vp, dp, ip, ip, dp, vp, ip, vp, vp, vp, vp, vp]
     return _lib
 
 
@@ -96,10 +153,11 @@ def camera_pose(arrays, cam_name, xpos, xquat):
     return R, p
 
 
-def cast(arrays, prims, gxpos, gxmat, xpos, xquat, cam_name, width, height, pix, second=False):
+def cast(arrays, prims, gxpos, gxmat, xpos, xquat, cam_name, width, height, pix, second=False, use_materials=True):
     """Rays of one env through the continuous pixel coordinates pix [n, 2] (x, y; centres at +0.5):
     (geom id [n] (-1: background), camera depth [n], shaded colour [n, 3] in [0, 1]); with
-    second=True also the depth of the nearest hit of any other geom [n] (inf if none)."""
+    second=True also the depth of the nearest hit of any other geom [n] (inf if none).  The
+    scene's materials and textures are applied when it carries them (use_materials)."""
     lib = _load()
     gm_all = np.asarray(gxmat, np.float64).reshape(-1, 9)
     plist = []
@@ -123,9 +181,11 @@ def cast(arrays, prims, gxpos, gxmat, xpos, xquat, cam_name, width, height, pix,
     tri = np.ascontiguousarray(arrays["rmesh_tri"] if "rmesh_tri" in arrays else np.zeros((1, 16), np.float32),
                                np.float32)
     Rf = np.ascontiguousarray(R.reshape(-1))
+    mat, _keep = materials(arrays) if use_materials else (None, None)
     lib.orc_render_rays(ctypes.cast(parr, ctypes.c_void_p), len(plist), tri.ctypes.data, Rf.ctypes.data, p.ctypes.data,
                         float(arrays["cam_fovy"][i]), int(width), int(height), znear, pix.ctypes.data, n,
-                        geom.ctypes.data, depth.ctypes.data, rgb.ctypes.data, depth2.ctypes.data)
+                        geom.ctypes.data, depth.ctypes.data, rgb.ctypes.data, depth2.ctypes.data,
+                        None if mat is None else ctypes.addressof(mat))
     if second:
         return geom, depth, rgb, np.where(depth2 >= 1e300, np.inf, depth2)
     return geom, depth, rgb

@@ -10,7 +10,10 @@
  * plane = local z = 0, unbounded; sphere / capsule / cylinder / box as MuJoCo sizes them; a camera
  * inside a primitive sees none of it; hits at t <= 1e-4 ignored; triangles two-sided and clipped at
  * t <= znear; nearest hit wins.  Shading 0.1 + 0.6 |n.v| + 0.3 max(0, n_z) (normal turned to the
- * viewer, light along world -z), times the material colour, clamped at 1; background (0.9, 1, 1).
+ * viewer, light along world -z), times the material colour, clamped at 1; background (0.9, 1, 1);
+ * with materials (round 6) the colour times the primitive's texture sample (2d / cube, trilinear
+ * over the mip pyramid, level of detail from the pixel's isotropic footprint) plus the emission, the light's
+ * Blinn-Phong specular term, and the gradient skybox behind.
  * Parity is "unpinned" against MuJoCo's OpenGL renderer (not in the image); this checks the ray
  * caster against its own specification.
  */
@@ -158,20 +161,145 @@ typedef struct {
   double t, n[3], rgb[3];
   int geom;
   double t2;  /* nearest hit of any other geom (1e300: none) */
+  const orc_prim* prim; /* the nearest surface's primitive (NULL: a mesh triangle) */
+  double pl[3];         /* its hit point in the primitive's frame */
 } orc_best;
 
-static void consider(orc_best* b, double t, int geom, const double* n, const double* rgb) {
+static void consider(orc_best* b, double t, int geom, const double* n, const double* rgb, const orc_prim* prim,
+                     const double* pl) {
   if (t < b->t || (t == b->t && geom < b->geom)) {
     if (geom != b->geom && b->t < b->t2) b->t2 = b->t;
     b->t = t;
     b->geom = geom;
+    b->prim = prim;
     for (int i = 0; i < 3; i++) {
       b->n[i] = n[i];
       b->rgb[i] = rgb[i];
+      b->pl[i] = pl ? pl[i] : 0.0;
     }
   } else if (geom != b->geom && t < b->t2) {
     b->t2 = t;
   }
+}
+
+/* Materials (the renderer's contract, include/rmbx.h rmbx_scene_tables): per geom its texture
+ * (-1: none) and (specular, shininess, texrepeat x, y, texuniform, emission); textures (type 0 2d /
+ * 1 cube, height, width, first texel) over RGB texels in file row order; the skybox gradient rgb1
+ * (up) / rgb2 (down).  NULL: flat material colours, no specular, background (0.9, 1, 1). */
+typedef struct {
+  const int32_t* geom_texid;
+  const float* geom_matinfo;
+  const uint8_t* tex_rgb;
+  const int32_t* tex_desc;
+  double sky[6];
+} orc_materials;
+
+static void orc_texel(const uint8_t* t, long idx, double w, double* c) {
+  for (int i = 0; i < 3; i++) c[i] += w * (double)t[3 * idx + i];
+}
+
+/* bilinear at continuous texel coordinates (texel centres at integers), wrapped (2d) or clamped
+   at the edges (cube faces) */
+static void orc_bilinear(const uint8_t* t, int H, int W, double fx, double fy, int wrap, double* c) {
+  const double x0f = floor(fx), y0f = floor(fy), ax = fx - x0f, ay = fy - y0f;
+  long x0 = (long)x0f, y0 = (long)y0f, x1 = x0 + 1, y1 = y0 + 1;
+  if (wrap) {
+    x0 = ((x0 % W) + W) % W; x1 = ((x1 % W) + W) % W;
+    y0 = ((y0 % H) + H) % H; y1 = ((y1 % H) + H) % H;
+  } else {
+    x0 = x0 < 0 ? 0 : (x0 > W - 1 ? W - 1 : x0); x1 = x1 < 0 ? 0 : (x1 > W - 1 ? W - 1 : x1);
+    y0 = y0 < 0 ? 0 : (y0 > H - 1 ? H - 1 : y0); y1 = y1 < 0 ? 0 : (y1 > H - 1 ? H - 1 : y1);
+  }
+  c[0] = c[1] = c[2] = 0.0;
+  orc_texel(t, y0 * W + x0, (1 - ax) * (1 - ay), c);
+  orc_texel(t, y0 * W + x1, ax * (1 - ay), c);
+  orc_texel(t, y1 * W + x0, (1 - ax) * ay, c);
+  orc_texel(t, y1 * W + x1, ax * ay, c);
+  for (int i = 0; i < 3; i++) c[i] /= 255.0;
+}
+
+/* texture coordinates in base-level texel units (fx = u W, fy = v H) of local point q and the
+   texture's density there (base texels per metre along the surface): 2d from (x, y); cube maps on
+   the major axis' face, OpenGL's face orientation */
+static void orc_tex_coords(int ttype, int H, int W, const orc_prim* P, const float* mi, const double* pl,
+                           double* fx, double* fy, double* dens) {
+  const int uni = mi[4] != 0.0f;
+  const double* s = P->size;
+  if (ttype == 0) { /* 2d: (x, y), texrepeat over the geom's extent, or per metre */
+    const double sx = s[0], sy = (P->type == 6 || P->type == 0) ? s[1] : s[0];
+    double u = pl[0] * mi[2], v = pl[1] * mi[3], kx = mi[2], ky = mi[3];
+    if (!uni && sx > 0 && sy > 0) {
+      kx = mi[2] / (2 * sx);
+      ky = mi[3] / (2 * sy);
+      u = mi[2] * (pl[0] / (2 * sx) + 0.5);
+      v = mi[3] * (pl[1] / (2 * sy) + 0.5);
+    }
+    *fx = u * W;
+    *fy = v * H;
+    *dens = kx * W > ky * H ? kx * W : ky * H;
+    return;
+  }
+  double q[3] = {pl[0], pl[1], pl[2]}, hmin = 1;
+  if (uni) { /* the unit object: local point over the half extents */
+    double h[3] = {s[0], s[0], s[0]};
+    if (P->type == 6) { h[1] = s[1]; h[2] = s[2]; }
+    else if (P->type == 3) h[2] = s[1] + s[0];
+    else if (P->type == 5) h[2] = s[1];
+    else if (P->type == 0) { h[1] = s[1]; h[2] = 1; }
+    for (int i = 0; i < 3; i++) q[i] = h[i] > 0 ? q[i] / h[i] : q[i];
+    for (int i = 0; i < 3; i++) {
+      const double hi = h[i] > 0 ? h[i] : 1;
+      if (i == 0 || hi < hmin) hmin = hi;
+    }
+  }
+  const double x = fabs(q[0]), y = fabs(q[1]), z = fabs(q[2]);
+  double sc, tc, ma;
+  if (x >= y && x >= z) {
+    ma = x; sc = q[0] > 0 ? -q[2] : q[2]; tc = -q[1];
+  } else if (y >= z) {
+    ma = y; sc = q[0]; tc = q[1] > 0 ? q[2] : -q[2];
+  } else {
+    ma = z; sc = q[2] > 0 ? q[0] : -q[0]; tc = -q[1];
+  }
+  if (!(ma > 1e-300)) ma = 1e-300;
+  *fx = 0.5 * (sc / ma + 1) * W;
+  *fy = 0.5 * (tc / ma + 1) * H;
+  *dens = 0.5 * (W > H ? W : H) / ma / hmin;
+}
+
+/* the texture colour of a primitive at its local hit point pl, trilinear (GL_LINEAR_MIPMAP_LINEAR)
+   with an isotropic footprint: the pixel spans `foot` metres of the surface, the level of detail is
+   log2(foot x density); the pyramid's level l (max(H >> l, 1) x max(W >> l, 1)) follows the levels
+   before it */
+static void orc_texture(const orc_materials* M, int tex, const orc_prim* P, const float* mi, const double* pl,
+                        double foot, double* c) {
+  const int32_t* td = M->tex_desc + 4 * tex;
+  const uint8_t* t = M->tex_rgb + 3 * (long)td[3];
+  const int H = td[1], W = td[2];
+  double fx, fy, dens;
+  orc_tex_coords(td[0], H, W, P, mi, pl, &fx, &fy, &dens);
+  const double rho = foot * dens;
+  int levels = 1;
+  while ((H >> levels) > 0 || (W >> levels) > 0) ++levels;
+  double lod = log2(rho > 1e-300 ? rho : 1e-300);
+  lod = lod < 0 ? 0 : (lod > levels - 1 ? levels - 1 : lod);
+  const int l0 = (int)lod;
+  const double fr = lod - l0;
+  const int wrap = td[0] == 0;
+  long off = 0;
+  for (int l = 0; l < l0; l++) off += (long)((H >> l) > 1 ? (H >> l) : 1) * ((W >> l) > 1 ? (W >> l) : 1);
+  double c0[3], c1[3];
+  int Hl = (H >> l0) > 1 ? (H >> l0) : 1, Wl = (W >> l0) > 1 ? (W >> l0) : 1;
+  orc_bilinear(t + 3 * off, Hl, Wl, fx * Wl / W - 0.5, fy * Hl / H - 0.5, wrap, c0);
+  if (fr > 0 && l0 + 1 < levels) {
+    off += (long)Hl * Wl;
+    Hl = (H >> (l0 + 1)) > 1 ? (H >> (l0 + 1)) : 1;
+    Wl = (W >> (l0 + 1)) > 1 ? (W >> (l0 + 1)) : 1;
+    orc_bilinear(t + 3 * off, Hl, Wl, fx * Wl / W - 0.5, fy * Hl / H - 0.5, wrap, c1);
+  } else {
+    for (int i = 0; i < 3; i++) c1[i] = c0[i];
+  }
+  for (int i = 0; i < 3; i++) c[i] = c0[i] + fr * (c1[i] - c0[i]);
 }
 
 /* Cast `nray` camera rays: pix [nray][2] = continuous pixel coordinates (x, y), pixel centres at
@@ -182,13 +310,13 @@ static void consider(orc_best* b, double t, int geom, const double* n, const dou
  * coincident surface there makes the pixel's geom a tie). */
 void orc_render_rays(const orc_prim* prims, int nprim, const float* tri, const double* cam_R, const double* cam_p,
                      double fovy_deg, int W, int H, double znear, const double* pix, int nray, int32_t* out_geom,
-                     double* out_depth, double* out_rgb, double* out_depth2) {
+                     double* out_depth, double* out_rgb, double* out_depth2, const orc_materials* mat) {
   const double tanh_ = tan(0.5 * fovy_deg * ORC_PI / 180.0), aspect = (double)W / (double)H;
   for (int k = 0; k < nray; k++) {
     const double dc[3] = {(2.0 * pix[2 * k] / W - 1.0) * tanh_ * aspect, (1.0 - 2.0 * pix[2 * k + 1] / H) * tanh_, -1.0};
     double dw[3];
     for (int i = 0; i < 3; i++) dw[i] = cam_R[3 * i] * dc[0] + cam_R[3 * i + 1] * dc[1] + cam_R[3 * i + 2] * dc[2];
-    orc_best b = {1e300, {0, 0, 1}, {0, 0, 0}, -1, 1e300};
+    orc_best b = {1e300, {0, 0, 1}, {0, 0, 0}, -1, 1e300, NULL, {0, 0, 0}};
     for (int q = 0; q < nprim; q++) {
       const orc_prim* P = prims + q;
       const double* c = P->pos;
@@ -227,7 +355,7 @@ void orc_render_rays(const orc_prim* prims, int nprim, const float* tri, const d
               const int gid = tag & 0xffff; /* tag = (mesh slot << 16) | geom id */
               const double nt[3] = {tr[9], tr[10], tr[11]}, rgb[3] = {tr[13], tr[14], tr[15]};
               for (int i = 0; i < 3; i++) nw[i] = R[3 * i] * nt[0] + R[3 * i + 1] * nt[1] + R[3 * i + 2] * nt[2];
-              consider(&b, tt, gid, nw, rgb);
+              consider(&b, tt, gid, nw, rgb, NULL, NULL);
             }
           }
           break;
@@ -236,31 +364,60 @@ void orc_render_rays(const orc_prim* prims, int nprim, const float* tri, const d
       }
       if (h) {
         for (int i = 0; i < 3; i++) nw[i] = R[3 * i] * nl[0] + R[3 * i + 1] * nl[1] + R[3 * i + 2] * nl[2];
-        consider(&b, t, P->geom, nw, P->rgb);
+        const double pl[3] = {o[0] + t * d[0], o[1] + t * d[1], o[2] + t * d[2]};
+        consider(&b, t, P->geom, nw, P->rgb, P, pl);
       }
     }
     out_geom[k] = b.geom;
     out_depth2[k] = b.t2;
+    const double inv = 1.0 / sqrt(dot3(dw, dw));
     if (b.geom < 0) {
       out_depth[k] = -1;
-      out_rgb[3 * k] = 0.9;
-      out_rgb[3 * k + 1] = 1.0;
-      out_rgb[3 * k + 2] = 1.0;
+      if (mat) { /* gradient skybox by the ray's world z */
+        const double f = 0.5 * (1.0 + dw[2] * inv);
+        for (int i = 0; i < 3; i++) out_rgb[3 * k + i] = mat->sky[3 + i] + f * (mat->sky[i] - mat->sky[3 + i]);
+      } else {
+        out_rgb[3 * k] = 0.9;
+        out_rgb[3 * k + 1] = 1.0;
+        out_rgb[3 * k + 2] = 1.0;
+      }
       continue;
     }
     out_depth[k] = b.t;
-    const double inv = 1.0 / sqrt(dot3(dw, dw));
     const double nn = sqrt(dot3(b.n, b.n));
-    double ndv = -(b.n[0] * dw[0] + b.n[1] * dw[1] + b.n[2] * dw[2]) * inv / nn;
-    double nz = b.n[2] / nn;
-    if (ndv < 0) {
+    double nw_[3] = {b.n[0] / nn, b.n[1] / nn, b.n[2] / nn};
+    double ndv = -(nw_[0] * dw[0] + nw_[1] * dw[1] + nw_[2] * dw[2]) * inv;
+    if (ndv < 0) { /* the normal turned to the viewer */
       ndv = -ndv;
-      nz = -nz;
+      for (int i = 0; i < 3; i++) nw_[i] = -nw_[i];
     }
-    const double ndl = nz > 0 ? nz : 0;
+    const double ndl = nw_[2] > 0 ? nw_[2] : 0; /* light towards world +z */
     const double shade = 0.1 + 0.6 * ndv + 0.3 * ndl;
+    if (!mat) {
+      for (int i = 0; i < 3; i++) {
+        const double x = b.rgb[i] * shade;
+        out_rgb[3 * k + i] = x < 1.0 ? x : 1.0;
+      }
+      continue;
+    }
+    const float* mi = mat->geom_matinfo + 6 * b.geom;
+    double tc[3] = {1, 1, 1};
+    if (b.prim && mat->geom_texid[b.geom] >= 0) {
+      /* the pixel's footprint on the surface: one pixel's step of the ray slope (2 tan(fovy/2) / H)
+         at camera depth t, over the cosine to the normal */
+      const double foot = b.t * (2.0 * tanh_ / H) / (ndv > 1e-3 ? ndv : 1e-3);
+      orc_texture(mat, mat->geom_texid[b.geom], b.prim, mi, b.pl, foot, tc);
+    }
+    double sp = 0;
+    if (ndl > 0 && mi[0] > 0) { /* Blinn-Phong: half vector of the light and the viewer */
+      const double hv[3] = {-dw[0] * inv, -dw[1] * inv, 1.0 - dw[2] * inv};
+      const double hn = sqrt(dot3(hv, hv));
+      double nh = dot3(nw_, hv) / hn;
+      nh = nh > 0 ? nh : 0;
+      sp = mi[0] * 0.3 * pow(nh, 128.0 * mi[1]);
+    }
     for (int i = 0; i < 3; i++) {
-      const double x = b.rgb[i] * shade;
+      const double x = b.rgb[i] * tc[i] * (shade + mi[5]) + sp;
       out_rgb[3 * k + i] = x < 1.0 ? x : 1.0;
     }
   }

@@ -132,7 +132,8 @@ class SceneTables(ctypes.Structure):
 
     _fields_ = [("prim_i32", _c_p), ("prim_f32", _c_p), ("nprim", ctypes.c_int32), ("ntri", ctypes.c_int32),
                 ("nmesh", ctypes.c_int32), ("mesh_tri", _c_p), ("mesh_body", _c_p), ("mesh_rad", _c_p), ("vis", _c_p),
-                ("tflag", _c_p)]
+                ("tflag", _c_p), ("geom_texid", _c_p), ("geom_matinfo", _c_p), ("tex_rgba", _c_p), ("tex_desc", _c_p),
+                ("tex_level_adr", _c_p), ("ntex", ctypes.c_int32), ("sky_rgb", ctypes.c_float * 6)]
 
 
 class EnvBuffers(ctypes.Structure):
@@ -142,6 +143,8 @@ class EnvBuffers(ctypes.Structure):
                                     "gxpos", "gxmat", "sensordata", "stats", "workspace")]
 
 # numpy mirror of rmbx_sched_t (include/rmbx.h)
+TEX_LEVELS = 16  # include/rmbx.h RMBX_TEX_LEVELS
+
 SCHED_DTYPE = np.dtype(
     [
         ("phase", np.int32),

@@ -55,7 +55,11 @@ def _headers_digest():
 # per-source extra flags: the GEMM's split runs beside the MFMAs, where the packed f32 ops the SLP
 # vectorizer forms (v_pk_add_f32 / v_pk_mul_f32) cost more than the scalar pairs they replace
 # (MI355X_MICROARCH.md, "price of one filler beside MFMAs")
-FILE_FLAGS = {"rmbx_gemm.hip": ["-fno-slp-vectorize"]}
+FILE_FLAGS = {"rmbx_gemm.hip": ["-fno-slp-vectorize"],
+              # the renderer's ray-cast kernel at 6 waves per SIMD (80 registers): with the textured
+              # shading, 13.7 vs 14.3 ms per 1024-env front-camera call at 8 (64 registers, spills)
+              # and 14.1 at 5 (profiles/r6_render_waves_ab.log)
+              "rmbx_render.hip": ["-DRMBX_RENDER_MINW=6"]}
 
 
 def _compile(src, hdr_digest, verbose):

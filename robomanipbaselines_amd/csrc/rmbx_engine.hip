@@ -803,35 +803,37 @@ constexpr double BOX_INSIDE_TOL = 1e-9;  // m
 
 __device__ int col_box_box(const double* ca, const double* Ra, const double* ha, const double* cb,
                            const double* Rb, const double* hb, double margin, Contact* out) {
-  double axes[15][3];
-  for (int k = 0; k < 3; k++) {
-    axes[k][0] = Ra[k];
-    axes[k][1] = Ra[3 + k];
-    axes[k][2] = Ra[6 + k];
-    axes[3 + k][0] = Rb[k];
-    axes[3 + k][1] = Rb[3 + k];
-    axes[3 + k][2] = Rb[6 + k];
-  }
-  int na = 6;
-  for (int i = 0; i < 3; i++)
-    for (int j = 0; j < 3; j++) {
-      double c[3];
-      cross3(axes[i], axes[3 + j], c);
-      const double l = norm3(c);
-      if (l < 1e-6) {
-        axes[na][0] = axes[na][1] = axes[na][2] = 0;
-      } else {
-        axes[na][0] = c[0] / l;
-        axes[na][1] = c[1] / l;
-        axes[na][2] = c[2] / l;
-      }
-      na++;
+  // the 15 separating-axis candidates, each formed when it is needed (a [15][3] table here, with
+  // the 16-contact table below, was most of the front kernel's 1,920 B of private scratch per
+  // lane): A's and B's face axes, then the normalised edge cross products (zero when parallel)
+  auto axis = [&](int k, double* a) {
+    if (k < 6) {
+      const double* R = k < 3 ? Ra : Rb;
+      const int c = k < 3 ? k : k - 3;
+      a[0] = R[c];
+      a[1] = R[3 + c];
+      a[2] = R[6 + c];
+      return;
     }
+    const int i = (k - 6) / 3, j = (k - 6) - 3 * i;
+    const double ai[3] = {Ra[i], Ra[3 + i], Ra[6 + i]}, bj[3] = {Rb[j], Rb[3 + j], Rb[6 + j]};
+    double c[3];
+    cross3(ai, bj, c);
+    const double l = norm3(c);
+    if (l < 1e-6) {
+      a[0] = a[1] = a[2] = 0;
+    } else {
+      a[0] = c[0] / l;
+      a[1] = c[1] / l;
+      a[2] = c[2] / l;
+    }
+  };
   const double dc[3] = {cb[0] - ca[0], cb[1] - ca[1], cb[2] - ca[2]};
   double best = -1e300;
   int bk = -1;
   for (int k = 0; k < 15; k++) {
-    const double* a = axes[k];
+    double a[3];
+    axis(k, a);
     if (a[0] == 0 && a[1] == 0 && a[2] == 0) continue;
     double ra = 0, rb = 0;
     for (int i = 0; i < 3; i++) {
@@ -850,13 +852,17 @@ __device__ int col_box_box(const double* ca, const double* Ra, const double* ha,
     }
   }
   if (bk < 0) return 0; /* non-finite geometry (a diverged env): no axis scored */
-  double n[3] = {axes[bk][0], axes[bk][1], axes[bk][2]};
+  double n[3];
+  axis(bk, n);
   if (dot3(n, dc) < 0) {
     n[0] = -n[0];
     n[1] = -n[1];
     n[2] = -n[2];
   }
-  Contact cand[16];
+  // contact candidates: each vertex of one box inside the other, kept as (depth, side << 3 | vertex);
+  // the four deepest are rebuilt from their vertex by the same arithmetic below
+  double cdist[16];
+  uint8_t ccode[16];
   int nc = 0;
   for (int side = 0; side < 2; side++) {
     const double* c = side == 0 ? cb : ca;
@@ -883,16 +889,12 @@ __device__ int col_box_box(const double* ca, const double* Ra, const double* ha,
         const double u[3] = {Ro[i], Ro[3 + i], Ro[6 + i]};
         sup += ho[i] * fabs(dot3(n, u));
       }
-      const double sgn = side == 0 ? 1.0 : -1.0;
       const double dist = side == 0 ? (dot3(dl, n) - sup) : (-dot3(dl, n) - sup);
       if (dist >= margin) continue;
       if (nc < 16) {
-        Contact* k = cand + nc++;
-        k->dist = dist;
-        for (int i = 0; i < 3; i++) {
-          k->n[i] = n[i];
-          k->pos[i] = x[i] - sgn * n[i] * (0.5 * dist);
-        }
+        cdist[nc] = dist;
+        ccode[nc] = (uint8_t)(side << 3 | v);
+        ++nc;
       }
     }
   }
@@ -952,66 +954,104 @@ __device__ int col_box_box(const double* ca, const double* Ra, const double* ha,
     out[0].dist = dist;
     return 1;
   }
+  // the exchange sort by quantised depth (contact_deeper) of the oracle, on (depth, code) pairs
   for (int i = 0; i < nc; i++)
     for (int j = i + 1; j < nc; j++)
-      if (contact_deeper(&cand[j], &cand[i])) {
-        const Contact t = cand[i];
-        cand[i] = cand[j];
-        cand[j] = t;
+      if (floor(cdist[j] * 1e9) < floor(cdist[i] * 1e9)) {
+        const double t = cdist[i];
+        cdist[i] = cdist[j];
+        cdist[j] = t;
+        const uint8_t tc = ccode[i];
+        ccode[i] = ccode[j];
+        ccode[j] = tc;
       }
   const int k = nc < 4 ? nc : 4;
-  for (int i = 0; i < k; i++) out[i] = cand[i];
+  for (int q = 0; q < k; q++) {
+    const int side = ccode[q] >> 3, v = ccode[q] & 7;
+    const double* c = side == 0 ? cb : ca;
+    const double* R = side == 0 ? Rb : Ra;
+    const double* h = side == 0 ? hb : ha;
+    const double l[3] = {(v & 1) ? h[0] : -h[0], (v & 2) ? h[1] : -h[1], (v & 4) ? h[2] : -h[2]};
+    double w[3];
+    matvec3(R, l, w);
+    const double x[3] = {c[0] + w[0], c[1] + w[1], c[2] + w[2]};
+    const double sgn = side == 0 ? 1.0 : -1.0;
+    const double dist = cdist[q];
+    out[q].dist = dist;
+    for (int i = 0; i < 3; i++) {
+      out[q].n[i] = n[i];
+      out[q].pos[i] = x[i] - sgn * n[i] * (0.5 * dist);
+    }
+  }
   return k;
 }
 
 __device__ int col_plane(const double* cp, const double* Rp, int tb, const double* cb,
                          const double* Rb, const double* sb, double margin, Contact* out) {
   const double n[3] = {Rp[2], Rp[5], Rp[8]};
-  double pts[8][3];
   double rad = 0;
   int np = 0;
   if (tb == RMBX_GEOM_SPHERE) {
-    pts[0][0] = cb[0];
-    pts[0][1] = cb[1];
-    pts[0][2] = cb[2];
     np = 1;
     rad = sb[0];
   } else if (tb == RMBX_GEOM_CAPSULE) {
-    capsule_ends(cb, Rb, sb[1], pts[0], pts[1]);
     np = 2;
     rad = sb[0];
   } else if (tb == RMBX_GEOM_BOX) {
-    for (int v = 0; v < 8; v++) {
-      const double l[3] = {(v & 1) ? sb[0] : -sb[0], (v & 2) ? sb[1] : -sb[1],
-                           (v & 4) ? sb[2] : -sb[2]};
-      double w[3];
-      matvec3(Rb, l, w);
-      for (int i = 0; i < 3; i++) pts[v][i] = cb[i] + w[i];
-    }
     np = 8;
   }
-  Contact cand[8];
+  // point k of the geom (the sphere's centre, the capsule's segment ends, the box's vertices),
+  // formed where it is needed instead of held in a table (private scratch)
+  auto point = [&](int k, double* p) {
+    if (tb == RMBX_GEOM_SPHERE) {
+      p[0] = cb[0];
+      p[1] = cb[1];
+      p[2] = cb[2];
+    } else if (tb == RMBX_GEOM_CAPSULE) {
+      double e0[3], e1[3];
+      capsule_ends(cb, Rb, sb[1], e0, e1);
+      for (int i = 0; i < 3; i++) p[i] = k == 0 ? e0[i] : e1[i];
+    } else {
+      const double l[3] = {(k & 1) ? sb[0] : -sb[0], (k & 2) ? sb[1] : -sb[1], (k & 4) ? sb[2] : -sb[2]};
+      double w[3];
+      matvec3(Rb, l, w);
+      for (int i = 0; i < 3; i++) p[i] = cb[i] + w[i];
+    }
+  };
+  double cdist[8];
+  uint8_t ccode[8];
   int nc = 0;
   for (int k = 0; k < np; k++) {
-    const double v[3] = {pts[k][0] - cp[0], pts[k][1] - cp[1], pts[k][2] - cp[2]};
+    double p[3];
+    point(k, p);
+    const double v[3] = {p[0] - cp[0], p[1] - cp[1], p[2] - cp[2]};
     const double dist = dot3(v, n) - rad;
     if (dist >= margin) continue;
-    Contact* c = cand + nc++;
-    c->dist = dist;
-    for (int i = 0; i < 3; i++) {
-      c->n[i] = n[i];
-      c->pos[i] = pts[k][i] - n[i] * (rad + 0.5 * dist);
-    }
+    cdist[nc] = dist;
+    ccode[nc] = (uint8_t)k;
+    ++nc;
   }
   for (int i = 0; i < nc; i++)
     for (int j = i + 1; j < nc; j++)
-      if (contact_deeper(&cand[j], &cand[i])) {
-        const Contact t = cand[i];
-        cand[i] = cand[j];
-        cand[j] = t;
+      if (floor(cdist[j] * 1e9) < floor(cdist[i] * 1e9)) {  // contact_deeper
+        const double t = cdist[i];
+        cdist[i] = cdist[j];
+        cdist[j] = t;
+        const uint8_t tc = ccode[i];
+        ccode[i] = ccode[j];
+        ccode[j] = tc;
       }
   const int k = nc < 4 ? nc : 4;
-  for (int i = 0; i < k; i++) out[i] = cand[i];
+  for (int q = 0; q < k; q++) {
+    double p[3];
+    point(ccode[q], p);
+    const double dist = cdist[q];
+    out[q].dist = dist;
+    for (int i = 0; i < 3; i++) {
+      out[q].n[i] = n[i];
+      out[q].pos[i] = p[i] - n[i] * (rad + 0.5 * dist);
+    }
+  }
   return k;
 }
 
@@ -1925,7 +1965,7 @@ __device__ double impedance(const double* solimp, double x) {
 }
 
 // stores b in efc_tmp, k*imp*pos in efc_D, R in efc_R (finalised after J is complete)
-__device__ void set_row(Env& e, int r, int type, double pos, double diag, const double* solref,
+__device__ __forceinline__ void set_row(Env& e, int r, int type, double pos, double diag, const double* solref,
                         const double* solimp, double impx) {
   const double dmax = fmin(fmax(solimp[1], 0.0001), 0.9999);
   double tc = solref[0];
@@ -3555,9 +3595,11 @@ __device__ __forceinline__ void make_env(const KArgs& args, int env, Env& e) {
 
 // front half of mj_step: kinematics -> constraint rows (one wavefront per env)
 // RUNS: the two-level broadphase (a separate instantiation, so models without pair runs keep the
-// one-level kernel's register allocation)
+// one-level kernel's register allocation).  flatten: every stage is inlined -- a stage left out of
+// line takes the Env (and through it the 1.5 KB kernel-argument block) by address, which hipcc then
+// copies to private memory per lane (the pair-run instance did: 2.4 KB of scratch per lane)
 template <bool RUNS>
-__global__ void __launch_bounds__(64) front_kernel(KArgs args) {
+__global__ void __launch_bounds__(64) __attribute__((flatten)) front_kernel(KArgs args) {
   extern __shared__ __attribute__((aligned(16))) double front_smem[];
   const int env = blockIdx.x;
   const int lane = threadIdx.x;

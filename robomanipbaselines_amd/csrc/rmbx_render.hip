@@ -17,7 +17,9 @@
 //      starts from its pixel's mesh hit and casts its ray against the surviving primitives, stopping
 //      at the first whose bound lies behind its nearest hit.
 // Shading: ambient + headlight + one directional light (the scene's <light> and MuJoCo's default
-// headlight), material colour only, flat-shaded triangles (textures are not sampled).  Outputs are
+// headlight), material colour times the material's texture (primitives: 2d / cube textures sampled
+// bilinearly at the hit's local coordinates) plus the directional light's Blinn-Phong specular term,
+// flat-shaded triangles; the gradient skybox behind (include/rmbx.h rmbx_scene_tables).  Outputs are
 // written once per pixel: u8 HWC RGB, f32 linear depth, the hit geom id, and/or the policy input
 // tensor (CHW, ImageNet-normalised, bf16 or f32, or the space-to-depth forms) fused so the policy
 // never re-reads the u8 image.
@@ -227,8 +229,160 @@ struct RenderArgs {
   int tiles_x, tiles_y;
   int groups;  // blocks per env (each renders a contiguous range of tiles)
   int dbg;     // diagnostic (RMBX_RENDER_DBG; 0 in production): 1 no ray loop, 2 no stores, 4 test counts, 8 sphere
-               // bounds only; visibility-pass timing probes: 16 frames only, 32 + set-up, 64 + ray tests, no writes
+               // bounds only; visibility-pass timing probes: 16 frames only, 32 + set-up, 64 + ray tests, no writes;
+               // materials: 128 textures at the base level only, 256 no texture sampling, 512 no footprint
+  // materials (NULL geom_matinfo: the flat round-5 shading); include/rmbx.h rmbx_scene_tables
+  const int32_t* geom_texid;
+  const float* geom_matinfo;
+  const uint32_t* tex_rgba;
+  const int4* tex_desc;
+  const int32_t* tex_level_adr;
+  float sky[6];
 };
+
+// one texel (RGBA8 word, R in the low byte) as floats in [0, 1]
+__device__ __forceinline__ void texel(const uint32_t* t, int idx, float w, float* c) {
+  const uint32_t v = __ldg(t + idx);
+  c[0] += w * (float)(v & 255u);
+  c[1] += w * (float)((v >> 8) & 255u);
+  c[2] += w * (float)((v >> 16) & 255u);
+}
+
+// bilinear sample at continuous texel coordinates (fx, fy) (texel centres at integers): wrap
+// (2d textures: GL_REPEAT) or clamp at the edges (cube faces: GL_CLAMP_TO_EDGE).  The wrap is done
+// on the integer-valued floats (exact below 2^24; an integer modulo costs ~40 instructions)
+__device__ __forceinline__ void tex_bilinear(const uint32_t* t, int H, int W, float fx, float fy, bool wrap, float* c) {
+  const float x0f = floorf(fx), y0f = floorf(fy);
+  const float ax = fx - x0f, ay = fy - y0f;
+  const float Wf = (float)W, Hf = (float)H;
+  int x0, y0, x1, y1;
+  if (wrap) {
+    const float xw = x0f - Wf * floorf(x0f * __builtin_amdgcn_rcpf(Wf));
+    const float yw = y0f - Hf * floorf(y0f * __builtin_amdgcn_rcpf(Hf));
+    // (the reciprocal's rounding can leave xw one period off: fold it back)
+    x0 = (int)xw;
+    y0 = (int)yw;
+    x0 += x0 < 0 ? W : (x0 >= W ? -W : 0);
+    y0 += y0 < 0 ? H : (y0 >= H ? -H : 0);
+    x1 = x0 + 1 == W ? 0 : x0 + 1;
+    y1 = y0 + 1 == H ? 0 : y0 + 1;
+  } else {
+    x0 = (int)fminf(fmaxf(x0f, 0.f), Wf - 1.f);
+    y0 = (int)fminf(fmaxf(y0f, 0.f), Hf - 1.f);
+    x1 = (int)fminf(fmaxf(x0f + 1.f, 0.f), Wf - 1.f);
+    y1 = (int)fminf(fmaxf(y0f + 1.f, 0.f), Hf - 1.f);
+  }
+  c[0] = c[1] = c[2] = 0.f;
+  if (x1 == x0 + 1) {  // the two texels of a row are adjacent words: one 8-byte load per row
+    uint2 r0, r1;
+    __builtin_memcpy(&r0, t + y0 * W + x0, 8);
+    __builtin_memcpy(&r1, t + y1 * W + x0, 8);
+    const float w00 = (1.f - ax) * (1.f - ay), w01 = ax * (1.f - ay), w10 = (1.f - ax) * ay, w11 = ax * ay;
+    const uint32_t v[4] = {r0.x, r0.y, r1.x, r1.y};
+    const float w[4] = {w00, w01, w10, w11};
+#pragma unroll
+    for (int k = 0; k < 4; k++) {
+      c[0] += w[k] * (float)(v[k] & 255u);
+      c[1] += w[k] * (float)((v[k] >> 8) & 255u);
+      c[2] += w[k] * (float)((v[k] >> 16) & 255u);
+    }
+  } else {
+    texel(t, y0 * W + x0, (1.f - ax) * (1.f - ay), c);
+    texel(t, y0 * W + x1, ax * (1.f - ay), c);
+    texel(t, y1 * W + x0, (1.f - ax) * ay, c);
+    texel(t, y1 * W + x1, ax * ay, c);
+  }
+  for (int i = 0; i < 3; i++) c[i] *= (1.0f / 255.0f);
+}
+
+// texture coordinates (in units of the base level's texels: fx = u W, fy = v H, before the -0.5
+// texel-centre shift) of local point q on a primitive of `type` / size s, and the texture's
+// density there (base texels per metre along the surface): 2d from (x, y); cube maps on the face of
+// the major axis, OpenGL's face orientation (include/rmbx.h rmbx_scene_tables)
+__device__ __forceinline__ void tex_coords(int ttype, int H, int W, int type, const float* s, const float* mi,
+                                           const float* pl, float& fx, float& fy, float& dens) {
+  const bool uni = mi[4] != 0.f;
+  if (ttype == 0) {  // 2d: (x, y), texrepeat over the geom's extent, or per metre
+    // the geom's half extents in its local x / y (round geoms: the radius)
+    const float sx = s[0];
+    const float sy = type == RMBX_GEOM_BOX || type == RMBX_GEOM_PLANE ? s[1] : s[0];
+    float u = pl[0] * mi[2], v = pl[1] * mi[3];
+    float kx = mi[2], ky = mi[3];  // periods per metre
+    if (!uni && sx > 0.f && sy > 0.f) {
+      kx = mi[2] / (2.f * sx);
+      ky = mi[3] / (2.f * sy);
+      u = mi[2] * (pl[0] / (2.f * sx) + 0.5f);
+      v = mi[3] * (pl[1] / (2.f * sy) + 0.5f);
+    }
+    fx = u * W;
+    fy = v * H;
+    dens = fmaxf(kx * W, ky * H);
+    return;
+  }
+  float q[3] = {pl[0], pl[1], pl[2]};
+  float hmin = 1.f;
+  if (uni) {  // the unit object: local point over the half extents
+    float h[3] = {s[0], s[0], s[0]};
+    if (type == RMBX_GEOM_BOX) { h[1] = s[1]; h[2] = s[2]; }
+    else if (type == RMBX_GEOM_CAPSULE) h[2] = s[1] + s[0];
+    else if (type == RMBX_GEOM_CYLINDER) h[2] = s[1];
+    else if (type == RMBX_GEOM_PLANE) { h[1] = s[1]; h[2] = 1.f; }
+    for (int i = 0; i < 3; i++) q[i] = h[i] > 0.f ? q[i] / h[i] : q[i];
+    hmin = fminf(fminf(h[0] > 0.f ? h[0] : 1.f, h[1] > 0.f ? h[1] : 1.f), h[2] > 0.f ? h[2] : 1.f);
+  }
+  const float x = fabsf(q[0]), y = fabsf(q[1]), z = fabsf(q[2]);
+  float sc, tc, ma;
+  if (x >= y && x >= z) {
+    ma = x; sc = q[0] > 0.f ? -q[2] : q[2]; tc = -q[1];
+  } else if (y >= z) {
+    ma = y; sc = q[0]; tc = q[1] > 0.f ? q[2] : -q[2];
+  } else {
+    ma = z; sc = q[2] > 0.f ? q[0] : -q[0]; tc = -q[1];
+  }
+  ma = fmaxf(ma, 1e-30f);
+  const float im = 1.0f / ma;
+  fx = 0.5f * (sc * im + 1.f) * W;
+  fy = 0.5f * (tc * im + 1.f) * H;
+  dens = 0.5f * (float)max(W, H) * im / hmin;
+}
+
+// the texture colour of a primitive at local hit point pl: OpenGL's GL_LINEAR_MIPMAP_LINEAR
+// (trilinear) with an isotropic footprint: a pixel spans foot = t pix / max(n.v, 1e-3) metres of
+// the surface at camera depth t (pix: one pixel's step of the ray slope), the level of detail is
+// log2(foot x the texture's density there); bilinear in the two nearest levels of the box-filtered
+// mip pyramid
+__device__ void sample_texture(const RenderArgs& a, int tex, int type, const float* s, const float* mi,
+                               const float* pl, float foot, float* c) {
+  const int4 td = a.tex_desc[tex];  // (type, H, W, first texel)
+  const uint32_t* t = a.tex_rgba + td.w;
+  const int H = td.y, W = td.z;
+  float fx, fy, dens;
+  tex_coords(td.x, H, W, type, s, mi, pl, fx, fy, dens);
+  const float rho = (a.dbg & 512) ? 0.f : foot * dens;  // (timing probe 512: no footprint)
+  // levels down to 1 x 1: 32 - clz(max(H, W)); level l's first texel from the host table
+  const int levels = 32 - __builtin_clz((unsigned)max(H, W));
+  float lod = fminf(fmaxf(__log2f(fmaxf(rho, 1e-30f)), 0.f), (float)(levels - 1));
+  if (a.dbg & 128) lod = 0.f;  // (timing probe: the base level only)
+  const int l0 = (int)lod;
+  const float fr = lod - (float)l0;
+  const bool wrap = td.x == 0;
+  const int* ladr = a.tex_level_adr + RMBX_TEX_LEVELS * tex;
+  const float iW = 1.0f / (float)W, iH = 1.0f / (float)H;
+  float c0[3] = {0.f, 0.f, 0.f}, c1[3] = {0.f, 0.f, 0.f};
+  {
+    const int Hl = max(H >> l0, 1), Wl = max(W >> l0, 1);
+    tex_bilinear(t + ladr[l0], Hl, Wl, fx * (Wl * iW) - 0.5f, fy * (Hl * iH) - 0.5f, wrap, c0);
+  }
+  if (fr > 0.f && l0 + 1 < levels) {
+    const int Hl = max(H >> (l0 + 1), 1), Wl = max(W >> (l0 + 1), 1);
+    tex_bilinear(t + ladr[l0 + 1], Hl, Wl, fx * (Wl * iW) - 0.5f, fy * (Hl * iH) - 0.5f, wrap, c1);
+  } else {
+    c1[0] = c0[0];
+    c1[1] = c0[1];
+    c1[2] = c0[2];
+  }
+  for (int i = 0; i < 3; i++) c[i] = c0[i] + fr * (c1[i] - c0[i]);
+}
 
 // camera pose of env `env` in world: R (columns = camera axes), p
 __device__ __forceinline__ void camera_frame(const RenderArgs& a, int env, CamFrame& cf) {
@@ -749,7 +903,8 @@ __global__ void __launch_bounds__(256, RMBX_RENDER_MINW) render_kernel(RenderArg
       for (int i = 0; i < 3; i++) bn[i] = P.R[3 * i] * nl[0] + P.R[3 * i + 1] * nl[1] + P.R[3 * i + 2] * nl[2];
     }
   }
-  if (bgeom == -2) {  // a primitive won: its geom and material colour
+  const bool prim_won = bgeom == -2;
+  if (prim_won) {  // a primitive won: its geom and material colour
     bgeom = a.prim_i32[4 * bp];
     brgb[0] = prims[bp].rgb[0];
     brgb[1] = prims[bp].rgb[1];
@@ -757,13 +912,20 @@ __global__ void __launch_bounds__(256, RMBX_RENDER_MINW) render_kernel(RenderArg
   }
   float col[3];
   float depth = a.cam.zfar;
+  const float inv = rsqrtf(dot3f(d, d));
+  const float vd[3] = {d[0] * inv, d[1] * inv, d[2] * inv};
   if (bgeom < 0) {
-    col[0] = 0.9f;  // skybox gradient colour of env_ur5e_common.xml
-    col[1] = 1.0f;
-    col[2] = 1.0f;
+    if (a.geom_matinfo) {
+      // the gradient skybox: rgb2 (down) to rgb1 (up) by the ray's world z
+      const float wz = cf.R[6] * vd[0] + cf.R[7] * vd[1] + cf.R[8] * vd[2];
+      const float f = 0.5f * (1.f + wz);
+      for (int i = 0; i < 3; i++) col[i] = a.sky[3 + i] + f * (a.sky[i] - a.sky[3 + i]);
+    } else {
+      col[0] = 0.9f;  // skybox gradient colour of env_ur5e_common.xml
+      col[1] = 1.0f;
+      col[2] = 1.0f;
+    }
   } else {
-    const float inv = rsqrtf(dot3f(d, d));
-    const float vd[3] = {d[0] * inv, d[1] * inv, d[2] * inv};
     float ndv = -(bn[0] * vd[0] + bn[1] * vd[1] + bn[2] * vd[2]);
     if (ndv < 0) {
       ndv = -ndv;
@@ -771,12 +933,39 @@ __global__ void __launch_bounds__(256, RMBX_RENDER_MINW) render_kernel(RenderArg
       bn[1] = -bn[1];
       bn[2] = -bn[2];
     }
-    // directional light pointing down (world -z) expressed in camera frame
-    const float Ld[3] = {-cf.R[6], -cf.R[7], -cf.R[8]};
-    float ndl = -(bn[0] * Ld[0] + bn[1] * Ld[1] + bn[2] * Ld[2]);
+    // directional light pointing down (world -z): L = world +z in the camera frame
+    const float L[3] = {cf.R[6], cf.R[7], cf.R[8]};
+    float ndl = bn[0] * L[0] + bn[1] * L[1] + bn[2] * L[2];
     ndl = ndl > 0 ? ndl : 0;
     const float shade = 0.1f + 0.6f * ndv + 0.3f * ndl;
-    for (int i = 0; i < 3; i++) col[i] = fminf(brgb[i] * shade, 1.0f);
+    if (a.geom_matinfo) {
+      const float* mi = a.geom_matinfo + 6 * bgeom;
+      float tc[3] = {1.f, 1.f, 1.f};
+      if (prim_won) {
+        const int tex = (a.dbg & 256) ? -1 : a.geom_texid[bgeom];  // (timing probe 256: no sampling)
+        if (tex >= 0) {
+          const PrimCam& P = prims[bp];
+          float o_l[3], d_l[3];
+          to_local(P, d, o_l, d_l);
+          const float pl[3] = {o_l[0] + best * d_l[0], o_l[1] + best * d_l[1], o_l[2] + best * d_l[2]};
+          // the pixel's footprint on the surface: one pixel's step of the ray slope (2 tan(fovy/2)
+          // / H, square pixels) at camera depth t, over the cosine to the normal
+          const float foot = best * (2.0f * tanh_ / H) / fmaxf(ndv, 1e-3f);
+          sample_texture(a, tex, P.type, P.s, mi, pl, foot, tc);
+        }
+      }
+      float sp = 0.f;
+      if (ndl > 0.f && mi[0] > 0.f) {
+        // Blinn-Phong half vector of the light and the viewer (-vd)
+        float h[3] = {L[0] - vd[0], L[1] - vd[1], L[2] - vd[2]};
+        const float hi = rsqrtf(dot3f(h, h));
+        const float nh = fmaxf((bn[0] * h[0] + bn[1] * h[1] + bn[2] * h[2]) * hi, 0.f);
+        sp = mi[0] * 0.3f * powf(nh, 128.f * mi[1]);
+      }
+      for (int i = 0; i < 3; i++) col[i] = fminf(brgb[i] * tc[i] * (shade + mi[5]) + sp, 1.0f);
+    } else {
+      for (int i = 0; i < 3; i++) col[i] = fminf(brgb[i] * shade, 1.0f);
+    }
     depth = best;  // d has unit -z component: t is the camera-z distance
   }
   const bool do_store = !(a.dbg & 2) || col[0] == 12345.f;  // (diagnostic: keep the shading live)
@@ -850,6 +1039,9 @@ extern "C" int rmbx_render_scene(const rmbx_camera* cam, const rmbx_scene_tables
                  "policy_dtype must be 0 (f32), 1 (bf16), 2 (bf16 s2d), 3 (f32 s2d) or 4 (u8 s2d)");
   RMBX_CHECK_ARG(policy_dtype < 2 || (cam->width % 2 == 0 && cam->height % 2 == 0),
                  "space-to-depth policy output needs an even image size");
+  RMBX_CHECK_ARG(!scene->geom_matinfo ||
+                     (scene->geom_texid && (scene->ntex == 0 || (scene->tex_rgba && scene->tex_desc && scene->tex_level_adr))),
+                 "materials need geom_texid, and tex_rgba / tex_desc / tex_level_adr when ntex > 0");
   const bool meshes = scene->ntri > 0;
   RMBX_CHECK_ARG(scene->ntri >= 0 && scene->ntri < (1 << 26) && scene->nmesh >= 0 && scene->nmesh <= MAX_MESH,
                  "bad mesh sizes (ntri=%d, nmesh=%d, at most %d mesh bodies)", scene->ntri, scene->nmesh, MAX_MESH);
@@ -883,6 +1075,12 @@ extern "C" int rmbx_render_scene(const rmbx_camera* cam, const rmbx_scene_tables
   a.policy_dtype = policy_dtype;
   a.active = active;
   a.n_env = n_env;
+  a.geom_matinfo = scene->geom_matinfo;
+  a.geom_texid = scene->geom_texid;
+  a.tex_rgba = scene->tex_rgba;
+  a.tex_desc = reinterpret_cast<const int4*>(scene->tex_desc);
+  a.tex_level_adr = scene->tex_level_adr;
+  for (int i = 0; i < 6; i++) a.sky[i] = scene->sky_rgb[i];
   a.tiles_x = (cam->width + RENDER_TILE - 1) / RENDER_TILE;
   a.tiles_y = (cam->height + RENDER_TILE - 1) / RENDER_TILE;
   a.groups = 16;

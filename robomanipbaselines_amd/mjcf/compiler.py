@@ -389,6 +389,7 @@ def compile_mjcf(path, missing_mesh_box=(0.045, 0.0125, 0.0125), convex_meshes=F
 
     # ---- compiler / option / statistic / visual
     meshdir = main_dir
+    texturedir = main_dir
     autolimits = True
     angle_deg = True
     timestep, gravity = 0.002, np.array([0, 0, -9.81])
@@ -397,6 +398,8 @@ def compile_mjcf(path, missing_mesh_box=(0.045, 0.0125, 0.0125), convex_meshes=F
     for c in root.iter("compiler"):
         if "meshdir" in c.attrib:
             meshdir = os.path.join(main_dir, c.attrib["meshdir"])
+        if "texturedir" in c.attrib:
+            texturedir = os.path.join(main_dir, c.attrib["texturedir"])
         if "autolimits" in c.attrib:
             autolimits = c.attrib["autolimits"] == "true"
         if "angle" in c.attrib:
@@ -438,6 +441,9 @@ def compile_mjcf(path, missing_mesh_box=(0.045, 0.0125, 0.0125), convex_meshes=F
     meshes = {}
     mesh_scales = {}
     materials = {}
+    material_props = {}  # name -> texture, texrepeat, texuniform, specular, shininess, emission
+    textures = {}  # name -> type, file (or builtin), rgb1, rgb2
+    skybox = None
     for asset in root.findall("asset"):
         for m in asset:
             a = attrs_of(m, m.attrib.get("class", "main"))
@@ -447,6 +453,22 @@ def compile_mjcf(path, missing_mesh_box=(0.045, 0.0125, 0.0125), convex_meshes=F
                 mesh_scales[name] = _floats(a.get("scale", "1 1 1"))
             elif m.tag == "material":
                 materials[m.attrib["name"]] = _floats(a.get("rgba", "1 1 1 1"))
+                material_props[m.attrib["name"]] = dict(
+                    texture=a.get("texture"), texrepeat=(_floats(a.get("texrepeat", "1 1")) + [1.0])[:2],
+                    texuniform=a.get("texuniform", "false") == "true", specular=float(a.get("specular", 0.5)),
+                    shininess=float(a.get("shininess", 0.5)), emission=float(a.get("emission", 0.0)))
+            elif m.tag == "texture":
+                t = dict(type=a.get("type", "cube"), builtin=a.get("builtin", "none"),
+                         rgb1=_floats(a.get("rgb1", "0.8 0.8 0.8")), rgb2=_floats(a.get("rgb2", "0.5 0.5 0.5")),
+                         file=None)
+                if "file" in a:
+                    t["file"] = a["file"] if os.path.isabs(a["file"]) else os.path.join(texturedir, a["file"])
+                if t["type"] == "skybox":
+                    skybox = t
+                else:
+                    # MuJoCo names an unnamed file texture after its file
+                    name = a.get("name", os.path.splitext(os.path.basename(a.get("file", "")))[0])
+                    textures[name] = t
 
     def frame_quat(a):
         if "quat" in a:
@@ -532,7 +554,7 @@ def compile_mjcf(path, missing_mesh_box=(0.045, 0.0125, 0.0125), convex_meshes=F
                     solref=_floats(a.get("solref", "0.02 1")), solimp=(_floats(a.get("solimp", "0.9 0.95 0.001 0.5 2")) + [0.5, 2.0])[:5],
                     solmix=float(a.get("solmix", 1.0)), margin=float(a.get("margin", 0)), gap=float(a.get("gap", 0)),
                     mass=float(a["mass"]) if "mass" in a else None, density=float(a.get("density", 1000.0)),
-                    group=int(a.get("group", 0)), rgba=np.array(rgba)))
+                    group=int(a.get("group", 0)), rgba=np.array(rgba), material=a.get("material")))
             elif ch.tag == "site":
                 a = attrs_of(ch, cc)
                 sites.append(dict(name=a.get("name", ""), body=bid, pos=np.array(_floats(a.get("pos", "0 0 0"))), quat=frame_quat(a)))
@@ -726,6 +748,7 @@ def compile_mjcf(path, missing_mesh_box=(0.045, 0.0125, 0.0125), convex_meshes=F
     M.dof_damping = np.array([joints[j]["damping"] for j in dof_jnt])
     M.qpos0 = qpos0
     M.geoms = geoms
+    M.textures, M.material_props, M.skybox = textures, material_props, skybox
     M.sites = sites
     M.cams = cams
 
@@ -979,3 +1002,71 @@ def _set_const(M):
                 rp[:3] = xmat[b1].T @ (xpos[b2] - xpos[b1])
                 rp[3:7] = mat2quat(xmat[b1].T @ xmat[b2])
             e["relpose"] = list(rp[:3]) + list(quat_normalize(rp[3:7]))
+
+
+# default material of a geom without one (mjsMaterial defaults, [ext] mujoco 3.1.6)
+DEFAULT_SPECULAR, DEFAULT_SHININESS = 0.5, 0.5
+TEX_2D, TEX_CUBE = 0, 1
+
+
+def visual_arrays(M):
+    """The renderer's material tables of a compiled model (csrc/rmbx_render.hip):
+
+    * geom_texid i32 [ngeom]: texture of the geom's material (-1: none)
+    * geom_matinfo f32 [ngeom, 6]: specular, shininess, texrepeat (2), texuniform, emission
+    * tex_type i32 [ntex] (0: 2d, 1: cube; a single image on all six faces), tex_size i32 [ntex, 2]
+      (height, width), tex_adr i32 [ntex] (first texel), tex_rgb u8 [texels, 3]: the texture files,
+      decoded (common/image_io.decode_png), rows in file order
+    * sky_rgb f64 [2, 3]: the builtin gradient skybox's rgb1 (up) / rgb2 (down); the default
+      background of MuJoCo when there is none is black
+
+    Only file textures and the gradient skybox are supported (the reference's scenes use nothing
+    else); a material whose texture file is missing from the checkout keeps its colour only."""
+    from ..common.image_io import decode_png
+
+    tex_ids, tex_type, tex_size, tex_adr, texels = {}, [], [], [], []
+    by_file = {}  # (file, type) -> texture index: one copy of an image several textures name
+    adr = 0
+    # textures the renderer samples: those of primitive geoms (a mesh's texture needs its UV
+    # coordinates, which the render meshes do not carry: textured meshes keep their colour)
+    used = {M.material_props[g["material"]]["texture"] for g in M.geoms
+            if g["type"] != GEOM_MESH and g.get("material") in M.material_props}
+    for name, t in M.textures.items():
+        if (name not in used or t["file"] is None or not os.path.exists(t["file"])
+                or t["type"] not in ("2d", "cube")):
+            continue
+        key = (os.path.realpath(t["file"]), t["type"])
+        if key in by_file:
+            tex_ids[name] = by_file[key]
+            continue
+        by_file[key] = len(tex_type)
+        with open(t["file"], "rb") as f:
+            img = decode_png(f.read())
+        if img.shape[2] in (1, 2):
+            img = np.repeat(img[..., :1], 3, axis=2)
+        img = np.ascontiguousarray(img[..., :3])
+        tex_ids[name] = len(tex_type)
+        tex_type.append(TEX_2D if t["type"] == "2d" else TEX_CUBE)
+        tex_size.append(img.shape[:2])
+        tex_adr.append(adr)
+        texels.append(img.reshape(-1, 3))
+        adr += img.shape[0] * img.shape[1]
+    ng = len(M.geoms)
+    texid = np.full(ng, -1, np.int32)
+    info = np.zeros((ng, 6), np.float32)
+    for g, geom in enumerate(M.geoms):
+        mp = M.material_props.get(geom.get("material"))
+        if mp is None:
+            info[g] = [DEFAULT_SPECULAR, DEFAULT_SHININESS, 1.0, 1.0, 0.0, 0.0]
+            continue
+        info[g] = [mp["specular"], mp["shininess"], mp["texrepeat"][0], mp["texrepeat"][1],
+                   1.0 if mp["texuniform"] else 0.0, mp["emission"]]
+        if mp["texture"] is not None and geom["type"] != GEOM_MESH:
+            texid[g] = tex_ids.get(mp["texture"], -1)
+    sky = np.zeros((2, 3))
+    if M.skybox is not None and M.skybox["builtin"] == "gradient":
+        sky[0], sky[1] = M.skybox["rgb1"], M.skybox["rgb2"]
+    return {"geom_texid": texid, "geom_matinfo": info,
+            "tex_type": np.array(tex_type, np.int32), "tex_size": np.array(tex_size, np.int32).reshape(-1, 2),
+            "tex_adr": np.array(tex_adr, np.int32),
+            "tex_rgb": np.concatenate(texels) if texels else np.zeros((0, 3), np.uint8), "sky_rgb": sky}

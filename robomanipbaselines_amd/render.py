@@ -5,8 +5,9 @@ PhysicsEngine.  The geoms MuJoCo draws by default (groups 0-2) are drawn: primit
 are (ray cast), visual mesh geoms as their triangles (scenes compiled with render meshes,
 mjcf/rmesh.py: vertex-clustered at 1 mm, grouped per body; rasterised into a per-pixel visibility
 buffer first), a mesh whose file is missing from the reference checkout as its bounding box;
-material colours, flat-shaded triangles, textures are not sampled (documented substitution: images
-are not pixel-identical to MuJoCo's OpenGL renderer).  Assets packed without
+material colours times the primitives' 2d / cube textures, the directional light's specular term,
+flat-shaded triangles, the gradient skybox (include/rmbx.h rmbx_scene_tables; documented
+substitution: images are not pixel-identical to MuJoCo's OpenGL renderer).  Assets packed without
 render meshes fall back to the round-3 form (visual meshes drawn through their body's collision
 primitives).
 """
@@ -79,6 +80,27 @@ def _build_prims_substitutes(arrays):
     return np.array(pi, np.int32), np.array(pf, np.float32)
 
 
+def mip_pyramid(img):
+    """Level 0 = img [H, W, 3] (integers), then box-filtered halvings down to 1 x 1: level l is
+    max(H >> l, 1) x max(W >> l, 1), texel (y, x) = (sum of the level above's rows 2y, 2y + 1 and
+    columns 2x, 2x + 1, each clamped to its last row / column, + 2) // 4 -- the levels OpenGL's
+    glGenerateMipmap box filter makes, in integers (include/rmbx.h rmbx_scene_tables)."""
+    img = np.asarray(img, np.uint32)
+    H, W = img.shape[:2]
+    out = [img]
+    l = 1
+    while (H >> l) > 0 or (W >> l) > 0:
+        prev = out[-1]
+        h, w = max(H >> l, 1), max(W >> l, 1)
+        ph, pw = prev.shape[:2]
+        r0, r1 = np.minimum(2 * np.arange(h), ph - 1), np.minimum(2 * np.arange(h) + 1, ph - 1)
+        c0, c1 = np.minimum(2 * np.arange(w), pw - 1), np.minimum(2 * np.arange(w) + 1, pw - 1)
+        acc = (prev[r0][:, c0] + prev[r0][:, c1] + prev[r1][:, c0] + prev[r1][:, c1] + 2) // 4
+        out.append(acc.astype(np.uint32))
+        l += 1
+    return out
+
+
 class Renderer:
     def __init__(self, arrays, device, width=640, height=480):
         self.arrays = arrays
@@ -101,6 +123,42 @@ class Renderer:
             sc.ntri, sc.nmesh = self.mesh_tri.shape[0], self.mesh_body.shape[0]
             sc.mesh_tri, sc.mesh_body, sc.mesh_rad = (self.mesh_tri.data_ptr(), self.mesh_body.data_ptr(),
                                                       self.mesh_rad.data_ptr())
+        # materials: texture, specular / shininess per geom, the texture images, the skybox
+        # (compiler.visual_arrays; assets compiled before round 6 keep the flat shading)
+        self.materials = "geom_matinfo" in arrays
+        if self.materials:
+            self.geom_texid = torch.tensor(arrays["geom_texid"], dtype=torch.int32, device=device)
+            self.geom_matinfo = torch.tensor(arrays["geom_matinfo"], dtype=torch.float32, device=device).contiguous()
+            # every texture with its box-filtered mip pyramid (the kernel samples trilinearly)
+            desc = np.zeros((len(arrays["tex_type"]), 4), np.int32)
+            ladr = np.zeros((max(1, len(desc)), N.TEX_LEVELS), np.int32)
+            chunks, adr = [], 0
+            for i in range(len(desc)):
+                h, w = (int(x) for x in arrays["tex_size"][i])
+                a0 = int(arrays["tex_adr"][i])
+                base = np.asarray(arrays["tex_rgb"][a0:a0 + h * w], np.uint32).reshape(h, w, 3)
+                levels = mip_pyramid(base)
+                if len(levels) > N.TEX_LEVELS:
+                    raise ValueError(f"texture {i}: {h} x {w} needs more than {N.TEX_LEVELS} mip levels")
+                desc[i] = (int(arrays["tex_type"][i]), h, w, adr)
+                rel = 0
+                for l, lv in enumerate(levels):
+                    ladr[i, l] = rel
+                    chunks.append(lv.reshape(-1, 3))
+                    rel += lv.shape[0] * lv.shape[1]
+                adr += rel
+            self.tex_level_adr = torch.tensor(ladr, device=device).contiguous()
+            rgb = np.concatenate(chunks) if chunks else np.zeros((0, 3), np.uint32)
+            words = rgb[:, 0] | (rgb[:, 1] << 8) | (rgb[:, 2] << 16) | np.uint32(255 << 24)
+            self.tex_rgba = torch.tensor(words.view(np.int32), device=device) if len(words) else None
+            self.tex_desc = torch.tensor(desc, device=device).contiguous() if len(desc) else None
+            sc.geom_texid, sc.geom_matinfo = self.geom_texid.data_ptr(), self.geom_matinfo.data_ptr()
+            sc.tex_rgba = self.tex_rgba.data_ptr() if self.tex_rgba is not None else None
+            sc.tex_desc = self.tex_desc.data_ptr() if self.tex_desc is not None else None
+            sc.tex_level_adr = self.tex_level_adr.data_ptr()
+            sc.ntex = len(desc)
+            for i, v in enumerate(np.asarray(arrays["sky_rgb"], np.float64).reshape(-1)):
+                sc.sky_rgb[i] = float(v)
         self._scene = sc
         self.width, self.height = width, height
         self.cam_names = [str(x) for x in arrays["names_cam"]]

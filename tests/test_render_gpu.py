@@ -67,6 +67,9 @@ def test_renderer_matches_the_brute_force_oracle_on_every_camera():
     gx, gm = eng.gxpos.cpu().numpy(), eng.gxmat.cpu().numpy()
     bx, bq = eng.xpos.cpu().numpy(), eng.xquat.cpu().numpy()
     mesh_geoms = set(int(g) for g in arrays["rmesh_geoms"])
+    # the scene's materials: every pixel of a textured geom samples its texture in both renderers
+    assert "geom_matinfo" in arrays and rnd.materials
+    textured = set(int(g) for g in np.nonzero(arrays["geom_texid"] >= 0)[0])
     report = []
     for cam in env.camera_names:
         rgb = torch.empty((n, H, W, 3), dtype=torch.uint8, device=DEV)
@@ -97,14 +100,16 @@ def test_renderer_matches_the_brute_force_oracle_on_every_camera():
                 amb[k] = spread
             unexplained = np.nonzero(bad & ~amb)[0]
             mesh_frac = float(np.isin(og, list(mesh_geoms)).mean())
-            report.append(f"{cam} env{e}: mesh pixels {mesh_frac:.3f}, differing {int(bad.sum())}, "
-                          f"all ambiguous in the oracle: {int(amb.sum())}")
+            tex_frac = float(np.isin(og, list(textured)).mean())
+            report.append(f"{cam} env{e}: mesh pixels {mesh_frac:.3f}, textured pixels {tex_frac:.3f}, differing "
+                          f"{int(bad.sum())}, all ambiguous in the oracle: {int(amb.sum())}")
             assert len(unexplained) == 0, (cam, e, [(int(xs[k]), int(ys[k]), int(gg[k]), int(og[k]), float(gd[k]),
                                                      float(od[k]), g8[k].tolist(), o8[k].tolist())
                                                     for k in unexplained[:8]])
             assert amb.sum() <= 0.02 * len(xs), (cam, e, int(amb.sum()))
             if cam == "front":
                 assert mesh_frac > 0.01, (cam, e, mesh_frac)  # the arm's meshes are in the policy view
+                assert tex_frac > 0.3, (cam, e, tex_frac)  # table, floor, poles, cable: textured
     print("\n" + "\n".join(report))
 
 

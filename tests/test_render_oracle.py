@@ -119,3 +119,124 @@ def test_body_frame_meshes_and_the_second_surface():
     g, d, rgb, d2 = OR.cast(a, prims, pos, gm, xpos, xquat, "cam", W, H, CENTRE, second=True)
     assert g[0] == 1 and abs(d[0] - 1.5) < 1e-12 and abs(d2[0] - 2.4) < 1e-12
     np.testing.assert_allclose(rgb[0], np.full(3, 0.5 * (0.1 + 0.6 + 0.3)), atol=1e-7)
+
+
+# ---- materials (round 6): textures, specular term, gradient skybox -----------------------------
+TEX2 = np.array([[[255, 0, 0], [0, 255, 0]], [[0, 0, 255], [255, 255, 0]]], np.uint8)  # 2 x 2 RGB texels
+
+
+def _with_materials(a, tex_type, spec=0.0, shin=0.5, rep=(1.0, 1.0), uniform=0.0, sky=((0.9, 1, 1), (0.9, 1, 1))):
+    """Give every geom of a _scene the same material: the 2 x 2 texture TEX2 (2d or cube)."""
+    n = len(a["geom_type"])
+    a["geom_texid"] = np.zeros(n, np.int32)
+    a["geom_matinfo"] = np.tile(np.array([spec, shin, rep[0], rep[1], uniform, 0.0], np.float32), (n, 1))
+    a["tex_type"] = np.array([tex_type], np.int32)
+    a["tex_size"] = np.array([[2, 2]], np.int32)
+    a["tex_adr"] = np.array([0], np.int32)
+    a["tex_rgb"] = TEX2.reshape(-1, 3)
+    a["sky_rgb"] = np.array(sky, np.float64)
+    return a
+
+
+def _pixel_of(point):
+    """Continuous pixel coordinates of a camera-frame point (the camera at the origin, looking along
+    -z, fovy 45 degrees, W x H)."""
+    t = np.tan(np.deg2rad(22.5))
+    x, y, z = point
+    return np.array([[(x / -z / (t * W / H) + 1.0) * W / 2, (1.0 - y / -z / t) * H / 2]])
+
+
+def _shade(point):
+    """0.1 + 0.6 n.v + 0.3 n.z of a face with n = +z seen from the origin at camera-frame `point`."""
+    return 0.1 + 0.6 * (-point[2] / np.linalg.norm(point)) + 0.3
+
+
+def test_2d_texture_on_a_plane_texel_centres_and_repeat():
+    # an infinite plane 3 m down, texuniform: one period per metre; texel (col, row) centred at
+    # ((col + 0.5) / 2, (row + 0.5) / 2) of the period, wrapped every metre
+    a, pos, gm = _scene([(0, (0, 0, 0), (0, 0, -3.0), (1, 1, 1))])
+    _with_materials(a, 0, uniform=1.0)
+    for (x, y), (row, col) in [((0.25, 0.25), (0, 0)), ((0.75, 0.25), (0, 1)), ((0.25, 0.75), (1, 0)),
+                               ((-0.25, -0.25), (1, 1)), ((1.75, 0.25), (0, 1))]:
+        _, _, rgb = _cast(a, pos, gm, _pixel_of((x, y, -3.0)))
+        np.testing.assert_allclose(rgb[0], TEX2[row, col] / 255.0 * _shade((x, y, -3.0)), atol=1e-9,
+                                   err_msg=str((x, y)))
+    # between texel centres: the bilinear blend of the four (wrapped) neighbours
+    _, _, rgb = _cast(a, pos, gm, _pixel_of((0.5, 0.5, -3.0)))
+    np.testing.assert_allclose(rgb[0], TEX2.reshape(-1, 3).mean(0) / 255.0 * _shade((0.5, 0.5, -3.0)), atol=1e-9)
+
+
+def test_2d_texture_repeated_over_a_finite_plane():
+    # plane half extents (1, 1), texrepeat (2, 2), not uniform: the image repeats twice over 2 m
+    a, pos, gm = _scene([(0, (1.0, 1.0, 0), (0, 0, -3.0), (1, 1, 1))])
+    _with_materials(a, 0, rep=(2.0, 2.0))
+    # u = 2 (x / 2 + 0.5): x = -0.75 -> u = 0.25 (texel column 0), x = -0.25 -> 0.75 (column 1),
+    # x = 0.25 -> 1.25 (column 0 of the second repeat)
+    for x, col in ((-0.75, 0), (-0.25, 1), (0.25, 0)):
+        _, _, rgb = _cast(a, pos, gm, _pixel_of((x, -0.75, -3.0)))
+        np.testing.assert_allclose(rgb[0], TEX2[0, col] / 255.0 * _shade((x, -0.75, -3.0)), atol=1e-9, err_msg=str(x))
+
+
+def test_cube_texture_on_a_box_face():
+    # a 0.8 m cube 2 m down the view axis, cube texture in metric coordinates: its +z face centre
+    # looks up the middle of the face image (the four texels' mean), (0.2, 0.2, 0.4) looks up
+    # s = 0.75, t = 0.25: texel (col 1, row 0) exactly
+    a, pos, gm = _scene([(6, (0.4, 0.4, 0.4), (0, 0, -2.4), (1, 1, 1))])
+    _with_materials(a, 1)
+    _, _, rgb = _cast(a, pos, gm, CENTRE)
+    np.testing.assert_allclose(rgb[0], TEX2.reshape(-1, 3).mean(0) / 255.0, atol=1e-9)
+    _, _, rgb = _cast(a, pos, gm, _pixel_of((0.2, 0.2, -2.0)))
+    np.testing.assert_allclose(rgb[0], TEX2[0, 1] / 255.0 * _shade((0.2, 0.2, -2.0)), atol=1e-9)
+
+
+def test_specular_highlight_of_a_face_under_the_light():
+    # camera looking down world -z at a face whose normal points at it and at the light: n.h = 1,
+    # so the specular term is specular x 0.3 whatever the shininess
+    a, pos, gm = _scene([(6, (0.2, 0.2, 0.2), (0, 0, -2.0), (0.5, 0.4, 0.2))])
+    _with_materials(a, 0, spec=0.5, shin=0.7)
+    a["geom_texid"][:] = -1
+    _, _, rgb = _cast(a, pos, gm, CENTRE)
+    np.testing.assert_allclose(rgb[0], np.array([0.5, 0.4, 0.2]) * 1.0 + 0.5 * 0.3, atol=1e-12)
+    # off-centre on the same face: n.h = cos of half the view angle, raised to 128 x shininess
+    pix = _pixel_of((0.1, 0.0, -1.8))
+    _, _, rgb2 = _cast(a, pos, gm, pix)
+    v = np.array([-0.1, 0.0, 1.8]) / np.linalg.norm([0.1, 0.0, 1.8])
+    h = (v + np.array([0, 0, 1.0])) / np.linalg.norm(v + np.array([0, 0, 1.0]))
+    want = np.array([0.5, 0.4, 0.2]) * (0.1 + 0.6 * v[2] + 0.3) + 0.5 * 0.3 * h[2] ** (128 * 0.7)
+    np.testing.assert_allclose(rgb2[0], want, atol=1e-12)
+
+
+def test_gradient_skybox_behind_everything():
+    a, pos, gm = _scene([(2, (0.1, 0, 0), (5.0, 5.0, -3.0), (1, 1, 1))])
+    _with_materials(a, 0, sky=((0.2, 0.4, 0.6), (0.8, 0.6, 0.4)))
+    g, _, rgb = _cast(a, pos, gm, CENTRE)  # straight down world -z: rgb2
+    assert g[0] == -1
+    np.testing.assert_allclose(rgb[0], [0.8, 0.6, 0.4], atol=1e-12)
+    c = np.cos(np.pi / 4)
+    a, pos, gm = _scene([(2, (0.1, 0, 0), (5.0, 5.0, -3.0), (1, 1, 1))], cam_quat=(c, c, 0, 0))
+    _with_materials(a, 0, sky=((0.2, 0.4, 0.6), (0.8, 0.6, 0.4)))
+    _, _, rgb = _cast(a, pos, gm, CENTRE)  # horizontal: halfway
+    np.testing.assert_allclose(rgb[0], [0.5, 0.5, 0.5], atol=1e-12)
+
+
+def test_mip_level_from_the_pixel_footprint():
+    # a 4 x 4 texture, one period per metre, on a plane facing the camera at the distance where one
+    # pixel step of the centre ray spans exactly 2 texels: level of detail 1, the level-1 texel
+    # (the rounded mean of its 2 x 2 block) at its centre, no blend with another level; at a tenth of
+    # that distance the footprint is below a texel: level 0, bilinear
+    tex = np.arange(48, dtype=np.uint8).reshape(4, 4, 3) * 5
+    step = 2 * np.tan(np.deg2rad(22.5)) / H  # one pixel's step of the ray slope (square pixels)
+    d = 2.0 / (4 * step)
+    a, pos, gm = _scene([(0, (0, 0, 0), (-0.25, -0.25, -d), (1, 1, 1))])
+    _with_materials(a, 0, uniform=1.0)
+    a["tex_size"] = np.array([[4, 4]], np.int32)
+    a["tex_rgb"] = tex.reshape(-1, 3)
+    _, _, rgb = _cast(a, pos, gm, CENTRE)
+    lvl1 = (tex[0, 0].astype(int) + tex[0, 1] + tex[1, 0] + tex[1, 1] + 2) // 4
+    np.testing.assert_allclose(rgb[0], lvl1 / 255.0, atol=1e-9)
+    a, pos, gm = _scene([(0, (0, 0, 0), (-0.25 + 1 / 8, -0.25 + 1 / 8, -d / 10), (1, 1, 1))])
+    _with_materials(a, 0, uniform=1.0)
+    a["tex_size"] = np.array([[4, 4]], np.int32)
+    a["tex_rgb"] = tex.reshape(-1, 3)
+    _, _, rgb = _cast(a, pos, gm, CENTRE)  # local (1/8, 1/8): texel (0, 0)'s centre of level 0
+    np.testing.assert_allclose(rgb[0], tex[0, 0] / 255.0, atol=1e-9)

@@ -44,9 +44,31 @@ def add_arm_ik(M, arrays, root_body="ur5e_root_frame"):
     arrays["arm_axis"] = np.ascontiguousarray(axes)
     arrays["arm_joint_names"] = np.array(names)
 
+def add_visual(name, path):
+    """Merge the renderer's material / texture tables (compiler.visual_arrays) into an existing
+    asset, leaving every physics array as it is (checked: the geom order must be the compiled one)."""
+    import numpy as np
+
+    M = C.compile_mjcf(path, **OPTIONS.get(name, {}))
+    out = os.path.join(MD.ASSET_DIR, name + ".npz")
+    arrays = MD.load(out)
+    names = [str(x) for x in arrays["names_geom"]]
+    if names != [g["name"] for g in M.geoms] or not np.array_equal(arrays["geom_type"], [g["type"] for g in M.geoms]):
+        raise RuntimeError(f"{name}: the asset's geoms are not the compiled model's: recompile the asset")
+    arrays.update(C.visual_arrays(M))
+    MD.save(arrays, out)
+    print(name, "textures", len(arrays["tex_type"]), "textured geoms", int((arrays["geom_texid"] >= 0).sum()), "->", out,
+          os.path.getsize(out), "bytes")
+
+
 if __name__ == "__main__":
     os.makedirs(MD.ASSET_DIR, exist_ok=True)
-    only = sys.argv[1:]
+    only = [a for a in sys.argv[1:] if not a.startswith("--")]
+    if "--visual" in sys.argv:
+        for name, path in SCENES.items():
+            if not only or name in only:
+                add_visual(name, path)
+        sys.exit(0)
     for name, path in SCENES.items():
         if only and name not in only:
             continue
@@ -55,6 +77,8 @@ if __name__ == "__main__":
         add_arm_ik(M, arrays)
         # render meshes: the visual mesh geoms' triangles per body (1 mm vertex clustering)
         arrays.update(MB.render_meshes(M.geoms, cell=RENDER_MESH_CELL))
+        # materials and textures of the renderer
+        arrays.update(C.visual_arrays(M))
         out = os.path.join(MD.ASSET_DIR, name + ".npz")
         MD.save(arrays, out)
         print(name, "nq", M.nq, "nv", M.nv, "pairs", len(M.pairs), "->", out, os.path.getsize(out), "bytes")
