@@ -245,6 +245,30 @@ def gemm_library_ceiling():
                     "same chip; the per_shape table above is this kernel at those shapes"}
 
 
+def mfma_utilisation(prefix):
+    """Matrix-core utilisation at the clock the chip held, per kernel instance, from the latest
+    committed counter pass over one fp32 ACT inference (SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x
+    GRBM_GUI_ACTIVE / 8); scripts/gpurun/r6_j.sh -> scripts/mfma_util.py ->
+    profiles/r<round>_mfma_util_act_inference.txt): {"source", "kernels": {name: {util, clock_GHz}}}
+    for the kernels whose name starts with `prefix`, or None."""
+    import glob
+
+    files = sorted(glob.glob(os.path.join(ROOT, "profiles", "r*_mfma_util_act_inference.txt")))
+    if not files:
+        return None
+    out = {}
+    with open(files[-1]) as f:
+        for line in f:
+            parts = [x.strip() for x in line.split("|")]
+            if len(parts) == 5 and parts[0].startswith(prefix):
+                out[parts[0]] = {"mfma_busy": float(parts[2]), "held_clock_GHz": float(parts[3]),
+                                 "launches": int(parts[1])}
+    return {"source": os.path.relpath(files[-1], ROOT), "kernels": out,
+            "note": "SQ_VALU_MFMA_BUSY_CYCLES / (1024 SIMDs x GRBM_GUI_ACTIVE / 8): the fraction of the matrix "
+                    "cores' cycles busy at the clock the chip held under this load (DVFS); `frac` above is "
+                    "against the nominal 2.5 PF (2.4 GHz)"} if out else None
+
+
 def _probe_line(probe, is_gemm):
     if not probe:
         return None
@@ -290,7 +314,8 @@ def _probe_line(probe, is_gemm):
             "ms_per_inference": round(ms, 3),
             "per_shape": {k: {"launches": L["launches"], "ms": round(L["ms"], 3),
                               "fp32_equiv_TFLOPs": round(L["flops"] / L["ms"] / 1e9, 1)} for k, L in shapes.items()},
-            "library_ceiling": gemm_library_ceiling() if is_gemm else None}
+            "library_ceiling": gemm_library_ceiling() if is_gemm else None,
+            "mfma_utilisation": mfma_utilisation("rmbx::gemm_f" if is_gemm else "rmbx::conv3x3p")}
 
 
 def policy_flops_per_inference(full_decoder):
