@@ -59,7 +59,11 @@ FILE_FLAGS = {"rmbx_gemm.hip": ["-fno-slp-vectorize"],
               # the renderer's ray-cast kernel at 6 waves per SIMD (80 registers): with the textured
               # shading, 13.7 vs 14.3 ms per 1024-env front-camera call at 8 (64 registers, spills)
               # and 14.1 at 5 (profiles/r6_render_waves_ab.log)
-              "rmbx_render.hip": ["-DRMBX_RENDER_MINW=6"]}
+              "rmbx_render.hip": ["-DRMBX_RENDER_MINW=6"],
+              # the attention kernels rescale their MFMA accumulators in the online softmax: in the
+              # VGPR form they are multiplied in place (the AGPR form moved 112 registers per key tile
+              # through v_accvgpr_read / write)
+              "rmbx_attn.hip": ["-mllvm", "-amdgpu-mfma-vgpr-form"]}
 
 
 def _compile(src, hdr_digest, verbose):

@@ -844,8 +844,10 @@ __global__ void __launch_bounds__(64 * AX_MAX_WAVES) attn_fwd_f16x3_kernel(AttnF
           l[e] = __float_as_uint(s[8 * u + 2 * e + 1]);
           continue;
         }
-        const float pa = exp2f(fmaf(s[8 * u + 2 * e], c, -mc)) * 16384.f;
-        const float pb = exp2f(fmaf(s[8 * u + 2 * e + 1], c, -mc)) * 16384.f;
+        // (v_exp_f32 alone: exp2f's denormal-result path only changes p' < 2^-112, which is zero
+        // in the f16 pieces and below the ulp of l >= 2^14)
+        const float pa = __builtin_amdgcn_exp2f(fmaf(s[8 * u + 2 * e], c, -mc)) * 16384.f;
+        const float pb = __builtin_amdgcn_exp2f(fmaf(s[8 * u + 2 * e + 1], c, -mc)) * 16384.f;
         l_run += pa + pb;
         ah_split_w(pa, pb, h[e], l[e]);
       }
@@ -897,6 +899,310 @@ __global__ void __launch_bounds__(64 * AX_MAX_WAVES) attn_fwd_f16x3_kernel(AttnF
   }
   const int any = __syncthreads_or(flag ? 1 : 0);
   if (tid == 0) a.redo[bh * a.parts + part] = any;  // the bf16x6 kernel's block order
+  if (any) return;
+  const float l_tot = l_run + __shfl_xor(l_run, 32);
+  if (!q_ok) return;
+  const float inv = 1.f / l_tot;
+  float* op = a.o + ((size_t)b * a.Lq + qi) * a.o_rstride + hd * 64 + 16 * kh;
+#pragma unroll
+  for (int q4 = 0; q4 < 4; ++q4) {
+    *reinterpret_cast<float4*>(op + 4 * q4) =
+        make_float4(acc0[4 * q4] * inv, acc0[4 * q4 + 1] * inv, acc0[4 * q4 + 2] * inv, acc0[4 * q4 + 3] * inv);
+    *reinterpret_cast<float4*>(op + 32 + 4 * q4) =
+        make_float4(acc1[4 * q4] * inv, acc1[4 * q4 + 1] * inv, acc1[4 * q4 + 2] * inv, acc1[4 * q4 + 3] * inv);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// f16x3 form with the key / value tiles staged by LDS-DMA (rmbx_attention_f16x3's default since
+// round 6; RMBX_ATTN_DMA=0 selects the register-staged kernel above).  The register-staged kernel
+// spends half its time staging (profiles/r5_attn_f16_phase_skips.log): the f32 tile loads into
+// registers one tile ahead, the split, and the V^T image written as 2-byte transposing stores.
+// Here, per 32-key tile:
+//   * DMA: the raw f32 K and V rows go global -> LDS by global_load_lds_dwordx4 (no registers, no
+//     LDS stores), two tiles ahead of the MFMAs; wave w moves rows 8 w .. 8 w + 7 of K and of V.
+//   * split (once per block, one tile ahead): wave w reads its 8 raw rows back, splits them into
+//     the staged-operand pieces (h = f16(x), l = f16((x - h) 2^11)), keeps the range statistics
+//     and writes the pieces ROW-major with 16-byte stores: K as the register-staged kernel's image,
+//     V key-major.
+//   * MFMAs: K fragments as 16-byte row reads; the V^T fragments of O^T += V^T P'^T by
+//     ds_read_b64_tr_b16 from the key-major V image (each 16-lane group reads a 4-key x 16-dim
+//     block and receives it dim-major; two per fragment), so V is never stored transposed.
+// One barrier per tile.  LDS per block: raw ring 2 x 16 KiB (row r = key 32 t + r, clamped to
+// Lk - 1 so the masked keys of a ragged tile are real rows; 256-B rows, 16-byte chunk c' holding
+// dims 4 (c' ^ (r & 15)) .. + 3) + pieces 2 x 16 KiB (K h, K l, V h, V l: 32 rows x 128 B; K chunk
+// c at c ^ ((r >> 1) & 7), V chunk c at c ^ (((r >> 1) & 1) << 2): the K row reads, the transposed V
+// reads and the piece stores are bank-conflict-free).  Same pieces and MFMA order as the
+// register-staged kernel: bitwise-equal results; the range checks and the bf16x6 re-run of the
+// flagged blocks are unchanged.  Waves whose 32 queries all lie past Lq only stage.
+// ---------------------------------------------------------------------------------------------
+constexpr int AD_WAVES = 4;
+constexpr int AD_RAW_B = 2 * 32 * 256;  // one raw stage: K and V, 32 keys x 64 f32
+constexpr int AD_PLANE_B = 32 * 128;    // one piece plane: 32 keys x 64 f16
+constexpr int AD_PCS_B = 4 * AD_PLANE_B;
+
+__device__ __forceinline__ void ad_glds16(const float* gsrc, const void* lds_dst) {
+  const uint32_t dst = (uint32_t)(uintptr_t)(const __attribute__((address_space(3))) char*)lds_dst;
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(__builtin_amdgcn_readfirstlane(dst))
+               : "memory");
+}
+// all of this wave's LDS-DMAs landed, then the block barrier (no __syncthreads: its fence is not
+// needed for LDS and would be placed by the compiler without the DMAs in view)
+__device__ __forceinline__ void ad_dma_barrier() { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+__device__ __forceinline__ void ad_split8(float4 x0, float4 x1, f16x8& h, f16x8& l) {
+  uint32_t hh[4], ll[4];
+  ah_split_a(x0.x, x0.y, hh[0], ll[0]);
+  ah_split_a(x0.z, x0.w, hh[1], ll[1]);
+  ah_split_a(x1.x, x1.y, hh[2], ll[2]);
+  ah_split_a(x1.z, x1.w, hh[3], ll[3]);
+  h = __builtin_bit_cast(f16x8, make_uint4(hh[0], hh[1], hh[2], hh[3]));
+  l = __builtin_bit_cast(f16x8, make_uint4(ll[0], ll[1], ll[2], ll[3]));
+}
+__device__ __forceinline__ float ad_amax4(float m, float4 x) {
+  return fmaxf(m, fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
+}
+typedef short ad_s4 __attribute__((ext_vector_type(4)));
+// 4 keys x 4 dims of a piece plane, delivered transposed across the 16-lane group (T10)
+__device__ __forceinline__ ad_s4 ad_tr(const unsigned char* p) {
+  return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) ad_s4*)p);
+}
+
+__global__ void __launch_bounds__(64 * AD_WAVES) attn_fwd_f16x3d_kernel(AttnF32Args a) {
+  __shared__ __attribute__((aligned(16))) unsigned char sR[2 * AD_RAW_B];
+  __shared__ __attribute__((aligned(16))) unsigned char sP[2 * AD_PCS_B];
+  __shared__ uint32_t sDim[64];  // per head dimension: max |v| over the keys (f32 bits)
+  __shared__ uint32_t sKmax;     // max |k| over the block (f32 bits)
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int bh = blockIdx.x / a.parts, part = blockIdx.x - bh * a.parts;
+  const int b = bh / a.heads, hd = bh - b * a.heads;
+  const int r32 = lane & 31, kh = lane >> 5;
+  const int q0 = (part * AD_WAVES + wave) * 32;  // the wave's first query (wave-uniform)
+  const bool live = q0 < a.Lq;
+  const int qi = q0 + r32;
+  const bool q_ok = qi < a.Lq;
+  const float* kbase = a.k + (size_t)b * a.k_bstride + hd * 64;
+  const float* vbase = a.v + (size_t)b * a.v_bstride + hd * 64;
+  const int nt = (a.Lk + 31) >> 5;
+  if (tid < 64) sDim[tid] = 0u;
+  if (tid == 0) sKmax = 0u;
+
+  const int dr = lane >> 4, dc = lane & 15;
+  auto dma_tile = [&](int t) {
+    unsigned char* st = sR + (t & 1) * AD_RAW_B;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r0 = 8 * wave + 4 * i, r = r0 + dr;
+      int key = 32 * t + r;
+      key = key < a.Lk ? key : a.Lk - 1;
+      const int c = dc ^ (r & 15);
+      ad_glds16(kbase + (size_t)key * a.k_rstride + 4 * c, st + r0 * 256);
+      ad_glds16(vbase + (size_t)key * a.v_rstride + 4 * c, st + 32 * 256 + r0 * 256);
+    }
+  };
+  // split of tile t: lane -> raw row rr = 8 wave + lane / 8, dims 8 jj .. 8 jj + 7
+  const int rr = 8 * wave + (lane >> 3), jj = lane & 7;
+  float kmx = 0.f;      // max |k| of this lane's elements
+  float vmx[8] = {};    // max |v| of dims 8 jj + e over this lane's keys
+  auto split_tile = [&](int t) {
+    const unsigned char* raw = sR + (t & 1) * AD_RAW_B + rr * 256;
+    unsigned char* pcs = sP + (t & 1) * AD_PCS_B + rr * 128;
+    const int sw = rr & 15;
+    const float4 x0 = *reinterpret_cast<const float4*>(raw + (((2 * jj) ^ sw) << 4));
+    const float4 x1 = *reinterpret_cast<const float4*>(raw + (((2 * jj + 1) ^ sw) << 4));
+    const float4 y0 = *reinterpret_cast<const float4*>(raw + 32 * 256 + (((2 * jj) ^ sw) << 4));
+    const float4 y1 = *reinterpret_cast<const float4*>(raw + 32 * 256 + (((2 * jj + 1) ^ sw) << 4));
+    kmx = ad_amax4(ad_amax4(kmx, x0), x1);
+    vmx[0] = fmaxf(vmx[0], fabsf(y0.x));
+    vmx[1] = fmaxf(vmx[1], fabsf(y0.y));
+    vmx[2] = fmaxf(vmx[2], fabsf(y0.z));
+    vmx[3] = fmaxf(vmx[3], fabsf(y0.w));
+    vmx[4] = fmaxf(vmx[4], fabsf(y1.x));
+    vmx[5] = fmaxf(vmx[5], fabsf(y1.y));
+    vmx[6] = fmaxf(vmx[6], fabsf(y1.z));
+    vmx[7] = fmaxf(vmx[7], fabsf(y1.w));
+    f16x8 h, l;
+    ad_split8(x0, x1, h, l);
+    const int kc = jj ^ ((rr >> 1) & 7);
+    *reinterpret_cast<f16x8*>(pcs + (kc << 4)) = h;
+    *reinterpret_cast<f16x8*>(pcs + AD_PLANE_B + (kc << 4)) = l;
+    ad_split8(y0, y1, h, l);
+    const int vc = jj ^ (((rr >> 1) & 1) << 2);
+    *reinterpret_cast<f16x8*>(pcs + 2 * AD_PLANE_B + (vc << 4)) = h;
+    *reinterpret_cast<f16x8*>(pcs + 3 * AD_PLANE_B + (vc << 4)) = l;
+  };
+
+  dma_tile(0);
+  if (nt > 1) dma_tile(1);
+
+  // Q pieces as in the register-staged kernel (dims 16 s + 8 kh .. +7 of query qi, scaled by the
+  // query's power of two 2^t; fq[s][2] = 2^-11 qh)
+  f16x8 fq[4][3];
+  float c = a.scale_log2;
+  bool q_inf = false;
+  {
+    const float* qp = a.q + (size_t)b * a.q_bstride + (size_t)(q_ok ? qi : 0) * a.q_rstride + hd * 64 + 8 * kh;
+    float4 x[4][2];
+    float qm = 0.f;
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      x[s][0] = *reinterpret_cast<const float4*>(qp + 16 * s);
+      x[s][1] = *reinterpret_cast<const float4*>(qp + 16 * s + 4);
+      qm = ad_amax4(ad_amax4(qm, x[s][0]), x[s][1]);
+    }
+    qm = fmaxf(qm, __shfl_xor(qm, 32));
+    int t = 0;
+    if (qm > 0.f && qm < INFINITY) {
+      int e;
+      frexpf(qm, &e);
+      t = 14 - e;
+      t = t < -100 ? -100 : (t > 100 ? 100 : t);
+    } else if (qm == INFINITY) {
+      q_inf = true;
+    }
+    c = ldexpf(c, -t);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      uint32_t h[4], l[4];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const float4 y = make_float4(ldexpf(x[s][u].x, t), ldexpf(x[s][u].y, t), ldexpf(x[s][u].z, t),
+                                     ldexpf(x[s][u].w, t));
+        ah_split_w(y.x, y.y, h[2 * u], l[2 * u]);
+        ah_split_w(y.z, y.w, h[2 * u + 1], l[2 * u + 1]);
+      }
+      fq[s][0] = __builtin_bit_cast(f16x8, make_uint4(h[0], h[1], h[2], h[3]));
+      fq[s][1] = __builtin_bit_cast(f16x8, make_uint4(l[0], l[1], l[2], l[3]));
+      fq[s][2] = fq[s][0] * (_Float16)0.00048828125f;
+    }
+  }
+  ad_dma_barrier();  // tile 0 (and 1) landed; sDim / sKmax cleared
+  split_tile(0);
+
+  const bool ragged = (a.Lk & 31) != 0;
+  // transposed V reads: lane 4 q + p of its 16-lane group g supplies key row q, dims dv .. dv + 3
+  // (the at_sigma order: lane i of the group, A row 16 (g & 1) + i, receives dim sigma(row))
+  const int vq = (lane & 15) >> 2, vp = lane & 3;
+  const int dv = 16 * (vp & 1) + 8 * ((lane >> 4) & 1) + 4 * (vp >> 1);
+  f32x16 acc0 = {}, acc1 = {};
+  float m_run = -INFINITY, l_run = 0.f;
+  for (int t = 0; t < nt; ++t) {
+    ad_dma_barrier();  // tile t + 1 landed; tile t's pieces written; every wave is past tile t - 1
+    if (t + 2 < nt) dma_tile(t + 2);
+    if (t + 1 < nt) split_tile(t + 1);
+    if (!live) continue;
+    const unsigned char* pc = sP + (t & 1) * AD_PCS_B;
+    f32x16 s = {};
+#pragma unroll
+    for (int ks = 0; ks < 4; ++ks) {
+      const int off = r32 * 128 + (((2 * ks + kh) ^ ((r32 >> 1) & 7)) << 4);
+      const f16x8 k0 = *reinterpret_cast<const f16x8*>(pc + off);
+      const f16x8 k1 = *reinterpret_cast<const f16x8*>(pc + AD_PLANE_B + off);
+      s = __builtin_amdgcn_mfma_f32_32x32x16_f16(k1, fq[ks][2], s, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_32x32x16_f16(k0, fq[ks][1], s, 0, 0, 0);
+      s = __builtin_amdgcn_mfma_f32_32x32x16_f16(k0, fq[ks][0], s, 0, 0, 0);
+    }
+    if (ragged && t == nt - 1) {
+#pragma unroll
+      for (int j = 0; j < 16; ++j)
+        if (32 * t + 4 * kh + (j & 3) + 8 * (j >> 2) >= a.Lk) s[j] = -INFINITY;
+    }
+    float mx = s[0];
+#pragma unroll
+    for (int j = 1; j < 16; ++j) mx = fmaxf(mx, s[j]);
+    mx = fmaxf(mx, __shfl_xor(mx, 32));
+    const float m_new = fmaxf(m_run, mx);
+    if (__any(m_new != m_run)) {
+      const float alpha = exp2f((m_run - m_new) * c);
+      l_run *= alpha;
+#pragma unroll
+      for (int j = 0; j < 16; ++j) {
+        acc0[j] *= alpha;
+        acc1[j] *= alpha;
+      }
+      m_run = m_new;
+    }
+    const float mc = m_run * c;
+    f16x8 fp[2][3];
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      uint32_t h[4], l[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        // (v_exp_f32 alone: exp2f's denormal-result path only changes p' < 2^-112, which is zero
+        // in the f16 pieces and below the ulp of l >= 2^14)
+        const float pa = __builtin_amdgcn_exp2f(fmaf(s[8 * u + 2 * e], c, -mc)) * 16384.f;
+        const float pb = __builtin_amdgcn_exp2f(fmaf(s[8 * u + 2 * e + 1], c, -mc)) * 16384.f;
+        l_run += pa + pb;
+        ah_split_w(pa, pb, h[e], l[e]);
+      }
+      fp[u][0] = __builtin_bit_cast(f16x8, make_uint4(h[0], h[1], h[2], h[3]));
+      fp[u][1] = __builtin_bit_cast(f16x8, make_uint4(l[0], l[1], l[2], l[3]));
+      fp[u][2] = fp[u][0] * (_Float16)0.00048828125f;
+    }
+    // V^T fragments of k-step u: elements 0-3 = keys 16 u + 4 kh + 0..3, elements 4-7 = keys
+    // 16 u + 8 + 4 kh + 0..3 (the keys the P' registers they meet hold)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      ad_s4 w[2][2][2];  // [key block][dims d / d + 32][piece]
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2) {
+        const int key = 16 * u + 8 * k2 + 4 * kh + vq;
+        const int fl = ((key >> 1) & 1) << 2;
+#pragma unroll
+        for (int dd = 0; dd < 2; ++dd) {
+          const int d = dv + 32 * dd;
+          const unsigned char* p = pc + 2 * AD_PLANE_B + key * 128 + ((((d >> 3) ^ fl) << 4) | ((d & 7) << 1));
+          w[k2][dd][0] = ad_tr(p);
+          w[k2][dd][1] = ad_tr(p + AD_PLANE_B);
+        }
+      }
+      auto cat = [](ad_s4 lo, ad_s4 hi) {
+        return __builtin_bit_cast(f16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      };
+      const f16x8 v0h = cat(w[0][0][0], w[1][0][0]), v0l = cat(w[0][0][1], w[1][0][1]);
+      const f16x8 v1h = cat(w[0][1][0], w[1][1][0]), v1l = cat(w[0][1][1], w[1][1][1]);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v0l, fp[u][2], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v1l, fp[u][2], acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v0h, fp[u][1], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v1h, fp[u][1], acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v0h, fp[u][0], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v1h, fp[u][0], acc1, 0, 0, 0);
+    }
+  }
+  // range check (the register-staged kernel's conditions): any |k|, |v| >= 2^15 or a non-finite
+  // query, the block's max |k| in (0, 2^-6), a dimension's max |v| over the keys in (0, 2^-6)
+  float vm = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    float x = vmx[e];
+    x = fmaxf(x, __shfl_xor(x, 8));
+    x = fmaxf(x, __shfl_xor(x, 16));
+    x = fmaxf(x, __shfl_xor(x, 32));
+    vmx[e] = x;
+    vm = fmaxf(vm, x);
+  }
+  if (lane < 8) {
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      if (vmx[e] > 0.f) atomicMax(&sDim[8 * jj + e], __float_as_uint(vmx[e]));
+  }
+  if (kmx > 0.f) atomicMax(&sKmax, __float_as_uint(kmx));
+  __syncthreads();
+  bool flag = q_inf || kmx >= AH_BIG || vm >= AH_BIG;
+  if (tid < 64) {
+    const float m = __uint_as_float(sDim[tid]);
+    flag = flag || (m > 0.f && m < AH_TINY);
+  }
+  if (tid == 0) {
+    const float km = __uint_as_float(sKmax);
+    flag = flag || (km > 0.f && km < AH_TINY);
+  }
+  const int any = __syncthreads_or(flag ? 1 : 0);
+  if (tid == 0) a.redo[blockIdx.x] = any;
   if (any) return;
   const float l_tot = l_run + __shfl_xor(l_run, 32);
   if (!q_ok) return;
@@ -1086,6 +1392,20 @@ extern "C" int rmbx_attention_f16x3(const float* q, const float* k, const float*
   // SIMD), 5 = up to five groups (2 parts; one 5-wave block per CU, so one SIMD carries two waves
   // and three carry one): 1.41 vs 1.75 ms encoder self-attention at 1024 envs
   // (profiles/r4_attention_waves_ab.log)
+  // RMBX_ATTN_DMA (read per launch): 1 (default) = the LDS-DMA-staged kernel, 0 = the
+  // register-staged kernel
+  const char* me = std::getenv("RMBX_ATTN_DMA");
+  if (!me || std::atoi(me) != 0) {
+    a.parts = (ngroups + rmbx::AD_WAVES - 1) / rmbx::AD_WAVES;
+    const long long nb = (long long)B * heads * a.parts;
+    RMBX_CHECK_ARG(nb < (1ll << 31), "rmbx_attention_f16x3: grid too large");
+    const dim3 g((unsigned)nb), blk(64 * rmbx::AD_WAVES);
+    hipLaunchKernelGGL(rmbx::attn_fwd_f16x3d_kernel, g, blk, 0, (hipStream_t)stream, a);
+    RMBX_CHECK_LAUNCH();
+    hipLaunchKernelGGL(rmbx::attn_fwd_f32x6_kernel, g, blk, 0, (hipStream_t)stream, a);
+    RMBX_CHECK_LAUNCH();
+    return RMBX_OK;
+  }
   const char* we = std::getenv("RMBX_ATTN_WAVES");
   const int wsel = we ? std::atoi(we) : 4;
   const int waves = (wsel == 5 && ngroups >= rmbx::AX_MAX_WAVES) ? rmbx::AX_MAX_WAVES : 4;

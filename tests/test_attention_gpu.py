@@ -236,6 +236,36 @@ def test_attention_f16x3_range_and_block_independence(case, shape):
 
 
 @torch.no_grad()
+@pytest.mark.parametrize("B,H,Lq,Lk,case", [(3, 8, 302, 302, None), (2, 8, 100, 302, None), (4, 8, 100, 100, None),
+                                             (1, 2, 1, 1, None), (2, 2, 257, 33, None), (1, 1, 130, 650, None),
+                                             (3, 2, 302, 90, "huge_k"), (3, 2, 100, 90, "tiny_v_dim")])
+def test_attention_f16x3_dma_staging_equals_register_staging(monkeypatch, B, H, Lq, Lk, case):
+    """The LDS-DMA-staged f16x3 kernel (the default, RMBX_ATTN_DMA=1: raw tiles by LDS-DMA, pieces
+    split once per block, V^T read through ds_read_b64_tr_b16) computes the register-staged kernel's
+    pieces in the same MFMA order: bitwise-equal outputs, including ragged key tiles, query parts
+    past Lq, long key sequences and re-run (flagged) blocks."""
+    from robomanipbaselines_amd import kernels as K
+
+    g = torch.Generator(device=DEV).manual_seed(Lq * 7 + Lk)
+    D = H * 64
+    q = torch.randn(B, Lq, D, device=DEV, generator=g) * 2
+    k = torch.randn(B, Lk, D, device=DEV, generator=g) * 2
+    v = torch.randn(B, Lk, D, device=DEV, generator=g)
+    if case == "huge_k":
+        k[1, :, :64] *= 4e4
+    elif case == "tiny_v_dim":
+        v[1, :, 3] *= 1e-4
+    monkeypatch.setenv("RMBX_ATTN_DMA", "1")
+    dma = K.attention_f32(q, k, v, H, form="f16x3")
+    monkeypatch.setenv("RMBX_ATTN_DMA", "0")
+    reg = K.attention_f32(q, k, v, H, form="f16x3")
+    torch.cuda.synchronize()
+    assert torch.equal(dma, reg)
+    if case is not None:  # item 1's first head re-ran on bf16x6
+        assert torch.equal(dma[1, :, :64], K.attention_f32(q, k, v, H, form="x6")[1, :, :64])
+
+
+@torch.no_grad()
 def test_attention_f16x3_non_finite_inputs():
     """A NaN in V propagates to the outputs that use it (as in f32); an inf in K re-runs the block on
     bf16x6 and gives that kernel's result."""
