@@ -915,7 +915,7 @@ __global__ void __launch_bounds__(64 * AX_MAX_WAVES) attn_fwd_f16x3_kernel(AttnF
 
 // ---------------------------------------------------------------------------------------------
 // f16x3 form with the key / value tiles staged by LDS-DMA (rmbx_attention_f16x3's default since
-// round 6; RMBX_ATTN_DMA=0 selects the register-staged kernel above).  The register-staged kernel
+// round 6, PIPE = true; RMBX_ATTN_DMA=0 selects the register-staged kernel above).  The register-staged kernel
 // spends half its time staging (profiles/r5_attn_f16_phase_skips.log): the f32 tile loads into
 // registers one tile ahead, the split, and the V^T image written as 2-byte transposing stores.
 // Here, per 32-key tile:
@@ -970,6 +970,7 @@ __device__ __forceinline__ ad_s4 ad_tr(const unsigned char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) ad_s4*)p);
 }
 
+template <bool PIPE>
 __global__ void __launch_bounds__(64 * AD_WAVES) attn_fwd_f16x3d_kernel(AttnF32Args a) {
   __shared__ __attribute__((aligned(16))) unsigned char sR[2 * AD_RAW_B];
   __shared__ __attribute__((aligned(16))) unsigned char sP[2 * AD_PCS_B];
@@ -991,31 +992,56 @@ __global__ void __launch_bounds__(64 * AD_WAVES) attn_fwd_f16x3d_kernel(AttnF32A
   if (tid == 0) sKmax = 0u;
 
   const int dr = lane >> 4, dc = lane & 15;
-  auto dma_tile = [&](int t) {
-    unsigned char* st = sR + (t & 1) * AD_RAW_B;
+  // DMA of one operand's raw rows (k = 0: K, 1: V) of tile t into raw stage t & 1
+  auto dma_op = [&](int t, int k) {
+    unsigned char* st = sR + (t & 1) * AD_RAW_B + k * 32 * 256;
+    const float* base = k ? vbase : kbase;
+    const long long rs = k ? a.v_rstride : a.k_rstride;
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int r0 = 8 * wave + 4 * i, r = r0 + dr;
       int key = 32 * t + r;
       key = key < a.Lk ? key : a.Lk - 1;
       const int c = dc ^ (r & 15);
+      ad_glds16(base + (size_t)key * rs + 4 * c, st + r0 * 256);
+    }
+  };
+  auto dma_tile = [&](int t) {
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int r0 = 8 * wave + 4 * i, r = r0 + dr;
+      int key = 32 * t + r;
+      key = key < a.Lk ? key : a.Lk - 1;
+      const int c = dc ^ (r & 15);
+      unsigned char* st = sR + (t & 1) * AD_RAW_B;
       ad_glds16(kbase + (size_t)key * a.k_rstride + 4 * c, st + r0 * 256);
       ad_glds16(vbase + (size_t)key * a.v_rstride + 4 * c, st + 32 * 256 + r0 * 256);
     }
   };
-  // split of tile t: lane -> raw row rr = 8 wave + lane / 8, dims 8 jj .. 8 jj + 7
+  // split of tile t: lane -> raw row rr = 8 wave + lane / 8, dims 8 jj .. 8 jj + 7 (the rows this
+  // wave's DMAs wrote: the raw stages are wave-private)
   const int rr = 8 * wave + (lane >> 3), jj = lane & 7;
   float kmx = 0.f;      // max |k| of this lane's elements
   float vmx[8] = {};    // max |v| of dims 8 jj + e over this lane's keys
-  auto split_tile = [&](int t) {
+  auto split_k = [&](int t) {
     const unsigned char* raw = sR + (t & 1) * AD_RAW_B + rr * 256;
     unsigned char* pcs = sP + (t & 1) * AD_PCS_B + rr * 128;
     const int sw = rr & 15;
     const float4 x0 = *reinterpret_cast<const float4*>(raw + (((2 * jj) ^ sw) << 4));
     const float4 x1 = *reinterpret_cast<const float4*>(raw + (((2 * jj + 1) ^ sw) << 4));
+    kmx = ad_amax4(ad_amax4(kmx, x0), x1);
+    f16x8 h, l;
+    ad_split8(x0, x1, h, l);
+    const int kc = jj ^ ((rr >> 1) & 7);
+    *reinterpret_cast<f16x8*>(pcs + (kc << 4)) = h;
+    *reinterpret_cast<f16x8*>(pcs + AD_PLANE_B + (kc << 4)) = l;
+  };
+  auto split_v = [&](int t) {
+    const unsigned char* raw = sR + (t & 1) * AD_RAW_B + rr * 256;
+    unsigned char* pcs = sP + (t & 1) * AD_PCS_B + rr * 128;
+    const int sw = rr & 15;
     const float4 y0 = *reinterpret_cast<const float4*>(raw + 32 * 256 + (((2 * jj) ^ sw) << 4));
     const float4 y1 = *reinterpret_cast<const float4*>(raw + 32 * 256 + (((2 * jj + 1) ^ sw) << 4));
-    kmx = ad_amax4(ad_amax4(kmx, x0), x1);
     vmx[0] = fmaxf(vmx[0], fabsf(y0.x));
     vmx[1] = fmaxf(vmx[1], fabsf(y0.y));
     vmx[2] = fmaxf(vmx[2], fabsf(y0.z));
@@ -1025,10 +1051,6 @@ __global__ void __launch_bounds__(64 * AD_WAVES) attn_fwd_f16x3d_kernel(AttnF32A
     vmx[6] = fmaxf(vmx[6], fabsf(y1.z));
     vmx[7] = fmaxf(vmx[7], fabsf(y1.w));
     f16x8 h, l;
-    ad_split8(x0, x1, h, l);
-    const int kc = jj ^ ((rr >> 1) & 7);
-    *reinterpret_cast<f16x8*>(pcs + (kc << 4)) = h;
-    *reinterpret_cast<f16x8*>(pcs + AD_PLANE_B + (kc << 4)) = l;
     ad_split8(y0, y1, h, l);
     const int vc = jj ^ (((rr >> 1) & 1) << 2);
     *reinterpret_cast<f16x8*>(pcs + 2 * AD_PLANE_B + (vc << 4)) = h;
@@ -1079,8 +1101,6 @@ __global__ void __launch_bounds__(64 * AD_WAVES) attn_fwd_f16x3d_kernel(AttnF32A
       fq[s][2] = fq[s][0] * (_Float16)0.00048828125f;
     }
   }
-  ad_dma_barrier();  // tile 0 (and 1) landed; sDim / sKmax cleared
-  split_tile(0);
 
   const bool ragged = (a.Lk & 31) != 0;
   // transposed V reads: lane 4 q + p of its 16-lane group g supplies key row q, dims dv .. dv + 3
@@ -1089,11 +1109,8 @@ __global__ void __launch_bounds__(64 * AD_WAVES) attn_fwd_f16x3d_kernel(AttnF32A
   const int dv = 16 * (vp & 1) + 8 * ((lane >> 4) & 1) + 4 * (vp >> 1);
   f32x16 acc0 = {}, acc1 = {};
   float m_run = -INFINITY, l_run = 0.f;
-  for (int t = 0; t < nt; ++t) {
-    ad_dma_barrier();  // tile t + 1 landed; tile t's pieces written; every wave is past tile t - 1
-    if (t + 2 < nt) dma_tile(t + 2);
-    if (t + 1 < nt) split_tile(t + 1);
-    if (!live) continue;
+  // S^T of tile t from the K pieces in piece stage t & 1
+  auto s_tile = [&](int t) {
     const unsigned char* pc = sP + (t & 1) * AD_PCS_B;
     f32x16 s = {};
 #pragma unroll
@@ -1105,6 +1122,12 @@ __global__ void __launch_bounds__(64 * AD_WAVES) attn_fwd_f16x3d_kernel(AttnF32A
       s = __builtin_amdgcn_mfma_f32_32x32x16_f16(k0, fq[ks][1], s, 0, 0, 0);
       s = __builtin_amdgcn_mfma_f32_32x32x16_f16(k0, fq[ks][0], s, 0, 0, 0);
     }
+    return s;
+  };
+  // online softmax of S^T (tile t) and O^T += V^T P'^T from the V pieces in piece stage t & 1
+  // (next: S^T of tile t + 1 is issued after the max / rescale, beside this tile's exponentials)
+  auto soft_pv = [&](f32x16 s, int t, bool next, f32x16& s_next) {
+    const unsigned char* pc = sP + (t & 1) * AD_PCS_B;
     if (ragged && t == nt - 1) {
 #pragma unroll
       for (int j = 0; j < 16; ++j)
@@ -1126,6 +1149,7 @@ __global__ void __launch_bounds__(64 * AD_WAVES) attn_fwd_f16x3d_kernel(AttnF32A
       m_run = m_new;
     }
     const float mc = m_run * c;
+    if (next) s_next = s_tile(t + 1);
     f16x8 fp[2][3];
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
@@ -1171,6 +1195,56 @@ __global__ void __launch_bounds__(64 * AD_WAVES) attn_fwd_f16x3d_kernel(AttnF32A
       acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v1h, fp[u][1], acc1, 0, 0, 0);
       acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v0h, fp[u][0], acc0, 0, 0, 0);
       acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v1h, fp[u][0], acc1, 0, 0, 0);
+    }
+  };
+
+  if constexpr (!PIPE) {
+    ad_dma_barrier();  // tile 0 (and 1) landed; sDim / sKmax cleared
+    split_k(0);
+    split_v(0);
+    for (int t = 0; t < nt; ++t) {
+      ad_dma_barrier();  // tile t + 1 landed; tile t's pieces written; every wave is past tile t - 1
+      if (t + 2 < nt) dma_tile(t + 2);
+      if (t + 1 < nt) {
+        split_k(t + 1);
+        split_v(t + 1);
+      }
+      if (!live) continue;
+      f32x16 unused;
+      soft_pv(s_tile(t), t, false, unused);
+    }
+  } else {
+    // K runs one tile ahead of V, so S^T of tile t + 1 is on the matrix cores while the softmax of
+    // tile t is on the vector ALUs.  Iteration t: DMA K(t + 3) and V(t + 2), split K(t + 2) and
+    // V(t + 1), S^T(t + 1), softmax and PV of tile t.  The raw stages are wave-private (each wave
+    // splits the rows its own DMAs wrote); the barrier at the top of iteration t publishes the
+    // pieces K(t + 1) / V(t) and retires every wave's reads of K(t) / V(t - 1), whose stages
+    // iteration t overwrites.  Same pieces, same MFMA order: bitwise-equal to PIPE = false.
+    ad_dma_barrier();  // K, V raw of tiles 0 and 1 landed; sDim / sKmax cleared
+    split_k(0);
+    split_v(0);
+    if (nt > 1) split_k(1);
+    if (nt > 2) dma_op(2, 0);  // K(2) into K stage 0 (this wave's own split of K(0) read it)
+    ad_dma_barrier();  // K pieces 0, 1 and V pieces 0 published; K(2) landed
+    f32x16 s_cur = {};
+    if (live) s_cur = s_tile(0);
+    for (int t = 0; t < nt - 1; ++t) {
+      ad_dma_barrier();
+      if (t + 3 < nt) dma_op(t + 3, 0);
+      if (t + 2 < nt) {
+        dma_op(t + 2, 1);
+        split_k(t + 2);
+      }
+      split_v(t + 1);
+      if (!live) continue;
+      f32x16 s_next;
+      soft_pv(s_cur, t, true, s_next);
+      s_cur = s_next;
+    }
+    ad_dma_barrier();  // V pieces of the last tile published
+    if (live) {
+      f32x16 unused;
+      soft_pv(s_cur, nt - 1, false, unused);
     }
   }
   // range check (the register-staged kernel's conditions): any |k|, |v| >= 2^15 or a non-finite
@@ -1392,15 +1466,20 @@ extern "C" int rmbx_attention_f16x3(const float* q, const float* k, const float*
   // SIMD), 5 = up to five groups (2 parts; one 5-wave block per CU, so one SIMD carries two waves
   // and three carry one): 1.41 vs 1.75 ms encoder self-attention at 1024 envs
   // (profiles/r4_attention_waves_ab.log)
-  // RMBX_ATTN_DMA (read per launch): 1 (default) = the LDS-DMA-staged kernel, 0 = the
-  // register-staged kernel
+  // RMBX_ATTN_DMA (read per launch): 2 (default) = the LDS-DMA-staged kernel with K one tile ahead
+  // of V (S^T of the next tile beside the softmax: 1.251 vs 1.277 ms encoder self-attention,
+  // profiles/r6_attn_dma_ab.log), 1 = the same kernel without the skew, 0 = the register-staged kernel
   const char* me = std::getenv("RMBX_ATTN_DMA");
-  if (!me || std::atoi(me) != 0) {
+  const int dma_form = me ? std::atoi(me) : 2;
+  if (dma_form != 0) {
     a.parts = (ngroups + rmbx::AD_WAVES - 1) / rmbx::AD_WAVES;
     const long long nb = (long long)B * heads * a.parts;
     RMBX_CHECK_ARG(nb < (1ll << 31), "rmbx_attention_f16x3: grid too large");
     const dim3 g((unsigned)nb), blk(64 * rmbx::AD_WAVES);
-    hipLaunchKernelGGL(rmbx::attn_fwd_f16x3d_kernel, g, blk, 0, (hipStream_t)stream, a);
+    if (dma_form == 2)
+      hipLaunchKernelGGL(rmbx::attn_fwd_f16x3d_kernel<true>, g, blk, 0, (hipStream_t)stream, a);
+    else
+      hipLaunchKernelGGL(rmbx::attn_fwd_f16x3d_kernel<false>, g, blk, 0, (hipStream_t)stream, a);
     RMBX_CHECK_LAUNCH();
     hipLaunchKernelGGL(rmbx::attn_fwd_f32x6_kernel, g, blk, 0, (hipStream_t)stream, a);
     RMBX_CHECK_LAUNCH();

@@ -1,5 +1,6 @@
 """A/B of the f16x3 attention's K / V staging: the register-staged kernel (RMBX_ATTN_DMA=0) vs the
-LDS-DMA-staged kernel (RMBX_ATTN_DMA=1), at the ACT shapes and 1024 envs, 8 heads:
+LDS-DMA-staged kernel (RMBX_ATTN_DMA=1) and its software-pipelined form (RMBX_ATTN_DMA=2, S^T of the
+next key tile beside the softmax), at the ACT shapes and 1024 envs, 8 heads:
 encoder self-attention 302 x 302, decoder cross-attention 100 x 302, decoder self-attention
 100 x 100.  Rounds interleaved in one process; min over rounds; the outputs of every variant are
 checked bitwise against the register-staged kernel's.
@@ -16,7 +17,8 @@ from robomanipbaselines_amd import kernels as K  # noqa: E402
 
 dev = "cuda"
 g = torch.Generator(device=dev).manual_seed(0)
-VARIANTS = (("register", {"RMBX_ATTN_DMA": "0"}), ("dma", {"RMBX_ATTN_DMA": "1"}))
+VARIANTS = (("register", {"RMBX_ATTN_DMA": "0"}), ("dma", {"RMBX_ATTN_DMA": "1"}),
+            ("dma+pipe", {"RMBX_ATTN_DMA": "2"}))
 
 
 def timeit(f, reps=10):
