@@ -915,7 +915,7 @@ __global__ void __launch_bounds__(64 * AX_MAX_WAVES) attn_fwd_f16x3_kernel(AttnF
 
 // ---------------------------------------------------------------------------------------------
 // f16x3 form with the key / value tiles staged by LDS-DMA (rmbx_attention_f16x3's default since
-// round 6, PIPE = true; RMBX_ATTN_DMA=0 selects the register-staged kernel above).  The register-staged kernel
+// round 6, PIPE = false; RMBX_ATTN_DMA=0 selects the register-staged kernel above).  The register-staged kernel
 // spends half its time staging (profiles/r5_attn_f16_phase_skips.log): the f32 tile loads into
 // registers one tile ahead, the split, and the V^T image written as 2-byte transposing stores.
 // Here, per 32-key tile:
@@ -964,21 +964,57 @@ __device__ __forceinline__ void ad_split8(float4 x0, float4 x1, f16x8& h, f16x8&
 __device__ __forceinline__ float ad_amax4(float m, float4 x) {
   return fmaxf(m, fmaxf(fmaxf(fabsf(x.x), fabsf(x.y)), fmaxf(fabsf(x.z), fabsf(x.w))));
 }
+// max(m, |x|, |y|) as one v_max3_f32 with source modifiers (fmaxf(m, fabsf(x)) also canonicalises
+// each input first, one more instruction per element; the values are the same)
+__device__ __forceinline__ float ad_max3abs(float m, float x, float y) {
+  float r;
+  asm("v_max3_f32 %0, |%1|, |%2|, %3" : "=v"(r) : "v"(x), "v"(y), "v"(m));
+  return r;
+}
+__device__ __forceinline__ float ad_maxabs(float m, float x) {
+  float r;
+  asm("v_max_f32_e64 %0, %1, |%2|" : "=v"(r) : "v"(m), "v"(x));
+  return r;
+}
+// s_waitcnt vmcnt(N) lgkmcnt(0), then the block barrier
+template <int N>
+__device__ __forceinline__ void ad_wait_barrier() {
+  asm volatile("s_waitcnt vmcnt(%0) lgkmcnt(0)\n\ts_barrier" ::"n"(N) : "memory");
+}
 typedef short ad_s4 __attribute__((ext_vector_type(4)));
 // 4 keys x 4 dims of a piece plane, delivered transposed across the 16-lane group (T10)
 __device__ __forceinline__ ad_s4 ad_tr(const unsigned char* p) {
   return __builtin_amdgcn_ds_read_tr16_b64_v4i16((__attribute__((address_space(3))) ad_s4*)p);
 }
 
-template <bool PIPE>
+// DBG (profiling phase skips of the PIPE form, RMBX_ATTN_F16_DBG with RMBX_ATTN_DMA=2; wrong results,
+// timing only): 1 = no splits in the loop, 2 = no softmax (the tile's S^T is not read), 4 = no DMA in
+// the loop, 8 = no S^T MFMAs, 16 = no PV MFMAs
+template <bool PIPE, int DBG = 0>
 __global__ void __launch_bounds__(64 * AD_WAVES) attn_fwd_f16x3d_kernel(AttnF32Args a) {
-  __shared__ __attribute__((aligned(16))) unsigned char sR[2 * AD_RAW_B];
+  // raw stages: 2, or 3 in the PIPE form (each DMA then has two key tiles of compute to land in);
+  // 3 x 16 + 2 x 16 KiB = 80 KiB, two blocks per CU, so the range statistics (sDim: per head
+  // dimension the max |v| over the keys, sKmax: the max |k|, f32 bits) take the raw ring's first
+  // bytes once the loop is done
+  constexpr int NR = PIPE ? 3 : 2;
+  __shared__ __attribute__((aligned(16))) unsigned char sR[NR * AD_RAW_B];
   __shared__ __attribute__((aligned(16))) unsigned char sP[2 * AD_PCS_B];
-  __shared__ uint32_t sDim[64];  // per head dimension: max |v| over the keys (f32 bits)
-  __shared__ uint32_t sKmax;     // max |k| over the block (f32 bits)
+  uint32_t* const sDim = reinterpret_cast<uint32_t*>(sR);
+  uint32_t* const sKmax = sDim + 64;
   const int tid = threadIdx.x, lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int bh = blockIdx.x / a.parts, part = blockIdx.x - bh * a.parts;
+  // block -> (head, query part): plain order, or (xcd_map) the parts of a head on one XCD in
+  // consecutive dispatch slots (block bid runs on XCD bid & 7), so the second and third parts'
+  // K / V DMAs hit that XCD's L2 instead of HBM
+  int bh, part;
+  if (a.xcd_map) {
+    const int j = blockIdx.x >> 3;
+    part = j % a.parts;
+    bh = (j / a.parts) * 8 + (blockIdx.x & 7);
+  } else {
+    bh = blockIdx.x / a.parts;
+    part = blockIdx.x - bh * a.parts;
+  }
   const int b = bh / a.heads, hd = bh - b * a.heads;
   const int r32 = lane & 31, kh = lane >> 5;
   const int q0 = (part * AD_WAVES + wave) * 32;  // the wave's first query (wave-uniform)
@@ -988,22 +1024,30 @@ __global__ void __launch_bounds__(64 * AD_WAVES) attn_fwd_f16x3d_kernel(AttnF32A
   const float* kbase = a.k + (size_t)b * a.k_bstride + hd * 64;
   const float* vbase = a.v + (size_t)b * a.v_bstride + hd * 64;
   const int nt = (a.Lk + 31) >> 5;
-  if (tid < 64) sDim[tid] = 0u;
-  if (tid == 0) sKmax = 0u;
+  auto stage = [](int t) { return PIPE ? t % 3 : t & 1; };
 
   const int dr = lane >> 4, dc = lane & 15;
-  // DMA of one operand's raw rows (k = 0: K, 1: V) of tile t into raw stage t & 1
+  // DMA of one operand's raw rows (k = 0: K, 1: V) of tile t into its raw stage: lane -> row
+  // 8 wave + 4 i + dr, 16-byte chunk dc ^ (row & 15); the per-lane offsets are formed once, the tile's
+  // row offset is wave-uniform, and only a ragged last tile clamps its rows to Lk - 1
+  long long doff[2][2];
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    const int r = 8 * wave + 4 * i + dr, c = dc ^ (r & 15);
+    doff[0][i] = (long long)r * a.k_rstride + 4 * c;
+    doff[1][i] = (long long)r * a.v_rstride + 4 * c;
+  }
   auto dma_op = [&](int t, int k) {
-    unsigned char* st = sR + (t & 1) * AD_RAW_B + k * 32 * 256;
+    unsigned char* st = sR + stage(t) * AD_RAW_B + k * 32 * 256;
     const float* base = k ? vbase : kbase;
     const long long rs = k ? a.v_rstride : a.k_rstride;
+    const bool clamp = 32 * t + 32 > a.Lk;  // (wave-uniform)
 #pragma unroll
     for (int i = 0; i < 2; ++i) {
       const int r0 = 8 * wave + 4 * i, r = r0 + dr;
-      int key = 32 * t + r;
-      key = key < a.Lk ? key : a.Lk - 1;
-      const int c = dc ^ (r & 15);
-      ad_glds16(base + (size_t)key * rs + 4 * c, st + r0 * 256);
+      long long o = (long long)(32 * t) * rs + doff[k][i];
+      if (clamp && 32 * t + r >= a.Lk) o = (long long)(a.Lk - 1) * rs + 4 * (dc ^ (r & 15));
+      ad_glds16(base + o, st + r0 * 256);
     }
   };
   auto dma_tile = [&](int t) {
@@ -1013,7 +1057,7 @@ __global__ void __launch_bounds__(64 * AD_WAVES) attn_fwd_f16x3d_kernel(AttnF32A
       int key = 32 * t + r;
       key = key < a.Lk ? key : a.Lk - 1;
       const int c = dc ^ (r & 15);
-      unsigned char* st = sR + (t & 1) * AD_RAW_B;
+      unsigned char* st = sR + stage(t) * AD_RAW_B;
       ad_glds16(kbase + (size_t)key * a.k_rstride + 4 * c, st + r0 * 256);
       ad_glds16(vbase + (size_t)key * a.v_rstride + 4 * c, st + 32 * 256 + r0 * 256);
     }
@@ -1024,12 +1068,12 @@ __global__ void __launch_bounds__(64 * AD_WAVES) attn_fwd_f16x3d_kernel(AttnF32A
   float kmx = 0.f;      // max |k| of this lane's elements
   float vmx[8] = {};    // max |v| of dims 8 jj + e over this lane's keys
   auto split_k = [&](int t) {
-    const unsigned char* raw = sR + (t & 1) * AD_RAW_B + rr * 256;
+    const unsigned char* raw = sR + stage(t) * AD_RAW_B + rr * 256;
     unsigned char* pcs = sP + (t & 1) * AD_PCS_B + rr * 128;
     const int sw = rr & 15;
     const float4 x0 = *reinterpret_cast<const float4*>(raw + (((2 * jj) ^ sw) << 4));
     const float4 x1 = *reinterpret_cast<const float4*>(raw + (((2 * jj + 1) ^ sw) << 4));
-    kmx = ad_amax4(ad_amax4(kmx, x0), x1);
+    kmx = ad_max3abs(ad_max3abs(ad_max3abs(ad_max3abs(kmx, x0.x, x0.y), x0.z, x0.w), x1.x, x1.y), x1.z, x1.w);
     f16x8 h, l;
     ad_split8(x0, x1, h, l);
     const int kc = jj ^ ((rr >> 1) & 7);
@@ -1037,19 +1081,19 @@ __global__ void __launch_bounds__(64 * AD_WAVES) attn_fwd_f16x3d_kernel(AttnF32A
     *reinterpret_cast<f16x8*>(pcs + AD_PLANE_B + (kc << 4)) = l;
   };
   auto split_v = [&](int t) {
-    const unsigned char* raw = sR + (t & 1) * AD_RAW_B + rr * 256;
+    const unsigned char* raw = sR + stage(t) * AD_RAW_B + rr * 256;
     unsigned char* pcs = sP + (t & 1) * AD_PCS_B + rr * 128;
     const int sw = rr & 15;
     const float4 y0 = *reinterpret_cast<const float4*>(raw + 32 * 256 + (((2 * jj) ^ sw) << 4));
     const float4 y1 = *reinterpret_cast<const float4*>(raw + 32 * 256 + (((2 * jj + 1) ^ sw) << 4));
-    vmx[0] = fmaxf(vmx[0], fabsf(y0.x));
-    vmx[1] = fmaxf(vmx[1], fabsf(y0.y));
-    vmx[2] = fmaxf(vmx[2], fabsf(y0.z));
-    vmx[3] = fmaxf(vmx[3], fabsf(y0.w));
-    vmx[4] = fmaxf(vmx[4], fabsf(y1.x));
-    vmx[5] = fmaxf(vmx[5], fabsf(y1.y));
-    vmx[6] = fmaxf(vmx[6], fabsf(y1.z));
-    vmx[7] = fmaxf(vmx[7], fabsf(y1.w));
+    vmx[0] = ad_maxabs(vmx[0], y0.x);
+    vmx[1] = ad_maxabs(vmx[1], y0.y);
+    vmx[2] = ad_maxabs(vmx[2], y0.z);
+    vmx[3] = ad_maxabs(vmx[3], y0.w);
+    vmx[4] = ad_maxabs(vmx[4], y1.x);
+    vmx[5] = ad_maxabs(vmx[5], y1.y);
+    vmx[6] = ad_maxabs(vmx[6], y1.z);
+    vmx[7] = ad_maxabs(vmx[7], y1.w);
     f16x8 h, l;
     ad_split8(y0, y1, h, l);
     const int vc = jj ^ (((rr >> 1) & 1) << 2);
@@ -1059,6 +1103,7 @@ __global__ void __launch_bounds__(64 * AD_WAVES) attn_fwd_f16x3d_kernel(AttnF32A
 
   dma_tile(0);
   if (nt > 1) dma_tile(1);
+  if (PIPE && nt > 2) dma_tile(2);
 
   // Q pieces as in the register-staged kernel (dims 16 s + 8 kh .. +7 of query qi, scaled by the
   // query's power of two 2^t; fq[s][2] = 2^-11 qh)
@@ -1118,16 +1163,66 @@ __global__ void __launch_bounds__(64 * AD_WAVES) attn_fwd_f16x3d_kernel(AttnF32A
       const int off = r32 * 128 + (((2 * ks + kh) ^ ((r32 >> 1) & 7)) << 4);
       const f16x8 k0 = *reinterpret_cast<const f16x8*>(pc + off);
       const f16x8 k1 = *reinterpret_cast<const f16x8*>(pc + AD_PLANE_B + off);
-      s = __builtin_amdgcn_mfma_f32_32x32x16_f16(k1, fq[ks][2], s, 0, 0, 0);
-      s = __builtin_amdgcn_mfma_f32_32x32x16_f16(k0, fq[ks][1], s, 0, 0, 0);
-      s = __builtin_amdgcn_mfma_f32_32x32x16_f16(k0, fq[ks][0], s, 0, 0, 0);
+      if constexpr (DBG & 8) {
+        s[ks] += (float)k0[0] + (float)k1[1];
+      } else {
+        s = __builtin_amdgcn_mfma_f32_32x32x16_f16(k1, fq[ks][2], s, 0, 0, 0);
+        s = __builtin_amdgcn_mfma_f32_32x32x16_f16(k0, fq[ks][1], s, 0, 0, 0);
+        s = __builtin_amdgcn_mfma_f32_32x32x16_f16(k0, fq[ks][0], s, 0, 0, 0);
+      }
     }
     return s;
+  };
+  // O^T += V^T P'^T from the V pieces at pc (V^T fragments of k-step u: elements 0-3 = keys
+  // 16 u + 4 kh + 0..3, elements 4-7 = keys 16 u + 8 + 4 kh + 0..3, the keys the P' registers hold)
+  auto pv_part = [&](const unsigned char* pc, const f16x8 (&fp)[2][3]) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      ad_s4 w[2][2][2];  // [key block][dims d / d + 32][piece]
+#pragma unroll
+      for (int k2 = 0; k2 < 2; ++k2) {
+        const int key = 16 * u + 8 * k2 + 4 * kh + vq;
+        const int fl = ((key >> 1) & 1) << 2;
+#pragma unroll
+        for (int dd = 0; dd < 2; ++dd) {
+          const int d = dv + 32 * dd;
+          const unsigned char* p = pc + 2 * AD_PLANE_B + key * 128 + ((((d >> 3) ^ fl) << 4) | ((d & 7) << 1));
+          w[k2][dd][0] = ad_tr(p);
+          w[k2][dd][1] = ad_tr(p + AD_PLANE_B);
+        }
+      }
+      auto cat = [](ad_s4 lo, ad_s4 hi) {
+        return __builtin_bit_cast(f16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
+      };
+      const f16x8 v0h = cat(w[0][0][0], w[1][0][0]), v0l = cat(w[0][0][1], w[1][0][1]);
+      const f16x8 v1h = cat(w[0][1][0], w[1][1][0]), v1l = cat(w[0][1][1], w[1][1][1]);
+      if constexpr ((DBG & 16) != 0) {
+        acc0[u] += (float)v0l[0] + (float)v1h[1] + (float)fp[u][2][0];
+        continue;
+      }
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v0l, fp[u][2], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v1l, fp[u][2], acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v0h, fp[u][1], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v1h, fp[u][1], acc1, 0, 0, 0);
+      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v0h, fp[u][0], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v1h, fp[u][0], acc1, 0, 0, 0);
+    }
   };
   // online softmax of S^T (tile t) and O^T += V^T P'^T from the V pieces in piece stage t & 1
   // (next: S^T of tile t + 1 is issued after the max / rescale, beside this tile's exponentials)
   auto soft_pv = [&](f32x16 s, int t, bool next, f32x16& s_next) {
     const unsigned char* pc = sP + (t & 1) * AD_PCS_B;
+    if constexpr ((DBG & 2) != 0) {
+      if (next) s_next = s_tile(t + 1);
+      f16x8 fp[2][3];
+#pragma unroll
+      for (int u = 0; u < 2; ++u)
+#pragma unroll
+        for (int i = 0; i < 3; ++i) fp[u][i] = fq[u][i];
+      l_run += s[0];
+      pv_part(pc, fp);
+      return;
+    }
     if (ragged && t == nt - 1) {
 #pragma unroll
       for (int j = 0; j < 16; ++j)
@@ -1167,35 +1262,7 @@ __global__ void __launch_bounds__(64 * AD_WAVES) attn_fwd_f16x3d_kernel(AttnF32A
       fp[u][1] = __builtin_bit_cast(f16x8, make_uint4(l[0], l[1], l[2], l[3]));
       fp[u][2] = fp[u][0] * (_Float16)0.00048828125f;
     }
-    // V^T fragments of k-step u: elements 0-3 = keys 16 u + 4 kh + 0..3, elements 4-7 = keys
-    // 16 u + 8 + 4 kh + 0..3 (the keys the P' registers they meet hold)
-#pragma unroll
-    for (int u = 0; u < 2; ++u) {
-      ad_s4 w[2][2][2];  // [key block][dims d / d + 32][piece]
-#pragma unroll
-      for (int k2 = 0; k2 < 2; ++k2) {
-        const int key = 16 * u + 8 * k2 + 4 * kh + vq;
-        const int fl = ((key >> 1) & 1) << 2;
-#pragma unroll
-        for (int dd = 0; dd < 2; ++dd) {
-          const int d = dv + 32 * dd;
-          const unsigned char* p = pc + 2 * AD_PLANE_B + key * 128 + ((((d >> 3) ^ fl) << 4) | ((d & 7) << 1));
-          w[k2][dd][0] = ad_tr(p);
-          w[k2][dd][1] = ad_tr(p + AD_PLANE_B);
-        }
-      }
-      auto cat = [](ad_s4 lo, ad_s4 hi) {
-        return __builtin_bit_cast(f16x8, __builtin_shufflevector(lo, hi, 0, 1, 2, 3, 4, 5, 6, 7));
-      };
-      const f16x8 v0h = cat(w[0][0][0], w[1][0][0]), v0l = cat(w[0][0][1], w[1][0][1]);
-      const f16x8 v1h = cat(w[0][1][0], w[1][1][0]), v1l = cat(w[0][1][1], w[1][1][1]);
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v0l, fp[u][2], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v1l, fp[u][2], acc1, 0, 0, 0);
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v0h, fp[u][1], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v1h, fp[u][1], acc1, 0, 0, 0);
-      acc0 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v0h, fp[u][0], acc0, 0, 0, 0);
-      acc1 = __builtin_amdgcn_mfma_f32_32x32x16_f16(v1h, fp[u][0], acc1, 0, 0, 0);
-    }
+    pv_part(pc, fp);
   };
 
   if constexpr (!PIPE) {
@@ -1215,27 +1282,42 @@ __global__ void __launch_bounds__(64 * AD_WAVES) attn_fwd_f16x3d_kernel(AttnF32A
     }
   } else {
     // K runs one tile ahead of V, so S^T of tile t + 1 is on the matrix cores while the softmax of
-    // tile t is on the vector ALUs.  Iteration t: DMA K(t + 3) and V(t + 2), split K(t + 2) and
-    // V(t + 1), S^T(t + 1), softmax and PV of tile t.  The raw stages are wave-private (each wave
-    // splits the rows its own DMAs wrote); the barrier at the top of iteration t publishes the
-    // pieces K(t + 1) / V(t) and retires every wave's reads of K(t) / V(t - 1), whose stages
+    // tile t is on the vector ALUs, and the raw ring has three stages, so a DMA lands while two key
+    // tiles compute.  Iteration t: DMA K(t + 4) and V(t + 3), split K(t + 2) and V(t + 1),
+    // S^T(t + 1), softmax and PV of tile t.  The raw stages are wave-private (each wave splits the
+    // rows its own DMAs wrote), so the wait at the top of iteration t covers only this wave's DMAs
+    // of iteration t - 2 and older (those of t - 1 stay in flight); the barrier publishes the pieces
+    // K(t + 1) / V(t) and retires every wave's reads of K(t) / V(t - 1), whose piece stages
     // iteration t overwrites.  Same pieces, same MFMA order: bitwise-equal to PIPE = false.
-    ad_dma_barrier();  // K, V raw of tiles 0 and 1 landed; sDim / sKmax cleared
+    ad_dma_barrier();  // K, V raw of tiles 0, 1, 2 landed
     split_k(0);
     split_v(0);
     if (nt > 1) split_k(1);
-    if (nt > 2) dma_op(2, 0);  // K(2) into K stage 0 (this wave's own split of K(0) read it)
-    ad_dma_barrier();  // K pieces 0, 1 and V pieces 0 published; K(2) landed
+    if (nt > 3) {
+      dma_op(3, 0);  // K(3) into stage 0 (this wave's own split of K(0) read it)
+      ad_wait_barrier<2>();  // K pieces 0, 1 and V pieces 0 published; K(3) in flight
+    } else {
+      ad_wait_barrier<0>();
+    }
     f32x16 s_cur = {};
     if (live) s_cur = s_tile(0);
     for (int t = 0; t < nt - 1; ++t) {
-      ad_dma_barrier();
-      if (t + 3 < nt) dma_op(t + 3, 0);
-      if (t + 2 < nt) {
-        dma_op(t + 2, 1);
-        split_k(t + 2);
+      // this wave's DMAs of iteration t - 1 (the prologue's K(3) for t = 0) may stay in flight
+      const int inflight = t == 0 ? (nt > 3 ? 2 : 0) : (t + 3 < nt ? 2 : 0) + (t + 2 < nt ? 2 : 0);
+      if (inflight == 4)
+        ad_wait_barrier<4>();
+      else if (inflight == 2)
+        ad_wait_barrier<2>();
+      else
+        ad_wait_barrier<0>();
+      if (!(DBG & 4)) {
+        if (t + 4 < nt) dma_op(t + 4, 0);  // into stage (t + 1) % 3: K(t + 1) was split at t - 1
+        if (t + 3 < nt) dma_op(t + 3, 1);  // into stage t % 3: V(t) was split at t - 1
       }
-      split_v(t + 1);
+      if (!(DBG & 1)) {
+        if (t + 2 < nt) split_k(t + 2);
+        split_v(t + 1);
+      }
       if (!live) continue;
       f32x16 s_next;
       soft_pv(s_cur, t, true, s_next);
@@ -1247,6 +1329,11 @@ __global__ void __launch_bounds__(64 * AD_WAVES) attn_fwd_f16x3d_kernel(AttnF32A
       soft_pv(s_cur, nt - 1, false, unused);
     }
   }
+  // the raw ring is dead (every DMA retired, every split done): its first bytes hold the range
+  // statistics
+  if (tid < 64) sDim[tid] = 0u;
+  if (tid < 2) sKmax[tid] = 0u;  // [0]: max |k|, [1]: the block's flag
+  __syncthreads();
   // range check (the register-staged kernel's conditions): any |k|, |v| >= 2^15 or a non-finite
   // query, the block's max |k| in (0, 2^-6), a dimension's max |v| over the keys in (0, 2^-6)
   float vm = 0.f;
@@ -1264,7 +1351,7 @@ __global__ void __launch_bounds__(64 * AD_WAVES) attn_fwd_f16x3d_kernel(AttnF32A
     for (int e = 0; e < 8; ++e)
       if (vmx[e] > 0.f) atomicMax(&sDim[8 * jj + e], __float_as_uint(vmx[e]));
   }
-  if (kmx > 0.f) atomicMax(&sKmax, __float_as_uint(kmx));
+  if (kmx > 0.f) atomicMax(sKmax, __float_as_uint(kmx));
   __syncthreads();
   bool flag = q_inf || kmx >= AH_BIG || vm >= AH_BIG;
   if (tid < 64) {
@@ -1272,11 +1359,15 @@ __global__ void __launch_bounds__(64 * AD_WAVES) attn_fwd_f16x3d_kernel(AttnF32A
     flag = flag || (m > 0.f && m < AH_TINY);
   }
   if (tid == 0) {
-    const float km = __uint_as_float(sKmax);
+    const float km = __uint_as_float(*sKmax);
     flag = flag || (km > 0.f && km < AH_TINY);
   }
-  const int any = __syncthreads_or(flag ? 1 : 0);
-  if (tid == 0) a.redo[blockIdx.x] = any;
+  // the block's OR of the flags through the LDS word sKmax[1] (__syncthreads_or would allocate
+  // 256 B of LDS for its reduction: two 80-KiB blocks per CU leave none)
+  if (__any(flag) && lane == 0) atomicOr(sKmax + 1, 1u);
+  __syncthreads();
+  const int any = sKmax[1] != 0u;
+  if (tid == 0) a.redo[bh * a.parts + part] = any;  // (the bf16x6 kernel's block order)
   if (any) return;
   const float l_tot = l_run + __shfl_xor(l_run, 32);
   if (!q_ok) return;
@@ -1466,19 +1557,36 @@ extern "C" int rmbx_attention_f16x3(const float* q, const float* k, const float*
   // SIMD), 5 = up to five groups (2 parts; one 5-wave block per CU, so one SIMD carries two waves
   // and three carry one): 1.41 vs 1.75 ms encoder self-attention at 1024 envs
   // (profiles/r4_attention_waves_ab.log)
-  // RMBX_ATTN_DMA (read per launch): 2 (default) = the LDS-DMA-staged kernel with K one tile ahead
-  // of V (S^T of the next tile beside the softmax: 1.251 vs 1.277 ms encoder self-attention,
-  // profiles/r6_attn_dma_ab.log), 1 = the same kernel without the skew, 0 = the register-staged kernel
+  // RMBX_ATTN_DMA (read per launch): 1 (default) = the LDS-DMA-staged kernel, 2 = the same kernel
+  // with K one tile ahead of V (S^T of the next tile beside the softmax) and a three-stage raw ring,
+  // 0 = the register-staged kernel.  Encoder self-attention at 1024 envs, one box
+  // (profiles/r6_attn_dma_ab.log): 1.371 (0) / 1.262 (1) / 1.219 (1, XCD) / 1.271 (2) / 1.241 ms (2, XCD)
+  // -- the skew only moves the MFMAs, and this kernel is not bound by them (phase skips,
+  // profiles/r6_attn_phases.log).  The DMA forms pair the parts of a head on one XCD unless
+  // RMBX_ATTN_XCD=0 (their K / V DMAs then hit L2 for the second and third parts)
   const char* me = std::getenv("RMBX_ATTN_DMA");
-  const int dma_form = me ? std::atoi(me) : 2;
+  const int dma_form = me ? std::atoi(me) : 1;
   if (dma_form != 0) {
     a.parts = (ngroups + rmbx::AD_WAVES - 1) / rmbx::AD_WAVES;
     const long long nb = (long long)B * heads * a.parts;
+    a.xcd_map = (!xe || std::atoi(xe) != 0) && a.parts > 1 && ((long long)B * heads) % 8 == 0;
     RMBX_CHECK_ARG(nb < (1ll << 31), "rmbx_attention_f16x3: grid too large");
     const dim3 g((unsigned)nb), blk(64 * rmbx::AD_WAVES);
-    if (dma_form == 2)
-      hipLaunchKernelGGL(rmbx::attn_fwd_f16x3d_kernel<true>, g, blk, 0, (hipStream_t)stream, a);
-    else
+    const char* de = std::getenv("RMBX_ATTN_F16_DBG");  // profiling phase skips (read per launch)
+    const int dbg = de ? std::atoi(de) : 0;
+    if (dma_form == 2) {
+      switch (dbg) {
+        case 0: hipLaunchKernelGGL((rmbx::attn_fwd_f16x3d_kernel<true, 0>), g, blk, 0, (hipStream_t)stream, a); break;
+        case 1: hipLaunchKernelGGL((rmbx::attn_fwd_f16x3d_kernel<true, 1>), g, blk, 0, (hipStream_t)stream, a); break;
+        case 2: hipLaunchKernelGGL((rmbx::attn_fwd_f16x3d_kernel<true, 2>), g, blk, 0, (hipStream_t)stream, a); break;
+        case 4: hipLaunchKernelGGL((rmbx::attn_fwd_f16x3d_kernel<true, 4>), g, blk, 0, (hipStream_t)stream, a); break;
+        case 8: hipLaunchKernelGGL((rmbx::attn_fwd_f16x3d_kernel<true, 8>), g, blk, 0, (hipStream_t)stream, a); break;
+        case 16: hipLaunchKernelGGL((rmbx::attn_fwd_f16x3d_kernel<true, 16>), g, blk, 0, (hipStream_t)stream, a); break;
+        case 24: hipLaunchKernelGGL((rmbx::attn_fwd_f16x3d_kernel<true, 24>), g, blk, 0, (hipStream_t)stream, a); break;
+        case 5: hipLaunchKernelGGL((rmbx::attn_fwd_f16x3d_kernel<true, 5>), g, blk, 0, (hipStream_t)stream, a); break;
+        default: RMBX_CHECK_ARG(false, "rmbx_attention_f16x3: RMBX_ATTN_F16_DBG=%d not instantiated", dbg);
+      }
+    } else
       hipLaunchKernelGGL(rmbx::attn_fwd_f16x3d_kernel<false>, g, blk, 0, (hipStream_t)stream, a);
     RMBX_CHECK_LAUNCH();
     hipLaunchKernelGGL(rmbx::attn_fwd_f32x6_kernel, g, blk, 0, (hipStream_t)stream, a);

@@ -1,6 +1,6 @@
 """A/B of the f16x3 attention's K / V staging: the register-staged kernel (RMBX_ATTN_DMA=0) vs the
 LDS-DMA-staged kernel (RMBX_ATTN_DMA=1) and its software-pipelined form (RMBX_ATTN_DMA=2, S^T of the
-next key tile beside the softmax), at the ACT shapes and 1024 envs, 8 heads:
+next key tile beside the softmax), each with the parts of a head on one XCD (RMBX_ATTN_XCD=1), at the ACT shapes and 1024 envs, 8 heads:
 encoder self-attention 302 x 302, decoder cross-attention 100 x 302, decoder self-attention
 100 x 100.  Rounds interleaved in one process; min over rounds; the outputs of every variant are
 checked bitwise against the register-staged kernel's.
@@ -17,8 +17,11 @@ from robomanipbaselines_amd import kernels as K  # noqa: E402
 
 dev = "cuda"
 g = torch.Generator(device=dev).manual_seed(0)
-VARIANTS = (("register", {"RMBX_ATTN_DMA": "0"}), ("dma", {"RMBX_ATTN_DMA": "1"}),
-            ("dma+pipe", {"RMBX_ATTN_DMA": "2"}))
+VARIANTS = (("register", {"RMBX_ATTN_DMA": "0", "RMBX_ATTN_XCD": "0"}),
+            ("dma", {"RMBX_ATTN_DMA": "1", "RMBX_ATTN_XCD": "0"}),
+            ("dma+xcd", {"RMBX_ATTN_DMA": "1", "RMBX_ATTN_XCD": "1"}),
+            ("dma+pipe", {"RMBX_ATTN_DMA": "2", "RMBX_ATTN_XCD": "0"}),
+            ("dma+pipe+xcd", {"RMBX_ATTN_DMA": "2", "RMBX_ATTN_XCD": "1"}))
 
 
 def timeit(f, reps=10):
@@ -50,3 +53,4 @@ with torch.no_grad():
               flush=True)
         del q, k, v, outs
 os.environ.pop("RMBX_ATTN_DMA", None)
+os.environ.pop("RMBX_ATTN_XCD", None)
