@@ -384,6 +384,34 @@ int rmbx_render_scene(const rmbx_camera* cam, const rmbx_scene_tables* scene, co
                       int nbody, uint8_t* rgb, float* depth, int32_t* hit_geom, void* policy_img,
                       int policy_dtype, const uint8_t* active, int n_env, void* stream);
 
+/* Static-background cache of one camera (rmbx_render_scene_cached; the caller keeps one per
+ * camera and image size).  A primitive is static when its body is welded to the world
+ * (prim_static [nprim] = 1; static_prims [nstatic] their indices); for a camera whose pose does not
+ * change either (a world camera: the rollout's policy camera), every pixel whose nearest surface
+ * among the static primitives is drawn once per episode: cache u32 [n_env][H][W][2] (8-byte
+ * aligned) = (its camera depth bits, 8-bit rgb | primitive << 24; primitive 0xff: none) is rebuilt
+ * for an env whenever the camera body's pose or a static primitive's pose differs from the snapshot
+ * snap f64 [n_env][7 + 12 nstatic] (caller-initialised to NaN: the first call builds every cache)
+ * it was built from; dirty u8 [n_env] is workspace.  Each call then casts only the other primitives
+ * and the meshes against the cached depth and primitive (the same nearest-hit order: meshes keep
+ * ties, primitives by index), so every output (rgb, depth, hit_geom, policy) equals
+ * rmbx_render_scene's, which is this call with cache NULL.  RMBX_RENDER_CACHE=0 ignores the
+ * cache. */
+typedef struct rmbx_render_cache {
+  const uint8_t* prim_static;
+  const int32_t* static_prims;
+  int32_t nstatic;
+  uint32_t* cache;
+  double* snap;
+  uint8_t* dirty;
+} rmbx_render_cache;
+
+int rmbx_render_scene_cached(const rmbx_camera* cam, const rmbx_scene_tables* scene, const double* gxpos,
+                             const double* gxmat, const double* xpos, const double* xquat, int ngeom,
+                             int nbody, uint8_t* rgb, float* depth, int32_t* hit_geom, void* policy_img,
+                             int policy_dtype, const uint8_t* active, int n_env,
+                             const rmbx_render_cache* cache, void* stream);
+
 /* ---------------------------------------------------------------------------------------------
  * Policy vision-trunk epilogues (ResNet-18 with frozen BN folded into the convs), NHWC.
  * Replace the per-element tail of torchvision's BasicBlock / stem as used by ACT's DETR backbone

@@ -58,6 +58,8 @@ SIGNATURES = {
                              _c_int, _c_p, _c_int, _c_p]),
     "rmbx_render_scene": (_c_int, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_int, _c_int, _c_p, _c_p, _c_p, _c_p,
                                    _c_int, _c_p, _c_int, _c_p]),
+    "rmbx_render_scene_cached": (_c_int, [_c_p, _c_p, _c_p, _c_p, _c_p, _c_p, _c_int, _c_int, _c_p, _c_p, _c_p,
+                                          _c_p, _c_int, _c_p, _c_int, _c_p, _c_p]),
     "rmbx_nhwc_bias_act": (_c_int, [_c_p] * 5 + [_c_sz, _c_int, _c_int, _c_int, _c_p]),
     "rmbx_nhwc_bias_relu_maxpool": (_c_int, [_c_p] * 3 + [_c_int] * 5 + [_c_p]),
     "rmbx_conv2d_nhwc": (_c_int, [_c_p] * 5 + [_c_int] * 10 + [_c_p]),
@@ -134,6 +136,13 @@ class SceneTables(ctypes.Structure):
                 ("nmesh", ctypes.c_int32), ("mesh_tri", _c_p), ("mesh_body", _c_p), ("mesh_rad", _c_p), ("vis", _c_p),
                 ("tflag", _c_p), ("geom_texid", _c_p), ("geom_matinfo", _c_p), ("tex_rgba", _c_p), ("tex_desc", _c_p),
                 ("tex_level_adr", _c_p), ("ntex", ctypes.c_int32), ("sky_rgb", ctypes.c_float * 6)]
+
+
+class RenderCache(ctypes.Structure):
+    """ctypes mirror of rmbx_render_cache (include/rmbx.h)."""
+
+    _fields_ = [("prim_static", _c_p), ("static_prims", _c_p), ("nstatic", ctypes.c_int32), ("cache", _c_p),
+                ("snap", _c_p), ("dirty", _c_p)]
 
 
 class EnvBuffers(ctypes.Structure):

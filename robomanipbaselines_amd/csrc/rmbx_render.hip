@@ -238,6 +238,12 @@ struct RenderArgs {
   const int4* tex_desc;
   const int32_t* tex_level_adr;
   float sky[6];
+  // static-background cache (rmbx_render_scene_cached; null: none): prim_static [nprim] 1 for a
+  // primitive of a body welded to the world; cache [n][H][W] = (depth bits, rgb | prim << 24) of the
+  // static-only scene (prim 0xff: none); dirty [n]: 1 where the cache is rebuilt this call
+  const uint8_t* prim_static;
+  uint2* cache;
+  const uint8_t* dirty;
 };
 
 // one texel (RGBA8 word, R in the low byte) as floats in [0, 1]
@@ -663,7 +669,10 @@ __global__ void __launch_bounds__(RASTER_THREADS) raster_kernel(RenderArgs a, in
 #ifndef RMBX_RENDER_MINW
 #define RMBX_RENDER_MINW 8
 #endif
-template <bool VIS>
+// CM: 0 = no cache (every primitive in one pass), 1 = the envs whose cache is valid, 2 = the envs
+// whose cache is rebuilt this call (rmbx_render_scene_cached launches 1 and 2 over all envs; each
+// block of the other kind returns at once)
+template <bool VIS, int CM>
 __global__ void __launch_bounds__(256, RMBX_RENDER_MINW) render_kernel(RenderArgs a) {
   __shared__ PrimCam prims[MAX_PRIM];
   __shared__ int order[MAX_PRIM];        // the block's primitives sorted front to back, once
@@ -671,12 +680,18 @@ __global__ void __launch_bounds__(256, RMBX_RENDER_MINW) render_kernel(RenderArg
   __shared__ int wcount[4];
   __shared__ CamFrame cf;
   __shared__ float mR[VIS ? MAX_MESH : 1][9];  // mesh slots' body rotations in the camera frame
+  __shared__ uint8_t pstat[MAX_PRIM];          // cached modes: 1 for a static primitive
   const int ntiles = a.tiles_x * a.tiles_y;
   const int env = blockIdx.x / a.groups;
   const int grp = blockIdx.x % a.groups;
   if (env >= a.n_env) return;
   if (a.active && !a.active[env]) return;
   const int tid = threadIdx.x;
+  // 0: no cache (every primitive in one pass); 1: the env's cache is valid (the static scene comes
+  // from it, only the other primitives are cast); 2: the cache is rebuilt (a static-only pass writes
+  // it, then the mode-1 pass)
+  constexpr int mode = CM;
+  if (CM != 0 && (a.dirty[env] != 0) != (CM == 2)) return;
   const int W = a.cam.width, H = a.cam.height;
   const float tanh_ = tanf(0.5f * a.cam.fovy_deg * 3.14159265358979f / 180.0f);
   const float aspect = (float)W / (float)H;
@@ -789,6 +804,7 @@ __global__ void __launch_bounds__(256, RMBX_RENDER_MINW) render_kernel(RenderArg
       if (r > 0.f) P.zmin = fmaxf(P.zmin, r * cos_max * (1.0f - 1e-5f) - 1e-5f);
     }
     prims[p] = P;
+    pstat[p] = mode ? a.prim_static[p] : 0;
   }
   __syncthreads();
   // order the primitives front to back by the depth bound (ties by index) once per block: a tile
@@ -836,6 +852,7 @@ __global__ void __launch_bounds__(256, RMBX_RENDER_MINW) render_kernel(RenderArg
       // the projected box against the tile's slope rectangle
       if (P.sx_hi < x_lo || P.sx_lo > x_hi || P.sy_hi < y_lo || P.sy_lo > y_hi) keep = false;
     }
+    if (mode == 1 && pstat[p_cull]) keep = false;  // (the cache holds the static scene)
   }
   // compact the survivors in sorted order: ballot per wave, wave offsets through LDS
   const unsigned long long kb = __ballot(keep);
@@ -855,10 +872,11 @@ __global__ void __launch_bounds__(256, RMBX_RENDER_MINW) render_kernel(RenderArg
   if (px < W && py < H) {
   const float d[3] = {((2.0f * (px + 0.5f) / W) - 1.0f) * tanh_ * aspect,
                       (1.0f - 2.0f * (py + 0.5f) / H) * tanh_, -1.0f};
-  float best = 1e30f, bn[3] = {0, 0, 1}, brgb[3] = {0.f, 0.f, 0.f};
-  int bp = -1, bgeom = -1;  // the winning primitive / surface geom (-2: a primitive, resolved below)
   const size_t pix = (size_t)py * W + px;
   const size_t hw = (size_t)H * W;
+  // the mesh candidate (the visibility pass's nearest triangle), kept for the final pass
+  float m_best = 1e30f, m_n[3] = {0, 0, 1}, m_rgb[3] = {0.f, 0.f, 0.f};
+  int m_geom = -1;
   if constexpr (VIS) {
     // the pixel's nearest mesh triangle from the visibility pass
     const unsigned long long key = tile_vis ? a.vis[(size_t)env * hw + pix] : VIS_EMPTY;
@@ -868,21 +886,59 @@ __global__ void __launch_bounds__(256, RMBX_RENDER_MINW) render_kernel(RenderArg
       const float4* tp = reinterpret_cast<const float4*>(a.mesh_tri) + 4 * (size_t)j;
       const float4 C = tp[2], D = tp[3];
       const int tag = __float_as_int(D.x), k = tag >> 16;
-      best = __uint_as_float((unsigned)(key >> 32));
-      bgeom = tag & 0xffff;
-      brgb[0] = D.y;
-      brgb[1] = D.z;
-      brgb[2] = D.w;
+      m_best = __uint_as_float((unsigned)(key >> 32));
+      m_geom = tag & 0xffff;
+      m_rgb[0] = D.y;
+      m_rgb[1] = D.z;
+      m_rgb[2] = D.w;
       const float nl[3] = {C.y, C.z, C.w};
-      for (int i = 0; i < 3; i++) bn[i] = mR[k][3 * i] * nl[0] + mR[k][3 * i + 1] * nl[1] + mR[k][3 * i + 2] * nl[2];
+      for (int i = 0; i < 3; i++) m_n[i] = mR[k][3 * i] * nl[0] + mR[k][3 * i + 1] * nl[1] + mR[k][3 * i + 2] * nl[2];
     }
+  }
+  // the static scene's candidate (mode 1: from the cache; mode 2: from pass 0): depth, primitive
+  // (0xff: none), 8-bit colour
+  float c_t = 1e30f;
+  unsigned c_p = 0xffu, c_rgb = 0u;
+  if (mode == 1) {
+    const uint2 ce = a.cache[(size_t)env * hw + pix];
+    c_t = __uint_as_float(ce.x);
+    c_p = ce.y >> 24;
+    c_rgb = ce.y & 0xffffffu;
   }
   const int cnt = tile_cnt;
   int ntest = 0;
+  float best, bn[3], brgb[3], col[3], depth;
+  int bp, bgeom;  // the winning primitive / surface geom (-2: a primitive, -3: the cached static scene)
+  uint8_t u[3];
+  // one pass (modes 0, 1) or two (mode 2: the static-only scene into the cache, then the rest); a
+  // single instance of the ray loop and the shading serves every pass, so the cached colours are
+  // the ones the one-pass form computes
+  auto pixel_pass = [&](const int pass) {
+  if (pass == 0) {
+    best = 1e30f;
+    bgeom = -1;
+    bn[0] = bn[1] = 0.f;
+    bn[2] = 1.f;
+    brgb[0] = brgb[1] = brgb[2] = 0.f;
+  } else {
+    best = m_best;
+    bgeom = m_geom;
+    for (int i = 0; i < 3; i++) {
+      bn[i] = m_n[i];
+      brgb[i] = m_rgb[i];
+    }
+  }
+  bp = -1;
+  if (pass == 1 && c_p != 0xffu && c_t < best) {  // (a triangle at the same depth keeps the pixel)
+    best = c_t;
+    bp = (int)c_p;
+    bgeom = -3;
+  }
   for (int k = 0; k < ((a.dbg & 1) ? 0 : cnt); k++) {
     const int p = tile_sorted[k];
     const PrimCam& P = prims[p];
     if (P.zmin > best + 1e-4f) break;  // every later primitive lies behind the current hit
+    if (mode == 2 && (pass == 0) != (pstat[p] != 0)) continue;  // pass 0: static only; pass 1: the others
     ++ntest;
     float o_l[3], d_l[3], t, nl[3];
     to_local(P, d, o_l, d_l);
@@ -904,17 +960,21 @@ __global__ void __launch_bounds__(256, RMBX_RENDER_MINW) render_kernel(RenderArg
     }
   }
   const bool prim_won = bgeom == -2;
+  const bool cached = bgeom == -3;
+  if (cached) bgeom = a.prim_i32[4 * bp];
   if (prim_won) {  // a primitive won: its geom and material colour
     bgeom = a.prim_i32[4 * bp];
     brgb[0] = prims[bp].rgb[0];
     brgb[1] = prims[bp].rgb[1];
     brgb[2] = prims[bp].rgb[2];
   }
-  float col[3];
-  float depth = a.cam.zfar;
+  depth = a.cam.zfar;
   const float inv = rsqrtf(dot3f(d, d));
   const float vd[3] = {d[0] * inv, d[1] * inv, d[2] * inv};
-  if (bgeom < 0) {
+  if (cached) {  // the cached static scene: its 8-bit colour as the shading below made it
+    depth = best;
+    col[0] = col[1] = col[2] = 0.f;
+  } else if (bgeom < 0) {
     if (a.geom_matinfo) {
       // the gradient skybox: rgb2 (down) to rgb1 (up) by the ray's world z
       const float wz = cf.R[6] * vd[0] + cf.R[7] * vd[1] + cf.R[8] * vd[2];
@@ -968,9 +1028,27 @@ __global__ void __launch_bounds__(256, RMBX_RENDER_MINW) render_kernel(RenderArg
     }
     depth = best;  // d has unit -z component: t is the camera-z distance
   }
+  if (cached) {
+    u[0] = (uint8_t)(c_rgb & 255u);
+    u[1] = (uint8_t)((c_rgb >> 8) & 255u);
+    u[2] = (uint8_t)(c_rgb >> 16);
+  } else {
+    for (int i = 0; i < 3; i++) u[i] = (uint8_t)(col[i] * 255.0f + 0.5f);
+  }
+  if (pass == 0) {  // the static-only scene of this pixel: into the cache and the final pass
+    c_t = best;
+    c_p = bp >= 0 ? (unsigned)bp : 0xffu;
+    c_rgb = (unsigned)u[0] | ((unsigned)u[1] << 8) | ((unsigned)u[2] << 16);
+    a.cache[(size_t)env * hw + pix] = make_uint2(__float_as_uint(c_t), c_rgb | (c_p << 24));
+  }
+  };  // pixel_pass
+  if constexpr (CM == 2) {
+#pragma nounroll
+    for (int pass = 0; pass < 2; ++pass) pixel_pass(pass);
+  } else {
+    pixel_pass(1);
+  }
   const bool do_store = !(a.dbg & 2) || col[0] == 12345.f;  // (diagnostic: keep the shading live)
-  uint8_t u[3];
-  for (int i = 0; i < 3; i++) u[i] = (uint8_t)(col[i] * 255.0f + 0.5f);
   if (a.rgb && do_store) {
     uint8_t* o = a.rgb + ((size_t)env * hw + pix) * 3;
     o[0] = u[0];
@@ -1023,12 +1101,39 @@ __global__ void __launch_bounds__(256, RMBX_RENDER_MINW) render_kernel(RenderArg
   }  // tiles
 }
 
+// Static-background cache validity, one wave per env: the camera body's pose and every static
+// primitive's pose are compared (exactly) with the snapshot the env's cache was built from; any
+// difference (or the NaN snapshot of a new cache) marks the env dirty -- its render pass rebuilds
+// the cache -- and takes the new snapshot.
+__global__ void __launch_bounds__(64) render_cache_check_kernel(RenderArgs a, const int32_t* static_prims,
+                                                               int nstatic, double* snap, uint8_t* dirty) {
+  const int env = blockIdx.x;
+  if (a.active && !a.active[env]) return;
+  const int n = 7 + 12 * nstatic, body = a.cam.body;
+  double* sn = snap + (size_t)env * n;
+  auto value = [&](int i) -> double {
+    if (i < 3) return a.xpos[((size_t)env * a.nbody + body) * 3 + i];
+    if (i < 7) return a.xquat[((size_t)env * a.nbody + body) * 4 + i - 3];
+    const int j = (i - 7) / 12, k = (i - 7) - 12 * j;
+    const int g = a.prim_i32[4 * static_prims[j]];
+    return k < 3 ? a.gxpos[((size_t)env * a.ngeom + g) * 3 + k] : a.gxmat[((size_t)env * a.ngeom + g) * 9 + k - 3];
+  };
+  bool diff = false;
+  for (int i = threadIdx.x; i < n; i += 64) diff = diff || !(value(i) == sn[i]);
+  const bool any = __any(diff);
+  if (any)
+    for (int i = threadIdx.x; i < n; i += 64) sn[i] = value(i);
+  if (threadIdx.x == 0) dirty[env] = any ? 1 : 0;
+}
+
 }  // namespace rmbx
 
-extern "C" int rmbx_render_scene(const rmbx_camera* cam, const rmbx_scene_tables* scene, const double* gxpos,
-                                 const double* gxmat, const double* xpos, const double* xquat, int ngeom,
-                                 int nbody, uint8_t* rgb, float* depth, int32_t* hit_geom, void* policy_img,
-                                 int policy_dtype, const uint8_t* active, int n_env, void* stream) {
+extern "C" int rmbx_render_scene_cached(const rmbx_camera* cam, const rmbx_scene_tables* scene,
+                                        const double* gxpos, const double* gxmat, const double* xpos,
+                                        const double* xquat, int ngeom, int nbody, uint8_t* rgb, float* depth,
+                                        int32_t* hit_geom, void* policy_img, int policy_dtype,
+                                        const uint8_t* active, int n_env, const rmbx_render_cache* cache,
+                                        void* stream) {
   RMBX_CHECK_ARG(cam && scene && scene->prim_i32 && scene->prim_f32 && gxpos && gxmat && xpos && xquat,
                  "NULL argument");
   RMBX_CHECK_ARG(scene->nprim > 0 && scene->nprim <= MAX_PRIM, "nprim=%d outside [1, %d]", scene->nprim, MAX_PRIM);
@@ -1081,6 +1186,21 @@ extern "C" int rmbx_render_scene(const rmbx_camera* cam, const rmbx_scene_tables
   a.tex_desc = reinterpret_cast<const int4*>(scene->tex_desc);
   a.tex_level_adr = scene->tex_level_adr;
   for (int i = 0; i < 6; i++) a.sky[i] = scene->sky_rgb[i];
+  a.prim_static = nullptr;
+  a.cache = nullptr;
+  a.dirty = nullptr;
+  const char* cache_env = std::getenv("RMBX_RENDER_CACHE");  // 0: render every pixel in full (A/B)
+  const bool use_cache = cache && cache->nstatic > 0 && !(cache_env && std::atoi(cache_env) == 0);
+  if (use_cache) {
+    RMBX_CHECK_ARG(cache->prim_static && cache->static_prims && cache->cache && cache->snap && cache->dirty &&
+                       ((uintptr_t)cache->cache & 7) == 0 && cache->nstatic <= scene->nprim,
+                   "rmbx_render_scene_cached: bad cache (null pointer, unaligned cache or nstatic=%d > nprim=%d)",
+                   cache->nstatic, scene->nprim);
+    RMBX_CHECK_ARG(cam->body >= 0 && cam->body < nbody && xpos && xquat, "rmbx_render_scene_cached: bad camera body");
+    a.prim_static = cache->prim_static;
+    a.cache = reinterpret_cast<uint2*>(cache->cache);
+    a.dirty = cache->dirty;
+  }
   a.tiles_x = (cam->width + RENDER_TILE - 1) / RENDER_TILE;
   a.tiles_y = (cam->height + RENDER_TILE - 1) / RENDER_TILE;
   a.groups = 16;
@@ -1089,6 +1209,11 @@ extern "C" int rmbx_render_scene(const rmbx_camera* cam, const rmbx_scene_tables
   const size_t nblocks = (size_t)n_env * a.groups;
   RMBX_CHECK_ARG(nblocks < (1ull << 31), "grid too large");
   hipStream_t st = reinterpret_cast<hipStream_t>(stream);
+  if (use_cache) {
+    hipLaunchKernelGGL(rmbx::render_cache_check_kernel, dim3((unsigned)n_env), dim3(64), 0, st, a,
+                       cache->static_prims, (int)cache->nstatic, cache->snap, cache->dirty);
+    RMBX_CHECK_LAUNCH();
+  }
   if (meshes) {
     // pass 1: the meshes' nearest triangle per pixel into the visibility buffer (empty on entry:
     // the ray-cast pass clears every key and tile flag it consumes)
@@ -1097,12 +1222,30 @@ extern "C" int rmbx_render_scene(const rmbx_camera* cam, const rmbx_scene_tables
     RMBX_CHECK_ARG(rblocks < (1ull << 31), "raster grid too large");
     hipLaunchKernelGGL(rmbx::raster_kernel, dim3((unsigned)rblocks), dim3(RASTER_THREADS), 0, st, a, chunks);
     RMBX_CHECK_LAUNCH();
-    hipLaunchKernelGGL(rmbx::render_kernel<true>, dim3((unsigned)nblocks), dim3(256), 0, st, a);
+    if (use_cache) {
+      hipLaunchKernelGGL((rmbx::render_kernel<true, 1>), dim3((unsigned)nblocks), dim3(256), 0, st, a);
+      RMBX_CHECK_LAUNCH();
+      hipLaunchKernelGGL((rmbx::render_kernel<true, 2>), dim3((unsigned)nblocks), dim3(256), 0, st, a);
+    } else {
+      hipLaunchKernelGGL((rmbx::render_kernel<true, 0>), dim3((unsigned)nblocks), dim3(256), 0, st, a);
+    }
+  } else if (use_cache) {
+    hipLaunchKernelGGL((rmbx::render_kernel<false, 1>), dim3((unsigned)nblocks), dim3(256), 0, st, a);
+    RMBX_CHECK_LAUNCH();
+    hipLaunchKernelGGL((rmbx::render_kernel<false, 2>), dim3((unsigned)nblocks), dim3(256), 0, st, a);
   } else {
-    hipLaunchKernelGGL(rmbx::render_kernel<false>, dim3((unsigned)nblocks), dim3(256), 0, st, a);
+    hipLaunchKernelGGL((rmbx::render_kernel<false, 0>), dim3((unsigned)nblocks), dim3(256), 0, st, a);
   }
   RMBX_CHECK_LAUNCH();
   return RMBX_OK;
+}
+
+extern "C" int rmbx_render_scene(const rmbx_camera* cam, const rmbx_scene_tables* scene, const double* gxpos,
+                                 const double* gxmat, const double* xpos, const double* xquat, int ngeom,
+                                 int nbody, uint8_t* rgb, float* depth, int32_t* hit_geom, void* policy_img,
+                                 int policy_dtype, const uint8_t* active, int n_env, void* stream) {
+  return rmbx_render_scene_cached(cam, scene, gxpos, gxmat, xpos, xquat, ngeom, nbody, rgb, depth, hit_geom,
+                                  policy_img, policy_dtype, active, n_env, nullptr, stream);
 }
 
 extern "C" int rmbx_render(const rmbx_camera* cam, const int32_t* prim_i32, const float* prim_f32,

@@ -160,6 +160,17 @@ class Renderer:
             for i, v in enumerate(np.asarray(arrays["sky_rgb"], np.float64).reshape(-1)):
                 sc.sky_rgb[i] = float(v)
         self._scene = sc
+        # static-background caches (rmbx_render_scene_cached): the primitives of bodies welded to the
+        # world, one cache per world-fixed camera (allocated at its first render)
+        if "body_weldid" in arrays and self.nprim:
+            weld, gbody = np.asarray(arrays["body_weldid"]), np.asarray(arrays["geom_body"])
+            mocap = set(int(b) for b in np.asarray(arrays["body_mocapid"]).nonzero()[0]) if "body_mocapid" in arrays else set()
+            stat = np.array([1 if weld[gbody[g]] == 0 and int(gbody[g]) not in mocap else 0 for g in pi[:, 0]], np.uint8)
+        else:
+            stat = np.zeros(self.nprim, np.uint8)
+        self.prim_static = torch.tensor(stat, device=device) if self.nprim else None
+        self.static_prims = torch.tensor(np.nonzero(stat)[0].astype(np.int32), device=device)
+        self._caches = {}
         self.width, self.height = width, height
         self.cam_names = [str(x) for x in arrays["names_cam"]]
         self.znear = float(arrays["_znear"]) * float(arrays["_extent"])
@@ -181,6 +192,26 @@ class Renderer:
             c.mean[k] = IMAGENET_MEAN[k]
             c.std[k] = IMAGENET_STD[k]
         return c
+
+    def _cache(self, camera_name, cam, n):
+        """The static-background cache of a world-fixed camera (include/rmbx.h rmbx_render_cache), or
+        None (a camera on a moving body, a scene without static primitives)."""
+        nst = int(self.static_prims.numel())
+        weld = self.arrays["body_weldid"] if "body_weldid" in self.arrays else None
+        if nst == 0 or weld is None or int(np.asarray(weld)[cam.body]) != 0:
+            return None
+        H, W = self.height, self.width
+        ent = self._caches.get(camera_name)
+        if ent is None or ent[0] != (n, H, W):
+            buf = torch.empty(n * H * W * 2, dtype=torch.int32, device=self.device)
+            snap = torch.full((n * (7 + 12 * nst),), float("nan"), dtype=torch.float64, device=self.device)
+            dirty = torch.zeros(n, dtype=torch.uint8, device=self.device)
+            c = N.RenderCache()
+            c.prim_static, c.static_prims, c.nstatic = self.prim_static.data_ptr(), self.static_prims.data_ptr(), nst
+            c.cache, c.snap, c.dirty = buf.data_ptr(), snap.data_ptr(), dirty.data_ptr()
+            ent = ((n, H, W), c, buf, snap, dirty)
+            self._caches[camera_name] = ent
+        return ent[1]
 
     def render(self, engine, camera_name, rgb=None, depth=None, policy=None, active=None, mean=None, std=None,
                hit_geom=None):
@@ -216,11 +247,12 @@ class Renderer:
                 self._vis = torch.full((n * H * W,), -1, dtype=torch.int64, device=self.device)
                 self._tflag = torch.zeros(n * ntiles, dtype=torch.uint8, device=self.device)
             self._scene.vis, self._scene.tflag = self._vis.data_ptr(), self._tflag.data_ptr()
+        cache = self._cache(camera_name, cam, n)
         try:
-            N.call("rmbx_render_scene", ctypes.byref(cam), ctypes.byref(self._scene),
+            N.call("rmbx_render_scene_cached", ctypes.byref(cam), ctypes.byref(self._scene),
                    N.ptr(engine.gxpos), N.ptr(engine.gxmat), N.ptr(engine.xpos), N.ptr(engine.xquat),
                    engine.ngeom, engine.nbody, N.ptr(rgb), N.ptr(depth), N.ptr(hit_geom), N.ptr(policy), pdt,
-                   N.ptr(active), n, N.stream_ptr())
+                   N.ptr(active), n, ctypes.byref(cache) if cache is not None else None, N.stream_ptr())
         except BaseException:
             # the ray-cast pass is what empties the workspaces again: if the call failed after the
             # visibility pass wrote them (or was interrupted between the launches), empty them here

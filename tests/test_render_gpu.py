@@ -143,3 +143,61 @@ def test_rerender_after_motion_equals_a_fresh_renderer():
         for a, b in zip(again, fresh):
             assert torch.equal(a, b), cam
         assert not torch.equal(before[2], again[2]), cam  # the arm moved in the frame
+
+
+@torch.no_grad()
+def test_static_background_cache_equals_the_full_render(monkeypatch):
+    """The static-background cache (rmbx_render_scene_cached: the primitives of bodies welded to the
+    world drawn once per world-fixed camera and reused while their poses and the camera's hold)
+    gives bitwise the frames of the full render (RMBX_RENDER_CACHE=0) -- rgb, depth, hit geom and the
+    policy tensors -- when the cache is built, when it is reused after the arm moved, and when one
+    env's static primitive moved (that env alone rebuilds it); the hand camera (on a moving body)
+    keeps no cache."""
+    env = _env_states()
+    eng, rnd = env.engine, env.renderer
+    n, H, W = eng.n_env, rnd.height, rnd.width
+    assert int(rnd.static_prims.numel()) > 0
+
+    def frame(cam, cached):
+        monkeypatch.setenv("RMBX_RENDER_CACHE", "1" if cached else "0")
+        rgb = torch.empty((n, H, W, 3), dtype=torch.uint8, device=DEV)
+        depth = torch.empty((n, H, W), dtype=torch.float32, device=DEV)
+        hit = torch.empty((n, H, W), dtype=torch.int32, device=DEV)
+        s2d = torch.empty((n, H // 2, W // 2, 16), dtype=torch.uint8, device=DEV)
+        chw = torch.empty((n, 3, H, W), dtype=torch.float32, device=DEV)
+        rnd.render(eng, cam, rgb=rgb, depth=depth, hit_geom=hit)
+        ent = rnd._caches.get(cam)
+        dirty = ent[4].tolist() if (cached and ent is not None) else None  # the first call's rebuilds
+        rnd.render(eng, cam, policy=s2d)
+        rnd.render(eng, cam, policy=chw)
+        torch.cuda.synchronize()
+        return (rgb, depth, hit, s2d, chw), dirty
+
+    def check(cam, what):
+        (got, dirty), (want, _) = frame(cam, True), frame(cam, False)
+        for name, a, b in zip(("rgb", "depth", "hit_geom", "s2d", "chw"), got, want):
+            assert torch.equal(a, b), (cam, what, name, int((a != b).sum()))
+        return dirty
+
+    stat_geom = int(rnd.prim_i32[rnd.static_prims[-1], 0])
+    for cam in env.camera_names:
+        world_cam = int(env.arrays["body_weldid"][int(env.arrays["cam_body"][env.camera_names.index(cam)])]) == 0
+        eng.forward()  # (undoes the previous camera's moved primitive before this camera's cache is built)
+        dirty = check(cam, "cache built")
+        assert (dirty is not None) == world_cam, cam
+        if world_cam:
+            assert dirty == [1, 1, 1], cam  # every cache built on first use
+        q = eng.qpos.clone()
+        q[:, :6] += torch.tensor([0.2, -0.15, 0.2, 0.3, -0.2, 0.4], dtype=torch.float64, device=DEV)
+        eng.qpos.copy_(q)
+        eng.forward()
+        dirty = check(cam, "arm moved")
+        if world_cam:
+            assert dirty == [0, 0, 0], cam  # no env rebuilt its cache: only the arm moved
+        eng.gxpos[1, stat_geom, 0] += 0.05  # one env's static primitive moves (a modify_world)
+        dirty = check(cam, "static primitive moved")
+        if world_cam:
+            assert dirty == [0, 1, 0], cam
+        dirty = check(cam, "after the rebuild")
+        if world_cam:
+            assert dirty == [0, 0, 0], cam
