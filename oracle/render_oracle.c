@@ -8,8 +8,8 @@
  * documented contract): primitives in their frame (world = R local + c: a geom's gxpos / gxmat, a
  * body's meshes in the body's xpos / xquat, each triangle carrying its geom id and colour);
  * plane = local z = 0, unbounded; sphere / capsule / cylinder / box as MuJoCo sizes them; a camera
- * inside a primitive sees none of it; hits at t <= 1e-4 ignored; triangles two-sided and clipped at
- * t <= znear; nearest hit wins.  Shading 0.1 + 0.6 |n.v| + 0.3 max(0, n_z) (normal turned to the
+ * inside a primitive sees none of it; hits at t <= 1e-4 ignored; triangles one-sided (back faces
+ * culled: MuJoCo's default mjRND_CULL_FACE) and clipped at t <= znear; nearest hit wins.  Shading 0.1 + 0.6 |n.v| + 0.3 max(0, n_z) (normal turned to the
  * viewer, light along world -z), times the material colour, clamped at 1; background (0.9, 1, 1);
  * with materials (round 6) the colour times the primitive's texture sample (2d / cube, trilinear
  * over the mip pyramid, level of detail from the pixel's isotropic footprint) plus the emission, the light's
@@ -141,6 +141,10 @@ static int hit_box(const double* o, const double* d, const double* s, double* t,
    geom id), rgb */
 static int hit_tri(const double* o, const double* d, const float* tr, double tmin, double* t) {
   const double v0[3] = {tr[0], tr[1], tr[2]}, e1[3] = {tr[3], tr[4], tr[5]}, e2[3] = {tr[6], tr[7], tr[8]};
+  /* back faces are culled (MuJoCo's default mjRND_CULL_FACE, OpenGL counter-clockwise front faces):
+     a triangle whose winding normal e1 x e2 does not point towards the eye is not drawn */
+  const double nw[3] = {e1[1] * e2[2] - e1[2] * e2[1], e1[2] * e2[0] - e1[0] * e2[2], e1[0] * e2[1] - e1[1] * e2[0]};
+  if (nw[0] * (o[0] - v0[0]) + nw[1] * (o[1] - v0[1]) + nw[2] * (o[2] - v0[2]) <= 0) return 0;
   const double p[3] = {d[1] * e2[2] - d[2] * e2[1], d[2] * e2[0] - d[0] * e2[2], d[0] * e2[1] - d[1] * e2[0]};
   const double det = dot3(e1, p);
   if (fabs(det) < 1e-300) return 0;

@@ -230,7 +230,8 @@ struct RenderArgs {
   int groups;  // blocks per env (each renders a contiguous range of tiles)
   int dbg;     // diagnostic (RMBX_RENDER_DBG; 0 in production): 1 no ray loop, 2 no stores, 4 test counts, 8 sphere
                // bounds only; visibility-pass timing probes: 16 frames only, 32 + set-up, 64 + ray tests, no writes;
-               // materials: 128 textures at the base level only, 256 no texture sampling, 512 no footprint
+               // materials: 128 textures at the base level only, 256 no texture sampling, 512 no footprint;
+               // 1024: back faces drawn (the round-5 two-sided triangles; A/B only)
   // materials (NULL geom_matinfo: the flat round-5 shading); include/rmbx.h rmbx_scene_tables
   const int32_t* geom_texid;
   const float* geom_matinfo;
@@ -456,6 +457,16 @@ __device__ __forceinline__ void tri_setup(const RenderArgs& a, const float4* tp,
     T.e2[i] = R[3 * i] * l2[0] + R[3 * i + 1] * l2[1] + R[3 * i + 2] * l2[2];
   }
   const int W = a.cam.width, H = a.cam.height;
+  T.x0 = 1;
+  T.x1 = 0;
+  T.y0 = T.y1 = 0;
+  {
+    // back faces are culled (MuJoCo's default mjRND_CULL_FACE, OpenGL counter-clockwise front
+    // faces): the winding normal e1 x e2 must point towards the eye at the origin
+    const float nw[3] = {T.e1[1] * T.e2[2] - T.e1[2] * T.e2[1], T.e1[2] * T.e2[0] - T.e1[0] * T.e2[2],
+                         T.e1[0] * T.e2[1] - T.e1[1] * T.e2[0]};
+    if (!(nw[0] * T.v0[0] + nw[1] * T.v0[1] + nw[2] * T.v0[2] < 0.f) && !(a.dbg & 1024)) return;
+  }
   const float znear = a.cam.znear;
   const float fx = 0.5f * W / (tanh_ * aspect), fy = 0.5f * H / tanh_;
   const float P[3][3] = {{T.v0[0], T.v0[1], T.v0[2]},

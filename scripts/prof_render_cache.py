@@ -46,3 +46,21 @@ for rnd in range(3):
     print(json.dumps({"round": rnd, "bitwise_equal": same}), flush=True)
 for k, v in res.items():
     print(json.dumps({"mode": k, "ms_per_call": round(min(v), 3)}), flush=True)
+# back-face culling (default) vs the two-sided triangles of round 5 (RMBX_RENDER_DBG=1024): time of
+# the full render and the share of pixels whose surface changes
+os.environ["RMBX_RENDER_CACHE"] = "0"
+hg = torch.empty((n, H, W), dtype=torch.int32, device="cuda:0")
+rgb = torch.empty((n, H, W, 3), dtype=torch.uint8, device="cuda:0")
+out = {}
+for name, dbg in (("culled", "0"), ("two_sided", "1024")):
+    os.environ["RMBX_RENDER_DBG"] = dbg
+    env.render_images("front", policy=pol)
+    t = min(timed(lambda: env.render_images("front", policy=pol)) for _ in range(3))
+    env.renderer.render(env.engine, "front", rgb=rgb, hit_geom=hg)
+    torch.cuda.synchronize()
+    out[name] = (t, hg.clone(), rgb.clone())
+os.environ["RMBX_RENDER_DBG"] = "0"
+os.environ["RMBX_RENDER_CACHE"] = "1"
+print(json.dumps({"full_ms_culled": round(out["culled"][0], 3), "full_ms_two_sided": round(out["two_sided"][0], 3),
+                  "pixels_surface_changed": float((out["culled"][1] != out["two_sided"][1]).float().mean()),
+                  "pixels_rgb_changed": float((out["culled"][2] != out["two_sided"][2]).any(-1).float().mean())}), flush=True)

@@ -1,7 +1,7 @@
 """Known answers pinning the renderer oracle (oracle/render_oracle.c): the restatement the GPU
 renderer is checked against (tests/test_render_gpu.py) is itself checked here against closed-form
 ray intersections of each primitive type and of a triangle mesh, the near-plane clip of
-triangles, the nearest-hit rule, the camera pose from body and camera frames, and the shading
+triangles, back-face culling, the nearest-hit rule, the camera pose from body and camera frames, and the shading
 formula, on a synthetic scene (no GPU)."""
 
 import numpy as np
@@ -90,6 +90,18 @@ def test_triangles_hit_and_near_clip():
     g, d, _ = _cast(a, pos, gm, np.array([[W / 2 + 3.3, H / 2 - 2.1]]))
     assert g[0] == 0
     np.testing.assert_allclose(d[0], 1.5, atol=1e-12)
+
+
+def test_back_faces_are_culled():
+    # the same square wound clockwise as seen from the camera (its winding normal points away): not
+    # drawn, as MuJoCo's default mjRND_CULL_FACE; the sphere behind it is seen through it
+    sq = [[[-0.5, -0.5, -1.5], [0.5, 0.5, -1.5], [0.5, -0.5, -1.5]], [[-0.5, -0.5, -1.5], [-0.5, 0.5, -1.5], [0.5, 0.5, -1.5]]]
+    a, pos, gm = _scene([(2, (0.2, 0, 0), (0, 0, -3.0), (1, 0, 0))], tris=sq)
+    g, d, _ = _cast(a, pos, gm, CENTRE)
+    assert g[0] == 0 and abs(d[0] - 2.8) < 1e-12
+    a, pos, gm = _scene([(2, (0.2, 0, 0), (0, 0, -3.0), (1, 0, 0))], tris=[[t[0], t[2], t[1]] for t in sq])
+    g, d, _ = _cast(a, pos, gm, CENTRE)
+    assert g[0] == 1 and abs(d[0] - 1.5) < 1e-12  # wound counter-clockwise: the square
 
 
 def test_camera_pose_from_the_camera_quaternion():
