@@ -952,12 +952,33 @@ __device__ __forceinline__ void ad_glds16(const float* gsrc, const void* lds_dst
 // all of this wave's LDS-DMAs landed, then the block barrier (no __syncthreads: its fence is not
 // needed for LDS and would be placed by the compiler without the DMAs in view)
 __device__ __forceinline__ void ad_dma_barrier() { asm volatile("s_waitcnt vmcnt(0) lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+// x - f32(h) for the f16 in the low / high half of packed h, exactly (v_fma_mix_f32 reads the f16
+// operand in place: one instruction instead of converting h back and subtracting)
+__device__ __forceinline__ float ad_rem_lo(uint32_t h, float x) {
+  float r;
+  asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h), "v"(x));
+  return r;
+}
+__device__ __forceinline__ float ad_rem_hi(uint32_t h, float x) {
+  float r;
+  asm("v_fma_mix_f32 %0, %1, -1.0, %2 op_sel:[1,0,0] op_sel_hi:[1,0,0]" : "=v"(r) : "v"(h), "v"(x));
+  return r;
+}
+// ah_split_a / ah_split_w with the remainders formed by v_fma_mix_f32 (the same bits)
+__device__ __forceinline__ void ad_split_a(float x, float y, uint32_t& h, uint32_t& l) {
+  h = ah_pk(x, y);
+  l = ah_pk(ad_rem_lo(h, x) * 2048.f, ad_rem_hi(h, y) * 2048.f);
+}
+__device__ __forceinline__ void ad_split_w(float x, float y, uint32_t& h, uint32_t& l) {
+  h = ah_pk(x, y);
+  l = ah_pk(ad_rem_lo(h, x), ad_rem_hi(h, y));
+}
 __device__ __forceinline__ void ad_split8(float4 x0, float4 x1, f16x8& h, f16x8& l) {
   uint32_t hh[4], ll[4];
-  ah_split_a(x0.x, x0.y, hh[0], ll[0]);
-  ah_split_a(x0.z, x0.w, hh[1], ll[1]);
-  ah_split_a(x1.x, x1.y, hh[2], ll[2]);
-  ah_split_a(x1.z, x1.w, hh[3], ll[3]);
+  ad_split_a(x0.x, x0.y, hh[0], ll[0]);
+  ad_split_a(x0.z, x0.w, hh[1], ll[1]);
+  ad_split_a(x1.x, x1.y, hh[2], ll[2]);
+  ad_split_a(x1.z, x1.w, hh[3], ll[3]);
   h = __builtin_bit_cast(f16x8, make_uint4(hh[0], hh[1], hh[2], hh[3]));
   l = __builtin_bit_cast(f16x8, make_uint4(ll[0], ll[1], ll[2], ll[3]));
 }
@@ -1256,7 +1277,7 @@ __global__ void __launch_bounds__(64 * AD_WAVES) attn_fwd_f16x3d_kernel(AttnF32A
         const float pa = __builtin_amdgcn_exp2f(fmaf(s[8 * u + 2 * e], c, -mc)) * 16384.f;
         const float pb = __builtin_amdgcn_exp2f(fmaf(s[8 * u + 2 * e + 1], c, -mc)) * 16384.f;
         l_run += pa + pb;
-        ah_split_w(pa, pb, h[e], l[e]);
+        ad_split_w(pa, pb, h[e], l[e]);
       }
       fp[u][0] = __builtin_bit_cast(f16x8, make_uint4(h[0], h[1], h[2], h[3]));
       fp[u][1] = __builtin_bit_cast(f16x8, make_uint4(l[0], l[1], l[2], l[3]));
@@ -1560,7 +1581,7 @@ extern "C" int rmbx_attention_f16x3(const float* q, const float* k, const float*
   // RMBX_ATTN_DMA (read per launch): 1 (default) = the LDS-DMA-staged kernel, 2 = the same kernel
   // with K one tile ahead of V (S^T of the next tile beside the softmax) and a three-stage raw ring,
   // 0 = the register-staged kernel.  Encoder self-attention at 1024 envs, one box
-  // (profiles/r6_attn_dma_ab.log): 1.371 (0) / 1.262 (1) / 1.219 (1, XCD) / 1.271 (2) / 1.241 ms (2, XCD)
+  // (profiles/r6_attn_dma_ab.log): 1.373 (0) / 1.225 (1) / 1.193 (1, XCD) / 1.241 (2) / 1.194 ms (2, XCD)
   // -- the skew only moves the MFMAs, and this kernel is not bound by them (phase skips,
   // profiles/r6_attn_phases.log).  The DMA forms pair the parts of a head on one XCD unless
   // RMBX_ATTN_XCD=0 (their K / V DMAs then hit L2 for the second and third parts)
