@@ -608,18 +608,23 @@ def weight_bounds(w, b):
     return wn * up, bm * up
 
 
-def linear_presplit_split(xs, planes, bias, bounds, relu=False):
+def linear_presplit_split(xs, planes, bias, bounds, relu=False, out=None):
     """relu?(x @ W^T + bias) from pre-split rows xs (PresplitRows with norm bounds) to pre-split rows
     (rmbx_linear_f16x3_presplit_split): the FFN's first Linear, whose output only feeds the second.
-    bounds = weight_bounds(W, bias)."""
+    bounds = weight_bounds(W, bias); out (optional): the PresplitRows to write ([2, M, N] planes and
+    [M] rinv, row-slice views allowed)."""
     Nn, K, h3 = _planes_nk(planes, "linear_presplit_split")
     if not h3 or xs.norm is None or xs.planes.shape[2] != K:
         raise ValueError("linear_presplit_split: f16x3 planes and pre-split rows with norm bounds of width K")
     M = xs.planes.shape[1]
     if bias is not None:
         _chk(bias, torch.float32, (Nn,), "bias")
-    out = PresplitRows(torch.empty((2, M, Nn), dtype=torch.float16, device=xs.planes.device),
-                       torch.empty(M, dtype=torch.float32, device=xs.planes.device))
+    if out is None:
+        out = PresplitRows(torch.empty((2, M, Nn), dtype=torch.float16, device=xs.planes.device),
+                           torch.empty(M, dtype=torch.float32, device=xs.planes.device))
+    elif (tuple(out.planes.shape) != (2, M, Nn) or out.planes.dtype != torch.float16 or out.planes.stride(2) != 1
+          or tuple(out.rinv.shape) != (M,) or out.rinv.dtype != torch.float32 or not out.rinv.is_contiguous()):
+        raise ValueError("linear_presplit_split: out must hold [2, M, N] f16 planes (unit column stride) and [M] f32 rinv")
     p, ap, op = planes.planes, xs.planes, out.planes
     _gemm_launch(f"linear M={M} N={Nn} K={K} presplit->split", 2.0 * M * Nn * K, 4 * M * K + 4 * Nn * K + 4 * M * Nn, 3,
                  "rmbx_linear_f16x3_presplit_split", N.ptr(ap), ap.stride(1), ap.stride(0), N.ptr(xs.rinv),
@@ -629,15 +634,19 @@ def linear_presplit_split(xs, planes, bias, bounds, relu=False):
     return out
 
 
-def linear_presplit(xs, planes, bias=None, relu=False):
-    """relu?(x @ W^T + bias) f32 [M, N] from pre-split rows xs (rmbx_linear_f16x3_presplit)."""
+def linear_presplit(xs, planes, bias=None, relu=False, out=None):
+    """relu?(x @ W^T + bias) f32 [M, N] from pre-split rows xs (rmbx_linear_f16x3_presplit); out
+    (optional): the f32 [M, N] rows to write (unit column stride)."""
     Nn, K, h3 = _planes_nk(planes, "linear_presplit")
     if not h3 or xs.planes.shape[2] != K or Nn % LINEAR_F32X6_BN != 0:
         raise ValueError("linear_presplit: f16x3 planes, N % 128 == 0 and pre-split rows of width K")
     M = xs.planes.shape[1]
     if bias is not None:
         _chk(bias, torch.float32, (Nn,), "bias")
-    out = torch.empty((M, Nn), dtype=torch.float32, device=xs.planes.device)
+    if out is None:
+        out = torch.empty((M, Nn), dtype=torch.float32, device=xs.planes.device)
+    elif tuple(out.shape) != (M, Nn) or out.dtype != torch.float32 or out.stride(1) != 1:
+        raise ValueError("linear_presplit: out must be f32 [M, N] with unit column stride")
     p, ap = planes.planes, xs.planes
     _gemm_launch(f"linear M={M} N={Nn} K={K} presplit", 2.0 * M * Nn * K, 4 * M * K + 4 * Nn * K + 4 * M * Nn, 3,
                  "rmbx_linear_f16x3_presplit", N.ptr(ap), ap.stride(1), ap.stride(0), N.ptr(xs.rinv), N.ptr(p),
