@@ -915,7 +915,7 @@ __global__ void __launch_bounds__(64 * AX_MAX_WAVES) attn_fwd_f16x3_kernel(AttnF
 
 // ---------------------------------------------------------------------------------------------
 // f16x3 form with the key / value tiles staged by LDS-DMA (rmbx_attention_f16x3's default since
-// round 6, PIPE = false; RMBX_ATTN_DMA=0 selects the register-staged kernel above).  The register-staged kernel
+// round 6: PIPE = false, ONE = true; RMBX_ATTN_DMA=0 selects the register-staged kernel above).  The register-staged kernel
 // spends half its time staging (profiles/r5_attn_f16_phase_skips.log): the f32 tile loads into
 // registers one tile ahead, the split, and the V^T image written as 2-byte transposing stores.
 // Here, per 32-key tile:
@@ -1011,13 +1011,18 @@ __device__ __forceinline__ ad_s4 ad_tr(const unsigned char* p) {
 // DBG (profiling phase skips of the PIPE form, RMBX_ATTN_F16_DBG with RMBX_ATTN_DMA=2; wrong results,
 // timing only): 1 = no splits in the loop, 2 = no softmax (the tile's S^T is not read), 4 = no DMA in
 // the loop, 8 = no S^T MFMAs, 16 = no PV MFMAs
-template <bool PIPE, int DBG = 0>
-__global__ void __launch_bounds__(64 * AD_WAVES) attn_fwd_f16x3d_kernel(AttnF32Args a) {
+// ONE (with PIPE = false): a single raw stage -- each wave splits tile t + 1 from it, then DMAs tile
+// t + 2 into the rows it just read, so the DMA still lands under a tile of compute -- 48 KiB of LDS
+// and at most 168 registers: three blocks (three waves per SIMD) per CU instead of two
+template <bool PIPE, int DBG = 0, bool ONE = false>
+__global__ void __launch_bounds__(64 * AD_WAVES) __attribute__((amdgpu_waves_per_eu(ONE ? 3 : 1)))
+attn_fwd_f16x3d_kernel(AttnF32Args a) {
   // raw stages: 2, or 3 in the PIPE form (each DMA then has two key tiles of compute to land in);
   // 3 x 16 + 2 x 16 KiB = 80 KiB, two blocks per CU, so the range statistics (sDim: per head
   // dimension the max |v| over the keys, sKmax: the max |k|, f32 bits) take the raw ring's first
   // bytes once the loop is done
-  constexpr int NR = PIPE ? 3 : 2;
+  static_assert(!(PIPE && ONE), "the single-stage form is the plain (PIPE = false) loop");
+  constexpr int NR = PIPE ? 3 : (ONE ? 1 : 2);
   __shared__ __attribute__((aligned(16))) unsigned char sR[NR * AD_RAW_B];
   __shared__ __attribute__((aligned(16))) unsigned char sP[2 * AD_PCS_B];
   uint32_t* const sDim = reinterpret_cast<uint32_t*>(sR);
@@ -1045,7 +1050,7 @@ __global__ void __launch_bounds__(64 * AD_WAVES) attn_fwd_f16x3d_kernel(AttnF32A
   const float* kbase = a.k + (size_t)b * a.k_bstride + hd * 64;
   const float* vbase = a.v + (size_t)b * a.v_bstride + hd * 64;
   const int nt = (a.Lk + 31) >> 5;
-  auto stage = [](int t) { return PIPE ? t % 3 : t & 1; };
+  auto stage = [](int t) { return PIPE ? t % 3 : (ONE ? 0 : t & 1); };
 
   const int dr = lane >> 4, dc = lane & 15;
   // DMA of one operand's raw rows (k = 0: K, 1: V) of tile t into its raw stage: lane -> row
@@ -1123,7 +1128,7 @@ __global__ void __launch_bounds__(64 * AD_WAVES) attn_fwd_f16x3d_kernel(AttnF32A
   };
 
   dma_tile(0);
-  if (nt > 1) dma_tile(1);
+  if (!ONE && nt > 1) dma_tile(1);
   if (PIPE && nt > 2) dma_tile(2);
 
   // Q pieces as in the register-staged kernel (dims 16 s + 8 kh .. +7 of query qi, scaled by the
@@ -1286,7 +1291,23 @@ __global__ void __launch_bounds__(64 * AD_WAVES) attn_fwd_f16x3d_kernel(AttnF32A
     pv_part(pc, fp);
   };
 
-  if constexpr (!PIPE) {
+  if constexpr (ONE) {
+    ad_dma_barrier();  // tile 0 landed
+    split_k(0);
+    split_v(0);
+    if (nt > 1) dma_tile(1);  // into the rows this wave's split just read
+    for (int t = 0; t < nt; ++t) {
+      ad_dma_barrier();  // tile t + 1 landed; tile t's pieces written; every wave is past tile t - 1
+      if (t + 1 < nt) {
+        split_k(t + 1);
+        split_v(t + 1);
+        if (t + 2 < nt) dma_tile(t + 2);
+      }
+      if (!live) continue;
+      f32x16 unused;
+      soft_pv(s_tile(t), t, false, unused);
+    }
+  } else if constexpr (!PIPE) {
     ad_dma_barrier();  // tile 0 (and 1) landed; sDim / sKmax cleared
     split_k(0);
     split_v(0);
@@ -1578,15 +1599,17 @@ extern "C" int rmbx_attention_f16x3(const float* q, const float* k, const float*
   // SIMD), 5 = up to five groups (2 parts; one 5-wave block per CU, so one SIMD carries two waves
   // and three carry one): 1.41 vs 1.75 ms encoder self-attention at 1024 envs
   // (profiles/r4_attention_waves_ab.log)
-  // RMBX_ATTN_DMA (read per launch): 1 (default) = the LDS-DMA-staged kernel, 2 = the same kernel
-  // with K one tile ahead of V (S^T of the next tile beside the softmax) and a three-stage raw ring,
-  // 0 = the register-staged kernel.  Encoder self-attention at 1024 envs, one box
-  // (profiles/r6_attn_dma_ab.log): 1.373 (0) / 1.225 (1) / 1.193 (1, XCD) / 1.241 (2) / 1.194 ms (2, XCD)
-  // -- the skew only moves the MFMAs, and this kernel is not bound by them (phase skips,
-  // profiles/r6_attn_phases.log).  The DMA forms pair the parts of a head on one XCD unless
-  // RMBX_ATTN_XCD=0 (their K / V DMAs then hit L2 for the second and third parts)
+  // RMBX_ATTN_DMA (read per launch): 3 (default) = the LDS-DMA-staged kernel with one raw stage
+  // (48 KiB, <= 168 registers: three blocks per CU), 1 = the same with two raw stages (64 KiB, two
+  // blocks per CU), 2 = two-stage with K one tile ahead of V (S^T of the next tile beside the
+  // softmax) and a three-stage raw ring, 0 = the register-staged kernel.  Encoder self-attention at
+  // 1024 envs, one box (profiles/r6_attn_dma_ab.log): 1.397 (0) / 1.227 (1) / 1.233 (2) / 1.095 ms (3),
+  // each DMA form with XCD pairing -- the kernel is latency-bound (each phase skip saves 0.15-0.25 ms
+  // of 1.24, profiles/r6_attn_phases.log), so the third block per CU pays and the skew does not.
+  // The DMA forms pair the parts of a head on one XCD unless RMBX_ATTN_XCD=0 (their K / V DMAs then
+  // hit L2 for the second and third parts)
   const char* me = std::getenv("RMBX_ATTN_DMA");
-  const int dma_form = me ? std::atoi(me) : 1;
+  const int dma_form = me ? std::atoi(me) : 3;
   if (dma_form != 0) {
     a.parts = (ngroups + rmbx::AD_WAVES - 1) / rmbx::AD_WAVES;
     const long long nb = (long long)B * heads * a.parts;
@@ -1607,8 +1630,11 @@ extern "C" int rmbx_attention_f16x3(const float* q, const float* k, const float*
         case 5: hipLaunchKernelGGL((rmbx::attn_fwd_f16x3d_kernel<true, 5>), g, blk, 0, (hipStream_t)stream, a); break;
         default: RMBX_CHECK_ARG(false, "rmbx_attention_f16x3: RMBX_ATTN_F16_DBG=%d not instantiated", dbg);
       }
-    } else
+    } else if (dma_form == 3) {
+      hipLaunchKernelGGL((rmbx::attn_fwd_f16x3d_kernel<false, 0, true>), g, blk, 0, (hipStream_t)stream, a);
+    } else {
       hipLaunchKernelGGL(rmbx::attn_fwd_f16x3d_kernel<false>, g, blk, 0, (hipStream_t)stream, a);
+    }
     RMBX_CHECK_LAUNCH();
     hipLaunchKernelGGL(rmbx::attn_fwd_f32x6_kernel, g, blk, 0, (hipStream_t)stream, a);
     RMBX_CHECK_LAUNCH();

@@ -21,7 +21,9 @@ VARIANTS = (("register", {"RMBX_ATTN_DMA": "0", "RMBX_ATTN_XCD": "0"}),
             ("dma", {"RMBX_ATTN_DMA": "1", "RMBX_ATTN_XCD": "0"}),
             ("dma+xcd", {"RMBX_ATTN_DMA": "1", "RMBX_ATTN_XCD": "1"}),
             ("dma+pipe", {"RMBX_ATTN_DMA": "2", "RMBX_ATTN_XCD": "0"}),
-            ("dma+pipe+xcd", {"RMBX_ATTN_DMA": "2", "RMBX_ATTN_XCD": "1"}))
+            ("dma+pipe+xcd", {"RMBX_ATTN_DMA": "2", "RMBX_ATTN_XCD": "1"}),
+            ("dma1stage", {"RMBX_ATTN_DMA": "3", "RMBX_ATTN_XCD": "0"}),
+            ("dma1stage+xcd", {"RMBX_ATTN_DMA": "3", "RMBX_ATTN_XCD": "1"}))
 
 
 def timeit(f, reps=10):

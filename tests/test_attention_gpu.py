@@ -239,11 +239,12 @@ def test_attention_f16x3_range_and_block_independence(case, shape):
 @pytest.mark.parametrize("B,H,Lq,Lk,case", [(3, 8, 302, 302, None), (2, 8, 100, 302, None), (4, 8, 100, 100, None),
                                              (1, 2, 1, 1, None), (2, 2, 257, 33, None), (1, 1, 130, 650, None),
                                              (3, 2, 302, 90, "huge_k"), (3, 2, 100, 90, "tiny_v_dim")])
-@pytest.mark.parametrize("form", ["1", "2", "1x", "2x"])
+@pytest.mark.parametrize("form", ["1", "2", "3", "1x", "2x", "3x"])
 def test_attention_f16x3_dma_staging_equals_register_staging(monkeypatch, B, H, Lq, Lk, case, form):
     """The LDS-DMA-staged f16x3 kernel (the default, RMBX_ATTN_DMA=1: raw tiles by LDS-DMA, pieces
     split once per block, V^T read through ds_read_b64_tr_b16; form 2 also runs K one tile ahead of V
-    so S^T of the next tile overlaps the softmax; "x": the parts of a head on one XCD) computes the register-staged kernel's
+    so S^T of the next tile overlaps the softmax; form 3: one raw stage, three blocks per CU; "x": the
+    parts of a head on one XCD) computes the register-staged kernel's
     pieces in the same MFMA order: bitwise-equal outputs, including ragged key tiles, query parts
     past Lq, long key sequences and re-run (flagged) blocks."""
     from robomanipbaselines_amd import kernels as K
