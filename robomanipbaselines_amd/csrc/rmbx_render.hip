@@ -28,6 +28,7 @@
 
 #include "rmbx_common.h"
 
+#include <algorithm>
 #include <cstdlib>
 #include "rmbx_math.h"
 #include "rmbx_model.h"
@@ -1214,7 +1215,39 @@ extern "C" int rmbx_render_scene_cached(const rmbx_camera* cam, const rmbx_scene
   }
   a.tiles_x = (cam->width + RENDER_TILE - 1) / RENDER_TILE;
   a.tiles_y = (cam->height + RENDER_TILE - 1) / RENDER_TILE;
-  a.groups = 16;
+  // blocks per env of the ray-cast pass (each a contiguous range of tiles), chosen so the grid fills
+  // whole rounds of the chip's block slots (CUs x RMBX_RENDER_MINW resident 4-wave blocks): front
+  // camera, 1024 envs, cached, 1536 slots (profiles/r6_render_groups_ab.log): 3.35 / 3.39 ms at 6 / 12
+  // groups (4 / 8 full rounds) vs 3.70 at 8 (5.3 rounds) and 4.49 at 16 (10.7): the last partial
+  // round of 75-tile blocks is the cost.  The largest g in [6, max(12, 2 slots / n)] with the best
+  // round fill; RMBX_RENDER_GROUPS overrides (A/B)
+  const char* ge = std::getenv("RMBX_RENDER_GROUPS");
+  const int ntl = a.tiles_x * a.tiles_y;
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess ||
+        cus <= 0)
+      cus = 256;
+  }
+  if (ge) {
+    a.groups = std::atoi(ge);
+  } else {
+    const long long slots = (long long)cus * RMBX_RENDER_MINW;
+    const int gmax = (int)std::min<long long>(ntl, std::max<long long>(12, (2 * slots + n_env - 1) / n_env));
+    int best = std::min(6, ntl);
+    double best_fill = -1.0;
+    for (int g = std::min(6, ntl); g <= gmax; ++g) {
+      const long long b = (long long)n_env * g, rounds = (b + slots - 1) / slots;
+      const double fill = (double)b / (double)(rounds * slots);
+      if (fill >= best_fill - 1e-12) {
+        best_fill = fill;
+        best = g;
+      }
+    }
+    a.groups = best;
+  }
+  RMBX_CHECK_ARG(a.groups >= 1 && a.groups <= a.tiles_x * a.tiles_y, "RMBX_RENDER_GROUPS=%d out of range", a.groups);
   const char* dbg_env = std::getenv("RMBX_RENDER_DBG");
   a.dbg = dbg_env ? std::atoi(dbg_env) : 0;
   const size_t nblocks = (size_t)n_env * a.groups;
