@@ -833,8 +833,30 @@ __global__ void __launch_bounds__(256, RMBX_RENDER_MINW) render_kernel(RenderArg
   }
   const int t_begin = (int)((long long)ntiles * grp / a.groups);
   const int t_end = (int)((long long)ntiles * (grp + 1) / a.groups);
+  const size_t hw = (size_t)H * W;
+  // the per-pixel global reads of a tile are issued a tile ahead (the tile flag and, with the cache,
+  // the cached static candidate) or at the tile's start (the mesh key), so their latency runs under
+  // the previous tile's rays and this tile's culling instead of in front of the ray loop
+  auto pix_of = [&](int t) {
+    const int x = (t % a.tiles_x) * RENDER_TILE + (tid % RENDER_TILE), y = (t / a.tiles_x) * RENDER_TILE + (tid / RENDER_TILE);
+    return (size_t)min(y, H - 1) * W + min(x, W - 1);  // (clamped: the loads of past-the-image lanes are unused)
+  };
+  uint2 nxt_ce = make_uint2(0u, 0u);
+  uint8_t nxt_tv = 0;
+  if (t_begin < t_end) {
+    if (mode == 1) nxt_ce = a.cache[(size_t)env * hw + pix_of(t_begin)];
+    if constexpr (VIS) nxt_tv = a.tflag[(size_t)env * ntiles + t_begin];
+  }
   for (int tile = t_begin; tile < t_end; ++tile) {
   __syncthreads();  // the previous tile's rays are done with tile_sorted (and order is complete)
+  const uint2 cur_ce = nxt_ce;
+  const bool tile_vis = VIS && nxt_tv != 0;
+  unsigned long long cur_key = VIS_EMPTY;
+  if (VIS && tile_vis) cur_key = a.vis[(size_t)env * hw + pix_of(tile)];
+  if (tile + 1 < t_end) {
+    if (mode == 1) nxt_ce = a.cache[(size_t)env * hw + pix_of(tile + 1)];
+    if constexpr (VIS) nxt_tv = a.tflag[(size_t)env * ntiles + tile + 1];
+  }
   const int tx0 = (tile % a.tiles_x) * RENDER_TILE, ty0 = (tile / a.tiles_x) * RENDER_TILE;
   // tile frustum in normalised image coords
   const float x_lo = (2.0f * tx0 / W - 1.0f) * tanh_ * aspect;
@@ -877,21 +899,18 @@ __global__ void __launch_bounds__(256, RMBX_RENDER_MINW) render_kernel(RenderArg
   // did the visibility pass write a pixel of this tile? (the flag is consumed: cleared below, after
   // every lane has read it, with the pixels' keys, so the workspace is back to empty for the next
   // call without a clearing pass)
-  bool tile_vis = false;
-  if constexpr (VIS) tile_vis = a.tflag[(size_t)env * ntiles + tile] != 0;
   __syncthreads();
   const int px = tx0 + (tid % RENDER_TILE), py = ty0 + (tid / RENDER_TILE);
   if (px < W && py < H) {
   const float d[3] = {((2.0f * (px + 0.5f) / W) - 1.0f) * tanh_ * aspect,
                       (1.0f - 2.0f * (py + 0.5f) / H) * tanh_, -1.0f};
   const size_t pix = (size_t)py * W + px;
-  const size_t hw = (size_t)H * W;
   // the mesh candidate (the visibility pass's nearest triangle), kept for the final pass
   float m_best = 1e30f, m_n[3] = {0, 0, 1}, m_rgb[3] = {0.f, 0.f, 0.f};
   int m_geom = -1;
   if constexpr (VIS) {
     // the pixel's nearest mesh triangle from the visibility pass
-    const unsigned long long key = tile_vis ? a.vis[(size_t)env * hw + pix] : VIS_EMPTY;
+    const unsigned long long key = cur_key;
     if (key != VIS_EMPTY) {
       a.vis[(size_t)env * hw + pix] = VIS_EMPTY;
       const unsigned j = (unsigned)key;
@@ -912,7 +931,7 @@ __global__ void __launch_bounds__(256, RMBX_RENDER_MINW) render_kernel(RenderArg
   float c_t = 1e30f;
   unsigned c_p = 0xffu, c_rgb = 0u;
   if (mode == 1) {
-    const uint2 ce = a.cache[(size_t)env * hw + pix];
+    const uint2 ce = cur_ce;
     c_t = __uint_as_float(ce.x);
     c_p = ce.y >> 24;
     c_rgb = ce.y & 0xffffffu;
